@@ -1,0 +1,214 @@
+"""Extender verbs: filter / prioritize / bind.
+
+Reference: pkg/scheduler/predicate.go:19-53, priority.go:19-42, bind.go:26-82 and the
+dealer calls behind them (dealer.go:89-203). The reference holds ONE mutex across
+filter, score and the API writes of bind; here filter/prioritize are lock-free reads of
+per-node snapshots and bind is
+
+    reserve (native ledger, µs)  ->  PATCH annotations  ->  POST binding  ->  commit
+                                  \\-> any failure: rollback + best-effort un-annotate
+
+so binds for different pods overlap their API round trips (the reference's
+bind rate is bounded by 1 / (2 x RTT)).
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import time
+from collections import OrderedDict
+
+from .. import types as T
+from ..k8s import podutil as pu
+from ..k8s.client import ApiError
+from ..obs import Metrics, Tracer
+from ..state.cluster import ClusterState, SchedulingError
+from .wire import BindingArgs, ExtenderArgs, binding_result, filter_result, priority_list
+
+log = logging.getLogger(__name__)
+
+
+class PodCache:
+    """Pods seen in filter/prioritize by UID, so bind can skip the reference's live GET
+    (bind.go:61-82) when the object is fresh. Bounded LRU."""
+
+    def __init__(self, cap: int = 16384):
+        self.cap = cap
+        self.d: OrderedDict[str, dict] = OrderedDict()
+
+    def put(self, pod: dict) -> None:
+        uid = pu.pod_uid(pod)
+        if not uid:
+            return
+        self.d[uid] = pod
+        self.d.move_to_end(uid)
+        if len(self.d) > self.cap:
+            self.d.popitem(last=False)
+
+    def pop(self, uid: str) -> dict | None:
+        return self.d.pop(uid, None)
+
+
+class Extender:
+    def __init__(self, state: ClusterState, api, metrics: Metrics | None = None,
+                 tracer: Tracer | None = None, verify_pod_on_bind: bool = False,
+                 api_retries: int = 2, record_events: bool = True):
+        self.state = state
+        self.api = api
+        self.metrics = metrics or Metrics()
+        self.tracer = tracer or Tracer()
+        self.verify_pod_on_bind = verify_pod_on_bind
+        self.api_retries = api_retries
+        self.record_events = record_events
+        self.pods = PodCache()
+        self._bg: set[asyncio.Task] = set()
+
+    # ------------------------------------------------------------------ filter
+    def filter(self, body) -> dict:
+        t0 = time.perf_counter()
+        try:
+            args = ExtenderArgs.decode(body)
+        except ValueError as e:
+            self.metrics.verb_total.labels("filter", "bad_request").inc()
+            return filter_result(None, {}, str(e))
+        with self.tracer.span("filter", pu.pod_key(args.pod)) as sp:
+            names = args.node_names
+            node_objs = None
+            if names is None:
+                if args.nodes is None:
+                    self.metrics.verb_total.labels("filter", "error").inc()
+                    return filter_result(None, {}, T.FILTER_NODE_CACHE_ERROR)
+                # nodeCacheCapable=false: full Node objects in the request (the reference rejects this)
+                for n in args.nodes:
+                    self.state.register_node(n)
+                node_objs = {pu.meta(n).get("name"): n for n in args.nodes}
+                names = list(node_objs)
+            self.pods.put(args.pod)
+            ok, failed = self.state.filter(args.pod, names)
+            sp.note = f"{len(ok)}/{len(names)} fit"
+        self.metrics.verb_latency.labels("filter").observe(time.perf_counter() - t0)
+        self.metrics.verb_total.labels("filter", "ok").inc()
+        if node_objs is not None:
+            return filter_result(None, failed, nodes=[node_objs[n] for n in ok])
+        return filter_result(ok, failed)
+
+    # ------------------------------------------------------------------ prioritize
+    def prioritize(self, body) -> list[dict]:
+        """Raises ValueError on a malformed body (server maps it to 400; reference panics,
+        routes.go:102-104)."""
+        t0 = time.perf_counter()
+        args = ExtenderArgs.decode(body)
+        names = args.node_names
+        if names is None:
+            names = [pu.meta(n).get("name") for n in (args.nodes or [])]
+            for n in args.nodes or []:
+                self.state.register_node(n)
+        with self.tracer.span("prioritize", pu.pod_key(args.pod)):
+            self.pods.put(args.pod)
+            scores = self.state.score(args.pod, names)
+        self.metrics.verb_latency.labels("prioritize").observe(time.perf_counter() - t0)
+        self.metrics.verb_total.labels("prioritize", "ok").inc()
+        return priority_list(names, scores)
+
+    # ------------------------------------------------------------------ bind
+    async def bind(self, body) -> dict:
+        t0 = time.perf_counter()
+        try:
+            args = BindingArgs.decode(body)
+        except ValueError as e:
+            self.metrics.verb_total.labels("bind", "bad_request").inc()
+            return binding_result(str(e))
+        err = ""
+        with self.tracer.span("bind", f"{args.pod_namespace}/{args.pod_name}") as sp:
+            try:
+                await self._bind(args, sp)
+            except (SchedulingError, ApiError, asyncio.TimeoutError, OSError) as e:
+                err = str(e) or e.__class__.__name__
+                sp.ok = False
+                sp.note = err
+        dt = time.perf_counter() - t0
+        self.metrics.verb_latency.labels("bind").observe(dt)
+        self.metrics.verb_total.labels("bind", "error" if err else "ok").inc()
+        if err:
+            log.info("bind %s/%s -> %s failed: %s", args.pod_namespace, args.pod_name, args.node, err)
+        return binding_result(err)
+
+    async def _get_pod(self, args: BindingArgs) -> dict:
+        """bind.go:61-82: live GET, re-GET once on UID mismatch."""
+        pod = await self.api.get_pod(args.pod_namespace, args.pod_name)
+        if args.pod_uid and pu.pod_uid(pod) != args.pod_uid:
+            pod = await self.api.get_pod(args.pod_namespace, args.pod_name)
+            if pu.pod_uid(pod) != args.pod_uid:
+                raise SchedulingError(f"pod {args.pod_name} in ns {args.pod_namespace}'s uid is "
+                                      f"{pu.pod_uid(pod)}, and it's not equal with expected {args.pod_uid}")
+        return pod
+
+    async def _retry(self, op: str, fn, *a):
+        for attempt in range(self.api_retries + 1):
+            try:
+                return await fn(*a)
+            except ApiError as e:
+                self.metrics.api_errors.labels(op, str(e.status)).inc()
+                if e.status < 500 and e.status != 429 or attempt == self.api_retries:
+                    raise
+            await asyncio.sleep(0.005 * (2 ** attempt))
+
+    async def _bind(self, args: BindingArgs, sp) -> None:
+        pod = None if self.verify_pod_on_bind else self.pods.pop(args.pod_uid)
+        tp = time.perf_counter()
+        if pod is None or (args.pod_uid and pu.pod_uid(pod) != args.pod_uid):
+            pod = await self._get_pod(args)
+            sp.phases["get"] = time.perf_counter() - tp
+        if pu.is_completed(pod):
+            raise SchedulingError(f"pod {args.pod_name}/{args.pod_namespace} already deleted or completed")
+        uid = pu.pod_uid(pod)
+        t1 = time.perf_counter()
+        plan, fresh = self.state.reserve(pod, args.node)
+        sp.phases["reserve"] = time.perf_counter() - t1
+        try:
+            t2 = time.perf_counter()
+            extra = {T.ANNOTATION_ASSUME_TIME: f"{time.time():.6f}"}
+            await self._retry("patch", self.api.patch_pod, args.pod_namespace, args.pod_name,
+                              pu.placement_patch(pod, plan, extra))
+            t3 = time.perf_counter()
+            try:
+                await self._retry("bind", self.api.bind_pod, args.pod_namespace, args.pod_name, uid, args.node)
+            except ApiError as e:
+                # A retried bind whose first attempt landed: already bound to this node is success.
+                if not e.conflict or pu.node_name_of(await self.api.get_pod(args.pod_namespace,
+                                                                            args.pod_name)) != args.node:
+                    raise
+            t4 = time.perf_counter()
+            sp.phases["patch"], sp.phases["binding"] = t3 - t2, t4 - t3
+            self.metrics.bind_phase.labels("patch").observe(t3 - t2)
+            self.metrics.bind_phase.labels("binding").observe(t4 - t3)
+        except BaseException as e:
+            # D2: the reference leaves the cache debited when the binding POST fails.
+            if not fresh:
+                raise
+            self.state.rollback(uid)
+            self.metrics.rollbacks.inc()
+            if not isinstance(e, asyncio.CancelledError):
+                self._background(self._unannotate(pod))
+                if self.record_events and isinstance(e, ApiError):
+                    self._background(self.api.create_event(
+                        args.pod_namespace, {"kind": "Pod", "name": args.pod_name, "namespace": args.pod_namespace,
+                                             "uid": uid}, "FailedBinding", f"nano-gpu bind failed: {e}"))
+            raise
+        self.state.commit(uid)
+        self.metrics.pods_bound.inc()
+
+    async def _unannotate(self, pod: dict) -> None:
+        ns, name = pu.pod_ns_name(pod)
+        ann = {T.container_annotation(c.get("name", "")): None for c in pu.containers(pod)}
+        ann[T.ANNOTATION_GPU_ASSUME] = None
+        try:
+            await self.api.patch_pod(ns, name, {"metadata": {"annotations": ann,
+                                                             "labels": {T.LABEL_GPU_ASSUME: None}}})
+        except (ApiError, OSError, asyncio.TimeoutError):
+            pass
+
+    def _background(self, coro) -> None:
+        t = asyncio.ensure_future(coro)
+        self._bg.add(t)
+        t.add_done_callback(self._bg.discard)

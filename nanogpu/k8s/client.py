@@ -1,0 +1,244 @@
+"""Minimal async Kubernetes REST client (pods, nodes, bindings, events, watch).
+
+Replaces client-go v0.18 (reference go.mod:16) for the calls the reference makes:
+List pods by label/field selector (dealer.go:58-60, 279-282), Get pod (bind.go:62, 68),
+Update pod (dealer.go:177, 184) -> here a JSON merge-patch of annotations/labels only,
+which cannot hit the optimistic-lock path the reference mishandles (D1), Create
+pods/binding (dealer.go:191-197), informers (list+watch) and the events sink.
+"""
+from __future__ import annotations
+
+import asyncio
+import base64
+import json
+import logging
+import os
+import ssl
+import tempfile
+import urllib.parse
+from dataclasses import dataclass
+from typing import Any, AsyncIterator
+
+import aiohttp
+
+log = logging.getLogger(__name__)
+
+SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
+
+
+class ApiError(Exception):
+    def __init__(self, status: int, message: str, reason: str = ""):
+        super().__init__(f"{status} {reason}: {message}")
+        self.status = status
+        self.reason = reason
+        self.message = message
+
+    @property
+    def not_found(self) -> bool:
+        return self.status == 404
+
+    @property
+    def conflict(self) -> bool:
+        return self.status == 409
+
+
+@dataclass
+class KubeConfig:
+    server: str
+    token: str | None = None
+    ca_file: str | None = None
+    cert_file: str | None = None
+    key_file: str | None = None
+    insecure: bool = False
+
+    @classmethod
+    def in_cluster(cls) -> "KubeConfig":
+        host, port = os.environ.get("KUBERNETES_SERVICE_HOST"), os.environ.get("KUBERNETES_SERVICE_PORT")
+        if not host or not port:
+            raise RuntimeError("not running in a cluster (KUBERNETES_SERVICE_HOST unset)")
+        with open(os.path.join(SA_DIR, "token")) as f:
+            token = f.read().strip()
+        if ":" in host:
+            host = f"[{host}]"
+        return cls(server=f"https://{host}:{port}", token=token, ca_file=os.path.join(SA_DIR, "ca.crt"))
+
+    @classmethod
+    def from_kubeconfig(cls, path: str, context: str | None = None) -> "KubeConfig":
+        import yaml
+
+        with open(path) as f:
+            cfg = yaml.safe_load(f) or {}
+        ctx_name = context or cfg.get("current-context")
+        ctx = next((c["context"] for c in cfg.get("contexts", []) if c.get("name") == ctx_name), None)
+        if ctx is None:
+            raise RuntimeError(f"kubeconfig {path}: context {ctx_name!r} not found")
+        cluster = next(c["cluster"] for c in cfg.get("clusters", []) if c.get("name") == ctx["cluster"])
+        user = next((u.get("user") or {} for u in cfg.get("users", []) if u.get("name") == ctx.get("user")), {})
+
+        def materialise(data_key: str, file_key: str, src: dict) -> str | None:
+            if src.get(file_key):
+                return src[file_key]
+            if src.get(data_key):
+                fd, p = tempfile.mkstemp(prefix="nanogpu-kc-")
+                with os.fdopen(fd, "wb") as f:
+                    f.write(base64.b64decode(src[data_key]))
+                return p
+            return None
+
+        return cls(server=cluster["server"].rstrip("/"), token=user.get("token"),
+                   ca_file=materialise("certificate-authority-data", "certificate-authority", cluster),
+                   cert_file=materialise("client-certificate-data", "client-certificate", user),
+                   key_file=materialise("client-key-data", "client-key", user),
+                   insecure=bool(cluster.get("insecure-skip-tls-verify")))
+
+    @classmethod
+    def auto(cls, kubeconfig: str | None = None, server: str | None = None) -> "KubeConfig":
+        """KUBECONFIG env / path first, then in-cluster (reference cmd/main.go:42-61)."""
+        if server:
+            return cls(server=server.rstrip("/"))
+        path = kubeconfig or os.environ.get("KUBECONFIG")
+        if path:
+            return cls.from_kubeconfig(path)
+        return cls.in_cluster()
+
+    def ssl_context(self) -> ssl.SSLContext | bool:
+        if not self.server.startswith("https"):
+            return False
+        ctx = ssl.create_default_context(cafile=self.ca_file) if self.ca_file else ssl.create_default_context()
+        if self.insecure:
+            ctx.check_hostname = False
+            ctx.verify_mode = ssl.CERT_NONE
+        if self.cert_file and self.key_file:
+            ctx.load_cert_chain(self.cert_file, self.key_file)
+        return ctx
+
+
+class KubeClient:
+    """Async client; one keep-alive connection pool per process."""
+
+    def __init__(self, config: KubeConfig, timeout_s: float = 30.0, pool: int = 64):
+        self.config = config
+        self._timeout = aiohttp.ClientTimeout(total=timeout_s)
+        self._pool = pool
+        self._session: aiohttp.ClientSession | None = None
+        self.calls = 0
+
+    async def _s(self) -> aiohttp.ClientSession:
+        if self._session is None or self._session.closed:
+            headers = {"Accept": "application/json", "User-Agent": "nano-gpu-scheduler-amd/0.1"}
+            if self.config.token:
+                headers["Authorization"] = f"Bearer {self.config.token}"
+            self._session = aiohttp.ClientSession(
+                headers=headers, timeout=self._timeout,
+                connector=aiohttp.TCPConnector(limit=self._pool, ssl=self.config.ssl_context()),
+                json_serialize=lambda o: json.dumps(o, separators=(",", ":")))
+        return self._session
+
+    async def close(self) -> None:
+        if self._session is not None:
+            await self._session.close()
+            self._session = None
+
+    async def request(self, method: str, path: str, body: Any = None, params: dict | None = None,
+                      content_type: str = "application/json") -> Any:
+        s = await self._s()
+        url = self.config.server + path
+        data = None if body is None else json.dumps(body, separators=(",", ":"))
+        self.calls += 1
+        async with s.request(method, url, data=data, params=params,
+                             headers={"Content-Type": content_type} if data is not None else None) as r:
+            text = await r.text()
+            if r.status >= 400:
+                try:
+                    st = json.loads(text)
+                    raise ApiError(r.status, st.get("message", text), st.get("reason", ""))
+                except (ValueError, AttributeError):
+                    raise ApiError(r.status, text) from None
+            return json.loads(text) if text else None
+
+    # --------------------------------------------------------------------- pods
+    async def get_pod(self, ns: str, name: str) -> dict:
+        return await self.request("GET", f"/api/v1/namespaces/{ns}/pods/{name}")
+
+    async def patch_pod(self, ns: str, name: str, patch: dict) -> dict:
+        return await self.request("PATCH", f"/api/v1/namespaces/{ns}/pods/{name}", patch,
+                                  content_type="application/merge-patch+json")
+
+    async def bind_pod(self, ns: str, name: str, uid: str, node: str) -> None:
+        body = {"apiVersion": "v1", "kind": "Binding",
+                "metadata": {"name": name, "namespace": ns, "uid": uid},
+                "target": {"apiVersion": "v1", "kind": "Node", "name": node}}
+        await self.request("POST", f"/api/v1/namespaces/{ns}/pods/{name}/binding", body)
+
+    async def create_pod(self, pod: dict) -> dict:
+        ns = (pod.get("metadata") or {}).get("namespace", "default")
+        return await self.request("POST", f"/api/v1/namespaces/{ns}/pods", pod)
+
+    async def delete_pod(self, ns: str, name: str) -> None:
+        await self.request("DELETE", f"/api/v1/namespaces/{ns}/pods/{name}")
+
+    async def list_pods(self, label_selector: str | None = None, field_selector: str | None = None,
+                        namespace: str | None = None) -> tuple[list[dict], str]:
+        params = {}
+        if label_selector:
+            params["labelSelector"] = label_selector
+        if field_selector:
+            params["fieldSelector"] = field_selector
+        path = f"/api/v1/namespaces/{namespace}/pods" if namespace else "/api/v1/pods"
+        r = await self.request("GET", path, params=params or None)
+        return r.get("items") or [], (r.get("metadata") or {}).get("resourceVersion", "")
+
+    # --------------------------------------------------------------------- nodes
+    async def get_node(self, name: str) -> dict:
+        return await self.request("GET", f"/api/v1/nodes/{name}")
+
+    async def list_nodes(self, label_selector: str | None = None) -> tuple[list[dict], str]:
+        r = await self.request("GET", "/api/v1/nodes",
+                               params={"labelSelector": label_selector} if label_selector else None)
+        return r.get("items") or [], (r.get("metadata") or {}).get("resourceVersion", "")
+
+    async def patch_node(self, name: str, patch: dict) -> dict:
+        return await self.request("PATCH", f"/api/v1/nodes/{name}", patch,
+                                  content_type="application/merge-patch+json")
+
+    async def patch_node_status(self, name: str, patch: dict) -> dict:
+        return await self.request("PATCH", f"/api/v1/nodes/{name}/status", patch,
+                                  content_type="application/merge-patch+json")
+
+    # --------------------------------------------------------------------- events
+    async def create_event(self, ns: str, involved: dict, reason: str, message: str,
+                           etype: str = "Warning") -> None:
+        import time
+        import uuid
+
+        ts = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
+        body = {"apiVersion": "v1", "kind": "Event",
+                "metadata": {"name": f"{involved.get('name', 'obj')}.{uuid.uuid4().hex[:10]}", "namespace": ns},
+                "involvedObject": involved, "reason": reason, "message": message, "type": etype,
+                "source": {"component": "nano-gpu-scheduler"}, "firstTimestamp": ts, "lastTimestamp": ts,
+                "count": 1}
+        try:
+            await self.request("POST", f"/api/v1/namespaces/{ns}/events", body)
+        except (ApiError, aiohttp.ClientError, asyncio.TimeoutError) as e:
+            log.debug("event not recorded: %s", e)
+
+    # --------------------------------------------------------------------- watch
+    async def watch(self, resource: str, resource_version: str, timeout_s: int = 300,
+                    label_selector: str | None = None) -> AsyncIterator[dict]:
+        """Streams watch events ({type, object}) for `pods` or `nodes` cluster-wide."""
+        s = await self._s()
+        params = {"watch": "1", "resourceVersion": resource_version, "timeoutSeconds": str(timeout_s),
+                  "allowWatchBookmarks": "true"}
+        if label_selector:
+            params["labelSelector"] = label_selector
+        url = f"{self.config.server}/api/v1/{resource}?{urllib.parse.urlencode(params)}"
+        async with s.get(url, timeout=aiohttp.ClientTimeout(total=None, sock_read=timeout_s + 30)) as r:
+            if r.status >= 400:
+                raise ApiError(r.status, await r.text())
+            buf = b""
+            async for chunk in r.content.iter_any():
+                buf += chunk
+                while b"\n" in buf:
+                    line, buf = buf.split(b"\n", 1)
+                    if line.strip():
+                        yield json.loads(line)

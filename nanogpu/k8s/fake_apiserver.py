@@ -1,0 +1,497 @@
+"""In-memory Kubernetes API server (pods, nodes, bindings, events, list+watch).
+
+The reference has no fake apiserver and no integration tests. This store
+backs three things: integration tests, the simulator, and the benchmark. It offers
+
+  * `FakeKubeStore`   — the object store (resourceVersion, selectors, watch fan-out,
+                         410 Gone on stale resourceVersion, 409 on binding conflicts);
+  * `InProcKube`      — the `KubeClient` interface served directly from the store (with an
+                         optional modelled RTT), for in-process runs;
+  * `make_app(store)` — the same store over HTTP (aiohttp), wire-compatible with the paths
+                         `KubeClient` uses, so the extender talks real REST in e2e tests;
+  * fault injection   — per-verb error rates (409/500), latency, and watch drops.
+"""
+from __future__ import annotations
+
+import asyncio
+import copy
+import json
+import random
+import time
+import uuid
+from collections import deque
+from dataclasses import dataclass, field
+from typing import Any, AsyncIterator
+
+from aiohttp import web
+
+from . import podutil as pu
+from .client import ApiError
+
+
+def _match_labels(obj: dict, selector: str | None) -> bool:
+    if not selector:
+        return True
+    labels = pu.meta(obj).get("labels") or {}
+    for term in selector.split(","):
+        term = term.strip()
+        if not term:
+            continue
+        if "!=" in term:
+            k, v = term.split("!=", 1)
+            if labels.get(k.strip()) == v.strip():
+                return False
+        elif "=" in term:
+            k, v = term.split("=", 1)
+            if labels.get(k.strip().rstrip("=")) != v.strip().lstrip("="):
+                return False
+        elif labels.get(term) is None:
+            return False
+    return True
+
+
+def _match_fields(obj: dict, selector: str | None) -> bool:
+    if not selector:
+        return True
+    for term in selector.split(","):
+        k, _, v = term.partition("=")
+        v = v.lstrip("=")
+        if k == "spec.nodeName" and pu.node_name_of(obj) != v:
+            return False
+        if k == "metadata.name" and pu.meta(obj).get("name") != v:
+            return False
+        if k == "metadata.namespace" and pu.meta(obj).get("namespace") != v:
+            return False
+        if k == "status.phase" and (obj.get("status") or {}).get("phase") != v:
+            return False
+    return True
+
+
+@dataclass
+class Faults:
+    latency_s: float = 0.0            # added to every API call (modelled RTT)
+    patch_error_rate: float = 0.0     # 500 on pod PATCH
+    bind_error_rate: float = 0.0      # 500 on binding POST
+    conflict_rate: float = 0.0        # 409 on binding POST
+    seed: int = 0
+    rng: random.Random = field(default_factory=random.Random)
+
+    def __post_init__(self):
+        self.rng.seed(self.seed)
+
+    def roll(self, p: float) -> bool:
+        return p > 0 and self.rng.random() < p
+
+
+class FakeKubeStore:
+    def __init__(self, history: int = 100000, faults: Faults | None = None):
+        self.rv = 0
+        self.pods: dict[tuple[str, str], dict] = {}
+        self.nodes: dict[str, dict] = {}
+        self.events: list[dict] = []
+        self.bindings: list[tuple[str, str, str]] = []
+        self.history: dict[str, deque] = {"pods": deque(maxlen=history), "nodes": deque(maxlen=history)}
+        self.watchers: dict[str, list[asyncio.Queue]] = {"pods": [], "nodes": []}
+        self.faults = faults or Faults()
+        self.counts: dict[str, int] = {}
+
+    # ------------------------------------------------------------------ internals
+    def _bump(self, obj: dict) -> dict:
+        self.rv += 1
+        obj.setdefault("metadata", {})["resourceVersion"] = str(self.rv)
+        return obj
+
+    def _emit(self, kind: str, etype: str, obj: dict) -> None:
+        ev = {"type": etype, "object": copy.deepcopy(obj)}
+        self.history[kind].append((self.rv, ev))
+        for q in list(self.watchers[kind]):
+            q.put_nowait(ev)
+
+    def _count(self, verb: str) -> None:
+        self.counts[verb] = self.counts.get(verb, 0) + 1
+
+    # ------------------------------------------------------------------ pods
+    def create_pod(self, pod: dict) -> dict:
+        self._count("create_pod")
+        pod = copy.deepcopy(pod)
+        m = pod.setdefault("metadata", {})
+        m.setdefault("namespace", "default")
+        m.setdefault("uid", str(uuid.uuid4()))
+        m.setdefault("creationTimestamp", time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()))
+        key = (m["namespace"], m["name"])
+        if key in self.pods:
+            raise ApiError(409, f'pods "{m["name"]}" already exists', "AlreadyExists")
+        pod.setdefault("status", {}).setdefault("phase", "Pending")
+        self._bump(pod)
+        self.pods[key] = pod
+        self._emit("pods", "ADDED", pod)
+        return copy.deepcopy(pod)
+
+    def get_pod(self, ns: str, name: str) -> dict:
+        self._count("get_pod")
+        p = self.pods.get((ns, name))
+        if p is None:
+            raise ApiError(404, f'pods "{name}" not found', "NotFound")
+        return copy.deepcopy(p)
+
+    def patch_pod(self, ns: str, name: str, patch: dict) -> dict:
+        self._count("patch_pod")
+        if self.faults.roll(self.faults.patch_error_rate):
+            raise ApiError(500, "injected patch failure", "InternalError")
+        p = self.pods.get((ns, name))
+        if p is None:
+            raise ApiError(404, f'pods "{name}" not found', "NotFound")
+        np_ = pu.apply_patch(p, patch)
+        self._bump(np_)
+        self.pods[(ns, name)] = np_
+        self._emit("pods", "MODIFIED", np_)
+        return copy.deepcopy(np_)
+
+    def update_pod(self, ns: str, name: str, pod: dict) -> dict:
+        self._count("update_pod")
+        cur = self.pods.get((ns, name))
+        if cur is None:
+            raise ApiError(404, f'pods "{name}" not found', "NotFound")
+        want = pu.meta(pod).get("resourceVersion")
+        if want and want != pu.meta(cur).get("resourceVersion"):
+            raise ApiError(409, f'Operation cannot be fulfilled on pods "{name}": the object has been '
+                                f'modified; please apply your changes to the latest version and try again',
+                           "Conflict")
+        pod = copy.deepcopy(pod)
+        self._bump(pod)
+        self.pods[(ns, name)] = pod
+        self._emit("pods", "MODIFIED", pod)
+        return copy.deepcopy(pod)
+
+    def bind_pod(self, ns: str, name: str, uid: str, node: str) -> None:
+        self._count("bind_pod")
+        if self.faults.roll(self.faults.bind_error_rate):
+            raise ApiError(500, "injected binding failure", "InternalError")
+        if self.faults.roll(self.faults.conflict_rate):
+            raise ApiError(409, f'Operation cannot be fulfilled on pods/binding "{name}": injected', "Conflict")
+        p = self.pods.get((ns, name))
+        if p is None:
+            raise ApiError(404, f'pods "{name}" not found', "NotFound")
+        if uid and pu.pod_uid(p) != uid:
+            raise ApiError(409, f"pod {name} uid mismatch", "Conflict")
+        if pu.node_name_of(p):
+            raise ApiError(409, f'pod {name} is already assigned to node "{pu.node_name_of(p)}"', "Conflict")
+        if node not in self.nodes:
+            raise ApiError(404, f'nodes "{node}" not found', "NotFound")
+        np_ = copy.deepcopy(p)
+        np_.setdefault("spec", {})["nodeName"] = node
+        np_.setdefault("status", {})["phase"] = "Running"
+        self._bump(np_)
+        self.pods[(ns, name)] = np_
+        self.bindings.append((ns, name, node))
+        self._emit("pods", "MODIFIED", np_)
+
+    def delete_pod(self, ns: str, name: str) -> None:
+        self._count("delete_pod")
+        p = self.pods.pop((ns, name), None)
+        if p is None:
+            raise ApiError(404, f'pods "{name}" not found', "NotFound")
+        self._bump(p)
+        self._emit("pods", "DELETED", p)
+
+    def set_phase(self, ns: str, name: str, phase: str) -> dict:
+        return self.patch_pod(ns, name, {"status": {"phase": phase}})
+
+    def list_pods(self, label_selector: str | None = None, field_selector: str | None = None,
+                  namespace: str | None = None) -> tuple[list[dict], str]:
+        self._count("list_pods")
+        items = [copy.deepcopy(p) for (ns, _), p in self.pods.items()
+                 if (namespace is None or ns == namespace) and _match_labels(p, label_selector)
+                 and _match_fields(p, field_selector)]
+        return items, str(self.rv)
+
+    # ------------------------------------------------------------------ nodes
+    def add_node(self, node: dict) -> dict:
+        node = copy.deepcopy(node)
+        name = pu.meta(node)["name"]
+        etype = "MODIFIED" if name in self.nodes else "ADDED"
+        self._bump(node)
+        self.nodes[name] = node
+        self._emit("nodes", etype, node)
+        return copy.deepcopy(node)
+
+    def get_node(self, name: str) -> dict:
+        self._count("get_node")
+        n = self.nodes.get(name)
+        if n is None:
+            raise ApiError(404, f'nodes "{name}" not found', "NotFound")
+        return copy.deepcopy(n)
+
+    def patch_node(self, name: str, patch: dict) -> dict:
+        n = self.nodes.get(name)
+        if n is None:
+            raise ApiError(404, f'nodes "{name}" not found', "NotFound")
+        nn = pu.apply_patch(n, patch)
+        self._bump(nn)
+        self.nodes[name] = nn
+        self._emit("nodes", "MODIFIED", nn)
+        return copy.deepcopy(nn)
+
+    def delete_node(self, name: str) -> None:
+        n = self.nodes.pop(name, None)
+        if n is not None:
+            self._bump(n)
+            self._emit("nodes", "DELETED", n)
+
+    def list_nodes(self, label_selector: str | None = None) -> tuple[list[dict], str]:
+        self._count("list_nodes")
+        return [copy.deepcopy(n) for n in self.nodes.values() if _match_labels(n, label_selector)], str(self.rv)
+
+    def add_event(self, ev: dict) -> None:
+        self.events.append(ev)
+
+    # ------------------------------------------------------------------ watch
+    async def watch(self, kind: str, resource_version: str, label_selector: str | None = None
+                    ) -> AsyncIterator[dict]:
+        try:
+            rv = int(resource_version or 0)
+        except ValueError:
+            rv = 0
+        q: asyncio.Queue = asyncio.Queue()
+        hist = self.history[kind]
+        if rv and hist and hist[0][0] > rv + 1 and len(hist) == hist.maxlen:
+            raise ApiError(410, "too old resource version", "Expired")
+        for ev_rv, ev in list(hist):
+            if ev_rv > rv:
+                q.put_nowait(ev)
+        self.watchers[kind].append(q)
+        try:
+            while True:
+                ev = await q.get()
+                if ev is None:
+                    return
+                if label_selector and not _match_labels(ev["object"], label_selector):
+                    continue
+                yield ev
+        finally:
+            self.watchers[kind].remove(q)
+
+    def drop_watches(self) -> None:
+        """Fault injection: terminates every open watch stream."""
+        for qs in self.watchers.values():
+            for q in qs:
+                q.put_nowait(None)
+
+
+class InProcKube:
+    """`KubeClient`-compatible facade over a FakeKubeStore (no sockets)."""
+
+    def __init__(self, store: FakeKubeStore):
+        self.store = store
+        self.calls = 0
+
+    async def _rtt(self) -> None:
+        self.calls += 1
+        if self.store.faults.latency_s > 0:
+            await asyncio.sleep(self.store.faults.latency_s)
+
+    async def get_pod(self, ns, name):
+        await self._rtt()
+        return self.store.get_pod(ns, name)
+
+    async def patch_pod(self, ns, name, patch):
+        await self._rtt()
+        return self.store.patch_pod(ns, name, patch)
+
+    async def bind_pod(self, ns, name, uid, node):
+        await self._rtt()
+        self.store.bind_pod(ns, name, uid, node)
+
+    async def create_pod(self, pod):
+        await self._rtt()
+        return self.store.create_pod(pod)
+
+    async def delete_pod(self, ns, name):
+        await self._rtt()
+        self.store.delete_pod(ns, name)
+
+    async def list_pods(self, label_selector=None, field_selector=None, namespace=None):
+        await self._rtt()
+        return self.store.list_pods(label_selector, field_selector, namespace)
+
+    async def get_node(self, name):
+        await self._rtt()
+        return self.store.get_node(name)
+
+    async def list_nodes(self, label_selector=None):
+        await self._rtt()
+        return self.store.list_nodes(label_selector)
+
+    async def patch_node(self, name, patch):
+        await self._rtt()
+        return self.store.patch_node(name, patch)
+
+    async def patch_node_status(self, name, patch):
+        return await self.patch_node(name, patch)
+
+    async def create_event(self, ns, involved, reason, message, etype="Warning"):
+        self.store.add_event({"namespace": ns, "involvedObject": involved, "reason": reason,
+                              "message": message, "type": etype})
+
+    async def watch(self, resource, resource_version, timeout_s=300, label_selector=None):
+        async for ev in self.store.watch(resource, resource_version, label_selector):
+            yield ev
+
+    async def close(self):
+        return None
+
+
+# ---------------------------------------------------------------------- HTTP facade
+def _err(e: ApiError) -> web.Response:
+    body = {"kind": "Status", "apiVersion": "v1", "status": "Failure", "message": e.message,
+            "reason": e.reason, "code": e.status}
+    return web.json_response(body, status=e.status)
+
+
+def make_app(store: FakeKubeStore) -> web.Application:
+    routes = web.RouteTableDef()
+
+    async def lat():
+        if store.faults.latency_s > 0:
+            await asyncio.sleep(store.faults.latency_s)
+
+    async def stream_watch(request: web.Request, kind: str, label_selector=None) -> web.StreamResponse:
+        resp = web.StreamResponse(headers={"Content-Type": "application/json"})
+        try:
+            gen = store.watch(kind, request.query.get("resourceVersion", "0"), label_selector)
+            await resp.prepare(request)
+            async for ev in gen:
+                await resp.write(json.dumps(ev, separators=(",", ":")).encode() + b"\n")
+        except ApiError as e:
+            if not resp.prepared:
+                return _err(e)
+        except (ConnectionResetError, asyncio.CancelledError):
+            pass
+        return resp
+
+    def listing(kind: str, items: list, rv: str) -> web.Response:
+        return web.json_response({"kind": kind, "apiVersion": "v1", "metadata": {"resourceVersion": rv},
+                                  "items": items})
+
+    @routes.get("/api/v1/pods")
+    async def list_all_pods(request):
+        await lat()
+        ls, fs = request.query.get("labelSelector"), request.query.get("fieldSelector")
+        if request.query.get("watch") in ("1", "true"):
+            return await stream_watch(request, "pods", ls)
+        items, rv = store.list_pods(ls, fs)
+        return listing("PodList", items, rv)
+
+    @routes.get("/api/v1/namespaces/{ns}/pods")
+    async def list_ns_pods(request):
+        await lat()
+        items, rv = store.list_pods(request.query.get("labelSelector"), request.query.get("fieldSelector"),
+                                    request.match_info["ns"])
+        return listing("PodList", items, rv)
+
+    @routes.post("/api/v1/namespaces/{ns}/pods")
+    async def create_pod(request):
+        await lat()
+        body = await request.json()
+        body.setdefault("metadata", {})["namespace"] = request.match_info["ns"]
+        try:
+            return web.json_response(store.create_pod(body), status=201)
+        except ApiError as e:
+            return _err(e)
+
+    @routes.get("/api/v1/namespaces/{ns}/pods/{name}")
+    async def get_pod(request):
+        await lat()
+        try:
+            return web.json_response(store.get_pod(request.match_info["ns"], request.match_info["name"]))
+        except ApiError as e:
+            return _err(e)
+
+    @routes.patch("/api/v1/namespaces/{ns}/pods/{name}")
+    async def patch_pod(request):
+        await lat()
+        try:
+            return web.json_response(store.patch_pod(request.match_info["ns"], request.match_info["name"],
+                                                     await request.json()))
+        except ApiError as e:
+            return _err(e)
+
+    @routes.put("/api/v1/namespaces/{ns}/pods/{name}")
+    async def put_pod(request):
+        await lat()
+        try:
+            return web.json_response(store.update_pod(request.match_info["ns"], request.match_info["name"],
+                                                      await request.json()))
+        except ApiError as e:
+            return _err(e)
+
+    @routes.delete("/api/v1/namespaces/{ns}/pods/{name}")
+    async def delete_pod(request):
+        await lat()
+        try:
+            store.delete_pod(request.match_info["ns"], request.match_info["name"])
+            return web.json_response({"kind": "Status", "status": "Success"})
+        except ApiError as e:
+            return _err(e)
+
+    @routes.post("/api/v1/namespaces/{ns}/pods/{name}/binding")
+    async def bind(request):
+        await lat()
+        body = await request.json()
+        try:
+            store.bind_pod(request.match_info["ns"], request.match_info["name"],
+                           (body.get("metadata") or {}).get("uid", ""), (body.get("target") or {}).get("name", ""))
+            return web.json_response({"kind": "Status", "status": "Success"}, status=201)
+        except ApiError as e:
+            return _err(e)
+
+    @routes.get("/api/v1/nodes")
+    async def list_nodes(request):
+        await lat()
+        ls = request.query.get("labelSelector")
+        if request.query.get("watch") in ("1", "true"):
+            return await stream_watch(request, "nodes", ls)
+        items, rv = store.list_nodes(ls)
+        return listing("NodeList", items, rv)
+
+    @routes.get("/api/v1/nodes/{name}")
+    async def get_node(request):
+        await lat()
+        try:
+            return web.json_response(store.get_node(request.match_info["name"]))
+        except ApiError as e:
+            return _err(e)
+
+    @routes.patch("/api/v1/nodes/{name}")
+    @routes.patch("/api/v1/nodes/{name}/status")
+    async def patch_node(request):
+        await lat()
+        try:
+            return web.json_response(store.patch_node(request.match_info["name"], await request.json()))
+        except ApiError as e:
+            return _err(e)
+
+    @routes.post("/api/v1/namespaces/{ns}/events")
+    async def event(request):
+        store.add_event(await request.json())
+        return web.json_response({}, status=201)
+
+    app = web.Application(client_max_size=16 * 1024 * 1024)
+    app.add_routes(routes)
+    app["store"] = store
+    return app
+
+
+async def serve(store: FakeKubeStore, host: str = "127.0.0.1", port: int = 0) -> tuple[web.AppRunner, int]:
+    runner = web.AppRunner(make_app(store), access_log=None)
+    await runner.setup()
+    site = web.TCPSite(runner, host, port)
+    await site.start()
+    port = site._server.sockets[0].getsockname()[1]  # type: ignore[union-attr]
+    return runner, port
+
+
+def store_summary(store: FakeKubeStore) -> dict[str, Any]:
+    bound = sum(1 for p in store.pods.values() if pu.node_name_of(p))
+    return {"pods": len(store.pods), "bound": bound, "nodes": len(store.nodes), "rv": store.rv,
+            "bindings": len(store.bindings), "calls": dict(store.counts)}

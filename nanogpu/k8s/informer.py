@@ -1,0 +1,186 @@
+"""List+watch informer and a de-duplicating async work queue.
+
+Replaces client-go shared informers + workqueue (reference controller.go:89-136, 247-268).
+The reference worker returns `false` after every successful item, so `wait.Until` sleeps a
+second between items (controller.go:256-261, 185). These workers drain the
+queue continuously and back off only on errors.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import random
+from typing import Awaitable, Callable
+
+from . import podutil as pu
+from .client import ApiError
+
+log = logging.getLogger(__name__)
+
+Handler = Callable[[str, dict, dict | None], None]   # (event_type, obj, old_obj)
+
+
+class Informer:
+    def __init__(self, api, resource: str, label_selector: str | None = None,
+                 resync_s: float = 0.0, key=None):
+        self.api = api
+        self.resource = resource               # "pods" | "nodes"
+        self.label_selector = label_selector
+        self.resync_s = resync_s
+        self.key = key or (lambda o: f"{pu.meta(o).get('namespace', '')}/{pu.meta(o).get('name', '')}"
+                           if resource == "pods" else pu.meta(o).get("name", ""))
+        self.store: dict[str, dict] = {}
+        self.handlers: list[Handler] = []
+        self.synced = asyncio.Event()
+        self.rv = ""
+        self._task: asyncio.Task | None = None
+        self.relists = 0
+
+    def add_handler(self, h: Handler) -> None:
+        self.handlers.append(h)
+
+    def get(self, key: str) -> dict | None:
+        return self.store.get(key)
+
+    def list(self) -> list[dict]:
+        return list(self.store.values())
+
+    def _dispatch(self, etype: str, obj: dict, old: dict | None) -> None:
+        for h in self.handlers:
+            try:
+                h(etype, obj, old)
+            except Exception:  # a handler bug must not kill the informer
+                log.exception("informer handler failed for %s %s", etype, self.key(obj))
+
+    async def _list(self) -> None:
+        if self.resource == "pods":
+            items, rv = await self.api.list_pods(label_selector=self.label_selector)
+        else:
+            items, rv = await self.api.list_nodes(label_selector=self.label_selector)
+        fresh = {self.key(o): o for o in items}
+        for k, old in list(self.store.items()):
+            if k not in fresh:
+                del self.store[k]
+                self._dispatch("DELETED", old, None)
+        for k, o in fresh.items():
+            old = self.store.get(k)
+            self.store[k] = o
+            self._dispatch("MODIFIED" if old is not None else "ADDED", o, old)
+        self.rv = rv
+        self.relists += 1
+
+    async def run(self) -> None:
+        backoff = 0.05
+        while True:
+            try:
+                await self._list()
+                self.synced.set()
+                backoff = 0.05
+                await self._watch()
+            except asyncio.CancelledError:
+                raise
+            except ApiError as e:
+                if e.status != 410:
+                    log.warning("%s informer: %s", self.resource, e)
+                    await asyncio.sleep(backoff)
+                    backoff = min(backoff * 2, 5.0)
+            except Exception as e:  # network errors: relist with backoff
+                log.warning("%s informer error: %s", self.resource, e)
+                await asyncio.sleep(backoff + random.random() * backoff)
+                backoff = min(backoff * 2, 5.0)
+
+    async def _watch(self) -> None:
+        async for ev in self.api.watch(self.resource, self.rv, label_selector=self.label_selector):
+            etype, obj = ev.get("type"), ev.get("object") or {}
+            if etype == "BOOKMARK":
+                self.rv = pu.meta(obj).get("resourceVersion", self.rv)
+                continue
+            if etype == "ERROR":
+                raise ApiError(int(obj.get("code", 500)), obj.get("message", "watch error"))
+            k = self.key(obj)
+            self.rv = pu.meta(obj).get("resourceVersion", self.rv)
+            if etype == "DELETED":
+                old = self.store.pop(k, None)
+                self._dispatch("DELETED", obj, old)
+            else:
+                old = self.store.get(k)
+                self.store[k] = obj
+                self._dispatch("MODIFIED" if old is not None else "ADDED", obj, old)
+
+    def start(self) -> asyncio.Task:
+        self._task = asyncio.ensure_future(self.run())
+        return self._task
+
+    async def stop(self) -> None:
+        if self._task:
+            self._task.cancel()
+            try:
+                await self._task
+            except (asyncio.CancelledError, Exception):
+                pass
+
+
+class WorkQueue:
+    """Keyed queue: a key is processed by at most one worker at a time and queued once."""
+
+    def __init__(self, name: str, max_retries: int = 5, base_backoff: float = 0.01, max_backoff: float = 5.0):
+        self.name = name
+        self.q: asyncio.Queue[str] = asyncio.Queue()
+        self.queued: set[str] = set()
+        self.processing: set[str] = set()
+        self.dirty: set[str] = set()
+        self.retries: dict[str, int] = {}
+        self.max_retries = max_retries
+        self.base_backoff = base_backoff
+        self.max_backoff = max_backoff
+        self.processed = 0
+        self.dropped = 0
+
+    def add(self, key: str) -> None:
+        if key in self.processing:
+            self.dirty.add(key)
+            return
+        if key in self.queued:
+            return
+        self.queued.add(key)
+        self.q.put_nowait(key)
+
+    def depth(self) -> int:
+        return self.q.qsize()
+
+    async def _process(self, key: str, fn: Callable[[str], Awaitable[None]]) -> None:
+        self.queued.discard(key)
+        self.processing.add(key)
+        try:
+            await fn(key)
+            self.retries.pop(key, None)
+            self.processed += 1
+        except asyncio.CancelledError:
+            raise
+        except Exception as e:
+            n = self.retries.get(key, 0) + 1
+            if n > self.max_retries:
+                log.error("%s: dropping %s after %d retries: %s", self.name, key, n - 1, e)
+                self.retries.pop(key, None)
+                self.dropped += 1
+            else:
+                self.retries[key] = n
+                delay = min(self.base_backoff * 2 ** (n - 1), self.max_backoff)
+                asyncio.get_running_loop().call_later(delay, self.add, key)
+        finally:
+            self.processing.discard(key)
+            if key in self.dirty:
+                self.dirty.discard(key)
+                self.add(key)
+
+    async def worker(self, fn: Callable[[str], Awaitable[None]]) -> None:
+        while True:
+            key = await self.q.get()
+            await self._process(key, fn)
+
+    async def drain(self, timeout: float = 10.0) -> bool:
+        loop = asyncio.get_running_loop()
+        end = loop.time() + timeout
+        while (self.q.qsize() or self.processing) and loop.time() < end:
+            await asyncio.sleep(0.002)
+        return not (self.q.qsize() or self.processing)

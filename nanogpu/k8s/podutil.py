@@ -1,0 +1,200 @@
+"""Pod / node helpers over raw Kubernetes JSON objects (dicts).
+
+Reference: pkg/utils/pod.go:15-100, pkg/utils/node.go:8-14, pkg/dealer/allocate.go:29-62.
+"""
+from __future__ import annotations
+
+import logging
+from typing import Iterable
+
+from .. import types as T
+from .quantity import QuantityError, quantity_to_mib, quantity_value
+
+log = logging.getLogger(__name__)
+
+Demand = list  # list[tuple[int, int]]: (gpu-percent, hbm-mib) per container
+Plan = list    # list[list[int]]: device indices per container ([-1] = no GPU)
+
+
+def meta(obj: dict) -> dict:
+    return obj.get("metadata") or {}
+
+
+def pod_uid(pod: dict) -> str:
+    return meta(pod).get("uid", "")
+
+
+def pod_ns_name(pod: dict) -> tuple[str, str]:
+    m = meta(pod)
+    return m.get("namespace", "default"), m.get("name", "")
+
+
+def pod_key(pod: dict) -> str:
+    ns, name = pod_ns_name(pod)
+    return f"{ns}/{name}"
+
+
+def containers(pod: dict) -> list[dict]:
+    return (pod.get("spec") or {}).get("containers") or []
+
+
+def node_name_of(pod: dict) -> str:
+    return (pod.get("spec") or {}).get("nodeName") or ""
+
+
+def is_completed(pod: dict) -> bool:
+    """pod.go:15-24: deletionTimestamp set, or phase Succeeded/Failed."""
+    if meta(pod).get("deletionTimestamp"):
+        return True
+    return ((pod.get("status") or {}).get("phase")) in ("Succeeded", "Failed")
+
+
+def _limit(c: dict, res: str):
+    lim = ((c.get("resources") or {}).get("limits")) or {}
+    return lim.get(res)
+
+
+def container_percent(c: dict) -> int:
+    """pod.go:94-100: Quantity.Value() of limits[nano-gpu/gpu-percent], 0 when absent."""
+    v = _limit(c, T.RESOURCE_GPU_PERCENT)
+    if v is None:
+        return 0
+    try:
+        return max(0, quantity_value(v))
+    except QuantityError:
+        log.warning("bad %s quantity %r", T.RESOURCE_GPU_PERCENT, v)
+        return 0
+
+
+def container_mib(c: dict) -> int:
+    v = _limit(c, T.RESOURCE_GPU_MEMORY)
+    if v is None:
+        return 0
+    try:
+        return max(0, quantity_to_mib(v))
+    except QuantityError:
+        log.warning("bad %s quantity %r", T.RESOURCE_GPU_MEMORY, v)
+        return 0
+
+
+def pod_demand(pod: dict) -> Demand:
+    """allocate.go:54-62 (+ HBM MiB as the second dimension). Init containers are ignored."""
+    return [(container_percent(c), container_mib(c)) for c in containers(pod)]
+
+
+def is_gpu_sharing(pod: dict) -> bool:
+    """pod.go:27-29 (Σ gpu-percent > 0), extended: an HBM-only request also counts."""
+    return any(p > 0 or m > 0 for p, m in pod_demand(pod))
+
+
+def is_assumed(pod: dict) -> bool:
+    return (meta(pod).get("annotations") or {}).get(T.ANNOTATION_GPU_ASSUME) == "true"
+
+
+def container_assignment(pod: dict, name: str) -> list[int] | None:
+    """pod.go:85-92; comma-separated indices for whole-device (multi-GPU) containers."""
+    val = (meta(pod).get("annotations") or {}).get(T.container_annotation(name))
+    if val is None:
+        return None
+    try:
+        return [int(x) for x in val.split(",") if x.strip() != ""]
+    except ValueError:
+        return None
+
+
+def plan_from_pod(pod: dict) -> Plan | None:
+    """allocate.go:29-50. A missing/garbled container index defaults to device 0 as in the
+    reference (allocate.go:42-45); a zero-demand container keeps -1."""
+    if not is_assumed(pod):
+        return None
+    plan: Plan = []
+    for c in containers(pod):
+        idx = container_assignment(pod, c.get("name", ""))
+        if not idx:
+            log.warning("pod %s: container %s has no assignment; defaulting to 0",
+                        pod_key(pod), c.get("name"))
+            idx = [0]
+        plan.append(idx)
+    return plan
+
+
+def placement_patch(pod: dict, plan: Plan, extra: dict | None = None) -> dict:
+    """Merge-patch body writing the reference annotation contract (pod.go:65-79)."""
+    ann = {T.container_annotation(c.get("name", "")): ",".join(str(i) for i in plan[k])
+           for k, c in enumerate(containers(pod))}
+    ann[T.ANNOTATION_GPU_ASSUME] = "true"
+    if extra:
+        ann.update(extra)
+    return {"metadata": {"annotations": ann, "labels": {T.LABEL_GPU_ASSUME: "true"}}}
+
+
+def apply_patch(obj: dict, patch: dict) -> dict:
+    """RFC 7386 JSON merge patch (what the fake apiserver and our tests use)."""
+    if not isinstance(patch, dict):
+        return patch
+    out = dict(obj) if isinstance(obj, dict) else {}
+    for k, v in patch.items():
+        if v is None:
+            out.pop(k, None)
+        elif isinstance(v, dict):
+            out[k] = apply_patch(out.get(k) or {}, v)
+        else:
+            out[k] = v
+    return out
+
+
+def node_capacity_percent(node: dict) -> int:
+    cap = ((node.get("status") or {}).get("capacity")) or {}
+    v = cap.get(T.RESOURCE_GPU_PERCENT)
+    if v is None:
+        return 0
+    try:
+        return quantity_value(v)
+    except QuantityError:
+        return 0
+
+
+def node_gpu_count(node: dict) -> int:
+    """node.go:8-14: ⌊capacity[gpu-percent] / 100⌋."""
+    return node_capacity_percent(node) // T.GPU_PERCENT_EACH_CARD
+
+
+def node_labels(node: dict) -> dict:
+    return meta(node).get("labels") or {}
+
+
+def make_pod(name: str, containers_spec: Iterable[tuple[str, int] | tuple[str, int, int]],
+             namespace: str = "default", uid: str | None = None,
+             scheduler_name: str = "default-scheduler") -> dict:
+    """Builds a pod object (tests, simulator, bench). containers_spec: (name, pct[, mib])."""
+    import uuid
+
+    cs = []
+    for spec in containers_spec:
+        cname, pct = spec[0], spec[1]
+        mib = spec[2] if len(spec) > 2 else 0
+        lim = {}
+        if pct:
+            lim[T.RESOURCE_GPU_PERCENT] = str(pct)
+        if mib:
+            lim[T.RESOURCE_GPU_MEMORY] = str(mib)
+        cs.append({"name": cname, "image": "busybox", "resources": {"limits": lim, "requests": dict(lim)}})
+    return {
+        "apiVersion": "v1", "kind": "Pod",
+        "metadata": {"name": name, "namespace": namespace, "uid": uid or str(uuid.uuid4()),
+                     "annotations": {}, "labels": {}},
+        "spec": {"containers": cs, "schedulerName": scheduler_name},
+        "status": {"phase": "Pending"},
+    }
+
+
+def make_node(name: str, gpus: int, topology_json: str | None = None, labels: dict | None = None) -> dict:
+    ann = {}
+    if topology_json:
+        ann[T.ANNOTATION_TOPOLOGY] = topology_json
+    return {
+        "apiVersion": "v1", "kind": "Node",
+        "metadata": {"name": name, "labels": dict(labels or {}), "annotations": ann},
+        "status": {"capacity": {T.RESOURCE_GPU_PERCENT: str(gpus * T.GPU_PERCENT_EACH_CARD)},
+                   "allocatable": {T.RESOURCE_GPU_PERCENT: str(gpus * T.GPU_PERCENT_EACH_CARD)}},
+    }

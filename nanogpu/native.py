@@ -1,0 +1,38 @@
+"""Loader for the in-tree native extensions.
+
+`_native` (C++ core) is mandatory: the scheduler has no pure-Python allocation path, so a
+missing build fails loudly instead of silently falling back. `_probe` (HIP, gfx950) is
+needed only by the node agent's calibration and GPU tests; `probe(required=True)` raises
+on a GPU host where it is missing.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+from types import ModuleType
+
+_BUILD_HINT = "build it in-tree with `python native/build.py` (or __graft_entry__.build())"
+
+
+def core() -> ModuleType:
+    try:
+        return importlib.import_module("nanogpu._native")
+    except ImportError as e:  # pragma: no cover - exercised only on broken installs
+        if os.environ.get("NANOGPU_AUTOBUILD", "1") == "1":
+            from pathlib import Path
+            import subprocess
+            import sys
+
+            root = Path(__file__).resolve().parent.parent
+            subprocess.run([sys.executable, str(root / "native" / "build.py"), "--no-hip"], check=True)
+            return importlib.import_module("nanogpu._native")
+        raise ImportError(f"nanogpu._native is not built; {_BUILD_HINT}") from e
+
+
+def probe(required: bool = False) -> ModuleType | None:
+    try:
+        return importlib.import_module("nanogpu._probe")
+    except ImportError as e:
+        if required:
+            raise ImportError(f"nanogpu._probe (HIP gfx950 kernels) is not built; {_BUILD_HINT}") from e
+        return None

@@ -1,0 +1,270 @@
+"""A kube-scheduler stand-in that speaks the extender protocol.
+
+Models what kube-scheduler does with an extender configured as in the reference README
+(README.md:43-58: urlPrefix .../scheduler, filter/priorities/bind verbs,
+nodeCacheCapable=true, managed resource nano-gpu/gpu-percent) [ext]:
+  * scheduling cycle, serial per scheduler instance: node-level resource fit
+    (NodeResourcesFit on the extended resource) -> POST filter -> POST priorities ->
+    select the max-score host (ties broken by a seeded RNG, like selectHost) [ext];
+  * binding cycle, asynchronous: POST bind (the extender is the binder);
+  * failed pods go back to the queue with exponential backoff.
+Transport is real HTTP (aiohttp) or in-process calls on an `Extender`.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import random
+import statistics
+import time
+from dataclasses import dataclass, field
+
+import aiohttp
+
+from .. import types as T
+from ..k8s import podutil as pu
+
+
+class HttpExtenderClient:
+    def __init__(self, base_url: str, pool: int = 256):
+        self.base = base_url.rstrip("/")
+        self.pool = pool
+        self.s: aiohttp.ClientSession | None = None
+
+    async def _session(self) -> aiohttp.ClientSession:
+        if self.s is None:
+            self.s = aiohttp.ClientSession(connector=aiohttp.TCPConnector(limit=self.pool),
+                                           timeout=aiohttp.ClientTimeout(total=30))
+        return self.s
+
+    async def _post(self, verb: str, body: dict):
+        s = await self._session()
+        async with s.post(f"{self.base}/scheduler/{verb}", data=json.dumps(body, separators=(",", ":")),
+                          headers={"Content-Type": "application/json"}) as r:
+            return r.status, await r.json(content_type=None)
+
+    async def filter(self, body):
+        return (await self._post("filter", body))[1]
+
+    async def prioritize(self, body):
+        return (await self._post("priorities", body))[1]
+
+    async def bind(self, body):
+        return (await self._post("bind", body))[1]
+
+    async def close(self):
+        if self.s is not None:
+            await self.s.close()
+
+
+class InProcExtenderClient:
+    def __init__(self, ext):
+        self.ext = ext
+
+    async def filter(self, body):
+        return self.ext.filter(body)
+
+    async def prioritize(self, body):
+        return self.ext.prioritize(body)
+
+    async def bind(self, body):
+        return await self.ext.bind(body)
+
+    async def close(self):
+        return None
+
+
+@dataclass
+class PodRecord:
+    pod: dict
+    t_enqueue: float = 0.0
+    t_first_attempt: float = 0.0
+    t_bound: float = 0.0
+    bind_latency: float = 0.0
+    node: str = ""
+    attempts: int = 0
+    error: str = ""
+
+
+@dataclass
+class DriverStats:
+    scheduled: int = 0
+    failed: int = 0
+    unschedulable_attempts: int = 0
+    bind_errors: int = 0
+    bind_latencies: list = field(default_factory=list)
+    e2e_latencies: list = field(default_factory=list)
+    t_first_filter: float = 0.0
+    t_last_bind: float = 0.0
+
+    def summary(self) -> dict:
+        span = max(1e-9, self.t_last_bind - self.t_first_filter)
+        bl = sorted(self.bind_latencies)
+
+        def pct(a, q):
+            return a[min(len(a) - 1, int(q * len(a)))] if a else 0.0
+
+        return {"scheduled": self.scheduled, "failed": self.failed, "bind_errors": self.bind_errors,
+                "unschedulable_attempts": self.unschedulable_attempts,
+                "pods_per_s": self.scheduled / span if self.scheduled else 0.0, "span_s": span,
+                "bind_p50_ms": 1e3 * (statistics.median(bl) if bl else 0.0),
+                "bind_p99_ms": 1e3 * pct(bl, 0.99),
+                "e2e_p50_ms": 1e3 * (statistics.median(self.e2e_latencies) if self.e2e_latencies else 0.0)}
+
+
+class SchedulerDriver:
+    def __init__(self, client, api, node_names: list[str], node_capacity: dict[str, int] | None = None,
+                 max_inflight_binds: int = 64, seed: int = 0, max_attempts: int = 8,
+                 backoff_s: float = 0.001, resource_fit: bool = True, send_nodes: bool = False,
+                 node_objects: dict[str, dict] | None = None):
+        self.client = client
+        self.api = api
+        self.nodes = list(node_names)
+        self.node_objects = node_objects or {}
+        self.send_nodes = send_nodes
+        self.capacity = dict(node_capacity or {})
+        self.requested: dict[str, int] = {n: 0 for n in self.nodes}
+        self.resource_fit = resource_fit and bool(self.capacity)
+        self.rng = random.Random(seed)
+        self.sem = asyncio.Semaphore(max_inflight_binds)
+        self.max_attempts = max_attempts
+        self.backoff_s = backoff_s
+        self.stats = DriverStats()
+        self._binds: set[asyncio.Task] = set()
+        self.placements: dict[str, str] = {}
+
+    def _candidates(self, need: int) -> list[str]:
+        if not self.resource_fit:
+            return self.nodes
+        return [n for n in self.nodes if self.requested.get(n, 0) + need <= self.capacity.get(n, 0)]
+
+    async def schedule_one(self, rec: PodRecord) -> bool:
+        """One scheduling cycle. Returns True when a bind was issued."""
+        pod = rec.pod
+        need = sum(p for p, _ in pu.pod_demand(pod))
+        cands = self._candidates(need)
+        rec.attempts += 1
+        if not rec.t_first_attempt:
+            rec.t_first_attempt = time.perf_counter()
+            if not self.stats.t_first_filter:
+                self.stats.t_first_filter = rec.t_first_attempt
+        if not cands:
+            self.stats.unschedulable_attempts += 1
+            return False
+        if self.send_nodes:
+            args = {"Pod": pod, "Nodes": {"items": [self.node_objects[n] for n in cands]}, "NodeNames": None}
+        else:
+            args = {"Pod": pod, "Nodes": None, "NodeNames": cands}
+        fr = await self.client.filter(args)
+        if fr.get("Error"):
+            rec.error = fr["Error"]
+            return False
+        fit = fr.get("NodeNames")
+        if fit is None and fr.get("Nodes"):
+            fit = [pu.meta(n).get("name") for n in fr["Nodes"].get("items", [])]
+        if not fit:
+            self.stats.unschedulable_attempts += 1
+            return False
+        if len(fit) == 1:
+            host = fit[0]
+        else:
+            args2 = {"Pod": pod, "Nodes": None, "NodeNames": fit}
+            prios = await self.client.prioritize(args2)
+            best, host, seen = None, None, 0
+            for hp in prios:
+                s = hp["Score"]
+                if best is None or s > best:
+                    best, host, seen = s, hp["Host"], 1
+                elif s == best:
+                    seen += 1
+                    if self.rng.randrange(seen) == 0:   # reservoir sampling, as selectHost [ext]
+                        host = hp["Host"]
+        # kube-scheduler "assumes" the pod in its cache before binding asynchronously
+        self.requested[host] = self.requested.get(host, 0) + need
+        await self.sem.acquire()
+        t = asyncio.ensure_future(self._bind(rec, host, need))
+        self._binds.add(t)
+        t.add_done_callback(self._binds.discard)
+        return True
+
+    async def _bind(self, rec: PodRecord, host: str, need: int) -> None:
+        ns, name = pu.pod_ns_name(rec.pod)
+        t0 = time.perf_counter()
+        try:
+            res = await self.client.bind({"PodName": name, "PodNamespace": ns, "PodUID": pu.pod_uid(rec.pod),
+                                          "Node": host})
+        finally:
+            self.sem.release()
+        t1 = time.perf_counter()
+        if res.get("Error"):
+            self.requested[host] -= need
+            self.stats.bind_errors += 1
+            rec.error = res["Error"]
+            if rec.attempts < self.max_attempts:
+                await asyncio.sleep(self.backoff_s * (2 ** rec.attempts))
+                await self._queue.put(rec)
+            else:
+                self.stats.failed += 1
+                self._done.release()
+            return
+        rec.t_bound = t1
+        rec.bind_latency = t1 - t0
+        rec.node = host
+        self.placements[pu.pod_uid(rec.pod)] = host
+        self.stats.scheduled += 1
+        self.stats.bind_latencies.append(rec.bind_latency)
+        self.stats.e2e_latencies.append(t1 - rec.t_enqueue)
+        self.stats.t_last_bind = max(self.stats.t_last_bind, t1)
+        self._done.release()
+
+    def release(self, pod: dict) -> None:
+        """Scheduler cache update when a bound pod goes away."""
+        host = self.placements.pop(pu.pod_uid(pod), None)
+        if host:
+            self.requested[host] -= sum(p for p, _ in pu.pod_demand(pod))
+
+    async def run(self, pods: list[dict], create: bool = True) -> DriverStats:
+        """Creates `pods` through the API (if `create`) and schedules all of them."""
+        self._queue: asyncio.Queue[PodRecord] = asyncio.Queue()
+        self._done = asyncio.Semaphore(0)
+        now = time.perf_counter()
+        for p in pods:
+            if create:
+                await self.api.create_pod(p)
+            await self._queue.put(PodRecord(p, t_enqueue=now))
+        remaining = len(pods)
+
+        async def loop():
+            while True:
+                rec = await self._queue.get()
+                ok = False
+                try:
+                    ok = await self.schedule_one(rec)
+                except (aiohttp.ClientError, asyncio.TimeoutError) as e:
+                    rec.error = str(e)
+                if not ok:
+                    if rec.attempts < self.max_attempts:
+                        asyncio.get_running_loop().call_later(self.backoff_s * (2 ** rec.attempts),
+                                                              self._queue.put_nowait, rec)
+                    else:
+                        self.stats.failed += 1
+                        self._done.release()
+
+        task = asyncio.ensure_future(loop())
+        try:
+            for _ in range(remaining):
+                await self._done.acquire()
+        finally:
+            task.cancel()
+            try:
+                await task
+            except asyncio.CancelledError:
+                pass
+        return self.stats
+
+
+def node_capacities(nodes: list[dict]) -> dict[str, int]:
+    return {pu.meta(n)["name"]: pu.node_capacity_percent(n) for n in nodes}
+
+
+__all__ = ["SchedulerDriver", "HttpExtenderClient", "InProcExtenderClient", "node_capacities", "T"]

@@ -1,0 +1,281 @@
+"""Cluster GPU state: node registry + pod ledger over the native core.
+
+Reference: pkg/dealer/dealer.go (DealerImpl, 20-method Dealer interface :23-43) and
+pkg/dealer/node.go (NodeInfo + PlanCache). Differences by design:
+  * no global lock: the native ledger has per-node locks and per-node generations, and the
+    plan cache is keyed by generation instead of being wiped on every filter (node.go:96-98);
+  * bind is reserve -> (API I/O, no lock) -> commit | rollback (fixes D1/D2);
+  * delete events release (fixes D3); completed pods are skipped at rebuild (fixes D14);
+  * G = 0 nodes are unfit instead of a divide-by-zero panic (fixes D6);
+  * nodes re-register when capacity/topology change (fixes D20).
+"""
+from __future__ import annotations
+
+import hashlib
+import logging
+import threading
+import time
+from collections import OrderedDict
+from dataclasses import dataclass
+from typing import Callable
+
+from .. import types as T
+from ..k8s import podutil as pu
+from ..native import core
+from ..topology.model import NodeTopology, from_node
+
+log = logging.getLogger(__name__)
+N = core()
+
+POLICY_ENUM = {
+    T.PRIORITY_BINPACK: N.Policy.BINPACK,
+    T.PRIORITY_SPREAD: N.Policy.SPREAD,
+    T.PRIORITY_RANDOM: N.Policy.RANDOM,
+    T.PRIORITY_FIRSTFIT: N.Policy.FIRSTFIT,
+}
+
+
+class SchedulingError(Exception):
+    pass
+
+
+@dataclass
+class NodeEntry:
+    id: int
+    name: str
+    topology: NodeTopology
+    fingerprint: str
+
+
+def demand_hash_compat(demand) -> str:
+    """Reference PlanCache key: sha256 of "(p0)(p1)..." truncated to 8 hex (allocate.go:64-75)."""
+    s = "".join(f"({p})" for p, _ in demand)
+    return hashlib.sha256(s.encode()).hexdigest()[:8]
+
+
+class ClusterState:
+    def __init__(self, policy: str = T.PRIORITY_BINPACK, compat: bool = False,
+                 load_aware: bool = False, topo_weight: float = 1.0, seed: int = 0,
+                 ledger_path: str = "", max_nodes: int = 4096, max_pods: int = 131072,
+                 track_hbm: bool = True, node_source: Callable[[str], dict | None] | None = None,
+                 score_normalize: bool = False):
+        self.ledger = N.Ledger(ledger_path, max_nodes, max_pods, True)
+        self.track_hbm = track_hbm
+        self.score_normalize = score_normalize
+        self.node_source = node_source
+        self._nodes: dict[str, NodeEntry] = {}
+        self._nodes_mu = threading.Lock()
+        self._released: OrderedDict[str, None] = OrderedDict()   # reference ReleasedPodMap
+        self._released_cap = 65536
+        self.set_policy(policy, compat=compat, load_aware=load_aware, topo_weight=topo_weight, seed=seed)
+
+    # ------------------------------------------------------------------ policy
+    def set_policy(self, policy: str, compat: bool | None = None, load_aware: bool | None = None,
+                   topo_weight: float | None = None, seed: int | None = None) -> None:
+        if policy not in POLICY_ENUM:
+            raise ValueError(f"Priority algorithm {policy} is not supported")
+        old = getattr(self, "options", None)
+        self.policy = policy
+        self.options = N.Options(
+            POLICY_ENUM[policy],
+            compat=bool(compat if compat is not None else (old.compat if old else False)),
+            load_aware=bool(load_aware if load_aware is not None else (old.load_aware if old else False)),
+            topo_weight=float(topo_weight if topo_weight is not None else (old.topo_weight if old else 1.0)),
+            seed=int(seed if seed is not None else (old.seed if old else 0)))
+
+    # ------------------------------------------------------------------ nodes
+    def register_node(self, node: dict) -> NodeEntry:
+        """Registers/refreshes a Node object (capacity + `nano-gpu/topology` annotation)."""
+        name = pu.meta(node).get("name", "")
+        topo = from_node(node)
+        devices = topo.ledger_devices(self.track_hbm)
+        fp = hashlib.blake2b(repr((devices, topo.link_bw)).encode(), digest_size=8).hexdigest()
+        with self._nodes_mu:
+            cur = self._nodes.get(name)
+            if cur and cur.fingerprint == fp:
+                return cur
+        nid = self.ledger.upsert_node(name, devices, topo.ledger_topo()) if devices else \
+            self.ledger.upsert_node(name, [], None)
+        entry = NodeEntry(nid, name, topo, fp)
+        with self._nodes_mu:
+            self._nodes[name] = entry
+        return entry
+
+    def forget_node(self, name: str) -> bool:
+        with self._nodes_mu:
+            e = self._nodes.pop(name, None)
+        return bool(e) and self.ledger.remove_node(e.id)
+
+    def node_entry(self, name: str) -> NodeEntry | None:
+        e = self._nodes.get(name)
+        if e is not None:
+            return e
+        # another worker (shared ledger) may have registered it; otherwise ask the lister
+        if self.node_source is not None:
+            node = self.node_source(name)
+            if node is not None:
+                return self.register_node(node)
+        nid = self.ledger.find_node(name)
+        if nid >= 0:
+            snap = self.ledger.snapshot(nid)
+            topo = NodeTopology.from_dict({"devices": [{"gpu": d["gpu"], "part": d["part"], "cus": d["cus"],
+                                                        "xcds": d["xcds"], "hbm_mib": d["mib_total"]}
+                                                       for d in snap["devices"]],
+                                           "gpus": [], "link_bw": snap["topo"]["link_bw"]})
+            entry = NodeEntry(nid, name, topo, "shared")
+            with self._nodes_mu:
+                self._nodes[name] = entry
+            return entry
+        return None
+
+    def node_ids(self, names: list[str]) -> list[int]:
+        out = []
+        for n in names:
+            e = self.node_entry(n)
+            out.append(e.id if e else -1)
+        return out
+
+    # ------------------------------------------------------------------ verbs
+    def filter(self, pod: dict, node_names: list[str]) -> tuple[list[str], dict[str, str]]:
+        """Reference Dealer.Assume (dealer.go:89-136) + Predicate.Handler (predicate.go:19-41)."""
+        demand = pu.pod_demand(pod)
+        ids = self.node_ids(node_names)
+        rcs = self.ledger.filter(ids, demand, self.options)
+        ok, failed = [], {}
+        for name, nid, rc in zip(node_names, ids, rcs):
+            if rc == N.OK:
+                ok.append(name)
+            elif nid < 0:
+                failed[name] = f"nano gpu scheduler get node failed: node {name} not found"
+            else:
+                failed[name] = f"can't allocate {self._demand_str(demand)} on node {name}: {N.err_str(rc)}"
+        return ok, failed
+
+    def score(self, pod: dict, node_names: list[str]) -> list[int]:
+        """Reference Dealer.Score (dealer.go:138-153); ScoreMin (0) for unknown/unfit nodes."""
+        demand = pu.pod_demand(pod)
+        ids = self.node_ids(node_names)
+        scores = self.ledger.score(ids, demand, self.options)
+        if self.score_normalize and scores:
+            scores = self._normalize(scores)
+        return scores
+
+    def _normalize(self, scores: list[int]) -> list[int]:
+        """Maps to kube-scheduler's extender range [0, 10] (MaxExtenderPriority) [ext]."""
+        if self.options.compat:
+            lo, hi = min(scores), max(scores)
+            if hi == lo:
+                return [10 if hi > 0 else 0 for _ in scores]
+            return [int(round(10 * (s - lo) / (hi - lo))) for s in scores]
+        return [max(0, min(10, int(round(s / 10)))) for s in scores]
+
+    def reserve(self, pod: dict, node_name: str) -> tuple[list[list[int]], bool]:
+        """First half of bind: allocate on the ledger (node.go:70-84 + allocate.go:102-118).
+
+        Returns (plan, fresh); fresh is False when the pod was already allocated on that
+        node (a retried bind), in which case a later failure must not roll it back."""
+        e = self.node_entry(node_name)
+        if e is None:
+            raise SchedulingError(f"node {node_name} not found")
+        uid = pu.pod_uid(pod)
+        rc, plan = self.ledger.reserve(e.id, uid, pu.pod_demand(pod), self.options)
+        if rc not in (N.OK, N.OK_EXISTING):
+            raise SchedulingError(f"assume {self._demand_str(pu.pod_demand(pod))} on {node_name} failed: "
+                                  f"{N.err_str(rc)}")
+        return plan, rc == N.OK
+
+    def commit(self, uid: str) -> None:
+        self.ledger.commit(uid)
+
+    def rollback(self, uid: str) -> None:
+        self.ledger.release(uid)
+
+    def allocate_existing(self, pod: dict) -> bool:
+        """Account a pod placed by someone else / found at restart (dealer.go:205-228)."""
+        node = pu.node_name_of(pod)
+        if not node:
+            return False
+        plan = pu.plan_from_pod(pod)
+        if plan is None:
+            return False
+        e = self.node_entry(node)
+        if e is None:
+            log.warning("allocate %s: node %s unknown", pu.pod_key(pod), node)
+            return False
+        rc = self.ledger.allocate_plan(e.id, pu.pod_uid(pod), pu.pod_demand(pod), plan, True)
+        if rc != N.OK:
+            log.warning("allocate %s on %s failed: %s", pu.pod_key(pod), node, N.err_str(rc))
+            return False
+        return True
+
+    def release(self, pod: dict) -> bool:
+        return self.release_uid(pu.pod_uid(pod))
+
+    def release_uid(self, uid: str) -> bool:
+        rc = self.ledger.release(uid)
+        if rc == N.OK:
+            self._released[uid] = None
+            if len(self._released) > self._released_cap:
+                self._released.popitem(last=False)
+            return True
+        return False
+
+    def known(self, uid: str) -> bool:
+        return self.ledger.lookup(uid) is not None
+
+    def released(self, uid: str) -> bool:
+        return uid in self._released
+
+    def forget(self, uid: str) -> None:
+        self._released.pop(uid, None)
+
+    def rebuild(self, pods: list[dict]) -> int:
+        """Checkpoint/resume: the API server is the checkpoint (dealer.go:58-72, 279-299)."""
+        n = 0
+        for p in pods:
+            if pu.is_assumed(p) and pu.node_name_of(p) and not pu.is_completed(p):
+                n += int(self.allocate_existing(p))
+        return n
+
+    def sweep_reservations(self, ttl_s: float) -> list[str]:
+        """Releases reservations whose bind never committed (crashed worker, lost request)."""
+        stale = self.ledger.expired_reservations(ttl_s)
+        for uid in stale:
+            self.ledger.release(uid)
+        return stale
+
+    # ------------------------------------------------------------------ telemetry
+    def set_load(self, node_name: str, device: int, usage: float) -> bool:
+        e = self._nodes.get(node_name)
+        return bool(e) and self.ledger.set_load(e.id, device, float(usage)) == N.OK
+
+    # ------------------------------------------------------------------ introspection
+    def frag(self, min_request: int = 0) -> dict:
+        return self.ledger.frag(min_request)
+
+    def status(self) -> dict:
+        """`/status` body in the reference's shape (NodeInfo JSON: routes.go:212-240)."""
+        out = {}
+        for name, e in list(self._nodes.items()):
+            snap = self.ledger.snapshot(e.id)
+            if snap is None:
+                continue
+            out[name] = {
+                "Rater": {},
+                "Name": name,
+                "GPUs": [{"Percent": d["pct_free"], "PercentTotal": d["pct_total"],
+                          "RemainLoad": d["remain_load"], "MemoryMiB": d["mib_free"],
+                          "MemoryMiBTotal": d["mib_total"], "GPU": d["gpu"], "Partition": d["part"],
+                          "Healthy": d["healthy"]} for d in snap["devices"]],
+                "PlanCache": {},
+                "Generation": snap["generation"],
+            }
+        return out
+
+    @staticmethod
+    def _demand_str(demand) -> str:
+        return "".join(f"({p})" if not m else f"({p},{m}Mi)" for p, m in demand)
+
+
+def now() -> float:
+    return time.monotonic()

@@ -1,0 +1,211 @@
+"""Node GPU topology model: what the node agent publishes and the extender schedules on.
+
+Reference: the reference knows only a GPU count, ⌊capacity/100⌋ (pkg/utils/node.go:8-14),
+and every device is a 100% slot (pkg/dealer/node.go:25-42). Here a node carries a
+`nano-gpu/topology` annotation (JSON, schema below) written by the node agent from the
+native reader (native/src/topo.cpp). The schedulable *device* is a compute partition
+(SPX: the whole MI355X; DPX/QPX/CPX: 2/4/8 partitions of its 8 XCDs); every device still
+counts 100 gpu-percent, so node capacity stays `100 x devices` and the reference
+annotation contract (`nano-gpu/container-<c>=<device index>`) is unchanged.
+
+Schema (version 1):
+{
+  "version": 1, "model": "AMD Instinct MI355X", "gfx": "gfx950",
+  "virtualization": "BAREMETAL",
+  "gpus":    [{"index": 0, "numa": 0, "cus": 256, "xcds": 8, "hbm_mib": 294912,
+               "compute_partition": "SPX", "memory_partition": "NPS1", "bdf": "0000:05:00.0"}],
+  "devices": [{"gpu": 0, "part": 0, "cus": 256, "xcds": 8, "hbm_mib": 294912}],
+  "link_bw": [[0.0, 153.0, ...], ...],     # GB/s between physical GPUs (0 = no direct link)
+  "calibration": {...}                      # optional probe results (HBM GB/s, CU map)
+}
+"""
+from __future__ import annotations
+
+import json
+from dataclasses import dataclass, field
+from typing import Any
+
+from .. import types as T
+
+PARTITIONS = {"SPX": 1, "DPX": 2, "TPX": 3, "QPX": 4, "CPX": 8}
+
+
+@dataclass
+class GpuSpec:
+    index: int
+    numa: int = -1
+    cus: int = T.MI355X_CUS
+    xcds: int = T.MI355X_XCDS
+    hbm_mib: int = 0
+    compute_partition: str = "SPX"
+    memory_partition: str = "NPS1"
+    bdf: str = ""
+
+
+@dataclass
+class DeviceSpec:
+    gpu: int
+    part: int = 0
+    cus: int = T.MI355X_CUS
+    xcds: int = T.MI355X_XCDS
+    hbm_mib: int = 0
+
+
+@dataclass
+class NodeTopology:
+    gpus: list[GpuSpec]
+    devices: list[DeviceSpec]
+    link_bw: list[list[float]] = field(default_factory=list)
+    model: str = "AMD Instinct MI355X"
+    gfx: str = "gfx950"
+    virtualization: str = "UNKNOWN"
+    calibration: dict = field(default_factory=dict)
+    version: int = 1
+
+    # --- serialisation -------------------------------------------------------------
+    def to_dict(self) -> dict:
+        return {
+            "version": self.version, "model": self.model, "gfx": self.gfx,
+            "virtualization": self.virtualization,
+            "gpus": [g.__dict__ for g in self.gpus],
+            "devices": [d.__dict__ for d in self.devices],
+            "link_bw": self.link_bw,
+            "calibration": self.calibration,
+        }
+
+    def to_json(self) -> str:
+        return json.dumps(self.to_dict(), separators=(",", ":"), sort_keys=True)
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "NodeTopology":
+        gpus = [GpuSpec(**{k: v for k, v in g.items() if k in GpuSpec.__dataclass_fields__})
+                for g in d.get("gpus", [])]
+        devs = [DeviceSpec(**{k: v for k, v in x.items() if k in DeviceSpec.__dataclass_fields__})
+                for x in d.get("devices", [])]
+        if not devs:
+            devs = [DeviceSpec(gpu=g.index, cus=g.cus, xcds=g.xcds, hbm_mib=g.hbm_mib) for g in gpus]
+        return cls(gpus=gpus, devices=devs, link_bw=[list(map(float, r)) for r in d.get("link_bw", [])],
+                   model=d.get("model", ""), gfx=d.get("gfx", ""),
+                   virtualization=d.get("virtualization", "UNKNOWN"),
+                   calibration=d.get("calibration") or {}, version=int(d.get("version", 1)))
+
+    @classmethod
+    def from_json(cls, s: str) -> "NodeTopology":
+        return cls.from_dict(json.loads(s))
+
+    # --- ledger views ----------------------------------------------------------------
+    @property
+    def n_gpus(self) -> int:
+        return len(self.gpus)
+
+    def ledger_devices(self, track_hbm: bool = True) -> list[dict]:
+        numa = {g.index: g.numa for g in self.gpus}
+        return [{"pct_total": T.GPU_PERCENT_EACH_CARD, "mib_total": d.hbm_mib if track_hbm else 0,
+                 "gpu": d.gpu, "part": d.part, "numa": numa.get(d.gpu, -1), "healthy": True,
+                 "xcds": d.xcds, "cus": d.cus} for d in self.devices]
+
+    def ledger_topo(self) -> dict:
+        return {"n_gpus": self.n_gpus, "numa": [g.numa for g in self.gpus], "link_bw": self.link_bw}
+
+
+def fallback_topology(n_devices: int) -> NodeTopology:
+    """Reference behaviour (node.go:25-42): N anonymous 100% devices, no HBM, no links."""
+    gpus = [GpuSpec(index=i, hbm_mib=0) for i in range(n_devices)]
+    return NodeTopology(gpus=gpus, devices=[DeviceSpec(gpu=i, hbm_mib=0) for i in range(n_devices)],
+                        link_bw=[[0.0] * n_devices for _ in range(n_devices)], model="", gfx="")
+
+
+def synthetic_mi355x(n_gpus: int = 8, compute: str = "SPX", memory: str = "NPS1",
+                     hbm_mib: int = 288 * 1024, link_gbs: float = 153.0,
+                     gpus_per_numa: int = 4) -> NodeTopology:
+    """An 8x MI355X platform (full xGMI mesh, 4 GPUs per socket) for tests and benches.
+
+    `link_gbs` is a placeholder until the probe measures it; the agent overwrites it with
+    what KFD/amdsmi or the peer-copy probe report.
+    """
+    parts = PARTITIONS[compute]
+    gpus, devs = [], []
+    for g in range(n_gpus):
+        gpus.append(GpuSpec(index=g, numa=g // max(1, gpus_per_numa), hbm_mib=hbm_mib,
+                            compute_partition=compute, memory_partition=memory,
+                            bdf=f"0000:{0x05 + 0x10 * g:02x}:00.0"))
+        for p in range(parts):
+            devs.append(DeviceSpec(gpu=g, part=p, cus=T.MI355X_CUS // parts,
+                                   xcds=max(1, T.MI355X_XCDS // parts), hbm_mib=hbm_mib // parts))
+    bw = [[0.0 if a == b else link_gbs for b in range(n_gpus)] for a in range(n_gpus)]
+    return NodeTopology(gpus=gpus, devices=devs, link_bw=bw, virtualization="BAREMETAL")
+
+
+def from_host_json(host: str | dict) -> NodeTopology:
+    """Converts the native reader's JSON (nanogpu-topo / _native.discover_topology)."""
+    h = json.loads(host) if isinstance(host, str) else host
+    gpus_by_parent: dict[int, GpuSpec] = {}
+    devices: list[DeviceSpec] = []
+    kfd_parent: dict[int, int] = {}
+    for g in h.get("gpus", []):
+        parent = int(g.get("parent", 0))
+        kfd_parent[int(g.get("kfd_node", -1))] = parent
+        part = int(g.get("partition", 0))
+        cp = (g.get("compute_partition") or "SPX").upper() or "SPX"
+        mib = int(g.get("vram_bytes", 0)) // (1 << 20)
+        if parent not in gpus_by_parent:
+            loc = int(g.get("location_id", 0))
+            gpus_by_parent[parent] = GpuSpec(
+                index=parent, numa=int(g.get("numa", -1)), cus=0, xcds=0, hbm_mib=0,
+                compute_partition=cp, memory_partition=(g.get("memory_partition") or "").upper(),
+                bdf=f"{int(g.get('domain', 0)):04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7}")
+        gs = gpus_by_parent[parent]
+        gs.cus += int(g.get("cus", 0))
+        gs.xcds += int(g.get("num_xcc", 1))
+        devices.append(DeviceSpec(gpu=parent, part=part, cus=int(g.get("cus", 0)),
+                                  xcds=int(g.get("num_xcc", 1)), hbm_mib=mib))
+    # HBM: in NPS1 every partition reports the whole pool; split it evenly for accounting.
+    for parent, gs in gpus_by_parent.items():
+        ds = [d for d in devices if d.gpu == parent]
+        total = max((d.hbm_mib for d in ds), default=0)
+        if ds and all(d.hbm_mib == total for d in ds) and len(ds) > 1:
+            for d in ds:
+                d.hbm_mib = total // len(ds)
+            gs.hbm_mib = total
+        else:
+            gs.hbm_mib = sum(d.hbm_mib for d in ds)
+    n = len(gpus_by_parent)
+    bw = [[0.0] * n for _ in range(n)]
+    for lk in h.get("links", []):
+        a, b = kfd_parent.get(int(lk.get("from", -1))), kfd_parent.get(int(lk.get("to", -1)))
+        if a is None or b is None or a == b:
+            continue
+        gbs = float(lk.get("max_bw_mbs", 0)) / 1000.0
+        if gbs <= 0 and int(lk.get("weight", 0)) > 0:
+            gbs = 1000.0 / float(lk["weight"])  # relative weight when bandwidth is not exposed
+        bw[a][b] = max(bw[a][b], gbs)
+    gpus = [gpus_by_parent[i] for i in sorted(gpus_by_parent)]
+    gfx = ""
+    if h.get("gpus"):
+        v = int(h["gpus"][0].get("gfx_target_version", 0))
+        if v:
+            gfx = f"gfx{v // 10000}{(v // 100) % 100:x}{v % 100:x}" if v >= 90000 else f"gfx{v}"
+    return NodeTopology(gpus=gpus, devices=devices, link_bw=bw, virtualization=h.get("virtualization", "UNKNOWN"),
+                        model="AMD Instinct MI355X" if gfx == "gfx950" else (gfx or "unknown"), gfx=gfx)
+
+
+def from_node(node: dict) -> NodeTopology:
+    """Topology annotation if present and consistent, else the reference fallback."""
+    from ..k8s.podutil import meta, node_gpu_count
+
+    ann = (meta(node).get("annotations") or {}).get(T.ANNOTATION_TOPOLOGY)
+    count = node_gpu_count(node)
+    if ann:
+        try:
+            t = NodeTopology.from_json(ann)
+            if t.devices and (count == 0 or len(t.devices) == count):
+                return t
+        except (ValueError, TypeError, KeyError):
+            pass
+    return fallback_topology(count)
+
+
+def describe(t: NodeTopology) -> dict[str, Any]:
+    return {"gpus": t.n_gpus, "devices": len(t.devices),
+            "partition": t.gpus[0].compute_partition if t.gpus else "",
+            "hbm_mib_total": sum(d.hbm_mib for d in t.devices), "gfx": t.gfx}

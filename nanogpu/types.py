@@ -1,0 +1,53 @@
+"""Resource names, annotation keys and constants (wire-compatible with the reference).
+
+Reference: pkg/types/types.go:7-21, pkg/dealer/type.go:5-9, pkg/controller/node.go:18-24.
+"""
+from __future__ import annotations
+
+# --- reference contract (kept byte-identical) -------------------------------------
+RESOURCE_GPU_PERCENT = "nano-gpu/gpu-percent"          # types.go:9
+GPU_PERCENT_EACH_CARD = 100                            # types.go:10
+GPU_ASSUME = "nano-gpu/assume"                         # types.go:12-14 (annotation AND label)
+ANNOTATION_GPU_ASSUME = GPU_ASSUME
+LABEL_GPU_ASSUME = GPU_ASSUME
+ANNOTATION_CONTAINER_FMT = "nano-gpu/container-{}"     # types.go:15 ("nano-gpu/container-%s")
+NODE_NAME_FIELD = "spec.nodeName"                      # types.go:8
+PRIORITY_BINPACK = "binpack"                           # types.go:19
+PRIORITY_SPREAD = "spread"                             # types.go:20
+NOT_NEED_GPU = -1                                      # allocate.go:15
+LOAD_TOTAL = 2                                         # allocate.go:16
+SCORE_MIN = 0                                          # rater.go:12
+SCORE_MAX = 100                                        # rater.go:13
+VERSION = "0.1.0"                                      # routes.go:30 (compat /version)
+FRAMEWORK_VERSION = "0.1.0-mi355x"
+
+GPU_CORE_USAGE_METRIC = "gpu_core_usage_avg"           # type.go:7
+GPU_MEMORY_USAGE_METRIC = "gpu_memory_usage_avg"       # type.go:8
+EXTENDER_ACTIVE_PERIOD_S = 300.0                       # type.go:6 (5 minutes)
+LEGACY_GPU_NODE_LABEL = ("nvidia-device-enable", "enable")  # controller/node.go:153-158
+
+# --- MI355X-native additions --------------------------------------------------------
+PRIORITY_RANDOM = "random"        # promised by reference README.md:14, absent in its code
+PRIORITY_FIRSTFIT = "firstfit"    # reference SampleRater (rater.go:21-50), test-only there
+POLICIES = (PRIORITY_BINPACK, PRIORITY_SPREAD, PRIORITY_RANDOM, PRIORITY_FIRSTFIT)
+
+RESOURCE_GPU_MEMORY = "nano-gpu/gpu-memory"   # HBM MiB per container (288 GB / MI355X)
+ANNOTATION_TOPOLOGY = "nano-gpu/topology"     # node: JSON from the node agent (topology.model)
+ANNOTATION_CU_MASK_FMT = "nano-gpu/cu-mask-{}"  # pod: per-container CU mask chosen by the agent
+ANNOTATION_ASSUME_TIME = "nano-gpu/assume-time"
+ANNOTATION_SCHEDULER = "nano-gpu/scheduler"
+AMD_GPU_NODE_LABEL = ("amd.com/gpu.present", "true")   # default telemetry node selector
+
+MI355X_CUS = 256
+MI355X_XCDS = 8
+MI355X_HBM_BYTES = 288 * 1000 ** 3   # datasheet; the agent reads the real value
+
+DEFAULT_PORT = 39999                 # cmd/main.go:96-99
+DEFAULT_POLICY_PATH = "/data/policy.yaml"          # cmd/main.go:34
+DEFAULT_PROMETHEUS_URL = "http://thanos-prometheus.kube-system:80"  # cmd/main.go:66-67
+FILTER_NODE_CACHE_ERROR = ("nano-gpu-scheduler extender must be configured with "
+                           "nodeCacheCapable=true")   # routes.go:66
+
+
+def container_annotation(name: str) -> str:
+    return ANNOTATION_CONTAINER_FMT.format(name)

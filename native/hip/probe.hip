@@ -1,0 +1,278 @@
+// nanogpu._probe — MI355X (gfx950) calibration kernels for the node agent.
+//
+// The reference scheduler never touches a GPU; it trusts an external NVIDIA device plugin
+// to realise "gpu-percent" (reference README.md:9, 30-34). On MI355X the agent realises a
+// fractional grant spatially: a container with p% of a device gets a CU mask covering
+// ceil(p/100 * CUs) compute units, XCD-aligned where possible (each XCD has its own 4 MiB
+// L2, so a grant that owns whole XCDs keeps its L2 to itself). These kernels measure the
+// facts that mapping needs, on the real device:
+//   * cu_census   — which XCD / SE / CU each CU-mask bit enables (s_getreg XCC_ID, HW_ID);
+//   * mfma_burn   — bf16 MFMA throughput of a masked stream (isolation check: TFLOP/s
+//                   must scale with the CUs granted);
+//   * hbm_copy    — streaming HBM3E bandwidth (16 B/lane, grid >> 256 WGs);
+//   * peer_copy   — xGMI peer bandwidth between two GPUs (link weights for the scorer).
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace py = pybind11;
+
+#define HIP_OK(expr)                                                                    \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      throw std::runtime_error(std::string(#expr) + ": " + hipGetErrorString(e_));      \
+  } while (0)
+
+namespace {
+
+// ---------------------------------------------------------------------------- kernels
+
+__global__ __launch_bounds__(256) void hbm_copy(const float4* __restrict__ src,
+                                                float4* __restrict__ dst, size_t n) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+    dst[i] = src[i];
+}
+
+// One record per workgroup: {xcc_id, hw_id, block}. A bounded sleep keeps each workgroup
+// resident long enough that the dispatcher spreads the grid over every enabled CU.
+__global__ __launch_bounds__(64) void cu_census(uint32_t* out, int sleep_iters) {
+  if (threadIdx.x != 0) return;
+  uint32_t xcc, hwid;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+  for (int i = 0; i < sleep_iters; ++i) __builtin_amdgcn_s_sleep(16);
+  out[3 * blockIdx.x + 0] = xcc;
+  out[3 * blockIdx.x + 1] = hwid;
+  out[3 * blockIdx.x + 2] = blockIdx.x;
+}
+
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+
+// MFMA-bound burn: 4 independent 32x32x16 bf16 accumulator chains per wave hide the
+// dependent-accumulator latency; each MFMA is 2*32*32*16 = 32768 FLOP.
+__global__ __launch_bounds__(256) void mfma_burn(float* out, int iters) {
+  const int lane = threadIdx.x & 63;
+  bf16x8 a, b;
+  for (int j = 0; j < 8; ++j) {
+    a[j] = static_cast<__bf16>(0.001f * static_cast<float>((lane + j) & 7));
+    b[j] = static_cast<__bf16>(0.002f * static_cast<float>((lane * 3 + j) & 7));
+  }
+  f32x16 c0 = {}, c1 = {}, c2 = {}, c3 = {};
+  for (int i = 0; i < iters; ++i) {
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, a, c1, 0, 0, 0);
+    c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, a, c2, 0, 0, 0);
+    c3 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, b, c3, 0, 0, 0);
+  }
+  float s = 0.f;
+  for (int r = 0; r < 16; ++r) s += c0[r] + c1[r] + c2[r] + c3[r];
+  if (s == 12345.678f) out[blockIdx.x * blockDim.x + threadIdx.x] = s;  // keeps the chains live
+}
+
+// ---------------------------------------------------------------------------- host helpers
+
+struct Stream {
+  hipStream_t s = nullptr;
+  explicit Stream(const std::vector<uint32_t>& mask) {
+    if (mask.empty())
+      HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    else
+      HIP_OK(hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(mask.size()), mask.data()));
+  }
+  ~Stream() {
+    if (s) (void)hipStreamDestroy(s);
+  }
+};
+
+struct Events {
+  hipEvent_t a = nullptr, b = nullptr;
+  Events() {
+    HIP_OK(hipEventCreate(&a));
+    HIP_OK(hipEventCreate(&b));
+  }
+  ~Events() {
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+  }
+  float ms() {
+    HIP_OK(hipEventSynchronize(b));
+    float t = 0.f;
+    HIP_OK(hipEventElapsedTime(&t, a, b));
+    return t;
+  }
+};
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  explicit DevBuf(size_t n) { HIP_OK(hipMalloc(&p, n * sizeof(T))); }
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+int cu_count(int dev) {
+  int n = 0;
+  HIP_OK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+  return n;
+}
+
+py::dict device_props(int dev) {
+  hipDeviceProp_t p;
+  HIP_OK(hipGetDeviceProperties(&p, dev));
+  py::dict d;
+  d["name"] = std::string(p.name);
+  d["gcn_arch"] = std::string(p.gcnArchName);
+  d["cus"] = p.multiProcessorCount;
+  d["total_mem_bytes"] = static_cast<uint64_t>(p.totalGlobalMem);
+  d["l2_bytes"] = p.l2CacheSize;
+  d["lds_per_block_bytes"] = static_cast<uint64_t>(p.sharedMemPerBlock);
+  d["max_shared_per_cu_bytes"] = static_cast<uint64_t>(p.maxSharedMemoryPerMultiProcessor);
+  d["warp_size"] = p.warpSize;
+  d["clock_khz"] = p.clockRate;
+  d["mem_clock_khz"] = p.memoryClockRate;
+  d["mem_bus_width"] = p.memoryBusWidth;
+  d["pci_bus"] = p.pciBusID;
+  d["pci_device"] = p.pciDeviceID;
+  d["pci_domain"] = p.pciDomainID;
+  d["multi_gpu_board"] = p.isMultiGpuBoard;
+  int count = 0;
+  HIP_OK(hipGetDeviceCount(&count));
+  d["device_count"] = count;
+  return d;
+}
+
+double hbm_bandwidth(int dev, size_t bytes, int iters) {
+  HIP_OK(hipSetDevice(dev));
+  const size_t n = bytes / sizeof(float4);
+  if (n == 0 || iters <= 0) throw std::invalid_argument("hbm_bandwidth: bytes/iters must be positive");
+  DevBuf<float4> a(n), b(n);
+  HIP_OK(hipMemset(a.p, 0, n * sizeof(float4)));
+  Stream st({});
+  Events ev;
+  const int blocks = cu_count(dev) * 8;
+  hipLaunchKernelGGL(hbm_copy, dim3(blocks), dim3(256), 0, st.s, a.p, b.p, n);  // warm-up
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(ev.a, st.s));
+  for (int i = 0; i < iters; ++i)
+    hipLaunchKernelGGL(hbm_copy, dim3(blocks), dim3(256), 0, st.s, a.p, b.p, n);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(ev.b, st.s));
+  const double ms = ev.ms();
+  return 2.0 * static_cast<double>(n * sizeof(float4)) * iters / (ms * 1e-3) / 1e9;  // GB/s, read+write
+}
+
+py::list census(int dev, const std::vector<uint32_t>& mask, int blocks, int sleep_iters) {
+  HIP_OK(hipSetDevice(dev));
+  if (blocks <= 0 || blocks > (1 << 20)) throw std::invalid_argument("census: bad block count");
+  DevBuf<uint32_t> out(static_cast<size_t>(blocks) * 3);
+  HIP_OK(hipMemset(out.p, 0xff, static_cast<size_t>(blocks) * 3 * sizeof(uint32_t)));
+  Stream st(mask);
+  hipLaunchKernelGGL(cu_census, dim3(blocks), dim3(64), 0, st.s, out.p, sleep_iters);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipStreamSynchronize(st.s));
+  std::vector<uint32_t> h(static_cast<size_t>(blocks) * 3);
+  HIP_OK(hipMemcpy(h.data(), out.p, h.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  py::list res;
+  for (int i = 0; i < blocks; ++i) res.append(py::make_tuple(h[3 * i], h[3 * i + 1]));
+  return res;
+}
+
+double mfma_ms_impl(int dev, const std::vector<uint32_t>& mask, int blocks, int iters);
+inline double mfma_ms(int dev, const std::vector<uint32_t>& mask, int blocks, int iters) {
+  return mfma_ms_impl(dev, mask, blocks, iters);
+}
+
+py::dict mfma_throughput(int dev, const std::vector<uint32_t>& mask, int blocks, int iters) {
+  double ms = 0.0;
+  {
+    py::gil_scoped_release nogil;  // device work without the GIL; py objects built after
+    ms = mfma_ms(dev, mask, blocks, iters);
+  }
+  const double flop = 4.0 * 32768.0 * iters * (static_cast<double>(blocks) * 256 / 64);
+  py::dict d;
+  d["ms"] = ms;
+  d["tflops"] = flop / (ms * 1e-3) / 1e12;
+  d["blocks"] = blocks;
+  d["iters"] = iters;
+  return d;
+}
+
+double mfma_ms_impl(int dev, const std::vector<uint32_t>& mask, int blocks, int iters) {
+  HIP_OK(hipSetDevice(dev));
+  if (blocks <= 0 || iters <= 0) throw std::invalid_argument("mfma_throughput: bad shape");
+  DevBuf<float> out(static_cast<size_t>(blocks) * 256);
+  Stream st(mask);
+  Events ev;
+  hipLaunchKernelGGL(mfma_burn, dim3(blocks), dim3(256), 0, st.s, out.p, 8);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(ev.a, st.s));
+  hipLaunchKernelGGL(mfma_burn, dim3(blocks), dim3(256), 0, st.s, out.p, iters);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(ev.b, st.s));
+  return ev.ms();
+}
+
+double peer_bandwidth(int src, int dst, size_t bytes, int iters) {
+  int n = 0;
+  HIP_OK(hipGetDeviceCount(&n));
+  if (src < 0 || dst < 0 || src >= n || dst >= n || src == dst)
+    throw std::invalid_argument("peer_bandwidth: need two distinct visible devices");
+  int can = 0;
+  HIP_OK(hipDeviceCanAccessPeer(&can, dst, src));
+  HIP_OK(hipSetDevice(dst));
+  if (can) {
+    hipError_t e = hipDeviceEnablePeerAccess(src, 0);
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIP_OK(e);
+    (void)hipGetLastError();
+  }
+  void* d_dst = nullptr;
+  HIP_OK(hipMalloc(&d_dst, bytes));
+  HIP_OK(hipSetDevice(src));
+  void* d_src = nullptr;
+  HIP_OK(hipMalloc(&d_src, bytes));
+  Stream st({});
+  Events ev;
+  HIP_OK(hipMemcpyPeerAsync(d_dst, dst, d_src, src, bytes, st.s));
+  HIP_OK(hipEventRecord(ev.a, st.s));
+  for (int i = 0; i < iters; ++i) HIP_OK(hipMemcpyPeerAsync(d_dst, dst, d_src, src, bytes, st.s));
+  HIP_OK(hipEventRecord(ev.b, st.s));
+  const double ms = ev.ms();
+  (void)hipFree(d_src);
+  HIP_OK(hipSetDevice(dst));
+  (void)hipFree(d_dst);
+  return static_cast<double>(bytes) * iters / (ms * 1e-3) / 1e9;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_probe, m) {
+  m.doc() = "MI355X calibration kernels (gfx950): CU census, MFMA burn, HBM and xGMI bandwidth";
+  m.def("device_count", []() {
+    int n = 0;
+    HIP_OK(hipGetDeviceCount(&n));
+    return n;
+  });
+  m.def("device_props", &device_props, py::arg("device") = 0);
+  m.def("hbm_bandwidth", &hbm_bandwidth, py::arg("device") = 0, py::arg("bytes") = size_t(1) << 30,
+        py::arg("iters") = 10, py::call_guard<py::gil_scoped_release>(),
+        "Streaming copy bandwidth in GB/s (read + write bytes).");
+  m.def("cu_census", &census, py::arg("device") = 0, py::arg("cu_mask") = std::vector<uint32_t>{},
+        py::arg("blocks") = 2048, py::arg("sleep_iters") = 64,
+        "Per-workgroup (xcc_id, hw_id) for a launch on a CU-masked stream.");
+  m.def("mfma_throughput", &mfma_throughput, py::arg("device") = 0,
+        py::arg("cu_mask") = std::vector<uint32_t>{}, py::arg("blocks") = 2048, py::arg("iters") = 2048,
+        "bf16 MFMA TFLOP/s on a CU-masked stream.");
+  m.def("peer_bandwidth", &peer_bandwidth, py::arg("src"), py::arg("dst"),
+        py::arg("bytes") = size_t(256) << 20, py::arg("iters") = 10,
+        py::call_guard<py::gil_scoped_release>(), "hipMemcpyPeer bandwidth in GB/s.");
+}

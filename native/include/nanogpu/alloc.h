@@ -1,0 +1,132 @@
+// Allocation algebra for fine-grained AMD Instinct scheduling.
+//
+// Reference parity map (reference = alex337/nano-gpu-scheduler):
+//   Device            ~ GPUResource{Percent, PercentTotal, RemainLoad}  pkg/dealer/allocate.go:141-161
+//   Demand            ~ Demand ([]GPUResource, one per container)      pkg/dealer/allocate.go:52-62
+//   Plan              ~ Plan{Demand, GPUIndexes, Score}                 pkg/dealer/allocate.go:23-27
+//   choose()/rate()   ~ Rater.Choose / Rater.Rate                       pkg/dealer/rater.go:16-163
+//   apply()/unapply() ~ GPUs.Allocate / GPUs.Release                    pkg/dealer/allocate.go:102-131
+//
+// MI355X-first extensions (not in the reference):
+//   * a second resource dimension, HBM MiB (288 GB per MI355X; read, never assumed);
+//   * schedulable devices may be compute partitions (SPX/DPX/QPX/CPX) that record
+//     their parent physical GPU, NUMA node, XCD and CU counts;
+//   * containers may request whole devices (gpu-percent 200, 300, ... => k devices),
+//     chosen as a set by an xGMI-link / partition-sibling / NUMA topology score;
+//   * native policies (best-fit binpack, worst-fit spread, random, first-fit) that
+//     are deterministic and HBM-aware, next to a bit-exact `compat` (Go 1.16) mode.
+#pragma once
+
+#include <cstdint>
+#include <string>
+
+namespace nanogpu {
+
+constexpr int kMaxDevs = 64;         // 8 GPUs x CPX (8 XCD partitions each)
+constexpr int kMaxGpus = 16;         // physical GPUs per node
+constexpr int kMaxContainers = 16;   // containers per pod
+constexpr int kMaxPlanIdx = 64;      // device indices per pod plan
+constexpr int kNotNeedGPU = -1;      // reference NotNeedGPU, allocate.go:15
+constexpr int kLoadTotal = 2;        // reference LoadTotal, allocate.go:16
+constexpr int kPercentPerDevice = 100;
+
+enum class Policy : int32_t { kBinpack = 0, kSpread = 1, kRandom = 2, kFirstFit = 3 };
+
+enum Err : int32_t {
+  kOk = 0,
+  kErrNoFit = 1,         // demand cannot be placed on this node
+  kErrNoDevices = 2,     // node advertises no devices (reference divides by zero: rater.go:68)
+  kErrBadPlan = 3,       // plan indices out of range / shape mismatch
+  kErrPlanNoLongerFits = 4,
+  kErrUnknownNode = 5,
+  kErrUnknownPod = 6,
+  kErrPodExists = 7,     // pod already allocated on a different node
+  kErrTableFull = 8,
+  kErrBadDemand = 9,
+  kOkExisting = 10,      // not an error: the pod was already reserved/committed on that node
+};
+
+const char* err_str(int32_t e);
+
+struct Device {
+  int32_t pct_free;
+  int32_t pct_total;
+  int64_t mib_free;
+  int64_t mib_total;    // 0 => HBM not tracked on this device
+  float load_usage;     // sum over fresh metrics of ceil(10u)/10 (reference allocate.go:173-195)
+  int16_t remain_load;  // reference RemainLoad = LoadTotal - int(load_usage)
+  int16_t gpu;          // physical GPU index within the node
+  int16_t part;         // partition index within the physical GPU (0 in SPX)
+  int16_t numa;         // NUMA node of the GPU, -1 unknown
+  int16_t healthy;      // 0 => never chosen
+  int16_t xcds;         // XCDs backing this device (8 for an SPX MI355X, 1 in CPX)
+  int32_t cus;          // compute units backing this device (256 for SPX MI355X)
+};
+
+struct Topology {
+  int32_t n_gpus;
+  int16_t numa[kMaxGpus];
+  float link_bw[kMaxGpus * kMaxGpus];  // GB/s between physical GPUs, 0 = no direct link
+};
+
+struct ContainerDemand {
+  int32_t pct;   // 0 => no GPU; <=100 => share of one device; k*100 => k whole devices
+  int32_t pad;
+  int64_t mib;   // HBM MiB requested (per device for whole-device requests it is ignored)
+};
+
+struct Demand {
+  int32_t n;
+  int32_t pad;
+  ContainerDemand c[kMaxContainers];
+  uint64_t hash() const;
+};
+
+struct Plan {
+  int32_t n;                          // containers
+  int32_t score;
+  int16_t off[kMaxContainers + 1];    // container c uses idx[off[c] .. off[c+1])
+  int16_t idx[kMaxPlanIdx];           // device indices; a single -1 for "no GPU"
+};
+
+struct Options {
+  Policy policy = Policy::kBinpack;
+  int32_t compat = 0;        // 1 => reproduce the reference (Go 1.16) bit for bit
+  int32_t load_aware = 0;    // reference --isLoadSchedule
+  float topo_weight = 1.0f;  // weight of the xGMI/partition term in native mode
+  uint64_t seed = 0;         // random policy seed (mixed with the demand hash)
+  uint64_t hash() const;
+};
+
+// Devices needed by one container (0 for "no GPU").
+int devices_needed(const ContainerDemand& c);
+
+// Computes a placement for `d` on `devs` (not modified). Returns kOk and fills `plan`
+// (including plan->score from rate()), or an error code.
+int32_t choose(const Device* devs, int n, const Topology* topo, const Demand& d,
+               const Options& o, Plan* plan);
+
+// Node score for `d` on the pre-placement state (reference semantics: rater.go:59-70,
+// 113-123 in compat mode; 0..100 utilisation/fragmentation score in native mode).
+int32_t rate(const Device* devs, int n, const Demand& d, const Options& o, const Plan* plan);
+
+// Debits the plan; on any misfit restores what was taken and returns an error.
+// (Fixes reference allocate.go:108-113, which restores Demand[i] instead of Demand[j].)
+int32_t apply(Device* devs, int n, const Demand& d, const Plan& p);
+int32_t unapply(Device* devs, int n, const Demand& d, const Plan& p);
+
+struct FragStats {
+  int64_t pct_free_total;
+  int64_t pct_free_partial;   // free percent on partially used devices
+  int64_t mib_free_total;
+  int64_t mib_free_partial;
+  int64_t pct_stranded;       // free percent on devices whose free < min_request
+  int32_t devices;
+  int32_t devices_full_free;
+  int32_t devices_used;
+};
+void frag_accumulate(const Device* devs, int n, int32_t min_request, FragStats* s);
+
+std::string plan_to_string(const Plan& p);
+
+}  // namespace nanogpu

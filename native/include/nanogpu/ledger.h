@@ -1,0 +1,182 @@
+// Cluster GPU ledger: the state cache of the scheduler, native and shareable.
+//
+// Reference: DealerImpl (pkg/dealer/dealer.go:76-87) keeps NodeMaps / PodMaps /
+// ReleasedPodMap behind ONE sync.Mutex that is held across filter fan-out, scoring and
+// the API-server writes of bind (dealer.go:90-91, 139-140, 156-203).  Here:
+//   * the state lives in one flat region (heap, or a /dev/shm file shared by several
+//     extender worker processes: SO_REUSEPORT replicas on one host see one ledger);
+//   * every node has its own robust, process-shared mutex and a generation counter;
+//     filter/score copy a node snapshot (3 KB) under the lock and compute outside it;
+//   * bind = reserve (allocate + record pod, microseconds under the node lock), the
+//     API-server I/O happens with no lock held, then commit or rollback;
+//   * pods live in a sharded open-addressing table (64 shards, one mutex each).
+// Lock order is always node -> pod shard.
+#pragma once
+
+#include <pthread.h>
+
+#include <atomic>
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "nanogpu/alloc.h"
+
+namespace nanogpu {
+
+constexpr int kNameLen = 256;
+constexpr int kKeyLen = 64;
+constexpr int kPodShards = 64;
+
+enum PodState : int32_t { kPodEmpty = 0, kPodReserved = 1, kPodCommitted = 2, kPodTombstone = 3 };
+
+struct NodeSlot {
+  char name[kNameLen];
+  pthread_mutex_t mu;
+  std::atomic<uint64_t> generation;
+  int32_t in_use;
+  int32_t n_devs;
+  int32_t n_pods;
+  int32_t pad;
+  Topology topo;
+  Device devs[kMaxDevs];
+};
+
+struct PodSlot {
+  uint64_t hash;
+  char key[kKeyLen];
+  int32_t node;
+  int32_t state;
+  double t_reserved;   // CLOCK_MONOTONIC seconds at reservation
+  Demand demand;
+  Plan plan;
+};
+
+struct LedgerHeader {
+  uint64_t magic;
+  uint32_t version;
+  uint32_t max_nodes;
+  uint32_t pods_per_shard;
+  uint32_t pad;
+  std::atomic<int32_t> n_nodes;
+  std::atomic<uint64_t> epoch;      // bumps on every mutation anywhere
+  std::atomic<int64_t> n_pods;
+  pthread_mutex_t registry_mu;
+  pthread_mutex_t shard_mu[kPodShards];
+  std::atomic<int32_t> attached;    // processes attached
+  int32_t shard_live[kPodShards];   // guarded by shard_mu[s]
+  int32_t shard_tomb[kPodShards];
+};
+
+struct NodeSnapshot {
+  int32_t n_devs;
+  uint64_t generation;
+  Topology topo;
+  Device devs[kMaxDevs];
+};
+
+struct PodRecord {
+  std::string key;
+  int32_t node;
+  int32_t state;
+  double t_reserved;
+  Demand demand;
+  Plan plan;
+};
+
+class Ledger {
+ public:
+  // path empty => private heap ledger. Otherwise a /dev/shm file (created if absent,
+  // attached if present with the same geometry).
+  Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, bool create);
+  ~Ledger();
+  Ledger(const Ledger&) = delete;
+  Ledger& operator=(const Ledger&) = delete;
+
+  // Registers or updates a node. Existing allocations are preserved: free = new_total - used.
+  // Devices that disappear while still in use are kept, marked unhealthy.
+  int32_t upsert_node(const std::string& name, const Device* devs, int n, const Topology& topo);
+  int32_t find_node(const std::string& name) const;
+  std::string node_name(int32_t id) const;
+  int32_t n_nodes() const { return hdr_->n_nodes.load(std::memory_order_acquire); }
+  bool remove_node(int32_t id);  // only when no pods are on it
+  bool snapshot(int32_t id, NodeSnapshot* out) const;
+  uint64_t generation(int32_t id) const;
+  uint64_t epoch() const { return hdr_->epoch.load(std::memory_order_acquire); }
+
+  // Filter/score: plan for `d` on node `id`, cached per (node, generation, demand, options).
+  int32_t assume(int32_t id, const Demand& d, const Options& o, Plan* plan);
+
+  // Bind: choose (cache hit if the node is unchanged) and allocate atomically; records the
+  // pod as Reserved. Idempotent for the same key on the same node.
+  int32_t reserve(int32_t id, const std::string& key, const Demand& d, const Options& o, Plan* plan);
+  // Allocates an explicit plan (pods bound by someone else / rebuild from annotations).
+  int32_t allocate_plan(int32_t id, const std::string& key, const Demand& d, const Plan& plan,
+                        bool committed);
+  int32_t commit(const std::string& key);
+  int32_t release(const std::string& key);
+  bool lookup(const std::string& key, PodRecord* out) const;
+  std::vector<PodRecord> pods_on(int32_t node) const;
+  std::vector<std::string> expired_reservations(double older_than_s) const;
+  int64_t n_pods() const { return hdr_->n_pods.load(std::memory_order_acquire); }
+
+  // Load-aware telemetry (reference nodeusage.go + allocate.go:173-195).
+  int32_t set_load(int32_t id, int dev, float usage);
+  int32_t set_health(int32_t id, int dev, bool healthy);
+
+  FragStats frag(int32_t min_request) const;
+
+  void clear_cache();
+  size_t cache_size() const;
+  const std::string& path() const { return path_; }
+  size_t bytes() const { return bytes_; }
+  static size_t region_bytes(uint32_t max_nodes, uint32_t max_pods);
+
+ private:
+  NodeSlot* node(int32_t id) const;
+  PodSlot* shard(int s) const;
+  int shard_of(uint64_t h) const { return static_cast<int>(h % kPodShards); }
+  PodSlot* find_pod_locked(int s, uint64_t h, const char* key) const;
+  PodSlot* insert_pod_locked(int s, uint64_t h, const char* key);
+
+  void lock_node(NodeSlot* n) const;
+  void lock_mu(pthread_mutex_t* m) const;
+
+  std::string path_;
+  bool owner_;
+  int fd_ = -1;
+  size_t bytes_ = 0;
+  char* base_ = nullptr;
+  LedgerHeader* hdr_ = nullptr;
+  NodeSlot* nodes_ = nullptr;
+  PodSlot* pods_ = nullptr;
+
+  struct CacheKey {
+    int32_t node;
+    uint64_t gen, dh, oh;
+    bool operator==(const CacheKey& o) const {
+      return node == o.node && gen == o.gen && dh == o.dh && oh == o.oh;
+    }
+  };
+  struct CacheHash {
+    size_t operator()(const CacheKey& k) const {
+      return static_cast<size_t>(k.dh ^ (k.gen * 0x9e3779b97f4a7c15ULL) ^ (k.oh << 1) ^
+                                 static_cast<uint64_t>(k.node) * 0xff51afd7ed558ccdULL);
+    }
+  };
+  struct CacheVal {
+    int32_t rc;
+    Plan plan;
+  };
+  mutable std::mutex cache_mu_;
+  std::unordered_map<CacheKey, CacheVal, CacheHash> cache_;
+  mutable std::mutex names_mu_;
+  mutable std::unordered_map<std::string, int32_t> names_;  // process-local name index
+};
+
+uint64_t key_hash(const char* key);
+double mono_now();
+
+}  // namespace nanogpu

@@ -1,0 +1,629 @@
+// Placement policies: reference-exact (compat) and MI355X-native.
+// See alloc.h for the reference parity map.
+#include "nanogpu/alloc.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <sstream>
+
+#include "nanogpu/gosort.h"
+
+namespace nanogpu {
+
+const char* err_str(int32_t e) {
+  switch (e) {
+    case kOk: return "ok";
+    case kErrNoFit: return "insufficient gpu resource";
+    case kErrNoDevices: return "node has no gpu devices";
+    case kErrBadPlan: return "plan does not match node devices";
+    case kErrPlanNoLongerFits: return "plan no longer fits node";
+    case kErrUnknownNode: return "unknown node";
+    case kErrUnknownPod: return "unknown pod";
+    case kErrPodExists: return "pod already allocated on another node";
+    case kErrTableFull: return "ledger table full";
+    case kErrBadDemand: return "invalid demand";
+    case kOkExisting: return "already allocated";
+    default: return "unknown error";
+  }
+}
+
+static inline uint64_t mix64(uint64_t x) {
+  x += 0x9e3779b97f4a7c15ULL;
+  x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  x = (x ^ (x >> 27)) * 0x94d049bb133111ebULL;
+  return x ^ (x >> 31);
+}
+
+uint64_t Demand::hash() const {
+  uint64_t h = 0xcbf29ce484222325ULL ^ static_cast<uint64_t>(n);
+  for (int i = 0; i < n; ++i) {
+    h = mix64(h ^ static_cast<uint64_t>(static_cast<uint32_t>(c[i].pct)));
+    h = mix64(h ^ static_cast<uint64_t>(c[i].mib));
+  }
+  return h;
+}
+
+uint64_t Options::hash() const {
+  uint64_t h = mix64(static_cast<uint64_t>(policy) | (static_cast<uint64_t>(compat) << 8) |
+                     (static_cast<uint64_t>(load_aware) << 16));
+  uint32_t tw;
+  std::memcpy(&tw, &topo_weight, sizeof(tw));
+  return mix64(h ^ tw ^ mix64(seed));
+}
+
+int devices_needed(const ContainerDemand& c) {
+  if (c.pct <= 0) return c.mib > 0 ? 1 : 0;
+  if (c.pct <= kPercentPerDevice) return 1;
+  return c.pct / kPercentPerDevice;
+}
+
+static inline bool hbm_fits(const Device& d, int64_t mib) {
+  return mib <= 0 || d.mib_total <= 0 || d.mib_free >= mib;
+}
+
+static inline float link_bw(const Topology* t, int a, int b) {
+  if (!t || a < 0 || b < 0 || a >= t->n_gpus || b >= t->n_gpus) return 0.f;
+  return t->link_bw[a * kMaxGpus + b];
+}
+
+static inline int numa_of(const Topology* t, int g) {
+  if (!t || g < 0 || g >= t->n_gpus) return -1;
+  return t->numa[g];
+}
+
+static void plan_init(Plan* p, int n) {
+  std::memset(p, 0, sizeof(*p));
+  p->n = n;
+}
+
+// ---------------------------------------------------------------------------
+// compat: reference Binpack/Spread/SampleRater, Go 1.16 ordering
+// ---------------------------------------------------------------------------
+
+namespace {
+
+struct SortDev {
+  int32_t free;
+  int32_t remain;
+  int64_t mib_free;
+  int64_t mib_total;
+  int32_t index;
+};
+
+struct SortDem {
+  int32_t pct;
+  int32_t index;
+  int64_t mib;
+};
+
+}  // namespace
+
+static int32_t compat_choose(const Device* devs, int n, const Demand& d, const Options& o,
+                             Plan* plan) {
+  const int C = d.n;
+  SortDem sd[kMaxContainers];
+  for (int i = 0; i < C; ++i) sd[i] = SortDem{d.c[i].pct, i, d.c[i].mib};
+  // Demand.ToSortableGPUs + sort.Sort: key = Percent + 50*RemainLoad, RemainLoad = 0.
+  gosort::sort(
+      C, [&](int i, int j) { return sd[i].pct < sd[j].pct; },
+      [&](int i, int j) { std::swap(sd[i], sd[j]); });
+
+  if (o.policy == Policy::kFirstFit) {
+    // SampleRater.Choose (rater.go:29-50), on a copy (fixes D19: the reference debits live GPUs).
+    int32_t free[kMaxDevs];
+    int64_t mfree[kMaxDevs];
+    for (int i = 0; i < n; ++i) {
+      free[i] = devs[i].pct_free;
+      mfree[i] = devs[i].mib_free;
+    }
+    plan_init(plan, C);
+    int placed = 0;
+    for (int c = 0; c < C; ++c) {
+      plan->off[c] = static_cast<int16_t>(c);
+      plan->idx[c] = kNotNeedGPU;
+      if (d.c[c].pct == 0) {
+        ++placed;
+        continue;
+      }
+      for (int j = 0; j < n; ++j) {
+        if (free[j] >= d.c[c].pct && (d.c[c].mib <= 0 || devs[j].mib_total <= 0 || mfree[j] >= d.c[c].mib)) {
+          plan->idx[c] = static_cast<int16_t>(j);
+          free[j] -= d.c[c].pct;
+          if (devs[j].mib_total > 0) mfree[j] -= d.c[c].mib;
+          ++placed;
+          break;
+        }
+      }
+    }
+    plan->off[C] = static_cast<int16_t>(C);
+    return placed == C ? kOk : kErrNoFit;
+  }
+
+  SortDev sg[kMaxDevs];
+  for (int i = 0; i < n; ++i)
+    sg[i] = SortDev{devs[i].pct_free, devs[i].remain_load, devs[i].mib_free, devs[i].mib_total, i};
+  auto less = [&](int i, int j) {
+    return sg[i].free + sg[i].remain * 50 < sg[j].free + sg[j].remain * 50;  // allocate.go:247
+  };
+  auto swp = [&](int i, int j) { std::swap(sg[i], sg[j]); };
+
+  int indexes[kMaxContainers];
+  int cnt = 0;
+  const bool spread = o.policy == Policy::kSpread;
+  for (int j = C - 1; j >= 0; --j) {
+    if (sd[j].pct == 0) {
+      indexes[cnt++] = kNotNeedGPU;
+      continue;
+    }
+    gosort::sort(n, less, swp);
+    auto fits = [&](int i) {
+      return sg[i].free >= sd[j].pct &&
+             (sd[j].mib <= 0 || sg[i].mib_total <= 0 || sg[i].mib_free >= sd[j].mib);
+    };
+    if (!spread) {
+      for (int i = 0; i < n; ++i) {
+        if (!fits(i)) continue;
+        indexes[cnt++] = sg[i].index;
+        sg[i].free -= sd[j].pct;
+        if (sg[i].mib_total > 0) sg[i].mib_free -= sd[j].mib;
+        break;
+      }
+    } else {
+      for (int i = n - 1; i >= 0; --i) {
+        if (!fits(i)) continue;
+        indexes[cnt++] = sg[i].index;
+        sg[i].free -= sd[j].pct;
+        if (sg[i].mib_total > 0) sg[i].mib_free -= sd[j].mib;
+        break;
+      }
+    }
+  }
+  if (cnt != C) return kErrNoFit;
+  plan_init(plan, C);
+  int result[kMaxContainers];
+  for (int j = C - 1; j >= 0; --j) result[sd[j].index] = indexes[C - 1 - j];
+  for (int c = 0; c < C; ++c) {
+    plan->off[c] = static_cast<int16_t>(c);
+    plan->idx[c] = static_cast<int16_t>(result[c]);
+  }
+  plan->off[C] = static_cast<int16_t>(C);
+  return kOk;
+}
+
+static int32_t compat_rate(const Device* devs, int n, const Options& o) {
+  if (n == 0) return 0;
+  double load = 0.0;
+  if (o.load_aware)
+    for (int i = 0; i < n; ++i) load += devs[i].load_usage;
+  const int load_int = static_cast<int>(load) / n;
+  if (o.policy == Policy::kBinpack) {
+    int64_t sum = 0, used = 0;
+    for (int i = 0; i < n; ++i) {
+      sum += devs[i].pct_total;
+      used += devs[i].pct_total - devs[i].pct_free;
+    }
+    const double usage = static_cast<double>(used) / static_cast<double>(sum);
+    return static_cast<int32_t>(usage * 100) + load_int * 50 - n;
+  }
+  if (o.policy == Policy::kSpread) {
+    int64_t avail = 0;
+    int free_cnt = 0;
+    for (int i = 0; i < n; ++i) {
+      avail += devs[i].pct_free;
+      if (devs[i].pct_free == devs[i].pct_total) ++free_cnt;
+    }
+    return static_cast<int32_t>(100 * free_cnt + avail / 10 - n - load_int);
+  }
+  return 100;  // SampleRater: ScoreMax
+}
+
+// ---------------------------------------------------------------------------
+// native policies
+// ---------------------------------------------------------------------------
+
+namespace {
+
+struct Work {
+  Device dev[kMaxDevs];
+  int n;
+  int16_t chosen[kMaxPlanIdx];
+  int n_chosen;
+};
+
+// Affinity of device `i` to the devices already chosen for this pod.
+// Binpack wants siblings (same physical GPU) and high-bandwidth neighbours;
+// spread wants distinct GPUs that are still well connected (max of the min link).
+float affinity(const Work& w, const Topology* t, int i, bool spread) {
+  if (w.n_chosen == 0) return 0.f;
+  const int gi = w.dev[i].gpu;
+  float sum = 0.f, mn = 1e30f;
+  int same = 0, same_numa = 0;
+  for (int k = 0; k < w.n_chosen; ++k) {
+    const int gk = w.dev[w.chosen[k]].gpu;
+    if (gk == gi) {
+      ++same;
+      continue;
+    }
+    const float bw = link_bw(t, gi, gk);
+    sum += bw;
+    mn = std::min(mn, bw);
+    if (numa_of(t, gi) >= 0 && numa_of(t, gi) == numa_of(t, gk)) ++same_numa;
+  }
+  if (mn > 1e29f) mn = 0.f;
+  if (spread) return (same ? -1000.f * same : 0.f) + mn + 10.f * same_numa;
+  return 1000.f * same + sum + 10.f * same_numa;
+}
+
+bool share_fits(const Device& d, const ContainerDemand& c) {
+  return d.healthy && d.pct_free >= c.pct && hbm_fits(d, c.mib);
+}
+
+int pick_share(Work& w, const Topology* t, const ContainerDemand& c, const Options& o,
+               uint64_t rnd) {
+  const bool spread = o.policy == Policy::kSpread;
+  int best = -1;
+  int64_t bk1 = 0, bk2 = 0;
+  float bk3 = 0.f;
+  int fit_cnt = 0;
+  for (int i = 0; i < w.n; ++i) {
+    const Device& d = w.dev[i];
+    if (!share_fits(d, c)) continue;
+    ++fit_cnt;
+    if (o.policy == Policy::kRandom) continue;
+    if (o.policy == Policy::kFirstFit) return i;
+    int64_t k1 = d.pct_free - c.pct;
+    if (o.load_aware) k1 += 50 * d.remain_load;
+    int64_t k2 = d.mib_total > 0 && c.mib > 0 ? (d.mib_free - c.mib) * 1000 / d.mib_total : 0;
+    const float k3 = o.topo_weight * affinity(w, t, i, spread);
+    if (spread) {
+      k1 = -k1;  // worst fit: most free first
+      k2 = -k2;
+    }
+    bool better;
+    if (best < 0) better = true;
+    else if (k1 != bk1) better = k1 < bk1;
+    else if (k2 != bk2) better = k2 < bk2;
+    else better = k3 > bk3;
+    if (better) {
+      best = i;
+      bk1 = k1;
+      bk2 = k2;
+      bk3 = k3;
+    }
+  }
+  if (o.policy == Policy::kRandom && fit_cnt > 0) {
+    int target = static_cast<int>(rnd % static_cast<uint64_t>(fit_cnt));
+    for (int i = 0; i < w.n; ++i) {
+      if (!share_fits(w.dev[i], c)) continue;
+      if (target-- == 0) return i;
+    }
+  }
+  return best;
+}
+
+bool whole_free(const Device& d) {
+  return d.healthy && d.pct_free == d.pct_total && d.pct_total > 0 &&
+         (d.mib_total <= 0 || d.mib_free == d.mib_total);
+}
+
+// Set score for whole-device groups (multi-GPU containers: TP/EP groups, RCCL rings).
+// Every pair of MI355X GPUs in a node is one xGMI hop, so hop count does not discriminate;
+// the score ranks partition siblings, min link bandwidth, NUMA locality, then policy intent.
+float group_score(const Work& w, const Topology* t, const int* set, int k, const Options& o) {
+  int siblings = 0, numa_mix = 0;
+  float min_bw = 1e30f;
+  bool any_pair = false;
+  for (int a = 0; a < k; ++a)
+    for (int b = a + 1; b < k; ++b) {
+      const int ga = w.dev[set[a]].gpu, gb = w.dev[set[b]].gpu;
+      if (ga == gb) {
+        ++siblings;
+        continue;
+      }
+      any_pair = true;
+      min_bw = std::min(min_bw, link_bw(t, ga, gb));
+      if (numa_of(t, ga) != numa_of(t, gb)) ++numa_mix;
+    }
+  if (!any_pair) min_bw = 0.f;
+  // Policy intent over the GPUs touched: binpack prefers GPUs already partly used (keeps
+  // untouched GPUs whole); spread prefers GPUs with the most free capacity.
+  float intent = 0.f;
+  for (int a = 0; a < k; ++a) {
+    const int g = w.dev[set[a]].gpu;
+    int64_t gfree = 0, gtot = 0;
+    for (int i = 0; i < w.n; ++i)
+      if (w.dev[i].gpu == g) {
+        gfree += w.dev[i].pct_free;
+        gtot += w.dev[i].pct_total;
+      }
+    const float frac = gtot > 0 ? static_cast<float>(gfree) / gtot : 0.f;
+    intent += o.policy == Policy::kSpread ? frac : (1.f - frac);
+  }
+  const float sib_w = o.policy == Policy::kSpread ? 20.f : 200.f;
+  return o.topo_weight * (sib_w * siblings + min_bw - 50.f * numa_mix) + 100.f * intent;
+}
+
+bool pick_group(Work& w, const Topology* t, int k, const Options& o, uint64_t rnd, int* out) {
+  int cand[kMaxDevs];
+  int m = 0;
+  for (int i = 0; i < w.n; ++i)
+    if (whole_free(w.dev[i])) cand[m++] = i;
+  if (m < k) return false;
+  if (o.policy == Policy::kFirstFit) {
+    for (int a = 0; a < k; ++a) out[a] = cand[a];
+    return true;
+  }
+  if (o.policy == Policy::kRandom) {
+    // partial Fisher-Yates with the pod's deterministic stream
+    for (int a = 0; a < k; ++a) {
+      rnd = mix64(rnd);
+      const int j = a + static_cast<int>(rnd % static_cast<uint64_t>(m - a));
+      std::swap(cand[a], cand[j]);
+      out[a] = cand[a];
+    }
+    return true;
+  }
+  float best = -1e30f;
+  int set[kMaxDevs];
+  for (int s = 0; s < m; ++s) {
+    int sz = 0;
+    set[sz++] = cand[s];
+    bool used[kMaxDevs] = {false};
+    used[s] = true;
+    while (sz < k) {
+      int bj = -1;
+      float bs = -1e30f;
+      for (int j = 0; j < m; ++j) {
+        if (used[j]) continue;
+        set[sz] = cand[j];
+        const float sc = group_score(w, t, set, sz + 1, o);
+        if (sc > bs) {
+          bs = sc;
+          bj = j;
+        }
+      }
+      used[bj] = true;
+      set[sz++] = cand[bj];
+    }
+    const float sc = group_score(w, t, set, k, o);
+    if (sc > best + 1e-4f) {
+      best = sc;
+      std::copy(set, set + k, out);
+    }
+  }
+  return true;
+}
+
+}  // namespace
+
+static int32_t native_choose(const Device* devs, int n, const Topology* topo, const Demand& d,
+                             const Options& o, Plan* plan) {
+  Work w;
+  w.n = n;
+  w.n_chosen = 0;
+  std::memcpy(w.dev, devs, sizeof(Device) * n);
+
+  // Hardest first: whole-device groups, then larger shares, then HBM; stable on index.
+  int order[kMaxContainers];
+  for (int i = 0; i < d.n; ++i) order[i] = i;
+  std::stable_sort(order, order + d.n, [&](int a, int b) {
+    const int na = devices_needed(d.c[a]), nb = devices_needed(d.c[b]);
+    if ((na > 1) != (nb > 1)) return na > nb;
+    if (d.c[a].pct != d.c[b].pct) return d.c[a].pct > d.c[b].pct;
+    return d.c[a].mib > d.c[b].mib;
+  });
+
+  int16_t start[kMaxContainers], count[kMaxContainers];
+  int16_t tmp_idx[kMaxPlanIdx];
+  int total = 0;
+  uint64_t rnd = mix64(o.seed ^ d.hash());
+  for (int q = 0; q < d.n; ++q) {
+    const int c = order[q];
+    const ContainerDemand& cd = d.c[c];
+    const int need = devices_needed(cd);
+    rnd = mix64(rnd + static_cast<uint64_t>(q));
+    if (need == 0) {
+      if (total >= kMaxPlanIdx) return kErrBadDemand;
+      start[c] = static_cast<int16_t>(total);
+      count[c] = 1;
+      tmp_idx[total++] = kNotNeedGPU;
+      continue;
+    }
+    if (cd.pct > kPercentPerDevice && cd.pct % kPercentPerDevice != 0) return kErrBadDemand;
+    if (total + need > kMaxPlanIdx) return kErrBadDemand;
+    start[c] = static_cast<int16_t>(total);
+    count[c] = static_cast<int16_t>(need);
+    if (need == 1) {
+      const int i = pick_share(w, topo, cd, o, rnd);
+      if (i < 0) return kErrNoFit;
+      w.dev[i].pct_free -= cd.pct;
+      if (w.dev[i].mib_total > 0) w.dev[i].mib_free -= cd.mib;
+      tmp_idx[total++] = static_cast<int16_t>(i);
+      w.chosen[w.n_chosen++] = static_cast<int16_t>(i);
+    } else {
+      int set[kMaxDevs];
+      if (!pick_group(w, topo, need, o, rnd, set)) return kErrNoFit;
+      for (int a = 0; a < need; ++a) {
+        Device& dv = w.dev[set[a]];
+        dv.pct_free = 0;
+        if (dv.mib_total > 0) dv.mib_free = 0;
+        tmp_idx[total++] = static_cast<int16_t>(set[a]);
+        w.chosen[w.n_chosen++] = static_cast<int16_t>(set[a]);
+      }
+    }
+  }
+  plan_init(plan, d.n);
+  int pos = 0;
+  for (int c = 0; c < d.n; ++c) {
+    plan->off[c] = static_cast<int16_t>(pos);
+    for (int a = 0; a < count[c]; ++a) plan->idx[pos++] = tmp_idx[start[c] + a];
+  }
+  plan->off[d.n] = static_cast<int16_t>(pos);
+  return kOk;
+}
+
+static int32_t native_rate(const Device* devs, int n, const Demand& d, const Options& o,
+                           const Plan* plan) {
+  if (n == 0) return 0;
+  Device after[kMaxDevs];
+  std::memcpy(after, devs, sizeof(Device) * n);
+  if (plan) apply(after, n, d, *plan);
+  int64_t pct_tot = 0, pct_used = 0, mib_tot = 0, mib_used = 0;
+  int full_free = 0;
+  float load = 0.f;
+  for (int i = 0; i < n; ++i) {
+    pct_tot += after[i].pct_total;
+    pct_used += after[i].pct_total - after[i].pct_free;
+    if (after[i].mib_total > 0) {
+      mib_tot += after[i].mib_total;
+      mib_used += after[i].mib_total - after[i].mib_free;
+    }
+    if (after[i].pct_free == after[i].pct_total) ++full_free;
+    load += devs[i].load_usage;
+  }
+  double util = pct_tot > 0 ? static_cast<double>(pct_used) / pct_tot : 0.0;
+  if (mib_tot > 0) util = 0.5 * util + 0.5 * static_cast<double>(mib_used) / mib_tot;
+  const double avg_load = o.load_aware ? load / (kLoadTotal * n) : 0.0;  // 0..1
+  double s;
+  switch (o.policy) {
+    case Policy::kBinpack:
+      s = 100.0 * util;
+      if (o.load_aware) s = 0.8 * s + 20.0 * avg_load;  // reference binpack rewards load (rater.go:69)
+      break;
+    case Policy::kSpread:
+      s = 50.0 * (1.0 - util) + 50.0 * static_cast<double>(full_free) / n;
+      if (o.load_aware) s = 0.8 * s + 20.0 * (1.0 - avg_load);
+      break;
+    case Policy::kRandom:
+      s = static_cast<double>(mix64(o.seed ^ d.hash() ^ static_cast<uint64_t>(pct_used) ^
+                                    (static_cast<uint64_t>(n) << 32)) %
+                              101);
+      break;
+    default:
+      s = 100.0;
+  }
+  return static_cast<int32_t>(std::clamp(s, 0.0, 100.0));
+}
+
+int32_t choose(const Device* devs, int n, const Topology* topo, const Demand& d,
+               const Options& o, Plan* plan) {
+  if (d.n < 0 || d.n > kMaxContainers) return kErrBadDemand;
+  if (n <= 0) return kErrNoDevices;
+  if (n > kMaxDevs) return kErrBadPlan;
+  int32_t rc;
+  if (o.compat && o.policy != Policy::kRandom) {
+    rc = compat_choose(devs, n, d, o, plan);
+  } else {
+    rc = native_choose(devs, n, topo, d, o, plan);
+  }
+  if (rc != kOk) return rc;
+  plan->score = rate(devs, n, d, o, plan);
+  return kOk;
+}
+
+int32_t rate(const Device* devs, int n, const Demand& d, const Options& o, const Plan* plan) {
+  if (o.compat && o.policy != Policy::kRandom) return compat_rate(devs, n, o);
+  return native_rate(devs, n, d, o, plan);
+}
+
+static bool plan_shape_ok(int n, const Demand& d, const Plan& p) {
+  if (p.n != d.n || p.n < 0 || p.n > kMaxContainers) return false;
+  if (p.off[0] != 0 || p.off[p.n] > kMaxPlanIdx) return false;
+  for (int c = 0; c < p.n; ++c) {
+    if (p.off[c + 1] < p.off[c]) return false;
+    for (int k = p.off[c]; k < p.off[c + 1]; ++k)
+      if (p.idx[k] >= n || p.idx[k] < kNotNeedGPU) return false;
+  }
+  return true;
+}
+
+// Whole-device entries (pct > 100) debit the full device; share entries debit (pct, mib).
+static inline void debit(Device& dv, const ContainerDemand& cd, int sign) {
+  if (cd.pct > kPercentPerDevice) {
+    if (sign < 0) {
+      dv.pct_free = 0;
+      if (dv.mib_total > 0) dv.mib_free = 0;
+    } else {
+      dv.pct_free = dv.pct_total;
+      if (dv.mib_total > 0) dv.mib_free = dv.mib_total;
+    }
+    return;
+  }
+  dv.pct_free += sign * cd.pct;
+  if (dv.mib_total > 0) dv.mib_free += sign * cd.mib;
+}
+
+static inline bool can_debit(const Device& dv, const ContainerDemand& cd) {
+  if (cd.pct > kPercentPerDevice)
+    return dv.pct_free == dv.pct_total && (dv.mib_total <= 0 || dv.mib_free == dv.mib_total);
+  return dv.pct_free >= cd.pct && hbm_fits(dv, cd.mib);
+}
+
+int32_t apply(Device* devs, int n, const Demand& d, const Plan& p) {
+  if (!plan_shape_ok(n, d, p)) return kErrBadPlan;
+  for (int c = 0; c < p.n; ++c) {
+    for (int k = p.off[c]; k < p.off[c + 1]; ++k) {
+      const int i = p.idx[k];
+      if (i < 0) continue;
+      if (!can_debit(devs[i], d.c[c])) {
+        // roll back exactly what this call debited
+        for (int c2 = 0; c2 <= c; ++c2) {
+          const int end = c2 == c ? k : p.off[c2 + 1];
+          for (int k2 = p.off[c2]; k2 < end; ++k2)
+            if (p.idx[k2] >= 0) debit(devs[p.idx[k2]], d.c[c2], +1);
+        }
+        return kErrPlanNoLongerFits;
+      }
+      debit(devs[i], d.c[c], -1);
+    }
+  }
+  return kOk;
+}
+
+int32_t unapply(Device* devs, int n, const Demand& d, const Plan& p) {
+  if (!plan_shape_ok(n, d, p)) return kErrBadPlan;
+  for (int c = 0; c < p.n; ++c)
+    for (int k = p.off[c]; k < p.off[c + 1]; ++k) {
+      const int i = p.idx[k];
+      if (i < 0) continue;
+      debit(devs[i], d.c[c], +1);
+      devs[i].pct_free = std::min(devs[i].pct_free, devs[i].pct_total);
+      if (devs[i].mib_total > 0) devs[i].mib_free = std::min(devs[i].mib_free, devs[i].mib_total);
+    }
+  return kOk;
+}
+
+void frag_accumulate(const Device* devs, int n, int32_t min_request, FragStats* s) {
+  for (int i = 0; i < n; ++i) {
+    const Device& d = devs[i];
+    if (!d.healthy) continue;
+    ++s->devices;
+    s->pct_free_total += d.pct_free;
+    s->mib_free_total += d.mib_total > 0 ? d.mib_free : 0;
+    const bool full = d.pct_free == d.pct_total;
+    if (full) ++s->devices_full_free;
+    if (d.pct_free < d.pct_total) ++s->devices_used;
+    if (d.pct_free > 0 && d.pct_free < d.pct_total) {
+      s->pct_free_partial += d.pct_free;
+      if (d.mib_total > 0) s->mib_free_partial += d.mib_free;
+    }
+    if (d.pct_free > 0 && d.pct_free < min_request) s->pct_stranded += d.pct_free;
+  }
+}
+
+std::string plan_to_string(const Plan& p) {
+  std::ostringstream os;
+  os << "[";
+  for (int c = 0; c < p.n; ++c) {
+    if (c) os << " ";
+    for (int k = p.off[c]; k < p.off[c + 1]; ++k) {
+      if (k > p.off[c]) os << ",";
+      os << p.idx[k];
+    }
+  }
+  os << "]";
+  return os.str();
+}
+
+}  // namespace nanogpu

@@ -1,0 +1,433 @@
+// pybind11 module `nanogpu._native`: ledger, policies, frag metrics, topology reader.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "nanogpu/alloc.h"
+#include "nanogpu/gosort.h"
+#include "nanogpu/ledger.h"
+#include "nanogpu/topo.h"
+
+namespace py = pybind11;
+using namespace nanogpu;
+
+namespace {
+
+Demand to_demand(const std::vector<std::pair<int32_t, int64_t>>& v) {
+  if (v.size() > static_cast<size_t>(kMaxContainers))
+    throw py::value_error("too many containers (max 16)");
+  Demand d;
+  std::memset(&d, 0, sizeof(d));
+  d.n = static_cast<int32_t>(v.size());
+  for (size_t i = 0; i < v.size(); ++i) {
+    if (v[i].first < 0 || v[i].second < 0) throw py::value_error("negative demand");
+    d.c[i].pct = v[i].first;
+    d.c[i].mib = v[i].second;
+  }
+  return d;
+}
+
+template <class T>
+T get(const py::dict& d, const char* k, T dflt) {
+  if (!d.contains(k)) return dflt;
+  return d[k].cast<T>();
+}
+
+Device to_device(const py::dict& d) {
+  Device v;
+  std::memset(&v, 0, sizeof(v));
+  v.pct_total = get<int32_t>(d, "pct_total", kPercentPerDevice);
+  v.pct_free = get<int32_t>(d, "pct_free", v.pct_total);
+  v.mib_total = get<int64_t>(d, "mib_total", 0);
+  v.mib_free = get<int64_t>(d, "mib_free", v.mib_total);
+  v.load_usage = get<float>(d, "load_usage", 0.f);
+  v.remain_load = get<int16_t>(d, "remain_load", 0);
+  v.gpu = get<int16_t>(d, "gpu", 0);
+  v.part = get<int16_t>(d, "part", 0);
+  v.numa = get<int16_t>(d, "numa", -1);
+  v.healthy = get<bool>(d, "healthy", true) ? 1 : 0;
+  v.xcds = get<int16_t>(d, "xcds", 0);
+  v.cus = get<int32_t>(d, "cus", 0);
+  return v;
+}
+
+py::dict from_device(const Device& v) {
+  py::dict d;
+  d["pct_free"] = v.pct_free;
+  d["pct_total"] = v.pct_total;
+  d["mib_free"] = v.mib_free;
+  d["mib_total"] = v.mib_total;
+  d["load_usage"] = v.load_usage;
+  d["remain_load"] = v.remain_load;
+  d["gpu"] = v.gpu;
+  d["part"] = v.part;
+  d["numa"] = v.numa;
+  d["healthy"] = v.healthy != 0;
+  d["xcds"] = v.xcds;
+  d["cus"] = v.cus;
+  return d;
+}
+
+std::vector<Device> to_devices(const py::list& l) {
+  if (l.size() > static_cast<size_t>(kMaxDevs)) throw py::value_error("too many devices (max 64)");
+  std::vector<Device> out;
+  out.reserve(l.size());
+  for (auto h : l) out.push_back(to_device(h.cast<py::dict>()));
+  return out;
+}
+
+Topology to_topo(const py::object& o, const std::vector<Device>& devs) {
+  Topology t;
+  std::memset(&t, 0, sizeof(t));
+  for (int i = 0; i < kMaxGpus; ++i) t.numa[i] = -1;
+  int n_gpus = 0;
+  for (const Device& d : devs) n_gpus = std::max<int>(n_gpus, d.gpu + 1);
+  if (!o.is_none()) {
+    py::dict d = o.cast<py::dict>();
+    n_gpus = std::max<int>(n_gpus, get<int>(d, "n_gpus", 0));
+    if (d.contains("numa")) {
+      auto v = d["numa"].cast<std::vector<int>>();
+      for (size_t i = 0; i < v.size() && i < static_cast<size_t>(kMaxGpus); ++i) t.numa[i] = static_cast<int16_t>(v[i]);
+    }
+    if (d.contains("link_bw")) {
+      auto m = d["link_bw"].cast<std::vector<std::vector<float>>>();
+      for (size_t a = 0; a < m.size() && a < static_cast<size_t>(kMaxGpus); ++a)
+        for (size_t b = 0; b < m[a].size() && b < static_cast<size_t>(kMaxGpus); ++b)
+          t.link_bw[a * kMaxGpus + b] = m[a][b];
+    }
+  }
+  if (n_gpus > kMaxGpus) throw py::value_error("too many physical GPUs (max 16)");
+  t.n_gpus = n_gpus;
+  return t;
+}
+
+py::dict from_topo(const Topology& t) {
+  py::dict d;
+  d["n_gpus"] = t.n_gpus;
+  std::vector<int> numa(t.numa, t.numa + t.n_gpus);
+  std::vector<std::vector<float>> bw(t.n_gpus, std::vector<float>(t.n_gpus));
+  for (int a = 0; a < t.n_gpus; ++a)
+    for (int b = 0; b < t.n_gpus; ++b) bw[a][b] = t.link_bw[a * kMaxGpus + b];
+  d["numa"] = numa;
+  d["link_bw"] = bw;
+  return d;
+}
+
+py::list plan_list(const Plan& p) {
+  py::list out;
+  for (int c = 0; c < p.n; ++c) {
+    py::list idx;
+    for (int k = p.off[c]; k < p.off[c + 1]; ++k) idx.append(static_cast<int>(p.idx[k]));
+    out.append(idx);
+  }
+  return out;
+}
+
+Plan to_plan(const std::vector<std::vector<int>>& v) {
+  Plan p;
+  std::memset(&p, 0, sizeof(p));
+  if (v.size() > static_cast<size_t>(kMaxContainers)) throw py::value_error("plan too long");
+  p.n = static_cast<int32_t>(v.size());
+  int pos = 0;
+  for (size_t c = 0; c < v.size(); ++c) {
+    p.off[c] = static_cast<int16_t>(pos);
+    if (v[c].empty()) throw py::value_error("empty plan entry");
+    for (int i : v[c]) {
+      if (pos >= kMaxPlanIdx) throw py::value_error("plan too long");
+      p.idx[pos++] = static_cast<int16_t>(i);
+    }
+  }
+  p.off[p.n] = static_cast<int16_t>(pos);
+  return p;
+}
+
+py::dict frag_dict(const FragStats& s) {
+  py::dict d;
+  d["pct_free_total"] = s.pct_free_total;
+  d["pct_free_partial"] = s.pct_free_partial;
+  d["mib_free_total"] = s.mib_free_total;
+  d["mib_free_partial"] = s.mib_free_partial;
+  d["pct_stranded"] = s.pct_stranded;
+  d["devices"] = s.devices;
+  d["devices_full_free"] = s.devices_full_free;
+  d["devices_used"] = s.devices_used;
+  d["frag_pct"] = s.pct_free_total > 0 ? 100.0 * s.pct_free_partial / s.pct_free_total : 0.0;
+  d["frag_mib"] = s.mib_free_total > 0 ? 100.0 * s.mib_free_partial / s.mib_free_total : 0.0;
+  d["stranded_pct"] = s.pct_free_total > 0 ? 100.0 * s.pct_stranded / s.pct_free_total : 0.0;
+  return d;
+}
+
+py::dict record_dict(const PodRecord& r) {
+  py::dict d;
+  d["key"] = r.key;
+  d["node"] = r.node;
+  d["state"] = r.state == kPodReserved ? "reserved" : "committed";
+  d["t_reserved"] = r.t_reserved;
+  std::vector<std::pair<int32_t, int64_t>> dem;
+  for (int i = 0; i < r.demand.n; ++i) dem.emplace_back(r.demand.c[i].pct, r.demand.c[i].mib);
+  d["demand"] = dem;
+  d["plan"] = plan_list(r.plan);
+  return d;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "nanogpu native core: ledger, placement policies, topology reader";
+  m.attr("MAX_DEVS") = kMaxDevs;
+  m.attr("MAX_GPUS") = kMaxGpus;
+  m.attr("MAX_CONTAINERS") = kMaxContainers;
+  m.attr("OK") = static_cast<int>(kOk);
+  m.attr("ERR_NO_FIT") = static_cast<int>(kErrNoFit);
+  m.attr("ERR_NO_DEVICES") = static_cast<int>(kErrNoDevices);
+  m.attr("ERR_BAD_PLAN") = static_cast<int>(kErrBadPlan);
+  m.attr("ERR_PLAN_NO_LONGER_FITS") = static_cast<int>(kErrPlanNoLongerFits);
+  m.attr("ERR_UNKNOWN_NODE") = static_cast<int>(kErrUnknownNode);
+  m.attr("ERR_UNKNOWN_POD") = static_cast<int>(kErrUnknownPod);
+  m.attr("ERR_POD_EXISTS") = static_cast<int>(kErrPodExists);
+  m.attr("ERR_TABLE_FULL") = static_cast<int>(kErrTableFull);
+  m.attr("ERR_BAD_DEMAND") = static_cast<int>(kErrBadDemand);
+  m.attr("OK_EXISTING") = static_cast<int>(kOkExisting);
+  m.def("err_str", &err_str);
+
+  py::enum_<Policy>(m, "Policy")
+      .value("BINPACK", Policy::kBinpack)
+      .value("SPREAD", Policy::kSpread)
+      .value("RANDOM", Policy::kRandom)
+      .value("FIRSTFIT", Policy::kFirstFit);
+
+  py::class_<Options>(m, "Options")
+      .def(py::init([](Policy p, bool compat, bool load_aware, float topo_weight, uint64_t seed) {
+             Options o;
+             o.policy = p;
+             o.compat = compat ? 1 : 0;
+             o.load_aware = load_aware ? 1 : 0;
+             o.topo_weight = topo_weight;
+             o.seed = seed;
+             return o;
+           }),
+           py::arg("policy") = Policy::kBinpack, py::arg("compat") = false,
+           py::arg("load_aware") = false, py::arg("topo_weight") = 1.0f, py::arg("seed") = 0)
+      .def_property_readonly("policy", [](const Options& o) { return o.policy; })
+      .def_property_readonly("compat", [](const Options& o) { return o.compat != 0; })
+      .def_property_readonly("load_aware", [](const Options& o) { return o.load_aware != 0; })
+      .def_property_readonly("topo_weight", [](const Options& o) { return o.topo_weight; })
+      .def_property_readonly("seed", [](const Options& o) { return o.seed; })
+      .def("__repr__", [](const Options& o) {
+        return "Options(policy=" + std::to_string(static_cast<int>(o.policy)) +
+               ", compat=" + std::to_string(o.compat) + ", load_aware=" + std::to_string(o.load_aware) + ")";
+      });
+
+  // Stateless policy entry points (tests, simulators, the reference oracle diff).
+  m.def(
+      "choose",
+      [](const py::list& devices, const std::vector<std::pair<int32_t, int64_t>>& demand,
+         const Options& o, const py::object& topo) -> py::tuple {
+        auto devs = to_devices(devices);
+        Topology t = to_topo(topo, devs);
+        Demand d = to_demand(demand);
+        Plan p;
+        std::memset(&p, 0, sizeof(p));
+        int32_t rc;
+        {
+          py::gil_scoped_release nogil;
+          rc = choose(devs.data(), static_cast<int>(devs.size()), &t, d, o, &p);
+        }
+        if (rc != kOk) return py::make_tuple(rc, py::none(), 0);
+        return py::make_tuple(rc, plan_list(p), p.score);
+      },
+      py::arg("devices"), py::arg("demand"), py::arg("options"), py::arg("topo") = py::none());
+  m.def(
+      "rate",
+      [](const py::list& devices, const std::vector<std::pair<int32_t, int64_t>>& demand,
+         const Options& o) {
+        auto devs = to_devices(devices);
+        Demand d = to_demand(demand);
+        return rate(devs.data(), static_cast<int>(devs.size()), d, o, nullptr);
+      },
+      py::arg("devices"), py::arg("demand"), py::arg("options"));
+  m.def(
+      "apply",
+      [](const py::list& devices, const std::vector<std::pair<int32_t, int64_t>>& demand,
+         const std::vector<std::vector<int>>& plan, bool release) {
+        auto devs = to_devices(devices);
+        Demand d = to_demand(demand);
+        Plan p = to_plan(plan);
+        const int32_t rc = release ? unapply(devs.data(), static_cast<int>(devs.size()), d, p)
+                                   : apply(devs.data(), static_cast<int>(devs.size()), d, p);
+        py::list out;
+        for (const Device& v : devs) out.append(from_device(v));
+        return py::make_tuple(rc, out);
+      },
+      py::arg("devices"), py::arg("demand"), py::arg("plan"), py::arg("release") = false);
+  m.def(
+      "frag",
+      [](const py::list& devices, int32_t min_request) {
+        auto devs = to_devices(devices);
+        FragStats s{};
+        frag_accumulate(devs.data(), static_cast<int>(devs.size()), min_request, &s);
+        return frag_dict(s);
+      },
+      py::arg("devices"), py::arg("min_request") = 0);
+  m.def("go116_sort_perm", [](const std::vector<int64_t>& keys) {
+    // Returns the permutation Go 1.16 sort.Sort leaves for ascending `keys`.
+    std::vector<int64_t> k = keys;
+    std::vector<int> idx(keys.size());
+    for (size_t i = 0; i < idx.size(); ++i) idx[i] = static_cast<int>(i);
+    gosort::sort(
+        static_cast<int>(k.size()), [&](int i, int j) { return k[i] < k[j]; },
+        [&](int i, int j) {
+          std::swap(k[i], k[j]);
+          std::swap(idx[i], idx[j]);
+        });
+    return idx;
+  });
+  m.def("demand_hash", [](const std::vector<std::pair<int32_t, int64_t>>& demand) {
+    return to_demand(demand).hash();
+  });
+
+  py::class_<Ledger, std::shared_ptr<Ledger>>(m, "Ledger")
+      .def(py::init<const std::string&, uint32_t, uint32_t, bool>(), py::arg("path") = "",
+           py::arg("max_nodes") = 1024, py::arg("max_pods") = 65536, py::arg("create") = true)
+      .def_static("region_bytes", &Ledger::region_bytes)
+      .def_property_readonly("path", &Ledger::path)
+      .def_property_readonly("bytes", &Ledger::bytes)
+      .def_property_readonly("n_nodes", &Ledger::n_nodes)
+      .def_property_readonly("n_pods", &Ledger::n_pods)
+      .def_property_readonly("epoch", &Ledger::epoch)
+      .def(
+          "upsert_node",
+          [](Ledger& l, const std::string& name, const py::list& devices, const py::object& topo) {
+            auto devs = to_devices(devices);
+            Topology t = to_topo(topo, devs);
+            const int32_t id = l.upsert_node(name, devs.data(), static_cast<int>(devs.size()), t);
+            if (id < 0) throw py::value_error(std::string("upsert_node: ") + err_str(-id));
+            return id;
+          },
+          py::arg("name"), py::arg("devices"), py::arg("topo") = py::none())
+      .def("find_node", &Ledger::find_node)
+      .def("node_name", &Ledger::node_name)
+      .def("remove_node", &Ledger::remove_node)
+      .def("generation", &Ledger::generation)
+      .def("snapshot",
+           [](const Ledger& l, int32_t id) -> py::object {
+             NodeSnapshot s;
+             if (!l.snapshot(id, &s)) return py::none();
+             py::dict d;
+             py::list devs;
+             for (int i = 0; i < s.n_devs; ++i) devs.append(from_device(s.devs[i]));
+             d["devices"] = devs;
+             d["generation"] = s.generation;
+             d["topo"] = from_topo(s.topo);
+             d["name"] = l.node_name(id);
+             return d;
+           })
+      .def(
+          "filter",
+          [](Ledger& l, const std::vector<int32_t>& ids,
+             const std::vector<std::pair<int32_t, int64_t>>& demand, const Options& o) {
+            Demand d = to_demand(demand);
+            std::vector<int32_t> rcs(ids.size());
+            {
+              py::gil_scoped_release nogil;
+              Plan p;
+              for (size_t i = 0; i < ids.size(); ++i) rcs[i] = ids[i] < 0 ? kErrUnknownNode : l.assume(ids[i], d, o, &p);
+            }
+            return rcs;
+          },
+          "Assume `demand` on every node id; returns one error code per node (0 = fits).")
+      .def(
+          "score",
+          [](Ledger& l, const std::vector<int32_t>& ids,
+             const std::vector<std::pair<int32_t, int64_t>>& demand, const Options& o) {
+            Demand d = to_demand(demand);
+            std::vector<int32_t> scores(ids.size());
+            {
+              py::gil_scoped_release nogil;
+              Plan p;
+              for (size_t i = 0; i < ids.size(); ++i) {
+                const int32_t rc = ids[i] < 0 ? kErrUnknownNode : l.assume(ids[i], d, o, &p);
+                scores[i] = rc == kOk ? p.score : 0;  // ScoreMin for unfit nodes (node.go:63-65)
+              }
+            }
+            return scores;
+          })
+      .def("assume",
+           [](Ledger& l, int32_t id, const std::vector<std::pair<int32_t, int64_t>>& demand,
+              const Options& o) -> py::tuple {
+             Demand d = to_demand(demand);
+             Plan p;
+             std::memset(&p, 0, sizeof(p));
+             int32_t rc;
+             {
+               py::gil_scoped_release nogil;
+               rc = l.assume(id, d, o, &p);
+             }
+             if (rc != kOk) return py::make_tuple(rc, py::none(), 0);
+             return py::make_tuple(rc, plan_list(p), p.score);
+           })
+      .def("reserve",
+           [](Ledger& l, int32_t id, const std::string& key,
+              const std::vector<std::pair<int32_t, int64_t>>& demand, const Options& o) -> py::tuple {
+             Demand d = to_demand(demand);
+             Plan p;
+             std::memset(&p, 0, sizeof(p));
+             int32_t rc;
+             {
+               py::gil_scoped_release nogil;
+               rc = l.reserve(id, key, d, o, &p);
+             }
+             if (rc != kOk && rc != kOkExisting) return py::make_tuple(rc, py::none());
+             return py::make_tuple(rc, plan_list(p));
+           })
+      .def("allocate_plan",
+           [](Ledger& l, int32_t id, const std::string& key,
+              const std::vector<std::pair<int32_t, int64_t>>& demand,
+              const std::vector<std::vector<int>>& plan, bool committed) {
+             Demand d = to_demand(demand);
+             Plan p = to_plan(plan);
+             py::gil_scoped_release nogil;
+             return l.allocate_plan(id, key, d, p, committed);
+           },
+           py::arg("node"), py::arg("key"), py::arg("demand"), py::arg("plan"),
+           py::arg("committed") = true)
+      .def("commit", &Ledger::commit, py::call_guard<py::gil_scoped_release>())
+      .def("release", &Ledger::release, py::call_guard<py::gil_scoped_release>())
+      .def("lookup",
+           [](const Ledger& l, const std::string& key) -> py::object {
+             PodRecord r;
+             if (!l.lookup(key, &r)) return py::none();
+             return record_dict(r);
+           })
+      .def("pods_on",
+           [](const Ledger& l, int32_t node) {
+             py::list out;
+             for (const PodRecord& r : l.pods_on(node)) out.append(record_dict(r));
+             return out;
+           },
+           py::arg("node") = -1)
+      .def("expired_reservations", &Ledger::expired_reservations)
+      .def("set_load", &Ledger::set_load)
+      .def("set_health", &Ledger::set_health)
+      .def("frag", [](const Ledger& l, int32_t min_request) { return frag_dict(l.frag(min_request)); },
+           py::arg("min_request") = 0)
+      .def("clear_cache", &Ledger::clear_cache)
+      .def_property_readonly("cache_size", &Ledger::cache_size);
+
+  m.def(
+      "discover_topology",
+      [](const std::string& root, bool use_amdsmi) {
+        HostTopology t;
+        {
+          py::gil_scoped_release nogil;
+          t = discover(root, use_amdsmi);
+        }
+        return to_json(t);
+      },
+      py::arg("root") = "", py::arg("use_amdsmi") = true,
+      "Reads KFD/DRM sysfs (+ libamd_smi) and returns the node GPU topology as JSON.");
+  m.def("mono_now", &mono_now);
+}

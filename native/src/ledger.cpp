@@ -1,0 +1,611 @@
+// Native cluster ledger (see ledger.h). Reference parity: pkg/dealer/dealer.go
+// (Assume :89-136, Score :138-153, Bind :155-203, Allocate :205-228, Release :230-255,
+// KnownPod :257-262, getNodeInfo :271-301) and pkg/dealer/node.go (PlanCache :18-98).
+#include "nanogpu/ledger.h"
+
+#include <errno.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <thread>
+
+namespace nanogpu {
+
+static constexpr uint64_t kMagic = 0x4e414e4f47505531ULL;  // "NANOGPU1"
+static constexpr uint32_t kVersion = 3;
+
+static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+uint64_t key_hash(const char* key) {
+  uint64_t h = 0xcbf29ce484222325ULL;
+  for (const unsigned char* p = reinterpret_cast<const unsigned char*>(key); *p; ++p) {
+    h ^= *p;
+    h *= 0x100000001b3ULL;
+  }
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdULL;
+  h ^= h >> 33;
+  return h;
+}
+
+double mono_now() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return static_cast<double>(ts.tv_sec) + 1e-9 * static_cast<double>(ts.tv_nsec);
+}
+
+static void init_mutex(pthread_mutex_t* m) {
+  pthread_mutexattr_t a;
+  pthread_mutexattr_init(&a);
+  pthread_mutexattr_setpshared(&a, PTHREAD_PROCESS_SHARED);
+  pthread_mutexattr_setrobust(&a, PTHREAD_MUTEX_ROBUST);
+  pthread_mutex_init(m, &a);
+  pthread_mutexattr_destroy(&a);
+}
+
+void Ledger::lock_mu(pthread_mutex_t* m) const {
+  const int rc = pthread_mutex_lock(m);
+  if (rc == EOWNERDEAD) {
+    // A worker died inside a critical section. Every mutation below validates before it
+    // writes and writes counters last, so the protected state is consistent enough to go on.
+    pthread_mutex_consistent(m);
+  } else if (rc != 0) {
+    throw std::runtime_error("ledger: pthread_mutex_lock failed");
+  }
+}
+
+void Ledger::lock_node(NodeSlot* n) const { lock_mu(&n->mu); }
+
+namespace {
+struct Unlock {
+  pthread_mutex_t* m;
+  ~Unlock() {
+    if (m) pthread_mutex_unlock(m);
+  }
+};
+uint32_t pods_per_shard_for(uint32_t max_pods) {
+  uint64_t per = (static_cast<uint64_t>(max_pods) * 3 / 2 + kPodShards - 1) / kPodShards;
+  return static_cast<uint32_t>(std::max<uint64_t>(per, 16));
+}
+}  // namespace
+
+size_t Ledger::region_bytes(uint32_t max_nodes, uint32_t max_pods) {
+  const size_t h = align_up(sizeof(LedgerHeader), 4096);
+  const size_t n = align_up(sizeof(NodeSlot) * max_nodes, 4096);
+  const size_t p = align_up(sizeof(PodSlot) * kPodShards * pods_per_shard_for(max_pods), 4096);
+  return h + n + p;
+}
+
+Ledger::Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, bool create)
+    : path_(path), owner_(false) {
+  if (max_nodes == 0 || max_pods == 0) throw std::invalid_argument("ledger: zero capacity");
+  bytes_ = region_bytes(max_nodes, max_pods);
+  bool init = false;
+  if (path.empty()) {
+    void* p = mmap(nullptr, bytes_, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (p == MAP_FAILED) throw std::runtime_error("ledger: mmap anonymous failed");
+    base_ = static_cast<char*>(p);
+    init = true;
+    owner_ = true;
+  } else {
+    if (create) {
+      fd_ = open(path.c_str(), O_RDWR | O_CREAT | O_EXCL, 0600);
+      if (fd_ >= 0) {
+        init = true;
+        owner_ = true;
+        if (ftruncate(fd_, static_cast<off_t>(bytes_)) != 0) {
+          close(fd_);
+          unlink(path.c_str());
+          throw std::runtime_error("ledger: ftruncate failed");
+        }
+      }
+    }
+    if (fd_ < 0) {
+      fd_ = open(path.c_str(), O_RDWR);
+      if (fd_ < 0) throw std::runtime_error("ledger: cannot open " + path);
+      // wait for the creator to size the file
+      for (int i = 0; i < 2000; ++i) {
+        struct stat st;
+        if (fstat(fd_, &st) == 0 && static_cast<size_t>(st.st_size) >= bytes_) break;
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      }
+    }
+    void* p = mmap(nullptr, bytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd_, 0);
+    if (p == MAP_FAILED) {
+      close(fd_);
+      throw std::runtime_error("ledger: mmap shared failed (geometry mismatch?)");
+    }
+    base_ = static_cast<char*>(p);
+  }
+  hdr_ = reinterpret_cast<LedgerHeader*>(base_);
+  nodes_ = reinterpret_cast<NodeSlot*>(base_ + align_up(sizeof(LedgerHeader), 4096));
+  pods_ = reinterpret_cast<PodSlot*>(reinterpret_cast<char*>(nodes_) +
+                                     align_up(sizeof(NodeSlot) * max_nodes, 4096));
+  if (init) {
+    hdr_->version = kVersion;
+    hdr_->max_nodes = max_nodes;
+    hdr_->pods_per_shard = pods_per_shard_for(max_pods);
+    hdr_->n_nodes.store(0);
+    hdr_->epoch.store(1);
+    hdr_->n_pods.store(0);
+    hdr_->attached.store(0);
+    init_mutex(&hdr_->registry_mu);
+    for (int s = 0; s < kPodShards; ++s) {
+      init_mutex(&hdr_->shard_mu[s]);
+      hdr_->shard_live[s] = 0;
+      hdr_->shard_tomb[s] = 0;
+    }
+    std::atomic_thread_fence(std::memory_order_release);
+    __atomic_store_n(&hdr_->magic, kMagic, __ATOMIC_RELEASE);
+  } else {
+    bool ok = false;
+    for (int i = 0; i < 5000; ++i) {
+      if (__atomic_load_n(&hdr_->magic, __ATOMIC_ACQUIRE) == kMagic) {
+        ok = true;
+        break;
+      }
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+    if (!ok || hdr_->version != kVersion || hdr_->max_nodes != max_nodes ||
+        hdr_->pods_per_shard != pods_per_shard_for(max_pods)) {
+      munmap(base_, bytes_);
+      close(fd_);
+      throw std::runtime_error("ledger: shared region has a different layout: " + path);
+    }
+  }
+  hdr_->attached.fetch_add(1);
+}
+
+Ledger::~Ledger() {
+  if (hdr_) hdr_->attached.fetch_sub(1);
+  if (base_) munmap(base_, bytes_);
+  if (fd_ >= 0) close(fd_);
+}
+
+NodeSlot* Ledger::node(int32_t id) const {
+  if (id < 0 || id >= hdr_->n_nodes.load(std::memory_order_acquire)) return nullptr;
+  return &nodes_[id];
+}
+
+PodSlot* Ledger::shard(int s) const {
+  return pods_ + static_cast<size_t>(s) * hdr_->pods_per_shard;
+}
+
+PodSlot* Ledger::find_pod_locked(int s, uint64_t h, const char* key) const {
+  PodSlot* t = shard(s);
+  const uint32_t cap = hdr_->pods_per_shard;
+  uint32_t i = static_cast<uint32_t>((h / kPodShards) % cap);
+  for (uint32_t probe = 0; probe < cap; ++probe, i = (i + 1) % cap) {
+    PodSlot& p = t[i];
+    if (p.state == kPodEmpty) return nullptr;
+    if (p.state != kPodTombstone && p.hash == h && std::strncmp(p.key, key, kKeyLen) == 0)
+      return &p;
+  }
+  return nullptr;
+}
+
+PodSlot* Ledger::insert_pod_locked(int s, uint64_t h, const char* key) {
+  const uint32_t cap = hdr_->pods_per_shard;
+  if (hdr_->shard_live[s] + hdr_->shard_tomb[s] + 1 > static_cast<int32_t>(cap * 9 / 10)) {
+    if (hdr_->shard_tomb[s] == 0) return nullptr;  // genuinely full
+    // compact: rehash live entries, dropping tombstones
+    PodSlot* t = shard(s);
+    std::vector<PodSlot> live;
+    live.reserve(hdr_->shard_live[s]);
+    for (uint32_t i = 0; i < cap; ++i)
+      if (t[i].state == kPodReserved || t[i].state == kPodCommitted) live.push_back(t[i]);
+    for (uint32_t i = 0; i < cap; ++i) t[i].state = kPodEmpty;
+    for (const PodSlot& p : live) {
+      uint32_t i = static_cast<uint32_t>((p.hash / kPodShards) % cap);
+      while (t[i].state != kPodEmpty) i = (i + 1) % cap;
+      t[i] = p;
+    }
+    hdr_->shard_tomb[s] = 0;
+  }
+  PodSlot* t = shard(s);
+  uint32_t i = static_cast<uint32_t>((h / kPodShards) % cap);
+  PodSlot* reuse = nullptr;
+  for (uint32_t probe = 0; probe < cap; ++probe, i = (i + 1) % cap) {
+    PodSlot& p = t[i];
+    if (p.state == kPodTombstone) {
+      if (!reuse) reuse = &p;
+      continue;
+    }
+    if (p.state == kPodEmpty) {
+      if (!reuse) reuse = &p;
+      break;
+    }
+  }
+  if (!reuse) return nullptr;
+  if (reuse->state == kPodTombstone) --hdr_->shard_tomb[s];
+  std::memset(reuse, 0, sizeof(PodSlot));
+  reuse->hash = h;
+  std::strncpy(reuse->key, key, kKeyLen - 1);
+  ++hdr_->shard_live[s];
+  return reuse;
+}
+
+int32_t Ledger::upsert_node(const std::string& name, const Device* devs, int n,
+                            const Topology& topo) {
+  if (n < 0 || n > kMaxDevs || name.empty() || name.size() >= kNameLen) return -kErrBadPlan;
+  lock_mu(&hdr_->registry_mu);
+  Unlock ur{&hdr_->registry_mu};
+  const int32_t count = hdr_->n_nodes.load(std::memory_order_acquire);
+  int32_t id = -1;
+  for (int32_t i = 0; i < count; ++i)
+    if (nodes_[i].in_use && std::strncmp(nodes_[i].name, name.c_str(), kNameLen) == 0) {
+      id = i;
+      break;
+    }
+  if (id < 0) {
+    if (static_cast<uint32_t>(count) >= hdr_->max_nodes) return -kErrTableFull;
+    id = count;
+    NodeSlot& s = nodes_[id];
+    std::memset(s.name, 0, kNameLen);
+    std::strncpy(s.name, name.c_str(), kNameLen - 1);
+    init_mutex(&s.mu);
+    s.generation.store(1);
+    s.n_devs = n;
+    s.n_pods = 0;
+    s.topo = topo;
+    std::memcpy(s.devs, devs, sizeof(Device) * n);
+    for (int i = 0; i < n; ++i) {
+      s.devs[i].pct_free = s.devs[i].pct_total;
+      s.devs[i].mib_free = s.devs[i].mib_total;
+    }
+    s.in_use = 1;
+    hdr_->n_nodes.store(count + 1, std::memory_order_release);
+  } else {
+    NodeSlot& s = nodes_[id];
+    lock_node(&s);
+    Unlock un{&s.mu};
+    Device merged[kMaxDevs];
+    int m = n;
+    for (int i = 0; i < n; ++i) {
+      merged[i] = devs[i];
+      if (i < s.n_devs) {
+        const Device& old = s.devs[i];
+        const int32_t used = old.pct_total - old.pct_free;
+        const int64_t mused = old.mib_total > 0 ? old.mib_total - old.mib_free : 0;
+        merged[i].pct_free = std::max(0, merged[i].pct_total - used);
+        merged[i].mib_free = merged[i].mib_total > 0 ? std::max<int64_t>(0, merged[i].mib_total - mused) : 0;
+        merged[i].load_usage = old.load_usage;
+        merged[i].remain_load = old.remain_load;
+      } else {
+        merged[i].pct_free = merged[i].pct_total;
+        merged[i].mib_free = merged[i].mib_total;
+      }
+    }
+    // Devices that vanished while still in use stay (unhealthy) until their pods release.
+    for (int i = n; i < s.n_devs; ++i)
+      if (s.devs[i].pct_free != s.devs[i].pct_total) m = i + 1;
+    for (int i = n; i < m; ++i) {
+      merged[i] = s.devs[i];
+      merged[i].healthy = 0;
+    }
+    std::memcpy(s.devs, merged, sizeof(Device) * m);
+    s.n_devs = m;
+    s.topo = topo;
+    s.generation.fetch_add(1);
+  }
+  hdr_->epoch.fetch_add(1);
+  {
+    std::lock_guard<std::mutex> g(names_mu_);
+    names_[name] = id;
+  }
+  return id;
+}
+
+int32_t Ledger::find_node(const std::string& name) const {
+  {
+    std::lock_guard<std::mutex> g(names_mu_);
+    auto it = names_.find(name);
+    if (it != names_.end() && nodes_[it->second].in_use) return it->second;
+  }
+  const int32_t count = hdr_->n_nodes.load(std::memory_order_acquire);
+  for (int32_t i = 0; i < count; ++i)
+    if (nodes_[i].in_use && std::strncmp(nodes_[i].name, name.c_str(), kNameLen) == 0) {
+      std::lock_guard<std::mutex> g(names_mu_);
+      names_[name] = i;
+      return i;
+    }
+  return -1;
+}
+
+std::string Ledger::node_name(int32_t id) const {
+  NodeSlot* n = node(id);
+  return n ? std::string(n->name) : std::string();
+}
+
+bool Ledger::remove_node(int32_t id) {
+  NodeSlot* n = node(id);
+  if (!n) return false;
+  lock_node(n);
+  Unlock un{&n->mu};
+  if (n->n_pods > 0) return false;
+  n->in_use = 0;
+  n->generation.fetch_add(1);
+  hdr_->epoch.fetch_add(1);
+  std::lock_guard<std::mutex> g(names_mu_);
+  names_.erase(n->name);
+  return true;
+}
+
+bool Ledger::snapshot(int32_t id, NodeSnapshot* out) const {
+  NodeSlot* n = node(id);
+  if (!n || !n->in_use) return false;
+  lock_node(n);
+  Unlock un{&n->mu};
+  out->n_devs = n->n_devs;
+  out->generation = n->generation.load(std::memory_order_relaxed);
+  out->topo = n->topo;
+  std::memcpy(out->devs, n->devs, sizeof(Device) * n->n_devs);
+  return true;
+}
+
+uint64_t Ledger::generation(int32_t id) const {
+  NodeSlot* n = node(id);
+  return n ? n->generation.load(std::memory_order_acquire) : 0;
+}
+
+int32_t Ledger::assume(int32_t id, const Demand& d, const Options& o, Plan* plan) {
+  NodeSnapshot snap;
+  if (!snapshot(id, &snap)) return kErrUnknownNode;
+  const CacheKey k{id, snap.generation, d.hash(), o.hash()};
+  {
+    std::lock_guard<std::mutex> g(cache_mu_);
+    auto it = cache_.find(k);
+    if (it != cache_.end()) {
+      *plan = it->second.plan;
+      return it->second.rc;
+    }
+  }
+  const int32_t rc = choose(snap.devs, snap.n_devs, &snap.topo, d, o, plan);
+  {
+    std::lock_guard<std::mutex> g(cache_mu_);
+    if (cache_.size() > 262144) cache_.clear();
+    cache_[k] = CacheVal{rc, *plan};
+  }
+  return rc;
+}
+
+int32_t Ledger::reserve(int32_t id, const std::string& key, const Demand& d, const Options& o,
+                        Plan* plan) {
+  NodeSlot* n = node(id);
+  if (!n || !n->in_use) return kErrUnknownNode;
+  if (key.empty() || key.size() >= kKeyLen) return kErrBadDemand;
+  const uint64_t h = key_hash(key.c_str());
+  const int s = shard_of(h);
+  lock_node(n);
+  Unlock un{&n->mu};
+  {
+    lock_mu(&hdr_->shard_mu[s]);
+    Unlock us{&hdr_->shard_mu[s]};
+    PodSlot* p = find_pod_locked(s, h, key.c_str());
+    if (p) {
+      if (p->node != id) return kErrPodExists;
+      *plan = p->plan;
+      return kOkExisting;
+    }
+  }
+  const uint64_t gen = n->generation.load(std::memory_order_relaxed);
+  const CacheKey k{id, gen, d.hash(), o.hash()};
+  bool hit = false;
+  int32_t rc = kOk;
+  {
+    std::lock_guard<std::mutex> g(cache_mu_);
+    auto it = cache_.find(k);
+    if (it != cache_.end()) {
+      hit = true;
+      rc = it->second.rc;
+      *plan = it->second.plan;
+    }
+  }
+  if (!hit) rc = choose(n->devs, n->n_devs, &n->topo, d, o, plan);
+  if (rc != kOk) return rc;
+  rc = apply(n->devs, n->n_devs, d, *plan);
+  if (rc != kOk) return rc;
+  {
+    lock_mu(&hdr_->shard_mu[s]);
+    Unlock us{&hdr_->shard_mu[s]};
+    PodSlot* p = insert_pod_locked(s, h, key.c_str());
+    if (!p) {
+      unapply(n->devs, n->n_devs, d, *plan);
+      return kErrTableFull;
+    }
+    p->node = id;
+    p->demand = d;
+    p->plan = *plan;
+    p->t_reserved = mono_now();
+    p->state = kPodReserved;
+  }
+  ++n->n_pods;
+  n->generation.fetch_add(1, std::memory_order_release);
+  hdr_->n_pods.fetch_add(1);
+  hdr_->epoch.fetch_add(1);
+  return kOk;
+}
+
+int32_t Ledger::allocate_plan(int32_t id, const std::string& key, const Demand& d,
+                              const Plan& plan, bool committed) {
+  NodeSlot* n = node(id);
+  if (!n || !n->in_use) return kErrUnknownNode;
+  if (key.empty() || key.size() >= kKeyLen) return kErrBadDemand;
+  const uint64_t h = key_hash(key.c_str());
+  const int s = shard_of(h);
+  lock_node(n);
+  Unlock un{&n->mu};
+  {
+    lock_mu(&hdr_->shard_mu[s]);
+    Unlock us{&hdr_->shard_mu[s]};
+    PodSlot* p = find_pod_locked(s, h, key.c_str());
+    if (p) {
+      if (p->node != id) return kErrPodExists;
+      if (committed) p->state = kPodCommitted;
+      return kOk;  // already accounted (reference dealer.go:214-216)
+    }
+  }
+  int32_t rc = apply(n->devs, n->n_devs, d, plan);
+  if (rc != kOk) return rc;
+  {
+    lock_mu(&hdr_->shard_mu[s]);
+    Unlock us{&hdr_->shard_mu[s]};
+    PodSlot* p = insert_pod_locked(s, h, key.c_str());
+    if (!p) {
+      unapply(n->devs, n->n_devs, d, plan);
+      return kErrTableFull;
+    }
+    p->node = id;
+    p->demand = d;
+    p->plan = plan;
+    p->t_reserved = mono_now();
+    p->state = committed ? kPodCommitted : kPodReserved;
+  }
+  ++n->n_pods;
+  n->generation.fetch_add(1, std::memory_order_release);
+  hdr_->n_pods.fetch_add(1);
+  hdr_->epoch.fetch_add(1);
+  return kOk;
+}
+
+int32_t Ledger::commit(const std::string& key) {
+  const uint64_t h = key_hash(key.c_str());
+  const int s = shard_of(h);
+  lock_mu(&hdr_->shard_mu[s]);
+  Unlock us{&hdr_->shard_mu[s]};
+  PodSlot* p = find_pod_locked(s, h, key.c_str());
+  if (!p) return kErrUnknownPod;
+  p->state = kPodCommitted;
+  return kOk;
+}
+
+int32_t Ledger::release(const std::string& key) {
+  const uint64_t h = key_hash(key.c_str());
+  const int s = shard_of(h);
+  int32_t id;
+  {
+    lock_mu(&hdr_->shard_mu[s]);
+    Unlock us{&hdr_->shard_mu[s]};
+    PodSlot* p = find_pod_locked(s, h, key.c_str());
+    if (!p) return kErrUnknownPod;
+    id = p->node;
+  }
+  NodeSlot* n = node(id);
+  if (!n) return kErrUnknownNode;
+  lock_node(n);
+  Unlock un{&n->mu};
+  lock_mu(&hdr_->shard_mu[s]);
+  Unlock us{&hdr_->shard_mu[s]};
+  PodSlot* p = find_pod_locked(s, h, key.c_str());
+  if (!p || p->node != id) return kErrUnknownPod;  // raced with another release
+  unapply(n->devs, n->n_devs, p->demand, p->plan);
+  p->state = kPodTombstone;
+  --hdr_->shard_live[s];
+  ++hdr_->shard_tomb[s];
+  --n->n_pods;
+  n->generation.fetch_add(1, std::memory_order_release);
+  hdr_->n_pods.fetch_sub(1);
+  hdr_->epoch.fetch_add(1);
+  return kOk;
+}
+
+bool Ledger::lookup(const std::string& key, PodRecord* out) const {
+  const uint64_t h = key_hash(key.c_str());
+  const int s = shard_of(h);
+  lock_mu(&hdr_->shard_mu[s]);
+  Unlock us{&hdr_->shard_mu[s]};
+  PodSlot* p = find_pod_locked(s, h, key.c_str());
+  if (!p) return false;
+  out->key = p->key;
+  out->node = p->node;
+  out->state = p->state;
+  out->t_reserved = p->t_reserved;
+  out->demand = p->demand;
+  out->plan = p->plan;
+  return true;
+}
+
+std::vector<PodRecord> Ledger::pods_on(int32_t node_id) const {
+  std::vector<PodRecord> out;
+  for (int s = 0; s < kPodShards; ++s) {
+    lock_mu(&hdr_->shard_mu[s]);
+    Unlock us{&hdr_->shard_mu[s]};
+    PodSlot* t = shard(s);
+    for (uint32_t i = 0; i < hdr_->pods_per_shard; ++i) {
+      const PodSlot& p = t[i];
+      if ((p.state == kPodReserved || p.state == kPodCommitted) && (node_id < 0 || p.node == node_id))
+        out.push_back(PodRecord{p.key, p.node, p.state, p.t_reserved, p.demand, p.plan});
+    }
+  }
+  return out;
+}
+
+std::vector<std::string> Ledger::expired_reservations(double older_than_s) const {
+  std::vector<std::string> out;
+  const double now = mono_now();
+  for (int s = 0; s < kPodShards; ++s) {
+    lock_mu(&hdr_->shard_mu[s]);
+    Unlock us{&hdr_->shard_mu[s]};
+    PodSlot* t = shard(s);
+    for (uint32_t i = 0; i < hdr_->pods_per_shard; ++i)
+      if (t[i].state == kPodReserved && now - t[i].t_reserved > older_than_s) out.emplace_back(t[i].key);
+  }
+  return out;
+}
+
+int32_t Ledger::set_load(int32_t id, int dev, float usage) {
+  NodeSlot* n = node(id);
+  if (!n) return kErrUnknownNode;
+  lock_node(n);
+  Unlock un{&n->mu};
+  if (dev < 0 || dev >= n->n_devs) return kErrBadPlan;
+  Device& d = n->devs[dev];
+  d.load_usage = usage;
+  d.remain_load = static_cast<int16_t>(kLoadTotal - static_cast<int>(usage));
+  n->generation.fetch_add(1, std::memory_order_release);
+  hdr_->epoch.fetch_add(1);
+  return kOk;
+}
+
+int32_t Ledger::set_health(int32_t id, int dev, bool healthy) {
+  NodeSlot* n = node(id);
+  if (!n) return kErrUnknownNode;
+  lock_node(n);
+  Unlock un{&n->mu};
+  if (dev < 0 || dev >= n->n_devs) return kErrBadPlan;
+  n->devs[dev].healthy = healthy ? 1 : 0;
+  n->generation.fetch_add(1, std::memory_order_release);
+  hdr_->epoch.fetch_add(1);
+  return kOk;
+}
+
+FragStats Ledger::frag(int32_t min_request) const {
+  FragStats s{};
+  const int32_t count = n_nodes();
+  for (int32_t i = 0; i < count; ++i) {
+    NodeSlot* n = &nodes_[i];
+    if (!n->in_use) continue;
+    lock_node(n);
+    Unlock un{&n->mu};
+    frag_accumulate(n->devs, n->n_devs, min_request, &s);
+  }
+  return s;
+}
+
+void Ledger::clear_cache() {
+  std::lock_guard<std::mutex> g(cache_mu_);
+  cache_.clear();
+}
+
+size_t Ledger::cache_size() const {
+  std::lock_guard<std::mutex> g(cache_mu_);
+  return cache_.size();
+}
+
+}  // namespace nanogpu

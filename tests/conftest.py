@@ -1,0 +1,43 @@
+import os
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu on the GPU box)")
+    config.addinivalue_line("markers", "slow: long-running (stress / multi-process)")
+
+
+def _ensure_built():
+    """Build the in-tree native core once per session (seconds; skipped when up to date)."""
+    sys.path.insert(0, str(ROOT / "native"))
+    import build  # native/build.py
+
+    build.build_core()
+    build.build_topo_cli()
+
+
+_ensure_built()
+
+
+@pytest.fixture
+def fake_store():
+    from nanogpu.k8s.fake_apiserver import FakeKubeStore
+
+    return FakeKubeStore()
+
+
+@pytest.fixture
+def tmp_shm(tmp_path):
+    """A ledger path in /dev/shm that is removed afterwards."""
+    p = Path("/dev/shm") / f"nanogpu-test-{os.getpid()}-{tmp_path.name}"
+    yield str(p)
+    try:
+        p.unlink()
+    except FileNotFoundError:
+        pass
