@@ -1,0 +1,311 @@
+"""Headline benchmark: pods/s + p50 bind latency + GPU frag%, 1k-pod burst on 8xMI355X nodes.
+
+Metric and config come from BASELINE.json ("pods/sec + p50 bind latency + GPU frag%, 1k-pod
+burst on 8xMI355X"). The reference publishes no number, so vs_baseline is null.
+
+What one step is (all of it inside the timed region):
+  * a burst of `--pods` (default 1000) pods is created in the API server, mixed
+    gpu-percent {10, 25, 50} with HBM requests {8, 16, 32, 64} GiB;
+  * every pod goes through the full extender protocol over loopback HTTP: a
+    kube-scheduler stand-in runs filter -> priorities -> select host, then an async bind;
+    the extender reserves on the native ledger, PATCHes the placement annotations and
+    POSTs the binding;
+  * after the burst the whole burst is deleted and the pod controller releases every
+    share from the ledger (the create/delete churn of BASELINE config 5).
+`value` = pods bound per second over the K timed steps (whole job, all ranks).
+
+Scaling (`--gpus N`, one torchrun rank per GPU): every rank is one extender worker; all
+workers share ONE native ledger in /dev/shm (the SO_REUSEPORT replica design of
+nanogpu.app), each drives 1/N of the burst through its own HTTP endpoint, so the burst and
+the cluster are fixed while workers are added ("strong" scaling). The GPUs are used for the
+node model: each rank reads its MI355X through the native KFD/amdsmi reader + HIP probe,
+and with N > 1 an RCCL all-reduce between rank pairs measures the xGMI link bandwidth that
+the topology scorer uses. Data: synthetic pods; cluster of `--nodes` simulated nodes cloned
+from the discovered MI355X.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import random
+import statistics
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "pods/sec + p50 bind latency + GPU frag%, 1k-pod burst on 8×MI355X"
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--pods", type=int, default=1000, help="pods per burst (whole job)")
+    ap.add_argument("--nodes", type=int, default=64, help="simulated 8xMI355X nodes")
+    ap.add_argument("--gpus-per-node", type=int, default=8)
+    ap.add_argument("--partition", default="SPX", choices=["SPX", "DPX", "QPX", "CPX"])
+    ap.add_argument("--policy", default="binpack")
+    ap.add_argument("--compat", action="store_true", help="reference (Go 1.16) placement semantics")
+    ap.add_argument("--api-rtt-ms", type=float, default=0.0, help="modelled API-server round trip")
+    ap.add_argument("--inflight-binds", type=int, default=64)
+    ap.add_argument("--no-gpu", action="store_true", help="skip GPU discovery (CPU-only rehearsal)")
+    ap.add_argument("--json-out", default="")
+    return ap.parse_args()
+
+
+# --------------------------------------------------------------------------- distributed
+class Dist:
+    def __init__(self, want: int):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        self.device = None
+        self.cuda = False
+        if want > 1 and self.world == 1:
+            print(f"bench: --gpus {want} requested without torchrun; running 1 rank", file=sys.stderr)
+
+    def init(self, use_gpu: bool):
+        import torch
+
+        self.cuda = use_gpu and torch.cuda.is_available()
+        if self.cuda:
+            torch.cuda.set_device(self.local_rank)
+            self.device = torch.device("cuda", self.local_rank)
+        if self.world > 1:
+            import torch.distributed as dist
+
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("nccl" if self.cuda else "gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist is not None:
+            if self.cuda:
+                self.dist.barrier(device_ids=[self.local_rank])
+            else:
+                self.dist.barrier()
+
+    def sync(self):
+        if self.cuda:
+            import torch
+
+            torch.cuda.synchronize()
+
+    def max(self, v: float) -> float:
+        if self.dist is None:
+            return v
+        import torch
+
+        t = torch.tensor([v], dtype=torch.float64, device=self.device if self.cuda else "cpu")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def gather_obj(self, obj):
+        if self.dist is None:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def bcast_obj(self, obj):
+        if self.dist is None:
+            return obj
+        lst = [obj]
+        self.dist.broadcast_object_list(lst, src=0)
+        return lst[0]
+
+    def close(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+
+
+# --------------------------------------------------------------------------- node template
+def node_template(d: Dist, args) -> tuple[object, dict]:
+    from nanogpu.topology.model import synthetic_mi355x
+
+    info = {"gpu": None, "link_bw_source": "placeholder"}
+    hbm_mib = 288 * 1024
+    if not args.no_gpu:
+        from nanogpu.probe.calibrate import local_gpu_facts
+
+        facts = local_gpu_facts(0 if not d.cuda else d.local_rank)
+        gpus = facts["host"].get("gpus") or []
+        props = facts.get("props") or {}
+        if gpus:
+            hbm_mib = int(gpus[0]["vram_bytes"]) // (1 << 20)
+        elif props.get("total_mem_bytes"):
+            hbm_mib = int(props["total_mem_bytes"]) // (1 << 20)
+        info["gpu"] = {"gcn_arch": props.get("gcn_arch"), "cus": props.get("cus"),
+                       "hbm_mib": hbm_mib, "partition": gpus[0].get("compute_partition") if gpus else None,
+                       "numa": gpus[0].get("numa") if gpus else None}
+    link = 153.0
+    if d.dist is not None and d.cuda:
+        from nanogpu.probe.calibrate import link_matrix
+
+        m = link_matrix(d.dist, d.device)
+        off = [m[a][b] for a in range(len(m)) for b in range(len(m)) if a != b and m[a][b] > 0]
+        if off:
+            link = statistics.mean(off)
+            info["link_bw_source"] = f"rccl all-reduce between {len(m)} ranks"
+            info["link_bw_matrix_gbs"] = [[round(x, 1) for x in r] for r in m]
+    info["link_bw_gbs"] = round(link, 1)
+    topo = synthetic_mi355x(args.gpus_per_node, args.partition, hbm_mib=hbm_mib, link_gbs=link)
+    return topo, info
+
+
+# --------------------------------------------------------------------------- workload
+SIZES = (10, 25, 50)
+HBM_GIB = (8, 16, 32, 64)
+
+
+def burst(rank: int, world: int, total: int, step: int, seed: int) -> list[dict]:
+    from nanogpu.k8s import podutil as pu
+
+    rng = random.Random(seed * 1000003 + step)
+    pods = []
+    for i in range(total):
+        pct, gib = rng.choice(SIZES), rng.choice(HBM_GIB)
+        if i % world != rank:
+            continue
+        pods.append(pu.make_pod(f"s{step}-p{i}", [("main", pct, gib * 1024)], namespace=f"bench-r{rank}"))
+    return pods
+
+
+async def run_rank(d: Dist, args, topo, ledger_path: str) -> dict:
+    from nanogpu import types as T
+    from nanogpu.app import Config, Runtime
+    from nanogpu.k8s import podutil as pu
+    from nanogpu.k8s.fake_apiserver import Faults, FakeKubeStore, InProcKube
+    from nanogpu.sim.driver import HttpExtenderClient, SchedulerDriver, node_capacities
+
+    store = FakeKubeStore(faults=Faults(latency_s=args.api_rtt_ms / 1e3))
+    topo_json = topo.to_json()
+    n_dev = len(topo.devices)
+    nodes = [pu.make_node(f"mi355x-{i:03d}", n_dev, topo_json, {"amd.com/gpu.present": "true"})
+             for i in range(args.nodes)]
+    for n in nodes:
+        store.add_node(n)
+    cfg = Config(port=0, host="127.0.0.1", priority=args.policy, compat=args.compat, ledger_path=ledger_path,
+                 max_nodes=max(1024, args.nodes), max_pods=max(65536, 4 * args.pods),
+                 policy_config_path="/nonexistent/policy.yaml", reservation_ttl_s=3600)
+    rt = Runtime(cfg, worker=0, api=InProcKube(store))
+    await rt.start()
+    client = HttpExtenderClient(f"http://127.0.0.1:{rt.bound_port}", pool=args.inflight_binds + 8)
+    names = [pu.meta(n)["name"] for n in nodes]
+    caps = node_capacities(nodes)
+    api = InProcKube(store)
+    pod_ctrl = rt.controllers[-1]
+    results = {"steps": [], "frag": []}
+
+    async def one_step(step: int, timed: bool) -> dict:
+        pods = burst(d.rank, d.world, args.pods, step, 7)
+        drv = SchedulerDriver(client, api, names, caps, max_inflight_binds=args.inflight_binds, seed=step)
+        stats = await drv.run(pods)
+        # all ranks finished their share of the burst: peak occupancy
+        d.barrier()
+        frag = rt.state.frag(min(SIZES))
+        ns = f"bench-r{d.rank}"
+        for p in pods:
+            try:
+                store.delete_pod(ns, pu.meta(p)["name"])
+            except Exception:
+                pass
+        # the pod controller releases on DELETED; wait until our shares are gone
+        uids = [pu.pod_uid(p) for p in pods]
+        for _ in range(20000):
+            if not any(rt.state.ledger.lookup(u) for u in uids):
+                break
+            await asyncio.sleep(0.0005)
+        await pod_ctrl.queue.drain(5.0)
+        return {"stats": stats.summary(), "frag": frag}
+
+    for w in range(args.warmup):
+        await one_step(10_000 + w, False)
+    rt.tracer.buf.clear()
+    d.barrier()
+    d.sync()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        r = await one_step(s, True)
+        results["steps"].append(r["stats"])
+        results["frag"].append(r["frag"])
+    d.barrier()
+    d.sync()
+    elapsed = time.perf_counter() - t0
+    binds = sorted(s["dur_ms"] for s in rt.tracer.dump(10 ** 9, "bind") if s["ok"])
+    results["elapsed_s"] = elapsed
+    results["bind_ms"] = binds
+    results["scheduled"] = sum(s["scheduled"] for s in results["steps"])
+    results["failed"] = sum(s["failed"] for s in results["steps"])
+    await client.close()
+    await rt.stop()
+    return results
+
+
+def main() -> int:
+    args = parse_args()
+    d = Dist(args.gpus)
+    d.init(use_gpu=not args.no_gpu)
+    topo, gpu_info = node_template(d, args)
+    # one shared ledger for all workers of this job
+    tag = os.environ.get("MASTER_PORT", str(os.getpid()))
+    ledger_path = d.bcast_obj(f"/dev/shm/nanogpu-bench-{tag}-{int(time.time())}" if d.rank == 0 else None)
+    from nanogpu.native import core
+
+    led = None
+    if d.rank == 0:
+        led = core().Ledger(ledger_path, max(1024, args.nodes), max(65536, 4 * args.pods), True)
+    d.barrier()
+    try:
+        res = asyncio.run(run_rank(d, args, topo, ledger_path))
+    finally:
+        d.barrier()
+        if d.rank == 0:
+            try:
+                os.unlink(ledger_path)
+            except OSError:
+                pass
+    elapsed = d.max(res["elapsed_s"])
+    all_binds = [b for r in d.gather_obj(res["bind_ms"]) for b in r]
+    scheduled = sum(d.gather_obj(res["scheduled"]))
+    failed = sum(d.gather_obj(res["failed"]))
+    del led
+    if d.rank == 0:
+        all_binds.sort()
+        p50 = statistics.median(all_binds) if all_binds else None
+        p99 = all_binds[min(len(all_binds) - 1, int(0.99 * len(all_binds)))] if all_binds else None
+        fr = res["frag"]
+        value = scheduled / elapsed if elapsed > 0 else 0.0
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "pods/s", "n_gpus": d.world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / max(1, args.steps), 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "n/a",
+            "data": "synthetic (pod bursts; simulated nodes cloned from the discovered MI355X)",
+            "config": {"model": f"nano-gpu-scheduler extender ({args.policy}{', compat' if args.compat else ''})",
+                       "global_batch": args.pods, "seq_len": None,
+                       "parallelism": f"{d.world} extender worker(s), shared native ledger",
+                       "cluster": f"{args.nodes} nodes x {args.gpus_per_node} MI355X ({args.partition})",
+                       "api_rtt_ms": args.api_rtt_ms},
+            "p50_bind_ms": round(p50, 4) if p50 is not None else None,
+            "p99_bind_ms": round(p99, 4) if p99 is not None else None,
+            "frag_pct": round(statistics.mean(f["frag_pct"] for f in fr), 3) if fr else None,
+            "frag_hbm_pct": round(statistics.mean(f["frag_mib"] for f in fr), 3) if fr else None,
+            "stranded_pct": round(statistics.mean(f["stranded_pct"] for f in fr), 3) if fr else None,
+            "scheduled": scheduled, "failed": failed, "gpu": gpu_info,
+        }
+        print(json.dumps(line), flush=True)
+        if args.json_out:
+            Path(args.json_out).write_text(json.dumps(line, indent=1))
+    d.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,265 @@
+"""Process wiring: informers, controllers, policy reload, telemetry, HTTP server, workers.
+
+Reference: cmd/main.go:75-137 (flags -> rater -> clientset -> signals -> informer factory
+-> controller -> DSContext -> verbs -> router -> ListenAndServe). Differences:
+  * the ledger is rebuilt after the informers sync (reference builds the dealer before
+    WaitForCacheSync, SURVEY §3.1 ordering hazard);
+  * `workers > 1` forks SO_REUSEPORT replicas that share one native ledger in /dev/shm;
+    worker 0 is the leader (pod controller, telemetry, reservation sweeper), every worker
+    runs a node informer and serves all verbs;
+  * first SIGINT/SIGTERM drains, a second exits(1) (reference signals.go:16-30).
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import os
+import signal
+import sys
+from dataclasses import dataclass, field
+
+from . import types as T
+
+log = logging.getLogger("nanogpu")
+
+
+@dataclass
+class Config:
+    priority: str = T.PRIORITY_BINPACK
+    policy_config_path: str = T.DEFAULT_POLICY_PATH
+    prometheus_url: str = T.DEFAULT_PROMETHEUS_URL
+    instance_port: str = "9100"                 # accepted for flag compatibility (unused, as in the reference)
+    sync_period_s: float = 5.0
+    is_load_schedule: bool = False
+    port: int = T.DEFAULT_PORT
+    host: str = "0.0.0.0"
+    threadness: int = 1
+    kubeconfig: str | None = None
+    kube_api: str | None = None                 # explicit API server URL (tests / fake cluster)
+    compat: bool = False
+    score_normalize: bool = False
+    topology_weight: float = 1.0
+    track_hbm: bool = True
+    workers: int = 1
+    ledger_path: str = ""
+    max_nodes: int = 4096
+    max_pods: int = 131072
+    verify_pod_on_bind: bool = False
+    reservation_ttl_s: float = 60.0
+    policy_reload_s: float = 3.0
+    fake_cluster: int = 0                       # >0: serve against an in-process fake cluster of N nodes
+    fake_gpus_per_node: int = 8
+    fake_partition: str = "SPX"
+    seed: int = 0
+    gpu_node_selectors: list = field(default_factory=lambda: [T.AMD_GPU_NODE_LABEL, T.LEGACY_GPU_NODE_LABEL])
+
+
+class Runtime:
+    """Everything one worker process runs; also used in-process by tests and the bench."""
+
+    def __init__(self, cfg: Config, worker: int = 0, api=None):
+        from .extender.verbs import Extender
+        from .obs import Metrics, Tracer
+        from .state.cluster import ClusterState
+
+        self.cfg = cfg
+        self.worker = worker
+        self.leader = worker == 0
+        self.api = api
+        self.node_informer = None
+        self.pod_informer = None
+        self.state = ClusterState(
+            policy=cfg.priority, compat=cfg.compat, load_aware=cfg.is_load_schedule,
+            topo_weight=cfg.topology_weight, seed=cfg.seed, ledger_path=cfg.ledger_path,
+            max_nodes=cfg.max_nodes, max_pods=cfg.max_pods, track_hbm=cfg.track_hbm,
+            node_source=self._node_from_cache, score_normalize=cfg.score_normalize)
+        self.metrics = Metrics()
+        self.tracer = Tracer()
+        self.extender: Extender | None = None
+        self.ready = asyncio.Event()
+        self.tasks: list[asyncio.Task] = []
+        self.controllers = []
+        self.poller = None
+        self.watcher = None
+        self.runner = None
+        self.bound_port = 0
+        self._fake = None
+
+    def _node_from_cache(self, name: str):
+        return self.node_informer.get(name) if self.node_informer else None
+
+    async def _make_api(self):
+        if self.api is not None:
+            return self.api
+        if self.cfg.fake_cluster > 0:
+            from .k8s import podutil as pu
+            from .k8s.fake_apiserver import FakeKubeStore, InProcKube
+            from .topology.model import synthetic_mi355x
+
+            store = FakeKubeStore()
+            topo = synthetic_mi355x(self.cfg.fake_gpus_per_node, self.cfg.fake_partition).to_json()
+            devices = self.cfg.fake_gpus_per_node * {"SPX": 1, "DPX": 2, "QPX": 4, "CPX": 8}[self.cfg.fake_partition]
+            for i in range(self.cfg.fake_cluster):
+                store.add_node(pu.make_node(f"mi355x-{i}", devices, topo, {"amd.com/gpu.present": "true"}))
+            self._fake = store
+            return InProcKube(store)
+        from .k8s.client import KubeClient, KubeConfig
+
+        return KubeClient(KubeConfig.auto(self.cfg.kubeconfig, self.cfg.kube_api))
+
+    async def start(self, serve: bool = True) -> None:
+        from .config.policy import PolicyWatcher
+        from .controller.pods import NodeController, PodController
+        from .extender import server
+        from .extender.verbs import Extender
+        from .k8s.informer import Informer
+
+        self.api = await self._make_api()
+        self.node_informer = Informer(self.api, "nodes", resync_s=self.cfg.sync_period_s)
+        self.controllers.append(NodeController(self.state, self.node_informer))
+        self.tasks.append(self.node_informer.start())
+        if self.leader:
+            self.pod_informer = Informer(self.api, "pods")
+            pc = PodController(self.state, self.pod_informer, workers=self.cfg.threadness, metrics=self.metrics)
+            self.controllers.append(pc)
+            pc.start()
+            self.tasks.append(self.pod_informer.start())
+        await self.node_informer.synced.wait()
+        if self.pod_informer is not None:
+            await self.pod_informer.synced.wait()
+            await self.controllers[-1].queue.drain(30.0)   # initial ADDs rebuild the ledger
+        self.extender = Extender(self.state, self.api, self.metrics, self.tracer,
+                                 verify_pod_on_bind=self.cfg.verify_pod_on_bind)
+        # policy file: real hot reload
+        self.watcher = PolicyWatcher(self.cfg.policy_config_path, self.cfg.policy_reload_s)
+        self.watcher.subscribe(self._apply_policy)
+        if self.cfg.is_load_schedule and self.leader:
+            from .telemetry.poller import LoadPoller
+            from .telemetry.prom import PromClient
+
+            self.poller = LoadPoller(self.state, PromClient(self.cfg.prometheus_url), self.node_informer.list,
+                                     selectors=self.cfg.gpu_node_selectors)
+            self.watcher.subscribe(self.poller.on_policy)
+        self.watcher.load_now()
+        if os.path.exists(self.cfg.policy_config_path):
+            self.tasks.append(self.watcher.start())
+        elif self.cfg.is_load_schedule:
+            log.warning("load-aware scheduling enabled but %s is missing; no metrics will be polled",
+                        self.cfg.policy_config_path)
+        if self.leader:
+            self.tasks.append(asyncio.ensure_future(self._sweeper()))
+        self.ready.set()
+        if serve:
+            app = server.make_app(self.extender, self.ready)
+            self.runner, self.bound_port = await server.start(app, self.cfg.host, self.cfg.port,
+                                                              reuse_port=self.cfg.workers > 1)
+            log.info("worker %d serving on :%d (policy=%s compat=%s)", self.worker, self.bound_port,
+                     self.state.policy, self.state.options.compat)
+
+    def _apply_policy(self, spec) -> None:
+        pol = spec.policy or self.state.policy
+        self.state.set_policy(pol, compat=spec.compat, topo_weight=spec.topology_weight)
+        if spec.score_normalize is not None:
+            self.state.score_normalize = bool(spec.score_normalize)
+
+    async def _sweeper(self) -> None:
+        while True:
+            await asyncio.sleep(max(1.0, self.cfg.reservation_ttl_s / 4))
+            stale = self.state.sweep_reservations(self.cfg.reservation_ttl_s)
+            if stale:
+                log.warning("released %d stale reservations", len(stale))
+            if self.poller is not None:
+                self.poller.sweep_stale()
+
+    async def stop(self) -> None:
+        if self.runner is not None:
+            await self.runner.cleanup()
+        for c in self.controllers:
+            if hasattr(c, "stop"):
+                await c.stop()
+        if self.poller is not None:
+            await self.poller.stop()
+        for t in self.tasks:
+            t.cancel()
+        for t in self.tasks:
+            try:
+                await t
+            except (asyncio.CancelledError, Exception):
+                pass
+        for inf in (self.node_informer, self.pod_informer):
+            if inf is not None:
+                await inf.stop()
+        if self.api is not None and hasattr(self.api, "close"):
+            await self.api.close()
+
+
+async def serve_forever(cfg: Config, worker: int = 0) -> int:
+    rt = Runtime(cfg, worker)
+    loop = asyncio.get_running_loop()
+    stop = asyncio.Event()
+    hits = {"n": 0}
+
+    def on_signal():
+        hits["n"] += 1
+        if hits["n"] > 1:
+            os._exit(1)
+        stop.set()
+
+    for sig in (signal.SIGINT, signal.SIGTERM):
+        loop.add_signal_handler(sig, on_signal)
+    await rt.start()
+    await stop.wait()
+    await rt.stop()
+    return 0
+
+
+def run(cfg: Config) -> int:
+    if cfg.workers <= 1:
+        return asyncio.run(serve_forever(cfg, 0))
+    if not cfg.ledger_path:
+        cfg.ledger_path = f"/dev/shm/nanogpu-ledger-{os.getpid()}"
+    # create the shared region before forking so every worker attaches to the same layout
+    from .native import core
+
+    core().Ledger(cfg.ledger_path, cfg.max_nodes, cfg.max_pods, True)
+    children = []
+    for w in range(cfg.workers):
+        pid = os.fork()
+        if pid == 0:
+            try:
+                code = asyncio.run(serve_forever(cfg, w))
+            except BaseException:
+                log.exception("worker %d crashed", w)
+                code = 1
+            os._exit(code)
+        children.append(pid)
+
+    def forward(sig, _frame):
+        for c in children:
+            try:
+                os.kill(c, sig)
+            except ProcessLookupError:
+                pass
+
+    signal.signal(signal.SIGINT, forward)
+    signal.signal(signal.SIGTERM, forward)
+    code = 0
+    for c in children:
+        _, status = os.waitpid(c, 0)
+        code = code or (os.waitstatus_to_exitcode(status) if hasattr(os, "waitstatus_to_exitcode") else 0)
+    try:
+        os.unlink(cfg.ledger_path)
+    except OSError:
+        pass
+    return code
+
+
+def main(argv: list[str] | None = None) -> int:
+    from .cli import parse
+
+    cfg = parse(argv)
+    return run(cfg)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,79 @@
+"""Command line: reference flag names and env vars, plus MI355X-native options.
+
+Reference: cmd/main.go:63-73 (flags), :27, 93-99 (KUBECONFIG, PORT default 39999 when
+not an int, THREADNESS default 1 when < 1 or not an int), :83-91 (priority switch:
+anything but binpack/spread logs an error and exits).
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+
+from . import types as T
+from .app import Config
+from .config.policy import parse_duration
+
+
+def _int_env(name: str, default: int, minimum: int | None = None) -> int:
+    try:
+        v = int(os.environ.get(name, ""))
+    except ValueError:
+        return default
+    if minimum is not None and v < minimum:
+        return default
+    return v
+
+
+def _bool(s: str) -> bool:
+    return str(s).lower() in ("1", "true", "yes", "on")
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser("nano-gpu-scheduler", description="MI355X-native fine-grained GPU scheduler extender")
+    # reference flags (Go flag package accepts -flag and --flag; so does this parser)
+    p.add_argument("--priority", "-priority", default=T.PRIORITY_BINPACK, help="binpack|spread|random|firstfit")
+    p.add_argument("--policyConfigPath", "-policyConfigPath", default=T.DEFAULT_POLICY_PATH)
+    p.add_argument("--prometheusUrl", "-prometheusUrl", default=T.DEFAULT_PROMETHEUS_URL)
+    p.add_argument("--instancePort", "-instancePort", default="9100")
+    p.add_argument("--sync-period", "-sync-period", default="5s")
+    p.add_argument("--isLoadSchedule", "-isLoadSchedule", default="false")
+    p.add_argument("-v", "--v", type=int, default=0, help="log verbosity (klog-style)")
+    # MI355X-native
+    p.add_argument("--compat", action="store_true", help="reproduce reference placements bit for bit (Go 1.16)")
+    p.add_argument("--score-normalize", action="store_true", help="map scores to kube-scheduler's [0,10]")
+    p.add_argument("--topology-weight", type=float, default=1.0, help="xGMI/partition term weight")
+    p.add_argument("--no-hbm", action="store_true", help="ignore the nano-gpu/gpu-memory dimension")
+    p.add_argument("--workers", type=int, default=1, help="SO_REUSEPORT worker processes sharing one ledger")
+    p.add_argument("--ledger-path", default="", help="/dev/shm path of the shared ledger")
+    p.add_argument("--max-nodes", type=int, default=4096)
+    p.add_argument("--max-pods", type=int, default=131072)
+    p.add_argument("--kube-api", default=None, help="API server URL (default: KUBECONFIG or in-cluster)")
+    p.add_argument("--host", default="0.0.0.0")
+    p.add_argument("--bind-verify-pod", action="store_true", help="GET the pod on every bind (reference behaviour)")
+    p.add_argument("--reservation-ttl", default="60s")
+    p.add_argument("--fake-cluster", type=int, default=0, help="serve against N in-process fake MI355X nodes")
+    p.add_argument("--fake-gpus-per-node", type=int, default=8)
+    p.add_argument("--fake-partition", default="SPX", choices=["SPX", "DPX", "QPX", "CPX"])
+    p.add_argument("--seed", type=int, default=0)
+    return p
+
+
+def parse(argv: list[str] | None = None) -> Config:
+    a = build_parser().parse_args(argv)
+    if a.priority not in T.POLICIES:
+        raise SystemExit(f"Priority algorithm {a.priority} is not supported")
+    logging.basicConfig(level=logging.DEBUG if a.v >= 4 else logging.INFO if a.v >= 1 else logging.WARNING,
+                        format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    port = _int_env("PORT", T.DEFAULT_PORT)
+    return Config(
+        priority=a.priority, policy_config_path=a.policyConfigPath, prometheus_url=a.prometheusUrl,
+        instance_port=a.instancePort, sync_period_s=parse_duration(a.sync_period),
+        is_load_schedule=_bool(a.isLoadSchedule), port=port, host=a.host,
+        threadness=_int_env("THREADNESS", 1, minimum=1), kubeconfig=os.environ.get("KUBECONFIG"),
+        kube_api=a.kube_api, compat=a.compat, score_normalize=a.score_normalize,
+        topology_weight=a.topology_weight, track_hbm=not a.no_hbm, workers=max(1, a.workers),
+        ledger_path=a.ledger_path, max_nodes=a.max_nodes, max_pods=a.max_pods,
+        verify_pod_on_bind=a.bind_verify_pod, reservation_ttl_s=parse_duration(a.reservation_ttl),
+        fake_cluster=a.fake_cluster, fake_gpus_per_node=a.fake_gpus_per_node, fake_partition=a.fake_partition,
+        seed=a.seed)

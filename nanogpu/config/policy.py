@@ -1,0 +1,184 @@
+"""policy.yaml schema + hot reload that actually reaches the scheduler.
+
+Reference: pkg/dealer/type.go:16-33 (Policy/PolicySpec/Period/PriorityPolicy),
+stats.go:13-28 (GetPolicyFromFile panics on unreadable file), context.go:19-59 (3 s mtime
+poll). The reference reloads into a DSContext that nothing reads after startup:
+main.go:118 copies the spec by value into the verb closures. Here the
+watcher publishes an immutable snapshot and calls subscribers (cluster policy, telemetry
+poller periods) on every change; a bad file keeps the last good snapshot instead of
+panicking.
+
+Schema (reference keys kept; MI355X additions are optional):
+  apiVersion: v1
+  kind: public-dynamic-scheduler
+  spec:
+    syncPeriod: [{name: gpu_core_usage_avg, period: 15s}, ...]
+    priority:   [{name: ..., weight: ...}]          # parsed, informational (as reference)
+    scheduling: {policy: binpack, compat: false, topologyWeight: 1.0, scoreNormalize: false}
+    metrics:    {gpu_core_usage_avg: {query: '<PromQL with {node} {card}>', fallback: '...'}}
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import os
+import re
+from dataclasses import dataclass, field
+from typing import Callable
+
+import yaml
+
+from .. import types as T
+
+log = logging.getLogger(__name__)
+
+_DUR = re.compile(r"(\d+(?:\.\d+)?)(ns|us|µs|ms|s|m|h)")
+_UNIT = {"ns": 1e-9, "us": 1e-6, "µs": 1e-6, "ms": 1e-3, "s": 1.0, "m": 60.0, "h": 3600.0}
+
+
+def parse_duration(v) -> float:
+    """Go time.ParseDuration subset ("15s", "1m30s", "500ms"); bare numbers are seconds."""
+    if isinstance(v, (int, float)):
+        return float(v)
+    s = str(v).strip()
+    if not s:
+        raise ValueError("empty duration")
+    if re.fullmatch(r"\d+(\.\d+)?", s):
+        return float(s)
+    pos, total = 0, 0.0
+    for m in _DUR.finditer(s):
+        if m.start() != pos:
+            raise ValueError(f"bad duration {v!r}")
+        total += float(m.group(1)) * _UNIT[m.group(2)]
+        pos = m.end()
+    if pos != len(s):
+        raise ValueError(f"bad duration {v!r}")
+    return total
+
+
+@dataclass(frozen=True)
+class Period:
+    name: str
+    period_s: float
+
+
+@dataclass(frozen=True)
+class MetricQuery:
+    query: str
+    fallback: str | None = None
+
+
+# Reference query shapes (prometheus.go:70-76) as the default templates.
+REFERENCE_QUERY = '{metric}{{node=~"{node}",card="{card}"}} /100'
+REFERENCE_FALLBACK = '{metric}{{node="{node}",cardNode="{card}"}} /100'
+# AMD device-metrics-exporter shaped templates (gfx / memory-controller activity in %).
+AMD_QUERIES = {
+    T.GPU_CORE_USAGE_METRIC: MetricQuery('avg_over_time(gpu_gfx_activity{{hostname="{node}",gpu_id="{card}"}}[1m]) / 100'),
+    T.GPU_MEMORY_USAGE_METRIC: MetricQuery('gpu_used_vram{{hostname="{node}",gpu_id="{card}"}} / '
+                                           'gpu_total_vram{{hostname="{node}",gpu_id="{card}"}}'),
+}
+
+
+@dataclass(frozen=True)
+class PolicySpec:
+    sync_period: tuple[Period, ...] = ()
+    priority: tuple[tuple[str, float], ...] = ()
+    policy: str | None = None
+    compat: bool | None = None
+    topology_weight: float | None = None
+    score_normalize: bool | None = None
+    metrics: tuple[tuple[str, MetricQuery], ...] = ()
+
+    def period_of(self, name: str) -> float:
+        for p in self.sync_period:
+            if p.name == name and p.period_s > 0:
+                return p.period_s
+        return 0.0
+
+    def active_duration(self, name: str) -> float:
+        """stats.go:57-66: period + ExtenderActivePeriod (5 min); 0 when unknown."""
+        p = self.period_of(name)
+        return p + T.EXTENDER_ACTIVE_PERIOD_S if p > 0 else 0.0
+
+    def query_for(self, name: str) -> MetricQuery:
+        for k, q in self.metrics:
+            if k == name:
+                return q
+        return MetricQuery(REFERENCE_QUERY, REFERENCE_FALLBACK)
+
+
+def parse_policy(text: str) -> PolicySpec:
+    doc = yaml.safe_load(text) or {}
+    spec = doc.get("spec") or {}
+    periods = []
+    for item in spec.get("syncPeriod") or []:
+        periods.append(Period(str(item["name"]), parse_duration(item.get("period", 0))))
+    prio = tuple((str(p.get("name", "")), float(p.get("weight", 0))) for p in spec.get("priority") or [])
+    sch = spec.get("scheduling") or {}
+    pol = sch.get("policy")
+    if pol is not None and pol not in T.POLICIES:
+        raise ValueError(f"unknown policy {pol!r}")
+    metrics = []
+    preset = spec.get("metricsPreset")
+    if preset == "amd":
+        metrics.extend(AMD_QUERIES.items())
+    for name, q in (spec.get("metrics") or {}).items():
+        metrics.append((name, MetricQuery(q["query"], q.get("fallback"))))
+    return PolicySpec(
+        sync_period=tuple(periods), priority=prio, policy=pol,
+        compat=sch.get("compat"), topology_weight=sch.get("topologyWeight"),
+        score_normalize=sch.get("scoreNormalize"), metrics=tuple(metrics))
+
+
+def load_policy(path: str) -> PolicySpec:
+    with open(path) as f:
+        return parse_policy(f.read())
+
+
+class PolicyWatcher:
+    """mtime poller (reference context.go:44-59 used 3 s); publishes snapshots to subscribers."""
+
+    def __init__(self, path: str, interval_s: float = 3.0):
+        self.path = path
+        self.interval_s = interval_s
+        self.spec = PolicySpec()
+        self.mtime = 0.0
+        self.subscribers: list[Callable[[PolicySpec], None]] = []
+        self.reloads = 0
+        self.errors = 0
+        self._task: asyncio.Task | None = None
+
+    def subscribe(self, fn: Callable[[PolicySpec], None]) -> None:
+        self.subscribers.append(fn)
+
+    def load_now(self) -> bool:
+        try:
+            st = os.stat(self.path)
+        except OSError:
+            return False
+        if st.st_mtime <= self.mtime:
+            return False
+        try:
+            spec = load_policy(self.path)
+        except (OSError, ValueError, KeyError, TypeError, yaml.YAMLError) as e:
+            self.errors += 1
+            log.error("policy %s invalid, keeping previous: %s", self.path, e)
+            self.mtime = st.st_mtime
+            return False
+        self.spec, self.mtime = spec, st.st_mtime
+        self.reloads += 1
+        for fn in self.subscribers:
+            try:
+                fn(spec)
+            except Exception:
+                log.exception("policy subscriber failed")
+        return True
+
+    async def run(self) -> None:
+        while True:
+            self.load_now()
+            await asyncio.sleep(self.interval_s)
+
+    def start(self) -> asyncio.Task:
+        self._task = asyncio.ensure_future(self.run())
+        return self._task

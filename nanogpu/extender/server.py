@@ -136,13 +136,16 @@ def make_app(ext: Extender, ready: asyncio.Event | None = None, extra_status=Non
 
     app = web.Application(client_max_size=64 * 1024 * 1024)
     app.add_routes(routes)
-    app["extender"] = ext
+    app[EXTENDER_KEY] = ext
     return app
+
+
+EXTENDER_KEY = web.AppKey("extender", Extender)
 
 
 async def start(app: web.Application, host: str = "0.0.0.0", port: int = T.DEFAULT_PORT,
                 reuse_port: bool = False) -> tuple[web.AppRunner, int]:
-    runner = web.AppRunner(app, access_log=None)
+    runner = web.AppRunner(app, access_log=None, shutdown_timeout=2.0)
     await runner.setup()
     site = web.TCPSite(runner, host, port, reuse_port=reuse_port or None, backlog=1024)
     await site.start()

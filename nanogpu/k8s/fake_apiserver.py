@@ -84,6 +84,10 @@ class Faults:
 
 
 class FakeKubeStore:
+    """Stored objects are immutable: every write replaces the object (copying only the
+    path it changes), reads and watch events share references. Callers must not mutate
+    what they get back (real clients get fresh JSON anyway)."""
+
     def __init__(self, history: int = 100000, faults: Faults | None = None):
         self.rv = 0
         self.pods: dict[tuple[str, str], dict] = {}
@@ -97,12 +101,16 @@ class FakeKubeStore:
 
     # ------------------------------------------------------------------ internals
     def _bump(self, obj: dict) -> dict:
+        """Returns a new top-level object with a new metadata dict (stored objects are
+        immutable: writers copy the path they change, readers share references)."""
         self.rv += 1
-        obj.setdefault("metadata", {})["resourceVersion"] = str(self.rv)
+        obj = dict(obj)
+        obj["metadata"] = dict(obj.get("metadata") or {})
+        obj["metadata"]["resourceVersion"] = str(self.rv)
         return obj
 
     def _emit(self, kind: str, etype: str, obj: dict) -> None:
-        ev = {"type": etype, "object": copy.deepcopy(obj)}
+        ev = {"type": etype, "object": obj}
         self.history[kind].append((self.rv, ev))
         for q in list(self.watchers[kind]):
             q.put_nowait(ev)
@@ -122,17 +130,17 @@ class FakeKubeStore:
         if key in self.pods:
             raise ApiError(409, f'pods "{m["name"]}" already exists', "AlreadyExists")
         pod.setdefault("status", {}).setdefault("phase", "Pending")
-        self._bump(pod)
+        pod = self._bump(pod)
         self.pods[key] = pod
         self._emit("pods", "ADDED", pod)
-        return copy.deepcopy(pod)
+        return pod
 
     def get_pod(self, ns: str, name: str) -> dict:
         self._count("get_pod")
         p = self.pods.get((ns, name))
         if p is None:
             raise ApiError(404, f'pods "{name}" not found', "NotFound")
-        return copy.deepcopy(p)
+        return p
 
     def patch_pod(self, ns: str, name: str, patch: dict) -> dict:
         self._count("patch_pod")
@@ -141,11 +149,10 @@ class FakeKubeStore:
         p = self.pods.get((ns, name))
         if p is None:
             raise ApiError(404, f'pods "{name}" not found', "NotFound")
-        np_ = pu.apply_patch(p, patch)
-        self._bump(np_)
+        np_ = self._bump(pu.apply_patch(p, patch))
         self.pods[(ns, name)] = np_
         self._emit("pods", "MODIFIED", np_)
-        return copy.deepcopy(np_)
+        return np_
 
     def update_pod(self, ns: str, name: str, pod: dict) -> dict:
         self._count("update_pod")
@@ -157,11 +164,10 @@ class FakeKubeStore:
             raise ApiError(409, f'Operation cannot be fulfilled on pods "{name}": the object has been '
                                 f'modified; please apply your changes to the latest version and try again',
                            "Conflict")
-        pod = copy.deepcopy(pod)
-        self._bump(pod)
+        pod = self._bump(copy.deepcopy(pod))
         self.pods[(ns, name)] = pod
         self._emit("pods", "MODIFIED", pod)
-        return copy.deepcopy(pod)
+        return pod
 
     def bind_pod(self, ns: str, name: str, uid: str, node: str) -> None:
         self._count("bind_pod")
@@ -178,10 +184,10 @@ class FakeKubeStore:
             raise ApiError(409, f'pod {name} is already assigned to node "{pu.node_name_of(p)}"', "Conflict")
         if node not in self.nodes:
             raise ApiError(404, f'nodes "{node}" not found', "NotFound")
-        np_ = copy.deepcopy(p)
-        np_.setdefault("spec", {})["nodeName"] = node
-        np_.setdefault("status", {})["phase"] = "Running"
-        self._bump(np_)
+        np_ = dict(p)
+        np_["spec"] = dict(p.get("spec") or {}, nodeName=node)
+        np_["status"] = dict(p.get("status") or {}, phase="Running")
+        np_ = self._bump(np_)
         self.pods[(ns, name)] = np_
         self.bindings.append((ns, name, node))
         self._emit("pods", "MODIFIED", np_)
@@ -191,8 +197,7 @@ class FakeKubeStore:
         p = self.pods.pop((ns, name), None)
         if p is None:
             raise ApiError(404, f'pods "{name}" not found', "NotFound")
-        self._bump(p)
-        self._emit("pods", "DELETED", p)
+        self._emit("pods", "DELETED", self._bump(p))
 
     def set_phase(self, ns: str, name: str, phase: str) -> dict:
         return self.patch_pod(ns, name, {"status": {"phase": phase}})
@@ -200,7 +205,7 @@ class FakeKubeStore:
     def list_pods(self, label_selector: str | None = None, field_selector: str | None = None,
                   namespace: str | None = None) -> tuple[list[dict], str]:
         self._count("list_pods")
-        items = [copy.deepcopy(p) for (ns, _), p in self.pods.items()
+        items = [p for (ns, _), p in self.pods.items()
                  if (namespace is None or ns == namespace) and _match_labels(p, label_selector)
                  and _match_fields(p, field_selector)]
         return items, str(self.rv)
@@ -210,37 +215,35 @@ class FakeKubeStore:
         node = copy.deepcopy(node)
         name = pu.meta(node)["name"]
         etype = "MODIFIED" if name in self.nodes else "ADDED"
-        self._bump(node)
+        node = self._bump(node)
         self.nodes[name] = node
         self._emit("nodes", etype, node)
-        return copy.deepcopy(node)
+        return node
 
     def get_node(self, name: str) -> dict:
         self._count("get_node")
         n = self.nodes.get(name)
         if n is None:
             raise ApiError(404, f'nodes "{name}" not found', "NotFound")
-        return copy.deepcopy(n)
+        return n
 
     def patch_node(self, name: str, patch: dict) -> dict:
         n = self.nodes.get(name)
         if n is None:
             raise ApiError(404, f'nodes "{name}" not found', "NotFound")
-        nn = pu.apply_patch(n, patch)
-        self._bump(nn)
+        nn = self._bump(pu.apply_patch(n, patch))
         self.nodes[name] = nn
         self._emit("nodes", "MODIFIED", nn)
-        return copy.deepcopy(nn)
+        return nn
 
     def delete_node(self, name: str) -> None:
         n = self.nodes.pop(name, None)
         if n is not None:
-            self._bump(n)
-            self._emit("nodes", "DELETED", n)
+            self._emit("nodes", "DELETED", self._bump(n))
 
     def list_nodes(self, label_selector: str | None = None) -> tuple[list[dict], str]:
         self._count("list_nodes")
-        return [copy.deepcopy(n) for n in self.nodes.values() if _match_labels(n, label_selector)], str(self.rv)
+        return [n for n in self.nodes.values() if _match_labels(n, label_selector)], str(self.rv)
 
     def add_event(self, ev: dict) -> None:
         self.events.append(ev)
@@ -478,14 +481,22 @@ def make_app(store: FakeKubeStore) -> web.Application:
 
     app = web.Application(client_max_size=16 * 1024 * 1024)
     app.add_routes(routes)
-    app["store"] = store
+    app[STORE_KEY] = store
+
+    async def _close_watches(_app):
+        store.drop_watches()
+
+    app.on_shutdown.append(_close_watches)
     return app
 
 
+STORE_KEY = web.AppKey("store", FakeKubeStore)
+
+
 async def serve(store: FakeKubeStore, host: str = "127.0.0.1", port: int = 0) -> tuple[web.AppRunner, int]:
-    runner = web.AppRunner(make_app(store), access_log=None)
+    runner = web.AppRunner(make_app(store), access_log=None, shutdown_timeout=1.0)
     await runner.setup()
-    site = web.TCPSite(runner, host, port)
+    site = web.TCPSite(runner, host, port, backlog=1024)
     await site.start()
     port = site._server.sockets[0].getsockname()[1]  # type: ignore[union-attr]
     return runner, port

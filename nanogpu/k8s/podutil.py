@@ -77,9 +77,26 @@ def container_mib(c: dict) -> int:
         return 0
 
 
+_DEMAND_CACHE: dict[str, Demand] = {}
+_DEMAND_CACHE_CAP = 65536
+
+
 def pod_demand(pod: dict) -> Demand:
-    """allocate.go:54-62 (+ HBM MiB as the second dimension). Init containers are ignored."""
-    return [(container_percent(c), container_mib(c)) for c in containers(pod)]
+    """allocate.go:54-62 (+ HBM MiB as the second dimension). Init containers are ignored.
+
+    Container resources are immutable for the life of a pod UID, so the parsed demand is
+    memoised per UID (filter, prioritize, bind and the controller all ask for it)."""
+    uid = meta(pod).get("uid")
+    if uid:
+        d = _DEMAND_CACHE.get(uid)
+        if d is not None:
+            return d
+    d = [(container_percent(c), container_mib(c)) for c in containers(pod)]
+    if uid:
+        if len(_DEMAND_CACHE) >= _DEMAND_CACHE_CAP:
+            _DEMAND_CACHE.clear()
+        _DEMAND_CACHE[uid] = d
+    return d
 
 
 def is_gpu_sharing(pod: dict) -> bool:

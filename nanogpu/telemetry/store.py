@@ -1,0 +1,56 @@
+"""Load telemetry store: per (node, metric, card) latest utilisation in [0, 1].
+
+Reference: pkg/dealer/nodeusage.go (string values + "Asia/Shanghai" wall-clock strings,
+re-parsed and tzdata-loaded on every filter: nodeusage.go:82-111, stats.go:30-55, D13).
+Here values are floats with monotonic timestamps, and the derived per-device load
+(`usage = Σ_metrics ceil(10u)/10`, RemainLoad = 2 - int(usage), allocate.go:173-195) is
+pushed into the native ledger when it changes, not recomputed inside the hot path.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass
+
+
+@dataclass
+class Sample:
+    value: float
+    t: float
+
+
+class TelemetryStore:
+    def __init__(self):
+        self.data: dict[tuple[str, str, int], Sample] = {}
+
+    def update(self, node: str, metric: str, card: int, value: float, t: float | None = None) -> None:
+        self.data[(node, metric, card)] = Sample(float(value), time.monotonic() if t is None else t)
+
+    def get(self, node: str, metric: str, card: int, active_s: float, now: float | None = None
+            ) -> tuple[bool, float, str | None]:
+        """(exists, value, error) like Dealer.GetUsage (nodeusage.go:82-111)."""
+        s = self.data.get((node, metric, card))
+        if s is None:
+            return False, 0.0, None
+        now = time.monotonic() if now is None else now
+        if now > s.t + active_s:
+            return True, 0.0, f"{metric} not in update period"
+        if not (0.0 <= s.value <= 1.0) or math.isnan(s.value):
+            return True, 0.0, f"{metric} usage < 0 || usage > 1"
+        return True, s.value, None
+
+    def device_usage(self, node: str, card: int, periods: list[tuple[str, float]], now: float | None = None
+                     ) -> float:
+        """Σ over policy metrics of ceil(10u)/10 for fresh, valid samples (allocate.go:173-195)."""
+        total = 0.0
+        for metric, active_s in periods:
+            if active_s <= 0:
+                continue
+            exists, v, err = self.get(node, metric, card, active_s, now)
+            if not exists or err:
+                continue
+            total += math.ceil(10 * v) / 10
+        return total
+
+    def nodes(self) -> set[str]:
+        return {k[0] for k in self.data}

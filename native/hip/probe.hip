@@ -17,6 +17,7 @@
 #include <pybind11/stl.h>
 
 #include <cstdint>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -78,7 +79,55 @@ __global__ __launch_bounds__(256) void mfma_burn(float* out, int iters) {
   if (s == 12345.678f) out[blockIdx.x * blockDim.x + threadIdx.x] = s;  // keeps the chains live
 }
 
+// One wave computes C[32x32] = A[32x16] * B[16x32] with a single bf16 MFMA: the numerics
+// self-test of the burn kernel's instruction (operand/accumulator lane maps per
+// cdna_hip_programming.md §3: lane l holds A[l&31][8(l>>5)+j], B[8(l>>5)+j][l&31];
+// C row = (reg&3) + 8(reg>>2) + 4(l>>5), col = l&31).
+__global__ __launch_bounds__(64) void mfma_tile(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
+                                                float* __restrict__ C) {
+  const int l = threadIdx.x, r = l & 31, h = l >> 5;
+  bf16x8 a, b;
+  for (int j = 0; j < 8; ++j) {
+    a[j] = A[r * 16 + 8 * h + j];
+    b[j] = B[(8 * h + j) * 32 + r];
+  }
+  f32x16 c = {};
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  for (int reg = 0; reg < 16; ++reg) C[((reg & 3) + 8 * (reg >> 2) + 4 * h) * 32 + r] = c[reg];
+}
+
 // ---------------------------------------------------------------------------- host helpers
+
+uint16_t f32_to_bf16_bits(float f) {  // round to nearest even
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7f800000u) == 0x7f800000u) return static_cast<uint16_t>(u >> 16);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<uint16_t>(u >> 16);
+}
+
+std::vector<float> gemm_tile(const std::vector<float>& a, const std::vector<float>& b) {
+  if (a.size() != 32 * 16 || b.size() != 16 * 32) throw std::invalid_argument("gemm_tile: A is 32x16, B is 16x32");
+  std::vector<uint16_t> ha(a.size()), hb(b.size());
+  for (size_t i = 0; i < a.size(); ++i) ha[i] = f32_to_bf16_bits(a[i]);
+  for (size_t i = 0; i < b.size(); ++i) hb[i] = f32_to_bf16_bits(b[i]);
+  uint16_t *da = nullptr, *db = nullptr;
+  float* dc = nullptr;
+  HIP_OK(hipMalloc(&da, ha.size() * 2));
+  HIP_OK(hipMalloc(&db, hb.size() * 2));
+  HIP_OK(hipMalloc(&dc, 32 * 32 * 4));
+  HIP_OK(hipMemcpy(da, ha.data(), ha.size() * 2, hipMemcpyHostToDevice));
+  HIP_OK(hipMemcpy(db, hb.data(), hb.size() * 2, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(mfma_tile, dim3(1), dim3(64), 0, 0, reinterpret_cast<const __bf16*>(da),
+                     reinterpret_cast<const __bf16*>(db), dc);
+  HIP_OK(hipGetLastError());
+  std::vector<float> c(32 * 32);
+  HIP_OK(hipMemcpy(c.data(), dc, c.size() * 4, hipMemcpyDeviceToHost));
+  (void)hipFree(da);
+  (void)hipFree(db);
+  (void)hipFree(dc);
+  return c;
+}
 
 struct Stream {
   hipStream_t s = nullptr;
@@ -149,6 +198,21 @@ py::dict device_props(int dev) {
   HIP_OK(hipGetDeviceCount(&count));
   d["device_count"] = count;
   return d;
+}
+
+bool copy_check(int dev, size_t n_floats) {
+  HIP_OK(hipSetDevice(dev));
+  const size_t n4 = (n_floats + 3) / 4;
+  std::vector<float> h(n4 * 4);
+  for (size_t i = 0; i < h.size(); ++i) h[i] = static_cast<float>((i * 2654435761u) % 1000003u);
+  DevBuf<float4> a(n4), b(n4);
+  HIP_OK(hipMemcpy(a.p, h.data(), n4 * 16, hipMemcpyHostToDevice));
+  HIP_OK(hipMemset(b.p, 0, n4 * 16));
+  hipLaunchKernelGGL(hbm_copy, dim3(cu_count(dev) * 8), dim3(256), 0, 0, a.p, b.p, n4);
+  HIP_OK(hipGetLastError());
+  std::vector<float> out(n4 * 4);
+  HIP_OK(hipMemcpy(out.data(), b.p, n4 * 16, hipMemcpyDeviceToHost));
+  return std::memcmp(out.data(), h.data(), n4 * 16) == 0;
 }
 
 double hbm_bandwidth(int dev, size_t bytes, int iters) {
@@ -272,6 +336,10 @@ PYBIND11_MODULE(_probe, m) {
   m.def("mfma_throughput", &mfma_throughput, py::arg("device") = 0,
         py::arg("cu_mask") = std::vector<uint32_t>{}, py::arg("blocks") = 2048, py::arg("iters") = 2048,
         "bf16 MFMA TFLOP/s on a CU-masked stream.");
+  m.def("gemm_tile", &gemm_tile, py::arg("a"), py::arg("b"),
+        "C[32x32] = bf16(A[32x16]) @ bf16(B[16x32]) with one v_mfma_f32_32x32x16_bf16 (fp32 accumulate).");
+  m.def("copy_check", &copy_check, py::arg("device") = 0, py::arg("n_floats") = size_t(1) << 24,
+        py::call_guard<py::gil_scoped_release>(), "hbm_copy kernel result == source, bit for bit.");
   m.def("peer_bandwidth", &peer_bandwidth, py::arg("src"), py::arg("dst"),
         py::arg("bytes") = size_t(256) << 20, py::arg("iters") = 10,
         py::call_guard<py::gil_scoped_release>(), "hipMemcpyPeer bandwidth in GB/s.");

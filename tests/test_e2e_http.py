@@ -1,0 +1,153 @@
+"""End-to-end over real HTTP: fake apiserver <- extender <- fake kube-scheduler.
+
+SURVEY §7.3 minimum slice (BASELINE configs 1 and 2): one node with
+`nano-gpu/gpu-percent: 800` and an MI355X topology annotation, one pod with a 20% limit,
+filter -> priorities -> bind, then check annotations + label + binding + /status, and
+that deleting the pod frees the share.
+"""
+import asyncio
+import json
+
+import aiohttp
+import pytest
+
+from nanogpu import types as T
+from nanogpu.app import Config, Runtime
+from nanogpu.k8s import podutil as pu
+from nanogpu.k8s.fake_apiserver import FakeKubeStore, serve
+from nanogpu.sim.driver import HttpExtenderClient, SchedulerDriver, node_capacities
+from nanogpu.topology.model import synthetic_mi355x
+
+
+async def _wait(pred, timeout=5.0):
+    loop = asyncio.get_running_loop()
+    end = loop.time() + timeout
+    while loop.time() < end:
+        if pred():
+            return True
+        await asyncio.sleep(0.01)
+    return pred()
+
+
+async def _stack(nodes, **cfg_kw):
+    store = FakeKubeStore()
+    for n in nodes:
+        store.add_node(n)
+    api_runner, api_port = await serve(store)
+    cfg = Config(kube_api=f"http://127.0.0.1:{api_port}", port=0, host="127.0.0.1",
+                 policy_config_path="/nonexistent/policy.yaml", **cfg_kw)
+    rt = Runtime(cfg)
+    await rt.start()
+    return store, api_runner, rt
+
+
+def test_minimum_slice_one_pod_binpack():
+    async def main():
+        node = pu.make_node("mi355x-0", 8, synthetic_mi355x(8).to_json())
+        store, api_runner, rt = await _stack([node])
+        base = f"http://127.0.0.1:{rt.bound_port}"
+        client = HttpExtenderClient(base)
+        try:
+            drv = SchedulerDriver(client, _ApiShim(store), ["mi355x-0"], node_capacities([node]))
+            pod = pu.make_pod("p1", [("main", 20)])
+            stats = await drv.run([pod])
+            assert stats.scheduled == 1, stats.summary()
+            got = store.get_pod("default", "p1")
+            ann = got["metadata"]["annotations"]
+            assert ann[T.container_annotation("main")] == "0"
+            assert ann[T.ANNOTATION_GPU_ASSUME] == "true"
+            assert got["metadata"]["labels"][T.LABEL_GPU_ASSUME] == "true"
+            assert got["spec"]["nodeName"] == "mi355x-0"
+            assert ("default", "p1", "mi355x-0") in store.bindings
+            async with aiohttp.ClientSession() as s:
+                async with s.post(base + "/status") as r:
+                    status = await r.json()
+                async with s.get(base + "/version") as r:
+                    assert (await r.text()) == T.VERSION
+                async with s.get(base + "/metrics") as r:
+                    assert "nanogpu_verb_latency_seconds" in await r.text()
+            gpus = status["mi355x-0"]["GPUs"]
+            assert gpus[0]["Percent"] == 80 and all(g["Percent"] == 100 for g in gpus[1:])
+            # delete frees the share (reference only Forgets on delete: D3)
+            store.delete_pod("default", "p1")
+            assert await _wait(lambda: rt.state.status()["mi355x-0"]["GPUs"][0]["Percent"] == 100)
+        finally:
+            await client.close()
+            await rt.stop()
+            await api_runner.cleanup()
+
+    asyncio.run(main())
+
+
+class _ApiShim:
+    """Creates pods directly in the store (the driver's kubectl)."""
+
+    def __init__(self, store):
+        self.store = store
+
+    async def create_pod(self, pod):
+        return self.store.create_pod(pod)
+
+
+def test_filter_requires_node_cache_capable_or_nodes():
+    async def main():
+        node = pu.make_node("n0", 2)
+        store, api_runner, rt = await _stack([node])
+        base = f"http://127.0.0.1:{rt.bound_port}"
+        try:
+            async with aiohttp.ClientSession() as s:
+                body = {"Pod": pu.make_pod("x", [("c", 10)])}
+                async with s.post(base + "/scheduler/filter", data=json.dumps(body)) as r:
+                    res = await r.json()
+                assert res["Error"] == T.FILTER_NODE_CACHE_ERROR
+                # nodeCacheCapable=false flavour: full Node objects (the reference rejects this)
+                body["Nodes"] = {"items": [node]}
+                async with s.post(base + "/scheduler/filter", data=json.dumps(body)) as r:
+                    res = await r.json()
+                assert res["Error"] == "" and [pu.meta(n)["name"] for n in res["Nodes"]["items"]] == ["n0"]
+                # bad JSON on priorities: 400, not a crash (D10)
+                async with s.post(base + "/scheduler/priorities", data=b"{nope") as r:
+                    assert r.status == 400
+                # bind of an unknown pod: 500 with Error set (routes.go:147-168)
+                async with s.post(base + "/scheduler/bind", data=json.dumps(
+                        {"PodName": "ghost", "PodNamespace": "default", "PodUID": "u", "Node": "n0"})) as r:
+                    assert r.status == 500 and (await r.json())["Error"]
+        finally:
+            await rt.stop()
+            await api_runner.cleanup()
+
+    asyncio.run(main())
+
+
+def test_burst_spread_mixed_percent_no_overcommit():
+    """BASELINE config 3 (scaled): mixed {10,25,50} burst, spread policy, 4 nodes."""
+    async def main():
+        nodes = [pu.make_node(f"n{i}", 8, synthetic_mi355x(8).to_json()) for i in range(4)]
+        store, api_runner, rt = await _stack(nodes, priority="spread")
+        client = HttpExtenderClient(f"http://127.0.0.1:{rt.bound_port}")
+        try:
+            import random
+
+            rng = random.Random(1)
+            pods = [pu.make_pod(f"p{i}", [("c", rng.choice([10, 25, 50]))]) for i in range(120)]
+            drv = SchedulerDriver(client, _ApiShim(store), [f"n{i}" for i in range(4)], node_capacities(nodes))
+            stats = await drv.run(pods)
+            assert stats.scheduled + stats.failed == 120
+            # device-level invariant from the API objects themselves
+            used = {}
+            for p in store.pods.values():
+                if not pu.node_name_of(p):
+                    continue
+                for c, (pct, _) in zip(pu.containers(p), pu.pod_demand(p)):
+                    idx = pu.container_assignment(p, c["name"])[0]
+                    used[(pu.node_name_of(p), idx)] = used.get((pu.node_name_of(p), idx), 0) + pct
+            assert used and max(used.values()) <= 100
+            st = rt.state.status()
+            for (n, i), u in used.items():
+                assert st[n]["GPUs"][i]["Percent"] == 100 - u
+        finally:
+            await client.close()
+            await rt.stop()
+            await api_runner.cleanup()
+
+    asyncio.run(main())
