@@ -145,6 +145,11 @@ def node_template(d: Dist, args) -> tuple[object, dict]:
         info["gpu"] = {"gcn_arch": props.get("gcn_arch"), "cus": props.get("cus"),
                        "hbm_mib": hbm_mib, "partition": gpus[0].get("compute_partition") if gpus else None,
                        "numa": gpus[0].get("numa") if gpus else None}
+        if d.cuda:
+            # node-agent calibration on the real device (untimed): streaming HBM3E rate
+            from nanogpu.probe.calibrate import hbm_bandwidth
+
+            info["gpu"]["hbm_copy_gbs"] = round(hbm_bandwidth(d.local_rank, 1 << 30, 10), 1)
     link = 153.0
     if d.dist is not None and d.cuda:
         from nanogpu.probe.calibrate import link_matrix
@@ -157,6 +162,8 @@ def node_template(d: Dist, args) -> tuple[object, dict]:
             info["link_bw_matrix_gbs"] = [[round(x, 1) for x in r] for r in m]
     info["link_bw_gbs"] = round(link, 1)
     topo = synthetic_mi355x(args.gpus_per_node, args.partition, hbm_mib=hbm_mib, link_gbs=link)
+    if info["gpu"]:
+        topo.calibration = {k: v for k, v in info["gpu"].items() if k in ("hbm_copy_gbs", "cus")}
     return topo, info
 
 

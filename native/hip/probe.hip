@@ -35,11 +35,32 @@ namespace {
 
 // ---------------------------------------------------------------------------- kernels
 
-__global__ __launch_bounds__(256) void hbm_copy(const float4* __restrict__ src,
-                                                float4* __restrict__ dst, size_t n) {
-  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
-  for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
-    dst[i] = src[i];
+// Streaming copy: each thread keeps kCopyUnroll 16-B loads in flight before its stores
+// (one pass, no grid-stride loop: the grid is n / 4096 workgroups, >> 256 CUs), with
+// non-temporal hints so the once-touched stream does not evict L2/MALL.
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+constexpr int kCopyUnroll = 4;
+constexpr int kCopyBlock = 256;
+
+__global__ __launch_bounds__(kCopyBlock) void hbm_copy(const float4* __restrict__ src,
+                                                       float4* __restrict__ dst, size_t n) {
+  const size_t base = static_cast<size_t>(blockIdx.x) * (kCopyBlock * kCopyUnroll) + threadIdx.x;
+  if (base + (kCopyUnroll - 1) * kCopyBlock < n) {
+    const f32x4* s4 = reinterpret_cast<const f32x4*>(src) + base;
+    f32x4* d4 = reinterpret_cast<f32x4*>(dst) + base;
+    f32x4 v[kCopyUnroll];
+#pragma unroll
+    for (int u = 0; u < kCopyUnroll; ++u) v[u] = __builtin_nontemporal_load(s4 + u * kCopyBlock);
+#pragma unroll
+    for (int u = 0; u < kCopyUnroll; ++u) __builtin_nontemporal_store(v[u], d4 + u * kCopyBlock);
+  } else {
+    for (int u = 0; u < kCopyUnroll; ++u)
+      if (base + u * kCopyBlock < n) dst[base + u * kCopyBlock] = src[base + u * kCopyBlock];
+  }
+}
+
+inline unsigned copy_grid(size_t n) {
+  return static_cast<unsigned>((n + kCopyBlock * kCopyUnroll - 1) / (kCopyBlock * kCopyUnroll));
 }
 
 // One record per workgroup: {xcc_id, hw_id, block}. A bounded sleep keeps each workgroup
@@ -208,7 +229,7 @@ bool copy_check(int dev, size_t n_floats) {
   DevBuf<float4> a(n4), b(n4);
   HIP_OK(hipMemcpy(a.p, h.data(), n4 * 16, hipMemcpyHostToDevice));
   HIP_OK(hipMemset(b.p, 0, n4 * 16));
-  hipLaunchKernelGGL(hbm_copy, dim3(cu_count(dev) * 8), dim3(256), 0, 0, a.p, b.p, n4);
+  hipLaunchKernelGGL(hbm_copy, dim3(copy_grid(n4)), dim3(kCopyBlock), 0, 0, a.p, b.p, n4);
   HIP_OK(hipGetLastError());
   std::vector<float> out(n4 * 4);
   HIP_OK(hipMemcpy(out.data(), b.p, n4 * 16, hipMemcpyDeviceToHost));
@@ -223,12 +244,12 @@ double hbm_bandwidth(int dev, size_t bytes, int iters) {
   HIP_OK(hipMemset(a.p, 0, n * sizeof(float4)));
   Stream st({});
   Events ev;
-  const int blocks = cu_count(dev) * 8;
-  hipLaunchKernelGGL(hbm_copy, dim3(blocks), dim3(256), 0, st.s, a.p, b.p, n);  // warm-up
+  const dim3 grid(copy_grid(n));
+  hipLaunchKernelGGL(hbm_copy, grid, dim3(kCopyBlock), 0, st.s, a.p, b.p, n);  // warm-up
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(ev.a, st.s));
   for (int i = 0; i < iters; ++i)
-    hipLaunchKernelGGL(hbm_copy, dim3(blocks), dim3(256), 0, st.s, a.p, b.p, n);
+    hipLaunchKernelGGL(hbm_copy, grid, dim3(kCopyBlock), 0, st.s, a.p, b.p, n);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(ev.b, st.s));
   const double ms = ev.ms();
