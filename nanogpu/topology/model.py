@@ -40,6 +40,8 @@ class GpuSpec:
     compute_partition: str = "SPX"
     memory_partition: str = "NPS1"
     bdf: str = ""
+    xgmi_peers: int = 0          # xGMI links of this GPU (visible or not from the agent's cgroup)
+    xgmi_link_gbs: float = 0.0   # slowest of them, GB/s (KFD io_link max_bandwidth)
 
 
 @dataclass
@@ -136,6 +138,11 @@ def synthetic_mi355x(n_gpus: int = 8, compute: str = "SPX", memory: str = "NPS1"
     return NodeTopology(gpus=gpus, devices=devs, link_bw=bw, virtualization="BAREMETAL")
 
 
+def _nps(mode: str) -> int:
+    m = (mode or "").upper()
+    return int(m[3:]) if m.startswith("NPS") and m[3:].isdigit() else 1
+
+
 def from_host_json(host: str | dict) -> NodeTopology:
     """Converts the native reader's JSON (nanogpu-topo / _native.discover_topology)."""
     h = json.loads(host) if isinstance(host, str) else host
@@ -153,20 +160,25 @@ def from_host_json(host: str | dict) -> NodeTopology:
             gpus_by_parent[parent] = GpuSpec(
                 index=parent, numa=int(g.get("numa", -1)), cus=0, xcds=0, hbm_mib=0,
                 compute_partition=cp, memory_partition=(g.get("memory_partition") or "").upper(),
+                xgmi_peers=int(g.get("xgmi_peers", 0)), xgmi_link_gbs=float(g.get("xgmi_min_bw_mbs", 0)) / 1000.0,
                 bdf=f"{int(g.get('domain', 0)):04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7}")
         gs = gpus_by_parent[parent]
         gs.cus += int(g.get("cus", 0))
         gs.xcds += int(g.get("num_xcc", 1))
         devices.append(DeviceSpec(gpu=parent, part=part, cus=int(g.get("cus", 0)),
                                   xcds=int(g.get("num_xcc", 1)), hbm_mib=mib))
-    # HBM: in NPS1 every partition reports the whole pool; split it evenly for accounting.
+    # HBM: a compute partition reports the memory partition it lives in (NPS1: the whole
+    # pool; NPSn: 1/n of it) and parts/n compute partitions share each memory partition, so
+    # the per-partition accounting share is reported * n / parts.
     for parent, gs in gpus_by_parent.items():
         ds = [d for d in devices if d.gpu == parent]
-        total = max((d.hbm_mib for d in ds), default=0)
-        if ds and all(d.hbm_mib == total for d in ds) and len(ds) > 1:
+        reported = max((d.hbm_mib for d in ds), default=0)
+        if ds and len(ds) > 1 and all(d.hbm_mib == reported for d in ds):
+            nps = _nps(gs.memory_partition)
+            share = reported * nps // len(ds) if len(ds) % nps == 0 else reported // len(ds)
             for d in ds:
-                d.hbm_mib = total // len(ds)
-            gs.hbm_mib = total
+                d.hbm_mib = share
+            gs.hbm_mib = share * len(ds)
         else:
             gs.hbm_mib = sum(d.hbm_mib for d in ds)
     n = len(gpus_by_parent)

@@ -37,6 +37,9 @@ struct GpuInfo {
   std::string compute_partition;          // SPX/DPX/QPX/CPX ("" if unknown)
   std::string memory_partition;           // NPS1/NPS2/NPS4/NPS8
   std::string available_compute_partitions;
+  int xgmi_peers = 0;              // xGMI io_links (type 11) to other GPU nodes, visible or not
+  int64_t xgmi_min_bw_mbs = 0;     // slowest / fastest of those links (KFD max_bandwidth, MB/s)
+  int64_t xgmi_max_bw_mbs = 0;
   int parent = -1;        // physical GPU index within the node (filled by group_partitions)
   int partition = 0;      // partition index within the physical GPU
 };

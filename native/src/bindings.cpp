@@ -429,5 +429,6 @@ PYBIND11_MODULE(_native, m) {
       },
       py::arg("root") = "", py::arg("use_amdsmi") = true,
       "Reads KFD/DRM sysfs (+ libamd_smi) and returns the node GPU topology as JSON.");
+  m.def("parse_properties", &parse_properties, "KFD `key value` properties text -> dict");
   m.def("mono_now", &mono_now);
 }

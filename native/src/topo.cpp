@@ -129,15 +129,25 @@ HostTopology read_sysfs(const std::string& root) {
     kfd_to_gpu[g.kfd_node] = static_cast<int>(t.gpus.size());
     t.gpus.push_back(g);
   }
-  for (const GpuInfo& g : t.gpus) {
+  for (size_t gi_idx = 0; gi_idx < t.gpus.size(); ++gi_idx) {
+    const GpuInfo g = t.gpus[gi_idx];
     const std::string base = kfd + "/" + std::to_string(g.kfd_node) + "/io_links";
     for (const std::string& l : list_dir(base)) {
       auto lp = parse_properties(read_file(base + "/" + l + "/properties"));
       LinkInfo li;
       li.from = static_cast<int>(as_i64(lp, "node_from", g.kfd_node));
       li.to = static_cast<int>(as_i64(lp, "node_to", -1));
-      if (kfd_to_gpu.find(li.to) == kfd_to_gpu.end()) continue;  // GPU<->CPU link
       li.type = static_cast<int>(as_i64(lp, "type"));
+      if (li.type == 11) {
+        // xGMI peer: counted even when the peer's node is hidden from this container (its
+        // KFD properties unreadable), so a 1-GPU view still knows its hive's link fabric.
+        GpuInfo& gi = t.gpus[kfd_to_gpu[g.kfd_node]];
+        const int64_t bw = as_i64(lp, "max_bandwidth");
+        gi.xgmi_peers += 1;
+        gi.xgmi_min_bw_mbs = gi.xgmi_peers == 1 ? bw : std::min(gi.xgmi_min_bw_mbs, bw);
+        gi.xgmi_max_bw_mbs = std::max(gi.xgmi_max_bw_mbs, bw);
+      }
+      if (kfd_to_gpu.find(li.to) == kfd_to_gpu.end()) continue;  // GPU<->CPU or hidden peer
       li.weight = static_cast<int>(as_i64(lp, "weight"));
       li.min_bw_mbs = as_i64(lp, "min_bandwidth");
       li.max_bw_mbs = as_i64(lp, "max_bandwidth");
@@ -343,7 +353,9 @@ std::string to_json(const HostTopology& t) {
        << ",\"lds_size_kib\":" << g.lds_size_kib << ",\"numa\":" << g.numa
        << ",\"compute_partition\":\"" << esc(g.compute_partition) << "\",\"memory_partition\":\""
        << esc(g.memory_partition) << "\",\"available_compute_partitions\":\""
-       << esc(g.available_compute_partitions) << "\",\"parent\":" << g.parent
+       << esc(g.available_compute_partitions) << "\",\"xgmi_peers\":" << g.xgmi_peers
+       << ",\"xgmi_min_bw_mbs\":" << g.xgmi_min_bw_mbs << ",\"xgmi_max_bw_mbs\":" << g.xgmi_max_bw_mbs
+       << ",\"parent\":" << g.parent
        << ",\"partition\":" << g.partition << "}";
   }
   os << "],\"links\":[";
