@@ -1,0 +1,179 @@
+"""Node agent: discovers the node's MI355X devices, publishes them, runs the device plugin.
+
+Reference counterpart: the node side is outside the reference repo (nano-gpu-agent,
+reference README.md:9, 30-34); the scheduler only reads `capacity["nano-gpu/gpu-percent"]`
+(reference pkg/utils/node.go:8-14). This agent publishes, per node:
+  * annotation `nano-gpu/topology`: devices (GPU or partition), CUs, XCDs, HBM MiB, NUMA,
+    xGMI link matrix, partition modes and optional probe calibration (topology.model);
+  * label `amd.com/gpu.present=true` (the load-aware poller's node selector);
+  * status capacity/allocatable `nano-gpu/gpu-memory` (HBM MiB) and, without the device
+    plugin (`--advertise status`), `nano-gpu/gpu-percent` = 100 x devices;
+and serves the kubelet device plugin (plugin.py) for `nano-gpu/gpu-percent`.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import os
+
+from .. import types as T
+from ..k8s import podutil as pu
+from ..topology.model import NodeTopology, from_host_json
+
+log = logging.getLogger(__name__)
+
+
+def discover(sysfs_root: str = "", use_amdsmi: bool = True) -> tuple[NodeTopology, dict]:
+    from ..native import core
+
+    host = json.loads(core().discover_topology(sysfs_root, use_amdsmi))
+    return from_host_json(host), host
+
+
+def calibrate(topo: NodeTopology, device: int = 0) -> dict:
+    """Measures what the annotation cannot read from sysfs, on the real device (HIP probe)."""
+    from ..probe.calibrate import hbm_bandwidth, local_gpu_facts
+
+    out: dict = {}
+    facts = local_gpu_facts(device)
+    props = facts.get("props") or {}
+    if props:
+        out["gcn_arch"] = props.get("gcn_arch")
+        out["hbm_copy_gbs"] = round(hbm_bandwidth(device, 1 << 30, 10), 1)
+    topo.calibration.update(out)
+    return out
+
+
+def node_patch(topo: NodeTopology) -> dict:
+    labels = {T.AMD_GPU_NODE_LABEL[0]: T.AMD_GPU_NODE_LABEL[1]}
+    if topo.gpus:
+        labels["nano-gpu/compute-partition"] = topo.gpus[0].compute_partition or "SPX"
+    return {"metadata": {"annotations": {T.ANNOTATION_TOPOLOGY: topo.to_json()}, "labels": labels}}
+
+
+def status_patch(topo: NodeTopology, advertise_percent: bool) -> dict:
+    res = {T.RESOURCE_GPU_MEMORY: str(sum(d.hbm_mib for d in topo.devices))}
+    if advertise_percent:
+        res[T.RESOURCE_GPU_PERCENT] = str(T.GPU_PERCENT_EACH_CARD * len(topo.devices))
+    return {"status": {"capacity": dict(res), "allocatable": dict(res)}}
+
+
+async def publish(api, node_name: str, topo: NodeTopology, advertise_percent: bool) -> None:
+    await api.patch_node(node_name, node_patch(topo))
+    await api.patch_node_status(node_name, status_patch(topo, advertise_percent))
+
+
+class NodeAgent:
+    def __init__(self, api, node_name: str, topo: NodeTopology, host: dict | None = None,
+                 device_plugin: bool = True, plugin_dir: str = "", health_period_s: float = 10.0,
+                 sysfs_root: str = ""):
+        self.api = api
+        self.node = node_name
+        self.topo = topo
+        self.host = host or {}
+        self.device_plugin = device_plugin
+        self.plugin_dir = plugin_dir
+        self.health_period_s = health_period_s
+        self.sysfs_root = sysfs_root
+        self.plugin = None
+        self.server = None
+        self.informer = None
+        self.tasks: list[asyncio.Task] = []
+
+    def render_minors(self) -> list[int]:
+        gpus = self.host.get("gpus") or []
+        if len(gpus) == len(self.topo.devices):
+            return [int(g.get("render_minor", 0)) for g in gpus]
+        return [128 + 8 * i for i in range(len(self.topo.devices))]
+
+    async def start(self, register: bool = True) -> None:
+        from ..k8s.informer import Informer
+        from .plugin import NanoGpuPlugin, serve
+
+        await publish(self.api, self.node, self.topo, advertise_percent=not self.device_plugin)
+        if not self.device_plugin:
+            return
+        self.plugin = NanoGpuPlugin(self.topo, self.api, self.node, self.render_minors())
+        # pods on this node: CU grants are rebuilt from the synced informer's view (the API
+        # server is the checkpoint), and released when pods finish or go away
+        self.informer = Informer(self.api, "pods", label_selector=f"{T.LABEL_GPU_ASSUME}=true")
+        self.informer.add_handler(self._on_pod)
+        self.tasks.append(self.informer.start())
+        await self.informer.synced.wait()
+        restored = await self.plugin.rebuild(self.informer.list())
+        log.info("agent %s: %d devices, %d CU grants restored", self.node, len(self.topo.devices), restored)
+        self.server, _ = await serve(self.plugin, self.plugin_dir or "/var/lib/kubelet/device-plugins",
+                                     register=register)
+        if self.health_period_s > 0:
+            self.tasks.append(asyncio.ensure_future(self._health_loop()))
+
+    def _on_pod(self, etype: str, pod: dict, old: dict | None) -> None:
+        if pu.node_name_of(pod) != self.node or self.plugin is None:
+            return
+        if etype == "DELETED" or pu.is_completed(pod):
+            self.plugin.release_pod(pu.pod_uid(pod))
+
+    async def _health_loop(self) -> None:
+        while True:
+            await asyncio.sleep(self.health_period_s)
+            try:
+                _, host = discover(self.sysfs_root, use_amdsmi=False)
+                present = {int(g["render_minor"]) for g in host.get("gpus", [])}
+                for i, minor in enumerate(self.render_minors()):
+                    self.plugin.set_health(i, minor in present)
+            except Exception:
+                log.exception("health check failed")
+
+    async def stop(self) -> None:
+        for t in self.tasks:
+            t.cancel()
+        if self.informer is not None:
+            await self.informer.stop()
+        if self.server is not None:
+            await self.server.stop(grace=1.0)
+
+
+def main(argv: list[str] | None = None) -> int:
+    import argparse
+
+    ap = argparse.ArgumentParser(prog="nanogpu-agent", description="MI355X node agent for nano-gpu-scheduler")
+    ap.add_argument("--node-name", default=os.environ.get("NODE_NAME", ""))
+    ap.add_argument("--sysfs-root", default="")
+    ap.add_argument("--no-amdsmi", action="store_true")
+    ap.add_argument("--calibrate", action="store_true", help="run the HIP probe (HBM GB/s) before publishing")
+    ap.add_argument("--advertise", choices=["device-plugin", "status"], default="device-plugin")
+    ap.add_argument("--plugin-dir", default="/var/lib/kubelet/device-plugins")
+    ap.add_argument("--kube-api", default=None)
+    ap.add_argument("--kubeconfig", default=os.environ.get("KUBECONFIG"))
+    ap.add_argument("--print", action="store_true", help="print the topology annotation and exit")
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    topo, host = discover(a.sysfs_root, not a.no_amdsmi)
+    if a.calibrate:
+        calibrate(topo)
+    if a.print:
+        print(json.dumps(topo.to_dict(), indent=1))
+        return 0 if topo.devices else 1
+    if not a.node_name:
+        ap.error("--node-name (or NODE_NAME) is required")
+
+    async def run() -> int:
+        import signal
+
+        from ..k8s.client import KubeClient, KubeConfig
+
+        api = KubeClient(KubeConfig.auto(a.kubeconfig, a.kube_api))
+        agent = NodeAgent(api, a.node_name, topo, host, device_plugin=a.advertise == "device-plugin",
+                          plugin_dir=a.plugin_dir, sysfs_root=a.sysfs_root)
+        await agent.start()
+        stop = asyncio.Event()
+        loop = asyncio.get_running_loop()
+        for sig in (signal.SIGINT, signal.SIGTERM):
+            loop.add_signal_handler(sig, stop.set)
+        await stop.wait()
+        await agent.stop()
+        await api.close()
+        return 0
+
+    return asyncio.run(run())

@@ -1,0 +1,261 @@
+"""nano-gpu device plugin for MI355X: kubelet side of the scheduler's placement.
+
+The reference scheduler writes `nano-gpu/container-<c>=<device>` on the pod and relies on
+an external NVIDIA device plugin (nano-gpu-agent, reference README.md:9, 30-34) to turn it
+into a device inside the container. This is the AMD equivalent:
+
+* advertises `nano-gpu/gpu-percent` as 100 virtual IDs per schedulable device (an SPX
+  GPU or a DPX/QPX/CPX partition), each carrying the device's NUMA node;
+* on Allocate, kubelet hands over N arbitrary virtual IDs for one container; the plugin
+  finds the container the extender placed on this node (assumed pod, not yet allocated,
+  a container whose gpu-percent == N, oldest `nano-gpu/assume-time` first) and reads its
+  device index from the annotation;
+* answers with the device nodes (`/dev/kfd` + the partition's `/dev/dri/renderD*`), a
+  spatial CU mask for fractional grants (`HSA_CU_MASK`, XCD-symmetric, see cumask.py),
+  and the HBM budget (`NANO_GPU_MEMORY_MIB`, enforced in-process by nanogpu.agent.guest);
+* records the CU grant as `nano-gpu/cu-mask-<c>` on the pod, so an agent restart
+  rebuilds its CU map from the API server (the same checkpoint contract as the
+  extender's, reference dealer.go:58-72).
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import os
+import time
+from dataclasses import dataclass
+
+from .. import types as T
+from ..k8s import podutil as pu
+from ..topology.model import NodeTopology
+from . import cumask
+from . import dpapi as D
+
+log = logging.getLogger(__name__)
+
+
+def virtual_ids(topo: NodeTopology) -> list[tuple[str, int]]:
+    """(ID, numa) for every percent unit of every schedulable device: "d<dev>-<k>"."""
+    numa = {g.index: g.numa for g in topo.gpus}
+    return [(f"d{i}-{k}", numa.get(d.gpu, -1)) for i, d in enumerate(topo.devices)
+            for k in range(T.GPU_PERCENT_EACH_CARD)]
+
+
+@dataclass
+class Assignment:
+    pod_key: str
+    container: str
+    devices: list[int]
+    percent: int
+    mib: int
+
+
+class Matcher:
+    """Finds which container an Allocate call is for (no pod identity in the request)."""
+
+    def __init__(self, api, node_name: str):
+        self.api = api
+        self.node = node_name
+        self.claimed: dict[tuple[str, str], float] = {}   # (pod uid, container) -> time
+
+    async def candidates(self) -> list[dict]:
+        pods, _ = await self.api.list_pods(label_selector=f"{T.LABEL_GPU_ASSUME}=true",
+                                           field_selector=f"{T.NODE_NAME_FIELD}={self.node}")
+        return [p for p in pods if pu.is_assumed(p) and not pu.is_completed(p)]
+
+    async def match(self, percent: int) -> tuple[dict, dict] | None:
+        best = None
+        for p in await self.candidates():
+            ann = pu.meta(p).get("annotations") or {}
+            t = float(ann.get(T.ANNOTATION_ASSUME_TIME, "0") or 0)
+            for c in pu.containers(p):
+                name = c.get("name", "")
+                if (pu.pod_uid(p), name) in self.claimed or T.ANNOTATION_CU_MASK_FMT.format(name) in ann:
+                    continue
+                if pu.container_percent(c) != percent or pu.container_assignment(p, name) is None:
+                    continue
+                if best is None or t < best[0]:
+                    best = (t, p, c)
+                break
+        if best is None:
+            return None
+        self.claimed[(pu.pod_uid(best[1]), best[2].get("name", ""))] = time.time()
+        return best[1], best[2]
+
+
+class NanoGpuPlugin:
+    """DevicePlugin service implementation (grpc.aio generic handlers)."""
+
+    def __init__(self, topo: NodeTopology, api, node_name: str, render_minors: list[int] | None = None,
+                 dev_root: str = "/dev"):
+        self.topo = topo
+        self.api = api
+        self.node = node_name
+        self.matcher = Matcher(api, node_name)
+        self.render = render_minors or [128 + 8 * i for i in range(len(topo.devices))]
+        self.dev_root = dev_root
+        self.cus = [cumask.DeviceCUs(d.cus, d.xcds) for d in topo.devices]
+        self.health = [True] * len(topo.devices)
+        self._changed = asyncio.Event()
+        self.allocations: list[Assignment] = []
+
+    # ---------------------------------------------------------------- restart rebuild
+    async def rebuild(self, pods: list[dict] | None = None) -> int:
+        n = 0
+        if pods is None:
+            pods = await self.matcher.candidates()
+        for p in pods:
+            if pu.node_name_of(p) != self.node or not pu.is_assumed(p) or pu.is_completed(p):
+                continue
+            ann = pu.meta(p).get("annotations") or {}
+            for c in pu.containers(p):
+                name = c.get("name", "")
+                mask = ann.get(T.ANNOTATION_CU_MASK_FMT.format(name))
+                idx = pu.container_assignment(p, name)
+                if mask is None or not idx:
+                    continue
+                self.matcher.claimed[(pu.pod_uid(p), name)] = 0.0
+                if mask not in ("", "full") and 0 <= idx[0] < len(self.cus):
+                    self.cus[idx[0]].restore(f"{pu.pod_uid(p)}/{name}", cumask.parse_ranges(mask.split(":")[-1]))
+                n += 1
+        return n
+
+    def release_pod(self, uid: str) -> None:
+        for d in self.cus:
+            for owner in [o for o in d.used if o.startswith(uid + "/")]:
+                d.release(owner)
+        for k in [k for k in self.matcher.claimed if k[0] == uid]:
+            del self.matcher.claimed[k]
+
+    def set_health(self, dev: int, healthy: bool) -> None:
+        if self.health[dev] != healthy:
+            self.health[dev] = healthy
+            self._changed.set()
+
+    # ---------------------------------------------------------------- gRPC methods
+    async def GetDevicePluginOptions(self, request, context):
+        return D.DevicePluginOptions(pre_start_required=False, get_preferred_allocation_available=True)
+
+    def _device_list(self):
+        resp = D.ListAndWatchResponse()
+        for vid, numa in virtual_ids(self.topo):
+            dev = int(vid[1:vid.index("-")])
+            d = resp.devices.add(ID=vid, health=D.HEALTHY if self.health[dev] else D.UNHEALTHY)
+            if numa >= 0:
+                d.topology.nodes.add(ID=numa)
+        return resp
+
+    async def ListAndWatch(self, request, context):
+        yield self._device_list()
+        while True:
+            await self._changed.wait()
+            self._changed.clear()
+            yield self._device_list()
+
+    async def GetPreferredAllocation(self, request, context):
+        """Prefers IDs of one device, so kubelet's own accounting mirrors a real share."""
+        resp = D.PreferredAllocationResponse()
+        for cr in request.container_requests:
+            by_dev: dict[str, list[str]] = {}
+            for vid in cr.available_deviceIDs:
+                by_dev.setdefault(vid.split("-")[0], []).append(vid)
+            chosen = list(cr.must_include_deviceIDs)
+            for ids in sorted(by_dev.values(), key=len):
+                if len(ids) >= cr.allocation_size - len(chosen):
+                    chosen += [i for i in ids if i not in chosen][:cr.allocation_size - len(chosen)]
+                    break
+            if len(chosen) < cr.allocation_size:
+                rest = [i for i in cr.available_deviceIDs if i not in chosen]
+                chosen += rest[:cr.allocation_size - len(chosen)]
+            resp.container_responses.add(deviceIDs=chosen)
+        return resp
+
+    async def PreStartContainer(self, request, context):
+        return D.PreStartContainerResponse()
+
+    async def Allocate(self, request, context):
+        resp = D.AllocateResponse()
+        for cr in request.container_requests:
+            percent = len(cr.devices_ids)
+            m = await self.matcher.match(percent)
+            if m is None:
+                msg = f"no assumed container with gpu-percent={percent} on node {self.node}"
+                log.warning("Allocate: %s", msg)
+                if context is not None:
+                    await context.abort(_grpc_status("FAILED_PRECONDITION"), msg)
+                raise RuntimeError(msg)
+            pod, c = m
+            resp.container_responses.append(await self._container_response(pod, c, percent))
+        return resp
+
+    async def _container_response(self, pod: dict, c: dict, percent: int):
+        name = c.get("name", "")
+        devs = pu.container_assignment(pod, name) or []
+        mib = pu.container_mib(c)
+        r = D.ContainerAllocateResponse()
+        r.devices.add(container_path="/dev/kfd", host_path=f"{self.dev_root}/kfd", permissions="rw")
+        for d in devs:
+            minor = self.render[d]
+            r.devices.add(container_path=f"/dev/dri/renderD{minor}", host_path=f"{self.dev_root}/dri/renderD{minor}",
+                          permissions="rw")
+        r.envs["NANO_GPU_DEVICES"] = ",".join(map(str, devs))
+        r.envs["NANO_GPU_PERCENT"] = str(percent)
+        mask_ann = "full"
+        if percent < T.GPU_PERCENT_EACH_CARD and len(devs) == 1:
+            bits = self.cus[devs[0]].grant(f"{pu.pod_uid(pod)}/{name}", percent)
+            if bits is None:
+                raise RuntimeError(f"device {devs[0]} has no free CUs for {percent}%")
+            mask_ann = cumask.hsa_cu_mask(0, bits)   # the container sees its device as index 0
+            r.envs["HSA_CU_MASK"] = mask_ann
+            r.envs["NANO_GPU_CUS"] = str(len(bits))
+        if mib:
+            r.envs["NANO_GPU_MEMORY_MIB"] = str(mib)
+            total = self.topo.devices[devs[0]].hbm_mib if devs else 0
+            if total:
+                r.envs["NANO_GPU_MEMORY_FRACTION"] = f"{min(1.0, mib / total):.6f}"
+        r.annotations["nano-gpu/devices"] = r.envs["NANO_GPU_DEVICES"]
+        ns, pname = pu.pod_ns_name(pod)
+        try:
+            await self.api.patch_pod(ns, pname, {"metadata": {"annotations": {
+                T.ANNOTATION_CU_MASK_FMT.format(name): mask_ann}}})
+        except Exception as e:  # the allocation stands; the annotation only speeds up rebuild
+            log.warning("annotating %s/%s failed: %s", ns, pname, e)
+        self.allocations.append(Assignment(pu.pod_key(pod), name, devs, percent, mib))
+        return r
+
+
+def _grpc_status(name: str):
+    import grpc
+
+    return getattr(grpc.StatusCode, name)
+
+
+# -------------------------------------------------------------------- serving / registration
+async def serve(plugin: NanoGpuPlugin, plugin_dir: str = D.PLUGIN_DIR, socket_name: str = "nanogpu-percent.sock",
+                kubelet_socket: str | None = None, resource: str = T.RESOURCE_GPU_PERCENT, register: bool = True):
+    """Starts the plugin's gRPC server on a unix socket and registers with kubelet."""
+    import grpc
+
+    path = os.path.join(plugin_dir, socket_name)
+    try:
+        os.unlink(path)
+    except FileNotFoundError:
+        pass
+    server = grpc.aio.server()
+    server.add_generic_rpc_handlers((D.generic_handler("DevicePlugin", plugin),))
+    server.add_insecure_port(f"unix://{path}")
+    await server.start()
+    if register:
+        await register_with_kubelet(kubelet_socket or os.path.join(plugin_dir, "kubelet.sock"), socket_name, resource)
+    return server, path
+
+
+async def register_with_kubelet(kubelet_socket: str, endpoint: str, resource: str) -> None:
+    import grpc
+
+    async with grpc.aio.insecure_channel(f"unix://{kubelet_socket}") as ch:
+        stub = D.Stub(ch, "Registration")
+        await stub.Register(D.RegisterRequest(
+            version=D.VERSION, endpoint=endpoint, resource_name=resource,
+            options=D.DevicePluginOptions(pre_start_required=False, get_preferred_allocation_available=True)),
+            timeout=10)

@@ -18,6 +18,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -307,6 +308,43 @@ double mfma_ms_impl(int dev, const std::vector<uint32_t>& mask, int blocks, int 
   return ev.ms();
 }
 
+// Co-located tenants: one MFMA burn per CU mask, each on its own CU-masked stream, all
+// launched back to back so they run concurrently. Returns per-tenant TFLOP/s, timed with
+// each stream's own events: with disjoint XCD-symmetric masks every tenant must get
+// throughput proportional to its CUs regardless of its neighbours (the agent's spatial
+// share, nanogpu/agent/cumask.py).
+std::vector<double> mfma_colocated(int dev, const std::vector<std::vector<uint32_t>>& masks,
+                                   const std::vector<int>& blocks, int iters) {
+  HIP_OK(hipSetDevice(dev));
+  if (masks.empty() || masks.size() != blocks.size() || iters <= 0)
+    throw std::invalid_argument("mfma_colocated: one block count per mask, iters > 0");
+  const size_t n = masks.size();
+  std::vector<std::unique_ptr<Stream>> streams;
+  std::vector<std::unique_ptr<Events>> evs;
+  std::vector<std::unique_ptr<DevBuf<float>>> outs;
+  for (size_t i = 0; i < n; ++i) {
+    if (blocks[i] <= 0) throw std::invalid_argument("mfma_colocated: bad block count");
+    streams.emplace_back(new Stream(masks[i]));
+    evs.emplace_back(new Events());
+    outs.emplace_back(new DevBuf<float>(static_cast<size_t>(blocks[i]) * 256));
+    hipLaunchKernelGGL(mfma_burn, dim3(blocks[i]), dim3(256), 0, streams[i]->s, outs[i]->p, 8);  // warm-up
+  }
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipDeviceSynchronize());
+  for (size_t i = 0; i < n; ++i) {
+    HIP_OK(hipEventRecord(evs[i]->a, streams[i]->s));
+    hipLaunchKernelGGL(mfma_burn, dim3(blocks[i]), dim3(256), 0, streams[i]->s, outs[i]->p, iters);
+    HIP_OK(hipEventRecord(evs[i]->b, streams[i]->s));
+  }
+  HIP_OK(hipGetLastError());
+  std::vector<double> tf(n);
+  for (size_t i = 0; i < n; ++i) {
+    const double ms = evs[i]->ms();
+    tf[i] = 4.0 * 32768.0 * iters * (static_cast<double>(blocks[i]) * 4) / (ms * 1e-3) / 1e12;
+  }
+  return tf;
+}
+
 double peer_bandwidth(int src, int dst, size_t bytes, int iters) {
   int n = 0;
   HIP_OK(hipGetDeviceCount(&n));
@@ -361,6 +399,9 @@ PYBIND11_MODULE(_probe, m) {
         "C[32x32] = bf16(A[32x16]) @ bf16(B[16x32]) with one v_mfma_f32_32x32x16_bf16 (fp32 accumulate).");
   m.def("copy_check", &copy_check, py::arg("device") = 0, py::arg("n_floats") = size_t(1) << 24,
         py::call_guard<py::gil_scoped_release>(), "hbm_copy kernel result == source, bit for bit.");
+  m.def("mfma_colocated", &mfma_colocated, py::arg("device"), py::arg("cu_masks"), py::arg("blocks"),
+        py::arg("iters") = 2048, py::call_guard<py::gil_scoped_release>(),
+        "Concurrent MFMA burns on CU-masked streams; per-stream TFLOP/s.");
   m.def("peer_bandwidth", &peer_bandwidth, py::arg("src"), py::arg("dst"),
         py::arg("bytes") = size_t(256) << 20, py::arg("iters") = 10,
         py::call_guard<py::gil_scoped_release>(), "hipMemcpyPeer bandwidth in GB/s.");

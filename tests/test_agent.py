@@ -1,0 +1,180 @@
+"""Node agent: CU-mask sharing, topology publishing and the kubelet device plugin.
+
+The device plugin is exercised over real gRPC on unix sockets: a fake kubelet serves the
+Registration service, the test plays kubelet's part of ListAndWatch / Allocate, and the
+pods come from the real extender scheduling them into a fake API server.
+"""
+import asyncio
+
+import grpc
+import pytest
+
+from nanogpu import types as T
+from nanogpu.agent import cumask
+from nanogpu.agent import dpapi as D
+from nanogpu.agent.node import NodeAgent, node_patch, status_patch
+from nanogpu.k8s import podutil as pu
+from nanogpu.k8s.fake_apiserver import FakeKubeStore, InProcKube
+from nanogpu.topology.model import synthetic_mi355x
+
+
+# ----------------------------------------------------------------------------- cumask
+def test_cu_grants_are_xcd_symmetric_and_disjoint():
+    d = cumask.DeviceCUs(256, 8)
+    a = d.grant("a", 25)
+    b = d.grant("b", 50)
+    c = d.grant("c", 25)
+    assert len(a) == 64 and len(b) == 128 and len(c) == 64
+    assert not set(a) & set(b) and not set(b) & set(c) and not set(a) & set(c)
+    for bits in (a, b, c):
+        per_xcd = [sum(1 for x in bits if x % 8 == k) for k in range(8)]
+        assert len(set(per_xcd)) == 1          # the same CU count on every XCD
+    assert d.grant("d", 10) is None            # full
+    assert d.grant("a", 25) == a               # idempotent
+    d.release("b")
+    assert d.grant("d", 10) is not None
+
+
+def test_cu_sizing_never_overcommits():
+    for parts in ((33, 33, 33), (10,) * 10, (1,) * 32, (3, 97)):
+        d = cumask.DeviceCUs(256, 8)
+        assert all(d.grant(str(i), p) is not None for i, p in enumerate(parts))
+    d = cumask.DeviceCUs(32, 1)                # CPX partition: one XCD, unit = 1 CU
+    assert len(d.grant("x", 50)) == 16
+
+
+def test_mask_text_and_words():
+    bits = list(range(0, 16)) + list(range(32, 40))
+    assert cumask.ranges(bits) == "0-15,32-39"
+    assert cumask.parse_ranges("0-15,32-39") == bits
+    assert cumask.hsa_cu_mask(0, [5]) == "0:5"
+    w = cumask.mask_words(bits, 256)
+    assert w[0] == 0xFFFF and w[1] == 0xFF and w[2:] == [0] * 6
+
+
+# ----------------------------------------------------------------------------- publisher
+def test_node_and_status_patches():
+    t = synthetic_mi355x(8, "CPX")
+    p = node_patch(t)
+    assert p["metadata"]["labels"]["amd.com/gpu.present"] == "true"
+    assert p["metadata"]["labels"]["nano-gpu/compute-partition"] == "CPX"
+    s = status_patch(t, advertise_percent=True)["status"]["capacity"]
+    assert s[T.RESOURCE_GPU_PERCENT] == "6400"
+    assert int(s[T.RESOURCE_GPU_MEMORY]) == sum(d.hbm_mib for d in t.devices)
+    assert T.RESOURCE_GPU_PERCENT not in status_patch(t, advertise_percent=False)["status"]["capacity"]
+
+
+# ----------------------------------------------------------------------------- device plugin
+class FakeKubelet:
+    def __init__(self):
+        self.registered = []
+
+    async def Register(self, request, context):
+        self.registered.append((request.version, request.endpoint, request.resource_name))
+        return D.Empty()
+
+
+async def _schedule(store, node_name, pods):
+    """Places pods with the real extender (in-process verbs, no HTTP)."""
+    from nanogpu.extender.verbs import Extender
+    from nanogpu.state.cluster import ClusterState
+
+    st = ClusterState()
+    st.register_node(store.get_node(node_name))
+    ext = Extender(st, InProcKube(store))
+    for p in pods:
+        p = store.create_pod(p)
+        assert ext.filter({"Pod": p, "NodeNames": [node_name]})["NodeNames"] == [node_name]
+        m = pu.meta(p)
+        res = await ext.bind({"PodName": m["name"], "PodNamespace": m["namespace"], "PodUID": m["uid"],
+                              "Node": node_name})
+        assert res["Error"] == "", res
+        await asyncio.sleep(0.002)   # distinct assume-times
+
+
+def test_device_plugin_end_to_end(tmp_path):
+    async def main():
+        store = FakeKubeStore()
+        topo = synthetic_mi355x(8)
+        store.add_node(pu.make_node("n0", 8, topo.to_json()))
+        api = InProcKube(store)
+        # fake kubelet
+        kubelet = FakeKubelet()
+        ksrv = grpc.aio.server()
+        ksrv.add_generic_rpc_handlers((D.generic_handler("Registration", kubelet),))
+        ksrv.add_insecure_port(f"unix://{tmp_path}/kubelet.sock")
+        await ksrv.start()
+
+        agent = NodeAgent(api, "n0", topo, device_plugin=True, plugin_dir=str(tmp_path), health_period_s=0)
+        await agent.start()
+        node = store.get_node("n0")
+        assert T.ANNOTATION_TOPOLOGY in node["metadata"]["annotations"]
+        assert node["status"]["capacity"][T.RESOURCE_GPU_MEMORY] == str(8 * topo.devices[0].hbm_mib)
+        assert kubelet.registered == [("v1beta1", "nanogpu-percent.sock", T.RESOURCE_GPU_PERCENT)]
+
+        await _schedule(store, "n0", [pu.make_pod("a", [("main", 20, 32 * 1024)]),
+                                      pu.make_pod("b", [("main", 30)]),
+                                      pu.make_pod("c", [("x", 0), ("y", 100)])])
+        async with grpc.aio.insecure_channel(f"unix://{tmp_path}/nanogpu-percent.sock") as ch:
+            stub = D.Stub(ch, "DevicePlugin")
+            opts = await stub.GetDevicePluginOptions(D.Empty())
+            assert opts.get_preferred_allocation_available
+            stream = stub.ListAndWatch(D.Empty())
+            first = await stream.read()
+            assert len(first.devices) == 800 and first.devices[0].ID == "d0-0"
+            assert first.devices[0].topology.nodes[0].ID == 0 and first.devices[799].topology.nodes[0].ID == 1
+            pref = await stub.GetPreferredAllocation(D.PreferredAllocationRequest(container_requests=[
+                D.ContainerPreferredAllocationRequest(available_deviceIDs=[f"d1-{k}" for k in range(50)] +
+                                                      [f"d2-{k}" for k in range(100)], allocation_size=30)]))
+            assert {i.split("-")[0] for i in pref.container_responses[0].deviceIDs} == {"d1"}
+
+            ra = await stub.Allocate(D.AllocateRequest(container_requests=[
+                D.ContainerAllocateRequest(devices_ids=[f"d5-{k}" for k in range(20)])]))
+            env = ra.container_responses[0].envs
+            # binpack put both shares on device 0: "a" (20%) gets 6 units = 48 CUs
+            assert env["NANO_GPU_DEVICES"] == "0" and env["HSA_CU_MASK"] == "0:0-47"
+            assert env["NANO_GPU_MEMORY_MIB"] == str(32 * 1024) and float(env["NANO_GPU_MEMORY_FRACTION"]) > 0.1
+            paths = [d.container_path for d in ra.container_responses[0].devices]
+            assert paths == ["/dev/kfd", "/dev/dri/renderD128"]
+            rb = await stub.Allocate(D.AllocateRequest(container_requests=[
+                D.ContainerAllocateRequest(devices_ids=[f"d7-{k}" for k in range(30)])]))
+            assert rb.container_responses[0].envs["HSA_CU_MASK"] == "0:48-119"   # 9 units, disjoint
+            rc = await stub.Allocate(D.AllocateRequest(container_requests=[
+                D.ContainerAllocateRequest(devices_ids=[f"d3-{k}" for k in range(100)])]))
+            envc = rc.container_responses[0].envs
+            assert "HSA_CU_MASK" not in envc and envc["NANO_GPU_DEVICES"] == "1"
+            with pytest.raises(grpc.aio.AioRpcError) as ei:
+                await stub.Allocate(D.AllocateRequest(container_requests=[
+                    D.ContainerAllocateRequest(devices_ids=["d0-1"] * 7)]))
+            assert ei.value.code() == grpc.StatusCode.FAILED_PRECONDITION
+            stream.cancel()
+        ann = store.get_pod("default", "a")["metadata"]["annotations"]
+        assert ann[T.ANNOTATION_CU_MASK_FMT.format("main")] == "0:0-47"
+
+        # agent restart: CU grants come back from the annotations
+        await agent.stop()
+        agent2 = NodeAgent(api, "n0", topo, device_plugin=True, plugin_dir=str(tmp_path), health_period_s=0)
+        await agent2.start()
+        assert agent2.plugin.cus[0].used == {f"{pu.pod_uid(store.get_pod('default', 'a'))}/main": list(range(6)),
+                                             f"{pu.pod_uid(store.get_pod('default', 'b'))}/main": list(range(6, 15))}
+        # deleting a pod frees its CUs
+        store.delete_pod("default", "a")
+        for _ in range(200):
+            if len(agent2.plugin.cus[0].used) == 1:
+                break
+            await asyncio.sleep(0.01)
+        assert len(agent2.plugin.cus[0].used) == 1
+        await agent2.stop()
+        await ksrv.stop(None)
+
+    asyncio.run(main())
+
+
+def test_guest_reads_grant(monkeypatch):
+    from nanogpu.agent import guest
+
+    monkeypatch.setenv("NANO_GPU_PERCENT", "20")
+    monkeypatch.setenv("HSA_CU_MASK", "0:0-47")
+    monkeypatch.setenv("NANO_GPU_MEMORY_FRACTION", "0.25")
+    g = guest.grant()
+    assert g["percent"] == 20 and g["cu_mask"] == "0:0-47" and g["memory_fraction"] == 0.25

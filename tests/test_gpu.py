@@ -116,3 +116,16 @@ def test_bench_one_step_on_gpu(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads(out.read_text())
     assert line["scheduled"] > 0 and line["gpu"]["gpu"]["cus"] == 256
+
+
+def test_colocated_cu_grants_are_isolated(P):
+    """Two tenants of one device with the agent's disjoint XCD-symmetric masks (25 % / 75 %)
+    run concurrently; each gets throughput in proportion to its CUs."""
+    from nanogpu.agent import cumask
+
+    d = cumask.DeviceCUs(256, 8)
+    a, b = d.grant("a", 25), d.grant("b", 75)
+    alone = P.mfma_throughput(0, [], 2048, 1024)["tflops"]
+    ta, tb = P.mfma_colocated(0, [cumask.mask_words(a), cumask.mask_words(b)], [len(a) * 8, len(b) * 8], 1024)
+    assert 0.17 < ta / alone < 0.34, (ta, tb, alone)
+    assert 0.55 < tb / alone < 0.85, (ta, tb, alone)
