@@ -51,6 +51,8 @@ class Config:
     fake_gpus_per_node: int = 8
     fake_partition: str = "SPX"
     seed: int = 0
+    frontend: str = "native"                    # native (C++ epoll front door) | aiohttp
+    frontend_threads: int = 2
     gpu_node_selectors: list = field(default_factory=lambda: [T.AMD_GPU_NODE_LABEL, T.LEGACY_GPU_NODE_LABEL])
 
 
@@ -82,6 +84,7 @@ class Runtime:
         self.poller = None
         self.watcher = None
         self.runner = None
+        self.native = None
         self.bound_port = 0
         self._fake = None
 
@@ -150,11 +153,17 @@ class Runtime:
             self.tasks.append(asyncio.ensure_future(self._sweeper()))
         self.ready.set()
         if serve:
-            app = server.make_app(self.extender, self.ready)
-            self.runner, self.bound_port = await server.start(app, self.cfg.host, self.cfg.port,
-                                                              reuse_port=self.cfg.workers > 1)
-            log.info("worker %d serving on :%d (policy=%s compat=%s)", self.worker, self.bound_port,
-                     self.state.policy, self.state.options.compat)
+            router = server.Router(self.extender, self.ready)
+            if self.cfg.frontend == "native":
+                self.native = server.NativeServer(router, self.cfg.host, self.cfg.port, self.cfg.frontend_threads)
+                self.native.start()
+                self.bound_port = self.native.port
+            else:
+                app = server.make_app(self.extender, self.ready, router=router)
+                self.runner, self.bound_port = await server.start(app, self.cfg.host, self.cfg.port,
+                                                                  reuse_port=self.cfg.workers > 1)
+            log.info("worker %d serving on :%d (%s front door, policy=%s compat=%s)", self.worker, self.bound_port,
+                     self.cfg.frontend, self.state.policy, self.state.options.compat)
 
     def _apply_policy(self, spec) -> None:
         pol = spec.policy or self.state.policy
@@ -172,6 +181,8 @@ class Runtime:
                 self.poller.sweep_stale()
 
     async def stop(self) -> None:
+        if self.native is not None:
+            await self.native.stop()
         if self.runner is not None:
             await self.runner.cleanup()
         for c in self.controllers:

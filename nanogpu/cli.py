@@ -56,6 +56,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--fake-gpus-per-node", type=int, default=8)
     p.add_argument("--fake-partition", default="SPX", choices=["SPX", "DPX", "QPX", "CPX"])
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--frontend", default="native", choices=["native", "aiohttp"],
+                   help="native: C++ epoll server answers filter/priorities without Python")
+    p.add_argument("--frontend-threads", type=int, default=2)
     return p
 
 
@@ -76,4 +79,4 @@ def parse(argv: list[str] | None = None) -> Config:
         ledger_path=a.ledger_path, max_nodes=a.max_nodes, max_pods=a.max_pods,
         verify_pod_on_bind=a.bind_verify_pod, reservation_ttl_s=parse_duration(a.reservation_ttl),
         fake_cluster=a.fake_cluster, fake_gpus_per_node=a.fake_gpus_per_node, fake_partition=a.fake_partition,
-        seed=a.seed)
+        seed=a.seed, frontend=a.frontend, frontend_threads=max(1, a.frontend_threads))

@@ -1,4 +1,4 @@
-"""HTTP API of the extender (aiohttp).
+"""HTTP API of the extender: one route table, two front doors.
 
 Reference routes (pkg/routes/routes.go:19-27, 176-210; pprof.go:10-21):
   POST /scheduler/filter | /scheduler/priorities | /scheduler/bind, GET /version,
@@ -7,6 +7,13 @@ Kept wire-compatible (paths, JSON keys, status codes: bind answers 500 when Erro
 set, routes.go:147-168). Fixed: prioritize answers 400 on a bad body instead of
 panicking (D10); /status is also served on GET (D9) and is read under the ledger's
 locks (D8). Added: /metrics, /healthz, /readyz, /debug/{trace,stacks,profile,state,frag}.
+
+Front doors:
+  * `NativeServer` (default): the C++ epoll server in nanogpu._native (native/src/
+    frontend.cpp) answers filter / priorities itself with no Python on the path and
+    queues everything else (bind, status, metrics, debug, and requests its fast path
+    declines) to `Router.dispatch` on the asyncio loop;
+  * `start()` : aiohttp, every route in Python (fallback / debugging).
 """
 from __future__ import annotations
 
@@ -14,6 +21,7 @@ import asyncio
 import json
 import logging
 import time
+from urllib.parse import parse_qs
 
 from aiohttp import web
 
@@ -23,119 +31,145 @@ from .verbs import Extender
 
 log = logging.getLogger(__name__)
 
+JSON = "application/json; charset=utf-8"
+TEXT = "text/plain; charset=utf-8"
+PROM = "text/plain; version=0.0.4; charset=utf-8"
 
-def _dumps(o) -> str:
-    return json.dumps(o, separators=(",", ":"))
+
+def _dumps(o) -> bytes:
+    return json.dumps(o, separators=(",", ":")).encode()
 
 
-async def _read_json(request: web.Request):
-    raw = await request.read()
+def _load(raw: bytes):
     if not raw:
         raise ValueError("Please send a request body")
     return json.loads(raw)
 
 
-def make_app(ext: Extender, ready: asyncio.Event | None = None, extra_status=None) -> web.Application:
-    routes = web.RouteTableDef()
+class Router:
+    """(method, path) -> handler; handlers return (status, content-type, body bytes)."""
 
-    @routes.post("/scheduler/filter")
-    async def filter_route(request: web.Request):
+    def __init__(self, ext: Extender, ready: asyncio.Event | None = None, extra_status=None):
+        self.ext = ext
+        self.ready = ready
+        self.extra_status = extra_status
+        self.native = None          # NativeServer, for /metrics
+        g, p = "GET", "POST"
+        self.table = {
+            (p, "/scheduler/filter"): self.filter, (p, "/scheduler/priorities"): self.prioritize,
+            (p, "/scheduler/bind"): self.bind, (g, "/version"): self.version,
+            (p, "/status"): self.status, (g, "/status"): self.status, (g, "/metrics"): self.metrics,
+            (g, "/healthz"): self.healthz, (g, "/readyz"): self.readyz, (g, "/debug/trace"): self.trace,
+            (g, "/debug/stacks"): self.stacks, (g, "/debug/pprof/goroutine/"): self.stacks,
+            (g, "/debug/profile"): self.profile, (g, "/debug/pprof/profile/"): self.profile,
+            (g, "/debug/state"): self.state, (g, "/debug/frag"): self.frag, (g, "/debug/pprof/"): self.pprof_index,
+        }
+        self.paths = {path for _, path in self.table}
+
+    async def dispatch(self, method: str, path: str, query: dict, body: bytes) -> tuple[int, str, bytes]:
+        h = self.table.get((method, path))
+        if h is None:
+            if path in self.paths:
+                return 405, TEXT, b"405: Method Not Allowed"
+            return 404, TEXT, b"404: Not Found"
+        return await h(query, body)
+
+    # ---------------------------------------------------------------- verbs
+    async def filter(self, q, body):
         try:
-            body = await _read_json(request)
+            args = _load(body)
         except ValueError as e:  # includes JSONDecodeError
-            return web.json_response({"Nodes": None, "NodeNames": None, "FailedNodes": None, "Error": str(e)},
-                                     dumps=_dumps)
-        return web.json_response(ext.filter(body), dumps=_dumps)
+            return 200, JSON, _dumps({"Nodes": None, "NodeNames": None, "FailedNodes": None, "Error": str(e)})
+        return 200, JSON, _dumps(self.ext.filter(args))
 
-    @routes.post("/scheduler/priorities")
-    async def prioritize_route(request: web.Request):
+    async def prioritize(self, q, body):
         try:
-            body = await _read_json(request)
-            return web.json_response(ext.prioritize(body), dumps=_dumps)
+            return 200, JSON, _dumps(self.ext.prioritize(_load(body)))
         except ValueError as e:
-            return web.json_response({"error": str(e)}, status=400, dumps=_dumps)
+            return 400, JSON, _dumps({"error": str(e)})
 
-    @routes.post("/scheduler/bind")
-    async def bind_route(request: web.Request):
+    async def bind(self, q, body):
         try:
-            body = await _read_json(request)
+            args = _load(body)
         except ValueError as e:
-            return web.json_response({"Error": str(e)}, status=500, dumps=_dumps)
-        res = await ext.bind(body)
-        return web.json_response(res, status=500 if res.get("Error") else 200, dumps=_dumps)
+            return 500, JSON, _dumps({"Error": str(e)})
+        res = await self.ext.bind(args)
+        return (500 if res.get("Error") else 200), JSON, _dumps(res)
 
-    @routes.get("/version")
-    async def version(_):
-        return web.Response(text=T.VERSION)
+    # ---------------------------------------------------------------- ops
+    async def version(self, q, body):
+        return 200, TEXT, T.VERSION.encode()
 
-    async def status(_):
-        body = ext.state.status()
-        if extra_status:
-            body = extra_status(body)
-        return web.json_response(body, dumps=_dumps)
+    async def status(self, q, body):
+        out = self.ext.state.status()
+        if self.extra_status:
+            out = self.extra_status(out)
+        return 200, JSON, _dumps(out)
 
-    routes.post("/status")(status)
-    routes.get("/status")(status)
-
-    @routes.get("/metrics")
-    async def metrics(_):
-        st = ext.state
+    async def metrics(self, q, body):
+        st = self.ext.state
         f = st.frag()
-        m = ext.metrics
+        m = self.ext.metrics
         m.frag_pct.set(f["frag_pct"])
         m.frag_mib.set(f["frag_mib"])
         m.free_pct.set(f["pct_free_total"])
         m.nodes.set(st.ledger.n_nodes)
         m.pods.set(st.ledger.n_pods)
-        return web.Response(body=m.render(), content_type="text/plain", charset="utf-8")
+        text = m.render()
+        if self.native is not None:
+            text += self.native.render_metrics()
+        return 200, PROM, text
 
-    @routes.get("/healthz")
-    async def healthz(_):
-        return web.Response(text="ok")
+    async def healthz(self, q, body):
+        return 200, TEXT, b"ok"
 
-    @routes.get("/readyz")
-    async def readyz(_):
-        if ready is not None and not ready.is_set():
-            return web.Response(status=503, text="informers not synced")
-        return web.Response(text="ok")
+    async def readyz(self, q, body):
+        if self.ready is not None and not self.ready.is_set():
+            return 503, TEXT, b"informers not synced"
+        return 200, TEXT, b"ok"
 
-    @routes.get("/debug/trace")
-    async def trace(request: web.Request):
-        limit = int(request.query.get("limit", "512"))
-        return web.json_response(ext.tracer.dump(limit, request.query.get("verb")), dumps=_dumps)
+    async def trace(self, q, body):
+        return 200, JSON, _dumps(self.ext.tracer.dump(int(q.get("limit", "512")), q.get("verb")))
 
-    @routes.get("/debug/stacks")
-    @routes.get("/debug/pprof/goroutine/")
-    async def stacks(_):
-        return web.Response(text=thread_stacks())
+    async def stacks(self, q, body):
+        return 200, TEXT, thread_stacks().encode()
 
-    @routes.get("/debug/profile")
-    @routes.get("/debug/pprof/profile/")
-    async def profile(request: web.Request):
-        secs = min(60.0, float(request.query.get("seconds", "5")))
-        loop = asyncio.get_running_loop()
-        text = await loop.run_in_executor(None, sample_profile, secs)
-        return web.Response(text=text)
+    async def profile(self, q, body):
+        secs = min(60.0, float(q.get("seconds", "5")))
+        text = await asyncio.get_running_loop().run_in_executor(None, sample_profile, secs)
+        return 200, TEXT, text.encode()
 
-    @routes.get("/debug/state")
-    async def state(_):
-        st = ext.state
-        return web.json_response({
-            "policy": st.policy, "compat": st.options.compat, "load_aware": st.options.load_aware,
-            "nodes": st.ledger.n_nodes, "pods": st.ledger.n_pods, "epoch": st.ledger.epoch,
-            "plan_cache": st.ledger.cache_size, "ledger_path": st.ledger.path, "ledger_bytes": st.ledger.bytes,
-            "pods_in_ledger": st.ledger.pods_on(-1)[:1000], "time": time.time()}, dumps=_dumps)
+    async def state(self, q, body):
+        st = self.ext.state
+        out = {"policy": st.policy, "compat": st.options.compat, "load_aware": st.options.load_aware,
+               "nodes": st.ledger.n_nodes, "pods": st.ledger.n_pods, "epoch": st.ledger.epoch,
+               "plan_cache": st.ledger.cache_size, "ledger_path": st.ledger.path, "ledger_bytes": st.ledger.bytes,
+               "pods_in_ledger": st.ledger.pods_on(-1)[:1000], "time": time.time()}
+        if self.native is not None:
+            out["native_frontend"] = self.native.fe.stats()
+        return 200, JSON, _dumps(out)
 
-    @routes.get("/debug/frag")
-    async def frag(request: web.Request):
-        return web.json_response(ext.state.frag(int(request.query.get("min_request", "0"))), dumps=_dumps)
+    async def frag(self, q, body):
+        return 200, JSON, _dumps(self.ext.state.frag(int(q.get("min_request", "0"))))
 
-    @routes.get("/debug/pprof/")
-    async def pprof_index(_):
-        return web.Response(text="goroutine/ profile/ (Python equivalents of the reference's pprof routes)\n")
+    async def pprof_index(self, q, body):
+        return 200, TEXT, b"goroutine/ profile/ (Python equivalents of the reference's pprof routes)\n"
+
+
+# ------------------------------------------------------------------------ aiohttp front door
+def make_app(ext: Extender, ready: asyncio.Event | None = None, extra_status=None,
+             router: Router | None = None) -> web.Application:
+    router = router or Router(ext, ready, extra_status)
+
+    async def handle(request: web.Request):
+        body = await request.read()
+        status, ctype, out = await router.dispatch(request.method, request.path, dict(request.query), body)
+        mime, _, cs = ctype.partition("; charset=")
+        return web.Response(status=status, body=out, content_type=mime.split(";")[0],
+                            charset=cs or None)
 
     app = web.Application(client_max_size=64 * 1024 * 1024)
-    app.add_routes(routes)
+    app.router.add_route("*", "/{tail:.*}", handle)
     app[EXTENDER_KEY] = ext
     return app
 
@@ -151,3 +185,77 @@ async def start(app: web.Application, host: str = "0.0.0.0", port: int = T.DEFAU
     await site.start()
     bound = site._server.sockets[0].getsockname()[1]  # type: ignore[union-attr]
     return runner, bound
+
+
+# ------------------------------------------------------------------------ native front door
+class NativeServer:
+    """C++ epoll front door (nanogpu._native.Frontend) bridged to the asyncio Router."""
+
+    def __init__(self, router: Router, host: str = "0.0.0.0", port: int = T.DEFAULT_PORT, threads: int = 2):
+        from ..native import core
+
+        self.router = router
+        st = router.ext.state
+        self.fe = core().Frontend(st.ledger, host, port, threads)
+        self.port = self.fe.port
+        self._tasks: set[asyncio.Task] = set()
+        self._loop: asyncio.AbstractEventLoop | None = None
+        router.native = self
+        st.add_listener(self.sync_options)
+        self.sync_options()
+
+    def sync_options(self) -> None:
+        st = self.router.ext.state
+        self.fe.set_options(st.options, bool(st.score_normalize))
+
+    def start(self) -> None:
+        self._loop = asyncio.get_running_loop()
+        self._loop.add_reader(self.fe.notify_fd(), self._drain)
+
+    def _drain(self) -> None:
+        for rid, method, path, query, body, pod_json, _t in self.fe.take():
+            if pod_json:
+                try:
+                    self.router.ext.pods.put(json.loads(pod_json))
+                except ValueError:
+                    pass
+            t = asyncio.ensure_future(self._one(rid, method, path, query, body))
+            self._tasks.add(t)
+            t.add_done_callback(self._tasks.discard)
+
+    async def _one(self, rid: int, method: str, path: str, query: str, body: bytes) -> None:
+        try:
+            q = {k: v[-1] for k, v in parse_qs(query).items()} if query else {}
+            status, ctype, out = await self.router.dispatch(method, path, q, body)
+        except Exception as e:  # never leave kube-scheduler hanging
+            log.exception("%s %s failed", method, path)
+            status, ctype, out = 500, JSON, _dumps({"Error": f"internal error: {e}"})
+        self.fe.respond(rid, status, ctype, out)
+
+    def render_metrics(self) -> bytes:
+        s = self.fe.stats()
+        lines = ["# HELP nanogpu_native_verb_total verbs answered by the native front door",
+                 "# TYPE nanogpu_native_verb_total counter"]
+        for verb in ("filter", "priorities"):
+            lines.append(f'nanogpu_native_verb_total{{verb="{verb}"}} {s[verb]["count"]}')
+        lines += ["# HELP nanogpu_native_verb_seconds_total time spent in native verbs",
+                  "# TYPE nanogpu_native_verb_seconds_total counter"]
+        for verb in ("filter", "priorities"):
+            lines.append(f'nanogpu_native_verb_seconds_total{{verb="{verb}"}} {s[verb]["seconds_total"]:.9f}')
+        lines += ["# HELP nanogpu_native_deferred_total requests handed to the Python runtime",
+                  "# TYPE nanogpu_native_deferred_total counter",
+                  f"nanogpu_native_deferred_total {s['python']['deferred']}",
+                  "# TYPE nanogpu_native_connections_total counter",
+                  f"nanogpu_native_connections_total {s['connections']}"]
+        return ("\n".join(lines) + "\n").encode()
+
+    async def stop(self) -> None:
+        if self._loop is not None:
+            self._loop.remove_reader(self.fe.notify_fd())
+        for t in list(self._tasks):
+            try:
+                await asyncio.wait_for(asyncio.shield(t), 2.0)
+            except (asyncio.TimeoutError, Exception):
+                pass
+        self.router.ext.state.remove_listener(self.sync_options)
+        await asyncio.get_running_loop().run_in_executor(None, self.fe.stop)

@@ -61,7 +61,8 @@ class ClusterState:
                  score_normalize: bool = False):
         self.ledger = N.Ledger(ledger_path, max_nodes, max_pods, True)
         self.track_hbm = track_hbm
-        self.score_normalize = score_normalize
+        self._listeners: list[Callable[[], None]] = []
+        self._score_normalize = bool(score_normalize)
         self.node_source = node_source
         self._nodes: dict[str, NodeEntry] = {}
         self._nodes_mu = threading.Lock()
@@ -70,6 +71,27 @@ class ClusterState:
         self.set_policy(policy, compat=compat, load_aware=load_aware, topo_weight=topo_weight, seed=seed)
 
     # ------------------------------------------------------------------ policy
+    def add_listener(self, fn: Callable[[], None]) -> None:
+        """Called after every policy / option change (the native front door mirrors them)."""
+        self._listeners.append(fn)
+
+    def remove_listener(self, fn: Callable[[], None]) -> None:
+        if fn in self._listeners:
+            self._listeners.remove(fn)
+
+    def _changed(self) -> None:
+        for fn in list(self._listeners):
+            fn()
+
+    @property
+    def score_normalize(self) -> bool:
+        return self._score_normalize
+
+    @score_normalize.setter
+    def score_normalize(self, v: bool) -> None:
+        self._score_normalize = bool(v)
+        self._changed()
+
     def set_policy(self, policy: str, compat: bool | None = None, load_aware: bool | None = None,
                    topo_weight: float | None = None, seed: int | None = None) -> None:
         if policy not in POLICY_ENUM:
@@ -82,6 +104,7 @@ class ClusterState:
             load_aware=bool(load_aware if load_aware is not None else (old.load_aware if old else False)),
             topo_weight=float(topo_weight if topo_weight is not None else (old.topo_weight if old else 1.0)),
             seed=int(seed if seed is not None else (old.seed if old else 0)))
+        self._changed()
 
     # ------------------------------------------------------------------ nodes
     def register_node(self, node: dict) -> NodeEntry:

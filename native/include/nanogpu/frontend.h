@@ -1,0 +1,107 @@
+// Native HTTP front door of the extender: kube-scheduler's filter / priorities verbs are
+// answered entirely in C++ (epoll workers, no GIL, no Python objects), everything else
+// (bind, /status, /metrics, /debug/*, and any request the fast path declines) is handed
+// to the Python asyncio runtime through a queue + eventfd and answered when it responds.
+//
+// Reference: pkg/routes/routes.go:40-122 (filter / prioritize routes) with the verbs of
+// pkg/scheduler/predicate.go:19-41 and priority.go:19-42 over dealer.go:89-153. The
+// reference serves every verb through net/http goroutines that all contend on the
+// dealer's one mutex; here N SO_REUSEPORT workers each own their connections and read
+// the ledger through per-node snapshots and its (node, generation)-keyed plan cache.
+// Responses are byte-identical to the Python verbs (nanogpu/extender/verbs.py), which
+// remain the fallback and the reference implementation for the tests.
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "nanogpu/alloc.h"
+#include "nanogpu/ledger.h"
+
+namespace nanogpu {
+
+// Kubernetes resource.Quantity -> int64 rounded up (Quantity.Value()); false if invalid
+// or out of range. `mib` = memory semantics: a bare integer is MiB, anything else is
+// bytes rounded up to MiB (nanogpu/k8s/quantity.py::quantity_to_mib).
+bool quantity_value(std::string_view s, bool mib, int64_t* out);
+
+struct PyRequest {
+  uint64_t id;
+  std::string method, path, query, body;
+  std::string pod_json;   // bind: the Pod seen by filter/prioritize for this UID ("" if none)
+  double t_arrival;
+};
+
+struct VerbStats {
+  std::atomic<uint64_t> count{0}, errors{0}, deferred{0};
+  std::atomic<uint64_t> ns_total{0};
+  std::atomic<uint64_t> buckets[16];   // latency histogram, bucket k: < 2^k * 8 us
+  VerbStats() {
+    for (auto& b : buckets) b.store(0);
+  }
+  void observe(uint64_t ns);
+};
+
+class Frontend {
+ public:
+  Frontend(std::shared_ptr<Ledger> ledger, const std::string& host, int port, int threads);
+  ~Frontend();
+  Frontend(const Frontend&) = delete;
+  Frontend& operator=(const Frontend&) = delete;
+
+  int port() const { return port_; }
+  int notify_fd() const { return py_efd_; }
+  void set_options(const Options& o, bool score_normalize);
+  // Drains requests waiting for Python (non-blocking).
+  std::vector<PyRequest> take();
+  // Completes request `id` (any thread). Unknown ids (connection gone) are dropped.
+  void respond(uint64_t id, int status, const std::string& content_type, const std::string& body);
+  void stop();
+
+  VerbStats filter_stats, prio_stats, py_stats;
+  std::atomic<uint64_t> connections{0}, requests{0};
+  size_t pod_cache_size() const;
+
+ private:
+  struct Conn;
+  struct Worker;
+  void run(Worker* w);
+  void on_readable(Worker* w, Conn* c);
+  void process(Worker* w, Conn* c);
+  bool handle_native(Worker* w, Conn* c, const std::string& method, const std::string& path,
+                     std::string_view body, std::string* out);
+  bool filter_verb(std::string_view body, bool prioritize, std::string* out);
+  void defer(Worker* w, Conn* c, std::string method, std::string path, std::string query, std::string body);
+  void flush(Worker* w, Conn* c);
+  void close_conn(Worker* w, Conn* c);
+  void put_pod(std::string_view uid, std::string_view raw);
+  std::string pod_for_bind(std::string_view body);
+
+  std::shared_ptr<Ledger> ledger_;
+  int port_ = 0;
+  int py_efd_ = -1;
+  std::atomic<bool> stop_{false};
+  std::vector<std::unique_ptr<Worker>> workers_;
+
+  mutable std::mutex opt_mu_;
+  Options opt_;
+  bool normalize_ = false;
+
+  std::mutex py_mu_;
+  std::deque<PyRequest> py_q_;
+
+  mutable std::mutex pod_mu_;
+  std::unordered_map<std::string, std::string> pods_;
+  std::deque<std::string> pod_order_;
+  size_t pod_cap_ = 16384;
+};
+
+}  // namespace nanogpu

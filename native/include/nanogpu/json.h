@@ -1,0 +1,62 @@
+// Minimal JSON DOM for the extender's request path (no external library in the image).
+//
+// Parses one document into a flat node array: objects/arrays link their children through
+// `first`/`next`, strings are unescaped into one arena, and every value remembers its byte
+// span in the source so the raw Pod object can be cached for bind without re-encoding.
+// Depth is bounded; any syntax error fails the whole parse (the caller then hands the
+// request to the Python path, which produces the reference's error message).
+#pragma once
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <string_view>
+#include <vector>
+
+namespace nanogpu::json {
+
+enum class Type : uint8_t { kNull, kBool, kNum, kStr, kArr, kObj };
+
+struct Node {
+  Type type = Type::kNull;
+  bool b = false;
+  int32_t first = -1;     // first child (arrays / objects)
+  int32_t next = -1;      // next sibling
+  int32_t count = 0;      // children
+  uint32_t key_off = 0, key_len = 0;  // member key (into arena), objects' children only
+  uint32_t str_off = 0, str_len = 0;  // string value (arena) or number text (source)
+  uint32_t src_begin = 0, src_end = 0;
+};
+
+class Doc {
+ public:
+  bool parse(std::string_view src);
+  const Node& at(int32_t i) const { return nodes_[i]; }
+  int32_t root() const { return nodes_.empty() ? -1 : 0; }
+  std::string_view str(int32_t i) const {
+    const Node& n = nodes_[i];
+    return n.type == Type::kNum ? src_.substr(n.str_off, n.str_len) : std::string_view(arena_).substr(n.str_off, n.str_len);
+  }
+  std::string_view key(int32_t i) const { return std::string_view(arena_).substr(nodes_[i].key_off, nodes_[i].key_len); }
+  std::string_view raw(int32_t i) const { return src_.substr(nodes_[i].src_begin, nodes_[i].src_end - nodes_[i].src_begin); }
+  // Member lookup; `ci` = ASCII case-insensitive (Go encoding/json field matching).
+  int32_t get(int32_t obj, std::string_view k, bool ci = false) const;
+  bool is(int32_t i, Type t) const { return i >= 0 && nodes_[i].type == t; }
+  size_t size() const { return nodes_.size(); }
+
+ private:
+  int32_t value(int depth);
+  bool string(uint32_t* off, uint32_t* len);
+  void ws() {
+    while (p_ < src_.size() && (src_[p_] == ' ' || src_[p_] == '\n' || src_[p_] == '\r' || src_[p_] == '\t')) ++p_;
+  }
+  std::string_view src_;
+  size_t p_ = 0;
+  std::vector<Node> nodes_;
+  std::string arena_;
+};
+
+// Appends `s` as a JSON string literal (quotes included).
+void append_quoted(std::string* out, std::string_view s);
+
+}  // namespace nanogpu::json

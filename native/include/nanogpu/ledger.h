@@ -170,8 +170,17 @@ class Ledger {
     int32_t rc;
     Plan plan;
   };
-  mutable std::mutex cache_mu_;
-  std::unordered_map<CacheKey, CacheVal, CacheHash> cache_;
+  // Plan cache, sharded by node id so concurrent filters (native front-end workers) on
+  // different nodes never contend on one mutex.
+  static constexpr int kCacheShards = 64;
+  struct CacheShard {
+    std::mutex mu;
+    std::unordered_map<CacheKey, CacheVal, CacheHash> map;
+  };
+  mutable CacheShard cache_[kCacheShards];
+  CacheShard& cache_shard(int32_t node) const { return cache_[static_cast<uint32_t>(node) % kCacheShards]; }
+  bool cache_get(const CacheKey& k, int32_t* rc, Plan* plan) const;
+  void cache_put(const CacheKey& k, int32_t rc, const Plan& plan);
   mutable std::mutex names_mu_;
   mutable std::unordered_map<std::string, int32_t> names_;  // process-local name index
 };

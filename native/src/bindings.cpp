@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "nanogpu/alloc.h"
+#include "nanogpu/frontend.h"
 #include "nanogpu/gosort.h"
 #include "nanogpu/ledger.h"
 #include "nanogpu/topo.h"
@@ -430,5 +431,60 @@ PYBIND11_MODULE(_native, m) {
       py::arg("root") = "", py::arg("use_amdsmi") = true,
       "Reads KFD/DRM sysfs (+ libamd_smi) and returns the node GPU topology as JSON.");
   m.def("parse_properties", &parse_properties, "KFD `key value` properties text -> dict");
+  m.def(
+      "quantity_value",
+      [](const std::string& s, bool mib) -> py::object {
+        int64_t v;
+        if (!quantity_value(s, mib, &v)) return py::none();
+        return py::int_(v);
+      },
+      py::arg("text"), py::arg("mib") = false, "Native Quantity.Value() (None when the fast path declines).");
+  py::class_<Frontend, std::shared_ptr<Frontend>>(m, "Frontend")
+      .def(py::init<std::shared_ptr<Ledger>, const std::string&, int, int>(), py::arg("ledger"),
+           py::arg("host") = "0.0.0.0", py::arg("port") = 0, py::arg("threads") = 2)
+      .def_property_readonly("port", &Frontend::port)
+      .def("notify_fd", &Frontend::notify_fd)
+      .def("set_options", &Frontend::set_options, py::arg("options"), py::arg("score_normalize") = false)
+      .def("take",
+           [](Frontend& f) {
+             std::vector<PyRequest> v;
+             {
+               py::gil_scoped_release nogil;
+               v = f.take();
+             }
+             py::list out;
+             for (auto& r : v)
+               out.append(py::make_tuple(r.id, r.method, r.path, r.query, py::bytes(r.body), py::bytes(r.pod_json),
+                                         r.t_arrival));
+             return out;
+           })
+      .def("respond",
+           [](Frontend& f, uint64_t id, int status, const std::string& ctype, const py::bytes& body) {
+             std::string b = body;
+             py::gil_scoped_release nogil;
+             f.respond(id, status, ctype, b);
+           })
+      .def("stop", &Frontend::stop, py::call_guard<py::gil_scoped_release>())
+      .def("pod_cache_size", &Frontend::pod_cache_size)
+      .def("stats", [](Frontend& f) {
+        auto one = [](const VerbStats& s) {
+          py::dict d;
+          d["count"] = s.count.load();
+          d["errors"] = s.errors.load();
+          d["deferred"] = s.deferred.load();
+          d["seconds_total"] = static_cast<double>(s.ns_total.load()) * 1e-9;
+          py::list b;
+          for (const auto& x : s.buckets) b.append(x.load());
+          d["buckets_8us_pow2"] = b;
+          return d;
+        };
+        py::dict d;
+        d["filter"] = one(f.filter_stats);
+        d["priorities"] = one(f.prio_stats);
+        d["python"] = one(f.py_stats);
+        d["connections"] = f.connections.load();
+        d["requests"] = f.requests.load();
+        return d;
+      });
   m.def("mono_now", &mono_now);
 }

@@ -1,0 +1,736 @@
+// Native extender front door (see frontend.h).
+#include "nanogpu/frontend.h"
+
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+
+#include "nanogpu/json.h"
+
+namespace nanogpu {
+
+namespace {
+
+constexpr size_t kMaxHeader = 64 * 1024;
+constexpr size_t kMaxBody = 64u * 1024 * 1024;
+constexpr const char* kPercent = "nano-gpu/gpu-percent";
+constexpr const char* kMemory = "nano-gpu/gpu-memory";
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+uint64_t now_ns() {
+  return static_cast<uint64_t>(
+      std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count());
+}
+
+bool ieq(std::string_view a, std::string_view b) {
+  if (a.size() != b.size()) return false;
+  for (size_t i = 0; i < a.size(); ++i)
+    if (std::tolower(static_cast<unsigned char>(a[i])) != std::tolower(static_cast<unsigned char>(b[i]))) return false;
+  return true;
+}
+
+std::string_view trim(std::string_view s) {
+  while (!s.empty() && (s.front() == ' ' || s.front() == '\t')) s.remove_prefix(1);
+  while (!s.empty() && (s.back() == ' ' || s.back() == '\t' || s.back() == '\r')) s.remove_suffix(1);
+  return s;
+}
+
+const char* reason(int status) {
+  switch (status) {
+    case 200: return "OK";
+    case 400: return "Bad Request";
+    case 404: return "Not Found";
+    case 405: return "Method Not Allowed";
+    case 413: return "Payload Too Large";
+    case 500: return "Internal Server Error";
+    case 503: return "Service Unavailable";
+    default: return "Status";
+  }
+}
+
+using i128 = __int128;
+
+bool mul_ok(i128 a, i128 b, i128* out) { return !__builtin_mul_overflow(a, b, out); }
+
+bool pow10(int e, i128* out) {
+  i128 v = 1;
+  for (int i = 0; i < e; ++i)
+    if (!mul_ok(v, 10, &v)) return false;
+  *out = v;
+  return true;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------ quantity
+bool quantity_value(std::string_view s, bool mib, int64_t* out) {
+  s = trim(s);
+  while (!s.empty() && (s.back() == '\n')) s.remove_suffix(1);
+  if (s.empty()) return false;
+  bool bare = true;
+  for (char c : s)
+    if (c < '0' || c > '9') bare = false;
+  if (mib && bare) {
+    if (s.size() > 18) return false;
+    *out = std::strtoll(std::string(s).c_str(), nullptr, 10);
+    return true;
+  }
+  // [+-]?[0-9.]+ ([eE][+-]?[0-9]+)? suffix?
+  size_t p = 0;
+  bool neg = false;
+  if (s[p] == '+' || s[p] == '-') neg = s[p++] == '-';
+  i128 m = 0;
+  int frac = 0, ndig = 0;
+  bool dot = false, any = false;
+  for (; p < s.size() && ((s[p] >= '0' && s[p] <= '9') || s[p] == '.'); ++p) {
+    if (s[p] == '.') {
+      if (dot) return false;  // "1.2.3": Decimal rejects it too
+      dot = true;
+      continue;
+    }
+    any = true;
+    if (m == 0 && s[p] == '0') {
+      if (dot) ++frac;
+      continue;
+    }
+    if (++ndig > 30) return false;
+    m = m * 10 + (s[p] - '0');
+    if (dot) ++frac;
+  }
+  if (!any) return false;
+  int e10 = 0;
+  if (p < s.size() && (s[p] == 'e' || s[p] == 'E')) {
+    // "E" alone is the exa suffix; an exponent needs digits after it
+    size_t q = p + 1;
+    bool eneg = false;
+    if (q < s.size() && (s[q] == '+' || s[q] == '-')) eneg = s[q++] == '-';
+    if (q < s.size() && s[q] >= '0' && s[q] <= '9') {
+      int v = 0;
+      for (; q < s.size() && s[q] >= '0' && s[q] <= '9'; ++q) {
+        v = v * 10 + (s[q] - '0');
+        if (v > 60) return false;
+      }
+      e10 = eneg ? -v : v;
+      p = q;
+    }
+  }
+  const std::string_view suf = s.substr(p);
+  int bin = 0, dec = 0;
+  if (suf.empty()) {
+  } else if (suf == "Ki") bin = 10;
+  else if (suf == "Mi") bin = 20;
+  else if (suf == "Gi") bin = 30;
+  else if (suf == "Ti") bin = 40;
+  else if (suf == "Pi") bin = 50;
+  else if (suf == "Ei") bin = 60;
+  else if (suf == "n") dec = -9;
+  else if (suf == "u") dec = -6;
+  else if (suf == "m") dec = -3;
+  else if (suf == "k") dec = 3;
+  else if (suf == "M") dec = 6;
+  else if (suf == "G") dec = 9;
+  else if (suf == "T") dec = 12;
+  else if (suf == "P") dec = 15;
+  else if (suf == "E") dec = 18;
+  else return false;
+  if (neg && m != 0) {  // every caller clamps negatives to 0
+    *out = 0;
+    return true;
+  }
+  // value = m * 10^(e10 + dec - frac) * 2^bin ; result = ceil(value / (mib ? 2^20 : 1))
+  int e = e10 + dec - frac;
+  int b = bin - (mib ? 20 : 0);
+  i128 num = m, den = 1, t;
+  if (e > 0) {
+    if (!pow10(e, &t) || !mul_ok(num, t, &num)) return false;
+  } else if (e < 0) {
+    if (!pow10(-e, &den)) return false;
+  }
+  if (b > 0) {
+    if (!mul_ok(num, static_cast<i128>(1) << b, &num)) return false;
+  } else if (b < 0) {
+    if (!mul_ok(den, static_cast<i128>(1) << (-b), &den)) return false;
+  }
+  const i128 q = num / den + (num % den != 0 ? 1 : 0);
+  if (q > static_cast<i128>(INT64_MAX)) return false;
+  *out = static_cast<int64_t>(q);
+  return true;
+}
+
+void VerbStats::observe(uint64_t ns) {
+  count.fetch_add(1, std::memory_order_relaxed);
+  ns_total.fetch_add(ns, std::memory_order_relaxed);
+  uint64_t us8 = ns / 8000;
+  int k = 0;
+  while (us8 > 0 && k < 15) {
+    us8 >>= 1;
+    ++k;
+  }
+  buckets[k].fetch_add(1, std::memory_order_relaxed);
+}
+
+// ------------------------------------------------------------------------------ plumbing
+struct Frontend::Conn {
+  int fd = -1;
+  uint64_t id = 0;
+  std::string in, out;
+  size_t out_off = 0;
+  bool waiting = false;      // a request is with Python; later requests wait their turn
+  bool close_after = false;
+  bool want_out = false;
+};
+
+struct Frontend::Worker {
+  int idx = 0;
+  int lfd = -1, ep = -1, efd = -1;
+  std::thread th;
+  std::unordered_map<uint64_t, std::unique_ptr<Conn>> conns;   // by conn id
+  std::mutex mb_mu;
+  std::vector<std::pair<uint64_t, std::string>> mailbox;       // (conn id, response bytes)
+  uint64_t next_conn = 1;
+};
+
+static uint64_t make_id(int worker, uint64_t conn) { return (conn << 8) | static_cast<uint64_t>(worker); }
+
+Frontend::Frontend(std::shared_ptr<Ledger> ledger, const std::string& host, int port, int threads)
+    : ledger_(std::move(ledger)) {
+  if (!ledger_) throw std::invalid_argument("Frontend: ledger required");
+  if (threads < 1) threads = 1;
+  if (threads > 64) threads = 64;
+  py_efd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+  if (py_efd_ < 0) throw std::runtime_error("eventfd failed");
+  sockaddr_in addr{};
+  addr.sin_family = AF_INET;
+  addr.sin_port = htons(static_cast<uint16_t>(port));
+  if (host.empty() || host == "0.0.0.0") {
+    addr.sin_addr.s_addr = htonl(INADDR_ANY);
+  } else if (inet_pton(AF_INET, host.c_str(), &addr.sin_addr) != 1) {
+    throw std::invalid_argument("Frontend: host must be an IPv4 address");
+  }
+  for (int i = 0; i < threads; ++i) {
+    auto w = std::make_unique<Worker>();
+    w->idx = i;
+    w->lfd = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+    int one = 1;
+    setsockopt(w->lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    setsockopt(w->lfd, SOL_SOCKET, SO_REUSEPORT, &one, sizeof(one));
+    if (bind(w->lfd, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) != 0 || listen(w->lfd, 1024) != 0) {
+      const std::string err = std::strerror(errno);
+      close(w->lfd);
+      for (auto& o : workers_) close(o->lfd);
+      close(py_efd_);
+      throw std::runtime_error("Frontend: bind/listen failed: " + err);
+    }
+    if (i == 0) {
+      socklen_t len = sizeof(addr);
+      getsockname(w->lfd, reinterpret_cast<sockaddr*>(&addr), &len);
+      port_ = ntohs(addr.sin_port);
+    }
+    w->ep = epoll_create1(EPOLL_CLOEXEC);
+    w->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.u64 = 0;  // listen socket
+    epoll_ctl(w->ep, EPOLL_CTL_ADD, w->lfd, &ev);
+    ev.data.u64 = 1;  // mailbox
+    epoll_ctl(w->ep, EPOLL_CTL_ADD, w->efd, &ev);
+    workers_.push_back(std::move(w));
+  }
+  for (auto& w : workers_) w->th = std::thread([this, p = w.get()] { run(p); });
+}
+
+Frontend::~Frontend() { stop(); }
+
+void Frontend::stop() {
+  if (stop_.exchange(true)) return;
+  for (auto& w : workers_) {
+    uint64_t one = 1;
+    (void)!write(w->efd, &one, sizeof(one));
+  }
+  for (auto& w : workers_) {
+    if (w->th.joinable()) w->th.join();
+    for (auto& kv : w->conns) close(kv.second->fd);
+    w->conns.clear();
+    close(w->lfd);
+    close(w->ep);
+    close(w->efd);
+  }
+  if (py_efd_ >= 0) close(py_efd_);
+  py_efd_ = -1;
+}
+
+void Frontend::set_options(const Options& o, bool score_normalize) {
+  std::lock_guard<std::mutex> g(opt_mu_);
+  opt_ = o;
+  normalize_ = score_normalize;
+}
+
+std::vector<PyRequest> Frontend::take() {
+  uint64_t v;
+  (void)!read(py_efd_, &v, sizeof(v));
+  std::lock_guard<std::mutex> g(py_mu_);
+  std::vector<PyRequest> out(std::make_move_iterator(py_q_.begin()), std::make_move_iterator(py_q_.end()));
+  py_q_.clear();
+  return out;
+}
+
+void Frontend::respond(uint64_t id, int status, const std::string& content_type, const std::string& body) {
+  const int widx = static_cast<int>(id & 0xff);
+  if (widx < 0 || widx >= static_cast<int>(workers_.size())) return;
+  Worker* w = workers_[widx].get();
+  std::string r;
+  r.reserve(body.size() + 128);
+  r += "HTTP/1.1 " + std::to_string(status) + " " + reason(status) + "\r\nContent-Type: " + content_type +
+       "\r\nContent-Length: " + std::to_string(body.size()) + "\r\n\r\n";
+  r += body;
+  {
+    std::lock_guard<std::mutex> g(w->mb_mu);
+    w->mailbox.emplace_back(id >> 8, std::move(r));
+  }
+  uint64_t one = 1;
+  (void)!write(w->efd, &one, sizeof(one));
+}
+
+size_t Frontend::pod_cache_size() const {
+  std::lock_guard<std::mutex> g(pod_mu_);
+  return pods_.size();
+}
+
+void Frontend::put_pod(std::string_view uid, std::string_view raw) {
+  if (uid.empty()) return;
+  std::lock_guard<std::mutex> g(pod_mu_);
+  auto it = pods_.find(std::string(uid));
+  if (it != pods_.end()) {
+    it->second.assign(raw.data(), raw.size());
+    return;
+  }
+  pods_.emplace(std::string(uid), std::string(raw));
+  pod_order_.emplace_back(uid);
+  while (pods_.size() > pod_cap_ && !pod_order_.empty()) {
+    pods_.erase(pod_order_.front());
+    pod_order_.pop_front();
+  }
+}
+
+std::string Frontend::pod_for_bind(std::string_view body) {
+  json::Doc d;
+  if (!d.parse(body)) return {};
+  const int32_t u = d.get(d.root(), "PodUID", true);
+  if (!d.is(u, json::Type::kStr)) return {};
+  std::lock_guard<std::mutex> g(pod_mu_);
+  auto it = pods_.find(std::string(d.str(u)));
+  if (it == pods_.end()) return {};
+  std::string s = std::move(it->second);
+  pods_.erase(it);   // one bind per pod UID (the deque entry expires lazily)
+  return s;
+}
+
+// ------------------------------------------------------------------------------ event loop
+void Frontend::run(Worker* w) {
+  epoll_event evs[128];
+  while (!stop_.load(std::memory_order_acquire)) {
+    const int n = epoll_wait(w->ep, evs, 128, 200);
+    for (int i = 0; i < n; ++i) {
+      const uint64_t tag = evs[i].data.u64;
+      if (tag == 0) {
+        for (;;) {
+          const int fd = accept4(w->lfd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+          if (fd < 0) break;
+          int one = 1;
+          setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+          auto c = std::make_unique<Conn>();
+          c->fd = fd;
+          c->id = w->next_conn++;
+          epoll_event ev{};
+          ev.events = EPOLLIN | EPOLLRDHUP;
+          ev.data.u64 = (c->id << 1) | (1ull << 63);
+          epoll_ctl(w->ep, EPOLL_CTL_ADD, fd, &ev);
+          connections.fetch_add(1, std::memory_order_relaxed);
+          w->conns.emplace(c->id, std::move(c));
+        }
+      } else if (tag == 1) {
+        uint64_t v;
+        (void)!read(w->efd, &v, sizeof(v));
+        std::vector<std::pair<uint64_t, std::string>> mb;
+        {
+          std::lock_guard<std::mutex> g(w->mb_mu);
+          mb.swap(w->mailbox);
+        }
+        for (auto& m : mb) {
+          auto it = w->conns.find(m.first);
+          if (it == w->conns.end()) continue;
+          Conn* c = it->second.get();
+          c->out += m.second;
+          c->waiting = false;
+          flush(w, c);
+          if (w->conns.count(m.first)) process(w, c);
+        }
+      } else {
+        const uint64_t cid = (tag & ~(1ull << 63)) >> 1;
+        auto it = w->conns.find(cid);
+        if (it == w->conns.end()) continue;
+        Conn* c = it->second.get();
+        if (evs[i].events & (EPOLLERR | EPOLLHUP)) {
+          close_conn(w, c);
+          continue;
+        }
+        if (evs[i].events & EPOLLOUT) {
+          flush(w, c);
+          if (!w->conns.count(cid)) continue;
+        }
+        if (evs[i].events & (EPOLLIN | EPOLLRDHUP)) on_readable(w, c);
+      }
+    }
+  }
+}
+
+void Frontend::on_readable(Worker* w, Conn* c) {
+  char buf[65536];
+  bool eof = false;
+  for (;;) {
+    const ssize_t r = recv(c->fd, buf, sizeof(buf), 0);
+    if (r > 0) {
+      c->in.append(buf, static_cast<size_t>(r));
+      if (c->in.size() > kMaxBody + kMaxHeader) {
+        close_conn(w, c);
+        return;
+      }
+      continue;
+    }
+    if (r == 0) eof = true;
+    else if (errno == EINTR) continue;
+    else if (errno != EAGAIN && errno != EWOULDBLOCK) eof = true;
+    break;
+  }
+  const uint64_t id = c->id;
+  process(w, c);
+  if (!w->conns.count(id)) return;
+  if (eof && !c->waiting && c->out.size() == c->out_off) close_conn(w, c);
+  else if (eof) c->close_after = true;
+}
+
+void Frontend::process(Worker* w, Conn* c) {
+  const uint64_t id = c->id;
+  while (!c->waiting) {
+    const size_t he = c->in.find("\r\n\r\n");
+    if (he == std::string::npos) {
+      if (c->in.size() > kMaxHeader) close_conn(w, c);
+      return;
+    }
+    const std::string_view head(c->in.data(), he);
+    const size_t le = head.find("\r\n");
+    const std::string_view line = head.substr(0, le);
+    const size_t s1 = line.find(' '), s2 = line.rfind(' ');
+    if (s1 == std::string_view::npos || s2 == s1) {
+      close_conn(w, c);
+      return;
+    }
+    std::string method(line.substr(0, s1));
+    std::string target(line.substr(s1 + 1, s2 - s1 - 1));
+    const bool http10 = line.substr(s2 + 1) == "HTTP/1.0";
+    size_t clen = 0;
+    bool chunked = false, close = http10, keep = false;
+    size_t pos = le == std::string_view::npos ? head.size() : le + 2;
+    while (pos < head.size()) {
+      size_t e = head.find("\r\n", pos);
+      if (e == std::string_view::npos) e = head.size();
+      const std::string_view h = head.substr(pos, e - pos);
+      const size_t colon = h.find(':');
+      if (colon != std::string_view::npos) {
+        const std::string_view k = trim(h.substr(0, colon)), v = trim(h.substr(colon + 1));
+        if (ieq(k, "content-length")) {
+          clen = std::strtoull(std::string(v).c_str(), nullptr, 10);
+        } else if (ieq(k, "transfer-encoding")) {
+          chunked = v.find("chunked") != std::string_view::npos;
+        } else if (ieq(k, "connection")) {
+          if (ieq(v, "close")) close = true;
+          if (ieq(v, "keep-alive")) keep = true;
+        }
+      }
+      pos = e + 2;
+    }
+    if (http10 && keep) close = false;
+    std::string body;
+    size_t consumed;
+    if (chunked) {
+      size_t p = he + 4;
+      for (;;) {
+        const size_t le2 = c->in.find("\r\n", p);
+        if (le2 == std::string::npos) return;  // need more
+        const size_t n = std::strtoull(c->in.substr(p, le2 - p).c_str(), nullptr, 16);
+        if (c->in.size() < le2 + 2 + n + 2) return;
+        if (n == 0) {
+          // skip trailers up to the blank line
+          const size_t end = c->in.find("\r\n\r\n", le2);
+          if (end == std::string::npos) {
+            if (c->in.compare(le2, 4, "\r\n\r\n") != 0 && c->in.size() < le2 + 4) return;
+          }
+          consumed = (end == std::string::npos ? le2 + 2 : end + 4);
+          break;
+        }
+        body.append(c->in, le2 + 2, n);
+        if (body.size() > kMaxBody) {
+          close_conn(w, c);
+          return;
+        }
+        p = le2 + 2 + n + 2;
+      }
+    } else {
+      if (clen > kMaxBody) {
+        close_conn(w, c);
+        return;
+      }
+      if (c->in.size() < he + 4 + clen) return;  // need more
+      body.assign(c->in, he + 4, clen);
+      consumed = he + 4 + clen;
+    }
+    c->in.erase(0, consumed);
+    if (close) c->close_after = true;
+    requests.fetch_add(1, std::memory_order_relaxed);
+    std::string path = target, query;
+    const size_t qm = target.find('?');
+    if (qm != std::string::npos) {
+      path = target.substr(0, qm);
+      query = target.substr(qm + 1);
+    }
+    std::string out;
+    if (handle_native(w, c, method, path, body, &out)) {
+      c->out += out;
+      flush(w, c);
+      if (!w->conns.count(id)) return;
+    } else {
+      defer(w, c, std::move(method), std::move(path), std::move(query), std::move(body));
+    }
+  }
+}
+
+void Frontend::defer(Worker* w, Conn* c, std::string method, std::string path, std::string query, std::string body) {
+  PyRequest r;
+  r.id = make_id(w->idx, c->id);
+  if (method == "POST" && path == "/scheduler/bind") r.pod_json = pod_for_bind(body);
+  r.method = std::move(method);
+  r.path = std::move(path);
+  r.query = std::move(query);
+  r.body = std::move(body);
+  r.t_arrival = now_s();
+  c->waiting = true;
+  py_stats.deferred.fetch_add(1, std::memory_order_relaxed);
+  {
+    std::lock_guard<std::mutex> g(py_mu_);
+    py_q_.push_back(std::move(r));
+  }
+  uint64_t one = 1;
+  (void)!write(py_efd_, &one, sizeof(one));
+}
+
+void Frontend::flush(Worker* w, Conn* c) {
+  while (c->out_off < c->out.size()) {
+    const ssize_t n = send(c->fd, c->out.data() + c->out_off, c->out.size() - c->out_off, MSG_NOSIGNAL);
+    if (n > 0) {
+      c->out_off += static_cast<size_t>(n);
+      continue;
+    }
+    if (n < 0 && errno == EINTR) continue;
+    if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+      if (!c->want_out) {
+        epoll_event ev{};
+        ev.events = EPOLLIN | EPOLLRDHUP | EPOLLOUT;
+        ev.data.u64 = (c->id << 1) | (1ull << 63);
+        epoll_ctl(w->ep, EPOLL_CTL_MOD, c->fd, &ev);
+        c->want_out = true;
+      }
+      return;
+    }
+    close_conn(w, c);
+    return;
+  }
+  c->out.clear();
+  c->out_off = 0;
+  if (c->want_out) {
+    epoll_event ev{};
+    ev.events = EPOLLIN | EPOLLRDHUP;
+    ev.data.u64 = (c->id << 1) | (1ull << 63);
+    epoll_ctl(w->ep, EPOLL_CTL_MOD, c->fd, &ev);
+    c->want_out = false;
+  }
+  if (c->close_after && !c->waiting) close_conn(w, c);
+}
+
+void Frontend::close_conn(Worker* w, Conn* c) {
+  epoll_ctl(w->ep, EPOLL_CTL_DEL, c->fd, nullptr);
+  close(c->fd);
+  w->conns.erase(c->id);   // destroys c
+}
+
+// ------------------------------------------------------------------------------ verbs
+bool Frontend::handle_native(Worker* w, Conn* c, const std::string& method, const std::string& path,
+                             std::string_view body, std::string* out) {
+  (void)w;
+  (void)c;
+  if (method != "POST") return false;
+  const bool prio = path == "/scheduler/priorities";
+  if (!prio && path != "/scheduler/filter") return false;
+  const uint64_t t0 = now_ns();
+  std::string resp;
+  if (!filter_verb(body, prio, &resp)) return false;
+  (prio ? prio_stats : filter_stats).observe(now_ns() - t0);
+  *out = "HTTP/1.1 200 OK\r\nContent-Type: application/json; charset=utf-8\r\nContent-Length: " +
+         std::to_string(resp.size()) + "\r\n\r\n";
+  *out += resp;
+  return true;
+}
+
+bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* out) {
+  json::Doc d;
+  if (body.empty() || !d.parse(body)) return false;
+  const int32_t root = d.root();
+  if (!d.is(root, json::Type::kObj)) return false;
+  const int32_t names = d.get(root, "NodeNames", true);
+  if (!d.is(names, json::Type::kArr)) return false;     // null / Nodes-only: Python path
+  const int32_t pod = d.get(root, "Pod", true);
+  Demand dem;
+  std::memset(&dem, 0, sizeof(dem));
+  std::string_view uid;
+  if (pod >= 0 && !d.is(pod, json::Type::kNull)) {
+    if (!d.is(pod, json::Type::kObj)) return false;
+    const int32_t md = d.get(pod, "metadata");
+    if (md >= 0 && !d.is(md, json::Type::kNull)) {
+      if (!d.is(md, json::Type::kObj)) return false;
+      const int32_t u = d.get(md, "uid");
+      if (u >= 0) {
+        if (!d.is(u, json::Type::kStr)) return false;
+        uid = d.str(u);
+      }
+    }
+    const int32_t spec = d.get(pod, "spec");
+    int32_t cons = -1;
+    if (spec >= 0 && !d.is(spec, json::Type::kNull)) {
+      if (!d.is(spec, json::Type::kObj)) return false;
+      cons = d.get(spec, "containers");
+    }
+    if (cons >= 0 && !d.is(cons, json::Type::kNull)) {
+      if (!d.is(cons, json::Type::kArr)) return false;
+      if (d.at(cons).count > kMaxContainers) return false;
+      for (int32_t c = d.at(cons).first; c >= 0; c = d.at(c).next) {
+        if (!d.is(c, json::Type::kObj)) return false;
+        ContainerDemand& cd = dem.c[dem.n++];
+        const int32_t res = d.get(c, "resources");
+        int32_t lim = -1;
+        if (res >= 0 && !d.is(res, json::Type::kNull)) {
+          if (!d.is(res, json::Type::kObj)) return false;
+          lim = d.get(res, "limits");
+        }
+        if (lim >= 0 && !d.is(lim, json::Type::kNull)) {
+          if (!d.is(lim, json::Type::kObj)) return false;
+          for (int k = 0; k < 2; ++k) {
+            const int32_t q = d.get(lim, k == 0 ? kPercent : kMemory);
+            if (q < 0 || d.is(q, json::Type::kNull)) continue;
+            if (!d.is(q, json::Type::kStr) && !d.is(q, json::Type::kNum)) return false;
+            int64_t v;
+            if (!quantity_value(d.str(q), k == 1, &v)) return false;  // Python logs + treats as 0
+            if (k == 0) {
+              if (v > INT32_MAX) return false;
+              cd.pct = static_cast<int32_t>(v);
+            } else {
+              cd.mib = v;
+            }
+          }
+        }
+      }
+    }
+  }
+  // node ids: any unknown node goes to Python, which can register it from its informer
+  const int32_t nn = d.at(names).count;
+  std::vector<int32_t> ids;
+  std::vector<std::string_view> nv;
+  ids.reserve(nn);
+  nv.reserve(nn);
+  for (int32_t c = d.at(names).first; c >= 0; c = d.at(c).next) {
+    if (!d.is(c, json::Type::kStr)) return false;
+    const std::string_view name = d.str(c);
+    const int32_t id = ledger_->find_node(std::string(name));
+    if (id < 0) return false;
+    ids.push_back(id);
+    nv.push_back(name);
+  }
+  Options o;
+  bool normalize;
+  {
+    std::lock_guard<std::mutex> g(opt_mu_);
+    o = opt_;
+    normalize = normalize_;
+  }
+  if (pod >= 0 && !uid.empty()) put_pod(uid, d.raw(pod));
+  Plan p;
+  std::string& r = *out;
+  r.reserve(64 + 48 * static_cast<size_t>(nn));
+  if (!prioritize) {
+    std::string ok = "[", failed = "{";
+    bool first_ok = true, first_f = true;
+    std::string dstr;
+    for (int i = 0; i < dem.n; ++i) {
+      dstr += "(" + std::to_string(dem.c[i].pct);
+      if (dem.c[i].mib) dstr += "," + std::to_string(dem.c[i].mib) + "Mi";
+      dstr += ")";
+    }
+    for (size_t i = 0; i < ids.size(); ++i) {
+      const int32_t rc = ledger_->assume(ids[i], dem, o, &p);
+      if (rc == kOk) {
+        if (!first_ok) ok += ",";
+        json::append_quoted(&ok, nv[i]);
+        first_ok = false;
+      } else {
+        if (!first_f) failed += ",";
+        json::append_quoted(&failed, nv[i]);
+        failed += ":";
+        std::string msg = "can't allocate " + dstr + " on node " + std::string(nv[i]) + ": " + err_str(rc);
+        json::append_quoted(&failed, msg);
+        first_f = false;
+      }
+    }
+    ok += "]";
+    failed += "}";
+    r = "{\"Nodes\":null,\"NodeNames\":" + ok + ",\"FailedNodes\":" + failed + ",\"Error\":\"\"}";
+    return true;
+  }
+  std::vector<int32_t> scores(ids.size());
+  for (size_t i = 0; i < ids.size(); ++i) {
+    const int32_t rc = ledger_->assume(ids[i], dem, o, &p);
+    scores[i] = rc == kOk ? p.score : 0;
+  }
+  if (normalize && !scores.empty()) {
+    // nanogpu/state/cluster.py::_normalize (Python round(): half to even)
+    if (o.compat) {
+      int32_t lo = scores[0], hi = scores[0];
+      for (int32_t s : scores) lo = std::min(lo, s), hi = std::max(hi, s);
+      for (int32_t& s : scores)
+        s = hi == lo ? (hi > 0 ? 10 : 0) : static_cast<int32_t>(std::nearbyint(10.0 * (s - lo) / (hi - lo)));
+    } else {
+      for (int32_t& s : scores) s = std::max(0, std::min(10, static_cast<int32_t>(std::nearbyint(s / 10.0))));
+    }
+  }
+  r = "[";
+  for (size_t i = 0; i < ids.size(); ++i) {
+    if (i) r += ",";
+    r += "{\"Host\":";
+    json::append_quoted(&r, nv[i]);
+    r += ",\"Score\":" + std::to_string(scores[i]) + "}";
+  }
+  r += "]";
+  return true;
+}
+
+}  // namespace nanogpu

@@ -1,0 +1,244 @@
+// JSON DOM parser (see json.h).
+#include "nanogpu/json.h"
+
+namespace nanogpu::json {
+
+namespace {
+constexpr int kMaxDepth = 64;
+
+int hexval(char c) {
+  if (c >= '0' && c <= '9') return c - '0';
+  if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+  if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+  return -1;
+}
+
+void put_utf8(std::string* a, uint32_t cp) {
+  if (cp < 0x80) {
+    a->push_back(static_cast<char>(cp));
+  } else if (cp < 0x800) {
+    a->push_back(static_cast<char>(0xC0 | (cp >> 6)));
+    a->push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+  } else if (cp < 0x10000) {
+    a->push_back(static_cast<char>(0xE0 | (cp >> 12)));
+    a->push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
+    a->push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+  } else {
+    a->push_back(static_cast<char>(0xF0 | (cp >> 18)));
+    a->push_back(static_cast<char>(0x80 | ((cp >> 12) & 0x3F)));
+    a->push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
+    a->push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+  }
+}
+
+bool ieq(std::string_view a, std::string_view b) {
+  if (a.size() != b.size()) return false;
+  for (size_t i = 0; i < a.size(); ++i) {
+    char x = a[i], y = b[i];
+    if (x >= 'A' && x <= 'Z') x = static_cast<char>(x - 'A' + 'a');
+    if (y >= 'A' && y <= 'Z') y = static_cast<char>(y - 'A' + 'a');
+    if (x != y) return false;
+  }
+  return true;
+}
+}  // namespace
+
+bool Doc::parse(std::string_view src) {
+  src_ = src;
+  p_ = 0;
+  nodes_.clear();
+  arena_.clear();
+  nodes_.reserve(src.size() / 8 + 16);
+  arena_.reserve(src.size());
+  ws();
+  if (value(0) < 0) return false;
+  ws();
+  return p_ == src_.size();
+}
+
+bool Doc::string(uint32_t* off, uint32_t* len) {
+  if (p_ >= src_.size() || src_[p_] != '"') return false;
+  ++p_;
+  *off = static_cast<uint32_t>(arena_.size());
+  while (p_ < src_.size()) {
+    const char c = src_[p_++];
+    if (c == '"') {
+      *len = static_cast<uint32_t>(arena_.size() - *off);
+      return true;
+    }
+    if (static_cast<unsigned char>(c) < 0x20) return false;
+    if (c != '\\') {
+      arena_.push_back(c);
+      continue;
+    }
+    if (p_ >= src_.size()) return false;
+    const char e = src_[p_++];
+    switch (e) {
+      case '"': arena_.push_back('"'); break;
+      case '\\': arena_.push_back('\\'); break;
+      case '/': arena_.push_back('/'); break;
+      case 'b': arena_.push_back('\b'); break;
+      case 'f': arena_.push_back('\f'); break;
+      case 'n': arena_.push_back('\n'); break;
+      case 'r': arena_.push_back('\r'); break;
+      case 't': arena_.push_back('\t'); break;
+      case 'u': {
+        auto hex4 = [&](uint32_t* v) {
+          if (p_ + 4 > src_.size()) return false;
+          *v = 0;
+          for (int i = 0; i < 4; ++i) {
+            const int h = hexval(src_[p_ + i]);
+            if (h < 0) return false;
+            *v = (*v << 4) | static_cast<uint32_t>(h);
+          }
+          p_ += 4;
+          return true;
+        };
+        uint32_t cp;
+        if (!hex4(&cp)) return false;
+        if (cp >= 0xD800 && cp < 0xDC00 && p_ + 1 < src_.size() && src_[p_] == '\\' && src_[p_ + 1] == 'u') {
+          p_ += 2;
+          uint32_t lo;
+          if (!hex4(&lo)) return false;
+          if (lo >= 0xDC00 && lo < 0xE000) {
+            cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+          } else {
+            put_utf8(&arena_, 0xFFFD);
+            cp = lo;
+          }
+        }
+        put_utf8(&arena_, cp);
+        break;
+      }
+      default:
+        return false;
+    }
+  }
+  return false;
+}
+
+int32_t Doc::value(int depth) {
+  if (depth > kMaxDepth || p_ >= src_.size()) return -1;
+  const int32_t idx = static_cast<int32_t>(nodes_.size());
+  nodes_.emplace_back();
+  nodes_[idx].src_begin = static_cast<uint32_t>(p_);
+  const char c = src_[p_];
+  if (c == '{' || c == '[') {
+    const bool obj = c == '{';
+    nodes_[idx].type = obj ? Type::kObj : Type::kArr;
+    ++p_;
+    ws();
+    int32_t prev = -1;
+    if (p_ < src_.size() && src_[p_] == (obj ? '}' : ']')) {
+      ++p_;
+    } else {
+      for (;;) {
+        uint32_t koff = 0, klen = 0;
+        if (obj) {
+          if (!string(&koff, &klen)) return -1;
+          ws();
+          if (p_ >= src_.size() || src_[p_] != ':') return -1;
+          ++p_;
+          ws();
+        }
+        const int32_t child = value(depth + 1);
+        if (child < 0) return -1;
+        nodes_[child].key_off = koff;
+        nodes_[child].key_len = klen;
+        if (prev < 0)
+          nodes_[idx].first = child;
+        else
+          nodes_[prev].next = child;
+        prev = child;
+        nodes_[idx].count += 1;
+        ws();
+        if (p_ >= src_.size()) return -1;
+        if (src_[p_] == ',') {
+          ++p_;
+          ws();
+          continue;
+        }
+        if (src_[p_] == (obj ? '}' : ']')) {
+          ++p_;
+          break;
+        }
+        return -1;
+      }
+    }
+  } else if (c == '"') {
+    nodes_[idx].type = Type::kStr;
+    uint32_t off, len;
+    if (!string(&off, &len)) return -1;
+    nodes_[idx].str_off = off;
+    nodes_[idx].str_len = len;
+  } else if (c == 't' && src_.substr(p_, 4) == "true") {
+    nodes_[idx].type = Type::kBool;
+    nodes_[idx].b = true;
+    p_ += 4;
+  } else if (c == 'f' && src_.substr(p_, 5) == "false") {
+    nodes_[idx].type = Type::kBool;
+    p_ += 5;
+  } else if (c == 'n' && src_.substr(p_, 4) == "null") {
+    nodes_[idx].type = Type::kNull;
+    p_ += 4;
+  } else if (c == '-' || (c >= '0' && c <= '9')) {
+    nodes_[idx].type = Type::kNum;
+    const size_t b = p_;
+    if (src_[p_] == '-') ++p_;
+    bool digits = false;
+    while (p_ < src_.size()) {
+      const char d = src_[p_];
+      if ((d >= '0' && d <= '9')) {
+        digits = true;
+      } else if (!(d == '.' || d == 'e' || d == 'E' || d == '+' || d == '-')) {
+        break;
+      }
+      ++p_;
+    }
+    if (!digits) return -1;
+    nodes_[idx].str_off = static_cast<uint32_t>(b);
+    nodes_[idx].str_len = static_cast<uint32_t>(p_ - b);
+  } else {
+    return -1;
+  }
+  nodes_[idx].src_end = static_cast<uint32_t>(p_);
+  return idx;
+}
+
+int32_t Doc::get(int32_t obj, std::string_view k, bool ci) const {
+  if (obj < 0 || nodes_[obj].type != Type::kObj) return -1;
+  int32_t found = -1;
+  for (int32_t c = nodes_[obj].first; c >= 0; c = nodes_[c].next) {
+    const std::string_view ck = key(c);
+    if (ck == k) return c;  // an exact match wins (Go prefers it as well)
+    if (ci && found < 0 && ieq(ck, k)) found = c;
+  }
+  return found;
+}
+
+void append_quoted(std::string* out, std::string_view s) {
+  out->push_back('"');
+  for (const char c : s) {
+    switch (c) {
+      case '"': out->append("\\\""); break;
+      case '\\': out->append("\\\\"); break;
+      case '\n': out->append("\\n"); break;
+      case '\r': out->append("\\r"); break;
+      case '\t': out->append("\\t"); break;
+      case '\b': out->append("\\b"); break;
+      case '\f': out->append("\\f"); break;
+      default:
+        if (static_cast<unsigned char>(c) < 0x20) {
+          static const char* hex = "0123456789abcdef";
+          out->append("\\u00");
+          out->push_back(hex[(c >> 4) & 0xF]);
+          out->push_back(hex[c & 0xF]);
+        } else {
+          out->push_back(c);
+        }
+    }
+  }
+  out->push_back('"');
+}
+
+}  // namespace nanogpu::json

@@ -354,24 +354,35 @@ uint64_t Ledger::generation(int32_t id) const {
   return n ? n->generation.load(std::memory_order_acquire) : 0;
 }
 
+bool Ledger::cache_get(const CacheKey& k, int32_t* rc, Plan* plan) const {
+  CacheShard& sh = cache_shard(k.node);
+  std::lock_guard<std::mutex> g(sh.mu);
+  auto it = sh.map.find(k);
+  if (it == sh.map.end()) return false;
+  *rc = it->second.rc;
+  *plan = it->second.plan;
+  return true;
+}
+
+void Ledger::cache_put(const CacheKey& k, int32_t rc, const Plan& plan) {
+  CacheShard& sh = cache_shard(k.node);
+  std::lock_guard<std::mutex> g(sh.mu);
+  if (sh.map.size() > 8192) sh.map.clear();
+  sh.map[k] = CacheVal{rc, plan};
+}
+
 int32_t Ledger::assume(int32_t id, const Demand& d, const Options& o, Plan* plan) {
+  // Fast path: the node's generation is read without copying its snapshot; a cached plan
+  // for (node, generation, demand, options) is exact for that generation.
+  NodeSlot* n = node(id);
+  if (!n || !n->in_use) return kErrUnknownNode;
+  const uint64_t dh = d.hash(), oh = o.hash();
+  int32_t rc;
+  if (cache_get(CacheKey{id, n->generation.load(std::memory_order_acquire), dh, oh}, &rc, plan)) return rc;
   NodeSnapshot snap;
   if (!snapshot(id, &snap)) return kErrUnknownNode;
-  const CacheKey k{id, snap.generation, d.hash(), o.hash()};
-  {
-    std::lock_guard<std::mutex> g(cache_mu_);
-    auto it = cache_.find(k);
-    if (it != cache_.end()) {
-      *plan = it->second.plan;
-      return it->second.rc;
-    }
-  }
-  const int32_t rc = choose(snap.devs, snap.n_devs, &snap.topo, d, o, plan);
-  {
-    std::lock_guard<std::mutex> g(cache_mu_);
-    if (cache_.size() > 262144) cache_.clear();
-    cache_[k] = CacheVal{rc, *plan};
-  }
+  rc = choose(snap.devs, snap.n_devs, &snap.topo, d, o, plan);
+  cache_put(CacheKey{id, snap.generation, dh, oh}, rc, *plan);
   return rc;
 }
 
@@ -396,17 +407,8 @@ int32_t Ledger::reserve(int32_t id, const std::string& key, const Demand& d, con
   }
   const uint64_t gen = n->generation.load(std::memory_order_relaxed);
   const CacheKey k{id, gen, d.hash(), o.hash()};
-  bool hit = false;
   int32_t rc = kOk;
-  {
-    std::lock_guard<std::mutex> g(cache_mu_);
-    auto it = cache_.find(k);
-    if (it != cache_.end()) {
-      hit = true;
-      rc = it->second.rc;
-      *plan = it->second.plan;
-    }
-  }
+  const bool hit = cache_get(k, &rc, plan);
   if (!hit) rc = choose(n->devs, n->n_devs, &n->topo, d, o, plan);
   if (rc != kOk) return rc;
   rc = apply(n->devs, n->n_devs, d, *plan);
@@ -599,13 +601,19 @@ FragStats Ledger::frag(int32_t min_request) const {
 }
 
 void Ledger::clear_cache() {
-  std::lock_guard<std::mutex> g(cache_mu_);
-  cache_.clear();
+  for (auto& sh : cache_) {
+    std::lock_guard<std::mutex> g(sh.mu);
+    sh.map.clear();
+  }
 }
 
 size_t Ledger::cache_size() const {
-  std::lock_guard<std::mutex> g(cache_mu_);
-  return cache_.size();
+  size_t n = 0;
+  for (auto& sh : cache_) {
+    std::lock_guard<std::mutex> g(sh.mu);
+    n += sh.map.size();
+  }
+  return n;
 }
 
 }  // namespace nanogpu

@@ -1,0 +1,234 @@
+"""Native C++ front door (native/src/frontend.cpp) against the Python verbs.
+
+The Python Extender is the specification: for every request the native fast path
+answers, the response bytes must equal `json.dumps(<python verb>(body))`; everything the
+fast path declines (bind, ops routes, Nodes-only filters, unknown nodes, malformed JSON)
+must come back from Python through the eventfd bridge, in order, on the same connection.
+"""
+import asyncio
+import json
+import random
+import socket
+
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from nanogpu import _native as N
+from nanogpu import types as T
+from nanogpu.app import Config, Runtime
+from nanogpu.k8s import podutil as pu
+from nanogpu.k8s.fake_apiserver import FakeKubeStore, InProcKube
+from nanogpu.k8s.quantity import QuantityError, quantity_to_mib, quantity_value
+from nanogpu.topology.model import synthetic_mi355x
+
+
+def _dumps(o) -> bytes:
+    return json.dumps(o, separators=(",", ":")).encode()
+
+
+async def _runtime(n_nodes=4, partition="SPX", **kw):
+    store = FakeKubeStore()
+    for i in range(n_nodes):
+        devs = 8 * {"SPX": 1, "CPX": 8}[partition]
+        store.add_node(pu.make_node(f"n{i}", devs, synthetic_mi355x(8, partition).to_json()))
+    rt = Runtime(Config(port=0, host="127.0.0.1", policy_config_path="/nonexistent", **kw), api=InProcKube(store))
+    await rt.start()
+    assert rt.native is not None
+    return store, rt
+
+
+def _http(port: int, reqs: list[tuple[str, str, bytes]], chunked: bool = False) -> list[tuple[int, bytes]]:
+    """Sends all requests on ONE keep-alive connection (pipelined), returns (status, body)."""
+    s = socket.create_connection(("127.0.0.1", port))
+    out = b""
+    for method, path, body in reqs:
+        if chunked and body:
+            mid = len(body) // 2
+            enc = b"".join(f"{len(p):x}\r\n".encode() + p + b"\r\n" for p in (body[:mid], body[mid:]) if p) + b"0\r\n\r\n"
+            out += f"{method} {path} HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n".encode() + enc
+        else:
+            out += f"{method} {path} HTTP/1.1\r\nHost: x\r\nContent-Length: {len(body)}\r\n\r\n".encode() + body
+    s.sendall(out)
+    res, buf = [], b""
+    s.settimeout(10)
+    while len(res) < len(reqs):
+        while b"\r\n\r\n" not in buf:
+            buf += s.recv(65536)
+        head, _, rest = buf.partition(b"\r\n\r\n")
+        status = int(head.split(b" ")[1])
+        clen = int([h.split(b":")[1] for h in head.split(b"\r\n") if h.lower().startswith(b"content-length")][0])
+        while len(rest) < clen:
+            rest += s.recv(65536)
+        res.append((status, rest[:clen]))
+        buf = rest[clen:]
+    s.close()
+    return res
+
+
+def _pods(rng, n):
+    out = []
+    for i in range(n):
+        cs = [(f"c{k}", rng.choice([0, 5, 10, 25, 50, 100, 200]), rng.choice([0, 0, 8192, 65536]))
+              for k in range(rng.choice([1, 1, 2, 3]))]
+        out.append(pu.make_pod(f"p{i}", cs))
+    return out
+
+
+@pytest.mark.parametrize("policy,partition,normalize", [("binpack", "SPX", False), ("spread", "CPX", True),
+                                                        ("random", "SPX", False), ("firstfit", "SPX", True)])
+def test_native_filter_and_priorities_are_byte_identical(policy, partition, normalize):
+    async def main():
+        store, rt = await _runtime(4, partition, priority=policy, score_normalize=normalize)
+        ext = rt.extender
+        rng = random.Random(7)
+        names = [f"n{i}" for i in range(4)]
+        loop = asyncio.get_running_loop()
+        try:
+            for k, pod in enumerate(_pods(rng, 40)):
+                pod = store.create_pod(pod)
+                body = {"Pod": pod, "Nodes": None, "NodeNames": rng.sample(names, rng.randint(1, 4))}
+                raw = _dumps(body)
+                got = await loop.run_in_executor(None, _http, rt.bound_port,
+                                                 [("POST", "/scheduler/filter", raw),
+                                                  ("POST", "/scheduler/priorities", raw)])
+                assert got[0] == (200, _dumps(ext.filter(json.loads(raw)))), got[0]
+                assert got[1] == (200, _dumps(ext.prioritize(json.loads(raw)))), got[1]
+                fit = json.loads(got[0][1])["NodeNames"]
+                if fit and k % 2 == 0:   # change state between requests
+                    m = pu.meta(pod)
+                    r = await ext.bind({"PodName": m["name"], "PodNamespace": m["namespace"],
+                                        "PodUID": m["uid"], "Node": fit[0]})
+                    assert r["Error"] == ""
+            st_ = rt.native.fe.stats()
+            assert st_["filter"]["count"] == 40 and st_["priorities"]["count"] == 40
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
+
+
+def test_deferred_routes_keep_order_on_one_connection():
+    async def main():
+        store, rt = await _runtime(2)
+        loop = asyncio.get_running_loop()
+        try:
+            pod = store.create_pod(pu.make_pod("a", [("main", 20)]))
+            m = pu.meta(pod)
+            f = _dumps({"Pod": pod, "NodeNames": ["n0", "n1"]})
+            node_objs = _dumps({"Pod": pod, "Nodes": {"items": [store.get_node("n0")]}, "NodeNames": None})
+            bind = _dumps({"PodName": "a", "PodNamespace": "default", "PodUID": m["uid"], "Node": "n0"})
+            reqs = [("POST", "/scheduler/filter", f),            # native
+                    ("POST", "/scheduler/filter", node_objs),    # Python (Nodes-only)
+                    ("POST", "/scheduler/priorities", f),        # native, queued behind Python
+                    ("POST", "/scheduler/bind", bind),           # Python, pod from the native cache
+                    ("GET", "/version", b""),
+                    ("POST", "/scheduler/filter", b"{nope"),     # Python error format
+                    ("POST", "/scheduler/priorities", b"{nope"), # 400
+                    ("GET", "/nothing", b""),
+                    ("GET", "/scheduler/filter", b""),           # 405
+                    ("GET", "/metrics", b"")]
+            res = await loop.run_in_executor(None, _http, rt.bound_port, reqs)
+            assert res[0][0] == 200 and json.loads(res[0][1])["NodeNames"] == ["n0", "n1"]
+            assert [pu.meta(n)["name"] for n in json.loads(res[1][1])["Nodes"]["items"]] == ["n0"]
+            assert [h["Host"] for h in json.loads(res[2][1])] == ["n0", "n1"]
+            assert res[3] == (200, b'{"Error":""}')
+            assert res[4] == (200, T.VERSION.encode())
+            assert res[5][0] == 200 and json.loads(res[5][1])["Error"]
+            assert res[6][0] == 400
+            assert res[7][0] == 404 and res[8][0] == 405
+            assert b'nanogpu_native_verb_total{verb="filter"}' in res[9][1]
+            # the bind used the pod cached by the native filter: no GET
+            assert store.counts.get("get_pod", 0) == 0
+            assert store.get_pod("default", "a")["spec"]["nodeName"] == "n0"
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
+
+
+def test_chunked_body_and_unknown_node_registration():
+    async def main():
+        store, rt = await _runtime(1)
+        loop = asyncio.get_running_loop()
+        try:
+            pod = store.create_pod(pu.make_pod("a", [("main", 30)]))
+            raw = _dumps({"Pod": pod, "NodeNames": ["n0"]})
+            res = await loop.run_in_executor(None, lambda: _http(rt.bound_port, [("POST", "/scheduler/filter", raw)],
+                                                                  chunked=True))
+            assert json.loads(res[0][1])["NodeNames"] == ["n0"]
+            # a node the ledger has not seen yet: Python registers it from the informer
+            store.add_node(pu.make_node("late", 8, synthetic_mi355x(8).to_json()))
+            await asyncio.sleep(0.05)
+            raw = _dumps({"Pod": pod, "NodeNames": ["late", "ghost"]})
+            res = await loop.run_in_executor(None, _http, rt.bound_port, [("POST", "/scheduler/filter", raw)])
+            body = json.loads(res[0][1])
+            assert body["NodeNames"] == ["late"] and "ghost" in body["FailedNodes"]
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
+
+
+def test_concurrent_clients_hammer_native_path():
+    async def main():
+        store, rt = await _runtime(8)
+        loop = asyncio.get_running_loop()
+        pods = [store.create_pod(pu.make_pod(f"p{i}", [("c", 10)])) for i in range(16)]
+        names = [f"n{i}" for i in range(8)]
+
+        def client(k):
+            reqs = [("POST", "/scheduler/filter", _dumps({"Pod": pods[(k + j) % 16], "NodeNames": names}))
+                    for j in range(50)]
+            return _http(rt.bound_port, reqs)
+
+        try:
+            outs = await asyncio.gather(*[loop.run_in_executor(None, client, k) for k in range(8)])
+            for out in outs:
+                assert all(s == 200 and json.loads(b)["NodeNames"] == names for s, b in out)
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
+
+
+def test_policy_reload_reaches_native_path():
+    async def main():
+        store, rt = await _runtime(2)
+        loop = asyncio.get_running_loop()
+        try:
+            pod = store.create_pod(pu.make_pod("a", [("main", 20)]))
+            raw = _dumps({"Pod": pod, "NodeNames": ["n0", "n1"]})
+            a = await loop.run_in_executor(None, _http, rt.bound_port, [("POST", "/scheduler/priorities", raw)])
+            rt.state.set_policy("spread", compat=True)
+            rt.state.score_normalize = True
+            b = await loop.run_in_executor(None, _http, rt.bound_port, [("POST", "/scheduler/priorities", raw)])
+            assert a[0][1] != b[0][1]
+            assert b[0][1] == _dumps(rt.extender.prioritize(json.loads(raw)))
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
+
+
+_q = st.one_of(
+    st.integers(0, 10 ** 6).map(str),
+    st.builds(lambda a, b, s: f"{a}.{b}{s}", st.integers(0, 999), st.integers(0, 999),
+              st.sampled_from(["", "m", "k", "M", "G", "Ki", "Mi", "Gi", "u", "n", "E"])),
+    st.builds(lambda a, e: f"{a}e{e}", st.integers(0, 99), st.integers(-5, 8)),
+    st.builds(lambda a, s: f"{a}{s}", st.integers(0, 10 ** 5), st.sampled_from(["Ki", "Mi", "Gi", "Ti", "m", "k"])),
+)
+
+
+@settings(max_examples=400, deadline=None)
+@given(_q, st.booleans())
+def test_native_quantity_matches_python(q, mib):
+    got = N.quantity_value(q, mib)
+    try:
+        want = max(0, quantity_to_mib(q) if mib else quantity_value(q))
+    except QuantityError:
+        want = None
+    if got is None:
+        assert want is None or want > 2 ** 62
+    else:
+        assert got == want, (q, mib)
