@@ -190,7 +190,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str) -> dict:
     from nanogpu.app import Config, Runtime
     from nanogpu.k8s import podutil as pu
     from nanogpu.k8s.fake_apiserver import Faults, FakeKubeStore, InProcKube
-    from nanogpu.sim.driver import HttpExtenderClient, SchedulerDriver, node_capacities
+    from nanogpu.sim.driver import FastExtenderClient, SchedulerDriver, node_capacities
 
     store = FakeKubeStore(faults=Faults(latency_s=args.api_rtt_ms / 1e3))
     topo_json = topo.to_json()
@@ -204,7 +204,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str) -> dict:
                  policy_config_path="/nonexistent/policy.yaml", reservation_ttl_s=3600)
     rt = Runtime(cfg, worker=0, api=InProcKube(store))
     await rt.start()
-    client = HttpExtenderClient(f"http://127.0.0.1:{rt.bound_port}", pool=args.inflight_binds + 8)
+    client = FastExtenderClient("127.0.0.1", rt.bound_port, pool=args.inflight_binds + 8)
     names = [pu.meta(n)["name"] for n in nodes]
     caps = node_capacities(nodes)
     api = InProcKube(store)

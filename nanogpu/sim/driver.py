@@ -57,6 +57,111 @@ class HttpExtenderClient:
             await self.s.close()
 
 
+class _HttpConn(asyncio.Protocol):
+    """One keep-alive HTTP/1.1 connection; responses resolve request futures in order."""
+
+    def __init__(self):
+        self.transport = None
+        self.buf = bytearray()
+        self.waiters: list[asyncio.Future] = []
+        self.closed = False
+
+    def connection_made(self, transport):
+        self.transport = transport
+
+    def connection_lost(self, exc):
+        self.closed = True
+        for w in self.waiters:
+            if not w.done():
+                w.set_exception(ConnectionError("connection lost"))
+        self.waiters.clear()
+
+    def data_received(self, data):
+        self.buf += data
+        while self.waiters:
+            he = self.buf.find(b"\r\n\r\n")
+            if he < 0:
+                return
+            head = bytes(self.buf[:he])
+            clen = 0
+            for line in head.split(b"\r\n")[1:]:
+                k, _, v = line.partition(b":")
+                if k.strip().lower() == b"content-length":
+                    clen = int(v)
+            if len(self.buf) < he + 4 + clen:
+                return
+            status = int(head[9:12])
+            body = bytes(self.buf[he + 4:he + 4 + clen])
+            del self.buf[:he + 4 + clen]
+            w = self.waiters.pop(0)
+            if not w.done():
+                w.set_result((status, body))
+
+
+class FastExtenderClient:
+    """Lean keep-alive client (asyncio.Protocol, no aiohttp) for driving an extender at
+    full speed: kube-scheduler's Go client costs microseconds per request, so the
+    stand-in should not be the bottleneck of an extender benchmark."""
+
+    def __init__(self, host: str, port: int, pool: int = 256):
+        self.host, self.port = host, port
+        self.pool = pool
+        self.idle: list[_HttpConn] = []
+        self.all: list[_HttpConn] = []
+        self._enc = json.JSONEncoder(separators=(",", ":"))
+        self._pod_json: dict[str, bytes] = {}
+
+    async def _conn(self) -> _HttpConn:
+        while self.idle:
+            c = self.idle.pop()
+            if not c.closed:
+                return c
+        loop = asyncio.get_running_loop()
+        _, c = await loop.create_connection(_HttpConn, self.host, self.port)
+        self.all.append(c)
+        return c
+
+    async def post(self, path: str, body: bytes) -> tuple[int, bytes]:
+        c = await self._conn()
+        fut = asyncio.get_running_loop().create_future()
+        c.waiters.append(fut)
+        c.transport.write(b"POST " + path.encode() + b" HTTP/1.1\r\nHost: extender\r\n"
+                          b"Content-Type: application/json\r\nContent-Length: " + str(len(body)).encode() +
+                          b"\r\n\r\n" + body)
+        try:
+            return await fut
+        finally:
+            if not c.closed:
+                self.idle.append(c)
+
+    def _args(self, body: dict) -> bytes:
+        pod = body.get("Pod")
+        uid = pu.pod_uid(pod) if pod else ""
+        pj = self._pod_json.get(uid) if uid else None
+        if pj is None:
+            pj = self._enc.encode(pod).encode()
+            if uid:
+                if len(self._pod_json) > 65536:
+                    self._pod_json.clear()
+                self._pod_json[uid] = pj
+        rest = {k: v for k, v in body.items() if k != "Pod"}
+        return b'{"Pod":' + pj + b"," + self._enc.encode(rest).encode()[1:]
+
+    async def filter(self, body):
+        return json.loads((await self.post("/scheduler/filter", self._args(body)))[1])
+
+    async def prioritize(self, body):
+        return json.loads((await self.post("/scheduler/priorities", self._args(body)))[1])
+
+    async def bind(self, body):
+        return json.loads((await self.post("/scheduler/bind", self._enc.encode(body).encode()))[1])
+
+    async def close(self):
+        for c in self.all:
+            if c.transport is not None:
+                c.transport.close()
+
+
 class InProcExtenderClient:
     def __init__(self, ext):
         self.ext = ext
@@ -240,7 +345,7 @@ class SchedulerDriver:
                 ok = False
                 try:
                     ok = await self.schedule_one(rec)
-                except (aiohttp.ClientError, asyncio.TimeoutError) as e:
+                except (aiohttp.ClientError, asyncio.TimeoutError, ConnectionError) as e:
                     rec.error = str(e)
                 if not ok:
                     if rec.attempts < self.max_attempts:
@@ -267,4 +372,4 @@ def node_capacities(nodes: list[dict]) -> dict[str, int]:
     return {pu.meta(n)["name"]: pu.node_capacity_percent(n) for n in nodes}
 
 
-__all__ = ["SchedulerDriver", "HttpExtenderClient", "InProcExtenderClient", "node_capacities", "T"]
+__all__ = ["SchedulerDriver", "HttpExtenderClient", "FastExtenderClient", "InProcExtenderClient", "node_capacities", "T"]

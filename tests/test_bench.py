@@ -1,0 +1,72 @@
+"""bench.py contract (single rank and a 2-rank gloo job) and the BASELINE config harness."""
+import asyncio
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _last_json(out: str) -> dict:
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out[-3000:]
+    return json.loads(lines[0])
+
+
+def test_bench_single_rank_cpu():
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--no-gpu", "--steps", "2", "--warmup", "1",
+                        "--pods", "200", "--nodes", "8"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["higher_is_better"] is True
+    assert d["scheduled"] == 400 and d["failed"] == 0 and d["value"] > 0
+    assert d["p50_bind_ms"] is not None and 0 <= d["frag_pct"] <= 100
+
+
+def test_bench_two_ranks_gloo():
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
+                        "--gpus", "2", "--no-gpu", "--steps", "2", "--warmup", "1", "--pods", "200", "--nodes", "8"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert d["n_gpus"] == 2 and d["scheduled"] == 400 and d["failed"] == 0
+    assert "2 extender worker" in d["config"]["parallelism"]
+
+
+def test_config_harness_plumbing_and_topology():
+    from nanogpu.sim import configs as C
+
+    async def main():
+        c1 = await C._both(C.config1)()
+        for k in ("ours", "reference_model"):
+            assert c1[k]["scheduled"] == 1 and c1[k]["placement"] == "0" and c1[k]["status_free"] == 80
+        c4 = await C._both(C.config4)()
+        o, f = c4["ours"], c4["reference_model"]
+        assert o["share_pod"]["distinct_gpus"] == 4
+        # the reference ignores links: it can put two ranks across the degraded GPU0-GPU1 link
+        assert o["share_pod"]["min_link_gbs"] >= f["share_pod"]["min_link_gbs"]
+        assert o["share_pod"]["min_link_gbs"] > 38.0
+        assert o["whole_gpu_group"]["scheduled"] == 1 and o["whole_gpu_group"]["min_link_gbs"] > 38.0
+        assert o["cpx_share_pod"]["distinct_gpus"] == 4
+        c2 = await C.config2(gpus=1)
+        assert c2["burst"]["scheduled"] == 5 and c2["hbm_probe"]["overcommitted_gib"] == 0
+        c2r = await C.config2(gpus=1, reference=True)
+        assert c2r["hbm_probe"]["overcommitted_gib"] > 0
+
+    asyncio.run(main())
