@@ -250,6 +250,10 @@ async def run_rank(d: Dist, args, topo, ledger_path: str) -> dict:
     results["elapsed_s"] = elapsed
     results["bind_ms"] = binds
     results["scheduled"] = sum(s["scheduled"] for s in results["steps"])
+    if rt.native is not None:
+        ns = rt.native.fe.stats()
+        results["native"] = {v: round(1e6 * ns[v]["seconds_total"] / max(1, ns[v]["count"]), 2)
+                             for v in ("filter", "priorities")}
     results["failed"] = sum(s["failed"] for s in results["steps"])
     await client.close()
     await rt.stop()
@@ -306,6 +310,7 @@ def main() -> int:
             "frag_hbm_pct": round(statistics.mean(f["frag_mib"] for f in fr), 3) if fr else None,
             "stranded_pct": round(statistics.mean(f["stranded_pct"] for f in fr), 3) if fr else None,
             "scheduled": scheduled, "failed": failed, "gpu": gpu_info,
+            "native_verb_mean_us": res.get("native"),
         }
         print(json.dumps(line), flush=True)
         if args.json_out:
