@@ -397,12 +397,75 @@ bool pick_group(Work& w, const Topology* t, int k, const Options& o, uint64_t rn
 
 }  // namespace
 
+// Greedy placement of every container (hardest first) on a working copy of the devices.
+// `forced` pins the first container to one device (-1 = free choice). `cost` accumulates
+// the policy's per-container keys (binpack: leftover percent; spread: minus free percent)
+// so whole-pod alternatives can be compared.
+struct Placement {
+  int16_t start[kMaxContainers], count[kMaxContainers];
+  int16_t idx[kMaxPlanIdx];
+  int total = 0;
+  int64_t cost = 0, cost_mib = 0;
+};
+
+static int32_t place_all(Work& w, const Topology* topo, const Demand& d, const Options& o, const int* order,
+                         int forced, Placement* pl) {
+  uint64_t rnd = mix64(o.seed ^ d.hash());
+  const bool spread = o.policy == Policy::kSpread;
+  for (int q = 0; q < d.n; ++q) {
+    const int c = order[q];
+    const ContainerDemand& cd = d.c[c];
+    const int need = devices_needed(cd);
+    rnd = mix64(rnd + static_cast<uint64_t>(q));
+    if (need == 0) {
+      if (pl->total >= kMaxPlanIdx) return kErrBadDemand;
+      pl->start[c] = static_cast<int16_t>(pl->total);
+      pl->count[c] = 1;
+      pl->idx[pl->total++] = kNotNeedGPU;
+      continue;
+    }
+    if (cd.pct > kPercentPerDevice && cd.pct % kPercentPerDevice != 0) return kErrBadDemand;
+    if (pl->total + need > kMaxPlanIdx) return kErrBadDemand;
+    pl->start[c] = static_cast<int16_t>(pl->total);
+    pl->count[c] = static_cast<int16_t>(need);
+    if (need == 1) {
+      int i;
+      if (q == 0 && forced >= 0) {
+        if (!share_fits(w.dev[forced], cd)) return kErrNoFit;
+        i = forced;
+      } else {
+        i = pick_share(w, topo, cd, o, rnd);
+      }
+      if (i < 0) return kErrNoFit;
+      const int64_t left = w.dev[i].pct_free - cd.pct;
+      pl->cost += spread ? -w.dev[i].pct_free : left;
+      if (w.dev[i].mib_total > 0 && cd.mib > 0)
+        pl->cost_mib += (spread ? -1 : 1) * (w.dev[i].mib_free - cd.mib) * 1000 / w.dev[i].mib_total;
+      w.dev[i].pct_free -= cd.pct;
+      if (w.dev[i].mib_total > 0) w.dev[i].mib_free -= cd.mib;
+      pl->idx[pl->total++] = static_cast<int16_t>(i);
+      w.chosen[w.n_chosen++] = static_cast<int16_t>(i);
+    } else {
+      int set[kMaxDevs];
+      if (!pick_group(w, topo, need, o, rnd, set)) return kErrNoFit;
+      for (int a = 0; a < need; ++a) {
+        Device& dv = w.dev[set[a]];
+        dv.pct_free = 0;
+        if (dv.mib_total > 0) dv.mib_free = 0;
+        pl->idx[pl->total++] = static_cast<int16_t>(set[a]);
+        w.chosen[w.n_chosen++] = static_cast<int16_t>(set[a]);
+      }
+    }
+  }
+  return kOk;
+}
+
 static int32_t native_choose(const Device* devs, int n, const Topology* topo, const Demand& d,
                              const Options& o, Plan* plan) {
-  Work w;
-  w.n = n;
-  w.n_chosen = 0;
-  std::memcpy(w.dev, devs, sizeof(Device) * n);
+  Work w0;
+  w0.n = n;
+  w0.n_chosen = 0;
+  std::memcpy(w0.dev, devs, sizeof(Device) * n);
 
   // Hardest first: whole-device groups, then larger shares, then HBM; stable on index.
   int order[kMaxContainers];
@@ -414,50 +477,49 @@ static int32_t native_choose(const Device* devs, int n, const Topology* topo, co
     return d.c[a].mib > d.c[b].mib;
   });
 
-  int16_t start[kMaxContainers], count[kMaxContainers];
-  int16_t tmp_idx[kMaxPlanIdx];
-  int total = 0;
-  uint64_t rnd = mix64(o.seed ^ d.hash());
-  for (int q = 0; q < d.n; ++q) {
-    const int c = order[q];
-    const ContainerDemand& cd = d.c[c];
-    const int need = devices_needed(cd);
-    rnd = mix64(rnd + static_cast<uint64_t>(q));
-    if (need == 0) {
-      if (total >= kMaxPlanIdx) return kErrBadDemand;
-      start[c] = static_cast<int16_t>(total);
-      count[c] = 1;
-      tmp_idx[total++] = kNotNeedGPU;
-      continue;
-    }
-    if (cd.pct > kPercentPerDevice && cd.pct % kPercentPerDevice != 0) return kErrBadDemand;
-    if (total + need > kMaxPlanIdx) return kErrBadDemand;
-    start[c] = static_cast<int16_t>(total);
-    count[c] = static_cast<int16_t>(need);
-    if (need == 1) {
-      const int i = pick_share(w, topo, cd, o, rnd);
-      if (i < 0) return kErrNoFit;
-      w.dev[i].pct_free -= cd.pct;
-      if (w.dev[i].mib_total > 0) w.dev[i].mib_free -= cd.mib;
-      tmp_idx[total++] = static_cast<int16_t>(i);
-      w.chosen[w.n_chosen++] = static_cast<int16_t>(i);
-    } else {
-      int set[kMaxDevs];
-      if (!pick_group(w, topo, need, o, rnd, set)) return kErrNoFit;
-      for (int a = 0; a < need; ++a) {
-        Device& dv = w.dev[set[a]];
-        dv.pct_free = 0;
-        if (dv.mib_total > 0) dv.mib_free = 0;
-        tmp_idx[total++] = static_cast<int16_t>(set[a]);
-        w.chosen[w.n_chosen++] = static_cast<int16_t>(set[a]);
+  // A pod whose containers land on several devices (TP/EP ranks, RCCL peers) is placed as
+  // a whole: every feasible device for its hardest single-device container is tried, the
+  // rest placed greedily, and the complete placements are ranked by the policy's summed
+  // keys, then by the set's topology score (partition siblings, min xGMI bandwidth, NUMA
+  // span). A greedy first pick alone would settle ties by device index and could split a
+  // group across sockets or over a degraded link.
+  int gpu_containers = 0;
+  for (int i = 0; i < d.n; ++i) gpu_containers += devices_needed(d.c[i]) > 0;
+  const bool joint = gpu_containers >= 2 && d.n > 0 && devices_needed(d.c[order[0]]) == 1 &&
+                     (o.policy == Policy::kBinpack || o.policy == Policy::kSpread) && o.topo_weight > 0.f;
+  Placement best;
+  int32_t best_rc = kErrNoFit;
+  if (!joint) {
+    Work w = w0;
+    best_rc = place_all(w, topo, d, o, order, -1, &best);
+  } else {
+    float best_topo = -1e30f;
+    for (int f = 0; f < n; ++f) {
+      if (!share_fits(w0.dev[f], d.c[order[0]])) continue;
+      Work w = w0;
+      Placement pl;
+      if (place_all(w, topo, d, o, order, f, &pl) != kOk) continue;
+      int set[kMaxPlanIdx];
+      int k = 0;
+      for (int a = 0; a < pl.total; ++a)
+        if (pl.idx[a] >= 0) set[k++] = pl.idx[a];
+      const float ts = group_score(w0, topo, set, k, o);
+      const bool better = best_rc != kOk || pl.cost < best.cost ||
+                          (pl.cost == best.cost && (pl.cost_mib < best.cost_mib ||
+                                                    (pl.cost_mib == best.cost_mib && ts > best_topo + 1e-4f)));
+      if (better) {
+        best = pl;
+        best_topo = ts;
+        best_rc = kOk;
       }
     }
   }
+  if (best_rc != kOk) return best_rc;
   plan_init(plan, d.n);
   int pos = 0;
   for (int c = 0; c < d.n; ++c) {
     plan->off[c] = static_cast<int16_t>(pos);
-    for (int a = 0; a < count[c]; ++a) plan->idx[pos++] = tmp_idx[start[c] + a];
+    for (int a = 0; a < best.count[c]; ++a) plan->idx[pos++] = best.idx[best.start[c] + a];
   }
   plan->off[d.n] = static_cast<int16_t>(pos);
   return kOk;

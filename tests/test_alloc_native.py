@@ -1,0 +1,120 @@
+"""Native (MI355X) placement mode of the C++ allocator: properties and topology behaviour.
+
+Compat mode is pinned bit-for-bit to the reference oracle in test_parity.py /
+test_alloc_golden.py; these tests pin what the native mode adds: the HBM dimension,
+partition / xGMI / NUMA-aware multi-container placement and the ledger invariants.
+"""
+import random
+
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from nanogpu import _native as N
+from nanogpu.topology.model import synthetic_mi355x
+
+BIN = N.Options(N.Policy.BINPACK)
+SPR = N.Options(N.Policy.SPREAD)
+
+
+def ledger_with(topo, n_nodes=1, track_hbm=True):
+    L = N.Ledger("", 16, 4096, True)
+    ids = [L.upsert_node(f"n{i}", topo.ledger_devices(track_hbm), topo.ledger_topo()) for i in range(n_nodes)]
+    return L, ids
+
+
+def devices_of(plan):
+    return [i for idx in plan for i in idx if i >= 0]
+
+
+def test_tp4_whole_gpus_stay_on_one_socket_and_fast_links():
+    t = synthetic_mi355x(8)
+    t.link_bw[0][1] = t.link_bw[1][0] = 38.0
+    L, (nid,) = ledger_with(t)
+    rc, _ = L.reserve(nid, "pre", [(50, 0)], BIN)       # GPU 0 half used
+    assert rc == N.OK
+    for opts in (BIN, SPR):
+        rc, plan, _ = L.assume(nid, [(100, 0)] * 4, opts)
+        assert rc == N.OK
+        gpus = {t.devices[i].gpu for i in devices_of(plan)}
+        assert gpus == {4, 5, 6, 7}, (opts, plan)       # NUMA 1, no degraded link
+
+
+def test_spread_share_pod_avoids_degraded_link():
+    t = synthetic_mi355x(8)
+    for a, b in ((0, 1), (4, 5)):
+        t.link_bw[a][b] = t.link_bw[b][a] = 20.0
+    L, (nid,) = ledger_with(t)
+    rc, plan, _ = L.assume(nid, [(25, 0)] * 4, SPR)
+    gpus = [t.devices[i].gpu for i in devices_of(plan)]
+    # every 4-GPU set inside one socket contains a 20 GB/s link here; xGMI joins all 8 GPUs
+    # directly, so the ring's slowest link matters more than the socket boundary
+    assert len(set(gpus)) == 4
+    assert all(t.link_bw[a][b] > 20.0 for a in gpus for b in gpus if a != b)
+
+
+def test_cpx_spread_uses_distinct_physical_gpus_binpack_uses_siblings():
+    t = synthetic_mi355x(8, "CPX")
+    L, (nid,) = ledger_with(t)
+    rc, plan, _ = L.assume(nid, [(50, 0)] * 4, SPR)
+    assert len({t.devices[i].gpu for i in devices_of(plan)}) == 4
+    rc, plan, _ = L.assume(nid, [(100, 0)] * 4, BIN)
+    assert len({t.devices[i].gpu for i in devices_of(plan)}) == 1   # four XCD partitions of one GPU
+    rc, plan, _ = L.assume(nid, [(200, 0)], BIN)                     # 2-device container
+    assert rc == N.OK and len(devices_of(plan)) == 2
+    assert len({t.devices[i].gpu for i in devices_of(plan)}) == 1
+
+
+def test_binpack_fills_one_device_before_the_next():
+    L, (nid,) = ledger_with(synthetic_mi355x(8))
+    devs = []
+    for k in range(10):
+        rc, plan = L.reserve(nid, f"p{k}", [(20, 0)], BIN)
+        assert rc == N.OK
+        devs.append(plan[0][0])
+    assert devs[:5] == [devs[0]] * 5 and devs[5:] == [devs[5]] * 5 and devs[0] != devs[5]
+
+
+def test_hbm_limits_colocation():
+    t = synthetic_mi355x(1)
+    L, (nid,) = ledger_with(t)
+    ok = sum(L.reserve(nid, f"p{k}", [(10, 64 * 1024)], BIN)[0] == N.OK for k in range(10))
+    assert ok == t.devices[0].hbm_mib // (64 * 1024)      # 4 x 64 GiB in 288 GB
+    L2, (nid2,) = ledger_with(t, track_hbm=False)
+    assert sum(L2.reserve(nid2, f"p{k}", [(10, 64 * 1024)], BIN)[0] == N.OK for k in range(10)) == 10
+
+
+_demand = st.lists(st.tuples(st.sampled_from([0, 5, 10, 20, 25, 33, 50, 100, 200]),
+                             st.sampled_from([0, 0, 1024, 16384, 65536])), min_size=1, max_size=4)
+
+
+@settings(max_examples=60, deadline=None)
+@given(st.lists(_demand, min_size=1, max_size=40), st.sampled_from(["SPX", "QPX", "CPX"]),
+       st.sampled_from([N.Policy.BINPACK, N.Policy.SPREAD, N.Policy.RANDOM, N.Policy.FIRSTFIT]), st.integers(0, 99))
+def test_ledger_invariants_under_random_churn(demands, mode, policy, seed):
+    t = synthetic_mi355x(8, mode)
+    L, ids = ledger_with(t, 2)
+    o = N.Options(policy, seed=seed)
+    rng = random.Random(seed)
+    live = []
+    for k, d in enumerate(demands):
+        nid = rng.choice(ids)
+        rc, plan = L.reserve(nid, f"p{k}", d, o)
+        if rc == N.OK:
+            assert len(plan) == len(d)
+            for (pct, mib), idx in zip(d, plan):
+                assert (idx == [-1]) == (pct == 0 and mib == 0)   # an HBM-only container needs a device
+                if pct > 100:
+                    assert len(idx) == pct // 100 and len(set(idx)) == len(idx)
+            L.commit(f"p{k}")
+            live.append(f"p{k}")
+        if live and rng.random() < 0.3:
+            L.release(live.pop(rng.randrange(len(live))))
+        for nid in ids:
+            for dv in L.snapshot(nid)["devices"]:
+                assert 0 <= dv["pct_free"] <= dv["pct_total"]
+                assert 0 <= dv["mib_free"] <= dv["mib_total"]
+    for u in live:
+        assert L.release(u) == N.OK
+    for nid in ids:   # allocate -> release is the identity
+        for dv in L.snapshot(nid)["devices"]:
+            assert dv["pct_free"] == dv["pct_total"] and dv["mib_free"] == dv["mib_total"]
