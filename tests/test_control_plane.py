@@ -1,0 +1,340 @@
+"""Control plane: pod/node controllers, restart rebuild, policy hot reload, Prometheus
+telemetry, API fault injection and concurrent-bind invariants.
+
+Reference behaviours covered (and the defects fixed): controller
+allocate/release (controller.go:210-243; D3 release on delete, D4 no 1 s sleep), rebuild
+from annotations (dealer.go:58-72, 271-301; D14 completed pods skipped), policy reload
+(context.go:44-59; D7 reload reaches scheduling), Prometheus query + fallback
+(prometheus.go:68-83; D12 errors surfaced), bind rollback (D2) and retries (D1).
+"""
+import asyncio
+import math
+
+import pytest
+from aiohttp import web
+
+from nanogpu import types as T
+from nanogpu.app import Config, Runtime
+from nanogpu.config.policy import MetricQuery, PolicySpec, Period, parse_duration, parse_policy
+from nanogpu.extender.verbs import Extender
+from nanogpu.k8s import podutil as pu
+from nanogpu.k8s.fake_apiserver import Faults, FakeKubeStore, InProcKube
+from nanogpu.state.cluster import ClusterState
+from nanogpu.telemetry.poller import LoadPoller
+from nanogpu.telemetry.prom import PromClient, PromError
+from nanogpu.topology.model import synthetic_mi355x
+
+
+async def wait_for(pred, timeout=5.0):
+    end = asyncio.get_running_loop().time() + timeout
+    while asyncio.get_running_loop().time() < end:
+        if pred():
+            return True
+        await asyncio.sleep(0.005)
+    return pred()
+
+
+def node(name="n0", gpus=8, partition="SPX"):
+    t = synthetic_mi355x(gpus, partition)
+    return pu.make_node(name, len(t.devices), t.to_json(), {"amd.com/gpu.present": "true"})
+
+
+def annotated(name, node_name, plan, pct=20, phase="Running"):
+    p = pu.make_pod(name, [(f"c{i}", pct) for i in range(len(plan))])
+    p["metadata"]["annotations"].update({T.container_annotation(f"c{i}"): ",".join(map(str, idx))
+                                         for i, idx in enumerate(plan)})
+    p["metadata"]["annotations"][T.ANNOTATION_GPU_ASSUME] = "true"
+    p["metadata"]["labels"][T.LABEL_GPU_ASSUME] = "true"
+    p["spec"]["nodeName"] = node_name
+    p["status"]["phase"] = phase
+    return p
+
+
+async def runtime(store, **kw):
+    rt = Runtime(Config(port=0, host="127.0.0.1", policy_config_path=kw.pop("policy", "/nonexistent"), **kw),
+                 api=InProcKube(store))
+    await rt.start()
+    return rt
+
+
+def free(rt, n="n0"):
+    return [g["Percent"] for g in rt.state.status()[n]["GPUs"]]
+
+
+# ----------------------------------------------------------------------------- controllers
+def test_controller_allocates_foreign_pods_and_releases_on_completion_and_delete():
+    async def main():
+        store = FakeKubeStore()
+        store.add_node(node())
+        rt = await runtime(store)
+        try:
+            store.create_pod(annotated("a", "n0", [[3]], 30))
+            store.create_pod(annotated("b", "n0", [[3], [5]], 20))
+            assert await wait_for(lambda: free(rt)[3] == 50 and free(rt)[5] == 80)
+            store.set_phase("default", "a", "Succeeded")             # completed -> release
+            assert await wait_for(lambda: free(rt)[3] == 80)
+            store.delete_pod("default", "b")                          # D3: delete releases
+            assert await wait_for(lambda: free(rt)[3] == 100 and free(rt)[5] == 100)
+            # same name, new object: the old incarnation is released
+            store.create_pod(annotated("c", "n0", [[1]], 50))
+            assert await wait_for(lambda: free(rt)[1] == 50)
+            store.delete_pod("default", "c")
+            store.create_pod(annotated("c", "n0", [[2]], 50))
+            assert await wait_for(lambda: free(rt)[1] == 100 and free(rt)[2] == 50)
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
+
+
+def test_restart_rebuilds_ledger_from_annotations_skipping_completed():
+    async def main():
+        store = FakeKubeStore()
+        store.add_node(node())
+        store.create_pod(annotated("a", "n0", [[0]], 40))
+        store.create_pod(annotated("b", "n0", [[0], [7]], 30))
+        store.create_pod(annotated("done", "n0", [[6]], 90, phase="Succeeded"))   # D14
+        pend = pu.make_pod("pending", [("c", 10)])
+        store.create_pod(pend)
+        rt = await runtime(store)
+        try:
+            f = free(rt)
+            assert f[0] == 30 and f[7] == 70 and f[6] == 100 and rt.state.ledger.n_pods == 2
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
+
+
+def test_node_capacity_change_and_delete():
+    async def main():
+        store = FakeKubeStore()
+        store.add_node(node("n0", 8))
+        rt = await runtime(store)
+        try:
+            assert len(free(rt)) == 8
+            store.add_node(node("n0", 4))                     # D20: capacity refresh
+            assert await wait_for(lambda: len(free(rt)) == 4)
+            store.delete_node("n0")
+            assert await wait_for(lambda: "n0" not in rt.state.status())
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
+
+
+# ----------------------------------------------------------------------------- policy
+def test_policy_parse_and_durations():
+    assert parse_duration("15s") == 15 and parse_duration("1m30s") == 90 and parse_duration("500ms") == 0.5
+    with pytest.raises(ValueError):
+        parse_duration("15 parsecs")
+    spec = parse_policy("""
+apiVersion: v1
+kind: public-dynamic-scheduler
+spec:
+  syncPeriod: [{name: gpu_core_usage_avg, period: 15s}, {name: gpu_memory_usage_avg, period: 1m}]
+  priority: [{name: x, weight: 2}]
+  scheduling: {policy: spread, compat: true, topologyWeight: 2.5, scoreNormalize: true}
+  metricsPreset: amd
+""")
+    assert spec.period_of("gpu_core_usage_avg") == 15 and spec.active_duration("gpu_memory_usage_avg") == 360
+    assert spec.policy == "spread" and spec.compat and spec.topology_weight == 2.5 and spec.score_normalize
+    assert "gpu_gfx_activity" in spec.query_for(T.GPU_CORE_USAGE_METRIC).query
+    assert "cardNode" in spec.query_for("other").fallback
+    with pytest.raises(ValueError):
+        parse_policy("spec: {scheduling: {policy: magic}}")
+
+
+def test_policy_hot_reload_reaches_scheduling(tmp_path):
+    async def main():
+        store = FakeKubeStore()
+        store.add_node(node())
+        path = tmp_path / "policy.yaml"
+        path.write_text("spec: {scheduling: {policy: binpack}}\n")
+        rt = await runtime(store, policy=str(path), policy_reload_s=0.05)
+        try:
+            assert rt.state.policy == "binpack"
+            await asyncio.sleep(0.02)
+            path.write_text("spec: {scheduling: {policy: spread, scoreNormalize: true}}\n")
+            import os
+            os.utime(path, (os.stat(path).st_atime, os.stat(path).st_mtime + 5))
+            assert await wait_for(lambda: rt.state.policy == "spread" and rt.state.score_normalize)
+            # a broken file keeps the last good policy (reference panics: stats.go:19)
+            path.write_text("spec: [unclosed\n")
+            os.utime(path, (os.stat(path).st_atime, os.stat(path).st_mtime + 10))
+            await asyncio.sleep(0.2)
+            assert rt.state.policy == "spread" and rt.watcher.errors >= 1
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
+
+
+# ----------------------------------------------------------------------------- telemetry
+async def fake_prometheus(series):
+    """series: {metric: {(node, card): [values...]}} -> /api/v1/query vectors."""
+    hits = []
+
+    async def query(request):
+        q = request.query["query"]
+        hits.append(q)
+        if "broken" in q:
+            return web.json_response({"status": "error", "error": "bad query"}, status=400)
+        for metric, by in series.items():
+            if q.startswith(metric):
+                for (n, c), vals in by.items():
+                    if f'"{n}"' in q and (f'card="{c}"' in q or f'cardNode="{c}"' in q):
+                        if "cardNode" in q and by.get("primary_only"):
+                            continue
+                        return web.json_response({"status": "success", "data": {"resultType": "vector", "result": [
+                            {"metric": {"node": n}, "value": [0, str(v)]} for v in vals]}})
+        return web.json_response({"status": "success", "data": {"resultType": "vector", "result": []}})
+
+    app = web.Application()
+    app.router.add_get("/api/v1/query", query)
+    runner = web.AppRunner(app)
+    await runner.setup()
+    site = web.TCPSite(runner, "127.0.0.1", 0)
+    await site.start()
+    return runner, site._server.sockets[0].getsockname()[1], hits
+
+
+def test_prom_client_semantics():
+    async def main():
+        runner, port, hits = await fake_prometheus({
+            "gpu_core_usage_avg": {("n0", 0): [0.2, 0.7], ("n0", 1): [float("nan")], ("n0", 2): [-3]}})
+        c = PromClient(f"http://127.0.0.1:{port}")
+        try:
+            q = MetricQuery('{metric}{{node=~"{node}",card="{card}"}} /100', '{metric}{{node="{node}",cardNode="{card}"}} /100')
+            assert await c.query_latest("n0", "gpu_core_usage_avg", 0, q) == 0.7      # last sample wins
+            assert await c.query_latest("n0", "gpu_core_usage_avg", 1, q) == 0.0      # NaN -> 0
+            assert await c.query_latest("n0", "gpu_core_usage_avg", 2, q) == 0.0      # negative -> 0
+            assert await c.query_latest("n0", "gpu_core_usage_avg", 9, q) is None
+            assert any("cardNode" in h for h in hits)                                 # fallback tried
+            with pytest.raises(PromError):                                             # D12: not swallowed
+                await c.query("broken")
+        finally:
+            await c.close()
+            await runner.cleanup()
+
+    asyncio.run(main())
+
+
+def test_load_poller_feeds_ledger_remain_load():
+    async def main():
+        runner, port, _ = await fake_prometheus({
+            "gpu_core_usage_avg": {("n0", 0): [0.95], ("n0", 1): [0.05]},
+            "gpu_memory_usage_avg": {("n0", 0): [0.91]}})
+        st = ClusterState(load_aware=True)
+        n = node("n0", 2)
+        st.register_node(n)
+        spec = PolicySpec(sync_period=(Period("gpu_core_usage_avg", 15), Period("gpu_memory_usage_avg", 15)))
+        poller = LoadPoller(st, PromClient(f"http://127.0.0.1:{port}"), lambda: [n], spec=spec, base_backoff_s=0.01)
+        try:
+            await poller.sync_metric("gpu_core_usage_avg")
+            await poller.sync_metric("gpu_memory_usage_avg")
+            gpus = st.status()["n0"]["GPUs"]
+            # usage = ceil(10*0.95)/10 + ceil(10*0.91)/10 = 2.0 -> RemainLoad 0; card 1: 0.1 -> 2 - 0 = 2
+            assert gpus[0]["RemainLoad"] == 0 and gpus[1]["RemainLoad"] == 2
+            # stale samples age out (period + 5 min)
+            poller.refresh_node("n0", 2, now=1e12)
+            assert st.status()["n0"]["GPUs"][0]["RemainLoad"] == 2
+        finally:
+            await poller.prom.close()
+            await runner.cleanup()
+
+    asyncio.run(main())
+
+
+# ----------------------------------------------------------------------------- faults
+def _ext(store, **kw):
+    st = ClusterState()
+    for n in store.nodes.values():
+        st.register_node(n)
+    return st, Extender(st, InProcKube(store), **kw)
+
+
+async def _bind(ext, store, pod, node_name="n0"):
+    m = pu.meta(pod)
+    ext.filter({"Pod": pod, "NodeNames": [node_name]})
+    return await ext.bind({"PodName": m["name"], "PodNamespace": m["namespace"], "PodUID": m["uid"],
+                           "Node": node_name})
+
+
+def test_bind_retries_transient_5xx_and_rolls_back_on_permanent_failure():
+    async def main():
+        store = FakeKubeStore(faults=Faults(bind_error_rate=0.5, seed=3))
+        store.add_node(node("n0", 2))
+        st, ext = _ext(store, api_retries=4)
+        ok = 0
+        for i in range(20):
+            p = store.create_pod(pu.make_pod(f"p{i}", [("c", 5)]))
+            r = await _bind(ext, store, p)
+            ok += r["Error"] == ""
+        assert ok >= 15                                     # retried through 50 % 5xx
+        store.faults.bind_error_rate = 1.0
+        before = st.status()["n0"]["GPUs"][0]["Percent"]
+        p = store.create_pod(pu.make_pod("doomed", [("c", 10)]))
+        r = await _bind(ext, store, p)
+        assert r["Error"] and st.status()["n0"]["GPUs"][0]["Percent"] == before     # D2 rollback
+        await asyncio.sleep(0.01)
+        ann = store.get_pod("default", "doomed")["metadata"].get("annotations") or {}
+        assert T.ANNOTATION_GPU_ASSUME not in ann                                   # un-annotated
+        assert any(e["reason"] == "FailedBinding" for e in store.events)
+
+    asyncio.run(main())
+
+
+def test_bind_conflict_on_already_bound_same_node_is_success():
+    async def main():
+        store = FakeKubeStore()
+        store.add_node(node("n0", 2))
+        st, ext = _ext(store)
+        p = store.create_pod(pu.make_pod("a", [("c", 20)]))
+        assert (await _bind(ext, store, p))["Error"] == ""
+        # kube-scheduler retries the same bind (e.g. after a timeout): idempotent
+        assert (await _bind(ext, store, p))["Error"] == ""
+        assert st.status()["n0"]["GPUs"][0]["Percent"] == 80
+        # a completed pod is refused (bind.go:46-50)
+        q = store.create_pod(pu.make_pod("b", [("c", 20)]))
+        store.set_phase("default", "b", "Failed")
+        ext.pods.d.clear()
+        assert "completed" in (await _bind(ext, store, store.get_pod("default", "b")))["Error"]
+
+    asyncio.run(main())
+
+
+def test_concurrent_binds_never_overcommit_with_api_latency():
+    async def main():
+        store = FakeKubeStore(faults=Faults(latency_s=0.001))
+        store.add_node(node("n0", 2))
+        st, ext = _ext(store)
+        pods = [store.create_pod(pu.make_pod(f"p{i}", [("c", 30)])) for i in range(20)]
+        # all filters first (every one sees room), then all binds race
+        for p in pods:
+            ext.filter({"Pod": p, "NodeNames": ["n0"]})
+        res = await asyncio.gather(*[ext.bind({"PodName": pu.meta(p)["name"], "PodNamespace": "default",
+                                                "PodUID": pu.meta(p)["uid"], "Node": "n0"}) for p in pods])
+        ok = sum(r["Error"] == "" for r in res)
+        assert ok == 6                                       # 3 x 30 % per device, 2 devices
+        used = {}
+        for p in store.pods.values():
+            if pu.node_name_of(p):
+                i = pu.container_assignment(p, "c")[0]
+                used[i] = used.get(i, 0) + 30
+        assert all(v <= 100 for v in used.values())
+        assert [g["Percent"] for g in st.status()["n0"]["GPUs"]] == [100 - used.get(0, 0), 100 - used.get(1, 0)]
+
+    asyncio.run(main())
+
+
+def test_reservation_ttl_sweeper_releases_lost_binds():
+    st = ClusterState()
+    st.register_node(node("n0", 1))
+    pod = pu.make_pod("lost", [("c", 40)])
+    st.reserve(pod, "n0")                 # a worker reserved, then died before commit
+    assert st.status()["n0"]["GPUs"][0]["Percent"] == 60
+    assert st.sweep_reservations(3600.0) == []
+    assert st.sweep_reservations(0.0) == [pu.pod_uid(pod)]
+    assert st.status()["n0"]["GPUs"][0]["Percent"] == 100
+    assert not math.isnan(0.0)
