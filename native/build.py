@@ -95,6 +95,24 @@ def build_topo_cli(force: bool = False) -> Path:
     return out
 
 
+SANITIZERS = {"plain": [], "asan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"],
+              "tsan": ["-fsanitize=thread"]}
+
+
+def build_stress(kind: str = "plain", force: bool = False) -> Path:
+    """Host-only stress driver (native/tests/stress_main.cpp) linked against the core
+    sources, optionally under ASan+UBSan or TSan (no GPU code involved)."""
+    out = NATIVE / "bin" / f"nanogpu-stress-{kind}"
+    srcs = [NATIVE / "src" / s for s in CORE_SOURCES] + [NATIVE / "tests" / "stress_main.cpp"]
+    if not force and _newer(out, srcs + _headers()):
+        return out
+    out.parent.mkdir(parents=True, exist_ok=True)
+    opt = ["-O2"] if kind == "plain" else ["-O1", "-g", "-fno-omit-frame-pointer"]
+    _run(["g++", "-std=c++17", *opt, *SANITIZERS[kind], f"-I{NATIVE / 'include'}", f"-I{ROCM / 'include'}",
+          *[str(x) for x in srcs], "-o", str(out), "-ldl", "-lpthread"])
+    return out
+
+
 def build_probe(force: bool = False) -> Path | None:
     hipcc = shutil.which("hipcc") or str(ROCM / "bin" / "hipcc")
     if not Path(hipcc).exists():
@@ -123,7 +141,11 @@ def main() -> None:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--no-hip", action="store_true")
     ap.add_argument("--sanitize", choices=["address", "thread", "undefined"])
+    ap.add_argument("--stress", choices=list(SANITIZERS), help="build the native stress driver")
     a = ap.parse_args()
+    if a.stress:
+        print(build_stress(a.stress, force=a.force))
+        return
     if a.sanitize:
         print(build_core(force=a.force, sanitize=a.sanitize))
         return

@@ -1,0 +1,194 @@
+// Native stress test for the sanitizer builds (ASan+UBSan, TSan): no Python involved.
+//
+//   * T threads reserve / commit / release pods on a shared-memory ledger while a checker
+//     thread snapshots every node and asserts 0 <= free <= total on both dimensions;
+//   * a second process (fork) attaches to the same /dev/shm ledger and churns too
+//     (SO_REUSEPORT workers share one ledger the same way);
+//   * a native front door serves filter / priorities to client threads over loopback
+//     HTTP while the ledger changes underneath it;
+//   * at the end every pod is released and every device must be whole again.
+// Exit code 0 = pass. Usage: nanogpu-stress [threads] [iterations]
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "nanogpu/frontend.h"
+#include "nanogpu/ledger.h"
+
+using namespace nanogpu;
+
+#define CHECK(c)                                                         \
+  do {                                                                   \
+    if (!(c)) {                                                          \
+      std::fprintf(stderr, "CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #c); \
+      std::_Exit(1);                                                     \
+    }                                                                    \
+  } while (0)
+
+static void add_nodes(Ledger& l, int n_nodes) {
+  for (int k = 0; k < n_nodes; ++k) {
+    Device devs[64];
+    std::memset(devs, 0, sizeof(devs));
+    const int parts = (k % 2) ? 8 : 1;  // alternate SPX and CPX nodes
+    const int n = 8 * parts;
+    for (int i = 0; i < n; ++i) {
+      devs[i].pct_total = 100;
+      devs[i].mib_total = 294896 / parts;
+      devs[i].gpu = static_cast<int16_t>(i / parts);
+      devs[i].part = static_cast<int16_t>(i % parts);
+      devs[i].numa = static_cast<int16_t>((i / parts) / 4);
+      devs[i].healthy = 1;
+      devs[i].xcds = static_cast<int16_t>(8 / parts);
+      devs[i].cus = 256 / parts;
+    }
+    Topology t;
+    std::memset(&t, 0, sizeof(t));
+    t.n_gpus = 8;
+    for (int a = 0; a < 8; ++a) {
+      t.numa[a] = static_cast<int16_t>(a / 4);
+      for (int b = 0; b < 8; ++b) t.link_bw[a * kMaxGpus + b] = a == b ? 0.f : 76.f;
+    }
+    CHECK(l.upsert_node("node-" + std::to_string(k), devs, n, t) == k);
+  }
+}
+
+static void churn(Ledger& l, int n_nodes, int seed, int iters, std::atomic<int>* reserved) {
+  std::mt19937_64 rng(seed);
+  std::vector<std::string> live;
+  Options o;
+  for (int it = 0; it < iters; ++it) {
+    o.policy = static_cast<Policy>(rng() % 4);
+    Demand d;
+    std::memset(&d, 0, sizeof(d));
+    d.n = 1 + static_cast<int>(rng() % 3);
+    static const int pcts[] = {0, 10, 25, 50, 100, 200};
+    for (int c = 0; c < d.n; ++c) {
+      d.c[c].pct = pcts[rng() % 6];
+      d.c[c].mib = static_cast<int64_t>(rng() % 4) * 8192;
+    }
+    const int node = static_cast<int>(rng() % n_nodes);
+    const std::string key = "s" + std::to_string(seed) + "-" + std::to_string(it);
+    Plan p;
+    const int32_t rc = l.reserve(node, key, d, o, &p);
+    if (rc == kOk) {
+      reserved->fetch_add(1);
+      if (rng() % 4) CHECK(l.commit(key) == kOk);
+      live.push_back(key);
+    }
+    if (!live.empty() && rng() % 3 == 0) {
+      const size_t i = rng() % live.size();
+      CHECK(l.release(live[i]) == kOk);
+      live.erase(live.begin() + static_cast<long>(i));
+    }
+  }
+  for (const auto& k : live) CHECK(l.release(k) == kOk);
+}
+
+static std::string post(int port, const std::string& path, const std::string& body) {
+  const int fd = socket(AF_INET, SOCK_STREAM, 0);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons(static_cast<uint16_t>(port));
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  CHECK(connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) == 0);
+  const std::string req = "POST " + path + " HTTP/1.1\r\nHost: x\r\nConnection: close\r\nContent-Length: " +
+                          std::to_string(body.size()) + "\r\n\r\n" + body;
+  CHECK(send(fd, req.data(), req.size(), MSG_NOSIGNAL) == static_cast<ssize_t>(req.size()));
+  std::string out;
+  char buf[4096];
+  for (;;) {
+    const ssize_t r = recv(fd, buf, sizeof(buf), 0);
+    if (r <= 0) break;
+    out.append(buf, static_cast<size_t>(r));
+  }
+  close(fd);
+  return out;
+}
+
+int main(int argc, char** argv) {
+  const int threads = argc > 1 ? std::atoi(argv[1]) : 4;
+  const int iters = argc > 2 ? std::atoi(argv[2]) : 2000;
+  const int n_nodes = 6;
+  const std::string path = "/dev/shm/nanogpu-stress-" + std::to_string(getpid());
+  auto ledger = std::make_shared<Ledger>(path, 64, 65536, true);
+  add_nodes(*ledger, n_nodes);
+
+  // second process on the same shared ledger
+  const pid_t child = fork();
+  if (child == 0) {
+    Ledger other(path, 64, 65536, true);
+    std::atomic<int> r{0};
+    churn(other, n_nodes, 9999, iters, &r);
+    std::_Exit(0);
+  }
+
+  std::atomic<bool> done{false};
+  std::atomic<int> reserved{0};
+  std::thread checker([&] {
+    while (!done.load()) {
+      for (int k = 0; k < n_nodes; ++k) {
+        NodeSnapshot s;
+        CHECK(ledger->snapshot(k, &s));
+        for (int i = 0; i < s.n_devs; ++i) {
+          CHECK(s.devs[i].pct_free >= 0 && s.devs[i].pct_free <= s.devs[i].pct_total);
+          CHECK(s.devs[i].mib_free >= 0 && s.devs[i].mib_free <= s.devs[i].mib_total);
+        }
+      }
+    }
+  });
+
+  Frontend fe(ledger, "127.0.0.1", 0, 2);
+  Options fo;
+  fe.set_options(fo, true);
+  std::vector<std::thread> clients;
+  for (int c = 0; c < 2; ++c)
+    clients.emplace_back([&, c] {
+      for (int i = 0; i < iters / 20; ++i) {
+        const std::string body =
+            "{\"Pod\":{\"metadata\":{\"uid\":\"u" + std::to_string(c * 100000 + i) +
+            "\"},\"spec\":{\"containers\":[{\"name\":\"c\",\"resources\":{\"limits\":{\"nano-gpu/gpu-percent\":\"" +
+            std::to_string(10 * (1 + i % 9)) + "\",\"nano-gpu/gpu-memory\":\"8Gi\"}}}]}},"
+            "\"NodeNames\":[\"node-0\",\"node-1\",\"node-2\",\"node-3\",\"node-4\",\"node-5\"]}";
+        const std::string r = post(fe.port(), i % 2 ? "/scheduler/priorities" : "/scheduler/filter", body);
+        CHECK(r.rfind("HTTP/1.1 200", 0) == 0);
+      }
+    });
+
+  std::vector<std::thread> ws;
+  for (int t = 0; t < threads; ++t) ws.emplace_back(churn, std::ref(*ledger), n_nodes, t + 1, iters, &reserved);
+  for (auto& w : ws) w.join();
+  for (auto& c : clients) c.join();
+  int status = 0;
+  CHECK(waitpid(child, &status, 0) == child);
+  CHECK(WIFEXITED(status) && WEXITSTATUS(status) == 0);
+  done.store(true);
+  checker.join();
+  fe.stop();
+
+  for (int k = 0; k < n_nodes; ++k) {
+    NodeSnapshot s;
+    CHECK(ledger->snapshot(k, &s));
+    for (int i = 0; i < s.n_devs; ++i) {
+      CHECK(s.devs[i].pct_free == s.devs[i].pct_total);
+      CHECK(s.devs[i].mib_free == s.devs[i].mib_total);
+    }
+  }
+  CHECK(ledger->n_pods() == 0);
+  const auto st = fe.filter_stats.count.load() + fe.prio_stats.count.load();
+  std::printf("stress ok: %d threads x %d iters, %d reservations, %llu native verbs\n", threads, iters,
+              reserved.load(), static_cast<unsigned long long>(st));
+  ledger.reset();
+  unlink(path.c_str());
+  return 0;
+}
