@@ -18,9 +18,9 @@ Scaling (`--gpus N`, one torchrun rank per GPU): every rank is one extender work
 workers share ONE native ledger in /dev/shm (the SO_REUSEPORT replica design of
 nanogpu.app), each drives 1/N of the burst through its own HTTP endpoint, so the burst and
 the cluster are fixed while workers are added ("strong" scaling). The GPUs are used for the
-node model: each rank reads its MI355X through the native KFD/amdsmi reader + HIP probe,
-and with N > 1 an RCCL all-reduce between rank pairs measures the xGMI link bandwidth that
-the topology scorer uses. Data: synthetic pods; cluster of `--nodes` simulated nodes cloned
+node model: each rank reads its MI355X through the native KFD/amdsmi reader + HIP probe
+(HBM copy rate), and with N > 1 one RCCL all-reduce over all ranks measures the ring bus
+bandwidth (per-link xGMI rate) that the topology scorer uses. All of that is untimed. Data: synthetic pods; cluster of `--nodes` simulated nodes cloned
 from the discovered MI355X.
 """
 from __future__ import annotations
@@ -152,14 +152,10 @@ def node_template(d: Dist, args) -> tuple[object, dict]:
             info["gpu"]["hbm_copy_gbs"] = round(hbm_bandwidth(d.local_rank, 1 << 30, 10), 1)
     link = 153.0
     if d.dist is not None and d.cuda:
-        from nanogpu.probe.calibrate import link_matrix
+        from nanogpu.probe.calibrate import ring_busbw
 
-        m = link_matrix(d.dist, d.device)
-        off = [m[a][b] for a in range(len(m)) for b in range(len(m)) if a != b and m[a][b] > 0]
-        if off:
-            link = statistics.mean(off)
-            info["link_bw_source"] = f"rccl all-reduce between {len(m)} ranks"
-            info["link_bw_matrix_gbs"] = [[round(x, 1) for x in r] for r in m]
+        link = ring_busbw(d.dist, d.device)
+        info["link_bw_source"] = f"rccl all-reduce busBW over {d.world} ranks"
     info["link_bw_gbs"] = round(link, 1)
     topo = synthetic_mi355x(args.gpus_per_node, args.partition, hbm_mib=hbm_mib, link_gbs=link)
     if info["gpu"]:

@@ -29,10 +29,19 @@ def core() -> ModuleType:
         raise ImportError(f"nanogpu._native is not built; {_BUILD_HINT}") from e
 
 
-def probe(required: bool = False) -> ModuleType | None:
+def probe(required: bool = False, build: bool = False) -> ModuleType | None:
     try:
         return importlib.import_module("nanogpu._probe")
     except ImportError as e:
+        if build and os.environ.get("NANOGPU_AUTOBUILD", "1") == "1":
+            from pathlib import Path
+            import subprocess
+            import sys
+
+            root = Path(__file__).resolve().parent.parent
+            r = subprocess.run([sys.executable, str(root / "native" / "build.py")], capture_output=True, text=True)
+            if r.returncode == 0:
+                return importlib.import_module("nanogpu._probe")
         if required:
             raise ImportError(f"nanogpu._probe (HIP gfx950 kernels) is not built; {_BUILD_HINT}") from e
         return None

@@ -4,8 +4,8 @@
   partition modes, NUMA) for the GPU this process owns;
 * hbm_bandwidth()    — streaming-copy GB/s from the HIP probe kernel;
 * cu_mask_isolation()— bf16 MFMA TFLOP/s on CU-masked streams (the agent's spatial share);
-* link_matrix()      — per-pair xGMI bandwidth measured with RCCL (torch.distributed,
-  backend "nccl" = RCCL on ROCm) between the ranks of one node; feeds the topology scorer.
+* ring_busbw()       — RCCL all-reduce bus bandwidth across the job's ranks (torch.distributed
+  backend "nccl" = RCCL on ROCm): the per-link xGMI rate that feeds the topology scorer.
 """
 from __future__ import annotations
 
@@ -29,7 +29,7 @@ def local_gpu_facts(device: int = 0, use_probe: bool = True) -> dict:
 
 
 def hbm_bandwidth(device: int = 0, nbytes: int = 1 << 30, iters: int = 10) -> float:
-    P = probe(required=True)
+    P = probe(required=True, build=True)
     return P.hbm_bandwidth(device, nbytes, iters)
 
 
@@ -57,30 +57,22 @@ def cu_mask_isolation(device: int = 0, fractions=(1, 2, 4, 8), iters: int = 2048
     return out
 
 
-def link_matrix(dist, device, nbytes: int = 64 << 20, iters: int = 5) -> list[list[float]]:
-    """Pairwise RCCL bandwidth (GB/s) between all ranks, via 2-rank sub-groups.
-
-    Every pair of MI355X GPUs in a node is one xGMI hop, so the matrix is expected to be
-    near-uniform; measuring it catches degraded links and PCIe-only pairs."""
+def ring_busbw(dist, device, nbytes: int = 256 << 20, iters: int = 5) -> float:
+    """RCCL all-reduce bus bandwidth (GB/s) over all ranks of the job, one collective on the
+    default group (no sub-communicators). On a fully connected 8x MI355X xGMI mesh a ring
+    all-reduce is bound by one link per step, so busBW = 2(n-1)/n x bytes / t estimates the
+    per-link bandwidth the topology scorer weights groups with."""
     import torch
 
-    world, rank = dist.get_world_size(), dist.get_rank()
-    bw = [[0.0] * world for _ in range(world)]
+    n = dist.get_world_size()
     buf = torch.ones(nbytes // 2, dtype=torch.bfloat16, device=device)
-    for a in range(world):
-        for b in range(a + 1, world):
-            g = dist.new_group([a, b])
-            if rank in (a, b):
-                dist.all_reduce(buf, group=g)  # warm-up
-                torch.cuda.synchronize(device)
-                t0 = time.perf_counter()
-                for _ in range(iters):
-                    dist.all_reduce(buf, group=g)
-                torch.cuda.synchronize(device)
-                dt = (time.perf_counter() - t0) / iters
-                # 2-rank ring all-reduce moves 2*(n-1)/n * bytes = bytes per rank
-                bw[a][b] = bw[b][a] = nbytes / dt / 1e9
-            dist.barrier()
-    t = torch.tensor(bw, dtype=torch.float64, device=device)
+    dist.all_reduce(buf)   # warm-up (communicator setup)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        dist.all_reduce(buf)
+    torch.cuda.synchronize(device)
+    dt = (time.perf_counter() - t0) / iters
+    t = torch.tensor([dt], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return t.cpu().tolist()
+    return 2.0 * (n - 1) / n * nbytes / float(t.item()) / 1e9
