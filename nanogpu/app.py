@@ -52,6 +52,13 @@ class Config:
     fake_partition: str = "SPX"
     seed: int = 0
     frontend: str = "native"                    # native (C++ epoll front door) | aiohttp
+    leader_elect: bool = False                  # Lease-based active/standby replicas
+    lease_name: str = "nano-gpu-scheduler"
+    lease_namespace: str = "kube-system"
+    lease_duration_s: float = 15.0
+    lease_renew_deadline_s: float = 10.0
+    lease_retry_s: float = 2.0
+    identity: str = ""
     frontend_threads: int = 2
     gpu_node_selectors: list = field(default_factory=lambda: [T.AMD_GPU_NODE_LABEL, T.LEGACY_GPU_NODE_LABEL])
 
@@ -85,6 +92,8 @@ class Runtime:
         self.watcher = None
         self.runner = None
         self.native = None
+        self.elector = None
+        self.router = None
         self.bound_port = 0
         self._fake = None
 
@@ -152,10 +161,24 @@ class Runtime:
         if self.leader:
             self.tasks.append(asyncio.ensure_future(self._sweeper()))
         self.ready.set()
+        if self.cfg.leader_elect and self.leader:
+            import socket
+
+            from .k8s.lease import LeaderElector
+
+            ident = self.cfg.identity or f"{socket.gethostname()}-{os.getpid()}"
+            self.elector = LeaderElector(self.api, ident, self.cfg.lease_namespace, self.cfg.lease_name,
+                                         self.cfg.lease_duration_s, self.cfg.lease_renew_deadline_s,
+                                         self.cfg.lease_retry_s, on_change=self._on_leadership)
+            self.tasks.append(self.elector.start())
         if serve:
             router = server.Router(self.extender, self.ready)
+            self.router = router
+            if self.elector is not None:
+                router.serving = lambda: self.elector.leader
             if self.cfg.frontend == "native":
                 self.native = server.NativeServer(router, self.cfg.host, self.cfg.port, self.cfg.frontend_threads)
+                self.native.fe.set_serving(self.elector is None or self.elector.leader)
                 self.native.start()
                 self.bound_port = self.native.port
             else:
@@ -164,6 +187,10 @@ class Runtime:
                                                                   reuse_port=self.cfg.workers > 1)
             log.info("worker %d serving on :%d (%s front door, policy=%s compat=%s)", self.worker, self.bound_port,
                      self.cfg.frontend, self.state.policy, self.state.options.compat)
+
+    def _on_leadership(self, leader: bool) -> None:
+        if self.native is not None:
+            self.native.fe.set_serving(leader)
 
     def _apply_policy(self, spec) -> None:
         pol = spec.policy or self.state.policy
@@ -181,6 +208,8 @@ class Runtime:
                 self.poller.sweep_stale()
 
     async def stop(self) -> None:
+        if self.elector is not None:
+            await self.elector.release()
         if self.native is not None:
             await self.native.stop()
         if self.runner is not None:

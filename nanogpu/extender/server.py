@@ -54,6 +54,7 @@ class Router:
         self.ready = ready
         self.extra_status = extra_status
         self.native = None          # NativeServer, for /metrics
+        self.serving = lambda: True  # False on a standby replica (leader election)
         g, p = "GET", "POST"
         self.table = {
             (p, "/scheduler/filter"): self.filter, (p, "/scheduler/priorities"): self.prioritize,
@@ -68,6 +69,8 @@ class Router:
 
     async def dispatch(self, method: str, path: str, query: dict, body: bytes) -> tuple[int, str, bytes]:
         h = self.table.get((method, path))
+        if path.startswith("/scheduler/") and h is not None and not self.serving():
+            return 503, JSON, _dumps({"Error": "nano-gpu-scheduler: this replica is not the leader"})
         if h is None:
             if path in self.paths:
                 return 405, TEXT, b"405: Method Not Allowed"
@@ -126,6 +129,8 @@ class Router:
     async def readyz(self, q, body):
         if self.ready is not None and not self.ready.is_set():
             return 503, TEXT, b"informers not synced"
+        if not self.serving():
+            return 503, TEXT, b"standby (not the leader)"
         return 200, TEXT, b"ok"
 
     async def trace(self, q, body):

@@ -205,6 +205,16 @@ class KubeClient:
         return await self.request("PATCH", f"/api/v1/nodes/{name}/status", patch,
                                   content_type="application/merge-patch+json")
 
+    # --------------------------------------------------------------------- leases
+    async def get_lease(self, ns: str, name: str) -> dict:
+        return await self.request("GET", f"/apis/coordination.k8s.io/v1/namespaces/{ns}/leases/{name}")
+
+    async def create_lease(self, ns: str, lease: dict) -> dict:
+        return await self.request("POST", f"/apis/coordination.k8s.io/v1/namespaces/{ns}/leases", lease)
+
+    async def update_lease(self, ns: str, name: str, lease: dict) -> dict:
+        return await self.request("PUT", f"/apis/coordination.k8s.io/v1/namespaces/{ns}/leases/{name}", lease)
+
     # --------------------------------------------------------------------- events
     async def create_event(self, ns: str, involved: dict, reason: str, message: str,
                            etype: str = "Warning") -> None:

@@ -98,6 +98,7 @@ class FakeKubeStore:
         self.watchers: dict[str, list[asyncio.Queue]] = {"pods": [], "nodes": []}
         self.faults = faults or Faults()
         self.counts: dict[str, int] = {}
+        self.leases: dict[tuple[str, str], dict] = {}
 
     # ------------------------------------------------------------------ internals
     def _bump(self, obj: dict) -> dict:
@@ -248,6 +249,31 @@ class FakeKubeStore:
     def add_event(self, ev: dict) -> None:
         self.events.append(ev)
 
+    # ------------------------------------------------------------------ leases (coordination.k8s.io/v1)
+    def get_lease(self, ns: str, name: str) -> dict:
+        le = self.leases.get((ns, name))
+        if le is None:
+            raise ApiError(404, f'leases.coordination.k8s.io "{name}" not found', "NotFound")
+        return le
+
+    def create_lease(self, ns: str, lease: dict) -> dict:
+        name = pu.meta(lease).get("name", "")
+        if (ns, name) in self.leases:
+            raise ApiError(409, f'leases.coordination.k8s.io "{name}" already exists', "AlreadyExists")
+        le = self._bump(copy.deepcopy(lease))
+        le["metadata"]["namespace"] = ns
+        self.leases[(ns, name)] = le
+        return le
+
+    def update_lease(self, ns: str, name: str, lease: dict) -> dict:
+        cur = self.get_lease(ns, name)
+        if pu.meta(lease).get("resourceVersion") != pu.meta(cur).get("resourceVersion"):
+            raise ApiError(409, f'Operation cannot be fulfilled on leases.coordination.k8s.io "{name}": '
+                                "the object has been modified", "Conflict")
+        le = self._bump(copy.deepcopy(lease))
+        self.leases[(ns, name)] = le
+        return le
+
     # ------------------------------------------------------------------ watch
     async def watch(self, kind: str, resource_version: str, label_selector: str | None = None
                     ) -> AsyncIterator[dict]:
@@ -339,6 +365,18 @@ class InProcKube:
     async def watch(self, resource, resource_version, timeout_s=300, label_selector=None):
         async for ev in self.store.watch(resource, resource_version, label_selector):
             yield ev
+
+    async def get_lease(self, ns, name):
+        await self._rtt()
+        return self.store.get_lease(ns, name)
+
+    async def create_lease(self, ns, lease):
+        await self._rtt()
+        return self.store.create_lease(ns, lease)
+
+    async def update_lease(self, ns, name, lease):
+        await self._rtt()
+        return self.store.update_lease(ns, name, lease)
 
     async def close(self):
         return None
@@ -471,6 +509,31 @@ def make_app(store: FakeKubeStore) -> web.Application:
         await lat()
         try:
             return web.json_response(store.patch_node(request.match_info["name"], await request.json()))
+        except ApiError as e:
+            return _err(e)
+
+    @routes.get("/apis/coordination.k8s.io/v1/namespaces/{ns}/leases/{name}")
+    async def get_lease(request):
+        await lat()
+        try:
+            return web.json_response(store.get_lease(request.match_info["ns"], request.match_info["name"]))
+        except ApiError as e:
+            return _err(e)
+
+    @routes.post("/apis/coordination.k8s.io/v1/namespaces/{ns}/leases")
+    async def create_lease(request):
+        await lat()
+        try:
+            return web.json_response(store.create_lease(request.match_info["ns"], await request.json()), status=201)
+        except ApiError as e:
+            return _err(e)
+
+    @routes.put("/apis/coordination.k8s.io/v1/namespaces/{ns}/leases/{name}")
+    async def update_lease(request):
+        await lat()
+        try:
+            return web.json_response(store.update_lease(request.match_info["ns"], request.match_info["name"],
+                                                        await request.json()))
         except ApiError as e:
             return _err(e)
 

@@ -60,6 +60,8 @@ class Frontend {
   int port() const { return port_; }
   int notify_fd() const { return py_efd_; }
   void set_options(const Options& o, bool score_normalize);
+  // false: every request goes to Python (a standby replica answers 503 from there).
+  void set_serving(bool on) { serving_.store(on, std::memory_order_release); }
   // Drains requests waiting for Python (non-blocking).
   std::vector<PyRequest> take();
   // Completes request `id` (any thread). Unknown ids (connection gone) are dropped.
@@ -89,6 +91,7 @@ class Frontend {
   int port_ = 0;
   int py_efd_ = -1;
   std::atomic<bool> stop_{false};
+  std::atomic<bool> serving_{true};
   std::vector<std::unique_ptr<Worker>> workers_;
 
   mutable std::mutex opt_mu_;

@@ -445,6 +445,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("port", &Frontend::port)
       .def("notify_fd", &Frontend::notify_fd)
       .def("set_options", &Frontend::set_options, py::arg("options"), py::arg("score_normalize") = false)
+      .def("set_serving", &Frontend::set_serving)
       .def("take",
            [](Frontend& f) {
              std::vector<PyRequest> v;

@@ -580,7 +580,7 @@ bool Frontend::handle_native(Worker* w, Conn* c, const std::string& method, cons
                              std::string_view body, std::string* out) {
   (void)w;
   (void)c;
-  if (method != "POST") return false;
+  if (method != "POST" || !serving_.load(std::memory_order_acquire)) return false;
   const bool prio = path == "/scheduler/priorities";
   if (!prio && path != "/scheduler/filter") return false;
   const uint64_t t0 = now_ns();
