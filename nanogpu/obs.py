@@ -41,6 +41,16 @@ class Metrics:
         self.pods = Gauge("nanogpu_pods", "pods in the ledger", registry=r)
         self.workqueue_depth = Gauge("nanogpu_workqueue_depth", "controller queue depth", ["queue"], registry=r)
 
+        self._children: dict = {}
+
+    def child(self, metric, *labels):
+        """Cached labelled child (prometheus_client's .labels() costs a lock + dict walk)."""
+        key = (id(metric), labels)
+        c = self._children.get(key)
+        if c is None:
+            c = self._children[key] = metric.labels(*labels)
+        return c
+
     def render(self) -> bytes:
         return generate_latest(self.registry)
 
