@@ -184,16 +184,28 @@ def _both(fn):
 
 
 # ----------------------------------------------------------------------------- configs
-async def config1(reference=False, **_):
-    """kind-style plumbing: real HTTP API server, 1 fake-GPU node, 1 pod gpu-percent=20, binpack."""
+async def config1(reference=False, reps=20, **_):
+    """kind-style plumbing: real HTTP API server, 1 fake-GPU node, 1 pod gpu-percent=20, binpack.
+    The one-pod flow (create -> filter -> priorities -> bind -> delete -> release) is repeated
+    `reps` times so the latency is a median, not one cold sample."""
     nodes = make_nodes(1, 1, prefix="kind-worker")
+    name = pu.meta(nodes[0])["name"]
+    binds, ok = [], 0
     async with Harness(nodes, "binpack", reference, http_api=True) as h:
-        r = await h.burst(_pods(1, (20,)))
-        pod = next(iter(h.store.pods.values()))
-        ann = pod["metadata"]["annotations"]
-        r.update(placement=ann.get(T.container_annotation("c0")), assume=ann.get(T.ANNOTATION_GPU_ASSUME),
-                 status_free=h.rt.state.status()[pu.meta(nodes[0])["name"]]["GPUs"][0]["Percent"])
-        return r
+        for k in range(reps):
+            pods = _pods(1, (20,), prefix=f"p{k}-")
+            r = await h.burst(pods)
+            pod = h.store.get_pod("default", pu.meta(pods[0])["name"])
+            ann = pod["metadata"]["annotations"]
+            free = h.rt.state.status()[name]["GPUs"][0]["Percent"]
+            ok += (r["scheduled"] == 1 and ann.get(T.container_annotation("c0")) == "0"
+                   and ann.get(T.ANNOTATION_GPU_ASSUME) == "true" and free == 80)
+            binds.append(r["bind_p50_ms"])
+            await h.delete(pods)
+        released = h.rt.state.status()[name]["GPUs"][0]["Percent"] == 100
+    return {"scheduled": 1 if ok == reps else 0, "placement": "0" if ok == reps else "?", "status_free": 80 if ok == reps else -1,
+            "reps_ok": ok, "reps": reps, "released_after_delete": released,
+            "bind_p50_ms": statistics.median(binds)}
 
 
 async def config2(gpus=1, reference=False, hbm_mib=None, **_):
@@ -315,7 +327,7 @@ def summary_md(r: dict) -> str:
     L = ["# BASELINE configs 1-5: this framework vs the reference model", "",
          "Generated by `python -m nanogpu.sim.configs` (see its docstring for the reference model).", ""]
     c1 = r["config1"]
-    L += ["## Config 1 — plumbing (real HTTP API server, 1 node, 1 pod @ 20 %)", "",
+    L += ["## Config 1 — plumbing (real HTTP API server, 1 node, 1 pod @ 20 %, median of 20 runs)", "",
           "| | scheduled | device | free % after | bind p50 ms (client) |", "|---|---:|---:|---:|---:|"]
     for k in ("ours", "reference_model"):
         v = c1[k]
