@@ -218,7 +218,12 @@ class NativeServer:
         self._loop.add_reader(self.fe.notify_fd(), self._drain)
 
     def _drain(self) -> None:
-        for rid, method, path, query, body, pod_json, _t in self.fe.take():
+        for rid, method, path, query, body, pod_json, _t, prepared in self.fe.take():
+            if prepared is not None:
+                t = asyncio.ensure_future(self._prepared(rid, prepared))
+                self._tasks.add(t)
+                t.add_done_callback(self._tasks.discard)
+                continue
             if pod_json:
                 try:
                     self.router.ext.pods.put(json.loads(pod_json))
@@ -227,6 +232,15 @@ class NativeServer:
             t = asyncio.ensure_future(self._one(rid, method, path, query, body))
             self._tasks.add(t)
             t.add_done_callback(self._tasks.discard)
+
+    async def _prepared(self, rid: int, p: dict) -> None:
+        try:
+            res = await self.router.ext.bind_prepared(p)
+            status, out = (500 if res.get("Error") else 200), _dumps(res)
+        except Exception as e:
+            log.exception("prepared bind failed")
+            status, out = 500, _dumps({"Error": f"internal error: {e}"})
+        self.fe.respond(rid, status, JSON, out)
 
     async def _one(self, rid: int, method: str, path: str, query: str, body: bytes) -> None:
         try:

@@ -22,7 +22,7 @@ from .. import types as T
 from ..k8s import podutil as pu
 from ..k8s.client import ApiError
 from ..obs import Metrics, Tracer
-from ..state.cluster import ClusterState, SchedulingError
+from ..state.cluster import N, ClusterState, SchedulingError
 from .wire import BindingArgs, ExtenderArgs, binding_result, filter_result, priority_list
 
 log = logging.getLogger(__name__)
@@ -165,18 +165,47 @@ class Extender:
         t1 = time.perf_counter()
         plan, fresh = self.state.reserve(pod, args.node)
         sp.phases["reserve"] = time.perf_counter() - t1
+        names = [c.get("name", "") for c in pu.containers(pod)]
+        ns, name = pu.pod_ns_name(pod)
+        await self._write(args.pod_namespace, args.pod_name, uid, args.node, names, plan, fresh, sp, (ns, name))
+
+    async def bind_prepared(self, p: dict) -> dict:
+        """Bind whose ledger reservation already ran in the native front door
+        (native/src/frontend.cpp::prepare_bind); only the API writes and commit remain."""
+        t0 = time.perf_counter()
+        err = ""
+        with self.tracer.span("bind", f"{p['ns']}/{p['name']}") as sp:
+            try:
+                rc = p["rc"]
+                if rc not in (N.OK, N.OK_EXISTING):
+                    raise self.state.reserve_error(p["demand"], p["node"], rc)
+                sp.phases["reserve"] = 0.0
+                await self._write(p["ns"], p["name"], p["uid"], p["node"], p["containers"], p["plan"],
+                                  rc == N.OK, sp, (p["ns"], p["name"]))
+            except (SchedulingError, ApiError, asyncio.TimeoutError, OSError) as e:
+                err = str(e) or e.__class__.__name__
+                sp.ok = False
+                sp.note = err
+        self.metrics.child(self.metrics.verb_latency, "bind").observe(time.perf_counter() - t0)
+        self.metrics.child(self.metrics.verb_total, "bind", "error" if err else "ok").inc()
+        if err:
+            log.info("bind %s/%s -> %s failed: %s", p["ns"], p["name"], p["node"], err)
+        return binding_result(err)
+
+    async def _write(self, ns: str, name: str, uid: str, node: str, names: list[str], plan, fresh: bool, sp,
+                     pod_ns_name: tuple[str, str]) -> None:
+        """Second half of bind: PATCH placement annotations, POST binding, commit; on any
+        failure roll the reservation back and un-annotate (fixes reference D1/D2)."""
         try:
             t2 = time.perf_counter()
             extra = {T.ANNOTATION_ASSUME_TIME: f"{time.time():.6f}"}
-            await self._retry("patch", self.api.patch_pod, args.pod_namespace, args.pod_name,
-                              pu.placement_patch(pod, plan, extra))
+            await self._retry("patch", self.api.patch_pod, ns, name, pu.placement_patch_names(names, plan, extra))
             t3 = time.perf_counter()
             try:
-                await self._retry("bind", self.api.bind_pod, args.pod_namespace, args.pod_name, uid, args.node)
+                await self._retry("bind", self.api.bind_pod, ns, name, uid, node)
             except ApiError as e:
                 # A retried bind whose first attempt landed: already bound to this node is success.
-                if not e.conflict or pu.node_name_of(await self.api.get_pod(args.pod_namespace,
-                                                                            args.pod_name)) != args.node:
+                if not e.conflict or pu.node_name_of(await self.api.get_pod(ns, name)) != node:
                     raise
             t4 = time.perf_counter()
             sp.phases["patch"], sp.phases["binding"] = t3 - t2, t4 - t3
@@ -189,18 +218,17 @@ class Extender:
             self.state.rollback(uid)
             self.metrics.rollbacks.inc()
             if not isinstance(e, asyncio.CancelledError):
-                self._background(self._unannotate(pod))
+                self._background(self._unannotate(*pod_ns_name, names))
                 if self.record_events and isinstance(e, ApiError):
                     self._background(self.api.create_event(
-                        args.pod_namespace, {"kind": "Pod", "name": args.pod_name, "namespace": args.pod_namespace,
-                                             "uid": uid}, "FailedBinding", f"nano-gpu bind failed: {e}"))
+                        ns, {"kind": "Pod", "name": name, "namespace": ns, "uid": uid}, "FailedBinding",
+                        f"nano-gpu bind failed: {e}"))
             raise
         self.state.commit(uid)
         self.metrics.pods_bound.inc()
 
-    async def _unannotate(self, pod: dict) -> None:
-        ns, name = pu.pod_ns_name(pod)
-        ann = {T.container_annotation(c.get("name", "")): None for c in pu.containers(pod)}
+    async def _unannotate(self, ns: str, name: str, names: list[str]) -> None:
+        ann = {T.container_annotation(n): None for n in names}
         ann[T.ANNOTATION_GPU_ASSUME] = None
         try:
             await self.api.patch_pod(ns, name, {"metadata": {"annotations": ann,

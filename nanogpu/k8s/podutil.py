@@ -137,8 +137,11 @@ def plan_from_pod(pod: dict) -> Plan | None:
 
 def placement_patch(pod: dict, plan: Plan, extra: dict | None = None) -> dict:
     """Merge-patch body writing the reference annotation contract (pod.go:65-79)."""
-    ann = {T.container_annotation(c.get("name", "")): ",".join(str(i) for i in plan[k])
-           for k, c in enumerate(containers(pod))}
+    return placement_patch_names([c.get("name", "") for c in containers(pod)], plan, extra)
+
+
+def placement_patch_names(names: list[str], plan: Plan, extra: dict | None = None) -> dict:
+    ann = {T.container_annotation(n): ",".join(str(i) for i in plan[k]) for k, n in enumerate(names)}
     ann[T.ANNOTATION_GPU_ASSUME] = "true"
     if extra:
         ann.update(extra)

@@ -203,9 +203,11 @@ class ClusterState:
         uid = pu.pod_uid(pod)
         rc, plan = self.ledger.reserve(e.id, uid, pu.pod_demand(pod), self.options)
         if rc not in (N.OK, N.OK_EXISTING):
-            raise SchedulingError(f"assume {self._demand_str(pu.pod_demand(pod))} on {node_name} failed: "
-                                  f"{N.err_str(rc)}")
+            raise self.reserve_error(pu.pod_demand(pod), node_name, rc)
         return plan, rc == N.OK
+
+    def reserve_error(self, demand, node_name: str, rc: int) -> SchedulingError:
+        return SchedulingError(f"assume {self._demand_str(demand)} on {node_name} failed: {N.err_str(rc)}")
 
     def commit(self, uid: str) -> None:
         self.ledger.commit(uid)

@@ -33,11 +33,30 @@ namespace nanogpu {
 // bytes rounded up to MiB (nanogpu/k8s/quantity.py::quantity_to_mib).
 bool quantity_value(std::string_view s, bool mib, int64_t* out);
 
+// Bind whose ledger half ran natively: the pod was seen by filter/prioritize, its demand
+// reserved on the ledger here; Python only performs the API writes and commits or rolls back.
+struct PreparedBind {
+  bool ok = false;                 // false: Python runs the whole bind (pod_json if cached)
+  int32_t rc = 0;                  // ledger reserve result (kOk, kOkExisting or an error)
+  std::string ns, name, uid, node;
+  std::vector<std::string> containers;
+  std::vector<std::vector<int32_t>> plan;
+  std::vector<std::pair<int32_t, int64_t>> demand;
+};
+
 struct PyRequest {
   uint64_t id;
   std::string method, path, query, body;
   std::string pod_json;   // bind: the Pod seen by filter/prioritize for this UID ("" if none)
+  PreparedBind bind;
   double t_arrival;
+};
+
+struct CachedPod {
+  std::string raw, ns, name;
+  std::vector<std::string> containers;
+  Demand demand;
+  bool completed = false;
 };
 
 struct VerbStats {
@@ -68,7 +87,7 @@ class Frontend {
   void respond(uint64_t id, int status, const std::string& content_type, const std::string& body);
   void stop();
 
-  VerbStats filter_stats, prio_stats, py_stats;
+  VerbStats filter_stats, prio_stats, py_stats, bind_stats;   // bind_stats: native reserve half
   std::atomic<uint64_t> connections{0}, requests{0};
   size_t pod_cache_size() const;
 
@@ -84,8 +103,8 @@ class Frontend {
   void defer(Worker* w, Conn* c, std::string method, std::string path, std::string query, std::string body);
   void flush(Worker* w, Conn* c);
   void close_conn(Worker* w, Conn* c);
-  void put_pod(std::string_view uid, std::string_view raw);
-  std::string pod_for_bind(std::string_view body);
+  void put_pod(std::string_view uid, CachedPod pod);
+  void prepare_bind(std::string_view body, PyRequest* r);
 
   std::shared_ptr<Ledger> ledger_;
   int port_ = 0;
@@ -102,7 +121,7 @@ class Frontend {
   std::deque<PyRequest> py_q_;
 
   mutable std::mutex pod_mu_;
-  std::unordered_map<std::string, std::string> pods_;
+  std::unordered_map<std::string, CachedPod> pods_;
   std::deque<std::string> pod_order_;
   size_t pod_cap_ = 16384;
 };

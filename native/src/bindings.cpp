@@ -454,9 +454,24 @@ PYBIND11_MODULE(_native, m) {
                v = f.take();
              }
              py::list out;
-             for (auto& r : v)
+             for (auto& r : v) {
+               py::object prep = py::none();
+               if (r.bind.ok) {
+                 const PreparedBind& b = r.bind;
+                 py::dict pd;
+                 pd["rc"] = b.rc;
+                 pd["ns"] = b.ns;
+                 pd["name"] = b.name;
+                 pd["uid"] = b.uid;
+                 pd["node"] = b.node;
+                 pd["containers"] = b.containers;
+                 pd["plan"] = b.plan;
+                 pd["demand"] = b.demand;
+                 prep = pd;
+               }
                out.append(py::make_tuple(r.id, r.method, r.path, r.query, py::bytes(r.body), py::bytes(r.pod_json),
-                                         r.t_arrival));
+                                         r.t_arrival, prep));
+             }
              return out;
            })
       .def("respond",
@@ -483,6 +498,7 @@ PYBIND11_MODULE(_native, m) {
         d["filter"] = one(f.filter_stats);
         d["priorities"] = one(f.prio_stats);
         d["python"] = one(f.py_stats);
+        d["bind_reserve"] = one(f.bind_stats);
         d["connections"] = f.connections.load();
         d["requests"] = f.requests.load();
         return d;

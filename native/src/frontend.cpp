@@ -309,15 +309,15 @@ size_t Frontend::pod_cache_size() const {
   return pods_.size();
 }
 
-void Frontend::put_pod(std::string_view uid, std::string_view raw) {
+void Frontend::put_pod(std::string_view uid, CachedPod pod) {
   if (uid.empty()) return;
   std::lock_guard<std::mutex> g(pod_mu_);
   auto it = pods_.find(std::string(uid));
   if (it != pods_.end()) {
-    it->second.assign(raw.data(), raw.size());
+    it->second = std::move(pod);
     return;
   }
-  pods_.emplace(std::string(uid), std::string(raw));
+  pods_.emplace(std::string(uid), std::move(pod));
   pod_order_.emplace_back(uid);
   while (pods_.size() > pod_cap_ && !pod_order_.empty()) {
     pods_.erase(pod_order_.front());
@@ -325,17 +325,54 @@ void Frontend::put_pod(std::string_view uid, std::string_view raw) {
   }
 }
 
-std::string Frontend::pod_for_bind(std::string_view body) {
+void Frontend::prepare_bind(std::string_view body, PyRequest* r) {
   json::Doc d;
-  if (!d.parse(body)) return {};
-  const int32_t u = d.get(d.root(), "PodUID", true);
-  if (!d.is(u, json::Type::kStr)) return {};
-  std::lock_guard<std::mutex> g(pod_mu_);
-  auto it = pods_.find(std::string(d.str(u)));
-  if (it == pods_.end()) return {};
-  std::string s = std::move(it->second);
-  pods_.erase(it);   // one bind per pod UID (the deque entry expires lazily)
-  return s;
+  if (!d.parse(body) || !d.is(d.root(), json::Type::kObj)) return;
+  auto str = [&](const char* k) -> std::string {
+    const int32_t v = d.get(d.root(), k, true);
+    return d.is(v, json::Type::kStr) ? std::string(d.str(v)) : std::string();
+  };
+  const std::string uid = str("PodUID"), name = str("PodName"), node = str("Node");
+  std::string ns = str("PodNamespace");
+  if (ns.empty()) ns = "default";
+  if (uid.empty() || name.empty() || node.empty()) return;
+  CachedPod pod;
+  {
+    std::lock_guard<std::mutex> g(pod_mu_);
+    auto it = pods_.find(uid);
+    if (it == pods_.end()) return;
+    pod = std::move(it->second);
+    pods_.erase(it);  // one bind per pod UID (the deque entry expires lazily)
+  }
+  if (pod.name != name || pod.ns != ns || pod.completed) {
+    r->pod_json = std::move(pod.raw);   // unusual: Python decides (and reports) with the object
+    return;
+  }
+  const int32_t id = ledger_->find_node(node);
+  if (id < 0) {
+    r->pod_json = std::move(pod.raw);
+    return;
+  }
+  Options o;
+  {
+    std::lock_guard<std::mutex> g(opt_mu_);
+    o = opt_;
+  }
+  const uint64_t t0 = now_ns();
+  Plan plan;
+  std::memset(&plan, 0, sizeof(plan));
+  PreparedBind& b = r->bind;
+  b.rc = ledger_->reserve(id, uid, pod.demand, o, &plan);
+  bind_stats.observe(now_ns() - t0);
+  b.ok = true;
+  b.ns = std::move(ns);
+  b.name = name;
+  b.uid = uid;
+  b.node = node;
+  b.containers = std::move(pod.containers);
+  for (int c = 0; c < pod.demand.n; ++c) b.demand.emplace_back(pod.demand.c[c].pct, pod.demand.c[c].mib);
+  if (b.rc == kOk || b.rc == kOkExisting)
+    for (int c = 0; c < plan.n; ++c) b.plan.emplace_back(plan.idx + plan.off[c], plan.idx + plan.off[c + 1]);
 }
 
 // ------------------------------------------------------------------------------ event loop
@@ -520,7 +557,8 @@ void Frontend::process(Worker* w, Conn* c) {
 void Frontend::defer(Worker* w, Conn* c, std::string method, std::string path, std::string query, std::string body) {
   PyRequest r;
   r.id = make_id(w->idx, c->id);
-  if (method == "POST" && path == "/scheduler/bind") r.pod_json = pod_for_bind(body);
+  if (method == "POST" && path == "/scheduler/bind" && serving_.load(std::memory_order_acquire))
+    prepare_bind(body, &r);
   r.method = std::move(method);
   r.path = std::move(path);
   r.query = std::move(query);
@@ -604,6 +642,7 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   Demand dem;
   std::memset(&dem, 0, sizeof(dem));
   std::string_view uid;
+  CachedPod cached;
   if (pod >= 0 && !d.is(pod, json::Type::kNull)) {
     if (!d.is(pod, json::Type::kObj)) return false;
     const int32_t md = d.get(pod, "metadata");
@@ -614,6 +653,16 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
         if (!d.is(u, json::Type::kStr)) return false;
         uid = d.str(u);
       }
+      const int32_t nm = d.get(md, "name"), ns = d.get(md, "namespace"), del = d.get(md, "deletionTimestamp");
+      if (d.is(nm, json::Type::kStr)) cached.name = std::string(d.str(nm));
+      cached.ns = d.is(ns, json::Type::kStr) ? std::string(d.str(ns)) : std::string("default");
+      if (del >= 0 && !d.is(del, json::Type::kNull) && !(d.is(del, json::Type::kStr) && d.str(del).empty()))
+        cached.completed = true;
+    }
+    const int32_t stt = d.get(pod, "status");
+    if (d.is(stt, json::Type::kObj)) {
+      const int32_t ph = d.get(stt, "phase");
+      if (d.is(ph, json::Type::kStr) && (d.str(ph) == "Succeeded" || d.str(ph) == "Failed")) cached.completed = true;
     }
     const int32_t spec = d.get(pod, "spec");
     int32_t cons = -1;
@@ -627,6 +676,8 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
       for (int32_t c = d.at(cons).first; c >= 0; c = d.at(c).next) {
         if (!d.is(c, json::Type::kObj)) return false;
         ContainerDemand& cd = dem.c[dem.n++];
+        const int32_t cn = d.get(c, "name");
+        cached.containers.emplace_back(d.is(cn, json::Type::kStr) ? std::string(d.str(cn)) : std::string());
         const int32_t res = d.get(c, "resources");
         int32_t lim = -1;
         if (res >= 0 && !d.is(res, json::Type::kNull)) {
@@ -673,7 +724,11 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     o = opt_;
     normalize = normalize_;
   }
-  if (pod >= 0 && !uid.empty()) put_pod(uid, d.raw(pod));
+  if (pod >= 0 && !uid.empty()) {
+    cached.raw.assign(d.raw(pod));
+    cached.demand = dem;
+    put_pod(uid, std::move(cached));
+  }
   Plan p;
   std::string& r = *out;
   r.reserve(64 + 48 * static_cast<size_t>(nn));

@@ -232,3 +232,30 @@ def test_native_quantity_matches_python(q, mib):
         assert want is None or want > 2 ** 62
     else:
         assert got == want, (q, mib)
+
+
+def test_native_prepared_bind_and_its_error_text():
+    async def main():
+        store, rt = await _runtime(1)
+        loop = asyncio.get_running_loop()
+        try:
+            big = store.create_pod(pu.make_pod("big", [("c", 100)] * 8))     # fills the node
+            other = store.create_pod(pu.make_pod("late", [("c", 100)]))
+            reqs = []
+            for p in (other, big):
+                reqs.append(("POST", "/scheduler/filter", _dumps({"Pod": p, "NodeNames": ["n0"]})))
+            for p in (big, other):
+                m = pu.meta(p)
+                reqs.append(("POST", "/scheduler/bind", _dumps({"PodName": m["name"], "PodNamespace": "default",
+                                                                 "PodUID": m["uid"], "Node": "n0"})))
+            res = await loop.run_in_executor(None, _http, rt.bound_port, reqs)
+            assert res[2] == (200, b'{"Error":""}')
+            assert res[3][0] == 500
+            assert json.loads(res[3][1])["Error"] == "assume (100) on n0 failed: insufficient gpu resource"
+            s = rt.native.fe.stats()
+            assert s["bind_reserve"]["count"] == 2 and store.counts.get("get_pod", 0) == 0
+            assert [g["Percent"] for g in rt.state.status()["n0"]["GPUs"]] == [0] * 8
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
