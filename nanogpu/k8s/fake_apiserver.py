@@ -122,8 +122,11 @@ class FakeKubeStore:
     # ------------------------------------------------------------------ pods
     def create_pod(self, pod: dict) -> dict:
         self._count("create_pod")
-        pod = copy.deepcopy(pod)
-        m = pod.setdefault("metadata", {})
+        # copy-on-write like every other write here: only the paths the store changes are
+        # copied (metadata, status); callers must not mutate a pod after handing it over
+        pod = dict(pod)
+        pod["metadata"] = m = dict(pod.get("metadata") or {})
+        pod["status"] = dict(pod.get("status") or {})
         m.setdefault("namespace", "default")
         m.setdefault("uid", str(uuid.uuid4()))
         m.setdefault("creationTimestamp", time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()))
