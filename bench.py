@@ -235,6 +235,9 @@ async def run_rank(d: Dist, args, topo, ledger_path: str) -> dict:
         await pod_ctrl.queue.drain(5.0)
         return {"stats": stats.summary(), "frag": frag}
 
+    from nanogpu.app import tune_gc
+
+    tune_gc()   # what `python -m nanogpu` does after start-up
     for w in range(args.warmup):
         await one_step(10_000 + w, False)
     rt.tracer.buf.clear()
