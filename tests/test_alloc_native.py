@@ -118,3 +118,16 @@ def test_ledger_invariants_under_random_churn(demands, mode, policy, seed):
     for nid in ids:   # allocate -> release is the identity
         for dv in L.snapshot(nid)["devices"]:
             assert dv["pct_free"] == dv["pct_total"] and dv["mib_free"] == dv["mib_total"]
+
+
+def test_partial_plan_failure_restores_exactly_D5():
+    """Reference allocate.go:108-113 restores Demand[i] (not [j]) and does not skip -1
+    indices when a multi-container allocation fails half way; here the debit is undone
+    exactly."""
+    L, (nid,) = ledger_with(synthetic_mi355x(2))
+    assert L.allocate_plan(nid, "a", [(70, 0)], [[1]], True) == N.OK
+    before = L.snapshot(nid)["devices"]
+    # container 0 fits on device 0, container 1 (40 %) does not fit on device 1 (30 % free)
+    rc = L.allocate_plan(nid, "b", [(50, 0), (0, 0), (40, 0)], [[0], [-1], [1]], True)
+    assert rc != N.OK
+    assert L.snapshot(nid)["devices"] == before and L.lookup("b") is None
