@@ -129,3 +129,27 @@ def test_colocated_cu_grants_are_isolated(P):
     ta, tb = P.mfma_colocated(0, [cumask.mask_words(a), cumask.mask_words(b)], [len(a) * 8, len(b) * 8], 1024)
     assert 0.17 < ta / alone < 0.34, (ta, tb, alone)
     assert 0.55 < tb / alone < 0.85, (ta, tb, alone)
+
+
+def test_cu_grant_unit_is_one_cu_per_xcd(P):
+    """The agent's grant unit (cumask.DeviceCUs: 8 consecutive mask bits) must enable exactly
+    one CU on each of the 8 XCDs, i.e. mask bits are XCC-interleaved; two units -> two per
+    XCD. (A mask leaving an XCC without CUs is not restrictive, so grants are >= 1 unit.)"""
+    import json
+    from pathlib import Path
+
+    from nanogpu.agent import cumask
+
+    out = {}
+    for units in (1, 2, 4):
+        d = cumask.DeviceCUs(256, 8)
+        bits = d.grant("t", max(1, (units * 100 + 31) // 32))   # percent giving `units` units
+        assert len(bits) == 8 * units, (units, bits)
+        recs = P.cu_census(0, cumask.mask_words(bits), 512, 64)
+        cus = {(x, (h >> 8) & 0xF, (h >> 12) & 1, (h >> 13) & 7) for x, h in recs}
+        per_xcd = {x: sum(1 for c in cus if c[0] == x) for x in range(8)}
+        out[units] = per_xcd
+    Path("gpurun_out").mkdir(exist_ok=True)
+    Path("gpurun_out/cu_grant_census.json").write_text(json.dumps(out))
+    for units, per_xcd in out.items():
+        assert all(v == units for v in per_xcd.values()), out
