@@ -13,6 +13,17 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
+def record(key: str, value) -> None:
+    """Measured facts for profiles/gpu_calibration.md (merged back from the GPU box)."""
+    from pathlib import Path
+
+    p = Path("gpurun_out/gpu_facts.json")
+    p.parent.mkdir(exist_ok=True)
+    d = json.loads(p.read_text()) if p.exists() else {}
+    d[key] = value
+    p.write_text(json.dumps(d, indent=1))
+
+
 @pytest.fixture(scope="module")
 def P():
     import torch
@@ -55,6 +66,7 @@ def test_mfma_tile_matches_fp32_reference(P):
 def test_hbm_copy_bit_exact_and_fast(P):
     assert P.copy_check(0, (1 << 24) + 3)
     gbs = P.hbm_bandwidth(0, 1 << 30, 10)
+    record("hbm_copy_gbs_1GiB", round(gbs, 1))
     # MI355X: 8 TB/s peak, ~6.3 TB/s achievable (MI355X_MICROARCH.md); catch gross regressions
     assert gbs > 3500, gbs
 
@@ -63,7 +75,8 @@ def test_cu_mask_spatial_share_scales(P):
     """A gpu-percent grant maps to an XCD-symmetric CU mask: TFLOP/s must track the CUs granted."""
     from nanogpu.probe.calibrate import cu_mask_isolation
 
-    r = cu_mask_isolation(0, fractions=(1, 4), iters=1024)
+    r = cu_mask_isolation(0, fractions=(1, 2, 4, 8), iters=1024)
+    record("mfma_tflops_by_cus", {str(k): round(v, 1) for k, v in r.items()})
     full, quarter = r[256], r[64]
     assert 0.18 < quarter / full < 0.35, r
 
@@ -127,6 +140,8 @@ def test_colocated_cu_grants_are_isolated(P):
     a, b = d.grant("a", 25), d.grant("b", 75)
     alone = P.mfma_throughput(0, [], 2048, 1024)["tflops"]
     ta, tb = P.mfma_colocated(0, [cumask.mask_words(a), cumask.mask_words(b)], [len(a) * 8, len(b) * 8], 1024)
+    record("colocated_25_75", {"alone_tflops": round(alone, 1), "tenant25_tflops": round(ta, 1),
+                               "tenant75_tflops": round(tb, 1)})
     assert 0.17 < ta / alone < 0.34, (ta, tb, alone)
     assert 0.55 < tb / alone < 0.85, (ta, tb, alone)
 
@@ -149,7 +164,6 @@ def test_cu_grant_unit_is_one_cu_per_xcd(P):
         cus = {(x, (h >> 8) & 0xF, (h >> 12) & 1, (h >> 13) & 7) for x, h in recs}
         per_xcd = {x: sum(1 for c in cus if c[0] == x) for x in range(8)}
         out[units] = per_xcd
-    Path("gpurun_out").mkdir(exist_ok=True)
-    Path("gpurun_out/cu_grant_census.json").write_text(json.dumps(out))
+    record("cu_grant_census_cus_per_xcd", {str(k): v for k, v in out.items()})
     for units, per_xcd in out.items():
         assert all(v == units for v in per_xcd.values()), out
