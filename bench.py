@@ -215,7 +215,9 @@ async def run_rank(d: Dist, args, topo, ledger_path: str) -> dict:
 
     async def one_step(step: int, timed: bool) -> dict:
         pods = bursts.pop(step)
-        drv = SchedulerDriver(client, api, names, caps, max_inflight_binds=args.inflight_binds, seed=step)
+        # one kube-scheduler stand-in per rank; distinct tie-break streams per rank
+        drv = SchedulerDriver(client, api, names, caps, max_inflight_binds=args.inflight_binds,
+                              seed=step * 1009 + d.rank)
         stats = await drv.run(pods)
         # all ranks finished their share of the burst: peak occupancy
         d.barrier()
@@ -274,6 +276,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str) -> dict:
         results["native"] = {v: round(1e6 * ns[v]["seconds_total"] / max(1, ns[v]["count"]), 2)
                              for v in ("filter", "priorities")}
     results["failed"] = sum(s["failed"] for s in results["steps"])
+    results["bind_errors"] = sum(s["bind_errors"] for s in results["steps"])
     await client.close()
     await rt.stop()
     return results
@@ -306,6 +309,7 @@ def main() -> int:
     all_binds = [b for r in d.gather_obj(res["bind_ms"]) for b in r]
     scheduled = sum(d.gather_obj(res["scheduled"]))
     failed = sum(d.gather_obj(res["failed"]))
+    bind_errors = sum(d.gather_obj(res["bind_errors"]))
     del led
     if d.rank == 0:
         all_binds.sort()
@@ -328,7 +332,7 @@ def main() -> int:
             "frag_pct": round(statistics.mean(f["frag_pct"] for f in fr), 3) if fr else None,
             "frag_hbm_pct": round(statistics.mean(f["frag_mib"] for f in fr), 3) if fr else None,
             "stranded_pct": round(statistics.mean(f["stranded_pct"] for f in fr), 3) if fr else None,
-            "scheduled": scheduled, "failed": failed, "gpu": gpu_info,
+            "scheduled": scheduled, "failed": failed, "bind_retries": bind_errors, "gpu": gpu_info,
             "native_verb_mean_us": res.get("native"),
         }
         print(json.dumps(line), flush=True)
