@@ -118,12 +118,29 @@ class NodeAgent:
         while True:
             await asyncio.sleep(self.health_period_s)
             try:
-                _, host = discover(self.sysfs_root, use_amdsmi=False)
-                present = {int(g["render_minor"]) for g in host.get("gpus", [])}
-                for i, minor in enumerate(self.render_minors()):
-                    self.plugin.set_health(i, minor in present)
+                await self.check_health()
             except Exception:
                 log.exception("health check failed")
+
+    async def check_health(self) -> list[int]:
+        """Re-reads KFD/DRM sysfs: a device whose render node vanished or whose GPU reports
+        uncorrectable RAS errors becomes Unhealthy for kubelet and unschedulable for the
+        extender (re-published topology annotation). Returns the devices that changed."""
+        topo, host = discover(self.sysfs_root, use_amdsmi=False)
+        present = {int(g["render_minor"]) for g in host.get("gpus", [])}
+        ras_ok = [d.healthy for d in topo.devices] if len(topo.devices) == len(self.topo.devices) else None
+        changed = []
+        for i, minor in enumerate(self.render_minors()):
+            ok = minor in present and (ras_ok is None or ras_ok[i])
+            if self.topo.devices[i].healthy != ok:
+                self.topo.devices[i].healthy = ok
+                changed.append(i)
+            if self.plugin is not None:
+                self.plugin.set_health(i, ok)
+        if changed:
+            log.warning("agent %s: devices %s health changed", self.node, changed)
+            await self.api.patch_node(self.node, node_patch(self.topo))
+        return changed
 
     async def stop(self) -> None:
         for t in self.tasks:

@@ -95,7 +95,7 @@ class NanoGpuPlugin:
         self.render = render_minors or [128 + 8 * i for i in range(len(topo.devices))]
         self.dev_root = dev_root
         self.cus = [cumask.DeviceCUs(d.cus, d.xcds) for d in topo.devices]
-        self.health = [True] * len(topo.devices)
+        self.health = [bool(d.healthy) for d in topo.devices]
         self._changed = asyncio.Event()
         self.allocations: list[Assignment] = []
 

@@ -32,13 +32,14 @@ def _props(d: dict) -> str:
 
 def write_mi355x_sysfs(root: str | Path, n_gpus: int = 8, compute: str = "SPX", memory: str = "NPS1",
                        n_numa: int = 2, hidden: tuple[int, ...] = (), xgmi: bool = True,
-                       degraded: dict | None = None) -> Path:
+                       degraded: dict | None = None, ras: dict | None = None) -> Path:
     """Writes /sys/class/{kfd,drm} for `n_gpus` MI355X under `root` and returns root.
 
     hidden:   physical GPUs whose KFD properties are unreadable (as for GPUs outside the
               container's cgroup on the real box: the node dirs and io_links exist, the
               properties file is empty);
-    degraded: {(a, b): MB/s} overrides for individual xGMI links.
+    degraded: {(a, b): MB/s} overrides for individual xGMI links;
+    ras:      {gpu: (ue, ce)} amdgpu RAS counters (written as umc_err_count).
     """
     root = Path(root)
     parts = PARTS[compute]
@@ -98,4 +99,7 @@ def write_mi355x_sysfs(root: str | Path, n_gpus: int = 8, compute: str = "SPX", 
         _w(drm / "mem_info_vram_total", f"{VRAM // nps}\n")
         _w(drm / "numa_node", f"{numa}\n")
         _w(drm / "product_name", "AMD Instinct MI355 OAM\n")
+        ue, ce = (ras or {}).get(g, (0, 0))
+        _w(drm / "ras/umc_err_count", f"ue: {ue}\nce: {ce}\n")
+        _w(drm / "ras/gfx_err_count", "ue: 0\nce: 0\n")
     return root

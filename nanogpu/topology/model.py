@@ -40,6 +40,8 @@ class GpuSpec:
     compute_partition: str = "SPX"
     memory_partition: str = "NPS1"
     bdf: str = ""
+    ras_ue: int = 0              # uncorrectable / correctable RAS errors (amdgpu ras/*_err_count)
+    ras_ce: int = 0
     xgmi_peers: int = 0          # xGMI links of this GPU (visible or not from the agent's cgroup)
     xgmi_link_gbs: float = 0.0   # slowest of them, GB/s (KFD io_link max_bandwidth)
 
@@ -51,6 +53,7 @@ class DeviceSpec:
     cus: int = T.MI355X_CUS
     xcds: int = T.MI355X_XCDS
     hbm_mib: int = 0
+    healthy: bool = True         # False: never chosen (uncorrectable RAS errors, device gone)
 
 
 @dataclass
@@ -103,7 +106,7 @@ class NodeTopology:
     def ledger_devices(self, track_hbm: bool = True) -> list[dict]:
         numa = {g.index: g.numa for g in self.gpus}
         return [{"pct_total": T.GPU_PERCENT_EACH_CARD, "mib_total": d.hbm_mib if track_hbm else 0,
-                 "gpu": d.gpu, "part": d.part, "numa": numa.get(d.gpu, -1), "healthy": True,
+                 "gpu": d.gpu, "part": d.part, "numa": numa.get(d.gpu, -1), "healthy": bool(d.healthy),
                  "xcds": d.xcds, "cus": d.cus} for d in self.devices]
 
     def ledger_topo(self) -> dict:
@@ -143,8 +146,9 @@ def _nps(mode: str) -> int:
     return int(m[3:]) if m.startswith("NPS") and m[3:].isdigit() else 1
 
 
-def from_host_json(host: str | dict) -> NodeTopology:
-    """Converts the native reader's JSON (nanogpu-topo / _native.discover_topology)."""
+def from_host_json(host: str | dict, max_ue: int = 0) -> NodeTopology:
+    """Converts the native reader's JSON (nanogpu-topo / _native.discover_topology).
+    Devices with more than `max_ue` uncorrectable RAS errors are published unhealthy."""
     h = json.loads(host) if isinstance(host, str) else host
     gpus_by_parent: dict[int, GpuSpec] = {}
     devices: list[DeviceSpec] = []
@@ -161,12 +165,14 @@ def from_host_json(host: str | dict) -> NodeTopology:
                 index=parent, numa=int(g.get("numa", -1)), cus=0, xcds=0, hbm_mib=0,
                 compute_partition=cp, memory_partition=(g.get("memory_partition") or "").upper(),
                 xgmi_peers=int(g.get("xgmi_peers", 0)), xgmi_link_gbs=float(g.get("xgmi_min_bw_mbs", 0)) / 1000.0,
+                ras_ue=int(g.get("ras_ue", 0)), ras_ce=int(g.get("ras_ce", 0)),
                 bdf=f"{int(g.get('domain', 0)):04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7}")
         gs = gpus_by_parent[parent]
         gs.cus += int(g.get("cus", 0))
         gs.xcds += int(g.get("num_xcc", 1))
         devices.append(DeviceSpec(gpu=parent, part=part, cus=int(g.get("cus", 0)),
-                                  xcds=int(g.get("num_xcc", 1)), hbm_mib=mib))
+                                  xcds=int(g.get("num_xcc", 1)), hbm_mib=mib,
+                                  healthy=int(g.get("ras_ue", 0)) <= max_ue))
     # HBM: a compute partition reports the memory partition it lives in (NPS1: the whole
     # pool; NPSn: 1/n of it) and parts/n compute partitions share each memory partition, so
     # the per-partition accounting share is reported * n / parts.

@@ -37,6 +37,10 @@ struct GpuInfo {
   std::string compute_partition;          // SPX/DPX/QPX/CPX ("" if unknown)
   std::string memory_partition;           // NPS1/NPS2/NPS4/NPS8
   std::string available_compute_partitions;
+  // RAS error counters summed over the amdgpu `ras/*_err_count` blocks (umc = HBM, gfx,
+  // sdma, xgmi_wafl, ...): uncorrectable errors make the device unschedulable.
+  bool ras_available = false;
+  int64_t ras_ue = 0, ras_ce = 0;
   int xgmi_peers = 0;              // xGMI io_links (type 11) to other GPU nodes, visible or not
   int64_t xgmi_min_bw_mbs = 0;     // slowest / fastest of those links (KFD max_bandwidth, MB/s)
   int64_t xgmi_max_bw_mbs = 0;

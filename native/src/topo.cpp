@@ -126,6 +126,19 @@ HostTopology read_sysfs(const std::string& root) {
     g.available_compute_partitions = trim(read_file(drm + "/available_compute_partition"));
     const std::string numa = trim(read_file(drm + "/numa_node"));
     if (!numa.empty()) g.numa = std::atoi(numa.c_str());
+    // RAS: every "<block>_err_count" file reads "ue: N\nce: M"
+    for (const std::string& f : list_dir(drm + "/ras")) {
+      if (f.size() <= 10 || f.compare(f.size() - 10, 10, "_err_count") != 0) continue;
+      for (const auto& kv : parse_properties(read_file(drm + "/ras/" + f))) {
+        std::string k = kv.first;
+        if (!k.empty() && k.back() == ':') k.pop_back();
+        const int64_t v = std::strtoll(kv.second.c_str(), nullptr, 10);
+        if (k == "ue") g.ras_ue += v;
+        else if (k == "ce") g.ras_ce += v;
+        else continue;
+        g.ras_available = true;
+      }
+    }
     kfd_to_gpu[g.kfd_node] = static_cast<int>(t.gpus.size());
     t.gpus.push_back(g);
   }
@@ -353,7 +366,8 @@ std::string to_json(const HostTopology& t) {
        << ",\"lds_size_kib\":" << g.lds_size_kib << ",\"numa\":" << g.numa
        << ",\"compute_partition\":\"" << esc(g.compute_partition) << "\",\"memory_partition\":\""
        << esc(g.memory_partition) << "\",\"available_compute_partitions\":\""
-       << esc(g.available_compute_partitions) << "\",\"xgmi_peers\":" << g.xgmi_peers
+       << esc(g.available_compute_partitions) << "\",\"ras_available\":" << (g.ras_available ? "true" : "false")
+       << ",\"ras_ue\":" << g.ras_ue << ",\"ras_ce\":" << g.ras_ce << ",\"xgmi_peers\":" << g.xgmi_peers
        << ",\"xgmi_min_bw_mbs\":" << g.xgmi_min_bw_mbs << ",\"xgmi_max_bw_mbs\":" << g.xgmi_max_bw_mbs
        << ",\"parent\":" << g.parent
        << ",\"partition\":" << g.partition << "}";

@@ -178,3 +178,43 @@ def test_guest_reads_grant(monkeypatch):
     monkeypatch.setenv("NANO_GPU_MEMORY_FRACTION", "0.25")
     g = guest.grant()
     assert g["percent"] == 20 and g["cu_mask"] == "0:0-47" and g["memory_fraction"] == 0.25
+
+
+def test_ras_errors_make_devices_unhealthy_end_to_end(tmp_path):
+    """Uncorrectable RAS errors on GPU 3: the agent reports its device Unhealthy to kubelet
+    and re-publishes the topology; the extender then never places on it."""
+    import json as _json
+
+    from nanogpu import _native as N
+    from nanogpu.agent.node import discover
+    from nanogpu.state.cluster import ClusterState
+    from nanogpu.topology.fixtures import write_mi355x_sysfs
+    from nanogpu.topology.model import from_host_json
+
+    root = write_mi355x_sysfs(tmp_path / "sys", 8, "CPX", ras={3: (2, 10)})
+    t = from_host_json(_json.loads(N.discover_topology(str(root), False)))
+    bad = [i for i, d in enumerate(t.devices) if not d.healthy]
+    assert bad == list(range(24, 32)) and t.gpus[3].ras_ue == 2 and t.gpus[3].ras_ce == 10
+
+    async def main():
+        store = FakeKubeStore()
+        root2 = write_mi355x_sysfs(tmp_path / "sys2", 8, "SPX")
+        topo, host = discover(str(root2), use_amdsmi=False)
+        store.add_node(pu.make_node("n0", 8, topo.to_json()))
+        api = InProcKube(store)
+        agent = NodeAgent(api, "n0", topo, host, device_plugin=False, sysfs_root=str(root2), health_period_s=0)
+        await agent.start()
+        assert await agent.check_health() == []
+        # GPU 5 starts reporting an uncorrectable HBM error
+        (root2 / "sys/class/drm/renderD168/device/ras/umc_err_count").write_text("ue: 1\nce: 0\n")
+        assert await agent.check_health() == [5]
+        node = store.get_node("n0")
+        st = ClusterState(policy="spread")
+        st.register_node(node)
+        for k in range(7):
+            rc, plan = st.ledger.reserve(st.node_entry("n0").id, f"p{k}", [(100, 0)], st.options)
+            assert rc == N.OK and plan[0] != [5]
+        assert st.ledger.reserve(st.node_entry("n0").id, "p7", [(100, 0)], st.options)[0] != N.OK
+        await agent.stop()
+
+    asyncio.run(main())

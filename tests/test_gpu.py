@@ -92,6 +92,9 @@ def test_topology_reader_on_real_sysfs(host, P):
     g = host["gpus"][0]
     assert g["cus"] == 256 and g["num_xcc"] == 8
     assert g["compute_partition"] in ("SPX", "DPX", "QPX", "CPX")
+    record("live_topology", {k: g.get(k) for k in ("cus", "num_xcc", "vram_bytes", "numa", "compute_partition",
+                                                    "memory_partition", "xgmi_peers", "xgmi_min_bw_mbs",
+                                                    "ras_available", "ras_ue", "ras_ce")})
     props = P.device_props(0)
     # the reader's VRAM equals what HIP reports (both come from the same KFD heap)
     assert abs(g["vram_bytes"] - props["total_mem_bytes"]) < (1 << 30)
