@@ -57,6 +57,8 @@ def parse_args():
     ap.add_argument("--no-gpu", action="store_true", help="skip GPU discovery (CPU-only rehearsal)")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--profile-out", default="", help="cProfile the timed steps (rank 0) into this file")
+    ap.add_argument("--inproc-driver", action="store_true",
+                    help="run the kube-scheduler stand-in inside the extender process (default: own process)")
     return ap.parse_args()
 
 
@@ -170,6 +172,9 @@ HBM_GIB = (8, 16, 32, 64)
 
 
 def burst(rank: int, world: int, total: int, step: int, seed: int) -> list[dict]:
+    """Deterministic (sizes and UIDs), so the driver process rebuilds the same objects."""
+    import uuid
+
     from nanogpu.k8s import podutil as pu
 
     rng = random.Random(seed * 1000003 + step)
@@ -178,11 +183,44 @@ def burst(rank: int, world: int, total: int, step: int, seed: int) -> list[dict]
         pct, gib = rng.choice(SIZES), rng.choice(HBM_GIB)
         if i % world != rank:
             continue
-        pods.append(pu.make_pod(f"s{step}-p{i}", [("main", pct, gib * 1024)], namespace=f"bench-r{rank}"))
+        uid = str(uuid.UUID(int=((step & 0xFFFFFFFF) << 64) | (rank << 32) | i))
+        pods.append(pu.make_pod(f"s{step}-p{i}", [("main", pct, gib * 1024)], namespace=f"bench-r{rank}", uid=uid))
     return pods
 
 
-async def run_rank(d: Dist, args, topo, ledger_path: str) -> dict:
+def driver_main(conn) -> None:
+    """kube-scheduler stand-in in its own process (as in a real cluster): receives the
+    extender's address once, then for every step schedules that step's pods (already
+    created in the API server by the main process) and returns the driver stats."""
+    from nanogpu.sim.driver import FastExtenderClient, SchedulerDriver
+
+    cfg = conn.recv()
+
+    async def serve() -> None:
+        loop = asyncio.get_running_loop()
+        client = FastExtenderClient("127.0.0.1", cfg["port"], pool=cfg["inflight"] + 8)
+        while True:
+            msg = await loop.run_in_executor(None, conn.recv)
+            if msg[0] != "step":
+                break
+            step = msg[1]
+            pods = burst(cfg["rank"], cfg["world"], cfg["pods"], step, 7)
+            drv = SchedulerDriver(client, None, cfg["names"], cfg["caps"], max_inflight_binds=cfg["inflight"],
+                                  seed=step * 1009 + cfg["rank"])
+            stats = await drv.run(pods, create=False)
+            conn.send(stats.summary())
+        await client.close()
+
+    prof_path = os.environ.get("NANOGPU_DRIVER_PROFILE")
+    if prof_path:
+        import cProfile
+
+        cProfile.runctx("asyncio.run(serve())", globals(), {"serve": serve, "asyncio": asyncio}, prof_path)
+    else:
+        asyncio.run(serve())
+
+
+async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
     from nanogpu import types as T
     from nanogpu.app import Config, Runtime
     from nanogpu.k8s import podutil as pu
@@ -213,12 +251,25 @@ async def run_rank(d: Dist, args, topo, ledger_path: str) -> dict:
     bursts = {s: burst(d.rank, d.world, args.pods, s, 7) for s in
               [10_000 + w for w in range(args.warmup)] + list(range(args.steps))}
 
+    loop = asyncio.get_running_loop()
+    if conn is not None:
+        conn.send({"port": rt.bound_port, "names": names, "caps": caps, "rank": d.rank, "world": d.world,
+                   "pods": args.pods, "inflight": args.inflight_binds})
+
     async def one_step(step: int, timed: bool) -> dict:
         pods = bursts.pop(step)
-        # one kube-scheduler stand-in per rank; distinct tie-break streams per rank
-        drv = SchedulerDriver(client, api, names, caps, max_inflight_binds=args.inflight_binds,
-                              seed=step * 1009 + d.rank)
-        stats = await drv.run(pods)
+        if conn is not None:
+            # the pods are created in the API server (this process), then the scheduler
+            # process schedules them through the extender's HTTP front door
+            for p in pods:
+                await api.create_pod(p)
+            conn.send(("step", step))
+            summary = await loop.run_in_executor(None, conn.recv)
+        else:
+            # one kube-scheduler stand-in per rank; distinct tie-break streams per rank
+            drv = SchedulerDriver(client, api, names, caps, max_inflight_binds=args.inflight_binds,
+                                  seed=step * 1009 + d.rank)
+            summary = (await drv.run(pods)).summary()
         # all ranks finished their share of the burst: peak occupancy
         d.barrier()
         frag = rt.state.frag(min(SIZES))
@@ -235,7 +286,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str) -> dict:
                 break
             await asyncio.sleep(0.0005)
         await pod_ctrl.queue.drain(5.0)
-        return {"stats": stats.summary(), "frag": frag}
+        return {"stats": summary, "frag": frag}
 
     from nanogpu.app import tune_gc
 
@@ -284,6 +335,15 @@ async def run_rank(d: Dist, args, topo, ledger_path: str) -> dict:
 
 def main() -> int:
     args = parse_args()
+    drv_proc, conn = None, None
+    if not args.inproc_driver:
+        # started before anything touches the GPU: a fresh interpreter, no HIP state
+        import multiprocessing as mp
+
+        ctx = mp.get_context("spawn")
+        conn, child = ctx.Pipe()
+        drv_proc = ctx.Process(target=driver_main, args=(child,), daemon=True)
+        drv_proc.start()
     d = Dist(args.gpus)
     d.init(use_gpu=not args.no_gpu)
     topo, gpu_info = node_template(d, args)
@@ -297,8 +357,16 @@ def main() -> int:
         led = core().Ledger(ledger_path, max(1024, args.nodes), max(65536, 4 * args.pods), True)
     d.barrier()
     try:
-        res = asyncio.run(run_rank(d, args, topo, ledger_path))
+        res = asyncio.run(run_rank(d, args, topo, ledger_path, conn))
     finally:
+        if drv_proc is not None:
+            try:
+                conn.send(("stop",))
+            except OSError:
+                pass
+            drv_proc.join(10)
+            if drv_proc.is_alive():
+                drv_proc.terminate()
         d.barrier()
         if d.rank == 0:
             try:

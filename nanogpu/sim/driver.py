@@ -110,6 +110,7 @@ class FastExtenderClient:
         self.all: list[_HttpConn] = []
         self._enc = json.JSONEncoder(separators=(",", ":"))
         self._pod_json: dict[str, bytes] = {}
+        self._names_json: dict[int, tuple] = {}
 
     async def _conn(self) -> _HttpConn:
         while self.idle:
@@ -144,6 +145,16 @@ class FastExtenderClient:
                 if len(self._pod_json) > 65536:
                     self._pod_json.clear()
                 self._pod_json[uid] = pj
+        names = body.get("NodeNames")
+        if names is not None and body.get("Nodes") is None and len(body) <= 3:
+            key = id(names)
+            hit = self._names_json.get(key)
+            if hit is None or hit[0] is not names:
+                hit = (names, self._enc.encode(names).encode())
+                if len(self._names_json) > 64:
+                    self._names_json.clear()
+                self._names_json[key] = hit
+            return b'{"Pod":' + pj + b',"Nodes":null,"NodeNames":' + hit[1] + b"}"
         rest = {k: v for k, v in body.items() if k != "Pod"}
         return b'{"Pod":' + pj + b"," + self._enc.encode(rest).encode()[1:]
 
@@ -241,7 +252,9 @@ class SchedulerDriver:
     def _candidates(self, need: int) -> list[str]:
         if not self.resource_fit:
             return self.nodes
-        return [n for n in self.nodes if self.requested.get(n, 0) + need <= self.capacity.get(n, 0)]
+        req, cap = self.requested, self.capacity
+        out = [n for n in self.nodes if req.get(n, 0) + need <= cap.get(n, 0)]
+        return self.nodes if len(out) == len(self.nodes) else out   # same object: encodings cached
 
     async def schedule_one(self, rec: PodRecord) -> bool:
         """One scheduling cycle. Returns True when a bind was issued."""
@@ -270,20 +283,17 @@ class SchedulerDriver:
         if not fit:
             self.stats.unschedulable_attempts += 1
             return False
+        if len(fit) == len(cands):
+            fit = cands            # all passed, same order: reuse the cached NodeNames encoding
         if len(fit) == 1:
             host = fit[0]
         else:
             args2 = {"Pod": pod, "Nodes": None, "NodeNames": fit}
             prios = await self.client.prioritize(args2)
-            best, host, seen = None, None, 0
-            for hp in prios:
-                s = hp["Score"]
-                if best is None or s > best:
-                    best, host, seen = s, hp["Host"], 1
-                elif s == best:
-                    seen += 1
-                    if self.rng.randrange(seen) == 0:   # reservoir sampling, as selectHost [ext]
-                        host = hp["Host"]
+            # selectHost [ext]: uniform among the max-score hosts
+            best = max(hp["Score"] for hp in prios)
+            ties = [hp["Host"] for hp in prios if hp["Score"] == best]
+            host = ties[0] if len(ties) == 1 else ties[self.rng.randrange(len(ties))]
         # kube-scheduler "assumes" the pod in its cache before binding asynchronously
         self.requested[host] = self.requested.get(host, 0) + need
         await self.sem.acquire()
