@@ -57,6 +57,8 @@ def parse_args():
     ap.add_argument("--no-gpu", action="store_true", help="skip GPU discovery (CPU-only rehearsal)")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--profile-out", default="", help="cProfile the timed steps (rank 0) into this file")
+    ap.add_argument("--busy-poll-us", type=int, default=int(os.environ.get("NANOGPU_BUSY_POLL_US", "0")),
+                    help="native front door busy-poll window")
     ap.add_argument("--inproc-driver", action="store_true",
                     help="run the kube-scheduler stand-in inside the extender process (default: own process)")
     return ap.parse_args()
@@ -191,33 +193,32 @@ def burst(rank: int, world: int, total: int, step: int, seed: int) -> list[dict]
 def driver_main(conn) -> None:
     """kube-scheduler stand-in in its own process (as in a real cluster): receives the
     extender's address once, then for every step schedules that step's pods (already
-    created in the API server by the main process) and returns the driver stats."""
-    from nanogpu.sim.driver import FastExtenderClient, SchedulerDriver
+    created in the API server by the main process) and returns the driver stats. The
+    scheduling cycle is serial on a blocking connection; binds run on a thread pool."""
+    from nanogpu.sim.driver import ThreadedSchedulerDriver
 
     cfg = conn.recv()
 
-    async def serve() -> None:
-        loop = asyncio.get_running_loop()
-        client = FastExtenderClient("127.0.0.1", cfg["port"], pool=cfg["inflight"] + 8)
+    def serve() -> None:
         while True:
-            msg = await loop.run_in_executor(None, conn.recv)
+            msg = conn.recv()
             if msg[0] != "step":
                 break
             step = msg[1]
             pods = burst(cfg["rank"], cfg["world"], cfg["pods"], step, 7)
-            drv = SchedulerDriver(client, None, cfg["names"], cfg["caps"], max_inflight_binds=cfg["inflight"],
-                                  seed=step * 1009 + cfg["rank"])
-            stats = await drv.run(pods, create=False)
+            drv = ThreadedSchedulerDriver("127.0.0.1", cfg["port"], cfg["names"], cfg["caps"],
+                                          bind_threads=min(32, cfg["inflight"]), seed=step * 1009 + cfg["rank"])
+            stats = drv.run(pods)
+            drv.close()
             conn.send(stats.summary())
-        await client.close()
 
     prof_path = os.environ.get("NANOGPU_DRIVER_PROFILE")
     if prof_path:
         import cProfile
 
-        cProfile.runctx("asyncio.run(serve())", globals(), {"serve": serve, "asyncio": asyncio}, prof_path)
+        cProfile.runctx("serve()", globals(), {"serve": serve}, prof_path)
     else:
-        asyncio.run(serve())
+        serve()
 
 
 async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
@@ -236,7 +237,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
         store.add_node(n)
     cfg = Config(port=0, host="127.0.0.1", priority=args.policy, compat=args.compat, ledger_path=ledger_path,
                  max_nodes=max(1024, args.nodes), max_pods=max(65536, 4 * args.pods),
-                 policy_config_path="/nonexistent/policy.yaml", reservation_ttl_s=3600)
+                 policy_config_path="/nonexistent/policy.yaml", reservation_ttl_s=3600,
+                 busy_poll_us=args.busy_poll_us)
     rt = Runtime(cfg, worker=0, api=InProcKube(store))
     await rt.start()
     client = FastExtenderClient("127.0.0.1", rt.bound_port, pool=args.inflight_binds + 8)

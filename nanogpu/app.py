@@ -60,6 +60,7 @@ class Config:
     lease_retry_s: float = 2.0
     identity: str = ""
     frontend_threads: int = 2
+    busy_poll_us: int = 0                       # native workers spin this long after an event
     gpu_node_selectors: list = field(default_factory=lambda: [T.AMD_GPU_NODE_LABEL, T.LEGACY_GPU_NODE_LABEL])
 
 
@@ -179,6 +180,7 @@ class Runtime:
             if self.cfg.frontend == "native":
                 self.native = server.NativeServer(router, self.cfg.host, self.cfg.port, self.cfg.frontend_threads)
                 self.native.fe.set_serving(self.elector is None or self.elector.leader)
+                self.native.fe.set_busy_poll_us(self.cfg.busy_poll_us)
                 self.native.start()
                 self.bound_port = self.native.port
             else:

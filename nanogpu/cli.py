@@ -59,6 +59,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--frontend", default="native", choices=["native", "aiohttp"],
                    help="native: C++ epoll server answers filter/priorities without Python")
     p.add_argument("--frontend-threads", type=int, default=2)
+    p.add_argument("--busy-poll-us", type=int, default=0,
+                   help="native workers keep polling this long after an event (lower latency, more CPU)")
     p.add_argument("--leader-elect", action="store_true", help="active/standby replicas on a Lease")
     p.add_argument("--lease-name", default="nano-gpu-scheduler")
     p.add_argument("--lease-namespace", default=os.environ.get("POD_NAMESPACE", "kube-system"))
@@ -83,5 +85,5 @@ def parse(argv: list[str] | None = None) -> Config:
         ledger_path=a.ledger_path, max_nodes=a.max_nodes, max_pods=a.max_pods,
         verify_pod_on_bind=a.bind_verify_pod, reservation_ttl_s=parse_duration(a.reservation_ttl),
         fake_cluster=a.fake_cluster, fake_gpus_per_node=a.fake_gpus_per_node, fake_partition=a.fake_partition,
-        seed=a.seed, frontend=a.frontend, frontend_threads=max(1, a.frontend_threads),
+        seed=a.seed, frontend=a.frontend, frontend_threads=max(1, a.frontend_threads), busy_poll_us=a.busy_poll_us,
         leader_elect=a.leader_elect, lease_name=a.lease_name, lease_namespace=a.lease_namespace, identity=a.identity)

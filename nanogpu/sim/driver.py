@@ -383,3 +383,169 @@ def node_capacities(nodes: list[dict]) -> dict[str, int]:
 
 
 __all__ = ["SchedulerDriver", "HttpExtenderClient", "FastExtenderClient", "InProcExtenderClient", "node_capacities", "T"]
+
+
+# ----------------------------------------------------------------------------- threaded driver
+class BlockingHttp:
+    """One blocking keep-alive HTTP/1.1 connection (the scheduling cycle is serial)."""
+
+    def __init__(self, host: str, port: int):
+        import socket
+
+        self.sock = socket.create_connection((host, port))
+        self.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        self.buf = b""
+
+    def post(self, path: bytes, body: bytes) -> tuple[int, bytes]:
+        self.sock.sendall(b"POST " + path + b" HTTP/1.1\r\nHost: extender\r\nContent-Type: application/json\r\n"
+                          b"Content-Length: " + str(len(body)).encode() + b"\r\n\r\n" + body)
+        buf = self.buf
+        while True:
+            he = buf.find(b"\r\n\r\n")
+            if he >= 0:
+                head = buf[:he]
+                i = head.lower().find(b"content-length:")
+                clen = int(head[i + 15:head.find(b"\r\n", i) if head.find(b"\r\n", i) > 0 else len(head)])
+                end = he + 4 + clen
+                if len(buf) >= end:
+                    self.buf = buf[end:]
+                    return int(head[9:12]), buf[he + 4:end]
+            chunk = self.sock.recv(262144)
+            if not chunk:
+                raise ConnectionError("extender closed the connection")
+            buf += chunk
+
+    def close(self) -> None:
+        self.sock.close()
+
+
+class ThreadedSchedulerDriver:
+    """kube-scheduler stand-in without an event loop: the scheduling cycle (filter ->
+    priorities -> select host) runs serially on one blocking connection, binds run
+    concurrently on a thread pool with one connection per thread (kube-scheduler's
+    binding goroutines). Same semantics as SchedulerDriver; lower per-cycle latency."""
+
+    def __init__(self, host: str, port: int, node_names: list[str], node_capacity: dict[str, int] | None = None,
+                 bind_threads: int = 16, seed: int = 0, max_attempts: int = 8, backoff_s: float = 0.001):
+        import threading
+
+        self.host, self.port = host, port
+        self.nodes = list(node_names)
+        self.capacity = dict(node_capacity or {})
+        self.requested: dict[str, int] = {n: 0 for n in self.nodes}
+        self.resource_fit = bool(self.capacity)
+        self.rng = random.Random(seed)
+        self.max_attempts = max_attempts
+        self.backoff_s = backoff_s
+        self.bind_threads = bind_threads
+        self.stats = DriverStats()
+        self.lock = threading.Lock()
+        self.cv = threading.Condition(self.lock)
+        self._enc = json.JSONEncoder(separators=(",", ":"))
+        self._names = self._enc.encode(self.nodes).encode()
+        self._local = threading.local()
+        self.cycle = BlockingHttp(host, port)
+
+    def _conn(self) -> BlockingHttp:
+        c = getattr(self._local, "c", None)
+        if c is None:
+            c = self._local.c = BlockingHttp(self.host, self.port)
+        return c
+
+    def _candidates(self, need: int) -> tuple[list[str], bytes]:
+        if not self.resource_fit:
+            return self.nodes, self._names
+        with self.lock:
+            out = [n for n in self.nodes if self.requested.get(n, 0) + need <= self.capacity.get(n, 0)]
+        if len(out) == len(self.nodes):
+            return self.nodes, self._names
+        return out, self._enc.encode(out).encode()
+
+    def run(self, pods: list[dict]) -> DriverStats:
+        import heapq
+        from concurrent.futures import ThreadPoolExecutor
+
+        now = time.perf_counter()
+        recs = [PodRecord(p, t_enqueue=now) for p in pods]
+        pod_json = {id(r): self._enc.encode(r.pod).encode() for r in recs}
+        ready: list[tuple[float, int, PodRecord]] = [(0.0, i, r) for i, r in enumerate(recs)]
+        seq = len(recs)
+        remaining = len(recs)
+        st = self.stats
+
+        def requeue(rec: PodRecord) -> None:
+            nonlocal seq, remaining
+            if rec.attempts < self.max_attempts:
+                heapq.heappush(ready, (time.perf_counter() + self.backoff_s * (2 ** rec.attempts), seq, rec))
+                seq += 1
+            else:
+                st.failed += 1
+                remaining -= 1
+            self.cv.notify_all()
+
+        def bind(rec: PodRecord, host: str, need: int) -> None:
+            nonlocal remaining
+            ns, name = pu.pod_ns_name(rec.pod)
+            body = self._enc.encode({"PodName": name, "PodNamespace": ns, "PodUID": pu.pod_uid(rec.pod),
+                                     "Node": host}).encode()
+            t0 = time.perf_counter()
+            try:
+                _, out = self._conn().post(b"/scheduler/bind", body)
+                err = json.loads(out).get("Error")
+            except (OSError, ValueError) as e:
+                err = str(e) or "bind failed"
+            t1 = time.perf_counter()
+            with self.lock:
+                if err:
+                    self.requested[host] -= need
+                    st.bind_errors += 1
+                    rec.error = err
+                    requeue(rec)
+                    return
+                rec.t_bound, rec.bind_latency, rec.node = t1, t1 - t0, host
+                st.scheduled += 1
+                st.bind_latencies.append(t1 - t0)
+                st.e2e_latencies.append(t1 - rec.t_enqueue)
+                st.t_last_bind = max(st.t_last_bind, t1)
+                remaining -= 1
+                self.cv.notify_all()
+
+        with ThreadPoolExecutor(self.bind_threads) as pool:
+            while True:
+                with self.lock:
+                    while remaining > 0 and (not ready or ready[0][0] > time.perf_counter()):
+                        self.cv.wait(max(0.0, ready[0][0] - time.perf_counter()) if ready else 0.05)
+                    if remaining == 0:
+                        break
+                    _, _, rec = heapq.heappop(ready)
+                rec.attempts += 1
+                if not st.t_first_filter:
+                    st.t_first_filter = time.perf_counter()
+                need = sum(p for p, _ in pu.pod_demand(rec.pod))
+                cands, cands_json = self._candidates(need)
+                host = None
+                if cands:
+                    head = b'{"Pod":' + pod_json[id(rec)] + b',"Nodes":null,"NodeNames":'
+                    _, out = self.cycle.post(b"/scheduler/filter", head + cands_json + b"}")
+                    fit = json.loads(out).get("NodeNames") or []
+                    if len(fit) == 1:
+                        host = fit[0]
+                    elif fit:
+                        fj = cands_json if len(fit) == len(cands) else self._enc.encode(fit).encode()
+                        _, out = self.cycle.post(b"/scheduler/priorities", head + fj + b"}")
+                        prios = json.loads(out)
+                        best = max(hp["Score"] for hp in prios)
+                        ties = [hp["Host"] for hp in prios if hp["Score"] == best]
+                        host = ties[0] if len(ties) == 1 else ties[self.rng.randrange(len(ties))]
+                if host is None:
+                    with self.lock:
+                        st.unschedulable_attempts += 1
+                        requeue(rec)
+                    continue
+                with self.lock:
+                    self.requested[host] = self.requested.get(host, 0) + need
+                pool.submit(bind, rec, host, need)
+        return st
+
+    def close(self) -> None:
+        self.cycle.close()

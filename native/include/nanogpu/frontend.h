@@ -81,6 +81,9 @@ class Frontend {
   void set_options(const Options& o, bool score_normalize);
   // false: every request goes to Python (a standby replica answers 503 from there).
   void set_serving(bool on) { serving_.store(on, std::memory_order_release); }
+  // After any event a worker keeps polling (epoll timeout 0) for this long before it
+  // blocks again: trades a little CPU during bursts for no wake-up latency per request.
+  void set_busy_poll_us(int us) { busy_poll_ns_.store(static_cast<int64_t>(us) * 1000, std::memory_order_relaxed); }
   // Drains requests waiting for Python (non-blocking).
   std::vector<PyRequest> take();
   // Completes request `id` (any thread). Unknown ids (connection gone) are dropped.
@@ -111,6 +114,7 @@ class Frontend {
   int py_efd_ = -1;
   std::atomic<bool> stop_{false};
   std::atomic<bool> serving_{true};
+  std::atomic<int64_t> busy_poll_ns_{0};
   std::vector<std::unique_ptr<Worker>> workers_;
 
   mutable std::mutex opt_mu_;

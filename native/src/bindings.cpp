@@ -446,6 +446,7 @@ PYBIND11_MODULE(_native, m) {
       .def("notify_fd", &Frontend::notify_fd)
       .def("set_options", &Frontend::set_options, py::arg("options"), py::arg("score_normalize") = false)
       .def("set_serving", &Frontend::set_serving)
+      .def("set_busy_poll_us", &Frontend::set_busy_poll_us)
       .def("take",
            [](Frontend& f) {
              std::vector<PyRequest> v;

@@ -378,8 +378,12 @@ void Frontend::prepare_bind(std::string_view body, PyRequest* r) {
 // ------------------------------------------------------------------------------ event loop
 void Frontend::run(Worker* w) {
   epoll_event evs[128];
+  uint64_t last_event = 0;
   while (!stop_.load(std::memory_order_acquire)) {
-    const int n = epoll_wait(w->ep, evs, 128, 200);
+    const int64_t spin = busy_poll_ns_.load(std::memory_order_relaxed);
+    const bool polling = spin > 0 && now_ns() - last_event < static_cast<uint64_t>(spin);
+    const int n = epoll_wait(w->ep, evs, 128, polling ? 0 : 200);
+    if (n > 0) last_event = now_ns();
     for (int i = 0; i < n; ++i) {
       const uint64_t tag = evs[i].data.u64;
       if (tag == 0) {
