@@ -6,13 +6,16 @@ burst on 8xMI355X"). The reference publishes no number, so vs_base
 What one step is (all of it inside the timed region):
   * a burst of `--pods` (default 1000) pods is created in the API server, mixed
     gpu-percent {10, 25, 50} with HBM requests {8, 16, 32, 64} GiB;
-  * every pod goes through the full extender protocol over loopback HTTP: a
-    kube-scheduler stand-in runs filter -> priorities -> select host, then an async bind;
-    the extender reserves on the native ledger, PATCHes the placement annotations and
-    POSTs the binding;
+  * every pod goes through the full extender protocol over loopback HTTP. A kube-scheduler
+    stand-in runs in its own process (as kube-scheduler does in a cluster): a serial
+    scheduling cycle filter -> priorities -> select host on one keep-alive connection, and
+    binds on a pool of threads. The extender (this process) answers filter/priorities in
+    its native C++ front door, reserves on the native ledger, PATCHes the placement
+    annotations and POSTs the binding;
   * after the burst the whole burst is deleted and the pod controller releases every
     share from the ledger (the create/delete churn of BASELINE config 5).
 `value` = pods bound per second over the K timed steps (whole job, all ranks).
+`--inproc-driver` runs the stand-in inside the extender's event loop instead.
 
 Scaling (`--gpus N`, one torchrun rank per GPU): every rank is one extender worker; all
 workers share ONE native ledger in /dev/shm (the SO_REUSEPORT replica design of
@@ -20,8 +23,8 @@ nanogpu.app), each drives 1/N of the burst through its own HTTP endpoint, so the
 the cluster are fixed while workers are added ("strong" scaling). The GPUs are used for the
 node model: each rank reads its MI355X through the native KFD/amdsmi reader + HIP probe
 (HBM copy rate), and with N > 1 one RCCL all-reduce over all ranks measures the ring bus
-bandwidth (per-link xGMI rate) that the topology scorer uses. All of that is untimed. Data: synthetic pods; cluster of `--nodes` simulated nodes cloned
-from the discovered MI355X.
+bandwidth (per-link xGMI rate) that the topology scorer uses. All of that is untimed.
+Data: synthetic pods; cluster of `--nodes` simulated nodes cloned from the discovered MI355X.
 """
 from __future__ import annotations
 
