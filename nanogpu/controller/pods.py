@@ -51,7 +51,10 @@ class PodController:
             self.state.release_uid(prev)
         self._uid_of[key] = uid
         if etype == "ADDED":
-            self.queue.add(key)
+            # only pods already placed (restart rebuild, someone else's bind) need work; a
+            # pending pod is the extender's own business until it is bound
+            if pu.node_name_of(pod) or pu.is_completed(pod):
+                self.queue.add(key)
             return
         known = self.state.known(uid)
         if known and pu.is_completed(pod):                                       # controller.go:303-306
