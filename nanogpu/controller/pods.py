@@ -14,6 +14,7 @@ from __future__ import annotations
 import asyncio
 import logging
 
+from .. import types as T
 from ..k8s import podutil as pu
 from ..k8s.informer import Informer, WorkQueue
 from ..state.cluster import ClusterState
@@ -30,37 +31,55 @@ class PodController:
         self.metrics = metrics
         self._tasks: list[asyncio.Task] = []
         self._uid_of: dict[str, str] = {}
+        self._sharing: dict[str, bool] = {}
         informer.add_handler(self._on_event)
 
     # ---------------------------------------------------------------- handlers
     def _on_event(self, etype: str, pod: dict, old: dict | None) -> None:
-        if not pu.is_gpu_sharing(pod):        # reference FilterFunc (controller.go:90-106)
+        # hot: every pod event of the cluster passes here, so fields are read once
+        m = pod.get("metadata") or {}
+        uid = m.get("uid", "")
+        sharing = self._sharing.get(uid) if uid else None
+        if sharing is None:
+            sharing = pu.is_gpu_sharing(pod)
+            if uid:
+                if len(self._sharing) > 262144:
+                    self._sharing.clear()
+                self._sharing[uid] = sharing
+        if not sharing:                        # reference FilterFunc (controller.go:90-106)
             return
-        key = pu.pod_key(pod)
-        uid = pu.pod_uid(pod)
+        key = f"{m.get('namespace', 'default')}/{m.get('name', '')}"
         if etype == "DELETED":
             # Release right away: the object is gone from the store, the worker would find nothing.
             if self.state.release_uid(uid) and self.metrics:
                 self.metrics.pods_released.inc()
             self.state.forget(uid)
             self._uid_of.pop(key, None)
+            self._sharing.pop(uid, None)
             return
         prev = self._uid_of.get(key)
-        if prev and prev != uid:
-            # same name, new object: the previous incarnation is gone
-            self.state.release_uid(prev)
-        self._uid_of[key] = uid
+        if prev != uid:
+            if prev:
+                # same name, new object: the previous incarnation is gone
+                self.state.release_uid(prev)
+            self._uid_of[key] = uid
+        spec = pod.get("spec") or {}
+        node = spec.get("nodeName")
+        completed = bool(m.get("deletionTimestamp")) or \
+            (pod.get("status") or {}).get("phase") in ("Succeeded", "Failed")
         if etype == "ADDED":
             # only pods already placed (restart rebuild, someone else's bind) need work; a
             # pending pod is the extender's own business until it is bound
-            if pu.node_name_of(pod) or pu.is_completed(pod):
+            if node or completed:
                 self.queue.add(key)
             return
+        if not completed and not node:
+            return                                 # still pending: nothing to account yet
         known = self.state.known(uid)
-        if known and pu.is_completed(pod):                                       # controller.go:303-306
+        if known and completed:                                                  # controller.go:303-306
             self.queue.add(key)
-        elif not known and not self.state.released(uid) and pu.is_assumed(pod) \
-                and pu.node_name_of(pod):                                          # :307-310
+        elif not known and not completed and not self.state.released(uid) and \
+                (m.get("annotations") or {}).get(T.ANNOTATION_GPU_ASSUME) == "true":     # :307-310
             self.queue.add(key)
 
     # ---------------------------------------------------------------- worker
