@@ -170,3 +170,61 @@ def test_cu_grant_unit_is_one_cu_per_xcd(P):
     record("cu_grant_census_cus_per_xcd", {str(k): v for k, v in out.items()})
     for units, per_xcd in out.items():
         assert all(v == units for v in per_xcd.values()), out
+
+
+_CHILD = r'''
+import json, os, sys
+sys.path.insert(0, os.environ["REPO"])
+from nanogpu.native import probe
+P = probe(required=True)
+r = P.mfma_throughput(0, [], 2048, 1024)
+out = {"tflops": r["tflops"]}
+from nanogpu.agent import guest
+if guest.apply(0):
+    import torch
+    free, total = torch.cuda.mem_get_info(0)
+    ok_small, ok_big = True, True
+    try:
+        a = torch.empty(int(0.05 * total), dtype=torch.uint8, device="cuda")
+        del a
+    except torch.OutOfMemoryError:
+        ok_small = False
+    try:
+        b = torch.empty(int(0.30 * total), dtype=torch.uint8, device="cuda")
+        del b
+    except torch.OutOfMemoryError:
+        ok_big = False
+    out.update(small_ok=ok_small, big_ok=ok_big)
+print(json.dumps(out))
+'''
+
+
+def _child(env_extra: dict) -> dict:
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parent.parent
+    env = dict(os.environ, REPO=str(root), **env_extra)
+    r = subprocess.run([sys.executable, "-c", _CHILD], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_device_plugin_env_is_honoured_by_rocr():
+    """The container environment the device plugin returns (nanogpu/agent/plugin.py) really
+    confines a process: HSA_CU_MASK in the plugin's "<dev>:<cu ranges>" format limits MFMA
+    throughput to the granted CUs, and NANO_GPU_MEMORY_FRACTION (applied by
+    nanogpu.agent.guest) caps what the PyTorch allocator can take."""
+    from nanogpu.agent import cumask
+
+    full = _child({})["tflops"]
+    d = cumask.DeviceCUs(256, 8)
+    mask = cumask.hsa_cu_mask(0, d.grant("pod/c", 25))
+    part = _child({"HSA_CU_MASK": mask, "NANO_GPU_MEMORY_FRACTION": "0.10"})
+    record("plugin_env_in_child", {"full_tflops": round(full, 1), "hsa_cu_mask": mask,
+                                    "masked_tflops": round(part["tflops"], 1),
+                                    "alloc_5pct_ok": part.get("small_ok"), "alloc_30pct_ok": part.get("big_ok")})
+    assert 0.15 < part["tflops"] / full < 0.40, (full, part)
+    assert part["small_ok"] is True and part["big_ok"] is False
