@@ -29,7 +29,19 @@ def core() -> ModuleType:
         raise ImportError(f"nanogpu._native is not built; {_BUILD_HINT}") from e
 
 
+def _hip_runtime_first() -> None:
+    """PyTorch-ROCm bundles its own libamdhip64.so.7 with the same SONAME as /opt/rocm's.
+    Whichever loads first serves the whole process, and torch's CUDA/HIP API fails on a
+    foreign runtime. So torch (when installed) is imported before the probe, and the
+    probe's kernels run on torch's runtime (verified on MI355X: tests/test_gpu.py)."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def probe(required: bool = False, build: bool = False) -> ModuleType | None:
+    _hip_runtime_first()
     try:
         return importlib.import_module("nanogpu._probe")
     except ImportError as e:
