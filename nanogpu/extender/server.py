@@ -64,6 +64,10 @@ class Router:
             (g, "/debug/stacks"): self.stacks, (g, "/debug/pprof/goroutine/"): self.stacks,
             (g, "/debug/profile"): self.profile, (g, "/debug/pprof/profile/"): self.profile,
             (g, "/debug/state"): self.state, (g, "/debug/frag"): self.frag, (g, "/debug/pprof/"): self.pprof_index,
+            (g, "/debug/pprof/cmdline/"): self.cmdline, (g, "/debug/pprof/heap/"): self.heap,
+            (g, "/debug/pprof/trace/"): self.trace, (g, "/debug/pprof/threadcreate/"): self.threads,
+            (g, "/debug/pprof/symbol/"): self.pprof_na, (g, "/debug/pprof/block/"): self.pprof_na,
+            (g, "/debug/pprof/mutex/"): self.pprof_na,
         }
         self.paths = {path for _, path in self.table}
 
@@ -158,7 +162,40 @@ class Router:
         return 200, JSON, _dumps(self.ext.state.frag(int(q.get("min_request", "0"))))
 
     async def pprof_index(self, q, body):
-        return 200, TEXT, b"goroutine/ profile/ (Python equivalents of the reference's pprof routes)\n"
+        return 200, TEXT, (b"Python/native equivalents of the reference's Go pprof routes (pprof.go:10-21):\n"
+                           b"goroutine/ profile/?seconds= heap/ trace/ threadcreate/ cmdline/ symbol/ block/ mutex/\n")
+
+    async def cmdline(self, q, body):
+        import sys
+
+        return 200, TEXT, "\x00".join(sys.argv).encode()
+
+    async def heap(self, q, body):
+        """Live Python objects by type (top 40) + tracemalloc top sites when tracing is on."""
+        import collections
+        import gc
+        import tracemalloc
+
+        counts = collections.Counter(type(o).__name__ for o in gc.get_objects())
+        lines = [f"gc objects: {sum(counts.values())}  gc counts: {gc.get_count()}  frozen: {gc.get_freeze_count()}"]
+        lines += [f"{n:10d} {t}" for t, n in counts.most_common(40)]
+        if tracemalloc.is_tracing():
+            lines.append("-- tracemalloc top 20")
+            lines += [str(st) for st in tracemalloc.take_snapshot().statistics("lineno")[:20]]
+        st = self.ext.state
+        lines.append(f"-- native ledger: {st.ledger.bytes} B at {st.ledger.path or '(heap)'}, "
+                     f"{st.ledger.n_nodes} nodes, {st.ledger.n_pods} pods, plan cache {st.ledger.cache_size}")
+        return 200, TEXT, "\n".join(lines).encode()
+
+    async def threads(self, q, body):
+        import threading
+
+        return 200, TEXT, "\n".join(f"{t.ident} {t.name} daemon={t.daemon}"
+                                     for t in threading.enumerate()).encode()
+
+    async def pprof_na(self, q, body):
+        return 200, TEXT, (b"not applicable: verbs do not share one mutex here (per-node robust mutexes in the "
+                           b"native ledger, lock-free reads for filter/priorities); see /debug/state\n")
 
 
 # ------------------------------------------------------------------------ aiohttp front door

@@ -151,3 +151,26 @@ def test_burst_spread_mixed_percent_no_overcommit():
             await api_runner.cleanup()
 
     asyncio.run(main())
+
+
+def test_debug_routes_reference_pprof_paths():
+    """Every reference pprof path (pprof.go:10-21) answers, plus the added debug routes."""
+    async def main():
+        node = pu.make_node("n0", 2)
+        store, api_runner, rt = await _stack([node])
+        base = f"http://127.0.0.1:{rt.bound_port}"
+        try:
+            async with aiohttp.ClientSession() as s:
+                for p in ("", "cmdline/", "profile/?seconds=0.05", "symbol/", "trace/", "heap/", "goroutine/",
+                          "block/", "threadcreate/", "mutex/"):
+                    async with s.get(f"{base}/debug/pprof/{p}") as r:
+                        assert r.status == 200, p
+                for p in ("/debug/trace", "/debug/stacks", "/debug/state", "/debug/frag", "/healthz", "/readyz",
+                          "/metrics", "/status"):
+                    async with s.get(base + p) as r:
+                        assert r.status == 200, p
+        finally:
+            await rt.stop()
+            await api_runner.cleanup()
+
+    asyncio.run(main())
