@@ -514,12 +514,10 @@ void Frontend::process(Worker* w, Conn* c) {
         const size_t n = std::strtoull(c->in.substr(p, le2 - p).c_str(), nullptr, 16);
         if (c->in.size() < le2 + 2 + n + 2) return;
         if (n == 0) {
-          // skip trailers up to the blank line
+          // last chunk: optional trailer lines, then the blank line
           const size_t end = c->in.find("\r\n\r\n", le2);
-          if (end == std::string::npos) {
-            if (c->in.compare(le2, 4, "\r\n\r\n") != 0 && c->in.size() < le2 + 4) return;
-          }
-          consumed = (end == std::string::npos ? le2 + 2 : end + 4);
+          if (end == std::string::npos) return;  // need more
+          consumed = end + 4;
           break;
         }
         body.append(c->in, le2 + 2, n);
