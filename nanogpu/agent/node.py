@@ -53,7 +53,7 @@ def node_patch(topo: NodeTopology) -> dict:
 
 
 def status_patch(topo: NodeTopology, advertise_percent: bool) -> dict:
-    res = {T.RESOURCE_GPU_MEMORY: str(sum(d.hbm_mib for d in topo.devices))}
+    res = {T.RESOURCE_GPU_MEMORY: str(topo.hbm_capacity_mib())}
     if advertise_percent:
         res[T.RESOURCE_GPU_PERCENT] = str(T.GPU_PERCENT_EACH_CARD * len(topo.devices))
     return {"status": {"capacity": dict(res), "allocatable": dict(res)}}

@@ -290,7 +290,8 @@ class ClusterState:
                 "Name": name,
                 "GPUs": [{"Percent": d["pct_free"], "PercentTotal": d["pct_total"],
                           "RemainLoad": d["remain_load"], "MemoryMiB": d["mib_free"],
-                          "MemoryMiBTotal": d["mib_total"], "GPU": d["gpu"], "Partition": d["part"],
+                          "MemoryMiBTotal": d["mib_total"], "MemoryPool": d["pool"], "GPU": d["gpu"],
+                          "Partition": d["part"],
                           "Healthy": d["healthy"]} for d in snap["devices"]],
                 "PlanCache": {},
                 "Generation": snap["generation"],

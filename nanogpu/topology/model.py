@@ -52,8 +52,10 @@ class DeviceSpec:
     part: int = 0
     cus: int = T.MI355X_CUS
     xcds: int = T.MI355X_XCDS
-    hbm_mib: int = 0
+    hbm_mib: int = 0             # HBM this device can draw from (its pool's size when pooled)
     healthy: bool = True         # False: never chosen (uncorrectable RAS errors, device gone)
+    pool: int = -1               # shared HBM pool (memory partition) id within the node, -1 = own HBM
+    mib_share: int = 0           # HBM a whole-device grant takes from the pool (pool / members)
 
 
 @dataclass
@@ -107,7 +109,13 @@ class NodeTopology:
         numa = {g.index: g.numa for g in self.gpus}
         return [{"pct_total": T.GPU_PERCENT_EACH_CARD, "mib_total": d.hbm_mib if track_hbm else 0,
                  "gpu": d.gpu, "part": d.part, "numa": numa.get(d.gpu, -1), "healthy": bool(d.healthy),
-                 "xcds": d.xcds, "cus": d.cus} for d in self.devices]
+                 "xcds": d.xcds, "cus": d.cus, "pool": d.pool if track_hbm else -1,
+                 "mib_share": d.mib_share or d.hbm_mib} for d in self.devices]
+
+    def hbm_capacity_mib(self) -> int:
+        """Node HBM: every pool once plus every device with its own HBM."""
+        pools = {d.pool: d.hbm_mib for d in self.devices if d.pool >= 0}
+        return sum(pools.values()) + sum(d.hbm_mib for d in self.devices if d.pool < 0)
 
     def ledger_topo(self) -> dict:
         return {"n_gpus": self.n_gpus, "numa": [g.numa for g in self.gpus], "link_bw": self.link_bw}
@@ -129,6 +137,7 @@ def synthetic_mi355x(n_gpus: int = 8, compute: str = "SPX", memory: str = "NPS1"
     what KFD/amdsmi or the peer-copy probe report.
     """
     parts = PARTITIONS[compute]
+    nps = _nps(memory)
     gpus, devs = [], []
     for g in range(n_gpus):
         gpus.append(GpuSpec(index=g, numa=g // max(1, gpus_per_numa), hbm_mib=hbm_mib,
@@ -136,9 +145,23 @@ def synthetic_mi355x(n_gpus: int = 8, compute: str = "SPX", memory: str = "NPS1"
                             bdf=f"0000:{0x05 + 0x10 * g:02x}:00.0"))
         for p in range(parts):
             devs.append(DeviceSpec(gpu=g, part=p, cus=T.MI355X_CUS // parts,
-                                   xcds=max(1, T.MI355X_XCDS // parts), hbm_mib=hbm_mib // parts))
+                                   xcds=max(1, T.MI355X_XCDS // parts)))
+        _assign_pools([d for d in devs if d.gpu == g], hbm_mib // nps, nps)
     bw = [[0.0 if a == b else link_gbs for b in range(n_gpus)] for a in range(n_gpus)]
     return NodeTopology(gpus=gpus, devices=devs, link_bw=bw, virtualization="BAREMETAL")
+
+
+def _assign_pools(ds: list, pool_mib: int, nps: int) -> None:
+    """Partitions of one GPU: `nps` memory partitions of `pool_mib` each, len(ds)/nps
+    compute partitions per memory partition. One member per pool = the device's own HBM."""
+    members = max(1, len(ds) // max(1, nps))
+    for k, d in enumerate(ds):
+        d.hbm_mib = pool_mib
+        if members > 1:
+            d.pool = d.gpu * 8 + k // members
+            d.mib_share = pool_mib // members
+        else:
+            d.pool, d.mib_share = -1, pool_mib
 
 
 def _nps(mode: str) -> int:
@@ -174,17 +197,15 @@ def from_host_json(host: str | dict, max_ue: int = 0) -> NodeTopology:
                                   xcds=int(g.get("num_xcc", 1)), hbm_mib=mib,
                                   healthy=int(g.get("ras_ue", 0)) <= max_ue))
     # HBM: a compute partition reports the memory partition it lives in (NPS1: the whole
-    # pool; NPSn: 1/n of it) and parts/n compute partitions share each memory partition, so
-    # the per-partition accounting share is reported * n / parts.
+    # pool; NPSn: 1/n of it); the parts/n compute partitions of one memory partition draw
+    # from it as a shared pool (mirrored in the ledger).
     for parent, gs in gpus_by_parent.items():
         ds = [d for d in devices if d.gpu == parent]
         reported = max((d.hbm_mib for d in ds), default=0)
         if ds and len(ds) > 1 and all(d.hbm_mib == reported for d in ds):
             nps = _nps(gs.memory_partition)
-            share = reported * nps // len(ds) if len(ds) % nps == 0 else reported // len(ds)
-            for d in ds:
-                d.hbm_mib = share
-            gs.hbm_mib = share * len(ds)
+            _assign_pools(ds, reported, nps if len(ds) % nps == 0 else 1)
+            gs.hbm_mib = reported * (nps if len(ds) % nps == 0 else 1)
         else:
             gs.hbm_mib = sum(d.hbm_mib for d in ds)
     n = len(gpus_by_parent)

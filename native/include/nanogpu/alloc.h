@@ -61,6 +61,13 @@ struct Device {
   int16_t healthy;      // 0 => never chosen
   int16_t xcds;         // XCDs backing this device (8 for an SPX MI355X, 1 in CPX)
   int32_t cus;          // compute units backing this device (256 for SPX MI355X)
+  // HBM pool: compute partitions that share one memory partition (CPX/QPX/DPX under
+  // NPS1, CPX under NPS2) draw from one pool. Every member mirrors the pool's
+  // mib_free/mib_total and every debit updates all members. -1: the device's own HBM.
+  int16_t pool;
+  int16_t pad16;
+  int32_t pad32;
+  int64_t mib_share;    // HBM a whole-device grant of a pooled member takes (pool / members)
 };
 
 struct Topology {

@@ -62,6 +62,41 @@ static inline bool hbm_fits(const Device& d, int64_t mib) {
   return mib <= 0 || d.mib_total <= 0 || d.mib_free >= mib;
 }
 
+// Adds `delta` MiB to device i's HBM, or to every member of its pool (mirrored state).
+static inline void mib_adjust(Device* devs, int n, int i, int64_t delta) {
+  if (devs[i].mib_total <= 0 || delta == 0) return;
+  const int16_t p = devs[i].pool;
+  if (p < 0) {
+    devs[i].mib_free += delta;
+    return;
+  }
+  for (int j = 0; j < n; ++j)
+    if (devs[j].pool == p) devs[j].mib_free += delta;
+}
+
+// HBM a whole-device grant takes: the device's own HBM, or its share of the pool.
+static inline int64_t whole_mib(const Device& d) {
+  if (d.mib_total <= 0) return 0;
+  return d.pool < 0 ? d.mib_total : d.mib_share;
+}
+
+// Pool-deduplicated HBM totals of a node (each pool counted once).
+static void hbm_totals(const Device* devs, int n, int64_t* total, int64_t* free_) {
+  uint64_t seen = 0;
+  *total = *free_ = 0;
+  for (int i = 0; i < n; ++i) {
+    const Device& d = devs[i];
+    if (d.mib_total <= 0) continue;
+    if (d.pool >= 0) {
+      const uint64_t bit = 1ULL << (d.pool & 63);
+      if (seen & bit) continue;
+      seen |= bit;
+    }
+    *total += d.mib_total;
+    *free_ += d.mib_free;
+  }
+}
+
 static inline float link_bw(const Topology* t, int a, int b) {
   if (!t || a < 0 || b < 0 || a >= t->n_gpus || b >= t->n_gpus) return 0.f;
   return t->link_bw[a * kMaxGpus + b];
@@ -89,6 +124,7 @@ struct SortDev {
   int64_t mib_free;
   int64_t mib_total;
   int32_t index;
+  int32_t pool;
 };
 
 struct SortDem {
@@ -130,7 +166,14 @@ static int32_t compat_choose(const Device* devs, int n, const Demand& d, const O
         if (free[j] >= d.c[c].pct && (d.c[c].mib <= 0 || devs[j].mib_total <= 0 || mfree[j] >= d.c[c].mib)) {
           plan->idx[c] = static_cast<int16_t>(j);
           free[j] -= d.c[c].pct;
-          if (devs[j].mib_total > 0) mfree[j] -= d.c[c].mib;
+          if (devs[j].mib_total > 0) {
+            if (devs[j].pool < 0) {
+              mfree[j] -= d.c[c].mib;
+            } else {
+              for (int k = 0; k < n; ++k)
+                if (devs[k].pool == devs[j].pool) mfree[k] -= d.c[c].mib;
+            }
+          }
           ++placed;
           break;
         }
@@ -142,7 +185,16 @@ static int32_t compat_choose(const Device* devs, int n, const Demand& d, const O
 
   SortDev sg[kMaxDevs];
   for (int i = 0; i < n; ++i)
-    sg[i] = SortDev{devs[i].pct_free, devs[i].remain_load, devs[i].mib_free, devs[i].mib_total, i};
+    sg[i] = SortDev{devs[i].pct_free, devs[i].remain_load, devs[i].mib_free, devs[i].mib_total, i, devs[i].pool};
+  auto sg_mib = [&](int i, int64_t mib) {  // pooled members mirror the pool's free HBM
+    if (sg[i].mib_total <= 0) return;
+    if (sg[i].pool < 0) {
+      sg[i].mib_free -= mib;
+      return;
+    }
+    for (int k = 0; k < n; ++k)
+      if (sg[k].pool == sg[i].pool) sg[k].mib_free -= mib;
+  };
   auto less = [&](int i, int j) {
     return sg[i].free + sg[i].remain * 50 < sg[j].free + sg[j].remain * 50;  // allocate.go:247
   };
@@ -166,7 +218,7 @@ static int32_t compat_choose(const Device* devs, int n, const Demand& d, const O
         if (!fits(i)) continue;
         indexes[cnt++] = sg[i].index;
         sg[i].free -= sd[j].pct;
-        if (sg[i].mib_total > 0) sg[i].mib_free -= sd[j].mib;
+        sg_mib(i, sd[j].mib);
         break;
       }
     } else {
@@ -174,7 +226,7 @@ static int32_t compat_choose(const Device* devs, int n, const Demand& d, const O
         if (!fits(i)) continue;
         indexes[cnt++] = sg[i].index;
         sg[i].free -= sd[j].pct;
-        if (sg[i].mib_total > 0) sg[i].mib_free -= sd[j].mib;
+        sg_mib(i, sd[j].mib);
         break;
       }
     }
@@ -304,7 +356,7 @@ int pick_share(Work& w, const Topology* t, const ContainerDemand& c, const Optio
 
 bool whole_free(const Device& d) {
   return d.healthy && d.pct_free == d.pct_total && d.pct_total > 0 &&
-         (d.mib_total <= 0 || d.mib_free == d.mib_total);
+         (d.mib_total <= 0 || (d.pool < 0 ? d.mib_free == d.mib_total : d.mib_free >= d.mib_share));
 }
 
 // Set score for whole-device groups (multi-GPU containers: TP/EP groups, RCCL rings).
@@ -442,7 +494,7 @@ static int32_t place_all(Work& w, const Topology* topo, const Demand& d, const O
       if (w.dev[i].mib_total > 0 && cd.mib > 0)
         pl->cost_mib += (spread ? -1 : 1) * (w.dev[i].mib_free - cd.mib) * 1000 / w.dev[i].mib_total;
       w.dev[i].pct_free -= cd.pct;
-      if (w.dev[i].mib_total > 0) w.dev[i].mib_free -= cd.mib;
+      mib_adjust(w.dev, w.n, i, -cd.mib);
       pl->idx[pl->total++] = static_cast<int16_t>(i);
       w.chosen[w.n_chosen++] = static_cast<int16_t>(i);
     } else {
@@ -451,7 +503,7 @@ static int32_t place_all(Work& w, const Topology* topo, const Demand& d, const O
       for (int a = 0; a < need; ++a) {
         Device& dv = w.dev[set[a]];
         dv.pct_free = 0;
-        if (dv.mib_total > 0) dv.mib_free = 0;
+        mib_adjust(w.dev, w.n, set[a], -whole_mib(dv));
         pl->idx[pl->total++] = static_cast<int16_t>(set[a]);
         w.chosen[w.n_chosen++] = static_cast<int16_t>(set[a]);
       }
@@ -537,12 +589,13 @@ static int32_t native_rate(const Device* devs, int n, const Demand& d, const Opt
   for (int i = 0; i < n; ++i) {
     pct_tot += after[i].pct_total;
     pct_used += after[i].pct_total - after[i].pct_free;
-    if (after[i].mib_total > 0) {
-      mib_tot += after[i].mib_total;
-      mib_used += after[i].mib_total - after[i].mib_free;
-    }
     if (after[i].pct_free == after[i].pct_total) ++full_free;
     load += devs[i].load_usage;
+  }
+  {
+    int64_t mfree = 0;
+    hbm_totals(after, n, &mib_tot, &mfree);
+    mib_used = mib_tot - mfree;
   }
   double util = pct_tot > 0 ? static_cast<double>(pct_used) / pct_tot : 0.0;
   if (mib_tot > 0) util = 0.5 * util + 0.5 * static_cast<double>(mib_used) / mib_tot;
@@ -600,25 +653,22 @@ static bool plan_shape_ok(int n, const Demand& d, const Plan& p) {
   return true;
 }
 
-// Whole-device entries (pct > 100) debit the full device; share entries debit (pct, mib).
-static inline void debit(Device& dv, const ContainerDemand& cd, int sign) {
+// Whole-device entries (pct > 100) debit the full device (and its HBM, or its share of
+// the HBM pool); share entries debit (pct, mib).
+static inline void debit(Device* devs, int n, int i, const ContainerDemand& cd, int sign) {
+  Device& dv = devs[i];
   if (cd.pct > kPercentPerDevice) {
-    if (sign < 0) {
-      dv.pct_free = 0;
-      if (dv.mib_total > 0) dv.mib_free = 0;
-    } else {
-      dv.pct_free = dv.pct_total;
-      if (dv.mib_total > 0) dv.mib_free = dv.mib_total;
-    }
+    dv.pct_free = sign < 0 ? 0 : dv.pct_total;
+    mib_adjust(devs, n, i, sign * whole_mib(dv));
     return;
   }
   dv.pct_free += sign * cd.pct;
-  if (dv.mib_total > 0) dv.mib_free += sign * cd.mib;
+  mib_adjust(devs, n, i, sign * cd.mib);
 }
 
 static inline bool can_debit(const Device& dv, const ContainerDemand& cd) {
   if (cd.pct > kPercentPerDevice)
-    return dv.pct_free == dv.pct_total && (dv.mib_total <= 0 || dv.mib_free == dv.mib_total);
+    return dv.pct_free == dv.pct_total && (dv.mib_total <= 0 || dv.mib_free >= whole_mib(dv));
   return dv.pct_free >= cd.pct && hbm_fits(dv, cd.mib);
 }
 
@@ -633,11 +683,11 @@ int32_t apply(Device* devs, int n, const Demand& d, const Plan& p) {
         for (int c2 = 0; c2 <= c; ++c2) {
           const int end = c2 == c ? k : p.off[c2 + 1];
           for (int k2 = p.off[c2]; k2 < end; ++k2)
-            if (p.idx[k2] >= 0) debit(devs[p.idx[k2]], d.c[c2], +1);
+            if (p.idx[k2] >= 0) debit(devs, n, p.idx[k2], d.c[c2], +1);
         }
         return kErrPlanNoLongerFits;
       }
-      debit(devs[i], d.c[c], -1);
+      debit(devs, n, i, d.c[c], -1);
     }
   }
   return kOk;
@@ -649,27 +699,42 @@ int32_t unapply(Device* devs, int n, const Demand& d, const Plan& p) {
     for (int k = p.off[c]; k < p.off[c + 1]; ++k) {
       const int i = p.idx[k];
       if (i < 0) continue;
-      debit(devs[i], d.c[c], +1);
+      debit(devs, n, i, d.c[c], +1);
       devs[i].pct_free = std::min(devs[i].pct_free, devs[i].pct_total);
-      if (devs[i].mib_total > 0) devs[i].mib_free = std::min(devs[i].mib_free, devs[i].mib_total);
     }
+  for (int i = 0; i < n; ++i)
+    if (devs[i].mib_total > 0) devs[i].mib_free = std::min(devs[i].mib_free, devs[i].mib_total);
   return kOk;
 }
 
 void frag_accumulate(const Device* devs, int n, int32_t min_request, FragStats* s) {
+  uint64_t pool_seen = 0, pool_partial = 0;
   for (int i = 0; i < n; ++i) {
     const Device& d = devs[i];
     if (!d.healthy) continue;
     ++s->devices;
     s->pct_free_total += d.pct_free;
-    s->mib_free_total += d.mib_total > 0 ? d.mib_free : 0;
+    const bool partial = d.pct_free > 0 && d.pct_free < d.pct_total;
+    if (d.mib_total > 0) {
+      if (d.pool < 0) {
+        s->mib_free_total += d.mib_free;
+        if (partial) s->mib_free_partial += d.mib_free;
+      } else {  // a pool counts once; its free HBM is "partial" if any member is partly used
+        const uint64_t bit = 1ULL << (d.pool & 63);
+        if (!(pool_seen & bit)) {
+          pool_seen |= bit;
+          s->mib_free_total += d.mib_free;
+        }
+        if (partial && !(pool_partial & bit)) {
+          pool_partial |= bit;
+          s->mib_free_partial += d.mib_free;
+        }
+      }
+    }
     const bool full = d.pct_free == d.pct_total;
     if (full) ++s->devices_full_free;
     if (d.pct_free < d.pct_total) ++s->devices_used;
-    if (d.pct_free > 0 && d.pct_free < d.pct_total) {
-      s->pct_free_partial += d.pct_free;
-      if (d.mib_total > 0) s->mib_free_partial += d.mib_free;
-    }
+    if (partial) s->pct_free_partial += d.pct_free;
     if (d.pct_free > 0 && d.pct_free < min_request) s->pct_stranded += d.pct_free;
   }
 }

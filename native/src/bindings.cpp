@@ -52,6 +52,9 @@ Device to_device(const py::dict& d) {
   v.healthy = get<bool>(d, "healthy", true) ? 1 : 0;
   v.xcds = get<int16_t>(d, "xcds", 0);
   v.cus = get<int32_t>(d, "cus", 0);
+  v.pool = get<int16_t>(d, "pool", -1);
+  v.mib_share = get<int64_t>(d, "mib_share", 0);
+  if (v.pool >= 0 && v.mib_share <= 0) v.mib_share = v.mib_total;
   return v;
 }
 
@@ -69,6 +72,8 @@ py::dict from_device(const Device& v) {
   d["healthy"] = v.healthy != 0;
   d["xcds"] = v.xcds;
   d["cus"] = v.cus;
+  d["pool"] = v.pool;
+  d["mib_share"] = v.mib_share;
   return d;
 }
 

@@ -18,7 +18,7 @@
 namespace nanogpu {
 
 static constexpr uint64_t kMagic = 0x4e414e4f47505531ULL;  // "NANOGPU1"
-static constexpr uint32_t kVersion = 3;
+static constexpr uint32_t kVersion = 4;  // 4: Device gained HBM pools
 
 static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 

@@ -60,7 +60,7 @@ def test_node_and_status_patches():
     assert p["metadata"]["labels"]["nano-gpu/compute-partition"] == "CPX"
     s = status_patch(t, advertise_percent=True)["status"]["capacity"]
     assert s[T.RESOURCE_GPU_PERCENT] == "6400"
-    assert int(s[T.RESOURCE_GPU_MEMORY]) == sum(d.hbm_mib for d in t.devices)
+    assert int(s[T.RESOURCE_GPU_MEMORY]) == 8 * 288 * 1024       # 8 HBM pools, not 64 partition views
     assert T.RESOURCE_GPU_PERCENT not in status_patch(t, advertise_percent=False)["status"]["capacity"]
 
 

@@ -131,3 +131,65 @@ def test_partial_plan_failure_restores_exactly_D5():
     rc = L.allocate_plan(nid, "b", [(50, 0), (0, 0), (40, 0)], [[0], [-1], [1]], True)
     assert rc != N.OK
     assert L.snapshot(nid)["devices"] == before and L.lookup("b") is None
+
+
+# ----------------------------------------------------------------------------- HBM pools
+def _pool_views(L, nid):
+    by = {}
+    for d in L.snapshot(nid)["devices"]:
+        if d["pool"] >= 0:
+            by.setdefault(d["pool"], set()).add((d["mib_free"], d["mib_total"]))
+    return by
+
+
+def test_cpx_partitions_share_the_gpu_hbm_pool():
+    """NPS1 + CPX: the 8 XCD partitions of a GPU draw from one 288 GB pool, so a 1-XCD pod can
+    take 100 GiB (a static 1/8 split would cap it at 36 GiB) while the pool is never
+    over-committed across siblings."""
+    t = synthetic_mi355x(1, "CPX")
+    pool = t.devices[0].hbm_mib
+    L, (nid,) = ledger_with(t)
+    big = 100 * 1024
+    placed = []
+    for k in range(3):
+        rc, plan = L.reserve(nid, f"m{k}", [(10, big)], BIN)
+        if rc == N.OK:
+            placed.append(plan[0][0])
+    assert len(placed) == 2                       # 2 x 100 GiB fit in 288 GB, the third does not
+    views = _pool_views(L, nid)
+    assert views == {0: {(pool - 2 * big, pool)}}  # every member mirrors the pool
+    f = L.frag(0)
+    assert f["mib_free_total"] == pool - 2 * big        # the pool is counted once, not 8 times
+    assert f["mib_free_partial"] == pool - 2 * big      # and it is partial (two members in use)
+    # a whole-partition grant (2 devices) takes 2 x (pool / 8)
+    rc, plan = L.reserve(nid, "w", [(200, 0)], BIN)
+    assert rc == N.OK and len(plan[0]) == 2
+    assert _pool_views(L, nid) == {0: {(pool - 2 * big - 2 * (pool // 8), pool)}}
+    for u in ("m0", "m1", "w"):
+        assert L.release(u) == N.OK
+    assert _pool_views(L, nid) == {0: {(pool, pool)}}
+
+
+@settings(max_examples=40, deadline=None)
+@given(st.lists(_demand, min_size=1, max_size=40), st.sampled_from([("CPX", "NPS1"), ("CPX", "NPS2"),
+                                                                    ("QPX", "NPS1"), ("DPX", "NPS2")]),
+       st.sampled_from([N.Policy.BINPACK, N.Policy.SPREAD, N.Policy.FIRSTFIT]), st.booleans(), st.integers(0, 99))
+def test_pool_mirrors_stay_consistent_under_churn(demands, modes, policy, compat, seed):
+    t = synthetic_mi355x(2, *modes)
+    L, (nid,) = ledger_with(t)
+    o = N.Options(policy, compat=compat, seed=seed)
+    rng = random.Random(seed)
+    live = []
+    for k, d in enumerate(demands):
+        if L.reserve(nid, f"p{k}", d, o)[0] == N.OK:
+            live.append(f"p{k}")
+        if live and rng.random() < 0.3:
+            L.release(live.pop(rng.randrange(len(live))))
+        for views in _pool_views(L, nid).values():
+            assert len(views) == 1                        # all members agree
+            (free, total), = views
+            assert 0 <= free <= total
+    for u in live:
+        L.release(u)
+    for d in L.snapshot(nid)["devices"]:
+        assert d["mib_free"] == d["mib_total"] and d["pct_free"] == d["pct_total"]

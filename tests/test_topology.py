@@ -49,7 +49,12 @@ def test_synthetic_8gpu_partition_modes(tmp_path, mode, parts):
     assert len(t.gpus) == 8 and len(t.devices) == 8 * parts
     for d in t.devices:
         assert d.cus == 256 // parts and d.xcds == 8 // parts
-        assert d.hbm_mib == (VRAM >> 20) // parts
+        # NPS1: every partition draws from its GPU's one 288 GB pool
+        assert d.hbm_mib == VRAM >> 20
+        if parts == 1:
+            assert d.pool == -1
+        else:
+            assert (d.pool, d.mib_share) == (d.gpu * 8, (VRAM >> 20) // parts)
     assert [d.part for d in t.devices[:parts]] == list(range(parts))
     assert {g.numa for g in t.gpus} == {0, 1}
     # full xGMI mesh between physical GPUs, 76 GB/s per link
@@ -59,12 +64,17 @@ def test_synthetic_8gpu_partition_modes(tmp_path, mode, parts):
     assert all(g.xgmi_peers == 7 for g in t.gpus)
 
 
-def test_cpx_nps2_hbm_share(tmp_path):
+def test_cpx_nps2_hbm_pools(tmp_path):
     write_mi355x_sysfs(tmp_path, 2, "CPX", "NPS2")
     t = from_host_json(discover(tmp_path))
-    # each CPX partition reports its NPS2 half; 4 partitions share a half
-    assert all(d.hbm_mib == ((VRAM // 2) >> 20) * 2 // 8 for d in t.devices)
-    assert t.gpus[0].hbm_mib == sum(d.hbm_mib for d in t.devices if d.gpu == 0)
+    # each CPX partition reports its NPS2 half; 4 partitions share each half as one pool
+    half = (VRAM // 2) >> 20
+    assert all(d.hbm_mib == half and d.mib_share == half // 4 for d in t.devices)
+    assert [d.pool for d in t.devices[:8]] == [0, 0, 0, 0, 1, 1, 1, 1]
+    assert t.gpus[0].hbm_mib == 2 * half and t.hbm_capacity_mib() == 4 * half
+    write_mi355x_sysfs(tmp_path / "dpx", 1, "DPX", "NPS2")     # one compute partition per memory partition
+    t2 = from_host_json(discover(tmp_path / "dpx"))
+    assert [(d.pool, d.hbm_mib) for d in t2.devices] == [(-1, half), (-1, half)]
 
 
 def test_hidden_gpus_and_degraded_link(tmp_path):
