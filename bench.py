@@ -15,7 +15,10 @@ What one step is (all of it inside the timed region):
   * after the burst the whole burst is deleted and the pod controller releases every
     share from the ledger (the create/delete churn of BASELINE config 5).
 `value` = pods bound per second over the K timed steps (whole job, all ranks).
-`--inproc-driver` runs the stand-in inside the extender's event loop instead.
+The stand-in is C++ by default (kube-scheduler is compiled Go; the Python stand-in's
+interpreter time per pod exceeded the extender's and capped the rate): `--driver python`
+selects the Python one, `--inproc-driver` runs a Python stand-in inside the extender's
+event loop.
 
 Scaling (`--gpus N`, one torchrun rank per GPU): every rank is one extender worker; all
 workers share ONE native ledger in /dev/shm (the SO_REUSEPORT replica design of
@@ -62,6 +65,8 @@ def parse_args():
     ap.add_argument("--profile-out", default="", help="cProfile the timed steps (rank 0) into this file")
     ap.add_argument("--busy-poll-us", type=int, default=int(os.environ.get("NANOGPU_BUSY_POLL_US", "0")),
                     help="native front door busy-poll window")
+    ap.add_argument("--driver", default="native", choices=["native", "python"],
+                    help="kube-scheduler stand-in: C++ (native/src/schedsim.cpp) or the Python threaded one")
     ap.add_argument("--inproc-driver", action="store_true",
                     help="run the kube-scheduler stand-in inside the extender process (default: own process)")
     return ap.parse_args()
@@ -198,9 +203,10 @@ def driver_main(conn) -> None:
     extender's address once, then for every step schedules that step's pods (already
     created in the API server by the main process) and returns the driver stats. The
     scheduling cycle is serial on a blocking connection; binds run on a thread pool."""
-    from nanogpu.sim.driver import ThreadedSchedulerDriver
+    from nanogpu.sim.driver import NativeSchedulerDriver, ThreadedSchedulerDriver
 
     cfg = conn.recv()
+    cls = ThreadedSchedulerDriver if cfg.get("driver") == "python" else NativeSchedulerDriver
 
     def serve() -> None:
         while True:
@@ -209,8 +215,11 @@ def driver_main(conn) -> None:
                 break
             step = msg[1]
             pods = burst(cfg["rank"], cfg["world"], cfg["pods"], step, 7)
-            drv = ThreadedSchedulerDriver("127.0.0.1", cfg["port"], cfg["names"], cfg["caps"],
-                                          bind_threads=min(32, cfg["inflight"]), seed=step * 1009 + cfg["rank"])
+            drv = cls("127.0.0.1", cfg["port"], cfg["names"], cfg["caps"],
+                      # native: connections of the epoll binder (a bind leaves as soon as its host is
+                      # chosen, as kube-scheduler's per-pod bind goroutines); Python: pool threads
+                      bind_threads=256 if cls is NativeSchedulerDriver else min(32, cfg["inflight"]),
+                      seed=step * 1009 + cfg["rank"])
             stats = drv.run(pods)
             drv.close()
             conn.send(stats.summary())
@@ -259,22 +268,26 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
     loop = asyncio.get_running_loop()
     if conn is not None:
         conn.send({"port": rt.bound_port, "names": names, "caps": caps, "rank": d.rank, "world": d.world,
-                   "pods": args.pods, "inflight": args.inflight_binds})
+                   "pods": args.pods, "inflight": args.inflight_binds, "driver": args.driver})
 
     async def one_step(step: int, timed: bool) -> dict:
         pods = bursts.pop(step)
+        tc = time.perf_counter()
         if conn is not None:
             # the pods are created in the API server (this process), then the scheduler
             # process schedules them through the extender's HTTP front door
             for p in pods:
                 await api.create_pod(p)
+            tc = time.perf_counter() - tc
             conn.send(("step", step))
             summary = await loop.run_in_executor(None, conn.recv)
         else:
             # one kube-scheduler stand-in per rank; distinct tie-break streams per rank
             drv = SchedulerDriver(client, api, names, caps, max_inflight_binds=args.inflight_binds,
                                   seed=step * 1009 + d.rank)
+            tc = 0.0
             summary = (await drv.run(pods)).summary()
+        ts = time.perf_counter()
         # all ranks finished their share of the burst: peak occupancy
         d.barrier()
         frag = rt.state.frag(min(SIZES))
@@ -291,7 +304,9 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
                 break
             await asyncio.sleep(0.0005)
         await pod_ctrl.queue.drain(5.0)
-        return {"stats": summary, "frag": frag}
+        phases = {"create_ms": 1e3 * tc, "schedule_ms": 1e3 * summary["span_s"],
+                  "release_ms": 1e3 * (time.perf_counter() - ts)}
+        return {"stats": summary, "frag": frag, "phases": phases}
 
     from nanogpu.app import tune_gc
 
@@ -307,22 +322,26 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
 
         prof = cProfile.Profile()
         prof.enable()
+    cpu0 = time.process_time()
     t0 = time.perf_counter()
     for s in range(args.steps):
         r = await one_step(s, True)
         results["steps"].append(r["stats"])
         results["frag"].append(r["frag"])
+        results.setdefault("phases", []).append(r["phases"])
     if prof is not None:
         import io
         import pstats
 
         prof.disable()
         buf = io.StringIO()
-        pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(45)
+        pstats.Stats(prof, stream=buf).sort_stats(os.environ.get("NANOGPU_PROF_SORT", "tottime")).print_stats(45)
         Path(args.profile_out).write_text(buf.getvalue())
     d.barrier()
     d.sync()
     elapsed = time.perf_counter() - t0
+    results["cpu_us_per_pod"] = 1e6 * (time.process_time() - cpu0) / max(
+        1, sum(st["scheduled"] for st in results["steps"]))
     binds = sorted(s["dur_ms"] for s in rt.tracer.dump(10 ** 9, "bind") if s["ok"])
     results["elapsed_s"] = elapsed
     results["bind_ms"] = binds
@@ -331,6 +350,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
         ns = rt.native.fe.stats()
         results["native"] = {v: round(1e6 * ns[v]["seconds_total"] / max(1, ns[v]["count"]), 2)
                              for v in ("filter", "priorities")}
+    results["phase_ms"] = {k: round(statistics.mean(p[k] for p in results["phases"]), 2)
+                           for k in ("create_ms", "schedule_ms", "release_ms")} if results.get("phases") else None
     results["failed"] = sum(s["failed"] for s in results["steps"])
     results["bind_errors"] = sum(s["bind_errors"] for s in results["steps"])
     await client.close()
@@ -407,6 +428,9 @@ def main() -> int:
             "stranded_pct": round(statistics.mean(f["stranded_pct"] for f in fr), 3) if fr else None,
             "scheduled": scheduled, "failed": failed, "bind_retries": bind_errors, "gpu": gpu_info,
             "native_verb_mean_us": res.get("native"),
+            "phase_ms_per_step_rank0": res.get("phase_ms"),
+            # CPU time of the rank-0 extender process (all its threads) per pod it handled
+            "extender_cpu_us_per_pod_rank0": round(res.get("cpu_us_per_pod", 0.0), 1),
         }
         print(json.dumps(line), flush=True)
         if args.json_out:

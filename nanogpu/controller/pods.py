@@ -30,57 +30,43 @@ class PodController:
         self.workers = max(1, workers)
         self.metrics = metrics
         self._tasks: list[asyncio.Task] = []
-        self._uid_of: dict[str, str] = {}
-        self._sharing: dict[str, bool] = {}
         informer.add_handler(self._on_event)
 
     # ---------------------------------------------------------------- handlers
+    def _release(self, uid: str) -> None:
+        if self.state.release_uid(uid) and self.metrics:
+            self.metrics.pods_released.inc()
+
     def _on_event(self, etype: str, pod: dict, old: dict | None) -> None:
-        # hot: every pod event of the cluster passes here, so fields are read once
+        # hot: every pod event of the cluster passes here (four per scheduled pod), so the
+        # cheap tests come first and the container limits are parsed only when they decide
         m = pod.get("metadata") or {}
         uid = m.get("uid", "")
-        sharing = self._sharing.get(uid) if uid else None
-        if sharing is None:
-            sharing = pu.is_gpu_sharing(pod)
-            if uid:
-                if len(self._sharing) > 262144:
-                    self._sharing.clear()
-                self._sharing[uid] = sharing
-        if not sharing:                        # reference FilterFunc (controller.go:90-106)
-            return
-        key = f"{m.get('namespace', 'default')}/{m.get('name', '')}"
+        if old is not None:
+            ouid = (old.get("metadata") or {}).get("uid", "")
+            if ouid and ouid != uid:
+                self._release(ouid)            # same name, new object: the previous one is gone
         if etype == "DELETED":
-            # Release right away: the object is gone from the store, the worker would find nothing.
-            if self.state.release_uid(uid) and self.metrics:
-                self.metrics.pods_released.inc()
+            # D3: release right away, the object is gone from the store (a pod that never
+            # held a share is simply not in the ledger)
+            self._release(uid)
             self.state.forget(uid)
-            self._uid_of.pop(key, None)
-            self._sharing.pop(uid, None)
             return
-        prev = self._uid_of.get(key)
-        if prev != uid:
-            if prev:
-                # same name, new object: the previous incarnation is gone
-                self.state.release_uid(prev)
-            self._uid_of[key] = uid
-        spec = pod.get("spec") or {}
-        node = spec.get("nodeName")
+        node = (pod.get("spec") or {}).get("nodeName")
         completed = bool(m.get("deletionTimestamp")) or \
             (pod.get("status") or {}).get("phase") in ("Succeeded", "Failed")
-        if etype == "ADDED":
-            # only pods already placed (restart rebuild, someone else's bind) need work; a
-            # pending pod is the extender's own business until it is bound
-            if node or completed:
-                self.queue.add(key)
+        if not node and not completed:
+            return                             # pending: the extender's own business until bound
+        if self.state.known(uid):
+            if completed:                                                        # controller.go:303-306
+                self.queue.add(f"{m.get('namespace', 'default')}/{m.get('name', '')}")
             return
-        if not completed and not node:
-            return                                 # still pending: nothing to account yet
-        known = self.state.known(uid)
-        if known and completed:                                                  # controller.go:303-306
-            self.queue.add(key)
-        elif not known and not completed and not self.state.released(uid) and \
-                (m.get("annotations") or {}).get(T.ANNOTATION_GPU_ASSUME) == "true":     # :307-310
-            self.queue.add(key)
+        if completed or self.state.released(uid):
+            return
+        # bound by someone else / found at restart (controller.go:307-310); reference
+        # FilterFunc (controller.go:90-106) keeps only GPU-sharing pods
+        if (m.get("annotations") or {}).get(T.ANNOTATION_GPU_ASSUME) == "true" and pu.is_gpu_sharing(pod):
+            self.queue.add(f"{m.get('namespace', 'default')}/{m.get('name', '')}")
 
     # ---------------------------------------------------------------- worker
     async def _sync(self, key: str) -> None:

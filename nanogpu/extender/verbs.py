@@ -21,7 +21,7 @@ from collections import OrderedDict
 from .. import types as T
 from ..k8s import podutil as pu
 from ..k8s.client import ApiError
-from ..obs import Metrics, Tracer
+from ..obs import Metrics, Span, Tracer
 from ..state.cluster import N, ClusterState, SchedulingError
 from .wire import BindingArgs, ExtenderArgs, binding_result, filter_result, priority_list
 
@@ -62,6 +62,13 @@ class Extender:
         self.record_events = record_events
         self.pods = PodCache()
         self._bg: set[asyncio.Task] = set()
+        m = self.metrics
+        # labelled children the bind path touches on every pod
+        self._m_bind_latency = m.child(m.verb_latency, "bind")
+        self._m_bind_ok = m.child(m.verb_total, "bind", "ok")
+        self._m_bind_err = m.child(m.verb_total, "bind", "error")
+        self._m_patch = m.child(m.bind_phase, "patch")
+        self._m_binding = m.child(m.bind_phase, "binding")
 
     # ------------------------------------------------------------------ filter
     def filter(self, body) -> dict:
@@ -171,25 +178,35 @@ class Extender:
 
     async def bind_prepared(self, p: dict) -> dict:
         """Bind whose ledger reservation already ran in the native front door
-        (native/src/frontend.cpp::prepare_bind); only the API writes and commit remain."""
+        (native/src/frontend.cpp::prepare_bind); only the API writes and commit remain.
+        Runs once per pod at the burst rate, so it records its span and metrics directly."""
         t0 = time.perf_counter()
+        ns, name = p["ns"], p["name"]
+        sp = Span("bind", f"{ns}/{name}", time.time())
         err = ""
-        with self.tracer.span("bind", f"{p['ns']}/{p['name']}") as sp:
-            try:
-                rc = p["rc"]
-                if rc not in (N.OK, N.OK_EXISTING):
-                    raise self.state.reserve_error(p["demand"], p["node"], rc)
-                sp.phases["reserve"] = 0.0
-                await self._write(p["ns"], p["name"], p["uid"], p["node"], p["containers"], p["plan"],
-                                  rc == N.OK, sp, (p["ns"], p["name"]))
-            except (SchedulingError, ApiError, asyncio.TimeoutError, OSError) as e:
-                err = str(e) or e.__class__.__name__
-                sp.ok = False
-                sp.note = err
-        self.metrics.child(self.metrics.verb_latency, "bind").observe(time.perf_counter() - t0)
-        self.metrics.child(self.metrics.verb_total, "bind", "error" if err else "ok").inc()
+        try:
+            rc = p["rc"]
+            if rc not in (N.OK, N.OK_EXISTING):
+                raise self.state.reserve_error(p["demand"], p["node"], rc)
+            sp.phases["reserve"] = 0.0
+            await self._write(ns, name, p["uid"], p["node"], p["containers"], p["plan"], rc == N.OK, sp, (ns, name))
+        except (SchedulingError, ApiError, asyncio.TimeoutError, OSError) as e:
+            err = str(e) or e.__class__.__name__
+            sp.ok = False
+            sp.note = err
+        except Exception as e:
+            sp.ok = False
+            sp.note = repr(e)
+            raise
+        finally:
+            sp.dur = time.perf_counter() - t0
+            self.tracer.buf.append(sp)
+        self._m_bind_latency.observe(sp.dur)
         if err:
-            log.info("bind %s/%s -> %s failed: %s", p["ns"], p["name"], p["node"], err)
+            self._m_bind_err.inc()
+            log.info("bind %s/%s -> %s failed: %s", ns, name, p["node"], err)
+        else:
+            self._m_bind_ok.inc()
         return binding_result(err)
 
     async def _write(self, ns: str, name: str, uid: str, node: str, names: list[str], plan, fresh: bool, sp,
@@ -209,8 +226,8 @@ class Extender:
                     raise
             t4 = time.perf_counter()
             sp.phases["patch"], sp.phases["binding"] = t3 - t2, t4 - t3
-            self.metrics.child(self.metrics.bind_phase, "patch").observe(t3 - t2)
-            self.metrics.child(self.metrics.bind_phase, "binding").observe(t4 - t3)
+            self._m_patch.observe(t3 - t2)
+            self._m_binding.observe(t4 - t3)
         except BaseException as e:
             # D2: the reference leaves the cache debited when the binding POST fails.
             if not fresh:

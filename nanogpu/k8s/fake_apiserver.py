@@ -313,6 +313,8 @@ class FakeKubeStore:
 class InProcKube:
     """`KubeClient`-compatible facade over a FakeKubeStore (no sockets)."""
 
+    completes_inline = True   # calls need no running Task (see NativeServer._eager)
+
     def __init__(self, store: FakeKubeStore):
         self.store = store
         self.calls = 0

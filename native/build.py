@@ -26,7 +26,7 @@ ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 ARCH = os.environ.get("NANOGPU_OFFLOAD_ARCH", "gfx950")
 
-CORE_SOURCES = ["alloc.cpp", "ledger.cpp", "topo.cpp", "json.cpp", "frontend.cpp"]
+CORE_SOURCES = ["alloc.cpp", "ledger.cpp", "topo.cpp", "json.cpp", "frontend.cpp", "schedsim.cpp"]
 
 
 def _pybind_includes() -> list[str]:

@@ -87,7 +87,11 @@ class Frontend {
   // Drains requests waiting for Python (non-blocking).
   std::vector<PyRequest> take();
   // Completes request `id` (any thread). Unknown ids (connection gone) are dropped.
-  void respond(uint64_t id, int status, const std::string& content_type, const std::string& body);
+  // notify=false queues the response without waking its worker: the caller batches
+  // several and wakes each worker once with wake_workers().
+  void respond(uint64_t id, int status, const std::string& content_type, const std::string& body,
+               bool notify = true);
+  void wake_workers();
   void stop();
 
   VerbStats filter_stats, prio_stats, py_stats, bind_stats;   // bind_stats: native reserve half

@@ -1,0 +1,52 @@
+// Native kube-scheduler stand-in for the benchmark harness.
+//
+// kube-scheduler is a compiled Go binary: its per-pod cost in front of an extender is a
+// few microseconds of JSON work plus the extender round trips. The Python stand-in
+// (nanogpu/sim/driver.py::ThreadedSchedulerDriver) spends ~150 us of interpreter time per
+// pod, so at thousands of pods/s it — not the extender — set the measured rate. This is the
+// same protocol loop in C++:
+//   * one serial scheduling cycle on a keep-alive connection: resource-fit pre-filter
+//     (NodeResourcesFit on the extended resource), POST /scheduler/filter with NodeNames
+//     (nodeCacheCapable), POST /scheduler/priorities when more than one node fits, highest
+//     score wins, ties broken uniformly at random;
+//   * binds leave as soon as their host is chosen (kube-scheduler's asynchronous binding
+//     cycle, a goroutine per pod): one epoll thread multiplexes up to `bind_threads`
+//     keep-alive connections, POST /scheduler/bind;
+//   * a failed attempt goes back to the queue with exponential backoff, up to max_attempts.
+// Times are steady_clock seconds (the clock of Python's time.perf_counter()).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace nanogpu::sim {
+
+struct SimPod {
+  std::string json;      // the Pod object as sent in ExtenderArgs.Pod
+  std::string ns, name, uid;
+  int64_t need = 0;      // Σ container gpu-percent (the pre-filter's request)
+};
+
+struct SimConfig {
+  std::string host = "127.0.0.1";
+  int port = 0;
+  std::vector<std::string> nodes;
+  std::vector<int64_t> capacity;   // per node; empty = no resource pre-filter
+  int bind_threads = 256;   // max concurrent bind connections
+  uint64_t seed = 0;
+  int max_attempts = 8;
+  double backoff_s = 0.001;
+};
+
+struct SimResult {
+  int64_t scheduled = 0, failed = 0, bind_errors = 0, unschedulable_attempts = 0;
+  double t_first_filter = 0.0, t_last_bind = 0.0;
+  std::vector<double> bind_latencies, e2e_latencies;
+  std::vector<std::string> node_of;   // per pod; "" = not scheduled
+  std::vector<std::string> last_error;
+};
+
+SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods);
+
+}  // namespace nanogpu::sim

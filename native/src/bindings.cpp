@@ -10,6 +10,7 @@
 #include "nanogpu/frontend.h"
 #include "nanogpu/gosort.h"
 #include "nanogpu/ledger.h"
+#include "nanogpu/schedsim.h"
 #include "nanogpu/topo.h"
 
 namespace py = pybind11;
@@ -481,11 +482,12 @@ PYBIND11_MODULE(_native, m) {
              return out;
            })
       .def("respond",
-           [](Frontend& f, uint64_t id, int status, const std::string& ctype, const py::bytes& body) {
+           [](Frontend& f, uint64_t id, int status, const std::string& ctype, const py::bytes& body, bool notify) {
              std::string b = body;
-             py::gil_scoped_release nogil;
-             f.respond(id, status, ctype, b);
-           })
+             f.respond(id, status, ctype, b, notify);   // a short mailbox lock: no GIL round trip
+           },
+           py::arg("id"), py::arg("status"), py::arg("content_type"), py::arg("body"), py::arg("notify") = true)
+      .def("flush", &Frontend::wake_workers, "wake the workers holding responses queued with notify=False")
       .def("stop", &Frontend::stop, py::call_guard<py::gil_scoped_release>())
       .def("pod_cache_size", &Frontend::pod_cache_size)
       .def("stats", [](Frontend& f) {
@@ -510,4 +512,50 @@ PYBIND11_MODULE(_native, m) {
         return d;
       });
   m.def("mono_now", &mono_now);
+  m.def(
+      "drive_scheduler",
+      [](const std::string& host, int port, const std::vector<std::tuple<py::bytes, std::string, std::string, std::string,
+                                                                       int64_t>>& pods,
+         const std::vector<std::string>& nodes, const std::vector<int64_t>& capacity, int bind_threads, uint64_t seed,
+         int max_attempts, double backoff_s) {
+        sim::SimConfig cfg;
+        cfg.host = host;
+        cfg.port = port;
+        cfg.nodes = nodes;
+        cfg.capacity = capacity;
+        cfg.bind_threads = bind_threads;
+        cfg.seed = seed;
+        cfg.max_attempts = max_attempts;
+        cfg.backoff_s = backoff_s;
+        if (!capacity.empty() && capacity.size() != nodes.size())
+          throw py::value_error("capacity must be empty or one entry per node");
+        std::vector<sim::SimPod> ps(pods.size());
+        for (size_t i = 0; i < pods.size(); ++i) {
+          ps[i].json = std::get<0>(pods[i]);
+          ps[i].ns = std::get<1>(pods[i]);
+          ps[i].name = std::get<2>(pods[i]);
+          ps[i].uid = std::get<3>(pods[i]);
+          ps[i].need = std::get<4>(pods[i]);
+        }
+        sim::SimResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = sim::drive(cfg, ps);
+        }
+        py::dict d;
+        d["scheduled"] = r.scheduled;
+        d["failed"] = r.failed;
+        d["bind_errors"] = r.bind_errors;
+        d["unschedulable_attempts"] = r.unschedulable_attempts;
+        d["t_first_filter"] = r.t_first_filter;
+        d["t_last_bind"] = r.t_last_bind;
+        d["bind_latencies"] = r.bind_latencies;
+        d["e2e_latencies"] = r.e2e_latencies;
+        d["node_of"] = r.node_of;
+        d["last_error"] = r.last_error;
+        return d;
+      },
+      py::arg("host"), py::arg("port"), py::arg("pods"), py::arg("nodes"), py::arg("capacity"),
+      py::arg("bind_threads") = 16, py::arg("seed") = 0, py::arg("max_attempts") = 8, py::arg("backoff_s") = 0.001,
+      "kube-scheduler stand-in (native/src/schedsim.cpp): schedule `pods` through the extender at host:port");
 }

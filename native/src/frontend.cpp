@@ -200,6 +200,7 @@ struct Frontend::Worker {
   std::unordered_map<uint64_t, std::unique_ptr<Conn>> conns;   // by conn id
   std::mutex mb_mu;
   std::vector<std::pair<uint64_t, std::string>> mailbox;       // (conn id, response bytes)
+  std::atomic<bool> unsignalled{false};                         // queued with notify=false
   uint64_t next_conn = 1;
 };
 
@@ -287,7 +288,8 @@ std::vector<PyRequest> Frontend::take() {
   return out;
 }
 
-void Frontend::respond(uint64_t id, int status, const std::string& content_type, const std::string& body) {
+void Frontend::respond(uint64_t id, int status, const std::string& content_type, const std::string& body,
+                       bool notify) {
   const int widx = static_cast<int>(id & 0xff);
   if (widx < 0 || widx >= static_cast<int>(workers_.size())) return;
   Worker* w = workers_[widx].get();
@@ -300,8 +302,20 @@ void Frontend::respond(uint64_t id, int status, const std::string& content_type,
     std::lock_guard<std::mutex> g(w->mb_mu);
     w->mailbox.emplace_back(id >> 8, std::move(r));
   }
+  if (!notify) {
+    w->unsignalled.store(true, std::memory_order_release);
+    return;
+  }
   uint64_t one = 1;
   (void)!write(w->efd, &one, sizeof(one));
+}
+
+void Frontend::wake_workers() {
+  for (auto& w : workers_) {
+    if (!w->unsignalled.exchange(false, std::memory_order_acq_rel)) continue;
+    uint64_t one = 1;
+    (void)!write(w->efd, &one, sizeof(one));
+  }
 }
 
 size_t Frontend::pod_cache_size() const {

@@ -1,0 +1,536 @@
+// Native kube-scheduler stand-in (see schedsim.h).
+#include "nanogpu/schedsim.h"
+
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cctype>
+#include <cerrno>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <queue>
+#include <random>
+#include <stdexcept>
+#include <thread>
+#include <unordered_map>
+
+#include "nanogpu/json.h"
+
+namespace nanogpu::sim {
+
+namespace {
+
+double now_s() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return static_cast<double>(ts.tv_sec) + 1e-9 * static_cast<double>(ts.tv_nsec);
+}
+
+// Pops one complete HTTP/1.1 response off the front of `buf`.
+// 1 = done (status/body/close set), 0 = incomplete, -1 = malformed or unsupported.
+int take_response(std::string* buf, int* status, std::string* body, bool* close) {
+  size_t hdr_end = buf->find("\r\n\r\n");
+  if (hdr_end == std::string::npos) return buf->size() > (64u << 10) ? -1 : 0;
+  std::string_view head(buf->data(), hdr_end);
+  size_t sp = head.find(' ');
+  if (sp == std::string_view::npos || head.size() < sp + 4) return -1;
+  *status = std::atoi(std::string(head.substr(sp + 1, 3)).c_str());
+  size_t len = 0;
+  *close = false;
+  size_t pos = head.find("\r\n");
+  while (pos != std::string_view::npos && pos < head.size()) {
+    size_t next = head.find("\r\n", pos + 2);
+    std::string_view line = head.substr(pos + 2, (next == std::string_view::npos ? head.size() : next) - pos - 2);
+    size_t colon = line.find(':');
+    if (colon != std::string_view::npos) {
+      std::string key(line.substr(0, colon));
+      for (char& c : key) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+      std::string_view v = line.substr(colon + 1);
+      while (!v.empty() && v.front() == ' ') v.remove_prefix(1);
+      if (key == "content-length") len = static_cast<size_t>(std::strtoull(std::string(v).c_str(), nullptr, 10));
+      else if (key == "connection" && (v.substr(0, 5) == "close" || v.substr(0, 5) == "Close")) *close = true;
+      else if (key == "transfer-encoding") return -1;   // the extender always sends a length
+    }
+    pos = next;
+  }
+  const size_t body0 = hdr_end + 4;
+  if (buf->size() < body0 + len) return 0;
+  body->assign(*buf, body0, len);
+  buf->erase(0, body0 + len);
+  return 1;
+}
+
+int open_socket(const std::string& host, int port, bool nonblock) {
+  int fd = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC | (nonblock ? SOCK_NONBLOCK : 0), 0);
+  if (fd < 0) return -1;
+  int one = 1;
+  ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons(static_cast<uint16_t>(port));
+  if (::inet_pton(AF_INET, host.c_str(), &a.sin_addr) != 1 ||
+      (::connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof a) != 0 && !(nonblock && errno == EINPROGRESS))) {
+    ::close(fd);
+    return -1;
+  }
+  return fd;
+}
+
+std::string post_request(std::string_view host, std::string_view path, std::string_view body) {
+  std::string r;
+  r.reserve(body.size() + 128);
+  r.append("POST ").append(path).append(" HTTP/1.1\r\nHost: ").append(host);
+  r.append("\r\nContent-Type: application/json\r\nContent-Length: ").append(std::to_string(body.size()));
+  r.append("\r\n\r\n").append(body);
+  return r;
+}
+
+// Blocking HTTP/1.1 client on one keep-alive connection; reconnects after any error.
+class Conn {
+ public:
+  Conn(std::string host, int port) : host_(std::move(host)), port_(port) {}
+  ~Conn() { close_fd(); }
+  Conn(const Conn&) = delete;
+  Conn& operator=(const Conn&) = delete;
+
+  // POST `body` to `path`; fills status and response body. false = transport error.
+  bool post(std::string_view path, std::string_view body, int* status, std::string* out) {
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      if (fd_ < 0 && !connect_fd()) return false;
+      req_ = post_request(host_, path, body);
+      if (send_all(req_) && read_response(status, out)) return true;
+      close_fd();   // stale keep-alive connection: one fresh attempt
+    }
+    return false;
+  }
+
+ private:
+  bool connect_fd() {
+    fd_ = open_socket(host_, port_, false);
+    buf_.clear();
+    return fd_ >= 0;
+  }
+  void close_fd() {
+    if (fd_ >= 0) ::close(fd_);
+    fd_ = -1;
+    buf_.clear();
+  }
+  bool send_all(const std::string& s) {
+    size_t off = 0;
+    while (off < s.size()) {
+      ssize_t n = ::send(fd_, s.data() + off, s.size() - off, MSG_NOSIGNAL);
+      if (n < 0 && errno == EINTR) continue;
+      if (n <= 0) return false;
+      off += static_cast<size_t>(n);
+    }
+    return true;
+  }
+  bool fill() {
+    char tmp[65536];
+    for (;;) {
+      ssize_t n = ::recv(fd_, tmp, sizeof tmp, 0);
+      if (n < 0 && errno == EINTR) continue;
+      if (n <= 0) return false;
+      buf_.append(tmp, static_cast<size_t>(n));
+      return true;
+    }
+  }
+  bool read_response(int* status, std::string* out) {
+    bool close = false;
+    int rc;
+    while ((rc = take_response(&buf_, status, out, &close)) == 0)
+      if (!fill()) return false;
+    if (rc < 0) return false;
+    if (close) close_fd();
+    return true;
+  }
+
+  std::string host_;
+  int port_;
+  int fd_ = -1;
+  std::string buf_, req_;
+};
+
+struct Ready {
+  double t;
+  uint64_t seq;
+  size_t pod;
+  bool operator>(const Ready& o) const { return t != o.t ? t > o.t : seq > o.seq; }
+};
+
+struct BindJob {
+  size_t pod;
+  int node;
+};
+
+}  // namespace
+
+SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods) {
+  SimResult r;
+  const size_t n_pods = pods.size(), n_nodes = cfg.nodes.size();
+  r.node_of.assign(n_pods, std::string());
+  r.last_error.assign(n_pods, std::string());
+  r.bind_latencies.reserve(n_pods);
+  r.e2e_latencies.reserve(n_pods);
+  std::unordered_map<std::string, int> node_index;
+  for (size_t i = 0; i < n_nodes; ++i) node_index.emplace(cfg.nodes[i], static_cast<int>(i));
+  const bool fit = !cfg.capacity.empty();
+  std::vector<int64_t> requested(n_nodes, 0);
+
+  auto names_json = [&](const std::vector<int>& idx) {
+    std::string s = "[";
+    for (size_t k = 0; k < idx.size(); ++k) {
+      if (k) s.push_back(',');
+      json::append_quoted(&s, cfg.nodes[idx[k]]);
+    }
+    s.push_back(']');
+    return s;
+  };
+  std::vector<int> all(n_nodes);
+  for (size_t i = 0; i < n_nodes; ++i) all[i] = static_cast<int>(i);
+  const std::string all_json = names_json(all);
+
+  std::mutex mu;
+  std::condition_variable cv;
+  std::priority_queue<Ready, std::vector<Ready>, std::greater<Ready>> ready;
+  std::deque<BindJob> jobs;
+  bool stop = false;   // the cycle is done: the binder exits once its binds finish
+  uint64_t seq = 0;
+  int64_t remaining = static_cast<int64_t>(n_pods);
+  std::vector<int> attempts(n_pods, 0);
+  const double t_enqueue = now_s();
+  for (size_t i = 0; i < n_pods; ++i) ready.push({0.0, seq++, i});
+
+  // mu held
+  auto requeue = [&](size_t i) {
+    if (attempts[i] < cfg.max_attempts) {
+      ready.push({now_s() + cfg.backoff_s * static_cast<double>(1u << std::min(attempts[i], 20)), seq++, i});
+    } else {
+      ++r.failed;
+      --remaining;
+    }
+    cv.notify_all();
+  };
+
+  // Binding cycle: kube-scheduler starts a goroutine per bind, so a bind goes out the
+  // moment its host is chosen. One epoll thread multiplexes up to `bind_threads`
+  // keep-alive connections (opened on demand) instead of a thread per request.
+  const int efd = ::eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
+  const int ep = ::epoll_create1(EPOLL_CLOEXEC);
+  if (efd < 0 || ep < 0) throw std::runtime_error("schedsim: eventfd/epoll_create1 failed");
+  {
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.u64 = UINT64_MAX;
+    ::epoll_ctl(ep, EPOLL_CTL_ADD, efd, &ev);
+  }
+  auto wake = [&] {
+    uint64_t one = 1;
+    (void)!::write(efd, &one, sizeof one);
+  };
+
+  // a finished bind (mu not held)
+  auto complete = [&](const BindJob& job, int status, const std::string* body, const char* transport, double t0) {
+    std::string err;
+    const double t1 = now_s();
+    if (transport) {
+      err = transport;
+    } else {
+      json::Doc doc;
+      if (!doc.parse(*body) || !doc.is(doc.root(), json::Type::kObj)) {
+        err = "bind: bad response";
+      } else {
+        int32_t e = doc.get(doc.root(), "Error", true);
+        if (doc.is(e, json::Type::kStr) && !doc.str(e).empty()) err = std::string(doc.str(e));
+        else if (status != 200) err = "bind: HTTP " + std::to_string(status);
+      }
+    }
+    std::lock_guard<std::mutex> lk(mu);
+    if (!err.empty()) {
+      requested[job.node] -= pods[job.pod].need;
+      ++r.bind_errors;
+      r.last_error[job.pod] = std::move(err);
+      requeue(job.pod);
+      return;
+    }
+    r.node_of[job.pod] = cfg.nodes[job.node];
+    ++r.scheduled;
+    r.bind_latencies.push_back(t1 - t0);
+    r.e2e_latencies.push_back(t1 - t_enqueue);
+    r.t_last_bind = std::max(r.t_last_bind, t1);
+    --remaining;
+    cv.notify_all();
+  };
+
+  std::thread binder([&] {
+    struct MConn {
+      int fd = -1;
+      bool busy = false;
+      BindJob job{};
+      double t0 = 0.0;
+      std::string out, in;
+      size_t off = 0;
+    };
+    const size_t max_conns = static_cast<size_t>(std::max(1, cfg.bind_threads));
+    std::vector<MConn> conns;
+    std::vector<size_t> idle;
+    std::deque<BindJob> pending;
+    std::string body, resp;
+    size_t busy = 0;
+    bool stopping = false;
+    auto drop = [&](size_t k, const char* why) {
+      MConn& c = conns[k];
+      if (c.fd >= 0) {
+        ::epoll_ctl(ep, EPOLL_CTL_DEL, c.fd, nullptr);
+        ::close(c.fd);
+      }
+      c.fd = -1;
+      c.in.clear();
+      if (c.busy) {
+        c.busy = false;
+        --busy;
+        complete(c.job, 0, nullptr, why, c.t0);
+      }
+      idle.push_back(k);
+    };
+    auto flush_out = [&](size_t k) {   // false = connection failed
+      MConn& c = conns[k];
+      while (c.off < c.out.size()) {
+        ssize_t n = ::send(c.fd, c.out.data() + c.off, c.out.size() - c.off, MSG_NOSIGNAL);
+        if (n > 0) {
+          c.off += static_cast<size_t>(n);
+          continue;
+        }
+        if (n < 0 && errno == EINTR) continue;
+        if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK || errno == ENOTCONN)) {
+          epoll_event ev{};
+          ev.events = EPOLLIN | EPOLLOUT;
+          ev.data.u64 = k;
+          ::epoll_ctl(ep, EPOLL_CTL_MOD, c.fd, &ev);
+          return true;
+        }
+        return false;
+      }
+      epoll_event ev{};
+      ev.events = EPOLLIN;
+      ev.data.u64 = k;
+      ::epoll_ctl(ep, EPOLL_CTL_MOD, c.fd, &ev);
+      return true;
+    };
+    auto dispatch = [&] {
+      while (!pending.empty() && (!idle.empty() || conns.size() < max_conns)) {
+        size_t k;
+        if (!idle.empty()) {
+          k = idle.back();
+          idle.pop_back();
+        } else {
+          k = conns.size();
+          conns.emplace_back();
+        }
+        MConn& c = conns[k];
+        BindJob job = pending.front();
+        pending.pop_front();
+        if (c.fd < 0) {
+          c.fd = open_socket(cfg.host, cfg.port, true);
+          if (c.fd < 0) {
+            c.job = job;
+            c.busy = true;
+            ++busy;
+            c.t0 = now_s();
+            drop(k, "bind: connect failed");
+            continue;
+          }
+          epoll_event ev{};
+          ev.events = EPOLLIN;
+          ev.data.u64 = k;
+          ::epoll_ctl(ep, EPOLL_CTL_ADD, c.fd, &ev);
+        }
+        const SimPod& p = pods[job.pod];
+        body.assign("{\"PodName\":");
+        json::append_quoted(&body, p.name);
+        body.append(",\"PodNamespace\":");
+        json::append_quoted(&body, p.ns);
+        body.append(",\"PodUID\":");
+        json::append_quoted(&body, p.uid);
+        body.append(",\"Node\":");
+        json::append_quoted(&body, cfg.nodes[job.node]);
+        body.push_back('}');
+        c.out = post_request(cfg.host, "/scheduler/bind", body);
+        c.off = 0;
+        c.job = job;
+        c.busy = true;
+        ++busy;
+        c.t0 = now_s();
+        if (!flush_out(k)) drop(k, "bind: transport error");
+      }
+    };
+    epoll_event evs[128];
+    for (;;) {
+      if (stopping && busy == 0 && pending.empty()) break;
+      int n = ::epoll_wait(ep, evs, 128, stopping ? 10 : -1);
+      if (n < 0 && errno != EINTR) break;
+      for (int e = 0; e < n; ++e) {
+        if (evs[e].data.u64 == UINT64_MAX) {
+          uint64_t v;
+          (void)!::read(efd, &v, sizeof v);
+          std::lock_guard<std::mutex> lk(mu);
+          while (!jobs.empty()) {
+            pending.push_back(jobs.front());
+            jobs.pop_front();
+          }
+          if (stop) stopping = true;
+          continue;
+        }
+        const size_t k = evs[e].data.u64;
+        if (k >= conns.size() || conns[k].fd < 0) continue;
+        MConn& c = conns[k];
+        if (evs[e].events & EPOLLOUT) {
+          if (!flush_out(k)) {
+            drop(k, "bind: transport error");
+            continue;
+          }
+        }
+        if (evs[e].events & (EPOLLIN | EPOLLERR | EPOLLHUP)) {
+          char tmp[16384];
+          ssize_t got = ::recv(c.fd, tmp, sizeof tmp, 0);
+          if (got <= 0) {
+            if (got < 0 && (errno == EAGAIN || errno == EINTR)) continue;
+            drop(k, "bind: connection closed");
+            continue;
+          }
+          c.in.append(tmp, static_cast<size_t>(got));
+          int status = 0;
+          bool close = false;
+          int rc = take_response(&c.in, &status, &resp, &close);
+          if (rc == 0) continue;
+          if (rc < 0 || !c.busy) {
+            drop(k, "bind: bad response");
+            continue;
+          }
+          c.busy = false;
+          --busy;
+          complete(c.job, status, &resp, nullptr, c.t0);
+          if (close) {
+            drop(k, nullptr);
+          } else {
+            idle.push_back(k);
+          }
+        }
+      }
+      dispatch();
+    }
+    for (size_t k = 0; k < conns.size(); ++k)
+      if (conns[k].fd >= 0) ::close(conns[k].fd);
+  });
+
+  Conn cycle(cfg.host, cfg.port);
+  std::mt19937_64 rng(cfg.seed);
+  std::string body, out, cands_json;
+  std::vector<int> cands, fits, ties;
+  json::Doc doc;
+  for (;;) {
+    size_t i;
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      for (;;) {
+        if (remaining <= 0) break;
+        if (!ready.empty()) {
+          double wait = ready.top().t - now_s();
+          if (wait <= 0) break;
+          cv.wait_for(lk, std::chrono::duration<double>(wait));
+        } else {
+          cv.wait_for(lk, std::chrono::milliseconds(50));
+        }
+      }
+      if (remaining <= 0) break;
+      i = ready.top().pod;
+      ready.pop();
+      ++attempts[i];
+      // resource-fit pre-filter on the scheduler's own accounting (requests of pods it bound)
+      cands.clear();
+      if (fit) {
+        for (size_t n = 0; n < n_nodes; ++n)
+          if (requested[n] + pods[i].need <= cfg.capacity[n]) cands.push_back(static_cast<int>(n));
+      }
+    }
+    if (r.t_first_filter == 0.0) r.t_first_filter = now_s();
+    const SimPod& p = pods[i];
+    const std::string* names = &all_json;
+    if (fit && cands.size() != n_nodes) {
+      cands_json = names_json(cands);
+      names = &cands_json;
+    }
+    int host = -1;
+    if (!fit || !cands.empty()) {
+      body.assign("{\"Pod\":").append(p.json).append(",\"Nodes\":null,\"NodeNames\":").append(*names).push_back('}');
+      int status = 0;
+      fits.clear();
+      if (cycle.post("/scheduler/filter", body, &status, &out) && doc.parse(out) &&
+          doc.is(doc.root(), json::Type::kObj)) {
+        int32_t nn = doc.get(doc.root(), "NodeNames", true);
+        if (doc.is(nn, json::Type::kArr))
+          for (int32_t c = doc.at(nn).first; c >= 0; c = doc.at(c).next) {
+            auto it = node_index.find(std::string(doc.str(c)));
+            if (it != node_index.end()) fits.push_back(it->second);
+          }
+      }
+      if (fits.size() == 1) {
+        host = fits[0];
+      } else if (!fits.empty()) {
+        const std::string* fj = names;
+        if (fits.size() != (fit ? cands.size() : n_nodes)) {
+          cands_json = names_json(fits);
+          fj = &cands_json;
+        }
+        body.assign("{\"Pod\":").append(p.json).append(",\"Nodes\":null,\"NodeNames\":").append(*fj).push_back('}');
+        if (cycle.post("/scheduler/priorities", body, &status, &out) && doc.parse(out) &&
+            doc.is(doc.root(), json::Type::kArr)) {
+          int64_t best = INT64_MIN;
+          ties.clear();
+          for (int32_t c = doc.at(doc.root()).first; c >= 0; c = doc.at(c).next) {
+            int32_t h = doc.get(c, "Host", true), s = doc.get(c, "Score", true);
+            if (!doc.is(h, json::Type::kStr) || !doc.is(s, json::Type::kNum)) continue;
+            auto it = node_index.find(std::string(doc.str(h)));
+            if (it == node_index.end()) continue;
+            int64_t score = std::strtoll(std::string(doc.str(s)).c_str(), nullptr, 10);
+            if (score > best) {
+              best = score;
+              ties.clear();
+            }
+            if (score == best) ties.push_back(it->second);
+          }
+          if (ties.size() == 1) host = ties[0];
+          else if (!ties.empty()) host = ties[std::uniform_int_distribution<size_t>(0, ties.size() - 1)(rng)];
+        }
+      }
+    }
+    std::lock_guard<std::mutex> lk(mu);
+    if (host < 0) {
+      ++r.unschedulable_attempts;
+      requeue(i);
+      continue;
+    }
+    requested[host] += p.need;
+    jobs.push_back({i, host});
+    wake();
+  }
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    stop = true;
+  }
+  wake();
+  binder.join();
+  ::close(ep);
+  ::close(efd);
+  return r;
+}
+
+}  // namespace nanogpu::sim

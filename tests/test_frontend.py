@@ -259,3 +259,65 @@ def test_native_prepared_bind_and_its_error_text():
             await rt.stop()
 
     asyncio.run(main())
+
+
+@pytest.mark.parametrize("latency_s", [0.0, 0.001])
+def test_native_scheduler_standin_binds_everything(latency_s):
+    """native/src/schedsim.cpp drives the real runtime: every pod bound exactly once, no
+    device over-committed. With API latency the in-place bind coroutine suspends and is
+    resumed by NativeServer._resume."""
+    from nanogpu.sim.driver import NativeSchedulerDriver, node_capacities
+
+    async def main():
+        store, rt = await _runtime(4)
+        store.faults.latency_s = latency_s
+        loop = asyncio.get_running_loop()
+        try:
+            rng = random.Random(3)
+            pods = [store.create_pod(pu.make_pod(f"p{i}", [("c", rng.choice([10, 25, 50]))])) for i in range(120)]
+            nodes = [f"n{i}" for i in range(4)]
+            drv = NativeSchedulerDriver("127.0.0.1", rt.bound_port, nodes,
+                                        node_capacities([store.get_node(n) for n in nodes]), bind_threads=32)
+            st = await loop.run_in_executor(None, drv.run, pods)
+            assert st.scheduled + st.failed == 120 and st.scheduled >= 100
+            assert len(drv.placements) == st.scheduled
+            bound = {(ns, name): node for ns, name, node in store.bindings}
+            assert len(bound) == len(store.bindings) == st.scheduled
+            for key, node in drv.placements.items():
+                assert bound[tuple(key.split("/"))] == node
+            used = {}
+            for p in store.pods.values():
+                if pu.node_name_of(p):
+                    idx = pu.container_assignment(p, "c")[0]
+                    k = (pu.node_name_of(p), idx)
+                    used[k] = used.get(k, 0) + pu.pod_demand(p)[0][0]
+            assert max(used.values()) <= 100
+            status = rt.state.status()
+            for (n, i), u in used.items():
+                assert status[n]["GPUs"][i]["Percent"] == 100 - u
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
+
+
+def test_inline_bind_failure_rolls_back():
+    """A patch failure inside the in-place bind: 500 with the error, reservation rolled back."""
+    async def main():
+        store, rt = await _runtime(1)
+        store.faults.patch_error_rate = 1.0
+        loop = asyncio.get_running_loop()
+        try:
+            p = store.create_pod(pu.make_pod("x", [("c", 30)]))
+            m = pu.meta(p)
+            res = await loop.run_in_executor(None, _http, rt.bound_port, [
+                ("POST", "/scheduler/filter", _dumps({"Pod": p, "NodeNames": ["n0"]})),
+                ("POST", "/scheduler/bind", _dumps({"PodName": "x", "PodNamespace": "default", "PodUID": m["uid"],
+                                                    "Node": "n0"}))])
+            assert res[1][0] == 500 and "injected patch failure" in json.loads(res[1][1])["Error"]
+            assert rt.state.ledger.lookup(m["uid"]) is None
+            assert all(g["Percent"] == 100 for g in rt.state.status()["n0"]["GPUs"])
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
