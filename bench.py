@@ -63,6 +63,7 @@ def parse_args():
     ap.add_argument("--no-gpu", action="store_true", help="skip GPU discovery (CPU-only rehearsal)")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--profile-out", default="", help="cProfile the timed steps (rank 0) into this file")
+    ap.add_argument("--frontend-threads", type=int, default=4, help="native front door epoll workers")
     ap.add_argument("--busy-poll-us", type=int, default=int(os.environ.get("NANOGPU_BUSY_POLL_US", "0")),
                     help="native front door busy-poll window")
     ap.add_argument("--driver", default="native", choices=["native", "python"],
@@ -208,19 +209,30 @@ def driver_main(conn) -> None:
     cfg = conn.recv()
     cls = ThreadedSchedulerDriver if cfg.get("driver") == "python" else NativeSchedulerDriver
 
+    # the pods of every step, built before the clock starts (the main process does the same)
+    native = cls is NativeSchedulerDriver
+    work = {}
+    for step in cfg["steps"]:
+        pods = burst(cfg["rank"], cfg["world"], cfg["pods"], step, 7)
+        work[step] = NativeSchedulerDriver.prepare(pods) if native else pods
+    conn.send("ready")
+    session = None
+    if native:
+        from nanogpu.native import core
+
+        session = core().SchedulerSession()   # keep-alive connections across steps
+
     def serve() -> None:
         while True:
             msg = conn.recv()
             if msg[0] != "step":
                 break
             step = msg[1]
-            pods = burst(cfg["rank"], cfg["world"], cfg["pods"], step, 7)
-            drv = cls("127.0.0.1", cfg["port"], cfg["names"], cfg["caps"],
-                      # native: connections of the epoll binder (a bind leaves as soon as its host is
-                      # chosen, as kube-scheduler's per-pod bind goroutines); Python: pool threads
-                      bind_threads=256 if cls is NativeSchedulerDriver else min(32, cfg["inflight"]),
-                      seed=step * 1009 + cfg["rank"])
-            stats = drv.run(pods)
+            # native: connections of the epoll binder (a bind leaves as soon as its host is
+            # chosen, as kube-scheduler's per-pod bind goroutines); Python: pool threads
+            kw = {"session": session, "bind_threads": 256} if native else {"bind_threads": min(32, cfg["inflight"])}
+            drv = cls("127.0.0.1", cfg["port"], cfg["names"], cfg["caps"], seed=step * 1009 + cfg["rank"], **kw)
+            stats = drv.run(prepared=work.pop(step)) if native else drv.run(work.pop(step))
             drv.close()
             conn.send(stats.summary())
 
@@ -250,7 +262,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
     cfg = Config(port=0, host="127.0.0.1", priority=args.policy, compat=args.compat, ledger_path=ledger_path,
                  max_nodes=max(1024, args.nodes), max_pods=max(65536, 4 * args.pods),
                  policy_config_path="/nonexistent/policy.yaml", reservation_ttl_s=3600,
-                 busy_poll_us=args.busy_poll_us)
+                 busy_poll_us=args.busy_poll_us, frontend_threads=args.frontend_threads)
     rt = Runtime(cfg, worker=0, api=InProcKube(store))
     await rt.start()
     client = FastExtenderClient("127.0.0.1", rt.bound_port, pool=args.inflight_binds + 8)
@@ -268,7 +280,9 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
     loop = asyncio.get_running_loop()
     if conn is not None:
         conn.send({"port": rt.bound_port, "names": names, "caps": caps, "rank": d.rank, "world": d.world,
-                   "pods": args.pods, "inflight": args.inflight_binds, "driver": args.driver})
+                   "pods": args.pods, "inflight": args.inflight_binds, "driver": args.driver,
+                   "steps": [10_000 + w for w in range(args.warmup)] + list(range(args.steps))})
+        await loop.run_in_executor(None, conn.recv)   # the stand-in has built its pods
 
     async def one_step(step: int, timed: bool) -> dict:
         pods = bursts.pop(step)

@@ -59,7 +59,7 @@ class Config:
     lease_renew_deadline_s: float = 10.0
     lease_retry_s: float = 2.0
     identity: str = ""
-    frontend_threads: int = 2
+    frontend_threads: int = 4
     busy_poll_us: int = 0                       # native workers spin this long after an event
     gpu_node_selectors: list = field(default_factory=lambda: [T.AMD_GPU_NODE_LABEL, T.LEGACY_GPU_NODE_LABEL])
 

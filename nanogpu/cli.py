@@ -58,7 +58,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--frontend", default="native", choices=["native", "aiohttp"],
                    help="native: C++ epoll server answers filter/priorities without Python")
-    p.add_argument("--frontend-threads", type=int, default=2)
+    p.add_argument("--frontend-threads", type=int, default=4)
     p.add_argument("--busy-poll-us", type=int, default=0,
                    help="native workers keep polling this long after an event (lower latency, more CPU)")
     p.add_argument("--leader-elect", action="store_true", help="active/standby replicas on a Lease")

@@ -128,8 +128,10 @@ class FakeKubeStore:
         pod["metadata"] = m = dict(pod.get("metadata") or {})
         pod["status"] = dict(pod.get("status") or {})
         m.setdefault("namespace", "default")
-        m.setdefault("uid", str(uuid.uuid4()))
-        m.setdefault("creationTimestamp", time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()))
+        if not m.get("uid"):
+            m["uid"] = str(uuid.uuid4())
+        if "creationTimestamp" not in m:
+            m["creationTimestamp"] = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
         key = (m["namespace"], m["name"])
         if key in self.pods:
             raise ApiError(409, f'pods "{m["name"]}" already exists', "AlreadyExists")
@@ -367,9 +369,8 @@ class InProcKube:
         self.store.add_event({"namespace": ns, "involvedObject": involved, "reason": reason,
                               "message": message, "type": etype})
 
-    async def watch(self, resource, resource_version, timeout_s=300, label_selector=None):
-        async for ev in self.store.watch(resource, resource_version, label_selector):
-            yield ev
+    def watch(self, resource, resource_version, timeout_s=300, label_selector=None):
+        return self.store.watch(resource, resource_version, label_selector)   # no extra async-gen hop
 
     async def get_lease(self, ns, name):
         await self._rtt()

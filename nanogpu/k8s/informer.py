@@ -12,12 +12,20 @@ import logging
 import random
 from typing import Awaitable, Callable
 
-from . import podutil as pu
 from .client import ApiError
 
 log = logging.getLogger(__name__)
 
 Handler = Callable[[str, dict, dict | None], None]   # (event_type, obj, old_obj)
+
+
+def _pod_key(o: dict) -> str:
+    m = o.get("metadata") or {}
+    return f"{m.get('namespace', '')}/{m.get('name', '')}"
+
+
+def _node_key(o: dict) -> str:
+    return (o.get("metadata") or {}).get("name", "")
 
 
 class Informer:
@@ -27,8 +35,7 @@ class Informer:
         self.resource = resource               # "pods" | "nodes"
         self.label_selector = label_selector
         self.resync_s = resync_s
-        self.key = key or (lambda o: f"{pu.meta(o).get('namespace', '')}/{pu.meta(o).get('name', '')}"
-                           if resource == "pods" else pu.meta(o).get("name", ""))
+        self.key = key or (_pod_key if resource == "pods" else _node_key)
         self.store: dict[str, dict] = {}
         self.handlers: list[Handler] = []
         self.synced = asyncio.Event()
@@ -90,22 +97,31 @@ class Informer:
                 backoff = min(backoff * 2, 5.0)
 
     async def _watch(self) -> None:
+        store, key, handlers = self.store, self.key, self.handlers
         async for ev in self.api.watch(self.resource, self.rv, label_selector=self.label_selector):
             etype, obj = ev.get("type"), ev.get("object") or {}
-            if etype == "BOOKMARK":
-                self.rv = pu.meta(obj).get("resourceVersion", self.rv)
-                continue
             if etype == "ERROR":
                 raise ApiError(int(obj.get("code", 500)), obj.get("message", "watch error"))
-            k = self.key(obj)
-            self.rv = pu.meta(obj).get("resourceVersion", self.rv)
+            self.rv = (obj.get("metadata") or {}).get("resourceVersion", self.rv)
+            if etype == "BOOKMARK":
+                continue
+            k = key(obj)
             if etype == "DELETED":
-                old = self.store.pop(k, None)
-                self._dispatch("DELETED", obj, old)
+                old = store.pop(k, None)
             else:
-                old = self.store.get(k)
-                self.store[k] = obj
-                self._dispatch("MODIFIED" if old is not None else "ADDED", obj, old)
+                old = store.get(k)
+                store[k] = obj
+                if etype == "ADDED" and old is not None:
+                    etype = "MODIFIED"
+                elif etype == "MODIFIED" and old is None:
+                    etype = "ADDED"
+            if len(handlers) == 1:
+                try:
+                    handlers[0](etype, obj, old)
+                except Exception:  # a handler bug must not kill the informer
+                    log.exception("informer handler failed for %s %s", etype, k)
+            else:
+                self._dispatch(etype, obj, old)
 
     def start(self) -> asyncio.Task:
         self._task = asyncio.ensure_future(self.run())

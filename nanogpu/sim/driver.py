@@ -559,8 +559,10 @@ class NativeSchedulerDriver:
     Tie-breaks draw from a different random stream than the Python drivers."""
 
     def __init__(self, host: str, port: int, node_names: list[str], node_capacity: dict[str, int] | None = None,
-                 bind_threads: int = 256, seed: int = 0, max_attempts: int = 8, backoff_s: float = 0.001):
+                 bind_threads: int = 256, seed: int = 0, max_attempts: int = 8, backoff_s: float = 0.001,
+                 session=None):
         self.host, self.port = host, port
+        self.session = session      # core().SchedulerSession(): keep-alive connections across runs
         self.nodes = list(node_names)
         self.capacity = [int(node_capacity.get(n, 0)) for n in self.nodes] if node_capacity else []
         self.bind_threads = bind_threads
@@ -570,16 +572,23 @@ class NativeSchedulerDriver:
         self.stats = DriverStats()
         self.placements: dict[str, str] = {}
 
-    def run(self, pods: list[dict]) -> DriverStats:
-        from ..native import core
-
+    @staticmethod
+    def prepare(pods: list[dict]) -> list[tuple]:
+        """The pods as the native loop takes them (kube-scheduler has them decoded from its
+        informer before a scheduling cycle starts; this is harness-side work)."""
         enc = json.JSONEncoder(separators=(",", ":"))
         args = []
         for p in pods:
             ns, name = pu.pod_ns_name(p)
             args.append((enc.encode(p).encode(), ns, name, pu.pod_uid(p), sum(c for c, _ in pu.pod_demand(p))))
+        return args
+
+    def run(self, pods: list[dict] | None = None, prepared: list[tuple] | None = None) -> DriverStats:
+        from ..native import core
+
+        args = prepared if prepared is not None else self.prepare(pods or [])
         r = core().drive_scheduler(self.host, self.port, args, self.nodes, self.capacity, self.bind_threads,
-                                   self.seed, self.max_attempts, self.backoff_s)
+                                   self.seed, self.max_attempts, self.backoff_s, self.session)
         st = self.stats
         st.scheduled, st.failed = r["scheduled"], r["failed"]
         st.bind_errors, st.unschedulable_attempts = r["bind_errors"], r["unschedulable_attempts"]

@@ -17,6 +17,7 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -47,6 +48,21 @@ struct SimResult {
   std::vector<std::string> last_error;
 };
 
-SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods);
+// Keep-alive connections carried from one drive() to the next (kube-scheduler's HTTP client
+// pool lives as long as the scheduler). Not thread-safe: one drive() at a time per session.
+struct SessionState;
+class Session {
+ public:
+  Session();
+  ~Session();
+  Session(const Session&) = delete;
+  Session& operator=(const Session&) = delete;
+  SessionState* state() { return st_.get(); }
+
+ private:
+  std::unique_ptr<SessionState> st_;
+};
+
+SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* session = nullptr);
 
 }  // namespace nanogpu::sim

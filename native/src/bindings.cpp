@@ -512,12 +512,14 @@ PYBIND11_MODULE(_native, m) {
         return d;
       });
   m.def("mono_now", &mono_now);
+  py::class_<sim::Session, std::shared_ptr<sim::Session>>(m, "SchedulerSession")
+      .def(py::init<>());
   m.def(
       "drive_scheduler",
       [](const std::string& host, int port, const std::vector<std::tuple<py::bytes, std::string, std::string, std::string,
                                                                        int64_t>>& pods,
          const std::vector<std::string>& nodes, const std::vector<int64_t>& capacity, int bind_threads, uint64_t seed,
-         int max_attempts, double backoff_s) {
+         int max_attempts, double backoff_s, std::shared_ptr<sim::Session> session) {
         sim::SimConfig cfg;
         cfg.host = host;
         cfg.port = port;
@@ -540,7 +542,7 @@ PYBIND11_MODULE(_native, m) {
         sim::SimResult r;
         {
           py::gil_scoped_release nogil;
-          r = sim::drive(cfg, ps);
+          r = sim::drive(cfg, ps, session.get());
         }
         py::dict d;
         d["scheduled"] = r.scheduled;
@@ -556,6 +558,7 @@ PYBIND11_MODULE(_native, m) {
         return d;
       },
       py::arg("host"), py::arg("port"), py::arg("pods"), py::arg("nodes"), py::arg("capacity"),
-      py::arg("bind_threads") = 16, py::arg("seed") = 0, py::arg("max_attempts") = 8, py::arg("backoff_s") = 0.001,
+      py::arg("bind_threads") = 256, py::arg("seed") = 0, py::arg("max_attempts") = 8, py::arg("backoff_s") = 0.001,
+      py::arg("session") = nullptr,
       "kube-scheduler stand-in (native/src/schedsim.cpp): schedule `pods` through the extender at host:port");
 }

@@ -15,6 +15,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <queue>
 #include <random>
@@ -173,7 +174,29 @@ struct BindJob {
 
 }  // namespace
 
-SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods) {
+struct SessionState {
+  std::string host;
+  int port = -1;
+  std::unique_ptr<Conn> cycle;
+  std::vector<int> bind_fds;
+  void reset() {
+    cycle.reset();
+    for (int fd : bind_fds) ::close(fd);
+    bind_fds.clear();
+  }
+  ~SessionState() { reset(); }
+};
+
+Session::Session() : st_(std::make_unique<SessionState>()) {}
+Session::~Session() = default;
+
+SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* session_handle) {
+  SessionState* session = session_handle ? session_handle->state() : nullptr;
+  if (session && (session->host != cfg.host || session->port != cfg.port)) {
+    session->reset();
+    session->host = cfg.host;
+    session->port = cfg.port;
+  }
   SimResult r;
   const size_t n_pods = pods.size(), n_nodes = cfg.nodes.size();
   r.node_of.assign(n_pods, std::string());
@@ -274,6 +297,7 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods) {
     struct MConn {
       int fd = -1;
       bool busy = false;
+      bool proven = true;   // false: kept from an earlier run, no response seen yet
       BindJob job{};
       double t0 = 0.0;
       std::string out, in;
@@ -286,6 +310,21 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods) {
     std::string body, resp;
     size_t busy = 0;
     bool stopping = false;
+    if (session) {
+      // keep-alive connections of earlier runs (kube-scheduler keeps its client's pool)
+      for (int fd : session->bind_fds) {
+        MConn c;
+        c.fd = fd;
+        c.proven = false;
+        epoll_event ev{};
+        ev.events = EPOLLIN;
+        ev.data.u64 = conns.size();
+        ::epoll_ctl(ep, EPOLL_CTL_ADD, fd, &ev);
+        idle.push_back(conns.size());
+        conns.push_back(std::move(c));
+      }
+      session->bind_fds.clear();
+    }
     auto drop = [&](size_t k, const char* why) {
       MConn& c = conns[k];
       if (c.fd >= 0) {
@@ -297,8 +336,13 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods) {
       if (c.busy) {
         c.busy = false;
         --busy;
-        complete(c.job, 0, nullptr, why, c.t0);
+        if (!c.proven && why) {
+          pending.push_front(c.job);   // a stale kept connection: resend on a fresh one
+        } else {
+          complete(c.job, 0, nullptr, why, c.t0);
+        }
       }
+      c.proven = true;
       idle.push_back(k);
     };
     auto flush_out = [&](size_t k) {   // false = connection failed
@@ -416,6 +460,7 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods) {
             continue;
           }
           c.busy = false;
+          c.proven = true;
           --busy;
           complete(c.job, status, &resp, nullptr, c.t0);
           if (close) {
@@ -427,11 +472,24 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods) {
       }
       dispatch();
     }
-    for (size_t k = 0; k < conns.size(); ++k)
-      if (conns[k].fd >= 0) ::close(conns[k].fd);
+    for (size_t k = 0; k < conns.size(); ++k) {
+      if (conns[k].fd < 0) continue;
+      ::epoll_ctl(ep, EPOLL_CTL_DEL, conns[k].fd, nullptr);
+      if (session && !conns[k].busy && conns[k].in.empty()) session->bind_fds.push_back(conns[k].fd);
+      else ::close(conns[k].fd);
+    }
   });
 
-  Conn cycle(cfg.host, cfg.port);
+  std::unique_ptr<Conn> own;
+  Conn* cycle_conn;
+  if (session) {
+    if (!session->cycle) session->cycle = std::make_unique<Conn>(cfg.host, cfg.port);
+    cycle_conn = session->cycle.get();
+  } else {
+    own = std::make_unique<Conn>(cfg.host, cfg.port);
+    cycle_conn = own.get();
+  }
+  Conn& cycle = *cycle_conn;
   std::mt19937_64 rng(cfg.seed);
   std::string body, out, cands_json;
   std::vector<int> cands, fits, ties;

@@ -276,10 +276,20 @@ def test_native_scheduler_standin_binds_everything(latency_s):
             rng = random.Random(3)
             pods = [store.create_pod(pu.make_pod(f"p{i}", [("c", rng.choice([10, 25, 50]))])) for i in range(120)]
             nodes = [f"n{i}" for i in range(4)]
+            session = N.SchedulerSession()
             drv = NativeSchedulerDriver("127.0.0.1", rt.bound_port, nodes,
-                                        node_capacities([store.get_node(n) for n in nodes]), bind_threads=32)
-            st = await loop.run_in_executor(None, drv.run, pods)
-            assert st.scheduled + st.failed == 120 and st.scheduled >= 100
+                                        node_capacities([store.get_node(n) for n in nodes]), bind_threads=32,
+                                        session=session)
+            st = await loop.run_in_executor(None, drv.run, pods[:60])
+            # a second run on the same session reuses the first run's keep-alive connections
+            drv2 = NativeSchedulerDriver("127.0.0.1", rt.bound_port, nodes,
+                                         node_capacities([store.get_node(n) for n in nodes]), bind_threads=32,
+                                         session=session)
+            st2 = await loop.run_in_executor(None, drv2.run, pods[60:])
+            drv.placements.update(drv2.placements)
+            assert st.scheduled + st.failed == 60 and st.scheduled == 60
+            assert st2.scheduled + st2.failed == 60 and st.scheduled + st2.scheduled >= 100
+            st.scheduled += st2.scheduled
             assert len(drv.placements) == st.scheduled
             bound = {(ns, name): node for ns, name, node in store.bindings}
             assert len(bound) == len(store.bindings) == st.scheduled
