@@ -46,6 +46,8 @@ class Config:
     max_pods: int = 131072
     verify_pod_on_bind: bool = False
     reservation_ttl_s: float = 60.0
+    nominate: bool = True              # priorities nominate the top node (Ledger::nominate)
+    nomination_ttl_s: float = 5.0
     policy_reload_s: float = 3.0
     fake_cluster: int = 0                       # >0: serve against an in-process fake cluster of N nodes
     fake_gpus_per_node: int = 8
@@ -82,7 +84,7 @@ class Runtime:
             policy=cfg.priority, compat=cfg.compat, load_aware=cfg.is_load_schedule,
             topo_weight=cfg.topology_weight, seed=cfg.seed, ledger_path=cfg.ledger_path,
             max_nodes=cfg.max_nodes, max_pods=cfg.max_pods, track_hbm=cfg.track_hbm,
-            node_source=self._node_from_cache, score_normalize=cfg.score_normalize)
+            node_source=self._node_from_cache, score_normalize=cfg.score_normalize, nominate=cfg.nominate)
         self.metrics = Metrics()
         self.tracer = Tracer()
         self.extender: Extender | None = None
@@ -201,8 +203,17 @@ class Runtime:
             self.state.score_normalize = bool(spec.score_normalize)
 
     async def _sweeper(self) -> None:
+        period = min(max(1.0, self.cfg.reservation_ttl_s / 4), max(0.05, self.cfg.nomination_ttl_s / 4))
+        next_res = 0.0
+        loop = asyncio.get_running_loop()
         while True:
-            await asyncio.sleep(max(1.0, self.cfg.reservation_ttl_s / 4))
+            await asyncio.sleep(period)
+            gone = self.state.sweep_nominations(self.cfg.nomination_ttl_s)
+            if gone:
+                log.info("released %d nominations no bind adopted", len(gone))
+            if loop.time() < next_res:
+                continue
+            next_res = loop.time() + max(1.0, self.cfg.reservation_ttl_s / 4)
             stale = self.state.sweep_reservations(self.cfg.reservation_ttl_s)
             if stale:
                 log.warning("released %d stale reservations", len(stale))

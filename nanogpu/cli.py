@@ -52,6 +52,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--host", default="0.0.0.0")
     p.add_argument("--bind-verify-pod", action="store_true", help="GET the pod on every bind (reference behaviour)")
     p.add_argument("--reservation-ttl", default="60s")
+    p.add_argument("--no-nominate", action="store_true",
+                   help="priorities do not tentatively reserve the top-scored node")
+    p.add_argument("--nomination-ttl", default="5s", help="release a nomination no bind adopted after this")
     p.add_argument("--fake-cluster", type=int, default=0, help="serve against N in-process fake MI355X nodes")
     p.add_argument("--fake-gpus-per-node", type=int, default=8)
     p.add_argument("--fake-partition", default="SPX", choices=["SPX", "DPX", "QPX", "CPX"])
@@ -84,6 +87,7 @@ def parse(argv: list[str] | None = None) -> Config:
         topology_weight=a.topology_weight, track_hbm=not a.no_hbm, workers=max(1, a.workers),
         ledger_path=a.ledger_path, max_nodes=a.max_nodes, max_pods=a.max_pods,
         verify_pod_on_bind=a.bind_verify_pod, reservation_ttl_s=parse_duration(a.reservation_ttl),
+        nominate=not a.no_nominate, nomination_ttl_s=parse_duration(a.nomination_ttl),
         fake_cluster=a.fake_cluster, fake_gpus_per_node=a.fake_gpus_per_node, fake_partition=a.fake_partition,
         seed=a.seed, frontend=a.frontend, frontend_threads=max(1, a.frontend_threads), busy_poll_us=a.busy_poll_us,
         leader_elect=a.leader_elect, lease_name=a.lease_name, lease_namespace=a.lease_namespace, identity=a.identity)

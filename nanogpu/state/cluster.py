@@ -58,8 +58,9 @@ class ClusterState:
                  load_aware: bool = False, topo_weight: float = 1.0, seed: int = 0,
                  ledger_path: str = "", max_nodes: int = 4096, max_pods: int = 131072,
                  track_hbm: bool = True, node_source: Callable[[str], dict | None] | None = None,
-                 score_normalize: bool = False):
+                 score_normalize: bool = False, nominate: bool = True):
         self.ledger = N.Ledger(ledger_path, max_nodes, max_pods, True)
+        self._nominate = bool(nominate)
         self.track_hbm = track_hbm
         self._listeners: list[Callable[[], None]] = []
         self._score_normalize = bool(score_normalize)
@@ -90,6 +91,17 @@ class ClusterState:
     @score_normalize.setter
     def score_normalize(self, v: bool) -> None:
         self._score_normalize = bool(v)
+        self._changed()
+
+    @property
+    def nominate(self) -> bool:
+        """Priorities nominate the unique top-scored node (Ledger::nominate). Off in compat
+        mode: the reference keeps no state between prioritize and bind."""
+        return self._nominate and not self.options.compat
+
+    @nominate.setter
+    def nominate(self, v: bool) -> None:
+        self._nominate = bool(v)
         self._changed()
 
     def set_policy(self, policy: str, compat: bool | None = None, load_aware: bool | None = None,
@@ -161,6 +173,8 @@ class ClusterState:
     # ------------------------------------------------------------------ verbs
     def filter(self, pod: dict, node_names: list[str]) -> tuple[list[str], dict[str, str]]:
         """Reference Dealer.Assume (dealer.go:89-136) + Predicate.Handler (predicate.go:19-41)."""
+        if self.nominate:
+            self._drop_own_nomination(pod)
         demand = pu.pod_demand(pod)
         ids = self.node_ids(node_names)
         rcs = self.ledger.filter(ids, demand, self.options)
@@ -176,12 +190,35 @@ class ClusterState:
 
     def score(self, pod: dict, node_names: list[str]) -> list[int]:
         """Reference Dealer.Score (dealer.go:138-153); ScoreMin (0) for unknown/unfit nodes."""
+        if self.nominate:
+            self._drop_own_nomination(pod)
         demand = pu.pod_demand(pod)
         ids = self.node_ids(node_names)
         scores = self.ledger.score(ids, demand, self.options)
+        if self.nominate and scores:
+            self._nominate_best(pod, demand, ids, scores)
         if self.score_normalize and scores:
             scores = self._normalize(scores)
         return scores
+
+    def _drop_own_nomination(self, pod: dict) -> None:
+        uid = pu.pod_uid(pod)
+        if uid:
+            self.ledger.drop_nomination(uid)
+
+    def _nominate_best(self, pod: dict, demand, ids: list[int], scores: list[int]) -> None:
+        """Same rule as the native front door: a unique best fitting node is nominated."""
+        uid = pu.pod_uid(pod)
+        if not uid or not any(p > 0 or m > 0 for p, m in demand):
+            return
+        fits = self.ledger.filter(ids, demand, self.options)
+        cand = [(s, i) for s, i, rc in zip(scores, ids, fits) if rc == N.OK and i >= 0]
+        if not cand:
+            return
+        best = max(s for s, _ in cand)
+        top = [i for s, i in cand if s == best]
+        if len(top) == 1:
+            self.ledger.nominate(top[0], uid, demand, self.options)
 
     def _normalize(self, scores: list[int]) -> list[int]:
         """Maps to kube-scheduler's extender range [0, 10] (MaxExtenderPriority) [ext]."""
@@ -265,6 +302,14 @@ class ClusterState:
     def sweep_reservations(self, ttl_s: float) -> list[str]:
         """Releases reservations whose bind never committed (crashed worker, lost request)."""
         stale = self.ledger.expired_reservations(ttl_s)
+        for uid in stale:
+            self.ledger.release(uid)
+        return stale
+
+    def sweep_nominations(self, ttl_s: float) -> list[str]:
+        """Releases nominations no bind adopted (kube-scheduler chose another node, or the
+        pod was never bound)."""
+        stale = self.ledger.expired_nominations(ttl_s)
         for uid in stale:
             self.ledger.release(uid)
         return stale

@@ -78,7 +78,9 @@ class Frontend {
 
   int port() const { return port_; }
   int notify_fd() const { return py_efd_; }
-  void set_options(const Options& o, bool score_normalize);
+  // nominate: priorities tentatively reserve the pod on its unique top-scored node
+  // (Ledger::nominate) so the next pods' filters see it before the bind arrives.
+  void set_options(const Options& o, bool score_normalize, bool nominate = false);
   // false: every request goes to Python (a standby replica answers 503 from there).
   void set_serving(bool on) { serving_.store(on, std::memory_order_release); }
   // After any event a worker keeps polling (epoll timeout 0) for this long before it
@@ -124,6 +126,7 @@ class Frontend {
   mutable std::mutex opt_mu_;
   Options opt_;
   bool normalize_ = false;
+  bool nominate_ = false;
 
   std::mutex py_mu_;
   std::deque<PyRequest> py_q_;

@@ -30,7 +30,8 @@ constexpr int kNameLen = 256;
 constexpr int kKeyLen = 64;
 constexpr int kPodShards = 64;
 
-enum PodState : int32_t { kPodEmpty = 0, kPodReserved = 1, kPodCommitted = 2, kPodTombstone = 3 };
+// Nominated: taken tentatively at priorities for the top-scored node (see nominate()).
+enum PodState : int32_t { kPodEmpty = 0, kPodReserved = 1, kPodCommitted = 2, kPodTombstone = 3, kPodNominated = 4 };
 
 struct NodeSlot {
   char name[kNameLen];
@@ -110,8 +111,21 @@ class Ledger {
   int32_t assume(int32_t id, const Demand& d, const Options& o, Plan* plan);
 
   // Bind: choose (cache hit if the node is unchanged) and allocate atomically; records the
-  // pod as Reserved. Idempotent for the same key on the same node.
+  // pod as Reserved. Idempotent for the same key on the same node. A nomination of the
+  // key on this node is adopted (kOk: the caller owns it, e.g. rolls it back on failure);
+  // one on another node is released first.
   int32_t reserve(int32_t id, const std::string& key, const Demand& d, const Options& o, Plan* plan);
+  // Priorities: takes `d` tentatively on node `id` for pod `key` (state Nominated), the node
+  // kube-scheduler is about to pick, so the filters of the pods scheduled right behind it
+  // (kube-scheduler's cycle does not wait for the bind) already see it — the extender-side
+  // counterpart of kube-scheduler's assume cache. Moves an older nomination of the key;
+  // leaves a Reserved/Committed key alone (kOkExisting). Unbound ones expire (below).
+  int32_t nominate(int32_t id, const std::string& key, const Demand& d, const Options& o);
+  std::vector<std::string> expired_nominations(double older_than_s) const;
+  // Releases `key` only while it is a nomination: every scheduling attempt of a pod starts
+  // by dropping its own nomination, so its filter and scores never count it against itself.
+  // kOk = dropped, kOkExisting = reserved/committed (left alone), kErrUnknownPod = none.
+  int32_t drop_nomination(const std::string& key);
   // Allocates an explicit plan (pods bound by someone else / rebuild from annotations).
   int32_t allocate_plan(int32_t id, const std::string& key, const Demand& d, const Plan& plan,
                         bool committed);
@@ -138,6 +152,10 @@ class Ledger {
   NodeSlot* node(int32_t id) const;
   PodSlot* shard(int s) const;
   int shard_of(uint64_t h) const { return static_cast<int>(h % kPodShards); }
+  int32_t reserve_as(int32_t id, const std::string& key, const Demand& d, const Options& o, Plan* plan,
+                     int32_t state);
+  std::vector<std::string> expired(int32_t state, double older_than_s) const;
+  int32_t release_if(const std::string& key, bool only_nominated);
   PodSlot* find_pod_locked(int s, uint64_t h, const char* key) const;
   PodSlot* insert_pod_locked(int s, uint64_t h, const char* key);
 

@@ -171,7 +171,7 @@ py::dict record_dict(const PodRecord& r) {
   py::dict d;
   d["key"] = r.key;
   d["node"] = r.node;
-  d["state"] = r.state == kPodReserved ? "reserved" : "committed";
+  d["state"] = r.state == kPodReserved ? "reserved" : r.state == kPodNominated ? "nominated" : "committed";
   d["t_reserved"] = r.t_reserved;
   std::vector<std::pair<int32_t, int64_t>> dem;
   for (int i = 0; i < r.demand.n; ++i) dem.emplace_back(r.demand.c[i].pct, r.demand.c[i].mib);
@@ -417,6 +417,17 @@ PYBIND11_MODULE(_native, m) {
            },
            py::arg("node") = -1)
       .def("expired_reservations", &Ledger::expired_reservations)
+      .def("expired_nominations", &Ledger::expired_nominations)
+      .def("drop_nomination", &Ledger::drop_nomination, py::call_guard<py::gil_scoped_release>())
+      .def(
+          "nominate",
+          [](Ledger& l, int32_t id, const std::string& key, const std::vector<std::pair<int32_t, int64_t>>& demand,
+             const Options& o) {
+            Demand d = to_demand(demand);
+            py::gil_scoped_release nogil;
+            return l.nominate(id, key, d, o);
+          },
+          "tentative reservation for the top-scored node (priorities); adopted by reserve()")
       .def("set_load", &Ledger::set_load)
       .def("set_health", &Ledger::set_health)
       .def("frag", [](const Ledger& l, int32_t min_request) { return frag_dict(l.frag(min_request)); },
@@ -450,7 +461,8 @@ PYBIND11_MODULE(_native, m) {
            py::arg("host") = "0.0.0.0", py::arg("port") = 0, py::arg("threads") = 2)
       .def_property_readonly("port", &Frontend::port)
       .def("notify_fd", &Frontend::notify_fd)
-      .def("set_options", &Frontend::set_options, py::arg("options"), py::arg("score_normalize") = false)
+      .def("set_options", &Frontend::set_options, py::arg("options"), py::arg("score_normalize") = false,
+           py::arg("nominate") = false)
       .def("set_serving", &Frontend::set_serving)
       .def("set_busy_poll_us", &Frontend::set_busy_poll_us)
       .def("take",

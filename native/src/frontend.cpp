@@ -273,10 +273,11 @@ void Frontend::stop() {
   py_efd_ = -1;
 }
 
-void Frontend::set_options(const Options& o, bool score_normalize) {
+void Frontend::set_options(const Options& o, bool score_normalize, bool nominate) {
   std::lock_guard<std::mutex> g(opt_mu_);
   opt_ = o;
   normalize_ = score_normalize;
+  nominate_ = nominate;
 }
 
 std::vector<PyRequest> Frontend::take() {
@@ -734,12 +735,14 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     nv.push_back(name);
   }
   Options o;
-  bool normalize;
+  bool normalize, nominate;
   {
     std::lock_guard<std::mutex> g(opt_mu_);
     o = opt_;
     normalize = normalize_;
+    nominate = nominate_;
   }
+  if (nominate && !uid.empty()) ledger_->drop_nomination(std::string(uid));   // not against itself
   if (pod >= 0 && !uid.empty()) {
     cached.raw.assign(d.raw(pod));
     cached.demand = dem;
@@ -778,9 +781,24 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     return true;
   }
   std::vector<int32_t> scores(ids.size());
+  int64_t best = -1;
+  int n_best = 0;
   for (size_t i = 0; i < ids.size(); ++i) {
     const int32_t rc = ledger_->assume(ids[i], dem, o, &p);
     scores[i] = rc == kOk ? p.score : 0;
+    if (rc != kOk) continue;
+    if (best < 0 || scores[i] > scores[best]) {
+      best = static_cast<int64_t>(i);
+      n_best = 1;
+    } else if (scores[i] == scores[best]) {
+      ++n_best;
+    }
+  }
+  // a unique winner is the node kube-scheduler picks (ties are broken at random there)
+  if (nominate && n_best == 1 && !uid.empty() && dem.n > 0) {
+    bool wants = false;
+    for (int i = 0; i < dem.n; ++i) wants = wants || dem.c[i].pct > 0 || dem.c[i].mib > 0;
+    if (wants) ledger_->nominate(ids[best], std::string(uid), dem, o);
   }
   if (normalize && !scores.empty()) {
     // nanogpu/state/cluster.py::_normalize (Python round(): half to even)

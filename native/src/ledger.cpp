@@ -199,7 +199,8 @@ PodSlot* Ledger::insert_pod_locked(int s, uint64_t h, const char* key) {
     std::vector<PodSlot> live;
     live.reserve(hdr_->shard_live[s]);
     for (uint32_t i = 0; i < cap; ++i)
-      if (t[i].state == kPodReserved || t[i].state == kPodCommitted) live.push_back(t[i]);
+      if (t[i].state == kPodReserved || t[i].state == kPodCommitted || t[i].state == kPodNominated)
+        live.push_back(t[i]);
     for (uint32_t i = 0; i < cap; ++i) t[i].state = kPodEmpty;
     for (const PodSlot& p : live) {
       uint32_t i = static_cast<uint32_t>((p.hash / kPodShards) % cap);
@@ -386,8 +387,34 @@ int32_t Ledger::assume(int32_t id, const Demand& d, const Options& o, Plan* plan
   return rc;
 }
 
+namespace {
+constexpr int32_t kNominatedElsewhere = -1000;   // internal: release the nomination, retry
+}
+
 int32_t Ledger::reserve(int32_t id, const std::string& key, const Demand& d, const Options& o,
                         Plan* plan) {
+  int32_t rc = reserve_as(id, key, d, o, plan, kPodReserved);
+  if (rc == kNominatedElsewhere) {
+    release(key);
+    rc = reserve_as(id, key, d, o, plan, kPodReserved);
+    if (rc == kNominatedElsewhere) rc = kErrPodExists;   // re-nominated concurrently
+  }
+  return rc;
+}
+
+int32_t Ledger::nominate(int32_t id, const std::string& key, const Demand& d, const Options& o) {
+  Plan plan;
+  int32_t rc = reserve_as(id, key, d, o, &plan, kPodNominated);
+  if (rc == kNominatedElsewhere) {
+    release(key);
+    rc = reserve_as(id, key, d, o, &plan, kPodNominated);
+    if (rc == kNominatedElsewhere) rc = kOkExisting;
+  }
+  return rc;
+}
+
+int32_t Ledger::reserve_as(int32_t id, const std::string& key, const Demand& d, const Options& o, Plan* plan,
+                           int32_t state) {
   NodeSlot* n = node(id);
   if (!n || !n->in_use) return kErrUnknownNode;
   if (key.empty() || key.size() >= kKeyLen) return kErrBadDemand;
@@ -400,6 +427,15 @@ int32_t Ledger::reserve(int32_t id, const std::string& key, const Demand& d, con
     Unlock us{&hdr_->shard_mu[s]};
     PodSlot* p = find_pod_locked(s, h, key.c_str());
     if (p) {
+      if (p->state == kPodNominated) {
+        if (p->node != id) return kNominatedElsewhere;
+        // adopt (bind) or refresh (a repeated priorities call) the nomination
+        p->state = state;
+        p->t_reserved = mono_now();
+        *plan = p->plan;
+        return state == kPodReserved ? kOk : kOkExisting;
+      }
+      if (state == kPodNominated) return kOkExisting;   // already bound or binding
       if (p->node != id) return kErrPodExists;
       *plan = p->plan;
       return kOkExisting;
@@ -425,7 +461,7 @@ int32_t Ledger::reserve(int32_t id, const std::string& key, const Demand& d, con
     p->demand = d;
     p->plan = *plan;
     p->t_reserved = mono_now();
-    p->state = kPodReserved;
+    p->state = state;
   }
   ++n->n_pods;
   n->generation.fetch_add(1, std::memory_order_release);
@@ -439,6 +475,11 @@ int32_t Ledger::allocate_plan(int32_t id, const std::string& key, const Demand& 
   NodeSlot* n = node(id);
   if (!n || !n->in_use) return kErrUnknownNode;
   if (key.empty() || key.size() >= kKeyLen) return kErrBadDemand;
+  {
+    // the annotations are the truth: a nomination of ours (maybe another node/plan) yields
+    PodRecord r;
+    if (lookup(key, &r) && r.state == kPodNominated) release(key);
+  }
   const uint64_t h = key_hash(key.c_str());
   const int s = shard_of(h);
   lock_node(n);
@@ -487,7 +528,11 @@ int32_t Ledger::commit(const std::string& key) {
   return kOk;
 }
 
-int32_t Ledger::release(const std::string& key) {
+int32_t Ledger::release(const std::string& key) { return release_if(key, false); }
+
+int32_t Ledger::drop_nomination(const std::string& key) { return release_if(key, true); }
+
+int32_t Ledger::release_if(const std::string& key, bool only_nominated) {
   const uint64_t h = key_hash(key.c_str());
   const int s = shard_of(h);
   int32_t id;
@@ -496,6 +541,7 @@ int32_t Ledger::release(const std::string& key) {
     Unlock us{&hdr_->shard_mu[s]};
     PodSlot* p = find_pod_locked(s, h, key.c_str());
     if (!p) return kErrUnknownPod;
+    if (only_nominated && p->state != kPodNominated) return kOkExisting;
     id = p->node;
   }
   NodeSlot* n = node(id);
@@ -506,6 +552,7 @@ int32_t Ledger::release(const std::string& key) {
   Unlock us{&hdr_->shard_mu[s]};
   PodSlot* p = find_pod_locked(s, h, key.c_str());
   if (!p || p->node != id) return kErrUnknownPod;  // raced with another release
+  if (only_nominated && p->state != kPodNominated) return kOkExisting;   // adopted meanwhile
   unapply(n->devs, n->n_devs, p->demand, p->plan);
   p->state = kPodTombstone;
   --hdr_->shard_live[s];
@@ -541,14 +588,15 @@ std::vector<PodRecord> Ledger::pods_on(int32_t node_id) const {
     PodSlot* t = shard(s);
     for (uint32_t i = 0; i < hdr_->pods_per_shard; ++i) {
       const PodSlot& p = t[i];
-      if ((p.state == kPodReserved || p.state == kPodCommitted) && (node_id < 0 || p.node == node_id))
+      if ((p.state == kPodReserved || p.state == kPodCommitted || p.state == kPodNominated) &&
+          (node_id < 0 || p.node == node_id))
         out.push_back(PodRecord{p.key, p.node, p.state, p.t_reserved, p.demand, p.plan});
     }
   }
   return out;
 }
 
-std::vector<std::string> Ledger::expired_reservations(double older_than_s) const {
+std::vector<std::string> Ledger::expired(int32_t state, double older_than_s) const {
   std::vector<std::string> out;
   const double now = mono_now();
   for (int s = 0; s < kPodShards; ++s) {
@@ -556,9 +604,17 @@ std::vector<std::string> Ledger::expired_reservations(double older_than_s) const
     Unlock us{&hdr_->shard_mu[s]};
     PodSlot* t = shard(s);
     for (uint32_t i = 0; i < hdr_->pods_per_shard; ++i)
-      if (t[i].state == kPodReserved && now - t[i].t_reserved > older_than_s) out.emplace_back(t[i].key);
+      if (t[i].state == state && now - t[i].t_reserved > older_than_s) out.emplace_back(t[i].key);
   }
   return out;
+}
+
+std::vector<std::string> Ledger::expired_reservations(double older_than_s) const {
+  return expired(kPodReserved, older_than_s);
+}
+
+std::vector<std::string> Ledger::expired_nominations(double older_than_s) const {
+  return expired(kPodNominated, older_than_s);
 }
 
 int32_t Ledger::set_load(int32_t id, int dev, float usage) {

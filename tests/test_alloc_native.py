@@ -193,3 +193,33 @@ def test_pool_mirrors_stay_consistent_under_churn(demands, modes, policy, compat
         L.release(u)
     for d in L.snapshot(nid)["devices"]:
         assert d["mib_free"] == d["mib_total"] and d["pct_free"] == d["pct_total"]
+
+
+def test_nomination_lifecycle():
+    """Ledger::nominate: tentative at priorities, adopted by reserve on the same node, moved
+    by a reserve elsewhere, dropped only while still a nomination, swept when stale."""
+    t = synthetic_mi355x(8)
+    L, (a, b) = ledger_with(t, 2)
+    free = lambda nid: sum(d["pct_free"] for d in L.snapshot(nid)["devices"])   # noqa: E731
+    assert L.nominate(a, "p", [(50, 0)], BIN) == N.OK
+    assert L.lookup("p")["state"] == "nominated" and free(a) == 750
+    assert L.nominate(a, "p", [(50, 0)], BIN) == N.OK_EXISTING            # repeated priorities
+    rc, plan = L.reserve(a, "p", [(50, 0)], BIN)
+    assert rc == N.OK and L.lookup("p")["state"] == "reserved" and free(a) == 750   # adopted, owned
+    assert L.drop_nomination("p") == N.OK_EXISTING and free(a) == 750            # bound: left alone
+    assert L.nominate(a, "p", [(50, 0)], BIN) == N.OK_EXISTING                  # bound: left alone
+    # nominated on a, bound on b: a is freed
+    assert L.nominate(a, "q", [(100, 0)], BIN) == N.OK and free(a) == 650
+    rc, _ = L.reserve(b, "q", [(100, 0)], BIN)
+    assert rc == N.OK and L.lookup("q")["node"] == b and free(a) == 750 and free(b) == 700
+    # a newer priorities call moves the nomination
+    assert L.nominate(a, "r", [(30, 0)], BIN) == N.OK and L.nominate(b, "r", [(30, 0)], BIN) == N.OK
+    assert free(a) == 750 and free(b) == 670
+    assert L.drop_nomination("r") == N.OK and L.lookup("r") is None and free(b) == 700
+    assert L.drop_nomination("r") == N.ERR_UNKNOWN_POD
+    # stale nominations are swept, reservations are not
+    assert L.nominate(a, "s", [(10, 0)], BIN) == N.OK
+    assert L.expired_nominations(-1.0) == ["s"] and "s" not in L.expired_reservations(-1.0)
+    # annotations of a pod bound elsewhere win over our nomination
+    assert L.allocate_plan(b, "s", [(10, 0)], [[3]], True) == N.OK
+    assert L.lookup("s")["node"] == b and free(a) == 750 and free(b) == 690

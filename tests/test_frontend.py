@@ -331,3 +331,66 @@ def test_inline_bind_failure_rolls_back():
             await rt.stop()
 
     asyncio.run(main())
+
+
+def test_priorities_nominate_unique_best_and_bind_adopts():
+    """Native priorities nominate the unique top node, so the next pod's filter sees the
+    pod before its bind arrives; ties nominate nothing; compat mode never nominates; the
+    bind adopts the nomination (a failed bind rolls it back)."""
+    async def main():
+        store, rt = await _runtime(2)
+        loop = asyncio.get_running_loop()
+        led = rt.state.ledger
+        try:
+            base = store.create_pod(pu.make_pod("base", [("c", 100)] * 7))   # n0 nearly full
+            mb = pu.meta(base)
+            await loop.run_in_executor(None, _http, rt.bound_port, [
+                ("POST", "/scheduler/filter", _dumps({"Pod": base, "NodeNames": ["n0"]})),
+                ("POST", "/scheduler/bind", _dumps({"PodName": "base", "PodNamespace": "default",
+                                                    "PodUID": mb["uid"], "Node": "n0"}))])
+            a = store.create_pod(pu.make_pod("a", [("c", 60)]))
+            b = store.create_pod(pu.make_pod("b", [("c", 60)]))
+            both = ["n0", "n1"]
+            res = await loop.run_in_executor(None, _http, rt.bound_port, [
+                ("POST", "/scheduler/filter", _dumps({"Pod": a, "NodeNames": both})),
+                ("POST", "/scheduler/priorities", _dumps({"Pod": a, "NodeNames": both})),
+                ("POST", "/scheduler/filter", _dumps({"Pod": b, "NodeNames": both}))])
+            rec = led.lookup(pu.pod_uid(a))
+            assert rec["state"] == "nominated" and rec["node"] == rt.state.node_entry("n0").id
+            # b no longer fits n0: a's nomination holds the last GPU
+            assert json.loads(res[2][1])["NodeNames"] == ["n1"]
+            # a's own next attempt does not count its nomination against itself
+            res = await loop.run_in_executor(None, _http, rt.bound_port, [
+                ("POST", "/scheduler/filter", _dumps({"Pod": a, "NodeNames": both}))])
+            assert json.loads(res[0][1])["NodeNames"] == both
+            assert led.lookup(pu.pod_uid(a)) is None
+            res = await loop.run_in_executor(None, _http, rt.bound_port, [
+                ("POST", "/scheduler/priorities", _dumps({"Pod": a, "NodeNames": both})),
+                ("POST", "/scheduler/bind", _dumps({"PodName": "a", "PodNamespace": "default",
+                                                    "PodUID": pu.pod_uid(a), "Node": "n0"}))])
+            assert res[1] == (200, b'{"Error":""}') and led.lookup(pu.pod_uid(a))["state"] == "committed"
+            # ties (two empty-equal candidates) nominate nothing
+            c = store.create_pod(pu.make_pod("c", [("c", 10)]))
+            store2_nodes = ["n1"]
+            await loop.run_in_executor(None, _http, rt.bound_port, [
+                ("POST", "/scheduler/priorities", _dumps({"Pod": c, "NodeNames": store2_nodes + store2_nodes}))])
+            assert led.lookup(pu.pod_uid(c)) is None
+            # compat mode (the reference keeps no state between verbs): no nominations
+            rt.state.set_policy("binpack", compat=True)
+            d = store.create_pod(pu.make_pod("d", [("c", 10)]))
+            await loop.run_in_executor(None, _http, rt.bound_port, [
+                ("POST", "/scheduler/priorities", _dumps({"Pod": d, "NodeNames": both}))])
+            assert led.lookup(pu.pod_uid(d)) is None
+            # a failed bind of an adopted nomination rolls it back
+            rt.state.set_policy("binpack", compat=False)
+            store.faults.patch_error_rate = 1.0
+            e = store.create_pod(pu.make_pod("e", [("c", 10)]))
+            res = await loop.run_in_executor(None, _http, rt.bound_port, [
+                ("POST", "/scheduler/priorities", _dumps({"Pod": e, "NodeNames": both})),
+                ("POST", "/scheduler/bind", _dumps({"PodName": "e", "PodNamespace": "default",
+                                                    "PodUID": pu.pod_uid(e), "Node": "n1"}))])
+            assert res[1][0] == 500 and led.lookup(pu.pod_uid(e)) is None
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
