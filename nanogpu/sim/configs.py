@@ -29,7 +29,7 @@ from ..extender import server as S
 from ..k8s import podutil as pu
 from ..k8s.fake_apiserver import Faults, FakeKubeStore, InProcKube, serve
 from ..topology.model import NodeTopology, synthetic_mi355x
-from .driver import FastExtenderClient, SchedulerDriver, node_capacities
+from .driver import FastExtenderClient, NativeSchedulerDriver, SchedulerDriver, node_capacities
 
 ROOT = Path(__file__).resolve().parents[2]
 PARTS = {"SPX": 1, "DPX": 2, "QPX": 4, "CPX": 8}
@@ -72,8 +72,9 @@ class Harness:
     """One extender (ours or the reference model) against one fake cluster."""
 
     def __init__(self, nodes: list[dict], policy: str, reference: bool = False, api_rtt_ms: float = 0.0,
-                 inflight: int = 64, http_api: bool = False, track_hbm: bool = True):
+                 inflight: int = 64, http_api: bool = False, track_hbm: bool = True, driver: str = "native"):
         self.track_hbm = track_hbm
+        self.driver = driver     # kube-scheduler stand-in: "native" (C++, own threads) or "python"
         self.nodes = nodes
         self.policy = policy
         self.reference = reference
@@ -118,10 +119,20 @@ class Harness:
     async def burst(self, pods: list[dict], seed: int = 0) -> dict:
         names = [pu.meta(n)["name"] for n in self.nodes]
         self.rt.tracer.buf.clear()
-        drv = SchedulerDriver(self.client, InProcKube(self.store), names, node_capacities(self.nodes),
-                              max_inflight_binds=self.inflight, seed=seed, max_attempts=3)
-        t0 = time.perf_counter()
-        stats = await drv.run(pods)
+        if self.driver == "native":
+            # pods created first (kubectl), then the C++ stand-in schedules them from its own
+            # threads (no GIL), as kube-scheduler would from its own process
+            created = [self.store.create_pod(p) for p in pods]
+            drv = NativeSchedulerDriver("127.0.0.1", self.port, names, node_capacities(self.nodes),
+                                        bind_threads=self.inflight, seed=seed, max_attempts=3)
+            loop = asyncio.get_running_loop()
+            t0 = time.perf_counter()
+            stats = await loop.run_in_executor(None, drv.run, created)
+        else:
+            drv = SchedulerDriver(self.client, InProcKube(self.store), names, node_capacities(self.nodes),
+                                  max_inflight_binds=self.inflight, seed=seed, max_attempts=3)
+            t0 = time.perf_counter()
+            stats = await drv.run(pods)
         wall = time.perf_counter() - t0
         binds = sorted(s["dur_ms"] for s in self.rt.tracer.dump(10 ** 9, "bind") if s["ok"])
         out = stats.summary()
@@ -232,13 +243,21 @@ async def config2(gpus=1, reference=False, hbm_mib=None, **_):
     return out
 
 
-async def config3(gpus=8, nodes_n=8, pods_per_gpu=25, reference=False, api_rtt_ms=0.0, **_):
-    """Burst of 25 pods per GPU (200 for 8 GPUs), mixed gpu-percent {10,25,50}, spread."""
-    nodes = make_nodes(nodes_n, gpus)
-    async with Harness(nodes, "spread", reference, api_rtt_ms=api_rtt_ms) as h:
-        r = await h.burst(_pods(pods_per_gpu * gpus, (10, 25, 50), seed=3))
-        r["frag"] = h.frag(10)
-        return r
+async def config3(gpus=8, nodes_n=8, pods_per_gpu=25, reference=False, api_rtt_ms=0.0, reps=7, **_):
+    """Burst of 25 pods per GPU (200 for 8 GPUs), mixed gpu-percent {10,25,50}, spread.
+    A burst lasts tens of milliseconds, so it runs `reps` times on a fresh cluster and the
+    run with the median rate is reported."""
+    runs = []
+    for _rep in range(reps):
+        nodes = make_nodes(nodes_n, gpus)
+        async with Harness(nodes, "spread", reference, api_rtt_ms=api_rtt_ms) as h:
+            r = await h.burst(_pods(pods_per_gpu * gpus, (10, 25, 50), seed=3))
+            r["frag"] = h.frag(10)
+            runs.append(r)
+    runs.sort(key=lambda r: r["pods_per_s"])
+    out = dict(runs[len(runs) // 2])
+    out["pods_per_s_runs"] = [round(r["pods_per_s"]) for r in runs]
+    return out
 
 
 async def config4(reference=False, **_):
@@ -345,12 +364,22 @@ def summary_md(r: dict) -> str:
                  f"{v['ours']['hbm_probe']['scheduled']} | {v['reference_model']['hbm_probe']['scheduled']} | "
                  f"{v['reference_model']['hbm_probe']['overcommitted_gib']} |")
     L += ["", "## Config 3 — 8 nodes, 25 pods per GPU, mixed {10,25,50} %, spread", "",
-          "| GPUs/node | pods | ours pods/s | ref pods/s | ours bind p50 ms | ref bind p50 ms | ours frag % | ref frag % |",
+          "Median of 7 bursts. Bind p50 is given twice: as kube-scheduler sees it (request to "
+          "response, including the wait in the extender's queue while the burst floods in) and "
+          "inside the extender (the verb itself).", "",
+          "| GPUs/node | pods | ours pods/s | ref pods/s | ours bind p50 ms (sched / ext) | "
+          "ref bind p50 ms (sched / ext) | ours frag % | ref frag % |",
           "|---:|---:|---:|---:|---:|---:|---:|---:|"]
+
+    def _ms(v):
+        return "-" if v is None else f"{v:.3f}"
+
     for g, v in list(r["config3"].items()) + [("8 (API RTT 2 ms)", r["config3_rtt2ms"])]:
         o, f = v["ours"], v["reference_model"]
-        L.append(f"| {g} | {o['scheduled']} | {o['pods_per_s']:.0f} | {f['pods_per_s']:.0f} | {o['bind_p50_ms']:.3f} | "
-                 f"{f['bind_p50_ms']:.3f} | {o['frag']['frag_pct']:.2f} | {f['frag']['frag_pct']:.2f} |")
+        L.append(f"| {g} | {o['scheduled']} | {o['pods_per_s']:.0f} | {f['pods_per_s']:.0f} | "
+                 f"{_ms(o['bind_p50_ms'])} / {_ms(o.get('ext_bind_p50_ms'))} | "
+                 f"{_ms(f['bind_p50_ms'])} / {_ms(f.get('ext_bind_p50_ms'))} | "
+                 f"{o['frag']['frag_pct']:.2f} | {f['frag']['frag_pct']:.2f} |")
     c4 = r["config4"]
     L += ["", "## Config 4 — 4-container pod on one 8-GPU node (GPU0–1 link degraded to 38 GB/s, GPU0 half used)", "",
           "| case | ours devices | ours min link GB/s | ours NUMA | ref devices | ref min link GB/s | ref NUMA |",
