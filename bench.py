@@ -63,6 +63,7 @@ def parse_args():
     ap.add_argument("--no-gpu", action="store_true", help="skip GPU discovery (CPU-only rehearsal)")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--profile-out", default="", help="cProfile the timed steps (rank 0) into this file")
+    ap.add_argument("--no-nominate", action="store_true", help="priorities do not nominate (Ledger::nominate)")
     ap.add_argument("--frontend-threads", type=int, default=4, help="native front door epoll workers")
     ap.add_argument("--busy-poll-us", type=int, default=int(os.environ.get("NANOGPU_BUSY_POLL_US", "0")),
                     help="native front door busy-poll window")
@@ -262,7 +263,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
     cfg = Config(port=0, host="127.0.0.1", priority=args.policy, compat=args.compat, ledger_path=ledger_path,
                  max_nodes=max(1024, args.nodes), max_pods=max(65536, 4 * args.pods),
                  policy_config_path="/nonexistent/policy.yaml", reservation_ttl_s=3600,
-                 busy_poll_us=args.busy_poll_us, frontend_threads=args.frontend_threads)
+                 busy_poll_us=args.busy_poll_us, frontend_threads=args.frontend_threads,
+                 nominate=not args.no_nominate)
     rt = Runtime(cfg, worker=0, api=InProcKube(store))
     await rt.start()
     client = FastExtenderClient("127.0.0.1", rt.bound_port, pool=args.inflight_binds + 8)
@@ -366,6 +368,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
                              for v in ("filter", "priorities")}
     results["phase_ms"] = {k: round(statistics.mean(p[k] for p in results["phases"]), 2)
                            for k in ("create_ms", "schedule_ms", "release_ms")} if results.get("phases") else None
+    results["schedule_ms_steps"] = [round(p["schedule_ms"], 1) for p in results.get("phases", [])]
     results["failed"] = sum(s["failed"] for s in results["steps"])
     results["bind_errors"] = sum(s["bind_errors"] for s in results["steps"])
     await client.close()
@@ -443,6 +446,7 @@ def main() -> int:
             "scheduled": scheduled, "failed": failed, "bind_retries": bind_errors, "gpu": gpu_info,
             "native_verb_mean_us": res.get("native"),
             "phase_ms_per_step_rank0": res.get("phase_ms"),
+            "schedule_ms_each_step_rank0": res.get("schedule_ms_steps"),
             # CPU time of the rank-0 extender process (all its threads) per pod it handled
             "extender_cpu_us_per_pod_rank0": round(res.get("cpu_us_per_pod", 0.0), 1),
         }

@@ -104,7 +104,8 @@ class Frontend {
   struct Conn;
   struct Worker;
   void run(Worker* w);
-  void on_readable(Worker* w, Conn* c);
+  bool read_in(Worker* w, Conn* c, bool* eof);      // false: connection closed
+  void after_read(Worker* w, Conn* c, bool eof);    // parse + answer what is buffered
   void process(Worker* w, Conn* c);
   bool handle_native(Worker* w, Conn* c, const std::string& method, const std::string& path,
                      std::string_view body, std::string* out);

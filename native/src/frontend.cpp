@@ -393,6 +393,7 @@ void Frontend::prepare_bind(std::string_view body, PyRequest* r) {
 // ------------------------------------------------------------------------------ event loop
 void Frontend::run(Worker* w) {
   epoll_event evs[128];
+  std::vector<uint64_t> later;   // connections whose next request is a bind
   uint64_t last_event = 0;
   while (!stop_.load(std::memory_order_acquire)) {
     const int64_t spin = busy_poll_ns_.load(std::memory_order_relaxed);
@@ -447,30 +448,49 @@ void Frontend::run(Worker* w) {
           flush(w, c);
           if (!w->conns.count(cid)) continue;
         }
-        if (evs[i].events & (EPOLLIN | EPOLLRDHUP)) on_readable(w, c);
+        if (evs[i].events & (EPOLLIN | EPOLLRDHUP)) {
+          bool eof = false;
+          if (!read_in(w, c, &eof)) continue;
+          // scheduling-cycle verbs first: kube-scheduler's next pod waits on filter /
+          // priorities, while a bind's reply only ends an asynchronous binding goroutine
+          if (!eof && c->in.compare(0, 20, "POST /scheduler/bind") == 0) {
+            later.push_back(cid);
+            continue;
+          }
+          after_read(w, c, eof);
+        }
       }
     }
+    for (uint64_t cid : later) {
+      auto it = w->conns.find(cid);
+      if (it != w->conns.end()) after_read(w, it->second.get(), false);
+    }
+    later.clear();
   }
 }
 
-void Frontend::on_readable(Worker* w, Conn* c) {
+bool Frontend::read_in(Worker* w, Conn* c, bool* eof) {
   char buf[65536];
-  bool eof = false;
+  *eof = false;
   for (;;) {
     const ssize_t r = recv(c->fd, buf, sizeof(buf), 0);
     if (r > 0) {
       c->in.append(buf, static_cast<size_t>(r));
       if (c->in.size() > kMaxBody + kMaxHeader) {
         close_conn(w, c);
-        return;
+        return false;
       }
       continue;
     }
-    if (r == 0) eof = true;
+    if (r == 0) *eof = true;
     else if (errno == EINTR) continue;
-    else if (errno != EAGAIN && errno != EWOULDBLOCK) eof = true;
+    else if (errno != EAGAIN && errno != EWOULDBLOCK) *eof = true;
     break;
   }
+  return true;
+}
+
+void Frontend::after_read(Worker* w, Conn* c, bool eof) {
   const uint64_t id = c->id;
   process(w, c);
   if (!w->conns.count(id)) return;
