@@ -69,6 +69,8 @@ def parse_args():
                     help="native front door busy-poll window")
     ap.add_argument("--driver", default="native", choices=["native", "python"],
                     help="kube-scheduler stand-in: C++ (native/src/schedsim.cpp) or the Python threaded one")
+    ap.add_argument("--stall-trace", default="",
+                    help="sample the extender's Python threads every ms in the timed steps; write gaps/stalls here")
     ap.add_argument("--inproc-driver", action="store_true",
                     help="run the kube-scheduler stand-in inside the extender process (default: own process)")
     return ap.parse_args()
@@ -139,6 +141,51 @@ class Dist:
     def close(self):
         if self.dist is not None:
             self.dist.destroy_process_group()
+
+
+class StallSampler:
+    """Diagnostics (--stall-trace): a thread samples every Python thread's stack each ms.
+    A gap between samples means the sampler could not get the GIL (a native call holding
+    it, or the process descheduled); a long run of identical main-thread stacks is a slow
+    Python call. Both are written out with the stacks around them."""
+
+    def __init__(self, period_s: float = 0.001):
+        import threading
+
+        self.period = period_s
+        self.samples: list = []
+        self.on = threading.Event()
+        self.stop_ev = threading.Event()
+        self.main_id = threading.main_thread().ident
+        self.th = threading.Thread(target=self._run, daemon=True)
+        self.th.start()
+
+    @staticmethod
+    def _stack(frame, depth: int = 10) -> list[str]:
+        out = []
+        while frame is not None and len(out) < depth:
+            c = frame.f_code
+            out.append(f"{Path(c.co_filename).name}:{frame.f_lineno}:{c.co_name}")
+            frame = frame.f_back
+        return out
+
+    def _run(self) -> None:
+        while not self.stop_ev.is_set():
+            if self.on.wait(0.05):
+                fr = sys._current_frames()
+                self.samples.append((time.perf_counter(), {tid: self._stack(f) for tid, f in fr.items()
+                                                           if tid != self.th.ident}))
+                time.sleep(self.period)
+
+    def report(self, path: str, gap_s: float = 0.01) -> None:
+        self.stop_ev.set()
+        out = {"gaps": [], "n_samples": len(self.samples)}
+        for (t0, s0), (t1, s1) in zip(self.samples, self.samples[1:]):
+            if t1 - t0 > gap_s:
+                out["gaps"].append({"t": round(t0, 4), "gap_ms": round(1e3 * (t1 - t0), 2),
+                                    "main_before": s0.get(self.main_id), "main_after": s1.get(self.main_id),
+                                    "others_before": {str(k): v[:4] for k, v in s0.items() if k != self.main_id}})
+        Path(path).write_text(json.dumps(out, indent=1))
 
 
 # --------------------------------------------------------------------------- node template
@@ -288,7 +335,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
 
     async def one_step(step: int, timed: bool) -> dict:
         pods = bursts.pop(step)
-        tc = time.perf_counter()
+        t_step0 = tc = time.perf_counter()
         if conn is not None:
             # the pods are created in the API server (this process), then the scheduler
             # process schedules them through the extender's HTTP front door
@@ -322,11 +369,43 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
         await pod_ctrl.queue.drain(5.0)
         phases = {"create_ms": 1e3 * tc, "schedule_ms": 1e3 * summary["span_s"],
                   "release_ms": 1e3 * (time.perf_counter() - ts)}
+        if timed:
+            diag = {"t0": round(t_step0, 4), "t1": round(time.perf_counter(), 4)}
+            diag.update({k: round(summary.get(k, 0.0), 2) for k in ("cycle_max_ms", "bind_max_ms")})
+            diag["unschedulable"] = summary.get("unschedulable_attempts", 0)
+            if rt.native is not None:
+                fs = rt.native.fe.stats()
+                diag["fe_loop_max_ms"] = round(1e3 * fs["loop_max_s"], 2)
+                diag["fe_phase_max_ms"] = [round(1e3 * x, 2) for x in fs["phase_max_s"]]
+                diag["fe_filter_max_ms"] = round(1e3 * fs["filter"]["max_s"], 2)
+                diag["fe_prio_max_ms"] = round(1e3 * fs["priorities"]["max_s"], 2)
+                diag["fe_reserve_max_ms"] = round(1e3 * fs["bind_reserve"]["max_s"], 2)
+                diag["py_take_wait_max_ms"] = round(1e3 * rt.native.take_wait_max_s, 2)
+                rt.native.fe.reset_max()
+                rt.native.take_wait_max_s = 0.0
+            diag["gc_ms"] = round(1e3 * gc_pause["sum"], 2)
+            diag["gc_max_ms"] = round(1e3 * gc_pause["max"], 2)
+            gc_pause.update(sum=0.0, max=0.0, n=0)
+            results.setdefault("diag", []).append(diag)
         return {"stats": summary, "frag": frag, "phases": phases}
 
     from nanogpu.app import tune_gc
 
     tune_gc()   # what `python -m nanogpu` does after start-up
+    import gc
+
+    gc_pause = {"t0": 0.0, "sum": 0.0, "max": 0.0, "n": 0}
+
+    def on_gc(phase, info):   # cyclic-GC pauses of this (extender) process
+        if phase == "start":
+            gc_pause["t0"] = time.perf_counter()
+        else:
+            dt = time.perf_counter() - gc_pause["t0"]
+            gc_pause["sum"] += dt
+            gc_pause["max"] = max(gc_pause["max"], dt)
+            gc_pause["n"] += 1
+
+    gc.callbacks.append(on_gc)
     for w in range(args.warmup):
         await one_step(10_000 + w, False)
     rt.tracer.buf.clear()
@@ -338,13 +417,18 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
 
         prof = cProfile.Profile()
         prof.enable()
+    sampler = StallSampler() if args.stall_trace and d.rank == 0 else None
     cpu0 = time.process_time()
     t0 = time.perf_counter()
+    if sampler is not None:
+        sampler.on.set()
     for s in range(args.steps):
         r = await one_step(s, True)
         results["steps"].append(r["stats"])
         results["frag"].append(r["frag"])
         results.setdefault("phases", []).append(r["phases"])
+    if sampler is not None:
+        sampler.report(args.stall_trace)
     if prof is not None:
         import io
         import pstats
@@ -369,6 +453,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
     results["phase_ms"] = {k: round(statistics.mean(p[k] for p in results["phases"]), 2)
                            for k in ("create_ms", "schedule_ms", "release_ms")} if results.get("phases") else None
     results["schedule_ms_steps"] = [round(p["schedule_ms"], 1) for p in results.get("phases", [])]
+    results["step_diag"] = results.get("diag", [])
     results["failed"] = sum(s["failed"] for s in results["steps"])
     results["bind_errors"] = sum(s["bind_errors"] for s in results["steps"])
     await client.close()
@@ -447,6 +532,9 @@ def main() -> int:
             "native_verb_mean_us": res.get("native"),
             "phase_ms_per_step_rank0": res.get("phase_ms"),
             "schedule_ms_each_step_rank0": res.get("schedule_ms_steps"),
+            # per timed step (rank 0): slowest scheduling cycle and bind seen by the stand-in,
+            # pods the cycle found no host for, cyclic-GC pause time of the extender process
+            "step_diag_rank0": res.get("step_diag"),
             # CPU time of the rank-0 extender process (all its threads) per pod it handled
             "extender_cpu_us_per_pod_rank0": round(res.get("cpu_us_per_pod", 0.0), 1),
         }

@@ -247,6 +247,7 @@ class NativeServer:
         self._loop: asyncio.AbstractEventLoop | None = None
         router.native = self
         self._inline_api = bool(getattr(router.ext.api, "completes_inline", False))
+        self.take_wait_max_s = 0.0
         st.add_listener(self.sync_options)
         self.sync_options()
 
@@ -259,7 +260,11 @@ class NativeServer:
         self._loop.add_reader(self.fe.notify_fd(), self._drain)
 
     def _drain(self) -> None:
-        for rid, method, path, query, body, pod_json, _t, prepared in self.fe.take():
+        reqs = self.fe.take()
+        if reqs:
+            # oldest request's wait between the worker's hand-off and this drain
+            self.take_wait_max_s = max(self.take_wait_max_s, time.monotonic() - reqs[0][6])
+        for rid, method, path, query, body, pod_json, _t, prepared in reqs:
             if prepared is not None:
                 if self._inline_api:
                     self._eager(rid, self.router.ext.bind_prepared(prepared))

@@ -62,12 +62,21 @@ struct CachedPod {
 struct VerbStats {
   std::atomic<uint64_t> count{0}, errors{0}, deferred{0};
   std::atomic<uint64_t> ns_total{0};
+  std::atomic<uint64_t> max_ns{0};     // slowest observation since the last reset_max()
   std::atomic<uint64_t> buckets[16];   // latency histogram, bucket k: < 2^k * 8 us
   VerbStats() {
     for (auto& b : buckets) b.store(0);
   }
   void observe(uint64_t ns);
 };
+
+// Grows this process's file-descriptor table to `want` slots (capped by RLIMIT_NOFILE) up
+// front. The kernel grows the table by doubling when an fd past its end is allocated, and in
+// a multi-threaded process each growth waits for an RCU grace period: on the 256-CPU MI355X
+// host that froze a front-door worker inside accept4() for 110-130 ms whenever a burst of new
+// connections crossed a power of two. Tables never shrink, so paying it once at start-up
+// removes the stall. Returns the number of slots now available (0 if nothing was done).
+int presize_fd_table(int want = 16384);
 
 class Frontend {
  public:
@@ -98,6 +107,11 @@ class Frontend {
 
   VerbStats filter_stats, prio_stats, py_stats, bind_stats;   // bind_stats: native reserve half
   std::atomic<uint64_t> connections{0}, requests{0};
+  std::atomic<uint64_t> loop_max_ns{0};   // longest event-batch a worker spent between epoll_waits
+  // longest single step of a batch: 0 accept, 1 mailbox, 2 read+cycle verbs, 3 deferred binds,
+  // 4 pod-cache lock wait (bind), 5 node lookup (bind), 6 Python hand-off (defer)
+  std::atomic<uint64_t> phase_max_ns[7] = {};
+  void reset_max();
   size_t pod_cache_size() const;
 
  private:

@@ -509,6 +509,7 @@ PYBIND11_MODULE(_native, m) {
           d["errors"] = s.errors.load();
           d["deferred"] = s.deferred.load();
           d["seconds_total"] = static_cast<double>(s.ns_total.load()) * 1e-9;
+          d["max_s"] = static_cast<double>(s.max_ns.load()) * 1e-9;
           py::list b;
           for (const auto& x : s.buckets) b.append(x.load());
           d["buckets_8us_pow2"] = b;
@@ -521,9 +522,16 @@ PYBIND11_MODULE(_native, m) {
         d["bind_reserve"] = one(f.bind_stats);
         d["connections"] = f.connections.load();
         d["requests"] = f.requests.load();
+        d["loop_max_s"] = static_cast<double>(f.loop_max_ns.load()) * 1e-9;
+        py::list ph;
+        for (const auto& x : f.phase_max_ns) ph.append(static_cast<double>(x.load()) * 1e-9);
+        d["phase_max_s"] = ph;
         return d;
-      });
+      })
+      .def("reset_max", &Frontend::reset_max, "zero the per-verb and event-loop maxima");
   m.def("mono_now", &mono_now);
+  m.def("presize_fd_table", &presize_fd_table, py::arg("want") = 16384,
+        "Grow the process fd table once up front (no RCU-synchronised growth under load).");
   py::class_<sim::Session, std::shared_ptr<sim::Session>>(m, "SchedulerSession")
       .def(py::init<>());
   m.def(
@@ -562,6 +570,7 @@ PYBIND11_MODULE(_native, m) {
         d["bind_errors"] = r.bind_errors;
         d["unschedulable_attempts"] = r.unschedulable_attempts;
         d["t_first_filter"] = r.t_first_filter;
+        d["cycle_max_s"] = r.cycle_max_s;
         d["t_last_bind"] = r.t_last_bind;
         d["bind_latencies"] = r.bind_latencies;
         d["e2e_latencies"] = r.e2e_latencies;

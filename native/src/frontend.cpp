@@ -7,9 +7,11 @@
 #include <netinet/tcp.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
+#include <sys/resource.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <chrono>
 #include <cmath>
@@ -170,6 +172,12 @@ bool quantity_value(std::string_view s, bool mib, int64_t* out) {
   return true;
 }
 
+static void atomic_max(std::atomic<uint64_t>* m, uint64_t v) {
+  uint64_t cur = m->load(std::memory_order_relaxed);
+  while (v > cur && !m->compare_exchange_weak(cur, v, std::memory_order_relaxed)) {
+  }
+}
+
 void VerbStats::observe(uint64_t ns) {
   count.fetch_add(1, std::memory_order_relaxed);
   ns_total.fetch_add(ns, std::memory_order_relaxed);
@@ -180,7 +188,22 @@ void VerbStats::observe(uint64_t ns) {
     ++k;
   }
   buckets[k].fetch_add(1, std::memory_order_relaxed);
+  atomic_max(&max_ns, ns);
 }
+
+void Frontend::reset_max() {
+  for (VerbStats* v : {&filter_stats, &prio_stats, &py_stats, &bind_stats}) v->max_ns.store(0);
+  loop_max_ns.store(0);
+  for (auto& p : phase_max_ns) p.store(0);
+}
+
+namespace {
+struct PhaseTimer {
+  std::atomic<uint64_t>* m;
+  uint64_t t0 = now_ns();
+  ~PhaseTimer() { atomic_max(m, now_ns() - t0); }
+};
+}  // namespace
 
 // ------------------------------------------------------------------------------ plumbing
 struct Frontend::Conn {
@@ -206,9 +229,31 @@ struct Frontend::Worker {
 
 static uint64_t make_id(int worker, uint64_t conn) { return (conn << 8) | static_cast<uint64_t>(worker); }
 
+int presize_fd_table(int want) {
+  rlimit rl{};
+  if (getrlimit(RLIMIT_NOFILE, &rl) != 0) return 0;
+  const rlim_t cap = rl.rlim_cur == RLIM_INFINITY ? static_cast<rlim_t>(want) : rl.rlim_cur;
+  const int top = static_cast<int>(std::min<rlim_t>(cap, static_cast<rlim_t>(want))) - 1;
+  if (top < 64) return 0;
+  // the lowest free fd >= top: allocating it sizes the table past `top`; closing keeps the size
+  const int fd = fcntl(0, F_DUPFD_CLOEXEC, top);
+  if (fd < 0) {
+    const int alt = open("/dev/null", O_RDONLY | O_CLOEXEC);
+    if (alt < 0) return 0;
+    const int fd2 = fcntl(alt, F_DUPFD_CLOEXEC, top);
+    close(alt);
+    if (fd2 < 0) return 0;
+    close(fd2);
+    return top + 1;
+  }
+  close(fd);
+  return top + 1;
+}
+
 Frontend::Frontend(std::shared_ptr<Ledger> ledger, const std::string& host, int port, int threads)
     : ledger_(std::move(ledger)) {
   if (!ledger_) throw std::invalid_argument("Frontend: ledger required");
+  presize_fd_table();
   if (threads < 1) threads = 1;
   if (threads > 64) threads = 64;
   py_efd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
@@ -353,7 +398,9 @@ void Frontend::prepare_bind(std::string_view body, PyRequest* r) {
   if (uid.empty() || name.empty() || node.empty()) return;
   CachedPod pod;
   {
+    const uint64_t tw = now_ns();
     std::lock_guard<std::mutex> g(pod_mu_);
+    atomic_max(&phase_max_ns[4], now_ns() - tw);
     auto it = pods_.find(uid);
     if (it == pods_.end()) return;
     pod = std::move(it->second);
@@ -363,7 +410,11 @@ void Frontend::prepare_bind(std::string_view body, PyRequest* r) {
     r->pod_json = std::move(pod.raw);   // unusual: Python decides (and reports) with the object
     return;
   }
-  const int32_t id = ledger_->find_node(node);
+  int32_t id;
+  {
+    PhaseTimer pt{&phase_max_ns[5]};
+    id = ledger_->find_node(node);
+  }
   if (id < 0) {
     r->pod_json = std::move(pod.raw);
     return;
@@ -399,10 +450,19 @@ void Frontend::run(Worker* w) {
     const int64_t spin = busy_poll_ns_.load(std::memory_order_relaxed);
     const bool polling = spin > 0 && now_ns() - last_event < static_cast<uint64_t>(spin);
     const int n = epoll_wait(w->ep, evs, 128, polling ? 0 : 200);
-    if (n > 0) last_event = now_ns();
+    const uint64_t t_batch = n > 0 ? now_ns() : 0;
+    if (n > 0) last_event = t_batch;
+    struct BatchTimer {
+      Frontend* f;
+      uint64_t t0;
+      ~BatchTimer() {
+        if (t0) atomic_max(&f->loop_max_ns, now_ns() - t0);
+      }
+    } batch_timer{this, t_batch};
     for (int i = 0; i < n; ++i) {
       const uint64_t tag = evs[i].data.u64;
       if (tag == 0) {
+        PhaseTimer pt{&phase_max_ns[0]};
         for (;;) {
           const int fd = accept4(w->lfd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
           if (fd < 0) break;
@@ -419,6 +479,7 @@ void Frontend::run(Worker* w) {
           w->conns.emplace(c->id, std::move(c));
         }
       } else if (tag == 1) {
+        PhaseTimer pt{&phase_max_ns[1]};
         uint64_t v;
         (void)!read(w->efd, &v, sizeof(v));
         std::vector<std::pair<uint64_t, std::string>> mb;
@@ -436,6 +497,7 @@ void Frontend::run(Worker* w) {
           if (w->conns.count(m.first)) process(w, c);
         }
       } else {
+        PhaseTimer pt{&phase_max_ns[2]};
         const uint64_t cid = (tag & ~(1ull << 63)) >> 1;
         auto it = w->conns.find(cid);
         if (it == w->conns.end()) continue;
@@ -462,6 +524,7 @@ void Frontend::run(Worker* w) {
       }
     }
     for (uint64_t cid : later) {
+      PhaseTimer pt{&phase_max_ns[3]};
       auto it = w->conns.find(cid);
       if (it != w->conns.end()) after_read(w, it->second.get(), false);
     }
@@ -603,6 +666,7 @@ void Frontend::defer(Worker* w, Conn* c, std::string method, std::string path, s
   r.t_arrival = now_s();
   c->waiting = true;
   py_stats.deferred.fetch_add(1, std::memory_order_relaxed);
+  PhaseTimer pt{&phase_max_ns[6]};
   {
     std::lock_guard<std::mutex> g(py_mu_);
     py_q_.push_back(std::move(r));

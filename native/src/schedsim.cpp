@@ -23,6 +23,7 @@
 #include <thread>
 #include <unordered_map>
 
+#include "nanogpu/frontend.h"
 #include "nanogpu/json.h"
 
 namespace nanogpu::sim {
@@ -187,11 +188,14 @@ struct SessionState {
   ~SessionState() { reset(); }
 };
 
-Session::Session() : st_(std::make_unique<SessionState>()) {}
+Session::Session() : st_(std::make_unique<SessionState>()) {
+  presize_fd_table();   // a long-running scheduler's client pool: no fd-table growth mid-burst
+}
 Session::~Session() = default;
 
 SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* session_handle) {
   SessionState* session = session_handle ? session_handle->state() : nullptr;
+  presize_fd_table();
   if (session && (session->host != cfg.host || session->port != cfg.port)) {
     session->reset();
     session->host = cfg.host;
@@ -519,7 +523,8 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* 
           if (requested[n] + pods[i].need <= cfg.capacity[n]) cands.push_back(static_cast<int>(n));
       }
     }
-    if (r.t_first_filter == 0.0) r.t_first_filter = now_s();
+    const double t_cycle = now_s();
+    if (r.t_first_filter == 0.0) r.t_first_filter = t_cycle;
     const SimPod& p = pods[i];
     const std::string* names = &all_json;
     if (fit && cands.size() != n_nodes) {
@@ -570,6 +575,7 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* 
         }
       }
     }
+    r.cycle_max_s = std::max(r.cycle_max_s, now_s() - t_cycle);
     std::lock_guard<std::mutex> lk(mu);
     if (host < 0) {
       ++r.unschedulable_attempts;
