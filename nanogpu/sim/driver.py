@@ -213,6 +213,7 @@ class DriverStats:
     t_first_filter: float = 0.0
     t_last_bind: float = 0.0
     cycle_max_s: float = 0.0
+    cycle_sum_s: float = 0.0
 
     def summary(self) -> dict:
         span = max(1e-9, self.t_last_bind - self.t_first_filter)
@@ -228,6 +229,7 @@ class DriverStats:
                 "bind_p99_ms": 1e3 * pct(bl, 0.99),
                 "bind_max_ms": 1e3 * (bl[-1] if bl else 0.0),
                 "cycle_max_ms": 1e3 * self.cycle_max_s,
+                "cycle_sum_ms": 1e3 * self.cycle_sum_s,
                 "e2e_p50_ms": 1e3 * (statistics.median(self.e2e_latencies) if self.e2e_latencies else 0.0)}
 
 
@@ -598,6 +600,7 @@ class NativeSchedulerDriver:
         st.bind_latencies, st.e2e_latencies = r["bind_latencies"], r["e2e_latencies"]
         st.t_first_filter, st.t_last_bind = r["t_first_filter"], r["t_last_bind"]
         st.cycle_max_s = r.get("cycle_max_s", 0.0)
+        st.cycle_sum_s = r.get("cycle_sum_s", 0.0)
         for (_, ns, name, _, _), node in zip(args, r["node_of"]):
             if node:
                 self.placements[f"{ns}/{name}"] = node

@@ -104,6 +104,9 @@ class Frontend {
                bool notify = true);
   void wake_workers();
   void stop();
+  // The native filter / priorities verb on a request body (what a worker runs per request);
+  // false = the request needs the Python path.
+  bool filter_verb(std::string_view body, bool prioritize, std::string* out);
 
   VerbStats filter_stats, prio_stats, py_stats, bind_stats;   // bind_stats: native reserve half
   std::atomic<uint64_t> connections{0}, requests{0};
@@ -123,7 +126,6 @@ class Frontend {
   void process(Worker* w, Conn* c);
   bool handle_native(Worker* w, Conn* c, const std::string& method, const std::string& path,
                      std::string_view body, std::string* out);
-  bool filter_verb(std::string_view body, bool prioritize, std::string* out);
   void defer(Worker* w, Conn* c, std::string method, std::string path, std::string query, std::string body);
   void flush(Worker* w, Conn* c);
   void close_conn(Worker* w, Conn* c);

@@ -19,6 +19,9 @@
 #include <cstdint>
 #include <mutex>
 #include <string>
+#include <string_view>
+#include <thread>
+#include <memory>
 #include <unordered_map>
 #include <vector>
 
@@ -100,6 +103,8 @@ class Ledger {
   // Devices that disappear while still in use are kept, marked unhealthy.
   int32_t upsert_node(const std::string& name, const Device* devs, int n, const Topology& topo);
   int32_t find_node(const std::string& name) const;
+  // Name of node `id` if it is registered (no lock: slot names are written before in_use).
+  bool node_named(int32_t id, std::string_view name) const;
   std::string node_name(int32_t id) const;
   int32_t n_nodes() const { return hdr_->n_nodes.load(std::memory_order_acquire); }
   bool remove_node(int32_t id);  // only when no pods are on it
@@ -109,6 +114,9 @@ class Ledger {
 
   // Filter/score: plan for `d` on node `id`, cached per (node, generation, demand, options).
   int32_t assume(int32_t id, const Demand& d, const Options& o, Plan* plan);
+  // assume() over many nodes for one demand (the filter / priorities verbs): the demand and
+  // option hashes are computed once and only rc + score leave the plan cache.
+  void assume_many(const int32_t* ids, int n, const Demand& d, const Options& o, int32_t* rc, int32_t* score);
 
   // Bind: choose (cache hit if the node is unchanged) and allocate atomically; records the
   // pod as Reserved. Idempotent for the same key on the same node. A nomination of the
@@ -178,26 +186,34 @@ class Ledger {
       return node == o.node && gen == o.gen && dh == o.dh && oh == o.oh;
     }
   };
-  struct CacheHash {
-    size_t operator()(const CacheKey& k) const {
-      return static_cast<size_t>(k.dh ^ (k.gen * 0x9e3779b97f4a7c15ULL) ^ (k.oh << 1) ^
-                                 static_cast<uint64_t>(k.node) * 0xff51afd7ed558ccdULL);
-    }
-  };
   struct CacheVal {
     int32_t rc;
     Plan plan;
   };
-  // Plan cache, sharded by node id so concurrent filters (native front-end workers) on
-  // different nodes never contend on one mutex.
-  static constexpr int kCacheShards = 64;
-  struct CacheShard {
-    std::mutex mu;
-    std::unordered_map<CacheKey, CacheVal, CacheHash> map;
+  // Plan cache: process-local, one small direct-mapped table per node slot (a 2-way probe
+  // on the demand/options hash), guarded by a per-node spin flag. Entries carry the node
+  // generation they were computed at, so a change to the node invalidates them without any
+  // clearing; filters of different nodes never share a lock.
+  static constexpr int kCacheWays = 32;
+  struct CacheEntry {
+    uint64_t gen = 0, dh = 0, oh = 0;
+    bool used = false;
+    CacheVal val{};
   };
-  mutable CacheShard cache_[kCacheShards];
-  CacheShard& cache_shard(int32_t node) const { return cache_[static_cast<uint32_t>(node) % kCacheShards]; }
+  struct NodeCache {
+    std::atomic<bool> busy{false};
+    CacheEntry e[kCacheWays];
+    void lock() {
+      for (int spins = 0; busy.exchange(true, std::memory_order_acquire);)
+        while (busy.load(std::memory_order_relaxed))
+          if (++spins > 64) std::this_thread::yield();
+    }
+    void unlock() { busy.store(false, std::memory_order_release); }
+  };
+  mutable std::unique_ptr<NodeCache[]> cache_;
+  uint32_t cache_nodes_ = 0;
   bool cache_get(const CacheKey& k, int32_t* rc, Plan* plan) const;
+  bool cache_get_score(const CacheKey& k, int32_t* rc, int32_t* score) const;
   void cache_put(const CacheKey& k, int32_t rc, const Plan& plan);
   mutable std::mutex names_mu_;
   mutable std::unordered_map<std::string, int32_t> names_;  // process-local name index

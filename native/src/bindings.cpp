@@ -528,6 +528,22 @@ PYBIND11_MODULE(_native, m) {
         d["phase_max_s"] = ph;
         return d;
       })
+      .def("time_verb",
+           [](Frontend& f, const py::bytes& body, bool prioritize, int iters) {
+             const std::string b = body;
+             std::string out;
+             bool ok = true;
+             double dt;
+             {
+               py::gil_scoped_release nogil;
+               const double t0 = mono_now();
+               for (int i = 0; i < iters && ok; ++i) ok = f.filter_verb(b, prioritize, &out);
+               dt = mono_now() - t0;
+             }
+             return py::make_tuple(ok, dt / std::max(1, iters), py::bytes(out));
+           },
+           py::arg("body"), py::arg("prioritize") = false, py::arg("iters") = 1000,
+           "Runs the native verb `iters` times in place (no socket): (ok, seconds per call, last body).")
       .def("reset_max", &Frontend::reset_max, "zero the per-verb and event-loop maxima");
   m.def("mono_now", &mono_now);
   m.def("presize_fd_table", &presize_fd_table, py::arg("want") = 16384,
@@ -571,6 +587,7 @@ PYBIND11_MODULE(_native, m) {
         d["unschedulable_attempts"] = r.unschedulable_attempts;
         d["t_first_filter"] = r.t_first_filter;
         d["cycle_max_s"] = r.cycle_max_s;
+        d["cycle_sum_s"] = r.cycle_sum_s;
         d["t_last_bind"] = r.t_last_bind;
         d["bind_latencies"] = r.bind_latencies;
         d["e2e_latencies"] = r.e2e_latencies;

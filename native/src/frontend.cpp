@@ -172,6 +172,23 @@ bool quantity_value(std::string_view s, bool mib, int64_t* out) {
   return true;
 }
 
+// 64-bit hash of a byte string, eight bytes per step (keys the per-worker node-id cache;
+// hits are verified name by name, so a collision costs a lookup, never a wrong answer).
+static uint64_t text_hash(std::string_view s) {
+  uint64_t h = 0x9e3779b97f4a7c15ULL ^ s.size();
+  size_t i = 0;
+  for (; i + 8 <= s.size(); i += 8) {
+    uint64_t w;
+    std::memcpy(&w, s.data() + i, 8);
+    h = (h ^ w) * 0xff51afd7ed558ccdULL;
+    h ^= h >> 32;
+  }
+  uint64_t tail = 0;
+  std::memcpy(&tail, s.data() + i, s.size() - i);
+  h = (h ^ tail) * 0xc4ceb9fe1a85ec53ULL;
+  return h ^ (h >> 29);
+}
+
 static void atomic_max(std::atomic<uint64_t>* m, uint64_t v) {
   uint64_t cur = m->load(std::memory_order_relaxed);
   while (v > cur && !m->compare_exchange_weak(cur, v, std::memory_order_relaxed)) {
@@ -804,19 +821,43 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
       }
     }
   }
-  // node ids: any unknown node goes to Python, which can register it from its informer
+  // node ids: any unknown node goes to Python, which can register it from its informer.
+  // kube-scheduler sends the same node list over and over, so each worker remembers the ids
+  // of the last lists it resolved (keyed by the array's raw text) and only checks that slot
+  // `id` still carries that name; a miss falls back to the ledger's name index.
   const int32_t nn = d.at(names).count;
-  std::vector<int32_t> ids;
   std::vector<std::string_view> nv;
-  ids.reserve(nn);
   nv.reserve(nn);
   for (int32_t c = d.at(names).first; c >= 0; c = d.at(c).next) {
     if (!d.is(c, json::Type::kStr)) return false;
-    const std::string_view name = d.str(c);
-    const int32_t id = ledger_->find_node(std::string(name));
-    if (id < 0) return false;
-    ids.push_back(id);
-    nv.push_back(name);
+    nv.push_back(d.str(c));
+  }
+  struct IdCache {
+    const Ledger* owner = nullptr;
+    uint64_t key[4] = {};
+    std::vector<int32_t> ids[4];
+    unsigned next = 0;
+  };
+  thread_local IdCache idc;
+  if (idc.owner != ledger_.get()) idc = IdCache{}, idc.owner = ledger_.get();
+  const std::string_view raw_names = d.raw(names);
+  const uint64_t nkey = text_hash(raw_names) | 1;   // 0 marks an empty slot
+  int slot = -1;
+  for (int k = 0; k < 4; ++k)
+    if (idc.key[k] == nkey && idc.ids[k].size() == nv.size()) slot = k;
+  if (slot < 0) {
+    slot = static_cast<int>(idc.next++ % 4);
+    idc.key[slot] = nkey;
+    idc.ids[slot].assign(nv.size(), -1);
+  }
+  std::vector<int32_t>& ids = idc.ids[slot];
+  for (size_t i = 0; i < nv.size(); ++i) {
+    if (ids[i] >= 0 && ledger_->node_named(ids[i], nv[i])) continue;
+    ids[i] = ledger_->find_node(std::string(nv[i]));
+    if (ids[i] < 0) {
+      idc.key[slot] = 0;
+      return false;
+    }
   }
   Options o;
   bool normalize, nominate;
@@ -844,8 +885,10 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
       if (dem.c[i].mib) dstr += "," + std::to_string(dem.c[i].mib) + "Mi";
       dstr += ")";
     }
+    std::vector<int32_t> rcs(ids.size()), sc(ids.size());
+    ledger_->assume_many(ids.data(), static_cast<int>(ids.size()), dem, o, rcs.data(), sc.data());
     for (size_t i = 0; i < ids.size(); ++i) {
-      const int32_t rc = ledger_->assume(ids[i], dem, o, &p);
+      const int32_t rc = rcs[i];
       if (rc == kOk) {
         if (!first_ok) ok += ",";
         json::append_quoted(&ok, nv[i]);
@@ -864,12 +907,13 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     r = "{\"Nodes\":null,\"NodeNames\":" + ok + ",\"FailedNodes\":" + failed + ",\"Error\":\"\"}";
     return true;
   }
-  std::vector<int32_t> scores(ids.size());
+  std::vector<int32_t> scores(ids.size()), rcs(ids.size());
+  ledger_->assume_many(ids.data(), static_cast<int>(ids.size()), dem, o, rcs.data(), scores.data());
   int64_t best = -1;
   int n_best = 0;
   for (size_t i = 0; i < ids.size(); ++i) {
-    const int32_t rc = ledger_->assume(ids[i], dem, o, &p);
-    scores[i] = rc == kOk ? p.score : 0;
+    const int32_t rc = rcs[i];
+    if (rc != kOk) scores[i] = 0;
     if (rc != kOk) continue;
     if (best < 0 || scores[i] > scores[best]) {
       best = static_cast<int64_t>(i);

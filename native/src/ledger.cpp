@@ -160,6 +160,8 @@ Ledger::Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, b
     }
   }
   hdr_->attached.fetch_add(1);
+  cache_nodes_ = hdr_->max_nodes;
+  cache_.reset(new NodeCache[cache_nodes_]);
 }
 
 Ledger::~Ledger() {
@@ -355,21 +357,97 @@ uint64_t Ledger::generation(int32_t id) const {
   return n ? n->generation.load(std::memory_order_acquire) : 0;
 }
 
+namespace {
+inline int cache_way(uint64_t dh, uint64_t oh) {
+  return static_cast<int>((dh ^ (oh * 0x9e3779b97f4a7c15ULL)) >> 59);   // top 5 bits: 0..31
+}
+}  // namespace
+
 bool Ledger::cache_get(const CacheKey& k, int32_t* rc, Plan* plan) const {
-  CacheShard& sh = cache_shard(k.node);
-  std::lock_guard<std::mutex> g(sh.mu);
-  auto it = sh.map.find(k);
-  if (it == sh.map.end()) return false;
-  *rc = it->second.rc;
-  *plan = it->second.plan;
-  return true;
+  if (static_cast<uint32_t>(k.node) >= cache_nodes_) return false;
+  NodeCache& c = cache_[k.node];
+  const int w = cache_way(k.dh, k.oh);
+  c.lock();
+  for (int j = 0; j < 2; ++j) {
+    const CacheEntry& e = c.e[(w + j) % kCacheWays];
+    if (e.used && e.gen == k.gen && e.dh == k.dh && e.oh == k.oh) {
+      *rc = e.val.rc;
+      *plan = e.val.plan;
+      c.unlock();
+      return true;
+    }
+  }
+  c.unlock();
+  return false;
+}
+
+bool Ledger::cache_get_score(const CacheKey& k, int32_t* rc, int32_t* score) const {
+  if (static_cast<uint32_t>(k.node) >= cache_nodes_) return false;
+  NodeCache& c = cache_[k.node];
+  const int w = cache_way(k.dh, k.oh);
+  c.lock();
+  for (int j = 0; j < 2; ++j) {
+    const CacheEntry& e = c.e[(w + j) % kCacheWays];
+    if (e.used && e.gen == k.gen && e.dh == k.dh && e.oh == k.oh) {
+      *rc = e.val.rc;
+      *score = e.val.plan.score;
+      c.unlock();
+      return true;
+    }
+  }
+  c.unlock();
+  return false;
 }
 
 void Ledger::cache_put(const CacheKey& k, int32_t rc, const Plan& plan) {
-  CacheShard& sh = cache_shard(k.node);
-  std::lock_guard<std::mutex> g(sh.mu);
-  if (sh.map.size() > 8192) sh.map.clear();
-  sh.map[k] = CacheVal{rc, plan};
+  if (static_cast<uint32_t>(k.node) >= cache_nodes_) return;
+  NodeCache& c = cache_[k.node];
+  const int w = cache_way(k.dh, k.oh);
+  c.lock();
+  // same key or an unused/stale way first; else replace the older-generation one
+  CacheEntry* a = &c.e[w];
+  CacheEntry* b = &c.e[(w + 1) % kCacheWays];
+  CacheEntry* dst = a;
+  if (a->used && a->gen == k.gen && !(a->dh == k.dh && a->oh == k.oh))
+    dst = (!b->used || b->gen != k.gen || (b->dh == k.dh && b->oh == k.oh)) ? b : a;
+  dst->gen = k.gen;
+  dst->dh = k.dh;
+  dst->oh = k.oh;
+  dst->used = true;
+  dst->val.rc = rc;
+  dst->val.plan = plan;
+  c.unlock();
+}
+
+bool Ledger::node_named(int32_t id, std::string_view name) const {
+  const NodeSlot* n = node(id);
+  return n && n->in_use && name.size() < kNameLen && std::strncmp(n->name, name.data(), name.size()) == 0 &&
+         n->name[name.size()] == '\0';
+}
+
+void Ledger::assume_many(const int32_t* ids, int count, const Demand& d, const Options& o, int32_t* rc,
+                         int32_t* score) {
+  const uint64_t dh = d.hash(), oh = o.hash();
+  Plan plan;
+  for (int i = 0; i < count; ++i) {
+    const int32_t id = ids[i];
+    NodeSlot* n = node(id);
+    score[i] = 0;
+    if (!n || !n->in_use) {
+      rc[i] = kErrUnknownNode;
+      continue;
+    }
+    if (cache_get_score(CacheKey{id, n->generation.load(std::memory_order_acquire), dh, oh}, &rc[i], &score[i]))
+      continue;
+    NodeSnapshot snap;
+    if (!snapshot(id, &snap)) {
+      rc[i] = kErrUnknownNode;
+      continue;
+    }
+    rc[i] = choose(snap.devs, snap.n_devs, &snap.topo, d, o, &plan);
+    score[i] = plan.score;
+    cache_put(CacheKey{id, snap.generation, dh, oh}, rc[i], plan);
+  }
 }
 
 int32_t Ledger::assume(int32_t id, const Demand& d, const Options& o, Plan* plan) {
@@ -657,17 +735,21 @@ FragStats Ledger::frag(int32_t min_request) const {
 }
 
 void Ledger::clear_cache() {
-  for (auto& sh : cache_) {
-    std::lock_guard<std::mutex> g(sh.mu);
-    sh.map.clear();
+  for (uint32_t i = 0; i < cache_nodes_; ++i) {
+    NodeCache& c = cache_[i];
+    c.lock();
+    for (auto& e : c.e) e.used = false;
+    c.unlock();
   }
 }
 
 size_t Ledger::cache_size() const {
   size_t n = 0;
-  for (auto& sh : cache_) {
-    std::lock_guard<std::mutex> g(sh.mu);
-    n += sh.map.size();
+  for (uint32_t i = 0; i < cache_nodes_; ++i) {
+    NodeCache& c = cache_[i];
+    c.lock();
+    for (const auto& e : c.e) n += e.used;
+    c.unlock();
   }
   return n;
 }

@@ -575,7 +575,9 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* 
         }
       }
     }
-    r.cycle_max_s = std::max(r.cycle_max_s, now_s() - t_cycle);
+    const double dt_cycle = now_s() - t_cycle;
+    r.cycle_max_s = std::max(r.cycle_max_s, dt_cycle);
+    r.cycle_sum_s += dt_cycle;
     std::lock_guard<std::mutex> lk(mu);
     if (host < 0) {
       ++r.unschedulable_attempts;
