@@ -206,15 +206,16 @@ class Runtime:
         period = min(max(1.0, self.cfg.reservation_ttl_s / 4), max(0.05, self.cfg.nomination_ttl_s / 4))
         next_res = 0.0
         loop = asyncio.get_running_loop()
+        # the scans walk the whole shared pod table with the GIL released: off the event loop
         while True:
             await asyncio.sleep(period)
-            gone = self.state.sweep_nominations(self.cfg.nomination_ttl_s)
+            gone = await loop.run_in_executor(None, self.state.sweep_nominations, self.cfg.nomination_ttl_s)
             if gone:
                 log.info("released %d nominations no bind adopted", len(gone))
             if loop.time() < next_res:
                 continue
             next_res = loop.time() + max(1.0, self.cfg.reservation_ttl_s / 4)
-            stale = self.state.sweep_reservations(self.cfg.reservation_ttl_s)
+            stale = await loop.run_in_executor(None, self.state.sweep_reservations, self.cfg.reservation_ttl_s)
             if stale:
                 log.warning("released %d stale reservations", len(stale))
             if self.poller is not None:

@@ -302,17 +302,15 @@ class ClusterState:
     def sweep_reservations(self, ttl_s: float) -> list[str]:
         """Releases reservations whose bind never committed (crashed worker, lost request)."""
         stale = self.ledger.expired_reservations(ttl_s)
-        for uid in stale:
-            self.ledger.release(uid)
-        return stale
+        # only while still reserved: a bind may commit between the scan and the release
+        return [uid for uid in stale if self.ledger.drop_reservation(uid) == N.OK]
 
     def sweep_nominations(self, ttl_s: float) -> list[str]:
         """Releases nominations no bind adopted (kube-scheduler chose another node, or the
         pod was never bound)."""
         stale = self.ledger.expired_nominations(ttl_s)
-        for uid in stale:
-            self.ledger.release(uid)
-        return stale
+        # only while still nominated: a bind may adopt it between the scan and the release
+        return [uid for uid in stale if self.ledger.drop_nomination(uid) == N.OK]
 
     # ------------------------------------------------------------------ telemetry
     def set_load(self, node_name: str, device: int, usage: float) -> bool:

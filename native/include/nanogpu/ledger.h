@@ -134,6 +134,8 @@ class Ledger {
   // by dropping its own nomination, so its filter and scores never count it against itself.
   // kOk = dropped, kOkExisting = reserved/committed (left alone), kErrUnknownPod = none.
   int32_t drop_nomination(const std::string& key);
+  // Releases `key` only while it is still a reservation (a sweep racing a commit).
+  int32_t drop_reservation(const std::string& key);
   // Allocates an explicit plan (pods bound by someone else / rebuild from annotations).
   int32_t allocate_plan(int32_t id, const std::string& key, const Demand& d, const Plan& plan,
                         bool committed);
@@ -163,7 +165,7 @@ class Ledger {
   int32_t reserve_as(int32_t id, const std::string& key, const Demand& d, const Options& o, Plan* plan,
                      int32_t state);
   std::vector<std::string> expired(int32_t state, double older_than_s) const;
-  int32_t release_if(const std::string& key, bool only_nominated);
+  int32_t release_if(const std::string& key, int32_t only_state);   // -1: any state
   PodSlot* find_pod_locked(int s, uint64_t h, const char* key) const;
   PodSlot* insert_pod_locked(int s, uint64_t h, const char* key);
 

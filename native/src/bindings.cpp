@@ -416,8 +416,9 @@ PYBIND11_MODULE(_native, m) {
              return out;
            },
            py::arg("node") = -1)
-      .def("expired_reservations", &Ledger::expired_reservations)
-      .def("expired_nominations", &Ledger::expired_nominations)
+      .def("expired_reservations", &Ledger::expired_reservations, py::call_guard<py::gil_scoped_release>())
+      .def("expired_nominations", &Ledger::expired_nominations, py::call_guard<py::gil_scoped_release>())
+      .def("drop_reservation", &Ledger::drop_reservation, py::call_guard<py::gil_scoped_release>())
       .def("drop_nomination", &Ledger::drop_nomination, py::call_guard<py::gil_scoped_release>())
       .def(
           "nominate",

@@ -606,11 +606,14 @@ int32_t Ledger::commit(const std::string& key) {
   return kOk;
 }
 
-int32_t Ledger::release(const std::string& key) { return release_if(key, false); }
+int32_t Ledger::release(const std::string& key) { return release_if(key, -1); }
 
-int32_t Ledger::drop_nomination(const std::string& key) { return release_if(key, true); }
+int32_t Ledger::drop_nomination(const std::string& key) { return release_if(key, kPodNominated); }
 
-int32_t Ledger::release_if(const std::string& key, bool only_nominated) {
+int32_t Ledger::drop_reservation(const std::string& key) { return release_if(key, kPodReserved); }
+
+int32_t Ledger::release_if(const std::string& key, int32_t only_state) {
+  const bool only = only_state >= 0;
   const uint64_t h = key_hash(key.c_str());
   const int s = shard_of(h);
   int32_t id;
@@ -619,7 +622,7 @@ int32_t Ledger::release_if(const std::string& key, bool only_nominated) {
     Unlock us{&hdr_->shard_mu[s]};
     PodSlot* p = find_pod_locked(s, h, key.c_str());
     if (!p) return kErrUnknownPod;
-    if (only_nominated && p->state != kPodNominated) return kOkExisting;
+    if (only && p->state != only_state) return kOkExisting;
     id = p->node;
   }
   NodeSlot* n = node(id);
@@ -630,7 +633,7 @@ int32_t Ledger::release_if(const std::string& key, bool only_nominated) {
   Unlock us{&hdr_->shard_mu[s]};
   PodSlot* p = find_pod_locked(s, h, key.c_str());
   if (!p || p->node != id) return kErrUnknownPod;  // raced with another release
-  if (only_nominated && p->state != kPodNominated) return kOkExisting;   // adopted meanwhile
+  if (only && p->state != only_state) return kOkExisting;   // adopted / committed meanwhile
   unapply(n->devs, n->n_devs, p->demand, p->plan);
   p->state = kPodTombstone;
   --hdr_->shard_live[s];

@@ -13,6 +13,7 @@ import math
 import pytest
 from aiohttp import web
 
+from nanogpu import _native as N
 from nanogpu import types as T
 from nanogpu.app import Config, Runtime
 from nanogpu.config.policy import MetricQuery, PolicySpec, Period, parse_duration, parse_policy
@@ -338,3 +339,18 @@ def test_reservation_ttl_sweeper_releases_lost_binds():
     assert st.sweep_reservations(0.0) == [pu.pod_uid(pod)]
     assert st.status()["n0"]["GPUs"][0]["Percent"] == 100
     assert not math.isnan(0.0)
+
+
+def test_sweeps_never_release_a_pod_that_moved_on():
+    """The scans run off the event loop, so a bind can commit a reservation (or adopt a
+    nomination) between the scan and the release: those releases are state-checked."""
+    st = ClusterState()
+    st.register_node(node("n0", 1))
+    pod = pu.make_pod("racer", [("c", 40)])
+    st.reserve(pod, "n0")
+    uid = pu.pod_uid(pod)
+    assert st.ledger.expired_reservations(0.0) == [uid]
+    st.commit(uid)                                    # the bind commits after the scan
+    assert st.ledger.drop_reservation(uid) != N.OK    # the sweep's release is a no-op
+    assert st.status()["n0"]["GPUs"][0]["Percent"] == 60
+    assert st.sweep_reservations(0.0) == []
