@@ -69,6 +69,9 @@ def parse_args():
                     help="native front door busy-poll window")
     ap.add_argument("--driver", default="native", choices=["native", "python"],
                     help="kube-scheduler stand-in: C++ (native/src/schedsim.cpp) or the Python threaded one")
+    ap.add_argument("--cpu-affinity", default="auto", choices=["auto", "none"],
+                    help="auto: pin each rank (extender + its scheduler stand-in) to one L3 domain on its "
+                         "GPU's NUMA node (nanogpu.affinity)")
     ap.add_argument("--stall-trace", default="",
                     help="sample the extender's Python threads every ms in the timed steps; write gaps/stalls here")
     ap.add_argument("--inproc-driver", action="store_true",
@@ -461,8 +464,24 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
     return results
 
 
+def _cpulist(cpus: list[int]) -> str:
+    return ",".join(map(str, cpus)) if cpus else "unpinned"
+
+
 def main() -> int:
     args = parse_args()
+    cpus: list[int] = []
+    if args.cpu_affinity == "auto":
+        # before any process is spawned or the GPU is touched: children inherit the mask
+        from nanogpu import affinity
+
+        lr, lws = int(os.environ.get("LOCAL_RANK", "0")), int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+        numas = [] if args.no_gpu else affinity.gpu_numa_nodes()
+        mine = numas[lr] if lr < len(numas) else -1
+        ranks = [numas[r] if r < len(numas) else -1 for r in range(lws)] if lws > 1 else None
+        cpus = affinity.pick_cpus(mine, lr, ranks)
+        if not affinity.apply(cpus):
+            cpus = []
     drv_proc, conn = None, None
     if not args.inproc_driver:
         # started before anything touches the GPU: a fresh interpreter, no HIP state
@@ -522,7 +541,8 @@ def main() -> int:
                        "global_batch": args.pods, "seq_len": None,
                        "parallelism": f"{d.world} extender worker(s), shared native ledger",
                        "cluster": f"{args.nodes} nodes x {args.gpus_per_node} MI355X ({args.partition})",
-                       "api_rtt_ms": args.api_rtt_ms},
+                       "api_rtt_ms": args.api_rtt_ms,
+                       "cpus_rank0": _cpulist(cpus)},
             "p50_bind_ms": round(p50, 4) if p50 is not None else None,
             "p99_bind_ms": round(p99, 4) if p99 is not None else None,
             "frag_pct": round(statistics.mean(f["frag_pct"] for f in fr), 3) if fr else None,

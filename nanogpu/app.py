@@ -63,6 +63,7 @@ class Config:
     identity: str = ""
     frontend_threads: int = 4
     busy_poll_us: int = 0                       # native workers spin this long after an event
+    cpu_affinity: str = "none"                  # none | auto (one L3 domain per worker) | cpu list
     gpu_node_selectors: list = field(default_factory=lambda: [T.AMD_GPU_NODE_LABEL, T.LEGACY_GPU_NODE_LABEL])
 
 
@@ -280,8 +281,26 @@ async def serve_forever(cfg: Config, worker: int = 0) -> int:
     return 0
 
 
+def pin_worker(cfg: Config, worker: int) -> list[int]:
+    """--cpu-affinity: `auto` gives each worker process its own L3 domain (nanogpu.affinity),
+    an explicit list ("0-7,16") pins every worker to it; `none` leaves placement to the OS."""
+    from . import affinity
+
+    if cfg.cpu_affinity in ("", "none"):
+        return []
+    if cfg.cpu_affinity == "auto":
+        cpus = affinity.pick_cpus(-1, worker, [-1] * cfg.workers if cfg.workers > 1 else None)
+    else:
+        cpus = affinity._parse_list(cfg.cpu_affinity)
+    if affinity.apply(cpus):
+        log.info("worker %d pinned to CPUs %s", worker, cpus)
+        return cpus
+    return []
+
+
 def run(cfg: Config) -> int:
     if cfg.workers <= 1:
+        pin_worker(cfg, 0)
         return asyncio.run(serve_forever(cfg, 0))
     if not cfg.ledger_path:
         cfg.ledger_path = f"/dev/shm/nanogpu-ledger-{os.getpid()}"
@@ -294,6 +313,7 @@ def run(cfg: Config) -> int:
         pid = os.fork()
         if pid == 0:
             try:
+                pin_worker(cfg, w)
                 code = asyncio.run(serve_forever(cfg, w))
             except BaseException:
                 log.exception("worker %d crashed", w)

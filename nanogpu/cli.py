@@ -68,6 +68,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--lease-name", default="nano-gpu-scheduler")
     p.add_argument("--lease-namespace", default=os.environ.get("POD_NAMESPACE", "kube-system"))
     p.add_argument("--identity", default=os.environ.get("POD_NAME", ""))
+    p.add_argument("--cpu-affinity", default="none",
+                   help="none | auto (each worker on its own L3 domain, nanogpu.affinity) | CPU list, e.g. 8-15")
     return p
 
 
@@ -90,4 +92,5 @@ def parse(argv: list[str] | None = None) -> Config:
         nominate=not a.no_nominate, nomination_ttl_s=parse_duration(a.nomination_ttl),
         fake_cluster=a.fake_cluster, fake_gpus_per_node=a.fake_gpus_per_node, fake_partition=a.fake_partition,
         seed=a.seed, frontend=a.frontend, frontend_threads=max(1, a.frontend_threads), busy_poll_us=a.busy_poll_us,
-        leader_elect=a.leader_elect, lease_name=a.lease_name, lease_namespace=a.lease_namespace, identity=a.identity)
+        leader_elect=a.leader_elect, lease_name=a.lease_name, lease_namespace=a.lease_namespace, identity=a.identity,
+        cpu_affinity=a.cpu_affinity)

@@ -1,0 +1,60 @@
+"""CPU placement (nanogpu.affinity) on a synthetic sysfs tree shaped like the MI355X host:
+2 sockets, L3 domains of physical cores with SMT siblings offset by the core count."""
+from pathlib import Path
+
+from nanogpu import affinity as A
+
+
+def make_tree(root: Path, sockets=2, doms_per_socket=3, cores_per_dom=4) -> set[int]:
+    ncores = sockets * doms_per_socket * cores_per_dom
+    for core in range(ncores):
+        dom = core // cores_per_dom
+        node = dom // doms_per_socket
+        l3 = [c for c in range(ncores) if c // cores_per_dom == dom]
+        l3_all = l3 + [c + ncores for c in l3]
+        for cpu in (core, core + ncores):           # SMT siblings
+            base = root / f"cpu{cpu}"
+            (base / "topology").mkdir(parents=True)
+            (base / "topology" / "thread_siblings_list").write_text(f"{core},{core + ncores}\n")
+            idx = base / "cache" / "index3"
+            idx.mkdir(parents=True)
+            (idx / "level").write_text("3\n")
+            (idx / "shared_cpu_list").write_text(f"{l3_all[0]}-{l3_all[len(l3) - 1]},{l3_all[len(l3)]}-{l3_all[-1]}\n")
+            (base / f"node{node}").mkdir()
+    return set(range(2 * ncores))
+
+
+def test_domains_are_physical_cores_per_l3(tmp_path):
+    allowed = make_tree(tmp_path)
+    doms = A.l3_domains(allowed, root=tmp_path)
+    assert doms == [[0, 1, 2, 3], [4, 5, 6, 7], [8, 9, 10, 11], [12, 13, 14, 15], [16, 17, 18, 19],
+                    [20, 21, 22, 23]]
+    assert A.numa_of_cpu(13, root=tmp_path) == 1
+    # a restricted cpuset keeps only what it allows (here: no SMT siblings at all)
+    assert A.l3_domains({8, 9, 30}, root=tmp_path) == [[8, 9]]
+
+
+def test_ranks_of_a_node_get_distinct_domains_on_their_gpu_numa(tmp_path, monkeypatch):
+    allowed = make_tree(tmp_path)
+    monkeypatch.setattr(A, "SYS_CPU", tmp_path)
+    monkeypatch.setattr(A.os, "sched_getaffinity", lambda pid: allowed)
+    real_l3, real_numa = A.l3_domains, A.numa_of_cpu
+    monkeypatch.setattr(A, "l3_domains", lambda allowed=None, root=tmp_path: real_l3(allowed, root))
+    monkeypatch.setattr(A, "numa_of_cpu", lambda cpu, root=tmp_path: real_numa(cpu, root))
+    gpu_numa = [0, 0, 1, 1]                          # 4 ranks, two GPUs per socket
+    picks = [A.pick_cpus(gpu_numa[r], r, gpu_numa) for r in range(4)]
+    # CPU 0's domain is skipped; each rank stays on its GPU's socket; no domain is shared
+    assert picks == [[4, 5, 6, 7], [8, 9, 10, 11], [12, 13, 14, 15], [16, 17, 18, 19]]
+
+
+def test_single_rank_takes_the_least_busy_domain(tmp_path, monkeypatch):
+    allowed = make_tree(tmp_path)
+    real_l3, real_numa = A.l3_domains, A.numa_of_cpu
+    monkeypatch.setattr(A.os, "sched_getaffinity", lambda pid: allowed)
+    monkeypatch.setattr(A, "l3_domains", lambda allowed=None, root=tmp_path: real_l3(allowed, root))
+    monkeypatch.setattr(A, "numa_of_cpu", lambda cpu, root=tmp_path: real_numa(cpu, root))
+    busy = {c: 0.9 for c in range(24)}
+    busy.update({c: 0.1 for c in (8, 9, 10, 11)})
+    monkeypatch.setattr(A, "_busy", lambda cpus, w: {c: busy[c] for c in cpus})
+    assert A.pick_cpus(0) == [8, 9, 10, 11]
+    assert A.pick_cpus(1) in ([12, 13, 14, 15], [16, 17, 18, 19], [20, 21, 22, 23])
