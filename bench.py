@@ -364,11 +364,14 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
             except Exception:
                 pass
         # the pod controller releases on DELETED; wait until our shares are gone
+        # (the in-process watch delivers the DELETED events on the next loop iterations: yield
+        # first, and only then back off to short sleeps)
         uids = [pu.pod_uid(p) for p in pods]
-        for _ in range(20000):
-            if not any(rt.state.ledger.lookup(u) for u in uids):
+        lookup = rt.state.ledger.lookup
+        for i in range(20000):
+            if not any(lookup(u) for u in uids):
                 break
-            await asyncio.sleep(0.0005)
+            await asyncio.sleep(0 if i < 50 else 0.0005)
         await pod_ctrl.queue.drain(5.0)
         phases = {"create_ms": 1e3 * tc, "schedule_ms": 1e3 * summary["span_s"],
                   "release_ms": 1e3 * (time.perf_counter() - ts)}
