@@ -15,6 +15,7 @@ import logging
 import os
 import ssl
 import tempfile
+import time
 import urllib.parse
 from dataclasses import dataclass
 from typing import Any, AsyncIterator
@@ -50,17 +51,20 @@ class KubeConfig:
     cert_file: str | None = None
     key_file: str | None = None
     insecure: bool = False
+    token_file: str | None = None      # re-read while running (projected tokens rotate)
 
     @classmethod
     def in_cluster(cls) -> "KubeConfig":
         host, port = os.environ.get("KUBERNETES_SERVICE_HOST"), os.environ.get("KUBERNETES_SERVICE_PORT")
         if not host or not port:
             raise RuntimeError("not running in a cluster (KUBERNETES_SERVICE_HOST unset)")
-        with open(os.path.join(SA_DIR, "token")) as f:
+        token_file = os.path.join(SA_DIR, "token")
+        with open(token_file) as f:
             token = f.read().strip()
         if ":" in host:
             host = f"[{host}]"
-        return cls(server=f"https://{host}:{port}", token=token, ca_file=os.path.join(SA_DIR, "ca.crt"))
+        return cls(server=f"https://{host}:{port}", token=token, ca_file=os.path.join(SA_DIR, "ca.crt"),
+                   token_file=token_file)
 
     @classmethod
     def from_kubeconfig(cls, path: str, context: str | None = None) -> "KubeConfig":
@@ -85,7 +89,12 @@ class KubeConfig:
                 return p
             return None
 
-        return cls(server=cluster["server"].rstrip("/"), token=user.get("token"),
+        token_file = user.get("tokenFile")
+        token = user.get("token")
+        if not token and token_file:
+            with open(token_file) as f:
+                token = f.read().strip()
+        return cls(server=cluster["server"].rstrip("/"), token=token, token_file=token_file,
                    ca_file=materialise("certificate-authority-data", "certificate-authority", cluster),
                    cert_file=materialise("client-certificate-data", "client-certificate", user),
                    key_file=materialise("client-key-data", "client-key", user),
@@ -114,20 +123,49 @@ class KubeConfig:
 
 
 class KubeClient:
-    """Async client; one keep-alive connection pool per process."""
+    """Async client; one keep-alive connection pool per process.
 
-    def __init__(self, config: KubeConfig, timeout_s: float = 30.0, pool: int = 64):
+    Bearer tokens from a file (the in-cluster service-account token, a kubeconfig
+    `tokenFile`) are re-read when the file changes, checked at most every
+    `token_check_s`, and at once after a 401: kubelet rotates projected tokens while the
+    extender keeps running (client-go reloads them the same way)."""
+
+    def __init__(self, config: KubeConfig, timeout_s: float = 30.0, pool: int = 64, token_check_s: float = 60.0):
         self.config = config
         self._timeout = aiohttp.ClientTimeout(total=timeout_s)
         self._pool = pool
         self._session: aiohttp.ClientSession | None = None
         self.calls = 0
+        self.token_check_s = token_check_s
+        self._token = config.token
+        self._token_mtime = self._mtime()
+        self._token_checked = time.monotonic()
+
+    def _mtime(self) -> float:
+        try:
+            return os.stat(self.config.token_file).st_mtime if self.config.token_file else 0.0
+        except OSError:
+            return 0.0
+
+    def _auth(self, force: bool = False) -> dict | None:
+        """Authorization header for the next request (re-reading a rotated token file)."""
+        if self.config.token_file:
+            now = time.monotonic()
+            if force or now - self._token_checked >= self.token_check_s:
+                self._token_checked = now
+                m = self._mtime()
+                if force or m != self._token_mtime:
+                    try:
+                        with open(self.config.token_file) as f:
+                            self._token = f.read().strip() or self._token
+                        self._token_mtime = m
+                    except OSError:
+                        pass
+        return {"Authorization": f"Bearer {self._token}"} if self._token else None
 
     async def _s(self) -> aiohttp.ClientSession:
         if self._session is None or self._session.closed:
             headers = {"Accept": "application/json", "User-Agent": "nano-gpu-scheduler-amd/0.1"}
-            if self.config.token:
-                headers["Authorization"] = f"Bearer {self.config.token}"
             self._session = aiohttp.ClientSession(
                 headers=headers, timeout=self._timeout,
                 connector=aiohttp.TCPConnector(limit=self._pool, ssl=self.config.ssl_context()),
@@ -144,17 +182,24 @@ class KubeClient:
         s = await self._s()
         url = self.config.server + path
         data = None if body is None else json.dumps(body, separators=(",", ":"))
-        self.calls += 1
-        async with s.request(method, url, data=data, params=params,
-                             headers={"Content-Type": content_type} if data is not None else None) as r:
-            text = await r.text()
-            if r.status >= 400:
-                try:
-                    st = json.loads(text)
-                    raise ApiError(r.status, st.get("message", text), st.get("reason", ""))
-                except (ValueError, AttributeError):
-                    raise ApiError(r.status, text) from None
-            return json.loads(text) if text else None
+        for attempt in (0, 1):
+            self.calls += 1
+            headers = dict(self._auth(force=attempt == 1) or {})
+            if data is not None:
+                headers["Content-Type"] = content_type
+            async with s.request(method, url, data=data, params=params, headers=headers or None) as r:
+                text = await r.text()
+                status = r.status
+            if status == 401 and attempt == 0 and self.config.token_file:
+                continue                      # the token may have rotated under us: re-read once
+            break
+        if status >= 400:
+            try:
+                st = json.loads(text)
+                raise ApiError(status, st.get("message", text), st.get("reason", ""))
+            except (ValueError, AttributeError):
+                raise ApiError(status, text) from None
+        return json.loads(text) if text else None
 
     # --------------------------------------------------------------------- pods
     async def get_pod(self, ns: str, name: str) -> dict:
@@ -242,7 +287,8 @@ class KubeClient:
         if label_selector:
             params["labelSelector"] = label_selector
         url = f"{self.config.server}/api/v1/{resource}?{urllib.parse.urlencode(params)}"
-        async with s.get(url, timeout=aiohttp.ClientTimeout(total=None, sock_read=timeout_s + 30)) as r:
+        async with s.get(url, timeout=aiohttp.ClientTimeout(total=None, sock_read=timeout_s + 30),
+                         headers=self._auth()) as r:
             if r.status >= 400:
                 raise ApiError(r.status, await r.text())
             buf = b""

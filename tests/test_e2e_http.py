@@ -174,3 +174,47 @@ def test_debug_routes_reference_pprof_paths():
             await api_runner.cleanup()
 
     asyncio.run(main())
+
+
+def test_client_follows_a_rotated_service_account_token(tmp_path):
+    """Projected service-account tokens rotate while the extender runs: the client re-reads
+    the token file when it changes and retries once after a 401."""
+    from aiohttp import web
+
+    from nanogpu.k8s.client import KubeClient, KubeConfig
+
+    tok = tmp_path / "token"
+    tok.write_text("t1\n")
+    valid = {"tok": "t1"}
+    seen = []
+
+    async def get_pod(request):
+        seen.append(request.headers.get("Authorization"))
+        if request.headers.get("Authorization") != f"Bearer {valid['tok']}":
+            return web.json_response({"kind": "Status", "message": "Unauthorized", "reason": "Unauthorized"},
+                                     status=401)
+        return web.json_response({"metadata": {"name": request.match_info["name"]}})
+
+    async def main():
+        app = web.Application()
+        app.router.add_get("/api/v1/namespaces/{ns}/pods/{name}", get_pod)
+        runner = web.AppRunner(app)
+        await runner.setup()
+        site = web.TCPSite(runner, "127.0.0.1", 0)
+        await site.start()
+        port = site._server.sockets[0].getsockname()[1]
+        c = KubeClient(KubeConfig(server=f"http://127.0.0.1:{port}", token="t1", token_file=str(tok)),
+                       token_check_s=3600.0)
+        try:
+            assert (await c.get_pod("default", "a"))["metadata"]["name"] == "a"
+            tok.write_text("t2\n")                      # kubelet rotates the file
+            valid["tok"] = "t2"                         # the old token stops working
+            assert (await c.get_pod("default", "b"))["metadata"]["name"] == "b"
+            assert seen == ["Bearer t1", "Bearer t1", "Bearer t2"]
+            assert (await c.get_pod("default", "c"))["metadata"]["name"] == "c"
+            assert seen[-1] == "Bearer t2"
+        finally:
+            await c.close()
+            await runner.cleanup()
+
+    asyncio.run(main())
