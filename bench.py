@@ -377,7 +377,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
                   "release_ms": 1e3 * (time.perf_counter() - ts)}
         if timed:
             diag = {"t0": round(t_step0, 4), "t1": round(time.perf_counter(), 4)}
-            diag.update({k: round(summary.get(k, 0.0), 2) for k in ("cycle_max_ms", "cycle_sum_ms", "bind_max_ms")})
+            diag.update({k: round(summary.get(k, 0.0), 2) for k in ("cycle_max_ms", "cycle_sum_ms", "cycle_wire_ms", "bind_max_ms")})
             diag["unschedulable"] = summary.get("unschedulable_attempts", 0)
             if rt.native is not None:
                 fs = rt.native.fe.stats()

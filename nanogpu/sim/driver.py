@@ -214,6 +214,7 @@ class DriverStats:
     t_last_bind: float = 0.0
     cycle_max_s: float = 0.0
     cycle_sum_s: float = 0.0
+    cycle_wire_s: float = 0.0
 
     def summary(self) -> dict:
         span = max(1e-9, self.t_last_bind - self.t_first_filter)
@@ -230,6 +231,7 @@ class DriverStats:
                 "bind_max_ms": 1e3 * (bl[-1] if bl else 0.0),
                 "cycle_max_ms": 1e3 * self.cycle_max_s,
                 "cycle_sum_ms": 1e3 * self.cycle_sum_s,
+                "cycle_wire_ms": 1e3 * self.cycle_wire_s,
                 "e2e_p50_ms": 1e3 * (statistics.median(self.e2e_latencies) if self.e2e_latencies else 0.0)}
 
 
@@ -601,6 +603,7 @@ class NativeSchedulerDriver:
         st.t_first_filter, st.t_last_bind = r["t_first_filter"], r["t_last_bind"]
         st.cycle_max_s = r.get("cycle_max_s", 0.0)
         st.cycle_sum_s = r.get("cycle_sum_s", 0.0)
+        st.cycle_wire_s = r.get("cycle_wire_s", 0.0)
         for (_, ns, name, _, _), node in zip(args, r["node_of"]):
             if node:
                 self.placements[f"{ns}/{name}"] = node

@@ -43,7 +43,8 @@ struct SimConfig {
 struct SimResult {
   int64_t scheduled = 0, failed = 0, bind_errors = 0, unschedulable_attempts = 0;
   double t_first_filter = 0.0, t_last_bind = 0.0;
-  double cycle_max_s = 0.0, cycle_sum_s = 0.0;   // slowest scheduling cycle (filter -> host chosen) of one pod
+  double cycle_max_s = 0.0, cycle_sum_s = 0.0;
+  double cycle_wire_s = 0.0;   // of which waiting on the extender (request sent -> response read)   // slowest scheduling cycle (filter -> host chosen) of one pod
   std::vector<double> bind_latencies, e2e_latencies;
   std::vector<std::string> node_of;   // per pod; "" = not scheduled
   std::vector<std::string> last_error;

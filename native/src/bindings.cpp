@@ -589,6 +589,7 @@ PYBIND11_MODULE(_native, m) {
         d["t_first_filter"] = r.t_first_filter;
         d["cycle_max_s"] = r.cycle_max_s;
         d["cycle_sum_s"] = r.cycle_sum_s;
+        d["cycle_wire_s"] = r.cycle_wire_s;
         d["t_last_bind"] = r.t_last_bind;
         d["bind_latencies"] = r.bind_latencies;
         d["e2e_latencies"] = r.e2e_latencies;

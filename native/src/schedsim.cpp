@@ -108,11 +108,15 @@ class Conn {
     for (int attempt = 0; attempt < 2; ++attempt) {
       if (fd_ < 0 && !connect_fd()) return false;
       req_ = post_request(host_, path, body);
-      if (send_all(req_) && read_response(status, out)) return true;
+      const double t0 = now_s();
+      const bool ok = send_all(req_) && read_response(status, out);
+      wire_s += now_s() - t0;
+      if (ok) return true;
       close_fd();   // stale keep-alive connection: one fresh attempt
     }
     return false;
   }
+  double wire_s = 0.0;   // time from the first byte sent to the whole response read
 
  private:
   bool connect_fd() {
@@ -494,6 +498,7 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* 
     cycle_conn = own.get();
   }
   Conn& cycle = *cycle_conn;
+  cycle.wire_s = 0.0;
   std::mt19937_64 rng(cfg.seed);
   std::string body, out, cands_json;
   std::vector<int> cands, fits, ties;
@@ -576,6 +581,7 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* 
       }
     }
     const double dt_cycle = now_s() - t_cycle;
+    r.cycle_wire_s = cycle.wire_s;
     r.cycle_max_s = std::max(r.cycle_max_s, dt_cycle);
     r.cycle_sum_s += dt_cycle;
     std::lock_guard<std::mutex> lk(mu);
