@@ -122,6 +122,22 @@ class KubeConfig:
         return ctx
 
 
+async def _ndjson_batches(chunks) -> AsyncIterator[list[dict]]:
+    """Newline-delimited JSON from a byte stream: the complete lines of each chunk as a list
+    (a partial last line waits for the next chunk)."""
+    tail = b""
+    async for chunk in chunks:
+        data = tail + chunk if tail else chunk
+        cut = data.rfind(b"\n")
+        if cut < 0:
+            tail = data
+            continue
+        tail = data[cut + 1:]
+        batch = [json.loads(line) for line in data[:cut].split(b"\n") if line.strip()]
+        if batch:
+            yield batch
+
+
 class KubeClient:
     """Async client; one keep-alive connection pool per process.
 
@@ -291,10 +307,22 @@ class KubeClient:
                          headers=self._auth()) as r:
             if r.status >= 400:
                 raise ApiError(r.status, await r.text())
-            buf = b""
-            async for chunk in r.content.iter_any():
-                buf += chunk
-                while b"\n" in buf:
-                    line, buf = buf.split(b"\n", 1)
-                    if line.strip():
-                        yield json.loads(line)
+            async for batch in _ndjson_batches(r.content.iter_any()):
+                for ev in batch:
+                    yield ev
+
+    async def watch_batches(self, resource: str, resource_version: str, timeout_s: int = 300,
+                            label_selector: str | None = None) -> AsyncIterator[list[dict]]:
+        """`watch`, one list per network read: every complete event line that arrived together."""
+        s = await self._s()
+        params = {"watch": "1", "resourceVersion": resource_version, "timeoutSeconds": str(timeout_s),
+                  "allowWatchBookmarks": "true"}
+        if label_selector:
+            params["labelSelector"] = label_selector
+        url = f"{self.config.server}/api/v1/{resource}?{urllib.parse.urlencode(params)}"
+        async with s.get(url, timeout=aiohttp.ClientTimeout(total=None, sock_read=timeout_s + 30),
+                         headers=self._auth()) as r:
+            if r.status >= 400:
+                raise ApiError(r.status, await r.text())
+            async for batch in _ndjson_batches(r.content.iter_any()):
+                yield batch

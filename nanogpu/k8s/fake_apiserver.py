@@ -95,10 +95,11 @@ class FakeKubeStore:
         self.events: list[dict] = []
         self.bindings: list[tuple[str, str, str]] = []
         self.history: dict[str, deque] = {"pods": deque(maxlen=history), "nodes": deque(maxlen=history)}
-        self.watchers: dict[str, list[asyncio.Queue]] = {"pods": [], "nodes": []}
+        self.watchers: dict[str, list[_WatchBuffer]] = {"pods": [], "nodes": []}
         self.faults = faults or Faults()
         self.counts: dict[str, int] = {}
         self.leases: dict[tuple[str, str], dict] = {}
+        self._ts_sec, self._ts_str = -1, ""
 
     # ------------------------------------------------------------------ internals
     def _bump(self, obj: dict) -> dict:
@@ -113,8 +114,15 @@ class FakeKubeStore:
     def _emit(self, kind: str, etype: str, obj: dict) -> None:
         ev = {"type": etype, "object": obj}
         self.history[kind].append((self.rv, ev))
-        for q in list(self.watchers[kind]):
-            q.put_nowait(ev)
+        for w in self.watchers[kind]:
+            w.push(ev)
+
+    def _now_rfc3339(self) -> str:
+        """Second-resolution RFC 3339 time (the API server's metav1.Time), formatted once per second."""
+        t = int(time.time())
+        if t != self._ts_sec:
+            self._ts_sec, self._ts_str = t, time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(t))
+        return self._ts_str
 
     def _count(self, verb: str) -> None:
         self.counts[verb] = self.counts.get(verb, 0) + 1
@@ -131,7 +139,7 @@ class FakeKubeStore:
         if not m.get("uid"):
             m["uid"] = str(uuid.uuid4())
         if "creationTimestamp" not in m:
-            m["creationTimestamp"] = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())
+            m["creationTimestamp"] = self._now_rfc3339()
         key = (m["namespace"], m["name"])
         if key in self.pods:
             raise ApiError(409, f'pods "{m["name"]}" already exists', "AlreadyExists")
@@ -280,36 +288,71 @@ class FakeKubeStore:
         return le
 
     # ------------------------------------------------------------------ watch
-    async def watch(self, kind: str, resource_version: str, label_selector: str | None = None
-                    ) -> AsyncIterator[dict]:
+    async def watch_batches(self, kind: str, resource_version: str, label_selector: str | None = None
+                            ) -> AsyncIterator[list[dict]]:
+        """Watch stream delivered as batches: everything emitted since the consumer last ran
+        arrives as one list (one wake-up per burst instead of one queue hop per event)."""
         try:
             rv = int(resource_version or 0)
         except ValueError:
             rv = 0
-        q: asyncio.Queue = asyncio.Queue()
+        buf = _WatchBuffer()
         hist = self.history[kind]
         if rv and hist and hist[0][0] > rv + 1 and len(hist) == hist.maxlen:
             raise ApiError(410, "too old resource version", "Expired")
         for ev_rv, ev in list(hist):
             if ev_rv > rv:
-                q.put_nowait(ev)
-        self.watchers[kind].append(q)
+                buf.evs.append(ev)
+        self.watchers[kind].append(buf)
         try:
             while True:
-                ev = await q.get()
-                if ev is None:
+                if not buf.evs:
+                    buf.waiter = asyncio.get_running_loop().create_future()
+                    try:
+                        await buf.waiter
+                    finally:
+                        buf.waiter = None
+                batch = list(buf.evs)
+                buf.evs.clear()
+                end = None in batch
+                if end:
+                    batch = batch[:batch.index(None)]
+                if label_selector:
+                    batch = [ev for ev in batch if _match_labels(ev["object"], label_selector)]
+                if batch:
+                    yield batch
+                if end:
                     return
-                if label_selector and not _match_labels(ev["object"], label_selector):
-                    continue
-                yield ev
         finally:
-            self.watchers[kind].remove(q)
+            self.watchers[kind].remove(buf)
+
+    async def watch(self, kind: str, resource_version: str, label_selector: str | None = None
+                    ) -> AsyncIterator[dict]:
+        async for batch in self.watch_batches(kind, resource_version, label_selector):
+            for ev in batch:
+                yield ev
 
     def drop_watches(self) -> None:
         """Fault injection: terminates every open watch stream."""
-        for qs in self.watchers.values():
-            for q in qs:
-                q.put_nowait(None)
+        for ws in self.watchers.values():
+            for w in ws:
+                w.push(None)
+
+
+class _WatchBuffer:
+    """One open watch: events appended by the store, drained by the watcher's task."""
+
+    __slots__ = ("evs", "waiter")
+
+    def __init__(self):
+        self.evs: deque = deque()
+        self.waiter: asyncio.Future | None = None
+
+    def push(self, ev: dict | None) -> None:
+        self.evs.append(ev)
+        w = self.waiter
+        if w is not None and not w.done():
+            w.set_result(None)
 
 
 class InProcKube:
@@ -371,6 +414,9 @@ class InProcKube:
 
     def watch(self, resource, resource_version, timeout_s=300, label_selector=None):
         return self.store.watch(resource, resource_version, label_selector)   # no extra async-gen hop
+
+    def watch_batches(self, resource, resource_version, timeout_s=300, label_selector=None):
+        return self.store.watch_batches(resource, resource_version, label_selector)
 
     async def get_lease(self, ns, name):
         await self._rtt()

@@ -97,31 +97,38 @@ class Informer:
                 backoff = min(backoff * 2, 5.0)
 
     async def _watch(self) -> None:
+        # API objects that can (the in-process store, the REST client) deliver the stream in
+        # batches: one loop wake-up per burst of events rather than one per event
+        if hasattr(self.api, "watch_batches"):
+            stream = self.api.watch_batches(self.resource, self.rv, label_selector=self.label_selector)
+        else:
+            stream = _singletons(self.api.watch(self.resource, self.rv, label_selector=self.label_selector))
         store, key, handlers = self.store, self.key, self.handlers
-        async for ev in self.api.watch(self.resource, self.rv, label_selector=self.label_selector):
-            etype, obj = ev.get("type"), ev.get("object") or {}
-            if etype == "ERROR":
-                raise ApiError(int(obj.get("code", 500)), obj.get("message", "watch error"))
-            self.rv = (obj.get("metadata") or {}).get("resourceVersion", self.rv)
-            if etype == "BOOKMARK":
-                continue
-            k = key(obj)
-            if etype == "DELETED":
-                old = store.pop(k, None)
-            else:
-                old = store.get(k)
-                store[k] = obj
-                if etype == "ADDED" and old is not None:
-                    etype = "MODIFIED"
-                elif etype == "MODIFIED" and old is None:
-                    etype = "ADDED"
-            if len(handlers) == 1:
-                try:
-                    handlers[0](etype, obj, old)
-                except Exception:  # a handler bug must not kill the informer
-                    log.exception("informer handler failed for %s %s", etype, k)
-            else:
-                self._dispatch(etype, obj, old)
+        async for batch in stream:
+            for ev in batch:
+                etype, obj = ev.get("type"), ev.get("object") or {}
+                if etype == "ERROR":
+                    raise ApiError(int(obj.get("code", 500)), obj.get("message", "watch error"))
+                self.rv = (obj.get("metadata") or {}).get("resourceVersion", self.rv)
+                if etype == "BOOKMARK":
+                    continue
+                k = key(obj)
+                if etype == "DELETED":
+                    old = store.pop(k, None)
+                else:
+                    old = store.get(k)
+                    store[k] = obj
+                    if etype == "ADDED" and old is not None:
+                        etype = "MODIFIED"
+                    elif etype == "MODIFIED" and old is None:
+                        etype = "ADDED"
+                if len(handlers) == 1:
+                    try:
+                        handlers[0](etype, obj, old)
+                    except Exception:  # a handler bug must not kill the informer
+                        log.exception("informer handler failed for %s %s", etype, k)
+                else:
+                    self._dispatch(etype, obj, old)
 
     def start(self) -> asyncio.Task:
         self._task = asyncio.ensure_future(self.run())
@@ -134,6 +141,11 @@ class Informer:
                 await self._task
             except (asyncio.CancelledError, Exception):
                 pass
+
+
+async def _singletons(events):
+    async for ev in events:
+        yield (ev,)
 
 
 class WorkQueue:
