@@ -303,7 +303,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
     from nanogpu.k8s.fake_apiserver import Faults, FakeKubeStore, InProcKube
     from nanogpu.sim.driver import FastExtenderClient, SchedulerDriver, node_capacities
 
-    store = FakeKubeStore(faults=Faults(latency_s=args.api_rtt_ms / 1e3))
+    # the watch history a real API server keeps is a bounded cache, and not in our process
+    store = FakeKubeStore(history=8192, faults=Faults(latency_s=args.api_rtt_ms / 1e3))
     topo_json = topo.to_json()
     n_dev = len(topo.devices)
     nodes = [pu.make_node(f"mi355x-{i:03d}", n_dev, topo_json, {"amd.com/gpu.present": "true"})
@@ -366,10 +367,11 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
         # the pod controller releases on DELETED; wait until our shares are gone
         # (the in-process watch delivers the DELETED events on the next loop iterations: yield
         # first, and only then back off to short sleeps)
+        # Deletions are delivered in order: wait for the last pod, then check them all once.
         uids = [pu.pod_uid(p) for p in pods]
         lookup = rt.state.ledger.lookup
         for i in range(20000):
-            if not any(lookup(u) for u in uids):
+            if not lookup(uids[-1]) and not any(lookup(u) for u in uids):
                 break
             await asyncio.sleep(0 if i < 50 else 0.0005)
         await pod_ctrl.queue.drain(5.0)
