@@ -64,8 +64,11 @@ def parse_args():
     ap.add_argument("--json-out", default="")
     ap.add_argument("--profile-out", default="", help="cProfile the timed steps (rank 0) into this file")
     ap.add_argument("--no-nominate", action="store_true", help="priorities do not nominate (Ledger::nominate)")
-    ap.add_argument("--frontend-threads", type=int, default=4, help="native front door epoll workers")
-    ap.add_argument("--busy-poll-us", type=int, default=int(os.environ.get("NANOGPU_BUSY_POLL_US", "0")),
+    # the deployment's front-door settings (deploy/nano-gpu-scheduler-amd.yaml): 2 epoll
+    # threads that poll 20 us after each event; `--busy-poll-us 0 --frontend-threads 4` is the
+    # server's plain default (about 10 % lower here, README "Results")
+    ap.add_argument("--frontend-threads", type=int, default=2, help="native front door epoll workers")
+    ap.add_argument("--busy-poll-us", type=int, default=int(os.environ.get("NANOGPU_BUSY_POLL_US", "20")),
                     help="native front door busy-poll window")
     ap.add_argument("--driver", default="native", choices=["native", "python"],
                     help="kube-scheduler stand-in: C++ (native/src/schedsim.cpp) or the Python threaded one")
@@ -547,7 +550,8 @@ def main() -> int:
                        "parallelism": f"{d.world} extender worker(s), shared native ledger",
                        "cluster": f"{args.nodes} nodes x {args.gpus_per_node} MI355X ({args.partition})",
                        "api_rtt_ms": args.api_rtt_ms,
-                       "cpus_rank0": _cpulist(cpus)},
+                       "cpus_rank0": _cpulist(cpus),
+                       "frontend": f"{args.frontend_threads} threads, busy-poll {args.busy_poll_us} us"},
             "p50_bind_ms": round(p50, 4) if p50 is not None else None,
             "p99_bind_ms": round(p99, 4) if p99 is not None else None,
             "frag_pct": round(statistics.mean(f["frag_pct"] for f in fr), 3) if fr else None,
