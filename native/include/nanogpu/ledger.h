@@ -212,8 +212,10 @@ class Ledger {
     }
     void unlock() { busy.store(false, std::memory_order_release); }
   };
-  mutable std::unique_ptr<NodeCache[]> cache_;
+  // allocated on a node's first cached plan (6.6 KB each), published with a CAS
+  mutable std::unique_ptr<std::atomic<NodeCache*>[]> cache_;
   uint32_t cache_nodes_ = 0;
+  NodeCache* node_cache(int32_t node, bool create) const;
   bool cache_get(const CacheKey& k, int32_t* rc, Plan* plan) const;
   bool cache_get_score(const CacheKey& k, int32_t* rc, int32_t* score) const;
   void cache_put(const CacheKey& k, int32_t rc, const Plan& plan);

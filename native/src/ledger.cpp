@@ -161,10 +161,23 @@ Ledger::Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, b
   }
   hdr_->attached.fetch_add(1);
   cache_nodes_ = hdr_->max_nodes;
-  cache_.reset(new NodeCache[cache_nodes_]);
+  cache_.reset(new std::atomic<NodeCache*>[cache_nodes_]);
+  for (uint32_t i = 0; i < cache_nodes_; ++i) cache_[i].store(nullptr, std::memory_order_relaxed);
+}
+
+Ledger::NodeCache* Ledger::node_cache(int32_t node, bool create) const {
+  if (static_cast<uint32_t>(node) >= cache_nodes_) return nullptr;
+  NodeCache* c = cache_[node].load(std::memory_order_acquire);
+  if (c || !create) return c;
+  auto* fresh = new NodeCache();
+  if (cache_[node].compare_exchange_strong(c, fresh, std::memory_order_acq_rel)) return fresh;
+  delete fresh;   // another thread published first
+  return c;
 }
 
 Ledger::~Ledger() {
+  if (cache_)
+    for (uint32_t i = 0; i < cache_nodes_; ++i) delete cache_[i].load(std::memory_order_relaxed);
   if (hdr_) hdr_->attached.fetch_sub(1);
   if (base_) munmap(base_, bytes_);
   if (fd_ >= 0) close(fd_);
@@ -364,8 +377,9 @@ inline int cache_way(uint64_t dh, uint64_t oh) {
 }  // namespace
 
 bool Ledger::cache_get(const CacheKey& k, int32_t* rc, Plan* plan) const {
-  if (static_cast<uint32_t>(k.node) >= cache_nodes_) return false;
-  NodeCache& c = cache_[k.node];
+  NodeCache* cp = node_cache(k.node, false);
+  if (!cp) return false;
+  NodeCache& c = *cp;
   const int w = cache_way(k.dh, k.oh);
   c.lock();
   for (int j = 0; j < 2; ++j) {
@@ -382,8 +396,9 @@ bool Ledger::cache_get(const CacheKey& k, int32_t* rc, Plan* plan) const {
 }
 
 bool Ledger::cache_get_score(const CacheKey& k, int32_t* rc, int32_t* score) const {
-  if (static_cast<uint32_t>(k.node) >= cache_nodes_) return false;
-  NodeCache& c = cache_[k.node];
+  NodeCache* cp = node_cache(k.node, false);
+  if (!cp) return false;
+  NodeCache& c = *cp;
   const int w = cache_way(k.dh, k.oh);
   c.lock();
   for (int j = 0; j < 2; ++j) {
@@ -400,8 +415,9 @@ bool Ledger::cache_get_score(const CacheKey& k, int32_t* rc, int32_t* score) con
 }
 
 void Ledger::cache_put(const CacheKey& k, int32_t rc, const Plan& plan) {
-  if (static_cast<uint32_t>(k.node) >= cache_nodes_) return;
-  NodeCache& c = cache_[k.node];
+  NodeCache* cp = node_cache(k.node, true);
+  if (!cp) return;
+  NodeCache& c = *cp;
   const int w = cache_way(k.dh, k.oh);
   c.lock();
   // same key or an unused/stale way first; else replace the older-generation one
@@ -739,7 +755,9 @@ FragStats Ledger::frag(int32_t min_request) const {
 
 void Ledger::clear_cache() {
   for (uint32_t i = 0; i < cache_nodes_; ++i) {
-    NodeCache& c = cache_[i];
+    NodeCache* cp = node_cache(static_cast<int32_t>(i), false);
+    if (!cp) continue;
+    NodeCache& c = *cp;
     c.lock();
     for (auto& e : c.e) e.used = false;
     c.unlock();
@@ -749,7 +767,9 @@ void Ledger::clear_cache() {
 size_t Ledger::cache_size() const {
   size_t n = 0;
   for (uint32_t i = 0; i < cache_nodes_; ++i) {
-    NodeCache& c = cache_[i];
+    NodeCache* cp = node_cache(static_cast<int32_t>(i), false);
+    if (!cp) continue;
+    NodeCache& c = *cp;
     c.lock();
     for (const auto& e : c.e) n += e.used;
     c.unlock();
