@@ -67,7 +67,7 @@ async def publish(api, node_name: str, topo: NodeTopology, advertise_percent: bo
 class NodeAgent:
     def __init__(self, api, node_name: str, topo: NodeTopology, host: dict | None = None,
                  device_plugin: bool = True, plugin_dir: str = "", health_period_s: float = 10.0,
-                 sysfs_root: str = ""):
+                 sysfs_root: str = "", kubelet_check_s: float = 1.0):
         self.api = api
         self.node = node_name
         self.topo = topo
@@ -76,8 +76,12 @@ class NodeAgent:
         self.plugin_dir = plugin_dir
         self.health_period_s = health_period_s
         self.sysfs_root = sysfs_root
+        self.kubelet_check_s = kubelet_check_s
+        self.registrations = 0
+        self._register = True
         self.plugin = None
         self.server = None
+        self.socket_path = ""
         self.informer = None
         self.tasks: list[asyncio.Task] = []
 
@@ -89,7 +93,7 @@ class NodeAgent:
 
     async def start(self, register: bool = True) -> None:
         from ..k8s.informer import Informer
-        from .plugin import NanoGpuPlugin, serve
+        from .plugin import NanoGpuPlugin
 
         await publish(self.api, self.node, self.topo, advertise_percent=not self.device_plugin)
         if not self.device_plugin:
@@ -103,10 +107,51 @@ class NodeAgent:
         await self.informer.synced.wait()
         restored = await self.plugin.rebuild(self.informer.list())
         log.info("agent %s: %d devices, %d CU grants restored", self.node, len(self.topo.devices), restored)
-        self.server, _ = await serve(self.plugin, self.plugin_dir or "/var/lib/kubelet/device-plugins",
-                                     register=register)
+        self._register = register
+        await self._serve()
+        if register and self.kubelet_check_s > 0:
+            self.tasks.append(asyncio.ensure_future(self._kubelet_watch()))
         if self.health_period_s > 0:
             self.tasks.append(asyncio.ensure_future(self._health_loop()))
+
+    def _dir(self) -> str:
+        return self.plugin_dir or "/var/lib/kubelet/device-plugins"
+
+    async def _serve(self) -> None:
+        from .plugin import serve
+
+        self.server, self.socket_path = await serve(self.plugin, self._dir(), register=self._register)
+        self.registrations += int(self._register)
+
+    @staticmethod
+    def _identity(path: str) -> tuple[int, int] | None:
+        try:
+            st = os.stat(path)
+            return st.st_ino, st.st_mtime_ns
+        except OSError:
+            return None
+
+    async def _kubelet_watch(self) -> None:
+        """A restarted kubelet removes every plugin socket and serves a new kubelet.sock; a
+        plugin has to notice, serve again and re-register (its devices are unknown to the new
+        kubelet until it does). Both files are polled every `kubelet_check_s`."""
+        kubelet_sock = os.path.join(self._dir(), "kubelet.sock")
+        seen = self._identity(kubelet_sock)
+        while True:
+            await asyncio.sleep(self.kubelet_check_s)
+            now = self._identity(kubelet_sock)
+            if now is None:
+                continue                                  # kubelet down: wait for it
+            if now == seen and os.path.exists(self.socket_path):
+                continue
+            log.warning("agent %s: kubelet restarted (or our socket vanished): registering again", self.node)
+            try:
+                if self.server is not None:
+                    await self.server.stop(grace=0.5)
+                await self._serve()
+                seen = now
+            except Exception:
+                log.exception("agent %s: re-registration failed; retrying", self.node)
 
     def _on_pod(self, etype: str, pod: dict, old: dict | None) -> None:
         if pu.node_name_of(pod) != self.node or self.plugin is None:

@@ -109,3 +109,48 @@ def test_full_stack_agent_extender_kubelet(tmp_path):
             await runner.cleanup()
 
     asyncio.run(main())
+
+
+def test_agent_re_registers_after_kubelet_restart(tmp_path):
+    """kubelet restarts wipe the device-plugin directory and serve a new kubelet.sock: the
+    agent notices, serves its socket again and re-registers, and the new kubelet sees the
+    devices through ListAndWatch."""
+    import os
+
+    async def main():
+        store = FakeKubeStore()
+        runner, port = await serve(store)
+        api = KubeClient(KubeConfig(server=f"http://127.0.0.1:{port}"))
+        n = "gpu-node-r"
+        store.add_node({"apiVersion": "v1", "kind": "Node", "metadata": {"name": n, "labels": {},
+                                                                         "annotations": {}}, "status": {}})
+        topo, host = discover(str(write_mi355x_sysfs(tmp_path / "sys", 8, "SPX")), use_amdsmi=False)
+        pdir = tmp_path / "dp"
+        pdir.mkdir()
+        kl = FakeKubelet(api, n, str(pdir))
+        await kl.start()
+        ag = NodeAgent(api, n, topo, host, device_plugin=True, plugin_dir=str(pdir), health_period_s=0,
+                       kubelet_check_s=0.05)
+        kl2 = None
+        try:
+            await ag.start()
+            await asyncio.wait_for(kl.ready.wait(), 10)
+            assert ag.registrations == 1
+            # kubelet restarts: stops, removes every socket in the directory, comes back
+            await kl.stop()
+            for f in os.listdir(pdir):
+                os.unlink(pdir / f)
+            kl2 = FakeKubelet(api, n, str(pdir))
+            await kl2.start()
+            await asyncio.wait_for(kl2.ready.wait(), 10)
+            assert kl2.registered and kl2.registered[0][2] == T.RESOURCE_GPU_PERCENT
+            assert len(kl2.devices) == 800 and ag.registrations == 2
+            assert os.path.exists(ag.socket_path)
+        finally:
+            await ag.stop()
+            if kl2 is not None:
+                await kl2.stop()
+            await api.close()
+            await runner.cleanup()
+
+    asyncio.run(main())
