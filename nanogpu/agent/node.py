@@ -209,6 +209,8 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--kube-api", default=None)
     ap.add_argument("--kubeconfig", default=os.environ.get("KUBECONFIG"))
     ap.add_argument("--print", action="store_true", help="print the topology annotation and exit")
+    ap.add_argument("--metrics-port", type=int, default=9410,
+                    help="device / pod / container GPU metrics on :PORT/metrics (0: off)")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     topo, host = discover(a.sysfs_root, not a.no_amdsmi)
@@ -229,11 +231,18 @@ def main(argv: list[str] | None = None) -> int:
         agent = NodeAgent(api, a.node_name, topo, host, device_plugin=a.advertise == "device-plugin",
                           plugin_dir=a.plugin_dir, sysfs_root=a.sysfs_root)
         await agent.start()
+        metrics = None
+        if a.metrics_port:
+            from .metrics import serve_metrics
+
+            metrics, _ = await serve_metrics(agent, port=a.metrics_port)
         stop = asyncio.Event()
         loop = asyncio.get_running_loop()
         for sig in (signal.SIGINT, signal.SIGTERM):
             loop.add_signal_handler(sig, stop.set)
         await stop.wait()
+        if metrics is not None:
+            await metrics.cleanup()
         await agent.stop()
         await api.close()
         return 0

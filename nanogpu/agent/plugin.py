@@ -48,6 +48,7 @@ class Assignment:
     devices: list[int]
     percent: int
     mib: int
+    cus: int = 0          # CUs granted by the mask (0: whole devices, no mask)
 
 
 class Matcher:
@@ -97,7 +98,8 @@ class NanoGpuPlugin:
         self.cus = [cumask.DeviceCUs(d.cus, d.xcds) for d in topo.devices]
         self.health = [bool(d.healthy) for d in topo.devices]
         self._changed = asyncio.Event()
-        self.allocations: list[Assignment] = []
+        # live grants by (pod uid, container): what the agent's /metrics reports per container
+        self.grants: dict[tuple[str, str], Assignment] = {}
 
     # ---------------------------------------------------------------- restart rebuild
     async def rebuild(self, pods: list[dict] | None = None) -> int:
@@ -115,8 +117,13 @@ class NanoGpuPlugin:
                 if mask is None or not idx:
                     continue
                 self.matcher.claimed[(pu.pod_uid(p), name)] = 0.0
+                cus = 0
                 if mask not in ("", "full") and 0 <= idx[0] < len(self.cus):
-                    self.cus[idx[0]].restore(f"{pu.pod_uid(p)}/{name}", cumask.parse_ranges(mask.split(":")[-1]))
+                    bits = cumask.parse_ranges(mask.split(":")[-1])
+                    self.cus[idx[0]].restore(f"{pu.pod_uid(p)}/{name}", bits)
+                    cus = len(bits)
+                self.grants[(pu.pod_uid(p), name)] = Assignment(pu.pod_key(p), name, list(idx),
+                                                                pu.container_percent(c), pu.container_mib(c), cus)
                 n += 1
         return n
 
@@ -126,6 +133,8 @@ class NanoGpuPlugin:
                 d.release(owner)
         for k in [k for k in self.matcher.claimed if k[0] == uid]:
             del self.matcher.claimed[k]
+        for k in [k for k in self.grants if k[0] == uid]:
+            del self.grants[k]
 
     def set_health(self, dev: int, healthy: bool) -> None:
         if self.health[dev] != healthy:
@@ -201,6 +210,7 @@ class NanoGpuPlugin:
         r.envs["NANO_GPU_DEVICES"] = ",".join(map(str, devs))
         r.envs["NANO_GPU_PERCENT"] = str(percent)
         mask_ann = "full"
+        cus = 0
         if percent < T.GPU_PERCENT_EACH_CARD and len(devs) == 1:
             bits = self.cus[devs[0]].grant(f"{pu.pod_uid(pod)}/{name}", percent)
             if bits is None:
@@ -208,6 +218,7 @@ class NanoGpuPlugin:
             mask_ann = cumask.hsa_cu_mask(0, bits)   # the container sees its device as index 0
             r.envs["HSA_CU_MASK"] = mask_ann
             r.envs["NANO_GPU_CUS"] = str(len(bits))
+            cus = len(bits)
         if mib:
             r.envs["NANO_GPU_MEMORY_MIB"] = str(mib)
             total = self.topo.devices[devs[0]].hbm_mib if devs else 0
@@ -220,7 +231,7 @@ class NanoGpuPlugin:
                 T.ANNOTATION_CU_MASK_FMT.format(name): mask_ann}}})
         except Exception as e:  # the allocation stands; the annotation only speeds up rebuild
             log.warning("annotating %s/%s failed: %s", ns, pname, e)
-        self.allocations.append(Assignment(pu.pod_key(pod), name, devs, percent, mib))
+        self.grants[(pu.pod_uid(pod), name)] = Assignment(pu.pod_key(pod), name, list(devs), percent, mib, cus)
         return r
 
 

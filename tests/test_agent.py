@@ -10,6 +10,7 @@ import grpc
 import pytest
 
 from nanogpu import types as T
+from nanogpu.agent.metrics import render as render_metrics
 from nanogpu.agent import cumask
 from nanogpu.agent import dpapi as D
 from nanogpu.agent.node import NodeAgent, node_patch, status_patch
@@ -148,6 +149,17 @@ def test_device_plugin_end_to_end(tmp_path):
                     D.ContainerAllocateRequest(devices_ids=["d0-1"] * 7)]))
             assert ei.value.code() == grpc.StatusCode.FAILED_PRECONDITION
             stream.cancel()
+        # pod / container level monitoring: the grants, joined with the devices
+        text = render_metrics(topo, agent.plugin, agent.render_minors(), str(tmp_path / "nosys"))
+        assert 'nanogpu_container_gpu_percent{namespace="default",pod="a",container="main",device="0"} 20' in text
+        assert 'nanogpu_container_cus{namespace="default",pod="a",container="main",device="0"} 48' in text
+        assert 'nanogpu_container_cus{namespace="default",pod="b",container="main",device="0"} 72' in text
+        assert 'nanogpu_container_cus{namespace="default",pod="c",container="y",device="1"} 256' in text
+        assert (f'nanogpu_container_hbm_budget_bytes{{namespace="default",pod="a",container="main",device="0"}} '
+                f'{32 << 30}') in text
+        assert 'nanogpu_device_granted_percent{device="0"} 50' in text
+        assert 'nanogpu_device_granted_cus{device="0"} 120' in text
+        assert "nanogpu_device_busy_percent" not in text      # no sysfs here: left out, not zero
         ann = store.get_pod("default", "a")["metadata"]["annotations"]
         assert ann[T.ANNOTATION_CU_MASK_FMT.format("main")] == "0:0-47"
 
@@ -164,6 +176,9 @@ def test_device_plugin_end_to_end(tmp_path):
                 break
             await asyncio.sleep(0.01)
         assert len(agent2.plugin.cus[0].used) == 1
+        text = render_metrics(topo, agent2.plugin, agent2.render_minors(), str(tmp_path / "nosys"))
+        assert 'pod="a"' not in text and 'nanogpu_container_cus{namespace="default",pod="b",container="main",' \
+            'device="0"} 72' in text                           # restored from annotations, "a" released
         await agent2.stop()
         await ksrv.stop(None)
 

@@ -228,3 +228,38 @@ def test_device_plugin_env_is_honoured_by_rocr():
                                     "alloc_5pct_ok": part.get("small_ok"), "alloc_30pct_ok": part.get("big_ok")})
     assert 0.15 < part["tflops"] / full < 0.40, (full, part)
     assert part["small_ok"] is True and part["big_ok"] is False
+
+
+def test_agent_metrics_read_real_amdgpu_sysfs(host, P):
+    """The node agent's /metrics reads gpu_busy_percent and VRAM use from the real device; VRAM
+    used grows by what a process allocates and the busy counter is a percentage."""
+    import re
+
+    import torch
+
+    from nanogpu.agent.metrics import render
+    from nanogpu.topology.model import from_host_json
+
+    topo = from_host_json(host)
+    minors = [int(g["render_minor"]) for g in host["gpus"]]
+    if len(minors) != len(topo.devices):
+        pytest.skip("partitioned GPU: render nodes are per partition")
+
+    def used() -> int:
+        m = re.search(r'nanogpu_device_vram_used_bytes\{device="0"\} (\d+)', render(topo, None, minors))
+        assert m, "mem_info_vram_used not read"
+        return int(m.group(1))
+
+    text = render(topo, None, minors)
+    busy = re.search(r'nanogpu_device_busy_percent\{device="0"\} (\d+)', text)
+    assert busy and 0 <= int(busy.group(1)) <= 100
+    assert f'nanogpu_device_vram_total_bytes{{device="0"}} {host["gpus"][0]["vram_bytes"]}' in text
+    before = used()
+    x = torch.empty(4 << 30, dtype=torch.uint8, device="cuda:0")
+    x.fill_(1)
+    torch.cuda.synchronize()
+    grew = used() - before
+    del x
+    torch.cuda.empty_cache()
+    record("agent_metrics_vram_delta_for_4GiB", grew)
+    assert grew >= (3 << 30), grew
