@@ -345,6 +345,43 @@ std::vector<double> mfma_colocated(int dev, const std::vector<std::vector<uint32
   return tf;
 }
 
+// Co-located streaming tenants: one HBM copy per CU mask, each on its own CU-masked stream,
+// launched together. Returns per-tenant GB/s (read + write) over each tenant's own events.
+// CU masks partition the compute units, not the memory system: this measures how the HBM3E
+// bandwidth splits between memory-bound neighbours (profiles/gpu_calibration.md).
+std::vector<double> hbm_colocated(int dev, const std::vector<std::vector<uint32_t>>& masks, size_t bytes,
+                                  int iters) {
+  HIP_OK(hipSetDevice(dev));
+  const size_t n = bytes / sizeof(float4);
+  if (masks.empty() || n == 0 || iters <= 0) throw std::invalid_argument("hbm_colocated: masks, bytes, iters");
+  const size_t k = masks.size();
+  std::vector<std::unique_ptr<Stream>> streams;
+  std::vector<std::unique_ptr<Events>> evs;
+  std::vector<std::unique_ptr<DevBuf<float4>>> src, dst;
+  const dim3 grid(copy_grid(n));
+  for (size_t i = 0; i < k; ++i) {
+    streams.emplace_back(new Stream(masks[i]));
+    evs.emplace_back(new Events());
+    src.emplace_back(new DevBuf<float4>(n));
+    dst.emplace_back(new DevBuf<float4>(n));
+    HIP_OK(hipMemset(src[i]->p, 0, n * sizeof(float4)));
+    hipLaunchKernelGGL(hbm_copy, grid, dim3(kCopyBlock), 0, streams[i]->s, src[i]->p, dst[i]->p, n);  // warm-up
+  }
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipDeviceSynchronize());
+  for (size_t i = 0; i < k; ++i) {
+    HIP_OK(hipEventRecord(evs[i]->a, streams[i]->s));
+    for (int it = 0; it < iters; ++it)
+      hipLaunchKernelGGL(hbm_copy, grid, dim3(kCopyBlock), 0, streams[i]->s, src[i]->p, dst[i]->p, n);
+    HIP_OK(hipEventRecord(evs[i]->b, streams[i]->s));
+  }
+  HIP_OK(hipGetLastError());
+  std::vector<double> gbs(k);
+  for (size_t i = 0; i < k; ++i)
+    gbs[i] = 2.0 * static_cast<double>(n * sizeof(float4)) * iters / (evs[i]->ms() * 1e-3) / 1e9;
+  return gbs;
+}
+
 double peer_bandwidth(int src, int dst, size_t bytes, int iters) {
   int n = 0;
   HIP_OK(hipGetDeviceCount(&n));
@@ -399,6 +436,9 @@ PYBIND11_MODULE(_probe, m) {
         "C[32x32] = bf16(A[32x16]) @ bf16(B[16x32]) with one v_mfma_f32_32x32x16_bf16 (fp32 accumulate).");
   m.def("copy_check", &copy_check, py::arg("device") = 0, py::arg("n_floats") = size_t(1) << 24,
         py::call_guard<py::gil_scoped_release>(), "hbm_copy kernel result == source, bit for bit.");
+  m.def("hbm_colocated", &hbm_colocated, py::arg("device"), py::arg("cu_masks"), py::arg("bytes") = size_t(1) << 30,
+        py::arg("iters") = 10, py::call_guard<py::gil_scoped_release>(),
+        "Per-tenant HBM copy GB/s for concurrent tenants on CU-masked streams.");
   m.def("mfma_colocated", &mfma_colocated, py::arg("device"), py::arg("cu_masks"), py::arg("blocks"),
         py::arg("iters") = 2048, py::call_guard<py::gil_scoped_release>(),
         "Concurrent MFMA burns on CU-masked streams; per-stream TFLOP/s.");

@@ -263,3 +263,23 @@ def test_agent_metrics_read_real_amdgpu_sysfs(host, P):
     torch.cuda.empty_cache()
     record("agent_metrics_vram_delta_for_4GiB", grew)
     assert grew >= (3 << 30), grew
+
+
+def test_hbm_bandwidth_under_cu_mask_sharing(P):
+    """CU masks partition compute, not the memory system. Measures (and records for
+    profiles/gpu_calibration.md) how HBM3E bandwidth splits between two memory-bound tenants
+    holding the agent's 25 % / 75 % masks, and what a 25 % tenant reaches alone."""
+    from nanogpu.agent import cumask
+
+    d = cumask.DeviceCUs(256, 8)
+    a, b = d.grant("a", 25), d.grant("b", 75)
+    ma, mb = cumask.mask_words(a), cumask.mask_words(b)
+    full = P.hbm_colocated(0, [[]], 1 << 30, 10)[0]
+    alone25 = P.hbm_colocated(0, [ma], 1 << 30, 10)[0]
+    ta, tb = P.hbm_colocated(0, [ma, mb], 1 << 30, 10)
+    record("hbm_cu_mask_sharing", {"full_gbs": round(full, 1), "alone_25pct_gbs": round(alone25, 1),
+                                   "colocated_25pct_gbs": round(ta, 1), "colocated_75pct_gbs": round(tb, 1)})
+    assert full > 4000, full
+    # every tenant moves data; the pair together cannot beat the device
+    assert ta > 0.05 * full and tb > 0.05 * full, (ta, tb, full)
+    assert min(ta, tb) < full * 1.05
