@@ -77,6 +77,20 @@ def container_mib(c: dict) -> int:
         return 0
 
 
+class Req(tuple):
+    """One container's demand with flags: unpacks as (percent, MiB) like the plain tuples and
+    carries `flags` (types.FLAG_MEM_BOUND) to the native core (bindings.cpp to_demand). Pods
+    without flags keep plain tuples."""
+
+    def __new__(cls, pct: int, mib: int, flags: int = 0):
+        r = tuple.__new__(cls, (pct, mib))
+        r.flags = flags
+        return r
+
+    def __repr__(self) -> str:
+        return f"Req({self[0]}, {self[1]}, flags={self.flags})"
+
+
 _DEMAND_CACHE: dict[str, Demand] = {}
 _DEMAND_CACHE_CAP = 65536
 
@@ -91,7 +105,14 @@ def pod_demand(pod: dict) -> Demand:
         d = _DEMAND_CACHE.get(uid)
         if d is not None:
             return d
-    d = [(container_percent(c), container_mib(c)) for c in containers(pod)]
+    cs = containers(pod)
+    mb = (meta(pod).get("annotations") or {}).get(T.ANNOTATION_MEMORY_BOUND)
+    if mb:
+        names = None if mb == "true" else {x.strip() for x in mb.split(",") if x.strip()}
+        d = [Req(container_percent(c), container_mib(c),
+                 T.FLAG_MEM_BOUND if names is None or c.get("name", "") in names else 0) for c in cs]
+    else:
+        d = [(container_percent(c), container_mib(c)) for c in cs]
     if uid:
         if len(_DEMAND_CACHE) >= _DEMAND_CACHE_CAP:
             _DEMAND_CACHE.clear()

@@ -36,6 +36,10 @@ ANNOTATION_TOPOLOGY = "nano-gpu/topology"     # node: JSON from the node agent (
 ANNOTATION_CU_MASK_FMT = "nano-gpu/cu-mask-{}"  # pod: per-container CU mask chosen by the agent
 ANNOTATION_ASSUME_TIME = "nano-gpu/assume-time"
 ANNOTATION_SCHEDULER = "nano-gpu/scheduler"
+# pod: "true" or a comma list of containers that stream HBM (memory-bound); native policies
+# keep them apart from each other on a device (native/include/nanogpu/alloc.h kFlagMemBound)
+ANNOTATION_MEMORY_BOUND = "nano-gpu/memory-bound"
+FLAG_MEM_BOUND = 1
 AMD_GPU_NODE_LABEL = ("amd.com/gpu.present", "true")   # default telemetry node selector
 
 MI355X_CUS = 256

@@ -65,7 +65,7 @@ struct Device {
   // NPS1, CPX under NPS2) draw from one pool. Every member mirrors the pool's
   // mib_free/mib_total and every debit updates all members. -1: the device's own HBM.
   int16_t pool;
-  int16_t pad16;
+  int16_t mem_bound;    // memory-bound share containers placed here (see kFlagMemBound)
   int32_t pad32;
   int64_t mib_share;    // HBM a whole-device grant of a pooled member takes (pool / members)
 };
@@ -76,10 +76,18 @@ struct Topology {
   float link_bw[kMaxGpus * kMaxGpus];  // GB/s between physical GPUs, 0 = no direct link
 };
 
+// Container flags. kFlagMemBound: the container streams HBM (pod annotation
+// nano-gpu/memory-bound). CU masks split the compute units but not the memory system: on
+// the MI355X box two streaming tenants with 25 % / 75 % masks split the HBM bandwidth
+// 25 / 75, while a 25 % tenant alone reaches 51 % of it (profiles/gpu_calibration.md). So
+// native policies place a memory-bound share on the device with the fewest memory-bound
+// tenants first, next to compute-bound neighbours, before the policy's own order.
+constexpr int32_t kFlagMemBound = 1;
+
 struct ContainerDemand {
-  int32_t pct;   // 0 => no GPU; <=100 => share of one device; k*100 => k whole devices
-  int32_t pad;
-  int64_t mib;   // HBM MiB requested (per device for whole-device requests it is ignored)
+  int32_t pct;    // 0 => no GPU; <=100 => share of one device; k*100 => k whole devices
+  int32_t flags;  // kFlag* bits
+  int64_t mib;    // HBM MiB requested (per device for whole-device requests it is ignored)
 };
 
 struct Demand {

@@ -40,6 +40,7 @@ uint64_t Demand::hash() const {
   for (int i = 0; i < n; ++i) {
     h = mix64(h ^ static_cast<uint64_t>(static_cast<uint32_t>(c[i].pct)));
     h = mix64(h ^ static_cast<uint64_t>(c[i].mib));
+    if (c[i].flags) h = mix64(h ^ (static_cast<uint64_t>(static_cast<uint32_t>(c[i].flags)) << 40));
   }
   return h;
 }
@@ -314,8 +315,9 @@ bool share_fits(const Device& d, const ContainerDemand& c) {
 int pick_share(Work& w, const Topology* t, const ContainerDemand& c, const Options& o,
                uint64_t rnd) {
   const bool spread = o.policy == Policy::kSpread;
+  const bool membound = (c.flags & kFlagMemBound) != 0;
   int best = -1;
-  int64_t bk1 = 0, bk2 = 0;
+  int64_t bk0 = 0, bk1 = 0, bk2 = 0;
   float bk3 = 0.f;
   int fit_cnt = 0;
   for (int i = 0; i < w.n; ++i) {
@@ -332,13 +334,16 @@ int pick_share(Work& w, const Topology* t, const ContainerDemand& c, const Optio
       k1 = -k1;  // worst fit: most free first
       k2 = -k2;
     }
+    const int64_t k0 = membound ? d.mem_bound : 0;   // fewest memory-bound neighbours first
     bool better;
     if (best < 0) better = true;
+    else if (k0 != bk0) better = k0 < bk0;
     else if (k1 != bk1) better = k1 < bk1;
     else if (k2 != bk2) better = k2 < bk2;
     else better = k3 > bk3;
     if (better) {
       best = i;
+      bk0 = k0;
       bk1 = k1;
       bk2 = k2;
       bk3 = k3;
@@ -618,6 +623,17 @@ static int32_t native_rate(const Device* devs, int n, const Demand& d, const Opt
     default:
       s = 100.0;
   }
+  if (plan && o.policy != Policy::kRandom) {
+    // a memory-bound share that would sit next to another memory-bound tenant costs this node
+    // points, so priorities prefer a node where it can pair with compute-bound neighbours
+    int crowded = 0;
+    for (int c = 0; c < plan->n && c < d.n; ++c) {
+      if (!(d.c[c].flags & kFlagMemBound) || d.c[c].pct > kPercentPerDevice) continue;
+      for (int k = plan->off[c]; k < plan->off[c + 1]; ++k)
+        if (plan->idx[k] >= 0 && devs[plan->idx[k]].mem_bound > 0) ++crowded;
+    }
+    s -= 15.0 * crowded;
+  }
   return static_cast<int32_t>(std::clamp(s, 0.0, 100.0));
 }
 
@@ -664,6 +680,7 @@ static inline void debit(Device* devs, int n, int i, const ContainerDemand& cd, 
   }
   dv.pct_free += sign * cd.pct;
   mib_adjust(devs, n, i, sign * cd.mib);
+  if (cd.flags & kFlagMemBound) dv.mem_bound = static_cast<int16_t>(std::max(0, dv.mem_bound - sign));
 }
 
 static inline bool can_debit(const Device& dv, const ContainerDemand& cd) {

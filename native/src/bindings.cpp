@@ -18,16 +18,25 @@ using namespace nanogpu;
 
 namespace {
 
-Demand to_demand(const std::vector<std::pair<int32_t, int64_t>>& v) {
+// A pod demand from Python: one (percent, MiB) tuple per container; an item may carry
+// `flags` (nanogpu.k8s.podutil.Req: kFlagMemBound). Called with the GIL held.
+Demand to_demand(const py::sequence& v) {
   if (v.size() > static_cast<size_t>(kMaxContainers))
     throw py::value_error("too many containers (max 16)");
   Demand d;
   std::memset(&d, 0, sizeof(d));
   d.n = static_cast<int32_t>(v.size());
   for (size_t i = 0; i < v.size(); ++i) {
-    if (v[i].first < 0 || v[i].second < 0) throw py::value_error("negative demand");
-    d.c[i].pct = v[i].first;
-    d.c[i].mib = v[i].second;
+    const py::handle it = v[i];
+    const py::sequence t = py::reinterpret_borrow<py::sequence>(it);
+    if (t.size() < 2) throw py::value_error("demand items are (percent, MiB)");
+    const int64_t pct = t[0].cast<int64_t>(), mib = t[1].cast<int64_t>();
+    if (pct < 0 || mib < 0) throw py::value_error("negative demand");
+    if (pct > INT32_MAX) throw py::value_error("percent out of range");
+    d.c[i].pct = static_cast<int32_t>(pct);
+    d.c[i].mib = mib;
+    if (t.size() >= 3) d.c[i].flags = t[2].cast<int32_t>();
+    else if (py::hasattr(it, "flags")) d.c[i].flags = it.attr("flags").cast<int32_t>();
   }
   return d;
 }
@@ -75,6 +84,7 @@ py::dict from_device(const Device& v) {
   d["cus"] = v.cus;
   d["pool"] = v.pool;
   d["mib_share"] = v.mib_share;
+  d["mem_bound"] = v.mem_bound;
   return d;
 }
 
@@ -188,6 +198,7 @@ PYBIND11_MODULE(_native, m) {
   m.attr("MAX_GPUS") = kMaxGpus;
   m.attr("MAX_CONTAINERS") = kMaxContainers;
   m.attr("OK") = static_cast<int>(kOk);
+  m.attr("FLAG_MEM_BOUND") = static_cast<int>(kFlagMemBound);
   m.attr("ERR_NO_FIT") = static_cast<int>(kErrNoFit);
   m.attr("ERR_NO_DEVICES") = static_cast<int>(kErrNoDevices);
   m.attr("ERR_BAD_PLAN") = static_cast<int>(kErrBadPlan);
@@ -231,7 +242,7 @@ PYBIND11_MODULE(_native, m) {
   // Stateless policy entry points (tests, simulators, the reference oracle diff).
   m.def(
       "choose",
-      [](const py::list& devices, const std::vector<std::pair<int32_t, int64_t>>& demand,
+      [](const py::list& devices, const py::sequence& demand,
          const Options& o, const py::object& topo) -> py::tuple {
         auto devs = to_devices(devices);
         Topology t = to_topo(topo, devs);
@@ -249,7 +260,7 @@ PYBIND11_MODULE(_native, m) {
       py::arg("devices"), py::arg("demand"), py::arg("options"), py::arg("topo") = py::none());
   m.def(
       "rate",
-      [](const py::list& devices, const std::vector<std::pair<int32_t, int64_t>>& demand,
+      [](const py::list& devices, const py::sequence& demand,
          const Options& o) {
         auto devs = to_devices(devices);
         Demand d = to_demand(demand);
@@ -258,7 +269,7 @@ PYBIND11_MODULE(_native, m) {
       py::arg("devices"), py::arg("demand"), py::arg("options"));
   m.def(
       "apply",
-      [](const py::list& devices, const std::vector<std::pair<int32_t, int64_t>>& demand,
+      [](const py::list& devices, const py::sequence& demand,
          const std::vector<std::vector<int>>& plan, bool release) {
         auto devs = to_devices(devices);
         Demand d = to_demand(demand);
@@ -292,7 +303,7 @@ PYBIND11_MODULE(_native, m) {
         });
     return idx;
   });
-  m.def("demand_hash", [](const std::vector<std::pair<int32_t, int64_t>>& demand) {
+  m.def("demand_hash", [](const py::sequence& demand) {
     return to_demand(demand).hash();
   });
 
@@ -335,7 +346,7 @@ PYBIND11_MODULE(_native, m) {
       .def(
           "filter",
           [](Ledger& l, const std::vector<int32_t>& ids,
-             const std::vector<std::pair<int32_t, int64_t>>& demand, const Options& o) {
+             const py::sequence& demand, const Options& o) {
             Demand d = to_demand(demand);
             std::vector<int32_t> rcs(ids.size());
             {
@@ -349,7 +360,7 @@ PYBIND11_MODULE(_native, m) {
       .def(
           "score",
           [](Ledger& l, const std::vector<int32_t>& ids,
-             const std::vector<std::pair<int32_t, int64_t>>& demand, const Options& o) {
+             const py::sequence& demand, const Options& o) {
             Demand d = to_demand(demand);
             std::vector<int32_t> scores(ids.size());
             {
@@ -363,7 +374,7 @@ PYBIND11_MODULE(_native, m) {
             return scores;
           })
       .def("assume",
-           [](Ledger& l, int32_t id, const std::vector<std::pair<int32_t, int64_t>>& demand,
+           [](Ledger& l, int32_t id, const py::sequence& demand,
               const Options& o) -> py::tuple {
              Demand d = to_demand(demand);
              Plan p;
@@ -378,7 +389,7 @@ PYBIND11_MODULE(_native, m) {
            })
       .def("reserve",
            [](Ledger& l, int32_t id, const std::string& key,
-              const std::vector<std::pair<int32_t, int64_t>>& demand, const Options& o) -> py::tuple {
+              const py::sequence& demand, const Options& o) -> py::tuple {
              Demand d = to_demand(demand);
              Plan p;
              std::memset(&p, 0, sizeof(p));
@@ -392,7 +403,7 @@ PYBIND11_MODULE(_native, m) {
            })
       .def("allocate_plan",
            [](Ledger& l, int32_t id, const std::string& key,
-              const std::vector<std::pair<int32_t, int64_t>>& demand,
+              const py::sequence& demand,
               const std::vector<std::vector<int>>& plan, bool committed) {
              Demand d = to_demand(demand);
              Plan p = to_plan(plan);
@@ -422,7 +433,7 @@ PYBIND11_MODULE(_native, m) {
       .def("drop_nomination", &Ledger::drop_nomination, py::call_guard<py::gil_scoped_release>())
       .def(
           "nominate",
-          [](Ledger& l, int32_t id, const std::string& key, const std::vector<std::pair<int32_t, int64_t>>& demand,
+          [](Ledger& l, int32_t id, const std::string& key, const py::sequence& demand,
              const Options& o) {
             Demand d = to_demand(demand);
             py::gil_scoped_release nogil;

@@ -172,6 +172,22 @@ bool quantity_value(std::string_view s, bool mib, int64_t* out) {
   return true;
 }
 
+constexpr const char* kMemBoundAnnotation = "nano-gpu/memory-bound";   // nanogpu/types.py
+
+// `name` is one of the comma-separated items of `list` (items trimmed of spaces).
+static bool list_has(std::string_view list, std::string_view name) {
+  while (!list.empty()) {
+    const size_t c = list.find(',');
+    std::string_view item = list.substr(0, c);
+    while (!item.empty() && item.front() == ' ') item.remove_prefix(1);
+    while (!item.empty() && item.back() == ' ') item.remove_suffix(1);
+    if (!item.empty() && item == name) return true;
+    if (c == std::string_view::npos) break;
+    list.remove_prefix(c + 1);
+  }
+  return false;
+}
+
 // 64-bit hash of a byte string, eight bytes per step (keys the per-worker node-id cache;
 // hits are verified name by name, so a collision costs a lookup, never a wrong answer).
 static uint64_t text_hash(std::string_view s) {
@@ -819,6 +835,17 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
           }
         }
       }
+    }
+  }
+  // nano-gpu/memory-bound: "true" (every container) or a comma list of container names
+  if (pod >= 0 && d.is(pod, json::Type::kObj)) {
+    const int32_t md = d.get(pod, "metadata");
+    const int32_t ann = d.is(md, json::Type::kObj) ? d.get(md, "annotations") : -1;
+    const int32_t mb = d.is(ann, json::Type::kObj) ? d.get(ann, kMemBoundAnnotation) : -1;
+    if (d.is(mb, json::Type::kStr)) {
+      const std::string_view v = d.str(mb);
+      for (int c = 0; c < dem.n; ++c)
+        if (v == "true" || list_has(v, cached.containers[c])) dem.c[c].flags |= kFlagMemBound;
     }
   }
   // node ids: any unknown node goes to Python, which can register it from its informer.

@@ -274,6 +274,7 @@ int32_t Ledger::upsert_node(const std::string& name, const Device* devs, int n,
     for (int i = 0; i < n; ++i) {
       s.devs[i].pct_free = s.devs[i].pct_total;
       s.devs[i].mib_free = s.devs[i].mib_total;
+      s.devs[i].mem_bound = 0;
     }
     s.in_use = 1;
     hdr_->n_nodes.store(count + 1, std::memory_order_release);
@@ -293,9 +294,11 @@ int32_t Ledger::upsert_node(const std::string& name, const Device* devs, int n,
         merged[i].mib_free = merged[i].mib_total > 0 ? std::max<int64_t>(0, merged[i].mib_total - mused) : 0;
         merged[i].load_usage = old.load_usage;
         merged[i].remain_load = old.remain_load;
+        merged[i].mem_bound = old.mem_bound;
       } else {
         merged[i].pct_free = merged[i].pct_total;
         merged[i].mib_free = merged[i].mib_total;
+        merged[i].mem_bound = 0;
       }
     }
     // Devices that vanished while still in use stay (unhealthy) until their pods release.

@@ -223,3 +223,42 @@ def test_nomination_lifecycle():
     # annotations of a pod bound elsewhere win over our nomination
     assert L.allocate_plan(b, "s", [(10, 0)], [[3]], True) == N.OK
     assert L.lookup("s")["node"] == b and free(a) == 750 and free(b) == 690
+
+
+def test_memory_bound_shares_pair_with_compute_bound_neighbours():
+    """CU masks do not split HBM bandwidth (profiles/gpu_calibration.md: a lone 25 % tenant
+    streams at 51 % of the device, two streaming tenants split it 25/75). Binpack therefore
+    places a memory-bound share (nano-gpu/memory-bound) on the device with the fewest
+    memory-bound tenants first; compute-bound shares still pack as before."""
+    from nanogpu.k8s.podutil import Req
+
+    t = synthetic_mi355x(2)
+    L, (nid,) = ledger_with(t)
+    mb = [Req(25, 0, N.FLAG_MEM_BOUND)]
+    rc, p1 = L.reserve(nid, "mb1", mb, BIN)
+    assert rc == N.OK and devices_of(p1) == [0]
+    rc, p2 = L.reserve(nid, "mb2", mb, BIN)          # plain binpack would stack it on device 0
+    assert rc == N.OK and devices_of(p2) == [1]
+    rc, p3 = L.reserve(nid, "cb", [(25, 0)], BIN)     # compute-bound: best fit, either device
+    assert rc == N.OK
+    assert [d["mem_bound"] for d in L.snapshot(nid)["devices"]] == [1, 1]
+    rc, p4 = L.reserve(nid, "mb3", mb, BIN)           # both hold one: best fit decides
+    assert rc == N.OK and devices_of(p4) == devices_of(p3)
+    assert L.release("mb2") == N.OK
+    assert sorted(d["mem_bound"] for d in L.snapshot(nid)["devices"]) == [0, 2]
+    # without the flag the same stream stacks on device 0 (the reference's behaviour)
+    L2, (n2,) = ledger_with(t)
+    assert [devices_of(L2.reserve(n2, f"p{i}", [(25, 0)], BIN)[1]) for i in range(2)] == [[0], [0]]
+
+
+def test_priorities_prefer_a_node_without_memory_bound_tenants():
+    from nanogpu.k8s.podutil import Req
+
+    t = synthetic_mi355x(1)
+    L, (a, b) = ledger_with(t, n_nodes=2)
+    assert L.reserve(a, "x", [Req(30, 0, N.FLAG_MEM_BOUND)], BIN)[0] == N.OK
+    assert L.reserve(b, "y", [(30, 0)], BIN)[0] == N.OK
+    sa, sb = L.score([a, b], [Req(30, 0, N.FLAG_MEM_BOUND)], BIN)
+    assert sb > sa                                    # pair with the compute-bound tenant
+    ca, cb = L.score([a, b], [(30, 0)], BIN)
+    assert ca == cb                                   # no preference for plain shares

@@ -71,7 +71,11 @@ def _pods(rng, n):
     for i in range(n):
         cs = [(f"c{k}", rng.choice([0, 5, 10, 25, 50, 100, 200]), rng.choice([0, 0, 8192, 65536]))
               for k in range(rng.choice([1, 1, 2, 3]))]
-        out.append(pu.make_pod(f"p{i}", cs))
+        pod = pu.make_pod(f"p{i}", cs)
+        mb = rng.choice([None, None, "true", "c0", "c1, c2"])   # memory-bound containers
+        if mb:
+            pod["metadata"]["annotations"][T.ANNOTATION_MEMORY_BOUND] = mb
+        out.append(pod)
     return out
 
 
@@ -415,3 +419,37 @@ def test_fd_table_is_presized():
         pytest.skip("RLIMIT_NOFILE too small")
     assert got == want
     assert _fd_slots() >= want
+
+
+def test_memory_bound_annotation_reaches_the_ledger_through_the_native_path():
+    """filter -> priorities -> bind over the native front door for a pod annotated
+    nano-gpu/memory-bound: the reservation the front door makes carries the flag, so the
+    device counts it, and the release takes it back."""
+    async def main():
+        store, rt = await _runtime(1, "SPX")
+        loop = asyncio.get_running_loop()
+        try:
+            pod = pu.make_pod("mb", [("main", 25, 8192)])
+            pod["metadata"]["annotations"][T.ANNOTATION_MEMORY_BOUND] = "true"
+            pod = store.create_pod(pod)
+            raw = _dumps({"Pod": pod, "Nodes": None, "NodeNames": ["n0"]})
+            m = pu.meta(pod)
+            bind = _dumps({"PodName": m["name"], "PodNamespace": m["namespace"], "PodUID": m["uid"], "Node": "n0"})
+            got = await loop.run_in_executor(None, _http, rt.bound_port,
+                                             [("POST", "/scheduler/filter", raw),
+                                              ("POST", "/scheduler/priorities", raw),
+                                              ("POST", "/scheduler/bind", bind)])
+            assert [g[0] for g in got] == [200, 200, 200], got
+            led = rt.state.ledger
+            nid = led.find_node("n0")
+            assert [d["mem_bound"] for d in led.snapshot(nid)["devices"]][0] == 1
+            store.delete_pod(m["namespace"], m["name"])
+            for _ in range(200):
+                if led.snapshot(nid)["devices"][0]["mem_bound"] == 0:
+                    break
+                await asyncio.sleep(0.01)
+            assert led.snapshot(nid)["devices"][0]["mem_bound"] == 0
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
