@@ -78,6 +78,16 @@ AMD_QUERIES = {
                                            'gpu_total_vram{{hostname="{node}",gpu_id="{card}"}}'),
 }
 
+# The node agent's own exporter (nanogpu/agent/metrics.py); assumes the scrape config puts
+# the node name in a `node` label (kubernetes_sd relabeling of __meta_kubernetes_pod_node_name).
+AGENT_QUERIES = {
+    T.GPU_CORE_USAGE_METRIC: MetricQuery('avg_over_time(nanogpu_device_busy_percent{{node="{node}",device="{card}"}}[1m])'
+                                         ' / 100'),
+    T.GPU_MEMORY_USAGE_METRIC: MetricQuery('nanogpu_device_vram_used_bytes{{node="{node}",device="{card}"}} / '
+                                           'nanogpu_device_vram_total_bytes{{node="{node}",device="{card}"}}'),
+}
+PRESETS = {"amd": AMD_QUERIES, "nanogpu-agent": AGENT_QUERIES}
+
 
 @dataclass(frozen=True)
 class PolicySpec:
@@ -120,8 +130,10 @@ def parse_policy(text: str) -> PolicySpec:
         raise ValueError(f"unknown policy {pol!r}")
     metrics = []
     preset = spec.get("metricsPreset")
-    if preset == "amd":
-        metrics.extend(AMD_QUERIES.items())
+    if preset is not None:
+        if preset not in PRESETS:
+            raise ValueError(f"unknown metricsPreset {preset!r} (one of {sorted(PRESETS)})")
+        metrics.extend(PRESETS[preset].items())
     for name, q in (spec.get("metrics") or {}).items():
         metrics.append((name, MetricQuery(q["query"], q.get("fallback"))))
     return PolicySpec(

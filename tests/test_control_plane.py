@@ -144,6 +144,13 @@ spec:
     assert "cardNode" in spec.query_for("other").fallback
     with pytest.raises(ValueError):
         parse_policy("spec: {scheduling: {policy: magic}}")
+    # the node agent's own exporter (nanogpu/agent/metrics.py) as the telemetry source
+    agent = parse_policy("spec: {metricsPreset: nanogpu-agent}")
+    q = agent.query_for(T.GPU_CORE_USAGE_METRIC).query.format(node="n0", card=3)
+    assert q == 'avg_over_time(nanogpu_device_busy_percent{node="n0",device="3"}[1m]) / 100'
+    assert "nanogpu_device_vram_used_bytes" in agent.query_for(T.GPU_MEMORY_USAGE_METRIC).query
+    with pytest.raises(ValueError):
+        parse_policy("spec: {metricsPreset: nvidia}")
 
 
 def test_policy_hot_reload_reaches_scheduling(tmp_path):
