@@ -488,8 +488,16 @@ def main() -> int:
         mine = numas[lr] if lr < len(numas) else -1
         ranks = [numas[r] if r < len(numas) else -1 for r in range(lws)] if lws > 1 else None
         cpus = affinity.pick_cpus(mine, lr, ranks)
+        sharing = sum(1 for r in range(lws) if affinity.pick_cpus(ranks[r], r, ranks) == cpus) if ranks else 1
         if not affinity.apply(cpus):
             cpus = []
+        cores = len(cpus) / max(1, sharing) if cpus else (os.cpu_count() or 1) / max(1, lws)
+    else:
+        cores = (os.cpu_count() or 1) / max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+    if cores < 6 and args.busy_poll_us:
+        # a rank keeps ~6 threads busy (2 front-door workers, its Python loop and executor, the
+        # stand-in's cycle and binder): with fewer cores, spinning workers would steal them
+        args.busy_poll_us = 0
     drv_proc, conn = None, None
     if not args.inproc_driver:
         # started before anything touches the GPU: a fresh interpreter, no HIP state
