@@ -28,7 +28,7 @@ from ..app import Config, Runtime
 from ..extender import server as S
 from ..k8s import podutil as pu
 from ..k8s.fake_apiserver import Faults, FakeKubeStore, InProcKube, serve
-from ..topology.model import NodeTopology, synthetic_mi355x
+from ..topology.model import NodeTopology, synthetic_mi355x, synthetic_sriov_guest
 from .driver import FastExtenderClient, NativeSchedulerDriver, SchedulerDriver, node_capacities
 
 ROOT = Path(__file__).resolve().parents[2]
@@ -302,9 +302,13 @@ async def config4(reference=False, **_):
     return res
 
 
-async def config5(reference=False, rounds=5, pods_n=1000, nodes_n=8, track_hbm=True, **_):
-    """8 MI355X nodes in CPX (64 partitions each), 1000-pod create/delete churn, binpack."""
-    nodes = make_nodes(nodes_n, 8, "CPX")
+async def config5(reference=False, rounds=5, pods_n=1000, nodes_n=8, track_hbm=True, sriov=False, **_):
+    """8 MI355X nodes in CPX (64 partitions each), 1000-pod create/delete churn, binpack.
+    `sriov`: the same 64 GPUs as 16 SR-IOV guest VMs with 4 virtual functions each."""
+    if sriov:
+        nodes = make_nodes(nodes_n * 2, 4, topo=synthetic_sriov_guest(4), prefix="mi355x-vm")
+    else:
+        nodes = make_nodes(nodes_n, 8, "CPX")
     rng = random.Random(5)
     live: list[dict] = []
     series = []
@@ -344,6 +348,8 @@ async def run_all(quick: bool = False) -> dict:
     out["config4"] = await _both(config4)()
     out["config5"] = await _both(config5)(rounds=3 if quick else 5)
     out["config5"]["ours_percent_only"] = await config5(rounds=3 if quick else 5, track_hbm=False)
+    # 64 whole-GPU VFs instead of 512 CPX partitions: the same load per device is 1/8 the pods
+    out["config5_sriov"] = await _both(config5)(rounds=3 if quick else 5, pods_n=125, sriov=True)
     return out
 
 
@@ -405,6 +411,19 @@ def summary_md(r: dict) -> str:
           "Reference release lag under churn (not simulated): ~1 released pod per second per controller "
           "worker (reference controller.go:185, 256-261), i.e. "
           f"{c5['reference_model']['release_lag_model_s']} s to release one churn round's deletions with THREADNESS=1.", ""]
+    c5s = r.get("config5_sriov")
+    if c5s:
+        L += ["## Config 5 (SR-IOV) — the same 64 GPUs as 16 guest VMs × 4 virtual functions, churn, binpack", "",
+              "Guests see their VFs' own VRAM but no xGMI links and no NUMA layout "
+              "(`topology.model.synthetic_sriov_guest`, virtualization GUEST). 125 pods: 64 whole-GPU VFs "
+              "hold 1/8 of the 512 CPX partitions' device count, so this is the same load per device.", "",
+              "| | scheduled | mean frag % | mean stranded % | max HBM-over-committed devices | max over-commit GiB | wall s |",
+              "|---|---:|---:|---:|---:|---:|---:|"]
+        for k in ("ours", "reference_model"):
+            v = c5s[k]
+            L.append(f"| {k} | {v['scheduled']} | {v['mean_frag_pct']} | {v['mean_stranded_pct']} | "
+                     f"{v['max_hbm_overcommitted_devices']} | {v['max_hbm_overcommitted_gib']} | {v['wall_s']:.2f} |")
+        L.append("")
     return "\n".join(L)
 
 

@@ -151,6 +151,18 @@ def synthetic_mi355x(n_gpus: int = 8, compute: str = "SPX", memory: str = "NPS1"
     return NodeTopology(gpus=gpus, devices=devs, link_bw=bw, virtualization="BAREMETAL")
 
 
+def synthetic_sriov_guest(n_vfs: int = 4, hbm_mib: int = 288 * 1024) -> NodeTopology:
+    """A VM on an MI355X host in SR-IOV (MxGPU) mode: `n_vfs` virtual functions passed
+    through, one whole GPU each. From inside the guest amd-smi reports virtualization mode
+    GUEST, the VFs' VRAM is their own, and neither the xGMI links between the physical GPUs
+    nor the host's NUMA layout are visible (link matrix all zero, NUMA unknown), so the
+    topology term stays neutral and placement follows the policy and HBM alone."""
+    gpus = [GpuSpec(index=g, numa=-1, hbm_mib=hbm_mib, bdf=f"0000:{0x10 + g:02x}:00.0") for g in range(n_vfs)]
+    devs = [DeviceSpec(gpu=g, hbm_mib=hbm_mib) for g in range(n_vfs)]
+    return NodeTopology(gpus=gpus, devices=devs, link_bw=[[0.0] * n_vfs for _ in range(n_vfs)],
+                        virtualization="GUEST")
+
+
 def _assign_pools(ds: list, pool_mib: int, nps: int) -> None:
     """Partitions of one GPU: `nps` memory partitions of `pool_mib` each, len(ds)/nps
     compute partitions per memory partition. One member per pool = the device's own HBM."""

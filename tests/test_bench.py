@@ -70,3 +70,16 @@ def test_config_harness_plumbing_and_topology():
         assert c2r["hbm_probe"]["overcommitted_gib"] > 0
 
     asyncio.run(main())
+
+
+def test_config5_sriov_guests_churn():
+    """SR-IOV guest VMs (virtual functions, no xGMI or NUMA visible): churn schedules every
+    pod and the HBM dimension keeps every VF within its VRAM."""
+    from nanogpu.sim import configs as C
+    from nanogpu.topology.model import NodeTopology, synthetic_sriov_guest
+
+    t = synthetic_sriov_guest(4)
+    assert t.virtualization == "GUEST" and NodeTopology.from_json(t.to_json()).virtualization == "GUEST"
+    assert all(g.numa == -1 for g in t.gpus) and not any(any(row) for row in t.link_bw)
+    r = asyncio.run(C.config5(rounds=5, pods_n=125, sriov=True))
+    assert r["scheduled"] == 125 and r["max_hbm_overcommitted_gib"] == 0
