@@ -453,3 +453,47 @@ def test_memory_bound_annotation_reaches_the_ledger_through_the_native_path():
             await rt.stop()
 
     asyncio.run(main())
+
+
+def test_native_node_id_cache_follows_node_removal_and_return():
+    """Each front-door worker caches the node ids of a NodeNames list it has seen; a node
+    deleted and re-created (new ledger slot) between identical filter requests must be
+    resolved again, and answers stay byte-identical to the Python path."""
+    async def main():
+        store, rt = await _runtime(4, "SPX")
+        ext = rt.extender
+        loop = asyncio.get_running_loop()
+        try:
+            pod = store.create_pod(pu.make_pod("q", [("main", 50, 0)]))
+            raw = _dumps({"Pod": pod, "Nodes": None, "NodeNames": ["n0", "n1", "n2", "n3"]})
+
+            async def both():
+                got = await loop.run_in_executor(None, _http, rt.bound_port, [("POST", "/scheduler/filter", raw),
+                                                                              ("POST", "/scheduler/priorities", raw)])
+                assert got[0] == (200, _dumps(ext.filter(json.loads(raw))))
+                assert got[1] == (200, _dumps(ext.prioritize(json.loads(raw))))
+                return json.loads(got[0][1])
+
+            old_id = rt.state.ledger.find_node("n1")
+            assert (await both())["NodeNames"] == ["n0", "n1", "n2", "n3"]
+            node1 = store.get_node("n1")
+            store.delete_node("n1")
+            assert await _wait_until(lambda: rt.state.ledger.find_node("n1") < 0)
+            r = await both()
+            assert "n1" in r["FailedNodes"] and "n1" not in r["NodeNames"]
+            store.add_node(node1)
+            assert await _wait_until(lambda: rt.state.ledger.find_node("n1") >= 0)
+            assert rt.state.ledger.find_node("n1") != old_id
+            assert (await both())["NodeNames"] == ["n0", "n1", "n2", "n3"]
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
+
+
+async def _wait_until(pred, timeout=5.0):
+    for _ in range(int(timeout / 0.01)):
+        if pred():
+            return True
+        await asyncio.sleep(0.01)
+    return pred()
