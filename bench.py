@@ -429,7 +429,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
         prof = cProfile.Profile()
         prof.enable()
     sampler = StallSampler() if args.stall_trace and d.rank == 0 else None
-    cpu0 = time.process_time()
+    cpu0, loop_cpu0 = time.process_time(), time.thread_time()
     t0 = time.perf_counter()
     if sampler is not None:
         sampler.on.set()
@@ -451,8 +451,9 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
     d.barrier()
     d.sync()
     elapsed = time.perf_counter() - t0
-    results["cpu_us_per_pod"] = 1e6 * (time.process_time() - cpu0) / max(
-        1, sum(st["scheduled"] for st in results["steps"]))
+    n_sched = max(1, sum(st["scheduled"] for st in results["steps"]))
+    results["cpu_us_per_pod"] = 1e6 * (time.process_time() - cpu0) / n_sched
+    results["loop_cpu_us_per_pod"] = 1e6 * (time.thread_time() - loop_cpu0) / n_sched
     binds = sorted(s["dur_ms"] for s in rt.tracer.dump(10 ** 9, "bind") if s["ok"])
     results["elapsed_s"] = elapsed
     results["bind_ms"] = binds
@@ -574,6 +575,8 @@ def main() -> int:
             "step_diag_rank0": res.get("step_diag"),
             # CPU time of the rank-0 extender process (all its threads) per pod it handled
             "extender_cpu_us_per_pod_rank0": round(res.get("cpu_us_per_pod", 0.0), 1),
+            # of which the Python event-loop thread (binds' API writes, informer, controller)
+            "extender_loop_cpu_us_per_pod_rank0": round(res.get("loop_cpu_us_per_pod", 0.0), 1),
         }
         print(json.dumps(line), flush=True)
         if args.json_out:
