@@ -160,6 +160,21 @@ class Extender:
                     raise
             await asyncio.sleep(0.005 * (2 ** attempt))
 
+    async def _retry_after(self, first: ApiError, op: str, fn, *a):
+        """`_retry` for a call whose first attempt already failed with `first`."""
+        self.metrics.child(self.metrics.api_errors, op, str(first.status)).inc()
+        if first.status < 500 and first.status != 429 or self.api_retries == 0:
+            raise first
+        await asyncio.sleep(0.005)
+        for attempt in range(1, self.api_retries + 1):
+            try:
+                return await fn(*a)
+            except ApiError as e:
+                self.metrics.child(self.metrics.api_errors, op, str(e.status)).inc()
+                if e.status < 500 and e.status != 429 or attempt == self.api_retries:
+                    raise
+            await asyncio.sleep(0.005 * (2 ** attempt))
+
     async def _bind(self, args: BindingArgs, sp) -> None:
         pod = None if self.verify_pod_on_bind else self.pods.pop(args.pod_uid)
         tp = time.perf_counter()
@@ -216,10 +231,17 @@ class Extender:
         try:
             t2 = time.perf_counter()
             extra = {T.ANNOTATION_ASSUME_TIME: f"{time.time():.6f}"}
-            await self._retry("patch", self.api.patch_pod, ns, name, pu.placement_patch_names(names, plan, extra))
+            patch = pu.placement_patch_names(names, plan, extra)
+            try:   # first attempt inline; the retry loop only after an API error
+                await self.api.patch_pod(ns, name, patch)
+            except ApiError as e:
+                await self._retry_after(e, "patch", self.api.patch_pod, ns, name, patch)
             t3 = time.perf_counter()
             try:
-                await self._retry("bind", self.api.bind_pod, ns, name, uid, node)
+                try:
+                    await self.api.bind_pod(ns, name, uid, node)
+                except ApiError as e0:
+                    await self._retry_after(e0, "bind", self.api.bind_pod, ns, name, uid, node)
             except ApiError as e:
                 # A retried bind whose first attempt landed: already bound to this node is success.
                 if not e.conflict or pu.node_name_of(await self.api.get_pod(ns, name)) != node:

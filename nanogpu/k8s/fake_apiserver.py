@@ -370,23 +370,33 @@ class InProcKube:
             await asyncio.sleep(self.store.faults.latency_s)
 
     async def get_pod(self, ns, name):
-        await self._rtt()
+        self.calls += 1
+        if self.store.faults.latency_s > 0:   # inline: no coroutine per call
+            await asyncio.sleep(self.store.faults.latency_s)
         return self.store.get_pod(ns, name)
 
     async def patch_pod(self, ns, name, patch):
-        await self._rtt()
+        self.calls += 1
+        if self.store.faults.latency_s > 0:   # inline: no coroutine per call
+            await asyncio.sleep(self.store.faults.latency_s)
         return self.store.patch_pod(ns, name, patch)
 
     async def bind_pod(self, ns, name, uid, node):
-        await self._rtt()
+        self.calls += 1
+        if self.store.faults.latency_s > 0:   # inline: no coroutine per call
+            await asyncio.sleep(self.store.faults.latency_s)
         self.store.bind_pod(ns, name, uid, node)
 
     async def create_pod(self, pod):
-        await self._rtt()
+        self.calls += 1
+        if self.store.faults.latency_s > 0:   # inline: no coroutine per call
+            await asyncio.sleep(self.store.faults.latency_s)
         return self.store.create_pod(pod)
 
     async def delete_pod(self, ns, name):
-        await self._rtt()
+        self.calls += 1
+        if self.store.faults.latency_s > 0:   # inline: no coroutine per call
+            await asyncio.sleep(self.store.faults.latency_s)
         self.store.delete_pod(ns, name)
 
     async def list_pods(self, label_selector=None, field_selector=None, namespace=None):
