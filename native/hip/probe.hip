@@ -349,12 +349,17 @@ std::vector<double> mfma_colocated(int dev, const std::vector<std::vector<uint32
 // launched together. Returns per-tenant GB/s (read + write) over each tenant's own events.
 // CU masks partition the compute units, not the memory system: this measures how the HBM3E
 // bandwidth splits between memory-bound neighbours (profiles/gpu_calibration.md).
+// `iters_each` (optional, one per mask) lets a neighbour outlast the tenant being measured.
 std::vector<double> hbm_colocated(int dev, const std::vector<std::vector<uint32_t>>& masks, size_t bytes,
-                                  int iters) {
+                                  int iters, std::vector<int> iters_each) {
   HIP_OK(hipSetDevice(dev));
   const size_t n = bytes / sizeof(float4);
   if (masks.empty() || n == 0 || iters <= 0) throw std::invalid_argument("hbm_colocated: masks, bytes, iters");
   const size_t k = masks.size();
+  if (iters_each.empty()) iters_each.assign(k, iters);
+  if (iters_each.size() != k) throw std::invalid_argument("hbm_colocated: one iteration count per mask");
+  for (int it : iters_each)
+    if (it <= 0 || it > 1000) throw std::invalid_argument("hbm_colocated: iterations in 1..1000");
   std::vector<std::unique_ptr<Stream>> streams;
   std::vector<std::unique_ptr<Events>> evs;
   std::vector<std::unique_ptr<DevBuf<float4>>> src, dst;
@@ -371,15 +376,50 @@ std::vector<double> hbm_colocated(int dev, const std::vector<std::vector<uint32_
   HIP_OK(hipDeviceSynchronize());
   for (size_t i = 0; i < k; ++i) {
     HIP_OK(hipEventRecord(evs[i]->a, streams[i]->s));
-    for (int it = 0; it < iters; ++it)
+    for (int it = 0; it < iters_each[i]; ++it)
       hipLaunchKernelGGL(hbm_copy, grid, dim3(kCopyBlock), 0, streams[i]->s, src[i]->p, dst[i]->p, n);
     HIP_OK(hipEventRecord(evs[i]->b, streams[i]->s));
   }
   HIP_OK(hipGetLastError());
   std::vector<double> gbs(k);
   for (size_t i = 0; i < k; ++i)
-    gbs[i] = 2.0 * static_cast<double>(n * sizeof(float4)) * iters / (evs[i]->ms() * 1e-3) / 1e9;
+    gbs[i] = 2.0 * static_cast<double>(n * sizeof(float4)) * iters_each[i] / (evs[i]->ms() * 1e-3) / 1e9;
   return gbs;
+}
+
+// A streaming tenant next to a compute-bound one: an HBM copy on `hbm_mask` and an MFMA
+// burn on `mfma_mask`, launched together on their own CU-masked streams. The burn is sized
+// (`mfma_iters`) to outlast the copy, so the copy's rate is measured entirely beside it.
+// Returns {copy GB/s, burn TFLOP/s}: what a memory-bound pod gets when the scheduler pairs
+// it with a compute-bound neighbour (kFlagMemBound) instead of another streaming one.
+std::vector<double> mixed_colocated(int dev, const std::vector<uint32_t>& hbm_mask,
+                                    const std::vector<uint32_t>& mfma_mask, size_t bytes, int iters,
+                                    int mfma_blocks, int mfma_iters) {
+  HIP_OK(hipSetDevice(dev));
+  const size_t n = bytes / sizeof(float4);
+  if (n == 0 || iters <= 0 || mfma_blocks <= 0 || mfma_iters <= 0)
+    throw std::invalid_argument("mixed_colocated: bytes, iters and the burn shape must be positive");
+  Stream sc(hbm_mask), sm(mfma_mask);
+  Events ec, em;
+  DevBuf<float4> src(n), dst(n);
+  DevBuf<float> out(static_cast<size_t>(mfma_blocks) * 256);
+  HIP_OK(hipMemset(src.p, 0, n * sizeof(float4)));
+  const dim3 grid(copy_grid(n));
+  hipLaunchKernelGGL(hbm_copy, grid, dim3(kCopyBlock), 0, sc.s, src.p, dst.p, n);    // warm-up
+  hipLaunchKernelGGL(mfma_burn, dim3(mfma_blocks), dim3(256), 0, sm.s, out.p, 8);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipEventRecord(em.a, sm.s));
+  hipLaunchKernelGGL(mfma_burn, dim3(mfma_blocks), dim3(256), 0, sm.s, out.p, mfma_iters);
+  HIP_OK(hipEventRecord(em.b, sm.s));
+  HIP_OK(hipEventRecord(ec.a, sc.s));
+  for (int it = 0; it < iters; ++it)
+    hipLaunchKernelGGL(hbm_copy, grid, dim3(kCopyBlock), 0, sc.s, src.p, dst.p, n);
+  HIP_OK(hipEventRecord(ec.b, sc.s));
+  HIP_OK(hipGetLastError());
+  const double gbs = 2.0 * static_cast<double>(n * sizeof(float4)) * iters / (ec.ms() * 1e-3) / 1e9;
+  const double tf = 4.0 * 32768.0 * mfma_iters * (static_cast<double>(mfma_blocks) * 4) / (em.ms() * 1e-3) / 1e12;
+  return {gbs, tf};
 }
 
 double peer_bandwidth(int src, int dst, size_t bytes, int iters) {
@@ -436,8 +476,12 @@ PYBIND11_MODULE(_probe, m) {
         "C[32x32] = bf16(A[32x16]) @ bf16(B[16x32]) with one v_mfma_f32_32x32x16_bf16 (fp32 accumulate).");
   m.def("copy_check", &copy_check, py::arg("device") = 0, py::arg("n_floats") = size_t(1) << 24,
         py::call_guard<py::gil_scoped_release>(), "hbm_copy kernel result == source, bit for bit.");
+  m.def("mixed_colocated", &mixed_colocated, py::arg("device"), py::arg("hbm_mask"), py::arg("mfma_mask"),
+        py::arg("bytes") = size_t(1) << 30, py::arg("iters") = 10, py::arg("mfma_blocks") = 1536,
+        py::arg("mfma_iters") = 4096, py::call_guard<py::gil_scoped_release>(),
+        "{copy GB/s, MFMA TFLOP/s} for a streaming tenant beside a compute-bound one.");
   m.def("hbm_colocated", &hbm_colocated, py::arg("device"), py::arg("cu_masks"), py::arg("bytes") = size_t(1) << 30,
-        py::arg("iters") = 10, py::call_guard<py::gil_scoped_release>(),
+        py::arg("iters") = 10, py::arg("iters_each") = std::vector<int>{}, py::call_guard<py::gil_scoped_release>(),
         "Per-tenant HBM copy GB/s for concurrent tenants on CU-masked streams.");
   m.def("mfma_colocated", &mfma_colocated, py::arg("device"), py::arg("cu_masks"), py::arg("blocks"),
         py::arg("iters") = 2048, py::call_guard<py::gil_scoped_release>(),

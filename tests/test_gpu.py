@@ -283,3 +283,24 @@ def test_hbm_bandwidth_under_cu_mask_sharing(P):
     # every tenant moves data; the pair together cannot beat the device
     assert ta > 0.05 * full and tb > 0.05 * full, (ta, tb, full)
     assert min(ta, tb) < full * 1.05
+
+
+def test_memory_bound_tenant_pairs_better_with_compute_bound_neighbour(P):
+    """What kFlagMemBound buys: a streaming 25 % tenant measured entirely beside (a) a
+    streaming 75 % neighbour and (b) an MFMA-bound 75 % neighbour, both neighbours outlasting
+    it. Recorded for profiles/gpu_calibration.md."""
+    from nanogpu.agent import cumask
+
+    d = cumask.DeviceCUs(256, 8)
+    a, b = d.grant("a", 25), d.grant("b", 75)
+    ma, mb = cumask.mask_words(a), cumask.mask_words(b)
+    alone = P.hbm_colocated(0, [ma], 1 << 30, 10)[0]
+    beside_stream = P.hbm_colocated(0, [ma, mb], 1 << 30, 10, [10, 40])[0]
+    beside_mfma, mfma_tf = P.mixed_colocated(0, ma, mb, 1 << 30, 10, len(b) * 8, 32768)
+    mfma_alone = P.mfma_throughput(0, mb, len(b) * 8, 4096)["tflops"]
+    record("memory_bound_pairing", {"stream25_alone_gbs": round(alone, 1),
+                                    "stream25_beside_stream75_gbs": round(beside_stream, 1),
+                                    "stream25_beside_mfma75_gbs": round(beside_mfma, 1),
+                                    "mfma75_beside_stream25_tflops": round(mfma_tf, 1),
+                                    "mfma75_alone_tflops": round(mfma_alone, 1)})
+    assert beside_mfma > beside_stream, (alone, beside_stream, beside_mfma)
