@@ -500,8 +500,11 @@ PYBIND11_MODULE(_native, m) {
                  pd["demand"] = b.demand;
                  prep = pd;
                }
-               out.append(py::make_tuple(r.id, r.method, r.path, r.query, py::bytes(r.body), py::bytes(r.pod_json),
-                                         r.t_arrival, prep));
+               // a prepared bind needs neither its request body nor the cached pod JSON in Python
+               const bool bare = r.bind.ok;
+               out.append(py::make_tuple(r.id, r.method, r.path, r.query,
+                                         bare ? py::bytes() : py::bytes(r.body),
+                                         bare ? py::bytes() : py::bytes(r.pod_json), r.t_arrival, prep));
              }
              return out;
            })
