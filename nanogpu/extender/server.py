@@ -61,7 +61,8 @@ class Router:
         g, p = "GET", "POST"
         self.table = {
             (p, "/scheduler/filter"): self.filter, (p, "/scheduler/priorities"): self.prioritize,
-            (p, "/scheduler/bind"): self.bind, (g, "/version"): self.version,
+            (p, "/scheduler/bind"): self.bind, (p, "/scheduler/preemption"): self.preempt,
+            (g, "/version"): self.version,
             (p, "/status"): self.status, (g, "/status"): self.status, (g, "/metrics"): self.metrics,
             (g, "/healthz"): self.healthz, (g, "/readyz"): self.readyz, (g, "/debug/trace"): self.trace,
             (g, "/debug/stacks"): self.stacks, (g, "/debug/pprof/goroutine/"): self.stacks,
@@ -105,6 +106,12 @@ class Router:
             return 500, JSON, _dumps({"Error": str(e)})
         res = await self.ext.bind(args)
         return (500 if res.get("Error") else 200), JSON, _dumps(res)
+
+    async def preempt(self, q, body):
+        try:
+            return 200, JSON, _dumps(self.ext.preempt(_load(body)))
+        except ValueError as e:
+            return 400, JSON, _dumps({"error": str(e)})
 
     # ---------------------------------------------------------------- ops
     async def version(self, q, body):

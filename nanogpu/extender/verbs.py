@@ -23,7 +23,8 @@ from ..k8s import podutil as pu
 from ..k8s.client import ApiError
 from ..obs import Metrics, Span, Tracer
 from ..state.cluster import N, ClusterState, SchedulingError
-from .wire import BindingArgs, ExtenderArgs, binding_result, filter_result, priority_list
+from .wire import (BindingArgs, ExtenderArgs, PreemptionArgs, binding_result, filter_result,
+                   preemption_result, priority_list)
 
 log = logging.getLogger(__name__)
 
@@ -116,6 +117,31 @@ class Extender:
         self.metrics.child(self.metrics.verb_latency, "prioritize").observe(time.perf_counter() - t0)
         self.metrics.child(self.metrics.verb_total, "prioritize", "ok").inc()
         return priority_list(names, scores)
+
+    # ------------------------------------------------------------------ preemption
+    def preempt(self, body) -> dict:
+        """kube-scheduler's preemptVerb. Its victims free `nano-gpu/gpu-percent` as a
+        node-wide scalar; whether the pod then fits depends on which devices, partitions and
+        HBM pools those shares held. A candidate node stays only if the preemptor fits once
+        its victims' shares are released. This is simulated on a copy of the node in the
+        ledger (Ledger::fits_without). Victims are passed through unchanged: kube-scheduler
+        chose them for every resource, not only GPU. Raises ValueError on a malformed body."""
+        t0 = time.perf_counter()
+        args = PreemptionArgs.decode(body)
+        demand = pu.pod_demand(args.pod)
+        keep: dict[str, list[str]] = {}
+        with self.tracer.span("preempt", pu.pod_key(args.pod)) as sp:
+            for node, uids in args.victims.items():
+                e = self.state.node_entry(node)
+                if e is None:
+                    continue
+                rc, _ = self.state.ledger.fits_without(e.id, uids, demand, self.state.options)
+                if rc == N.OK:
+                    keep[node] = uids
+            sp.note = f"{len(keep)}/{len(args.victims)} nodes"
+        self.metrics.child(self.metrics.verb_latency, "preempt").observe(time.perf_counter() - t0)
+        self.metrics.child(self.metrics.verb_total, "preempt", "ok").inc()
+        return preemption_result(keep, args.pdb)
 
     # ------------------------------------------------------------------ bind
     async def bind(self, body) -> dict:

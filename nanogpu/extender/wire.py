@@ -76,3 +76,44 @@ class BindingArgs:
 
 def binding_result(error: str = "") -> dict:
     return {"Error": error}
+
+
+class PreemptionArgs:
+    """ExtenderPreemptionArgs: the preemptor and, per candidate node, the victims
+    kube-scheduler chose. With nodeCacheCapable it sends NodeNameToMetaVictims
+    ({"Pods": [{"UID"}], "NumPDBViolations"}); otherwise NodeNameToVictims with full pods.
+    Not in the reference (it registers no preemptVerb)."""
+    __slots__ = ("pod", "victims", "pdb")
+
+    def __init__(self, pod: dict, victims: dict[str, list[str]], pdb: dict[str, int]):
+        self.pod, self.victims, self.pdb = pod, victims, pdb
+
+    @classmethod
+    def decode(cls, body: Any) -> "PreemptionArgs":
+        if not isinstance(body, dict):
+            raise ValueError("ExtenderPreemptionArgs must be a JSON object")
+        pod = field(body, "Pod") or {}
+        if not isinstance(pod, dict):
+            raise ValueError("Pod must be an object")
+        meta = field(body, "NodeNameToMetaVictims")
+        full = field(body, "NodeNameToVictims")
+        src = meta if isinstance(meta, dict) else full if isinstance(full, dict) else {}
+        victims: dict[str, list[str]] = {}
+        pdb: dict[str, int] = {}
+        for node, v in src.items():
+            pods = field(v, "Pods") or []
+            uids = []
+            for p in pods:
+                if not isinstance(p, dict):
+                    continue
+                uid = field(p, "UID") if src is meta else ((p.get("metadata") or {}).get("uid"))
+                if uid:
+                    uids.append(str(uid))
+            victims[node] = uids
+            pdb[node] = int(field(v, "NumPDBViolations", 0) or 0)
+        return cls(pod, victims, pdb)
+
+
+def preemption_result(victims: dict[str, list[str]], pdb: dict[str, int]) -> dict:
+    return {"NodeNameToMetaVictims": {n: {"Pods": [{"UID": u} for u in uids], "NumPDBViolations": pdb.get(n, 0)}
+                                      for n, uids in victims.items()}}

@@ -143,6 +143,10 @@ class Ledger {
   int32_t release(const std::string& key);
   bool lookup(const std::string& key, PodRecord* out) const;
   std::vector<PodRecord> pods_on(int32_t node) const;
+  // Preemption check (extender preemptVerb): does demand `d` fit on node `id` once the
+  // shares of `victims` (pod keys) are released? Simulated on a copy; nothing changes.
+  int32_t fits_without(int32_t id, const std::vector<std::string>& victims, const Demand& d, const Options& o,
+                       Plan* plan) const;
   std::vector<std::string> expired_reservations(double older_than_s) const;
   int64_t n_pods() const { return hdr_->n_pods.load(std::memory_order_acquire); }
 

@@ -427,6 +427,22 @@ PYBIND11_MODULE(_native, m) {
              return out;
            },
            py::arg("node") = -1)
+      .def(
+          "fits_without",
+          [](const Ledger& l, int32_t id, const std::vector<std::string>& victims, const py::sequence& demand,
+             const Options& o) {
+            Demand d = to_demand(demand);
+            Plan p;
+            std::memset(&p, 0, sizeof(p));
+            int32_t rc;
+            {
+              py::gil_scoped_release nogil;
+              rc = l.fits_without(id, victims, d, o, &p);
+            }
+            return py::make_tuple(rc, rc == kOk ? plan_list(p) : py::list());
+          },
+          py::arg("node"), py::arg("victims"), py::arg("demand"), py::arg("options"),
+          "(rc, plan): would `demand` fit on `node` once the victims' shares are released (simulated)")
       .def("expired_reservations", &Ledger::expired_reservations, py::call_guard<py::gil_scoped_release>())
       .def("expired_nominations", &Ledger::expired_nominations, py::call_guard<py::gil_scoped_release>())
       .def("drop_reservation", &Ledger::drop_reservation, py::call_guard<py::gil_scoped_release>())

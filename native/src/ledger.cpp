@@ -680,6 +680,31 @@ bool Ledger::lookup(const std::string& key, PodRecord* out) const {
   return true;
 }
 
+int32_t Ledger::fits_without(int32_t id, const std::vector<std::string>& victims, const Demand& d,
+                             const Options& o, Plan* plan) const {
+  NodeSnapshot snap;
+  if (!snapshot(id, &snap)) return kErrUnknownNode;
+  // take the victims' shares back on a copy of the node (a victim the ledger does not hold,
+  // or holds on another node, frees nothing here)
+  for (const std::string& key : victims) {
+    if (key.empty() || key.size() >= kKeyLen) continue;
+    const uint64_t h = key_hash(key.c_str());
+    const int s = shard_of(h);
+    Demand vd;
+    Plan vp;
+    {
+      lock_mu(&hdr_->shard_mu[s]);
+      Unlock us{&hdr_->shard_mu[s]};
+      const PodSlot* p = find_pod_locked(s, h, key.c_str());
+      if (!p || p->node != id) continue;
+      vd = p->demand;
+      vp = p->plan;
+    }
+    unapply(snap.devs, snap.n_devs, vd, vp);
+  }
+  return choose(snap.devs, snap.n_devs, &snap.topo, d, o, plan);
+}
+
 std::vector<PodRecord> Ledger::pods_on(int32_t node_id) const {
   std::vector<PodRecord> out;
   for (int s = 0; s < kPodShards; ++s) {

@@ -8,6 +8,7 @@ from annotations (dealer.go:58-72, 271-301; D14 completed pods skipped), policy 
 (prometheus.go:68-83; D12 errors surfaced), bind rollback (D2) and retries (D1).
 """
 import asyncio
+import json
 import math
 
 import pytest
@@ -361,3 +362,73 @@ def test_sweeps_never_release_a_pod_that_moved_on():
     assert st.ledger.drop_reservation(uid) != N.OK    # the sweep's release is a no-op
     assert st.status()["n0"]["GPUs"][0]["Percent"] == 60
     assert st.sweep_reservations(0.0) == []
+
+
+# ----------------------------------------------------------------------------- preemption
+def test_preemption_verb_keeps_only_nodes_where_the_victims_free_a_fitting_device():
+    """preemptVerb (not in the reference): kube-scheduler frees gpu-percent as a node-wide
+    scalar. A 100 % pod needs one whole device, so victims spread over two devices do not
+    make room even though their percents add up."""
+    st = ClusterState(policy="binpack")
+    for n in ("n0", "n1"):
+        st.register_node(node(n, 2))
+    pods = {}
+    for name, nd in (("a", "n0"), ("x", "n0"), ("b", "n1"), ("c", "n1")):
+        pods[name] = p = pu.make_pod(name, [("m", 50)])
+        st.reserve(p, nd)
+        st.commit(pu.pod_uid(p))
+    # n0: a and x share device 0 (binpack) and device 1 is free -> take x's device 1 away
+    hog = pu.make_pod("hog", [("m", 100)])
+    st.reserve(hog, "n0")
+    st.commit(pu.pod_uid(hog))
+    assert sorted(free_of(st, "n0")) == [0, 0] and sorted(free_of(st, "n1")) == [0, 100]
+    ext = Extender(st, api=None)
+    uid = pu.pod_uid
+    big = pu.make_pod("big", [("m", 100)])
+    body = {"Pod": big, "NodeNameToMetaVictims": {
+        "n0": {"Pods": [{"UID": uid(pods["a"])}], "NumPDBViolations": 0},           # 50 % of device 0 only
+        "n1": {"Pods": [{"UID": uid(pods["b"])}, {"UID": uid(pods["c"])}], "NumPDBViolations": 1},
+        "ghost": {"Pods": [{"UID": "nope"}]}}}
+    res = ext.preempt(body)
+    assert set(res["NodeNameToMetaVictims"]) == {"n1"}
+    assert res["NodeNameToMetaVictims"]["n1"] == {"Pods": [{"UID": uid(pods["b"])}, {"UID": uid(pods["c"])}],
+                                                  "NumPDBViolations": 1}
+    # victims holding a whole device on n0 (the hog) do make room there; nothing changed in the ledger
+    res = ext.preempt({"Pod": big, "NodeNameToMetaVictims": {"n0": {"Pods": [{"UID": uid(hog)}]}}})
+    assert set(res["NodeNameToMetaVictims"]) == {"n0"}
+    assert sorted(free_of(st, "n0")) == [0, 0]
+    # the full-pod form (nodeCacheCapable=false) carries pod objects
+    res = ext.preempt({"Pod": big, "NodeNameToVictims": {"n1": {"Pods": [pods["b"], pods["c"]]}}})
+    assert set(res["NodeNameToMetaVictims"]) == {"n1"}
+    with pytest.raises(ValueError):
+        ext.preempt([1, 2])
+
+
+def free_of(st, n):
+    return [g["Percent"] for g in st.status()[n]["GPUs"]]
+
+
+def test_preemption_route_over_http():
+    async def main():
+        store = FakeKubeStore()
+        store.add_node(node("n0", 1))
+        rt = await runtime(store)
+        try:
+            p = pu.make_pod("low", [("m", 60)])
+            rt.state.reserve(p, "n0")
+            rt.state.commit(pu.pod_uid(p))
+            body = json.dumps({"Pod": pu.make_pod("high", [("m", 80)]),
+                               "NodeNameToMetaVictims": {"n0": {"Pods": [{"UID": pu.pod_uid(p)}]}}}).encode()
+            import aiohttp
+
+            async with aiohttp.ClientSession() as s:
+                async with s.post(f"http://127.0.0.1:{rt.bound_port}/scheduler/preemption", data=body) as r:
+                    assert r.status == 200
+                    out = await r.json()
+                async with s.post(f"http://127.0.0.1:{rt.bound_port}/scheduler/preemption", data=b"[") as r:
+                    assert r.status == 400
+            assert list(out["NodeNameToMetaVictims"]) == ["n0"]
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
