@@ -254,11 +254,27 @@ def test_agent_metrics_read_real_amdgpu_sysfs(host, P):
     busy = re.search(r'nanogpu_device_busy_percent\{device="0"\} (\d+)', text)
     assert busy and 0 <= int(busy.group(1)) <= 100
     assert f'nanogpu_device_vram_total_bytes{{device="0"}} {host["gpus"][0]["vram_bytes"]}' in text
-    before = used()
+    import time
+
+    def settled() -> int:
+        # device-wide counter: memory of processes that just exited (earlier tests' children)
+        # drains asynchronously, so wait until two readings agree
+        prev = used()
+        for _ in range(50):
+            time.sleep(0.1)
+            cur = used()
+            if abs(cur - prev) < (64 << 20):
+                return cur
+            prev = cur
+        return prev
+
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    before = settled()
     x = torch.empty(4 << 30, dtype=torch.uint8, device="cuda:0")
     x.fill_(1)
     torch.cuda.synchronize()
-    grew = used() - before
+    grew = settled() - before
     del x
     torch.cuda.empty_cache()
     record("agent_metrics_vram_delta_for_4GiB", grew)
