@@ -192,21 +192,20 @@ class Ledger {
       return node == o.node && gen == o.gen && dh == o.dh && oh == o.oh;
     }
   };
-  struct CacheVal {
-    int32_t rc;
-    Plan plan;
-  };
   // Plan cache: process-local, one small direct-mapped table per node slot (a 2-way probe
-  // on the demand/options hash), guarded by a per-node spin flag. Entries carry the node
-  // generation they were computed at, so a change to the node invalidates them without any
-  // clearing; filters of different nodes never share a lock.
+  // on the demand/options hash). Entries carry the node generation they were computed at,
+  // so a change to the node invalidates them without any clearing. Writers and plan readers
+  // take a per-node spin flag; the filter/priorities path (rc + score only) reads through a
+  // sequence counter without any read-modify-write, so 64 nodes cost 64 plain load pairs.
   static constexpr int kCacheWays = 32;
   struct CacheEntry {
-    uint64_t gen = 0, dh = 0, oh = 0;
-    bool used = false;
-    CacheVal val{};
+    std::atomic<uint64_t> gen{0}, dh{0}, oh{0};
+    std::atomic<int32_t> rc{0}, score{0};
+    std::atomic<bool> used{false};
+    Plan plan{};   // under `busy`
   };
   struct NodeCache {
+    std::atomic<uint32_t> seq{0};   // odd while a writer updates entries
     std::atomic<bool> busy{false};
     CacheEntry e[kCacheWays];
     void lock() {

@@ -379,6 +379,15 @@ inline int cache_way(uint64_t dh, uint64_t oh) {
 }
 }  // namespace
 
+namespace {
+constexpr auto kRlx = std::memory_order_relaxed;
+
+template <class E>
+inline bool entry_is(const E& e, uint64_t gen, uint64_t dh, uint64_t oh) {
+  return e.used.load(kRlx) && e.gen.load(kRlx) == gen && e.dh.load(kRlx) == dh && e.oh.load(kRlx) == oh;
+}
+}  // namespace
+
 bool Ledger::cache_get(const CacheKey& k, int32_t* rc, Plan* plan) const {
   NodeCache* cp = node_cache(k.node, false);
   if (!cp) return false;
@@ -387,9 +396,9 @@ bool Ledger::cache_get(const CacheKey& k, int32_t* rc, Plan* plan) const {
   c.lock();
   for (int j = 0; j < 2; ++j) {
     const CacheEntry& e = c.e[(w + j) % kCacheWays];
-    if (e.used && e.gen == k.gen && e.dh == k.dh && e.oh == k.oh) {
-      *rc = e.val.rc;
-      *plan = e.val.plan;
+    if (entry_is(e, k.gen, k.dh, k.oh)) {
+      *rc = e.rc.load(kRlx);
+      *plan = e.plan;
       c.unlock();
       return true;
     }
@@ -398,17 +407,40 @@ bool Ledger::cache_get(const CacheKey& k, int32_t* rc, Plan* plan) const {
   return false;
 }
 
+// Sequence-counter read (no read-modify-write): sample seq, read the entry's atomic fields,
+// and accept them if seq is even and unchanged; a writer in between makes the reader retry,
+// and a reader that keeps losing falls back to the lock.
 bool Ledger::cache_get_score(const CacheKey& k, int32_t* rc, int32_t* score) const {
   NodeCache* cp = node_cache(k.node, false);
   if (!cp) return false;
   NodeCache& c = *cp;
   const int w = cache_way(k.dh, k.oh);
+  for (int tries = 0; tries < 4; ++tries) {
+    const uint32_t s0 = c.seq.load(std::memory_order_acquire);
+    if (s0 & 1u) continue;
+    int found = -1;
+    int32_t r = 0, sc = 0;
+    for (int j = 0; j < 2 && found < 0; ++j) {
+      const CacheEntry& e = c.e[(w + j) % kCacheWays];
+      if (entry_is(e, k.gen, k.dh, k.oh)) {
+        found = j;
+        r = e.rc.load(kRlx);
+        sc = e.score.load(kRlx);
+      }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    if (c.seq.load(kRlx) != s0) continue;
+    if (found < 0) return false;
+    *rc = r;
+    *score = sc;
+    return true;
+  }
   c.lock();
   for (int j = 0; j < 2; ++j) {
     const CacheEntry& e = c.e[(w + j) % kCacheWays];
-    if (e.used && e.gen == k.gen && e.dh == k.dh && e.oh == k.oh) {
-      *rc = e.val.rc;
-      *score = e.val.plan.score;
+    if (entry_is(e, k.gen, k.dh, k.oh)) {
+      *rc = e.rc.load(kRlx);
+      *score = e.score.load(kRlx);
       c.unlock();
       return true;
     }
@@ -427,14 +459,20 @@ void Ledger::cache_put(const CacheKey& k, int32_t rc, const Plan& plan) {
   CacheEntry* a = &c.e[w];
   CacheEntry* b = &c.e[(w + 1) % kCacheWays];
   CacheEntry* dst = a;
-  if (a->used && a->gen == k.gen && !(a->dh == k.dh && a->oh == k.oh))
-    dst = (!b->used || b->gen != k.gen || (b->dh == k.dh && b->oh == k.oh)) ? b : a;
-  dst->gen = k.gen;
-  dst->dh = k.dh;
-  dst->oh = k.oh;
-  dst->used = true;
-  dst->val.rc = rc;
-  dst->val.plan = plan;
+  auto same_key = [&](const CacheEntry* e) { return e->dh.load(kRlx) == k.dh && e->oh.load(kRlx) == k.oh; };
+  if (a->used.load(kRlx) && a->gen.load(kRlx) == k.gen && !same_key(a))
+    dst = (!b->used.load(kRlx) || b->gen.load(kRlx) != k.gen || same_key(b)) ? b : a;
+  const uint32_t s = c.seq.load(kRlx);
+  c.seq.store(s + 1, kRlx);                              // odd: lock-free readers retry
+  std::atomic_thread_fence(std::memory_order_release);
+  dst->gen.store(k.gen, kRlx);
+  dst->dh.store(k.dh, kRlx);
+  dst->oh.store(k.oh, kRlx);
+  dst->rc.store(rc, kRlx);
+  dst->score.store(plan.score, kRlx);
+  dst->used.store(true, kRlx);
+  dst->plan = plan;
+  c.seq.store(s + 2, std::memory_order_release);
   c.unlock();
 }
 
@@ -787,7 +825,11 @@ void Ledger::clear_cache() {
     if (!cp) continue;
     NodeCache& c = *cp;
     c.lock();
-    for (auto& e : c.e) e.used = false;
+    const uint32_t sq = c.seq.load(kRlx);
+    c.seq.store(sq + 1, kRlx);
+    std::atomic_thread_fence(std::memory_order_release);
+    for (auto& e : c.e) e.used.store(false, kRlx);
+    c.seq.store(sq + 2, std::memory_order_release);
     c.unlock();
   }
 }
@@ -799,7 +841,7 @@ size_t Ledger::cache_size() const {
     if (!cp) continue;
     NodeCache& c = *cp;
     c.lock();
-    for (const auto& e : c.e) n += e.used;
+    for (const auto& e : c.e) n += e.used.load(kRlx);
     c.unlock();
   }
   return n;
