@@ -111,6 +111,12 @@ class FakeKubeStore:
         obj["metadata"]["resourceVersion"] = str(self.rv)
         return obj
 
+    def _stamp(self, obj: dict) -> dict:
+        """`_bump` for an object whose top level and metadata the caller already copied."""
+        self.rv += 1
+        obj["metadata"]["resourceVersion"] = str(self.rv)
+        return obj
+
     def _emit(self, kind: str, etype: str, obj: dict) -> None:
         ev = {"type": etype, "object": obj}
         self.history[kind].append((self.rv, ev))
@@ -143,8 +149,8 @@ class FakeKubeStore:
         key = (m["namespace"], m["name"])
         if key in self.pods:
             raise ApiError(409, f'pods "{m["name"]}" already exists', "AlreadyExists")
-        pod.setdefault("status", {}).setdefault("phase", "Pending")
-        pod = self._bump(pod)
+        pod["status"].setdefault("phase", "Pending")
+        pod = self._stamp(pod)
         self.pods[key] = pod
         self._emit("pods", "ADDED", pod)
         return pod
@@ -158,12 +164,13 @@ class FakeKubeStore:
 
     def patch_pod(self, ns: str, name: str, patch: dict) -> dict:
         self._count("patch_pod")
-        if self.faults.roll(self.faults.patch_error_rate):
+        if self.faults.patch_error_rate and self.faults.roll(self.faults.patch_error_rate):
             raise ApiError(500, "injected patch failure", "InternalError")
         p = self.pods.get((ns, name))
         if p is None:
             raise ApiError(404, f'pods "{name}" not found', "NotFound")
-        np_ = self._bump(pu.apply_patch(p, patch))
+        np_ = pu.apply_patch(p, patch)
+        np_ = self._stamp(np_) if np_.get("metadata") is not p.get("metadata") else self._bump(np_)
         self.pods[(ns, name)] = np_
         self._emit("pods", "MODIFIED", np_)
         return np_
@@ -185,9 +192,9 @@ class FakeKubeStore:
 
     def bind_pod(self, ns: str, name: str, uid: str, node: str) -> None:
         self._count("bind_pod")
-        if self.faults.roll(self.faults.bind_error_rate):
+        if self.faults.bind_error_rate and self.faults.roll(self.faults.bind_error_rate):
             raise ApiError(500, "injected binding failure", "InternalError")
-        if self.faults.roll(self.faults.conflict_rate):
+        if self.faults.conflict_rate and self.faults.roll(self.faults.conflict_rate):
             raise ApiError(409, f'Operation cannot be fulfilled on pods/binding "{name}": injected', "Conflict")
         p = self.pods.get((ns, name))
         if p is None:
@@ -201,7 +208,8 @@ class FakeKubeStore:
         np_ = dict(p)
         np_["spec"] = dict(p.get("spec") or {}, nodeName=node)
         np_["status"] = dict(p.get("status") or {}, phase="Running")
-        np_ = self._bump(np_)
+        np_["metadata"] = dict(p.get("metadata") or {})
+        np_ = self._stamp(np_)
         self.pods[(ns, name)] = np_
         self.bindings.append((ns, name, node))
         self._emit("pods", "MODIFIED", np_)
