@@ -45,6 +45,29 @@ def calibrate(topo: NodeTopology, device: int = 0) -> dict:
     return out
 
 
+def gpu_selftest(P, device: int) -> bool:
+    """Active check of one HIP device with the probe's kernels: a bit-exact 16 MiB HBM copy
+    and one bf16 MFMA tile (32x32x16, small integers, so the fp32 result is exact) against
+    a host reference. A device that loads its driver and shows in sysfs can still compute
+    wrong or fault; the agent then reports it Unhealthy (kubelet) and unschedulable (the
+    extender). Runs on the calling thread (HIP's current device)."""
+    try:
+        if not P.copy_check(device, 1 << 22):
+            return False
+        a = [float((i * 7) % 7 - 3) for i in range(32 * 16)]
+        b = [float((i * 5) % 5 - 2) for i in range(16 * 32)]
+        c = P.gemm_tile(a, b)                  # on `device`: copy_check made it current
+        for r in range(32):
+            row = a[r * 16:(r + 1) * 16]
+            for col in range(32):
+                if c[r * 32 + col] != sum(row[k] * b[k * 32 + col] for k in range(16)):
+                    return False
+        return True
+    except Exception:                          # a HIP error is a failed device
+        log.exception("self-test of device %d raised", device)
+        return False
+
+
 def node_patch(topo: NodeTopology) -> dict:
     labels = {T.AMD_GPU_NODE_LABEL[0]: T.AMD_GPU_NODE_LABEL[1]}
     if topo.gpus:
@@ -77,6 +100,7 @@ class NodeAgent:
         self.health_period_s = health_period_s
         self.sysfs_root = sysfs_root
         self.kubelet_check_s = kubelet_check_s
+        self.selftest_failed: set[int] = set()   # devices whose active self-test failed
         self.registrations = 0
         self._register = True
         self.plugin = None
@@ -176,7 +200,7 @@ class NodeAgent:
         ras_ok = [d.healthy for d in topo.devices] if len(topo.devices) == len(self.topo.devices) else None
         changed = []
         for i, minor in enumerate(self.render_minors()):
-            ok = minor in present and (ras_ok is None or ras_ok[i])
+            ok = minor in present and (ras_ok is None or ras_ok[i]) and i not in self.selftest_failed
             if self.topo.devices[i].healthy != ok:
                 self.topo.devices[i].healthy = ok
                 changed.append(i)
@@ -186,6 +210,43 @@ class NodeAgent:
             log.warning("agent %s: devices %s health changed", self.node, changed)
             await self.api.patch_node(self.node, node_patch(self.topo))
         return changed
+
+    def run_selftest(self, P=None) -> list[int] | None:
+        """`gpu_selftest` on every HIP device; returns the failed device indices, or None when
+        the probe is missing or its device count does not match the topology (HIP orders
+        devices like the KFD nodes the topology is read from)."""
+        if P is None:
+            from ..native import probe
+
+            P = probe(required=False)
+        if P is None:
+            return None
+        n = P.device_count()
+        if n != len(self.topo.devices):
+            log.warning("agent %s: %d HIP devices vs %d topology devices: self-test skipped", self.node, n,
+                        len(self.topo.devices))
+            return None
+        return [i for i in range(n) if not gpu_selftest(P, i)]
+
+    async def selftest(self, P=None) -> list[int] | None:
+        """Runs the self-test off the event loop and applies it: failed devices become
+        Unhealthy for kubelet and unschedulable in the published topology."""
+        failed = await asyncio.get_running_loop().run_in_executor(None, self.run_selftest, P)
+        if failed is None:
+            return None
+        self.selftest_failed = set(failed)
+        changed = False
+        for i, d in enumerate(self.topo.devices):
+            ok = i not in self.selftest_failed and d.healthy
+            if i in self.selftest_failed and d.healthy:
+                d.healthy = False
+                changed = True
+            if self.plugin is not None:
+                self.plugin.set_health(i, ok)
+        if changed:
+            log.warning("agent %s: self-test failed on devices %s", self.node, sorted(self.selftest_failed))
+            await self.api.patch_node(self.node, node_patch(self.topo))
+        return failed
 
     async def stop(self) -> None:
         for t in self.tasks:
@@ -209,6 +270,8 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--kube-api", default=None)
     ap.add_argument("--kubeconfig", default=os.environ.get("KUBECONFIG"))
     ap.add_argument("--print", action="store_true", help="print the topology annotation and exit")
+    ap.add_argument("--selftest", action="store_true",
+                    help="run the HIP self-test (HBM copy + MFMA tile) on every device at start-up")
     ap.add_argument("--metrics-port", type=int, default=9410,
                     help="device / pod / container GPU metrics on :PORT/metrics (0: off)")
     a = ap.parse_args(argv)
@@ -231,6 +294,10 @@ def main(argv: list[str] | None = None) -> int:
         agent = NodeAgent(api, a.node_name, topo, host, device_plugin=a.advertise == "device-plugin",
                           plugin_dir=a.plugin_dir, sysfs_root=a.sysfs_root)
         await agent.start()
+        if a.selftest:
+            failed = await agent.selftest()
+            log.info("agent %s: self-test %s", a.node_name,
+                     "skipped" if failed is None else f"failed on {failed}" if failed else "passed")
         metrics = None
         if a.metrics_port:
             from .metrics import serve_metrics

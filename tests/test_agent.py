@@ -233,3 +233,46 @@ def test_ras_errors_make_devices_unhealthy_end_to_end(tmp_path):
         await agent.stop()
 
     asyncio.run(main())
+
+
+class _FakeProbe:
+    """Stands in for nanogpu._probe: device 3's HBM copy is corrupt, device 5's MFMA tile
+    computes wrong values (gemm_tile runs on the device copy_check made current)."""
+
+    def __init__(self, n=8):
+        self.n, self.cur = n, 0
+
+    def device_count(self):
+        return self.n
+
+    def copy_check(self, dev, n_floats):
+        self.cur = dev
+        return dev != 3
+
+    def gemm_tile(self, a, b):
+        c = [sum(a[r * 16 + k] * b[k * 32 + col] for k in range(16)) for r in range(32) for col in range(32)]
+        if self.cur == 5:
+            c[17] += 1.0
+        return c
+
+
+def test_agent_selftest_marks_failing_devices_unhealthy():
+    async def main():
+        store = FakeKubeStore()
+        topo = synthetic_mi355x(8)
+        store.add_node(pu.make_node("n0", 8, topo.to_json()))
+        agent = NodeAgent(InProcKube(store), "n0", topo, device_plugin=False, health_period_s=0)
+        await agent.start()
+        failed = await agent.selftest(_FakeProbe())
+        assert failed == [3, 5]
+        published = store.get_node("n0")["metadata"]["annotations"][T.ANNOTATION_TOPOLOGY]
+        from nanogpu.topology.model import NodeTopology
+
+        assert [d.healthy for d in NodeTopology.from_json(published).devices] == \
+            [True, True, True, False, True, False, True, True]
+        # a probe that sees a different device count cannot map devices: skipped, nothing changes
+        assert await agent.selftest(_FakeProbe(4)) is None
+        assert agent.selftest_failed == {3, 5}
+        await agent.stop()
+
+    asyncio.run(main())

@@ -320,3 +320,18 @@ def test_memory_bound_tenant_pairs_better_with_compute_bound_neighbour(P):
                                     "mfma75_beside_stream25_tflops": round(mfma_tf, 1),
                                     "mfma75_alone_tflops": round(mfma_alone, 1)})
     assert beside_mfma > beside_stream, (alone, beside_stream, beside_mfma)
+
+
+def test_agent_selftest_passes_on_the_real_device(host, P):
+    """The node agent's active self-test (HBM copy bit-exact + one MFMA tile against a host
+    reference) on the real MI355X."""
+    import asyncio
+
+    from nanogpu.agent.node import NodeAgent, gpu_selftest
+    from nanogpu.topology.model import from_host_json
+
+    assert gpu_selftest(P, 0)
+    topo = from_host_json(host)
+    agent = NodeAgent(api=None, node_name="box", topo=topo, device_plugin=False)
+    failed = asyncio.run(agent.selftest(P)) if len(topo.devices) == P.device_count() else []
+    assert failed == [], failed
