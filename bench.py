@@ -345,9 +345,13 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
         t_step0 = tc = time.perf_counter()
         if conn is not None:
             # the pods are created in the API server (this process), then the scheduler
-            # process schedules them through the extender's HTTP front door
-            for p in pods:
-                await api.create_pod(p)
+            # process schedules them through the extender's HTTP front door. A burst comes
+            # from many clients at once: with a modelled API RTT the creates overlap.
+            if args.api_rtt_ms > 0:
+                await asyncio.gather(*(api.create_pod(p) for p in pods))
+            else:
+                for p in pods:
+                    await api.create_pod(p)
             tc = time.perf_counter() - tc
             conn.send(("step", step))
             summary = await loop.run_in_executor(None, conn.recv)
