@@ -104,31 +104,38 @@ class Informer:
         else:
             stream = _singletons(self.api.watch(self.resource, self.rv, label_selector=self.label_selector))
         store, key, handlers = self.store, self.key, self.handlers
+        pop, get = store.pop, store.get
         async for batch in stream:
-            for ev in batch:
-                etype, obj = ev.get("type"), ev.get("object") or {}
-                if etype == "ERROR":
-                    raise ApiError(int(obj.get("code", 500)), obj.get("message", "watch error"))
-                self.rv = (obj.get("metadata") or {}).get("resourceVersion", self.rv)
-                if etype == "BOOKMARK":
-                    continue
-                k = key(obj)
-                if etype == "DELETED":
-                    old = store.pop(k, None)
-                else:
-                    old = store.get(k)
-                    store[k] = obj
-                    if etype == "ADDED" and old is not None:
-                        etype = "MODIFIED"
-                    elif etype == "MODIFIED" and old is None:
-                        etype = "ADDED"
-                if len(handlers) == 1:
-                    try:
-                        handlers[0](etype, obj, old)
-                    except Exception:  # a handler bug must not kill the informer
-                        log.exception("informer handler failed for %s %s", etype, k)
-                else:
-                    self._dispatch(etype, obj, old)
+            last = None
+            try:
+                for ev in batch:
+                    etype, obj = ev.get("type"), ev.get("object") or {}
+                    if etype == "ERROR":
+                        raise ApiError(int(obj.get("code", 500)), obj.get("message", "watch error"))
+                    last = obj
+                    if etype == "BOOKMARK":
+                        continue
+                    k = key(obj)
+                    if etype == "DELETED":
+                        old = pop(k, None)
+                    else:
+                        old = get(k)
+                        store[k] = obj
+                        if etype == "ADDED" and old is not None:
+                            etype = "MODIFIED"
+                        elif etype == "MODIFIED" and old is None:
+                            etype = "ADDED"
+                    if len(handlers) == 1:
+                        try:
+                            handlers[0](etype, obj, old)
+                        except Exception:  # a handler bug must not kill the informer
+                            log.exception("informer handler failed for %s %s", etype, k)
+                    else:
+                        self._dispatch(etype, obj, old)
+            finally:
+                # resume point: the last event handled (events arrive in resourceVersion order)
+                if last is not None:
+                    self.rv = (last.get("metadata") or {}).get("resourceVersion", self.rv)
 
     def start(self) -> asyncio.Task:
         self._task = asyncio.ensure_future(self.run())
