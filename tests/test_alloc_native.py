@@ -120,6 +120,29 @@ def test_ledger_invariants_under_random_churn(demands, mode, policy, seed):
             assert dv["pct_free"] == dv["pct_total"] and dv["mib_free"] == dv["mib_total"]
 
 
+@settings(max_examples=60, deadline=None)
+@given(_demand, st.sampled_from(["SPX", "CPX"]), st.sampled_from([N.Policy.BINPACK, N.Policy.SPREAD]),
+       st.booleans(), st.lists(st.tuples(st.sampled_from([10, 30, 60]), st.just(0)), max_size=6), st.randoms())
+def test_container_order_does_not_change_the_placement(d, mode, policy, compat, pre, rnd):
+    """SURVEY §4 property: containers are placed largest-first and mapped back, so a
+    permutation of a pod's containers lands the same (demand, devices) multiset. (First-fit
+    is the reference's SampleRater, rater.go:29-50, which places in container order.)"""
+    o = N.Options(policy, compat=compat)
+    perm = list(d)
+    rnd.shuffle(perm)
+    results = []
+    for demand in (d, perm):
+        L, (nid,) = ledger_with(synthetic_mi355x(2, mode))
+        for k, p in enumerate(pre):            # the same partly used node both times
+            L.reserve(nid, f"pre{k}", [p], o)
+        rc, plan = L.reserve(nid, "pod", demand, o)
+        # compat mode ignores HBM as the reference does: containers of equal percent are
+        # interchangeable there, so only the percent identifies a container
+        key = (lambda c: c[0]) if compat else (lambda c: c)
+        results.append((rc, sorted((key(c), tuple(ix)) for c, ix in zip(demand, plan)) if rc == N.OK else None))
+    assert results[0] == results[1]
+
+
 def test_partial_plan_failure_restores_exactly_D5():
     """Reference allocate.go:108-113 restores Demand[i] (not [j]) and does not skip -1
     indices when a multi-container allocation fails half way; here the debit is undone
