@@ -9,7 +9,6 @@ import asyncio
 import json
 
 import aiohttp
-import pytest
 
 from nanogpu import types as T
 from nanogpu.app import Config, Runtime

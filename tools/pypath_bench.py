@@ -1,6 +1,6 @@
 """CPU time of the extender's Python pod path per 1000 pods (create, bind_prepared, watch events,
 delete + release) against the in-process API server, without sockets: min over 10 bursts."""
-import sys, asyncio, time, statistics
+import sys, asyncio, time
 sys.path.insert(0, __import__('os').path.dirname(__import__('os').path.dirname(__import__('os').path.abspath(__file__))))
 import bench
 from nanogpu.app import Config, Runtime
