@@ -542,3 +542,61 @@ def test_native_verbs_survive_mutated_bodies():
         assert handled > 50 and declined > 50
 
     asyncio.run(main())
+
+
+def test_front_door_survives_mutated_http_framing():
+    """Fuzz the HTTP layer: pipelined Content-Length and chunked requests with bytes flipped,
+    inserted, deleted or cut off, each on its own connection that the client half-closes.
+    The front door must answer or close every one of them and keep serving good requests."""
+    def blast(port, data):
+        s = socket.create_connection(("127.0.0.1", port))
+        s.settimeout(0.5)
+        try:
+            s.sendall(data)
+            s.shutdown(socket.SHUT_WR)
+            while s.recv(65536):
+                pass
+        except (socket.timeout, ConnectionResetError, BrokenPipeError):
+            pass
+        finally:
+            s.close()
+
+    async def main():
+        store, rt = await _runtime(4)
+        rng = random.Random(3)
+        pods = [store.create_pod(p) for p in _pods(rng, 4)]
+        loop = asyncio.get_running_loop()
+        good = _dumps({"Pod": pods[0], "Nodes": None, "NodeNames": ["n0", "n1"]})
+        alphabet = b"\r\n: 0123456789abcdefABCDEF-;chunkedContent-LengthTransfer-Encoding"
+        try:
+            for it in range(400):
+                path = rng.choice([b"/scheduler/filter", b"/scheduler/priorities", b"/version", b"/status"])
+                if rng.random() < 0.5:
+                    req = b"POST " + path + b" HTTP/1.1\r\nHost: x\r\nContent-Length: " + \
+                        str(len(good)).encode() + b"\r\n\r\n" + good
+                else:
+                    mid = len(good) // 2
+                    req = b"POST " + path + b" HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n" + \
+                        b"".join(f"{len(p):x}\r\n".encode() + p + b"\r\n" for p in (good[:mid], good[mid:])) + \
+                        b"0\r\n\r\n"
+                data = bytearray(req * rng.randint(1, 3))
+                for _ in range(rng.randint(1, 4)):
+                    at, op = rng.randrange(len(data)), rng.random()
+                    if op < 0.4:
+                        data[at] = rng.choice(alphabet)
+                    elif op < 0.7:
+                        data.insert(at, rng.choice(alphabet))
+                    elif op < 0.9:
+                        del data[at]
+                    else:
+                        del data[at:]
+                    if not data:
+                        break
+                await loop.run_in_executor(None, blast, rt.bound_port, bytes(data))
+                if it % 50 == 49:
+                    got = await loop.run_in_executor(None, _http, rt.bound_port, [("POST", "/scheduler/filter", good)])
+                    assert got[0][0] == 200
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
