@@ -36,16 +36,24 @@ constexpr int kPodShards = 64;
 // Nominated: taken tentatively at priorities for the top-scored node (see nominate()).
 enum PodState : int32_t { kPodEmpty = 0, kPodReserved = 1, kPodCommitted = 2, kPodTombstone = 3, kPodNominated = 4 };
 
+// Cache-line layout: a filter reads, per node, the name and in_use (verifying its id cache)
+// and the generation (its plan-cache key) without locking. Those live apart from the mutex,
+// whose line every lock/unlock by any worker process dirties, so lock traffic on a node does
+// not turn the filters of the other workers into cross-CCD misses; the generation has a
+// line of its own as it changes on every mutation.
 struct NodeSlot {
-  char name[kNameLen];
-  pthread_mutex_t mu;
-  std::atomic<uint64_t> generation;
+  char name[kNameLen];                              // written at registration only
   int32_t in_use;
   int32_t n_devs;
-  int32_t n_pods;
-  int32_t pad;
-  Topology topo;
+  alignas(64) std::atomic<uint64_t> generation;
+  alignas(64) pthread_mutex_t mu;
+  int32_t n_pods;                                   // under mu
+  alignas(64) Topology topo;
   Device devs[kMaxDevs];
+};
+
+struct alignas(64) PaddedMutex {   // one line per pod-shard lock (no false sharing)
+  pthread_mutex_t m;
 };
 
 struct PodSlot {
@@ -65,11 +73,11 @@ struct LedgerHeader {
   uint32_t pods_per_shard;
   uint32_t pad;
   std::atomic<int32_t> n_nodes;
-  std::atomic<uint64_t> epoch;      // bumps on every mutation anywhere
-  std::atomic<int64_t> n_pods;
-  pthread_mutex_t registry_mu;
-  pthread_mutex_t shard_mu[kPodShards];
   std::atomic<int32_t> attached;    // processes attached
+  pthread_mutex_t registry_mu;
+  alignas(64) std::atomic<uint64_t> epoch;      // bumps on every mutation anywhere
+  alignas(64) std::atomic<int64_t> n_pods;
+  PaddedMutex shard_mu[kPodShards];
   int32_t shard_live[kPodShards];   // guarded by shard_mu[s]
   int32_t shard_tomb[kPodShards];
 };

@@ -18,7 +18,7 @@
 namespace nanogpu {
 
 static constexpr uint64_t kMagic = 0x4e414e4f47505531ULL;  // "NANOGPU1"
-static constexpr uint32_t kVersion = 4;  // 4: Device gained HBM pools
+static constexpr uint32_t kVersion = 5;  // 4: Device gained HBM pools; 5: cache-line layout
 
 static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -137,7 +137,7 @@ Ledger::Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, b
     hdr_->attached.store(0);
     init_mutex(&hdr_->registry_mu);
     for (int s = 0; s < kPodShards; ++s) {
-      init_mutex(&hdr_->shard_mu[s]);
+      init_mutex(&hdr_->shard_mu[s].m);
       hdr_->shard_live[s] = 0;
       hdr_->shard_tomb[s] = 0;
     }
@@ -558,8 +558,8 @@ int32_t Ledger::reserve_as(int32_t id, const std::string& key, const Demand& d, 
   lock_node(n);
   Unlock un{&n->mu};
   {
-    lock_mu(&hdr_->shard_mu[s]);
-    Unlock us{&hdr_->shard_mu[s]};
+    lock_mu(&hdr_->shard_mu[s].m);
+    Unlock us{&hdr_->shard_mu[s].m};
     PodSlot* p = find_pod_locked(s, h, key.c_str());
     if (p) {
       if (p->state == kPodNominated) {
@@ -585,8 +585,8 @@ int32_t Ledger::reserve_as(int32_t id, const std::string& key, const Demand& d, 
   rc = apply(n->devs, n->n_devs, d, *plan);
   if (rc != kOk) return rc;
   {
-    lock_mu(&hdr_->shard_mu[s]);
-    Unlock us{&hdr_->shard_mu[s]};
+    lock_mu(&hdr_->shard_mu[s].m);
+    Unlock us{&hdr_->shard_mu[s].m};
     PodSlot* p = insert_pod_locked(s, h, key.c_str());
     if (!p) {
       unapply(n->devs, n->n_devs, d, *plan);
@@ -620,8 +620,8 @@ int32_t Ledger::allocate_plan(int32_t id, const std::string& key, const Demand& 
   lock_node(n);
   Unlock un{&n->mu};
   {
-    lock_mu(&hdr_->shard_mu[s]);
-    Unlock us{&hdr_->shard_mu[s]};
+    lock_mu(&hdr_->shard_mu[s].m);
+    Unlock us{&hdr_->shard_mu[s].m};
     PodSlot* p = find_pod_locked(s, h, key.c_str());
     if (p) {
       if (p->node != id) return kErrPodExists;
@@ -632,8 +632,8 @@ int32_t Ledger::allocate_plan(int32_t id, const std::string& key, const Demand& 
   int32_t rc = apply(n->devs, n->n_devs, d, plan);
   if (rc != kOk) return rc;
   {
-    lock_mu(&hdr_->shard_mu[s]);
-    Unlock us{&hdr_->shard_mu[s]};
+    lock_mu(&hdr_->shard_mu[s].m);
+    Unlock us{&hdr_->shard_mu[s].m};
     PodSlot* p = insert_pod_locked(s, h, key.c_str());
     if (!p) {
       unapply(n->devs, n->n_devs, d, plan);
@@ -655,8 +655,8 @@ int32_t Ledger::allocate_plan(int32_t id, const std::string& key, const Demand& 
 int32_t Ledger::commit(const std::string& key) {
   const uint64_t h = key_hash(key.c_str());
   const int s = shard_of(h);
-  lock_mu(&hdr_->shard_mu[s]);
-  Unlock us{&hdr_->shard_mu[s]};
+  lock_mu(&hdr_->shard_mu[s].m);
+  Unlock us{&hdr_->shard_mu[s].m};
   PodSlot* p = find_pod_locked(s, h, key.c_str());
   if (!p) return kErrUnknownPod;
   p->state = kPodCommitted;
@@ -675,8 +675,8 @@ int32_t Ledger::release_if(const std::string& key, int32_t only_state) {
   const int s = shard_of(h);
   int32_t id;
   {
-    lock_mu(&hdr_->shard_mu[s]);
-    Unlock us{&hdr_->shard_mu[s]};
+    lock_mu(&hdr_->shard_mu[s].m);
+    Unlock us{&hdr_->shard_mu[s].m};
     PodSlot* p = find_pod_locked(s, h, key.c_str());
     if (!p) return kErrUnknownPod;
     if (only && p->state != only_state) return kOkExisting;
@@ -686,8 +686,8 @@ int32_t Ledger::release_if(const std::string& key, int32_t only_state) {
   if (!n) return kErrUnknownNode;
   lock_node(n);
   Unlock un{&n->mu};
-  lock_mu(&hdr_->shard_mu[s]);
-  Unlock us{&hdr_->shard_mu[s]};
+  lock_mu(&hdr_->shard_mu[s].m);
+  Unlock us{&hdr_->shard_mu[s].m};
   PodSlot* p = find_pod_locked(s, h, key.c_str());
   if (!p || p->node != id) return kErrUnknownPod;  // raced with another release
   if (only && p->state != only_state) return kOkExisting;   // adopted / committed meanwhile
@@ -705,8 +705,8 @@ int32_t Ledger::release_if(const std::string& key, int32_t only_state) {
 bool Ledger::lookup(const std::string& key, PodRecord* out) const {
   const uint64_t h = key_hash(key.c_str());
   const int s = shard_of(h);
-  lock_mu(&hdr_->shard_mu[s]);
-  Unlock us{&hdr_->shard_mu[s]};
+  lock_mu(&hdr_->shard_mu[s].m);
+  Unlock us{&hdr_->shard_mu[s].m};
   PodSlot* p = find_pod_locked(s, h, key.c_str());
   if (!p) return false;
   out->key = p->key;
@@ -731,8 +731,8 @@ int32_t Ledger::fits_without(int32_t id, const std::vector<std::string>& victims
     Demand vd;
     Plan vp;
     {
-      lock_mu(&hdr_->shard_mu[s]);
-      Unlock us{&hdr_->shard_mu[s]};
+      lock_mu(&hdr_->shard_mu[s].m);
+      Unlock us{&hdr_->shard_mu[s].m};
       const PodSlot* p = find_pod_locked(s, h, key.c_str());
       if (!p || p->node != id) continue;
       vd = p->demand;
@@ -746,8 +746,8 @@ int32_t Ledger::fits_without(int32_t id, const std::vector<std::string>& victims
 std::vector<PodRecord> Ledger::pods_on(int32_t node_id) const {
   std::vector<PodRecord> out;
   for (int s = 0; s < kPodShards; ++s) {
-    lock_mu(&hdr_->shard_mu[s]);
-    Unlock us{&hdr_->shard_mu[s]};
+    lock_mu(&hdr_->shard_mu[s].m);
+    Unlock us{&hdr_->shard_mu[s].m};
     PodSlot* t = shard(s);
     for (uint32_t i = 0; i < hdr_->pods_per_shard; ++i) {
       const PodSlot& p = t[i];
@@ -763,8 +763,8 @@ std::vector<std::string> Ledger::expired(int32_t state, double older_than_s) con
   std::vector<std::string> out;
   const double now = mono_now();
   for (int s = 0; s < kPodShards; ++s) {
-    lock_mu(&hdr_->shard_mu[s]);
-    Unlock us{&hdr_->shard_mu[s]};
+    lock_mu(&hdr_->shard_mu[s].m);
+    Unlock us{&hdr_->shard_mu[s].m};
     PodSlot* t = shard(s);
     for (uint32_t i = 0; i < hdr_->pods_per_shard; ++i)
       if (t[i].state == state && now - t[i].t_reserved > older_than_s) out.emplace_back(t[i].key);
