@@ -67,6 +67,12 @@ def test_minimum_slice_one_pod_binpack():
                     assert "nanogpu_verb_latency_seconds" in await r.text()
             gpus = status["mi355x-0"]["GPUs"]
             assert gpus[0]["Percent"] == 80 and all(g["Percent"] == 100 for g in gpus[1:])
+            # the operator's view of the same body (python -m nanogpu.top)
+            from nanogpu import top
+            table = top.render(await asyncio.get_running_loop().run_in_executor(None, top.fetch, base))
+            dev0 = next(r for r in table.splitlines() if r.startswith("mi355x-0") and r.split()[1] == "0")
+            assert "20%" in dev0 and "ok" in dev0
+            assert "1 nodes, 8 devices, 7.8 device-equivalents free, 10.3% of the free compute" in table
             # delete frees the share (reference only Forgets on delete: D3)
             store.delete_pod("default", "p1")
             assert await _wait(lambda: rt.state.status()["mi355x-0"]["GPUs"][0]["Percent"] == 100)
