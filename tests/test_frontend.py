@@ -544,10 +544,12 @@ def test_native_verbs_survive_mutated_bodies():
     asyncio.run(main())
 
 
-def test_front_door_survives_mutated_http_framing():
+@pytest.mark.parametrize("routes", ["native", "python"])
+def test_front_door_survives_mutated_http_framing(routes):
     """Fuzz the HTTP layer: pipelined Content-Length and chunked requests with bytes flipped,
     inserted, deleted or cut off, each on its own connection that the client half-closes.
-    The front door must answer or close every one of them and keep serving good requests."""
+    The front door must answer or close every one of them and keep serving good requests,
+    both on the routes it answers itself and on those it hands to Python (bind, preemption)."""
     def blast(port, data):
         s = socket.create_connection(("127.0.0.1", port))
         s.settimeout(0.5)
@@ -567,17 +569,24 @@ def test_front_door_survives_mutated_http_framing():
         pods = [store.create_pod(p) for p in _pods(rng, 4)]
         loop = asyncio.get_running_loop()
         good = _dumps({"Pod": pods[0], "Nodes": None, "NodeNames": ["n0", "n1"]})
+        bodies = {b"/scheduler/bind": _dumps({"PodName": "p0", "PodNamespace": "default",
+                                               "PodUID": pods[0]["metadata"]["uid"], "Node": "n0"}),
+                  b"/scheduler/preemption": _dumps({"Pod": pods[0], "NodeNameToMetaVictims": {
+                      "n0": {"Pods": [{"UID": "x"}], "NumPDBViolations": 0}}})}
+        paths = [b"/scheduler/filter", b"/scheduler/priorities", b"/version", b"/status"] if routes == "native" \
+            else [b"/scheduler/bind", b"/scheduler/preemption", b"/status"]
         alphabet = b"\r\n: 0123456789abcdefABCDEF-;chunkedContent-LengthTransfer-Encoding"
         try:
             for it in range(400):
-                path = rng.choice([b"/scheduler/filter", b"/scheduler/priorities", b"/version", b"/status"])
+                path = rng.choice(paths)
+                body = bodies.get(path, good)
                 if rng.random() < 0.5:
                     req = b"POST " + path + b" HTTP/1.1\r\nHost: x\r\nContent-Length: " + \
-                        str(len(good)).encode() + b"\r\n\r\n" + good
+                        str(len(body)).encode() + b"\r\n\r\n" + body
                 else:
-                    mid = len(good) // 2
+                    mid = len(body) // 2
                     req = b"POST " + path + b" HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n" + \
-                        b"".join(f"{len(p):x}\r\n".encode() + p + b"\r\n" for p in (good[:mid], good[mid:])) + \
+                        b"".join(f"{len(p):x}\r\n".encode() + p + b"\r\n" for p in (body[:mid], body[mid:])) + \
                         b"0\r\n\r\n"
                 data = bytearray(req * rng.randint(1, 3))
                 for _ in range(rng.randint(1, 4)):
