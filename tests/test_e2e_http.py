@@ -223,3 +223,18 @@ def test_client_follows_a_rotated_service_account_token(tmp_path):
             await runner.cleanup()
 
     asyncio.run(main())
+
+
+def test_top_cli_reports_an_unreachable_extender(capsys):
+    from nanogpu import top
+
+    assert top.main(["--url", "http://127.0.0.1:9"]) == 1      # discard port: refused
+    assert "nanogpu.top: http://127.0.0.1:9" in capsys.readouterr().err
+    st = {"n1": {"GPUs": [{"Percent": 50, "PercentTotal": 100, "MemoryMiB": 1024, "MemoryMiBTotal": 4096,
+                           "MemoryPool": 0, "GPU": 0, "Partition": 0, "Healthy": True},
+                          {"Percent": 100, "PercentTotal": 100, "MemoryMiB": 1024, "MemoryMiBTotal": 4096,
+                           "MemoryPool": 0, "GPU": 0, "Partition": 1, "Healthy": False}]}}
+    out = top.render(st).splitlines()
+    assert "50%" in out[1] and "(pool)" not in out[1]
+    assert "(pool)" in out[2] and "UNHEALTHY" in out[2]          # second member of one HBM pool
+    assert "1.5 device-equivalents free, 33.3% of the free compute" in out[-1]
