@@ -257,7 +257,7 @@ class NodeAgent:
             await self.server.stop(grace=1.0)
 
 
-def main(argv: list[str] | None = None) -> int:
+def build_parser():
     import argparse
 
     ap = argparse.ArgumentParser(prog="nanogpu-agent", description="MI355X node agent for nano-gpu-scheduler")
@@ -274,7 +274,11 @@ def main(argv: list[str] | None = None) -> int:
                     help="run the HIP self-test (HBM copy + MFMA tile) on every device at start-up")
     ap.add_argument("--metrics-port", type=int, default=9410,
                     help="device / pod / container GPU metrics on :PORT/metrics (0: off)")
-    a = ap.parse_args(argv)
+    return ap
+
+
+def main(argv: list[str] | None = None) -> int:
+    a = build_parser().parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     topo, host = discover(a.sysfs_root, not a.no_amdsmi)
     if a.calibrate:

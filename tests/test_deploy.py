@@ -1,0 +1,61 @@
+"""deploy/ manifests agree with the code they run: every argument is one the CLI accepts, the
+policy ConfigMap loads, and the KubeSchedulerConfiguration's verbs and managed resources are
+the routes and resource names the extender serves (reference deploy/*.yaml, README.md:43-58)."""
+import json
+from pathlib import Path
+
+import yaml
+
+from nanogpu import cli
+from nanogpu import types as T
+from nanogpu.agent import node as agent
+from nanogpu.config.policy import parse_policy
+from nanogpu.extender.server import Router
+
+DEPLOY = Path(__file__).resolve().parent.parent / "deploy"
+
+
+def _docs(name):
+    return [d for d in yaml.safe_load_all((DEPLOY / name).read_text()) if d]
+
+
+def _container(name, kind):
+    obj = next(d for d in _docs(name) if d["kind"] == kind)
+    return obj["spec"]["template"]["spec"]["containers"][0]
+
+
+def test_extender_deployment_args_parse():
+    c = _container("nano-gpu-scheduler-amd.yaml", "Deployment")
+    assert c["command"][-2:] == ["-m", "nanogpu"]
+    cfg = cli.parse(c["args"])
+    assert cfg.priority == "binpack" and cfg.workers == 4 and cfg.leader_elect
+    assert cfg.frontend_threads == 2 and cfg.busy_poll_us == 20 and cfg.cpu_affinity == "auto"
+    ports = {p["containerPort"] for p in c.get("ports", [])}
+    env = {e["name"]: e.get("value") for e in c.get("env", [])}
+    assert int(env.get("PORT", 39999)) in ports or not ports
+
+
+def test_agent_daemonset_args_parse():
+    c = _container("nano-gpu-agent-amd.yaml", "DaemonSet")
+    assert c["command"][:3] == ["python3", "-m", "nanogpu.agent"]
+    a = agent.build_parser().parse_args(c["command"][3:] + (c.get("args") or []))
+    assert a.selftest and a.calibrate and a.metrics_port == 9410
+
+
+def test_policy_configmap_loads():
+    cm = next(d for d in _docs("policy-configmap.yaml") if d["kind"] == "ConfigMap")
+    spec = parse_policy(cm["data"]["policy.yaml"])
+    assert {name for name, _ in spec.metrics} >= {"gpu_core_usage_avg", "gpu_memory_usage_avg"}
+
+
+def test_scheduler_config_matches_the_served_routes():
+    ext = _docs("kube-scheduler-config.yaml")[0]["extenders"][0]
+    assert ext["nodeCacheCapable"] is True
+    prefix = "/" + ext["urlPrefix"].split("/", 3)[3]
+    paths = {path for (method, path) in Router(None).table if method == "POST"}
+    for verb in ("filterVerb", "prioritizeVerb", "bindVerb", "preemptVerb"):
+        path = f"{prefix}/{ext[verb]}"
+        assert path in paths, path
+    assert {r["name"] for r in ext["managedResources"]} == {T.RESOURCE_GPU_PERCENT, T.RESOURCE_GPU_MEMORY}
+    legacy = json.loads((DEPLOY / "scheduler-policy.json").read_text())["extenders"][0]
+    assert legacy["filterVerb"] == ext["filterVerb"] and legacy["bindVerb"] == ext["bindVerb"]
