@@ -109,11 +109,18 @@ Ledger::Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, b
     if (fd_ < 0) {
       fd_ = open(path.c_str(), O_RDWR);
       if (fd_ < 0) throw std::runtime_error("ledger: cannot open " + path);
-      // wait for the creator to size the file
-      for (int i = 0; i < 2000; ++i) {
+      // wait for the creator to size the file; a file that stays short (another geometry, or a
+      // creator that died before ftruncate) is refused here: touching a page past its end
+      // would raise SIGBUS
+      bool sized = false;
+      for (int i = 0; i < 2000 && !sized; ++i) {
         struct stat st;
-        if (fstat(fd_, &st) == 0 && static_cast<size_t>(st.st_size) >= bytes_) break;
-        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        sized = fstat(fd_, &st) == 0 && static_cast<size_t>(st.st_size) >= bytes_;
+        if (!sized) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      }
+      if (!sized) {
+        close(fd_);
+        throw std::runtime_error("ledger: shared region is smaller than this geometry needs: " + path);
       }
     }
     void* p = mmap(nullptr, bytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd_, 0);

@@ -100,3 +100,27 @@ def test_two_workers_share_one_ledger():
                 pass
 
     asyncio.run(main())
+
+
+def test_ledger_refuses_a_short_or_foreign_region(tmp_path):
+    """Attaching to a /dev/shm file of another geometry, another layout version, or one whose
+    creator died before sizing it must fail cleanly (not SIGBUS past the end of the file)."""
+    import pytest
+
+    from nanogpu import _native as N
+
+    short = f"/dev/shm/nanogpu-test-short-{os.getpid()}"
+    other = f"/dev/shm/nanogpu-test-other-{os.getpid()}"
+    try:
+        open(short, "wb").close()                       # creator died before ftruncate
+        with pytest.raises(RuntimeError, match="smaller"):
+            N.Ledger(short, 16, 64, False)
+        a = N.Ledger(other, 16, 64, True)               # live region, other geometry
+        with pytest.raises(RuntimeError):
+            N.Ledger(other, 32, 64, False)
+        b = N.Ledger(other, 16, 64, False)              # same geometry attaches
+        del a, b
+    finally:
+        for p in (short, other):
+            if os.path.exists(p):
+                os.unlink(p)
