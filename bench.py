@@ -59,6 +59,9 @@ def parse_args():
     ap.add_argument("--policy", default="binpack")
     ap.add_argument("--compat", action="store_true", help="reference (Go 1.16) placement semantics")
     ap.add_argument("--api-rtt-ms", type=float, default=0.0, help="modelled API-server round trip")
+    ap.add_argument("--rtt-variant-ms", type=float, default=2.0,
+                    help="after the timed steps, a second pass with this API round trip (0: none)")
+    ap.add_argument("--rtt-variant-steps", type=int, default=3)
     ap.add_argument("--inflight-binds", type=int, default=64)
     ap.add_argument("--no-gpu", action="store_true", help="skip GPU discovery (CPU-only rehearsal)")
     ap.add_argument("--json-out", default="")
@@ -254,33 +257,41 @@ def burst(rank: int, world: int, total: int, step: int, seed: int) -> list[dict]
 
 
 def driver_main(conn) -> None:
-    """kube-scheduler stand-in in its own process (as in a real cluster): receives the
-    extender's address once, then for every step schedules that step's pods (already
-    created in the API server by the main process) and returns the driver stats. The
-    scheduling cycle is serial on a blocking connection; binds run on a thread pool."""
+    """kube-scheduler stand-in in its own process (as in a real cluster): for each pass of
+    the bench it receives the extender's address and the pass's steps, builds their pods,
+    then for every step schedules that step's pods (already created in the API server by the
+    main process) and returns the driver stats. The scheduling cycle is serial on a blocking
+    connection; binds run on a thread pool."""
     from nanogpu.sim.driver import NativeSchedulerDriver, ThreadedSchedulerDriver
 
-    cfg = conn.recv()
-    cls = ThreadedSchedulerDriver if cfg.get("driver") == "python" else NativeSchedulerDriver
+    st = {"cfg": None, "work": {}, "session": None, "cls": NativeSchedulerDriver}
 
-    # the pods of every step, built before the clock starts (the main process does the same)
-    native = cls is NativeSchedulerDriver
-    work = {}
-    for step in cfg["steps"]:
-        pods = burst(cfg["rank"], cfg["world"], cfg["pods"], step, 7)
-        work[step] = NativeSchedulerDriver.prepare(pods) if native else pods
-    conn.send("ready")
-    session = None
-    if native:
-        from nanogpu.native import core
+    def configure(cfg: dict) -> None:
+        cls = ThreadedSchedulerDriver if cfg.get("driver") == "python" else NativeSchedulerDriver
+        native = cls is NativeSchedulerDriver
+        # the pods of every step, built before the clock starts (the main process does the same)
+        work = {}
+        for step in cfg["steps"]:
+            pods = burst(cfg["rank"], cfg["world"], cfg["pods"], step, 7)
+            work[step] = NativeSchedulerDriver.prepare(pods) if native else pods
+        session = None
+        if native:
+            from nanogpu.native import core
 
-        session = core().SchedulerSession()   # keep-alive connections across steps
+            session = core().SchedulerSession()   # keep-alive connections across the pass's steps
+        st.update(cfg=cfg, work=work, session=session, cls=cls)
+        conn.send("ready")
 
     def serve() -> None:
         while True:
             msg = conn.recv()
+            if isinstance(msg, dict):
+                configure(msg)
+                continue
             if msg[0] != "step":
                 break
+            cfg, work, session, cls = st["cfg"], st["work"], st["session"], st["cls"]
+            native = cls is NativeSchedulerDriver
             step = msg[1]
             # native: connections of the epoll binder (a bind leaves as soon as its host is
             # chosen, as kube-scheduler's per-pod bind goroutines); Python: pool threads
@@ -326,7 +337,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
     caps = node_capacities(nodes)
     api = InProcKube(store)
     pod_ctrl = rt.controllers[-1]
-    results = {"steps": [], "frag": []}
+    results = {"steps": [], "frag": [], "client_bind_ms": [], "frontdoor_bind_ms": []}
 
     # synthetic pod objects are generated up front (client-side data, not scheduler work);
     # their creation in the API server, scheduling, deletion and release are all timed
@@ -384,7 +395,11 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
         await pod_ctrl.queue.drain(5.0)
         phases = {"create_ms": 1e3 * tc, "schedule_ms": 1e3 * summary["span_s"],
                   "release_ms": 1e3 * (time.perf_counter() - ts)}
+        walls = rt.native.fe.take_bind_wall() if rt.native is not None else []
+        client_ms = summary.pop("bind_ms_all", [])
         if timed:
+            results["client_bind_ms"].extend(client_ms)
+            results["frontdoor_bind_ms"].extend(1e3 * x for x in walls)
             diag = {"t0": round(t_step0, 4), "t1": round(time.perf_counter(), 4)}
             diag.update({k: round(summary.get(k, 0.0), 2) for k in ("cycle_max_ms", "cycle_sum_ms", "cycle_wire_ms", "bind_max_ms")})
             diag["unschedulable"] = summary.get("unschedulable_attempts", 0)
@@ -458,6 +473,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
     n_sched = max(1, sum(st["scheduled"] for st in results["steps"]))
     results["cpu_us_per_pod"] = 1e6 * (time.process_time() - cpu0) / n_sched
     results["loop_cpu_us_per_pod"] = 1e6 * (time.thread_time() - loop_cpu0) / n_sched
+    # the Python part of each bind (API writes + commit): a sub-phase of the wall time
     binds = sorted(s["dur_ms"] for s in rt.tracer.dump(10 ** 9, "bind") if s["ok"])
     results["elapsed_s"] = elapsed
     results["bind_ms"] = binds
@@ -515,17 +531,19 @@ def main() -> int:
     d = Dist(args.gpus)
     d.init(use_gpu=not args.no_gpu)
     topo, gpu_info = node_template(d, args)
-    # one shared ledger for all workers of this job
-    tag = os.environ.get("MASTER_PORT", str(os.getpid()))
-    ledger_path = d.bcast_obj(f"/dev/shm/nanogpu-bench-{tag}-{int(time.time())}" if d.rank == 0 else None)
-    from nanogpu.native import core
-
-    led = None
-    if d.rank == 0:
-        led = core().Ledger(ledger_path, max(1024, args.nodes), max(65536, 4 * args.pods), True)
-    d.barrier()
+    variant = None
     try:
-        res = asyncio.run(run_rank(d, args, topo, ledger_path, conn))
+        res = run_pass(d, args, topo, conn, "main")
+        if args.rtt_variant_ms > 0:
+            # the same burst with a modelled API-server round trip on every API call (untimed
+            # for `value`; its own clock): what the pods/s above excludes
+            v_args = argparse.Namespace(**{**vars(args), "api_rtt_ms": args.rtt_variant_ms,
+                                           "steps": args.rtt_variant_steps, "warmup": 1, "profile_out": "",
+                                           "stall_trace": ""})
+            try:
+                variant = summarize(d, v_args, run_pass(d, v_args, topo, conn, "rtt"))
+            except Exception as e:   # the headline result stands; say what failed
+                variant = {"error": f"{type(e).__name__}: {e}"}
     finally:
         if drv_proc is not None:
             try:
@@ -535,27 +553,12 @@ def main() -> int:
             drv_proc.join(10)
             if drv_proc.is_alive():
                 drv_proc.terminate()
-        d.barrier()
-        if d.rank == 0:
-            try:
-                os.unlink(ledger_path)
-            except OSError:
-                pass
-    elapsed = d.max(res["elapsed_s"])
-    all_binds = [b for r in d.gather_obj(res["bind_ms"]) for b in r]
-    scheduled = sum(d.gather_obj(res["scheduled"]))
-    failed = sum(d.gather_obj(res["failed"]))
-    bind_errors = sum(d.gather_obj(res["bind_errors"]))
-    del led
+    out = summarize(d, args, res)
     if d.rank == 0:
-        all_binds.sort()
-        p50 = statistics.median(all_binds) if all_binds else None
-        p99 = all_binds[min(len(all_binds) - 1, int(0.99 * len(all_binds)))] if all_binds else None
         fr = res["frag"]
-        value = scheduled / elapsed if elapsed > 0 else 0.0
         line = {
-            "metric": METRIC, "value": round(value, 2), "unit": "pods/s", "n_gpus": d.world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / max(1, args.steps), 3),
+            "metric": METRIC, "value": out["value"], "unit": "pods/s", "n_gpus": d.world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": out["ms_per_step"],
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "n/a",
             "data": "synthetic (pod bursts; simulated nodes cloned from the discovered MI355X)",
             "config": {"model": f"nano-gpu-scheduler extender ({args.policy}{', compat' if args.compat else ''})",
@@ -563,14 +566,24 @@ def main() -> int:
                        "parallelism": f"{d.world} extender worker(s), shared native ledger",
                        "cluster": f"{args.nodes} nodes x {args.gpus_per_node} MI355X ({args.partition})",
                        "api_rtt_ms": args.api_rtt_ms,
+                       # value is the extender's throughput: the API server is an in-process
+                       # store per rank with no round trip (see value_rtt*ms for a modelled one)
+                       "api_server": "in-process store per rank, extender-isolated",
                        "cpus_rank0": _cpulist(cpus),
                        "frontend": f"{args.frontend_threads} threads, busy-poll {args.busy_poll_us} us"},
-            "p50_bind_ms": round(p50, 4) if p50 is not None else None,
-            "p99_bind_ms": round(p99, 4) if p99 is not None else None,
+            # POST /scheduler/bind wall time as kube-scheduler's stand-in sees it (request
+            # written -> reply read), over every bind of the timed steps on all ranks
+            "p50_bind_ms": out["p50_bind_ms"], "p99_bind_ms": out["p99_bind_ms"],
+            # extender side of the same binds: request bytes read -> reply handed to the kernel
+            "p50_bind_frontdoor_ms": out["p50_bind_frontdoor_ms"],
+            "p99_bind_frontdoor_ms": out["p99_bind_frontdoor_ms"],
+            # sub-phase: the Python half (API writes + ledger commit)
+            "p50_bind_python_ms": out["p50_bind_python_ms"],
             "frag_pct": round(statistics.mean(f["frag_pct"] for f in fr), 3) if fr else None,
             "frag_hbm_pct": round(statistics.mean(f["frag_mib"] for f in fr), 3) if fr else None,
             "stranded_pct": round(statistics.mean(f["stranded_pct"] for f in fr), 3) if fr else None,
-            "scheduled": scheduled, "failed": failed, "bind_retries": bind_errors, "gpu": gpu_info,
+            "scheduled": out["scheduled"], "failed": out["failed"], "bind_retries": out["bind_errors"],
+            "gpu": gpu_info,
             "native_verb_mean_us": res.get("native"),
             "phase_ms_per_step_rank0": res.get("phase_ms"),
             "schedule_ms_each_step_rank0": res.get("schedule_ms_steps"),
@@ -582,11 +595,84 @@ def main() -> int:
             # of which the Python event-loop thread (binds' API writes, informer, controller)
             "extender_loop_cpu_us_per_pod_rank0": round(res.get("loop_cpu_us_per_pod", 0.0), 1),
         }
+        line.update(reference_model_frag(args, topo))
+        if variant is not None:
+            tag = f"rtt{args.rtt_variant_ms:g}ms"
+            if "error" in variant:
+                line[f"value_{tag}"] = None
+                line[f"error_{tag}"] = variant["error"]
+            else:
+                line[f"value_{tag}"] = variant["value"]
+                line[f"p50_bind_ms_{tag}"] = variant["p50_bind_ms"]
+                line[f"p99_bind_ms_{tag}"] = variant["p99_bind_ms"]
+                line[f"steps_{tag}"] = args.rtt_variant_steps
         print(json.dumps(line), flush=True)
         if args.json_out:
             Path(args.json_out).write_text(json.dumps(line, indent=1))
     d.close()
     return 0
+
+
+def run_pass(d: Dist, args, topo, conn, tag: str) -> dict:
+    """One bench pass on a fresh shared ledger (all ranks)."""
+    ledger_path = d.bcast_obj(f"/dev/shm/nanogpu-bench-{os.environ.get('MASTER_PORT', os.getpid())}-{tag}-"
+                              f"{int(time.time())}" if d.rank == 0 else None)
+    from nanogpu.native import core
+
+    led = None
+    if d.rank == 0:
+        led = core().Ledger(ledger_path, max(1024, args.nodes), max(65536, 4 * args.pods), True)
+    d.barrier()
+    try:
+        return asyncio.run(run_rank(d, args, topo, ledger_path, conn))
+    finally:
+        d.barrier()
+        del led
+        if d.rank == 0:
+            try:
+                os.unlink(ledger_path)
+            except OSError:
+                pass
+
+
+def _pct(a: list, q: float):
+    return round(a[min(len(a) - 1, int(q * len(a)))], 4) if a else None
+
+
+def summarize(d: Dist, args, res: dict) -> dict:
+    """Whole-job numbers of one pass (collective: every rank calls it)."""
+    elapsed = d.max(res["elapsed_s"])
+    client = sorted(b for r in d.gather_obj(res["client_bind_ms"]) for b in r)
+    front = sorted(b for r in d.gather_obj(res["frontdoor_bind_ms"]) for b in r)
+    py = sorted(b for r in d.gather_obj(res["bind_ms"]) for b in r)
+    scheduled = sum(d.gather_obj(res["scheduled"]))
+    return {"value": round(scheduled / elapsed, 2) if elapsed > 0 else 0.0,
+            "ms_per_step": round(1e3 * elapsed / max(1, args.steps), 3),
+            "p50_bind_ms": round(statistics.median(client), 4) if client else None,
+            "p99_bind_ms": _pct(client, 0.99),
+            "p50_bind_frontdoor_ms": round(statistics.median(front), 4) if front else None,
+            "p99_bind_frontdoor_ms": _pct(front, 0.99),
+            "p50_bind_python_ms": round(statistics.median(py), 4) if py else None,
+            "scheduled": scheduled, "failed": sum(d.gather_obj(res["failed"])),
+            "bind_errors": sum(d.gather_obj(res["bind_errors"]))}
+
+
+def reference_model_frag(args, topo) -> dict:
+    """frag% of the reference algorithm (compat mode: the Go raters bit for bit) on the same
+    bursts, replayed offline through the same ledger (nanogpu.sim.fragsim) — the reference
+    publishes no number; this is its placement on this workload. Also the native replay, so
+    the live run's frag_pct can be checked against a serial replay."""
+    if args.partition != "SPX" or args.policy != "binpack" or args.compat:
+        return {"frag_pct_reference_model": None}
+    from nanogpu.sim import fragsim
+
+    hbm = topo.devices[0].hbm_mib if topo.devices else 288 * 1024
+    kw = dict(steps=args.steps, nodes=args.nodes, hbm_mib=hbm, pods=args.pods)
+    ref, nat = fragsim.headline(True, **kw), fragsim.headline(False, **kw)
+    return {"frag_pct_reference_model": ref["frag_pct"], "frag_hbm_pct_reference_model": ref["frag_hbm_pct"],
+            "stranded_pct_reference_model": ref["stranded_pct"], "frag_pct_native_replay": nat["frag_pct"],
+            "frag_reference_model_source": "offline serial replay of the timed bursts, reference binpack "
+                                           "(compat mode, bit-exact with rater.go) vs native binpack"}
 
 
 if __name__ == "__main__":

@@ -64,6 +64,8 @@ class Config:
     frontend_threads: int = 4
     busy_poll_us: int = 0                       # native workers spin this long after an event
     cpu_affinity: str = "none"                  # none | auto (one L3 domain per worker) | cpu list
+    request_sizes: list = field(default_factory=list)   # share sizes binpack's waste model fixes
+    learn_sizes: bool = True                    # ...plus the sizes the ledger sees requested
     gpu_node_selectors: list = field(default_factory=lambda: [T.AMD_GPU_NODE_LABEL, T.LEGACY_GPU_NODE_LABEL])
 
 
@@ -85,7 +87,8 @@ class Runtime:
             policy=cfg.priority, compat=cfg.compat, load_aware=cfg.is_load_schedule,
             topo_weight=cfg.topology_weight, seed=cfg.seed, ledger_path=cfg.ledger_path,
             max_nodes=cfg.max_nodes, max_pods=cfg.max_pods, track_hbm=cfg.track_hbm,
-            node_source=self._node_from_cache, score_normalize=cfg.score_normalize, nominate=cfg.nominate)
+            node_source=self._node_from_cache, score_normalize=cfg.score_normalize, nominate=cfg.nominate,
+            request_sizes=cfg.request_sizes, learn_sizes=cfg.learn_sizes)
         self.metrics = Metrics()
         self.tracer = Tracer()
         self.extender: Extender | None = None

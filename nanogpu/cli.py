@@ -44,6 +44,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--score-normalize", action="store_true", help="map scores to kube-scheduler's [0,10]")
     p.add_argument("--topology-weight", type=float, default=1.0, help="xGMI/partition term weight")
     p.add_argument("--no-hbm", action="store_true", help="ignore the nano-gpu/gpu-memory dimension")
+    p.add_argument("--request-sizes", default="",
+                   help="comma-separated share sizes (percent) binpack keeps holes fillable for, e.g. 10,25,50")
+    p.add_argument("--no-learn-sizes", action="store_true",
+                   help="binpack uses only --request-sizes, not the sizes it sees requested")
     p.add_argument("--workers", type=int, default=1, help="SO_REUSEPORT worker processes sharing one ledger")
     p.add_argument("--ledger-path", default="", help="/dev/shm path of the shared ledger")
     p.add_argument("--max-nodes", type=int, default=4096)
@@ -73,6 +77,16 @@ def build_parser() -> argparse.ArgumentParser:
     return p
 
 
+def _sizes(text: str) -> list[int]:
+    out = []
+    for part in filter(None, (x.strip() for x in text.split(","))):
+        v = int(part)
+        if not 1 <= v <= 100:
+            raise SystemExit(f"--request-sizes: {v} is not a percent of one device (1..100)")
+        out.append(v)
+    return out
+
+
 def parse(argv: list[str] | None = None) -> Config:
     a = build_parser().parse_args(argv)
     if a.priority not in T.POLICIES:
@@ -93,4 +107,4 @@ def parse(argv: list[str] | None = None) -> Config:
         fake_cluster=a.fake_cluster, fake_gpus_per_node=a.fake_gpus_per_node, fake_partition=a.fake_partition,
         seed=a.seed, frontend=a.frontend, frontend_threads=max(1, a.frontend_threads), busy_poll_us=a.busy_poll_us,
         leader_elect=a.leader_elect, lease_name=a.lease_name, lease_namespace=a.lease_namespace, identity=a.identity,
-        cpu_affinity=a.cpu_affinity)
+        cpu_affinity=a.cpu_affinity, request_sizes=_sizes(a.request_sizes), learn_sizes=not a.no_learn_sizes)

@@ -232,7 +232,9 @@ class DriverStats:
                 "cycle_max_ms": 1e3 * self.cycle_max_s,
                 "cycle_sum_ms": 1e3 * self.cycle_sum_s,
                 "cycle_wire_ms": 1e3 * self.cycle_wire_s,
-                "e2e_p50_ms": 1e3 * (statistics.median(self.e2e_latencies) if self.e2e_latencies else 0.0)}
+                "e2e_p50_ms": 1e3 * (statistics.median(self.e2e_latencies) if self.e2e_latencies else 0.0),
+                # every POST /scheduler/bind as the scheduler saw it (request written -> reply read)
+                "bind_ms_all": [round(1e3 * x, 4) for x in self.bind_latencies]}
 
 
 class SchedulerDriver:

@@ -1,0 +1,156 @@
+"""Offline placement-quality simulator: replays the bench / BASELINE-config pod streams
+through the native ledger (filter -> score -> arg-max with random tie-break -> reserve ->
+commit), with no HTTP, so a policy change can be judged on frag% in seconds.
+
+It models a serial kube-scheduler cycle that takes the extender's arg-max (what the bench
+stand-in does). The reference algorithm runs in compat mode (bit-exact with the Go raters,
+tests/test_parity.py) without the HBM dimension, as the reference has none.
+
+    python -m nanogpu.sim.fragsim                       # every scenario, native vs reference
+    python -m nanogpu.sim.fragsim --scenario headline
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import random
+import statistics
+import sys
+
+from nanogpu.native import core
+from nanogpu.topology.model import synthetic_mi355x, synthetic_sriov_guest
+
+N = core()
+POL = {"binpack": N.Policy.BINPACK, "spread": N.Policy.SPREAD}
+
+
+class Cluster:
+    def __init__(self, topo, n_nodes: int, compat: bool, track_hbm: bool, policy: str = "binpack", seed: int = 0):
+        self.L = N.Ledger("", max(64, n_nodes), 1 << 16, True)
+        self.ids = [self.L.upsert_node(f"n{i:03d}", topo.ledger_devices(track_hbm), topo.ledger_topo())
+                    for i in range(n_nodes)]
+        self.opts = N.Options(POL[policy], compat=compat)
+        self.track_hbm = track_hbm
+        self.rng = random.Random(seed)
+        self.live: dict[str, int] = {}
+        self.unsched = 0
+
+    def place(self, uid: str, demand: list) -> bool:
+        if not self.track_hbm:
+            demand = [(p, 0) for p, _ in demand]
+        rcs = self.L.filter(self.ids, demand, self.opts)
+        fit = [i for i, rc in zip(self.ids, rcs) if rc == 0]
+        if not fit:
+            self.unsched += 1
+            return False
+        if len(fit) == 1:
+            host = fit[0]
+        else:
+            scores = self.L.score(fit, demand, self.opts)
+            best = max(scores)
+            host = self.rng.choice([i for i, s in zip(fit, scores) if s == best])
+        rc, _ = self.L.reserve(host, uid, demand, self.opts)
+        assert rc == 0, rc
+        self.L.commit(uid)
+        self.live[uid] = host
+        return True
+
+    def delete(self, uid: str) -> None:
+        if self.live.pop(uid, None) is not None:
+            self.L.release(uid)
+
+    def frag(self, min_req: int) -> dict:
+        return self.L.frag(min_req)
+
+    def hbm_overcommit(self) -> int:
+        """MiB granted beyond a device's (or pool's) HBM, summed over the cluster."""
+        over = 0
+        for i in self.ids:
+            for d in self.L.snapshot(i)["devices"]:
+                over += max(0, -d["mib_free"])
+        return over
+
+
+def headline(compat: bool, steps: int = 20, nodes: int = 64, hbm_mib: int = 294_896, pods: int = 1000,
+             step0: int = 0, **_) -> dict:
+    """bench.py's workload: a 1000-pod burst of {10,25,50} % x {8,16,32,64} GiB on 64 SPX nodes,
+    frag measured at peak occupancy, then the burst is deleted (bench.burst's RNG stream).
+    The reference model sees the HBM requests too (the bench runs it with --compat)."""
+    topo = synthetic_mi355x(8, "SPX", hbm_mib=hbm_mib)
+    c = Cluster(topo, nodes, compat, track_hbm=True, seed=1)
+    out = []
+    for step in range(step0, step0 + steps):
+        rng = random.Random(7 * 1000003 + step)
+        uids = []
+        for i in range(pods):
+            pct, gib = rng.choice((10, 25, 50)), rng.choice((8, 16, 32, 64))
+            uid = f"s{step}-{i}"
+            if c.place(uid, [(pct, gib * 1024)]):
+                uids.append(uid)
+        out.append(c.frag(10))
+        for u in uids:
+            c.delete(u)
+    return summarize(out, c)
+
+
+def config5(compat: bool, rounds: int = 5, pods_n: int = 1000, nodes_n: int = 8, sriov: bool = False,
+            reps: int = 10, **_) -> dict:
+    """BASELINE config 5: CPX nodes (or SR-IOV guests), 1000-pod create/delete churn, binpack.
+    The reference model has no HBM dimension (as in nanogpu.sim.configs)."""
+    frs, unsched = [], 0
+    for rep in range(reps):
+        if sriov:
+            topo, n = synthetic_sriov_guest(4), nodes_n * 2
+        else:
+            topo, n = synthetic_mi355x(8, "CPX"), nodes_n
+        c = Cluster(topo, n, compat, track_hbm=not compat, seed=rep)
+        rng = random.Random(5 + rep)
+        live: list[str] = []
+        for r in range(rounds):
+            prng = random.Random(100 + r + 1000 * rep)
+            for i in range(pods_n // rounds):
+                uid = f"r{rep}-{r}-{i}"
+                if c.place(uid, [(prng.choice((10, 25, 50, 100)), prng.choice((0, 8, 16, 32)) * 1024)]):
+                    live.append(uid)
+            frs.append(c.frag(10))
+            rng.shuffle(live)
+            half, live = live[: len(live) // 2], live[len(live) // 2:]
+            for u in half:
+                c.delete(u)
+        unsched += c.unsched
+    return summarize(frs, None, unsched)
+
+
+def summarize(frs: list[dict], c: Cluster | None, unsched: int | None = None) -> dict:
+    return {"frag_pct": round(statistics.mean(f["frag_pct"] for f in frs), 3),
+            "frag_hbm_pct": round(statistics.mean(f["frag_mib"] for f in frs), 3),
+            "stranded_pct": round(statistics.mean(f["stranded_pct"] for f in frs), 3),
+            "unschedulable": c.unsched if c is not None else unsched,
+            "hbm_overcommit_mib": c.hbm_overcommit() if c is not None else 0}
+
+
+SCENARIOS = {
+    "headline": headline,
+    "config5": config5,
+    "config5_sriov": lambda compat, **kw: config5(compat, sriov=True, pods_n=125, **kw),
+}
+
+
+def run(names=None) -> dict:
+    res = {}
+    for name in names or SCENARIOS:
+        fn = SCENARIOS[name]
+        res[name] = {"native": fn(False), "reference_model": fn(True)}
+    return res
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scenario", action="append", choices=sorted(SCENARIOS))
+    args = ap.parse_args(argv)
+    print(json.dumps(run(args.scenario), indent=1))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -58,7 +58,8 @@ class ClusterState:
                  load_aware: bool = False, topo_weight: float = 1.0, seed: int = 0,
                  ledger_path: str = "", max_nodes: int = 4096, max_pods: int = 131072,
                  track_hbm: bool = True, node_source: Callable[[str], dict | None] | None = None,
-                 score_normalize: bool = False, nominate: bool = True):
+                 score_normalize: bool = False, nominate: bool = True, request_sizes: list[int] | None = None,
+                 learn_sizes: bool = True):
         self.ledger = N.Ledger(ledger_path, max_nodes, max_pods, True)
         self._nominate = bool(nominate)
         self.track_hbm = track_hbm
@@ -69,7 +70,8 @@ class ClusterState:
         self._nodes_mu = threading.Lock()
         self._released: OrderedDict[str, None] = OrderedDict()   # reference ReleasedPodMap
         self._released_cap = 65536
-        self.set_policy(policy, compat=compat, load_aware=load_aware, topo_weight=topo_weight, seed=seed)
+        self.set_policy(policy, compat=compat, load_aware=load_aware, topo_weight=topo_weight, seed=seed,
+                        request_sizes=request_sizes or [], learn_sizes=learn_sizes)
 
     # ------------------------------------------------------------------ policy
     def add_listener(self, fn: Callable[[], None]) -> None:
@@ -105,7 +107,10 @@ class ClusterState:
         self._changed()
 
     def set_policy(self, policy: str, compat: bool | None = None, load_aware: bool | None = None,
-                   topo_weight: float | None = None, seed: int | None = None) -> None:
+                   topo_weight: float | None = None, seed: int | None = None,
+                   request_sizes: list[int] | None = None, learn_sizes: bool | None = None) -> None:
+        """`request_sizes` fixes share sizes (percent) binpack treats as common; with
+        `learn_sizes` the ledger adds the sizes it sees requested (alloc.h SizeSet)."""
         if policy not in POLICY_ENUM:
             raise ValueError(f"Priority algorithm {policy} is not supported")
         old = getattr(self, "options", None)
@@ -115,7 +120,9 @@ class ClusterState:
             compat=bool(compat if compat is not None else (old.compat if old else False)),
             load_aware=bool(load_aware if load_aware is not None else (old.load_aware if old else False)),
             topo_weight=float(topo_weight if topo_weight is not None else (old.topo_weight if old else 1.0)),
-            seed=int(seed if seed is not None else (old.seed if old else 0)))
+            seed=int(seed if seed is not None else (old.seed if old else 0)),
+            request_sizes=list(request_sizes if request_sizes is not None else (old.request_sizes if old else [])),
+            learn_sizes=bool(learn_sizes if learn_sizes is not None else (old.learn_sizes if old else True)))
         self._changed()
 
     # ------------------------------------------------------------------ nodes

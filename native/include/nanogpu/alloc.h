@@ -29,6 +29,7 @@ constexpr int kMaxPlanIdx = 64;      // device indices per pod plan
 constexpr int kNotNeedGPU = -1;      // reference NotNeedGPU, allocate.go:15
 constexpr int kLoadTotal = 2;        // reference LoadTotal, allocate.go:16
 constexpr int kPercentPerDevice = 100;
+constexpr int kWasteSlots = kPercentPerDevice + 1;
 
 enum class Policy : int32_t { kBinpack = 0, kSpread = 1, kRandom = 2, kFirstFit = 3 };
 
@@ -104,12 +105,36 @@ struct Plan {
   int16_t idx[kMaxPlanIdx];           // device indices; a single -1 for "no GPU"
 };
 
+// Request-size model of native binpack. A hole of h percent left on a device is only as
+// useful as the share requests that can still fill it: with {10, 25, 50} % requests a 5 %
+// hole is dead and a 15 % hole ends as 5 % whatever arrives. waste[h] = h minus the largest
+// sum of common request sizes that fits in h (unbounded knapsack over `sizes`), so binpack
+// avoids placements that turn a fillable hole into a dead one (a 10 % share into a 25 % hole,
+// where the 25 % hole would have paired with the next 25 % request). `sizes` is a 101-bit set
+// (bit s: s % requests are common); the ledger learns it from the requests it sees
+// (Ledger::note_request) unless fixed by the operator (--request-sizes).
+struct SizeSet {
+  uint64_t bits[2] = {0, 0};
+  bool empty() const { return (bits[0] | bits[1]) == 0; }
+  bool has(int s) const { return s >= 0 && s < 128 && ((bits[s >> 6] >> (s & 63)) & 1u); }
+  void add(int s) {
+    if (s > 0 && s <= kPercentPerDevice) bits[s >> 6] |= 1ULL << (s & 63);
+  }
+  bool operator==(const SizeSet& o) const { return bits[0] == o.bits[0] && bits[1] == o.bits[1]; }
+};
+
 struct Options {
   Policy policy = Policy::kBinpack;
   int32_t compat = 0;        // 1 => reproduce the reference (Go 1.16) bit for bit
   int32_t load_aware = 0;    // reference --isLoadSchedule
   float topo_weight = 1.0f;  // weight of the xGMI/partition term in native mode
   uint64_t seed = 0;         // random policy seed (mixed with the demand hash)
+  int32_t learn_sizes = 1;   // native binpack: add the ledger's learned request sizes
+  int32_t pad = 0;
+  SizeSet sizes;             // request sizes in force (fixed ones, plus learned ones)
+  uint8_t waste[kWasteSlots] = {};   // derived from `sizes` by set_sizes()
+  void set_sizes(const SizeSet& s);
+  bool waste_aware() const { return !sizes.empty(); }
   uint64_t hash() const;
 };
 

@@ -116,6 +116,11 @@ class Frontend {
   std::atomic<uint64_t> phase_max_ns[7] = {};
   void reset_max();
   size_t pod_cache_size() const;
+  // Extender-side wall time of each POST /scheduler/bind answered since the last call: from
+  // the first request bytes read to the response handed to the kernel (BASELINE's "p50 bind
+  // latency"). Bounded at kMaxWallSamples between calls.
+  std::vector<uint64_t> take_bind_wall();
+  static constexpr size_t kMaxWallSamples = 1u << 20;
 
  private:
   struct Conn;
@@ -131,6 +136,7 @@ class Frontend {
   void close_conn(Worker* w, Conn* c);
   void put_pod(std::string_view uid, CachedPod pod);
   void prepare_bind(std::string_view body, PyRequest* r);
+  void note_bind_wall(uint64_t ns);
 
   std::shared_ptr<Ledger> ledger_;
   int port_ = 0;
@@ -147,6 +153,9 @@ class Frontend {
 
   std::mutex py_mu_;
   std::deque<PyRequest> py_q_;
+
+  std::mutex wall_mu_;
+  std::vector<uint64_t> bind_wall_ns_;
 
   mutable std::mutex pod_mu_;
   std::unordered_map<std::string, CachedPod> pods_;

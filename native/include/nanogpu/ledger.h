@@ -77,6 +77,11 @@ struct LedgerHeader {
   pthread_mutex_t registry_mu;
   alignas(64) std::atomic<uint64_t> epoch;      // bumps on every mutation anywhere
   alignas(64) std::atomic<int64_t> n_pods;
+  // learned request-size mix (Ledger::note_request): decayed counts of share sizes and the
+  // set of the common ones, which native binpack's waste model uses (alloc.h SizeSet)
+  alignas(64) std::atomic<uint32_t> size_total;
+  std::atomic<uint64_t> size_bits[2];
+  std::atomic<uint32_t> size_hist[kWasteSlots];
   PaddedMutex shard_mu[kPodShards];
   int32_t shard_live[kPodShards];   // guarded by shard_mu[s]
   int32_t shard_tomb[kPodShards];
@@ -163,6 +168,14 @@ class Ledger {
   int32_t set_health(int32_t id, int dev, bool healthy);
 
   FragStats frag(int32_t min_request) const;
+
+  // Request-size learning: every new reservation/allocation counts its share sizes; a size
+  // is common once it is >= 2 % of the decayed count (dropped below 1 %).
+  void note_request(const Demand& d);
+  SizeSet learned_sizes() const;
+  // The options a placement runs with: native binpack gets the request-size set (fixed |
+  // learned | this demand's sizes) and its waste table; everything else is unchanged.
+  Options resolve(const Options& o, const Demand& d) const;
 
   void clear_cache();
   size_t cache_size() const;

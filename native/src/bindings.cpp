@@ -161,6 +161,13 @@ Plan to_plan(const std::vector<std::vector<int>>& v) {
   return p;
 }
 
+std::vector<int> size_list(const SizeSet& s) {
+  std::vector<int> out;
+  for (int q = 1; q <= kPercentPerDevice; ++q)
+    if (s.has(q)) out.push_back(q);
+  return out;
+}
+
 py::dict frag_dict(const FragStats& s) {
   py::dict d;
   d["pct_free_total"] = s.pct_free_total;
@@ -218,17 +225,31 @@ PYBIND11_MODULE(_native, m) {
       .value("FIRSTFIT", Policy::kFirstFit);
 
   py::class_<Options>(m, "Options")
-      .def(py::init([](Policy p, bool compat, bool load_aware, float topo_weight, uint64_t seed) {
+      .def(py::init([](Policy p, bool compat, bool load_aware, float topo_weight, uint64_t seed,
+                       const std::vector<int>& request_sizes, bool learn_sizes) {
              Options o;
              o.policy = p;
              o.compat = compat ? 1 : 0;
              o.load_aware = load_aware ? 1 : 0;
              o.topo_weight = topo_weight;
              o.seed = seed;
+             o.learn_sizes = learn_sizes ? 1 : 0;
+             SizeSet ss;
+             for (int q : request_sizes) {
+               if (q <= 0 || q > kPercentPerDevice) throw py::value_error("request size must be 1..100");
+               ss.add(q);
+             }
+             o.set_sizes(ss);
              return o;
            }),
            py::arg("policy") = Policy::kBinpack, py::arg("compat") = false,
-           py::arg("load_aware") = false, py::arg("topo_weight") = 1.0f, py::arg("seed") = 0)
+           py::arg("load_aware") = false, py::arg("topo_weight") = 1.0f, py::arg("seed") = 0,
+           py::arg("request_sizes") = std::vector<int>{}, py::arg("learn_sizes") = true)
+      .def_property_readonly("request_sizes", [](const Options& o) { return size_list(o.sizes); })
+      .def_property_readonly("learn_sizes", [](const Options& o) { return o.learn_sizes != 0; })
+      .def_property_readonly("waste", [](const Options& o) {
+        return std::vector<int>(o.waste, o.waste + kWasteSlots);
+      })
       .def_property_readonly("policy", [](const Options& o) { return o.policy; })
       .def_property_readonly("compat", [](const Options& o) { return o.compat != 0; })
       .def_property_readonly("load_aware", [](const Options& o) { return o.load_aware != 0; })
@@ -460,6 +481,9 @@ PYBIND11_MODULE(_native, m) {
       .def("set_health", &Ledger::set_health)
       .def("frag", [](const Ledger& l, int32_t min_request) { return frag_dict(l.frag(min_request)); },
            py::arg("min_request") = 0)
+      .def("learned_sizes", [](const Ledger& l) { return size_list(l.learned_sizes()); },
+           "share sizes (percent) the ledger has learned are common (native binpack's waste model)")
+      .def("note_request", [](Ledger& l, const py::sequence& demand) { l.note_request(to_demand(demand)); })
       .def("clear_cache", &Ledger::clear_cache)
       .def_property_readonly("cache_size", &Ledger::cache_size);
 
@@ -533,6 +557,13 @@ PYBIND11_MODULE(_native, m) {
       .def("flush", &Frontend::wake_workers, "wake the workers holding responses queued with notify=False")
       .def("stop", &Frontend::stop, py::call_guard<py::gil_scoped_release>())
       .def("pod_cache_size", &Frontend::pod_cache_size)
+      .def("take_bind_wall", [](Frontend& f) {
+             std::vector<uint64_t> ns = f.take_bind_wall();
+             std::vector<double> s(ns.size());
+             for (size_t i = 0; i < ns.size(); ++i) s[i] = static_cast<double>(ns[i]) * 1e-9;
+             return s;
+           },
+           "seconds from request read to response written, per bind since the last call")
       .def("stats", [](Frontend& f) {
         auto one = [](const VerbStats& s) {
           py::dict d;

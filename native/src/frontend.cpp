@@ -224,6 +224,18 @@ void VerbStats::observe(uint64_t ns) {
   atomic_max(&max_ns, ns);
 }
 
+void Frontend::note_bind_wall(uint64_t ns) {
+  std::lock_guard<std::mutex> g(wall_mu_);
+  if (bind_wall_ns_.size() < kMaxWallSamples) bind_wall_ns_.push_back(ns);
+}
+
+std::vector<uint64_t> Frontend::take_bind_wall() {
+  std::lock_guard<std::mutex> g(wall_mu_);
+  std::vector<uint64_t> out;
+  out.swap(bind_wall_ns_);
+  return out;
+}
+
 void Frontend::reset_max() {
   for (VerbStats* v : {&filter_stats, &prio_stats, &py_stats, &bind_stats}) v->max_ns.store(0);
   loop_max_ns.store(0);
@@ -247,6 +259,9 @@ struct Frontend::Conn {
   bool waiting = false;      // a request is with Python; later requests wait their turn
   bool close_after = false;
   bool want_out = false;
+  bool bind_waiting = false; // the request with Python is a bind (its wall time is recorded)
+  uint64_t t_in_ns = 0;      // first bytes of the request being parsed arrived
+  uint64_t t_req_ns = 0;     // ... of the request now with Python
 };
 
 struct Frontend::Worker {
@@ -527,6 +542,10 @@ void Frontend::run(Worker* w) {
           c->out += m.second;
           c->waiting = false;
           flush(w, c);
+          if (c->bind_waiting) {   // response handed to the kernel: the extender-side wall time
+            c->bind_waiting = false;
+            note_bind_wall(now_ns() - c->t_req_ns);
+          }
           if (w->conns.count(m.first)) process(w, c);
         }
       } else {
@@ -571,6 +590,7 @@ bool Frontend::read_in(Worker* w, Conn* c, bool* eof) {
   for (;;) {
     const ssize_t r = recv(c->fd, buf, sizeof(buf), 0);
     if (r > 0) {
+      if (c->in.empty()) c->t_in_ns = now_ns();
       c->in.append(buf, static_cast<size_t>(r));
       if (c->in.size() > kMaxBody + kMaxHeader) {
         close_conn(w, c);
@@ -698,6 +718,9 @@ void Frontend::defer(Worker* w, Conn* c, std::string method, std::string path, s
   r.body = std::move(body);
   r.t_arrival = now_s();
   c->waiting = true;
+  c->bind_waiting = r.path == "/scheduler/bind";
+  c->t_req_ns = c->t_in_ns ? c->t_in_ns : now_ns();
+  c->t_in_ns = c->in.empty() ? 0 : now_ns();   // pipelined bytes behind it: their clock starts now
   py_stats.deferred.fetch_add(1, std::memory_order_relaxed);
   PhaseTimer pt{&phase_max_ns[6]};
   {

@@ -18,7 +18,7 @@
 namespace nanogpu {
 
 static constexpr uint64_t kMagic = 0x4e414e4f47505531ULL;  // "NANOGPU1"
-static constexpr uint32_t kVersion = 5;  // 4: Device gained HBM pools; 5: cache-line layout
+static constexpr uint32_t kVersion = 6;  // 4: HBM pools; 5: cache-line layout; 6: request-size mix
 
 static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -142,6 +142,10 @@ Ledger::Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, b
     hdr_->epoch.store(1);
     hdr_->n_pods.store(0);
     hdr_->attached.store(0);
+    hdr_->size_total.store(0);
+    hdr_->size_bits[0].store(0);
+    hdr_->size_bits[1].store(0);
+    for (auto& c : hdr_->size_hist) c.store(0);
     init_mutex(&hdr_->registry_mu);
     for (int s = 0; s < kPodShards; ++s) {
       init_mutex(&hdr_->shard_mu[s].m);
@@ -489,8 +493,9 @@ bool Ledger::node_named(int32_t id, std::string_view name) const {
          n->name[name.size()] == '\0';
 }
 
-void Ledger::assume_many(const int32_t* ids, int count, const Demand& d, const Options& o, int32_t* rc,
+void Ledger::assume_many(const int32_t* ids, int count, const Demand& d, const Options& o_in, int32_t* rc,
                          int32_t* score) {
+  const Options o = resolve(o_in, d);
   const uint64_t dh = d.hash(), oh = o.hash();
   Plan plan;
   for (int i = 0; i < count; ++i) {
@@ -514,11 +519,12 @@ void Ledger::assume_many(const int32_t* ids, int count, const Demand& d, const O
   }
 }
 
-int32_t Ledger::assume(int32_t id, const Demand& d, const Options& o, Plan* plan) {
+int32_t Ledger::assume(int32_t id, const Demand& d, const Options& o_in, Plan* plan) {
   // Fast path: the node's generation is read without copying its snapshot; a cached plan
   // for (node, generation, demand, options) is exact for that generation.
   NodeSlot* n = node(id);
   if (!n || !n->in_use) return kErrUnknownNode;
+  const Options o = resolve(o_in, d);
   const uint64_t dh = d.hash(), oh = o.hash();
   int32_t rc;
   if (cache_get(CacheKey{id, n->generation.load(std::memory_order_acquire), dh, oh}, &rc, plan)) return rc;
@@ -555,9 +561,10 @@ int32_t Ledger::nominate(int32_t id, const std::string& key, const Demand& d, co
   return rc;
 }
 
-int32_t Ledger::reserve_as(int32_t id, const std::string& key, const Demand& d, const Options& o, Plan* plan,
+int32_t Ledger::reserve_as(int32_t id, const std::string& key, const Demand& d, const Options& o_in, Plan* plan,
                            int32_t state) {
   NodeSlot* n = node(id);
+  const Options o = resolve(o_in, d);
   if (!n || !n->in_use) return kErrUnknownNode;
   if (key.empty() || key.size() >= kKeyLen) return kErrBadDemand;
   const uint64_t h = key_hash(key.c_str());
@@ -609,6 +616,7 @@ int32_t Ledger::reserve_as(int32_t id, const std::string& key, const Demand& d, 
   n->generation.fetch_add(1, std::memory_order_release);
   hdr_->n_pods.fetch_add(1);
   hdr_->epoch.fetch_add(1);
+  note_request(d);
   return kOk;
 }
 
@@ -656,6 +664,7 @@ int32_t Ledger::allocate_plan(int32_t id, const std::string& key, const Demand& 
   n->generation.fetch_add(1, std::memory_order_release);
   hdr_->n_pods.fetch_add(1);
   hdr_->epoch.fetch_add(1);
+  note_request(d);
   return kOk;
 }
 
@@ -747,7 +756,8 @@ int32_t Ledger::fits_without(int32_t id, const std::vector<std::string>& victims
     }
     unapply(snap.devs, snap.n_devs, vd, vp);
   }
-  return choose(snap.devs, snap.n_devs, &snap.topo, d, o, plan);
+  const Options ro = resolve(o, d);
+  return choose(snap.devs, snap.n_devs, &snap.topo, d, ro, plan);
 }
 
 std::vector<PodRecord> Ledger::pods_on(int32_t node_id) const {
@@ -824,6 +834,78 @@ FragStats Ledger::frag(int32_t min_request) const {
     frag_accumulate(n->devs, n->n_devs, min_request, &s);
   }
   return s;
+}
+
+namespace {
+constexpr uint32_t kSizeDecayAt = 4096;   // halve the counts when they reach this many
+inline bool size_common(uint32_t cnt, uint32_t total) { return cnt * 50u >= total && cnt > 0; }
+inline bool size_rare(uint32_t cnt, uint32_t total) { return cnt * 100u < total; }
+}  // namespace
+
+void Ledger::note_request(const Demand& d) {
+  for (int c = 0; c < d.n; ++c) {
+    const int s = d.c[c].pct;
+    if (s <= 0 || s > kPercentPerDevice) continue;
+    const uint32_t cnt = hdr_->size_hist[s].fetch_add(1, kRlx) + 1;
+    uint32_t total = hdr_->size_total.fetch_add(1, kRlx) + 1;
+    if (total >= kSizeDecayAt) {
+      // one process wins the halving; counts racing with it are off by a request or two
+      if (hdr_->size_total.compare_exchange_strong(total, total / 2, kRlx)) {
+        uint64_t bits[2] = {0, 0};
+        for (int q = 1; q <= kPercentPerDevice; ++q) {
+          const uint32_t h = hdr_->size_hist[q].load(kRlx) / 2;
+          hdr_->size_hist[q].store(h, kRlx);
+          const bool was = (hdr_->size_bits[q >> 6].load(kRlx) >> (q & 63)) & 1u;
+          if (size_common(h, total / 2) || (was && !size_rare(h, total / 2))) bits[q >> 6] |= 1ULL << (q & 63);
+        }
+        hdr_->size_bits[0].store(bits[0], std::memory_order_release);
+        hdr_->size_bits[1].store(bits[1], std::memory_order_release);
+      }
+      continue;
+    }
+    if (size_common(cnt, total)) hdr_->size_bits[s >> 6].fetch_or(1ULL << (s & 63), std::memory_order_release);
+  }
+}
+
+SizeSet Ledger::learned_sizes() const {
+  SizeSet s;
+  s.bits[0] = hdr_->size_bits[0].load(std::memory_order_acquire);
+  s.bits[1] = hdr_->size_bits[1].load(std::memory_order_acquire);
+  // sizes that went rare since they were set (no decay pass yet) are dropped on read
+  const uint32_t total = hdr_->size_total.load(kRlx);
+  for (int w = 0; w < 2; ++w)
+    for (uint64_t b = s.bits[w]; b; b &= b - 1) {
+      const int q = w * 64 + __builtin_ctzll(b);
+      if (q > kPercentPerDevice || size_rare(hdr_->size_hist[q].load(kRlx), total)) s.bits[w] &= ~(1ULL << (q & 63));
+    }
+  return s;
+}
+
+Options Ledger::resolve(const Options& o, const Demand& d) const {
+  if (o.compat || o.policy != Policy::kBinpack) return o;
+  SizeSet s = o.sizes;
+  if (o.learn_sizes) {
+    const SizeSet l = learned_sizes();
+    s.bits[0] |= l.bits[0];
+    s.bits[1] |= l.bits[1];
+  }
+  for (int c = 0; c < d.n; ++c) s.add(d.c[c].pct);
+  if (s.empty()) return o;
+  // the knapsack table costs ~5k operations: keep the last one per thread
+  thread_local SizeSet last_set;
+  thread_local uint8_t last_waste[kWasteSlots];
+  thread_local bool have = false;
+  Options r = o;
+  if (have && last_set == s) {
+    r.sizes = s;
+    std::memcpy(r.waste, last_waste, sizeof(last_waste));
+    return r;
+  }
+  r.set_sizes(s);
+  last_set = s;
+  std::memcpy(last_waste, r.waste, sizeof(last_waste));
+  have = true;
+  return r;
 }
 
 void Ledger::clear_cache() {

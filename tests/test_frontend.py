@@ -346,7 +346,9 @@ def test_priorities_nominate_unique_best_and_bind_adopts():
         loop = asyncio.get_running_loop()
         led = rt.state.ledger
         try:
-            base = store.create_pod(pu.make_pod("base", [("c", 100)] * 7))   # n0 nearly full
+            # n0 nearly full: 7 whole GPUs and 40 % of the last one, so a 60 % share fills
+            # that GPU exactly (the unique best fit; on n1 it would leave a 40 % hole)
+            base = store.create_pod(pu.make_pod("base", [("c", 100)] * 7 + [("d", 40)]))
             mb = pu.meta(base)
             await loop.run_in_executor(None, _http, rt.bound_port, [
                 ("POST", "/scheduler/filter", _dumps({"Pod": base, "NodeNames": ["n0"]})),
