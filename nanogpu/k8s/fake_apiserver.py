@@ -70,6 +70,7 @@ def _match_fields(obj: dict, selector: str | None) -> bool:
 @dataclass
 class Faults:
     latency_s: float = 0.0            # added to every API call (modelled RTT)
+    watch_timeout_s: float = 0.0      # >0: watch streams end cleanly after this long (timeoutSeconds)
     patch_error_rate: float = 0.0     # 500 on pod PATCH
     bind_error_rate: float = 0.0      # 500 on binding POST
     conflict_rate: float = 0.0        # 409 on binding POST
@@ -100,6 +101,8 @@ class FakeKubeStore:
         self.counts: dict[str, int] = {}
         self.leases: dict[tuple[str, str], dict] = {}
         self._ts_sec, self._ts_str = -1, ""
+        # watch-cache floor per kind: a watch from an older resourceVersion gets 410 Gone
+        self.compacted: dict[str, int] = {"pods": 0, "nodes": 0}
 
     # ------------------------------------------------------------------ internals
     def _bump(self, obj: dict) -> dict:
@@ -306,8 +309,11 @@ class FakeKubeStore:
             rv = 0
         buf = _WatchBuffer()
         hist = self.history[kind]
-        if rv and hist and hist[0][0] > rv + 1 and len(hist) == hist.maxlen:
-            raise ApiError(410, "too old resource version", "Expired")
+        if rv and ((hist and hist[0][0] > rv + 1 and len(hist) == hist.maxlen) or rv < self.compacted[kind]):
+            raise ApiError(410, f"too old resource version: {rv} ({self.compacted[kind] or hist[0][0]})", "Expired")
+        timer = None
+        if self.faults.watch_timeout_s > 0:
+            timer = asyncio.get_running_loop().call_later(self.faults.watch_timeout_s, buf.push, None)
         for ev_rv, ev in list(hist):
             if ev_rv > rv:
                 buf.evs.append(ev)
@@ -326,12 +332,14 @@ class FakeKubeStore:
                 if end:
                     batch = batch[:batch.index(None)]
                 if label_selector:
-                    batch = [ev for ev in batch if _match_labels(ev["object"], label_selector)]
+                    batch = [ev for ev in batch if ev["type"] == "ERROR" or _match_labels(ev["object"], label_selector)]
                 if batch:
                     yield batch
                 if end:
                     return
         finally:
+            if timer is not None:
+                timer.cancel()
             self.watchers[kind].remove(buf)
 
     async def watch(self, kind: str, resource_version: str, label_selector: str | None = None
@@ -345,6 +353,23 @@ class FakeKubeStore:
         for ws in self.watchers.values():
             for w in ws:
                 w.push(None)
+
+    def compact(self, kind: str | None = None) -> None:
+        """Fault injection: the watch cache forgets its history (etcd compaction), so a watch
+        resumed from any resourceVersion seen so far is answered 410 Gone."""
+        for k in ([kind] if kind else list(self.history)):
+            self.history[k].clear()
+            self.compacted[k] = self.rv   # a watch from here on misses nothing
+
+    def inject_watch_error(self, kind: str, code: int = 410, message: str = "too old resource version") -> None:
+        """Fault injection: every open watch of `kind` receives an ERROR event (the API server
+        sends one in-stream when a watcher's resourceVersion expires) and ends."""
+        ev = {"type": "ERROR", "object": {"kind": "Status", "apiVersion": "v1", "status": "Failure",
+                                          "message": message, "reason": "Expired" if code == 410 else "",
+                                          "code": code}}
+        for w in self.watchers[kind]:
+            w.push(ev)
+            w.push(None)
 
 
 class _WatchBuffer:
@@ -476,6 +501,14 @@ def make_app(store: FakeKubeStore) -> web.Application:
         except ApiError as e:
             if not resp.prepared:
                 return _err(e)
+            # the stream is already open: the API server reports the failure in-stream
+            status = {"kind": "Status", "apiVersion": "v1", "status": "Failure", "message": e.message,
+                      "reason": e.reason, "code": e.status}
+            try:
+                await resp.write(json.dumps({"type": "ERROR", "object": status}, separators=(",", ":")).encode()
+                                 + b"\n")
+            except (ConnectionResetError, RuntimeError):
+                pass
         except (ConnectionResetError, asyncio.CancelledError):
             pass
         return resp

@@ -10,6 +10,7 @@ from __future__ import annotations
 import asyncio
 import logging
 import random
+import time
 from typing import Awaitable, Callable
 
 from .client import ApiError
@@ -28,6 +29,10 @@ def _node_key(o: dict) -> str:
     return (o.get("metadata") or {}).get("name", "")
 
 
+def _rv(o: dict) -> str:
+    return (o.get("metadata") or {}).get("resourceVersion", "")
+
+
 class Informer:
     def __init__(self, api, resource: str, label_selector: str | None = None,
                  resync_s: float = 0.0, key=None):
@@ -41,7 +46,10 @@ class Informer:
         self.synced = asyncio.Event()
         self.rv = ""
         self._task: asyncio.Task | None = None
-        self.relists = 0
+        self.relists = 0      # LISTs (the first one included)
+        self.rewatches = 0    # watches resumed from the last resourceVersion after a clean end
+        self.expired = 0      # 410 Gone / expired resourceVersion answers (each forces a LIST)
+        self.events = 0       # watch events handled
 
     def add_handler(self, h: Handler) -> None:
         self.handlers.append(h)
@@ -72,26 +80,55 @@ class Informer:
         for k, o in fresh.items():
             old = self.store.get(k)
             self.store[k] = o
+            if old is not None and _rv(old) == _rv(o) and _rv(o):
+                continue              # unchanged since we last saw it: nothing to hand on
             self._dispatch("MODIFIED" if old is not None else "ADDED", o, old)
         self.rv = rv
         self.relists += 1
 
     async def run(self) -> None:
+        """client-go reflector semantics (/root/reference/go.mod:16, client-go v0.18 informers
+        started at /root/reference/pkg/controller/controller.go:136): LIST once, then WATCH from
+        the last resourceVersion seen. A watch that ends cleanly (the server's timeoutSeconds,
+        a proxy closing the stream) is re-opened from that resourceVersion with no LIST. Only
+        410 Gone / an ERROR event (the resourceVersion fell out of the server's watch cache)
+        or a transport failure re-LISTs; the relist diff turns objects deleted while the watch
+        was down into DELETED events."""
         backoff = 0.05
+        need_list = True
+        gone_in_a_row = 0
         while True:
             try:
-                await self._list()
-                self.synced.set()
-                backoff = 0.05
+                if need_list:
+                    await self._list()
+                    need_list = False
+                    self.synced.set()
+                t0, n0 = time.monotonic(), self.events
                 await self._watch()
+                gone_in_a_row = 0
+                self.rewatches += 1          # clean end: resume from self.rv
+                if self.events == n0 and time.monotonic() - t0 < 0.1:
+                    # client-go's "very short watch": a server that closes every stream at once
+                    # must not turn this loop into a busy one
+                    await asyncio.sleep(backoff)
+                    backoff = min(backoff * 2, 5.0)
+                else:
+                    backoff = 0.05
             except asyncio.CancelledError:
                 raise
             except ApiError as e:
-                if e.status != 410:
+                need_list = True
+                if e.status == 410:
+                    self.expired += 1
+                    gone_in_a_row += 1
+                    if gone_in_a_row <= 3:
+                        continue             # relist at once: the cache has moved past us
+                else:
                     log.warning("%s informer: %s", self.resource, e)
-                    await asyncio.sleep(backoff)
-                    backoff = min(backoff * 2, 5.0)
-            except Exception as e:  # network errors: relist with backoff
+                await asyncio.sleep(backoff)
+                backoff = min(backoff * 2, 5.0)
+            except Exception as e:  # transport failure: relist with backoff
+                need_list = True
                 log.warning("%s informer error: %s", self.resource, e)
                 await asyncio.sleep(backoff + random.random() * backoff)
                 backoff = min(backoff * 2, 5.0)
@@ -107,6 +144,7 @@ class Informer:
         pop, get = store.pop, store.get
         async for batch in stream:
             last = None
+            self.events += len(batch)
             try:
                 for ev in batch:
                     etype, obj = ev.get("type"), ev.get("object") or {}
