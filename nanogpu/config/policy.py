@@ -15,7 +15,8 @@ Schema (reference keys kept; MI355X additions are optional):
     syncPeriod: [{name: gpu_core_usage_avg, period: 15s}, ...]
     priority:   [{name: ..., weight: ...}]          # parsed, informational (as reference)
     scheduling: {policy: binpack, compat: false, topologyWeight: 1.0, scoreNormalize: false}
-    metrics:    {gpu_core_usage_avg: {query: '<PromQL with {node} {card}>', fallback: '...'}}
+    metrics:    {gpu_core_usage_avg: {query: '<PromQL with {node} {card}>', fallback: '...',
+                                      batch: '<PromQL with {node}: all cards>', cardLabel: card}}
 """
 from __future__ import annotations
 
@@ -66,25 +67,40 @@ class Period:
 class MetricQuery:
     query: str
     fallback: str | None = None
+    # One query for every card of a node ({metric} {node}, no {card}); each series names its
+    # card in the first of `card_labels` it carries. None: one query per card (the reference).
+    batch: str | None = None
+    card_labels: tuple[str, ...] = ("card",)
 
 
 # Reference query shapes (prometheus.go:70-76) as the default templates.
 REFERENCE_QUERY = '{metric}{{node=~"{node}",card="{card}"}} /100'
 REFERENCE_FALLBACK = '{metric}{{node="{node}",cardNode="{card}"}} /100'
+# every card of the node in one query: series labelled `card` (the primary template) win
+# over `cardNode` ones (the fallback's label)
+REFERENCE_BATCH = '{metric}{{node=~"{node}"}} /100'
+REFERENCE_CARD_LABELS = ("card", "cardNode")
 # AMD device-metrics-exporter shaped templates (gfx / memory-controller activity in %).
 AMD_QUERIES = {
-    T.GPU_CORE_USAGE_METRIC: MetricQuery('avg_over_time(gpu_gfx_activity{{hostname="{node}",gpu_id="{card}"}}[1m]) / 100'),
-    T.GPU_MEMORY_USAGE_METRIC: MetricQuery('gpu_used_vram{{hostname="{node}",gpu_id="{card}"}} / '
-                                           'gpu_total_vram{{hostname="{node}",gpu_id="{card}"}}'),
+    T.GPU_CORE_USAGE_METRIC: MetricQuery(
+        'avg_over_time(gpu_gfx_activity{{hostname="{node}",gpu_id="{card}"}}[1m]) / 100',
+        batch='avg_over_time(gpu_gfx_activity{{hostname="{node}"}}[1m]) / 100', card_labels=("gpu_id",)),
+    T.GPU_MEMORY_USAGE_METRIC: MetricQuery(
+        'gpu_used_vram{{hostname="{node}",gpu_id="{card}"}} / gpu_total_vram{{hostname="{node}",gpu_id="{card}"}}',
+        batch='gpu_used_vram{{hostname="{node}"}} / gpu_total_vram{{hostname="{node}"}}', card_labels=("gpu_id",)),
 }
 
 # The node agent's own exporter (nanogpu/agent/metrics.py); assumes the scrape config puts
 # the node name in a `node` label (kubernetes_sd relabeling of __meta_kubernetes_pod_node_name).
 AGENT_QUERIES = {
-    T.GPU_CORE_USAGE_METRIC: MetricQuery('avg_over_time(nanogpu_device_busy_percent{{node="{node}",device="{card}"}}[1m])'
-                                         ' / 100'),
-    T.GPU_MEMORY_USAGE_METRIC: MetricQuery('nanogpu_device_vram_used_bytes{{node="{node}",device="{card}"}} / '
-                                           'nanogpu_device_vram_total_bytes{{node="{node}",device="{card}"}}'),
+    T.GPU_CORE_USAGE_METRIC: MetricQuery(
+        'avg_over_time(nanogpu_device_busy_percent{{node="{node}",device="{card}"}}[1m]) / 100',
+        batch='avg_over_time(nanogpu_device_busy_percent{{node="{node}"}}[1m]) / 100', card_labels=("device",)),
+    T.GPU_MEMORY_USAGE_METRIC: MetricQuery(
+        'nanogpu_device_vram_used_bytes{{node="{node}",device="{card}"}} / '
+        'nanogpu_device_vram_total_bytes{{node="{node}",device="{card}"}}',
+        batch='nanogpu_device_vram_used_bytes{{node="{node}"}} / nanogpu_device_vram_total_bytes{{node="{node}"}}',
+        card_labels=("device",)),
 }
 PRESETS = {"amd": AMD_QUERIES, "nanogpu-agent": AGENT_QUERIES}
 
@@ -114,7 +130,7 @@ class PolicySpec:
         for k, q in self.metrics:
             if k == name:
                 return q
-        return MetricQuery(REFERENCE_QUERY, REFERENCE_FALLBACK)
+        return MetricQuery(REFERENCE_QUERY, REFERENCE_FALLBACK, REFERENCE_BATCH, REFERENCE_CARD_LABELS)
 
 
 def parse_policy(text: str) -> PolicySpec:
@@ -135,7 +151,9 @@ def parse_policy(text: str) -> PolicySpec:
             raise ValueError(f"unknown metricsPreset {preset!r} (one of {sorted(PRESETS)})")
         metrics.extend(PRESETS[preset].items())
     for name, q in (spec.get("metrics") or {}).items():
-        metrics.append((name, MetricQuery(q["query"], q.get("fallback"))))
+        labels = q.get("cardLabel") or ["card"]
+        metrics.append((name, MetricQuery(q["query"], q.get("fallback"), q.get("batch"),
+                                          tuple([labels] if isinstance(labels, str) else labels))))
     return PolicySpec(
         sync_period=tuple(periods), priority=prio, policy=pol,
         compat=sch.get("compat"), topology_weight=sch.get("topologyWeight"),

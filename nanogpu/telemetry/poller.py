@@ -1,21 +1,24 @@
 """Load-aware scheduling inputs: per-metric periodic polls -> store -> ledger.
 
 Reference: pkg/controller/node.go (syncMetricLoop :31-43 one goroutine per metric that
-never stops, syncNode :85-109 one query per card, retries 10 s..360 s x5 :68-83, node
-label `nvidia-device-enable=enable` :153-158). Here: one cancellable task per metric,
-periods follow policy reloads, AMD node selector by default (legacy label also
-accepted), bounded query concurrency, and the derived device load is written to the
-native ledger so filter/score never parse strings or load tzdata.
+enqueues `node/metric` for every node each period, nodeWorker -> syncNode :85-109 with one
+query per card, failures re-queued per key with rate limiting 10 s..360 s x5 :57-83 and
+controller.go:35-36,126; node label `nvidia-device-enable=enable` :153-158). Here: one
+cancellable ticker per metric (periods follow policy reloads), the same per-key queue (a
+failing node/metric key backs off on its own while every other key keeps its period), one
+PromQL query per node and metric for all its cards instead of one per card (MetricQuery.batch),
+the AMD node selector by default (legacy label accepted), and the derived device load written
+to the native ledger so filter/score never parse strings or load tzdata.
 """
 from __future__ import annotations
 
 import asyncio
 import logging
-import time
 
 from .. import types as T
 from ..config.policy import PolicySpec
 from ..k8s import podutil as pu
+from ..k8s.informer import WorkQueue
 from .store import TelemetryStore
 
 log = logging.getLogger(__name__)
@@ -36,13 +39,15 @@ class LoadPoller:
         self.spec = spec or PolicySpec()
         self.selectors = selectors or [T.AMD_GPU_NODE_LABEL, T.LEGACY_GPU_NODE_LABEL]
         self.store = TelemetryStore()
-        self.sem = asyncio.Semaphore(concurrency)
-        self.max_retries = max_retries
-        self.base_backoff_s = base_backoff_s
-        self.max_backoff_s = max_backoff_s
+        # `node/metric` keys, rate-limited per key (the reference's nodeQueue)
+        self.queue = WorkQueue("metrics", max_retries=max_retries, base_backoff=base_backoff_s,
+                               max_backoff=max_backoff_s)
+        self.concurrency = concurrency
         self.tasks: dict[str, asyncio.Task] = {}
+        self.workers: list[asyncio.Task] = []
         self.errors = 0
-        self.polls = 0
+        self.polls = 0        # successful node/metric syncs
+        self.queries = 0
 
     # -------------------------------------------------------------- policy changes
     def on_policy(self, spec: PolicySpec) -> None:
@@ -53,53 +58,78 @@ class LoadPoller:
         for t in self.tasks.values():
             t.cancel()
         self.tasks.clear()
+        if not self.workers:
+            self.workers = [asyncio.ensure_future(self.queue.worker(self._sync_key))
+                            for _ in range(self.concurrency)]
         for p in self.spec.sync_period:
             if p.period_s > 0:
                 self.tasks[p.name] = asyncio.ensure_future(self._loop(p.name, p.period_s))
 
     async def stop(self) -> None:
-        for t in self.tasks.values():
+        tasks = list(self.tasks.values()) + self.workers
+        for t in tasks:
             t.cancel()
-        for t in self.tasks.values():
+        for t in tasks:
             try:
                 await t
             except (asyncio.CancelledError, Exception):
                 pass
         self.tasks.clear()
+        self.workers = []
 
     # -------------------------------------------------------------- polling
     async def _loop(self, metric: str, period: float) -> None:
         while True:
-            t0 = time.monotonic()
-            await self.sync_metric(metric)
-            await asyncio.sleep(max(0.0, period - (time.monotonic() - t0)))
+            self.enqueue(metric)
+            await asyncio.sleep(period)
+
+    def enqueue(self, metric: str) -> int:
+        """One period tick (reference syncMetric, node.go:45-55): every GPU node's key."""
+        n = 0
+        for node in self.list_nodes():
+            if is_gpu_node(node, self.selectors):
+                self.queue.add(f"{pu.meta(node).get('name', '')}/{metric}")
+                n += 1
+        return n
 
     async def sync_metric(self, metric: str) -> None:
-        nodes = [n for n in self.list_nodes() if is_gpu_node(n, self.selectors)]
-        await asyncio.gather(*(self._sync_node(n, metric) for n in nodes))
+        """Polls `metric` on every GPU node now (no retries): tests and one-shot use."""
+        await asyncio.gather(*(self.sync_node(n, metric) for n in self.list_nodes()
+                               if is_gpu_node(n, self.selectors)), return_exceptions=True)
 
-    async def _sync_node(self, node: dict, metric: str) -> None:
+    async def _sync_key(self, key: str) -> None:
+        name, _, metric = key.rpartition("/")
+        node = next((n for n in self.list_nodes() if pu.meta(n).get("name") == name), None)
+        if node is None or not is_gpu_node(node, self.selectors):
+            return                                   # node gone or no longer a GPU node
+        await self.sync_node(node, metric)
+
+    async def sync_node(self, node: dict, metric: str) -> None:
+        """All cards of one node for one metric; raises on a failed query (the queue backs
+        the key off; nothing else waits for it)."""
         name = pu.meta(node).get("name", "")
         entry = self.state.node_entry(name)
         n_dev = len(entry.topology.devices) if entry else pu.node_gpu_count(node)
         q = self.spec.query_for(metric)
-        for card in range(n_dev):
-            for attempt in range(self.max_retries + 1):
-                try:
-                    async with self.sem:
-                        v = await self.prom.query_latest(name, metric, card, q)
-                    self.polls += 1
+        try:
+            if q.batch:
+                self.queries += 1
+                for card, v in (await self.prom.query_node(name, metric, q)).items():
+                    if 0 <= card < n_dev:
+                        self.store.update(name, metric, card, v)
+            else:
+                for card in range(n_dev):
+                    self.queries += 1
+                    v = await self.prom.query_latest(name, metric, card, q)
                     if v is not None:
                         self.store.update(name, metric, card, v)
-                    break
-                except asyncio.CancelledError:
-                    raise
-                except Exception as e:
-                    self.errors += 1
-                    if attempt == self.max_retries:
-                        log.warning("metric %s node %s card %d dropped: %s", metric, name, card, e)
-                        break
-                    await asyncio.sleep(min(self.base_backoff_s * 2 ** attempt, self.max_backoff_s))
+        except asyncio.CancelledError:
+            raise
+        except Exception as e:
+            self.errors += 1
+            log.debug("metric %s node %s: %s", metric, name, e)
+            raise
+        self.polls += 1
         self.refresh_node(name, n_dev)
 
     def refresh_node(self, name: str, n_dev: int, now: float | None = None) -> None:

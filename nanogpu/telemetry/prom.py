@@ -58,6 +58,27 @@ class PromClient:
             out.append((el.get("metric") or {}, v))
         return out
 
+    async def query_node(self, node: str, metric: str, q: MetricQuery) -> dict[int, float]:
+        """Every card of `node` in one query (q.batch): {card: last sample}. A series names its
+        card in the first of q.card_labels it carries; earlier labels win (the reference's
+        primary `card` over its fallback `cardNode`, prometheus.go:70-76)."""
+        res = await self.query(q.batch.format(metric=metric, node=node))
+        out: dict[int, float] = {}
+        rank: dict[int, int] = {}
+        for labels, v in res:
+            for r, lab in enumerate(q.card_labels):
+                raw = labels.get(lab)
+                if raw is None:
+                    continue
+                try:
+                    card = int(raw)
+                except ValueError:
+                    break
+                if card not in rank or r <= rank[card]:   # later samples of equal rank win
+                    out[card], rank[card] = round(v, 5), r
+                break
+        return out
+
     async def query_latest(self, node: str, metric: str, card: int, q: MetricQuery) -> float | None:
         """Last sample of the primary template, else of the fallback (prometheus.go:68-83)."""
         res = await self.query(q.query.format(metric=metric, node=node, card=card))

@@ -189,7 +189,19 @@ async def fake_prometheus(series):
         hits.append(q)
         if "broken" in q:
             return web.json_response({"status": "error", "error": "bad query"}, status=400)
+        if any(f'"{n}"' in q for n in series.get("slow_nodes", ())):
+            await asyncio.sleep(2)                       # an exporter that hangs
+        fail = series.get("fail_nodes", ())
+        if any(f'"{n}"' in q for n in fail):
+            return web.json_response({"status": "error", "error": "exporter down"}, status=503)
         for metric, by in series.items():
+            if metric in ("fail_nodes", "slow_nodes"):
+                continue
+            if q.startswith(metric) and 'card="' not in q and 'cardNode="' not in q:
+                # batched query: every card of the node, each series labelled with its card
+                res = [{"metric": {"node": n, "card": str(c)}, "value": [0, str(v)]}
+                       for (n, c), vals in by.items() if f'"{n}"' in q for v in vals]
+                return web.json_response({"status": "success", "data": {"resultType": "vector", "result": res}})
             if q.startswith(metric):
                 for (n, c), vals in by.items():
                     if f'"{n}"' in q and (f'card="{c}"' in q or f'cardNode="{c}"' in q):
@@ -248,6 +260,72 @@ def test_load_poller_feeds_ledger_remain_load():
             # stale samples age out (period + 5 min)
             poller.refresh_node("n0", 2, now=1e12)
             assert st.status()["n0"]["GPUs"][0]["RemainLoad"] == 2
+        finally:
+            await poller.prom.close()
+            await runner.cleanup()
+
+    asyncio.run(main())
+
+
+def test_load_poller_one_query_per_node_and_a_failing_node_never_delays_the_others():
+    """Reference node.go:57-83: a failing `node/metric` key is re-queued with rate limiting
+    while the other keys keep their period. Here one exporter hangs and one answers 503;
+    every other node is refreshed each period, with one query per node for all its cards."""
+    async def main():
+        names = [f"n{i}" for i in range(6)]
+        series = {"gpu_core_usage_avg": {(n, c): [0.3] for n in names for c in range(8)},
+                  "slow_nodes": ("n1",), "fail_nodes": ("n2",)}
+        runner, port, hits = await fake_prometheus(series)
+        st = ClusterState(load_aware=True)
+        nodes = [node(n, 8) for n in names]
+        for n in nodes:
+            st.register_node(n)
+        spec = PolicySpec(sync_period=(Period("gpu_core_usage_avg", 0.05),))
+        poller = LoadPoller(st, PromClient(f"http://127.0.0.1:{port}"), lambda: nodes, spec=spec,
+                            base_backoff_s=10.0, concurrency=4)
+        try:
+            poller.restart()
+            await asyncio.sleep(0.6)
+            healthy = [n for n in names if n not in ("n1", "n2")]
+            # ~12 periods went by: every healthy node was refreshed in (nearly) all of them
+            for n in healthy:
+                t = poller.store.data[(n, "gpu_core_usage_avg", 0)].t
+                assert asyncio.get_running_loop().time() - t < 0.2, n
+            per_node = {n: sum(1 for h in hits if f'"{n}"' in h) for n in names}
+            assert min(per_node[n] for n in healthy) >= 8, per_node
+            assert all('card="' not in h for h in hits)          # batched: no per-card queries
+            assert ("n2", "gpu_core_usage_avg", 0) not in poller.store.data and poller.errors >= 1
+            # n2's key was re-queued with backoff after each failure, then dropped after 5 as in
+            # the reference (it comes back with the next period's tick)
+            assert poller.queue.dropped >= 1 or poller.queue.retries.get("n2/gpu_core_usage_avg", 0) >= 1
+            assert st.status()["n0"]["GPUs"][7]["RemainLoad"] == 2 - 0   # ceil(3)/10 -> usage 0.3
+        finally:
+            await poller.stop()
+            await poller.prom.close()
+            await runner.cleanup()
+
+    asyncio.run(main())
+
+
+def test_load_aware_spread_moves_off_the_loaded_device():
+    """End to end: Prometheus samples -> poller -> ledger -> placement changes with the load."""
+    async def main():
+        series = {"gpu_core_usage_avg": {("n0", 0): [0.95], ("n0", 1): [0.05]}}
+        runner, port, _ = await fake_prometheus(series)
+        st = ClusterState(policy="spread", load_aware=True)
+        n = node("n0", 2)
+        st.register_node(n)
+        spec = PolicySpec(sync_period=(Period("gpu_core_usage_avg", 15),))
+        poller = LoadPoller(st, PromClient(f"http://127.0.0.1:{port}"), lambda: [n], spec=spec)
+        nid = st.node_entry("n0").id
+        try:
+            await poller.sync_metric("gpu_core_usage_avg")
+            _, plan, _ = st.ledger.assume(nid, [(10, 0)], st.options)
+            assert plan == [[1]]                      # GPU 0 is busy
+            series["gpu_core_usage_avg"] = {("n0", 0): [0.05], ("n0", 1): [0.95]}
+            await poller.sync_metric("gpu_core_usage_avg")
+            _, plan, _ = st.ledger.assume(nid, [(10, 0)], st.options)
+            assert plan == [[0]]                      # the load moved, so does the pod
         finally:
             await poller.prom.close()
             await runner.cleanup()
