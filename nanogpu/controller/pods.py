@@ -112,4 +112,4 @@ class NodeController:
             self.state.forget_node(name)
             return
         if pu.node_gpu_count(node) > 0 or name in self.state._nodes:
-            self.state.register_node(node)
+            self.state.try_register_node(node)

@@ -88,11 +88,15 @@ class Extender:
                     return filter_result(None, {}, T.FILTER_NODE_CACHE_ERROR)
                 # nodeCacheCapable=false: full Node objects in the request (the reference rejects this)
                 for n in args.nodes:
-                    self.state.register_node(n)
+                    self.state.try_register_node(n)
                 node_objs = {pu.meta(n).get("name"): n for n in args.nodes}
                 names = list(node_objs)
             self.pods.put(args.pod)
-            ok, failed = self.state.filter(args.pod, names)
+            try:
+                ok, failed = self.state.filter(args.pod, names)
+            except Exception as e:   # a protocol answer, never a 500 (every node fails with the reason)
+                log.exception("filter %s", pu.pod_key(args.pod))
+                ok, failed = [], {n: f"nano-gpu: {type(e).__name__}: {e}" for n in names}
             sp.note = f"{len(ok)}/{len(names)} fit"
         self.metrics.child(self.metrics.verb_latency, "filter").observe(time.perf_counter() - t0)
         self.metrics.child(self.metrics.verb_total, "filter", "ok").inc()
@@ -110,10 +114,14 @@ class Extender:
         if names is None:
             names = [pu.meta(n).get("name") for n in (args.nodes or [])]
             for n in args.nodes or []:
-                self.state.register_node(n)
+                self.state.try_register_node(n)
         with self.tracer.span("prioritize", pu.pod_key(args.pod)):
             self.pods.put(args.pod)
-            scores = self.state.score(args.pod, names)
+            try:
+                scores = self.state.score(args.pod, names)
+            except Exception:
+                log.exception("prioritize %s", pu.pod_key(args.pod))
+                scores = [0] * len(names)            # ScoreMin everywhere (dealer.go:147)
         self.metrics.child(self.metrics.verb_latency, "prioritize").observe(time.perf_counter() - t0)
         self.metrics.child(self.metrics.verb_total, "prioritize", "ok").inc()
         return priority_list(names, scores)
@@ -128,8 +136,11 @@ class Extender:
         chose them for every resource, not only GPU. Raises ValueError on a malformed body."""
         t0 = time.perf_counter()
         args = PreemptionArgs.decode(body)
-        demand = pu.pod_demand(args.pod)
         keep: dict[str, list[str]] = {}
+        try:
+            demand, _ = pu.ledger_view(pu.pod_demand(args.pod))
+        except pu.TooManyGpuContainers:
+            return preemption_result(keep, args.pdb)
         with self.tracer.span("preempt", pu.pod_key(args.pod)) as sp:
             for node, uids in args.victims.items():
                 e = self.state.node_entry(node)
@@ -157,6 +168,11 @@ class Extender:
                 await self._bind(args, sp)
             except (SchedulingError, ApiError, asyncio.TimeoutError, OSError) as e:
                 err = str(e) or e.__class__.__name__
+                sp.ok = False
+                sp.note = err
+            except Exception as e:   # reported in ExtenderBindingResult.Error, not as a crash
+                log.exception("bind %s/%s", args.pod_namespace, args.pod_name)
+                err = f"nano-gpu: {type(e).__name__}: {e}"
                 sp.ok = False
                 sp.note = err
         dt = time.perf_counter() - t0

@@ -120,6 +120,46 @@ def pod_demand(pod: dict) -> Demand:
     return d
 
 
+# Containers one ledger record holds (native alloc.h kMaxContainers).
+LEDGER_MAX_CONTAINERS = 16
+
+
+class TooManyGpuContainers(ValueError):
+    pass
+
+
+def ledger_view(demand: Demand) -> tuple[Demand, list[int] | None]:
+    """The demand as the native ledger stores it, and the container each entry belongs to.
+
+    The reference places any number of containers (allocate.go:54-62, rater.go:74-110); a
+    ledger record holds 16. A pod within that is passed as is (None: entries ARE containers,
+    so compat placements stay bit-exact with the reference). A larger pod keeps only its
+    GPU-requesting containers, which is placement-neutral in native mode (zero-demand
+    containers take no device and sort last); more than 16 of those raises."""
+    if len(demand) <= LEDGER_MAX_CONTAINERS:
+        return demand, None
+    idx = [i for i, d in enumerate(demand) if d[0] > 0 or d[1] > 0]
+    if len(idx) > LEDGER_MAX_CONTAINERS:
+        raise TooManyGpuContainers(f"pod requests GPUs in {len(idx)} containers; at most "
+                                   f"{LEDGER_MAX_CONTAINERS} per pod are supported")
+    return [demand[i] for i in idx], idx
+
+
+def full_plan(plan: Plan, idx: list[int] | None, n_containers: int) -> Plan:
+    """Ledger plan -> one entry per container ([-1]: no GPU)."""
+    if idx is None:
+        return plan
+    out: Plan = [[-1] for _ in range(n_containers)]
+    for k, i in enumerate(idx):
+        out[i] = plan[k]
+    return out
+
+
+def ledger_plan(plan: Plan, idx: list[int] | None) -> Plan:
+    """One entry per container -> the ledger's entries."""
+    return plan if idx is None else [plan[i] for i in idx]
+
+
 def is_gpu_sharing(pod: dict) -> bool:
     """pod.go:27-29 (Σ gpu-percent > 0), extended: an HBM-only request also counts."""
     return any(p > 0 or m > 0 for p, m in pod_demand(pod))

@@ -69,6 +69,7 @@ class ClusterState:
         self._nodes: dict[str, NodeEntry] = {}
         self._nodes_mu = threading.Lock()
         self._released: OrderedDict[str, None] = OrderedDict()   # reference ReleasedPodMap
+        self._rejected: dict[str, str] = {}     # nodes the ledger cannot hold, with the reason
         self._released_cap = 65536
         self.set_policy(policy, compat=compat, load_aware=load_aware, topo_weight=topo_weight, seed=seed,
                         request_sizes=request_sizes or [], learn_sizes=learn_sizes)
@@ -143,6 +144,20 @@ class ClusterState:
             self._nodes[name] = entry
         return entry
 
+    def try_register_node(self, node: dict) -> NodeEntry | None:
+        """register_node for a node that may not fit a ledger slot (more than 64 schedulable
+        devices, 16 physical GPUs): logged once, reported as the node's filter failure."""
+        name = pu.meta(node).get("name", "")
+        try:
+            e = self.register_node(node)
+        except ValueError as err:
+            if self._rejected.get(name) != str(err):
+                log.warning("node %s not schedulable: %s", name, err)
+            self._rejected[name] = str(err)
+            return None
+        self._rejected.pop(name, None)
+        return e
+
     def forget_node(self, name: str) -> bool:
         with self._nodes_mu:
             e = self._nodes.pop(name, None)
@@ -156,7 +171,7 @@ class ClusterState:
         if self.node_source is not None:
             node = self.node_source(name)
             if node is not None:
-                return self.register_node(node)
+                return self.try_register_node(node)
         nid = self.ledger.find_node(name)
         if nid >= 0:
             snap = self.ledger.snapshot(nid)
@@ -182,7 +197,10 @@ class ClusterState:
         """Reference Dealer.Assume (dealer.go:89-136) + Predicate.Handler (predicate.go:19-41)."""
         if self.nominate:
             self._drop_own_nomination(pod)
-        demand = pu.pod_demand(pod)
+        try:
+            demand, _ = pu.ledger_view(pu.pod_demand(pod))
+        except pu.TooManyGpuContainers as e:
+            return [], {name: f"nano-gpu: {e}" for name in node_names}
         ids = self.node_ids(node_names)
         rcs = self.ledger.filter(ids, demand, self.options)
         ok, failed = [], {}
@@ -190,7 +208,9 @@ class ClusterState:
             if rc == N.OK:
                 ok.append(name)
             elif nid < 0:
-                failed[name] = f"nano gpu scheduler get node failed: node {name} not found"
+                failed[name] = (f"nano gpu scheduler get node failed: node {name}: {self._rejected[name]}"
+                                if name in self._rejected else
+                                f"nano gpu scheduler get node failed: node {name} not found")
             else:
                 failed[name] = f"can't allocate {self._demand_str(demand)} on node {name}: {N.err_str(rc)}"
         return ok, failed
@@ -199,7 +219,10 @@ class ClusterState:
         """Reference Dealer.Score (dealer.go:138-153); ScoreMin (0) for unknown/unfit nodes."""
         if self.nominate:
             self._drop_own_nomination(pod)
-        demand = pu.pod_demand(pod)
+        try:
+            demand, _ = pu.ledger_view(pu.pod_demand(pod))
+        except pu.TooManyGpuContainers:
+            return [0] * len(node_names)             # filter already failed every node
         ids = self.node_ids(node_names)
         scores = self.ledger.score(ids, demand, self.options)
         if self.nominate and scores:
@@ -245,10 +268,15 @@ class ClusterState:
         if e is None:
             raise SchedulingError(f"node {node_name} not found")
         uid = pu.pod_uid(pod)
-        rc, plan = self.ledger.reserve(e.id, uid, pu.pod_demand(pod), self.options)
+        full = pu.pod_demand(pod)
+        try:
+            demand, idx = pu.ledger_view(full)
+        except pu.TooManyGpuContainers as e:
+            raise SchedulingError(str(e)) from None
+        rc, plan = self.ledger.reserve(e.id, uid, demand, self.options)
         if rc not in (N.OK, N.OK_EXISTING):
-            raise self.reserve_error(pu.pod_demand(pod), node_name, rc)
-        return plan, rc == N.OK
+            raise self.reserve_error(demand, node_name, rc)
+        return pu.full_plan(plan, idx, len(full)), rc == N.OK
 
     def reserve_error(self, demand, node_name: str, rc: int) -> SchedulingError:
         return SchedulingError(f"assume {self._demand_str(demand)} on {node_name} failed: {N.err_str(rc)}")
@@ -271,7 +299,16 @@ class ClusterState:
         if e is None:
             log.warning("allocate %s: node %s unknown", pu.pod_key(pod), node)
             return False
-        rc = self.ledger.allocate_plan(e.id, pu.pod_uid(pod), pu.pod_demand(pod), plan, True)
+        try:
+            demand, idx = pu.ledger_view(pu.pod_demand(pod))
+        except pu.TooManyGpuContainers as err:
+            log.warning("allocate %s: %s", pu.pod_key(pod), err)
+            return False
+        if len(plan) != len(pu.pod_demand(pod)):
+            log.warning("allocate %s: %d assignments for %d containers", pu.pod_key(pod), len(plan),
+                        len(pu.pod_demand(pod)))
+            return False
+        rc = self.ledger.allocate_plan(e.id, pu.pod_uid(pod), demand, pu.ledger_plan(plan, idx), True)
         if rc != N.OK:
             log.warning("allocate %s on %s failed: %s", pu.pod_key(pod), node, N.err_str(rc))
             return False

@@ -1,0 +1,158 @@
+"""Pods with any number of containers (reference allocate.go:54-62 and rater.go:74-110 place
+one demand slot per container, without a limit).
+
+A ledger record holds 16 containers; larger pods keep only their GPU-requesting containers
+there (podutil.ledger_view). Every verb answers in the extender protocol whatever the pod
+looks like: filter reports unplaceable pods in FailedNodes, never as an HTTP error.
+"""
+import asyncio
+import json
+import random
+
+from nanogpu import types as T
+from nanogpu.k8s import podutil as pu
+
+from nanogpu.app import Config, Runtime
+from nanogpu.k8s.fake_apiserver import FakeKubeStore, InProcKube
+from test_control_plane import annotated, runtime, wait_for
+from test_control_plane import node as mknode
+from test_frontend import _dumps, _http
+
+
+async def _runtime(n_nodes, **kw):
+    store = FakeKubeStore()
+    for i in range(n_nodes):
+        store.add_node(mknode(f"n{i}"))
+    rt = Runtime(Config(port=0, host="127.0.0.1", policy_config_path="/nonexistent", **kw), api=InProcKube(store))
+    await rt.start()
+    assert (rt.native is not None) == (kw.get("frontend", "native") == "native")
+    return store, rt
+
+
+def _sidecar_pod(name, n_containers, gpu_at, pct=20):
+    cs = [(f"c{k}", pct if k in gpu_at else 0, 0) for k in range(n_containers)]
+    return pu.make_pod(name, cs)
+
+
+def _schedule(rt, store, pod, nodes):
+    """filter -> priorities -> bind over HTTP on the extender; returns the three responses."""
+    m = pu.meta(pod)
+    res = _http(rt.bound_port, [
+        ("POST", "/scheduler/filter", _dumps({"Pod": pod, "NodeNames": nodes})),
+        ("POST", "/scheduler/priorities", _dumps({"Pod": pod, "NodeNames": nodes}))])
+    fit = json.loads(res[0][1])["NodeNames"] or []
+    if not fit:
+        return res + [None]
+    bind = _http(rt.bound_port, [("POST", "/scheduler/bind", _dumps(
+        {"PodName": m["name"], "PodNamespace": m["namespace"], "PodUID": m["uid"], "Node": fit[0]}))])
+    return res + bind
+
+
+def test_forty_container_pod_schedules_through_both_front_doors():
+    for frontend in ("native", "aiohttp"):
+        async def main():
+            store, rt = await _runtime(2, frontend=frontend)
+            loop = asyncio.get_running_loop()
+            try:
+                pod = store.create_pod(_sidecar_pod("big", 40, {25}, pct=30))
+                f, p, b = await loop.run_in_executor(None, _schedule, rt, store, pod, ["n0", "n1"])
+                assert f[0] == 200 and json.loads(f[1])["NodeNames"], (frontend, f)
+                assert p[0] == 200 and len(json.loads(p[1])) == 2
+                assert b == (200, b'{"Error":""}'), (frontend, b)
+                ann = store.get_pod("default", "big")["metadata"]["annotations"]
+                assert ann[T.container_annotation("c25")] != "-1"
+                assert all(ann[T.container_annotation(f"c{k}")] == "-1" for k in range(40) if k != 25)
+                node = pu.node_name_of(store.get_pod("default", "big"))
+                dev = int(ann[T.container_annotation("c25")])
+                assert rt.state.status()[node]["GPUs"][dev]["Percent"] == 70
+                store.delete_pod("default", "big")
+                assert await wait_for(lambda: rt.state.status()[node]["GPUs"][dev]["Percent"] == 100)
+            finally:
+                await rt.stop()
+
+        asyncio.run(main())
+
+
+def test_too_many_gpu_containers_is_a_failed_node_not_an_error():
+    for frontend in ("native", "aiohttp"):
+        async def main():
+            store, rt = await _runtime(2, frontend=frontend)
+            loop = asyncio.get_running_loop()
+            try:
+                pod = store.create_pod(_sidecar_pod("huge", 30, set(range(20)), pct=5))
+                f, p, b = await loop.run_in_executor(None, _schedule, rt, store, pod, ["n0", "n1"])
+                body = json.loads(f[1])
+                assert f[0] == 200 and not body["NodeNames"] and body["Error"] == ""
+                assert all("at most 16" in r for r in body["FailedNodes"].values()), body
+                assert p[0] == 200 and [h["Score"] for h in json.loads(p[1])] == [0, 0]
+                assert b is None
+            finally:
+                await rt.stop()
+
+        asyncio.run(main())
+
+
+def test_fuzz_container_counts_never_answer_5xx():
+    async def main():
+        store, rt = await _runtime(4)
+        loop = asyncio.get_running_loop()
+        rng = random.Random(11)
+        try:
+            for i in range(40):
+                n = rng.randint(0, 64)
+                gpu = set(rng.sample(range(n), min(n, rng.choice([0, 1, 2, 5, 17])))) if n else set()
+                pod = store.create_pod(_sidecar_pod(f"f{i}", n, gpu, pct=rng.choice([5, 10, 25])))
+                f, p, b = await loop.run_in_executor(None, _schedule, rt, store, pod, ["n0", "n1", "n2", "n3"])
+                assert f[0] == 200 and p[0] == 200, (n, len(gpu), f, p)
+                fit = json.loads(f[1])["NodeNames"]
+                assert bool(fit) == (len(gpu) <= 16), (n, len(gpu), f)
+                if b is not None:
+                    assert b == (200, b'{"Error":""}'), (n, len(gpu), b)
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
+
+
+def test_restart_rebuilds_a_pod_with_more_than_16_containers():
+    async def main():
+        store = FakeKubeStore()
+        store.add_node(mknode("n0"))
+        plan = [[-1]] * 20
+        plan[3], plan[17] = [2], [5]
+        p = annotated("wide", "n0", plan, pct=0)
+        for k in (3, 17):
+            p["spec"]["containers"][k]["resources"]["limits"][T.RESOURCE_GPU_PERCENT] = "40"
+        store.create_pod(p)
+        rt = await runtime(store)
+        try:
+            gpus = rt.state.status()["n0"]["GPUs"]
+            assert gpus[2]["Percent"] == 60 and gpus[5]["Percent"] == 60
+            assert rt.state.ledger.n_pods == 1
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
+
+
+def test_node_with_more_devices_than_a_slot_holds_fails_alone():
+    """A 10-GPU CPX node exposes 80 schedulable devices (a ledger slot holds 64): it is
+    reported in FailedNodes with the reason while the other nodes keep scheduling."""
+    from nanogpu.topology.model import synthetic_mi355x
+
+    async def main():
+        store, rt = await _runtime(1)
+        big = synthetic_mi355x(10, "CPX")
+        store.add_node(pu.make_node("wide", len(big.devices), big.to_json(), {"amd.com/gpu.present": "true"}))
+        loop = asyncio.get_running_loop()
+        try:
+            pod = store.create_pod(_sidecar_pod("p", 1, {0}, pct=10))
+            f, p, b = await loop.run_in_executor(None, _schedule, rt, store, pod, ["wide", "n0"])
+            body = json.loads(f[1])
+            assert f[0] == 200 and body["NodeNames"] == ["n0"], body
+            assert "too many devices" in body["FailedNodes"]["wide"], body
+            assert b == (200, b'{"Error":""}')
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
