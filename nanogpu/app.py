@@ -15,6 +15,7 @@ import asyncio
 import logging
 import os
 import signal
+import time
 import sys
 from dataclasses import dataclass, field
 
@@ -167,6 +168,9 @@ class Runtime:
                         self.cfg.policy_config_path)
         if self.leader:
             self.tasks.append(asyncio.ensure_future(self._sweeper()))
+        if self.cfg.leader_elect and self.leader:
+            # not before the Lease says so; the other workers read the same shared flag
+            self.state.ledger.serving = False
         self.ready.set()
         if self.cfg.leader_elect and self.leader:
             import socket
@@ -181,11 +185,14 @@ class Runtime:
         if serve:
             router = server.Router(self.extender, self.ready)
             self.router = router
-            if self.elector is not None:
-                router.serving = lambda: self.elector.leader
+            if self.cfg.leader_elect:
+                # every worker of the replica follows the elector's flag in the shared ledger
+                # (only worker 0 runs the elector)
+                ledger = self.state.ledger
+                router.serving = lambda: ledger.serving
             if self.cfg.frontend == "native":
                 self.native = server.NativeServer(router, self.cfg.host, self.cfg.port, self.cfg.frontend_threads)
-                self.native.fe.set_serving(self.elector is None or self.elector.leader)
+                self.native.fe.set_serving(True)   # the ledger's shared flag gates it as well
                 self.native.fe.set_busy_poll_us(self.cfg.busy_poll_us)
                 self.native.start()
                 self.bound_port = self.native.port
@@ -197,8 +204,7 @@ class Runtime:
                      self.cfg.frontend, self.state.policy, self.state.options.compat)
 
     def _on_leadership(self, leader: bool) -> None:
-        if self.native is not None:
-            self.native.fe.set_serving(leader)
+        self.state.ledger.serving = leader
 
     def _apply_policy(self, spec) -> None:
         pol = spec.policy or self.state.policy
@@ -301,16 +307,34 @@ def pin_worker(cfg: Config, worker: int) -> list[int]:
     return []
 
 
+def _drop_stale_region(path: str) -> None:
+    """The server owns its region. One left behind by a previous incarnation (SIGKILL, OOM:
+    /dev/shm outlives a container restart, and pid 1 names the same path again) holds pods
+    that may have been deleted meanwhile, and nothing would ever release them: start clean.
+    The ledger is rebuilt from the API server (the checkpoint) before serving."""
+    try:
+        os.unlink(path)
+        log.warning("removed a stale ledger region at %s", path)
+    except FileNotFoundError:
+        pass
+
+
 def run(cfg: Config) -> int:
     if cfg.workers <= 1:
+        if cfg.ledger_path:
+            _drop_stale_region(cfg.ledger_path)
         pin_worker(cfg, 0)
         return asyncio.run(serve_forever(cfg, 0))
     if not cfg.ledger_path:
         cfg.ledger_path = f"/dev/shm/nanogpu-ledger-{os.getpid()}"
+    _drop_stale_region(cfg.ledger_path)
     # create the shared region before forking so every worker attaches to the same layout
     from .native import core
 
-    core().Ledger(cfg.ledger_path, cfg.max_nodes, cfg.max_pods, True)
+    led = core().Ledger(cfg.ledger_path, cfg.max_nodes, cfg.max_pods, True)
+    if cfg.leader_elect:
+        led.serving = False          # no worker schedules before the Lease is won
+    del led
     children = []
     for w in range(cfg.workers):
         pid = os.fork()
@@ -331,16 +355,62 @@ def run(cfg: Config) -> int:
             except ProcessLookupError:
                 pass
 
-    signal.signal(signal.SIGINT, forward)
-    signal.signal(signal.SIGTERM, forward)
-    code = 0
-    for c in children:
-        _, status = os.waitpid(c, 0)
-        code = code or (os.waitstatus_to_exitcode(status) if hasattr(os, "waitstatus_to_exitcode") else 0)
+    stopping = {"on": False}
+
+    def forward_and_stop(sig, frame):
+        stopping["on"] = True
+        forward(sig, frame)
+
+    signal.signal(signal.SIGINT, forward_and_stop)
+    signal.signal(signal.SIGTERM, forward_and_stop)
+    code = supervise(children, stopping)
     try:
         os.unlink(cfg.ledger_path)
     except OSError:
         pass
+    return code
+
+
+def supervise(children: list[int], stopping: dict, grace_s: float = 10.0) -> int:
+    """Waits for the workers. A worker that exits while the replica is not shutting down
+    (a crash, an OOM kill) takes the replica down: the others are stopped and the exit code
+    is non-zero, so the kubelet restarts the pod as a whole — worker 0 runs the pod
+    controller, sweeper and leader elector, and half a replica must not keep serving."""
+    live = set(children)
+    code = 0
+    while live:
+        try:
+            pid, status = os.wait()
+        except ChildProcessError:
+            break
+        except InterruptedError:
+            continue
+        if pid not in live:
+            continue
+        live.discard(pid)
+        rc = os.waitstatus_to_exitcode(status)
+        code = code or rc
+        if not stopping["on"] and live:
+            log.error("worker pid %d exited (%d): stopping the replica", pid, rc)
+            code = code or 1
+            stopping["on"] = True
+            for c in live:
+                try:
+                    os.kill(c, signal.SIGTERM)
+                except ProcessLookupError:
+                    pass
+            deadline = time.monotonic() + grace_s
+            while live and time.monotonic() < deadline:
+                for c in list(live):
+                    done, st = os.waitpid(c, os.WNOHANG)
+                    if done:
+                        live.discard(c)
+                time.sleep(0.05)
+            for c in live:
+                try:
+                    os.kill(c, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
     return code
 
 

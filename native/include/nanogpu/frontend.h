@@ -92,6 +92,9 @@ class Frontend {
   void set_options(const Options& o, bool score_normalize, bool nominate = false);
   // false: every request goes to Python (a standby replica answers 503 from there).
   void set_serving(bool on) { serving_.store(on, std::memory_order_release); }
+  // this process's switch AND the replica's shared flag in the ledger (leader election runs
+  // in one worker; every worker's front door follows it)
+  bool serving() const { return serving_.load(std::memory_order_acquire) && ledger_->serving(); }
   // After any event a worker keeps polling (epoll timeout 0) for this long before it
   // blocks again: trades a little CPU during bursts for no wake-up latency per request.
   void set_busy_poll_us(int us) { busy_poll_ns_.store(static_cast<int64_t>(us) * 1000, std::memory_order_relaxed); }

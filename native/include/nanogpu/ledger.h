@@ -76,6 +76,9 @@ struct LedgerHeader {
   std::atomic<int32_t> attached;    // processes attached
   pthread_mutex_t registry_mu;
   alignas(64) std::atomic<uint64_t> epoch;      // bumps on every mutation anywhere
+  // 1 while this replica may schedule: the worker running the leader elector writes it, every
+  // worker (front door, Python router, /readyz) reads it. 1 without leader election.
+  std::atomic<int32_t> serving;
   alignas(64) std::atomic<int64_t> n_pods;
   // learned request-size mix (Ledger::note_request): decayed counts of share sizes and the
   // set of the common ones, which native binpack's waste model uses (alloc.h SizeSet)
@@ -124,6 +127,8 @@ class Ledger {
   bool snapshot(int32_t id, NodeSnapshot* out) const;
   uint64_t generation(int32_t id) const;
   uint64_t epoch() const { return hdr_->epoch.load(std::memory_order_acquire); }
+  bool serving() const { return hdr_->serving.load(std::memory_order_acquire) != 0; }
+  void set_serving(bool on) { hdr_->serving.store(on ? 1 : 0, std::memory_order_release); }
 
   // Filter/score: plan for `d` on node `id`, cached per (node, generation, demand, options).
   int32_t assume(int32_t id, const Demand& d, const Options& o, Plan* plan);

@@ -347,6 +347,8 @@ PYBIND11_MODULE(_native, m) {
             return id;
           },
           py::arg("name"), py::arg("devices"), py::arg("topo") = py::none())
+      .def_property("serving", &Ledger::serving, &Ledger::set_serving,
+                    "shared across workers: whether this replica schedules (leader election)")
       .def("find_node", &Ledger::find_node)
       .def("node_name", &Ledger::node_name)
       .def("remove_node", &Ledger::remove_node)

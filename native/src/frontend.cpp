@@ -710,7 +710,7 @@ void Frontend::process(Worker* w, Conn* c) {
 void Frontend::defer(Worker* w, Conn* c, std::string method, std::string path, std::string query, std::string body) {
   PyRequest r;
   r.id = make_id(w->idx, c->id);
-  if (method == "POST" && path == "/scheduler/bind" && serving_.load(std::memory_order_acquire))
+  if (method == "POST" && path == "/scheduler/bind" && serving())
     prepare_bind(body, &r);
   r.method = std::move(method);
   r.path = std::move(path);
@@ -775,7 +775,7 @@ bool Frontend::handle_native(Worker* w, Conn* c, const std::string& method, cons
                              std::string_view body, std::string* out) {
   (void)w;
   (void)c;
-  if (method != "POST" || !serving_.load(std::memory_order_acquire)) return false;
+  if (method != "POST" || !serving()) return false;
   const bool prio = path == "/scheduler/priorities";
   if (!prio && path != "/scheduler/filter") return false;
   const uint64_t t0 = now_ns();

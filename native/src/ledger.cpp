@@ -18,7 +18,7 @@
 namespace nanogpu {
 
 static constexpr uint64_t kMagic = 0x4e414e4f47505531ULL;  // "NANOGPU1"
-static constexpr uint32_t kVersion = 6;  // 4: HBM pools; 5: cache-line layout; 6: request-size mix
+static constexpr uint32_t kVersion = 7;  // 4: HBM pools; 5: cache lines; 6: request sizes; 7: serving
 
 static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -140,6 +140,7 @@ Ledger::Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, b
     hdr_->pods_per_shard = pods_per_shard_for(max_pods);
     hdr_->n_nodes.store(0);
     hdr_->epoch.store(1);
+    hdr_->serving.store(1);
     hdr_->n_pods.store(0);
     hdr_->attached.store(0);
     hdr_->size_total.store(0);

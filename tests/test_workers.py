@@ -124,3 +124,126 @@ def test_ledger_refuses_a_short_or_foreign_region(tmp_path):
         for p in (short, other):
             if os.path.exists(p):
                 os.unlink(p)
+
+
+async def _start_replica(api_port, port, ledger, *extra):
+    proc = subprocess.Popen([sys.executable, "-m", "nanogpu", "--kube-api", f"http://127.0.0.1:{api_port}",
+                             "--workers", "2", "--host", "127.0.0.1", "--ledger-path", ledger,
+                             "--policyConfigPath", "/nonexistent", *extra],
+                            env=dict(os.environ, PORT=str(port)), cwd=str(ROOT),
+                            stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
+    deadline = time.time() + 60
+    while True:
+        try:
+            r, w = await asyncio.open_connection("127.0.0.1", port)
+            w.close()
+            break
+        except OSError:
+            assert time.time() < deadline and proc.poll() is None
+            await asyncio.sleep(0.2)
+    await asyncio.sleep(1.0)     # both workers listening
+    return proc
+
+
+def _stop(proc):
+    try:
+        os.killpg(proc.pid, signal.SIGTERM)
+    except ProcessLookupError:
+        return
+    try:
+        proc.wait(timeout=15)
+    except subprocess.TimeoutExpired:
+        os.killpg(proc.pid, signal.SIGKILL)
+
+
+async def _statuses(port, method, path, body=b"", n=16):
+    """`n` fresh connections (SO_REUSEPORT spreads them over the workers)."""
+    out = []
+    for _ in range(n):
+        r, w = await asyncio.open_connection("127.0.0.1", port)
+        w.write(f"{method} {path} HTTP/1.1\r\nHost: x\r\nConnection: close\r\nContent-Length: {len(body)}\r\n\r\n"
+                .encode() + body)
+        data = await r.read()
+        w.close()
+        out.append(int(data.split(b" ", 2)[1]))
+    return out
+
+
+def test_standby_replica_answers_503_on_every_worker_until_it_wins_the_lease():
+    """with --workers 2 --leader-elect only worker 0 runs the elector; every worker
+    must follow it (shared flag in the ledger), or a standby replica schedules against its
+    own ledger next to the leader's."""
+    from datetime import datetime, timedelta, timezone
+
+    async def main():
+        store = FakeKubeStore()
+        node = pu.make_node("n0", 2, synthetic_mi355x(2).to_json())
+        store.add_node(node)
+        fmt = "%Y-%m-%dT%H:%M:%S.%fZ"
+        now = datetime.now(timezone.utc)
+        store.create_lease("kube-system", {"metadata": {"name": "nano-gpu-scheduler"}, "spec": {
+            "holderIdentity": "someone-else", "leaseDurationSeconds": 4,
+            "acquireTime": now.strftime(fmt), "renewTime": now.strftime(fmt), "leaseTransitions": 0}})
+        runner, api_port = await serve(store)
+        port = _free_port()
+        ledger = f"/dev/shm/nanogpu-test-standby-{os.getpid()}"
+        proc = await _start_replica(api_port, port, ledger, "--leader-elect", "--identity", "me")
+        try:
+            pod = store.create_pod(pu.make_pod("p", [("c", 30)]))
+            body = json.dumps({"Pod": pod, "NodeNames": ["n0"]}).encode()
+            assert set(await _statuses(port, "POST", "/scheduler/filter", body)) == {503}
+            assert set(await _statuses(port, "GET", "/readyz")) == {503}
+            # the other holder stops renewing: after the lease expires this replica leads, and
+            # every worker serves
+            deadline = time.time() + 20
+            while time.time() < deadline:
+                if set(await _statuses(port, "GET", "/readyz", n=8)) == {200}:
+                    break
+                await asyncio.sleep(0.3)
+            assert set(await _statuses(port, "POST", "/scheduler/filter", body)) == {200}
+            assert store.get_lease("kube-system", "nano-gpu-scheduler")["spec"]["holderIdentity"] == "me"
+        finally:
+            _stop(proc)
+            await runner.cleanup()
+            if os.path.exists(ledger):
+                os.unlink(ledger)
+
+    asyncio.run(main())
+
+
+def test_a_crashed_worker_takes_the_replica_down_and_a_stale_region_is_not_reused():
+    async def main():
+        store = FakeKubeStore()
+        store.add_node(pu.make_node("n0", 2, synthetic_mi355x(2).to_json()))
+        runner, api_port = await serve(store)
+        port = _free_port()
+        ledger = f"/dev/shm/nanogpu-test-crash-{os.getpid()}"
+        from nanogpu import _native as N
+
+        # a region left by a killed incarnation, holding a pod that no longer exists
+        stale = N.Ledger(ledger, 4096, 131072, True)
+        t = synthetic_mi355x(2)
+        nid = stale.upsert_node("n0", t.ledger_devices(True), t.ledger_topo())
+        assert stale.allocate_plan(nid, "ghost", [(60, 0)], [[0]]) == N.OK
+        del stale
+        proc = await _start_replica(api_port, port, ledger)
+        try:
+            r, w = await asyncio.open_connection("127.0.0.1", port)
+            w.write(b"GET /status HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n")
+            status = json.loads((await r.read()).split(b"\r\n\r\n", 1)[1])
+            w.close()
+            assert [g["Percent"] for g in status["n0"]["GPUs"]] == [100, 100]   # the ghost is gone
+            workers = [int(p) for p in subprocess.check_output(["pgrep", "-P", str(proc.pid)]).split()]
+            assert len(workers) == 2
+            os.kill(workers[1], signal.SIGKILL)
+            assert proc.wait(timeout=20) != 0                 # the whole replica exits non-zero
+            for w_pid in workers:
+                assert not os.path.exists(f"/proc/{w_pid}") or \
+                    open(f"/proc/{w_pid}/stat").read().split()[2] == "Z"
+        finally:
+            _stop(proc)
+            await runner.cleanup()
+            if os.path.exists(ledger):
+                os.unlink(ledger)
+
+    asyncio.run(main())
