@@ -67,6 +67,9 @@ def parse_args():
     ap.add_argument("--json-out", default="")
     ap.add_argument("--profile-out", default="", help="cProfile the timed steps (rank 0) into this file")
     ap.add_argument("--no-nominate", action="store_true", help="priorities do not nominate (Ledger::nominate)")
+    ap.add_argument("--no-kube-combine", action="store_true",
+                    help="the stand-in takes the extender's arg-max instead of kube-scheduler's plugin + "
+                         "weighted-extender sum (nanogpu/sim/kubescore.py)")
     # the deployment's front-door settings (deploy/nano-gpu-scheduler-amd.yaml): 2 epoll
     # threads that poll 20 us after each event; `--busy-poll-us 0 --frontend-threads 4` is the
     # server's plain default (about 10 % lower here, README "Results")
@@ -263,6 +266,7 @@ def driver_main(conn) -> None:
     main process) and returns the driver stats. The scheduling cycle is serial on a blocking
     connection; binds run on a thread pool."""
     from nanogpu.sim.driver import NativeSchedulerDriver, ThreadedSchedulerDriver
+    from nanogpu.sim.kubescore import KubeScoring
 
     st = {"cfg": None, "work": {}, "session": None, "cls": NativeSchedulerDriver}
 
@@ -274,6 +278,7 @@ def driver_main(conn) -> None:
         for step in cfg["steps"]:
             pods = burst(cfg["rank"], cfg["world"], cfg["pods"], step, 7)
             work[step] = NativeSchedulerDriver.prepare(pods) if native else pods
+        cfg["kube_obj"] = KubeScoring() if cfg.get("kube") else None
         session = None
         if native:
             from nanogpu.native import core
@@ -295,7 +300,8 @@ def driver_main(conn) -> None:
             step = msg[1]
             # native: connections of the epoll binder (a bind leaves as soon as its host is
             # chosen, as kube-scheduler's per-pod bind goroutines); Python: pool threads
-            kw = {"session": session, "bind_threads": 256} if native else {"bind_threads": min(32, cfg["inflight"])}
+            kw = ({"session": session, "bind_threads": 256, "kube": cfg["kube_obj"]} if native
+                  else {"bind_threads": min(32, cfg["inflight"])})
             drv = cls("127.0.0.1", cfg["port"], cfg["names"], cfg["caps"], seed=step * 1009 + cfg["rank"], **kw)
             stats = drv.run(prepared=work.pop(step)) if native else drv.run(work.pop(step))
             drv.close()
@@ -348,6 +354,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
     if conn is not None:
         conn.send({"port": rt.bound_port, "names": names, "caps": caps, "rank": d.rank, "world": d.world,
                    "pods": args.pods, "inflight": args.inflight_binds, "driver": args.driver,
+                   "kube": not args.no_kube_combine,
                    "steps": [10_000 + w for w in range(args.warmup)] + list(range(args.steps))})
         await loop.run_in_executor(None, conn.recv)   # the stand-in has built its pods
 
@@ -368,8 +375,10 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
             summary = await loop.run_in_executor(None, conn.recv)
         else:
             # one kube-scheduler stand-in per rank; distinct tie-break streams per rank
+            from nanogpu.sim.kubescore import KubeScoring
+
             drv = SchedulerDriver(client, api, names, caps, max_inflight_binds=args.inflight_binds,
-                                  seed=step * 1009 + d.rank)
+                                  seed=step * 1009 + d.rank, kube=None if args.no_kube_combine else KubeScoring())
             tc = 0.0
             summary = (await drv.run(pods)).summary()
         ts = time.perf_counter()
@@ -448,6 +457,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
         prof = cProfile.Profile()
         prof.enable()
     sampler = StallSampler() if args.stall_trace and d.rank == 0 else None
+    nom0 = rt.state.ledger.nomination_counts()
     cpu0, loop_cpu0 = time.process_time(), time.thread_time()
     t0 = time.perf_counter()
     if sampler is not None:
@@ -470,6 +480,10 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
     d.barrier()
     d.sync()
     elapsed = time.perf_counter() - t0
+    nom1 = rt.state.ledger.nomination_counts()
+    results["nominations"] = {k: nom1[k] - nom0[k] for k in nom1}
+    results["nomination_margin"] = rt.state.ledger.nomination_margin
+    results["unschedulable_attempts"] = sum(st.get("unschedulable_attempts", 0) for st in results["steps"])
     n_sched = max(1, sum(st["scheduled"] for st in results["steps"]))
     results["cpu_us_per_pod"] = 1e6 * (time.process_time() - cpu0) / n_sched
     results["loop_cpu_us_per_pod"] = 1e6 * (time.thread_time() - loop_cpu0) / n_sched
@@ -583,6 +597,17 @@ def main() -> int:
             "frag_hbm_pct": round(statistics.mean(f["frag_mib"] for f in fr), 3) if fr else None,
             "stranded_pct": round(statistics.mean(f["stranded_pct"] for f in fr), 3) if fr else None,
             "scheduled": out["scheduled"], "failed": out["failed"], "bind_retries": out["bind_errors"],
+            # how kube-scheduler's stand-in picks among the extender's scores: its plugin +
+            # weight x 10 x extender sum ("kube", nanogpu/sim/kubescore.py) or the arg-max
+            "host_selection": "extender arg-max" if args.no_kube_combine else
+                              "kube-scheduler combining (LeastAllocated + BalancedAllocation + 10 x extender)",
+            # priorities-time nominations (shared ledger, timed steps): share adopted by the bind,
+            # moved elsewhere by kube-scheduler's own scores, and the adaptive score lead
+            "nominations": res["nominations"],
+            "nomination_adopt_pct": (round(100.0 * res["nominations"]["adopted"] / res["nominations"]["made"], 2)
+                                     if res["nominations"]["made"] else None),
+            "nomination_margin": res["nomination_margin"],
+            "unschedulable_attempts": out["unschedulable"],
             "gpu": gpu_info,
             "native_verb_mean_us": res.get("native"),
             "phase_ms_per_step_rank0": res.get("phase_ms"),
@@ -654,6 +679,7 @@ def summarize(d: Dist, args, res: dict) -> dict:
             "p99_bind_frontdoor_ms": _pct(front, 0.99),
             "p50_bind_python_ms": round(statistics.median(py), 4) if py else None,
             "scheduled": scheduled, "failed": sum(d.gather_obj(res["failed"])),
+            "unschedulable": sum(d.gather_obj(res["unschedulable_attempts"])),
             "bind_errors": sum(d.gather_obj(res["bind_errors"]))}
 
 

@@ -23,6 +23,7 @@ import aiohttp
 
 from .. import types as T
 from ..k8s import podutil as pu
+from .kubescore import KubeScoring
 
 
 class HttpExtenderClient:
@@ -241,8 +242,11 @@ class SchedulerDriver:
     def __init__(self, client, api, node_names: list[str], node_capacity: dict[str, int] | None = None,
                  max_inflight_binds: int = 64, seed: int = 0, max_attempts: int = 8,
                  backoff_s: float = 0.001, resource_fit: bool = True, send_nodes: bool = False,
-                 node_objects: dict[str, dict] | None = None):
+                 node_objects: dict[str, dict] | None = None, kube: KubeScoring | None = None):
         self.client = client
+        # kube-scheduler score combining (nanogpu/sim/kubescore.py); None: extender arg-max
+        self.kube = kube
+        self.used: dict[str, tuple[int, int]] = {n: (0, 0) for n in node_names}
         self.api = api
         self.nodes = list(node_names)
         self.node_objects = node_objects or {}
@@ -257,6 +261,24 @@ class SchedulerDriver:
         self.stats = DriverStats()
         self._binds: set[asyncio.Task] = set()
         self.placements: dict[str, str] = {}
+
+    def _select(self, prios: list[dict], pod: dict) -> str:
+        """selectHost [ext]: uniform among the max-total hosts; the total is the extender's
+        score alone, or kube-scheduler's plugin + weighted extender sum (self.kube)."""
+        if self.kube is None:
+            totals = [hp["Score"] for hp in prios]
+        else:
+            req = self.kube.pod_requests(pu.pod_demand(pod))
+            totals = [self.kube.total(hp["Score"], self.used.get(hp["Host"], (0, 0)), req) for hp in prios]
+        best = max(totals)
+        ties = [hp["Host"] for hp, t in zip(prios, totals) if t == best]
+        return ties[0] if len(ties) == 1 else ties[self.rng.randrange(len(ties))]
+
+    def _use(self, host: str, pod: dict, sign: int) -> None:
+        if self.kube is not None:
+            c, m = self.kube.pod_requests(pu.pod_demand(pod))
+            u = self.used.get(host, (0, 0))
+            self.used[host] = (u[0] + sign * c, u[1] + sign * m)
 
     def _candidates(self, need: int) -> list[str]:
         if not self.resource_fit:
@@ -299,12 +321,10 @@ class SchedulerDriver:
         else:
             args2 = {"Pod": pod, "Nodes": None, "NodeNames": fit}
             prios = await self.client.prioritize(args2)
-            # selectHost [ext]: uniform among the max-score hosts
-            best = max(hp["Score"] for hp in prios)
-            ties = [hp["Host"] for hp in prios if hp["Score"] == best]
-            host = ties[0] if len(ties) == 1 else ties[self.rng.randrange(len(ties))]
+            host = self._select(prios, pod)
         # kube-scheduler "assumes" the pod in its cache before binding asynchronously
         self.requested[host] = self.requested.get(host, 0) + need
+        self._use(host, pod, +1)
         await self.sem.acquire()
         t = asyncio.ensure_future(self._bind(rec, host, need))
         self._binds.add(t)
@@ -346,6 +366,7 @@ class SchedulerDriver:
         host = self.placements.pop(pu.pod_uid(pod), None)
         if host:
             self.requested[host] -= sum(p for p, _ in pu.pod_demand(pod))
+            self._use(host, pod, -1)
 
     async def run(self, pods: list[dict], create: bool = True) -> DriverStats:
         """Creates `pods` through the API (if `create`) and schedules all of them."""
@@ -569,8 +590,9 @@ class NativeSchedulerDriver:
 
     def __init__(self, host: str, port: int, node_names: list[str], node_capacity: dict[str, int] | None = None,
                  bind_threads: int = 256, seed: int = 0, max_attempts: int = 8, backoff_s: float = 0.001,
-                 session=None):
+                 session=None, kube: KubeScoring | None = None):
         self.host, self.port = host, port
+        self.kube = kube     # combining in C++ (same model as nanogpu/sim/kubescore.py)
         self.session = session      # core().SchedulerSession(): keep-alive connections across runs
         self.nodes = list(node_names)
         self.capacity = [int(node_capacity.get(n, 0)) for n in self.nodes] if node_capacity else []
@@ -582,14 +604,18 @@ class NativeSchedulerDriver:
         self.placements: dict[str, str] = {}
 
     @staticmethod
-    def prepare(pods: list[dict]) -> list[tuple]:
+    def prepare(pods: list[dict], kube: KubeScoring | None = None) -> list[tuple]:
         """The pods as the native loop takes them (kube-scheduler has them decoded from its
-        informer before a scheduling cycle starts; this is harness-side work)."""
+        informer before a scheduling cycle starts; this is harness-side work), with the
+        CPU / memory requests kube-scheduler's own score plugins see."""
         enc = json.JSONEncoder(separators=(",", ":"))
+        ks = kube or KubeScoring()
         args = []
         for p in pods:
             ns, name = pu.pod_ns_name(p)
-            args.append((enc.encode(p).encode(), ns, name, pu.pod_uid(p), sum(c for c, _ in pu.pod_demand(p))))
+            d = pu.pod_demand(p)
+            cpu, mem = ks.pod_requests(d)
+            args.append((enc.encode(p).encode(), ns, name, pu.pod_uid(p), sum(c for c, _ in d), cpu, mem))
         return args
 
     def run(self, pods: list[dict] | None = None, prepared: list[tuple] | None = None) -> DriverStats:
@@ -597,7 +623,9 @@ class NativeSchedulerDriver:
 
         args = prepared if prepared is not None else self.prepare(pods or [])
         r = core().drive_scheduler(self.host, self.port, args, self.nodes, self.capacity, self.bind_threads,
-                                   self.seed, self.max_attempts, self.backoff_s, self.session)
+                                   self.seed, self.max_attempts, self.backoff_s, self.session,
+                                   kube_combine=int(self.kube is not None),
+                                   extender_weight=self.kube.extender_weight if self.kube else 1)
         st = self.stats
         st.scheduled, st.failed = r["scheduled"], r["failed"]
         st.bind_errors, st.unschedulable_attempts = r["bind_errors"], r["unschedulable_attempts"]
@@ -606,7 +634,7 @@ class NativeSchedulerDriver:
         st.cycle_max_s = r.get("cycle_max_s", 0.0)
         st.cycle_sum_s = r.get("cycle_sum_s", 0.0)
         st.cycle_wire_s = r.get("cycle_wire_s", 0.0)
-        for (_, ns, name, _, _), node in zip(args, r["node_of"]):
+        for (_, ns, name, *_), node in zip(args, r["node_of"]):
             if node:
                 self.placements[f"{ns}/{name}"] = node
         return st

@@ -18,6 +18,7 @@ import statistics
 import sys
 
 from nanogpu.native import core
+from nanogpu.sim.kubescore import KubeScoring
 from nanogpu.topology.model import synthetic_mi355x, synthetic_sriov_guest
 
 N = core()
@@ -25,7 +26,8 @@ POL = {"binpack": N.Policy.BINPACK, "spread": N.Policy.SPREAD}
 
 
 class Cluster:
-    def __init__(self, topo, n_nodes: int, compat: bool, track_hbm: bool, policy: str = "binpack", seed: int = 0):
+    def __init__(self, topo, n_nodes: int, compat: bool, track_hbm: bool, policy: str = "binpack", seed: int = 0,
+                 kube: KubeScoring | None = None):
         self.L = N.Ledger("", max(64, n_nodes), 1 << 16, True)
         self.ids = [self.L.upsert_node(f"n{i:03d}", topo.ledger_devices(track_hbm), topo.ledger_topo())
                     for i in range(n_nodes)]
@@ -34,6 +36,12 @@ class Cluster:
         self.rng = random.Random(seed)
         self.live: dict[str, int] = {}
         self.unsched = 0
+        # kube-scheduler combining (None: the extender's arg-max, random ties)
+        self.kube = kube
+        if kube is not None:
+            kube.rng.seed(seed)
+        self.requested = {i: (0, 0) for i in self.ids}
+        self.pod_req: dict[str, tuple[int, int]] = {}
 
     def place(self, uid: str, demand: list) -> bool:
         if not self.track_hbm:
@@ -43,8 +51,12 @@ class Cluster:
         if not fit:
             self.unsched += 1
             return False
+        req = self.kube.pod_requests(demand) if self.kube is not None else (0, 0)
         if len(fit) == 1:
             host = fit[0]
+        elif self.kube is not None:
+            scores = self.L.score(fit, demand, self.opts)
+            host = fit[self.kube.select([self.kube.total(s, self.requested[i], req) for s, i in zip(scores, fit)])]
         else:
             scores = self.L.score(fit, demand, self.opts)
             best = max(scores)
@@ -53,11 +65,17 @@ class Cluster:
         assert rc == 0, rc
         self.L.commit(uid)
         self.live[uid] = host
+        u = self.requested[host]
+        self.requested[host] = (u[0] + req[0], u[1] + req[1])
+        self.pod_req[uid] = req
         return True
 
     def delete(self, uid: str) -> None:
-        if self.live.pop(uid, None) is not None:
+        host = self.live.pop(uid, None)
+        if host is not None:
             self.L.release(uid)
+            req, u = self.pod_req.pop(uid, (0, 0)), self.requested[host]
+            self.requested[host] = (u[0] - req[0], u[1] - req[1])
 
     def frag(self, min_req: int) -> dict:
         return self.L.frag(min_req)
@@ -72,12 +90,12 @@ class Cluster:
 
 
 def headline(compat: bool, steps: int = 20, nodes: int = 64, hbm_mib: int = 294_896, pods: int = 1000,
-             step0: int = 0, **_) -> dict:
+             step0: int = 0, kube: bool = False, **_) -> dict:
     """bench.py's workload: a 1000-pod burst of {10,25,50} % x {8,16,32,64} GiB on 64 SPX nodes,
     frag measured at peak occupancy, then the burst is deleted (bench.burst's RNG stream).
     The reference model sees the HBM requests too (the bench runs it with --compat)."""
     topo = synthetic_mi355x(8, "SPX", hbm_mib=hbm_mib)
-    c = Cluster(topo, nodes, compat, track_hbm=True, seed=1)
+    c = Cluster(topo, nodes, compat, track_hbm=True, seed=1, kube=KubeScoring() if kube else None)
     out = []
     for step in range(step0, step0 + steps):
         rng = random.Random(7 * 1000003 + step)
@@ -94,7 +112,7 @@ def headline(compat: bool, steps: int = 20, nodes: int = 64, hbm_mib: int = 294_
 
 
 def config5(compat: bool, rounds: int = 5, pods_n: int = 1000, nodes_n: int = 8, sriov: bool = False,
-            reps: int = 10, **_) -> dict:
+            reps: int = 10, kube: bool = False, **_) -> dict:
     """BASELINE config 5: CPX nodes (or SR-IOV guests), 1000-pod create/delete churn, binpack.
     The reference model has no HBM dimension (as in nanogpu.sim.configs)."""
     frs, unsched = [], 0
@@ -103,7 +121,7 @@ def config5(compat: bool, rounds: int = 5, pods_n: int = 1000, nodes_n: int = 8,
             topo, n = synthetic_sriov_guest(4), nodes_n * 2
         else:
             topo, n = synthetic_mi355x(8, "CPX"), nodes_n
-        c = Cluster(topo, n, compat, track_hbm=not compat, seed=rep)
+        c = Cluster(topo, n, compat, track_hbm=not compat, seed=rep, kube=KubeScoring() if kube else None)
         rng = random.Random(5 + rep)
         live: list[str] = []
         for r in range(rounds):
@@ -136,19 +154,20 @@ SCENARIOS = {
 }
 
 
-def run(names=None) -> dict:
+def run(names=None, kube: bool = False) -> dict:
     res = {}
     for name in names or SCENARIOS:
         fn = SCENARIOS[name]
-        res[name] = {"native": fn(False), "reference_model": fn(True)}
+        res[name] = {"native": fn(False, kube=kube), "reference_model": fn(True, kube=kube)}
     return res
 
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--scenario", action="append", choices=sorted(SCENARIOS))
+    ap.add_argument("--kube", action="store_true", help="kube-scheduler score combining (nanogpu.sim.kubescore)")
     args = ap.parse_args(argv)
-    print(json.dumps(run(args.scenario), indent=1))
+    print(json.dumps(run(args.scenario, args.kube), indent=1))
     return 0
 
 

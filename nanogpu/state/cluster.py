@@ -247,7 +247,9 @@ class ClusterState:
             return
         best = max(s for s, _ in cand)
         top = [i for s, i in cand if s == best]
-        if len(top) == 1:
+        rest = [s for s, _ in cand if s != best]
+        # the lead must survive kube-scheduler's own plugins (Ledger::nomination_margin)
+        if len(top) == 1 and (not rest or best - max(rest) >= self.ledger.nomination_margin):
             self.ledger.nominate(top[0], uid, demand, self.options)
 
     def _normalize(self, scores: list[int]) -> list[int]:

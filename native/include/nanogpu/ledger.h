@@ -79,6 +79,13 @@ struct LedgerHeader {
   // 1 while this replica may schedule: the worker running the leader elector writes it, every
   // worker (front door, Python router, /readyz) reads it. 1 without leader election.
   std::atomic<int32_t> serving;
+  // nominations (Ledger::nominate): made, adopted by their pod's bind on the same node, moved
+  // (the bind went to another node: kube-scheduler's own scores overrode ours), and the score
+  // lead a node needs over the runner-up before priorities nominate it (adaptive)
+  alignas(64) std::atomic<uint64_t> nom_made;
+  std::atomic<uint64_t> nom_adopted;
+  std::atomic<uint64_t> nom_moved;
+  std::atomic<int32_t> nom_margin;
   alignas(64) std::atomic<int64_t> n_pods;
   // learned request-size mix (Ledger::note_request): decayed counts of share sizes and the
   // set of the common ones, which native binpack's waste model uses (alloc.h SizeSet)
@@ -128,6 +135,15 @@ class Ledger {
   uint64_t generation(int32_t id) const;
   uint64_t epoch() const { return hdr_->epoch.load(std::memory_order_acquire); }
   bool serving() const { return hdr_->serving.load(std::memory_order_acquire) != 0; }
+  // Score lead over the runner-up a top node needs before priorities nominate it. Starts at
+  // 0 (any unique top node); each nomination a bind moves elsewhere raises it by 2 (to 40),
+  // every 16 adopted ones lower it by 1: nominations stay where kube-scheduler agrees.
+  int32_t nomination_margin() const { return hdr_->nom_margin.load(std::memory_order_relaxed); }
+  void nomination_counts(uint64_t* made, uint64_t* adopted, uint64_t* moved) const {
+    *made = hdr_->nom_made.load(std::memory_order_relaxed);
+    *adopted = hdr_->nom_adopted.load(std::memory_order_relaxed);
+    *moved = hdr_->nom_moved.load(std::memory_order_relaxed);
+  }
   void set_serving(bool on) { hdr_->serving.store(on ? 1 : 0, std::memory_order_release); }
 
   // Filter/score: plan for `d` on node `id`, cached per (node, generation, demand, options).

@@ -27,6 +27,8 @@ struct SimPod {
   std::string json;      // the Pod object as sent in ExtenderArgs.Pod
   std::string ns, name, uid;
   int64_t need = 0;      // Σ container gpu-percent (the pre-filter's request)
+  int64_t cpu_m = 0;     // CPU (millicores) and memory (bytes) requests: kube-scheduler's own
+  int64_t mem = 0;       // score plugins see these (nanogpu/sim/kubescore.py)
 };
 
 struct SimConfig {
@@ -38,6 +40,13 @@ struct SimConfig {
   uint64_t seed = 0;
   int max_attempts = 8;
   double backoff_s = 0.001;
+  // kube-scheduler score combining (nanogpu/sim/kubescore.py): total = LeastAllocated +
+  // BalancedAllocation (0..100 each, on CPU/memory requests) + weight x extender score x 10,
+  // random among the maxima. 0: take the extender's arg-max (random ties).
+  int kube_combine = 0;
+  int extender_weight = 1;
+  int64_t node_cpu_m = 256000;
+  int64_t node_mem = int64_t{3} << 40;
 };
 
 struct SimResult {

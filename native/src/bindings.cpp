@@ -349,6 +349,16 @@ PYBIND11_MODULE(_native, m) {
           py::arg("name"), py::arg("devices"), py::arg("topo") = py::none())
       .def_property("serving", &Ledger::serving, &Ledger::set_serving,
                     "shared across workers: whether this replica schedules (leader election)")
+      .def_property_readonly("nomination_margin", &Ledger::nomination_margin)
+      .def("nomination_counts", [](const Ledger& l) {
+        uint64_t m, a, v;
+        l.nomination_counts(&m, &a, &v);
+        py::dict d;
+        d["made"] = m;
+        d["adopted"] = a;
+        d["moved"] = v;
+        return d;
+      })
       .def("find_node", &Ledger::find_node)
       .def("node_name", &Ledger::node_name)
       .def("remove_node", &Ledger::remove_node)
@@ -616,10 +626,10 @@ PYBIND11_MODULE(_native, m) {
       .def(py::init<>());
   m.def(
       "drive_scheduler",
-      [](const std::string& host, int port, const std::vector<std::tuple<py::bytes, std::string, std::string, std::string,
-                                                                       int64_t>>& pods,
+      [](const std::string& host, int port, const py::list& pods,
          const std::vector<std::string>& nodes, const std::vector<int64_t>& capacity, int bind_threads, uint64_t seed,
-         int max_attempts, double backoff_s, std::shared_ptr<sim::Session> session) {
+         int max_attempts, double backoff_s, std::shared_ptr<sim::Session> session, int kube_combine,
+         int extender_weight) {
         sim::SimConfig cfg;
         cfg.host = host;
         cfg.port = port;
@@ -629,15 +639,24 @@ PYBIND11_MODULE(_native, m) {
         cfg.seed = seed;
         cfg.max_attempts = max_attempts;
         cfg.backoff_s = backoff_s;
+        cfg.kube_combine = kube_combine;
+        cfg.extender_weight = extender_weight;
         if (!capacity.empty() && capacity.size() != nodes.size())
           throw py::value_error("capacity must be empty or one entry per node");
         std::vector<sim::SimPod> ps(pods.size());
         for (size_t i = 0; i < pods.size(); ++i) {
-          ps[i].json = std::get<0>(pods[i]);
-          ps[i].ns = std::get<1>(pods[i]);
-          ps[i].name = std::get<2>(pods[i]);
-          ps[i].uid = std::get<3>(pods[i]);
-          ps[i].need = std::get<4>(pods[i]);
+          // (json, ns, name, uid, need[, cpu_m, mem])
+          auto t = pods[i].cast<py::tuple>();
+          if (t.size() != 5 && t.size() != 7) throw py::value_error("pod tuple: (json, ns, name, uid, need[, cpu_m, mem])");
+          ps[i].json = t[0].cast<std::string>();
+          ps[i].ns = t[1].cast<std::string>();
+          ps[i].name = t[2].cast<std::string>();
+          ps[i].uid = t[3].cast<std::string>();
+          ps[i].need = t[4].cast<int64_t>();
+          if (t.size() == 7) {
+            ps[i].cpu_m = t[5].cast<int64_t>();
+            ps[i].mem = t[6].cast<int64_t>();
+          }
         }
         sim::SimResult r;
         {
@@ -662,6 +681,6 @@ PYBIND11_MODULE(_native, m) {
       },
       py::arg("host"), py::arg("port"), py::arg("pods"), py::arg("nodes"), py::arg("capacity"),
       py::arg("bind_threads") = 256, py::arg("seed") = 0, py::arg("max_attempts") = 8, py::arg("backoff_s") = 0.001,
-      py::arg("session") = nullptr,
+      py::arg("session") = nullptr, py::arg("kube_combine") = 0, py::arg("extender_weight") = 1,
       "kube-scheduler stand-in (native/src/schedsim.cpp): schedule `pods` through the extender at host:port");
 }

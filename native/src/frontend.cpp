@@ -961,19 +961,25 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   ledger_->assume_many(ids.data(), static_cast<int>(ids.size()), dem, o, rcs.data(), scores.data());
   int64_t best = -1;
   int n_best = 0;
+  int32_t second = -1;   // best score among the other fitting nodes
   for (size_t i = 0; i < ids.size(); ++i) {
     const int32_t rc = rcs[i];
     if (rc != kOk) scores[i] = 0;
     if (rc != kOk) continue;
     if (best < 0 || scores[i] > scores[best]) {
+      if (best >= 0) second = scores[best];
       best = static_cast<int64_t>(i);
       n_best = 1;
     } else if (scores[i] == scores[best]) {
       ++n_best;
+    } else {
+      second = std::max(second, scores[i]);
     }
   }
-  // a unique winner is the node kube-scheduler picks (ties are broken at random there)
-  if (nominate && n_best == 1 && !uid.empty() && dem.n > 0) {
+  // a unique winner is the node kube-scheduler picks (ties are broken at random there) when
+  // its lead survives kube-scheduler's own score plugins (Ledger::nomination_margin)
+  const bool lead = n_best == 1 && (second < 0 || scores[best] - second >= ledger_->nomination_margin());
+  if (nominate && lead && !uid.empty() && dem.n > 0) {
     bool wants = false;
     for (int i = 0; i < dem.n; ++i) wants = wants || dem.c[i].pct > 0 || dem.c[i].mib > 0;
     if (wants) ledger_->nominate(ids[best], std::string(uid), dem, o);

@@ -18,7 +18,7 @@
 namespace nanogpu {
 
 static constexpr uint64_t kMagic = 0x4e414e4f47505531ULL;  // "NANOGPU1"
-static constexpr uint32_t kVersion = 7;  // 4: HBM pools; 5: cache lines; 6: request sizes; 7: serving
+static constexpr uint32_t kVersion = 8;  // 4: HBM pools; 5: cache lines; 6: sizes; 7: serving; 8: nominations
 
 static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -141,6 +141,10 @@ Ledger::Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, b
     hdr_->n_nodes.store(0);
     hdr_->epoch.store(1);
     hdr_->serving.store(1);
+    hdr_->nom_made.store(0);
+    hdr_->nom_adopted.store(0);
+    hdr_->nom_moved.store(0);
+    hdr_->nom_margin.store(0);
     hdr_->n_pods.store(0);
     hdr_->attached.store(0);
     hdr_->size_total.store(0);
@@ -544,6 +548,11 @@ int32_t Ledger::reserve(int32_t id, const std::string& key, const Demand& d, con
                         Plan* plan) {
   int32_t rc = reserve_as(id, key, d, o, plan, kPodReserved);
   if (rc == kNominatedElsewhere) {
+    // kube-scheduler bound the pod elsewhere than its nomination: nominate less eagerly
+    hdr_->nom_moved.fetch_add(1, std::memory_order_relaxed);
+    int32_t m = hdr_->nom_margin.load(std::memory_order_relaxed);
+    while (m < 40 && !hdr_->nom_margin.compare_exchange_weak(m, std::min(40, m + 2), std::memory_order_relaxed)) {
+    }
     release(key);
     rc = reserve_as(id, key, d, o, plan, kPodReserved);
     if (rc == kNominatedElsewhere) rc = kErrPodExists;   // re-nominated concurrently
@@ -580,6 +589,12 @@ int32_t Ledger::reserve_as(int32_t id, const std::string& key, const Demand& d, 
       if (p->state == kPodNominated) {
         if (p->node != id) return kNominatedElsewhere;
         // adopt (bind) or refresh (a repeated priorities call) the nomination
+        if (state == kPodReserved &&
+            (hdr_->nom_adopted.fetch_add(1, std::memory_order_relaxed) + 1) % 16 == 0) {
+          int32_t m = hdr_->nom_margin.load(std::memory_order_relaxed);
+          while (m > 0 && !hdr_->nom_margin.compare_exchange_weak(m, m - 1, std::memory_order_relaxed)) {
+          }
+        }
         p->state = state;
         p->t_reserved = mono_now();
         *plan = p->plan;
@@ -617,6 +632,7 @@ int32_t Ledger::reserve_as(int32_t id, const std::string& key, const Demand& d, 
   n->generation.fetch_add(1, std::memory_order_release);
   hdr_->n_pods.fetch_add(1);
   hdr_->epoch.fetch_add(1);
+  if (state == kPodNominated) hdr_->nom_made.fetch_add(1, std::memory_order_relaxed);
   note_request(d);
   return kOk;
 }

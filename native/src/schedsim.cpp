@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cctype>
+#include <cmath>
 #include <cerrno>
 #include <condition_variable>
 #include <cstring>
@@ -215,6 +216,15 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* 
   for (size_t i = 0; i < n_nodes; ++i) node_index.emplace(cfg.nodes[i], static_cast<int>(i));
   const bool fit = !cfg.capacity.empty();
   std::vector<int64_t> requested(n_nodes, 0);
+  std::vector<int64_t> req_cpu(n_nodes, 0), req_mem(n_nodes, 0);   // for kube_combine
+  // NodeResourcesLeastAllocated + NodeResourcesBalancedAllocation with the pod added
+  auto plugin_score = [&](size_t n, const SimPod& p) {
+    const double cf = std::min(1.0, static_cast<double>(req_cpu[n] + p.cpu_m) / static_cast<double>(cfg.node_cpu_m));
+    const double mf = std::min(1.0, static_cast<double>(req_mem[n] + p.mem) / static_cast<double>(cfg.node_mem));
+    const int64_t least = static_cast<int64_t>(((1.0 - cf) * 100.0 + (1.0 - mf) * 100.0) / 2.0);
+    const int64_t balanced = static_cast<int64_t>((1.0 - std::fabs(cf - mf)) * 100.0);
+    return least + balanced;
+  };
 
   auto names_json = [&](const std::vector<int>& idx) {
     std::string s = "[";
@@ -287,6 +297,8 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* 
     std::lock_guard<std::mutex> lk(mu);
     if (!err.empty()) {
       requested[job.node] -= pods[job.pod].need;
+      req_cpu[job.node] -= pods[job.pod].cpu_m;
+      req_mem[job.node] -= pods[job.pod].mem;
       ++r.bind_errors;
       r.last_error[job.pod] = std::move(err);
       requeue(job.pod);
@@ -563,12 +575,17 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* 
             doc.is(doc.root(), json::Type::kArr)) {
           int64_t best = INT64_MIN;
           ties.clear();
+          // req_cpu / req_mem also change on the binder thread (a failed bind): read under mu
+          std::unique_lock<std::mutex> plk(mu, std::defer_lock);
+          if (cfg.kube_combine) plk.lock();
           for (int32_t c = doc.at(doc.root()).first; c >= 0; c = doc.at(c).next) {
             int32_t h = doc.get(c, "Host", true), s = doc.get(c, "Score", true);
             if (!doc.is(h, json::Type::kStr) || !doc.is(s, json::Type::kNum)) continue;
             auto it = node_index.find(std::string(doc.str(h)));
             if (it == node_index.end()) continue;
             int64_t score = std::strtoll(std::string(doc.str(s)).c_str(), nullptr, 10);
+            if (cfg.kube_combine)
+              score = score * cfg.extender_weight * 10 + plugin_score(static_cast<size_t>(it->second), p);
             if (score > best) {
               best = score;
               ties.clear();
@@ -591,6 +608,8 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* 
       continue;
     }
     requested[host] += p.need;
+    req_cpu[host] += p.cpu_m;
+    req_mem[host] += p.mem;
     jobs.push_back({i, host});
     wake();
   }
