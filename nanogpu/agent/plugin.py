@@ -65,23 +65,37 @@ class Matcher:
         return [p for p in pods if pu.is_assumed(p) and not pu.is_completed(p)]
 
     async def match(self, percent: int) -> tuple[dict, dict] | None:
+        """The container kubelet is admitting: kubelet admits pods in the order they reach the
+        node (bind order; HandlePodAdditions sorts one batch by creation time) and allocates
+        a pod's containers in spec order. So: the first not-yet-allocated container asking
+        for `percent` of the earliest-bound pod (assume time, then creation time, then name).
+        An AllocateRequest carries no pod identity (device plugin v1beta1), so this order is
+        the contract; `nanogpu.sim.kubelet.admission_order` is the same order."""
         best = None
         for p in await self.candidates():
             ann = pu.meta(p).get("annotations") or {}
-            t = float(ann.get(T.ANNOTATION_ASSUME_TIME, "0") or 0)
             for c in pu.containers(p):
                 name = c.get("name", "")
                 if (pu.pod_uid(p), name) in self.claimed or T.ANNOTATION_CU_MASK_FMT.format(name) in ann:
                     continue
                 if pu.container_percent(c) != percent or pu.container_assignment(p, name) is None:
                     continue
-                if best is None or t < best[0]:
-                    best = (t, p, c)
+                key = admission_key(p)
+                if best is None or key < best[0]:
+                    best = (key, p, c)
                 break
         if best is None:
             return None
         self.claimed[(pu.pod_uid(best[1]), best[2].get("name", ""))] = time.time()
         return best[1], best[2]
+
+
+def admission_key(pod: dict) -> tuple:
+    """kubelet's admission order for pods bound to one node (see Matcher.match)."""
+    m = pu.meta(pod)
+    ann = m.get("annotations") or {}
+    return (float(ann.get(T.ANNOTATION_ASSUME_TIME, "0") or 0), m.get("creationTimestamp") or "",
+            m.get("namespace") or "", m.get("name") or "")
 
 
 class NanoGpuPlugin:

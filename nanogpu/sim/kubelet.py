@@ -18,6 +18,14 @@ from ..agent import dpapi as D
 from ..k8s import podutil as pu
 
 
+def admission_order(pods: list[dict]) -> list[dict]:
+    """Pods bound to one node in the order a kubelet admits them: as they reach the node
+    (bind order), ties by creation time. The device plugin's Matcher relies on it."""
+    from ..agent.plugin import admission_key
+
+    return sorted(pods, key=admission_key)
+
+
 class FakeKubelet:
     def __init__(self, api, node_name: str, plugin_dir: str):
         self.api = api

@@ -75,16 +75,16 @@ class FakeKubelet:
         return D.Empty()
 
 
-async def _schedule(store, node_name, pods):
-    """Places pods with the real extender (in-process verbs, no HTTP)."""
+async def _schedule(store, node_name, pods, bound=()):
+    """Places pods with the real extender (in-process verbs, no HTTP). `pods` are created
+    first; `bound` are already in the store."""
     from nanogpu.extender.verbs import Extender
     from nanogpu.state.cluster import ClusterState
 
     st = ClusterState()
     st.register_node(store.get_node(node_name))
     ext = Extender(st, InProcKube(store))
-    for p in pods:
-        p = store.create_pod(p)
+    for p in [store.create_pod(p) for p in pods] + list(bound):
         assert ext.filter({"Pod": p, "NodeNames": [node_name]})["NodeNames"] == [node_name]
         m = pu.meta(p)
         res = await ext.bind({"PodName": m["name"], "PodNamespace": m["namespace"], "PodUID": m["uid"],
@@ -181,6 +181,49 @@ def test_device_plugin_end_to_end(tmp_path):
             'device="0"} 72' in text                           # restored from annotations, "a" released
         await agent2.stop()
         await ksrv.stop(None)
+
+    asyncio.run(main())
+
+
+def test_same_percent_pods_get_their_own_devices(tmp_path):
+    """Four 60 % pods on one node land on four different GPUs (two never fit one GPU). They
+    are created in one order and bound in another, and all four requests look identical to
+    the plugin (60 IDs, no pod identity). Admitted the way kubelet does it (bind order),
+    every container is handed the device its own pod's annotation names."""
+    from nanogpu.sim.kubelet import FakeKubelet as SimKubelet, admission_order
+
+    async def main():
+        store = FakeKubeStore()
+        topo = synthetic_mi355x(8)
+        store.add_node(pu.make_node("n0", 8, topo.to_json()))
+        api = InProcKube(store)
+        kl = SimKubelet(api, "n0", str(tmp_path))
+        await kl.start()
+        agent = NodeAgent(api, "n0", topo, device_plugin=True, plugin_dir=str(tmp_path), health_period_s=0)
+        await agent.start()
+        try:
+            await asyncio.wait_for(kl.ready.wait(), 10)
+            pods = [store.create_pod(pu.make_pod(f"p{k}", [("main", 60)])) for k in range(4)]
+            # bind in reverse creation order: p3 first
+            await _schedule(store, "n0", [], bound=list(reversed(pods)))
+            bound = [store.get_pod("default", f"p{k}") for k in range(4)]
+            devs = {pu.container_assignment(p, "main")[0] for p in bound}
+            assert len(devs) == 4
+            order = admission_order(bound)
+            assert [pu.meta(p)["name"] for p in order] == ["p3", "p2", "p1", "p0"]
+            for p in order:
+                spec = await kl.admit(p)
+                assert spec["main"]["envs"]["NANO_GPU_DEVICES"] == ",".join(
+                    map(str, pu.container_assignment(p, "main"))), pu.meta(p)["name"]
+            # the CU-mask annotation landed on the pod the grant was made for
+            for p in bound:
+                cur = store.get_pod("default", pu.meta(p)["name"])
+                dev = pu.container_assignment(cur, "main")[0]
+                owner = f"{pu.pod_uid(cur)}/main"
+                assert owner in agent.plugin.cus[dev].used
+        finally:
+            await agent.stop()
+            await kl.stop()
 
     asyncio.run(main())
 

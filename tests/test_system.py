@@ -18,7 +18,7 @@ from nanogpu.k8s import podutil as pu
 from nanogpu.k8s.client import KubeClient, KubeConfig
 from nanogpu.k8s.fake_apiserver import FakeKubeStore, InProcKube, serve
 from nanogpu.sim.driver import FastExtenderClient, SchedulerDriver, node_capacities
-from nanogpu.sim.kubelet import FakeKubelet
+from nanogpu.sim.kubelet import FakeKubelet, admission_order
 from nanogpu.topology.fixtures import write_mi355x_sysfs
 
 
@@ -74,8 +74,8 @@ def test_full_stack_agent_extender_kubelet(tmp_path):
                 assert stats.scheduled == 7, stats.summary()
                 # kubelet admits each bound pod on its node through the device plugin
                 masks: dict[tuple[str, str], list[int]] = {}
-                for p in pods:
-                    cur = store.get_pod("default", pu.meta(p)["name"])
+                bound = [store.get_pod("default", pu.meta(p)["name"]) for p in pods]
+                for cur in admission_order(bound):     # kubelet admits in bind order
                     node = pu.node_name_of(cur)
                     kl = kubelets[names.index(node)]
                     spec = await kl.admit(cur)

@@ -1,14 +1,13 @@
-#!/bin/bash
-# Round-end check on one MI355X box (run through gpurun): GPU tests, smoke(), default bench.
-# Each GPU step has its own time limit; the first failure ends the script.
 set -o pipefail
-tag=${1:-v}
-mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
-  > gpurun_out/gpu_tests_$tag.log 2>&1 || exit $?
-timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke(); print('SMOKE OK')" \
-  > gpurun_out/smoke_$tag.log 2>&1 || exit $?
-timeout -k 10 250 python bench.py > gpurun_out/bench_$tag.json 2> gpurun_out/bench_$tag.err || exit $?
-tail -1 gpurun_out/gpu_tests_$tag.log
-tail -1 gpurun_out/smoke_$tag.log
-tail -1 gpurun_out/bench_$tag.json | cut -c1-200
+R=$GRAFT_REPO_ROOT
+mkdir -p $R/gpurun_out
+cd $R
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gputest.log 2>&1 || { echo "gpu tests failed rc=$?"; tail -30 gpurun_out/gputest.log; exit 1; }
+tail -5 gpurun_out/gputest.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail -30 gpurun_out/smoke.log; exit 1; }
+tail -2 gpurun_out/smoke.log
+timeout -k 10 600 python -u bench.py --steps 20 --warmup 3 > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -30 gpurun_out/bench.log; exit 1; }
+tail -1 gpurun_out/bench.log | cut -c1-1500
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run -- python3 $R/bench.py --steps 5 --warmup 1 > $R/gpurun_out/prof.log 2>&1 || { echo "prof failed"; tail -20 $R/gpurun_out/prof.log; exit 1; }
+echo done
