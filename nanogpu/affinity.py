@@ -135,3 +135,27 @@ def gpu_numa_nodes() -> list[int]:
         return [int(g.get("numa", -1)) for g in host.get("gpus", [])]
     except Exception:
         return []
+
+
+def available_cores(cgroup_root: Path = Path("/sys/fs/cgroup")) -> float:
+    """CPUs this process may actually use: its affinity mask, capped by a cgroup v2 CPU quota
+    (`cpu.max`, what a pod's `limits.cpu` becomes) or a v1 CFS quota."""
+    n = float(len(os.sched_getaffinity(0)))
+    quota = _read(cgroup_root / "cpu.max").split()
+    if len(quota) == 2 and quota[0] != "max":
+        try:
+            n = min(n, int(quota[0]) / max(1, int(quota[1])))
+        except ValueError:
+            pass
+    else:
+        q, p = _read(cgroup_root / "cpu" / "cpu.cfs_quota_us").strip(), _read(cgroup_root / "cpu" / "cpu.cfs_period_us").strip()
+        if q.lstrip("-").isdigit() and p.isdigit() and int(q) > 0 and int(p) > 0:
+            n = min(n, int(q) / int(p))
+    return n
+
+
+def busy_poll_fits(workers: int, frontend_threads: int, cores: float) -> bool:
+    """Busy-polling front-door threads only pay off while each has a core of its own: every
+    worker keeps its epoll threads plus its Python loop runnable (the same budget bench.py
+    checks per rank). With fewer cores the spinning threads would steal them."""
+    return cores >= workers * (frontend_threads + 1)

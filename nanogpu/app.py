@@ -319,7 +319,22 @@ def _drop_stale_region(path: str) -> None:
         pass
 
 
+def guard_busy_poll(cfg: Config) -> None:
+    """--busy-poll-us is switched off when the replica's CPUs cannot hold every spinning
+    front-door thread (`affinity.busy_poll_fits`)."""
+    from . import affinity
+
+    if cfg.busy_poll_us <= 0 or cfg.frontend != "native":
+        return
+    cores = affinity.available_cores()
+    if not affinity.busy_poll_fits(cfg.workers, cfg.frontend_threads, cores):
+        log.warning("busy-poll off: %d worker(s) x %d front-door threads + loops need %d cores, %.1f available",
+                    cfg.workers, cfg.frontend_threads, cfg.workers * (cfg.frontend_threads + 1), cores)
+        cfg.busy_poll_us = 0
+
+
 def run(cfg: Config) -> int:
+    guard_busy_poll(cfg)
     if cfg.workers <= 1:
         if cfg.ledger_path:
             _drop_stale_region(cfg.ledger_path)

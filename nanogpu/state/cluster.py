@@ -382,9 +382,19 @@ class ClusterState:
                           "MemoryMiBTotal": d["mib_total"], "MemoryPool": d["pool"], "GPU": d["gpu"],
                           "Partition": d["part"],
                           "Healthy": d["healthy"]} for d in snap["devices"]],
-                "PlanCache": {},
+                "PlanCache": self._plan_cache(e.id),
                 "Generation": snap["generation"],
             }
+        return out
+
+    def _plan_cache(self, node_id: int) -> dict:
+        """This process's cached plans still valid for the node (the reference dumps
+        NodeInfo.PlanCache, node.go:18-23, keyed by a demand hash). Keys are the native
+        demand/options hashes; GPUIndexes holds each container's devices ([-1]: no GPU)."""
+        out = {}
+        for dh, oh, rc, plan, score in self.ledger.cached_plans(node_id):
+            out[f"{dh:016x}/{oh:08x}"] = {"GPUIndexes": plan if rc == N.OK else [], "Score": score if rc == N.OK else 0,
+                                          "Fits": rc == N.OK}
         return out
 
     @staticmethod

@@ -10,6 +10,7 @@ Usage: python native/build.py [--force] [--no-hip] [--sanitize address|thread|un
 from __future__ import annotations
 
 import argparse
+import hashlib
 import os
 import shutil
 import subprocess
@@ -35,11 +36,28 @@ def _pybind_includes() -> list[str]:
     return [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
 
 
-def _newer(out: Path, deps: list[Path]) -> bool:
-    if not out.exists():
-        return False
-    t = out.stat().st_mtime
-    return all(d.stat().st_mtime <= t for d in deps)
+def _digest(deps: list[Path], flags: list[str]) -> str:
+    h = hashlib.sha256("\0".join(flags).encode())
+    for d in sorted(deps):
+        h.update(str(d.relative_to(ROOT) if d.is_relative_to(ROOT) else d).encode())
+        h.update(d.read_bytes())
+    return h.hexdigest()
+
+
+def _stamp(out: Path) -> Path:
+    return out.with_name(out.name + ".sha256")
+
+
+def _fresh(out: Path, deps: list[Path], flags: list[str]) -> bool:
+    """`out` was built from exactly these sources and flags (a content hash, not mtimes: a
+    copied tree or a checkout keeps stale binaries' mtimes newer than changed sources)."""
+    st = _stamp(out)
+    return out.exists() and st.exists() and st.read_text().strip() == _digest(deps, flags)
+
+
+def _done(out: Path, deps: list[Path], flags: list[str]) -> Path:
+    _stamp(out).write_text(_digest(deps, flags) + "\n")
+    return out
 
 
 def _run(cmd: list[str]) -> None:
@@ -58,7 +76,8 @@ def build_core(force: bool = False, sanitize: str | None = None) -> Path:
     srcs = [NATIVE / "src" / s for s in CORE_SOURCES] + [NATIVE / "src" / "bindings.cpp"]
     if sanitize:
         out = BUILD / f"san-{sanitize}" / "nanogpu" / f"_native{EXT}"
-    if not force and _newer(out, srcs + _headers() + [Path(__file__)]):
+    deps = srcs + _headers() + [Path(__file__)]
+    if not force and _fresh(out, deps, [sanitize or ""]):
         return out
     objdir = BUILD / (f"san-{sanitize}" if sanitize else "obj")
     objdir.mkdir(parents=True, exist_ok=True)
@@ -81,18 +100,19 @@ def build_core(force: bool = False, sanitize: str | None = None) -> Path:
     if sanitize:
         link.append(f"-fsanitize={sanitize}")
     _run(link)
-    return out
+    return _done(out, deps, [sanitize or ""])
 
 
 def build_topo_cli(force: bool = False) -> Path:
     out = NATIVE / "bin" / "nanogpu-topo"
     srcs = [NATIVE / "src" / "topo.cpp", NATIVE / "tools" / "topo_main.cpp"]
-    if not force and _newer(out, srcs + _headers()):
+    deps = srcs + _headers() + [Path(__file__)]
+    if not force and _fresh(out, deps, []):
         return out
     out.parent.mkdir(parents=True, exist_ok=True)
     _run(["g++", "-std=c++17", "-O2", f"-I{NATIVE / 'include'}", f"-I{ROCM / 'include'}",
           *[str(s) for s in srcs], "-o", str(out), "-ldl"])
-    return out
+    return _done(out, deps, [])
 
 
 SANITIZERS = {"plain": [], "asan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"],
@@ -104,13 +124,14 @@ def build_stress(kind: str = "plain", force: bool = False) -> Path:
     sources, optionally under ASan+UBSan or TSan (no GPU code involved)."""
     out = NATIVE / "bin" / f"nanogpu-stress-{kind}"
     srcs = [NATIVE / "src" / s for s in CORE_SOURCES] + [NATIVE / "tests" / "stress_main.cpp"]
-    if not force and _newer(out, srcs + _headers()):
+    deps = srcs + _headers() + [Path(__file__)]
+    if not force and _fresh(out, deps, [kind]):
         return out
     out.parent.mkdir(parents=True, exist_ok=True)
     opt = ["-O2"] if kind == "plain" else ["-O1", "-g", "-fno-omit-frame-pointer"]
     _run(["g++", "-std=c++17", *opt, *SANITIZERS[kind], f"-I{NATIVE / 'include'}", f"-I{ROCM / 'include'}",
           *[str(x) for x in srcs], "-o", str(out), "-ldl", "-lpthread"])
-    return out
+    return _done(out, deps, [kind])
 
 
 def build_probe(force: bool = False) -> Path | None:
@@ -119,13 +140,14 @@ def build_probe(force: bool = False) -> Path | None:
         return None
     out = PKG / f"_probe{EXT}"
     srcs = [NATIVE / "hip" / "probe.hip"]
-    if not force and _newer(out, srcs + _headers()):
+    deps = srcs + _headers() + [Path(__file__)]
+    if not force and _fresh(out, deps, [ARCH]):
         return out
     BUILD.mkdir(parents=True, exist_ok=True)
     _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
           "-fvisibility=hidden", "-Wno-unused-result", f"-I{NATIVE / 'include'}", *_pybind_includes(),
           str(srcs[0]), "-o", str(out)])
-    return out
+    return _done(out, deps, [ARCH])
 
 
 def build_all(force: bool = False, hip: bool = True) -> dict[str, str]:

@@ -132,6 +132,14 @@ class Ledger {
   int32_t n_nodes() const { return hdr_->n_nodes.load(std::memory_order_acquire); }
   bool remove_node(int32_t id);  // only when no pods are on it
   bool snapshot(int32_t id, NodeSnapshot* out) const;
+  // This process's plan cache for node `id`: the entries still valid at the node's current
+  // generation (the reference's NodeInfo.PlanCache dump in /status, node.go:18-23).
+  struct CachedPlan {
+    uint64_t demand_hash, options_hash;
+    int32_t rc;
+    Plan plan;
+  };
+  std::vector<CachedPlan> cached_plans(int32_t id) const;
   uint64_t generation(int32_t id) const;
   uint64_t epoch() const { return hdr_->epoch.load(std::memory_order_acquire); }
   bool serving() const { return hdr_->serving.load(std::memory_order_acquire) != 0; }

@@ -376,6 +376,19 @@ PYBIND11_MODULE(_native, m) {
              d["name"] = l.node_name(id);
              return d;
            })
+      .def("cached_plans",
+           [](const Ledger& l, int32_t id) {
+             std::vector<Ledger::CachedPlan> v;
+             {
+               py::gil_scoped_release nogil;
+               v = l.cached_plans(id);
+             }
+             py::list out;
+             for (const auto& c : v)
+               out.append(py::make_tuple(c.demand_hash, c.options_hash, c.rc, plan_list(c.plan), c.plan.score));
+             return out;
+           },
+           "Valid plan-cache entries of node `id` in this process: (demand hash, options hash, rc, plan, score).")
       .def(
           "filter",
           [](Ledger& l, const std::vector<int32_t>& ids,

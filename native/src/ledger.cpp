@@ -465,6 +465,20 @@ bool Ledger::cache_get_score(const CacheKey& k, int32_t* rc, int32_t* score) con
   return false;
 }
 
+std::vector<Ledger::CachedPlan> Ledger::cached_plans(int32_t id) const {
+  std::vector<CachedPlan> out;
+  NodeSlot* n = node(id);
+  NodeCache* cp = n ? node_cache(id, false) : nullptr;
+  if (!cp) return out;
+  const uint64_t gen = n->generation.load(std::memory_order_acquire);
+  cp->lock();
+  for (const CacheEntry& e : cp->e)
+    if (e.used.load(kRlx) && e.gen.load(kRlx) == gen)
+      out.push_back(CachedPlan{e.dh.load(kRlx), e.oh.load(kRlx), e.rc.load(kRlx), e.plan});
+  cp->unlock();
+  return out;
+}
+
 void Ledger::cache_put(const CacheKey& k, int32_t rc, const Plan& plan) {
   NodeCache* cp = node_cache(k.node, true);
   if (!cp) return;

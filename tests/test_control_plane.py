@@ -372,6 +372,26 @@ def test_bind_retries_transient_5xx_and_rolls_back_on_permanent_failure():
     asyncio.run(main())
 
 
+def test_status_dumps_the_plan_cache_valid_at_the_current_generation():
+    """/status carries each node's cached plans like the reference's NodeInfo.PlanCache
+    (node.go:18-23); a change to the node (a bind) invalidates them."""
+    store = FakeKubeStore()
+    store.add_node(node("n0", 2))
+    st, ext = _ext(store)
+    p = store.create_pod(pu.make_pod("a", [("c", 30)]))
+    ext.filter({"Pod": p, "NodeNames": ["n0"]})
+    big = store.create_pod(pu.make_pod("b", [("c", 100), ("d", 100), ("e", 100)]))
+    ext.filter({"Pod": big, "NodeNames": ["n0"]})
+    cache = st.status()["n0"]["PlanCache"]
+    fits = [v for v in cache.values() if v["Fits"]]
+    assert len(fits) == 1 and fits[0]["GPUIndexes"] == [[0]] and fits[0]["Score"] > 0
+    assert any(not v["Fits"] and v["GPUIndexes"] == [] for v in cache.values())   # 3 GPUs on a 2-GPU node
+    json.dumps(st.status())
+    r = asyncio.run(_bind(ext, store, p))
+    assert r["Error"] == ""
+    assert st.status()["n0"]["PlanCache"] == {}      # computed at an older generation
+
+
 def test_bind_conflict_on_already_bound_same_node_is_success():
     async def main():
         store = FakeKubeStore()

@@ -7,6 +7,7 @@ from pathlib import Path
 import yaml
 
 from nanogpu import cli
+from nanogpu.affinity import available_cores, busy_poll_fits
 from nanogpu import types as T
 from nanogpu.agent import node as agent
 from nanogpu.config.policy import parse_policy
@@ -28,8 +29,11 @@ def test_extender_deployment_args_parse():
     c = _container("nano-gpu-scheduler-amd.yaml", "Deployment")
     assert c["command"][-2:] == ["-m", "nanogpu"]
     cfg = cli.parse(c["args"])
-    assert cfg.priority == "binpack" and cfg.workers == 4 and cfg.leader_elect
+    assert cfg.priority == "binpack" and cfg.workers == 2 and cfg.leader_elect
     assert cfg.frontend_threads == 2 and cfg.busy_poll_us == 20 and cfg.cpu_affinity == "auto"
+    # the CPU request holds every busy-polling thread (else the server turns polling off)
+    cpu = float(c["resources"]["requests"]["cpu"])
+    assert busy_poll_fits(cfg.workers, cfg.frontend_threads, cpu)
     ports = {p["containerPort"] for p in c.get("ports", [])}
     env = {e["name"]: e.get("value") for e in c.get("env", [])}
     assert int(env.get("PORT", 39999)) in ports or not ports
@@ -59,3 +63,18 @@ def test_scheduler_config_matches_the_served_routes():
     assert {r["name"] for r in ext["managedResources"]} == {T.RESOURCE_GPU_PERCENT, T.RESOURCE_GPU_MEMORY}
     legacy = json.loads((DEPLOY / "scheduler-policy.json").read_text())["extenders"][0]
     assert legacy["filterVerb"] == ext["filterVerb"] and legacy["bindVerb"] == ext["bindVerb"]
+
+
+def test_busy_poll_guard_reads_the_cgroup_quota(tmp_path, monkeypatch):
+    from nanogpu import app
+
+    (tmp_path / "cpu.max").write_text("400000 100000\n")          # limits.cpu: 4
+    assert available_cores(tmp_path) <= 4.0
+    monkeypatch.setattr("nanogpu.affinity.available_cores", lambda *a: 4.0)
+    cfg = app.Config(workers=4, frontend_threads=2, busy_poll_us=20)
+    app.guard_busy_poll(cfg)
+    assert cfg.busy_poll_us == 0                                   # 12 cores needed
+    monkeypatch.setattr("nanogpu.affinity.available_cores", lambda *a: 6.0)
+    cfg = app.Config(workers=2, frontend_threads=2, busy_poll_us=20)
+    app.guard_busy_poll(cfg)
+    assert cfg.busy_poll_us == 20
