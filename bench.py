@@ -25,8 +25,10 @@ workers share ONE native ledger in /dev/shm (the SO_REUSEPORT replica design of
 nanogpu.app), each drives 1/N of the burst through its own HTTP endpoint, so the burst and
 the cluster are fixed while workers are added ("strong" scaling). The GPUs are used for the
 node model: each rank reads its MI355X through the native KFD/amdsmi reader + HIP probe
-(HBM copy rate), and with N > 1 one RCCL all-reduce over all ranks measures the ring bus
-bandwidth (per-link xGMI rate) that the topology scorer uses. All of that is untimed.
+(HBM copy rate); the xGMI link weights the topology scorer uses come from the peer-pull probe
+over every pair of visible GPUs (all ranks together), else from the rate KFD publishes for the
+links (`measured_links`). With N > 1 the RCCL all-reduce busBW is reported as a labelled
+collective aggregate. All of that is untimed.
 Data: synthetic pods; cluster of `--nodes` simulated nodes cloned from the discovered MI355X.
 """
 from __future__ import annotations
@@ -201,6 +203,37 @@ class StallSampler:
 
 
 # --------------------------------------------------------------------------- node template
+def measured_links(d: Dist, host: dict, gpus_per_node: int) -> tuple[float, list | None, str]:
+    """Per-link xGMI weights for the node model (per direction, GB/s): the peer-pull probe
+    over every visible pair when this job sees the node's GPUs (all ranks take part), else
+    the rate KFD publishes for this GPU's links (a 1-GPU container still sees them), else
+    the placeholder. A probe failure is recorded and never aborts the bench."""
+    from nanogpu.probe.calibrate import link_matrix, reader_link_gbs
+
+    link, src = 153.0, "placeholder (no xGMI link visible)"
+    rd = reader_link_gbs(host)
+    if rd > 0:
+        link, src = rd, "kfd io_link max_bandwidth (native topology reader)"
+    if not d.cuda:
+        return link, None, src
+    import torch
+
+    ndev = torch.cuda.device_count()
+    try:
+        m = None
+        if d.dist is not None and d.world == ndev and d.world > 1:
+            m = link_matrix(ndev, dist=d.dist, rank=d.local_rank)
+        elif d.dist is None and ndev > 1:
+            m = link_matrix(ndev)
+        if m is not None:
+            off = [v for a, r in enumerate(m) for b, v in enumerate(r) if a != b]
+            src = f"peer-pull probe, {ndev} GPUs, every pair (copy kernel over xGMI)"
+            return min(off), (m if ndev == gpus_per_node else None), src
+    except Exception as e:
+        src += f"; peer probe failed: {type(e).__name__}: {e}"
+    return link, None, src
+
+
 def node_template(d: Dist, args) -> tuple[object, dict]:
     from nanogpu.topology.model import synthetic_mi355x
 
@@ -224,14 +257,23 @@ def node_template(d: Dist, args) -> tuple[object, dict]:
             from nanogpu.probe.calibrate import hbm_bandwidth
 
             info["gpu"]["hbm_copy_gbs"] = round(hbm_bandwidth(d.local_rank, 1 << 30, 10), 1)
-    link = 153.0
-    if d.dist is not None and d.cuda:
-        from nanogpu.probe.calibrate import ring_busbw
+    link, matrix = 153.0, None
+    if not args.no_gpu:
+        link, matrix, src = measured_links(d, facts["host"], args.gpus_per_node)
+        info["link_bw_source"] = src
+        if matrix is not None:
+            info["link_bw_matrix_gbs"] = [[round(v, 1) for v in r] for r in matrix]
+        if d.dist is not None and d.cuda:
+            # RCCL all-reduce busBW over all ranks: a collective aggregate, labelled as such
+            try:
+                from nanogpu.probe.calibrate import ring_busbw
 
-        link = ring_busbw(d.dist, d.device)
-        info["link_bw_source"] = f"rccl all-reduce busBW over {d.world} ranks"
+                info["rccl_allreduce_busbw_gbs"] = round(ring_busbw(d.dist, d.device), 1)
+            except Exception as e:
+                info["rccl_allreduce_busbw_gbs"] = f"error: {type(e).__name__}: {e}"
     info["link_bw_gbs"] = round(link, 1)
-    topo = synthetic_mi355x(args.gpus_per_node, args.partition, hbm_mib=hbm_mib, link_gbs=link)
+    topo = synthetic_mi355x(args.gpus_per_node, args.partition, hbm_mib=hbm_mib, link_gbs=link,
+                            link_matrix=matrix)
     if info["gpu"]:
         topo.calibration = {k: v for k, v in info["gpu"].items() if k in ("hbm_copy_gbs", "cus")}
     return topo, info

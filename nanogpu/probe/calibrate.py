@@ -4,8 +4,15 @@
   partition modes, NUMA) for the GPU this process owns;
 * hbm_bandwidth()    — streaming-copy GB/s from the HIP probe kernel;
 * cu_mask_isolation()— bf16 MFMA TFLOP/s on CU-masked streams (the agent's spatial share);
+* link_matrix()      — per-pair xGMI rates (GB/s, one direction) from the peer-pull probe:
+  what the topology scorer weights GPU groups with. Single process: every visible pair in
+  turn. One rank per GPU: rank r pulls from (r + k) % n in round k, so each round is a
+  permutation and every link direction carries exactly one transfer; rows are all-gathered.
+* reader_link_gbs()  — the per-link rate KFD publishes (io_link max_bandwidth), when the
+  peers themselves are hidden from this process (a 1-GPU container still sees its links).
 * ring_busbw()       — RCCL all-reduce bus bandwidth across the job's ranks (torch.distributed
-  backend "nccl" = RCCL on ROCm): the per-link xGMI rate that feeds the topology scorer.
+  backend "nccl" = RCCL on ROCm). An aggregate collective figure: on a full xGMI mesh RCCL
+  drives several links at once, so it is reported as such and never as a per-link rate.
 """
 from __future__ import annotations
 
@@ -57,11 +64,48 @@ def cu_mask_isolation(device: int = 0, fractions=(1, 2, 4, 8), iters: int = 2048
     return out
 
 
+def reader_link_gbs(host: dict) -> float:
+    """Slowest xGMI link of the first visible GPU as KFD reports it, GB/s (0: none)."""
+    gpus = host.get("gpus") or []
+    return float(gpus[0].get("xgmi_min_bw_mbs", 0)) / 1000.0 if gpus else 0.0
+
+
+def link_matrix(n: int, nbytes: int = 64 << 20, iters: int = 3, dist=None, rank: int = 0) -> list[list[float]]:
+    """n x n per-direction GB/s, m[src][dst], from the peer-pull probe (0 on the diagonal)."""
+    P = probe(required=True)
+    m = [[0.0] * n for _ in range(n)]
+    if dist is None:
+        for dst in range(n):
+            for src in range(n):
+                if src != dst:
+                    m[src][dst] = P.peer_bandwidth(src, dst, nbytes, iters)["gbs"]
+        return m
+    import torch
+
+    row = [0.0] * n                      # this rank's GPU as the destination
+    for k in range(1, n):
+        src = (rank + k) % n
+        dist.barrier()
+        try:                             # a failed pair must not leave the other ranks waiting
+            row[src] = P.peer_bandwidth(src, rank, nbytes, iters)["gbs"]
+        except Exception:
+            row[src] = -1.0
+    torch.cuda.set_device(rank)
+    t = torch.tensor(row, dtype=torch.float64, device=torch.device("cuda", rank))
+    rows = [torch.zeros_like(t) for _ in range(n)]
+    dist.all_gather(rows, t)
+    for dst, r in enumerate(rows):
+        for src, v in enumerate(r.tolist()):
+            m[src][dst] = v
+    if any(v < 0 for r in m for v in r):  # every rank sees the same gathered matrix
+        raise RuntimeError("peer_bandwidth failed on some pair")
+    return m
+
+
 def ring_busbw(dist, device, nbytes: int = 256 << 20, iters: int = 5) -> float:
     """RCCL all-reduce bus bandwidth (GB/s) over all ranks of the job, one collective on the
-    default group (no sub-communicators). On a fully connected 8x MI355X xGMI mesh a ring
-    all-reduce is bound by one link per step, so busBW = 2(n-1)/n x bytes / t estimates the
-    per-link bandwidth the topology scorer weights groups with."""
+    default group: busBW = 2(n-1)/n x bytes / t. A collective aggregate (several xGMI links
+    at once on a full mesh), not a per-link rate."""
     import torch
 
     n = dist.get_world_size()

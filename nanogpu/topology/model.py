@@ -130,11 +130,12 @@ def fallback_topology(n_devices: int) -> NodeTopology:
 
 def synthetic_mi355x(n_gpus: int = 8, compute: str = "SPX", memory: str = "NPS1",
                      hbm_mib: int = 288 * 1024, link_gbs: float = 153.0,
-                     gpus_per_numa: int = 4) -> NodeTopology:
+                     gpus_per_numa: int = 4, link_matrix: list[list[float]] | None = None) -> NodeTopology:
     """An 8x MI355X platform (full xGMI mesh, 4 GPUs per socket) for tests and benches.
 
     `link_gbs` is a placeholder until the probe measures it; the agent overwrites it with
-    what KFD/amdsmi or the peer-copy probe report.
+    what KFD/amdsmi or the peer-copy probe report. `link_matrix` (n_gpus x n_gpus GB/s, as
+    measured by `probe.calibrate.link_matrix`) replaces the uniform mesh when given.
     """
     parts = PARTITIONS[compute]
     nps = _nps(memory)
@@ -147,7 +148,12 @@ def synthetic_mi355x(n_gpus: int = 8, compute: str = "SPX", memory: str = "NPS1"
             devs.append(DeviceSpec(gpu=g, part=p, cus=T.MI355X_CUS // parts,
                                    xcds=max(1, T.MI355X_XCDS // parts)))
         _assign_pools([d for d in devs if d.gpu == g], hbm_mib // nps, nps)
-    bw = [[0.0 if a == b else link_gbs for b in range(n_gpus)] for a in range(n_gpus)]
+    if link_matrix is not None and len(link_matrix) == n_gpus:
+        # a link's weight is the slower of its two directions
+        bw = [[0.0 if a == b else min(link_matrix[a][b], link_matrix[b][a]) for b in range(n_gpus)]
+              for a in range(n_gpus)]
+    else:
+        bw = [[0.0 if a == b else link_gbs for b in range(n_gpus)] for a in range(n_gpus)]
     return NodeTopology(gpus=gpus, devices=devs, link_bw=bw, virtualization="BAREMETAL")
 
 

@@ -10,12 +10,13 @@
 //   * mfma_burn   — bf16 MFMA throughput of a masked stream (isolation check: TFLOP/s
 //                   must scale with the CUs granted);
 //   * hbm_copy    — streaming HBM3E bandwidth (16 B/lane, grid >> 256 WGs);
-//   * peer_copy   — xGMI peer bandwidth between two GPUs (link weights for the scorer).
+//   * peer_bandwidth — per-pair xGMI rate: copy kernel pulling over peer access, and SDMA
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <memory>
@@ -422,11 +423,24 @@ std::vector<double> mixed_colocated(int dev, const std::vector<uint32_t>& hbm_ma
   return {gbs, tf};
 }
 
-double peer_bandwidth(int src, int dst, size_t bytes, int iters) {
-  int n = 0;
-  HIP_OK(hipGetDeviceCount(&n));
-  if (src < 0 || dst < 0 || src >= n || dst >= n || src == dst)
+struct PeerRate {
+  double pull_gbs;   // copy kernel on `dst` reading `src`'s HBM over xGMI (one link, one direction)
+  double dma_gbs;    // hipMemcpyPeerAsync (SDMA engines) over the same link
+  bool peer_access;
+};
+
+// Per-pair link rate for the topology scorer. The copy kernel runs on the destination GPU and
+// loads straight from the peer's memory (peer access enabled), so every byte crosses the one
+// xGMI link between the pair in one direction; its grid (n / 4096 WGs, >> 256 CUs) keeps
+// enough loads in flight to saturate the link rather than one SDMA engine.
+PeerRate peer_bandwidth(int src, int dst, size_t bytes, int iters) {
+  int n_dev = 0;
+  HIP_OK(hipGetDeviceCount(&n_dev));
+  if (src < 0 || dst < 0 || src >= n_dev || dst >= n_dev || src == dst)
     throw std::invalid_argument("peer_bandwidth: need two distinct visible devices");
+  const size_t n = bytes / sizeof(float4);
+  if (n == 0 || iters <= 0) throw std::invalid_argument("peer_bandwidth: bytes/iters must be positive");
+  PeerRate r{0.0, 0.0, false};
   int can = 0;
   HIP_OK(hipDeviceCanAccessPeer(&can, dst, src));
   HIP_OK(hipSetDevice(dst));
@@ -434,23 +448,37 @@ double peer_bandwidth(int src, int dst, size_t bytes, int iters) {
     hipError_t e = hipDeviceEnablePeerAccess(src, 0);
     if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIP_OK(e);
     (void)hipGetLastError();
+    r.peer_access = true;
   }
-  void* d_dst = nullptr;
-  HIP_OK(hipMalloc(&d_dst, bytes));
   HIP_OK(hipSetDevice(src));
-  void* d_src = nullptr;
-  HIP_OK(hipMalloc(&d_src, bytes));
-  Stream st({});
-  Events ev;
-  HIP_OK(hipMemcpyPeerAsync(d_dst, dst, d_src, src, bytes, st.s));
-  HIP_OK(hipEventRecord(ev.a, st.s));
-  for (int i = 0; i < iters; ++i) HIP_OK(hipMemcpyPeerAsync(d_dst, dst, d_src, src, bytes, st.s));
-  HIP_OK(hipEventRecord(ev.b, st.s));
-  const double ms = ev.ms();
-  (void)hipFree(d_src);
+  DevBuf<float4> a(n);
+  HIP_OK(hipMemset(a.p, 0, n * sizeof(float4)));
+  HIP_OK(hipDeviceSynchronize());
   HIP_OK(hipSetDevice(dst));
-  (void)hipFree(d_dst);
-  return static_cast<double>(bytes) * iters / (ms * 1e-3) / 1e9;
+  DevBuf<float4> b(n);
+  {
+    Stream st({});
+    Events ev;
+    HIP_OK(hipMemcpyPeerAsync(b.p, dst, a.p, src, n * sizeof(float4), st.s));   // warm-up
+    HIP_OK(hipEventRecord(ev.a, st.s));
+    for (int i = 0; i < iters; ++i) HIP_OK(hipMemcpyPeerAsync(b.p, dst, a.p, src, n * sizeof(float4), st.s));
+    HIP_OK(hipEventRecord(ev.b, st.s));
+    r.dma_gbs = static_cast<double>(n * sizeof(float4)) * iters / (ev.ms() * 1e-3) / 1e9;
+  }
+  if (r.peer_access) {
+    Stream st({});
+    Events ev;
+    const dim3 grid(copy_grid(n));
+    hipLaunchKernelGGL(hbm_copy, grid, dim3(kCopyBlock), 0, st.s, a.p, b.p, n);   // warm-up
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(ev.a, st.s));
+    for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(hbm_copy, grid, dim3(kCopyBlock), 0, st.s, a.p, b.p, n);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(ev.b, st.s));
+    r.pull_gbs = static_cast<double>(n * sizeof(float4)) * iters / (ev.ms() * 1e-3) / 1e9;
+  }
+  HIP_OK(hipDeviceSynchronize());
+  return r;
 }
 
 }  // namespace
@@ -486,7 +514,21 @@ PYBIND11_MODULE(_probe, m) {
   m.def("mfma_colocated", &mfma_colocated, py::arg("device"), py::arg("cu_masks"), py::arg("blocks"),
         py::arg("iters") = 2048, py::call_guard<py::gil_scoped_release>(),
         "Concurrent MFMA burns on CU-masked streams; per-stream TFLOP/s.");
-  m.def("peer_bandwidth", &peer_bandwidth, py::arg("src"), py::arg("dst"),
-        py::arg("bytes") = size_t(256) << 20, py::arg("iters") = 10,
-        py::call_guard<py::gil_scoped_release>(), "hipMemcpyPeer bandwidth in GB/s.");
+  m.def(
+      "peer_bandwidth",
+      [](int src, int dst, size_t bytes, int iters) {
+        PeerRate r;
+        {
+          py::gil_scoped_release nogil;
+          r = peer_bandwidth(src, dst, bytes, iters);
+        }
+        py::dict d;
+        d["pull_gbs"] = r.pull_gbs;
+        d["dma_gbs"] = r.dma_gbs;
+        d["peer_access"] = r.peer_access;
+        d["gbs"] = std::max(r.pull_gbs, r.dma_gbs);
+        return d;
+      },
+      py::arg("src"), py::arg("dst"), py::arg("bytes") = size_t(256) << 20, py::arg("iters") = 10,
+      "One-direction xGMI rate src -> dst in GB/s: copy kernel pulling over peer access, and SDMA.");
 }

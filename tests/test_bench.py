@@ -1,4 +1,4 @@
-"""bench.py contract (single rank and a 2-rank gloo job) and the BASELINE config harness."""
+"""bench.py contract (single rank and 2- and 4-rank gloo jobs) and the BASELINE config harness."""
 import asyncio
 import json
 import os
@@ -6,6 +6,8 @@ import socket
 import subprocess
 import sys
 from pathlib import Path
+
+import pytest
 
 ROOT = Path(__file__).resolve().parent.parent
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
@@ -37,16 +39,38 @@ def test_bench_single_rank_cpu():
     assert d["p50_bind_ms"] is not None and 0 <= d["frag_pct"] <= 100
 
 
-def test_bench_two_ranks_gloo():
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_bench_multi_rank_gloo(ranks):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
                         "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
-                        "--gpus", "2", "--no-gpu", "--steps", "2", "--warmup", "1", "--pods", "200", "--nodes", "8"],
-                       capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
+                        "--gpus", str(ranks), "--no-gpu", "--steps", "2", "--warmup", "1", "--pods", "200",
+                        "--nodes", "8", "--rtt-variant-steps", "1"],
+                       capture_output=True, text=True, timeout=400, env=env, cwd="/tmp")
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
-    assert d["n_gpus"] == 2 and d["scheduled"] == 400 and d["failed"] == 0
-    assert "2 extender worker" in d["config"]["parallelism"]
+    assert d["n_gpus"] == ranks and d["scheduled"] == 400 and d["failed"] == 0
+    assert f"{ranks} extender worker" in d["config"]["parallelism"]
+    assert d["value_rtt2ms"] and d["p50_bind_ms"] is not None
+
+
+def test_link_weights_fall_back_to_the_reader_and_a_matrix_sets_the_mesh():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", ROOT / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    d = bench.Dist(1)                          # no GPU: no probe
+    host = {"gpus": [{"xgmi_min_bw_mbs": 76000}]}
+    link, m, src = bench.measured_links(d, host, 8)
+    assert link == 76.0 and m is None and "kfd io_link" in src
+    link, m, src = bench.measured_links(d, {"gpus": [{}]}, 8)
+    assert link == 153.0 and src.startswith("placeholder")
+    from nanogpu.topology.model import synthetic_mi355x
+
+    mat = [[0.0, 70.0, 60.0], [50.0, 0.0, 65.0], [61.0, 64.0, 0.0]]
+    t = synthetic_mi355x(3, link_matrix=mat)
+    assert t.link_bw[0][1] == t.link_bw[1][0] == 50.0 and t.link_bw[1][2] == 64.0 and t.link_bw[0][0] == 0.0
 
 
 def test_config_harness_plumbing_and_topology():
