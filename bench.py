@@ -64,6 +64,13 @@ def parse_args():
     ap.add_argument("--rtt-variant-ms", type=float, default=2.0,
                     help="after the timed steps, a second pass with this API round trip (0: none)")
     ap.add_argument("--rtt-variant-steps", type=int, default=3)
+    ap.add_argument("--shared-api", action="store_true",
+                    help="one API server for the whole job over HTTP (the native API server, "
+                         "native/src/apiserver.cpp, in its own process): every rank's extender talks "
+                         "REST to it and only rank 0 runs the pod controller, as worker 0 of a replica")
+    ap.add_argument("--shared-variant-steps", type=int, default=3,
+                    help="after the timed steps, a pass with --shared-api (0: none)")
+    ap.add_argument("--apiserver-threads", type=int, default=4, help="--shared-api: API server IO threads")
     ap.add_argument("--inflight-binds", type=int, default=64)
     ap.add_argument("--no-gpu", action="store_true", help="skip GPU discovery (CPU-only rehearsal)")
     ap.add_argument("--json-out", default="")
@@ -119,6 +126,9 @@ class Dist:
     def barrier(self):
         if self.dist is not None:
             if self.cuda:
+                import torch
+
+                torch.cuda.set_device(self.local_rank)   # also when called from a helper thread
                 self.dist.barrier(device_ids=[self.local_rank])
             else:
                 self.dist.barrier()
@@ -301,6 +311,92 @@ def burst(rank: int, world: int, total: int, step: int, seed: int) -> list[dict]
     return pods
 
 
+def apiserver_main(conn, threads: int) -> None:
+    """The shared API server's process: a native API server (native/src/apiserver.cpp) on its
+    own L3 domain, plus a command pipe through which rank 0 plays the workload's clients
+    (bulk create / delete of a step's pods; the pod JSON is shipped before the clock starts)."""
+    import json as _json
+
+    from nanogpu import affinity
+    from nanogpu.native import core
+
+    try:   # off the ranks' CCDs: widen the inherited mask, then take the least busy domain
+        os.sched_setaffinity(0, range(os.cpu_count() or 1))
+    except OSError:
+        pass
+    affinity.apply(affinity.pick_cpus())
+    srv = core().ApiServer("127.0.0.1", 0, threads, 1 << 20)
+    steps: dict = {}
+    conn.send(srv.port)
+    while True:
+        msg = conn.recv()
+        op = msg[0]
+        if op == "nodes":
+            for n in msg[1]:
+                srv.call("POST", "/api/v1/nodes", n)
+            conn.send(len(msg[1]))
+        elif op == "load":
+            steps[msg[1]] = msg[2]
+            conn.send(True)
+        elif op == "create":
+            texts = steps[msg[1]]
+            codes = srv.create_pods(texts)
+            conn.send(sum(1 for c in codes if c == 201))
+        elif op == "delete":
+            keys = []
+            for t in steps.pop(msg[1]):
+                m = _json.loads(t)["metadata"]
+                keys.append((m.get("namespace", "default"), m["name"]))
+            conn.send(srv.delete_pods(keys))
+        elif op == "stats":
+            conn.send(_json.loads(srv.stats()))
+        else:
+            srv.stop()
+            conn.send(True)
+            return
+
+
+class ApiServerProc:
+    """Rank 0's handle on the shared API server process."""
+
+    def __init__(self, threads: int):
+        import multiprocessing as mp
+
+        ctx = mp.get_context("spawn")
+        self.conn, child = ctx.Pipe()
+        self.proc = ctx.Process(target=apiserver_main, args=(child, threads), daemon=True)
+        self.proc.start()
+        self.url = f"http://127.0.0.1:{self.conn.recv()}"
+
+    def _rpc(self, *msg):
+        self.conn.send(msg)
+        return self.conn.recv()
+
+    def add_nodes(self, nodes: list[dict]) -> None:
+        self._rpc("nodes", [json.dumps(n, separators=(",", ":")) for n in nodes])
+
+    def load(self, step: int, pods: list[dict]) -> None:
+        self._rpc("load", step, [json.dumps(p, separators=(",", ":")) for p in pods])
+
+    def create(self, step: int) -> int:
+        return self._rpc("create", step)
+
+    def delete(self, step: int) -> int:
+        return self._rpc("delete", step)
+
+    def stats(self) -> dict:
+        return self._rpc("stats")
+
+    def close(self) -> None:
+        try:
+            self._rpc("stop")
+        except (OSError, EOFError):
+            pass
+        self.proc.join(10)
+        if self.proc.is_alive():
+            self.proc.terminate()
+
+
 def driver_main(conn) -> None:
     """kube-scheduler stand-in in its own process (as in a real cluster): for each pass of
     the bench it receives the extender's address and the pass's steps, builds their pods,
@@ -365,34 +461,64 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
     from nanogpu.k8s.fake_apiserver import Faults, FakeKubeStore, InProcKube
     from nanogpu.sim.driver import FastExtenderClient, SchedulerDriver, node_capacities
 
-    # the watch history a real API server keeps is a bounded cache, and not in our process
-    store = FakeKubeStore(history=8192, faults=Faults(latency_s=args.api_rtt_ms / 1e3))
+    # --shared-api: ONE API server for the job, as in a cluster: the native API server in its
+    # own process (ApiServerProc), reached over HTTP by every rank's extender. Only rank 0 runs
+    # the pod controller (worker 0 of a replica), so every release goes through its watch.
+    # Rank 0 is also the workload's client: it has the API server create and delete every
+    # rank's pods. Without it each rank has an in-process store of its own (extender-isolated).
+    shared = bool(getattr(args, "shared_api", False)) and conn is not None
+    loop = asyncio.get_running_loop()
+
+    async def barrier() -> None:
+        if shared:   # keep the loop turning (watch, controller) while other ranks catch up
+            await loop.run_in_executor(None, d.barrier)
+        else:
+            d.barrier()
+
     topo_json = topo.to_json()
     n_dev = len(topo.devices)
     nodes = [pu.make_node(f"mi355x-{i:03d}", n_dev, topo_json, {"amd.com/gpu.present": "true"})
              for i in range(args.nodes)]
-    for n in nodes:
-        store.add_node(n)
+    store, apisrv = None, None
+    if shared:
+        url = None
+        if d.rank == 0:
+            apisrv = ApiServerProc(args.apiserver_threads)
+            apisrv.add_nodes(nodes)
+            url = apisrv.url
+        url = d.bcast_obj(url)
+        from nanogpu.k8s.client import KubeClient, KubeConfig
+
+        rt_api = KubeClient(KubeConfig(server=url), pool=args.inflight_binds + 8)
+    else:
+        # the watch history a real API server keeps is a bounded cache, and not in our process
+        store = FakeKubeStore(history=8192, faults=Faults(latency_s=args.api_rtt_ms / 1e3))
+        for n in nodes:
+            store.add_node(n)
+        rt_api = InProcKube(store)
     cfg = Config(port=0, host="127.0.0.1", priority=args.policy, compat=args.compat, ledger_path=ledger_path,
                  max_nodes=max(1024, args.nodes), max_pods=max(65536, 4 * args.pods),
                  policy_config_path="/nonexistent/policy.yaml", reservation_ttl_s=3600,
                  busy_poll_us=args.busy_poll_us, frontend_threads=args.frontend_threads,
                  nominate=not args.no_nominate)
-    rt = Runtime(cfg, worker=0, api=InProcKube(store))
+    all_steps_pre = [10_000 + w for w in range(args.warmup)] + list(range(args.steps))
+    rt = Runtime(cfg, worker=d.rank if shared else 0, api=rt_api)
     await rt.start()
     client = FastExtenderClient("127.0.0.1", rt.bound_port, pool=args.inflight_binds + 8)
     names = [pu.meta(n)["name"] for n in nodes]
     caps = node_capacities(nodes)
-    api = InProcKube(store)
-    pod_ctrl = rt.controllers[-1]
+    api = InProcKube(store) if store is not None else None   # the workload's client (creates, deletes)
+    if apisrv is not None:
+        for st in all_steps_pre:
+            apisrv.load(st, [p for r in range(d.world) for p in burst(r, d.world, args.pods, st, 7)])
+    pod_ctrl = rt.controllers[-1] if rt.leader else None
     results = {"steps": [], "frag": [], "client_bind_ms": [], "frontdoor_bind_ms": []}
 
     # synthetic pod objects are generated up front (client-side data, not scheduler work);
     # their creation in the API server, scheduling, deletion and release are all timed
-    bursts = {s: burst(d.rank, d.world, args.pods, s, 7) for s in
-              [10_000 + w for w in range(args.warmup)] + list(range(args.steps))}
+    all_steps = [10_000 + w for w in range(args.warmup)] + list(range(args.steps))
+    bursts = {s: burst(d.rank, d.world, args.pods, s, 7) for s in all_steps}
 
-    loop = asyncio.get_running_loop()
     if conn is not None:
         conn.send({"port": rt.bound_port, "names": names, "caps": caps, "rank": d.rank, "world": d.world,
                    "pods": args.pods, "inflight": args.inflight_binds, "driver": args.driver,
@@ -407,12 +533,17 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
             # the pods are created in the API server (this process), then the scheduler
             # process schedules them through the extender's HTTP front door. A burst comes
             # from many clients at once: with a modelled API RTT the creates overlap.
-            if args.api_rtt_ms > 0:
-                await asyncio.gather(*(api.create_pod(p) for p in pods))
-            else:
-                for p in pods:
-                    await api.create_pod(p)
+            if api is not None:
+                if args.api_rtt_ms > 0:
+                    await asyncio.gather(*(api.create_pod(p) for p in pods))
+                else:
+                    for p in pods:
+                        await api.create_pod(p)
+            elif apisrv is not None:
+                await loop.run_in_executor(None, apisrv.create, step)   # every rank's pods
             tc = time.perf_counter() - tc
+            if shared:
+                await barrier()                     # every rank's pods exist
             conn.send(("step", step))
             summary = await loop.run_in_executor(None, conn.recv)
         else:
@@ -425,14 +556,17 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
             summary = (await drv.run(pods)).summary()
         ts = time.perf_counter()
         # all ranks finished their share of the burst: peak occupancy
-        d.barrier()
+        await barrier()
         frag = rt.state.frag(min(SIZES))
-        ns = f"bench-r{d.rank}"
-        for p in pods:
-            try:
-                store.delete_pod(ns, pu.meta(p)["name"])
-            except Exception:
-                pass
+        if store is not None:
+            for p in pods:
+                m = pu.meta(p)
+                try:
+                    store.delete_pod(m["namespace"], m["name"])
+                except Exception:
+                    pass
+        elif apisrv is not None:
+            await loop.run_in_executor(None, apisrv.delete, step)
         # the pod controller releases on DELETED; wait until our shares are gone
         # (the in-process watch delivers the DELETED events on the next loop iterations: yield
         # first, and only then back off to short sleeps)
@@ -443,7 +577,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
             if not lookup(uids[-1]) and not any(lookup(u) for u in uids):
                 break
             await asyncio.sleep(0 if i < 50 else 0.0005)
-        await pod_ctrl.queue.drain(5.0)
+        if pod_ctrl is not None:
+            await pod_ctrl.queue.drain(5.0)
         phases = {"create_ms": 1e3 * tc, "schedule_ms": 1e3 * summary["span_s"],
                   "release_ms": 1e3 * (time.perf_counter() - ts)}
         walls = rt.native.fe.take_bind_wall() if rt.native is not None else []
@@ -490,7 +625,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
     for w in range(args.warmup):
         await one_step(10_000 + w, False)
     rt.tracer.buf.clear()
-    d.barrier()
+    await barrier()
     d.sync()
     prof = None
     if args.profile_out and d.rank == 0:
@@ -519,7 +654,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
         buf = io.StringIO()
         pstats.Stats(prof, stream=buf).sort_stats(os.environ.get("NANOGPU_PROF_SORT", "tottime")).print_stats(45)
         Path(args.profile_out).write_text(buf.getvalue())
-    d.barrier()
+    await barrier()
     d.sync()
     elapsed = time.perf_counter() - t0
     nom1 = rt.state.ledger.nomination_counts()
@@ -545,7 +680,12 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
     results["failed"] = sum(s["failed"] for s in results["steps"])
     results["bind_errors"] = sum(s["bind_errors"] for s in results["steps"])
     await client.close()
+    if apisrv is not None:
+        results["apiserver"] = apisrv.stats()
+    await barrier()          # no rank still talks to the shared API server
     await rt.stop()
+    if apisrv is not None:
+        apisrv.close()
     return results
 
 
@@ -587,7 +727,7 @@ def main() -> int:
     d = Dist(args.gpus)
     d.init(use_gpu=not args.no_gpu)
     topo, gpu_info = node_template(d, args)
-    variant = None
+    variant = shared_v = None
     try:
         res = run_pass(d, args, topo, conn, "main")
         if args.rtt_variant_ms > 0:
@@ -600,6 +740,15 @@ def main() -> int:
                 variant = summarize(d, v_args, run_pass(d, v_args, topo, conn, "rtt"))
             except Exception as e:   # the headline result stands; say what failed
                 variant = {"error": f"{type(e).__name__}: {e}"}
+        if args.shared_variant_steps > 0 and not args.shared_api and not args.inproc_driver:
+            # the same bursts through ONE HTTP API server shared by every rank (the native one)
+            s_args = argparse.Namespace(**{**vars(args), "shared_api": True, "api_rtt_ms": 0.0,
+                                           "steps": args.shared_variant_steps, "warmup": 1,
+                                           "profile_out": "", "stall_trace": ""})
+            try:
+                shared_v = summarize(d, s_args, run_pass(d, s_args, topo, conn, "shared"))
+            except Exception as e:
+                shared_v = {"error": f"{type(e).__name__}: {e}"}
     finally:
         if drv_proc is not None:
             try:
@@ -623,8 +772,10 @@ def main() -> int:
                        "cluster": f"{args.nodes} nodes x {args.gpus_per_node} MI355X ({args.partition})",
                        "api_rtt_ms": args.api_rtt_ms,
                        # value is the extender's throughput: the API server is an in-process
-                       # store per rank with no round trip (see value_rtt*ms for a modelled one)
-                       "api_server": "in-process store per rank, extender-isolated",
+                       # store per rank with no round trip (see value_rtt*ms for a modelled one,
+                       # value_shared_api for one API server shared by all ranks)
+                       "api_server": ("one native HTTP API server for all ranks, own process"
+                                      if args.shared_api else "in-process store per rank, extender-isolated"),
                        "cpus_rank0": _cpulist(cpus),
                        "frontend": f"{args.frontend_threads} threads, busy-poll {args.busy_poll_us} us"},
             # POST /scheduler/bind wall time as kube-scheduler's stand-in sees it (request
@@ -673,6 +824,15 @@ def main() -> int:
                 line[f"p50_bind_ms_{tag}"] = variant["p50_bind_ms"]
                 line[f"p99_bind_ms_{tag}"] = variant["p99_bind_ms"]
                 line[f"steps_{tag}"] = args.rtt_variant_steps
+        if shared_v is not None:
+            if "error" in shared_v:
+                line["value_shared_api"] = None
+                line["error_shared_api"] = shared_v["error"]
+            else:
+                line["value_shared_api"] = shared_v["value"]
+                line["p50_bind_ms_shared_api"] = shared_v["p50_bind_ms"]
+                line["p99_bind_ms_shared_api"] = shared_v["p99_bind_ms"]
+                line["steps_shared_api"] = args.shared_variant_steps
         print(json.dumps(line), flush=True)
         if args.json_out:
             Path(args.json_out).write_text(json.dumps(line, indent=1))

@@ -46,6 +46,8 @@ class Config:
     max_nodes: int = 4096
     max_pods: int = 131072
     verify_pod_on_bind: bool = False
+    native_bind_writes: bool = True             # C++ writer threads do the bind's API writes
+    bind_writer_threads: int = 32
     reservation_ttl_s: float = 60.0
     nominate: bool = True              # priorities nominate the top node (Ledger::nominate)
     nomination_ttl_s: float = 5.0
@@ -194,6 +196,13 @@ class Runtime:
                 self.native = server.NativeServer(router, self.cfg.host, self.cfg.port, self.cfg.frontend_threads)
                 self.native.fe.set_serving(True)   # the ledger's shared flag gates it as well
                 self.native.fe.set_busy_poll_us(self.cfg.busy_poll_us)
+                api_cfg = getattr(self.api, "config", None)
+                if self.cfg.native_bind_writes and not self.cfg.verify_pod_on_bind and api_cfg is not None:
+                    ext = self.extender
+                    if self.native.enable_native_writes(api_cfg, self.cfg.bind_writer_threads, ext.api_retries,
+                                                        ext.record_events):
+                        log.info("worker %d: bind API writes in native writer threads (%d)", self.worker,
+                                 self.cfg.bind_writer_threads)
                 self.native.start()
                 self.bound_port = self.native.port
             else:

@@ -55,6 +55,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--kube-api", default=None, help="API server URL (default: KUBECONFIG or in-cluster)")
     p.add_argument("--host", default="0.0.0.0")
     p.add_argument("--bind-verify-pod", action="store_true", help="GET the pod on every bind (reference behaviour)")
+    p.add_argument("--native-bind-writes", action=argparse.BooleanOptionalAction, default=True,
+                   help="the native front door's C++ threads do each bind's PATCH + binding POST + commit "
+                        "(native/src/kubewriter.cpp); --no-native-bind-writes keeps them in Python")
+    p.add_argument("--bind-writer-threads", type=int, default=32,
+                   help="native bind writers: concurrent binds in flight to kube-apiserver")
     p.add_argument("--reservation-ttl", default="60s")
     p.add_argument("--no-nominate", action="store_true",
                    help="priorities do not tentatively reserve the top-scored node")
@@ -102,7 +107,8 @@ def parse(argv: list[str] | None = None) -> Config:
         kube_api=a.kube_api, compat=a.compat, score_normalize=a.score_normalize,
         topology_weight=a.topology_weight, track_hbm=not a.no_hbm, workers=max(1, a.workers),
         ledger_path=a.ledger_path, max_nodes=a.max_nodes, max_pods=a.max_pods,
-        verify_pod_on_bind=a.bind_verify_pod, reservation_ttl_s=parse_duration(a.reservation_ttl),
+        verify_pod_on_bind=a.bind_verify_pod, native_bind_writes=a.native_bind_writes,
+        bind_writer_threads=max(1, a.bind_writer_threads), reservation_ttl_s=parse_duration(a.reservation_ttl),
         nominate=not a.no_nominate, nomination_ttl_s=parse_duration(a.nomination_ttl),
         fake_cluster=a.fake_cluster, fake_gpus_per_node=a.fake_gpus_per_node, fake_partition=a.fake_partition,
         seed=a.seed, frontend=a.frontend, frontend_threads=max(1, a.frontend_threads), busy_poll_us=a.busy_poll_us,

@@ -374,7 +374,38 @@ class NativeServer:
                   f"nanogpu_native_deferred_total {s['python']['deferred']}",
                   "# TYPE nanogpu_native_connections_total counter",
                   f"nanogpu_native_connections_total {s['connections']}"]
+        kw = self.fe.kube_writer_stats()
+        if kw is not None:
+            lines += ["# HELP nanogpu_native_binds_total binds finished by the native API writer",
+                      "# TYPE nanogpu_native_binds_total counter",
+                      f'nanogpu_native_binds_total{{result="ok"}} {kw["ok"]}',
+                      f'nanogpu_native_binds_total{{result="error"}} {kw["failed"]}',
+                      "# TYPE nanogpu_native_bind_rollbacks_total counter",
+                      f"nanogpu_native_bind_rollbacks_total {kw['rollbacks']}",
+                      "# TYPE nanogpu_native_api_retries_total counter",
+                      f"nanogpu_native_api_retries_total {kw['retries']}",
+                      "# HELP nanogpu_native_api_write_seconds_total time in the bind's API writes",
+                      "# TYPE nanogpu_native_api_write_seconds_total counter",
+                      f'nanogpu_native_api_write_seconds_total{{op="patch"}} {kw["patch_seconds_total"]:.9f}',
+                      f'nanogpu_native_api_write_seconds_total{{op="binding"}} {kw["binding_seconds_total"]:.9f}',
+                      "# TYPE nanogpu_native_binds_inflight gauge",
+                      f"nanogpu_native_binds_inflight {kw['inflight']}"]
         return ("\n".join(lines) + "\n").encode()
+
+    def enable_native_writes(self, config, threads: int, retries: int, record_events: bool) -> bool:
+        """Hands the bind's API writes to the front door's C++ writer threads (native/src/
+        kubewriter.cpp) when the API server is a REST endpoint this process reaches with a
+        bearer token or a client certificate; False (Python writes) otherwise."""
+        from urllib.parse import urlsplit
+
+        u = urlsplit(config.server)
+        if u.scheme not in ("http", "https") or not u.hostname:
+            return False
+        tls = u.scheme == "https"
+        self.fe.set_kube_writer(u.hostname, u.port or (443 if tls else 80), tls, config.token or "",
+                                config.token_file or "", config.ca_file or "", config.cert_file or "",
+                                config.key_file or "", bool(config.insecure), threads, retries, record_events)
+        return True
 
     async def stop(self) -> None:
         if self._loop is not None:

@@ -598,6 +598,11 @@ def make_app(store: FakeKubeStore) -> web.Application:
         items, rv = store.list_nodes(ls)
         return listing("NodeList", items, rv)
 
+    @routes.post("/api/v1/nodes")
+    async def create_node(request):
+        await lat()
+        return web.json_response(store.add_node(await request.json()), status=201)
+
     @routes.get("/api/v1/nodes/{name}")
     async def get_node(request):
         await lat()

@@ -27,7 +27,8 @@ ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 ARCH = os.environ.get("NANOGPU_OFFLOAD_ARCH", "gfx950")
 
-CORE_SOURCES = ["alloc.cpp", "ledger.cpp", "topo.cpp", "json.cpp", "frontend.cpp", "schedsim.cpp"]
+CORE_SOURCES = ["alloc.cpp", "ledger.cpp", "topo.cpp", "json.cpp", "frontend.cpp", "schedsim.cpp", "apiserver.cpp",
+                "kubewriter.cpp"]
 
 
 def _pybind_includes() -> list[str]:
@@ -96,7 +97,7 @@ def build_core(force: bool = False, sanitize: str | None = None) -> Path:
 
     with ThreadPoolExecutor(max_workers=min(4, os.cpu_count() or 1)) as ex:
         objs = list(ex.map(compile_one, srcs))
-    link = ["g++", "-shared", *[str(o) for o in objs], "-o", str(out), "-ldl", "-lpthread"]
+    link = ["g++", "-shared", *[str(o) for o in objs], "-o", str(out), "-ldl", "-lpthread", "-lssl", "-lcrypto"]
     if sanitize:
         link.append(f"-fsanitize={sanitize}")
     _run(link)
@@ -130,7 +131,7 @@ def build_stress(kind: str = "plain", force: bool = False) -> Path:
     out.parent.mkdir(parents=True, exist_ok=True)
     opt = ["-O2"] if kind == "plain" else ["-O1", "-g", "-fno-omit-frame-pointer"]
     _run(["g++", "-std=c++17", *opt, *SANITIZERS[kind], f"-I{NATIVE / 'include'}", f"-I{ROCM / 'include'}",
-          *[str(x) for x in srcs], "-o", str(out), "-ldl", "-lpthread"])
+          *[str(x) for x in srcs], "-o", str(out), "-ldl", "-lpthread", "-lssl", "-lcrypto"])
     return _done(out, deps, [kind])
 
 

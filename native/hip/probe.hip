@@ -441,6 +441,12 @@ PeerRate peer_bandwidth(int src, int dst, size_t bytes, int iters) {
   const size_t n = bytes / sizeof(float4);
   if (n == 0 || iters <= 0) throw std::invalid_argument("peer_bandwidth: bytes/iters must be positive");
   PeerRate r{0.0, 0.0, false};
+  int prev = 0;   // the caller's current device comes back on return (torch tracks it)
+  HIP_OK(hipGetDevice(&prev));
+  struct Restore {
+    int d;
+    ~Restore() { (void)hipSetDevice(d); }
+  } restore{prev};
   int can = 0;
   HIP_OK(hipDeviceCanAccessPeer(&can, dst, src));
   HIP_OK(hipSetDevice(dst));

@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "nanogpu/alloc.h"
+#include "nanogpu/kubewriter.h"
 #include "nanogpu/ledger.h"
 
 namespace nanogpu {
@@ -107,6 +108,10 @@ class Frontend {
                bool notify = true);
   void wake_workers();
   void stop();
+  // Native bind writes: from now on a bind whose reservation succeeded here is finished by
+  // KubeWriter threads (PATCH + binding + commit / rollback) without Python. Set once.
+  void set_kube_writer(const KubeTarget& t, int threads, int retries, bool record_events);
+  const KubeWriter* kube_writer() const { return writer_.load(std::memory_order_acquire); }
   // The native filter / priorities verb on a request body (what a worker runs per request);
   // false = the request needs the Python path.
   bool filter_verb(std::string_view body, bool prioritize, std::string* out);
@@ -142,6 +147,8 @@ class Frontend {
   void note_bind_wall(uint64_t ns);
 
   std::shared_ptr<Ledger> ledger_;
+  std::unique_ptr<KubeWriter> writer_owner_;
+  std::atomic<KubeWriter*> writer_{nullptr};
   int port_ = 0;
   int py_efd_ = -1;
   std::atomic<bool> stop_{false};

@@ -1,0 +1,1202 @@
+// Native in-memory Kubernetes API server (see apiserver.h).
+//
+// Behaviour mirrors nanogpu/k8s/fake_apiserver.py (the Python store the in-process tests use):
+// same routes, status codes and Status bodies, merge-patch semantics, binding conflicts, and
+// the watch cache (bounded history per kind, resume from a resourceVersion, 410 Gone when the
+// version is older than what the cache holds).
+#include "nanogpu/apiserver.h"
+
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstring>
+#include <ctime>
+#include <deque>
+#include <map>
+#include <mutex>
+#include <random>
+#include <stdexcept>
+#include <unordered_map>
+
+#include "nanogpu/frontend.h"
+#include "nanogpu/json.h"
+
+namespace nanogpu::apisrv {
+
+// ------------------------------------------------------------------------------ JSON value
+const JV* JV::get(std::string_view k) const {
+  if (t != T::kObj) return nullptr;
+  for (const auto& kv : o)
+    if (kv.first == k) return &kv.second;
+  return nullptr;
+}
+JV* JV::get(std::string_view k) { return const_cast<JV*>(static_cast<const JV*>(this)->get(k)); }
+
+JV& JV::set(std::string_view k, JV v) {
+  if (t != T::kObj) {
+    *this = obj();
+  }
+  for (auto& kv : o)
+    if (kv.first == k) return kv.second = std::move(v);
+  o.emplace_back(std::string(k), std::move(v));
+  return o.back().second;
+}
+
+JV& JV::child(std::string_view k) {
+  JV* c = get(k);
+  if (c && c->t == T::kObj) return *c;
+  return set(k, obj());
+}
+
+void JV::erase(std::string_view k) {
+  for (size_t i = 0; i < o.size(); ++i)
+    if (o[i].first == k) {
+      o.erase(o.begin() + static_cast<long>(i));
+      return;
+    }
+}
+
+namespace {
+JV from_doc(const json::Doc& d, int32_t i) {
+  JV v;
+  const json::Node& n = d.at(i);
+  switch (n.type) {
+    case json::Type::kNull: break;
+    case json::Type::kBool: v.t = JV::T::kBool, v.b = n.b; break;
+    case json::Type::kNum: v.t = JV::T::kNum, v.s = std::string(d.str(i)); break;
+    case json::Type::kStr: v.t = JV::T::kStr, v.s = std::string(d.str(i)); break;
+    case json::Type::kArr:
+      v.t = JV::T::kArr;
+      v.a.reserve(static_cast<size_t>(n.count));
+      for (int32_t c = n.first; c >= 0; c = d.at(c).next) v.a.push_back(from_doc(d, c));
+      break;
+    case json::Type::kObj:
+      v.t = JV::T::kObj;
+      v.o.reserve(static_cast<size_t>(n.count));
+      for (int32_t c = n.first; c >= 0; c = d.at(c).next) v.o.emplace_back(std::string(d.key(c)), from_doc(d, c));
+      break;
+  }
+  return v;
+}
+}  // namespace
+
+bool parse(std::string_view text, JV* out) {
+  json::Doc d;
+  if (!d.parse(text) || d.root() < 0) return false;
+  *out = from_doc(d, d.root());
+  return true;
+}
+
+void dump(const JV& v, std::string* out) {
+  switch (v.t) {
+    case JV::T::kNull: out->append("null"); break;
+    case JV::T::kBool: out->append(v.b ? "true" : "false"); break;
+    case JV::T::kNum: out->append(v.s); break;
+    case JV::T::kStr: json::append_quoted(out, v.s); break;
+    case JV::T::kArr:
+      out->push_back('[');
+      for (size_t i = 0; i < v.a.size(); ++i) {
+        if (i) out->push_back(',');
+        dump(v.a[i], out);
+      }
+      out->push_back(']');
+      break;
+    case JV::T::kObj:
+      out->push_back('{');
+      for (size_t i = 0; i < v.o.size(); ++i) {
+        if (i) out->push_back(',');
+        json::append_quoted(out, v.o[i].first);
+        out->push_back(':');
+        dump(v.o[i].second, out);
+      }
+      out->push_back('}');
+      break;
+  }
+}
+
+void merge_patch(JV* target, const JV& patch) {
+  if (patch.t != JV::T::kObj) {
+    *target = patch;
+    return;
+  }
+  if (target->t != JV::T::kObj) *target = JV::obj();
+  for (const auto& kv : patch.o) {
+    if (kv.second.t == JV::T::kNull) {
+      target->erase(kv.first);
+    } else if (kv.second.t == JV::T::kObj) {
+      JV* cur = target->get(kv.first);
+      if (!cur) cur = &target->set(kv.first, JV::obj());
+      merge_patch(cur, kv.second);
+    } else {
+      target->set(kv.first, kv.second);
+    }
+  }
+}
+
+namespace {
+
+// ------------------------------------------------------------------------------ helpers
+std::string str_of(const JV* v) { return v && v->t == JV::T::kStr ? v->s : std::string(); }
+
+std::string now_rfc3339() {
+  const std::time_t t = std::time(nullptr);
+  std::tm g{};
+  gmtime_r(&t, &g);
+  char buf[32];
+  std::strftime(buf, sizeof buf, "%Y-%m-%dT%H:%M:%SZ", &g);
+  return buf;
+}
+
+std::string new_uid() {
+  static thread_local std::mt19937_64 rng{std::random_device{}() ^
+                                           static_cast<uint64_t>(std::hash<std::thread::id>{}(std::this_thread::get_id()))};
+  const uint64_t a = rng(), b = rng();
+  char buf[40];
+  std::snprintf(buf, sizeof buf, "%08x-%04x-4%03x-%04x-%012llx", static_cast<unsigned>(a >> 32),
+                static_cast<unsigned>((a >> 16) & 0xffff), static_cast<unsigned>(a & 0xfff),
+                static_cast<unsigned>(0x8000 | ((b >> 48) & 0x3fff)),
+                static_cast<unsigned long long>(b & 0xffffffffffffULL));
+  return buf;
+}
+
+std::string url_decode(std::string_view s) {
+  std::string out;
+  out.reserve(s.size());
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '+') {
+      out.push_back(' ');
+    } else if (s[i] == '%' && i + 2 < s.size() && std::isxdigit(static_cast<unsigned char>(s[i + 1])) &&
+               std::isxdigit(static_cast<unsigned char>(s[i + 2]))) {
+      out.push_back(static_cast<char>(std::stoi(std::string(s.substr(i + 1, 2)), nullptr, 16)));
+      i += 2;
+    } else {
+      out.push_back(s[i]);
+    }
+  }
+  return out;
+}
+
+std::vector<std::string_view> split(std::string_view s, char c) {
+  std::vector<std::string_view> out;
+  size_t p = 0;
+  while (p <= s.size()) {
+    const size_t q = s.find(c, p);
+    const size_t e = q == std::string_view::npos ? s.size() : q;
+    out.push_back(s.substr(p, e - p));
+    if (q == std::string_view::npos) break;
+    p = q + 1;
+  }
+  return out;
+}
+
+std::string_view trim(std::string_view s) {
+  while (!s.empty() && (s.front() == ' ' || s.front() == '\t')) s.remove_prefix(1);
+  while (!s.empty() && (s.back() == ' ' || s.back() == '\t' || s.back() == '\r')) s.remove_suffix(1);
+  return s;
+}
+
+std::string status_body(int code, std::string_view reason, std::string_view message) {
+  std::string b = "{\"kind\":\"Status\",\"apiVersion\":\"v1\",\"status\":\"Failure\",\"message\":";
+  json::append_quoted(&b, message);
+  b += ",\"reason\":";
+  json::append_quoted(&b, reason);
+  b += ",\"code\":" + std::to_string(code) + "}";
+  return b;
+}
+
+const char* reason_phrase(int code) {
+  switch (code) {
+    case 200: return "OK";
+    case 201: return "Created";
+    case 400: return "Bad Request";
+    case 404: return "Not Found";
+    case 405: return "Method Not Allowed";
+    case 409: return "Conflict";
+    case 410: return "Gone";
+    case 413: return "Payload Too Large";
+    case 422: return "Unprocessable Entity";
+    default: return "Status";
+  }
+}
+
+// ------------------------------------------------------------------------------ store
+enum Kind { kPods = 0, kNodes = 1, kKinds = 2 };
+
+struct Obj {
+  JV v;
+  std::string json;
+  std::string ns, name, uid, node, phase;
+  uint64_t rv = 0;
+  const JV* labels() const {
+    const JV* m = v.get("metadata");
+    return m ? m->get("labels") : nullptr;
+  }
+};
+using ObjP = std::shared_ptr<const Obj>;
+
+// Stamps the resourceVersion, extracts the indexed fields and serializes once.
+ObjP seal(JV v, uint64_t rv) {
+  auto o = std::make_shared<Obj>();
+  JV& m = v.child("metadata");
+  m.set("resourceVersion", JV::str(std::to_string(rv)));
+  o->ns = str_of(m.get("namespace"));
+  o->name = str_of(m.get("name"));
+  o->uid = str_of(m.get("uid"));
+  if (const JV* sp = v.get("spec")) o->node = str_of(sp->get("nodeName"));
+  if (const JV* st = v.get("status")) o->phase = str_of(st->get("phase"));
+  o->rv = rv;
+  o->v = std::move(v);
+  dump(o->v, &o->json);
+  return o;
+}
+
+struct Selector {
+  struct Term {
+    std::string k, v;
+    int op;  // 0 =, 1 !=, 2 exists
+  };
+  std::vector<Term> terms;
+  static Selector parse(std::string_view s) {
+    Selector out;
+    for (std::string_view t : split(s, ',')) {
+      t = trim(t);
+      if (t.empty()) continue;
+      Term x;
+      size_t p;
+      if ((p = t.find("!=")) != std::string_view::npos) {
+        x = {std::string(trim(t.substr(0, p))), std::string(trim(t.substr(p + 2))), 1};
+      } else if ((p = t.find('=')) != std::string_view::npos) {
+        std::string_view v = t.substr(p + 1);
+        if (!v.empty() && v.front() == '=') v.remove_prefix(1);
+        x = {std::string(trim(t.substr(0, p))), std::string(trim(v)), 0};
+      } else {
+        x = {std::string(t), std::string(), 2};
+      }
+      out.terms.push_back(std::move(x));
+    }
+    return out;
+  }
+  bool labels_match(const Obj& o) const {
+    const JV* l = o.labels();
+    for (const Term& t : terms) {
+      const JV* v = l ? l->get(t.k) : nullptr;
+      if (t.op == 0 && (!v || v->sv() != t.v)) return false;
+      if (t.op == 1 && v && v->sv() == t.v) return false;
+      if (t.op == 2 && !v) return false;
+    }
+    return true;
+  }
+  bool fields_match(const Obj& o) const {
+    for (const Term& t : terms) {
+      std::string_view have;
+      if (t.k == "spec.nodeName") have = o.node;
+      else if (t.k == "metadata.name") have = o.name;
+      else if (t.k == "metadata.namespace") have = o.ns;
+      else if (t.k == "status.phase") have = o.phase;
+      else continue;
+      if ((t.op == 0) != (have == t.v)) return false;
+    }
+    return true;
+  }
+};
+
+struct Ev {
+  uint64_t rv;
+  ObjP obj;
+  std::shared_ptr<const std::string> line;   // {"type":..,"object":..}\n
+};
+
+std::shared_ptr<const std::string> ev_line(const char* type, const std::string& obj_json) {
+  auto s = std::make_shared<std::string>();
+  s->reserve(obj_json.size() + 32);
+  *s += "{\"type\":\"";
+  *s += type;
+  *s += "\",\"object\":";
+  *s += obj_json;
+  *s += "}\n";
+  return s;
+}
+
+struct Conn;
+
+struct Watch {
+  int kind;
+  Selector ls, fs;
+  std::shared_ptr<Conn> conn;
+};
+
+struct ApiErr {
+  int code;
+  std::string reason, message;
+};
+
+}  // namespace
+
+// ------------------------------------------------------------------------------ connection
+namespace {
+struct IoThread;
+
+struct Conn {
+  int fd = -1;
+  IoThread* owner = nullptr;
+  std::string in;
+  std::string out;                 // owner thread only
+  // watch stream state
+  std::mutex mu;                   // guards pending / ended (written by store writers)
+  std::string pending;             // event lines not yet framed
+  bool ended = false;              // the stream is to be terminated after pending
+  std::atomic<bool> queued{false}; // on the owner's flush list
+  bool watching = false;
+  double deadline = 0;             // steady seconds; 0 = none
+  bool close_after = false;
+};
+
+double steady_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+struct IoThread {
+  int ep = -1, efd = -1;
+  std::thread th;
+  std::mutex mu;
+  std::vector<std::shared_ptr<Conn>> flush;   // watch conns with pending output
+  std::unordered_map<int, std::shared_ptr<Conn>> conns;
+  void wake(const std::shared_ptr<Conn>& c) {
+    if (c->queued.exchange(true)) return;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      flush.push_back(c);
+    }
+    const uint64_t one = 1;
+    (void)!write(efd, &one, sizeof one);
+  }
+};
+}  // namespace
+
+struct Server::Impl {
+  Config cfg;
+  int lfd = -1;
+  std::atomic<bool> stopping{false};
+  std::vector<std::unique_ptr<IoThread>> io;
+
+  // ---- store (under mu)
+  mutable std::mutex mu;
+  uint64_t rv = 0;
+  std::unordered_map<std::string, ObjP> pods;          // "ns/name"
+  std::map<std::string, ObjP> nodes;
+  std::map<std::string, ObjP> leases;                  // "ns/name"
+  std::deque<Ev> hist[kKinds];
+  uint64_t compacted[kKinds] = {0, 0};
+  std::vector<Watch> watches;
+  std::atomic<uint64_t> n_create{0}, n_get{0}, n_patch{0}, n_bind{0}, n_delete{0}, n_list{0}, n_watch{0},
+      n_events{0}, n_requests{0}, n_lease{0};
+  uint64_t bindings = 0;
+
+  static std::string key(std::string_view ns, std::string_view name) {
+    std::string k(ns);
+    k.push_back('/');
+    k.append(name);
+    return k;
+  }
+
+  // -- emit under mu
+  void emit(int kind, const char* type, const ObjP& o) {
+    Ev e{o->rv, o, ev_line(type, o->json)};
+    for (const Watch& w : watches) {
+      if (w.kind != kind) continue;
+      if (!w.ls.labels_match(*o) || !w.fs.fields_match(*o)) continue;
+      {
+        std::lock_guard<std::mutex> g(w.conn->mu);
+        if (w.conn->ended) continue;
+        w.conn->pending += *e.line;
+      }
+      w.conn->owner->wake(w.conn);
+    }
+    auto& h = hist[kind];
+    h.push_back(std::move(e));
+    while (h.size() > cfg.history) h.pop_front();
+  }
+
+  // -- pods
+  ObjP create_pod_locked(JV v, std::string_view ns_path) {
+    JV& m = v.child("metadata");
+    if (!ns_path.empty()) m.set("namespace", JV::str(std::string(ns_path)));
+    if (str_of(m.get("namespace")).empty()) m.set("namespace", JV::str("default"));
+    if (str_of(m.get("name")).empty()) throw ApiErr{422, "Invalid", "metadata.name: Required value"};
+    if (str_of(m.get("uid")).empty()) m.set("uid", JV::str(new_uid()));
+    if (!m.get("creationTimestamp")) m.set("creationTimestamp", JV::str(now_rfc3339()));
+    JV& st = v.child("status");
+    if (!st.get("phase")) st.set("phase", JV::str("Pending"));
+    const std::string k = key(str_of(m.get("namespace")), str_of(m.get("name")));
+    if (pods.count(k)) throw ApiErr{409, "AlreadyExists", "pods \"" + str_of(m.get("name")) + "\" already exists"};
+    ObjP o = seal(std::move(v), ++rv);
+    pods.emplace(k, o);
+    emit(kPods, "ADDED", o);
+    return o;
+  }
+  ObjP pod_or_404(std::string_view ns, std::string_view name) const {
+    auto it = pods.find(key(ns, name));
+    if (it == pods.end()) throw ApiErr{404, "NotFound", "pods \"" + std::string(name) + "\" not found"};
+    return it->second;
+  }
+  ObjP patch_pod_locked(std::string_view ns, std::string_view name, const JV& patch) {
+    ObjP cur = pod_or_404(ns, name);
+    JV v = cur->v;
+    merge_patch(&v, patch);
+    ObjP o = seal(std::move(v), ++rv);
+    pods[key(ns, name)] = o;
+    emit(kPods, "MODIFIED", o);
+    return o;
+  }
+  ObjP update_pod_locked(std::string_view ns, std::string_view name, JV v) {
+    ObjP cur = pod_or_404(ns, name);
+    const JV* m = v.get("metadata");
+    const std::string want = m ? str_of(m->get("resourceVersion")) : std::string();
+    if (!want.empty() && want != std::to_string(cur->rv))
+      throw ApiErr{409, "Conflict", "Operation cannot be fulfilled on pods \"" + std::string(name) +
+                                        "\": the object has been modified; please apply your changes to the latest "
+                                        "version and try again"};
+    ObjP o = seal(std::move(v), ++rv);
+    pods[key(ns, name)] = o;
+    emit(kPods, "MODIFIED", o);
+    return o;
+  }
+  void bind_locked(std::string_view ns, std::string_view name, std::string_view uid, std::string_view node) {
+    ObjP cur = pod_or_404(ns, name);
+    if (!uid.empty() && cur->uid != uid) throw ApiErr{409, "Conflict", "pod " + std::string(name) + " uid mismatch"};
+    if (!cur->node.empty())
+      throw ApiErr{409, "Conflict", "pod " + std::string(name) + " is already assigned to node \"" + cur->node + "\""};
+    if (!nodes.count(std::string(node))) throw ApiErr{404, "NotFound", "nodes \"" + std::string(node) + "\" not found"};
+    JV v = cur->v;
+    v.child("spec").set("nodeName", JV::str(std::string(node)));
+    v.child("status").set("phase", JV::str("Running"));
+    ObjP o = seal(std::move(v), ++rv);
+    pods[key(ns, name)] = o;
+    ++bindings;
+    emit(kPods, "MODIFIED", o);
+  }
+  bool delete_pod_locked(std::string_view ns, std::string_view name) {
+    auto it = pods.find(key(ns, name));
+    if (it == pods.end()) return false;
+    ObjP cur = it->second;
+    pods.erase(it);
+    ObjP o = seal(cur->v, ++rv);
+    emit(kPods, "DELETED", o);
+    return true;
+  }
+
+  // -- nodes
+  ObjP put_node_locked(JV v) {
+    const std::string name = str_of(v.child("metadata").get("name"));
+    if (name.empty()) throw ApiErr{422, "Invalid", "metadata.name: Required value"};
+    const bool existed = nodes.count(name) > 0;
+    ObjP o = seal(std::move(v), ++rv);
+    nodes[name] = o;
+    emit(kNodes, existed ? "MODIFIED" : "ADDED", o);
+    return o;
+  }
+  ObjP node_or_404(std::string_view name) const {
+    auto it = nodes.find(std::string(name));
+    if (it == nodes.end()) throw ApiErr{404, "NotFound", "nodes \"" + std::string(name) + "\" not found"};
+    return it->second;
+  }
+
+  // -- listing
+  std::string listing(const char* kind, const std::vector<ObjP>& items) const {
+    size_t n = 96;
+    for (const auto& o : items) n += o->json.size() + 1;
+    std::string b;
+    b.reserve(n);
+    b += "{\"kind\":\"";
+    b += kind;
+    b += "\",\"apiVersion\":\"v1\",\"metadata\":{\"resourceVersion\":\"" + std::to_string(rv) + "\"},\"items\":[";
+    for (size_t i = 0; i < items.size(); ++i) {
+      if (i) b.push_back(',');
+      b += items[i]->json;
+    }
+    b += "]}";
+    return b;
+  }
+
+  // ------------------------------------------------------------------ request dispatch
+  struct Req {
+    std::string_view method, path;
+    std::unordered_map<std::string, std::string> q;
+    std::string_view body;
+  };
+
+  static bool is_watch(const Req& r) {
+    auto it = r.q.find("watch");
+    return it != r.q.end() && (it->second == "1" || it->second == "true");
+  }
+
+  static std::string qv(const Req& r, const char* k) {
+    auto it = r.q.find(k);
+    return it == r.q.end() ? std::string() : it->second;
+  }
+
+  JV body_json(const Req& r) const {
+    JV v;
+    if (!parse(r.body, &v)) throw ApiErr{400, "BadRequest", "request body is not valid JSON"};
+    return v;
+  }
+
+  std::pair<int, std::string> handle(const Req& r) {
+    n_requests.fetch_add(1, std::memory_order_relaxed);
+    try {
+      return route(r);
+    } catch (const ApiErr& e) {
+      return {e.code, status_body(e.code, e.reason, e.message)};
+    }
+  }
+
+  std::pair<int, std::string> route(const Req& r) {
+    const auto parts = split(r.path.substr(r.path.empty() || r.path[0] != '/' ? 0 : 1), '/');
+    const size_t n = parts.size();
+    auto at = [&](size_t i) -> std::string_view { return i < n ? parts[i] : std::string_view(); };
+    const std::string_view m = r.method;
+    static const std::string kOk = "{\"kind\":\"Status\",\"apiVersion\":\"v1\",\"status\":\"Success\"}";
+    if (n == 1 && (at(0) == "healthz" || at(0) == "readyz")) return {200, "ok"};
+    if (at(0) == "api" && at(1) == "v1") {
+      // /api/v1/pods
+      if (n == 3 && at(2) == "pods" && m == "GET") return list_pods(r, "");
+      // /api/v1/nodes...
+      if (at(2) == "nodes") {
+        if (n == 3 && m == "GET") return list_nodes(r);
+        if (n == 3 && m == "POST") {
+          JV v = body_json(r);
+          std::lock_guard<std::mutex> g(mu);
+          return {201, put_node_locked(std::move(v))->json};
+        }
+        if (n == 4 || (n == 5 && at(4) == "status")) {
+          const std::string name(at(3));
+          if (m == "GET" && n == 4) {
+            std::lock_guard<std::mutex> g(mu);
+            return {200, node_or_404(name)->json};
+          }
+          if (m == "PATCH") {
+            JV p = body_json(r);
+            std::lock_guard<std::mutex> g(mu);
+            JV v = node_or_404(name)->v;
+            merge_patch(&v, p);
+            return {200, put_node_locked(std::move(v))->json};
+          }
+          if (m == "DELETE" && n == 4) {
+            std::lock_guard<std::mutex> g(mu);
+            auto it = nodes.find(name);
+            if (it == nodes.end()) throw ApiErr{404, "NotFound", "nodes \"" + name + "\" not found"};
+            ObjP cur = it->second;
+            nodes.erase(it);
+            emit(kNodes, "DELETED", seal(cur->v, ++rv));
+            return {200, kOk};
+          }
+        }
+        return {405, status_body(405, "MethodNotAllowed", "method not allowed")};
+      }
+      // /api/v1/namespaces/{ns}/...
+      if (at(2) == "namespaces" && n >= 5) {
+        const std::string_view ns = at(3);
+        if (at(4) == "events" && n == 5 && m == "POST") {
+          n_events.fetch_add(1, std::memory_order_relaxed);
+          return {201, "{}"};
+        }
+        if (at(4) == "pods") {
+          if (n == 5 && m == "GET") return list_pods(r, ns);
+          if (n == 5 && m == "POST") {
+            JV v = body_json(r);
+            n_create.fetch_add(1, std::memory_order_relaxed);
+            std::lock_guard<std::mutex> g(mu);
+            return {201, create_pod_locked(std::move(v), ns)->json};
+          }
+          const std::string_view name = at(5);
+          if (n == 6) {
+            if (m == "GET") {
+              n_get.fetch_add(1, std::memory_order_relaxed);
+              std::lock_guard<std::mutex> g(mu);
+              return {200, pod_or_404(ns, name)->json};
+            }
+            if (m == "PATCH") {
+              JV p = body_json(r);
+              n_patch.fetch_add(1, std::memory_order_relaxed);
+              std::lock_guard<std::mutex> g(mu);
+              return {200, patch_pod_locked(ns, name, p)->json};
+            }
+            if (m == "PUT") {
+              JV v = body_json(r);
+              std::lock_guard<std::mutex> g(mu);
+              return {200, update_pod_locked(ns, name, std::move(v))->json};
+            }
+            if (m == "DELETE") {
+              n_delete.fetch_add(1, std::memory_order_relaxed);
+              std::lock_guard<std::mutex> g(mu);
+              if (!delete_pod_locked(ns, name))
+                throw ApiErr{404, "NotFound", "pods \"" + std::string(name) + "\" not found"};
+              return {200, kOk};
+            }
+          }
+          if (n == 7 && at(6) == "binding" && m == "POST") {
+            JV b = body_json(r);
+            const JV* md = b.get("metadata");
+            const JV* tg = b.get("target");
+            n_bind.fetch_add(1, std::memory_order_relaxed);
+            std::lock_guard<std::mutex> g(mu);
+            bind_locked(ns, name, md ? str_of(md->get("uid")) : std::string(), tg ? str_of(tg->get("name")) : "");
+            return {201, kOk};
+          }
+        }
+      }
+    }
+    // leases (coordination.k8s.io/v1)
+    if (at(0) == "apis" && at(1) == "coordination.k8s.io" && at(2) == "v1" && at(3) == "namespaces" &&
+        at(5) == "leases") {
+      n_lease.fetch_add(1, std::memory_order_relaxed);
+      const std::string_view ns = at(4);
+      if (n == 6 && m == "POST") {
+        JV v = body_json(r);
+        v.child("metadata").set("namespace", JV::str(std::string(ns)));
+        const std::string name = str_of(v.child("metadata").get("name"));
+        std::lock_guard<std::mutex> g(mu);
+        const std::string k = key(ns, name);
+        if (leases.count(k))
+          throw ApiErr{409, "AlreadyExists", "leases.coordination.k8s.io \"" + name + "\" already exists"};
+        ObjP o = seal(std::move(v), ++rv);
+        leases[k] = o;
+        return {201, o->json};
+      }
+      if (n == 7) {
+        const std::string k = key(ns, at(6));
+        std::lock_guard<std::mutex> g(mu);
+        auto it = leases.find(k);
+        if (it == leases.end())
+          throw ApiErr{404, "NotFound", "leases.coordination.k8s.io \"" + std::string(at(6)) + "\" not found"};
+        if (m == "GET") return {200, it->second->json};
+        if (m == "PUT") {
+          JV v = body_json(r);
+          const JV* md = v.get("metadata");
+          if ((md ? str_of(md->get("resourceVersion")) : std::string()) != std::to_string(it->second->rv))
+            throw ApiErr{409, "Conflict", "Operation cannot be fulfilled on leases.coordination.k8s.io \"" +
+                                              std::string(at(6)) + "\": the object has been modified"};
+          v.child("metadata").set("namespace", JV::str(std::string(ns)));
+          ObjP o = seal(std::move(v), ++rv);
+          it->second = o;
+          return {200, o->json};
+        }
+      }
+    }
+    return {404, status_body(404, "NotFound", "the server could not find the requested resource")};
+  }
+
+  std::pair<int, std::string> list_pods(const Req& r, std::string_view ns) {
+    n_list.fetch_add(1, std::memory_order_relaxed);
+    const Selector ls = Selector::parse(qv(r, "labelSelector")), fs = Selector::parse(qv(r, "fieldSelector"));
+    std::vector<ObjP> items;
+    std::lock_guard<std::mutex> g(mu);
+    items.reserve(pods.size());
+    for (const auto& kv : pods) {
+      const Obj& o = *kv.second;
+      if ((ns.empty() || o.ns == ns) && ls.labels_match(o) && fs.fields_match(o)) items.push_back(kv.second);
+    }
+    return {200, listing("PodList", items)};
+  }
+
+  std::pair<int, std::string> list_nodes(const Req& r) {
+    n_list.fetch_add(1, std::memory_order_relaxed);
+    const Selector ls = Selector::parse(qv(r, "labelSelector"));
+    std::vector<ObjP> items;
+    std::lock_guard<std::mutex> g(mu);
+    for (const auto& kv : nodes)
+      if (ls.labels_match(*kv.second)) items.push_back(kv.second);
+    return {200, listing("NodeList", items)};
+  }
+
+  // Registers a watch and queues its replay; returns false (and an in-stream 410) when the
+  // requested version is older than the cache.
+  void start_watch(const std::shared_ptr<Conn>& c, int kind, const Req& r) {
+    n_watch.fetch_add(1, std::memory_order_relaxed);
+    Watch w{kind, Selector::parse(qv(r, "labelSelector")), Selector::parse(qv(r, "fieldSelector")), c};
+    uint64_t from = 0;
+    const std::string rvs = qv(r, "resourceVersion");
+    if (!rvs.empty()) from = std::strtoull(rvs.c_str(), nullptr, 10);
+    const std::string to = qv(r, "timeoutSeconds");
+    if (!to.empty()) c->deadline = steady_s() + std::strtod(to.c_str(), nullptr);
+    std::lock_guard<std::mutex> g(mu);
+    std::string replay;
+    const auto& h = hist[kind];
+    const bool truncated = !h.empty() && h.size() >= cfg.history && h.front().rv > from + 1;
+    if (from > 0 && (from < compacted[kind] || truncated)) {
+      std::string msg = "too old resource version: " + std::to_string(from) + " (" +
+                        std::to_string(compacted[kind] ? compacted[kind] : (h.empty() ? 0 : h.front().rv)) + ")";
+      std::lock_guard<std::mutex> cg(c->mu);
+      c->pending = "{\"type\":\"ERROR\",\"object\":" + status_body(410, "Expired", msg) + "}\n";
+      c->ended = true;
+      c->owner->wake(c);
+      return;
+    }
+    if (from == 0) {
+      // no version: the current state as ADDED events, then live
+      auto add = [&](const ObjP& o) {
+        if (w.ls.labels_match(*o) && w.fs.fields_match(*o)) replay += *ev_line("ADDED", o->json);
+      };
+      if (kind == kPods)
+        for (const auto& kv : pods) add(kv.second);
+      else
+        for (const auto& kv : nodes) add(kv.second);
+    } else {
+      for (const Ev& e : h)
+        if (e.rv > from && w.ls.labels_match(*e.obj) && w.fs.fields_match(*e.obj)) replay += *e.line;
+    }
+    {
+      std::lock_guard<std::mutex> cg(c->mu);
+      c->pending += replay;
+    }
+    watches.push_back(std::move(w));
+    if (!replay.empty()) c->owner->wake(c);
+  }
+
+  void unwatch(const Conn* c) {
+    std::lock_guard<std::mutex> g(mu);
+    for (size_t i = 0; i < watches.size();)
+      if (watches[i].conn.get() == c) {
+        watches[i] = std::move(watches.back());
+        watches.pop_back();
+      } else {
+        ++i;
+      }
+  }
+
+  void end_watches(int kind) {   // under mu
+    for (size_t i = 0; i < watches.size();) {
+      if (kind < 0 || watches[i].kind == kind) {
+        {
+          std::lock_guard<std::mutex> cg(watches[i].conn->mu);
+          watches[i].conn->ended = true;
+        }
+        watches[i].conn->owner->wake(watches[i].conn);
+        watches[i] = std::move(watches.back());
+        watches.pop_back();
+      } else {
+        ++i;
+      }
+    }
+  }
+
+  // ------------------------------------------------------------------ IO
+  void io_loop(IoThread* t);
+  void on_readable(IoThread* t, const std::shared_ptr<Conn>& c);
+  void flush_watch(const std::shared_ptr<Conn>& c);
+  bool write_out(Conn* c);
+  void close_conn(IoThread* t, const std::shared_ptr<Conn>& c);
+};
+
+namespace {
+std::string head(int code, size_t len, bool chunked = false) {
+  std::string h = "HTTP/1.1 " + std::to_string(code) + " " + reason_phrase(code) +
+                  "\r\nContent-Type: application/json\r\n";
+  if (chunked)
+    h += "Transfer-Encoding: chunked\r\n\r\n";
+  else
+    h += "Content-Length: " + std::to_string(len) + "\r\n\r\n";
+  return h;
+}
+
+void frame_chunk(std::string* out, std::string_view data) {
+  char hex[24];
+  std::snprintf(hex, sizeof hex, "%zx\r\n", data.size());
+  out->append(hex);
+  out->append(data);
+  out->append("\r\n");
+}
+}  // namespace
+
+bool Server::Impl::write_out(Conn* c) {
+  while (!c->out.empty()) {
+    const ssize_t w = ::send(c->fd, c->out.data(), c->out.size(), MSG_NOSIGNAL);
+    if (w > 0) {
+      c->out.erase(0, static_cast<size_t>(w));
+      continue;
+    }
+    if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) return true;
+    if (w < 0 && errno == EINTR) continue;
+    return false;
+  }
+  return true;
+}
+
+void Server::Impl::flush_watch(const std::shared_ptr<Conn>& c) {
+  std::string data;
+  bool end;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    data.swap(c->pending);
+    end = c->ended;
+  }
+  if (!c->watching) return;
+  if (!data.empty()) frame_chunk(&c->out, data);
+  if (end) {
+    c->out += "0\r\n\r\n";
+    c->watching = false;
+    c->deadline = 0;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->ended = false;
+    c->pending.clear();
+  }
+}
+
+void Server::Impl::close_conn(IoThread* t, const std::shared_ptr<Conn>& c) {
+  if (c->watching) unwatch(c.get());
+  epoll_ctl(t->ep, EPOLL_CTL_DEL, c->fd, nullptr);
+  ::close(c->fd);
+  t->conns.erase(c->fd);
+}
+
+void Server::Impl::on_readable(IoThread* t, const std::shared_ptr<Conn>& c) {
+  char buf[65536];
+  for (;;) {
+    const ssize_t r = ::recv(c->fd, buf, sizeof buf, 0);
+    if (r > 0) {
+      c->in.append(buf, static_cast<size_t>(r));
+      if (c->in.size() > (64u << 20)) {
+        close_conn(t, c);
+        return;
+      }
+      continue;
+    }
+    if (r == 0) {
+      close_conn(t, c);
+      return;
+    }
+    if (errno == EAGAIN || errno == EWOULDBLOCK) break;
+    if (errno == EINTR) continue;
+    close_conn(t, c);
+    return;
+  }
+  // requests (pipelined ones in order); none while a watch stream is open on the connection
+  while (!c->watching) {
+    const size_t he = c->in.find("\r\n\r\n");
+    if (he == std::string::npos) break;
+    std::string_view hdr(c->in.data(), he);
+    const size_t l1 = hdr.find("\r\n");
+    std::string_view line = hdr.substr(0, l1);
+    const size_t s1 = line.find(' '), s2 = line.rfind(' ');
+    if (s1 == std::string_view::npos || s2 == s1) {
+      close_conn(t, c);
+      return;
+    }
+    size_t clen = 0;
+    bool chunked = false, close_req = false;
+    for (std::string_view h : split(l1 == std::string_view::npos ? std::string_view() : hdr.substr(l1 + 2), '\n')) {
+      h = trim(h);
+      const size_t colon = h.find(':');
+      if (colon == std::string_view::npos) continue;
+      std::string name(h.substr(0, colon));
+      for (char& ch : name) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
+      const std::string_view val = trim(h.substr(colon + 1));
+      if (name == "content-length") clen = static_cast<size_t>(std::strtoull(std::string(val).c_str(), nullptr, 10));
+      else if (name == "transfer-encoding" && val.find("chunked") != std::string_view::npos) chunked = true;
+      else if (name == "connection" && (val == "close" || val == "Close")) close_req = true;
+    }
+    std::string body;
+    size_t consumed;
+    if (chunked) {
+      size_t p = he + 4;
+      bool done = false;
+      for (;;) {
+        const size_t le = c->in.find("\r\n", p);
+        if (le == std::string::npos) break;
+        const size_t sz = static_cast<size_t>(std::strtoull(c->in.substr(p, le - p).c_str(), nullptr, 16));
+        if (sz == 0) {
+          const size_t fe = c->in.find("\r\n", le + 2);
+          if (fe == std::string::npos) break;
+          p = fe + 2;
+          done = true;
+          break;
+        }
+        if (c->in.size() < le + 2 + sz + 2) break;
+        body.append(c->in, le + 2, sz);
+        p = le + 2 + sz + 2;
+      }
+      if (!done) break;
+      consumed = p;
+    } else {
+      if (c->in.size() < he + 4 + clen) break;
+      body.assign(c->in, he + 4, clen);
+      consumed = he + 4 + clen;
+    }
+    Req req;
+    req.method = line.substr(0, s1);
+    std::string_view target = line.substr(s1 + 1, s2 - s1 - 1);
+    const size_t qm = target.find('?');
+    req.path = target.substr(0, qm);
+    if (qm != std::string_view::npos)
+      for (std::string_view kv : split(target.substr(qm + 1), '&')) {
+        const size_t eq = kv.find('=');
+        if (eq == std::string_view::npos) req.q[url_decode(kv)] = "";
+        else req.q[url_decode(kv.substr(0, eq))] = url_decode(kv.substr(eq + 1));
+      }
+    req.body = body;
+    const bool watch_pods = req.method == "GET" && req.path == "/api/v1/pods" && is_watch(req);
+    const bool watch_nodes = req.method == "GET" && req.path == "/api/v1/nodes" && is_watch(req);
+    if (watch_pods || watch_nodes) {
+      c->out += head(200, 0, true);
+      c->watching = true;
+      // the rest of the buffer (nothing, from a well-behaved client) waits for the stream end
+      std::string rest = c->in.substr(consumed);
+      start_watch(c, watch_pods ? kPods : kNodes, req);
+      c->in.swap(rest);
+      break;
+    }
+    auto [code, resp] = handle(req);
+    c->in.erase(0, consumed);
+    c->out += head(code, resp.size());
+    c->out += resp;
+    if (close_req) c->close_after = true;
+  }
+  if (!write_out(c.get())) {
+    close_conn(t, c);
+    return;
+  }
+  if (c->out.empty() && c->close_after) {
+    close_conn(t, c);
+    return;
+  }
+  epoll_event ev{};
+  ev.events = EPOLLIN | EPOLLRDHUP | (c->out.empty() ? 0u : EPOLLOUT);
+  ev.data.fd = c->fd;
+  epoll_ctl(t->ep, EPOLL_CTL_MOD, c->fd, &ev);
+}
+
+void Server::Impl::io_loop(IoThread* t) {
+  epoll_event evs[256];
+  while (!stopping.load(std::memory_order_acquire)) {
+    const int n = epoll_wait(t->ep, evs, 256, 200);
+    for (int i = 0; i < n; ++i) {
+      const int fd = evs[i].data.fd;
+      if (fd == lfd) {
+        for (;;) {
+          const int cfd = accept4(lfd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+          if (cfd < 0) break;
+          int one = 1;
+          setsockopt(cfd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+          auto c = std::make_shared<Conn>();
+          c->fd = cfd;
+          c->owner = t;
+          t->conns[cfd] = c;
+          epoll_event ce{};
+          ce.events = EPOLLIN | EPOLLRDHUP;
+          ce.data.fd = cfd;
+          epoll_ctl(t->ep, EPOLL_CTL_ADD, cfd, &ce);
+        }
+        continue;
+      }
+      if (fd == t->efd) {
+        uint64_t v;
+        (void)!read(t->efd, &v, sizeof v);
+        std::vector<std::shared_ptr<Conn>> fl;
+        {
+          std::lock_guard<std::mutex> g(t->mu);
+          fl.swap(t->flush);
+        }
+        for (auto& c : fl) {
+          c->queued.store(false);
+          if (!t->conns.count(c->fd) || t->conns[c->fd] != c) continue;   // closed meanwhile
+          flush_watch(c);
+          if (!write_out(c.get())) {
+            close_conn(t, c);
+            continue;
+          }
+          epoll_event ce{};
+          ce.events = EPOLLIN | EPOLLRDHUP | (c->out.empty() ? 0u : EPOLLOUT);
+          ce.data.fd = c->fd;
+          epoll_ctl(t->ep, EPOLL_CTL_MOD, c->fd, &ce);
+          if (!c->watching && !c->in.empty()) on_readable(t, c);   // requests queued behind a stream
+        }
+        continue;
+      }
+      auto it = t->conns.find(fd);
+      if (it == t->conns.end()) continue;
+      std::shared_ptr<Conn> c = it->second;
+      if (evs[i].events & (EPOLLERR | EPOLLHUP)) {
+        close_conn(t, c);
+        continue;
+      }
+      if (evs[i].events & EPOLLOUT) {
+        if (!write_out(c.get())) {
+          close_conn(t, c);
+          continue;
+        }
+        if (c->out.empty() && c->close_after) {
+          close_conn(t, c);
+          continue;
+        }
+      }
+      if (evs[i].events & (EPOLLIN | EPOLLRDHUP)) on_readable(t, c);
+      else if (c->out.empty()) {
+        epoll_event ce{};
+        ce.events = EPOLLIN | EPOLLRDHUP;
+        ce.data.fd = c->fd;
+        epoll_ctl(t->ep, EPOLL_CTL_MOD, c->fd, &ce);
+      }
+    }
+    // watch deadlines (timeoutSeconds): the stream ends cleanly
+    const double now = steady_s();
+    std::vector<std::shared_ptr<Conn>> due;
+    for (auto& kv : t->conns)
+      if (kv.second->watching && kv.second->deadline > 0 && now >= kv.second->deadline) due.push_back(kv.second);
+    for (auto& c : due) {
+      unwatch(c.get());
+      {
+        std::lock_guard<std::mutex> g(c->mu);
+        c->ended = true;
+      }
+      flush_watch(c);
+      if (!write_out(c.get())) close_conn(t, c);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ Server
+Server::Server(const Config& cfg) : impl_(new Impl) {
+  presize_fd_table();
+  impl_->cfg = cfg;
+  if (impl_->cfg.threads < 1) impl_->cfg.threads = 1;
+  if (impl_->cfg.history < 16) impl_->cfg.history = 16;
+  sockaddr_in addr{};
+  addr.sin_family = AF_INET;
+  addr.sin_port = htons(static_cast<uint16_t>(cfg.port));
+  if (cfg.host.empty() || cfg.host == "0.0.0.0") addr.sin_addr.s_addr = htonl(INADDR_ANY);
+  else if (inet_pton(AF_INET, cfg.host.c_str(), &addr.sin_addr) != 1)
+    throw std::invalid_argument("ApiServer: host must be an IPv4 address");
+  const int lfd = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+  if (lfd < 0) throw std::runtime_error("ApiServer: socket failed");
+  int one = 1;
+  setsockopt(lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  if (bind(lfd, reinterpret_cast<sockaddr*>(&addr), sizeof addr) != 0 || listen(lfd, 4096) != 0) {
+    ::close(lfd);
+    throw std::runtime_error(std::string("ApiServer: bind/listen failed: ") + std::strerror(errno));
+  }
+  socklen_t len = sizeof addr;
+  getsockname(lfd, reinterpret_cast<sockaddr*>(&addr), &len);
+  port_ = ntohs(addr.sin_port);
+  impl_->lfd = lfd;
+  for (int i = 0; i < impl_->cfg.threads; ++i) {
+    auto t = std::make_unique<IoThread>();
+    t->ep = epoll_create1(EPOLL_CLOEXEC);
+    t->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    if (t->ep < 0 || t->efd < 0) throw std::runtime_error("ApiServer: epoll/eventfd failed");
+    epoll_event le{};
+    le.events = EPOLLIN | EPOLLEXCLUSIVE;
+    le.data.fd = lfd;
+    epoll_ctl(t->ep, EPOLL_CTL_ADD, lfd, &le);
+    epoll_event ee{};
+    ee.events = EPOLLIN;
+    ee.data.fd = t->efd;
+    epoll_ctl(t->ep, EPOLL_CTL_ADD, t->efd, &ee);
+    impl_->io.push_back(std::move(t));
+  }
+  for (auto& t : impl_->io) {
+    IoThread* tp = t.get();
+    Impl* im = impl_.get();
+    t->th = std::thread([im, tp] { im->io_loop(tp); });
+  }
+}
+
+Server::~Server() { stop(); }
+
+void Server::stop() {
+  if (!impl_ || impl_->stopping.exchange(true)) return;
+  for (auto& t : impl_->io) {
+    const uint64_t one = 1;
+    (void)!write(t->efd, &one, sizeof one);
+  }
+  for (auto& t : impl_->io)
+    if (t->th.joinable()) t->th.join();
+  {
+    std::lock_guard<std::mutex> g(impl_->mu);
+    impl_->watches.clear();
+  }
+  for (auto& t : impl_->io) {
+    for (auto& kv : t->conns) ::close(kv.first);
+    t->conns.clear();
+    ::close(t->ep);
+    ::close(t->efd);
+  }
+  ::close(impl_->lfd);
+}
+
+std::pair<int, std::string> Server::call(std::string_view method, std::string_view target, std::string_view body) {
+  Impl::Req r;
+  r.method = method;
+  const size_t qm = target.find('?');
+  r.path = target.substr(0, qm);
+  if (qm != std::string_view::npos)
+    for (std::string_view kv : split(target.substr(qm + 1), '&')) {
+      const size_t eq = kv.find('=');
+      if (eq == std::string_view::npos) r.q[url_decode(kv)] = "";
+      else r.q[url_decode(kv.substr(0, eq))] = url_decode(kv.substr(eq + 1));
+    }
+  r.body = body;
+  if (Impl::is_watch(r)) return {400, status_body(400, "BadRequest", "watch needs a connection")};
+  return impl_->handle(r);
+}
+
+std::vector<int> Server::create_pods(const std::vector<std::string>& texts) {
+  std::vector<JV> vs(texts.size());
+  std::vector<int> codes(texts.size(), 201);
+  for (size_t i = 0; i < texts.size(); ++i)
+    if (!parse(texts[i], &vs[i])) codes[i] = 400;
+  std::lock_guard<std::mutex> g(impl_->mu);
+  for (size_t i = 0; i < texts.size(); ++i) {
+    if (codes[i] != 201) continue;
+    try {
+      impl_->create_pod_locked(std::move(vs[i]), "");
+      impl_->n_create.fetch_add(1, std::memory_order_relaxed);
+    } catch (const ApiErr& e) {
+      codes[i] = e.code;
+    }
+  }
+  return codes;
+}
+
+int Server::delete_pods(const std::vector<std::pair<std::string, std::string>>& keys) {
+  int n = 0;
+  std::lock_guard<std::mutex> g(impl_->mu);
+  for (const auto& k : keys) n += impl_->delete_pod_locked(k.first, k.second) ? 1 : 0;
+  impl_->n_delete.fetch_add(static_cast<uint64_t>(keys.size()), std::memory_order_relaxed);
+  return n;
+}
+
+std::string Server::stats_json() const {
+  const Impl& m = *impl_;
+  std::lock_guard<std::mutex> g(m.mu);
+  auto ld = [](const std::atomic<uint64_t>& a) { return std::to_string(a.load(std::memory_order_relaxed)); };
+  return "{\"rv\":" + std::to_string(m.rv) + ",\"pods\":" + std::to_string(m.pods.size()) +
+         ",\"nodes\":" + std::to_string(m.nodes.size()) + ",\"bindings\":" + std::to_string(m.bindings) +
+         ",\"watches\":" + std::to_string(m.watches.size()) + ",\"requests\":" + ld(m.n_requests) +
+         ",\"calls\":{\"create_pod\":" + ld(m.n_create) + ",\"get_pod\":" + ld(m.n_get) + ",\"patch_pod\":" +
+         ld(m.n_patch) + ",\"bind_pod\":" + ld(m.n_bind) + ",\"delete_pod\":" + ld(m.n_delete) + ",\"list\":" +
+         ld(m.n_list) + ",\"watch\":" + ld(m.n_watch) + ",\"events\":" + ld(m.n_events) + ",\"lease\":" +
+         ld(m.n_lease) + "}}";
+}
+
+void Server::compact(std::string_view kind) {
+  std::lock_guard<std::mutex> g(impl_->mu);
+  for (int k = 0; k < kKinds; ++k) {
+    if (!kind.empty() && kind != (k == kPods ? "pods" : "nodes")) continue;
+    impl_->hist[k].clear();
+    impl_->compacted[k] = impl_->rv;
+  }
+}
+
+void Server::drop_watches(std::string_view kind) {
+  std::lock_guard<std::mutex> g(impl_->mu);
+  impl_->end_watches(kind.empty() ? -1 : (kind == "pods" ? kPods : kNodes));
+}
+
+}  // namespace nanogpu::apisrv

@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "nanogpu/alloc.h"
+#include "nanogpu/apiserver.h"
 #include "nanogpu/frontend.h"
 #include "nanogpu/gosort.h"
 #include "nanogpu/ledger.h"
@@ -542,6 +543,43 @@ PYBIND11_MODULE(_native, m) {
            py::arg("nominate") = false)
       .def("set_serving", &Frontend::set_serving)
       .def("set_busy_poll_us", &Frontend::set_busy_poll_us)
+      .def(
+          "set_kube_writer",
+          [](Frontend& f, const std::string& host, int port, bool tls, const std::string& token,
+             const std::string& token_file, const std::string& ca_file, const std::string& cert_file,
+             const std::string& key_file, bool insecure, int threads, int retries, bool record_events) {
+            KubeTarget t;
+            t.host = host;
+            t.port = port;
+            t.tls = tls;
+            t.token = token;
+            t.token_file = token_file;
+            t.ca_file = ca_file;
+            t.cert_file = cert_file;
+            t.key_file = key_file;
+            t.insecure = insecure;
+            f.set_kube_writer(t, threads, retries, record_events);
+          },
+          py::arg("host"), py::arg("port"), py::arg("tls") = false, py::arg("token") = "",
+          py::arg("token_file") = "", py::arg("ca_file") = "", py::arg("cert_file") = "", py::arg("key_file") = "",
+          py::arg("insecure") = false, py::arg("threads") = 32, py::arg("retries") = 3,
+          py::arg("record_events") = true,
+          "Binds whose reservation succeeded natively are finished by C++ writer threads "
+          "(PATCH + binding + commit/rollback) on keep-alive connections to kube-apiserver.")
+      .def("kube_writer_stats",
+           [](const Frontend& f) -> py::object {
+             const KubeWriter* w = f.kube_writer();
+             if (!w) return py::none();
+             py::dict d;
+             d["ok"] = w->stats.ok.load();
+             d["failed"] = w->stats.failed.load();
+             d["rollbacks"] = w->stats.rollbacks.load();
+             d["retries"] = w->stats.retries.load();
+             d["inflight"] = w->stats.inflight.load();
+             d["patch_seconds_total"] = static_cast<double>(w->stats.patch_ns.load()) * 1e-9;
+             d["binding_seconds_total"] = static_cast<double>(w->stats.binding_ns.load()) * 1e-9;
+             return d;
+           })
       .def("take",
            [](Frontend& f) {
              std::vector<PyRequest> v;
@@ -696,4 +734,39 @@ PYBIND11_MODULE(_native, m) {
       py::arg("bind_threads") = 256, py::arg("seed") = 0, py::arg("max_attempts") = 8, py::arg("backoff_s") = 0.001,
       py::arg("session") = nullptr, py::arg("kube_combine") = 0, py::arg("extender_weight") = 1,
       "kube-scheduler stand-in (native/src/schedsim.cpp): schedule `pods` through the extender at host:port");
+
+  // ------------------------------------------------------------------ native API server
+  py::class_<apisrv::Server, std::shared_ptr<apisrv::Server>>(
+      m, "ApiServer", "In-memory Kubernetes API server over HTTP (native/src/apiserver.cpp)")
+      .def(py::init([](const std::string& host, int port, int threads, size_t history) {
+             apisrv::Config c;
+             c.host = host;
+             c.port = port;
+             c.threads = threads;
+             c.history = history;
+             return std::make_shared<apisrv::Server>(c);
+           }),
+           py::arg("host") = "127.0.0.1", py::arg("port") = 0, py::arg("threads") = 4,
+           py::arg("history") = size_t(200000))
+      .def_property_readonly("port", &apisrv::Server::port)
+      .def("stop", &apisrv::Server::stop, py::call_guard<py::gil_scoped_release>())
+      .def(
+          "call",
+          [](apisrv::Server& s, const std::string& method, const std::string& target, const std::string& body) {
+            std::pair<int, std::string> r;
+            {
+              py::gil_scoped_release nogil;
+              r = s.call(method, target, body);
+            }
+            return py::make_tuple(r.first, py::bytes(r.second));
+          },
+          py::arg("method"), py::arg("target"), py::arg("body") = "",
+          "One request without a socket: (status, body bytes).")
+      .def("create_pods", &apisrv::Server::create_pods, py::arg("pods"), py::call_guard<py::gil_scoped_release>(),
+           "Creates pods from JSON texts under one lock hold; one status code per pod.")
+      .def("delete_pods", &apisrv::Server::delete_pods, py::arg("keys"), py::call_guard<py::gil_scoped_release>(),
+           "Deletes (namespace, name) pods; returns how many existed.")
+      .def("stats", [](const apisrv::Server& s) { return s.stats_json(); })
+      .def("compact", &apisrv::Server::compact, py::arg("kind") = "")
+      .def("drop_watches", &apisrv::Server::drop_watches, py::arg("kind") = "");
 }

@@ -348,8 +348,17 @@ Frontend::Frontend(std::shared_ptr<Ledger> ledger, const std::string& host, int 
 
 Frontend::~Frontend() { stop(); }
 
+void Frontend::set_kube_writer(const KubeTarget& t, int threads, int retries, bool record_events) {
+  if (writer_.load()) throw std::logic_error("Frontend: the kube writer is already set");
+  writer_owner_ = std::make_unique<KubeWriter>(
+      t, ledger_, [this](uint64_t id, int status, const std::string& body) { respond(id, status, "application/json", body); },
+      threads, retries, record_events);
+  writer_.store(writer_owner_.get(), std::memory_order_release);
+}
+
 void Frontend::stop() {
   if (stop_.exchange(true)) return;
+  if (writer_owner_) writer_owner_->stop();   // answers what it still holds through the workers
   for (auto& w : workers_) {
     uint64_t one = 1;
     (void)!write(w->efd, &one, sizeof(one));
@@ -710,8 +719,29 @@ void Frontend::process(Worker* w, Conn* c) {
 void Frontend::defer(Worker* w, Conn* c, std::string method, std::string path, std::string query, std::string body) {
   PyRequest r;
   r.id = make_id(w->idx, c->id);
-  if (method == "POST" && path == "/scheduler/bind" && serving())
+  if (method == "POST" && path == "/scheduler/bind" && serving()) {
     prepare_bind(body, &r);
+    KubeWriter* kw = writer_.load(std::memory_order_acquire);
+    if (kw && r.bind.ok && (r.bind.rc == kOk || r.bind.rc == kOkExisting)) {
+      // the whole bind stays native: API writes and commit on the writer's threads
+      BindJob j;
+      j.id = r.id;
+      j.ns = std::move(r.bind.ns);
+      j.name = std::move(r.bind.name);
+      j.uid = std::move(r.bind.uid);
+      j.node = std::move(r.bind.node);
+      j.containers = std::move(r.bind.containers);
+      j.plan = std::move(r.bind.plan);
+      j.fresh = r.bind.rc == kOk;
+      j.t0_ns = now_ns();
+      c->waiting = true;
+      c->bind_waiting = true;
+      c->t_req_ns = c->t_in_ns ? c->t_in_ns : now_ns();
+      c->t_in_ns = c->in.empty() ? 0 : now_ns();
+      kw->submit(std::move(j));
+      return;
+    }
+  }
   r.method = std::move(method);
   r.path = std::move(path);
   r.query = std::move(query);

@@ -1,0 +1,504 @@
+// Native bind writes to kube-apiserver (see kubewriter.h).
+#include "nanogpu/kubewriter.h"
+
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <openssl/err.h>
+#include <openssl/ssl.h>
+#include <sys/socket.h>
+#include <sys/stat.h>
+#include <sys/time.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <stdexcept>
+
+#include "nanogpu/json.h"
+
+namespace nanogpu {
+
+namespace {
+constexpr const char* kAssume = "nano-gpu/assume";
+constexpr const char* kAssumeTime = "nano-gpu/assume-time";
+constexpr const char* kContainerPrefix = "nano-gpu/container-";
+constexpr const char* kMergePatch = "application/merge-patch+json";
+constexpr const char* kJson = "application/json";
+
+uint64_t now_ns() {
+  return static_cast<uint64_t>(
+      std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count());
+}
+double wall_s() {
+  return std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+}
+double mono_s() { return static_cast<double>(now_ns()) * 1e-9; }
+
+std::string read_token(const std::string& path, int64_t* mtime) {
+  struct stat st {};
+  if (stat(path.c_str(), &st) != 0) return std::string();
+  *mtime = static_cast<int64_t>(st.st_mtim.tv_sec) * 1000000000LL + st.st_mtim.tv_nsec;
+  std::ifstream f(path);
+  std::stringstream ss;
+  ss << f.rdbuf();
+  std::string t = ss.str();
+  while (!t.empty() && (t.back() == '\n' || t.back() == '\r' || t.back() == ' ')) t.pop_back();
+  return t;
+}
+
+// Status.message of an error body, else the body itself.
+std::string api_message(const std::string& body) {
+  json::Doc d;
+  if (d.parse(body) && d.is(d.root(), json::Type::kObj)) {
+    const int32_t m = d.get(d.root(), "message");
+    if (d.is(m, json::Type::kStr)) return std::string(d.str(m));
+  }
+  return body.substr(0, 512);
+}
+std::string api_reason(const std::string& body) {
+  json::Doc d;
+  if (d.parse(body) && d.is(d.root(), json::Type::kObj)) {
+    const int32_t m = d.get(d.root(), "reason");
+    if (d.is(m, json::Type::kStr)) return std::string(d.str(m));
+  }
+  return std::string();
+}
+// ApiError's text in the Python client: "<status> <reason>: <message>"
+std::string api_error(int status, const std::string& body) {
+  if (status == 0) return body.empty() ? "connection to the API server failed" : body;
+  return std::to_string(status) + " " + api_reason(body) + ": " + api_message(body);
+}
+
+std::string pod_node(const std::string& body) {
+  json::Doc d;
+  if (!d.parse(body) || !d.is(d.root(), json::Type::kObj)) return std::string();
+  const int32_t sp = d.get(d.root(), "spec");
+  if (!d.is(sp, json::Type::kObj)) return std::string();
+  const int32_t n = d.get(sp, "nodeName");
+  return d.is(n, json::Type::kStr) ? std::string(d.str(n)) : std::string();
+}
+}  // namespace
+
+// ------------------------------------------------------------------------------ HttpConn
+HttpConn::~HttpConn() { close_(); }
+
+void HttpConn::close_() {
+  if (ssl_) {
+    SSL_free(static_cast<SSL*>(ssl_));
+    ssl_ = nullptr;
+  }
+  if (fd_ >= 0) ::close(fd_);
+  fd_ = -1;
+  buf_.clear();
+}
+
+bool HttpConn::connect_() {
+  close_();
+  addrinfo hints{};
+  hints.ai_family = AF_UNSPEC;
+  hints.ai_socktype = SOCK_STREAM;
+  addrinfo* res = nullptr;
+  if (getaddrinfo(t_->host.c_str(), std::to_string(t_->port).c_str(), &hints, &res) != 0 || !res) return false;
+  for (addrinfo* a = res; a; a = a->ai_next) {
+    const int fd = socket(a->ai_family, a->ai_socktype | SOCK_CLOEXEC, a->ai_protocol);
+    if (fd < 0) continue;
+    timeval tv{30, 0};
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+    setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    if (::connect(fd, a->ai_addr, a->ai_addrlen) == 0) {
+      fd_ = fd;
+      break;
+    }
+    ::close(fd);
+  }
+  freeaddrinfo(res);
+  if (fd_ < 0) return false;
+  if (ctx_) {
+    SSL* s = SSL_new(static_cast<SSL_CTX*>(ctx_));
+    if (!s) return close_(), false;
+    SSL_set_fd(s, fd_);
+    SSL_set_tlsext_host_name(s, t_->host.c_str());
+    if (!t_->insecure) SSL_set1_host(s, t_->host.c_str());
+    ssl_ = s;
+    if (SSL_connect(s) != 1) return close_(), false;
+  }
+  return true;
+}
+
+bool HttpConn::send_all(const char* p, size_t n) {
+  while (n) {
+    long w;
+    if (ssl_) {
+      const int r = SSL_write(static_cast<SSL*>(ssl_), p, static_cast<int>(std::min<size_t>(n, 1 << 30)));
+      w = r > 0 ? r : -1;
+    } else {
+      w = ::send(fd_, p, n, MSG_NOSIGNAL);
+      if (w < 0 && errno == EINTR) continue;
+    }
+    if (w <= 0) return false;
+    p += w;
+    n -= static_cast<size_t>(w);
+  }
+  return true;
+}
+
+long HttpConn::recv_some(char* p, size_t n) {
+  if (ssl_) {
+    const int r = SSL_read(static_cast<SSL*>(ssl_), p, static_cast<int>(n));
+    return r > 0 ? r : (SSL_get_error(static_cast<SSL*>(ssl_), r) == SSL_ERROR_ZERO_RETURN ? 0 : -1);
+  }
+  for (;;) {
+    const long r = ::recv(fd_, p, n, 0);
+    if (r < 0 && errno == EINTR) continue;
+    return r;
+  }
+}
+
+int HttpConn::exchange(const std::string& req, std::string* resp, bool* retryable) {
+  *retryable = false;
+  if (!send_all(req.data(), req.size())) {
+    *retryable = true;
+    return 0;
+  }
+  char tmp[16384];
+  size_t he;
+  bool got_any = !buf_.empty();
+  while ((he = buf_.find("\r\n\r\n")) == std::string::npos) {
+    const long r = recv_some(tmp, sizeof tmp);
+    if (r <= 0) {
+      *retryable = !got_any;   // the server closed an idle keep-alive connection
+      return 0;
+    }
+    got_any = true;
+    buf_.append(tmp, static_cast<size_t>(r));
+  }
+  const std::string head = buf_.substr(0, he);
+  buf_.erase(0, he + 4);
+  int status = 0;
+  if (head.size() > 12) status = std::atoi(head.c_str() + 9);
+  long clen = -1;
+  bool chunked = false, close_after = false;
+  size_t p = head.find("\r\n");
+  while (p != std::string::npos && p + 2 < head.size()) {
+    const size_t e = head.find("\r\n", p + 2);
+    std::string line = head.substr(p + 2, (e == std::string::npos ? head.size() : e) - p - 2);
+    const size_t colon = line.find(':');
+    if (colon != std::string::npos) {
+      std::string k = line.substr(0, colon);
+      for (char& ch : k) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
+      std::string v = line.substr(colon + 1);
+      while (!v.empty() && v.front() == ' ') v.erase(0, 1);
+      if (k == "content-length") clen = std::atol(v.c_str());
+      else if (k == "transfer-encoding" && v.find("chunked") != std::string::npos) chunked = true;
+      else if (k == "connection" && (v == "close" || v == "Close")) close_after = true;
+    }
+    p = e;
+  }
+  resp->clear();
+  if (chunked) {
+    for (;;) {
+      size_t le;
+      while ((le = buf_.find("\r\n")) == std::string::npos) {
+        const long r = recv_some(tmp, sizeof tmp);
+        if (r <= 0) return close_(), 0;
+        buf_.append(tmp, static_cast<size_t>(r));
+      }
+      const size_t sz = std::strtoul(buf_.c_str(), nullptr, 16);
+      while (buf_.size() < le + 2 + sz + 2) {
+        const long r = recv_some(tmp, sizeof tmp);
+        if (r <= 0) return close_(), 0;
+        buf_.append(tmp, static_cast<size_t>(r));
+      }
+      resp->append(buf_, le + 2, sz);
+      buf_.erase(0, le + 2 + sz + 2);
+      if (sz == 0) break;
+    }
+  } else if (clen >= 0) {
+    while (buf_.size() < static_cast<size_t>(clen)) {
+      const long r = recv_some(tmp, sizeof tmp);
+      if (r <= 0) return close_(), 0;
+      buf_.append(tmp, static_cast<size_t>(r));
+    }
+    resp->assign(buf_, 0, static_cast<size_t>(clen));
+    buf_.erase(0, static_cast<size_t>(clen));
+  } else {
+    for (;;) {   // no length: the body runs to the end of the connection
+      const long r = recv_some(tmp, sizeof tmp);
+      if (r <= 0) break;
+      buf_.append(tmp, static_cast<size_t>(r));
+    }
+    resp->swap(buf_);
+    close_after = true;
+  }
+  if (close_after) close_();
+  return status;
+}
+
+int HttpConn::request(const char* method, const std::string& path, const std::string& content_type,
+                      const std::string& body, const std::string& auth, std::string* resp) {
+  std::string req;
+  req.reserve(256 + body.size());
+  req += method;
+  req += ' ';
+  req += path;
+  req += " HTTP/1.1\r\nHost: ";
+  req += t_->host;
+  req += "\r\nUser-Agent: nano-gpu-scheduler-amd/0.1\r\nAccept: application/json\r\n";
+  if (!auth.empty()) req += "Authorization: Bearer " + auth + "\r\n";
+  if (!body.empty() || std::strcmp(method, "POST") == 0 || std::strcmp(method, "PATCH") == 0) {
+    req += "Content-Type: " + content_type + "\r\nContent-Length: " + std::to_string(body.size()) + "\r\n";
+  }
+  req += "\r\n";
+  req += body;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    const bool reused = fd_ >= 0;
+    if (!reused && !connect_()) {
+      *resp = "cannot connect to " + t_->host + ":" + std::to_string(t_->port);
+      return 0;
+    }
+    bool retryable = false;
+    const int st = exchange(req, resp, &retryable);
+    if (st > 0) return st;
+    close_();
+    if (!(reused && retryable)) {
+      if (resp->empty()) *resp = "connection to the API server failed";
+      return 0;
+    }
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------------------ KubeWriter
+KubeWriter::KubeWriter(KubeTarget target, std::shared_ptr<Ledger> ledger, Respond respond, int threads, int retries,
+                       bool record_events)
+    : t_(std::move(target)), ledger_(std::move(ledger)), respond_(std::move(respond)), retries_(retries),
+      events_(record_events) {
+  if (t_.tls) {
+    SSL_CTX* ctx = SSL_CTX_new(TLS_client_method());
+    if (!ctx) throw std::runtime_error("KubeWriter: SSL_CTX_new failed");
+    if (!t_.ca_file.empty()) {
+      if (SSL_CTX_load_verify_locations(ctx, t_.ca_file.c_str(), nullptr) != 1) {
+        SSL_CTX_free(ctx);
+        throw std::runtime_error("KubeWriter: cannot load CA file " + t_.ca_file);
+      }
+    } else {
+      SSL_CTX_set_default_verify_paths(ctx);
+    }
+    SSL_CTX_set_verify(ctx, t_.insecure ? SSL_VERIFY_NONE : SSL_VERIFY_PEER, nullptr);
+    if (!t_.cert_file.empty() && !t_.key_file.empty()) {
+      if (SSL_CTX_use_certificate_chain_file(ctx, t_.cert_file.c_str()) != 1 ||
+          SSL_CTX_use_PrivateKey_file(ctx, t_.key_file.c_str(), SSL_FILETYPE_PEM) != 1) {
+        SSL_CTX_free(ctx);
+        throw std::runtime_error("KubeWriter: cannot load the client certificate / key");
+      }
+    }
+    ctx_ = ctx;
+  }
+  token_ = t_.token;
+  if (!t_.token_file.empty()) {
+    const std::string tok = read_token(t_.token_file, &token_mtime_);
+    if (!tok.empty()) token_ = tok;
+  }
+  token_checked_ = mono_s();
+  if (threads < 1) threads = 1;
+  for (int i = 0; i < threads; ++i) threads_.emplace_back([this] { run(); });
+}
+
+KubeWriter::~KubeWriter() {
+  stop();
+  if (ctx_) SSL_CTX_free(static_cast<SSL_CTX*>(ctx_));
+}
+
+void KubeWriter::stop() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (stop_) return;
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : threads_)
+    if (t.joinable()) t.join();
+  // anything still queued: kube-scheduler gets an answer (and retries), the ledger is clean
+  for (BindJob& j : q_) {
+    if (j.fresh) ledger_->release(j.uid);
+    respond_(j.id, 500, "{\"Error\":\"nano-gpu: extender shutting down\"}");
+  }
+  q_.clear();
+}
+
+void KubeWriter::submit(BindJob job) {
+  stats.inflight.fetch_add(1, std::memory_order_relaxed);
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    q_.push_back(std::move(job));
+  }
+  cv_.notify_one();
+}
+
+std::string KubeWriter::auth() {
+  std::lock_guard<std::mutex> g(tok_mu_);
+  if (!t_.token_file.empty() && mono_s() - token_checked_ > 60.0) {
+    token_checked_ = mono_s();
+    int64_t mt = 0;
+    struct stat st {};
+    if (stat(t_.token_file.c_str(), &st) == 0) {
+      mt = static_cast<int64_t>(st.st_mtim.tv_sec) * 1000000000LL + st.st_mtim.tv_nsec;
+      if (mt != token_mtime_) {
+        const std::string tok = read_token(t_.token_file, &token_mtime_);
+        if (!tok.empty()) token_ = tok;
+      }
+    }
+  }
+  return token_;
+}
+
+int KubeWriter::call(HttpConn* c, const char* method, const std::string& path, const std::string& ctype,
+                     const std::string& body, std::string* resp, bool retry) {
+  int st = 0;
+  for (int attempt = 0;; ++attempt) {
+    st = c->request(method, path, ctype, body, auth(), resp);
+    if (st == 401 && !t_.token_file.empty() && attempt == 0) {
+      std::lock_guard<std::mutex> g(tok_mu_);   // rotated under us: re-read once
+      const std::string tok = read_token(t_.token_file, &token_mtime_);
+      if (!tok.empty()) token_ = tok;
+      continue;
+    }
+    const bool transient = st >= 500 || st == 429;
+    if (!retry || !transient || attempt >= retries_) return st;
+    stats.retries.fetch_add(1, std::memory_order_relaxed);
+    std::this_thread::sleep_for(std::chrono::microseconds(5000LL << attempt));
+  }
+}
+
+void KubeWriter::process(HttpConn* c, BindJob& j) {
+  const std::string base = "/api/v1/namespaces/" + j.ns + "/pods/" + j.name;
+  std::string err;
+  std::string resp;
+  // 1. placement annotations + assume label (pu.placement_patch_names)
+  std::string patch = "{\"metadata\":{\"annotations\":{";
+  for (size_t k = 0; k < j.containers.size() && k < j.plan.size(); ++k) {
+    json::append_quoted(&patch, kContainerPrefix + j.containers[k]);
+    patch += ":\"";
+    for (size_t i = 0; i < j.plan[k].size(); ++i) {
+      if (i) patch += ',';
+      patch += std::to_string(j.plan[k][i]);
+    }
+    patch += "\",";
+  }
+  char ts[48];
+  std::snprintf(ts, sizeof ts, "%.6f", wall_s());
+  patch += "\"";
+  patch += kAssume;
+  patch += "\":\"true\",\"";
+  patch += kAssumeTime;
+  patch += "\":\"";
+  patch += ts;
+  patch += "\"},\"labels\":{\"";
+  patch += kAssume;
+  patch += "\":\"true\"}}}";
+  const uint64_t t1 = now_ns();
+  int st = call(c, "PATCH", base, kMergePatch, patch, &resp, true);
+  const uint64_t t2 = now_ns();
+  stats.patch_ns.fetch_add(t2 - t1, std::memory_order_relaxed);
+  if (st < 200 || st >= 300) {
+    err = api_error(st, resp);
+  } else {
+    // 2. the binding
+    std::string b = "{\"apiVersion\":\"v1\",\"kind\":\"Binding\",\"metadata\":{\"name\":";
+    json::append_quoted(&b, j.name);
+    b += ",\"namespace\":";
+    json::append_quoted(&b, j.ns);
+    b += ",\"uid\":";
+    json::append_quoted(&b, j.uid);
+    b += "},\"target\":{\"apiVersion\":\"v1\",\"kind\":\"Node\",\"name\":";
+    json::append_quoted(&b, j.node);
+    b += "}}";
+    st = call(c, "POST", base + "/binding", kJson, b, &resp, true);
+    stats.binding_ns.fetch_add(now_ns() - t2, std::memory_order_relaxed);
+    if (st == 409) {
+      // a retried POST whose first attempt landed: already on this node is success
+      std::string got;
+      const int gs = call(c, "GET", base, kJson, std::string(), &got, true);
+      if (gs == 200 && pod_node(got) == j.node) st = 201;
+    }
+    if (st < 200 || st >= 300) err = api_error(st, resp);
+  }
+  if (err.empty()) {
+    ledger_->commit(j.uid);
+    stats.ok.fetch_add(1, std::memory_order_relaxed);
+    respond_(j.id, 200, "{\"Error\":\"\"}");
+    return;
+  }
+  stats.failed.fetch_add(1, std::memory_order_relaxed);
+  if (j.fresh) {
+    // D2: roll the reservation back, then un-annotate (best effort) and record the event
+    ledger_->release(j.uid);
+    stats.rollbacks.fetch_add(1, std::memory_order_relaxed);
+    std::string un = "{\"metadata\":{\"annotations\":{";
+    for (const std::string& n : j.containers) {
+      json::append_quoted(&un, kContainerPrefix + n);
+      un += ":null,";
+    }
+    un += "\"";
+    un += kAssume;
+    un += "\":null},\"labels\":{\"";
+    un += kAssume;
+    un += "\":null}}}";
+    std::string ignored;
+    call(c, "PATCH", base, kMergePatch, un, &ignored, false);
+    if (events_ && st > 0) {
+      char tbuf[32];
+      const std::time_t now = std::time(nullptr);
+      std::tm g{};
+      gmtime_r(&now, &g);
+      std::strftime(tbuf, sizeof tbuf, "%Y-%m-%dT%H:%M:%SZ", &g);
+      char suffix[24];
+      std::snprintf(suffix, sizeof suffix, ".%016llx", static_cast<unsigned long long>(now_ns()));
+      std::string ev = "{\"apiVersion\":\"v1\",\"kind\":\"Event\",\"metadata\":{\"name\":";
+      json::append_quoted(&ev, j.name + suffix);
+      ev += ",\"namespace\":";
+      json::append_quoted(&ev, j.ns);
+      ev += "},\"involvedObject\":{\"kind\":\"Pod\",\"name\":";
+      json::append_quoted(&ev, j.name);
+      ev += ",\"namespace\":";
+      json::append_quoted(&ev, j.ns);
+      ev += ",\"uid\":";
+      json::append_quoted(&ev, j.uid);
+      ev += "},\"reason\":\"FailedBinding\",\"message\":";
+      json::append_quoted(&ev, "nano-gpu bind failed: " + err);
+      ev += ",\"type\":\"Warning\",\"source\":{\"component\":\"nano-gpu-scheduler\"},\"firstTimestamp\":\"";
+      ev += tbuf;
+      ev += "\",\"lastTimestamp\":\"";
+      ev += tbuf;
+      ev += "\",\"count\":1}";
+      call(c, "POST", "/api/v1/namespaces/" + j.ns + "/events", kJson, ev, &ignored, false);
+    }
+  }
+  std::string body = "{\"Error\":";
+  json::append_quoted(&body, err);
+  body += "}";
+  respond_(j.id, 500, body);
+}
+
+void KubeWriter::run() {
+  HttpConn c(&t_, ctx_);
+  for (;;) {
+    BindJob j;
+    {
+      std::unique_lock<std::mutex> g(mu_);
+      cv_.wait(g, [this] { return stop_ || !q_.empty(); });
+      if (stop_) return;
+      j = std::move(q_.front());
+      q_.pop_front();
+    }
+    process(&c, j);
+    stats.inflight.fetch_sub(1, std::memory_order_relaxed);
+  }
+}
+
+}  // namespace nanogpu

@@ -1,0 +1,211 @@
+"""The native API server (native/src/apiserver.cpp) against the Python HTTP fake
+(nanogpu/k8s/fake_apiserver.py): one behaviour suite, run over the REST client against both,
+so the bench's shared API server answers exactly what the tests' fake answers (codes, Status
+bodies, merge-patch, binding conflicts, selectors, watch resume, 410 Gone)."""
+import asyncio
+import json
+
+import pytest
+
+from nanogpu import _native as N
+from nanogpu.k8s import podutil as pu
+from nanogpu.k8s.client import ApiError, KubeClient, KubeConfig
+from nanogpu.k8s.fake_apiserver import FakeKubeStore, serve
+
+
+class PyServer:
+    async def start(self):
+        self.store = FakeKubeStore(history=64)
+        self.runner, port = await serve(self.store)
+        return f"http://127.0.0.1:{port}"
+
+    def compact(self):
+        self.store.compact("pods")
+
+    async def stop(self):
+        await self.runner.cleanup()
+
+
+class NativeServer:
+    async def start(self):
+        self.srv = N.ApiServer("127.0.0.1", 0, 2, 64)
+        return f"http://127.0.0.1:{self.srv.port}"
+
+    def compact(self):
+        self.srv.compact("pods")
+
+    async def stop(self):
+        self.srv.stop()
+
+
+def run(kind, body):
+    async def main():
+        srv = PyServer() if kind == "python" else NativeServer()
+        url = await srv.start()
+        api = KubeClient(KubeConfig(server=url))
+        try:
+            await body(api, srv)
+        finally:
+            await api.close()
+            await srv.stop()
+
+    asyncio.run(main())
+
+
+KINDS = ["python", "native"]
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_pod_lifecycle_codes_and_bodies(kind):
+    async def body(api, srv):
+        await api.request("POST", "/api/v1/nodes", pu.make_node("n0", 8, "{}"))
+        p = await api.create_pod(pu.make_pod("a", [("main", 20)], namespace="ns1"))
+        m = pu.meta(p)
+        assert m["namespace"] == "ns1" and m["uid"] and m["resourceVersion"] and p["status"]["phase"] == "Pending"
+        with pytest.raises(ApiError) as e:
+            await api.create_pod(pu.make_pod("a", [("main", 20)], namespace="ns1"))
+        assert e.value.status == 409 and e.value.reason == "AlreadyExists"
+        q = await api.patch_pod("ns1", "a", {"metadata": {"annotations": {"x": "1"}, "labels": {"l": "v"}}})
+        assert q["metadata"]["annotations"]["x"] == "1" and int(q["metadata"]["resourceVersion"]) > int(m["resourceVersion"])
+        q = await api.patch_pod("ns1", "a", {"metadata": {"annotations": {"x": None}}})
+        assert "x" not in q["metadata"]["annotations"] and q["metadata"]["labels"]["l"] == "v"
+        with pytest.raises(ApiError) as e:
+            await api.bind_pod("ns1", "a", "wrong-uid", "n0")
+        assert e.value.status == 409
+        with pytest.raises(ApiError) as e:
+            await api.bind_pod("ns1", "a", m["uid"], "nope")
+        assert e.value.status == 404
+        await api.bind_pod("ns1", "a", m["uid"], "n0")
+        got = await api.get_pod("ns1", "a")
+        assert got["spec"]["nodeName"] == "n0" and got["status"]["phase"] == "Running"
+        with pytest.raises(ApiError) as e:
+            await api.bind_pod("ns1", "a", m["uid"], "n0")
+        assert e.value.status == 409 and "already assigned" in e.value.message
+        await api.delete_pod("ns1", "a")
+        with pytest.raises(ApiError) as e:
+            await api.get_pod("ns1", "a")
+        assert e.value.status == 404 and e.value.reason == "NotFound"
+        with pytest.raises(ApiError) as e:
+            await api.delete_pod("ns1", "a")
+        assert e.value.status == 404
+
+    run(kind, body)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_selectors_and_listing(kind):
+    async def body(api, srv):
+        await api.request("POST", "/api/v1/nodes", pu.make_node("n0", 8, "{}", {"gpu": "yes"}))
+        await api.request("POST", "/api/v1/nodes", pu.make_node("n1", 8, "{}"))
+        for i in range(4):
+            p = await api.create_pod(pu.make_pod(f"p{i}", [("main", 10)]))
+            if i % 2:
+                await api.patch_pod("default", f"p{i}", {"metadata": {"labels": {"nano-gpu/assume": "true"}}})
+                await api.bind_pod("default", f"p{i}", pu.pod_uid(p), "n0")
+        items, rv = await api.list_pods(label_selector="nano-gpu/assume=true", field_selector="spec.nodeName=n0")
+        assert sorted(pu.meta(p)["name"] for p in items) == ["p1", "p3"] and int(rv) > 0
+        items, _ = await api.list_pods(label_selector="nano-gpu/assume!=true")
+        assert sorted(pu.meta(p)["name"] for p in items) == ["p0", "p2"]
+        items, _ = await api.list_pods(namespace="other")
+        assert items == []
+        nodes, _ = await api.list_nodes(label_selector="gpu")
+        assert [pu.meta(n)["name"] for n in nodes] == ["n0"]
+        n = await api.patch_node_status("n1", {"status": {"capacity": {"nano-gpu/gpu-percent": "800"}}})
+        assert n["status"]["capacity"]["nano-gpu/gpu-percent"] == "800"
+
+    run(kind, body)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_watch_resume_and_gone(kind):
+    async def body(api, srv):
+        await api.create_pod(pu.make_pod("a", [("main", 10)]))
+        _, rv = await api.list_pods()
+        await api.create_pod(pu.make_pod("b", [("main", 10)]))
+        await api.patch_pod("default", "b", {"metadata": {"annotations": {"k": "v"}}})
+        await api.delete_pod("default", "a")
+        seen = []
+
+        async def consume():
+            async for batch in api.watch_batches("pods", rv, timeout_s=1):
+                seen.extend((ev["type"], pu.meta(ev["object"])["name"]) for ev in batch)
+                if len(seen) >= 3:
+                    return
+
+        await asyncio.wait_for(consume(), 5)
+        assert seen == [("ADDED", "b"), ("MODIFIED", "b"), ("DELETED", "a")]
+        # live events reach an open watch
+        _, rv2 = await api.list_pods()
+        got = []
+
+        async def live():
+            async for ev in api.watch("pods", rv2, timeout_s=2):
+                got.append(ev["type"])
+                return
+
+        task = asyncio.ensure_future(live())
+        await asyncio.sleep(0.1)
+        await api.create_pod(pu.make_pod("c", [("main", 10)]))
+        await asyncio.wait_for(task, 5)
+        assert got == ["ADDED"]
+        # the watch cache forgets: a resume from an old version is 410 Gone (HTTP or in-stream)
+        srv.compact()
+        gone = None
+        try:
+            async for ev in api.watch("pods", rv, timeout_s=1):
+                gone = ev
+                break
+        except ApiError as e:
+            gone = {"type": "ERROR", "object": {"code": e.status}}
+        assert gone["type"] == "ERROR" and gone["object"]["code"] == 410
+
+    run(kind, body)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_leases_and_events(kind):
+    async def body(api, srv):
+        lease = {"apiVersion": "coordination.k8s.io/v1", "kind": "Lease", "metadata": {"name": "x"},
+                 "spec": {"holderIdentity": "a"}}
+        le = await api.create_lease("kube-system", lease)
+        with pytest.raises(ApiError) as e:
+            await api.create_lease("kube-system", lease)
+        assert e.value.status == 409
+        le["spec"]["holderIdentity"] = "b"
+        le2 = await api.update_lease("kube-system", "x", le)
+        assert le2["spec"]["holderIdentity"] == "b"
+        with pytest.raises(ApiError) as e:
+            await api.update_lease("kube-system", "x", le)            # stale resourceVersion
+        assert e.value.status == 409
+        assert (await api.get_lease("kube-system", "x"))["spec"]["holderIdentity"] == "b"
+        await api.create_event("default", {"kind": "Pod", "name": "p"}, "FailedBinding", "m")
+
+    run(kind, body)
+
+
+def test_native_bulk_create_delete_and_timeout_ends_the_stream():
+    srv = N.ApiServer("127.0.0.1", 0, 2, 1000)
+    try:
+        pods = [json.dumps(pu.make_pod(f"p{i}", [("main", 10)], namespace="b")) for i in range(50)]
+        assert srv.create_pods(pods) == [201] * 50
+        assert srv.create_pods(pods[:1]) == [409]
+        code, body = srv.call("GET", "/api/v1/namespaces/b/pods")
+        assert code == 200 and len(json.loads(body)["items"]) == 50
+        assert srv.delete_pods([("b", f"p{i}") for i in range(60)]) == 50
+        st = json.loads(srv.stats())
+        assert st["pods"] == 0 and st["calls"]["create_pod"] == 50
+
+        async def main():
+            api = KubeClient(KubeConfig(server=f"http://127.0.0.1:{srv.port}"))
+            try:
+                _, rv = await api.list_pods()
+                t0 = asyncio.get_running_loop().time()
+                async for _ in api.watch("pods", rv, timeout_s=1):
+                    pass                                   # nothing happens; the stream ends cleanly
+                assert 0.8 < asyncio.get_running_loop().time() - t0 < 3.0
+            finally:
+                await api.close()
+
+        asyncio.run(main())
+    finally:
+        srv.stop()

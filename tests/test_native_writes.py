@@ -1,0 +1,197 @@
+"""Native bind writes (native/src/kubewriter.cpp): the front door's C++ threads do the
+bind's PATCH + binding POST + ledger commit. Same contract as the Python path
+(nanogpu/extender/verbs.py::Extender._write, the reference's Bind at dealer.go:155-203 with
+D1/D2 fixed): transient 5xx retried, a failed binding rolls the reservation back, takes the
+placement annotations off again and records a FailedBinding event; kube-scheduler gets
+{"Error": ...}. Each test runs with the writer on and off and expects the same outcome."""
+import asyncio
+import json
+
+import aiohttp
+import pytest
+
+from nanogpu import types as T
+from nanogpu.app import Config, Runtime
+from nanogpu.k8s import podutil as pu
+from nanogpu.k8s.client import ApiError
+from nanogpu.k8s.fake_apiserver import Faults, FakeKubeStore, serve
+from nanogpu.topology.model import synthetic_mi355x
+
+
+async def _stack(store, native: bool):
+    runner, port = await serve(store)
+    rt = Runtime(Config(kube_api=f"http://127.0.0.1:{port}", port=0, host="127.0.0.1",
+                        policy_config_path="/nonexistent", native_bind_writes=native))
+    await rt.start()
+    return runner, rt
+
+
+async def _schedule(base, pod, node):
+    async with aiohttp.ClientSession() as s:
+        args = {"Pod": pod, "NodeNames": [node]}
+        async with s.post(f"{base}/scheduler/filter", json=args) as r:
+            assert (await r.json())["NodeNames"] == [node]
+        m = pu.meta(pod)
+        async with s.post(f"{base}/scheduler/bind", json={"PodName": m["name"], "PodNamespace": m["namespace"],
+                                                            "PodUID": m["uid"], "Node": node}) as r:
+            return r.status, await r.json()
+
+
+async def _metrics(base):
+    async with aiohttp.ClientSession() as s:
+        async with s.get(f"{base}/metrics") as r:
+            return await r.text()
+
+
+@pytest.mark.parametrize("native", [True, False])
+def test_bind_writes_retry_transient_errors(native):
+    async def main():
+        store = FakeKubeStore(faults=Faults(patch_error_rate=0.3, bind_error_rate=0.3, seed=11))
+        store.add_node(pu.make_node("n0", 8, synthetic_mi355x(8).to_json()))
+        runner, rt = await _stack(store, native)
+        base = f"http://127.0.0.1:{rt.bound_port}"
+        try:
+            ok = 0
+            for i in range(12):
+                p = store.create_pod(pu.make_pod(f"p{i}", [("main", 10)]))
+                status, res = await _schedule(base, p, "n0")
+                ok += res["Error"] == ""
+            assert ok >= 10                     # 3 retries through 30 % 5xx
+            assert rt.state.ledger.n_pods == ok
+            text = await _metrics(base)
+            if native:
+                assert 'nanogpu_native_binds_total{result="ok"} ' + str(ok) in text
+                assert "nanogpu_native_api_retries_total" in text
+            else:
+                assert "nanogpu_native_binds_total" not in text
+        finally:
+            await rt.stop()
+            await runner.cleanup()
+
+    asyncio.run(main())
+
+
+@pytest.mark.parametrize("native", [True, False])
+def test_failed_binding_rolls_back_and_unannotates(native):
+    async def main():
+        store = FakeKubeStore(faults=Faults(bind_error_rate=1.0))
+        store.add_node(pu.make_node("n0", 8, synthetic_mi355x(8).to_json()))
+        runner, rt = await _stack(store, native)
+        base = f"http://127.0.0.1:{rt.bound_port}"
+        try:
+            p = store.create_pod(pu.make_pod("doomed", [("main", 40)]))
+            status, res = await _schedule(base, p, "n0")
+            assert status == 500 and "500" in res["Error"] and "injected binding failure" in res["Error"]
+            assert rt.state.status()["n0"]["GPUs"][0]["Percent"] == 100      # D2: rolled back
+            assert rt.state.ledger.lookup(pu.pod_uid(p)) is None
+
+            def clean():
+                ann = store.get_pod("default", "doomed")["metadata"].get("annotations") or {}
+                return T.ANNOTATION_GPU_ASSUME not in ann and T.container_annotation("main") not in ann
+
+            for _ in range(200):
+                if clean() and any(e["reason"] == "FailedBinding" for e in store.events):
+                    break
+                await asyncio.sleep(0.01)
+            assert clean()
+            ev = next(e for e in store.events if e["reason"] == "FailedBinding")
+            assert ev["involvedObject"]["name"] == "doomed" and ev["message"].startswith("nano-gpu bind failed: ")
+        finally:
+            await rt.stop()
+            await runner.cleanup()
+
+    asyncio.run(main())
+
+
+@pytest.mark.parametrize("native", [True, False])
+def test_binding_conflict_on_the_same_node_is_success(native):
+    """A retried binding POST whose first attempt landed answers 409; the pod already sits on
+    the requested node, so the bind succeeded."""
+    async def main():
+        store = FakeKubeStore()
+        store.add_node(pu.make_node("n0", 8, synthetic_mi355x(8).to_json()))
+        runner, rt = await _stack(store, native)
+        base = f"http://127.0.0.1:{rt.bound_port}"
+        try:
+            p = store.create_pod(pu.make_pod("a", [("main", 30)]))
+            orig = store.bind_pod
+
+            def bind_then_conflict(ns, name, uid, node):
+                orig(ns, name, uid, node)
+                raise ApiError(409, "already assigned", "Conflict")
+
+            store.bind_pod = bind_then_conflict
+            status, res = await _schedule(base, p, "n0")
+            assert status == 200 and res == {"Error": ""}
+            assert store.get_pod("default", "a")["spec"]["nodeName"] == "n0"
+            assert rt.state.status()["n0"]["GPUs"][0]["Percent"] == 70
+            ann = store.get_pod("default", "a")["metadata"]["annotations"]
+            assert ann[T.container_annotation("main")] == "0" and float(ann[T.ANNOTATION_ASSUME_TIME]) > 0
+        finally:
+            await rt.stop()
+            await runner.cleanup()
+
+    asyncio.run(main())
+
+
+def test_native_writer_speaks_tls_with_a_bearer_token(tmp_path):
+    """https + token (how an in-cluster extender reaches kube-apiserver): a TLS proxy with a
+    self-signed certificate in front of the fake API server checks the Authorization header."""
+    import shutil
+    import ssl
+    import subprocess
+
+    if shutil.which("openssl") is None:
+        pytest.skip("openssl CLI not available")
+    key, crt = tmp_path / "k.pem", tmp_path / "c.pem"
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", str(key), "-out", str(crt),
+                    "-days", "1", "-subj", "/CN=127.0.0.1", "-addext", "subjectAltName=IP:127.0.0.1"],
+                   check=True, capture_output=True)
+    tok = tmp_path / "token"
+    tok.write_text("s3cret\n")
+
+    async def main():
+        from aiohttp import web
+
+        from nanogpu.k8s.client import KubeConfig
+        from nanogpu.k8s.fake_apiserver import make_app
+
+        store = FakeKubeStore()
+        store.add_node(pu.make_node("n0", 8, synthetic_mi355x(8).to_json()))
+        seen = []
+
+        @web.middleware
+        async def auth(request, handler):
+            seen.append(request.headers.get("Authorization"))
+            if request.headers.get("Authorization") != "Bearer s3cret":
+                return web.json_response({"kind": "Status", "code": 401, "message": "Unauthorized"}, status=401)
+            return await handler(request)
+
+        app = make_app(store)
+        app.middlewares.append(auth)
+        runner = web.AppRunner(app)
+        await runner.setup()
+        sctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+        sctx.load_cert_chain(str(crt), str(key))
+        site = web.TCPSite(runner, "127.0.0.1", 0, ssl_context=sctx)
+        await site.start()
+        port = site._server.sockets[0].getsockname()[1]
+        from nanogpu.k8s.client import KubeClient
+
+        api = KubeClient(KubeConfig(server=f"https://127.0.0.1:{port}", ca_file=str(crt), token_file=str(tok),
+                                    token="s3cret"))
+        rt = Runtime(Config(port=0, host="127.0.0.1", policy_config_path="/nonexistent"), api=api)
+        await rt.start()
+        try:
+            assert rt.native.fe.kube_writer_stats() is not None
+            base = f"http://127.0.0.1:{rt.bound_port}"
+            p = store.create_pod(pu.make_pod("t", [("main", 20)]))
+            status, res = await _schedule(base, p, "n0")
+            assert status == 200 and res == {"Error": ""}, res
+            assert store.get_pod("default", "t")["spec"]["nodeName"] == "n0"
+            assert rt.native.fe.kube_writer_stats()["ok"] == 1
+        finally:
+            await rt.stop()
+            await runner.cleanup()
+
+    asyncio.run(main())

@@ -1,3 +1,4 @@
+# GPU validation on the gpurun box: GPU tests, smoke(), a 20-step bench, a kernel-trace profile.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
@@ -6,8 +7,10 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout
 tail -5 gpurun_out/gputest.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail -30 gpurun_out/smoke.log; exit 1; }
 tail -2 gpurun_out/smoke.log
-timeout -k 10 600 python -u bench.py --steps 20 --warmup 3 > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -30 gpurun_out/bench.log; exit 1; }
+timeout -k 10 600 python -u bench.py --steps ${BENCH_STEPS:-20} --warmup 3 > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -30 gpurun_out/bench.log; exit 1; }
 tail -1 gpurun_out/bench.log | cut -c1-1500
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run -- python3 $R/bench.py --steps 5 --warmup 1 > $R/gpurun_out/prof.log 2>&1 || { echo "prof failed"; tail -20 $R/gpurun_out/prof.log; exit 1; }
+if [ "${PROFILE:-1}" = "1" ]; then
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run -- python3 $R/bench.py --steps 5 --warmup 1 > $R/gpurun_out/prof.log 2>&1 || { echo "prof failed"; tail -20 $R/gpurun_out/prof.log; exit 1; }
+fi
 echo done
