@@ -8,13 +8,19 @@ What one step is (all of it inside the timed region):
     gpu-percent {10, 25, 50} with HBM requests {8, 16, 32, 64} GiB;
   * every pod goes through the full extender protocol over loopback HTTP. A kube-scheduler
     stand-in runs in its own process (as kube-scheduler does in a cluster): a serial
-    scheduling cycle filter -> priorities -> select host on one keep-alive connection, and
-    binds on a pool of threads. The extender (this process) answers filter/priorities in
-    its native C++ front door, reserves on the native ledger, PATCHes the placement
-    annotations and POSTs the binding;
-  * after the burst the whole burst is deleted and the pod controller releases every
-    share from the ledger (the create/delete churn of BASELINE config 5).
+    scheduling cycle filter -> priorities -> select host on one keep-alive connection
+    (kube-scheduler's score combining, nanogpu/sim/kubescore.py), and binds sent the moment a
+    host is chosen. The extender answers filter/priorities in its native C++ front door,
+    reserves on the native ledger, and its C++ writer threads PATCH the placement
+    annotations and POST the binding to the API server, then commit;
+  * after the burst the whole burst is deleted; the pod controller sees the DELETED events
+    on its watch and releases every share from the ledger (BASELINE config 5's churn).
+The API server (default) is ONE native HTTP API server (native/src/apiserver.cpp) in a
+process of its own, shared by every rank: binds are real REST writes, the pod controller
+(rank 0 only, worker 0 of a replica) follows a real chunked watch. `--inproc-api` gives each
+rank an in-process store instead (round 1's extender-isolated setup; `value_inproc_api`).
 `value` = pods bound per second over the K timed steps (whole job, all ranks).
+`value_rtt2ms` repeats the run with a 2 ms round trip on every API answer.
 The stand-in is C++ by default (kube-scheduler is compiled Go; the Python stand-in's
 interpreter time per pod exceeded the extender's and capped the rate): `--driver python`
 selects the Python one, `--inproc-driver` runs a Python stand-in inside the extender's
@@ -22,8 +28,8 @@ event loop.
 
 Scaling (`--gpus N`, one torchrun rank per GPU): every rank is one extender worker; all
 workers share ONE native ledger in /dev/shm (the SO_REUSEPORT replica design of
-nanogpu.app), each drives 1/N of the burst through its own HTTP endpoint, so the burst and
-the cluster are fixed while workers are added ("strong" scaling). The GPUs are used for the
+nanogpu.app) and ONE API server, each drives 1/N of the burst through its own HTTP
+endpoint, so the burst and the cluster are fixed while workers are added ("strong" scaling). The GPUs are used for the
 node model: each rank reads its MI355X through the native KFD/amdsmi reader + HIP probe
 (HBM copy rate); the xGMI link weights the topology scorer uses come from the peer-pull probe
 over every pair of visible GPUs (all ranks together), else from the rate KFD publishes for the
@@ -64,13 +70,14 @@ def parse_args():
     ap.add_argument("--rtt-variant-ms", type=float, default=2.0,
                     help="after the timed steps, a second pass with this API round trip (0: none)")
     ap.add_argument("--rtt-variant-steps", type=int, default=3)
-    ap.add_argument("--shared-api", action="store_true",
-                    help="one API server for the whole job over HTTP (the native API server, "
-                         "native/src/apiserver.cpp, in its own process): every rank's extender talks "
-                         "REST to it and only rank 0 runs the pod controller, as worker 0 of a replica")
-    ap.add_argument("--shared-variant-steps", type=int, default=3,
-                    help="after the timed steps, a pass with --shared-api (0: none)")
-    ap.add_argument("--apiserver-threads", type=int, default=4, help="--shared-api: API server IO threads")
+    ap.add_argument("--inproc-api", action="store_true",
+                    help="each rank gets an in-process API store of its own (round 1's extender-isolated "
+                         "setup) instead of the default: ONE API server for the whole job over HTTP (the "
+                         "native API server, native/src/apiserver.cpp, in its own process) that every "
+                         "rank's extender talks REST to, with only rank 0 running the pod controller")
+    ap.add_argument("--inproc-variant-steps", type=int, default=3,
+                    help="after the timed steps, a pass with --inproc-api (0: none)")
+    ap.add_argument("--apiserver-threads", type=int, default=4, help="shared API server IO threads")
     ap.add_argument("--inflight-binds", type=int, default=64)
     ap.add_argument("--no-gpu", action="store_true", help="skip GPU discovery (CPU-only rehearsal)")
     ap.add_argument("--json-out", default="")
@@ -311,7 +318,7 @@ def burst(rank: int, world: int, total: int, step: int, seed: int) -> list[dict]
     return pods
 
 
-def apiserver_main(conn, threads: int) -> None:
+def apiserver_main(conn, threads: int, latency_s: float = 0.0) -> None:
     """The shared API server's process: a native API server (native/src/apiserver.cpp) on its
     own L3 domain, plus a command pipe through which rank 0 plays the workload's clients
     (bulk create / delete of a step's pods; the pod JSON is shipped before the clock starts)."""
@@ -326,6 +333,7 @@ def apiserver_main(conn, threads: int) -> None:
         pass
     affinity.apply(affinity.pick_cpus())
     srv = core().ApiServer("127.0.0.1", 0, threads, 1 << 20)
+    srv.set_latency(latency_s)     # modelled API round trip on every REST answer
     steps: dict = {}
     conn.send(srv.port)
     while True:
@@ -359,12 +367,12 @@ def apiserver_main(conn, threads: int) -> None:
 class ApiServerProc:
     """Rank 0's handle on the shared API server process."""
 
-    def __init__(self, threads: int):
+    def __init__(self, threads: int, latency_s: float = 0.0):
         import multiprocessing as mp
 
         ctx = mp.get_context("spawn")
         self.conn, child = ctx.Pipe()
-        self.proc = ctx.Process(target=apiserver_main, args=(child, threads), daemon=True)
+        self.proc = ctx.Process(target=apiserver_main, args=(child, threads, latency_s), daemon=True)
         self.proc.start()
         self.url = f"http://127.0.0.1:{self.conn.recv()}"
 
@@ -466,7 +474,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
     # the pod controller (worker 0 of a replica), so every release goes through its watch.
     # Rank 0 is also the workload's client: it has the API server create and delete every
     # rank's pods. Without it each rank has an in-process store of its own (extender-isolated).
-    shared = bool(getattr(args, "shared_api", False)) and conn is not None
+    shared = not getattr(args, "inproc_api", False) and conn is not None
     loop = asyncio.get_running_loop()
 
     async def barrier() -> None:
@@ -483,7 +491,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
     if shared:
         url = None
         if d.rank == 0:
-            apisrv = ApiServerProc(args.apiserver_threads)
+            apisrv = ApiServerProc(args.apiserver_threads, args.api_rtt_ms / 1e3)
             apisrv.add_nodes(nodes)
             url = apisrv.url
         url = d.bcast_obj(url)
@@ -727,7 +735,7 @@ def main() -> int:
     d = Dist(args.gpus)
     d.init(use_gpu=not args.no_gpu)
     topo, gpu_info = node_template(d, args)
-    variant = shared_v = None
+    variant = inproc_v = None
     try:
         res = run_pass(d, args, topo, conn, "main")
         if args.rtt_variant_ms > 0:
@@ -740,15 +748,15 @@ def main() -> int:
                 variant = summarize(d, v_args, run_pass(d, v_args, topo, conn, "rtt"))
             except Exception as e:   # the headline result stands; say what failed
                 variant = {"error": f"{type(e).__name__}: {e}"}
-        if args.shared_variant_steps > 0 and not args.shared_api and not args.inproc_driver:
-            # the same bursts through ONE HTTP API server shared by every rank (the native one)
-            s_args = argparse.Namespace(**{**vars(args), "shared_api": True, "api_rtt_ms": 0.0,
-                                           "steps": args.shared_variant_steps, "warmup": 1,
+        if args.inproc_variant_steps > 0 and not args.inproc_api and not args.inproc_driver:
+            # round 1's extender-isolated setup: an in-process store per rank, no HTTP
+            i_args = argparse.Namespace(**{**vars(args), "inproc_api": True, "api_rtt_ms": 0.0,
+                                           "steps": args.inproc_variant_steps, "warmup": 1,
                                            "profile_out": "", "stall_trace": ""})
             try:
-                shared_v = summarize(d, s_args, run_pass(d, s_args, topo, conn, "shared"))
+                inproc_v = summarize(d, i_args, run_pass(d, i_args, topo, conn, "inproc"))
             except Exception as e:
-                shared_v = {"error": f"{type(e).__name__}: {e}"}
+                inproc_v = {"error": f"{type(e).__name__}: {e}"}
     finally:
         if drv_proc is not None:
             try:
@@ -771,11 +779,12 @@ def main() -> int:
                        "parallelism": f"{d.world} extender worker(s), shared native ledger",
                        "cluster": f"{args.nodes} nodes x {args.gpus_per_node} MI355X ({args.partition})",
                        "api_rtt_ms": args.api_rtt_ms,
-                       # value is the extender's throughput: the API server is an in-process
-                       # store per rank with no round trip (see value_rtt*ms for a modelled one,
-                       # value_shared_api for one API server shared by all ranks)
-                       "api_server": ("one native HTTP API server for all ranks, own process"
-                                      if args.shared_api else "in-process store per rank, extender-isolated"),
+                       # the API server every bind writes to and the pod controller watches:
+                       # one native HTTP API server in its own process shared by all ranks
+                       # (default), or --inproc-api's per-rank in-process store (value_inproc_api)
+                       "api_server": ("in-process store per rank, extender-isolated" if args.inproc_api else
+                                      f"one native HTTP API server for all ranks, own process "
+                                      f"({args.apiserver_threads} IO threads), REST + watch"),
                        "cpus_rank0": _cpulist(cpus),
                        "frontend": f"{args.frontend_threads} threads, busy-poll {args.busy_poll_us} us"},
             # POST /scheduler/bind wall time as kube-scheduler's stand-in sees it (request
@@ -824,15 +833,15 @@ def main() -> int:
                 line[f"p50_bind_ms_{tag}"] = variant["p50_bind_ms"]
                 line[f"p99_bind_ms_{tag}"] = variant["p99_bind_ms"]
                 line[f"steps_{tag}"] = args.rtt_variant_steps
-        if shared_v is not None:
-            if "error" in shared_v:
-                line["value_shared_api"] = None
-                line["error_shared_api"] = shared_v["error"]
+        if inproc_v is not None:
+            if "error" in inproc_v:
+                line["value_inproc_api"] = None
+                line["error_inproc_api"] = inproc_v["error"]
             else:
-                line["value_shared_api"] = shared_v["value"]
-                line["p50_bind_ms_shared_api"] = shared_v["p50_bind_ms"]
-                line["p99_bind_ms_shared_api"] = shared_v["p99_bind_ms"]
-                line["steps_shared_api"] = args.shared_variant_steps
+                line["value_inproc_api"] = inproc_v["value"]
+                line["p50_bind_ms_inproc_api"] = inproc_v["p50_bind_ms"]
+                line["p99_bind_ms_inproc_api"] = inproc_v["p99_bind_ms"]
+                line["steps_inproc_api"] = args.inproc_variant_steps
         print(json.dumps(line), flush=True)
         if args.json_out:
             Path(args.json_out).write_text(json.dumps(line, indent=1))

@@ -141,7 +141,9 @@ class Runtime:
         self.controllers.append(NodeController(self.state, self.node_informer))
         self.tasks.append(self.node_informer.start())
         if self.leader:
-            self.pod_informer = Informer(self.api, "pods")
+            # the controllers read a pod's identity, nano-gpu/* annotations and limits, node
+            # and phase: the REST watch decodes just those (native), not the whole object
+            self.pod_informer = Informer(self.api, "pods", slim=True)
             pc = PodController(self.state, self.pod_informer, workers=self.cfg.threadness, metrics=self.metrics)
             self.controllers.append(pc)
             pc.start()

@@ -122,9 +122,10 @@ class KubeConfig:
         return ctx
 
 
-async def _ndjson_batches(chunks) -> AsyncIterator[list[dict]]:
+async def _ndjson_batches(chunks, decode=None) -> AsyncIterator[list[dict]]:
     """Newline-delimited JSON from a byte stream: the complete lines of each chunk as a list
-    (a partial last line waits for the next chunk)."""
+    (a partial last line waits for the next chunk). `decode(bytes) -> list` replaces
+    json.loads per line (the native slim pod decoder)."""
     tail = b""
     async for chunk in chunks:
         data = tail + chunk if tail else chunk
@@ -133,7 +134,10 @@ async def _ndjson_batches(chunks) -> AsyncIterator[list[dict]]:
             tail = data
             continue
         tail = data[cut + 1:]
-        batch = [json.loads(line) for line in data[:cut].split(b"\n") if line.strip()]
+        if decode is not None:
+            batch = decode(data[:cut])
+        else:
+            batch = [json.loads(line) for line in data[:cut].split(b"\n") if line.strip()]
         if batch:
             yield batch
 
@@ -145,6 +149,8 @@ class KubeClient:
     `tokenFile`) are re-read when the file changes, checked at most every
     `token_check_s`, and at once after a 401: kubelet rotates projected tokens while the
     extender keeps running (client-go reloads them the same way)."""
+
+    supports_slim_watch = True   # watch_batches(slim=True): native slim pod decoding
 
     def __init__(self, config: KubeConfig, timeout_s: float = 30.0, pool: int = 64, token_check_s: float = 60.0):
         self.config = config
@@ -312,8 +318,15 @@ class KubeClient:
                     yield ev
 
     async def watch_batches(self, resource: str, resource_version: str, timeout_s: int = 300,
-                            label_selector: str | None = None) -> AsyncIterator[list[dict]]:
-        """`watch`, one list per network read: every complete event line that arrived together."""
+                            label_selector: str | None = None, slim: bool = False) -> AsyncIterator[list[dict]]:
+        """`watch`, one list per network read: every complete event line that arrived together.
+        slim (pods): each Pod decoded natively down to what the pod informer reads
+        (nanogpu._native.decode_pod_watch) instead of json.loads of the whole object."""
+        decode = None
+        if slim and resource == "pods":
+            from ..native import core
+
+            decode = core().decode_pod_watch
         s = await self._s()
         params = {"watch": "1", "resourceVersion": resource_version, "timeoutSeconds": str(timeout_s),
                   "allowWatchBookmarks": "true"}
@@ -324,5 +337,5 @@ class KubeClient:
                          headers=self._auth()) as r:
             if r.status >= 400:
                 raise ApiError(r.status, await r.text())
-            async for batch in _ndjson_batches(r.content.iter_any()):
+            async for batch in _ndjson_batches(r.content.iter_any(), decode):
                 yield batch

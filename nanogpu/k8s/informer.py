@@ -35,7 +35,7 @@ def _rv(o: dict) -> str:
 
 class Informer:
     def __init__(self, api, resource: str, label_selector: str | None = None,
-                 resync_s: float = 0.0, key=None):
+                 resync_s: float = 0.0, key=None, slim: bool = False):
         self.api = api
         self.resource = resource               # "pods" | "nodes"
         self.label_selector = label_selector
@@ -50,6 +50,9 @@ class Informer:
         self.rewatches = 0    # watches resumed from the last resourceVersion after a clean end
         self.expired = 0      # 410 Gone / expired resourceVersion answers (each forces a LIST)
         self.events = 0       # watch events handled
+        # pods only: watch events decoded natively to the fields the controllers read (a
+        # REST client that offers it; the in-process store shares its objects anyway)
+        self.slim = slim and resource == "pods" and bool(getattr(api, "supports_slim_watch", False))
 
     def add_handler(self, h: Handler) -> None:
         self.handlers.append(h)
@@ -137,7 +140,8 @@ class Informer:
         # API objects that can (the in-process store, the REST client) deliver the stream in
         # batches: one loop wake-up per burst of events rather than one per event
         if hasattr(self.api, "watch_batches"):
-            stream = self.api.watch_batches(self.resource, self.rv, label_selector=self.label_selector)
+            kw = {"slim": True} if self.slim else {}
+            stream = self.api.watch_batches(self.resource, self.rv, label_selector=self.label_selector, **kw)
         else:
             stream = _singletons(self.api.watch(self.resource, self.rv, label_selector=self.label_selector))
         store, key, handlers = self.store, self.key, self.handlers

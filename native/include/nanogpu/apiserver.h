@@ -80,6 +80,9 @@ class Server {
   // Deletes (namespace, name) pairs; returns how many existed.
   int delete_pods(const std::vector<std::pair<std::string, std::string>>& keys);
   std::string stats_json() const;
+  // Modelled API round trip: every HTTP response is held this long after its request was
+  // handled (watch events are not delayed). 0 = none.
+  void set_latency(double seconds);
   // Watch-cache control for tests: forget history (a resumed watch gets 410 Gone), end every
   // open watch of `kind` ("pods" | "nodes" | "" = both).
   void compact(std::string_view kind);

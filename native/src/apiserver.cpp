@@ -23,6 +23,7 @@
 #include <mutex>
 #include <random>
 #include <stdexcept>
+#include <tuple>
 #include <unordered_map>
 
 #include "nanogpu/frontend.h"
@@ -365,6 +366,8 @@ double steady_s() {
 struct IoThread {
   int ep = -1, efd = -1;
   std::thread th;
+  // modelled round trip: responses held until due, in arrival order (one latency for all)
+  std::deque<std::tuple<double, std::weak_ptr<Conn>, std::string>> delayed;
   std::mutex mu;
   std::vector<std::shared_ptr<Conn>> flush;   // watch conns with pending output
   std::unordered_map<int, std::shared_ptr<Conn>> conns;
@@ -383,6 +386,7 @@ struct IoThread {
 struct Server::Impl {
   Config cfg;
   int lfd = -1;
+  std::atomic<double> latency_s{0.0};
   std::atomic<bool> stopping{false};
   std::vector<std::unique_ptr<IoThread>> io;
 
@@ -954,8 +958,14 @@ void Server::Impl::on_readable(IoThread* t, const std::shared_ptr<Conn>& c) {
     }
     auto [code, resp] = handle(req);
     c->in.erase(0, consumed);
-    c->out += head(code, resp.size());
-    c->out += resp;
+    const double lat = latency_s.load(std::memory_order_relaxed);
+    if (lat > 0 || !t->delayed.empty()) {
+      // earlier responses of this thread may still be held: keep every connection's order
+      t->delayed.emplace_back(steady_s() + lat, c, head(code, resp.size()) + resp);
+    } else {
+      c->out += head(code, resp.size());
+      c->out += resp;
+    }
     if (close_req) c->close_after = true;
   }
   if (!write_out(c.get())) {
@@ -975,7 +985,10 @@ void Server::Impl::on_readable(IoThread* t, const std::shared_ptr<Conn>& c) {
 void Server::Impl::io_loop(IoThread* t) {
   epoll_event evs[256];
   while (!stopping.load(std::memory_order_acquire)) {
-    const int n = epoll_wait(t->ep, evs, 256, 200);
+    int timeout_ms = 200;
+    if (!t->delayed.empty())
+      timeout_ms = std::max(0, std::min(200, static_cast<int>((std::get<0>(t->delayed.front()) - steady_s()) * 1e3)));
+    const int n = epoll_wait(t->ep, evs, 256, timeout_ms);
     for (int i = 0; i < n; ++i) {
       const int fd = evs[i].data.fd;
       if (fd == lfd) {
@@ -1044,8 +1057,24 @@ void Server::Impl::io_loop(IoThread* t) {
         epoll_ctl(t->ep, EPOLL_CTL_MOD, c->fd, &ce);
       }
     }
-    // watch deadlines (timeoutSeconds): the stream ends cleanly
+    // held responses that are due
     const double now = steady_s();
+    while (!t->delayed.empty() && std::get<0>(t->delayed.front()) <= now) {
+      auto c = std::get<1>(t->delayed.front()).lock();
+      std::string bytes = std::move(std::get<2>(t->delayed.front()));
+      t->delayed.pop_front();
+      if (!c || !t->conns.count(c->fd) || t->conns[c->fd] != c) continue;
+      c->out += bytes;
+      if (!write_out(c.get()) || (c->out.empty() && c->close_after)) {
+        close_conn(t, c);
+        continue;
+      }
+      epoll_event ce{};
+      ce.events = EPOLLIN | EPOLLRDHUP | (c->out.empty() ? 0u : EPOLLOUT);
+      ce.data.fd = c->fd;
+      epoll_ctl(t->ep, EPOLL_CTL_MOD, c->fd, &ce);
+    }
+    // watch deadlines (timeoutSeconds): the stream ends cleanly
     std::vector<std::shared_ptr<Conn>> due;
     for (auto& kv : t->conns)
       if (kv.second->watching && kv.second->deadline > 0 && now >= kv.second->deadline) due.push_back(kv.second);
@@ -1184,6 +1213,8 @@ std::string Server::stats_json() const {
          ld(m.n_list) + ",\"watch\":" + ld(m.n_watch) + ",\"events\":" + ld(m.n_events) + ",\"lease\":" +
          ld(m.n_lease) + "}}";
 }
+
+void Server::set_latency(double seconds) { impl_->latency_s.store(seconds > 0 ? seconds : 0.0); }
 
 void Server::compact(std::string_view kind) {
   std::lock_guard<std::mutex> g(impl_->mu);

@@ -10,6 +10,7 @@
 #include "nanogpu/apiserver.h"
 #include "nanogpu/frontend.h"
 #include "nanogpu/gosort.h"
+#include "nanogpu/json.h"
 #include "nanogpu/ledger.h"
 #include "nanogpu/schedsim.h"
 #include "nanogpu/topo.h"
@@ -136,7 +137,9 @@ py::dict from_topo(const Topology& t) {
 
 py::list plan_list(const Plan& p) {
   py::list out;
+  if (p.n < 0 || p.n > kMaxContainers) return out;
   for (int c = 0; c < p.n; ++c) {
+    if (p.off[c] < 0 || p.off[c + 1] > kMaxPlanIdx || p.off[c] > p.off[c + 1]) break;
     py::list idx;
     for (int k = p.off[c]; k < p.off[c + 1]; ++k) idx.append(static_cast<int>(p.idx[k]));
     out.append(idx);
@@ -199,6 +202,101 @@ py::dict record_dict(const PodRecord& r) {
 }
 
 }  // namespace
+
+
+// ------------------------------------------------------------------ slim pod watch decoding
+// What the pod informer keeps of a Pod (nanogpu/k8s/informer.py, pods.py, podutil.py):
+// metadata identity + labels + the nano-gpu/* annotations, nodeName, each container's name
+// and nano-gpu/* limits/requests, and the phase. Everything else of a real Pod (env, volumes,
+// probes, managedFields, other annotations) is never read, so it is not turned into Python
+// objects: one C++ parse per event instead of json.loads of the whole object.
+static py::object jnode(const json::Doc& d, int32_t i) {
+  const json::Node& n = d.at(i);
+  switch (n.type) {
+    case json::Type::kNull: return py::none();
+    case json::Type::kBool: return py::bool_(n.b);
+    case json::Type::kNum: {
+      const std::string_view t = d.str(i);
+      if (t.find_first_of(".eE") == std::string_view::npos) {
+        try {
+          return py::int_(std::stoll(std::string(t)));
+        } catch (...) {
+        }
+      }
+      return py::float_(std::stod(std::string(t)));
+    }
+    case json::Type::kStr: return py::str(std::string(d.str(i)));
+    case json::Type::kArr: {
+      py::list l;
+      for (int32_t c = n.first; c >= 0; c = d.at(c).next) l.append(jnode(d, c));
+      return std::move(l);
+    }
+    case json::Type::kObj: {
+      py::dict o;
+      for (int32_t c = n.first; c >= 0; c = d.at(c).next) o[py::str(std::string(d.key(c)))] = jnode(d, c);
+      return std::move(o);
+    }
+  }
+  return py::none();
+}
+
+static bool nanogpu_key(std::string_view k) { return k.rfind("nano-gpu/", 0) == 0; }
+
+static py::dict slim_map(const json::Doc& d, int32_t obj, bool only_ours) {
+  py::dict o;
+  if (!d.is(obj, json::Type::kObj)) return o;
+  for (int32_t c = d.at(obj).first; c >= 0; c = d.at(c).next)
+    if (!only_ours || nanogpu_key(d.key(c))) o[py::str(std::string(d.key(c)))] = jnode(d, c);
+  return o;
+}
+
+static void copy_str(const json::Doc& d, int32_t obj, const char* k, py::dict& out) {
+  const int32_t v = d.get(obj, k);
+  if (v >= 0 && d.at(v).type != json::Type::kNull) out[k] = jnode(d, v);
+}
+
+static py::dict slim_pod(const json::Doc& d, int32_t pod) {
+  py::dict out, md, spec, st;
+  const int32_t m = d.get(pod, "metadata");
+  if (d.is(m, json::Type::kObj)) {
+    for (const char* k : {"name", "namespace", "uid", "resourceVersion", "creationTimestamp", "deletionTimestamp"})
+      copy_str(d, m, k, md);
+    md["labels"] = slim_map(d, d.get(m, "labels"), false);
+    md["annotations"] = slim_map(d, d.get(m, "annotations"), true);
+  }
+  const int32_t sp = d.get(pod, "spec");
+  if (d.is(sp, json::Type::kObj)) {
+    copy_str(d, sp, "nodeName", spec);
+    copy_str(d, sp, "schedulerName", spec);
+    for (const char* list : {"containers", "initContainers"}) {
+      const int32_t cs = d.get(sp, list);
+      if (!d.is(cs, json::Type::kArr)) continue;
+      py::list out_cs;
+      for (int32_t c = d.at(cs).first; c >= 0; c = d.at(c).next) {
+        py::dict oc;
+        copy_str(d, c, "name", oc);
+        const int32_t res = d.get(c, "resources");
+        if (d.is(res, json::Type::kObj)) {
+          py::dict ores;
+          for (const char* k : {"limits", "requests"}) {
+            const int32_t lm = d.get(res, k);
+            if (d.is(lm, json::Type::kObj)) ores[k] = slim_map(d, lm, true);
+          }
+          oc["resources"] = ores;
+        }
+        out_cs.append(oc);
+      }
+      spec[list] = out_cs;
+    }
+  }
+  const int32_t s = d.get(pod, "status");
+  if (d.is(s, json::Type::kObj)) copy_str(d, s, "phase", st);
+  for (const char* k : {"apiVersion", "kind"}) copy_str(d, pod, k, out);
+  out["metadata"] = md;
+  out["spec"] = spec;
+  out["status"] = st;
+  return out;
+}
 
 PYBIND11_MODULE(_native, m) {
   m.doc() = "nanogpu native core: ledger, placement policies, topology reader";
@@ -385,8 +483,12 @@ PYBIND11_MODULE(_native, m) {
                v = l.cached_plans(id);
              }
              py::list out;
-             for (const auto& c : v)
-               out.append(py::make_tuple(c.demand_hash, c.options_hash, c.rc, plan_list(c.plan), c.plan.score));
+             for (const auto& c : v) {
+               // an entry that does not fit carries no plan (its Plan bytes are not filled in)
+               const bool fits = c.rc == kOk || c.rc == kOkExisting;
+               out.append(py::make_tuple(c.demand_hash, c.options_hash, c.rc, fits ? plan_list(c.plan) : py::list(),
+                                         fits ? c.plan.score : 0));
+             }
              return out;
            },
            "Valid plan-cache entries of node `id` in this process: (demand hash, options hash, rc, plan, score).")
@@ -767,6 +869,36 @@ PYBIND11_MODULE(_native, m) {
       .def("delete_pods", &apisrv::Server::delete_pods, py::arg("keys"), py::call_guard<py::gil_scoped_release>(),
            "Deletes (namespace, name) pods; returns how many existed.")
       .def("stats", [](const apisrv::Server& s) { return s.stats_json(); })
+      .def("set_latency", &apisrv::Server::set_latency, py::arg("seconds"))
       .def("compact", &apisrv::Server::compact, py::arg("kind") = "")
       .def("drop_watches", &apisrv::Server::drop_watches, py::arg("kind") = "");
+
+  m.def(
+      "decode_pod_watch",
+      [](py::bytes data) {
+        std::string_view sv = data;
+        py::list out;
+        size_t p = 0;
+        json::Doc d;
+        while (p < sv.size()) {
+          size_t e = sv.find('\n', p);
+          if (e == std::string_view::npos) e = sv.size();
+          std::string_view line = sv.substr(p, e - p);
+          p = e + 1;
+          while (!line.empty() && (line.back() == '\r' || line.back() == ' ')) line.remove_suffix(1);
+          if (line.empty()) continue;
+          if (!d.parse(line) || !d.is(d.root(), json::Type::kObj)) throw py::value_error("bad watch event line");
+          py::dict ev;
+          const int32_t t = d.get(d.root(), "type");
+          const int32_t obj = d.get(d.root(), "object");
+          ev["type"] = d.is(t, json::Type::kStr) ? py::str(std::string(d.str(t))) : py::str("");
+          const bool plain = d.is(t, json::Type::kStr) && (d.str(t) == "ERROR" || d.str(t) == "BOOKMARK");
+          ev["object"] = d.is(obj, json::Type::kObj) ? (plain ? jnode(d, obj) : py::object(slim_pod(d, obj))) : py::dict();
+          out.append(ev);
+        }
+        return out;
+      },
+      py::arg("data"),
+      "Newline-delimited pod watch events -> [{type, object}] with each Pod reduced to the fields the "
+      "pod informer reads (identity, labels, nano-gpu/* annotations and resources, nodeName, phase).");
 }

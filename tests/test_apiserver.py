@@ -209,3 +209,37 @@ def test_native_bulk_create_delete_and_timeout_ends_the_stream():
         asyncio.run(main())
     finally:
         srv.stop()
+
+
+def test_slim_pod_decoding_keeps_what_the_controllers_read():
+    """decode_pod_watch (the pod informer's native decoder) drops everything but identity,
+    labels, nano-gpu/* annotations and resources, nodeName and phase; every podutil reading
+    the controllers do gives the same answer on the slim object as on the full one."""
+    from hypothesis import given, settings, strategies as st
+
+    @settings(max_examples=60, deadline=None)
+    @given(st.lists(st.tuples(st.integers(0, 300), st.integers(0, 1 << 20)), min_size=1, max_size=6),
+           st.booleans(), st.sampled_from(["Pending", "Running", "Succeeded", "Failed"]), st.booleans())
+    def check(conts, assumed, phase, deleting):
+        pod = pu.make_pod("p", [(f"c{i}", p, m) for i, (p, m) in enumerate(conts)], namespace="x")
+        pod["metadata"]["annotations"]["other/huge"] = "y" * 500
+        pod["spec"]["containers"][0]["env"] = [{"name": "A", "value": "1"}]
+        pod["spec"]["nodeName"] = "n1"
+        pod["status"]["phase"] = phase
+        if assumed:
+            pod["metadata"]["annotations"]["nano-gpu/assume"] = "true"
+            for i in range(len(conts)):
+                pod["metadata"]["annotations"][f"nano-gpu/container-c{i}"] = str(i % 8)
+        if deleting:
+            pod["metadata"]["deletionTimestamp"] = "2026-01-01T00:00:00Z"
+        line = json.dumps({"type": "MODIFIED", "object": pod}).encode() + b"\n"
+        (ev,) = N.decode_pod_watch(line)
+        slim = ev["object"]
+        assert ev["type"] == "MODIFIED" and "other/huge" not in slim["metadata"]["annotations"]
+        for f in (pu.plan_from_pod, pu.pod_demand, pu.is_completed, pu.is_assumed, pu.node_name_of, pu.pod_uid,
+                  pu.is_gpu_sharing):
+            assert f(slim) == f(pod), f.__name__
+
+    check()
+    err = N.decode_pod_watch(b'{"type":"ERROR","object":{"kind":"Status","code":410,"message":"gone"}}\n')
+    assert err[0]["object"]["code"] == 410

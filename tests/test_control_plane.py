@@ -384,7 +384,7 @@ def test_status_dumps_the_plan_cache_valid_at_the_current_generation():
     ext.filter({"Pod": big, "NodeNames": ["n0"]})
     cache = st.status()["n0"]["PlanCache"]
     fits = [v for v in cache.values() if v["Fits"]]
-    assert len(fits) == 1 and fits[0]["GPUIndexes"] == [[0]] and fits[0]["Score"] > 0
+    assert len(fits) == 1 and fits[0]["GPUIndexes"] in ([[0]], [[1]]) and fits[0]["Score"] > 0
     assert any(not v["Fits"] and v["GPUIndexes"] == [] for v in cache.values())   # 3 GPUs on a 2-GPU node
     json.dumps(st.status())
     r = asyncio.run(_bind(ext, store, p))
