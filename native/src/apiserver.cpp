@@ -16,6 +16,7 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <cmath>
 #include <cstring>
 #include <ctime>
 #include <deque>
@@ -368,6 +369,7 @@ struct IoThread {
   std::thread th;
   // modelled round trip: responses held until due, in arrival order (one latency for all)
   std::deque<std::tuple<double, std::weak_ptr<Conn>, std::string>> delayed;
+  double last_flush = 0, flush_due = 0;   // watch output coalescing (Impl::flush_watches)
   std::mutex mu;
   std::vector<std::shared_ptr<Conn>> flush;   // watch conns with pending output
   std::unordered_map<int, std::shared_ptr<Conn>> conns;
@@ -387,6 +389,7 @@ struct Server::Impl {
   Config cfg;
   int lfd = -1;
   std::atomic<double> latency_s{0.0};
+  double linger_s = 200e-6;   // watch output coalescing window under load
   std::atomic<bool> stopping{false};
   std::vector<std::unique_ptr<IoThread>> io;
 
@@ -795,6 +798,7 @@ struct Server::Impl {
   void io_loop(IoThread* t);
   void on_readable(IoThread* t, const std::shared_ptr<Conn>& c);
   void flush_watch(const std::shared_ptr<Conn>& c);
+  void flush_watches(IoThread* t);
   bool write_out(Conn* c);
   void close_conn(IoThread* t, const std::shared_ptr<Conn>& c);
 };
@@ -982,12 +986,38 @@ void Server::Impl::on_readable(IoThread* t, const std::shared_ptr<Conn>& c) {
   epoll_ctl(t->ep, EPOLL_CTL_MOD, c->fd, &ev);
 }
 
+void Server::Impl::flush_watches(IoThread* t) {
+  t->flush_due = 0;
+  t->last_flush = steady_s();
+  std::vector<std::shared_ptr<Conn>> fl;
+  {
+    std::lock_guard<std::mutex> g(t->mu);
+    fl.swap(t->flush);
+  }
+  for (auto& c : fl) {
+    c->queued.store(false);
+    if (!t->conns.count(c->fd) || t->conns[c->fd] != c) continue;   // closed meanwhile
+    flush_watch(c);
+    if (!write_out(c.get())) {
+      close_conn(t, c);
+      continue;
+    }
+    epoll_event ce{};
+    ce.events = EPOLLIN | EPOLLRDHUP | (c->out.empty() ? 0u : EPOLLOUT);
+    ce.data.fd = c->fd;
+    epoll_ctl(t->ep, EPOLL_CTL_MOD, c->fd, &ce);
+    if (!c->watching && !c->in.empty()) on_readable(t, c);   // requests queued behind a stream
+  }
+}
+
 void Server::Impl::io_loop(IoThread* t) {
   epoll_event evs[256];
   while (!stopping.load(std::memory_order_acquire)) {
     int timeout_ms = 200;
     if (!t->delayed.empty())
       timeout_ms = std::max(0, std::min(200, static_cast<int>((std::get<0>(t->delayed.front()) - steady_s()) * 1e3)));
+    if (t->flush_due > 0)
+      timeout_ms = std::max(0, std::min(timeout_ms, static_cast<int>(std::ceil((t->flush_due - steady_s()) * 1e3))));
     const int n = epoll_wait(t->ep, evs, 256, timeout_ms);
     for (int i = 0; i < n; ++i) {
       const int fd = evs[i].data.fd;
@@ -1011,25 +1041,11 @@ void Server::Impl::io_loop(IoThread* t) {
       if (fd == t->efd) {
         uint64_t v;
         (void)!read(t->efd, &v, sizeof v);
-        std::vector<std::shared_ptr<Conn>> fl;
-        {
-          std::lock_guard<std::mutex> g(t->mu);
-          fl.swap(t->flush);
-        }
-        for (auto& c : fl) {
-          c->queued.store(false);
-          if (!t->conns.count(c->fd) || t->conns[c->fd] != c) continue;   // closed meanwhile
-          flush_watch(c);
-          if (!write_out(c.get())) {
-            close_conn(t, c);
-            continue;
-          }
-          epoll_event ce{};
-          ce.events = EPOLLIN | EPOLLRDHUP | (c->out.empty() ? 0u : EPOLLOUT);
-          ce.data.fd = c->fd;
-          epoll_ctl(t->ep, EPOLL_CTL_MOD, c->fd, &ce);
-          if (!c->watching && !c->in.empty()) on_readable(t, c);   // requests queued behind a stream
-        }
+        // a busy stream is flushed at most once per linger window, so a burst of events
+        // leaves as a few large chunks instead of one chunk per event; an idle one at once
+        const double now = steady_s();
+        if (now - t->last_flush >= linger_s) flush_watches(t);
+        else if (t->flush_due == 0) t->flush_due = t->last_flush + linger_s;
         continue;
       }
       auto it = t->conns.find(fd);
@@ -1059,6 +1075,7 @@ void Server::Impl::io_loop(IoThread* t) {
     }
     // held responses that are due
     const double now = steady_s();
+    if (t->flush_due > 0 && now >= t->flush_due) flush_watches(t);
     while (!t->delayed.empty() && std::get<0>(t->delayed.front()) <= now) {
       auto c = std::get<1>(t->delayed.front()).lock();
       std::string bytes = std::move(std::get<2>(t->delayed.front()));
