@@ -231,13 +231,26 @@ const char* reason_phrase(int code) {
 // ------------------------------------------------------------------------------ store
 enum Kind { kPods = 0, kNodes = 1, kKinds = 2 };
 
+// One stored version of an object: its JSON text (what every read and watch event sends)
+// and, built on first need only, its tree (what a patch edits and label selectors read).
+// A create or delete whose text only gains a resourceVersion never builds the tree.
 struct Obj {
-  JV v;
   std::string json;
   std::string ns, name, uid, node, phase;
   uint64_t rv = 0;
+  mutable std::once_flag once;
+  mutable std::shared_ptr<const JV> tree;
+  const JV& v() const {
+    std::call_once(once, [this] {
+      if (tree) return;
+      auto t = std::make_shared<JV>();
+      parse(json, t.get());
+      tree = std::move(t);
+    });
+    return *tree;
+  }
   const JV* labels() const {
-    const JV* m = v.get("metadata");
+    const JV* m = v().get("metadata");
     return m ? m->get("labels") : nullptr;
   }
 };
@@ -254,9 +267,68 @@ ObjP seal(JV v, uint64_t rv) {
   if (const JV* sp = v.get("spec")) o->node = str_of(sp->get("nodeName"));
   if (const JV* st = v.get("status")) o->phase = str_of(st->get("phase"));
   o->rv = rv;
-  o->v = std::move(v);
-  dump(o->v, &o->json);
+  auto t = std::make_shared<JV>(std::move(v));
+  dump(*t, &o->json);
+  o->tree = std::move(t);
   return o;
+}
+
+// The same object at a new resourceVersion, text spliced (a delete's final version).
+ObjP restamp(const ObjP& cur, uint64_t rv) {
+  const std::string old = "\"resourceVersion\":\"" + std::to_string(cur->rv) + "\"";
+  const size_t at = cur->json.find(old);
+  if (at == std::string::npos) return seal(cur->v(), rv);
+  auto o = std::make_shared<Obj>();
+  o->json.reserve(cur->json.size() + 4);
+  o->json.append(cur->json, 0, at);
+  o->json += "\"resourceVersion\":\"" + std::to_string(rv) + "\"";
+  o->json.append(cur->json, at + old.size(), std::string::npos);
+  o->ns = cur->ns, o->name = cur->name, o->uid = cur->uid, o->node = cur->node, o->phase = cur->phase;
+  o->rv = rv;
+  // the tree (if built) stays usable as the base of later patches, which re-stamp anyway
+  if (cur->tree) o->tree = cur->tree;
+  return o;
+}
+
+// A create whose body already has everything the store fills in except the resourceVersion
+// (and maybe the creationTimestamp): the stored text is the body with those spliced into
+// metadata, no tree. Anything else goes through the tree path (create_pod_locked).
+struct FastCreate {
+  bool ok = false;
+  std::string ns, name, uid, node, phase;
+  std::string_view text;
+  size_t meta_open = 0;   // offset just past metadata's '{'
+  bool need_ts = false;
+};
+
+FastCreate fast_create(std::string_view text, std::string_view ns_path) {
+  FastCreate f;
+  json::Doc d;
+  if (!d.parse(text) || !d.is(d.root(), json::Type::kObj)) return f;
+  const int32_t m = d.get(d.root(), "metadata");
+  if (!d.is(m, json::Type::kObj) || d.at(m).count == 0) return f;
+  auto sget = [&](int32_t obj, const char* k) -> std::string {
+    const int32_t v = d.get(obj, k);
+    return d.is(v, json::Type::kStr) ? std::string(d.str(v)) : std::string();
+  };
+  f.ns = sget(m, "namespace");
+  f.name = sget(m, "name");
+  f.uid = sget(m, "uid");
+  if (f.name.empty() || f.uid.empty() || f.ns.empty() || (!ns_path.empty() && f.ns != ns_path)) return f;
+  if (d.get(m, "resourceVersion") >= 0) return f;
+  f.need_ts = d.get(m, "creationTimestamp") < 0;
+  const int32_t st = d.get(d.root(), "status");
+  if (!d.is(st, json::Type::kObj)) return f;
+  f.phase = sget(st, "phase");
+  if (f.phase.empty()) return f;
+  const int32_t sp = d.get(d.root(), "spec");
+  if (d.is(sp, json::Type::kObj)) f.node = sget(sp, "nodeName");
+  const uint32_t b = d.at(m).src_begin;
+  if (b >= text.size() || text[b] != '{') return f;
+  f.meta_open = b + 1;
+  f.text = text;
+  f.ok = true;
+  return f;
 }
 
 struct Selector {
@@ -448,19 +520,76 @@ struct Server::Impl {
     emit(kPods, "ADDED", o);
     return o;
   }
+  // `f` from fast_create (parsed outside the lock)
+  ObjP create_fast_locked(const FastCreate& f) {
+    const std::string k = key(f.ns, f.name);
+    if (pods.count(k)) throw ApiErr{409, "AlreadyExists", "pods \"" + f.name + "\" already exists"};
+    auto o = std::make_shared<Obj>();
+    o->rv = ++rv;
+    std::string ins = "\"resourceVersion\":\"" + std::to_string(o->rv) + "\"";
+    if (f.need_ts) ins += ",\"creationTimestamp\":\"" + now_rfc3339() + "\"";
+    ins += ',';
+    o->json.reserve(f.text.size() + ins.size());
+    o->json.append(f.text.substr(0, f.meta_open));
+    o->json += ins;
+    o->json.append(f.text.substr(f.meta_open));
+    o->ns = f.ns, o->name = f.name, o->uid = f.uid, o->node = f.node, o->phase = f.phase;
+    pods.emplace(k, o);
+    emit(kPods, "ADDED", o);
+    return o;
+  }
   ObjP pod_or_404(std::string_view ns, std::string_view name) const {
     auto it = pods.find(key(ns, name));
     if (it == pods.end()) throw ApiErr{404, "NotFound", "pods \"" + std::string(name) + "\" not found"};
     return it->second;
   }
-  ObjP patch_pod_locked(std::string_view ns, std::string_view name, const JV& patch) {
-    ObjP cur = pod_or_404(ns, name);
-    JV v = cur->v;
-    merge_patch(&v, patch);
-    ObjP o = seal(std::move(v), ++rv);
-    pods[key(ns, name)] = o;
-    emit(kPods, "MODIFIED", o);
-    return o;
+  // Writes that derive the new version from the current one: the tree copy, the edit and
+  // the serialization run outside the store lock against a snapshot; the lock is held only
+  // to check the snapshot is still current, splice the resourceVersion in and publish.
+  // A concurrent write to the same pod makes the loser redo its edit (optimistic).
+  template <class Edit>
+  ObjP write_pod(std::string_view ns, std::string_view name, Edit edit) {
+    const std::string k = key(ns, name);
+    for (;;) {
+      ObjP cur;
+      {
+        std::lock_guard<std::mutex> g(mu);
+        cur = pod_or_404(ns, name);
+      }
+      JV v = cur->v();
+      edit(*cur, &v);                       // may throw ApiErr (checked against this version)
+      ObjP draft = seal(std::move(v), 0);
+      std::lock_guard<std::mutex> g(mu);
+      auto it = pods.find(k);
+      if (it == pods.end()) throw ApiErr{404, "NotFound", "pods \"" + std::string(name) + "\" not found"};
+      if (it->second != cur) continue;       // someone wrote in between: redo on theirs
+      ObjP o = restamp(draft, ++rv);
+      it->second = o;
+      emit(kPods, "MODIFIED", o);
+      return o;
+    }
+  }
+  ObjP patch_pod(std::string_view ns, std::string_view name, const JV& patch) {
+    return write_pod(ns, name, [&](const Obj&, JV* v) { merge_patch(v, patch); });
+  }
+  void bind_pod(std::string_view ns, std::string_view name, std::string_view uid, std::string_view node) {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      if (!nodes.count(std::string(node))) {
+        (void)pod_or_404(ns, name);
+        throw ApiErr{404, "NotFound", "nodes \"" + std::string(node) + "\" not found"};
+      }
+    }
+    write_pod(ns, name, [&](const Obj& cur, JV* v) {
+      if (!uid.empty() && cur.uid != uid) throw ApiErr{409, "Conflict", "pod " + std::string(name) + " uid mismatch"};
+      if (!cur.node.empty())
+        throw ApiErr{409, "Conflict",
+                     "pod " + std::string(name) + " is already assigned to node \"" + cur.node + "\""};
+      v->child("spec").set("nodeName", JV::str(std::string(node)));
+      v->child("status").set("phase", JV::str("Running"));
+    });
+    std::lock_guard<std::mutex> g(mu);
+    ++bindings;
   }
   ObjP update_pod_locked(std::string_view ns, std::string_view name, JV v) {
     ObjP cur = pod_or_404(ns, name);
@@ -475,27 +604,12 @@ struct Server::Impl {
     emit(kPods, "MODIFIED", o);
     return o;
   }
-  void bind_locked(std::string_view ns, std::string_view name, std::string_view uid, std::string_view node) {
-    ObjP cur = pod_or_404(ns, name);
-    if (!uid.empty() && cur->uid != uid) throw ApiErr{409, "Conflict", "pod " + std::string(name) + " uid mismatch"};
-    if (!cur->node.empty())
-      throw ApiErr{409, "Conflict", "pod " + std::string(name) + " is already assigned to node \"" + cur->node + "\""};
-    if (!nodes.count(std::string(node))) throw ApiErr{404, "NotFound", "nodes \"" + std::string(node) + "\" not found"};
-    JV v = cur->v;
-    v.child("spec").set("nodeName", JV::str(std::string(node)));
-    v.child("status").set("phase", JV::str("Running"));
-    ObjP o = seal(std::move(v), ++rv);
-    pods[key(ns, name)] = o;
-    ++bindings;
-    emit(kPods, "MODIFIED", o);
-  }
   bool delete_pod_locked(std::string_view ns, std::string_view name) {
     auto it = pods.find(key(ns, name));
     if (it == pods.end()) return false;
     ObjP cur = it->second;
     pods.erase(it);
-    ObjP o = seal(cur->v, ++rv);
-    emit(kPods, "DELETED", o);
+    emit(kPods, "DELETED", restamp(cur, ++rv));
     return true;
   }
 
@@ -591,7 +705,7 @@ struct Server::Impl {
           if (m == "PATCH") {
             JV p = body_json(r);
             std::lock_guard<std::mutex> g(mu);
-            JV v = node_or_404(name)->v;
+            JV v = node_or_404(name)->v();
             merge_patch(&v, p);
             return {200, put_node_locked(std::move(v))->json};
           }
@@ -601,7 +715,7 @@ struct Server::Impl {
             if (it == nodes.end()) throw ApiErr{404, "NotFound", "nodes \"" + name + "\" not found"};
             ObjP cur = it->second;
             nodes.erase(it);
-            emit(kNodes, "DELETED", seal(cur->v, ++rv));
+            emit(kNodes, "DELETED", restamp(cur, ++rv));
             return {200, kOk};
           }
         }
@@ -617,8 +731,13 @@ struct Server::Impl {
         if (at(4) == "pods") {
           if (n == 5 && m == "GET") return list_pods(r, ns);
           if (n == 5 && m == "POST") {
-            JV v = body_json(r);
             n_create.fetch_add(1, std::memory_order_relaxed);
+            const FastCreate f = fast_create(r.body, ns);
+            if (f.ok) {
+              std::lock_guard<std::mutex> g(mu);
+              return {201, create_fast_locked(f)->json};
+            }
+            JV v = body_json(r);
             std::lock_guard<std::mutex> g(mu);
             return {201, create_pod_locked(std::move(v), ns)->json};
           }
@@ -632,8 +751,7 @@ struct Server::Impl {
             if (m == "PATCH") {
               JV p = body_json(r);
               n_patch.fetch_add(1, std::memory_order_relaxed);
-              std::lock_guard<std::mutex> g(mu);
-              return {200, patch_pod_locked(ns, name, p)->json};
+              return {200, patch_pod(ns, name, p)->json};
             }
             if (m == "PUT") {
               JV v = body_json(r);
@@ -653,8 +771,7 @@ struct Server::Impl {
             const JV* md = b.get("metadata");
             const JV* tg = b.get("target");
             n_bind.fetch_add(1, std::memory_order_relaxed);
-            std::lock_guard<std::mutex> g(mu);
-            bind_locked(ns, name, md ? str_of(md->get("uid")) : std::string(), tg ? str_of(tg->get("name")) : "");
+            bind_pod(ns, name, md ? str_of(md->get("uid")) : std::string(), tg ? str_of(tg->get("name")) : "");
             return {201, kOk};
           }
         }
@@ -1193,15 +1310,19 @@ std::pair<int, std::string> Server::call(std::string_view method, std::string_vi
 }
 
 std::vector<int> Server::create_pods(const std::vector<std::string>& texts) {
+  std::vector<FastCreate> fast(texts.size());
   std::vector<JV> vs(texts.size());
   std::vector<int> codes(texts.size(), 201);
-  for (size_t i = 0; i < texts.size(); ++i)
-    if (!parse(texts[i], &vs[i])) codes[i] = 400;
+  for (size_t i = 0; i < texts.size(); ++i) {
+    fast[i] = fast_create(texts[i], "");
+    if (!fast[i].ok && !parse(texts[i], &vs[i])) codes[i] = 400;
+  }
   std::lock_guard<std::mutex> g(impl_->mu);
   for (size_t i = 0; i < texts.size(); ++i) {
     if (codes[i] != 201) continue;
     try {
-      impl_->create_pod_locked(std::move(vs[i]), "");
+      if (fast[i].ok) impl_->create_fast_locked(fast[i]);
+      else impl_->create_pod_locked(std::move(vs[i]), "");
       impl_->n_create.fetch_add(1, std::memory_order_relaxed);
     } catch (const ApiErr& e) {
       codes[i] = e.code;
