@@ -318,10 +318,11 @@ def burst(rank: int, world: int, total: int, step: int, seed: int) -> list[dict]
     return pods
 
 
-def apiserver_main(conn, threads: int, latency_s: float = 0.0) -> None:
-    """The shared API server's process: a native API server (native/src/apiserver.cpp) on its
-    own L3 domain, plus a command pipe through which rank 0 plays the workload's clients
-    (bulk create / delete of a step's pods; the pod JSON is shipped before the clock starts)."""
+def apiserver_main(conn) -> None:
+    """The shared API server's process: native API servers (native/src/apiserver.cpp), one
+    per bench pass, on an L3 domain of their own, plus a command pipe through which rank 0
+    plays the workload's clients (bulk create / delete of a step's pods; the pod JSON is
+    shipped before the clock starts). Started before the bench touches the GPU."""
     import json as _json
 
     from nanogpu import affinity
@@ -332,14 +333,19 @@ def apiserver_main(conn, threads: int, latency_s: float = 0.0) -> None:
     except OSError:
         pass
     affinity.apply(affinity.pick_cpus())
-    srv = core().ApiServer("127.0.0.1", 0, threads, 1 << 20)
-    srv.set_latency(latency_s)     # modelled API round trip on every REST answer
+    srv = None
     steps: dict = {}
-    conn.send(srv.port)
     while True:
         msg = conn.recv()
         op = msg[0]
-        if op == "nodes":
+        if op == "start":            # a fresh server: (threads, modelled RTT in seconds)
+            if srv is not None:
+                srv.stop()
+            steps.clear()
+            srv = core().ApiServer("127.0.0.1", 0, msg[1], 1 << 20)
+            srv.set_latency(msg[2])
+            conn.send(srv.port)
+        elif op == "nodes":
             for n in msg[1]:
                 srv.call("POST", "/api/v1/nodes", n)
             conn.send(len(msg[1]))
@@ -347,8 +353,7 @@ def apiserver_main(conn, threads: int, latency_s: float = 0.0) -> None:
             steps[msg[1]] = msg[2]
             conn.send(True)
         elif op == "create":
-            texts = steps[msg[1]]
-            codes = srv.create_pods(texts)
+            codes = srv.create_pods(steps[msg[1]])
             conn.send(sum(1 for c in codes if c == 201))
         elif op == "delete":
             keys = []
@@ -358,27 +363,38 @@ def apiserver_main(conn, threads: int, latency_s: float = 0.0) -> None:
             conn.send(srv.delete_pods(keys))
         elif op == "stats":
             conn.send(_json.loads(srv.stats()))
+        elif op == "end":            # the pass is over
+            if srv is not None:
+                srv.stop()
+                srv = None
+            conn.send(True)
         else:
-            srv.stop()
+            if srv is not None:
+                srv.stop()
             conn.send(True)
             return
 
 
 class ApiServerProc:
-    """Rank 0's handle on the shared API server process."""
+    """Rank 0's handle on the shared API server process (spawned once, before any GPU use;
+    `start()` gives each bench pass a fresh server)."""
 
-    def __init__(self, threads: int, latency_s: float = 0.0):
+    def __init__(self):
         import multiprocessing as mp
 
         ctx = mp.get_context("spawn")
         self.conn, child = ctx.Pipe()
-        self.proc = ctx.Process(target=apiserver_main, args=(child, threads, latency_s), daemon=True)
+        self.proc = ctx.Process(target=apiserver_main, args=(child,), daemon=True)
         self.proc.start()
-        self.url = f"http://127.0.0.1:{self.conn.recv()}"
+        self.url = ""
 
     def _rpc(self, *msg):
         self.conn.send(msg)
         return self.conn.recv()
+
+    def start(self, threads: int, latency_s: float = 0.0) -> str:
+        self.url = f"http://127.0.0.1:{self._rpc('start', threads, latency_s)}"
+        return self.url
 
     def add_nodes(self, nodes: list[dict]) -> None:
         self._rpc("nodes", [json.dumps(n, separators=(",", ":")) for n in nodes])
@@ -394,6 +410,9 @@ class ApiServerProc:
 
     def stats(self) -> dict:
         return self._rpc("stats")
+
+    def end(self) -> None:
+        self._rpc("end")
 
     def close(self) -> None:
         try:
@@ -462,7 +481,7 @@ def driver_main(conn) -> None:
         serve()
 
 
-async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
+async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: ApiServerProc | None = None) -> dict:
     from nanogpu import types as T
     from nanogpu.app import Config, Runtime
     from nanogpu.k8s import podutil as pu
@@ -474,7 +493,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
     # the pod controller (worker 0 of a replica), so every release goes through its watch.
     # Rank 0 is also the workload's client: it has the API server create and delete every
     # rank's pods. Without it each rank has an in-process store of its own (extender-isolated).
-    shared = not getattr(args, "inproc_api", False) and conn is not None
+    shared = not getattr(args, "inproc_api", False) and conn is not None and (api_proc is not None or d.rank != 0)
     loop = asyncio.get_running_loop()
 
     async def barrier() -> None:
@@ -491,9 +510,9 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
     if shared:
         url = None
         if d.rank == 0:
-            apisrv = ApiServerProc(args.apiserver_threads, args.api_rtt_ms / 1e3)
+            apisrv = api_proc
+            url = apisrv.start(args.apiserver_threads, args.api_rtt_ms / 1e3)
             apisrv.add_nodes(nodes)
-            url = apisrv.url
         url = d.bcast_obj(url)
         from nanogpu.k8s.client import KubeClient, KubeConfig
 
@@ -693,7 +712,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None) -> dict:
     await barrier()          # no rank still talks to the shared API server
     await rt.stop()
     if apisrv is not None:
-        apisrv.close()
+        apisrv.end()
     return results
 
 
@@ -732,12 +751,16 @@ def main() -> int:
         conn, child = ctx.Pipe()
         drv_proc = ctx.Process(target=driver_main, args=(child,), daemon=True)
         drv_proc.start()
+    api_proc = None
+    if int(os.environ.get("RANK", "0")) == 0 and not args.inproc_driver:
+        # the shared API server's process, like the stand-in's: before anything touches the GPU
+        api_proc = ApiServerProc()
     d = Dist(args.gpus)
     d.init(use_gpu=not args.no_gpu)
     topo, gpu_info = node_template(d, args)
     variant = inproc_v = None
     try:
-        res = run_pass(d, args, topo, conn, "main")
+        res = run_pass(d, args, topo, conn, "main", api_proc)
         if args.rtt_variant_ms > 0:
             # the same burst with a modelled API-server round trip on every API call (untimed
             # for `value`; its own clock): what the pods/s above excludes
@@ -745,7 +768,7 @@ def main() -> int:
                                            "steps": args.rtt_variant_steps, "warmup": 1, "profile_out": "",
                                            "stall_trace": ""})
             try:
-                variant = summarize(d, v_args, run_pass(d, v_args, topo, conn, "rtt"))
+                variant = summarize(d, v_args, run_pass(d, v_args, topo, conn, "rtt", api_proc))
             except Exception as e:   # the headline result stands; say what failed
                 variant = {"error": f"{type(e).__name__}: {e}"}
         if args.inproc_variant_steps > 0 and not args.inproc_api and not args.inproc_driver:
@@ -766,6 +789,8 @@ def main() -> int:
             drv_proc.join(10)
             if drv_proc.is_alive():
                 drv_proc.terminate()
+        if api_proc is not None:
+            api_proc.close()
     out = summarize(d, args, res)
     if d.rank == 0:
         fr = res["frag"]
@@ -849,7 +874,7 @@ def main() -> int:
     return 0
 
 
-def run_pass(d: Dist, args, topo, conn, tag: str) -> dict:
+def run_pass(d: Dist, args, topo, conn, tag: str, api_proc=None) -> dict:
     """One bench pass on a fresh shared ledger (all ranks)."""
     ledger_path = d.bcast_obj(f"/dev/shm/nanogpu-bench-{os.environ.get('MASTER_PORT', os.getpid())}-{tag}-"
                               f"{int(time.time())}" if d.rank == 0 else None)
@@ -860,7 +885,7 @@ def run_pass(d: Dist, args, topo, conn, tag: str) -> dict:
         led = core().Ledger(ledger_path, max(1024, args.nodes), max(65536, 4 * args.pods), True)
     d.barrier()
     try:
-        return asyncio.run(run_rank(d, args, topo, ledger_path, conn))
+        return asyncio.run(run_rank(d, args, topo, ledger_path, conn, api_proc))
     finally:
         d.barrier()
         del led

@@ -143,7 +143,7 @@ class Runtime:
         if self.leader:
             # the controllers read a pod's identity, nano-gpu/* annotations and limits, node
             # and phase: the REST watch decodes just those (native), not the whole object
-            self.pod_informer = Informer(self.api, "pods", slim=True)
+            self.pod_informer = Informer(self.api, "pods", slim=True, prefilter=self.state.ledger)
             pc = PodController(self.state, self.pod_informer, workers=self.cfg.threadness, metrics=self.metrics)
             self.controllers.append(pc)
             pc.start()

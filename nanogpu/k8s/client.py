@@ -318,15 +318,18 @@ class KubeClient:
                     yield ev
 
     async def watch_batches(self, resource: str, resource_version: str, timeout_s: int = 300,
-                            label_selector: str | None = None, slim: bool = False) -> AsyncIterator[list[dict]]:
+                            label_selector: str | None = None, slim: bool = False,
+                            ledger=None) -> AsyncIterator[list[dict]]:
         """`watch`, one list per network read: every complete event line that arrived together.
         slim (pods): each Pod decoded natively down to what the pod informer reads
-        (nanogpu._native.decode_pod_watch) instead of json.loads of the whole object."""
+        (nanogpu._native.decode_pod_watch) instead of json.loads of the whole object; with a
+        `ledger`, the events the pod controller would ignore are dropped there as well."""
         decode = None
         if slim and resource == "pods":
             from ..native import core
 
-            decode = core().decode_pod_watch
+            dec = core().decode_pod_watch
+            decode = dec if ledger is None else (lambda data: dec(data, ledger))
         s = await self._s()
         params = {"watch": "1", "resourceVersion": resource_version, "timeoutSeconds": str(timeout_s),
                   "allowWatchBookmarks": "true"}

@@ -35,7 +35,7 @@ def _rv(o: dict) -> str:
 
 class Informer:
     def __init__(self, api, resource: str, label_selector: str | None = None,
-                 resync_s: float = 0.0, key=None, slim: bool = False):
+                 resync_s: float = 0.0, key=None, slim: bool = False, prefilter=None):
         self.api = api
         self.resource = resource               # "pods" | "nodes"
         self.label_selector = label_selector
@@ -53,6 +53,9 @@ class Informer:
         # pods only: watch events decoded natively to the fields the controllers read (a
         # REST client that offers it; the in-process store shares its objects anyway)
         self.slim = slim and resource == "pods" and bool(getattr(api, "supports_slim_watch", False))
+        # slim pods + a native ledger: the decoder drops the events the pod controller would
+        # ignore (pending pods, bound pods the ledger holds); the store then keeps only the rest
+        self.prefilter = prefilter if self.slim else None
 
     def add_handler(self, h: Handler) -> None:
         self.handlers.append(h)
@@ -140,7 +143,7 @@ class Informer:
         # API objects that can (the in-process store, the REST client) deliver the stream in
         # batches: one loop wake-up per burst of events rather than one per event
         if hasattr(self.api, "watch_batches"):
-            kw = {"slim": True} if self.slim else {}
+            kw = {"slim": True, "ledger": self.prefilter} if self.slim else {}
             stream = self.api.watch_batches(self.resource, self.rv, label_selector=self.label_selector, **kw)
         else:
             stream = _singletons(self.api.watch(self.resource, self.rv, label_selector=self.label_selector))

@@ -875,11 +875,12 @@ PYBIND11_MODULE(_native, m) {
 
   m.def(
       "decode_pod_watch",
-      [](py::bytes data) {
+      [](py::bytes data, std::shared_ptr<Ledger> ledger) {
         std::string_view sv = data;
         py::list out;
         size_t p = 0;
         json::Doc d;
+        std::string last_rv;   // resourceVersion of dropped events after the last kept one
         while (p < sv.size()) {
           size_t e = sv.find('\n', p);
           if (e == std::string_view::npos) e = sv.size();
@@ -891,14 +892,51 @@ PYBIND11_MODULE(_native, m) {
           py::dict ev;
           const int32_t t = d.get(d.root(), "type");
           const int32_t obj = d.get(d.root(), "object");
+          if (ledger && d.is(t, json::Type::kStr) && d.is(obj, json::Type::kObj) &&
+              (d.str(t) == "ADDED" || d.str(t) == "MODIFIED")) {
+            // what the pod controller would ignore (pods.py::_on_event) never reaches Python:
+            // a pending pod, or a bound and running one whose share the ledger already holds
+            const int32_t md = d.get(obj, "metadata"), sp = d.get(obj, "spec"), st = d.get(obj, "status");
+            auto field = [&](int32_t o, const char* k) -> std::string_view {
+              const int32_t v = d.is(o, json::Type::kObj) ? d.get(o, k) : -1;
+              return d.is(v, json::Type::kStr) ? d.str(v) : std::string_view();
+            };
+            const std::string_view node = field(sp, "nodeName"), phase = field(st, "phase");
+            const bool completed = (d.is(md, json::Type::kObj) && d.get(md, "deletionTimestamp") >= 0 &&
+                                    !d.is(d.get(md, "deletionTimestamp"), json::Type::kNull)) ||
+                                   phase == "Succeeded" || phase == "Failed";
+            bool drop = false;
+            if (!completed && node.empty()) {
+              drop = true;
+            } else if (!completed) {
+              PodRecord rec;
+              drop = ledger->lookup(std::string(field(md, "uid")), &rec);
+            }
+            if (drop) {
+              last_rv = std::string(field(md, "resourceVersion"));
+              continue;
+            }
+          }
           ev["type"] = d.is(t, json::Type::kStr) ? py::str(std::string(d.str(t))) : py::str("");
           const bool plain = d.is(t, json::Type::kStr) && (d.str(t) == "ERROR" || d.str(t) == "BOOKMARK");
           ev["object"] = d.is(obj, json::Type::kObj) ? (plain ? jnode(d, obj) : py::object(slim_pod(d, obj))) : py::dict();
           out.append(ev);
+          last_rv.clear();
+        }
+        if (!last_rv.empty()) {
+          // events were dropped after the last one kept: a bookmark carries the resume point
+          py::dict md, o, ev;
+          md["resourceVersion"] = last_rv;
+          o["metadata"] = md;
+          ev["type"] = "BOOKMARK";
+          ev["object"] = o;
+          out.append(ev);
         }
         return out;
       },
-      py::arg("data"),
+      py::arg("data"), py::arg("ledger") = nullptr,
       "Newline-delimited pod watch events -> [{type, object}] with each Pod reduced to the fields the "
-      "pod informer reads (identity, labels, nano-gpu/* annotations and resources, nodeName, phase).");
+      "pod informer reads (identity, labels, nano-gpu/* annotations and resources, nodeName, phase). "
+      "With `ledger`, ADDED/MODIFIED events the pod controller ignores (pending pods; bound, running pods "
+      "the ledger already holds) are dropped, a trailing BOOKMARK keeping the resume resourceVersion.");
 }

@@ -243,3 +243,35 @@ def test_slim_pod_decoding_keeps_what_the_controllers_read():
     check()
     err = N.decode_pod_watch(b'{"type":"ERROR","object":{"kind":"Status","code":410,"message":"gone"}}\n')
     assert err[0]["object"]["code"] == 410
+
+
+def test_prefiltered_decoding_drops_only_what_the_pod_controller_ignores():
+    from nanogpu.state.cluster import ClusterState
+    from nanogpu.topology.model import synthetic_mi355x
+
+    st = ClusterState()
+    st.register_node(pu.make_node("n0", 8, synthetic_mi355x(8).to_json()))
+    known = pu.make_pod("known", [("main", 20)])
+    nid = st.node_ids(["n0"])[0]
+    rc = st.ledger.reserve(nid, pu.pod_uid(known), [(20, 0)], st.options)[0]
+    assert rc == N.OK
+
+    def ev(etype, pod, node="", phase="Running", rv="1"):
+        p = json.loads(json.dumps(pod))
+        p["metadata"]["resourceVersion"] = rv
+        if node:
+            p["spec"]["nodeName"] = node
+        p["status"]["phase"] = phase
+        return json.dumps({"type": etype, "object": p}).encode() + b"\n"
+
+    pending = pu.make_pod("pending", [("main", 10)])
+    foreign = pu.make_pod("foreign", [("main", 10)])
+    data = (ev("ADDED", pending, rv="10") + ev("MODIFIED", known, "n0", rv="11") +
+            ev("MODIFIED", foreign, "n0", rv="12") + ev("MODIFIED", known, "n0", "Succeeded", rv="13") +
+            ev("DELETED", known, "n0", rv="14") + ev("MODIFIED", known, "n0", rv="15"))
+    out = N.decode_pod_watch(data, st.ledger)
+    got = [(e["type"], e["object"]["metadata"].get("name"), e["object"]["metadata"]["resourceVersion"]) for e in out]
+    assert got == [("MODIFIED", "foreign", "12"), ("MODIFIED", "known", "13"), ("DELETED", "known", "14"),
+                   ("BOOKMARK", None, "15")]
+    assert [e["type"] for e in N.decode_pod_watch(data)] == ["ADDED", "MODIFIED", "MODIFIED", "MODIFIED", "DELETED",
+                                                            "MODIFIED"]
