@@ -16,9 +16,12 @@ PY
 for spec in ${MATRIX:-default shared}; do
   case $spec in
     default) run default --steps 20 --warmup 3 || exit 1 ;;
-    shared) run shared --shared-api --steps 20 --warmup 3 --rtt-variant-ms 0 --shared-variant-steps 0 || exit 1 ;;
-    shared_t8) run shared_t8 --shared-api --apiserver-threads 8 --steps 20 --warmup 3 --rtt-variant-ms 0 --shared-variant-steps 0 || exit 1 ;;
-    nokube) run nokube --no-kube-combine --steps 20 --warmup 3 --rtt-variant-ms 0 --shared-variant-steps 0 || exit 1 ;;
+    nokube) run nokube --no-kube-combine --steps 20 --warmup 3 --rtt-variant-ms 0 --inproc-variant-steps 0 || exit 1 ;;
+    w8) run w8 --bind-writer-threads 8 --steps 20 --warmup 3 --rtt-variant-ms 0 --inproc-variant-steps 0 || exit 1 ;;
+    w32) run w32 --bind-writer-threads 32 --steps 20 --warmup 3 --rtt-variant-ms 0 --inproc-variant-steps 0 || exit 1 ;;
+    w128) run w128 --steps 20 --warmup 3 --rtt-variant-ms 0 --inproc-variant-steps 0 || exit 1 ;;
+    fe4) run fe4 --frontend-threads 4 --steps 20 --warmup 3 --rtt-variant-ms 0 --inproc-variant-steps 0 || exit 1 ;;
+    t8) run t8 --apiserver-threads 8 --steps 20 --warmup 3 --rtt-variant-ms 0 --inproc-variant-steps 0 || exit 1 ;;
   esac
 done
 echo done
