@@ -70,9 +70,11 @@ def reader_link_gbs(host: dict) -> float:
     return float(gpus[0].get("xgmi_min_bw_mbs", 0)) / 1000.0 if gpus else 0.0
 
 
-def link_matrix(n: int, nbytes: int = 64 << 20, iters: int = 3, dist=None, rank: int = 0) -> list[list[float]]:
-    """n x n per-direction GB/s, m[src][dst], from the peer-pull probe (0 on the diagonal)."""
-    P = probe(required=True)
+def link_matrix(n: int, nbytes: int = 64 << 20, iters: int = 3, dist=None, rank: int = 0,
+                P=None) -> list[list[float]]:
+    """n x n per-direction GB/s, m[src][dst], from the peer-pull probe (0 on the diagonal).
+    `P`: the probe module (tests pass a stand-in)."""
+    P = P or probe(required=True)
     m = [[0.0] * n for _ in range(n)]
     if dist is None:
         for dst in range(n):
@@ -90,8 +92,12 @@ def link_matrix(n: int, nbytes: int = 64 << 20, iters: int = 3, dist=None, rank:
             row[src] = P.peer_bandwidth(src, rank, nbytes, iters)["gbs"]
         except Exception:
             row[src] = -1.0
-    torch.cuda.set_device(rank)
-    t = torch.tensor(row, dtype=torch.float64, device=torch.device("cuda", rank))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(rank)
+        dev = torch.device("cuda", rank)
+    else:                                # gloo rehearsal of the same exchange
+        dev = torch.device("cpu")
+    t = torch.tensor(row, dtype=torch.float64, device=dev)
     rows = [torch.zeros_like(t) for _ in range(n)]
     dist.all_gather(rows, t)
     for dst, r in enumerate(rows):

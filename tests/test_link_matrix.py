@@ -1,0 +1,72 @@
+"""Per-pair link calibration (nanogpu/probe/calibrate.py::link_matrix) as the bench runs it
+with one rank per GPU: in round k every rank pulls from rank (r + k) % n, so each round is a
+permutation over the links, and the rows are all-gathered. Rehearsed with gloo and a stand-in
+probe whose "link rate" encodes the pair, so the assembled matrix can be checked exactly."""
+import os
+import socket
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+class FakeProbe:
+    def __init__(self, fail_pair=None):
+        self.calls = []
+        self.fail_pair = fail_pair
+
+    def peer_bandwidth(self, src, dst, nbytes, iters):
+        self.calls.append((src, dst))
+        if (src, dst) == self.fail_pair:
+            raise RuntimeError("peer access denied")
+        return {"gbs": 10.0 * src + dst + 1, "pull_gbs": 0.0, "dma_gbs": 0.0, "peer_access": True}
+
+
+def _rank(rank, world, port, fail_pair, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from nanogpu.probe.calibrate import link_matrix
+
+    fp = FakeProbe(fail_pair)
+    try:
+        m = link_matrix(world, dist=dist, rank=rank, P=fp)
+        q.put((rank, "ok", m, fp.calls))
+    except RuntimeError as e:
+        q.put((rank, "error", str(e), fp.calls))
+    dist.destroy_process_group()
+
+
+def _run(world, fail_pair=None):
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, fail_pair, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+    return sorted(out)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_link_matrix_rounds_are_permutations_and_rows_gather(world):
+    out = _run(world)
+    for rank, status, m, calls in out:
+        assert status == "ok"
+        assert calls == [((rank + k) % world, rank) for k in range(1, world)]   # this rank's GPU pulls
+        for a in range(world):
+            for b in range(world):
+                assert m[a][b] == (0.0 if a == b else 10.0 * a + b + 1)
+    # round k: the (src, dst) pairs over all ranks form a permutation (each link direction once)
+    for k in range(1, world):
+        srcs = sorted(calls[k - 1][0] for _, _, _, calls in out)
+        assert srcs == list(range(world))
+
+
+def test_a_failed_pair_fails_every_rank_without_a_hang():
+    out = _run(2, fail_pair=(1, 0))
+    assert [status for _, status, _, _ in out] == ["error", "error"]
