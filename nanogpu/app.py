@@ -189,6 +189,7 @@ class Runtime:
         if serve:
             router = server.Router(self.extender, self.ready)
             self.router = router
+            router.extra_metrics = self._informer_metrics
             if self.cfg.leader_elect:
                 # every worker of the replica follows the elector's flag in the shared ledger
                 # (only worker 0 runs the elector)
@@ -213,6 +214,17 @@ class Runtime:
                                                                   reuse_port=self.cfg.workers > 1)
             log.info("worker %d serving on :%d (%s front door, policy=%s compat=%s)", self.worker, self.bound_port,
                      self.cfg.frontend, self.state.policy, self.state.options.compat)
+
+    def _informer_metrics(self) -> bytes:
+        f = self.pod_informer.watch_filter if self.pod_informer is not None else None
+        if f is None:
+            return b""
+        return ("# HELP nanogpu_pod_watch_native_released_total deleted pods released by the native watch filter\n"
+                "# TYPE nanogpu_pod_watch_native_released_total counter\n"
+                f"nanogpu_pod_watch_native_released_total {f.released}\n"
+                "# HELP nanogpu_pod_watch_dropped_total pod events the native filter kept from the controller\n"
+                "# TYPE nanogpu_pod_watch_dropped_total counter\n"
+                f"nanogpu_pod_watch_dropped_total {f.dropped}\n").encode()
 
     def _on_leadership(self, leader: bool) -> None:
         self.state.ledger.serving = leader

@@ -56,6 +56,7 @@ class Router:
         self.ext = ext
         self.ready = ready
         self.extra_status = extra_status
+        self.extra_metrics = None       # () -> bytes appended to /metrics (the runtime's)
         self.native = None          # NativeServer, for /metrics
         self.serving = lambda: True  # False on a standby replica (leader election)
         g, p = "GET", "POST"
@@ -135,6 +136,8 @@ class Router:
         text = m.render()
         if self.native is not None:
             text += self.native.render_metrics()
+        if self.extra_metrics is not None:
+            text += self.extra_metrics()
         return 200, PROM, text
 
     async def healthz(self, q, body):

@@ -319,17 +319,17 @@ class KubeClient:
 
     async def watch_batches(self, resource: str, resource_version: str, timeout_s: int = 300,
                             label_selector: str | None = None, slim: bool = False,
-                            ledger=None) -> AsyncIterator[list[dict]]:
+                            watch_filter=None) -> AsyncIterator[list[dict]]:
         """`watch`, one list per network read: every complete event line that arrived together.
         slim (pods): each Pod decoded natively down to what the pod informer reads
-        (nanogpu._native.decode_pod_watch) instead of json.loads of the whole object; with a
-        `ledger`, the events the pod controller would ignore are dropped there as well."""
+        (nanogpu._native.decode_pod_watch) instead of json.loads of the whole object; a
+        `watch_filter` (nanogpu._native.PodWatchFilter) also does the pod controller's
+        ledger-only work natively and passes on only the rest."""
         decode = None
         if slim and resource == "pods":
             from ..native import core
 
-            dec = core().decode_pod_watch
-            decode = dec if ledger is None else (lambda data: dec(data, ledger))
+            decode = watch_filter.decode if watch_filter is not None else core().decode_pod_watch
         s = await self._s()
         params = {"watch": "1", "resourceVersion": resource_version, "timeoutSeconds": str(timeout_s),
                   "allowWatchBookmarks": "true"}

@@ -53,9 +53,14 @@ class Informer:
         # pods only: watch events decoded natively to the fields the controllers read (a
         # REST client that offers it; the in-process store shares its objects anyway)
         self.slim = slim and resource == "pods" and bool(getattr(api, "supports_slim_watch", False))
-        # slim pods + a native ledger: the decoder drops the events the pod controller would
-        # ignore (pending pods, bound pods the ledger holds); the store then keeps only the rest
-        self.prefilter = prefilter if self.slim else None
+        # slim pods + a native ledger: the native filter does the pod controller's ledger-only
+        # work (drops pending pods and bound pods the ledger holds, releases deletions of pods
+        # never handed on) and passes on the rest; the store keeps only what it passed on
+        self.watch_filter = None
+        if self.slim and prefilter is not None:
+            from ..native import core
+
+            self.watch_filter = core().PodWatchFilter(prefilter)
 
     def add_handler(self, h: Handler) -> None:
         self.handlers.append(h)
@@ -91,6 +96,8 @@ class Informer:
             self._dispatch("MODIFIED" if old is not None else "ADDED", o, old)
         self.rv = rv
         self.relists += 1
+        if getattr(self, "watch_filter", None) is not None:
+            self.watch_filter.reset(list(self.store))   # everything listed is in the store now
 
     async def run(self) -> None:
         """client-go reflector semantics (/root/reference/go.mod:16, client-go v0.18 informers
@@ -143,7 +150,7 @@ class Informer:
         # API objects that can (the in-process store, the REST client) deliver the stream in
         # batches: one loop wake-up per burst of events rather than one per event
         if hasattr(self.api, "watch_batches"):
-            kw = {"slim": True, "ledger": self.prefilter} if self.slim else {}
+            kw = {"slim": True, "watch_filter": self.watch_filter} if self.slim else {}
             stream = self.api.watch_batches(self.resource, self.rv, label_selector=self.label_selector, **kw)
         else:
             stream = _singletons(self.api.watch(self.resource, self.rv, label_selector=self.label_selector))

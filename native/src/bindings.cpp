@@ -4,6 +4,7 @@
 
 #include <cstring>
 #include <memory>
+#include <unordered_set>
 #include <vector>
 
 #include "nanogpu/alloc.h"
@@ -295,6 +296,87 @@ static py::dict slim_pod(const json::Doc& d, int32_t pod) {
   out["metadata"] = md;
   out["spec"] = spec;
   out["status"] = st;
+  return out;
+}
+
+
+// What the pod informer needs from the native side (nanogpu/k8s/informer.py): keys handed to
+// Python (its store) and the ledger the controller would only look up or release.
+struct PodWatchFilter {
+  std::shared_ptr<Ledger> ledger;
+  std::unordered_set<std::string> forwarded;   // "ns/name" in the Python store
+  uint64_t released = 0, dropped = 0;
+};
+
+static py::list decode_pod_events(const py::bytes& data, PodWatchFilter* f) {
+  std::string_view sv = data;
+  py::list out;
+  size_t p = 0;
+  json::Doc d;
+  std::string last_rv;   // resourceVersion of dropped events after the last kept one
+  while (p < sv.size()) {
+    size_t e = sv.find('\n', p);
+    if (e == std::string_view::npos) e = sv.size();
+    std::string_view line = sv.substr(p, e - p);
+    p = e + 1;
+    while (!line.empty() && (line.back() == '\r' || line.back() == ' ')) line.remove_suffix(1);
+    if (line.empty()) continue;
+    if (!d.parse(line) || !d.is(d.root(), json::Type::kObj)) throw py::value_error("bad watch event line");
+    const int32_t t = d.get(d.root(), "type");
+    const int32_t obj = d.get(d.root(), "object");
+    const std::string_view type = d.is(t, json::Type::kStr) ? d.str(t) : std::string_view();
+    if (f && d.is(obj, json::Type::kObj) && (type == "ADDED" || type == "MODIFIED" || type == "DELETED")) {
+      const int32_t md = d.get(obj, "metadata"), sp = d.get(obj, "spec"), st = d.get(obj, "status");
+      auto field = [&](int32_t o, const char* k) -> std::string_view {
+        const int32_t v = d.is(o, json::Type::kObj) ? d.get(o, k) : -1;
+        return d.is(v, json::Type::kStr) ? d.str(v) : std::string_view();
+      };
+      std::string key(field(md, "namespace"));
+      key.push_back('/');
+      key.append(field(md, "name"));
+      const bool seen = f->forwarded.count(key) > 0;
+      bool drop = false;
+      if (!seen && type == "DELETED") {
+        // Python never held it: releasing is all the controller would do (pods.py::_on_event)
+        if (f->ledger->release(std::string(field(md, "uid"))) == kOk) ++f->released;
+        drop = true;
+      } else if (!seen) {
+        // what the controller ignores: a pending pod, or a bound, running one the ledger holds
+        const std::string_view node = field(sp, "nodeName"), phase = field(st, "phase");
+        const int32_t dts = d.is(md, json::Type::kObj) ? d.get(md, "deletionTimestamp") : -1;
+        const bool completed =
+            (dts >= 0 && !d.is(dts, json::Type::kNull)) || phase == "Succeeded" || phase == "Failed";
+        if (!completed && node.empty()) {
+          drop = true;
+        } else if (!completed) {
+          PodRecord rec;
+          drop = f->ledger->lookup(std::string(field(md, "uid")), &rec);
+        }
+      }
+      if (drop) {
+        ++f->dropped;
+        last_rv = std::string(field(md, "resourceVersion"));
+        continue;
+      }
+      if (type == "DELETED") f->forwarded.erase(key);
+      else f->forwarded.insert(std::move(key));
+    }
+    py::dict ev;
+    ev["type"] = py::str(std::string(type));
+    const bool plain = type == "ERROR" || type == "BOOKMARK";
+    ev["object"] = d.is(obj, json::Type::kObj) ? (plain ? jnode(d, obj) : py::object(slim_pod(d, obj))) : py::dict();
+    out.append(ev);
+    last_rv.clear();
+  }
+  if (f && !last_rv.empty()) {
+    // events were dropped after the last one kept: a bookmark carries the resume point
+    py::dict md, o, ev;
+    md["resourceVersion"] = last_rv;
+    o["metadata"] = md;
+    ev["type"] = "BOOKMARK";
+    ev["object"] = o;
+    out.append(ev);
+  }
   return out;
 }
 
@@ -874,69 +956,31 @@ PYBIND11_MODULE(_native, m) {
       .def("drop_watches", &apisrv::Server::drop_watches, py::arg("kind") = "");
 
   m.def(
-      "decode_pod_watch",
-      [](py::bytes data, std::shared_ptr<Ledger> ledger) {
-        std::string_view sv = data;
-        py::list out;
-        size_t p = 0;
-        json::Doc d;
-        std::string last_rv;   // resourceVersion of dropped events after the last kept one
-        while (p < sv.size()) {
-          size_t e = sv.find('\n', p);
-          if (e == std::string_view::npos) e = sv.size();
-          std::string_view line = sv.substr(p, e - p);
-          p = e + 1;
-          while (!line.empty() && (line.back() == '\r' || line.back() == ' ')) line.remove_suffix(1);
-          if (line.empty()) continue;
-          if (!d.parse(line) || !d.is(d.root(), json::Type::kObj)) throw py::value_error("bad watch event line");
-          py::dict ev;
-          const int32_t t = d.get(d.root(), "type");
-          const int32_t obj = d.get(d.root(), "object");
-          if (ledger && d.is(t, json::Type::kStr) && d.is(obj, json::Type::kObj) &&
-              (d.str(t) == "ADDED" || d.str(t) == "MODIFIED")) {
-            // what the pod controller would ignore (pods.py::_on_event) never reaches Python:
-            // a pending pod, or a bound and running one whose share the ledger already holds
-            const int32_t md = d.get(obj, "metadata"), sp = d.get(obj, "spec"), st = d.get(obj, "status");
-            auto field = [&](int32_t o, const char* k) -> std::string_view {
-              const int32_t v = d.is(o, json::Type::kObj) ? d.get(o, k) : -1;
-              return d.is(v, json::Type::kStr) ? d.str(v) : std::string_view();
-            };
-            const std::string_view node = field(sp, "nodeName"), phase = field(st, "phase");
-            const bool completed = (d.is(md, json::Type::kObj) && d.get(md, "deletionTimestamp") >= 0 &&
-                                    !d.is(d.get(md, "deletionTimestamp"), json::Type::kNull)) ||
-                                   phase == "Succeeded" || phase == "Failed";
-            bool drop = false;
-            if (!completed && node.empty()) {
-              drop = true;
-            } else if (!completed) {
-              PodRecord rec;
-              drop = ledger->lookup(std::string(field(md, "uid")), &rec);
-            }
-            if (drop) {
-              last_rv = std::string(field(md, "resourceVersion"));
-              continue;
-            }
-          }
-          ev["type"] = d.is(t, json::Type::kStr) ? py::str(std::string(d.str(t))) : py::str("");
-          const bool plain = d.is(t, json::Type::kStr) && (d.str(t) == "ERROR" || d.str(t) == "BOOKMARK");
-          ev["object"] = d.is(obj, json::Type::kObj) ? (plain ? jnode(d, obj) : py::object(slim_pod(d, obj))) : py::dict();
-          out.append(ev);
-          last_rv.clear();
-        }
-        if (!last_rv.empty()) {
-          // events were dropped after the last one kept: a bookmark carries the resume point
-          py::dict md, o, ev;
-          md["resourceVersion"] = last_rv;
-          o["metadata"] = md;
-          ev["type"] = "BOOKMARK";
-          ev["object"] = o;
-          out.append(ev);
-        }
-        return out;
-      },
-      py::arg("data"), py::arg("ledger") = nullptr,
+      "decode_pod_watch", [](py::bytes data) { return decode_pod_events(data, nullptr); }, py::arg("data"),
       "Newline-delimited pod watch events -> [{type, object}] with each Pod reduced to the fields the "
-      "pod informer reads (identity, labels, nano-gpu/* annotations and resources, nodeName, phase). "
-      "With `ledger`, ADDED/MODIFIED events the pod controller ignores (pending pods; bound, running pods "
-      "the ledger already holds) are dropped, a trailing BOOKMARK keeping the resume resourceVersion.");
+      "pod informer reads (identity, labels, nano-gpu/* annotations and resources, nodeName, phase).");
+
+  py::class_<PodWatchFilter, std::shared_ptr<PodWatchFilter>>(
+      m, "PodWatchFilter",
+      "decode_pod_watch plus the pod controller's ledger-only work done natively: ADDED/MODIFIED of "
+      "pending pods and of bound pods the ledger holds are dropped, DELETED of pods Python never saw "
+      "is released from the ledger here and dropped; every event of a pod once handed to Python keeps "
+      "going to Python. A trailing BOOKMARK carries the resume resourceVersion of dropped events.")
+      .def(py::init([](std::shared_ptr<Ledger> l) {
+             auto f = std::make_shared<PodWatchFilter>();
+             f->ledger = std::move(l);
+             return f;
+           }),
+           py::arg("ledger"))
+      .def("decode", [](PodWatchFilter& f, py::bytes data) { return decode_pod_events(data, &f); }, py::arg("data"))
+      .def(
+          "reset",
+          [](PodWatchFilter& f, const std::vector<std::string>& keys) {
+            f.forwarded.clear();
+            f.forwarded.insert(keys.begin(), keys.end());
+          },
+          py::arg("keys"), "After a relist: the keys now in the informer's store.")
+      .def_property_readonly("released", [](const PodWatchFilter& f) { return f.released; })
+      .def_property_readonly("dropped", [](const PodWatchFilter& f) { return f.dropped; })
+      .def_property_readonly("forwarded", [](const PodWatchFilter& f) { return f.forwarded.size(); });
 }

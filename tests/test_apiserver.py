@@ -245,16 +245,20 @@ def test_slim_pod_decoding_keeps_what_the_controllers_read():
     assert err[0]["object"]["code"] == 410
 
 
-def test_prefiltered_decoding_drops_only_what_the_pod_controller_ignores():
+def test_watch_filter_does_the_controllers_ledger_only_work():
+    """PodWatchFilter: pending pods and bound pods the ledger holds never reach Python; a
+    deletion of a pod Python never saw is released natively; a pod once handed to Python
+    (foreign, completed) keeps going to Python so the informer's store stays current."""
     from nanogpu.state.cluster import ClusterState
     from nanogpu.topology.model import synthetic_mi355x
 
     st = ClusterState()
     st.register_node(pu.make_node("n0", 8, synthetic_mi355x(8).to_json()))
-    known = pu.make_pod("known", [("main", 20)])
     nid = st.node_ids(["n0"])[0]
-    rc = st.ledger.reserve(nid, pu.pod_uid(known), [(20, 0)], st.options)[0]
-    assert rc == N.OK
+    known = pu.make_pod("known", [("main", 20)])
+    done = pu.make_pod("done", [("main", 20)])
+    for p in (known, done):
+        assert st.ledger.reserve(nid, pu.pod_uid(p), [(20, 0)], st.options)[0] == N.OK
 
     def ev(etype, pod, node="", phase="Running", rv="1"):
         p = json.loads(json.dumps(pod))
@@ -266,12 +270,21 @@ def test_prefiltered_decoding_drops_only_what_the_pod_controller_ignores():
 
     pending = pu.make_pod("pending", [("main", 10)])
     foreign = pu.make_pod("foreign", [("main", 10)])
+    f = N.PodWatchFilter(st.ledger)
     data = (ev("ADDED", pending, rv="10") + ev("MODIFIED", known, "n0", rv="11") +
-            ev("MODIFIED", foreign, "n0", rv="12") + ev("MODIFIED", known, "n0", "Succeeded", rv="13") +
-            ev("DELETED", known, "n0", rv="14") + ev("MODIFIED", known, "n0", rv="15"))
-    out = N.decode_pod_watch(data, st.ledger)
+            ev("MODIFIED", foreign, "n0", rv="12") + ev("MODIFIED", done, "n0", "Succeeded", rv="13") +
+            ev("DELETED", known, "n0", rv="14") + ev("MODIFIED", foreign, "n0", rv="15") +
+            ev("DELETED", pending, rv="16"))
+    out = f.decode(data)
     got = [(e["type"], e["object"]["metadata"].get("name"), e["object"]["metadata"]["resourceVersion"]) for e in out]
-    assert got == [("MODIFIED", "foreign", "12"), ("MODIFIED", "known", "13"), ("DELETED", "known", "14"),
-                   ("BOOKMARK", None, "15")]
+    assert got == [("MODIFIED", "foreign", "12"), ("MODIFIED", "done", "13"), ("MODIFIED", "foreign", "15"),
+                   ("BOOKMARK", None, "16")]
+    assert st.ledger.lookup(pu.pod_uid(known)) is None             # released natively
+    assert st.ledger.lookup(pu.pod_uid(done)) is not None          # Python's to release (completed)
+    assert f.released == 1 and f.dropped == 4 and f.forwarded == 2
+    out = f.decode(ev("DELETED", done, "n0", "Succeeded", rv="17") + ev("DELETED", foreign, "n0", rv="18"))
+    assert [e["type"] for e in out] == ["DELETED", "DELETED"] and f.forwarded == 0
+    f.reset(["default/x"])
+    assert f.forwarded == 1
     assert [e["type"] for e in N.decode_pod_watch(data)] == ["ADDED", "MODIFIED", "MODIFIED", "MODIFIED", "DELETED",
-                                                            "MODIFIED"]
+                                                            "MODIFIED", "DELETED"]
