@@ -78,7 +78,8 @@ def parse_args():
     ap.add_argument("--inproc-variant-steps", type=int, default=3,
                     help="after the timed steps, a pass with --inproc-api (0: none)")
     ap.add_argument("--apiserver-threads", type=int, default=4, help="shared API server IO threads")
-    ap.add_argument("--bind-writer-threads", type=int, default=128, help="extender's native bind writers per rank")
+    ap.add_argument("--bind-writer-threads", type=int, default=0,
+                    help="extender's native bind writers per rank (0: 128 split over the ranks, at least 16)")
     ap.add_argument("--inflight-binds", type=int, default=64)
     ap.add_argument("--no-gpu", action="store_true", help="skip GPU discovery (CPU-only rehearsal)")
     ap.add_argument("--json-out", default="")
@@ -528,7 +529,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                  max_nodes=max(1024, args.nodes), max_pods=max(65536, 4 * args.pods),
                  policy_config_path="/nonexistent/policy.yaml", reservation_ttl_s=3600,
                  busy_poll_us=args.busy_poll_us, frontend_threads=args.frontend_threads,
-                 nominate=not args.no_nominate, bind_writer_threads=args.bind_writer_threads)
+                 nominate=not args.no_nominate,
+                 bind_writer_threads=args.bind_writer_threads or max(16, 128 // d.world))
     all_steps_pre = [10_000 + w for w in range(args.warmup)] + list(range(args.steps))
     rt = Runtime(cfg, worker=d.rank if shared else 0, api=rt_api)
     await rt.start()
