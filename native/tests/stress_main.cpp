@@ -6,7 +6,11 @@
 //     (SO_REUSEPORT workers share one ledger the same way);
 //   * a native front door serves filter / priorities to client threads over loopback
 //     HTTP while the ledger changes underneath it;
-//   * at the end every pod is released and every device must be whole again.
+//   * at the end every pod is released and every device must be whole again;
+//   * then the native API server and the native bind writers: writer threads bind pods
+//     reserved on the ledger (PATCH + binding + commit) while other threads patch the same
+//     pods and a watch stream reads every event; every bind must land, no patch may be lost
+//     (optimistic writes redo on conflict) and the watch must see every version.
 // Exit code 0 = pass. Usage: nanogpu-stress [threads] [iterations]
 #include <arpa/inet.h>
 #include <netinet/in.h>
@@ -14,7 +18,9 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -23,7 +29,9 @@
 #include <thread>
 #include <vector>
 
+#include "nanogpu/apiserver.h"
 #include "nanogpu/frontend.h"
+#include "nanogpu/kubewriter.h"
 #include "nanogpu/ledger.h"
 
 using namespace nanogpu;
@@ -93,6 +101,149 @@ static void churn(Ledger& l, int n_nodes, int seed, int iters, std::atomic<int>*
     }
   }
   for (const auto& k : live) CHECK(l.release(k) == kOk);
+}
+
+static std::string http(int port, const std::string& method, const std::string& path, const std::string& body) {
+  const int fd = socket(AF_INET, SOCK_STREAM, 0);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons(static_cast<uint16_t>(port));
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  CHECK(connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) == 0);
+  const std::string req = method + " " + path + " HTTP/1.1\r\nHost: x\r\nConnection: close\r\nContent-Length: " +
+                          std::to_string(body.size()) + "\r\n\r\n" + body;
+  CHECK(send(fd, req.data(), req.size(), MSG_NOSIGNAL) == static_cast<ssize_t>(req.size()));
+  std::string out;
+  char buf[4096];
+  for (;;) {
+    const ssize_t r = recv(fd, buf, sizeof(buf), 0);
+    if (r <= 0) break;
+    out.append(buf, static_cast<size_t>(r));
+  }
+  close(fd);
+  return out;
+}
+
+// Native API server + native bind writers under concurrency (see the header comment).
+static void apiserver_and_writers(int pods) {
+  apisrv::Config cfg;
+  cfg.threads = 2;
+  apisrv::Server srv(cfg);
+  const int port = srv.port();
+  CHECK(http(port, "POST", "/api/v1/nodes", "{\"metadata\":{\"name\":\"n0\"}}").rfind("HTTP/1.1 201", 0) == 0);
+  std::vector<std::string> texts;
+  for (int i = 0; i < pods; ++i)
+    texts.push_back("{\"metadata\":{\"name\":\"p" + std::to_string(i) + "\",\"namespace\":\"s\",\"uid\":\"w" +
+                    std::to_string(i) + "\"},\"spec\":{\"containers\":[{\"name\":\"c\"}]},\"status\":{\"phase\":\"Pending\"}}");
+  for (int c : srv.create_pods(texts)) CHECK(c == 201);
+
+  // watch from the current version: every later write must arrive
+  const std::string list = http(port, "GET", "/api/v1/pods", "");
+  const size_t rvp = list.find("\"resourceVersion\":\"");
+  CHECK(rvp != std::string::npos);
+  const std::string rv0 = list.substr(rvp + 19, list.find('"', rvp + 19) - rvp - 19);
+  std::atomic<int> events{0};
+  std::atomic<bool> stop_watch{false};
+  std::thread watcher([&] {
+    const int fd = socket(AF_INET, SOCK_STREAM, 0);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons(static_cast<uint16_t>(port));
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    CHECK(connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) == 0);
+    timeval tv{0, 200000};
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+    const std::string req = "GET /api/v1/pods?watch=1&resourceVersion=" + rv0 + " HTTP/1.1\r\nHost: x\r\n\r\n";
+    CHECK(send(fd, req.data(), req.size(), MSG_NOSIGNAL) == static_cast<ssize_t>(req.size()));
+    char buf[65536];
+    while (!stop_watch.load()) {
+      const ssize_t r = recv(fd, buf, sizeof(buf), 0);
+      if (r <= 0) continue;
+      for (ssize_t i = 0; i + 7 < r; ++i)
+        if (std::memcmp(buf + i, "\"type\":", 7) == 0) events.fetch_add(1);
+    }
+    close(fd);
+  });
+
+  auto ledger = std::make_shared<Ledger>("", 8, 4096, true);
+  Device devs[8];
+  std::memset(devs, 0, sizeof(devs));
+  for (int i = 0; i < 8; ++i) {
+    devs[i].pct_total = 100;
+    devs[i].mib_total = 294896;
+    devs[i].gpu = static_cast<int16_t>(i);
+    devs[i].healthy = 1;
+    devs[i].xcds = 8;
+    devs[i].cus = 256;
+  }
+  Topology t;
+  std::memset(&t, 0, sizeof(t));
+  t.n_gpus = 8;
+  const int32_t nid = ledger->upsert_node("n0", devs, 8, t);
+  CHECK(nid >= 0);
+
+  std::atomic<int> ok{0}, bad{0};
+  KubeTarget tgt;
+  tgt.host = "127.0.0.1";
+  tgt.port = port;
+  tgt.tls = false;
+  {
+    KubeWriter kw(
+        tgt, ledger,
+        [&](uint64_t, int status, const std::string& body) {
+          if (status == 200 && body == "{\"Error\":\"\"}") ok.fetch_add(1);
+          else bad.fetch_add(1);
+        },
+        4, 2, false);
+    std::vector<std::thread> patchers;
+    for (int t2 = 0; t2 < 2; ++t2)
+      patchers.emplace_back([&, t2] {
+        for (int i = 0; i < pods; ++i)
+          CHECK(http(port, "PATCH", "/api/v1/namespaces/s/pods/p" + std::to_string(i),
+                     "{\"metadata\":{\"annotations\":{\"k" + std::to_string(t2) + "\":\"v\"}}}")
+                    .rfind("HTTP/1.1 200", 0) == 0);
+      });
+    for (int i = 0; i < pods; ++i) {
+      Demand dm;
+      std::memset(&dm, 0, sizeof(dm));
+      dm.n = 1;
+      dm.c[0].pct = 1;
+      Plan plan;
+      std::memset(&plan, 0, sizeof(plan));
+      Options o;
+      CHECK(ledger->reserve(nid, "w" + std::to_string(i), dm, o, &plan) == kOk);
+      BindJob j;
+      j.id = static_cast<uint64_t>(i);
+      j.ns = "s";
+      j.name = "p" + std::to_string(i);
+      j.uid = "w" + std::to_string(i);
+      j.node = "n0";
+      j.containers = {"c"};
+      j.plan = {{plan.idx[plan.off[0]]}};
+      kw.submit(std::move(j));
+    }
+    for (auto& p2 : patchers) p2.join();
+    for (int spin = 0; ok.load() + bad.load() < pods && spin < 3000; ++spin)
+      std::this_thread::sleep_for(std::chrono::milliseconds(2));
+    kw.stop();
+  }
+  CHECK(ok.load() == pods && bad.load() == 0);
+  for (int i = 0; i < pods; ++i) {
+    const std::string r = http(port, "GET", "/api/v1/namespaces/s/pods/p" + std::to_string(i), "");
+    CHECK(r.find("\"nodeName\":\"n0\"") != std::string::npos);          // bound
+    CHECK(r.find("\"k0\":\"v\"") != std::string::npos && r.find("\"k1\":\"v\"") != std::string::npos);   // no lost patch
+    CHECK(r.find("\"nano-gpu/container-c\"") != std::string::npos);
+    PodRecord rec;
+    CHECK(ledger->lookup("w" + std::to_string(i), &rec));
+  }
+  // every write after rv0 reached the watch: 2 patches + placement PATCH + binding per pod
+  for (int spin = 0; events.load() < 4 * pods && spin < 1000; ++spin)
+    std::this_thread::sleep_for(std::chrono::milliseconds(2));
+  stop_watch.store(true);
+  watcher.join();
+  CHECK(events.load() == 4 * pods);
+  srv.stop();
+  std::printf("apiserver ok: %d pods bound by native writers, %d watch events\n", pods, events.load());
 }
 
 static std::string post(int port, const std::string& path, const std::string& body) {
@@ -190,5 +341,6 @@ int main(int argc, char** argv) {
               reserved.load(), static_cast<unsigned long long>(st));
   ledger.reset();
   unlink(path.c_str());
+  apiserver_and_writers(std::max(50, iters / 20));
   return 0;
 }
