@@ -2,7 +2,9 @@
 
 native/tests/stress_main.cpp churns a /dev/shm ledger from several threads and a forked
 second process while the native HTTP front door answers filter/priorities, then checks
-that every device is whole again (SURVEY §4 lesson 5)."""
+that every device is whole again (SURVEY §4 lesson 5); then drives the native API server
+with native bind writers, concurrent patches and a watch stream (no lost update, every event
+delivered)."""
 import subprocess
 import sys
 from pathlib import Path

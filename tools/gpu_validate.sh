@@ -13,4 +13,8 @@ if [ "${PROFILE:-1}" = "1" ]; then
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run -- python3 $R/bench.py --steps 5 --warmup 1 > $R/gpurun_out/prof.log 2>&1 || { echo "prof failed"; tail -20 $R/gpurun_out/prof.log; exit 1; }
 fi
+if [ "${CONFIGS:-0}" = "1" ]; then
+  cd $R && timeout -k 10 600 python -u -m nanogpu.sim.configs --out gpurun_out/configs.json > gpurun_out/configs.log 2>&1 || { echo "configs failed"; tail -20 gpurun_out/configs.log; exit 1; }
+  tail -3 gpurun_out/configs.log
+fi
 echo done
