@@ -1,11 +1,13 @@
 // Native bind writes to kube-apiserver (see kubewriter.h).
 #include "nanogpu/kubewriter.h"
 
+#include <arpa/inet.h>
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <openssl/err.h>
 #include <openssl/ssl.h>
+#include <openssl/x509v3.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
 #include <sys/time.h>
@@ -122,8 +124,15 @@ bool HttpConn::connect_() {
     SSL* s = SSL_new(static_cast<SSL_CTX*>(ctx_));
     if (!s) return close_(), false;
     SSL_set_fd(s, fd_);
-    SSL_set_tlsext_host_name(s, t_->host.c_str());
-    if (!t_->insecure) SSL_set1_host(s, t_->host.c_str());
+    // in-cluster the API server is an IP (KUBERNETES_SERVICE_HOST): verify it against the
+    // certificate's IP SANs; a name goes through SNI and the DNS SANs
+    in6_addr a6{};
+    const bool ip = inet_pton(AF_INET, t_->host.c_str(), &a6) == 1 || inet_pton(AF_INET6, t_->host.c_str(), &a6) == 1;
+    if (!ip) SSL_set_tlsext_host_name(s, t_->host.c_str());
+    if (!t_->insecure) {
+      if (ip) X509_VERIFY_PARAM_set1_ip_asc(SSL_get0_param(s), t_->host.c_str());
+      else SSL_set1_host(s, t_->host.c_str());
+    }
     ssl_ = s;
     if (SSL_connect(s) != 1) return close_(), false;
   }

@@ -136,7 +136,9 @@ def test_binding_conflict_on_the_same_node_is_success(native):
 
 def test_native_writer_speaks_tls_with_a_bearer_token(tmp_path):
     """https + token (how an in-cluster extender reaches kube-apiserver): a TLS proxy with a
-    self-signed certificate in front of the fake API server checks the Authorization header."""
+    self-signed certificate in front of the fake API server checks the Authorization header.
+    The certificate names the server the way kube-apiserver's does (CN kube-apiserver, the
+    service IP as an IP SAN), so the writer must verify the IP against the IP SANs."""
     import shutil
     import ssl
     import subprocess
@@ -145,7 +147,8 @@ def test_native_writer_speaks_tls_with_a_bearer_token(tmp_path):
         pytest.skip("openssl CLI not available")
     key, crt = tmp_path / "k.pem", tmp_path / "c.pem"
     subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", str(key), "-out", str(crt),
-                    "-days", "1", "-subj", "/CN=127.0.0.1", "-addext", "subjectAltName=IP:127.0.0.1"],
+                    "-days", "1", "-subj", "/CN=kube-apiserver",
+                    "-addext", "subjectAltName=DNS:kubernetes.default.svc,IP:127.0.0.1"],
                    check=True, capture_output=True)
     tok = tmp_path / "token"
     tok.write_text("s3cret\n")
