@@ -143,6 +143,7 @@ class Frontend {
   void flush(Worker* w, Conn* c);
   void close_conn(Worker* w, Conn* c);
   void put_pod(std::string_view uid, CachedPod pod);
+  bool has_pod(std::string_view uid) const;
   void prepare_bind(std::string_view body, PyRequest* r);
   void note_bind_wall(uint64_t ns);
 

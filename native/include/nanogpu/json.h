@@ -23,8 +23,8 @@ struct Node {
   int32_t first = -1;     // first child (arrays / objects)
   int32_t next = -1;      // next sibling
   int32_t count = 0;      // children
-  uint32_t key_off = 0, key_len = 0;  // member key (into arena), objects' children only
-  uint32_t str_off = 0, str_len = 0;  // string value (arena) or number text (source)
+  uint32_t key_off = 0, key_len = 0;  // member key (arena or source, see Doc::kInSrc), objects' children only
+  uint32_t str_off = 0, str_len = 0;  // string value (arena or source) or number text (source)
   uint32_t src_begin = 0, src_end = 0;
 };
 
@@ -33,11 +33,15 @@ class Doc {
   bool parse(std::string_view src);
   const Node& at(int32_t i) const { return nodes_[i]; }
   int32_t root() const { return nodes_.empty() ? -1 : 0; }
+  // A string with no escape is not copied: its length carries kInSrc and its offset points
+  // into the source; only unescaped text lives in the arena.
+  static constexpr uint32_t kInSrc = 0x80000000u;
   std::string_view str(int32_t i) const {
     const Node& n = nodes_[i];
-    return n.type == Type::kNum ? src_.substr(n.str_off, n.str_len) : std::string_view(arena_).substr(n.str_off, n.str_len);
+    if (n.type == Type::kNum) return src_.substr(n.str_off, n.str_len);
+    return text(n.str_off, n.str_len);
   }
-  std::string_view key(int32_t i) const { return std::string_view(arena_).substr(nodes_[i].key_off, nodes_[i].key_len); }
+  std::string_view key(int32_t i) const { return text(nodes_[i].key_off, nodes_[i].key_len); }
   std::string_view raw(int32_t i) const { return src_.substr(nodes_[i].src_begin, nodes_[i].src_end - nodes_[i].src_begin); }
   // Member lookup; `ci` = ASCII case-insensitive (Go encoding/json field matching).
   int32_t get(int32_t obj, std::string_view k, bool ci = false) const;
@@ -45,6 +49,9 @@ class Doc {
   size_t size() const { return nodes_.size(); }
 
  private:
+  std::string_view text(uint32_t off, uint32_t len) const {
+    return (len & kInSrc) ? src_.substr(off, len & ~kInSrc) : std::string_view(arena_).substr(off, len);
+  }
   int32_t value(int depth);
   bool string(uint32_t* off, uint32_t* len);
   void ws() {

@@ -12,6 +12,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <charconv>
 #include <cerrno>
 #include <chrono>
 #include <cmath>
@@ -421,6 +422,11 @@ void Frontend::wake_workers() {
   }
 }
 
+bool Frontend::has_pod(std::string_view uid) const {
+  std::lock_guard<std::mutex> g(pod_mu_);
+  return pods_.find(std::string(uid)) != pods_.end();
+}
+
 size_t Frontend::pod_cache_size() const {
   std::lock_guard<std::mutex> g(pod_mu_);
   return pods_.size();
@@ -819,7 +825,11 @@ bool Frontend::handle_native(Worker* w, Conn* c, const std::string& method, cons
 }
 
 bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* out) {
-  json::Doc d;
+  // per-thread scratch: the DOM, the name views and the result arrays keep their capacity
+  // from one request to the next (every cycle of a burst sends the same-sized bodies)
+  thread_local json::Doc d;
+  thread_local std::vector<std::string_view> nv;
+  thread_local std::vector<int32_t> rcs, scores;
   if (body.empty() || !d.parse(body)) return false;
   const int32_t root = d.root();
   if (!d.is(root, json::Type::kObj)) return false;
@@ -906,11 +916,26 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   // of the last lists it resolved (keyed by the array's raw text) and only checks that slot
   // `id` still carries that name; a miss falls back to the ledger's name index.
   const int32_t nn = d.at(names).count;
-  std::vector<std::string_view> nv;
+  nv.clear();
   nv.reserve(nn);
+  thread_local std::vector<std::string_view> nraw;   // each name's JSON token, quotes included
+  nraw.clear();
+  nraw.reserve(nn);
   for (int32_t c = d.at(names).first; c >= 0; c = d.at(c).next) {
     if (!d.is(c, json::Type::kStr)) return false;
     nv.push_back(d.str(c));
+    // the token is reused as written unless it holds an escape (then it is re-quoted, so the
+    // reply stays byte-identical to the Python verb's json.dumps)
+    const std::string_view tok = d.raw(c);
+    if (tok.size() == nv.back().size() + 2) {
+      nraw.push_back(tok);
+    } else {
+      thread_local std::deque<std::string> requoted;   // stable storage for this request
+      if (nraw.empty()) requoted.clear();
+      requoted.emplace_back();
+      json::append_quoted(&requoted.back(), nv.back());
+      nraw.push_back(requoted.back());
+    }
   }
   struct IdCache {
     const Ledger* owner = nullptr;
@@ -948,7 +973,8 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     nominate = nominate_;
   }
   if (nominate && !uid.empty()) ledger_->drop_nomination(std::string(uid));   // not against itself
-  if (pod >= 0 && !uid.empty()) {
+  if (pod >= 0 && !uid.empty() && !(prioritize && has_pod(uid))) {
+    // filter caches the pod for its bind; priorities of the same cycle find it there
     cached.raw.assign(d.raw(pod));
     cached.demand = dem;
     put_pod(uid, std::move(cached));
@@ -957,37 +983,45 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   std::string& r = *out;
   r.reserve(64 + 48 * static_cast<size_t>(nn));
   if (!prioritize) {
-    std::string ok = "[", failed = "{";
-    bool first_ok = true, first_f = true;
-    std::string dstr;
-    for (int i = 0; i < dem.n; ++i) {
-      dstr += "(" + std::to_string(dem.c[i].pct);
-      if (dem.c[i].mib) dstr += "," + std::to_string(dem.c[i].mib) + "Mi";
-      dstr += ")";
-    }
-    std::vector<int32_t> rcs(ids.size()), sc(ids.size());
-    ledger_->assume_many(ids.data(), static_cast<int>(ids.size()), dem, o, rcs.data(), sc.data());
+    rcs.resize(ids.size());
+    scores.resize(ids.size());
+    ledger_->assume_many(ids.data(), static_cast<int>(ids.size()), dem, o, rcs.data(), scores.data());
+    // written straight into the reply; a fitting node's name is its request token, as is
+    r.clear();
+    r += "{\"Nodes\":null,\"NodeNames\":[";
+    bool first = true, any_failed = false;
     for (size_t i = 0; i < ids.size(); ++i) {
-      const int32_t rc = rcs[i];
-      if (rc == kOk) {
-        if (!first_ok) ok += ",";
-        json::append_quoted(&ok, nv[i]);
-        first_ok = false;
-      } else {
-        if (!first_f) failed += ",";
-        json::append_quoted(&failed, nv[i]);
-        failed += ":";
-        std::string msg = "can't allocate " + dstr + " on node " + std::string(nv[i]) + ": " + err_str(rc);
-        json::append_quoted(&failed, msg);
-        first_f = false;
+      if (rcs[i] != kOk) {
+        any_failed = true;
+        continue;
+      }
+      if (!first) r += ',';
+      r += nraw[i];
+      first = false;
+    }
+    r += "],\"FailedNodes\":{";
+    if (any_failed) {
+      std::string dstr;
+      for (int i = 0; i < dem.n; ++i) {
+        dstr += "(" + std::to_string(dem.c[i].pct);
+        if (dem.c[i].mib) dstr += "," + std::to_string(dem.c[i].mib) + "Mi";
+        dstr += ")";
+      }
+      first = true;
+      for (size_t i = 0; i < ids.size(); ++i) {
+        if (rcs[i] == kOk) continue;
+        if (!first) r += ',';
+        r += nraw[i];
+        r += ':';
+        json::append_quoted(&r, "can't allocate " + dstr + " on node " + std::string(nv[i]) + ": " + err_str(rcs[i]));
+        first = false;
       }
     }
-    ok += "]";
-    failed += "}";
-    r = "{\"Nodes\":null,\"NodeNames\":" + ok + ",\"FailedNodes\":" + failed + ",\"Error\":\"\"}";
+    r += "},\"Error\":\"\"}";
     return true;
   }
-  std::vector<int32_t> scores(ids.size()), rcs(ids.size());
+  scores.resize(ids.size());
+  rcs.resize(ids.size());
   ledger_->assume_many(ids.data(), static_cast<int>(ids.size()), dem, o, rcs.data(), scores.data());
   int64_t best = -1;
   int n_best = 0;
@@ -1025,14 +1059,19 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
       for (int32_t& s : scores) s = std::max(0, std::min(10, static_cast<int32_t>(std::nearbyint(s / 10.0))));
     }
   }
-  r = "[";
+  r.clear();
+  r += '[';
+  char num[16];
   for (size_t i = 0; i < ids.size(); ++i) {
-    if (i) r += ",";
+    if (i) r += ',';
     r += "{\"Host\":";
-    json::append_quoted(&r, nv[i]);
-    r += ",\"Score\":" + std::to_string(scores[i]) + "}";
+    r += nraw[i];
+    r += ",\"Score\":";
+    const auto res = std::to_chars(num, num + sizeof num, scores[i]);
+    r.append(num, static_cast<size_t>(res.ptr - num));
+    r += '}';
   }
-  r += "]";
+  r += ']';
   return true;
 }
 

@@ -59,18 +59,41 @@ bool Doc::parse(std::string_view src) {
 bool Doc::string(uint32_t* off, uint32_t* len) {
   if (p_ >= src_.size() || src_[p_] != '"') return false;
   ++p_;
+  const char* s = src_.data();
+  const size_t n = src_.size();
+  {
+    // common case: no escape before the closing quote -> the text stays in the source
+    size_t q = p_;
+    while (q < n) {
+      const unsigned char ch = static_cast<unsigned char>(s[q]);
+      if (ch == '"' || ch == '\\' || ch < 0x20) break;
+      ++q;
+    }
+    if (q < n && s[q] == '"') {
+      *off = static_cast<uint32_t>(p_);
+      *len = static_cast<uint32_t>(q - p_) | kInSrc;
+      p_ = q + 1;
+      return true;
+    }
+  }
   *off = static_cast<uint32_t>(arena_.size());
-  while (p_ < src_.size()) {
-    const char c = src_[p_++];
+  while (p_ < n) {
+    // a run of plain characters is copied in one go; only quotes, escapes and control
+    // characters need a look
+    const size_t run = p_;
+    while (p_ < n) {
+      const unsigned char ch = static_cast<unsigned char>(s[p_]);
+      if (ch == '"' || ch == '\\' || ch < 0x20) break;
+      ++p_;
+    }
+    if (p_ > run) arena_.append(s + run, p_ - run);
+    if (p_ >= n) return false;
+    const char c = s[p_++];
     if (c == '"') {
       *len = static_cast<uint32_t>(arena_.size() - *off);
       return true;
     }
     if (static_cast<unsigned char>(c) < 0x20) return false;
-    if (c != '\\') {
-      arena_.push_back(c);
-      continue;
-    }
     if (p_ >= src_.size()) return false;
     const char e = src_[p_++];
     switch (e) {
@@ -218,7 +241,13 @@ int32_t Doc::get(int32_t obj, std::string_view k, bool ci) const {
 
 void append_quoted(std::string* out, std::string_view s) {
   out->push_back('"');
-  for (const char c : s) {
+  size_t run = 0;
+  for (size_t i = 0; i < s.size(); ++i) {
+    const char c = s[i];
+    const unsigned char u = static_cast<unsigned char>(c);
+    if (c != '"' && c != '\\' && u >= 0x20) continue;
+    out->append(s.data() + run, i - run);   // the plain run before it, in one copy
+    run = i + 1;
     switch (c) {
       case '"': out->append("\\\""); break;
       case '\\': out->append("\\\\"); break;
@@ -227,17 +256,14 @@ void append_quoted(std::string* out, std::string_view s) {
       case '\t': out->append("\\t"); break;
       case '\b': out->append("\\b"); break;
       case '\f': out->append("\\f"); break;
-      default:
-        if (static_cast<unsigned char>(c) < 0x20) {
-          static const char* hex = "0123456789abcdef";
-          out->append("\\u00");
-          out->push_back(hex[(c >> 4) & 0xF]);
-          out->push_back(hex[c & 0xF]);
-        } else {
-          out->push_back(c);
-        }
+      default: {
+        static const char* hex = "0123456789abcdef";
+        char esc[7] = {'\\', 'u', '0', '0', hex[u >> 4], hex[u & 15], 0};
+        out->append(esc, 6);
+      }
     }
   }
+  out->append(s.data() + run, s.size() - run);
   out->push_back('"');
 }
 

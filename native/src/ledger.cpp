@@ -512,10 +512,56 @@ bool Ledger::node_named(int32_t id, std::string_view name) const {
          n->name[name.size()] == '\0';
 }
 
+namespace {
+// Per-thread memo of (rc, score) per node for the few demands a burst repeats: a flat array
+// indexed by node id, valid while the node's generation is the one it was computed at. A
+// filter or priorities request over 64 nodes then reads 64 generations and 64 contiguous
+// entries instead of probing 64 separately allocated plan-cache tables (~100 ns a node).
+// Any node added or removed (the ledger's epoch) clears it.
+struct ScoreMemo {
+  const void* owner = nullptr;
+  uint64_t dh = 0, oh = 0, epoch = 0, used = 0;
+  struct E {
+    uint64_t gen;   // generation + 1; 0 = empty
+    int32_t rc, score;
+  };
+  std::vector<E> e;
+};
+constexpr int kMemoSlots = 16;
+thread_local ScoreMemo t_memo[kMemoSlots];
+thread_local uint64_t t_memo_clock = 0;
+
+ScoreMemo& memo_for(const void* owner, uint64_t dh, uint64_t oh, uint64_t epoch, uint32_t n_nodes) {
+  ScoreMemo* lru = &t_memo[0];
+  for (ScoreMemo& m : t_memo) {
+    if (m.owner == owner && m.dh == dh && m.oh == oh) {
+      if (m.epoch != epoch) {
+        m.e.assign(n_nodes, ScoreMemo::E{0, 0, 0});
+        m.epoch = epoch;
+      }
+      if (m.e.size() < n_nodes) m.e.resize(n_nodes, ScoreMemo::E{0, 0, 0});
+      m.used = ++t_memo_clock;
+      return m;
+    }
+    if (m.used < lru->used) lru = &m;
+  }
+  lru->owner = owner;
+  lru->dh = dh;
+  lru->oh = oh;
+  lru->epoch = epoch;
+  lru->e.assign(n_nodes, ScoreMemo::E{0, 0, 0});
+  lru->used = ++t_memo_clock;
+  return *lru;
+}
+}  // namespace
+
 void Ledger::assume_many(const int32_t* ids, int count, const Demand& d, const Options& o_in, int32_t* rc,
                          int32_t* score) {
   const Options o = resolve(o_in, d);
   const uint64_t dh = d.hash(), oh = o.hash();
+  const int32_t n_nodes = hdr_->n_nodes.load(std::memory_order_acquire);
+  ScoreMemo& memo = memo_for(this, dh, oh, hdr_->epoch.load(std::memory_order_acquire),
+                             static_cast<uint32_t>(std::max(0, n_nodes)));
   Plan plan;
   for (int i = 0; i < count; ++i) {
     const int32_t id = ids[i];
@@ -525,16 +571,26 @@ void Ledger::assume_many(const int32_t* ids, int count, const Demand& d, const O
       rc[i] = kErrUnknownNode;
       continue;
     }
-    if (cache_get_score(CacheKey{id, n->generation.load(std::memory_order_acquire), dh, oh}, &rc[i], &score[i]))
+    const uint64_t gen = n->generation.load(std::memory_order_acquire);
+    ScoreMemo::E* me = static_cast<size_t>(id) < memo.e.size() ? &memo.e[id] : nullptr;
+    if (me && me->gen == gen + 1) {
+      rc[i] = me->rc;
+      score[i] = me->score;
       continue;
+    }
+    if (cache_get_score(CacheKey{id, gen, dh, oh}, &rc[i], &score[i])) {
+      if (me) *me = ScoreMemo::E{gen + 1, rc[i], score[i]};
+      continue;
+    }
     NodeSnapshot snap;
     if (!snapshot(id, &snap)) {
       rc[i] = kErrUnknownNode;
       continue;
     }
     rc[i] = choose(snap.devs, snap.n_devs, &snap.topo, d, o, &plan);
-    score[i] = plan.score;
+    score[i] = rc[i] == kOk ? plan.score : 0;
     cache_put(CacheKey{id, snap.generation, dh, oh}, rc[i], plan);
+    if (me) *me = ScoreMemo::E{snap.generation + 1, rc[i], score[i]};
   }
 }
 

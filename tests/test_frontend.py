@@ -611,3 +611,26 @@ def test_front_door_survives_mutated_http_framing(routes):
             await rt.stop()
 
     asyncio.run(main())
+
+
+def test_escaped_node_names_still_answer_byte_identical():
+    """The native verbs reuse each NodeNames token as written; a token with an escape is
+    re-quoted, so the reply still equals json.dumps of the Python verb's answer."""
+    from nanogpu.extender.verbs import Extender
+    from nanogpu.k8s.fake_apiserver import FakeKubeStore, InProcKube
+    from nanogpu.state.cluster import ClusterState
+
+    st = ClusterState()
+    for n in ("n0", "n1"):
+        st.register_node(pu.make_node(n, 8, synthetic_mi355x(8).to_json()))
+    ext = Extender(st, InProcKube(FakeKubeStore()))
+    fe = N.Frontend(st.ledger, "127.0.0.1", 0, 1)
+    try:
+        fe.set_options(st.options, False, False)
+        raw = ('{"Pod":' + json.dumps(pu.make_pod("p", [("c", 20)])) + ',"NodeNames":["n\\u0030","n1"]}').encode()
+        ok, _, out = fe.time_verb(raw, False, 1)
+        assert ok and out == _dumps(ext.filter(json.loads(raw)))
+        ok, _, out = fe.time_verb(raw, True, 1)
+        assert ok and out == _dumps(ext.prioritize(json.loads(raw)))
+    finally:
+        fe.stop()
