@@ -1313,10 +1313,20 @@ std::vector<int> Server::create_pods(const std::vector<std::string>& texts) {
   std::vector<FastCreate> fast(texts.size());
   std::vector<JV> vs(texts.size());
   std::vector<int> codes(texts.size(), 201);
-  for (size_t i = 0; i < texts.size(); ++i) {
-    fast[i] = fast_create(texts[i], "");
-    if (!fast[i].ok && !parse(texts[i], &vs[i])) codes[i] = 400;
-  }
+  // parsing needs no lock: a large batch is parsed by a few threads, only the inserts are serial
+  auto parse_range = [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) {
+      fast[i] = fast_create(texts[i], "");
+      if (!fast[i].ok && !parse(texts[i], &vs[i])) codes[i] = 400;
+    }
+  };
+  const size_t workers = texts.size() >= 256 ? 4 : 1;
+  std::vector<std::thread> pool;
+  const size_t per = (texts.size() + workers - 1) / workers;
+  for (size_t w = 1; w < workers; ++w)
+    pool.emplace_back(parse_range, std::min(texts.size(), w * per), std::min(texts.size(), (w + 1) * per));
+  parse_range(0, std::min(texts.size(), per));
+  for (auto& t : pool) t.join();
   std::lock_guard<std::mutex> g(impl_->mu);
   for (size_t i = 0; i < texts.size(); ++i) {
     if (codes[i] != 201) continue;
