@@ -837,6 +837,10 @@ def main() -> int:
             "nomination_adopt_pct": (round(100.0 * res["nominations"]["adopted"] / res["nominations"]["made"], 2)
                                      if res["nominations"]["made"] else None),
             "nomination_margin": res["nomination_margin"],
+            # also end to end, from the pod entering the stand-in's queue (the burst
+            # is created at once) to its bind answered; rank 0, mean of the per-step medians
+            "p50_queue_to_bound_ms_rank0": (round(statistics.mean(st.get("e2e_p50_ms", 0.0) for st in res["steps"]), 3)
+                                            if res["steps"] else None),
             "unschedulable_attempts": out["unschedulable"],
             "gpu": gpu_info,
             "native_verb_mean_us": res.get("native"),
