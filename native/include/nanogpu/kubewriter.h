@@ -86,6 +86,7 @@ class KubeWriter {
  private:
   void run();
   void process(HttpConn* c, BindJob& j);
+  void refuse(BindJob& j);
   int call(HttpConn* c, const char* method, const std::string& path, const std::string& ctype,
            const std::string& body, std::string* resp, bool retry);
   std::string auth();

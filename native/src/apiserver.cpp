@@ -238,16 +238,18 @@ struct Obj {
   std::string json;
   std::string ns, name, uid, node, phase;
   uint64_t rv = 0;
+  // set before the object is published (seal, restamp), or once by v(); read through
+  // atomic_load because restamp may copy it while another thread is building it
   mutable std::once_flag once;
   mutable std::shared_ptr<const JV> tree;
   const JV& v() const {
     std::call_once(once, [this] {
-      if (tree) return;
+      if (std::atomic_load(&tree)) return;
       auto t = std::make_shared<JV>();
       parse(json, t.get());
-      tree = std::move(t);
+      std::atomic_store(&tree, std::shared_ptr<const JV>(std::move(t)));
     });
-    return *tree;
+    return *std::atomic_load(&tree);
   }
   const JV* labels() const {
     const JV* m = v().get("metadata");
@@ -277,7 +279,7 @@ ObjP seal(JV v, uint64_t rv) {
 ObjP restamp(const ObjP& cur, uint64_t rv) {
   const std::string old = "\"resourceVersion\":\"" + std::to_string(cur->rv) + "\"";
   const size_t at = cur->json.find(old);
-  if (at == std::string::npos) return seal(cur->v(), rv);
+  if (at == std::string::npos) return seal(cur->v(), rv);   // (not ours: no stamp to splice)
   auto o = std::make_shared<Obj>();
   o->json.reserve(cur->json.size() + 4);
   o->json.append(cur->json, 0, at);
@@ -286,7 +288,7 @@ ObjP restamp(const ObjP& cur, uint64_t rv) {
   o->ns = cur->ns, o->name = cur->name, o->uid = cur->uid, o->node = cur->node, o->phase = cur->phase;
   o->rv = rv;
   // the tree (if built) stays usable as the base of later patches, which re-stamp anyway
-  if (cur->tree) o->tree = cur->tree;
+  if (auto t = std::atomic_load(&cur->tree)) o->tree = std::move(t);
   return o;
 }
 

@@ -323,6 +323,12 @@ KubeWriter::~KubeWriter() {
   if (ctx_) SSL_CTX_free(static_cast<SSL_CTX*>(ctx_));
 }
 
+void KubeWriter::refuse(BindJob& j) {
+  // kube-scheduler gets an answer (and retries elsewhere); the ledger is left clean
+  if (j.fresh) ledger_->release(j.uid);
+  respond_(j.id, 500, "{\"Error\":\"nano-gpu: extender shutting down\"}");
+}
+
 void KubeWriter::stop() {
   {
     std::lock_guard<std::mutex> g(mu_);
@@ -332,21 +338,28 @@ void KubeWriter::stop() {
   cv_.notify_all();
   for (auto& t : threads_)
     if (t.joinable()) t.join();
-  // anything still queued: kube-scheduler gets an answer (and retries), the ledger is clean
-  for (BindJob& j : q_) {
-    if (j.fresh) ledger_->release(j.uid);
-    respond_(j.id, 500, "{\"Error\":\"nano-gpu: extender shutting down\"}");
+  std::deque<BindJob> left;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    left.swap(q_);
   }
-  q_.clear();
+  for (BindJob& j : left) {
+    refuse(j);
+    stats.inflight.fetch_sub(1, std::memory_order_relaxed);
+  }
 }
 
 void KubeWriter::submit(BindJob job) {
-  stats.inflight.fetch_add(1, std::memory_order_relaxed);
   {
     std::lock_guard<std::mutex> g(mu_);
-    q_.push_back(std::move(job));
+    if (!stop_) {
+      stats.inflight.fetch_add(1, std::memory_order_relaxed);
+      q_.push_back(std::move(job));
+      cv_.notify_one();
+      return;
+    }
   }
-  cv_.notify_one();
+  refuse(job);   // a bind that arrives while the writer shuts down
 }
 
 std::string KubeWriter::auth() {

@@ -242,6 +242,23 @@ static void apiserver_and_writers(int pods) {
   stop_watch.store(true);
   watcher.join();
   CHECK(events.load() == 4 * pods);
+  // deletes racing patches on the same pods (a delete re-stamps the object while a patch may
+  // be building its tree outside the store lock)
+  {
+    std::thread patcher([&] {
+      for (int i = 0; i < pods; ++i)
+        http(port, "PATCH", "/api/v1/namespaces/s/pods/p" + std::to_string(i), "{\"metadata\":{\"labels\":{\"x\":\"y\"}}}");
+    });
+    std::thread deleter([&] {
+      for (int i = 0; i < pods; ++i) {
+        const std::string r = http(port, "DELETE", "/api/v1/namespaces/s/pods/p" + std::to_string(i), "");
+        CHECK(r.rfind("HTTP/1.1 200", 0) == 0);
+      }
+    });
+    patcher.join();
+    deleter.join();
+    CHECK(http(port, "GET", "/api/v1/namespaces/s/pods", "").find("\"items\":[]") != std::string::npos);
+  }
   srv.stop();
   std::printf("apiserver ok: %d pods bound by native writers, %d watch events\n", pods, events.load());
 }
