@@ -60,8 +60,9 @@ class Matcher:
         self.claimed: dict[tuple[str, str], float] = {}   # (pod uid, container) -> time
 
     async def candidates(self) -> list[dict]:
-        pods, _ = await self.api.list_pods(label_selector=f"{T.LABEL_GPU_ASSUME}=true",
-                                           field_selector=f"{T.NODE_NAME_FIELD}={self.node}")
+        # by node and annotation, not by the assume label: the placement annotations land
+        # with the binding itself, the label in a PATCH that may arrive a moment later
+        pods, _ = await self.api.list_pods(field_selector=f"{T.NODE_NAME_FIELD}={self.node}")
         return [p for p in pods if pu.is_assumed(p) and not pu.is_completed(p)]
 
     async def match(self, percent: int) -> tuple[dict, dict] | None:

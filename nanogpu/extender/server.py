@@ -387,10 +387,13 @@ class NativeServer:
                       f"nanogpu_native_bind_rollbacks_total {kw['rollbacks']}",
                       "# TYPE nanogpu_native_api_retries_total counter",
                       f"nanogpu_native_api_retries_total {kw['retries']}",
-                      "# HELP nanogpu_native_api_write_seconds_total time in the bind's API writes",
+                      "# HELP nanogpu_native_api_write_seconds_total time in the bind's API writes: the "
+                      "binding and the label PATCH in flight together, then label-PATCH retries",
                       "# TYPE nanogpu_native_api_write_seconds_total counter",
-                      f'nanogpu_native_api_write_seconds_total{{op="patch"}} {kw["patch_seconds_total"]:.9f}',
-                      f'nanogpu_native_api_write_seconds_total{{op="binding"}} {kw["binding_seconds_total"]:.9f}',
+                      f'nanogpu_native_api_write_seconds_total{{op="binding+patch"}} {kw["binding_seconds_total"]:.9f}',
+                      f'nanogpu_native_api_write_seconds_total{{op="patch_retry"}} {kw["patch_seconds_total"]:.9f}',
+                      "# TYPE nanogpu_native_label_failures_total counter",
+                      f"nanogpu_native_label_failures_total {kw['label_failures']}",
                       "# TYPE nanogpu_native_binds_inflight gauge",
                       f"nanogpu_native_binds_inflight {kw['inflight']}"]
         return ("\n".join(lines) + "\n").encode()

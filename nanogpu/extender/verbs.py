@@ -268,26 +268,50 @@ class Extender:
 
     async def _write(self, ns: str, name: str, uid: str, node: str, names: list[str], plan, fresh: bool, sp,
                      pod_ns_name: tuple[str, str]) -> None:
-        """Second half of bind: PATCH placement annotations, POST binding, commit; on any
-        failure roll the reservation back and un-annotate (fixes reference D1/D2)."""
+        """Second half of bind: the placement annotations and the binding, then commit; on
+        any failure roll the reservation back and un-annotate (fixes reference D1/D2).
+
+        The Binding itself carries the placement annotations, which kube-apiserver sets on
+        the pod together with spec.nodeName (setPodHostAndAnnotations): a bound pod never
+        lacks them, whichever write lands first. The PATCH (annotations + the assume label)
+        is sent at the same time, so a bind costs one API round trip, not two. In-process
+        APIs that complete inline keep the writes sequential (no Tasks)."""
         try:
             t2 = time.perf_counter()
             extra = {T.ANNOTATION_ASSUME_TIME: f"{time.time():.6f}"}
             patch = pu.placement_patch_names(names, plan, extra)
-            try:   # first attempt inline; the retry loop only after an API error
-                await self.api.patch_pod(ns, name, patch)
-            except ApiError as e:
-                await self._retry_after(e, "patch", self.api.patch_pod, ns, name, patch)
-            t3 = time.perf_counter()
-            try:
+            ann = patch["metadata"]["annotations"]
+
+            async def write_patch() -> None:
+                try:   # first attempt inline; the retry loop only after an API error
+                    await self.api.patch_pod(ns, name, patch)
+                except ApiError as e:
+                    await self._retry_after(e, "patch", self.api.patch_pod, ns, name, patch)
+
+            async def write_binding() -> None:
                 try:
-                    await self.api.bind_pod(ns, name, uid, node)
-                except ApiError as e0:
-                    await self._retry_after(e0, "bind", self.api.bind_pod, ns, name, uid, node)
-            except ApiError as e:
-                # A retried bind whose first attempt landed: already bound to this node is success.
-                if not e.conflict or pu.node_name_of(await self.api.get_pod(ns, name)) != node:
-                    raise
+                    try:
+                        await self.api.bind_pod(ns, name, uid, node, ann)
+                    except ApiError as e0:
+                        await self._retry_after(e0, "bind", self.api.bind_pod, ns, name, uid, node, ann)
+                except ApiError as e:
+                    # A retried bind whose first attempt landed: already bound to this node is success.
+                    if not e.conflict or pu.node_name_of(await self.api.get_pod(ns, name)) != node:
+                        raise
+
+            if getattr(self.api, "completes_inline", False):
+                await write_patch()
+                t3 = time.perf_counter()
+                await write_binding()
+            else:
+                pe, be = await asyncio.gather(write_patch(), write_binding(), return_exceptions=True)
+                t3 = time.perf_counter()
+                if isinstance(be, BaseException):
+                    raise be
+                if isinstance(pe, BaseException):
+                    # bound, annotations on the pod with the binding: only the label is late
+                    log.warning("bind %s/%s: label PATCH failed (%s); retrying in the background", ns, name, pe)
+                    self._background(self._relabel(ns, name, patch))
             t4 = time.perf_counter()
             sp.phases["patch"], sp.phases["binding"] = t3 - t2, t4 - t3
             self._m_patch.observe(t3 - t2)
@@ -307,6 +331,18 @@ class Extender:
             raise
         self.state.commit(uid)
         self.metrics.pods_bound.inc()
+
+    async def _relabel(self, ns: str, name: str, patch: dict) -> None:
+        for attempt in range(6):
+            await asyncio.sleep(0.05 * (2 ** attempt))
+            try:
+                await self.api.patch_pod(ns, name, patch)
+                return
+            except ApiError as e:
+                if e.not_found:
+                    return
+            except (OSError, asyncio.TimeoutError):
+                pass
 
     async def _unannotate(self, ns: str, name: str, names: list[str]) -> None:
         ann = {T.container_annotation(n): None for n in names}

@@ -231,9 +231,12 @@ class KubeClient:
         return await self.request("PATCH", f"/api/v1/namespaces/{ns}/pods/{name}", patch,
                                   content_type="application/merge-patch+json")
 
-    async def bind_pod(self, ns: str, name: str, uid: str, node: str) -> None:
-        body = {"apiVersion": "v1", "kind": "Binding",
-                "metadata": {"name": name, "namespace": ns, "uid": uid},
+    async def bind_pod(self, ns: str, name: str, uid: str, node: str, annotations: dict | None = None) -> None:
+        """pods/binding; `annotations` land on the pod atomically with spec.nodeName."""
+        md = {"name": name, "namespace": ns, "uid": uid}
+        if annotations:
+            md["annotations"] = annotations
+        body = {"apiVersion": "v1", "kind": "Binding", "metadata": md,
                 "target": {"apiVersion": "v1", "kind": "Node", "name": node}}
         await self.request("POST", f"/api/v1/namespaces/{ns}/pods/{name}/binding", body)
 

@@ -193,7 +193,9 @@ class FakeKubeStore:
         self._emit("pods", "MODIFIED", pod)
         return pod
 
-    def bind_pod(self, ns: str, name: str, uid: str, node: str) -> None:
+    def bind_pod(self, ns: str, name: str, uid: str, node: str, annotations: dict | None = None) -> None:
+        """pods/binding. As kube-apiserver does (setPodHostAndAnnotations), the Binding's own
+        metadata.annotations are set on the pod together with spec.nodeName."""
         self._count("bind_pod")
         if self.faults.bind_error_rate and self.faults.roll(self.faults.bind_error_rate):
             raise ApiError(500, "injected binding failure", "InternalError")
@@ -212,6 +214,8 @@ class FakeKubeStore:
         np_["spec"] = dict(p.get("spec") or {}, nodeName=node)
         np_["status"] = dict(p.get("status") or {}, phase="Running")
         np_["metadata"] = dict(p.get("metadata") or {})
+        if annotations:
+            np_["metadata"]["annotations"] = dict(np_["metadata"].get("annotations") or {}, **annotations)
         np_ = self._stamp(np_)
         self.pods[(ns, name)] = np_
         self.bindings.append((ns, name, node))
@@ -414,11 +418,11 @@ class InProcKube:
             await asyncio.sleep(self.store.faults.latency_s)
         return self.store.patch_pod(ns, name, patch)
 
-    async def bind_pod(self, ns, name, uid, node):
+    async def bind_pod(self, ns, name, uid, node, annotations=None):
         self.calls += 1
         if self.store.faults.latency_s > 0:   # inline: no coroutine per call
             await asyncio.sleep(self.store.faults.latency_s)
-        self.store.bind_pod(ns, name, uid, node)
+        self.store.bind_pod(ns, name, uid, node, annotations)
 
     async def create_pod(self, pod):
         self.calls += 1
@@ -584,7 +588,8 @@ def make_app(store: FakeKubeStore) -> web.Application:
         body = await request.json()
         try:
             store.bind_pod(request.match_info["ns"], request.match_info["name"],
-                           (body.get("metadata") or {}).get("uid", ""), (body.get("target") or {}).get("name", ""))
+                           (body.get("metadata") or {}).get("uid", ""), (body.get("target") or {}).get("name", ""),
+                           (body.get("metadata") or {}).get("annotations"))
             return web.json_response({"kind": "Status", "status": "Success"}, status=201)
         except ApiError as e:
             return _err(e)

@@ -45,13 +45,20 @@ class HttpConn {
   // failed on a connection the server had already closed.
   int request(const char* method, const std::string& path, const std::string& content_type,
               const std::string& body, const std::string& auth, std::string* resp);
+  // The same in two halves, so that requests on two connections are in flight together:
+  // start() sends, finish() reads the answer (with request()'s one retry on a fresh connection).
+  bool start(const char* method, const std::string& path, const std::string& content_type,
+             const std::string& body, const std::string& auth);
+  int finish(std::string* resp);
 
  private:
   bool connect_();
   void close_();
   bool send_all(const char* p, size_t n);
   long recv_some(char* p, size_t n);
-  int exchange(const std::string& req, std::string* resp, bool* retryable);
+  int receive(std::string* resp, bool* retryable);
+  std::string req_;
+  bool reused_ = false, sent_ = false;
 
   const KubeTarget* t_;
   void* ctx_;               // SSL_CTX* (nullptr: plain HTTP)
@@ -70,7 +77,8 @@ struct BindJob {
 };
 
 struct KubeWriterStats {
-  std::atomic<uint64_t> ok{0}, failed{0}, rollbacks{0}, retries{0}, patch_ns{0}, binding_ns{0}, inflight{0};
+  std::atomic<uint64_t> ok{0}, failed{0}, rollbacks{0}, retries{0}, patch_ns{0}, binding_ns{0}, inflight{0},
+      label_failures{0};
 };
 
 class KubeWriter {
@@ -85,7 +93,7 @@ class KubeWriter {
 
  private:
   void run();
-  void process(HttpConn* c, BindJob& j);
+  void process(HttpConn* c, HttpConn* c2, BindJob& j);
   void refuse(BindJob& j);
   int call(HttpConn* c, const char* method, const std::string& path, const std::string& ctype,
            const std::string& body, std::string* resp, bool retry);

@@ -574,7 +574,10 @@ struct Server::Impl {
   ObjP patch_pod(std::string_view ns, std::string_view name, const JV& patch) {
     return write_pod(ns, name, [&](const Obj&, JV* v) { merge_patch(v, patch); });
   }
-  void bind_pod(std::string_view ns, std::string_view name, std::string_view uid, std::string_view node) {
+  // pods/binding; the Binding's metadata.annotations land on the pod with spec.nodeName, as
+  // kube-apiserver's setPodHostAndAnnotations does
+  void bind_pod(std::string_view ns, std::string_view name, std::string_view uid, std::string_view node,
+                const JV* annotations = nullptr) {
     {
       std::lock_guard<std::mutex> g(mu);
       if (!nodes.count(std::string(node))) {
@@ -589,6 +592,10 @@ struct Server::Impl {
                      "pod " + std::string(name) + " is already assigned to node \"" + cur.node + "\""};
       v->child("spec").set("nodeName", JV::str(std::string(node)));
       v->child("status").set("phase", JV::str("Running"));
+      if (annotations && annotations->is_obj()) {
+        JV& ann = v->child("metadata").child("annotations");
+        for (const auto& kv : annotations->o) ann.set(kv.first, kv.second);
+      }
     });
     std::lock_guard<std::mutex> g(mu);
     ++bindings;
@@ -773,7 +780,8 @@ struct Server::Impl {
             const JV* md = b.get("metadata");
             const JV* tg = b.get("target");
             n_bind.fetch_add(1, std::memory_order_relaxed);
-            bind_pod(ns, name, md ? str_of(md->get("uid")) : std::string(), tg ? str_of(tg->get("name")) : "");
+            bind_pod(ns, name, md ? str_of(md->get("uid")) : std::string(), tg ? str_of(tg->get("name")) : "",
+                     md ? md->get("annotations") : nullptr);
             return {201, kOk};
           }
         }

@@ -762,6 +762,7 @@ PYBIND11_MODULE(_native, m) {
              d["inflight"] = w->stats.inflight.load();
              d["patch_seconds_total"] = static_cast<double>(w->stats.patch_ns.load()) * 1e-9;
              d["binding_seconds_total"] = static_cast<double>(w->stats.binding_ns.load()) * 1e-9;
+             d["label_failures"] = w->stats.label_failures.load();
              return d;
            })
       .def("take",

@@ -168,12 +168,8 @@ long HttpConn::recv_some(char* p, size_t n) {
   }
 }
 
-int HttpConn::exchange(const std::string& req, std::string* resp, bool* retryable) {
+int HttpConn::receive(std::string* resp, bool* retryable) {
   *retryable = false;
-  if (!send_all(req.data(), req.size())) {
-    *retryable = true;
-    return 0;
-  }
   char tmp[16384];
   size_t he;
   bool got_any = !buf_.empty();
@@ -248,38 +244,62 @@ int HttpConn::exchange(const std::string& req, std::string* resp, bool* retryabl
   return status;
 }
 
+bool HttpConn::start(const char* method, const std::string& path, const std::string& content_type,
+                     const std::string& body, const std::string& auth) {
+  req_.clear();
+  req_.reserve(256 + body.size());
+  req_ += method;
+  req_ += ' ';
+  req_ += path;
+  req_ += " HTTP/1.1\r\nHost: ";
+  req_ += t_->host;
+  req_ += "\r\nUser-Agent: nano-gpu-scheduler-amd/0.1\r\nAccept: application/json\r\n";
+  if (!auth.empty()) req_ += "Authorization: Bearer " + auth + "\r\n";
+  if (!body.empty() || std::strcmp(method, "POST") == 0 || std::strcmp(method, "PATCH") == 0) {
+    req_ += "Content-Type: " + content_type + "\r\nContent-Length: " + std::to_string(body.size()) + "\r\n";
+  }
+  req_ += "\r\n";
+  req_ += body;
+  reused_ = fd_ >= 0;
+  sent_ = false;
+  if (!reused_ && !connect_()) return false;
+  sent_ = send_all(req_.data(), req_.size());
+  return sent_;
+}
+
+int HttpConn::finish(std::string* resp) {
+  resp->clear();
+  bool retryable = false;
+  if (sent_) {
+    const int st = receive(resp, &retryable);
+    if (st > 0) return st;
+  } else {
+    retryable = reused_;   // the send failed on an idle connection the server had closed
+  }
+  close_();
+  if (!(reused_ && retryable)) {
+    if (resp->empty()) *resp = sent_ || reused_ ? "connection to the API server failed"
+                                                : "cannot connect to " + t_->host + ":" + std::to_string(t_->port);
+    return 0;
+  }
+  // once more on a fresh connection
+  if (!connect_()) {
+    *resp = "cannot connect to " + t_->host + ":" + std::to_string(t_->port);
+    return 0;
+  }
+  if (send_all(req_.data(), req_.size())) {
+    const int st = receive(resp, &retryable);
+    if (st > 0) return st;
+  }
+  close_();
+  if (resp->empty()) *resp = "connection to the API server failed";
+  return 0;
+}
+
 int HttpConn::request(const char* method, const std::string& path, const std::string& content_type,
                       const std::string& body, const std::string& auth, std::string* resp) {
-  std::string req;
-  req.reserve(256 + body.size());
-  req += method;
-  req += ' ';
-  req += path;
-  req += " HTTP/1.1\r\nHost: ";
-  req += t_->host;
-  req += "\r\nUser-Agent: nano-gpu-scheduler-amd/0.1\r\nAccept: application/json\r\n";
-  if (!auth.empty()) req += "Authorization: Bearer " + auth + "\r\n";
-  if (!body.empty() || std::strcmp(method, "POST") == 0 || std::strcmp(method, "PATCH") == 0) {
-    req += "Content-Type: " + content_type + "\r\nContent-Length: " + std::to_string(body.size()) + "\r\n";
-  }
-  req += "\r\n";
-  req += body;
-  for (int attempt = 0; attempt < 2; ++attempt) {
-    const bool reused = fd_ >= 0;
-    if (!reused && !connect_()) {
-      *resp = "cannot connect to " + t_->host + ":" + std::to_string(t_->port);
-      return 0;
-    }
-    bool retryable = false;
-    const int st = exchange(req, resp, &retryable);
-    if (st > 0) return st;
-    close_();
-    if (!(reused && retryable)) {
-      if (resp->empty()) *resp = "connection to the API server failed";
-      return 0;
-    }
-  }
-  return 0;
+  start(method, path, content_type, body, auth);
+  return finish(resp);
 }
 
 // ------------------------------------------------------------------------------ KubeWriter
@@ -397,58 +417,66 @@ int KubeWriter::call(HttpConn* c, const char* method, const std::string& path, c
   }
 }
 
-void KubeWriter::process(HttpConn* c, BindJob& j) {
+void KubeWriter::process(HttpConn* c, HttpConn* c2, BindJob& j) {
   const std::string base = "/api/v1/namespaces/" + j.ns + "/pods/" + j.name;
   std::string err;
-  std::string resp;
-  // 1. placement annotations + assume label (pu.placement_patch_names)
-  std::string patch = "{\"metadata\":{\"annotations\":{";
+  // placement annotations (pu.placement_patch_names): the Binding carries them, so they land
+  // on the pod atomically with spec.nodeName (kube-apiserver setPodHostAndAnnotations); the
+  // PATCH, sent at the same time on a second connection, adds the assume label
+  std::string ann = "{";
   for (size_t k = 0; k < j.containers.size() && k < j.plan.size(); ++k) {
-    json::append_quoted(&patch, kContainerPrefix + j.containers[k]);
-    patch += ":\"";
+    json::append_quoted(&ann, kContainerPrefix + j.containers[k]);
+    ann += ":\"";
     for (size_t i = 0; i < j.plan[k].size(); ++i) {
-      if (i) patch += ',';
-      patch += std::to_string(j.plan[k][i]);
+      if (i) ann += ',';
+      ann += std::to_string(j.plan[k][i]);
     }
-    patch += "\",";
+    ann += "\",";
   }
   char ts[48];
   std::snprintf(ts, sizeof ts, "%.6f", wall_s());
-  patch += "\"";
-  patch += kAssume;
-  patch += "\":\"true\",\"";
-  patch += kAssumeTime;
-  patch += "\":\"";
-  patch += ts;
-  patch += "\"},\"labels\":{\"";
-  patch += kAssume;
-  patch += "\":\"true\"}}}";
+  ann += "\"";
+  ann += kAssume;
+  ann += "\":\"true\",\"";
+  ann += kAssumeTime;
+  ann += "\":\"";
+  ann += ts;
+  ann += "\"}";
+  const std::string patch = "{\"metadata\":{\"annotations\":" + ann + ",\"labels\":{\"" + kAssume + "\":\"true\"}}}";
+  std::string b = "{\"apiVersion\":\"v1\",\"kind\":\"Binding\",\"metadata\":{\"name\":";
+  json::append_quoted(&b, j.name);
+  b += ",\"namespace\":";
+  json::append_quoted(&b, j.ns);
+  b += ",\"uid\":";
+  json::append_quoted(&b, j.uid);
+  b += ",\"annotations\":" + ann + "},\"target\":{\"apiVersion\":\"v1\",\"kind\":\"Node\",\"name\":";
+  json::append_quoted(&b, j.node);
+  b += "}}";
   const uint64_t t1 = now_ns();
-  int st = call(c, "PATCH", base, kMergePatch, patch, &resp, true);
+  const std::string a = auth();
+  std::string rp, rb;
+  c->start("PATCH", base, kMergePatch, patch, a);
+  c2->start("POST", base + "/binding", kJson, b, a);
+  int sb = c2->finish(&rb);
+  int sp = c->finish(&rp);
   const uint64_t t2 = now_ns();
-  stats.patch_ns.fetch_add(t2 - t1, std::memory_order_relaxed);
-  if (st < 200 || st >= 300) {
-    err = api_error(st, resp);
-  } else {
-    // 2. the binding
-    std::string b = "{\"apiVersion\":\"v1\",\"kind\":\"Binding\",\"metadata\":{\"name\":";
-    json::append_quoted(&b, j.name);
-    b += ",\"namespace\":";
-    json::append_quoted(&b, j.ns);
-    b += ",\"uid\":";
-    json::append_quoted(&b, j.uid);
-    b += "},\"target\":{\"apiVersion\":\"v1\",\"kind\":\"Node\",\"name\":";
-    json::append_quoted(&b, j.node);
-    b += "}}";
-    st = call(c, "POST", base + "/binding", kJson, b, &resp, true);
-    stats.binding_ns.fetch_add(now_ns() - t2, std::memory_order_relaxed);
-    if (st == 409) {
-      // a retried POST whose first attempt landed: already on this node is success
-      std::string got;
-      const int gs = call(c, "GET", base, kJson, std::string(), &got, true);
-      if (gs == 200 && pod_node(got) == j.node) st = 201;
-    }
-    if (st < 200 || st >= 300) err = api_error(st, resp);
+  stats.binding_ns.fetch_add(t2 - t1, std::memory_order_relaxed);   // the pair, in flight together
+  auto transient = [](int st) { return st == 0 || st == 401 || st == 429 || st >= 500; };
+  if (transient(sb)) sb = call(c2, "POST", base + "/binding", kJson, b, &rb, true);
+  if (sb == 409) {
+    // a retried POST whose first attempt landed: already on this node is success
+    std::string got;
+    const int gs = call(c2, "GET", base, kJson, std::string(), &got, true);
+    if (gs == 200 && pod_node(got) == j.node) sb = 201;
+  }
+  if (sb < 200 || sb >= 300) {
+    err = api_error(sb, rb);
+  } else if (sp < 200 || sp >= 300) {
+    // bound, with its annotations (they came with the binding): only the label is missing
+    const uint64_t t3 = now_ns();
+    if (transient(sp)) sp = call(c, "PATCH", base, kMergePatch, patch, &rp, true);
+    stats.patch_ns.fetch_add(now_ns() - t3, std::memory_order_relaxed);
+    if (sp < 200 || sp >= 300) stats.label_failures.fetch_add(1, std::memory_order_relaxed);
   }
   if (err.empty()) {
     ledger_->commit(j.uid);
@@ -473,7 +501,7 @@ void KubeWriter::process(HttpConn* c, BindJob& j) {
     un += "\":null}}}";
     std::string ignored;
     call(c, "PATCH", base, kMergePatch, un, &ignored, false);
-    if (events_ && st > 0) {
+    if (events_ && sb > 0) {
       char tbuf[32];
       const std::time_t now = std::time(nullptr);
       std::tm g{};
@@ -508,7 +536,7 @@ void KubeWriter::process(HttpConn* c, BindJob& j) {
 }
 
 void KubeWriter::run() {
-  HttpConn c(&t_, ctx_);
+  HttpConn c(&t_, ctx_), c2(&t_, ctx_);
   for (;;) {
     BindJob j;
     {
@@ -518,7 +546,7 @@ void KubeWriter::run() {
       j = std::move(q_.front());
       q_.pop_front();
     }
-    process(&c, j);
+    process(&c, &c2, j);
     stats.inflight.fetch_sub(1, std::memory_order_relaxed);
   }
 }

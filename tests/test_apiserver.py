@@ -75,9 +75,11 @@ def test_pod_lifecycle_codes_and_bodies(kind):
         with pytest.raises(ApiError) as e:
             await api.bind_pod("ns1", "a", m["uid"], "nope")
         assert e.value.status == 404
-        await api.bind_pod("ns1", "a", m["uid"], "n0")
+        await api.bind_pod("ns1", "a", m["uid"], "n0", annotations={"nano-gpu/container-main": "3", "l": "v2"})
         got = await api.get_pod("ns1", "a")
         assert got["spec"]["nodeName"] == "n0" and got["status"]["phase"] == "Running"
+        # the Binding's annotations land with the node (kube-apiserver setPodHostAndAnnotations)
+        assert got["metadata"]["annotations"]["nano-gpu/container-main"] == "3"
         with pytest.raises(ApiError) as e:
             await api.bind_pod("ns1", "a", m["uid"], "n0")
         assert e.value.status == 409 and "already assigned" in e.value.message

@@ -116,8 +116,8 @@ def test_binding_conflict_on_the_same_node_is_success(native):
             p = store.create_pod(pu.make_pod("a", [("main", 30)]))
             orig = store.bind_pod
 
-            def bind_then_conflict(ns, name, uid, node):
-                orig(ns, name, uid, node)
+            def bind_then_conflict(ns, name, uid, node, annotations=None):
+                orig(ns, name, uid, node, annotations)
                 raise ApiError(409, "already assigned", "Conflict")
 
             store.bind_pod = bind_then_conflict
