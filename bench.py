@@ -344,7 +344,7 @@ def apiserver_main(conn) -> None:
             if srv is not None:
                 srv.stop()
             steps.clear()
-            srv = core().ApiServer("127.0.0.1", 0, msg[1], 1 << 20)
+            srv = core().ApiServer("127.0.0.1", 0, msg[1], 1 << 16)   # watch cache: 64k events per kind
             srv.set_latency(msg[2])
             conn.send(srv.port)
         elif op == "nodes":
