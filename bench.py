@@ -77,7 +77,8 @@ def parse_args():
                          "rank's extender talks REST to, with only rank 0 running the pod controller")
     ap.add_argument("--inproc-variant-steps", type=int, default=3,
                     help="after the timed steps, a pass with --inproc-api (0: none)")
-    ap.add_argument("--apiserver-threads", type=int, default=4, help="shared API server IO threads")
+    ap.add_argument("--apiserver-threads", type=int, default=0,
+                    help="shared API server IO threads (0: one per rank, 4 to 16)")
     ap.add_argument("--bind-writer-threads", type=int, default=0,
                     help="extender's native bind writers per rank (0: 128 split over the ranks, at least 16)")
     ap.add_argument("--inflight-binds", type=int, default=64)
@@ -513,7 +514,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         url = None
         if d.rank == 0:
             apisrv = api_proc
-            url = apisrv.start(args.apiserver_threads, args.api_rtt_ms / 1e3)
+            url = apisrv.start(args.apiserver_threads or min(16, max(4, d.world)), args.api_rtt_ms / 1e3)
             apisrv.add_nodes(nodes)
         url = d.bcast_obj(url)
         from nanogpu.k8s.client import KubeClient, KubeConfig
@@ -812,7 +813,7 @@ def main() -> int:
                        # (default), or --inproc-api's per-rank in-process store (value_inproc_api)
                        "api_server": ("in-process store per rank, extender-isolated" if args.inproc_api else
                                       f"one native HTTP API server for all ranks, own process "
-                                      f"({args.apiserver_threads} IO threads), REST + watch"),
+                                      f"({args.apiserver_threads or min(16, max(4, d.world))} IO threads), REST + watch"),
                        "cpus_rank0": _cpulist(cpus),
                        "frontend": f"{args.frontend_threads} threads, busy-poll {args.busy_poll_us} us"},
             # POST /scheduler/bind wall time as kube-scheduler's stand-in sees it (request
