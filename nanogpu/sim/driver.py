@@ -234,6 +234,8 @@ class DriverStats:
                 "cycle_sum_ms": 1e3 * self.cycle_sum_s,
                 "cycle_wire_ms": 1e3 * self.cycle_wire_s,
                 "e2e_p50_ms": 1e3 * (statistics.median(self.e2e_latencies) if self.e2e_latencies else 0.0),
+                # the burst's window on the monotonic clock (comparable across processes of a node)
+                "t_first_filter": self.t_first_filter, "t_last_bind": self.t_last_bind,
                 # every POST /scheduler/bind as the scheduler saw it (request written -> reply read)
                 "bind_ms_all": [round(1e3 * x, 4) for x in self.bind_latencies]}
 
