@@ -80,7 +80,8 @@ def parse_args():
     ap.add_argument("--apiserver-threads", type=int, default=0,
                     help="shared API server IO threads (0: one per rank, 4 to 16)")
     ap.add_argument("--bind-writer-threads", type=int, default=0,
-                    help="extender's native bind writers per rank (0: 128 split over the ranks, at least 16)")
+                    help="extender's native bind writer threads per rank, 8 binds in flight each "
+                         "(0: 16 split over the ranks, at least 2)")
     ap.add_argument("--inflight-binds", type=int, default=64)
     ap.add_argument("--no-gpu", action="store_true", help="skip GPU discovery (CPU-only rehearsal)")
     ap.add_argument("--json-out", default="")
@@ -531,7 +532,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                  policy_config_path="/nonexistent/policy.yaml", reservation_ttl_s=3600,
                  busy_poll_us=args.busy_poll_us, frontend_threads=args.frontend_threads,
                  nominate=not args.no_nominate,
-                 bind_writer_threads=args.bind_writer_threads or max(16, 128 // d.world))
+                 bind_writer_threads=args.bind_writer_threads or max(2, 16 // d.world))
     all_steps_pre = [10_000 + w for w in range(args.warmup)] + list(range(args.steps))
     rt = Runtime(cfg, worker=d.rank if shared else 0, api=rt_api)
     await rt.start()

@@ -47,7 +47,7 @@ class Config:
     max_pods: int = 131072
     verify_pod_on_bind: bool = False
     native_bind_writes: bool = True             # C++ writer threads do the bind's API writes
-    bind_writer_threads: int = 128
+    bind_writer_threads: int = 16               # x KubeWriter::kBatch (8) binds in flight
     reservation_ttl_s: float = 60.0
     nominate: bool = True              # priorities nominate the top node (Ledger::nominate)
     nomination_ttl_s: float = 5.0

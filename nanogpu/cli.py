@@ -58,8 +58,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--native-bind-writes", action=argparse.BooleanOptionalAction, default=True,
                    help="the native front door's C++ threads do each bind's PATCH + binding POST + commit "
                         "(native/src/kubewriter.cpp); --no-native-bind-writes keeps them in Python")
-    p.add_argument("--bind-writer-threads", type=int, default=128,
-                   help="native bind writers: concurrent binds in flight to kube-apiserver")
+    p.add_argument("--bind-writer-threads", type=int, default=16,
+                   help="native bind writer threads; each pipelines up to 8 binds (16 x 8 = 128 in flight)")
     p.add_argument("--reservation-ttl", default="60s")
     p.add_argument("--no-nominate", action="store_true",
                    help="priorities do not tentatively reserve the top-scored node")

@@ -92,8 +92,13 @@ class KubeWriter {
   KubeWriterStats stats;
 
  private:
+  // binds one writer thread pipelines together (two connections each)
+  static constexpr int kBatch = 8;
   void run();
-  void process(HttpConn* c, HttpConn* c2, BindJob& j);
+  void build(BindJob& j, std::string* patch, std::string* binding);
+  void process_batch(std::vector<BindJob>& jobs, std::vector<std::unique_ptr<HttpConn>>& conns);
+  void finish(HttpConn* c, HttpConn* c2, BindJob& j, const std::string& patch, const std::string& binding, int sp,
+              std::string* rp, int sb, std::string* rb);
   void refuse(BindJob& j);
   int call(HttpConn* c, const char* method, const std::string& path, const std::string& ctype,
            const std::string& body, std::string* resp, bool retry);

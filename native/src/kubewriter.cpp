@@ -417,12 +417,11 @@ int KubeWriter::call(HttpConn* c, const char* method, const std::string& path, c
   }
 }
 
-void KubeWriter::process(HttpConn* c, HttpConn* c2, BindJob& j) {
-  const std::string base = "/api/v1/namespaces/" + j.ns + "/pods/" + j.name;
-  std::string err;
-  // placement annotations (pu.placement_patch_names): the Binding carries them, so they land
-  // on the pod atomically with spec.nodeName (kube-apiserver setPodHostAndAnnotations); the
-  // PATCH, sent at the same time on a second connection, adds the assume label
+// The two request bodies of one bind. Placement annotations (pu.placement_patch_names): the
+// Binding carries them, so they land on the pod atomically with spec.nodeName (kube-apiserver
+// setPodHostAndAnnotations); the PATCH, in flight at the same time on a second connection,
+// adds the assume label.
+void KubeWriter::build(BindJob& j, std::string* patch, std::string* binding) {
   std::string ann = "{";
   for (size_t k = 0; k < j.containers.size() && k < j.plan.size(); ++k) {
     json::append_quoted(&ann, kContainerPrefix + j.containers[k]);
@@ -442,8 +441,9 @@ void KubeWriter::process(HttpConn* c, HttpConn* c2, BindJob& j) {
   ann += "\":\"";
   ann += ts;
   ann += "\"}";
-  const std::string patch = "{\"metadata\":{\"annotations\":" + ann + ",\"labels\":{\"" + kAssume + "\":\"true\"}}}";
-  std::string b = "{\"apiVersion\":\"v1\",\"kind\":\"Binding\",\"metadata\":{\"name\":";
+  *patch = "{\"metadata\":{\"annotations\":" + ann + ",\"labels\":{\"" + kAssume + "\":\"true\"}}}";
+  std::string& b = *binding;
+  b = "{\"apiVersion\":\"v1\",\"kind\":\"Binding\",\"metadata\":{\"name\":";
   json::append_quoted(&b, j.name);
   b += ",\"namespace\":";
   json::append_quoted(&b, j.ns);
@@ -452,17 +452,39 @@ void KubeWriter::process(HttpConn* c, HttpConn* c2, BindJob& j) {
   b += ",\"annotations\":" + ann + "},\"target\":{\"apiVersion\":\"v1\",\"kind\":\"Node\",\"name\":";
   json::append_quoted(&b, j.node);
   b += "}}";
-  const uint64_t t1 = now_ns();
+}
+
+// A batch of binds taken together: every bind's PATCH and binding are sent first (two
+// connections per bind), then the answers are read and each bind is finished in turn.
+void KubeWriter::process_batch(std::vector<BindJob>& jobs, std::vector<std::unique_ptr<HttpConn>>& conns) {
+  const size_t n = jobs.size();
+  std::vector<std::string> patch(n), binding(n), rp(n), rb(n);
+  std::vector<int> sp(n), sb(n);
   const std::string a = auth();
-  std::string rp, rb;
-  c->start("PATCH", base, kMergePatch, patch, a);
-  c2->start("POST", base + "/binding", kJson, b, a);
-  int sb = c2->finish(&rb);
-  int sp = c->finish(&rp);
-  const uint64_t t2 = now_ns();
-  stats.binding_ns.fetch_add(t2 - t1, std::memory_order_relaxed);   // the pair, in flight together
+  const uint64_t t1 = now_ns();
+  for (size_t i = 0; i < n; ++i) {
+    build(jobs[i], &patch[i], &binding[i]);
+    const std::string base = "/api/v1/namespaces/" + jobs[i].ns + "/pods/" + jobs[i].name;
+    conns[2 * i]->start("PATCH", base, kMergePatch, patch[i], a);
+    conns[2 * i + 1]->start("POST", base + "/binding", kJson, binding[i], a);
+  }
+  for (size_t i = 0; i < n; ++i) {
+    sb[i] = conns[2 * i + 1]->finish(&rb[i]);
+    sp[i] = conns[2 * i]->finish(&rp[i]);
+  }
+  stats.binding_ns.fetch_add(now_ns() - t1, std::memory_order_relaxed);   // the pairs, in flight together
+  for (size_t i = 0; i < n; ++i) {
+    finish(conns[2 * i].get(), conns[2 * i + 1].get(), jobs[i], patch[i], binding[i], sp[i], &rp[i], sb[i], &rb[i]);
+    stats.inflight.fetch_sub(1, std::memory_order_relaxed);
+  }
+}
+
+void KubeWriter::finish(HttpConn* c, HttpConn* c2, BindJob& j, const std::string& patch, const std::string& b,
+                        int sp, std::string* rp, int sb, std::string* rb) {
+  const std::string base = "/api/v1/namespaces/" + j.ns + "/pods/" + j.name;
+  std::string err;
   auto transient = [](int st) { return st == 0 || st == 401 || st == 429 || st >= 500; };
-  if (transient(sb)) sb = call(c2, "POST", base + "/binding", kJson, b, &rb, true);
+  if (transient(sb)) sb = call(c2, "POST", base + "/binding", kJson, b, rb, true);
   if (sb == 409) {
     // a retried POST whose first attempt landed: already on this node is success
     std::string got;
@@ -470,11 +492,11 @@ void KubeWriter::process(HttpConn* c, HttpConn* c2, BindJob& j) {
     if (gs == 200 && pod_node(got) == j.node) sb = 201;
   }
   if (sb < 200 || sb >= 300) {
-    err = api_error(sb, rb);
+    err = api_error(sb, *rb);
   } else if (sp < 200 || sp >= 300) {
     // bound, with its annotations (they came with the binding): only the label is missing
     const uint64_t t3 = now_ns();
-    if (transient(sp)) sp = call(c, "PATCH", base, kMergePatch, patch, &rp, true);
+    if (transient(sp)) sp = call(c, "PATCH", base, kMergePatch, patch, rp, true);
     stats.patch_ns.fetch_add(now_ns() - t3, std::memory_order_relaxed);
     if (sp < 200 || sp >= 300) stats.label_failures.fetch_add(1, std::memory_order_relaxed);
   }
@@ -490,8 +512,8 @@ void KubeWriter::process(HttpConn* c, HttpConn* c2, BindJob& j) {
     ledger_->release(j.uid);
     stats.rollbacks.fetch_add(1, std::memory_order_relaxed);
     std::string un = "{\"metadata\":{\"annotations\":{";
-    for (const std::string& n : j.containers) {
-      json::append_quoted(&un, kContainerPrefix + n);
+    for (const std::string& nm : j.containers) {
+      json::append_quoted(&un, kContainerPrefix + nm);
       un += ":null,";
     }
     un += "\"";
@@ -536,18 +558,21 @@ void KubeWriter::process(HttpConn* c, HttpConn* c2, BindJob& j) {
 }
 
 void KubeWriter::run() {
-  HttpConn c(&t_, ctx_), c2(&t_, ctx_);
+  std::vector<std::unique_ptr<HttpConn>> conns;
+  for (int i = 0; i < 2 * kBatch; ++i) conns.push_back(std::make_unique<HttpConn>(&t_, ctx_));
+  std::vector<BindJob> jobs;
   for (;;) {
-    BindJob j;
+    jobs.clear();
     {
       std::unique_lock<std::mutex> g(mu_);
       cv_.wait(g, [this] { return stop_ || !q_.empty(); });
       if (stop_) return;
-      j = std::move(q_.front());
-      q_.pop_front();
+      while (!q_.empty() && static_cast<int>(jobs.size()) < kBatch) {
+        jobs.push_back(std::move(q_.front()));
+        q_.pop_front();
+      }
     }
-    process(&c, &c2, j);
-    stats.inflight.fetch_sub(1, std::memory_order_relaxed);
+    process_batch(jobs, conns);
   }
 }
 
