@@ -113,6 +113,10 @@ def render(topo, plugin=None, render_minors: list[int] | None = None, sysfs_root
     family("nanogpu_container_gpu_percent", "gauge", "gpu-percent of the device granted to the container", rows_p)
     family("nanogpu_container_cus", "gauge", "compute units the container may use on the device", rows_c)
     family("nanogpu_container_hbm_budget_bytes", "gauge", "HBM budget of the container on the device", rows_m)
+    if plugin is not None:
+        family("nanogpu_plugin_id_mismatches_total", "counter",
+               "Allocate calls whose kubelet IDs named another device than the container's placement",
+               [("", plugin.id_mismatches)])
     return "\n".join(out) + "\n"
 
 

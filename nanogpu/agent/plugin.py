@@ -65,7 +65,7 @@ class Matcher:
         pods, _ = await self.api.list_pods(field_selector=f"{T.NODE_NAME_FIELD}={self.node}")
         return [p for p in pods if pu.is_assumed(p) and not pu.is_completed(p)]
 
-    async def match(self, percent: int) -> tuple[dict, dict] | None:
+    async def match(self, percent: int, claim: bool = True) -> tuple[dict, dict] | None:
         """The container kubelet is admitting: kubelet admits pods in the order they reach the
         node (bind order; HandlePodAdditions sorts one batch by creation time) and allocates
         a pod's containers in spec order. So: the first not-yet-allocated container asking
@@ -87,7 +87,8 @@ class Matcher:
                 break
         if best is None:
             return None
-        self.claimed[(pu.pod_uid(best[1]), best[2].get("name", ""))] = time.time()
+        if claim:
+            self.claimed[(pu.pod_uid(best[1]), best[2].get("name", ""))] = time.time()
         return best[1], best[2]
 
 
@@ -115,6 +116,7 @@ class NanoGpuPlugin:
         self._changed = asyncio.Event()
         # live grants by (pod uid, container): what the agent's /metrics reports per container
         self.grants: dict[tuple[str, str], Assignment] = {}
+        self.id_mismatches = 0   # Allocate IDs on another device than the placement (see Allocate)
 
     # ---------------------------------------------------------------- restart rebuild
     async def rebuild(self, pods: list[dict] | None = None) -> int:
@@ -177,14 +179,24 @@ class NanoGpuPlugin:
             yield self._device_list()
 
     async def GetPreferredAllocation(self, request, context):
-        """Prefers IDs of one device, so kubelet's own accounting mirrors a real share."""
+        """Prefers IDs of the device the container about to be admitted was placed on (the
+        Matcher's next pick for this size, not yet claimed), else of one device: kubelet's
+        own per-ID accounting then mirrors the real share, and Allocate can check that the
+        IDs it is handed name the device it answers with (`id_mismatches`)."""
         resp = D.PreferredAllocationResponse()
         for cr in request.container_requests:
             by_dev: dict[str, list[str]] = {}
             for vid in cr.available_deviceIDs:
                 by_dev.setdefault(vid.split("-")[0], []).append(vid)
             chosen = list(cr.must_include_deviceIDs)
+            nxt = await self.matcher.match(cr.allocation_size, claim=False)
+            idx = pu.container_assignment(nxt[0], nxt[1].get("name", "")) if nxt else None
+            want = by_dev.get(f"d{idx[0]}") if idx and len(idx) == 1 and idx[0] >= 0 else None
+            if want and len(want) >= cr.allocation_size - len(chosen):
+                chosen += [i for i in want if i not in chosen][:cr.allocation_size - len(chosen)]
             for ids in sorted(by_dev.values(), key=len):
+                if len(chosen) >= cr.allocation_size:
+                    break
                 if len(ids) >= cr.allocation_size - len(chosen):
                     chosen += [i for i in ids if i not in chosen][:cr.allocation_size - len(chosen)]
                     break
@@ -209,6 +221,13 @@ class NanoGpuPlugin:
                     await context.abort(_grpc_status("FAILED_PRECONDITION"), msg)
                 raise RuntimeError(msg)
             pod, c = m
+            idx = pu.container_assignment(pod, c.get("name", "")) or []
+            got = {vid.split("-")[0] for vid in cr.devices_ids}
+            if len(idx) == 1 and idx[0] >= 0 and got != {f"d{idx[0]}"}:
+                # kubelet did not take our preferred IDs (or admitted out of order): the answer
+                # still follows the placement; counted so an operator can see it happen
+                self.id_mismatches += 1
+                log.info("Allocate: IDs on %s for a container placed on device %d", sorted(got), idx[0])
             resp.container_responses.append(await self._container_response(pod, c, percent))
         return resp
 

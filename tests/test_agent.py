@@ -128,6 +128,11 @@ def test_device_plugin_end_to_end(tmp_path):
                 D.ContainerPreferredAllocationRequest(available_deviceIDs=[f"d1-{k}" for k in range(50)] +
                                                       [f"d2-{k}" for k in range(100)], allocation_size=30)]))
             assert {i.split("-")[0] for i in pref.container_responses[0].deviceIDs} == {"d1"}
+            # with the placed device among the free IDs, the preference names it ("a": 20 % on 0)
+            pref = await stub.GetPreferredAllocation(D.PreferredAllocationRequest(container_requests=[
+                D.ContainerPreferredAllocationRequest(available_deviceIDs=[f"d1-{k}" for k in range(100)] +
+                                                      [f"d0-{k}" for k in range(100)], allocation_size=20)]))
+            assert {i.split("-")[0] for i in pref.container_responses[0].deviceIDs} == {"d0"}
 
             ra = await stub.Allocate(D.AllocateRequest(container_requests=[
                 D.ContainerAllocateRequest(devices_ids=[f"d5-{k}" for k in range(20)])]))
@@ -148,6 +153,7 @@ def test_device_plugin_end_to_end(tmp_path):
                 await stub.Allocate(D.AllocateRequest(container_requests=[
                     D.ContainerAllocateRequest(devices_ids=["d0-1"] * 7)]))
             assert ei.value.code() == grpc.StatusCode.FAILED_PRECONDITION
+            assert agent.plugin.id_mismatches == 3      # the IDs above were not the preferred ones
             stream.cancel()
         # pod / container level monitoring: the grants, joined with the devices
         text = render_metrics(topo, agent.plugin, agent.render_minors(), str(tmp_path / "nosys"))
@@ -215,6 +221,8 @@ def test_same_percent_pods_get_their_own_devices(tmp_path):
                 spec = await kl.admit(p)
                 assert spec["main"]["envs"]["NANO_GPU_DEVICES"] == ",".join(
                     map(str, pu.container_assignment(p, "main"))), pu.meta(p)["name"]
+            # kubelet took the preferred IDs: each container's IDs name its own device
+            assert agent.plugin.id_mismatches == 0
             # the CU-mask annotation landed on the pod the grant was made for
             for p in bound:
                 cur = store.get_pod("default", pu.meta(p)["name"])
