@@ -83,6 +83,9 @@ def parse_args():
                     help="extender's native bind writer threads per rank, 8 binds in flight each "
                          "(0: 16 split over the ranks, at least 2)")
     ap.add_argument("--inflight-binds", type=int, default=64)
+    ap.add_argument("--no-overlap-create", action="store_true",
+                    help="create the next burst only after this one is released (by default the "
+                         "workload's clients create it while the pod controller releases)")
     ap.add_argument("--no-gpu", action="store_true", help="skip GPU discovery (CPU-only rehearsal)")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--profile-out", default="", help="cProfile the timed steps (rank 0) into this file")
@@ -339,6 +342,7 @@ def apiserver_main(conn) -> None:
     affinity.apply(affinity.pick_cpus())
     srv = None
     steps: dict = {}
+    keys: dict = {}   # the clients know their pods' names: keyed at load, not per delete
     while True:
         msg = conn.recv()
         op = msg[0]
@@ -346,6 +350,7 @@ def apiserver_main(conn) -> None:
             if srv is not None:
                 srv.stop()
             steps.clear()
+            keys.clear()
             srv = core().ApiServer("127.0.0.1", 0, msg[1], 1 << 16)   # watch cache: 64k events per kind
             srv.set_latency(msg[2])
             conn.send(srv.port)
@@ -355,16 +360,22 @@ def apiserver_main(conn) -> None:
             conn.send(len(msg[1]))
         elif op == "load":
             steps[msg[1]] = msg[2]
+            keys[msg[1]] = [(m.get("namespace", "default"), m["name"])
+                            for m in (_json.loads(t)["metadata"] for t in msg[2])]
             conn.send(True)
         elif op == "create":
+            t = time.perf_counter()
             codes = srv.create_pods(steps[msg[1]])
-            conn.send(sum(1 for c in codes if c == 201))
+            conn.send((sum(1 for c in codes if c == 201), time.perf_counter() - t))
+            if os.environ.get("NANOGPU_BENCH_DEBUG"):
+                print(f"create {msg[1]} {t:.4f} -> {time.perf_counter():.4f}", file=sys.stderr)
         elif op == "delete":
-            keys = []
-            for t in steps.pop(msg[1]):
-                m = _json.loads(t)["metadata"]
-                keys.append((m.get("namespace", "default"), m["name"]))
-            conn.send(srv.delete_pods(keys))
+            steps.pop(msg[1], None)
+            t = time.perf_counter()
+            n = srv.delete_pods(keys.pop(msg[1]))
+            conn.send((n, time.perf_counter() - t))
+            if os.environ.get("NANOGPU_BENCH_DEBUG"):
+                print(f"delete {msg[1]} {t:.4f} -> {time.perf_counter():.4f}", file=sys.stderr)
         elif op == "stats":
             conn.send(_json.loads(srv.stats()))
         elif op == "end":            # the pass is over
@@ -406,10 +417,13 @@ class ApiServerProc:
     def load(self, step: int, pods: list[dict]) -> None:
         self._rpc("load", step, [json.dumps(p, separators=(",", ":")) for p in pods])
 
-    def create(self, step: int) -> int:
+    def create(self, step: int) -> tuple[int, float]:
+        """(pods created, seconds the server spent on them)"""
+        if os.environ.get("NANOGPU_BENCH_DEBUG"):
+            print(f"rpc-create {step} {time.perf_counter():.4f}", file=sys.stderr)
         return self._rpc("create", step)
 
-    def delete(self, step: int) -> int:
+    def delete(self, step: int) -> tuple[int, float]:
         return self._rpc("delete", step)
 
     def stats(self) -> dict:
@@ -558,7 +572,15 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                    "steps": [10_000 + w for w in range(args.warmup)] + list(range(args.steps))})
         await loop.run_in_executor(None, conn.recv)   # the stand-in has built its pods
 
-    async def one_step(step: int, timed: bool) -> dict:
+    # The workload's clients create the next burst while the pod controller releases this one
+    # (delete, then create, in the API server; the scheduling of the next burst still starts
+    # only after every release). Each timed step's create and release stay inside the clock:
+    # the first timed burst is created in the timed region, never during a warm-up release.
+    overlap = apisrv is not None and not getattr(args, "no_overlap_create", False)
+    created: dict = {}       # step -> its create, started during the previous step's release
+    srv_ms: dict = {}        # step -> the API server's own create/delete time
+
+    async def one_step(step: int, timed: bool, nxt: int | None = None) -> dict:
         pods = bursts.pop(step)
         t_step0 = tc = time.perf_counter()
         if conn is not None:
@@ -572,7 +594,9 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                     for p in pods:
                         await api.create_pod(p)
             elif apisrv is not None:
-                await loop.run_in_executor(None, apisrv.create, step)   # every rank's pods
+                fut = created.pop(step, None)   # every rank's pods
+                n_c, dt_c = await (fut if fut is not None else loop.run_in_executor(None, apisrv.create, step))
+                srv_ms.setdefault(step, {})["create_srv_ms"] = 1e3 * dt_c
             tc = time.perf_counter() - tc
             if shared:
                 await barrier()                     # every rank's pods exist
@@ -598,7 +622,12 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                 except Exception:
                     pass
         elif apisrv is not None:
-            await loop.run_in_executor(None, apisrv.delete, step)
+            n_d, dt_d = await loop.run_in_executor(None, apisrv.delete, step)
+            srv_ms.setdefault(step, {})["delete_srv_ms"] = 1e3 * dt_d
+            if overlap and nxt is not None:
+                if os.environ.get("NANOGPU_BENCH_DEBUG"):
+                    print(f"submit {nxt} {time.perf_counter():.4f}", file=sys.stderr)
+                created[nxt] = loop.run_in_executor(None, apisrv.create, nxt)
         # the pod controller releases on DELETED; wait until our shares are gone
         # (the in-process watch delivers the DELETED events on the next loop iterations: yield
         # first, and only then back off to short sleeps)
@@ -611,8 +640,11 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
             await asyncio.sleep(0 if i < 50 else 0.0005)
         if pod_ctrl is not None:
             await pod_ctrl.queue.drain(5.0)
+        if os.environ.get("NANOGPU_BENCH_DEBUG"):
+            print(f"step {step} start {t_step0:.4f} release {ts:.4f} end {time.perf_counter():.4f}", file=sys.stderr)
         phases = {"create_ms": 1e3 * tc, "schedule_ms": 1e3 * summary["span_s"],
                   "release_ms": 1e3 * (time.perf_counter() - ts)}
+        phases.update(srv_ms.pop(step, {}))
         walls = rt.native.fe.take_bind_wall() if rt.native is not None else []
         client_ms = summary.pop("bind_ms_all", [])
         if timed:
@@ -621,6 +653,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
             diag = {"t0": round(t_step0, 4), "t1": round(time.perf_counter(), 4)}
             diag.update({k: round(summary.get(k, 0.0), 2) for k in ("cycle_max_ms", "cycle_sum_ms", "cycle_wire_ms", "bind_max_ms")})
             diag["unschedulable"] = summary.get("unschedulable_attempts", 0)
+            diag.update({k: round(v, 2) for k, v in phases.items() if k != "schedule_ms"})
             if rt.native is not None:
                 fs = rt.native.fe.stats()
                 diag["fe_loop_max_ms"] = round(1e3 * fs["loop_max_s"], 2)
@@ -655,7 +688,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
 
     gc.callbacks.append(on_gc)
     for w in range(args.warmup):
-        await one_step(10_000 + w, False)
+        await one_step(10_000 + w, False, 10_000 + w + 1 if w + 1 < args.warmup else None)
     rt.tracer.buf.clear()
     await barrier()
     d.sync()
@@ -672,7 +705,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     if sampler is not None:
         sampler.on.set()
     for s in range(args.steps):
-        r = await one_step(s, True)
+        r = await one_step(s, True, s + 1 if s + 1 < args.steps else None)
         results["steps"].append(r["stats"])
         results["frag"].append(r["frag"])
         results.setdefault("phases", []).append(r["phases"])
@@ -706,7 +739,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         results["native"] = {v: round(1e6 * ns[v]["seconds_total"] / max(1, ns[v]["count"]), 2)
                              for v in ("filter", "priorities")}
     results["phase_ms"] = {k: round(statistics.mean(p[k] for p in results["phases"]), 2)
-                           for k in ("create_ms", "schedule_ms", "release_ms")} if results.get("phases") else None
+                           for k in ("create_ms", "schedule_ms", "release_ms", "create_srv_ms", "delete_srv_ms")
+                           if all(k in p for p in results["phases"])} if results.get("phases") else None
     results["schedule_ms_steps"] = [round(p["schedule_ms"], 1) for p in results.get("phases", [])]
     results["step_diag"] = results.get("diag", [])
     results["failed"] = sum(s["failed"] for s in results["steps"])
@@ -816,6 +850,8 @@ def main() -> int:
                                       f"one native HTTP API server for all ranks, own process "
                                       f"({args.apiserver_threads or min(16, max(4, d.world))} IO threads), REST + watch"),
                        "cpus_rank0": _cpulist(cpus),
+                       # next burst created by the clients while this one is released
+                       "create_overlaps_release": not (args.inproc_api or args.no_overlap_create),
                        "frontend": f"{args.frontend_threads} threads, busy-poll {args.busy_poll_us} us"},
             # POST /scheduler/bind wall time as kube-scheduler's stand-in sees it (request
             # written -> reply read), over every bind of the timed steps on all ranks

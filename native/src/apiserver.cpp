@@ -148,11 +148,17 @@ namespace {
 std::string str_of(const JV* v) { return v && v->t == JV::T::kStr ? v->s : std::string(); }
 
 std::string now_rfc3339() {
+  // one-second resolution: formatted once per second per thread (a bulk create stamps
+  // thousands of pods within the same second)
+  thread_local std::time_t last = -1;
+  thread_local char buf[32];
   const std::time_t t = std::time(nullptr);
-  std::tm g{};
-  gmtime_r(&t, &g);
-  char buf[32];
-  std::strftime(buf, sizeof buf, "%Y-%m-%dT%H:%M:%SZ", &g);
+  if (t != last) {
+    std::tm g{};
+    gmtime_r(&t, &g);
+    std::strftime(buf, sizeof buf, "%Y-%m-%dT%H:%M:%SZ", &g);
+    last = t;
+  }
   return buf;
 }
 
@@ -360,6 +366,7 @@ struct Selector {
     return out;
   }
   bool labels_match(const Obj& o) const {
+    if (terms.empty()) return true;   // no selector: never build the object's tree for it
     const JV* l = o.labels();
     for (const Term& t : terms) {
       const JV* v = l ? l->get(t.k) : nullptr;
@@ -478,6 +485,8 @@ struct Server::Impl {
   std::vector<Watch> watches;
   std::atomic<uint64_t> n_create{0}, n_get{0}, n_patch{0}, n_bind{0}, n_delete{0}, n_list{0}, n_watch{0},
       n_events{0}, n_requests{0}, n_lease{0};
+  // bulk create/delete phases (steady ns): parse outside the lock, store + emit under it
+  std::atomic<uint64_t> bulk_parse_ns{0}, bulk_insert_ns{0}, bulk_delete_ns{0};
   uint64_t bindings = 0;
 
   static std::string key(std::string_view ns, std::string_view name) {
@@ -1320,6 +1329,7 @@ std::pair<int, std::string> Server::call(std::string_view method, std::string_vi
 }
 
 std::vector<int> Server::create_pods(const std::vector<std::string>& texts) {
+  const auto t0 = std::chrono::steady_clock::now();
   std::vector<FastCreate> fast(texts.size());
   std::vector<JV> vs(texts.size());
   std::vector<int> codes(texts.size(), 201);
@@ -1337,6 +1347,7 @@ std::vector<int> Server::create_pods(const std::vector<std::string>& texts) {
     pool.emplace_back(parse_range, std::min(texts.size(), w * per), std::min(texts.size(), (w + 1) * per));
   parse_range(0, std::min(texts.size(), per));
   for (auto& t : pool) t.join();
+  const auto t1 = std::chrono::steady_clock::now();
   std::lock_guard<std::mutex> g(impl_->mu);
   for (size_t i = 0; i < texts.size(); ++i) {
     if (codes[i] != 201) continue;
@@ -1348,14 +1359,22 @@ std::vector<int> Server::create_pods(const std::vector<std::string>& texts) {
       codes[i] = e.code;
     }
   }
+  const auto t2 = std::chrono::steady_clock::now();
+  auto ns = [](auto d) { return static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(d).count()); };
+  impl_->bulk_parse_ns.fetch_add(ns(t1 - t0), std::memory_order_relaxed);
+  impl_->bulk_insert_ns.fetch_add(ns(t2 - t1), std::memory_order_relaxed);
   return codes;
 }
 
 int Server::delete_pods(const std::vector<std::pair<std::string, std::string>>& keys) {
   int n = 0;
+  const auto t0 = std::chrono::steady_clock::now();
   std::lock_guard<std::mutex> g(impl_->mu);
   for (const auto& k : keys) n += impl_->delete_pod_locked(k.first, k.second) ? 1 : 0;
   impl_->n_delete.fetch_add(static_cast<uint64_t>(keys.size()), std::memory_order_relaxed);
+  impl_->bulk_delete_ns.fetch_add(
+      static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count()),
+      std::memory_order_relaxed);
   return n;
 }
 
@@ -1369,7 +1388,8 @@ std::string Server::stats_json() const {
          ",\"calls\":{\"create_pod\":" + ld(m.n_create) + ",\"get_pod\":" + ld(m.n_get) + ",\"patch_pod\":" +
          ld(m.n_patch) + ",\"bind_pod\":" + ld(m.n_bind) + ",\"delete_pod\":" + ld(m.n_delete) + ",\"list\":" +
          ld(m.n_list) + ",\"watch\":" + ld(m.n_watch) + ",\"events\":" + ld(m.n_events) + ",\"lease\":" +
-         ld(m.n_lease) + "}}";
+         ld(m.n_lease) + "},\"bulk_ns\":{\"parse\":" + ld(m.bulk_parse_ns) + ",\"insert\":" +
+         ld(m.bulk_insert_ns) + ",\"delete\":" + ld(m.bulk_delete_ns) + "}}";
 }
 
 void Server::set_latency(double seconds) { impl_->latency_s.store(seconds > 0 ? seconds : 0.0); }
