@@ -632,12 +632,15 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         # (the in-process watch delivers the DELETED events on the next loop iterations: yield
         # first, and only then back off to short sleeps)
         # Deletions are delivered in order: wait for the last pod, then check them all once.
+        # (yield-only polling for the first 3 ms, so noticing the last release costs no
+        # sleep quantum; then 0.2 ms naps)
         uids = [pu.pod_uid(p) for p in pods]
         lookup = rt.state.ledger.lookup
-        for i in range(20000):
+        t_spin = time.perf_counter() + 0.003
+        for i in range(50000):
             if not lookup(uids[-1]) and not any(lookup(u) for u in uids):
                 break
-            await asyncio.sleep(0 if i < 50 else 0.0005)
+            await asyncio.sleep(0 if time.perf_counter() < t_spin else 0.0002)
         if pod_ctrl is not None:
             await pod_ctrl.queue.drain(5.0)
         if os.environ.get("NANOGPU_BENCH_DEBUG"):

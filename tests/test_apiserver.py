@@ -165,6 +165,33 @@ def test_watch_resume_and_gone(kind):
 
 
 @pytest.mark.parametrize("kind", KINDS)
+def test_watch_label_selector_filters_and_no_selector_sees_all(kind):
+    async def body(api, srv):
+        await api.create_pod(pu.make_pod("seed", [("main", 10)]))
+        _, rv = await api.list_pods()
+        await api.create_pod(pu.make_pod("plain", [("main", 10)]))
+        tagged = pu.make_pod("tagged", [("main", 10)])
+        pu.meta(tagged).setdefault("labels", {})["team"] = "a"
+        await api.create_pod(tagged)
+        await api.delete_pod("default", "plain")
+        await api.delete_pod("default", "tagged")
+
+        async def take(n, sel):
+            seen = []
+            async for batch in api.watch_batches("pods", rv, timeout_s=1, label_selector=sel):
+                seen.extend((ev["type"], pu.meta(ev["object"])["name"]) for ev in batch)
+                if len(seen) >= n:
+                    return seen
+            return seen
+
+        assert await asyncio.wait_for(take(4, None), 5) == [
+            ("ADDED", "plain"), ("ADDED", "tagged"), ("DELETED", "plain"), ("DELETED", "tagged")]
+        assert await asyncio.wait_for(take(2, "team=a"), 5) == [("ADDED", "tagged"), ("DELETED", "tagged")]
+
+    run(kind, body)
+
+
+@pytest.mark.parametrize("kind", KINDS)
 def test_leases_and_events(kind):
     async def body(api, srv):
         lease = {"apiVersion": "coordination.k8s.io/v1", "kind": "Lease", "metadata": {"name": "x"},
