@@ -1146,15 +1146,33 @@ void Server::Impl::flush_watches(IoThread* t) {
   }
 }
 
+namespace {
+// epoll_pwait2's nanosecond timeout where the kernel has it (5.11+), else milliseconds
+// rounded up
+int wait_events(int ep, epoll_event* evs, int max, double wait_s) {
+  static std::atomic<bool> no_pwait2{false};
+  if (!no_pwait2.load(std::memory_order_relaxed)) {
+    timespec ts;
+    ts.tv_sec = static_cast<time_t>(wait_s);
+    ts.tv_nsec = static_cast<long>((wait_s - static_cast<double>(ts.tv_sec)) * 1e9);
+    const int n = epoll_pwait2(ep, evs, max, &ts, nullptr);
+    if (n >= 0 || errno != ENOSYS) return n;
+    no_pwait2.store(true, std::memory_order_relaxed);
+  }
+  return epoll_wait(ep, evs, max, static_cast<int>(std::ceil(wait_s * 1e3)));
+}
+}  // namespace
+
 void Server::Impl::io_loop(IoThread* t) {
   epoll_event evs[256];
   while (!stopping.load(std::memory_order_acquire)) {
-    int timeout_ms = 200;
-    if (!t->delayed.empty())
-      timeout_ms = std::max(0, std::min(200, static_cast<int>((std::get<0>(t->delayed.front()) - steady_s()) * 1e3)));
-    if (t->flush_due > 0)
-      timeout_ms = std::max(0, std::min(timeout_ms, static_cast<int>(std::ceil((t->flush_due - steady_s()) * 1e3))));
-    const int n = epoll_wait(t->ep, evs, 256, timeout_ms);
+    // sub-millisecond deadlines (the 200 us watch linger, modelled round trips): a
+    // millisecond epoll timeout would hold the last chunk of a burst up to 1 ms
+    double wait_s = 0.2;
+    if (!t->delayed.empty()) wait_s = std::min(wait_s, std::get<0>(t->delayed.front()) - steady_s());
+    if (t->flush_due > 0) wait_s = std::min(wait_s, t->flush_due - steady_s());
+    wait_s = std::max(0.0, wait_s);
+    const int n = wait_events(t->ep, evs, 256, wait_s);
     for (int i = 0; i < n; ++i) {
       const int fd = evs[i].data.fd;
       if (fd == lfd) {
