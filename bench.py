@@ -600,8 +600,12 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
             tc = time.perf_counter() - tc
             if shared:
                 await barrier()                     # every rank's pods exist
+            t_send = time.perf_counter()
             conn.send(("step", step))
             summary = await loop.run_in_executor(None, conn.recv)
+            # the stand-in's span is first filter -> last bind; this adds its per-step set-up,
+            # summary and the pipe
+            srv_ms.setdefault(step, {})["schedule_wall_ms"] = 1e3 * (time.perf_counter() - t_send)
         else:
             # one kube-scheduler stand-in per rank; distinct tie-break streams per rank
             from nanogpu.sim.kubescore import KubeScoring
@@ -614,6 +618,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         # all ranks finished their share of the burst: peak occupancy
         await barrier()
         frag = rt.state.frag(min(SIZES))
+        t_frag = time.perf_counter()
         if store is not None:
             for p in pods:
                 m = pu.meta(p)
@@ -623,7 +628,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                     pass
         elif apisrv is not None:
             n_d, dt_d = await loop.run_in_executor(None, apisrv.delete, step)
-            srv_ms.setdefault(step, {})["delete_srv_ms"] = 1e3 * dt_d
+            srv_ms.setdefault(step, {}).update(delete_srv_ms=1e3 * dt_d, peak_ms=1e3 * (t_frag - ts),
+                                               delete_rpc_ms=1e3 * (time.perf_counter() - t_frag))
             if overlap and nxt is not None:
                 if os.environ.get("NANOGPU_BENCH_DEBUG"):
                     print(f"submit {nxt} {time.perf_counter():.4f}", file=sys.stderr)
@@ -641,8 +647,10 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
             if not lookup(uids[-1]) and not any(lookup(u) for u in uids):
                 break
             await asyncio.sleep(0 if time.perf_counter() < t_spin else 0.0002)
+        t_rel = time.perf_counter()
         if pod_ctrl is not None:
             await pod_ctrl.queue.drain(5.0)
+        srv_ms.setdefault(step, {})["drain_ms"] = 1e3 * (time.perf_counter() - t_rel)
         if os.environ.get("NANOGPU_BENCH_DEBUG"):
             print(f"step {step} start {t_step0:.4f} release {ts:.4f} end {time.perf_counter():.4f}", file=sys.stderr)
         phases = {"create_ms": 1e3 * tc, "schedule_ms": 1e3 * summary["span_s"],
