@@ -460,7 +460,7 @@ def driver_main(conn) -> None:
         work = {}
         for step in cfg["steps"]:
             pods = burst(cfg["rank"], cfg["world"], cfg["pods"], step, 7)
-            work[step] = NativeSchedulerDriver.prepare(pods) if native else pods
+            work[step] = NativeSchedulerDriver.prepare_native(pods) if native else pods
         cfg["kube_obj"] = KubeScoring() if cfg.get("kube") else None
         session = None
         if native:
@@ -485,10 +485,18 @@ def driver_main(conn) -> None:
             # chosen, as kube-scheduler's per-pod bind goroutines); Python: pool threads
             kw = ({"session": session, "bind_threads": 256, "kube": cfg["kube_obj"]} if native
                   else {"bind_threads": min(32, cfg["inflight"])})
+            t0 = time.perf_counter()
             drv = cls("127.0.0.1", cfg["port"], cfg["names"], cfg["caps"], seed=step * 1009 + cfg["rank"], **kw)
             stats = drv.run(prepared=work.pop(step)) if native else drv.run(work.pop(step))
             drv.close()
-            conn.send(stats.summary())
+            t1 = time.perf_counter()
+            sm = stats.summary()
+            t2 = time.perf_counter()
+            conn.send(sm)
+            if os.environ.get("NANOGPU_BENCH_DEBUG"):
+                print(f"drv step {step}: pre {1e3*(stats.t_first_filter-t0):.3f} run {1e3*(t1-t0):.3f} "
+                      f"post {1e3*(t1-stats.t_last_bind):.3f} summary {1e3*(t2-t1):.3f} send {1e3*(time.perf_counter()-t2):.3f}",
+                      file=sys.stderr)
 
     prof_path = os.environ.get("NANOGPU_DRIVER_PROFILE")
     if prof_path:
@@ -558,7 +566,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         for st in all_steps_pre:
             apisrv.load(st, [p for r in range(d.world) for p in burst(r, d.world, args.pods, st, 7)])
     pod_ctrl = rt.controllers[-1] if rt.leader else None
-    results = {"steps": [], "frag": [], "client_bind_ms": [], "frontdoor_bind_ms": []}
+    results = {"steps": [], "frag": [], "client_bind_s": [], "frontdoor_bind_ms": []}
 
     # synthetic pod objects are generated up front (client-side data, not scheduler work);
     # their creation in the API server, scheduling, deletion and release are all timed
@@ -657,9 +665,9 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                   "release_ms": 1e3 * (time.perf_counter() - ts)}
         phases.update(srv_ms.pop(step, {}))
         walls = rt.native.fe.take_bind_wall() if rt.native is not None else []
-        client_ms = summary.pop("bind_ms_all", [])
+        client_s = summary.pop("bind_s_all", [])
         if timed:
-            results["client_bind_ms"].extend(client_ms)
+            results["client_bind_s"].extend(client_s)
             results["frontdoor_bind_ms"].extend(1e3 * x for x in walls)
             diag = {"t0": round(t_step0, 4), "t1": round(time.perf_counter(), 4)}
             diag.update({k: round(summary.get(k, 0.0), 2) for k in ("cycle_max_ms", "cycle_sum_ms", "cycle_wire_ms", "bind_max_ms")})
@@ -754,6 +762,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                            if all(k in p for p in results["phases"])} if results.get("phases") else None
     results["schedule_ms_steps"] = [round(p["schedule_ms"], 1) for p in results.get("phases", [])]
     results["step_diag"] = results.get("diag", [])
+    results["client_bind_ms"] = [round(1e3 * x, 4) for x in results.pop("client_bind_s")]
     results["failed"] = sum(s["failed"] for s in results["steps"])
     results["bind_errors"] = sum(s["bind_errors"] for s in results["steps"])
     await client.close()

@@ -136,7 +136,7 @@ class Harness:
         wall = time.perf_counter() - t0
         binds = sorted(s["dur_ms"] for s in self.rt.tracer.dump(10 ** 9, "bind") if s["ok"])
         out = stats.summary()
-        out.pop("bind_ms_all", None)
+        out.pop("bind_s_all", None)
         out["wall_s"] = wall
         out["ext_bind_p50_ms"] = statistics.median(binds) if binds else None
         return out

@@ -15,7 +15,6 @@ from __future__ import annotations
 import asyncio
 import json
 import random
-import statistics
 import time
 from dataclasses import dataclass, field
 
@@ -220,24 +219,30 @@ class DriverStats:
     def summary(self) -> dict:
         span = max(1e-9, self.t_last_bind - self.t_first_filter)
         bl = sorted(self.bind_latencies)
+        e2e = sorted(self.e2e_latencies)
 
         def pct(a, q):
             return a[min(len(a) - 1, int(q * len(a)))] if a else 0.0
 
+        def median(a):   # of a sorted list
+            n = len(a)
+            return 0.0 if not n else (a[n // 2] if n % 2 else 0.5 * (a[n // 2 - 1] + a[n // 2]))
+
         return {"scheduled": self.scheduled, "failed": self.failed, "bind_errors": self.bind_errors,
                 "unschedulable_attempts": self.unschedulable_attempts,
                 "pods_per_s": self.scheduled / span if self.scheduled else 0.0, "span_s": span,
-                "bind_p50_ms": 1e3 * (statistics.median(bl) if bl else 0.0),
+                "bind_p50_ms": 1e3 * median(bl),
                 "bind_p99_ms": 1e3 * pct(bl, 0.99),
                 "bind_max_ms": 1e3 * (bl[-1] if bl else 0.0),
                 "cycle_max_ms": 1e3 * self.cycle_max_s,
                 "cycle_sum_ms": 1e3 * self.cycle_sum_s,
                 "cycle_wire_ms": 1e3 * self.cycle_wire_s,
-                "e2e_p50_ms": 1e3 * (statistics.median(self.e2e_latencies) if self.e2e_latencies else 0.0),
+                "e2e_p50_ms": 1e3 * median(e2e),
                 # the burst's window on the monotonic clock (comparable across processes of a node)
                 "t_first_filter": self.t_first_filter, "t_last_bind": self.t_last_bind,
-                # every POST /scheduler/bind as the scheduler saw it (request written -> reply read)
-                "bind_ms_all": [round(1e3 * x, 4) for x in self.bind_latencies]}
+                # every POST /scheduler/bind as the scheduler saw it (request written -> reply
+                # read), in seconds, unrounded
+                "bind_s_all": self.bind_latencies}
 
 
 class SchedulerDriver:
@@ -603,7 +608,22 @@ class NativeSchedulerDriver:
         self.max_attempts = max_attempts
         self.backoff_s = backoff_s
         self.stats = DriverStats()
-        self.placements: dict[str, str] = {}
+        self._placed: list = []    # (pod tuples, node per pod) of each run
+
+    @property
+    def placements(self) -> dict[str, str]:
+        """ns/name -> node of every pod these runs scheduled (built when asked for)."""
+        return {f"{ns}/{name}": node for args, nodes in self._placed
+                for (_, ns, name, *_), node in zip(args, nodes) if node}
+
+    @staticmethod
+    def prepare_native(pods: list[dict], kube: KubeScoring | None = None):
+        """`prepare`, then converted to the native loop's own pod records once
+        (core().SimBurst): a run takes them without per-run conversion."""
+        from ..native import core
+
+        args = NativeSchedulerDriver.prepare(pods, kube)
+        return args, core().SimBurst(args)
 
     @staticmethod
     def prepare(pods: list[dict], kube: KubeScoring | None = None) -> list[tuple]:
@@ -624,7 +644,11 @@ class NativeSchedulerDriver:
         from ..native import core
 
         args = prepared if prepared is not None else self.prepare(pods or [])
-        r = core().drive_scheduler(self.host, self.port, args, self.nodes, self.capacity, self.bind_threads,
+        native = None
+        if isinstance(args, tuple):   # prepare_native: (pod tuples, SimBurst)
+            args, native = args
+        r = core().drive_scheduler(self.host, self.port, native if native is not None else args,
+                                   self.nodes, self.capacity, self.bind_threads,
                                    self.seed, self.max_attempts, self.backoff_s, self.session,
                                    kube_combine=int(self.kube is not None),
                                    extender_weight=self.kube.extender_weight if self.kube else 1)
@@ -636,9 +660,7 @@ class NativeSchedulerDriver:
         st.cycle_max_s = r.get("cycle_max_s", 0.0)
         st.cycle_sum_s = r.get("cycle_sum_s", 0.0)
         st.cycle_wire_s = r.get("cycle_wire_s", 0.0)
-        for (_, ns, name, *_), node in zip(args, r["node_of"]):
-            if node:
-                self.placements[f"{ns}/{name}"] = node
+        self._placed.append((args, r["node_of"]))
         return st
 
     def close(self) -> None:

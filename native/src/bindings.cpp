@@ -860,9 +860,40 @@ PYBIND11_MODULE(_native, m) {
         "Grow the process fd table once up front (no RCU-synchronised growth under load).");
   py::class_<sim::Session, std::shared_ptr<sim::Session>>(m, "SchedulerSession")
       .def(py::init<>());
+  // a burst's pods converted once (kube-scheduler holds its pods decoded in the informer
+  // before a cycle starts): drive_scheduler then takes them without per-run conversion
+  struct SimBurst {
+    std::vector<sim::SimPod> pods;
+  };
+  auto to_sim_pods = [](const py::list& pods) {
+    std::vector<sim::SimPod> ps(pods.size());
+    for (size_t i = 0; i < pods.size(); ++i) {
+      // (json, ns, name, uid, need[, cpu_m, mem])
+      auto t = pods[i].cast<py::tuple>();
+      if (t.size() != 5 && t.size() != 7) throw py::value_error("pod tuple: (json, ns, name, uid, need[, cpu_m, mem])");
+      ps[i].json = t[0].cast<std::string>();
+      ps[i].ns = t[1].cast<std::string>();
+      ps[i].name = t[2].cast<std::string>();
+      ps[i].uid = t[3].cast<std::string>();
+      ps[i].need = t[4].cast<int64_t>();
+      if (t.size() == 7) {
+        ps[i].cpu_m = t[5].cast<int64_t>();
+        ps[i].mem = t[6].cast<int64_t>();
+      }
+    }
+    return ps;
+  };
+  py::class_<SimBurst, std::shared_ptr<SimBurst>>(m, "SimBurst")
+      .def(py::init([to_sim_pods](const py::list& pods) {
+             auto b = std::make_shared<SimBurst>();
+             b->pods = to_sim_pods(pods);
+             return b;
+           }),
+           py::arg("pods"))
+      .def("__len__", [](const SimBurst& b) { return b.pods.size(); });
   m.def(
       "drive_scheduler",
-      [](const std::string& host, int port, const py::list& pods,
+      [to_sim_pods](const std::string& host, int port, const py::object& pods,
          const std::vector<std::string>& nodes, const std::vector<int64_t>& capacity, int bind_threads, uint64_t seed,
          int max_attempts, double backoff_s, std::shared_ptr<sim::Session> session, int kube_combine,
          int extender_weight) {
@@ -879,25 +910,17 @@ PYBIND11_MODULE(_native, m) {
         cfg.extender_weight = extender_weight;
         if (!capacity.empty() && capacity.size() != nodes.size())
           throw py::value_error("capacity must be empty or one entry per node");
-        std::vector<sim::SimPod> ps(pods.size());
-        for (size_t i = 0; i < pods.size(); ++i) {
-          // (json, ns, name, uid, need[, cpu_m, mem])
-          auto t = pods[i].cast<py::tuple>();
-          if (t.size() != 5 && t.size() != 7) throw py::value_error("pod tuple: (json, ns, name, uid, need[, cpu_m, mem])");
-          ps[i].json = t[0].cast<std::string>();
-          ps[i].ns = t[1].cast<std::string>();
-          ps[i].name = t[2].cast<std::string>();
-          ps[i].uid = t[3].cast<std::string>();
-          ps[i].need = t[4].cast<int64_t>();
-          if (t.size() == 7) {
-            ps[i].cpu_m = t[5].cast<int64_t>();
-            ps[i].mem = t[6].cast<int64_t>();
-          }
+        std::shared_ptr<SimBurst> burst;
+        if (py::isinstance<SimBurst>(pods)) {
+          burst = pods.cast<std::shared_ptr<SimBurst>>();
+        } else {
+          burst = std::make_shared<SimBurst>();
+          burst->pods = to_sim_pods(pods.cast<py::list>());
         }
         sim::SimResult r;
         {
           py::gil_scoped_release nogil;
-          r = sim::drive(cfg, ps, session.get());
+          r = sim::drive(cfg, burst->pods, session.get());
         }
         py::dict d;
         d["scheduled"] = r.scheduled;

@@ -290,14 +290,14 @@ def test_native_scheduler_standin_binds_everything(latency_s):
                                          node_capacities([store.get_node(n) for n in nodes]), bind_threads=32,
                                          session=session)
             st2 = await loop.run_in_executor(None, drv2.run, pods[60:])
-            drv.placements.update(drv2.placements)
+            placements = {**drv.placements, **drv2.placements}
             assert st.scheduled + st.failed == 60 and st.scheduled == 60
             assert st2.scheduled + st2.failed == 60 and st.scheduled + st2.scheduled >= 100
             st.scheduled += st2.scheduled
-            assert len(drv.placements) == st.scheduled
+            assert len(placements) == st.scheduled
             bound = {(ns, name): node for ns, name, node in store.bindings}
             assert len(bound) == len(store.bindings) == st.scheduled
-            for key, node in drv.placements.items():
+            for key, node in placements.items():
                 assert bound[tuple(key.split("/"))] == node
             used = {}
             for p in store.pods.values():
