@@ -390,6 +390,26 @@ def apiserver_main(conn) -> None:
             return
 
 
+async def arecv(conn):
+    """conn.recv() awaited on the event loop (the pipe's fd in the selector): no executor
+    thread, whose start can wait milliseconds for the GIL while the loop is busy."""
+    if not conn.poll():
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        fd = conn.fileno()
+
+        def ready():
+            if not fut.done():
+                fut.set_result(None)
+
+        loop.add_reader(fd, ready)
+        try:
+            await fut
+        finally:
+            loop.remove_reader(fd)
+    return conn.recv()
+
+
 class ApiServerProc:
     """Rank 0's handle on the shared API server process (spawned once, before any GPU use;
     `start()` gives each bench pass a fresh server)."""
@@ -417,14 +437,14 @@ class ApiServerProc:
     def load(self, step: int, pods: list[dict]) -> None:
         self._rpc("load", step, [json.dumps(p, separators=(",", ":")) for p in pods])
 
-    def create(self, step: int) -> tuple[int, float]:
+    async def create(self, step: int) -> tuple[int, float]:
         """(pods created, seconds the server spent on them)"""
-        if os.environ.get("NANOGPU_BENCH_DEBUG"):
-            print(f"rpc-create {step} {time.perf_counter():.4f}", file=sys.stderr)
-        return self._rpc("create", step)
+        self.conn.send(("create", step))
+        return await arecv(self.conn)
 
-    def delete(self, step: int) -> tuple[int, float]:
-        return self._rpc("delete", step)
+    async def delete(self, step: int) -> tuple[int, float]:
+        self.conn.send(("delete", step))
+        return await arecv(self.conn)
 
     def stats(self) -> dict:
         return self._rpc("stats")
@@ -603,14 +623,14 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                         await api.create_pod(p)
             elif apisrv is not None:
                 fut = created.pop(step, None)   # every rank's pods
-                n_c, dt_c = await (fut if fut is not None else loop.run_in_executor(None, apisrv.create, step))
+                n_c, dt_c = await (fut if fut is not None else apisrv.create(step))
                 srv_ms.setdefault(step, {})["create_srv_ms"] = 1e3 * dt_c
             tc = time.perf_counter() - tc
             if shared:
                 await barrier()                     # every rank's pods exist
             t_send = time.perf_counter()
             conn.send(("step", step))
-            summary = await loop.run_in_executor(None, conn.recv)
+            summary = await arecv(conn)
             # the stand-in's span is first filter -> last bind; this adds its per-step set-up,
             # summary and the pipe
             srv_ms.setdefault(step, {})["schedule_wall_ms"] = 1e3 * (time.perf_counter() - t_send)
@@ -635,13 +655,11 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                 except Exception:
                     pass
         elif apisrv is not None:
-            n_d, dt_d = await loop.run_in_executor(None, apisrv.delete, step)
+            n_d, dt_d = await apisrv.delete(step)
             srv_ms.setdefault(step, {}).update(delete_srv_ms=1e3 * dt_d, peak_ms=1e3 * (t_frag - ts),
                                                delete_rpc_ms=1e3 * (time.perf_counter() - t_frag))
             if overlap and nxt is not None:
-                if os.environ.get("NANOGPU_BENCH_DEBUG"):
-                    print(f"submit {nxt} {time.perf_counter():.4f}", file=sys.stderr)
-                created[nxt] = loop.run_in_executor(None, apisrv.create, nxt)
+                created[nxt] = asyncio.ensure_future(apisrv.create(nxt))
         # the pod controller releases on DELETED; wait until our shares are gone
         # (the in-process watch delivers the DELETED events on the next loop iterations: yield
         # first, and only then back off to short sleeps)
