@@ -376,6 +376,28 @@ def apiserver_main(conn) -> None:
             conn.send((n, time.perf_counter() - t))
             if os.environ.get("NANOGPU_BENCH_DEBUG"):
                 print(f"delete {msg[1]} {t:.4f} -> {time.perf_counter():.4f}", file=sys.stderr)
+        elif op == "churn":
+            # the workload's clients at one moment: this burst's deletes and the next burst's
+            # creates arrive together. The create runs on a second thread (both calls drop the
+            # GIL): its parsing overlaps the delete; its inserts follow the delete's lock hold.
+            # Replies: the delete's first, then the create's.
+            import threading
+
+            out: dict = {}
+
+            def create_next(step=msg[2]):
+                t0 = time.perf_counter()
+                codes = srv.create_pods(steps[step])
+                out["v"] = (sum(1 for c in codes if c == 201), time.perf_counter() - t0)
+
+            th = threading.Thread(target=create_next)
+            th.start()
+            steps.pop(msg[1], None)
+            t = time.perf_counter()
+            n = srv.delete_pods(keys.pop(msg[1]))
+            conn.send((n, time.perf_counter() - t))
+            th.join()
+            conn.send(out["v"])
         elif op == "stats":
             conn.send(_json.loads(srv.stats()))
         elif op == "end":            # the pass is over
@@ -445,6 +467,13 @@ class ApiServerProc:
     async def delete(self, step: int) -> tuple[int, float]:
         self.conn.send(("delete", step))
         return await arecv(self.conn)
+
+    async def churn(self, step: int, nxt: int) -> tuple[tuple[int, float], asyncio.Future]:
+        """Delete `step`'s pods while `nxt`'s are created: the delete's answer, and a future of
+        the create's."""
+        self.conn.send(("churn", step, nxt))
+        deleted = await arecv(self.conn)
+        return deleted, asyncio.ensure_future(arecv(self.conn))
 
     def stats(self) -> dict:
         return self._rpc("stats")
@@ -655,11 +684,12 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                 except Exception:
                     pass
         elif apisrv is not None:
-            n_d, dt_d = await apisrv.delete(step)
+            if overlap and nxt is not None:
+                (n_d, dt_d), created[nxt] = await apisrv.churn(step, nxt)
+            else:
+                n_d, dt_d = await apisrv.delete(step)
             srv_ms.setdefault(step, {}).update(delete_srv_ms=1e3 * dt_d, peak_ms=1e3 * (t_frag - ts),
                                                delete_rpc_ms=1e3 * (time.perf_counter() - t_frag))
-            if overlap and nxt is not None:
-                created[nxt] = asyncio.ensure_future(apisrv.create(nxt))
         # the pod controller releases on DELETED; wait until our shares are gone
         # (the in-process watch delivers the DELETED events on the next loop iterations: yield
         # first, and only then back off to short sleeps)
