@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cctype>
+#include <charconv>
 #include <cmath>
 #include <cerrno>
 #include <condition_variable>
@@ -21,6 +22,7 @@
 #include <queue>
 #include <random>
 #include <stdexcept>
+#include <string_view>
 #include <thread>
 #include <unordered_map>
 
@@ -212,8 +214,22 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* 
   r.last_error.assign(n_pods, std::string());
   r.bind_latencies.reserve(n_pods);
   r.e2e_latencies.reserve(n_pods);
-  std::unordered_map<std::string, int> node_index;
+  std::unordered_map<std::string_view, int> node_index;   // views into cfg.nodes
   for (size_t i = 0; i < n_nodes; ++i) node_index.emplace(cfg.nodes[i], static_cast<int>(i));
+  // A name in a reply -> node index. The extender answers in the order the names were sent
+  // (filter: the passing ones; priorities: all of them), so the next expected position of
+  // the sent list is tried before the hash lookup.
+  auto resolve = [&](std::string_view name, const std::vector<int>* sent, size_t* cursor) -> int {
+    if (sent) {
+      for (size_t k = *cursor; k < sent->size(); ++k)
+        if (cfg.nodes[(*sent)[k]] == name) {
+          *cursor = k + 1;
+          return (*sent)[k];
+        }
+    }
+    auto it = node_index.find(name);
+    return it == node_index.end() ? -1 : it->second;
+  };
   const bool fit = !cfg.capacity.empty();
   std::vector<int64_t> requested(n_nodes, 0);
   std::vector<int64_t> req_cpu(n_nodes, 0), req_mem(n_nodes, 0);   // for kube_combine
@@ -556,19 +572,24 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* 
       if (cycle.post("/scheduler/filter", body, &status, &out) && doc.parse(out) &&
           doc.is(doc.root(), json::Type::kObj)) {
         int32_t nn = doc.get(doc.root(), "NodeNames", true);
+        const std::vector<int>* sent = names == &all_json ? &all : &cands;
+        size_t cursor = 0;
         if (doc.is(nn, json::Type::kArr))
           for (int32_t c = doc.at(nn).first; c >= 0; c = doc.at(c).next) {
-            auto it = node_index.find(std::string(doc.str(c)));
-            if (it != node_index.end()) fits.push_back(it->second);
+            if (!doc.is(c, json::Type::kStr)) continue;
+            const int n = resolve(doc.str(c), sent, &cursor);
+            if (n >= 0) fits.push_back(n);
           }
       }
       if (fits.size() == 1) {
         host = fits[0];
       } else if (!fits.empty()) {
         const std::string* fj = names;
+        const std::vector<int>* psent = names == &all_json ? &all : &cands;
         if (fits.size() != (fit ? cands.size() : n_nodes)) {
           cands_json = names_json(fits);
           fj = &cands_json;
+          psent = &fits;
         }
         body.assign("{\"Pod\":").append(p.json).append(",\"Nodes\":null,\"NodeNames\":").append(*fj).push_back('}');
         if (cycle.post("/scheduler/priorities", body, &status, &out) && doc.parse(out) &&
@@ -578,19 +599,23 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* 
           // req_cpu / req_mem also change on the binder thread (a failed bind): read under mu
           std::unique_lock<std::mutex> plk(mu, std::defer_lock);
           if (cfg.kube_combine) plk.lock();
+          size_t cursor = 0;
           for (int32_t c = doc.at(doc.root()).first; c >= 0; c = doc.at(c).next) {
             int32_t h = doc.get(c, "Host", true), s = doc.get(c, "Score", true);
             if (!doc.is(h, json::Type::kStr) || !doc.is(s, json::Type::kNum)) continue;
-            auto it = node_index.find(std::string(doc.str(h)));
-            if (it == node_index.end()) continue;
-            int64_t score = std::strtoll(std::string(doc.str(s)).c_str(), nullptr, 10);
+            const int node = resolve(doc.str(h), psent, &cursor);
+            if (node < 0) continue;
+            const std::string_view st = doc.str(s);
+            int64_t score = 0;
+            if (std::from_chars(st.data(), st.data() + st.size(), score).ec != std::errc())
+              score = std::strtoll(std::string(st).c_str(), nullptr, 10);
             if (cfg.kube_combine)
-              score = score * cfg.extender_weight * 10 + plugin_score(static_cast<size_t>(it->second), p);
+              score = score * cfg.extender_weight * 10 + plugin_score(static_cast<size_t>(node), p);
             if (score > best) {
               best = score;
               ties.clear();
             }
-            if (score == best) ties.push_back(it->second);
+            if (score == best) ties.push_back(node);
           }
           if (ties.size() == 1) host = ties[0];
           else if (!ties.empty()) host = ties[std::uniform_int_distribution<size_t>(0, ties.size() - 1)(rng)];
