@@ -380,6 +380,7 @@ def apiserver_main(conn) -> None:
             # the workload's clients at one moment: this burst's deletes and the next burst's
             # creates arrive together. The create runs on a second thread (both calls drop the
             # GIL): its parsing overlaps the delete; its inserts follow the delete's lock hold.
+            # One parse thread: more would slow the delete, which the release waits on.
             # Replies: the delete's first, then the create's.
             import threading
 
@@ -387,7 +388,7 @@ def apiserver_main(conn) -> None:
 
             def create_next(step=msg[2]):
                 t0 = time.perf_counter()
-                codes = srv.create_pods(steps[step])
+                codes = srv.create_pods(steps[step], 1)
                 out["v"] = (sum(1 for c in codes if c == 201), time.perf_counter() - t0)
 
             th = threading.Thread(target=create_next)

@@ -76,7 +76,8 @@ class Server {
   // (status, body). Watches are not served this way.
   std::pair<int, std::string> call(std::string_view method, std::string_view target, std::string_view body);
   // Creates many pods (JSON texts, namespace taken from each object) under one lock hold.
-  std::vector<int> create_pods(const std::vector<std::string>& pods);
+  // `threads`: parse workers for a large batch (0: NANOGPU_APISERVER_BULK_THREADS, default 4)
+  std::vector<int> create_pods(const std::vector<std::string>& pods, int threads = 0);
   // Deletes (namespace, name) pairs; returns how many existed.
   int delete_pods(const std::vector<std::pair<std::string, std::string>>& keys);
   std::string stats_json() const;

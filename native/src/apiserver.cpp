@@ -1376,13 +1376,13 @@ void parallel_for(size_t n, size_t workers, size_t min_parallel, Fn&& fn) {
 }
 }  // namespace
 
-std::vector<int> Server::create_pods(const std::vector<std::string>& texts) {
+std::vector<int> Server::create_pods(const std::vector<std::string>& texts, int threads) {
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<FastCreate> fast(texts.size());
   std::vector<JV> vs(texts.size());
   std::vector<int> codes(texts.size(), 201);
   // parsing needs no lock: a large batch is parsed by a few threads, only the inserts are serial
-  parallel_for(texts.size(), bulk_threads(), 256, [&](size_t b, size_t e) {
+  parallel_for(texts.size(), threads > 0 ? static_cast<size_t>(threads) : bulk_threads(), 256, [&](size_t b, size_t e) {
     for (size_t i = b; i < e; ++i) {
       fast[i] = fast_create(texts[i], "");
       if (!fast[i].ok && !parse(texts[i], &vs[i])) codes[i] = 400;

@@ -970,7 +970,8 @@ PYBIND11_MODULE(_native, m) {
           },
           py::arg("method"), py::arg("target"), py::arg("body") = "",
           "One request without a socket: (status, body bytes).")
-      .def("create_pods", &apisrv::Server::create_pods, py::arg("pods"), py::call_guard<py::gil_scoped_release>(),
+      .def("create_pods", &apisrv::Server::create_pods, py::arg("pods"), py::arg("threads") = 0,
+           py::call_guard<py::gil_scoped_release>(),
            "Creates pods from JSON texts under one lock hold; one status code per pod.")
       .def("delete_pods", &apisrv::Server::delete_pods, py::arg("keys"), py::call_guard<py::gil_scoped_release>(),
            "Deletes (namespace, name) pods; returns how many existed.")
