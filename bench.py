@@ -341,6 +341,7 @@ def apiserver_main(conn) -> None:
         pass
     affinity.apply(affinity.pick_cpus())
     srv = None
+    pool = None
     steps: dict = {}
     keys: dict = {}   # the clients know their pods' names: keyed at load, not per delete
     while True:
@@ -382,23 +383,22 @@ def apiserver_main(conn) -> None:
             # GIL): its parsing overlaps the delete; its inserts follow the delete's lock hold.
             # One parse thread: more would slow the delete, which the release waits on.
             # Replies: the delete's first, then the create's.
-            import threading
+            if pool is None:   # one long-lived worker: no thread start per step
+                from concurrent.futures import ThreadPoolExecutor
 
-            out: dict = {}
+                pool = ThreadPoolExecutor(1)
 
             def create_next(step=msg[2]):
                 t0 = time.perf_counter()
                 codes = srv.create_pods(steps[step], 1)
-                out["v"] = (sum(1 for c in codes if c == 201), time.perf_counter() - t0)
+                return sum(1 for c in codes if c == 201), time.perf_counter() - t0
 
-            th = threading.Thread(target=create_next)
-            th.start()
+            fut = pool.submit(create_next)
             steps.pop(msg[1], None)
             t = time.perf_counter()
             n = srv.delete_pods(keys.pop(msg[1]))
             conn.send((n, time.perf_counter() - t))
-            th.join()
-            conn.send(out["v"])
+            conn.send(fut.result())
         elif op == "stats":
             conn.send(_json.loads(srv.stats()))
         elif op == "end":            # the pass is over
