@@ -31,6 +31,11 @@ struct Node {
 class Doc {
  public:
   bool parse(std::string_view src);
+  // Objects and arrays nested deeper than `max_depth` (the root is depth 0) are checked for
+  // balanced brackets and well-formed strings but get no child nodes: they read as empty,
+  // and raw() still spans their text. For readers that need a few shallow fields of a large
+  // document (the pod watch's filter); a caller that needs more parses again in full.
+  bool parse_shallow(std::string_view src, int max_depth);
   const Node& at(int32_t i) const { return nodes_[i]; }
   int32_t root() const { return nodes_.empty() ? -1 : 0; }
   // A string with no escape is not copied: its length carries kInSrc and its offset points
@@ -54,6 +59,8 @@ class Doc {
   }
   int32_t value(int depth);
   bool string(uint32_t* off, uint32_t* len);
+  bool skip_container();
+  int max_depth_ = 1 << 30;
   void ws() {
     while (p_ < src_.size() && (src_[p_] == ' ' || src_[p_] == '\n' || src_[p_] == '\r' || src_[p_] == '\t')) ++p_;
   }

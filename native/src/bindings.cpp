@@ -321,10 +321,14 @@ static py::list decode_pod_events(const py::bytes& data, PodWatchFilter* f) {
     p = e + 1;
     while (!line.empty() && (line.back() == '\r' || line.back() == ' ')) line.remove_suffix(1);
     if (line.empty()) continue;
-    if (!d.parse(line) || !d.is(d.root(), json::Type::kObj)) throw py::value_error("bad watch event line");
-    const int32_t t = d.get(d.root(), "type");
-    const int32_t obj = d.get(d.root(), "object");
-    const std::string_view type = d.is(t, json::Type::kStr) ? d.str(t) : std::string_view();
+    // with a filter most events are dropped on a few shallow fields (type, metadata's
+    // identity, nodeName, phase): parse to that depth first, in full only for what goes on
+    bool shallow = f != nullptr;
+    if (!(shallow ? d.parse_shallow(line, 3) : d.parse(line)) || !d.is(d.root(), json::Type::kObj))
+      throw py::value_error("bad watch event line");
+    int32_t t = d.get(d.root(), "type");
+    int32_t obj = d.get(d.root(), "object");
+    std::string_view type = d.is(t, json::Type::kStr) ? d.str(t) : std::string_view();
     if (f && d.is(obj, json::Type::kObj) && (type == "ADDED" || type == "MODIFIED" || type == "DELETED")) {
       const int32_t md = d.get(obj, "metadata"), sp = d.get(obj, "spec"), st = d.get(obj, "status");
       auto field = [&](int32_t o, const char* k) -> std::string_view {
@@ -360,6 +364,13 @@ static py::list decode_pod_events(const py::bytes& data, PodWatchFilter* f) {
       }
       if (type == "DELETED") f->forwarded.erase(key);
       else f->forwarded.insert(std::move(key));
+    }
+    if (shallow) {   // kept: the whole event is needed (slim_pod reads labels, containers)
+      if (!d.parse(line)) throw py::value_error("bad watch event line");
+      t = d.get(d.root(), "type");
+      obj = d.get(d.root(), "object");
+      type = d.is(t, json::Type::kStr) ? d.str(t) : std::string_view();
+      shallow = false;
     }
     py::dict ev;
     ev["type"] = py::str(std::string(type));

@@ -43,6 +43,43 @@ bool ieq(std::string_view a, std::string_view b) {
 }
 }  // namespace
 
+bool Doc::parse_shallow(std::string_view src, int max_depth) {
+  max_depth_ = max_depth;
+  const bool ok = parse(src);
+  max_depth_ = 1 << 30;
+  return ok;
+}
+
+// At an opening bracket: to just past its matching close. Strings are skipped whole (an
+// escaped quote does not end one); control characters inside them are rejected as parse()
+// would.
+bool Doc::skip_container() {
+  const char* s = src_.data();
+  const size_t n = src_.size();
+  int depth = 0;
+  while (p_ < n) {
+    const char c = s[p_++];
+    if (c == '"') {
+      for (;;) {
+        if (p_ >= n) return false;
+        const unsigned char ch = static_cast<unsigned char>(s[p_++]);
+        if (ch == '"') break;
+        if (ch == '\\') {
+          if (p_ >= n) return false;
+          ++p_;
+        } else if (ch < 0x20) {
+          return false;
+        }
+      }
+    } else if (c == '{' || c == '[') {
+      if (++depth > kMaxDepth) return false;
+    } else if (c == '}' || c == ']') {
+      if (--depth == 0) return true;
+    }
+  }
+  return false;
+}
+
 bool Doc::parse(std::string_view src) {
   src_ = src;
   p_ = 0;
@@ -146,7 +183,10 @@ int32_t Doc::value(int depth) {
   nodes_.emplace_back();
   nodes_[idx].src_begin = static_cast<uint32_t>(p_);
   const char c = src_[p_];
-  if (c == '{' || c == '[') {
+  if ((c == '{' || c == '[') && depth >= max_depth_) {
+    nodes_[idx].type = c == '{' ? Type::kObj : Type::kArr;
+    if (!skip_container()) return -1;
+  } else if (c == '{' || c == '[') {
     const bool obj = c == '{';
     nodes_[idx].type = obj ? Type::kObj : Type::kArr;
     ++p_;

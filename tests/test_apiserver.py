@@ -317,3 +317,39 @@ def test_watch_filter_does_the_controllers_ledger_only_work():
     assert f.forwarded == 1
     assert [e["type"] for e in N.decode_pod_watch(data)] == ["ADDED", "MODIFIED", "MODIFIED", "MODIFIED", "DELETED",
                                                             "MODIFIED", "DELETED"]
+
+
+def test_watch_filter_shallow_parse_skips_deep_fields_exactly():
+    """The filter parses events only down to metadata's fields; deeper objects are skipped
+    as text. Tricky text in skipped parts (escaped quotes, brackets inside strings, nested
+    arrays) must neither end a skip early nor hide a malformed event; a kept event still
+    carries its deep fields (labels, container limits) to Python."""
+    from nanogpu.state.cluster import ClusterState
+    from nanogpu.topology.model import synthetic_mi355x
+
+    st = ClusterState()
+    st.register_node(pu.make_node("n0", 8, synthetic_mi355x(8).to_json()))
+    tricky = {"a": 'x"}]{[\\', "b": "\\u005d]", "nested": "[[{}]]"}
+    pending = pu.make_pod("pending", [("main", 10)])
+    pending["metadata"]["labels"] = dict(tricky)
+    pending["spec"]["extra"] = [[1, [2, {"k": "}"}]], {"q": ["]"]}]
+    kept = pu.make_pod("kept", [("main", 30)])
+    kept["metadata"]["labels"] = dict(tricky)
+    kept["spec"]["nodeName"] = "n0"
+    kept["status"]["phase"] = "Running"
+    f = N.PodWatchFilter(st.ledger)
+    data = b"".join(json.dumps({"type": t, "object": p}).encode() + b"\n"
+                    for t, p in (("ADDED", pending), ("MODIFIED", kept)))
+    out = f.decode(data)
+    assert [(e["type"], e["object"]["metadata"]["name"]) for e in out] == [("MODIFIED", "kept")]
+    assert out[0]["object"]["metadata"]["labels"] == tricky
+    assert out[0]["object"]["spec"]["containers"][0]["resources"]["limits"] == kept["spec"]["containers"][0]["resources"]["limits"]
+    assert f.dropped == 1
+    # a skipped part is checked for structure only (strings, bracket balance): a broken one
+    # still fails the event
+    unbalanced = json.dumps({"type": "ADDED", "object": pending}).replace('"labels": {', '"labels": {[').encode() + b"\n"
+    with pytest.raises(ValueError):
+        f.decode(unbalanced)
+    unterminated = b'{"type":"ADDED","object":{"metadata":{"labels":{"a":"x\\"}}}}\n'
+    with pytest.raises(ValueError):
+        f.decode(unterminated)
