@@ -325,7 +325,7 @@ def burst(rank: int, world: int, total: int, step: int, seed: int) -> list[dict]
     return pods
 
 
-def apiserver_main(conn) -> None:
+def apiserver_main(conn, avoid: list[int] | None = None, near: int = -1) -> None:
     """The shared API server's process: native API servers (native/src/apiserver.cpp), one
     per bench pass, on an L3 domain of their own, plus a command pipe through which rank 0
     plays the workload's clients (bulk create / delete of a step's pods; the pod JSON is
@@ -339,7 +339,7 @@ def apiserver_main(conn) -> None:
         os.sched_setaffinity(0, range(os.cpu_count() or 1))
     except OSError:
         pass
-    affinity.apply(affinity.pick_cpus())
+    affinity.apply(affinity.pick_cpus_avoiding(avoid or [], near))
     srv = None
     pool = None
     steps: dict = {}
@@ -354,7 +354,7 @@ def apiserver_main(conn) -> None:
             keys.clear()
             srv = core().ApiServer("127.0.0.1", 0, msg[1], 1 << 16)   # watch cache: 64k events per kind
             srv.set_latency(msg[2])
-            conn.send(srv.port)
+            conn.send((srv.port, sorted(os.sched_getaffinity(0))))
         elif op == "nodes":
             for n in msg[1]:
                 srv.call("POST", "/api/v1/nodes", n)
@@ -437,21 +437,23 @@ class ApiServerProc:
     """Rank 0's handle on the shared API server process (spawned once, before any GPU use;
     `start()` gives each bench pass a fresh server)."""
 
-    def __init__(self):
+    def __init__(self, avoid: list[int] | None = None, near: int = -1):
         import multiprocessing as mp
 
         ctx = mp.get_context("spawn")
         self.conn, child = ctx.Pipe()
-        self.proc = ctx.Process(target=apiserver_main, args=(child,), daemon=True)
+        self.proc = ctx.Process(target=apiserver_main, args=(child, avoid, near), daemon=True)
         self.proc.start()
         self.url = ""
+        self.cpus: list[int] = []
 
     def _rpc(self, *msg):
         self.conn.send(msg)
         return self.conn.recv()
 
     def start(self, threads: int, latency_s: float = 0.0) -> str:
-        self.url = f"http://127.0.0.1:{self._rpc('start', threads, latency_s)}"
+        port, self.cpus = self._rpc("start", threads, latency_s)
+        self.url = f"http://127.0.0.1:{port}"
         return self.url
 
     def add_nodes(self, nodes: list[dict]) -> None:
@@ -831,6 +833,8 @@ def _cpulist(cpus: list[int]) -> str:
 def main() -> int:
     args = parse_args()
     cpus: list[int] = []
+    rank_cpus: list[int] = []
+    rank0_numa = -1
     if args.cpu_affinity == "auto":
         # before any process is spawned or the GPU is touched: children inherit the mask
         from nanogpu import affinity
@@ -840,6 +844,10 @@ def main() -> int:
         mine = numas[lr] if lr < len(numas) else -1
         ranks = [numas[r] if r < len(numas) else -1 for r in range(lws)] if lws > 1 else None
         cpus = affinity.pick_cpus(mine, lr, ranks)
+        # every local rank's domain (deterministic with several ranks): the shared API server
+        # keeps off all of them, though they are idle when it starts
+        rank_cpus = [c for r in range(lws) for c in affinity.pick_cpus(ranks[r], r, ranks)] if ranks else list(cpus)
+        rank0_numa = ranks[0] if ranks else mine
         sharing = sum(1 for r in range(lws) if affinity.pick_cpus(ranks[r], r, ranks) == cpus) if ranks else 1
         if not affinity.apply(cpus):
             cpus = []
@@ -862,7 +870,7 @@ def main() -> int:
     api_proc = None
     if int(os.environ.get("RANK", "0")) == 0 and not args.inproc_driver:
         # the shared API server's process, like the stand-in's: before anything touches the GPU
-        api_proc = ApiServerProc()
+        api_proc = ApiServerProc(avoid=rank_cpus, near=rank0_numa)
     d = Dist(args.gpus)
     d.init(use_gpu=not args.no_gpu)
     topo, gpu_info = node_template(d, args)
@@ -919,6 +927,7 @@ def main() -> int:
                                       f"one native HTTP API server for all ranks, own process "
                                       f"({args.apiserver_threads or min(16, max(4, d.world))} IO threads), REST + watch"),
                        "cpus_rank0": _cpulist(cpus),
+                       "cpus_apiserver": _cpulist(api_proc.cpus) if api_proc is not None else None,
                        # next burst created by the clients while this one is released
                        "create_overlaps_release": not (args.inproc_api or args.no_overlap_create),
                        "frontend": f"{args.frontend_threads} threads, busy-poll {args.busy_poll_us} us"},

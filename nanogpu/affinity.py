@@ -113,6 +113,24 @@ def pick_cpus(numa: int = -1, local_rank: int = 0, local_ranks_numa: list[int] |
     return min(doms, key=lambda d: (sum(load.get(c, 0.0) for c in d) / len(d), d[0]))
 
 
+def pick_cpus_avoiding(taken: list[int], near: int = -1, window_s: float = 0.1) -> list[int]:
+    """An L3 domain for a helper process (the bench's shared API server) that shares no core
+    with `taken` (the ranks' domains, which may not be busy yet when the helper starts):
+    the least busy such domain, NUMA node `near` first on a tie; any domain if all are taken."""
+    doms = l3_domains()
+    if not doms:
+        return []
+    avoid = set(taken)
+    free = [d for d in doms if not avoid.intersection(d)]
+    if len(free) > 1:
+        free = [d for d in free if 0 not in d] or free   # CPU 0 carries housekeeping work
+    if not free:
+        return pick_cpus()
+    load = _busy([c for d in free for c in d], window_s)
+    return min(free, key=lambda d: (round(sum(load.get(c, 0.0) for c in d) / len(d), 1),
+                                    near >= 0 and numa_of_cpu(d[0]) != near, d[0]))
+
+
 def apply(cpus: list[int]) -> bool:
     """Pins this process (and the threads and children it creates later) to `cpus`."""
     if not cpus:

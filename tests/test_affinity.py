@@ -58,3 +58,19 @@ def test_single_rank_takes_the_least_busy_domain(tmp_path, monkeypatch):
     monkeypatch.setattr(A, "_busy", lambda cpus, w: {c: busy[c] for c in cpus})
     assert A.pick_cpus(0) == [8, 9, 10, 11]
     assert A.pick_cpus(1) in ([12, 13, 14, 15], [16, 17, 18, 19], [20, 21, 22, 23])
+
+
+def test_bench_api_server_keeps_off_every_ranks_domain(tmp_path, monkeypatch):
+    """The shared API server starts before the ranks are busy, so it must avoid their
+    domains by construction, not by load: the least busy free domain, rank 0's socket on a tie."""
+    allowed = make_tree(tmp_path)
+    real_l3, real_numa = A.l3_domains, A.numa_of_cpu
+    monkeypatch.setattr(A.os, "sched_getaffinity", lambda pid: allowed)
+    monkeypatch.setattr(A, "l3_domains", lambda allowed=None, root=tmp_path: real_l3(allowed, root))
+    monkeypatch.setattr(A, "numa_of_cpu", lambda cpu, root=tmp_path: real_numa(cpu, root))
+    monkeypatch.setattr(A, "_busy", lambda cpus, w: {c: 0.0 for c in cpus})   # all idle
+    gpu_numa = [0, 0, 1, 1]
+    taken = [c for r in range(4) for c in A.pick_cpus(gpu_numa[r], r, gpu_numa)]
+    assert A.pick_cpus_avoiding(taken, near=0) == [20, 21, 22, 23]   # socket 0 has no free domain but CPU 0's
+    assert A.pick_cpus_avoiding(taken[:4], near=0) == [8, 9, 10, 11]
+    assert A.pick_cpus_avoiding(taken[:4], near=1) == [12, 13, 14, 15]
