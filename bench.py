@@ -659,7 +659,9 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                 srv_ms.setdefault(step, {})["create_srv_ms"] = 1e3 * dt_c
             tc = time.perf_counter() - tc
             if shared:
+                tb = time.perf_counter()
                 await barrier()                     # every rank's pods exist
+                srv_ms.setdefault(step, {})["barrier_create_ms"] = 1e3 * (time.perf_counter() - tb)
             t_send = time.perf_counter()
             conn.send(("step", step))
             summary = await arecv(conn)
@@ -677,6 +679,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         ts = time.perf_counter()
         # all ranks finished their share of the burst: peak occupancy
         await barrier()
+        srv_ms.setdefault(step, {})["barrier_peak_ms"] = 1e3 * (time.perf_counter() - ts)
         frag = rt.state.frag(min(SIZES))
         t_frag = time.perf_counter()
         if store is not None:
@@ -965,6 +968,7 @@ def main() -> int:
             "native_verb_mean_us": res.get("native"),
             "phase_ms_per_step_rank0": res.get("phase_ms"),
             "schedule_ms_each_step_rank0": res.get("schedule_ms_steps"),
+            "schedule_ms_by_rank": out["schedule_ms_by_rank"],
             # per timed step (rank 0): slowest scheduling cycle and bind seen by the stand-in,
             # pods the cycle found no host for, cyclic-GC pause time of the extender process
             "step_diag_rank0": res.get("step_diag"),
@@ -1052,7 +1056,9 @@ def summarize(d: Dist, args, res: dict) -> dict:
             "p50_bind_python_ms": round(statistics.median(py), 4) if py else None,
             "scheduled": scheduled, "failed": sum(d.gather_obj(res["failed"])),
             "unschedulable": sum(d.gather_obj(res["unschedulable_attempts"])),
-            "bind_errors": sum(d.gather_obj(res["bind_errors"]))}
+            "bind_errors": sum(d.gather_obj(res["bind_errors"])),
+            # each rank's mean stand-in span per step: the slowest sets the peak barrier
+            "schedule_ms_by_rank": [round(v, 2) for v in d.gather_obj((res.get("phase_ms") or {}).get("schedule_ms", 0.0))]}
 
 
 def reference_model_frag(args, topo) -> dict:
