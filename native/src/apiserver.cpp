@@ -451,6 +451,7 @@ struct IoThread {
   // modelled round trip: responses held until due, in arrival order (one latency for all)
   std::deque<std::tuple<double, std::weak_ptr<Conn>, std::string>> delayed;
   double last_flush = 0, flush_due = 0;   // watch output coalescing (Impl::flush_watches)
+  std::atomic<bool> urgent{false};        // flush now, without the linger (a bulk write ended)
   std::mutex mu;
   std::vector<std::shared_ptr<Conn>> flush;   // watch conns with pending output
   std::unordered_map<int, std::shared_ptr<Conn>> conns;
@@ -494,6 +495,15 @@ struct Server::Impl {
     k.push_back('/');
     k.append(name);
     return k;
+  }
+
+  // A bulk write is complete: its last events leave now rather than after the linger.
+  void flush_now() {
+    for (auto& t : io) {
+      t->urgent.store(true, std::memory_order_relaxed);
+      const uint64_t one = 1;
+      (void)!write(t->efd, &one, sizeof one);
+    }
   }
 
   // -- emit under mu
@@ -1200,7 +1210,7 @@ void Server::Impl::io_loop(IoThread* t) {
         // a busy stream is flushed at most once per linger window, so a burst of events
         // leaves as a few large chunks instead of one chunk per event; an idle one at once
         const double now = steady_s();
-        if (now - t->last_flush >= linger_s) flush_watches(t);
+        if (t->urgent.exchange(false) || now - t->last_flush >= linger_s) flush_watches(t);
         else if (t->flush_due == 0) t->flush_due = t->last_flush + linger_s;
         continue;
       }
@@ -1400,6 +1410,7 @@ std::vector<int> Server::create_pods(const std::vector<std::string>& texts, int 
       codes[i] = e.code;
     }
   }
+  impl_->flush_now();
   const auto t2 = std::chrono::steady_clock::now();
   auto ns = [](auto d) { return static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(d).count()); };
   impl_->bulk_parse_ns.fetch_add(ns(t1 - t0), std::memory_order_relaxed);
@@ -1414,6 +1425,7 @@ int Server::delete_pods(const std::vector<std::pair<std::string, std::string>>& 
   // than one thread (allocator contention outweighs ~1 us of work per pod)
   int n = 0;
   for (const auto& k : keys) n += impl_->delete_pod_locked(k.first, k.second) ? 1 : 0;
+  impl_->flush_now();
   impl_->n_delete.fetch_add(static_cast<uint64_t>(keys.size()), std::memory_order_relaxed);
   impl_->bulk_delete_ns.fetch_add(
       static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count()),
