@@ -15,6 +15,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <charconv>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -244,6 +245,9 @@ struct Obj {
   std::string json;
   std::string ns, name, uid, node, phase;
   uint64_t rv = 0;
+  // where metadata.resourceVersion's digits sit in `json` (rv_len 0: not known), so a new
+  // version is spliced without searching the text
+  uint32_t rv_at = 0, rv_len = 0;
   // set before the object is published (seal, restamp), or once by v(); read through
   // atomic_load because restamp may copy it while another thread is building it
   mutable std::once_flag once;
@@ -278,19 +282,35 @@ ObjP seal(JV v, uint64_t rv) {
   auto t = std::make_shared<JV>(std::move(v));
   dump(*t, &o->json);
   o->tree = std::move(t);
+  const std::string digits = std::to_string(rv);
+  const size_t at = o->json.find("\"resourceVersion\":\"" + digits + "\"");
+  if (at != std::string::npos) {
+    o->rv_at = static_cast<uint32_t>(at + 19);   // past "resourceVersion":"
+    o->rv_len = static_cast<uint32_t>(digits.size());
+  }
   return o;
 }
 
 // The same object at a new resourceVersion, text spliced (a delete's final version).
 ObjP restamp(const ObjP& cur, uint64_t rv) {
-  const std::string old = "\"resourceVersion\":\"" + std::to_string(cur->rv) + "\"";
-  const size_t at = cur->json.find(old);
-  if (at == std::string::npos) return seal(cur->v(), rv);   // (not ours: no stamp to splice)
+  size_t at = cur->rv_at, len = cur->rv_len;
+  if (len == 0) {
+    const std::string digits = std::to_string(cur->rv);
+    const size_t hit = cur->json.find("\"resourceVersion\":\"" + digits + "\"");
+    if (hit == std::string::npos) return seal(cur->v(), rv);   // (not ours: no stamp to splice)
+    at = hit + 19;
+    len = digits.size();
+  }
+  char buf[24];
+  const auto res = std::to_chars(buf, buf + sizeof buf, rv);
+  const size_t n = static_cast<size_t>(res.ptr - buf);
   auto o = std::make_shared<Obj>();
   o->json.reserve(cur->json.size() + 4);
   o->json.append(cur->json, 0, at);
-  o->json += "\"resourceVersion\":\"" + std::to_string(rv) + "\"";
-  o->json.append(cur->json, at + old.size(), std::string::npos);
+  o->json.append(buf, n);
+  o->json.append(cur->json, at + len, std::string::npos);
+  o->rv_at = static_cast<uint32_t>(at);
+  o->rv_len = static_cast<uint32_t>(n);
   o->ns = cur->ns, o->name = cur->name, o->uid = cur->uid, o->node = cur->node, o->phase = cur->phase;
   o->rv = rv;
   // the tree (if built) stays usable as the base of later patches, which re-stamp anyway
@@ -556,6 +576,8 @@ struct Server::Impl {
     o->json.append(f.text.substr(0, f.meta_open));
     o->json += ins;
     o->json.append(f.text.substr(f.meta_open));
+    o->rv_at = static_cast<uint32_t>(f.meta_open + 19);
+    o->rv_len = static_cast<uint32_t>(std::to_string(o->rv).size());
     o->ns = f.ns, o->name = f.name, o->uid = f.uid, o->node = f.node, o->phase = f.phase;
     pods.emplace(k, o);
     emit(kPods, "ADDED", o);
