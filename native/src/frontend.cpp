@@ -827,15 +827,31 @@ bool Frontend::handle_native(Worker* w, Conn* c, const std::string& method, cons
 bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* out) {
   // per-thread scratch: the DOM, the name views and the result arrays keep their capacity
   // from one request to the next (every cycle of a burst sends the same-sized bodies)
-  thread_local json::Doc d;
+  thread_local json::Doc top, d;
   thread_local std::vector<std::string_view> nv;
   thread_local std::vector<int32_t> rcs, scores;
-  if (body.empty() || !d.parse(body)) return false;
-  const int32_t root = d.root();
-  if (!d.is(root, json::Type::kObj)) return false;
-  const int32_t names = d.get(root, "NodeNames", true);
-  if (!d.is(names, json::Type::kArr)) return false;     // null / Nodes-only: Python path
-  const int32_t pod = d.get(root, "Pod", true);
+  // The body's top level only (Pod and NodeNames stay unparsed text), then the Pod on its own
+  // (`d`); the node-name list is parsed only when this worker has not seen that exact text.
+  if (body.empty() || !top.parse_shallow(body, 1)) return false;
+  const int32_t root = top.root();
+  if (!top.is(root, json::Type::kObj)) return false;
+  const int32_t names = top.get(root, "NodeNames", true);
+  if (!top.is(names, json::Type::kArr)) return false;     // null / Nodes-only: Python path
+  const int32_t pod_top = top.get(root, "Pod", true);
+  // any other member that is an object or array was only bracket-checked: the whole body
+  // must be valid JSON, as for the Python verb (which answers 400 otherwise)
+  for (int32_t c = top.at(root).first; c >= 0; c = top.at(c).next) {
+    if (c == names || c == pod_top) continue;
+    if (top.is(c, json::Type::kObj) || top.is(c, json::Type::kArr)) {
+      thread_local json::Doc other;
+      if (!other.parse(top.raw(c))) return false;
+    }
+  }
+  int32_t pod = -1;
+  if (pod_top >= 0 && !top.is(pod_top, json::Type::kNull)) {
+    if (!top.is(pod_top, json::Type::kObj) || !d.parse(top.raw(pod_top))) return false;
+    pod = d.root();
+  }
   Demand dem;
   std::memset(&dem, 0, sizeof(dem));
   std::string_view uid;
@@ -915,54 +931,79 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   // kube-scheduler sends the same node list over and over, so each worker remembers the ids
   // of the last lists it resolved (keyed by the array's raw text) and only checks that slot
   // `id` still carries that name; a miss falls back to the ledger's name index.
-  const int32_t nn = d.at(names).count;
-  nv.clear();
-  nv.reserve(nn);
+  const std::string_view raw_names = top.raw(names);
   thread_local std::vector<std::string_view> nraw;   // each name's JSON token, quotes included
+  nv.clear();
   nraw.clear();
-  nraw.reserve(nn);
-  for (int32_t c = d.at(names).first; c >= 0; c = d.at(c).next) {
-    if (!d.is(c, json::Type::kStr)) return false;
-    nv.push_back(d.str(c));
-    // the token is reused as written unless it holds an escape (then it is re-quoted, so the
-    // reply stays byte-identical to the Python verb's json.dumps)
-    const std::string_view tok = d.raw(c);
-    if (tok.size() == nv.back().size() + 2) {
-      nraw.push_back(tok);
-    } else {
-      thread_local std::deque<std::string> requoted;   // stable storage for this request
-      if (nraw.empty()) requoted.clear();
-      requoted.emplace_back();
-      json::append_quoted(&requoted.back(), nv.back());
-      nraw.push_back(requoted.back());
-    }
-  }
   struct IdCache {
     const Ledger* owner = nullptr;
     uint64_t key[4] = {};
+    uint64_t epoch[4] = {};     // the ledger's node epoch the ids were checked at
+    size_t len[4] = {};
     std::vector<int32_t> ids[4];
+    std::vector<std::pair<uint32_t, uint32_t>> tok[4];   // token (offset, length) in the list text
     unsigned next = 0;
   };
   thread_local IdCache idc;
   if (idc.owner != ledger_.get()) idc = IdCache{}, idc.owner = ledger_.get();
-  const std::string_view raw_names = d.raw(names);
   const uint64_t nkey = text_hash(raw_names) | 1;   // 0 marks an empty slot
+  const uint64_t epoch = ledger_->epoch();
   int slot = -1;
   for (int k = 0; k < 4; ++k)
-    if (idc.key[k] == nkey && idc.ids[k].size() == nv.size()) slot = k;
-  if (slot < 0) {
-    slot = static_cast<int>(idc.next++ % 4);
-    idc.key[slot] = nkey;
-    idc.ids[slot].assign(nv.size(), -1);
-  }
-  std::vector<int32_t>& ids = idc.ids[slot];
-  for (size_t i = 0; i < nv.size(); ++i) {
-    if (ids[i] >= 0 && ledger_->node_named(ids[i], nv[i])) continue;
-    ids[i] = ledger_->find_node(std::string(nv[i]));
-    if (ids[i] < 0) {
-      idc.key[slot] = 0;
-      return false;
+    if (idc.key[k] == nkey && idc.len[k] == raw_names.size()) slot = k;
+  if (slot >= 0) {
+    // the same list text as before: its tokens sit at the same offsets (escape-free lists
+    // only are cached); names and ids come from the cache
+    for (const auto& t : idc.tok[slot]) {
+      nraw.push_back(raw_names.substr(t.first, t.second));
+      nv.push_back(raw_names.substr(t.first + 1, t.second - 2));
     }
+  } else {
+    thread_local json::Doc dn;
+    if (!dn.parse(raw_names) || !dn.is(dn.root(), json::Type::kArr)) return false;
+    bool plain = true;
+    for (int32_t c = dn.at(dn.root()).first; c >= 0; c = dn.at(c).next) {
+      if (!dn.is(c, json::Type::kStr)) return false;
+      nv.push_back(dn.str(c));
+      // the token is reused as written unless it holds an escape (then it is re-quoted, so
+      // the reply stays byte-identical to the Python verb's json.dumps)
+      const std::string_view tok = dn.raw(c);
+      if (tok.size() == nv.back().size() + 2) {
+        nraw.push_back(tok);
+      } else {
+        plain = false;
+        thread_local std::deque<std::string> requoted;   // stable storage for this request
+        if (nraw.empty()) requoted.clear();
+        requoted.emplace_back();
+        json::append_quoted(&requoted.back(), nv.back());
+        nraw.push_back(requoted.back());
+      }
+    }
+    slot = static_cast<int>(idc.next++ % 4);
+    idc.key[slot] = plain ? nkey : 0;   // a list with escapes is parsed every time
+    idc.len[slot] = raw_names.size();
+    idc.epoch[slot] = 0;                // ids checked below
+    idc.ids[slot].assign(nv.size(), -1);
+    idc.tok[slot].clear();
+    if (plain)
+      for (const std::string_view t : nraw)
+        idc.tok[slot].emplace_back(static_cast<uint32_t>(t.data() - raw_names.data()), static_cast<uint32_t>(t.size()));
+  }
+  const int32_t nn = static_cast<int32_t>(nv.size());
+  // node ids: any unknown node goes to Python, which can register it from its informer. The
+  // ids of a cached list are re-checked (slot `id` still carries that name, else the ledger's
+  // name index) only when a node was added or removed since (the ledger's epoch moved).
+  std::vector<int32_t>& ids = idc.ids[slot];
+  if (idc.epoch[slot] != epoch) {
+    for (size_t i = 0; i < nv.size(); ++i) {
+      if (ids[i] >= 0 && ledger_->node_named(ids[i], nv[i])) continue;
+      ids[i] = ledger_->find_node(std::string(nv[i]));
+      if (ids[i] < 0) {
+        idc.key[slot] = 0;
+        return false;
+      }
+    }
+    idc.epoch[slot] = epoch;
   }
   Options o;
   bool normalize, nominate;
