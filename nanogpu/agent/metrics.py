@@ -9,6 +9,7 @@ format, joined with what it granted:
     nanogpu_device_info{device,gpu,partition,part,numa,render}       1
     nanogpu_device_healthy{device}                                   1 | 0
     nanogpu_device_busy_percent{device}                              gpu_busy_percent
+    nanogpu_device_mem_busy_percent{device}                          mem_busy_percent (HBM activity)
     nanogpu_device_vram_used_bytes{device} / _vram_total_bytes        mem_info_vram_{used,total}
     nanogpu_device_granted_percent{device}                           sum of container shares
     nanogpu_device_granted_cus{device} / nanogpu_device_cus{device}  CU-mask grants vs CUs
@@ -71,10 +72,11 @@ def render(topo, plugin=None, render_minors: list[int] | None = None, sysfs_root
         out.extend(f"{name}{lab} {val}" for lab, val in rows)
 
     root = Path(sysfs_root or "/")
-    busy, used, total = [], [], []
+    busy, mbusy, used, total = [], [], [], []
     for i, d in enumerate(devs):
         base = root / "sys/class/drm" / f"renderD{minors[i]}" / "device"
-        for rows, f in ((busy, "gpu_busy_percent"), (used, "mem_info_vram_used"), (total, "mem_info_vram_total")):
+        for rows, f in ((busy, "gpu_busy_percent"), (mbusy, "mem_busy_percent"),
+                        (used, "mem_info_vram_used"), (total, "mem_info_vram_total")):
             v = _read_int(base / f)
             if v is not None:
                 rows.append((_labels(device=i), v))
@@ -90,6 +92,7 @@ def render(topo, plugin=None, render_minors: list[int] | None = None, sysfs_root
     family("nanogpu_device_healthy", "gauge", "1 if the device is advertised Healthy to kubelet",
            [(_labels(device=i), int(bool(health[i]))) for i in range(len(devs))])
     family("nanogpu_device_busy_percent", "gauge", "amdgpu gpu_busy_percent", busy)
+    family("nanogpu_device_mem_busy_percent", "gauge", "amdgpu mem_busy_percent (HBM activity)", mbusy)
     family("nanogpu_device_vram_used_bytes", "gauge", "amdgpu mem_info_vram_used", used)
     family("nanogpu_device_vram_total_bytes", "gauge", "amdgpu mem_info_vram_total", total)
     family("nanogpu_device_granted_percent", "gauge", "gpu-percent granted to running containers",

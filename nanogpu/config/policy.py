@@ -88,6 +88,9 @@ AMD_QUERIES = {
     T.GPU_MEMORY_USAGE_METRIC: MetricQuery(
         'gpu_used_vram{{hostname="{node}",gpu_id="{card}"}} / gpu_total_vram{{hostname="{node}",gpu_id="{card}"}}',
         batch='gpu_used_vram{{hostname="{node}"}} / gpu_total_vram{{hostname="{node}"}}', card_labels=("gpu_id",)),
+    T.GPU_HBM_ACTIVITY_METRIC: MetricQuery(
+        'avg_over_time(gpu_umc_activity{{hostname="{node}",gpu_id="{card}"}}[1m]) / 100',
+        batch='avg_over_time(gpu_umc_activity{{hostname="{node}"}}[1m]) / 100', card_labels=("gpu_id",)),
 }
 
 # The node agent's own exporter (nanogpu/agent/metrics.py); assumes the scrape config puts
@@ -101,6 +104,9 @@ AGENT_QUERIES = {
         'nanogpu_device_vram_total_bytes{{node="{node}",device="{card}"}}',
         batch='nanogpu_device_vram_used_bytes{{node="{node}"}} / nanogpu_device_vram_total_bytes{{node="{node}"}}',
         card_labels=("device",)),
+    T.GPU_HBM_ACTIVITY_METRIC: MetricQuery(
+        'avg_over_time(nanogpu_device_mem_busy_percent{{node="{node}",device="{card}"}}[1m]) / 100',
+        batch='avg_over_time(nanogpu_device_mem_busy_percent{{node="{node}"}}[1m]) / 100', card_labels=("device",)),
 }
 PRESETS = {"amd": AMD_QUERIES, "nanogpu-agent": AGENT_QUERIES}
 

@@ -363,6 +363,12 @@ class ClusterState:
         e = self._nodes.get(node_name)
         return bool(e) and self.ledger.set_load(e.id, device, float(usage)) == N.OK
 
+    def set_mem_hot(self, node_name: str, device: int, hot: bool) -> bool:
+        """Measured HBM activity above the threshold (telemetry): the device counts as
+        holding a streaming tenant for memory-bound placement (alloc.h Device::mem_hot)."""
+        e = self._nodes.get(node_name)
+        return bool(e) and self.ledger.set_mem_hot(e.id, device, bool(hot)) == N.OK
+
     # ------------------------------------------------------------------ introspection
     def frag(self, min_request: int = 0) -> dict:
         return self.ledger.frag(min_request)

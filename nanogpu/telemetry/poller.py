@@ -48,6 +48,7 @@ class LoadPoller:
         self.errors = 0
         self.polls = 0        # successful node/metric syncs
         self.queries = 0
+        self.hbm_threshold = T.HBM_HOT_THRESHOLD
 
     # -------------------------------------------------------------- policy changes
     def on_policy(self, spec: PolicySpec) -> None:
@@ -133,9 +134,16 @@ class LoadPoller:
         self.refresh_node(name, n_dev)
 
     def refresh_node(self, name: str, n_dev: int, now: float | None = None) -> None:
-        periods = [(p.name, self.spec.active_duration(p.name)) for p in self.spec.sync_period]
+        # HBM activity marks streaming devices (Device::mem_hot); it is not part of the
+        # reference's load sum
+        periods = [(p.name, self.spec.active_duration(p.name)) for p in self.spec.sync_period
+                   if p.name != T.GPU_HBM_ACTIVITY_METRIC]
+        hbm_active = self.spec.active_duration(T.GPU_HBM_ACTIVITY_METRIC)
         for card in range(n_dev):
             self.state.set_load(name, card, self.store.device_usage(name, card, periods, now))
+            # unpolled (or no longer polled) metric: the mark clears
+            self.state.set_mem_hot(name, card, self.store.hbm_hot(
+                name, card, hbm_active, self.hbm_threshold, now))
 
     def sweep_stale(self) -> None:
         """Re-derives loads so samples that aged out stop counting (called periodically)."""

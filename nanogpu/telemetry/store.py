@@ -12,6 +12,8 @@ import math
 import time
 from dataclasses import dataclass
 
+from .. import types as T
+
 
 @dataclass
 class Sample:
@@ -51,6 +53,14 @@ class TelemetryStore:
                 continue
             total += math.ceil(10 * v) / 10
         return total
+
+    def hbm_hot(self, node: str, card: int, active_s: float, threshold: float, now: float | None = None
+                ) -> bool:
+        """Fresh, valid HBM-activity sample at or above `threshold` (types.GPU_HBM_ACTIVITY_METRIC)."""
+        if active_s <= 0:
+            return False
+        exists, v, err = self.get(node, T.GPU_HBM_ACTIVITY_METRIC, card, active_s, now)
+        return exists and err is None and v >= threshold
 
     def nodes(self) -> set[str]:
         return {k[0] for k in self.data}

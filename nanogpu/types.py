@@ -40,6 +40,12 @@ ANNOTATION_SCHEDULER = "nano-gpu/scheduler"
 # keep them apart from each other on a device (native/include/nanogpu/alloc.h kFlagMemBound)
 ANNOTATION_MEMORY_BOUND = "nano-gpu/memory-bound"
 FLAG_MEM_BOUND = 1
+# Measured memory-boundness: a policy that polls this metric (HBM / memory-controller activity
+# in [0, 1]) marks a device whose activity is at or above HBM_HOT_THRESHOLD as holding a
+# streaming tenant (alloc.h Device::mem_hot), declared or not. It feeds only that mark, not the
+# reference's load sum (RemainLoad), so the reference's load semantics are unchanged.
+GPU_HBM_ACTIVITY_METRIC = "gpu_hbm_activity_avg"
+HBM_HOT_THRESHOLD = 0.5
 AMD_GPU_NODE_LABEL = ("amd.com/gpu.present", "true")   # default telemetry node selector
 
 MI355X_CUS = 256

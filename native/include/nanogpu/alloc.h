@@ -67,7 +67,8 @@ struct Device {
   // mib_free/mib_total and every debit updates all members. -1: the device's own HBM.
   int16_t pool;
   int16_t mem_bound;    // memory-bound share containers placed here (see kFlagMemBound)
-  int32_t pad32;
+  int32_t mem_hot;      // measured: the device's HBM activity is above the policy threshold
+                        // (telemetry, Ledger::set_mem_hot), whatever its tenants declared
   int64_t mib_share;    // HBM a whole-device grant of a pooled member takes (pool / members)
 };
 
@@ -82,7 +83,9 @@ struct Topology {
 // the MI355X box two streaming tenants with 25 % / 75 % masks split the HBM bandwidth
 // 25 / 75, while a 25 % tenant alone reaches 51 % of it (profiles/gpu_calibration.md). So
 // native policies place a memory-bound share on the device with the fewest memory-bound
-// tenants first, next to compute-bound neighbours, before the policy's own order.
+// tenants first, next to compute-bound neighbours, before the policy's own order. A device
+// whose measured HBM activity is high (Device::mem_hot) counts as holding one more streaming
+// tenant, so undeclared streaming workloads are seen too.
 constexpr int32_t kFlagMemBound = 1;
 
 struct ContainerDemand {

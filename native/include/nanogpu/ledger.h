@@ -195,6 +195,8 @@ class Ledger {
   // Load-aware telemetry (reference nodeusage.go + allocate.go:173-195).
   int32_t set_load(int32_t id, int dev, float usage);
   int32_t set_health(int32_t id, int dev, bool healthy);
+  // measured HBM activity above the policy threshold (Device::mem_hot)
+  int32_t set_mem_hot(int32_t id, int dev, bool hot);
 
   FragStats frag(int32_t min_request) const;
 

@@ -362,7 +362,8 @@ int pick_share(Work& w, const Topology* t, const ContainerDemand& c, const Optio
       k1 = -k1;  // worst fit: most free first
       k2 = -k2;
     }
-    const int64_t k0 = membound ? d.mem_bound : 0;   // fewest memory-bound neighbours first
+    // fewest memory-bound neighbours first, declared or measured
+    const int64_t k0 = membound ? d.mem_bound + (d.mem_hot ? 1 : 0) : 0;
     bool better;
     if (best < 0) better = true;
     else if (k0 != bk0) better = k0 < bk0;
@@ -706,7 +707,8 @@ static int32_t native_rate(const Device* devs, int n, const Demand& d, const Opt
     for (int c = 0; c < plan->n && c < d.n; ++c) {
       if (!(d.c[c].flags & kFlagMemBound) || d.c[c].pct > kPercentPerDevice) continue;
       for (int k = plan->off[c]; k < plan->off[c + 1]; ++k)
-        if (plan->idx[k] >= 0 && devs[plan->idx[k]].mem_bound > 0) ++crowded;
+        if (plan->idx[k] >= 0 && (devs[plan->idx[k]].mem_bound > 0 || devs[plan->idx[k]].mem_hot))
+          ++crowded;
     }
     s -= 15.0 * crowded;
   }

@@ -67,6 +67,7 @@ Device to_device(const py::dict& d) {
   v.cus = get<int32_t>(d, "cus", 0);
   v.pool = get<int16_t>(d, "pool", -1);
   v.mib_share = get<int64_t>(d, "mib_share", 0);
+  v.mem_hot = get<bool>(d, "mem_hot", false) ? 1 : 0;
   if (v.pool >= 0 && v.mib_share <= 0) v.mib_share = v.mib_total;
   return v;
 }
@@ -88,6 +89,7 @@ py::dict from_device(const Device& v) {
   d["pool"] = v.pool;
   d["mib_share"] = v.mib_share;
   d["mem_bound"] = v.mem_bound;
+  d["mem_hot"] = v.mem_hot != 0;
   return d;
 }
 
@@ -700,6 +702,7 @@ PYBIND11_MODULE(_native, m) {
           "tentative reservation for the top-scored node (priorities); adopted by reserve()")
       .def("set_load", &Ledger::set_load)
       .def("set_health", &Ledger::set_health)
+      .def("set_mem_hot", &Ledger::set_mem_hot)
       .def("frag", [](const Ledger& l, int32_t min_request) { return frag_dict(l.frag(min_request)); },
            py::arg("min_request") = 0)
       .def("learned_sizes", [](const Ledger& l) { return size_list(l.learned_sizes()); },

@@ -291,6 +291,7 @@ int32_t Ledger::upsert_node(const std::string& name, const Device* devs, int n,
       s.devs[i].pct_free = s.devs[i].pct_total;
       s.devs[i].mib_free = s.devs[i].mib_total;
       s.devs[i].mem_bound = 0;
+      s.devs[i].mem_hot = 0;
     }
     s.in_use = 1;
     hdr_->n_nodes.store(count + 1, std::memory_order_release);
@@ -311,10 +312,12 @@ int32_t Ledger::upsert_node(const std::string& name, const Device* devs, int n,
         merged[i].load_usage = old.load_usage;
         merged[i].remain_load = old.remain_load;
         merged[i].mem_bound = old.mem_bound;
+        merged[i].mem_hot = old.mem_hot;
       } else {
         merged[i].pct_free = merged[i].pct_total;
         merged[i].mib_free = merged[i].mib_total;
         merged[i].mem_bound = 0;
+        merged[i].mem_hot = 0;
       }
     }
     // Devices that vanished while still in use stay (unhealthy) until their pods release.
@@ -893,6 +896,20 @@ int32_t Ledger::set_load(int32_t id, int dev, float usage) {
   Device& d = n->devs[dev];
   d.load_usage = usage;
   d.remain_load = static_cast<int16_t>(kLoadTotal - static_cast<int>(usage));
+  n->generation.fetch_add(1, std::memory_order_release);
+  hdr_->epoch.fetch_add(1);
+  return kOk;
+}
+
+int32_t Ledger::set_mem_hot(int32_t id, int dev, bool hot) {
+  NodeSlot* n = node(id);
+  if (!n) return kErrUnknownNode;
+  lock_node(n);
+  Unlock un{&n->mu};
+  if (dev < 0 || dev >= n->n_devs) return kErrBadPlan;
+  Device& d = n->devs[dev];
+  if ((d.mem_hot != 0) == hot) return kOk;   // unchanged: cached plans stay valid
+  d.mem_hot = hot ? 1 : 0;
   n->generation.fetch_add(1, std::memory_order_release);
   hdr_->epoch.fetch_add(1);
   return kOk;

@@ -327,3 +327,22 @@ def test_agent_selftest_marks_failing_devices_unhealthy():
         await agent.stop()
 
     asyncio.run(main())
+
+
+def test_agent_metrics_export_hbm_activity_from_sysfs(tmp_path):
+    """mem_busy_percent (amdgpu's memory-controller activity) is exported per device as
+    nanogpu_device_mem_busy_percent, the series the nanogpu-agent preset's HBM-activity query
+    reads (types.GPU_HBM_ACTIVITY_METRIC -> Device::mem_hot)."""
+    from nanogpu.agent.metrics import render as render_metrics
+    from nanogpu.topology.model import synthetic_mi355x
+
+    topo = synthetic_mi355x(2)
+    for i, (busy, mbusy) in enumerate(((40, 85), (3, 0))):
+        d = tmp_path / "sys/class/drm" / f"renderD{128 + 8 * i}" / "device"
+        d.mkdir(parents=True)
+        (d / "gpu_busy_percent").write_text(f"{busy}\n")
+        (d / "mem_busy_percent").write_text(f"{mbusy}\n")
+    text = render_metrics(topo, None, None, str(tmp_path))
+    assert 'nanogpu_device_mem_busy_percent{device="0"} 85' in text
+    assert 'nanogpu_device_mem_busy_percent{device="1"} 0' in text
+    assert 'nanogpu_device_busy_percent{device="0"} 40' in text

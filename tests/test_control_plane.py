@@ -530,3 +530,52 @@ def test_preemption_route_over_http():
             await rt.stop()
 
     asyncio.run(main())
+
+
+def test_measured_hbm_activity_steers_memory_bound_shares_without_touching_load():
+    """A device whose measured HBM activity (types.GPU_HBM_ACTIVITY_METRIC, the agent's
+    nanogpu_device_mem_busy_percent) is at or above the threshold counts as holding a streaming
+    tenant, declared or not: a memory-bound share goes to the quiet device, a compute-bound one
+    still packs best-fit. The metric stays out of the reference's load sum (RemainLoad)."""
+    from nanogpu.k8s.podutil import Req
+
+    async def main():
+        series = {T.GPU_HBM_ACTIVITY_METRIC: {("n0", 0): [0.85], ("n0", 1): [0.10]}}
+        runner, port, _ = await fake_prometheus(series)
+        st = ClusterState(policy="binpack", load_aware=True)
+        n = node("n0", 2)
+        st.register_node(n)
+        nid = st.node_entry("n0").id
+        assert st.ledger.reserve(nid, "cb", [(30, 0)], st.options)[0] == N.OK   # device 0 is fuller
+        spec = PolicySpec(sync_period=(Period(T.GPU_HBM_ACTIVITY_METRIC, 15),))
+        poller = LoadPoller(st, PromClient(f"http://127.0.0.1:{port}"), lambda: [n], spec=spec)
+        mb = [Req(20, 0, N.FLAG_MEM_BOUND)]
+        try:
+            _, plan, _ = st.ledger.assume(nid, mb, st.options)
+            assert plan == [[0]]                      # nothing measured yet: best fit
+            await poller.sync_metric(T.GPU_HBM_ACTIVITY_METRIC)
+            devs = st.ledger.snapshot(nid)["devices"]
+            assert [d["mem_hot"] for d in devs] == [True, False]
+            assert [d["remain_load"] for d in devs] == [T.LOAD_TOTAL, T.LOAD_TOTAL]   # not load
+            _, plan, _ = st.ledger.assume(nid, mb, st.options)
+            assert plan == [[1]]                      # the measured streamer is avoided
+            _, plan, _ = st.ledger.assume(nid, [(20, 0)], st.options)
+            assert plan == [[0]]                      # compute-bound shares still pack
+            # a stale sample (period + 5 min) clears the mark
+            poller.refresh_node("n0", 2, now=1e12)
+            assert [d["mem_hot"] for d in st.ledger.snapshot(nid)["devices"]] == [False, False]
+            _, plan, _ = st.ledger.assume(nid, mb, st.options)
+            assert plan == [[0]]
+        finally:
+            await poller.prom.close()
+            await runner.cleanup()
+
+    asyncio.run(main())
+
+
+def test_hbm_activity_presets_query_the_agent_and_the_amd_exporter():
+    for preset, needle in (("nanogpu-agent", "nanogpu_device_mem_busy_percent"), ("amd", "gpu_umc_activity")):
+        spec = parse_policy(f"spec:\n  metricsPreset: {preset}\n  syncPeriod:\n"
+                            f"  - name: {T.GPU_HBM_ACTIVITY_METRIC}\n    period: 15s\n")
+        q = spec.query_for(T.GPU_HBM_ACTIVITY_METRIC)
+        assert needle in q.query and needle in q.batch and "{card}" not in q.batch

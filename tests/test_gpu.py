@@ -254,6 +254,9 @@ def test_agent_metrics_read_real_amdgpu_sysfs(host, P):
     text = render(topo, None, minors)
     busy = re.search(r'nanogpu_device_busy_percent\{device="0"\} (\d+)', text)
     assert busy and 0 <= int(busy.group(1)) <= 100
+    mbusy = re.search(r'nanogpu_device_mem_busy_percent\{device="0"\} (\d+)', text)
+    print("mem_busy_percent:", mbusy.group(1) if mbusy else "not exposed by this device")
+    assert mbusy is None or 0 <= int(mbusy.group(1)) <= 100
     assert f'nanogpu_device_vram_total_bytes{{device="0"}} {host["gpus"][0]["vram_bytes"]}' in text
     import time
 
