@@ -71,6 +71,10 @@ class MetricQuery:
     # card in the first of `card_labels` it carries. None: one query per card (the reference).
     batch: str | None = None
     card_labels: tuple[str, ...] = ("card",)
+    # One query for every node and card ({metric} only); each series names its node in the
+    # first of `node_labels` it carries. Used when the policy sets `metricsScope: cluster`.
+    cluster: str | None = None
+    node_labels: tuple[str, ...] = ("node",)
 
 
 # Reference query shapes (prometheus.go:70-76) as the default templates.
@@ -80,17 +84,21 @@ REFERENCE_FALLBACK = '{metric}{{node="{node}",cardNode="{card}"}} /100'
 # over `cardNode` ones (the fallback's label)
 REFERENCE_BATCH = '{metric}{{node=~"{node}"}} /100'
 REFERENCE_CARD_LABELS = ("card", "cardNode")
+REFERENCE_CLUSTER = '{metric} /100'
 # AMD device-metrics-exporter shaped templates (gfx / memory-controller activity in %).
 AMD_QUERIES = {
     T.GPU_CORE_USAGE_METRIC: MetricQuery(
         'avg_over_time(gpu_gfx_activity{{hostname="{node}",gpu_id="{card}"}}[1m]) / 100',
-        batch='avg_over_time(gpu_gfx_activity{{hostname="{node}"}}[1m]) / 100', card_labels=("gpu_id",)),
+        batch='avg_over_time(gpu_gfx_activity{{hostname="{node}"}}[1m]) / 100', card_labels=("gpu_id",),
+        cluster='avg_over_time(gpu_gfx_activity[1m]) / 100', node_labels=("hostname",)),
     T.GPU_MEMORY_USAGE_METRIC: MetricQuery(
         'gpu_used_vram{{hostname="{node}",gpu_id="{card}"}} / gpu_total_vram{{hostname="{node}",gpu_id="{card}"}}',
-        batch='gpu_used_vram{{hostname="{node}"}} / gpu_total_vram{{hostname="{node}"}}', card_labels=("gpu_id",)),
+        batch='gpu_used_vram{{hostname="{node}"}} / gpu_total_vram{{hostname="{node}"}}', card_labels=("gpu_id",),
+        cluster='gpu_used_vram / gpu_total_vram', node_labels=("hostname",)),
     T.GPU_HBM_ACTIVITY_METRIC: MetricQuery(
         'avg_over_time(gpu_umc_activity{{hostname="{node}",gpu_id="{card}"}}[1m]) / 100',
-        batch='avg_over_time(gpu_umc_activity{{hostname="{node}"}}[1m]) / 100', card_labels=("gpu_id",)),
+        batch='avg_over_time(gpu_umc_activity{{hostname="{node}"}}[1m]) / 100', card_labels=("gpu_id",),
+        cluster='avg_over_time(gpu_umc_activity[1m]) / 100', node_labels=("hostname",)),
 }
 
 # The node agent's own exporter (nanogpu/agent/metrics.py); assumes the scrape config puts
@@ -98,15 +106,17 @@ AMD_QUERIES = {
 AGENT_QUERIES = {
     T.GPU_CORE_USAGE_METRIC: MetricQuery(
         'avg_over_time(nanogpu_device_busy_percent{{node="{node}",device="{card}"}}[1m]) / 100',
-        batch='avg_over_time(nanogpu_device_busy_percent{{node="{node}"}}[1m]) / 100', card_labels=("device",)),
+        batch='avg_over_time(nanogpu_device_busy_percent{{node="{node}"}}[1m]) / 100', card_labels=("device",),
+        cluster='avg_over_time(nanogpu_device_busy_percent[1m]) / 100'),
     T.GPU_MEMORY_USAGE_METRIC: MetricQuery(
         'nanogpu_device_vram_used_bytes{{node="{node}",device="{card}"}} / '
         'nanogpu_device_vram_total_bytes{{node="{node}",device="{card}"}}',
         batch='nanogpu_device_vram_used_bytes{{node="{node}"}} / nanogpu_device_vram_total_bytes{{node="{node}"}}',
-        card_labels=("device",)),
+        card_labels=("device",), cluster='nanogpu_device_vram_used_bytes / nanogpu_device_vram_total_bytes'),
     T.GPU_HBM_ACTIVITY_METRIC: MetricQuery(
         'avg_over_time(nanogpu_device_mem_busy_percent{{node="{node}",device="{card}"}}[1m]) / 100',
-        batch='avg_over_time(nanogpu_device_mem_busy_percent{{node="{node}"}}[1m]) / 100', card_labels=("device",)),
+        batch='avg_over_time(nanogpu_device_mem_busy_percent{{node="{node}"}}[1m]) / 100', card_labels=("device",),
+        cluster='avg_over_time(nanogpu_device_mem_busy_percent[1m]) / 100'),
 }
 PRESETS = {"amd": AMD_QUERIES, "nanogpu-agent": AGENT_QUERIES}
 
@@ -120,6 +130,9 @@ class PolicySpec:
     topology_weight: float | None = None
     score_normalize: bool | None = None
     metrics: tuple[tuple[str, MetricQuery], ...] = ()
+    # "node": one query per GPU node and metric each period, failures backed off per node (the
+    # reference's node/metric keys). "cluster": one query per metric for the whole cluster.
+    metrics_scope: str = "node"
 
     def period_of(self, name: str) -> float:
         for p in self.sync_period:
@@ -136,7 +149,8 @@ class PolicySpec:
         for k, q in self.metrics:
             if k == name:
                 return q
-        return MetricQuery(REFERENCE_QUERY, REFERENCE_FALLBACK, REFERENCE_BATCH, REFERENCE_CARD_LABELS)
+        return MetricQuery(REFERENCE_QUERY, REFERENCE_FALLBACK, REFERENCE_BATCH, REFERENCE_CARD_LABELS,
+                           REFERENCE_CLUSTER)
 
 
 def parse_policy(text: str) -> PolicySpec:
@@ -158,12 +172,18 @@ def parse_policy(text: str) -> PolicySpec:
         metrics.extend(PRESETS[preset].items())
     for name, q in (spec.get("metrics") or {}).items():
         labels = q.get("cardLabel") or ["card"]
+        nlabels = q.get("nodeLabel") or ["node"]
         metrics.append((name, MetricQuery(q["query"], q.get("fallback"), q.get("batch"),
-                                          tuple([labels] if isinstance(labels, str) else labels))))
+                                          tuple([labels] if isinstance(labels, str) else labels),
+                                          q.get("cluster"),
+                                          tuple([nlabels] if isinstance(nlabels, str) else nlabels))))
+    scope = spec.get("metricsScope", "node")
+    if scope not in ("node", "cluster"):
+        raise ValueError(f"unknown metricsScope {scope!r} (node or cluster)")
     return PolicySpec(
         sync_period=tuple(periods), priority=prio, policy=pol,
         compat=sch.get("compat"), topology_weight=sch.get("topologyWeight"),
-        score_normalize=sch.get("scoreNormalize"), metrics=tuple(metrics))
+        score_normalize=sch.get("scoreNormalize"), metrics=tuple(metrics), metrics_scope=scope)
 
 
 def load_policy(path: str) -> PolicySpec:

@@ -22,6 +22,7 @@ from ..k8s.informer import WorkQueue
 from .store import TelemetryStore
 
 log = logging.getLogger(__name__)
+CLUSTER_KEY = "*"          # queue key prefix of a cluster-scoped metric (never a node name)
 
 
 def is_gpu_node(node: dict, selectors: list[tuple[str, str]]) -> bool:
@@ -84,8 +85,15 @@ class LoadPoller:
             self.enqueue(metric)
             await asyncio.sleep(period)
 
+    def cluster_scoped(self, metric: str) -> bool:
+        return self.spec.metrics_scope == "cluster" and self.spec.query_for(metric).cluster is not None
+
     def enqueue(self, metric: str) -> int:
-        """One period tick (reference syncMetric, node.go:45-55): every GPU node's key."""
+        """One period tick (reference syncMetric, node.go:45-55): every GPU node's key, or the
+        one cluster-wide key `*/metric` under `metricsScope: cluster`."""
+        if self.cluster_scoped(metric):
+            self.queue.add(f"{CLUSTER_KEY}/{metric}")
+            return 1
         n = 0
         for node in self.list_nodes():
             if is_gpu_node(node, self.selectors):
@@ -95,11 +103,17 @@ class LoadPoller:
 
     async def sync_metric(self, metric: str) -> None:
         """Polls `metric` on every GPU node now (no retries): tests and one-shot use."""
+        if self.cluster_scoped(metric):
+            await self.sync_cluster(metric)
+            return
         await asyncio.gather(*(self.sync_node(n, metric) for n in self.list_nodes()
                                if is_gpu_node(n, self.selectors)), return_exceptions=True)
 
     async def _sync_key(self, key: str) -> None:
         name, _, metric = key.rpartition("/")
+        if name == CLUSTER_KEY:
+            await self.sync_cluster(metric)
+            return
         node = next((n for n in self.list_nodes() if pu.meta(n).get("name") == name), None)
         if node is None or not is_gpu_node(node, self.selectors):
             return                                   # node gone or no longer a GPU node
@@ -132,6 +146,32 @@ class LoadPoller:
             raise
         self.polls += 1
         self.refresh_node(name, n_dev)
+
+    async def sync_cluster(self, metric: str) -> None:
+        """Every GPU node's cards for one metric from one query; raises on a failed query (the
+        one key backs off). A node absent from the answer keeps its samples until they age out,
+        as a node whose per-node query returned no series would."""
+        q = self.spec.query_for(metric)
+        try:
+            self.queries += 1
+            res = await self.prom.query_cluster(metric, q)
+        except asyncio.CancelledError:
+            raise
+        except Exception as e:
+            self.errors += 1
+            log.debug("metric %s (cluster): %s", metric, e)
+            raise
+        for node in self.list_nodes():
+            if not is_gpu_node(node, self.selectors):
+                continue
+            name = pu.meta(node).get("name", "")
+            entry = self.state.node_entry(name)
+            n_dev = len(entry.topology.devices) if entry else pu.node_gpu_count(node)
+            for card, v in res.get(name, {}).items():
+                if 0 <= card < n_dev:
+                    self.store.update(name, metric, card, v)
+            self.polls += 1
+            self.refresh_node(name, n_dev)
 
     def refresh_node(self, name: str, n_dev: int, now: float | None = None) -> None:
         # HBM activity marks streaming devices (Device::mem_hot); it is not part of the

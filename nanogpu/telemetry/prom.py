@@ -58,13 +58,10 @@ class PromClient:
             out.append((el.get("metric") or {}, v))
         return out
 
-    async def query_node(self, node: str, metric: str, q: MetricQuery) -> dict[int, float]:
-        """Every card of `node` in one query (q.batch): {card: last sample}. A series names its
-        card in the first of q.card_labels it carries; earlier labels win (the reference's
-        primary `card` over its fallback `cardNode`, prometheus.go:70-76)."""
-        res = await self.query(q.batch.format(metric=metric, node=node))
-        out: dict[int, float] = {}
-        rank: dict[int, int] = {}
+    @staticmethod
+    def _by_card(res, q: MetricQuery, out: dict[int, float], rank: dict[int, int]) -> None:
+        """A series names its card in the first of q.card_labels it carries; earlier labels win
+        (the reference's primary `card` over its fallback `cardNode`, prometheus.go:70-76)."""
         for labels, v in res:
             for r, lab in enumerate(q.card_labels):
                 raw = labels.get(lab)
@@ -77,6 +74,26 @@ class PromClient:
                 if card not in rank or r <= rank[card]:   # later samples of equal rank win
                     out[card], rank[card] = round(v, 5), r
                 break
+
+    async def query_node(self, node: str, metric: str, q: MetricQuery) -> dict[int, float]:
+        """Every card of `node` in one query (q.batch): {card: last sample}."""
+        res = await self.query(q.batch.format(metric=metric, node=node))
+        out: dict[int, float] = {}
+        self._by_card(res, q, out, {})
+        return out
+
+    async def query_cluster(self, metric: str, q: MetricQuery) -> dict[str, dict[int, float]]:
+        """Every node and card in one query (q.cluster): {node: {card: last sample}}. A series
+        names its node in the first of q.node_labels it carries; series without one are skipped."""
+        res = await self.query(q.cluster.format(metric=metric))
+        groups: dict[str, list] = {}
+        for labels, v in res:
+            node = next((labels[k] for k in q.node_labels if labels.get(k)), None)
+            if node is not None:
+                groups.setdefault(node, []).append((labels, v))
+        out: dict[str, dict[int, float]] = {}
+        for node, rows in groups.items():
+            self._by_card(rows, q, out.setdefault(node, {}), {})
         return out
 
     async def query_latest(self, node: str, metric: str, card: int, q: MetricQuery) -> float | None:

@@ -197,6 +197,12 @@ async def fake_prometheus(series):
         for metric, by in series.items():
             if metric in ("fail_nodes", "slow_nodes"):
                 continue
+            if q.startswith(metric) and "node" not in q:
+                # cluster-wide query: every node and card (plus one series with no node label)
+                res = [{"metric": {"node": n, "card": str(c)}, "value": [0, str(v)]}
+                       for (n, c), vals in by.items() for v in vals]
+                res.append({"metric": {"card": "0"}, "value": [0, "0.99"]})
+                return web.json_response({"status": "success", "data": {"resultType": "vector", "result": res}})
             if q.startswith(metric) and 'card="' not in q and 'cardNode="' not in q:
                 # batched query: every card of the node, each series labelled with its card
                 res = [{"metric": {"node": n, "card": str(c)}, "value": [0, str(v)]}
@@ -579,3 +585,37 @@ def test_hbm_activity_presets_query_the_agent_and_the_amd_exporter():
                             f"  - name: {T.GPU_HBM_ACTIVITY_METRIC}\n    period: 15s\n")
         q = spec.query_for(T.GPU_HBM_ACTIVITY_METRIC)
         assert needle in q.query and needle in q.batch and "{card}" not in q.batch
+
+
+def test_cluster_scoped_metrics_one_query_per_metric_for_every_node():
+    """`metricsScope: cluster`: one PromQL query per metric and period for the whole cluster
+    (series grouped by their node label) instead of one per node: 1000 GPU nodes cost one query
+    per 15 s, not 1000. A failed query backs off its one key; node-scoped is the default."""
+    async def main():
+        names = [f"n{i}" for i in range(5)]
+        series = {"gpu_core_usage_avg": {(n, c): [0.05 if n != "n3" else 0.95] for n in names for c in range(2)}}
+        runner, port, hits = await fake_prometheus(series)
+        st = ClusterState(load_aware=True)
+        nodes = [node(n, 2) for n in names]
+        for n in nodes:
+            st.register_node(n)
+        spec = parse_policy("spec:\n  metricsScope: cluster\n  syncPeriod:\n"
+                            "  - {name: gpu_core_usage_avg, period: 15s}\n")
+        assert spec.metrics_scope == "cluster"
+        poller = LoadPoller(st, PromClient(f"http://127.0.0.1:{port}"), lambda: nodes, spec=spec)
+        try:
+            assert poller.enqueue("gpu_core_usage_avg") == 1 and poller.queue.queued == {"*/gpu_core_usage_avg"}
+            await poller.sync_metric("gpu_core_usage_avg")
+            assert hits == ["gpu_core_usage_avg /100"]
+            status = st.status()
+            assert [g["RemainLoad"] for g in status["n3"]["GPUs"]] == [1, 1]    # usage ceil(9.5)/10 = 1.0
+            assert all(g["RemainLoad"] == 2 for n in names if n != "n3" for g in status[n]["GPUs"])
+            assert poller.polls == len(names)
+        finally:
+            await poller.prom.close()
+            await runner.cleanup()
+        with pytest.raises(ValueError):
+            parse_policy("spec:\n  metricsScope: region\n")
+        assert parse_policy("spec: {}\n").metrics_scope == "node"
+
+    asyncio.run(main())
