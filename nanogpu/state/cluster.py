@@ -387,7 +387,10 @@ class ClusterState:
                           "RemainLoad": d["remain_load"], "MemoryMiB": d["mib_free"],
                           "MemoryMiBTotal": d["mib_total"], "MemoryPool": d["pool"], "GPU": d["gpu"],
                           "Partition": d["part"],
-                          "Healthy": d["healthy"]} for d in snap["devices"]],
+                          "Healthy": d["healthy"],
+                          # streaming tenants: declared (nano-gpu/memory-bound) and measured
+                          "MemoryBoundTenants": d["mem_bound"], "HBMHot": d["mem_hot"]}
+                         for d in snap["devices"]],
                 "PlanCache": self._plan_cache(e.id),
                 "Generation": snap["generation"],
             }

@@ -49,7 +49,9 @@ def render(status: dict, node_filter: str = "") -> str:
                 " (pool)" if shared else "")
             rows.append(f"{name[:20]:<20} {i:>3}  {g.get('GPU', i):>3} {g.get('Partition', 0):>4}  "
                         f"{100 * used // max(1, total):>4}%  [{_bar(used, total)}]  {hbm:<13} "
-                        f"{'ok' if g.get('Healthy', True) else 'UNHEALTHY'}")
+                        f"{'ok' if g.get('Healthy', True) else 'UNHEALTHY'}"
+                        + (f"  streaming x{g.get('MemoryBoundTenants', 0)}" if g.get("MemoryBoundTenants") else "")
+                        + ("  HBM-hot" if g.get("HBMHot") else ""))
     frag = 100.0 * partial / free_pct if free_pct else 0.0
     rows.append(f"\n{len(status)} nodes, {tot_pct // 100} devices, {free_pct / 100:.1f} device-equivalents free, "
                 f"{frag:.1f}% of the free compute is on partly used devices")

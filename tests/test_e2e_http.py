@@ -231,10 +231,13 @@ def test_top_cli_reports_an_unreachable_extender(capsys):
     assert top.main(["--url", "http://127.0.0.1:9"]) == 1      # discard port: refused
     assert "nanogpu.top: http://127.0.0.1:9" in capsys.readouterr().err
     st = {"n1": {"GPUs": [{"Percent": 50, "PercentTotal": 100, "MemoryMiB": 1024, "MemoryMiBTotal": 4096,
-                           "MemoryPool": 0, "GPU": 0, "Partition": 0, "Healthy": True},
+                           "MemoryPool": 0, "GPU": 0, "Partition": 0, "Healthy": True,
+                           "MemoryBoundTenants": 1, "HBMHot": True},
                           {"Percent": 100, "PercentTotal": 100, "MemoryMiB": 1024, "MemoryMiBTotal": 4096,
                            "MemoryPool": 0, "GPU": 0, "Partition": 1, "Healthy": False}]}}
     out = top.render(st).splitlines()
     assert "50%" in out[1] and "(pool)" not in out[1]
+    assert out[1].endswith("ok  streaming x1  HBM-hot")            # declared + measured streamers
+    assert "streaming" not in out[2] and "HBM-hot" not in out[2]
     assert "(pool)" in out[2] and "UNHEALTHY" in out[2]          # second member of one HBM pool
     assert "1.5 device-equivalents free, 33.3% of the free compute" in out[-1]
