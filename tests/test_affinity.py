@@ -74,3 +74,22 @@ def test_bench_api_server_keeps_off_every_ranks_domain(tmp_path, monkeypatch):
     assert A.pick_cpus_avoiding(taken, near=0) == [20, 21, 22, 23]   # socket 0 has no free domain but CPU 0's
     assert A.pick_cpus_avoiding(taken[:4], near=0) == [8, 9, 10, 11]
     assert A.pick_cpus_avoiding(taken[:4], near=1) == [12, 13, 14, 15]
+
+
+def test_bench_api_server_stays_on_rank0s_socket_unless_it_is_busy(tmp_path, monkeypatch):
+    """A near-socket domain that is a little busier (a shared host) still beats an idle domain
+    on the far socket: every bind and watch event would cross the socket otherwise. Only a
+    near domain at least half busy loses to a quieter far one."""
+    allowed = make_tree(tmp_path)
+    real_l3, real_numa = A.l3_domains, A.numa_of_cpu
+    monkeypatch.setattr(A.os, "sched_getaffinity", lambda pid: allowed)
+    monkeypatch.setattr(A, "l3_domains", lambda allowed=None, root=tmp_path: real_l3(allowed, root))
+    monkeypatch.setattr(A, "numa_of_cpu", lambda cpu, root=tmp_path: real_numa(cpu, root))
+    busy = {c: 0.0 for c in range(24)}
+    busy.update({c: 0.2 for c in (8, 9, 10, 11)})          # socket 0's free domain: lightly used
+    monkeypatch.setattr(A, "_busy", lambda cpus, w: {c: busy[c] for c in cpus})
+    taken = A.pick_cpus(0, 0, [0])                          # rank 0 on socket 0
+    assert A.numa_of_cpu(taken[0]) == 0
+    assert A.pick_cpus_avoiding(taken, near=0) == [8, 9, 10, 11]
+    busy.update({c: 0.7 for c in (8, 9, 10, 11)})           # now mostly busy: go far
+    assert A.numa_of_cpu(A.pick_cpus_avoiding(taken, near=0)[0]) == 1
