@@ -49,7 +49,12 @@ def test_agent_daemonset_args_parse():
 def test_policy_configmap_loads():
     cm = next(d for d in _docs("policy-configmap.yaml") if d["kind"] == "ConfigMap")
     spec = parse_policy(cm["data"]["policy.yaml"])
-    assert {name for name, _ in spec.metrics} >= {"gpu_core_usage_avg", "gpu_memory_usage_avg"}
+    assert {name for name, _ in spec.metrics} >= {"gpu_core_usage_avg", "gpu_memory_usage_avg",
+                                                  T.GPU_HBM_ACTIVITY_METRIC}
+    assert spec.metrics_scope == "cluster"
+    for name, q in spec.metrics:      # every metric can be polled cluster-wide, by the exporter's labels
+        assert q.cluster and "{node}" not in q.cluster and q.node_labels == ("hostname",)
+        assert q.card_labels == ("gpu_id",)
 
 
 def test_scheduler_config_matches_the_served_routes():
