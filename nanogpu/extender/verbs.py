@@ -138,7 +138,7 @@ class Extender:
         args = PreemptionArgs.decode(body)
         keep: dict[str, list[str]] = {}
         try:
-            demand, _ = pu.ledger_view(pu.pod_demand(args.pod))
+            demand, _ = pu.ledger_view(self.state.pod_demand(args.pod))
         except pu.TooManyGpuContainers:
             return preemption_result(keep, args.pdb)
         with self.tracer.span("preempt", pu.pod_key(args.pod)) as sp:

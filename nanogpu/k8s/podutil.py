@@ -95,11 +95,25 @@ _DEMAND_CACHE: dict[str, Demand] = {}
 _DEMAND_CACHE_CAP = 65536
 
 
-def pod_demand(pod: dict) -> Demand:
+def controller_uid(pod: dict) -> str:
+    """UID of the pod's controlling owner (the first ownerReferences entry with controller:
+    true, else the first entry); "" when there is none (frontend.cpp controller_uid)."""
+    refs = [r for r in (meta(pod).get("ownerReferences") or []) if isinstance(r, dict) and r.get("uid")]
+    for r in refs:
+        if r.get("controller") is True:
+            return str(r["uid"])
+    return str(refs[0]["uid"]) if refs else ""
+
+
+def pod_demand(pod: dict, is_stream_owner=None) -> Demand:
     """allocate.go:54-62 (+ HBM MiB as the second dimension). Init containers are ignored.
 
     Container resources are immutable for the life of a pod UID, so the parsed demand is
-    memoised per UID (filter, prioritize, bind and the controller all ask for it)."""
+    memoised per UID (filter, prioritize, bind and the controller all ask for it).
+    `is_stream_owner(uid)` (the ledger's learned streaming owners): a pod with no
+    nano-gpu/memory-bound annotation whose controlling owner was measured streaming HBM counts
+    as memory-bound; "false" opts out. Decided at the pod's first sight, so its filter and its
+    bind see the same demand."""
     uid = meta(pod).get("uid")
     if uid:
         d = _DEMAND_CACHE.get(uid)
@@ -107,6 +121,10 @@ def pod_demand(pod: dict) -> Demand:
             return d
     cs = containers(pod)
     mb = (meta(pod).get("annotations") or {}).get(T.ANNOTATION_MEMORY_BOUND)
+    if mb is None and is_stream_owner is not None:
+        owner = controller_uid(pod)
+        if owner and is_stream_owner(owner):
+            mb = "true"
     if mb:
         names = None if mb == "true" else {x.strip() for x in mb.split(",") if x.strip()}
         d = [Req(container_percent(c), container_mib(c),

@@ -192,13 +192,17 @@ class ClusterState:
             out.append(e.id if e else -1)
         return out
 
+    def pod_demand(self, pod: dict):
+        """The pod's demand; an unannotated pod of a learned streaming owner is memory-bound."""
+        return pu.pod_demand(pod, self.ledger.is_stream_owner)
+
     # ------------------------------------------------------------------ verbs
     def filter(self, pod: dict, node_names: list[str]) -> tuple[list[str], dict[str, str]]:
         """Reference Dealer.Assume (dealer.go:89-136) + Predicate.Handler (predicate.go:19-41)."""
         if self.nominate:
             self._drop_own_nomination(pod)
         try:
-            demand, _ = pu.ledger_view(pu.pod_demand(pod))
+            demand, _ = pu.ledger_view(self.pod_demand(pod))
         except pu.TooManyGpuContainers as e:
             return [], {name: f"nano-gpu: {e}" for name in node_names}
         ids = self.node_ids(node_names)
@@ -220,7 +224,7 @@ class ClusterState:
         if self.nominate:
             self._drop_own_nomination(pod)
         try:
-            demand, _ = pu.ledger_view(pu.pod_demand(pod))
+            demand, _ = pu.ledger_view(self.pod_demand(pod))
         except pu.TooManyGpuContainers:
             return [0] * len(node_names)             # filter already failed every node
         ids = self.node_ids(node_names)
@@ -270,7 +274,7 @@ class ClusterState:
         if e is None:
             raise SchedulingError(f"node {node_name} not found")
         uid = pu.pod_uid(pod)
-        full = pu.pod_demand(pod)
+        full = self.pod_demand(pod)
         try:
             demand, idx = pu.ledger_view(full)
         except pu.TooManyGpuContainers as e:
@@ -278,6 +282,9 @@ class ClusterState:
         rc, plan = self.ledger.reserve(e.id, uid, demand, self.options)
         if rc not in (N.OK, N.OK_EXISTING):
             raise self.reserve_error(demand, node_name, rc)
+        owner = pu.controller_uid(pod)
+        if owner:                     # what the streaming-owner learner reads (learn_stream_owners)
+            self.ledger.set_pod_owner(uid, owner)
         return pu.full_plan(plan, idx, len(full)), rc == N.OK
 
     def reserve_error(self, demand, node_name: str, rc: int) -> SchedulingError:
@@ -302,18 +309,21 @@ class ClusterState:
             log.warning("allocate %s: node %s unknown", pu.pod_key(pod), node)
             return False
         try:
-            demand, idx = pu.ledger_view(pu.pod_demand(pod))
+            demand, idx = pu.ledger_view(self.pod_demand(pod))
         except pu.TooManyGpuContainers as err:
             log.warning("allocate %s: %s", pu.pod_key(pod), err)
             return False
-        if len(plan) != len(pu.pod_demand(pod)):
+        if len(plan) != len(self.pod_demand(pod)):
             log.warning("allocate %s: %d assignments for %d containers", pu.pod_key(pod), len(plan),
-                        len(pu.pod_demand(pod)))
+                        len(self.pod_demand(pod)))
             return False
         rc = self.ledger.allocate_plan(e.id, pu.pod_uid(pod), demand, pu.ledger_plan(plan, idx), True)
         if rc != N.OK:
             log.warning("allocate %s on %s failed: %s", pu.pod_key(pod), node, N.err_str(rc))
             return False
+        owner = pu.controller_uid(pod)
+        if owner:
+            self.ledger.set_pod_owner(pu.pod_uid(pod), owner)
         return True
 
     def release(self, pod: dict) -> bool:

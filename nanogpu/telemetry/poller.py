@@ -50,6 +50,8 @@ class LoadPoller:
         self.polls = 0        # successful node/metric syncs
         self.queries = 0
         self.hbm_threshold = T.HBM_HOT_THRESHOLD
+        self.owners_learned = 0
+        self.owners_forgotten = 0
 
     # -------------------------------------------------------------- policy changes
     def on_policy(self, spec: PolicySpec) -> None:
@@ -82,8 +84,21 @@ class LoadPoller:
     # -------------------------------------------------------------- polling
     async def _loop(self, metric: str, period: float) -> None:
         while True:
+            if metric == T.GPU_HBM_ACTIVITY_METRIC:
+                self.learn_owners()
             self.enqueue(metric)
             await asyncio.sleep(period)
+
+    def learn_owners(self) -> tuple[int, int]:
+        """Streaming owners from the last period's marks (Ledger::learn_stream_owners): a
+        device measured HBM-hot while it held one pod alone makes that pod's controlling owner
+        (ReplicaSet, Job, ...) streaming, so the owner's next unannotated pods are placed as
+        memory-bound; an owner alone on a device that is no longer hot is forgotten. One pass
+        over the ledger per HBM-activity period, off the GIL."""
+        learned, forgotten = self.state.ledger.learn_stream_owners(True)
+        self.owners_learned += learned
+        self.owners_forgotten += forgotten
+        return learned, forgotten
 
     def cluster_scoped(self, metric: str) -> bool:
         return self.spec.metrics_scope == "cluster" and self.spec.query_for(metric).cluster is not None

@@ -58,6 +58,7 @@ struct CachedPod {
   std::vector<std::string> containers;
   Demand demand;
   bool completed = false;
+  uint64_t owner = 0;   // owner_hash of the controlling owner's UID, 0: none
 };
 
 struct VerbStats {

@@ -32,6 +32,12 @@ namespace nanogpu {
 constexpr int kNameLen = 256;
 constexpr int kKeyLen = 64;
 constexpr int kPodShards = 64;
+// learned streaming owners (Ledger::set_stream_owner): direct-mapped, a collision forgets the
+// older owner (it falls back to its pods' own annotation)
+constexpr int kStreamOwners = 4096;
+
+// Hash of an owner's UID (ownerReferences[controller].uid), never 0.
+uint64_t owner_hash(std::string_view uid);
 
 // Nominated: taken tentatively at priorities for the top-scored node (see nominate()).
 enum PodState : int32_t { kPodEmpty = 0, kPodReserved = 1, kPodCommitted = 2, kPodTombstone = 3, kPodNominated = 4 };
@@ -64,6 +70,7 @@ struct PodSlot {
   double t_reserved;   // CLOCK_MONOTONIC seconds at reservation
   Demand demand;
   Plan plan;
+  uint64_t owner;      // owner_hash of the pod's controlling owner (set_pod_owner), 0: unknown
 };
 
 struct LedgerHeader {
@@ -92,6 +99,11 @@ struct LedgerHeader {
   alignas(64) std::atomic<uint32_t> size_total;
   std::atomic<uint64_t> size_bits[2];
   std::atomic<uint32_t> size_hist[kWasteSlots];
+  // owners (ReplicaSet, Job, ...) whose pods were measured streaming HBM: a device at or above
+  // the HBM-activity threshold while it held one of their pods alone. Their new pods count as
+  // memory-bound unless annotated otherwise. Written by the telemetry worker, read by every
+  // worker's front door without a lock.
+  alignas(64) std::atomic<uint64_t> stream_owner[kStreamOwners];
   PaddedMutex shard_mu[kPodShards];
   int32_t shard_live[kPodShards];   // guarded by shard_mu[s]
   int32_t shard_tomb[kPodShards];
@@ -111,6 +123,7 @@ struct PodRecord {
   double t_reserved;
   Demand demand;
   Plan plan;
+  uint64_t owner = 0;
 };
 
 class Ledger {
@@ -203,6 +216,15 @@ class Ledger {
   // Request-size learning: every new reservation/allocation counts its share sizes; a size
   // is common once it is >= 2 % of the decayed count (dropped below 1 %).
   void note_request(const Demand& d);
+  void set_stream_owner(uint64_t owner, bool streaming);
+  bool is_stream_owner(uint64_t owner) const;
+  // records the controlling owner of a pod the ledger holds (what learn_stream_owners reads)
+  int32_t set_pod_owner(const std::string& key, uint64_t owner);
+  // One pass over the committed pods: a device marked mem_hot (measured HBM activity) that
+  // holds exactly one pod with a known owner makes that owner a streaming owner; with
+  // `forget_cool`, an owner alone on a device that is not hot is forgotten. Returns
+  // {owners learned, owners forgotten}.
+  std::pair<int32_t, int32_t> learn_stream_owners(bool forget_cool);
   SizeSet learned_sizes() const;
   // The options a placement runs with: native binpack gets the request-size set (fixed |
   // learned | this demand's sizes) and its waste table; everything else is unchanged.

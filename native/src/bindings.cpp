@@ -201,6 +201,7 @@ py::dict record_dict(const PodRecord& r) {
   for (int i = 0; i < r.demand.n; ++i) dem.emplace_back(r.demand.c[i].pct, r.demand.c[i].mib);
   d["demand"] = dem;
   d["plan"] = plan_list(r.plan);
+  d["owner"] = r.owner;
   return d;
 }
 
@@ -703,6 +704,31 @@ PYBIND11_MODULE(_native, m) {
       .def("set_load", &Ledger::set_load)
       .def("set_health", &Ledger::set_health)
       .def("set_mem_hot", &Ledger::set_mem_hot)
+      .def(
+          "set_stream_owner",
+          [](Ledger& l, const std::string& uid, bool streaming) { l.set_stream_owner(owner_hash(uid), streaming); },
+          py::arg("uid"), py::arg("streaming"))
+      .def(
+          "is_stream_owner", [](const Ledger& l, const std::string& uid) { return l.is_stream_owner(owner_hash(uid)); },
+          py::arg("uid"))
+      .def(
+          "set_pod_owner",
+          [](Ledger& l, const std::string& key, const std::string& owner_uid) {
+            return l.set_pod_owner(key, owner_uid.empty() ? 0 : owner_hash(owner_uid));
+          },
+          py::arg("key"), py::arg("owner_uid"))
+      .def(
+          "learn_stream_owners",
+          [](Ledger& l, bool forget_cool) {
+            std::pair<int32_t, int32_t> r;
+            {
+              py::gil_scoped_release nogil;
+              r = l.learn_stream_owners(forget_cool);
+            }
+            return r;
+          },
+          py::arg("forget_cool") = true)
+      .def_static("owner_hash", [](const std::string& uid) { return owner_hash(uid); })
       .def("frag", [](const Ledger& l, int32_t min_request) { return frag_dict(l.frag(min_request)); },
            py::arg("min_request") = 0)
       .def("learned_sizes", [](const Ledger& l) { return size_list(l.learned_sizes()); },

@@ -189,6 +189,22 @@ static bool list_has(std::string_view list, std::string_view name) {
   return false;
 }
 
+// UID of the controlling owner in a pod's ownerReferences (the first entry with
+// controller: true, else the first entry); empty when there is none.
+static std::string_view controller_uid(const json::Doc& d, int32_t refs) {
+  if (!d.is(refs, json::Type::kArr)) return {};
+  std::string_view first;
+  for (int32_t r = d.at(refs).first; r >= 0; r = d.at(r).next) {
+    if (!d.is(r, json::Type::kObj)) continue;
+    const int32_t u = d.get(r, "uid");
+    if (!d.is(u, json::Type::kStr)) continue;
+    const int32_t ctl = d.get(r, "controller");
+    if (d.is(ctl, json::Type::kBool) && d.at(ctl).b) return d.str(u);
+    if (first.empty()) first = d.str(u);
+  }
+  return first;
+}
+
 // 64-bit hash of a byte string, eight bytes per step (keys the per-worker node-id cache;
 // hits are verified name by name, so a collision costs a lookup, never a wrong answer).
 static uint64_t text_hash(std::string_view s) {
@@ -492,6 +508,7 @@ void Frontend::prepare_bind(std::string_view body, PyRequest* r) {
   std::memset(&plan, 0, sizeof(plan));
   PreparedBind& b = r->bind;
   b.rc = ledger_->reserve(id, uid, pod.demand, o, &plan);
+  if ((b.rc == kOk || b.rc == kOkExisting) && pod.owner) ledger_->set_pod_owner(uid, pod.owner);
   bind_stats.observe(now_ns() - t0);
   b.ok = true;
   b.ns = std::move(ns);
@@ -916,7 +933,9 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
       }
     }
   }
-  // nano-gpu/memory-bound: "true" (every container) or a comma list of container names
+  // nano-gpu/memory-bound: "true" (every container) or a comma list of container names. With
+  // no annotation, a pod whose controlling owner was measured streaming (Ledger stream owners,
+  // nanogpu.telemetry.poller.OwnerLearner) counts as memory-bound; "false" opts out.
   if (pod >= 0 && d.is(pod, json::Type::kObj)) {
     const int32_t md = d.get(pod, "metadata");
     const int32_t ann = d.is(md, json::Type::kObj) ? d.get(md, "annotations") : -1;
@@ -926,6 +945,12 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
       for (int c = 0; c < dem.n; ++c)
         if (v == "true" || list_has(v, cached.containers[c])) dem.c[c].flags |= kFlagMemBound;
     }
+    if (d.is(md, json::Type::kObj)) {
+      const std::string_view owner = controller_uid(d, d.get(md, "ownerReferences"));
+      if (!owner.empty()) cached.owner = owner_hash(owner);
+    }
+    if (!d.is(mb, json::Type::kStr) && cached.owner && ledger_->is_stream_owner(cached.owner))
+      for (int c = 0; c < dem.n; ++c) dem.c[c].flags |= kFlagMemBound;
   }
   // node ids: any unknown node goes to Python, which can register it from its informer.
   // kube-scheduler sends the same node list over and over, so each worker remembers the ids

@@ -18,7 +18,7 @@
 namespace nanogpu {
 
 static constexpr uint64_t kMagic = 0x4e414e4f47505531ULL;  // "NANOGPU1"
-static constexpr uint32_t kVersion = 8;  // 4: HBM pools; 5: cache lines; 6: sizes; 7: serving; 8: nominations
+static constexpr uint32_t kVersion = 9;  // 4: HBM pools; 5: cache lines; 6: sizes; 7: serving; 8: nominations; 9: stream owners
 
 static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -151,6 +151,7 @@ Ledger::Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, b
     hdr_->size_bits[0].store(0);
     hdr_->size_bits[1].store(0);
     for (auto& c : hdr_->size_hist) c.store(0);
+    for (auto& o : hdr_->stream_owner) o.store(0);
     init_mutex(&hdr_->registry_mu);
     for (int s = 0; s < kPodShards; ++s) {
       init_mutex(&hdr_->shard_mu[s].m);
@@ -699,6 +700,7 @@ int32_t Ledger::reserve_as(int32_t id, const std::string& key, const Demand& d, 
     p->demand = d;
     p->plan = *plan;
     p->t_reserved = mono_now();
+    p->owner = 0;
     p->state = state;
   }
   ++n->n_pods;
@@ -748,6 +750,7 @@ int32_t Ledger::allocate_plan(int32_t id, const std::string& key, const Demand& 
     p->demand = d;
     p->plan = plan;
     p->t_reserved = mono_now();
+    p->owner = 0;
     p->state = committed ? kPodCommitted : kPodReserved;
   }
   ++n->n_pods;
@@ -821,7 +824,65 @@ bool Ledger::lookup(const std::string& key, PodRecord* out) const {
   out->t_reserved = p->t_reserved;
   out->demand = p->demand;
   out->plan = p->plan;
+  out->owner = p->owner;
   return true;
+}
+
+int32_t Ledger::set_pod_owner(const std::string& key, uint64_t owner) {
+  if (key.empty() || key.size() >= kKeyLen) return kErrUnknownPod;
+  const uint64_t h = key_hash(key.c_str());
+  const int s = shard_of(h);
+  lock_mu(&hdr_->shard_mu[s].m);
+  Unlock us{&hdr_->shard_mu[s].m};
+  PodSlot* p = find_pod_locked(s, h, key.c_str());
+  if (!p) return kErrUnknownPod;
+  p->owner = owner;
+  return kOk;
+}
+
+std::pair<int32_t, int32_t> Ledger::learn_stream_owners(bool forget_cool) {
+  // (node, device) -> tenant pods and the owner of the last one seen
+  struct Tenancy {
+    int32_t pods = 0;
+    uint64_t owner = 0;
+  };
+  std::unordered_map<uint64_t, Tenancy> dev;
+  for (int s = 0; s < kPodShards; ++s) {
+    lock_mu(&hdr_->shard_mu[s].m);
+    Unlock us{&hdr_->shard_mu[s].m};
+    const PodSlot* t = shard(s);
+    for (uint32_t i = 0; i < hdr_->pods_per_shard; ++i) {
+      const PodSlot& p = t[i];
+      if (p.state != kPodCommitted || p.node < 0) continue;
+      int16_t seen[kMaxPlanIdx];
+      int n_seen = 0;
+      for (int k = 0; k < p.plan.off[p.plan.n] && k < kMaxPlanIdx; ++k) {
+        const int16_t x = p.plan.idx[k];
+        if (x < 0 || std::find(seen, seen + n_seen, x) != seen + n_seen) continue;
+        seen[n_seen++] = x;
+        Tenancy& te = dev[(static_cast<uint64_t>(p.node) << 16) | static_cast<uint16_t>(x)];
+        ++te.pods;
+        te.owner = p.owner;
+      }
+    }
+  }
+  int32_t learned = 0, forgotten = 0;
+  for (const auto& [key, te] : dev) {
+    if (te.pods != 1 || te.owner == 0) continue;
+    const int32_t id = static_cast<int32_t>(key >> 16);
+    const int x = static_cast<int>(key & 0xffff);
+    const NodeSlot* n = node(id);
+    if (!n || x >= n->n_devs) continue;
+    const bool hot = __atomic_load_n(&n->devs[x].mem_hot, __ATOMIC_RELAXED) != 0;
+    if (hot && !is_stream_owner(te.owner)) {
+      set_stream_owner(te.owner, true);
+      ++learned;
+    } else if (!hot && forget_cool && is_stream_owner(te.owner)) {
+      set_stream_owner(te.owner, false);
+      ++forgotten;
+    }
+  }
+  return {learned, forgotten};
 }
 
 int32_t Ledger::fits_without(int32_t id, const std::vector<std::string>& victims, const Demand& d,
@@ -860,7 +921,7 @@ std::vector<PodRecord> Ledger::pods_on(int32_t node_id) const {
       const PodSlot& p = t[i];
       if ((p.state == kPodReserved || p.state == kPodCommitted || p.state == kPodNominated) &&
           (node_id < 0 || p.node == node_id))
-        out.push_back(PodRecord{p.key, p.node, p.state, p.t_reserved, p.demand, p.plan});
+        out.push_back(PodRecord{p.key, p.node, p.state, p.t_reserved, p.demand, p.plan, p.owner});
     }
   }
   return out;
@@ -945,6 +1006,26 @@ constexpr uint32_t kSizeDecayAt = 4096;   // halve the counts when they reach th
 inline bool size_common(uint32_t cnt, uint32_t total) { return cnt * 50u >= total && cnt > 0; }
 inline bool size_rare(uint32_t cnt, uint32_t total) { return cnt * 100u < total; }
 }  // namespace
+
+uint64_t owner_hash(std::string_view uid) {
+  uint64_t h = 0xcbf29ce484222325ULL;   // FNV-1a
+  for (unsigned char c : uid) h = (h ^ c) * 0x100000001b3ULL;
+  return h ? h : 1;
+}
+
+void Ledger::set_stream_owner(uint64_t owner, bool streaming) {
+  std::atomic<uint64_t>& slot = hdr_->stream_owner[owner % kStreamOwners];
+  if (streaming) {
+    slot.store(owner, std::memory_order_relaxed);
+  } else {
+    uint64_t cur = owner;
+    slot.compare_exchange_strong(cur, 0, std::memory_order_relaxed);
+  }
+}
+
+bool Ledger::is_stream_owner(uint64_t owner) const {
+  return hdr_->stream_owner[owner % kStreamOwners].load(std::memory_order_relaxed) == owner;
+}
 
 void Ledger::note_request(const Demand& d) {
   for (int c = 0; c < d.n; ++c) {

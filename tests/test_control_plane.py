@@ -619,3 +619,42 @@ def test_cluster_scoped_metrics_one_query_per_metric_for_every_node():
         assert parse_policy("spec: {}\n").metrics_scope == "node"
 
     asyncio.run(main())
+
+
+def test_owner_learning_through_the_poller_and_the_python_verbs():
+    """Prometheus HBM activity -> poller marks the device hot -> the period's learner makes the
+    lone tenant's owner streaming -> the Python verbs place the owner's next pod as memory-bound
+    (off the hot device); a pod of another owner still packs best-fit."""
+    from nanogpu.k8s.podutil import make_pod
+
+    async def main():
+        st = ClusterState(policy="binpack", load_aware=True)
+        n = node("n0", 2)
+        st.register_node(n)
+        nid = st.node_entry("n0").id
+
+        def owned(name, owner):
+            p = make_pod(name, [("main", 20, 0)])
+            p["metadata"]["uid"] = f"uid-{name}"
+            p["metadata"]["ownerReferences"] = [{"kind": "Job", "name": owner, "uid": f"{owner}-uid"}]
+            return p
+
+        a = owned("a", "job1")
+        plan, fresh = st.reserve(a, "n0")
+        assert fresh and plan == [[0]]
+        st.commit("uid-a")
+        series = {T.GPU_HBM_ACTIVITY_METRIC: {("n0", 0): [0.9], ("n0", 1): [0.0]}}
+        runner, port, _ = await fake_prometheus(series)
+        spec = PolicySpec(sync_period=(Period(T.GPU_HBM_ACTIVITY_METRIC, 15),))
+        poller = LoadPoller(st, PromClient(f"http://127.0.0.1:{port}"), lambda: [n], spec=spec)
+        try:
+            await poller.sync_metric(T.GPU_HBM_ACTIVITY_METRIC)
+            assert poller.learn_owners() == (1, 0) and poller.owners_learned == 1
+            assert st.pod_demand(owned("b", "job1"))[0].flags == N.FLAG_MEM_BOUND
+            assert st.reserve(owned("b", "job1"), "n0")[0] == [[1]]      # off the hot device
+            assert st.reserve(owned("c", "job2"), "n0")[0] == [[0]]      # other owner: best fit
+        finally:
+            await poller.prom.close()
+            await runner.cleanup()
+
+    asyncio.run(main())

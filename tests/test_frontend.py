@@ -634,3 +634,58 @@ def test_escaped_node_names_still_answer_byte_identical():
         assert ok and out == _dumps(ext.prioritize(json.loads(raw)))
     finally:
         fe.stop()
+
+
+def test_learned_streaming_owner_marks_its_next_pods_memory_bound_on_the_native_path():
+    """A device measured HBM-hot while it holds one pod alone makes that pod's controlling
+    owner a streaming owner (Ledger::learn_stream_owners). The owner's next unannotated pods
+    then reach the ledger memory-bound through the native front door: they keep off the hot
+    device that best fit would pick. nano-gpu/memory-bound: "false" opts a pod out."""
+    async def main():
+        store, rt = await _runtime(1, "SPX")
+        loop = asyncio.get_running_loop()
+        led = rt.state.ledger
+        nid = led.find_node("n0")
+
+        async def schedule(name, ann=None):
+            pod = pu.make_pod(name, [("main", 25, 8192)])
+            pod["metadata"]["ownerReferences"] = [
+                {"apiVersion": "apps/v1", "kind": "ReplicaSet", "name": "rs", "uid": "rs-uid-1", "controller": True}]
+            if ann is not None:
+                pod["metadata"]["annotations"][T.ANNOTATION_MEMORY_BOUND] = ann
+            pod = store.create_pod(pod)
+            raw = _dumps({"Pod": pod, "Nodes": None, "NodeNames": ["n0"]})
+            m = pu.meta(pod)
+            bind = _dumps({"PodName": m["name"], "PodNamespace": m["namespace"], "PodUID": m["uid"], "Node": "n0"})
+            got = await loop.run_in_executor(None, _http, rt.bound_port,
+                                             [("POST", "/scheduler/filter", raw),
+                                              ("POST", "/scheduler/priorities", raw),
+                                              ("POST", "/scheduler/bind", bind)])
+            assert [g[0] for g in got] == [200, 200, 200], got
+            for _ in range(200):
+                rec = led.lookup(m["uid"])
+                if rec and rec["state"] == "committed":
+                    return rec
+                await asyncio.sleep(0.01)
+            raise AssertionError(f"{name} not committed")
+
+        try:
+            a = await schedule("a")
+            assert a["owner"] == N.Ledger.owner_hash("rs-uid-1")
+            (dev_a,) = a["plan"][0]
+            assert led.learn_stream_owners(True) == (0, 0)         # nothing measured hot yet
+            assert led.set_mem_hot(nid, dev_a, True) == N.OK
+            assert led.learn_stream_owners(True) == (1, 0) and led.is_stream_owner("rs-uid-1")
+            b = await schedule("b")                                # same owner, no annotation
+            (dev_b,) = b["plan"][0]
+            assert dev_b != dev_a                                  # best fit alone would stack it on a
+            mb = [d["mem_bound"] for d in led.snapshot(nid)["devices"]]
+            assert mb[dev_b] == 1 and sum(mb) == 1                 # b reached the ledger memory-bound
+            await schedule("c", ann="false")                       # opted out
+            assert sum(d["mem_bound"] for d in led.snapshot(nid)["devices"]) == 1
+            assert led.set_mem_hot(nid, dev_a, False) == N.OK      # a's device cooled: forgotten
+            assert led.learn_stream_owners(True) == (0, 1) and not led.is_stream_owner("rs-uid-1")
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
