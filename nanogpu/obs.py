@@ -121,6 +121,10 @@ class Metrics:
         self.nodes = Gauge("nanogpu_nodes", "nodes in the ledger", registry=r)
         self.pods = Gauge("nanogpu_pods", "pods in the ledger", registry=r)
         self.workqueue_depth = Gauge("nanogpu_workqueue_depth", "controller queue depth", ["queue"], registry=r)
+        self.stream_owners = LoopCounter("nanogpu_stream_owners_total",
+                                         "owners learned / forgotten as HBM-streaming (telemetry)", ["event"], r)
+        self.metric_polls = LoopCounter("nanogpu_metric_queries_total", "PromQL queries of the load poller",
+                                        ["result"], r)
 
         self._children: dict = {}
 

@@ -33,7 +33,8 @@ def is_gpu_node(node: dict, selectors: list[tuple[str, str]]) -> bool:
 class LoadPoller:
     def __init__(self, state, prom, list_nodes, spec: PolicySpec | None = None,
                  selectors: list[tuple[str, str]] | None = None, concurrency: int = 32,
-                 max_retries: int = 5, base_backoff_s: float = 10.0, max_backoff_s: float = 360.0):
+                 max_retries: int = 5, base_backoff_s: float = 10.0, max_backoff_s: float = 360.0,
+                 metrics=None):
         self.state = state
         self.prom = prom
         self.list_nodes = list_nodes          # () -> list[node dict]
@@ -52,6 +53,7 @@ class LoadPoller:
         self.hbm_threshold = T.HBM_HOT_THRESHOLD
         self.owners_learned = 0
         self.owners_forgotten = 0
+        self.metrics = metrics      # obs.Metrics (stream_owners counter), optional
 
     # -------------------------------------------------------------- policy changes
     def on_policy(self, spec: PolicySpec) -> None:
@@ -89,6 +91,10 @@ class LoadPoller:
             self.enqueue(metric)
             await asyncio.sleep(period)
 
+    def _count(self, result: str) -> None:
+        if self.metrics is not None:
+            self.metrics.child(self.metrics.metric_polls, result).inc()
+
     def learn_owners(self) -> tuple[int, int]:
         """Streaming owners from the last period's marks (Ledger::learn_stream_owners): a
         device measured HBM-hot while it held one pod alone makes that pod's controlling owner
@@ -98,6 +104,9 @@ class LoadPoller:
         learned, forgotten = self.state.ledger.learn_stream_owners(True)
         self.owners_learned += learned
         self.owners_forgotten += forgotten
+        if self.metrics is not None:
+            self.metrics.child(self.metrics.stream_owners, "learned").inc(learned)
+            self.metrics.child(self.metrics.stream_owners, "forgotten").inc(forgotten)
         return learned, forgotten
 
     def cluster_scoped(self, metric: str) -> bool:
@@ -157,9 +166,11 @@ class LoadPoller:
             raise
         except Exception as e:
             self.errors += 1
+            self._count("error")
             log.debug("metric %s node %s: %s", metric, name, e)
             raise
         self.polls += 1
+        self._count("ok")
         self.refresh_node(name, n_dev)
 
     async def sync_cluster(self, metric: str) -> None:
@@ -174,8 +185,10 @@ class LoadPoller:
             raise
         except Exception as e:
             self.errors += 1
+            self._count("error")
             log.debug("metric %s (cluster): %s", metric, e)
             raise
+        self._count("ok")
         for node in self.list_nodes():
             if not is_gpu_node(node, self.selectors):
                 continue

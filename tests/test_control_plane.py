@@ -658,3 +658,30 @@ def test_owner_learning_through_the_poller_and_the_python_verbs():
             await runner.cleanup()
 
     asyncio.run(main())
+
+
+def test_poller_counts_queries_and_learned_owners_in_extender_metrics():
+    from nanogpu.obs import Metrics
+
+    async def main():
+        series = {T.GPU_HBM_ACTIVITY_METRIC: {("n0", 0): [0.9]}, "fail_nodes": ("n1",)}
+        runner, port, _ = await fake_prometheus(series)
+        st = ClusterState(policy="binpack")
+        nodes = [node("n0", 2), node("n1", 2)]
+        for n in nodes:
+            st.register_node(n)
+        m = Metrics()
+        spec = PolicySpec(sync_period=(Period(T.GPU_HBM_ACTIVITY_METRIC, 15),))
+        poller = LoadPoller(st, PromClient(f"http://127.0.0.1:{port}"), lambda: nodes, spec=spec, metrics=m)
+        try:
+            await poller.sync_metric(T.GPU_HBM_ACTIVITY_METRIC)
+            poller.learn_owners()
+            text = m.render().decode()
+            assert 'nanogpu_metric_queries_total{result="ok"} 1.0' in text
+            assert 'nanogpu_metric_queries_total{result="error"} 1.0' in text
+            assert 'nanogpu_stream_owners_total{event="learned"} 0.0' in text
+        finally:
+            await poller.prom.close()
+            await runner.cleanup()
+
+    asyncio.run(main())
