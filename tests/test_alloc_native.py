@@ -285,3 +285,31 @@ def test_priorities_prefer_a_node_without_memory_bound_tenants():
     assert sb > sa                                    # pair with the compute-bound tenant
     ca, cb = L.score([a, b], [(30, 0)], BIN)
     assert ca == cb                                   # no preference for plain shares
+
+
+def test_stream_owner_learning_needs_a_lone_committed_tenant():
+    """Ledger::learn_stream_owners: only a hot device holding exactly one committed pod with a
+    known owner teaches anything (HBM activity is a device counter); reserved (not yet bound)
+    pods and shared devices teach nothing; a whole-device pod is alone on each of its devices."""
+    t = synthetic_mi355x(4)
+    L, (nid,) = ledger_with(t)
+    for key, owner, demand, plan in (("p1", "o1", [(30, 0)], [[0]]), ("p2", "o2", [(30, 0)], [[1]]),
+                                     ("p3", "o3", [(30, 0)], [[1]]), ("p4", "o4", [(200, 0)], [[2, 3]])):
+        assert L.allocate_plan(nid, key, demand, plan, True) == N.OK
+        assert L.set_pod_owner(key, owner) == N.OK
+    assert L.reserve(nid, "p5", [(30, 0)], BIN)[0] == N.OK           # reserved only
+    assert L.set_pod_owner("p5", "o5") == N.OK
+    assert L.set_pod_owner("nope", "o9") == N.ERR_UNKNOWN_POD
+    for dev in range(4):
+        assert L.set_mem_hot(nid, dev, True) == N.OK
+    learned, forgotten = L.learn_stream_owners(True)
+    assert (learned, forgotten) == (2, 0)
+    assert [L.is_stream_owner(o) for o in ("o1", "o2", "o3", "o4", "o5")] == [True, False, False, True, False]
+    assert L.learn_stream_owners(True) == (0, 0)                     # already known
+    assert L.set_mem_hot(nid, 0, False) == N.OK
+    assert L.learn_stream_owners(False) == (0, 0) and L.is_stream_owner("o1")   # no forgetting asked
+    assert L.learn_stream_owners(True) == (0, 1) and not L.is_stream_owner("o1")
+    # a released pod's slot reused by a new pod does not inherit the old owner
+    assert L.release("p1") == N.OK
+    assert L.allocate_plan(nid, "p1", [(30, 0)], [[0]], True) == N.OK
+    assert L.lookup("p1")["owner"] == 0
