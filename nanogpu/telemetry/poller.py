@@ -87,7 +87,8 @@ class LoadPoller:
     async def _loop(self, metric: str, period: float) -> None:
         while True:
             if metric == T.GPU_HBM_ACTIVITY_METRIC:
-                self.learn_owners()
+                # a pass over the whole pod table (milliseconds at 100k pods): off the loop
+                self.learn_owners(await asyncio.get_running_loop().run_in_executor(None, self._learn_pass))
             self.enqueue(metric)
             await asyncio.sleep(period)
 
@@ -95,13 +96,16 @@ class LoadPoller:
         if self.metrics is not None:
             self.metrics.child(self.metrics.metric_polls, result).inc()
 
-    def learn_owners(self) -> tuple[int, int]:
+    def _learn_pass(self) -> tuple[int, int]:
+        return self.state.ledger.learn_stream_owners(True)
+
+    def learn_owners(self, counts: tuple[int, int] | None = None) -> tuple[int, int]:
         """Streaming owners from the last period's marks (Ledger::learn_stream_owners): a
         device measured HBM-hot while it held one pod alone makes that pod's controlling owner
         (ReplicaSet, Job, ...) streaming, so the owner's next unannotated pods are placed as
         memory-bound; an owner alone on a device that is no longer hot is forgotten. One pass
         over the ledger per HBM-activity period, off the GIL."""
-        learned, forgotten = self.state.ledger.learn_stream_owners(True)
+        learned, forgotten = counts if counts is not None else self._learn_pass()
         self.owners_learned += learned
         self.owners_forgotten += forgotten
         if self.metrics is not None:

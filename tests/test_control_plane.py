@@ -685,3 +685,33 @@ def test_poller_counts_queries_and_learned_owners_in_extender_metrics():
             await runner.cleanup()
 
     asyncio.run(main())
+
+
+def test_hbm_ticker_learns_owners_each_period():
+    from nanogpu.k8s.podutil import make_pod
+
+    async def main():
+        st = ClusterState(policy="binpack")
+        n = node("n0", 2)
+        st.register_node(n)
+        p = make_pod("a", [("main", 20, 0)])
+        p["metadata"]["uid"] = "uid-a"
+        p["metadata"]["ownerReferences"] = [{"kind": "Job", "name": "j", "uid": "job-uid", "controller": True}]
+        st.reserve(p, "n0")
+        st.commit("uid-a")
+        runner, port, _ = await fake_prometheus({T.GPU_HBM_ACTIVITY_METRIC: {("n0", 0): [0.8]}})
+        spec = PolicySpec(sync_period=(Period(T.GPU_HBM_ACTIVITY_METRIC, 0.05),))
+        poller = LoadPoller(st, PromClient(f"http://127.0.0.1:{port}"), lambda: [n], spec=spec)
+        try:
+            poller.restart()
+            for _ in range(100):
+                if poller.owners_learned:
+                    break
+                await asyncio.sleep(0.02)
+            assert poller.owners_learned == 1 and st.ledger.is_stream_owner("job-uid")
+        finally:
+            await poller.stop()
+            await poller.prom.close()
+            await runner.cleanup()
+
+    asyncio.run(main())
