@@ -87,3 +87,51 @@ def test_config5_churn_native_beats_reference_frag():
         assert nat["unschedulable"] <= ref["unschedulable"], (sriov, nat, ref)
         assert nat["frag_pct"] <= ref["frag_pct"], (sriov, nat, ref)
         assert nat["hbm_overcommit_mib"] == 0
+
+
+def _stacked_streamers(mode: str) -> int:
+    """Streaming pods that share a device with another streaming pod, after a deployment of
+    streaming replicas (owner "s") and one of compute-bound replicas (owner "c") scale up
+    together on one 8-GPU node. The first streaming replica ran alone for one HBM-activity
+    period. mode: "none" (no annotation, no learning: the reference's view), "learn" (the
+    device counter marks the lone replica's device hot and the owner is learned), "declared"
+    (every streaming pod annotated)."""
+    from nanogpu.k8s.podutil import Req
+
+    L, (nid,) = _ledger()
+    truth: dict[int, int] = {}           # device -> streaming tenants (ground truth)
+
+    def place(key: str, owner: str):
+        streams = owner == "s"
+        flagged = streams and (mode == "declared" or (mode == "learn" and L.is_stream_owner(owner)))
+        d = [Req(25, 0, N.FLAG_MEM_BOUND)] if flagged else [(25, 0)]
+        rc, plan = L.reserve(nid, key, d, BIN)
+        assert rc == N.OK
+        L.commit(key)
+        L.set_pod_owner(key, owner)
+        (dev,) = plan[0]
+        truth[dev] = truth.get(dev, 0) + (1 if streams else 0)
+
+    def period():                        # the device counter: hot where a streamer runs
+        for dev in range(8):
+            L.set_mem_hot(nid, dev, truth.get(dev, 0) > 0)
+        if mode == "learn":
+            L.learn_stream_owners(True)
+
+    place("s0", "s")
+    period()
+    for i in range(1, 8):             # 8 streaming replicas: one per GPU is possible
+        place(f"s{i}", "s")
+        place(f"c{i}", "c")
+        if i % 4 == 0:
+            period()
+    return sum(n for n in truth.values() if n > 1)
+
+
+def test_learned_streaming_owner_stops_streamers_stacking():
+    """With the owner learned from its first replica's device counter, later replicas stop
+    stacking on streaming devices, as when every pod is declared; without it, best fit packs
+    the streamers together."""
+    none, learn, declared = (_stacked_streamers(m) for m in ("none", "learn", "declared"))
+    assert none >= 6
+    assert learn == declared == 0
