@@ -970,7 +970,7 @@ int32_t Ledger::set_mem_hot(int32_t id, int dev, bool hot) {
   if (dev < 0 || dev >= n->n_devs) return kErrBadPlan;
   Device& d = n->devs[dev];
   if ((d.mem_hot != 0) == hot) return kOk;   // unchanged: cached plans stay valid
-  d.mem_hot = hot ? 1 : 0;
+  __atomic_store_n(&d.mem_hot, hot ? 1 : 0, __ATOMIC_RELAXED);   // learn_stream_owners reads it unlocked
   n->generation.fetch_add(1, std::memory_order_release);
   hdr_->epoch.fetch_add(1);
   return kOk;

@@ -92,6 +92,7 @@ static void churn(Ledger& l, int n_nodes, int seed, int iters, std::atomic<int>*
     if (rc == kOk) {
       reserved->fetch_add(1);
       if (rng() % 4) CHECK(l.commit(key) == kOk);
+      CHECK(l.set_pod_owner(key, owner_hash("owner-" + std::to_string(rng() % 8))) == kOk);
       live.push_back(key);
     }
     if (!live.empty() && rng() % 3 == 0) {
@@ -303,6 +304,16 @@ int main(int argc, char** argv) {
 
   std::atomic<bool> done{false};
   std::atomic<int> reserved{0};
+  // telemetry worker: HBM-hot marks flip and the streaming-owner learner scans the pod table
+  // while pods are reserved, committed and released around it
+  std::thread learner([&] {
+    std::mt19937_64 rng(77);
+    while (!done.load()) {
+      CHECK(ledger->set_mem_hot(static_cast<int32_t>(rng() % n_nodes), static_cast<int>(rng() % 8),
+                                rng() % 2 == 0) == kOk);
+      ledger->learn_stream_owners(true);
+    }
+  });
   std::thread checker([&] {
     while (!done.load()) {
       for (int k = 0; k < n_nodes; ++k) {
@@ -342,6 +353,7 @@ int main(int argc, char** argv) {
   CHECK(WIFEXITED(status) && WEXITSTATUS(status) == 0);
   done.store(true);
   checker.join();
+  learner.join();
   fe.stop();
 
   for (int k = 0; k < n_nodes; ++k) {
