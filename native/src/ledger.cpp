@@ -871,9 +871,15 @@ std::pair<int32_t, int32_t> Ledger::learn_stream_owners(bool forget_cool) {
     if (te.pods != 1 || te.owner == 0) continue;
     const int32_t id = static_cast<int32_t>(key >> 16);
     const int x = static_cast<int>(key & 0xffff);
-    const NodeSlot* n = node(id);
-    if (!n || x >= n->n_devs) continue;
-    const bool hot = __atomic_load_n(&n->devs[x].mem_hot, __ATOMIC_RELAXED) != 0;
+    NodeSlot* n = node(id);
+    if (!n) continue;
+    bool hot;
+    {
+      lock_node(n);
+      Unlock un{&n->mu};
+      if (x >= n->n_devs) continue;
+      hot = n->devs[x].mem_hot != 0;
+    }
     if (hot && !is_stream_owner(te.owner)) {
       set_stream_owner(te.owner, true);
       ++learned;
@@ -970,7 +976,7 @@ int32_t Ledger::set_mem_hot(int32_t id, int dev, bool hot) {
   if (dev < 0 || dev >= n->n_devs) return kErrBadPlan;
   Device& d = n->devs[dev];
   if ((d.mem_hot != 0) == hot) return kOk;   // unchanged: cached plans stay valid
-  __atomic_store_n(&d.mem_hot, hot ? 1 : 0, __ATOMIC_RELAXED);   // learn_stream_owners reads it unlocked
+  d.mem_hot = hot ? 1 : 0;
   n->generation.fetch_add(1, std::memory_order_release);
   hdr_->epoch.fetch_add(1);
   return kOk;
