@@ -92,6 +92,7 @@ class Req(tuple):
 
 
 _DEMAND_CACHE: dict[str, Demand] = {}
+_DEMAND_CACHE_OWNED: dict[str, Demand] = {}   # demands decided with the streaming-owner lookup
 _DEMAND_CACHE_CAP = 65536
 
 
@@ -115,8 +116,9 @@ def pod_demand(pod: dict, is_stream_owner=None) -> Demand:
     as memory-bound; "false" opts out. Decided at the pod's first sight, so its filter and its
     bind see the same demand."""
     uid = meta(pod).get("uid")
+    cache = _DEMAND_CACHE if is_stream_owner is None else _DEMAND_CACHE_OWNED
     if uid:
-        d = _DEMAND_CACHE.get(uid)
+        d = cache.get(uid)
         if d is not None:
             return d
     cs = containers(pod)
@@ -132,9 +134,9 @@ def pod_demand(pod: dict, is_stream_owner=None) -> Demand:
     else:
         d = [(container_percent(c), container_mib(c)) for c in cs]
     if uid:
-        if len(_DEMAND_CACHE) >= _DEMAND_CACHE_CAP:
-            _DEMAND_CACHE.clear()
-        _DEMAND_CACHE[uid] = d
+        if len(cache) >= _DEMAND_CACHE_CAP:
+            cache.clear()
+        cache[uid] = d
     return d
 
 

@@ -715,3 +715,17 @@ def test_hbm_ticker_learns_owners_each_period():
             await runner.cleanup()
 
     asyncio.run(main())
+
+
+def test_demand_memo_without_the_owner_lookup_does_not_hide_a_learned_owner():
+    """A caller that asks for a pod's demand without the streaming-owner lookup (the pod
+    controller's GPU check) must not fix the unflagged demand for the verbs that use it."""
+    from nanogpu.k8s.podutil import make_pod
+
+    st = ClusterState(policy="binpack")
+    st.ledger.set_stream_owner("rs-9", True)
+    p = make_pod("x", [("main", 20, 0)])
+    p["metadata"]["uid"] = "uid-memo-x"
+    p["metadata"]["ownerReferences"] = [{"kind": "ReplicaSet", "name": "rs", "uid": "rs-9", "controller": True}]
+    assert pu.pod_demand(p) == [(20, 0)] and not hasattr(pu.pod_demand(p)[0], "flags")
+    assert st.pod_demand(p)[0].flags == N.FLAG_MEM_BOUND

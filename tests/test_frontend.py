@@ -537,6 +537,7 @@ def test_native_verbs_survive_mutated_bodies():
                     continue
                 handled += 1
                 pu._DEMAND_CACHE.clear()   # Python memoises demands per UID (immutable in k8s)
+                pu._DEMAND_CACHE_OWNED.clear()
                 want = _dumps(ext.filter(json.loads(raw)))
                 assert out == want, (raw, out, want)
         finally:
