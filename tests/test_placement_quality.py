@@ -89,7 +89,7 @@ def test_config5_churn_native_beats_reference_frag():
         assert nat["hbm_overcommit_mib"] == 0
 
 
-def _stacked_streamers(mode: str) -> int:
+def _stacked_streamers(mode: str, opts=BIN) -> int:
     """Streaming pods that share a device with another streaming pod, after a deployment of
     streaming replicas (owner "s") and one of compute-bound replicas (owner "c") scale up
     together on one 8-GPU node. The first streaming replica ran alone for one HBM-activity
@@ -105,7 +105,7 @@ def _stacked_streamers(mode: str) -> int:
         streams = owner == "s"
         flagged = streams and (mode == "declared" or (mode == "learn" and L.is_stream_owner(owner)))
         d = [Req(25, 0, N.FLAG_MEM_BOUND)] if flagged else [(25, 0)]
-        rc, plan = L.reserve(nid, key, d, BIN)
+        rc, plan = L.reserve(nid, key, d, opts)
         assert rc == N.OK
         L.commit(key)
         L.set_pod_owner(key, owner)
@@ -135,3 +135,4 @@ def test_learned_streaming_owner_stops_streamers_stacking():
     none, learn, declared = (_stacked_streamers(m) for m in ("none", "learn", "declared"))
     assert none >= 6
     assert learn == declared == 0
+    assert _stacked_streamers("none", N.Options(N.Policy.BINPACK, compat=True)) == none   # the reference's
