@@ -339,3 +339,36 @@ def test_agent_selftest_passes_on_the_real_device(host, P):
     agent = NodeAgent(api=None, node_name="box", topo=topo, device_plugin=False)
     failed = asyncio.run(agent.selftest(P)) if len(topo.devices) == P.device_count() else []
     assert failed == [], failed
+
+
+def test_streaming_tenant_drives_mem_busy_percent_over_the_hot_threshold(host, P):
+    """The signal behind Device::mem_hot: while the HBM copy streams on this GPU, amdgpu's
+    mem_busy_percent (exported by the agent as nanogpu_device_mem_busy_percent and polled as
+    gpu_hbm_activity_avg) rises to at least types.HBM_HOT_THRESHOLD."""
+    import threading
+    import time
+    from pathlib import Path
+
+    from nanogpu import types as T
+
+    f = Path(f"/sys/class/drm/renderD{int(host['gpus'][0]['render_minor'])}/device/mem_busy_percent")
+    if not f.exists():
+        pytest.skip("mem_busy_percent not exposed")
+    idle = int(f.read_text())
+    done = threading.Event()
+    rate: list[float] = []
+
+    def stream():
+        rate.append(P.hbm_bandwidth(0, 1 << 30, 4000))   # ~1.5 s of copying, GIL released
+        done.set()
+
+    th = threading.Thread(target=stream)
+    th.start()
+    samples = []
+    while not done.wait(0.01):
+        samples.append(int(f.read_text()))
+    th.join(timeout=60)
+    print(f"mem_busy_percent idle {idle}, while streaming max {max(samples)} over {len(samples)} samples; "
+          f"copy {rate[0]:.0f} GB/s")
+    assert rate and rate[0] > 1000
+    assert max(samples) >= 100 * T.HBM_HOT_THRESHOLD
