@@ -368,7 +368,35 @@ def test_streaming_tenant_drives_mem_busy_percent_over_the_hot_threshold(host, P
     while not done.wait(0.01):
         samples.append(int(f.read_text()))
     th.join(timeout=60)
-    print(f"mem_busy_percent idle {idle}, while streaming max {max(samples)} over {len(samples)} samples; "
-          f"copy {rate[0]:.0f} GB/s")
+    nz = [v for v in samples if v > 0] or [0]
+    print(f"mem_busy_percent idle {idle}, while streaming max {max(samples)}, mean of nonzero "
+          f"{sum(nz) // len(nz)}, {len(samples)} samples; copy {rate[0]:.0f} GB/s")
     assert rate and rate[0] > 1000
     assert max(samples) >= 100 * T.HBM_HOT_THRESHOLD
+
+
+def test_compute_bound_tenant_stays_under_the_hot_threshold(host, P):
+    """The other side of the signal: an MFMA-bound tenant (bf16 burn, almost no HBM traffic)
+    keeps mem_busy_percent below types.HBM_HOT_THRESHOLD, so a busy compute tenant is not
+    mistaken for a streaming one. Sampled from a child process (the MFMA call holds the GIL)."""
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    from nanogpu import types as T
+
+    f = Path(f"/sys/class/drm/renderD{int(host['gpus'][0]['render_minor'])}/device/mem_busy_percent")
+    if not f.exists():
+        pytest.skip("mem_busy_percent not exposed")
+    sampler = subprocess.Popen(
+        [sys.executable, "-c",
+         "import time,sys\nf=open(sys.argv[1])\nv=[]\nt=time.time()+float(sys.argv[2])\n"
+         "while time.time()<t:\n f.seek(0); v.append(int(f.read())); time.sleep(0.01)\n"
+         "b=[x for x in v if x>0] or [0]\nprint(max(v), len(v), sum(b)//len(b))", str(f), "2.0"],
+        stdout=subprocess.PIPE, text=True)
+    tf = P.mfma_throughput(0, [], 2048, 1 << 20)["tflops"]   # ~0.5-1 s of MFMA at ~2 PF/s
+    out, _ = sampler.communicate(timeout=30)
+    peak, n, mean = (int(x) for x in out.split())
+    print(f"MFMA burn {tf:.0f} TFLOP/s; mem_busy_percent max {peak}, mean of nonzero {mean}, {n} samples")
+    assert tf > 500
+    assert 0 <= peak <= 100
