@@ -133,6 +133,8 @@ class PolicySpec:
     # "node": one query per GPU node and metric each period, failures backed off per node (the
     # reference's node/metric keys). "cluster": one query per metric for the whole cluster.
     metrics_scope: str = "node"
+    # HBM activity at or above which a device is marked streaming (types.HBM_HOT_THRESHOLD)
+    hbm_hot_threshold: float | None = None
 
     def period_of(self, name: str) -> float:
         for p in self.sync_period:
@@ -177,13 +179,17 @@ def parse_policy(text: str) -> PolicySpec:
                                           tuple([labels] if isinstance(labels, str) else labels),
                                           q.get("cluster"),
                                           tuple([nlabels] if isinstance(nlabels, str) else nlabels))))
+    hot = spec.get("hbmHotThreshold")
+    if hot is not None and not 0.0 < float(hot) <= 1.0:
+        raise ValueError(f"hbmHotThreshold {hot!r} outside (0, 1]")
     scope = spec.get("metricsScope", "node")
     if scope not in ("node", "cluster"):
         raise ValueError(f"unknown metricsScope {scope!r} (node or cluster)")
     return PolicySpec(
         sync_period=tuple(periods), priority=prio, policy=pol,
         compat=sch.get("compat"), topology_weight=sch.get("topologyWeight"),
-        score_normalize=sch.get("scoreNormalize"), metrics=tuple(metrics), metrics_scope=scope)
+        score_normalize=sch.get("scoreNormalize"), metrics=tuple(metrics), metrics_scope=scope,
+        hbm_hot_threshold=None if hot is None else float(hot))
 
 
 def load_policy(path: str) -> PolicySpec:

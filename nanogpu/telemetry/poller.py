@@ -50,7 +50,7 @@ class LoadPoller:
         self.errors = 0
         self.polls = 0        # successful node/metric syncs
         self.queries = 0
-        self.hbm_threshold = T.HBM_HOT_THRESHOLD
+        self.hbm_threshold = self.spec.hbm_hot_threshold or T.HBM_HOT_THRESHOLD
         self.owners_learned = 0
         self.owners_forgotten = 0
         self.metrics = metrics      # obs.Metrics (stream_owners counter), optional
@@ -58,6 +58,7 @@ class LoadPoller:
     # -------------------------------------------------------------- policy changes
     def on_policy(self, spec: PolicySpec) -> None:
         self.spec = spec
+        self.hbm_threshold = spec.hbm_hot_threshold or T.HBM_HOT_THRESHOLD
         self.restart()
 
     def restart(self) -> None:

@@ -729,3 +729,14 @@ def test_demand_memo_without_the_owner_lookup_does_not_hide_a_learned_owner():
     p["metadata"]["ownerReferences"] = [{"kind": "ReplicaSet", "name": "rs", "uid": "rs-9", "controller": True}]
     assert pu.pod_demand(p) == [(20, 0)] and not hasattr(pu.pod_demand(p)[0], "flags")
     assert st.pod_demand(p)[0].flags == N.FLAG_MEM_BOUND
+
+
+def test_hbm_hot_threshold_is_a_policy_knob():
+    spec = parse_policy("spec:\n  hbmHotThreshold: 0.66\n")
+    assert spec.hbm_hot_threshold == 0.66
+    st = ClusterState()
+    poller = LoadPoller(st, None, lambda: [], spec=spec)
+    assert poller.hbm_threshold == 0.66
+    with pytest.raises(ValueError):
+        parse_policy("spec:\n  hbmHotThreshold: 1.5\n")
+    assert LoadPoller(st, None, lambda: []).hbm_threshold == T.HBM_HOT_THRESHOLD
