@@ -399,4 +399,5 @@ def test_compute_bound_tenant_stays_under_the_hot_threshold(host, P):
     peak, n, mean = (int(x) for x in out.split())
     print(f"MFMA burn {tf:.0f} TFLOP/s; mem_busy_percent max {peak}, mean of nonzero {mean}, {n} samples")
     assert tf > 500
-    assert 0 <= peak <= 100
+    # single samples can spike (61 % seen); the policy reads a 1-minute average
+    assert mean < 100 * T.HBM_HOT_THRESHOLD
