@@ -30,12 +30,28 @@ class PodController:
         self.workers = max(1, workers)
         self.metrics = metrics
         self._tasks: list[asyncio.Task] = []
+        self.reconciled = 0        # shares released because a relist no longer held their pod
         informer.add_handler(self._on_event)
+        informer.add_relist_hook(self._on_relist)
 
     # ---------------------------------------------------------------- handlers
     def _release(self, uid: str) -> None:
         if self.state.release_uid(uid) and self.metrics:
             self.metrics.pods_released.inc()
+
+    def _on_relist(self, pods: list[dict], before: float) -> None:
+        """client-go's reflector turns every key missing from a relist into a delete, and the
+        reference's informer handlers rely on it (controller.go:89-136, 337-357). The store's
+        own diff (informer.py::_list) covers the pods Python held; pods the native watch filter
+        kept away from Python (bound by this extender, held only by the ledger) are reconciled
+        here: a committed share whose pod the LIST no longer returns is released."""
+        uids = [(p.get("metadata") or {}).get("uid", "") for p in pods]
+        gone = self.state.reconcile([u for u in uids if u], before)
+        if gone:
+            self.reconciled += len(gone)
+            if self.metrics:
+                self.metrics.pods_released.inc(len(gone))
+            log.info("relist: released %d pods deleted while the watch was down", len(gone))
 
     def _on_event(self, etype: str, pod: dict, old: dict | None) -> None:
         # hot: every pod event of the cluster passes here (four per scheduled pod), so the

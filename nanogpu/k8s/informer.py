@@ -43,6 +43,9 @@ class Informer:
         self.key = key or (_pod_key if resource == "pods" else _node_key)
         self.store: dict[str, dict] = {}
         self.handlers: list[Handler] = []
+        # called after every LIST with (listed objects, time.monotonic() taken before the LIST
+        # was sent): client-go's reflector Replace, for state kept outside this store
+        self.relist_hooks: list[Callable[[list[dict], float], None]] = []
         self.synced = asyncio.Event()
         self.rv = ""
         self._task: asyncio.Task | None = None
@@ -65,6 +68,12 @@ class Informer:
     def add_handler(self, h: Handler) -> None:
         self.handlers.append(h)
 
+    def add_relist_hook(self, h: Callable[[list[dict], float], None]) -> None:
+        """`h(items, before)` runs after each LIST. The native watch filter keeps the pods this
+        extender bound out of the store, so the store's diff below cannot see them vanish;
+        the hook lets the ledger reconcile against the listed objects directly."""
+        self.relist_hooks.append(h)
+
     def get(self, key: str) -> dict | None:
         return self.store.get(key)
 
@@ -79,6 +88,7 @@ class Informer:
                 log.exception("informer handler failed for %s %s", etype, self.key(obj))
 
     async def _list(self) -> None:
+        before = time.monotonic()      # CLOCK_MONOTONIC, the ledger's clock (ledger.cpp mono_now)
         if self.resource == "pods":
             items, rv = await self.api.list_pods(label_selector=self.label_selector)
         else:
@@ -98,6 +108,11 @@ class Informer:
         self.relists += 1
         if getattr(self, "watch_filter", None) is not None:
             self.watch_filter.reset(list(self.store))   # everything listed is in the store now
+        for h in self.relist_hooks:
+            try:
+                h(items, before)
+            except Exception:  # a hook bug must not kill the informer
+                log.exception("%s informer relist hook failed", self.resource)
 
     async def run(self) -> None:
         """client-go reflector semantics (/root/reference/go.mod:16, client-go v0.18 informers

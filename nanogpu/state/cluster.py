@@ -338,6 +338,16 @@ class ClusterState:
             return True
         return False
 
+    def reconcile(self, live_uids: list[str], before: float) -> list[str]:
+        """After a pod LIST: releases committed shares recorded before `before` whose pod is
+        not among `live_uids` (Ledger::reconcile). Returns the UIDs released."""
+        gone = self.ledger.reconcile(live_uids, float(before))
+        for uid in gone:
+            self._released[uid] = None
+        while len(self._released) > self._released_cap:
+            self._released.popitem(last=False)
+        return gone
+
     def known(self, uid: str) -> bool:
         return self.ledger.lookup(uid) is not None
 

@@ -203,6 +203,15 @@ class Ledger {
   int32_t fits_without(int32_t id, const std::vector<std::string>& victims, const Demand& d, const Options& o,
                        Plan* plan) const;
   std::vector<std::string> expired_reservations(double older_than_s) const;
+  // Relist reconciliation (client-go reflector Replace: what a LIST no longer holds was
+  // deleted). Releases every Committed pod recorded before `before` (CLOCK_MONOTONIC, taken
+  // before the LIST was sent) whose key is absent from `live`, the UIDs the LIST returned.
+  // Reservations (binds in flight) and nominations are left to their sweepers; a pod committed
+  // after `before` may postdate the LIST's snapshot and is left alone too. Returns the keys
+  // released.
+  std::vector<std::string> reconcile(const std::vector<std::string>& live, double before);
+  // Releases `key` only while it is Committed (reconcile racing a re-bind of the same key).
+  int32_t drop_committed(const std::string& key);
   int64_t n_pods() const { return hdr_->n_pods.load(std::memory_order_acquire); }
 
   // Load-aware telemetry (reference nodeusage.go + allocate.go:173-195).

@@ -691,6 +691,11 @@ PYBIND11_MODULE(_native, m) {
       .def("expired_reservations", &Ledger::expired_reservations, py::call_guard<py::gil_scoped_release>())
       .def("expired_nominations", &Ledger::expired_nominations, py::call_guard<py::gil_scoped_release>())
       .def("drop_reservation", &Ledger::drop_reservation, py::call_guard<py::gil_scoped_release>())
+      .def("drop_committed", &Ledger::drop_committed, py::call_guard<py::gil_scoped_release>())
+      .def("reconcile", &Ledger::reconcile, py::arg("live"), py::arg("before"),
+           py::call_guard<py::gil_scoped_release>(),
+           "Relist: release Committed pods recorded before `before` (mono_now) whose key is not in "
+           "`live`; returns the keys released")
       .def("drop_nomination", &Ledger::drop_nomination, py::call_guard<py::gil_scoped_release>())
       .def(
           "nominate",

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <thread>
+#include <unordered_set>
 
 namespace nanogpu {
 
@@ -948,6 +949,29 @@ std::vector<std::string> Ledger::expired(int32_t state, double older_than_s) con
 
 std::vector<std::string> Ledger::expired_reservations(double older_than_s) const {
   return expired(kPodReserved, older_than_s);
+}
+
+int32_t Ledger::drop_committed(const std::string& key) { return release_if(key, kPodCommitted); }
+
+std::vector<std::string> Ledger::reconcile(const std::vector<std::string>& live, double before) {
+  std::unordered_set<std::string_view> alive;
+  alive.reserve(live.size() * 2);
+  for (const std::string& k : live) alive.insert(k);
+  std::vector<std::string> gone;
+  for (int s = 0; s < kPodShards; ++s) {
+    lock_mu(&hdr_->shard_mu[s].m);
+    Unlock us{&hdr_->shard_mu[s].m};
+    const PodSlot* t = shard(s);
+    for (uint32_t i = 0; i < hdr_->pods_per_shard; ++i) {
+      const PodSlot& p = t[i];
+      if (p.state == kPodCommitted && p.t_reserved < before && !alive.count(std::string_view(p.key)))
+        gone.emplace_back(p.key);
+    }
+  }
+  std::vector<std::string> released;
+  for (const std::string& k : gone)
+    if (drop_committed(k) == kOk) released.push_back(k);
+  return released;
 }
 
 std::vector<std::string> Ledger::expired_nominations(double older_than_s) const {

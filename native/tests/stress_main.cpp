@@ -10,7 +10,10 @@
 //   * then the native API server and the native bind writers: writer threads bind pods
 //     reserved on the ledger (PATCH + binding + commit) while other threads patch the same
 //     pods and a watch stream reads every event; every bind must land, no patch may be lost
-//     (optimistic writes redo on conflict) and the watch must see every version.
+//     (optimistic writes redo on conflict) and the watch must see every version;
+//   * relist reconciliation (Ledger::reconcile): binder threads create, bind and delete pods,
+//     some deletions in a watch gap (never released by an event), while a relister LISTs the
+//     live set and reconciles; it must never release a live pod and must take back every ghost.
 // Exit code 0 = pass. Usage: nanogpu-stress [threads] [iterations]
 #include <arpa/inet.h>
 #include <netinet/in.h>
@@ -24,9 +27,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <random>
 #include <string>
 #include <thread>
+#include <unordered_set>
 #include <vector>
 
 #include "nanogpu/apiserver.h"
@@ -123,6 +128,90 @@ static std::string http(int port, const std::string& method, const std::string& 
   }
   close(fd);
   return out;
+}
+
+// Watch-gap deletions under concurrency (see the header comment). The "API server" is a set of
+// live pod keys: a pod is created (inserted) before it is bound and deleted (erased) before its
+// release event, like the real ordering.
+static void relist_gap(int iters) {
+  Ledger l("", 8, 65536, true);
+  add_nodes(l, 4);
+  std::mutex api_mu;
+  std::unordered_set<std::string> api;
+  std::atomic<bool> done{false};
+  std::atomic<int> ghosts{0}, reconciled{0};
+  std::thread relister([&] {
+    while (!done.load()) {
+      const double before = mono_now();
+      std::vector<std::string> listed;
+      {
+        std::lock_guard<std::mutex> g(api_mu);
+        listed.assign(api.begin(), api.end());
+      }
+      reconciled.fetch_add(static_cast<int>(l.reconcile(listed, before).size()));
+    }
+  });
+  std::vector<std::thread> binders;
+  for (int t = 0; t < 3; ++t)
+    binders.emplace_back([&, t] {
+      std::mt19937_64 rng(500 + t);
+      std::vector<std::string> mine;
+      Options o;
+      for (int i = 0; i < iters; ++i) {
+        const std::string key = "g" + std::to_string(t) + "-" + std::to_string(i);
+        {
+          std::lock_guard<std::mutex> g(api_mu);
+          api.insert(key);
+        }
+        Demand d;
+        std::memset(&d, 0, sizeof(d));
+        d.n = 1;
+        d.c[0].pct = 10;
+        Plan p;
+        if (l.reserve(static_cast<int32_t>(rng() % 4), key, d, o, &p) == kOk) {
+          CHECK(l.commit(key) == kOk);
+          mine.push_back(key);
+        } else {
+          std::lock_guard<std::mutex> g(api_mu);
+          api.erase(key);
+        }
+        if (!mine.empty() && rng() % 2 == 0) {
+          const size_t j = rng() % mine.size();
+          const std::string k = mine[j];
+          mine.erase(mine.begin() + static_cast<long>(j));
+          {
+            std::lock_guard<std::mutex> g(api_mu);
+            api.erase(k);
+          }
+          if (rng() % 2) {
+            const int32_t rc = l.release(k);   // the DELETED event (a relist may have been first)
+            CHECK(rc == kOk || rc == kErrUnknownPod);
+          } else {
+            ghosts.fetch_add(1);               // deleted while the watch was down
+          }
+        }
+      }
+      // every pod still in the API server must still hold its share: reconcile never took it
+      for (const auto& k : mine) {
+        {
+          std::lock_guard<std::mutex> g(api_mu);
+          api.erase(k);
+        }
+        CHECK(l.release(k) == kOk);
+      }
+    });
+  for (auto& b : binders) b.join();
+  done.store(true);
+  relister.join();
+  reconciled.fetch_add(static_cast<int>(l.reconcile({}, mono_now() + 1.0).size()));
+  CHECK(l.n_pods() == 0);
+  CHECK(reconciled.load() >= ghosts.load());
+  for (int k = 0; k < 4; ++k) {
+    NodeSnapshot s;
+    CHECK(l.snapshot(k, &s));
+    for (int i = 0; i < s.n_devs; ++i) CHECK(s.devs[i].pct_free == s.devs[i].pct_total);
+  }
+  std::printf("relist ok: %d ghosts, %d reconciled\n", ghosts.load(), reconciled.load());
 }
 
 // Native API server + native bind writers under concurrency (see the header comment).
@@ -371,5 +460,6 @@ int main(int argc, char** argv) {
   ledger.reset();
   unlink(path.c_str());
   apiserver_and_writers(std::max(50, iters / 20));
+  relist_gap(std::max(200, iters / 4));
   return 0;
 }
