@@ -180,7 +180,9 @@ class NodeAgent:
     def _on_pod(self, etype: str, pod: dict, old: dict | None) -> None:
         if pu.node_name_of(pod) != self.node or self.plugin is None:
             return
-        if etype == "DELETED" or pu.is_completed(pod):
+        # a terminating pod's containers still run on their CUs through the grace period: the
+        # grant goes back when they stop (Succeeded/Failed) or the pod object is gone
+        if etype == "DELETED" or pu.is_terminated(pod):
             self.plugin.release_pod(pu.pod_uid(pod))
 
     async def _health_loop(self) -> None:

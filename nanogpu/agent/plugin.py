@@ -124,7 +124,8 @@ class NanoGpuPlugin:
         if pods is None:
             pods = await self.matcher.candidates()
         for p in pods:
-            if pu.node_name_of(p) != self.node or not pu.is_assumed(p) or pu.is_completed(p):
+            # terminating pods still hold their CUs: restore their grants too
+            if pu.node_name_of(p) != self.node or not pu.is_assumed(p) or pu.is_terminated(p):
                 continue
             ann = pu.meta(p).get("annotations") or {}
             for c in pu.containers(p):

@@ -4,6 +4,10 @@ Reference: pkg/controller/controller.go (NewController :77-162, syncPod :210-243
 add/update/delete handlers :270-357). Semantics kept: a pod bound by someone else (or found
 after a restart) with the assume annotation is allocated from its annotations; a
 completed pod is released. Fixed:
+  * a terminating pod (deletionTimestamp, still in its grace period) keeps its percent, HBM
+    and CUs until it stops (Succeeded/Failed) or is DELETED; the reference releases at the
+    deletionTimestamp (pod.go:15-24), which hands a running pod's HBM to the next one
+    (compat mode keeps the reference behaviour);
   * D3 — the reference's delete handler only `Forget`s (dealer.go:311-319), leaking the
     GPU share whenever the pod disappears before the worker runs; here DELETED releases;
   * D4 — no one-second sleep between work items;
@@ -33,6 +37,14 @@ class PodController:
         self.reconciled = 0        # shares released because a relist no longer held their pod
         informer.add_handler(self._on_event)
         informer.add_relist_hook(self._on_relist)
+        if getattr(informer, "watch_filter", None) is not None:
+            state.add_listener(self._mirror_policy)
+            self._mirror_policy()
+
+    def _mirror_policy(self) -> None:
+        # the native watch filter drops what this controller would ignore: it must agree on
+        # when a terminating pod's share ends
+        self.informer.watch_filter.release_on_terminating = bool(self.state.options.compat)
 
     # ---------------------------------------------------------------- handlers
     def _release(self, uid: str) -> None:
@@ -69,8 +81,10 @@ class PodController:
             self.state.forget(uid)
             return
         node = (pod.get("spec") or {}).get("nodeName")
-        completed = bool(m.get("deletionTimestamp")) or \
-            (pod.get("status") or {}).get("phase") in ("Succeeded", "Failed")
+        # a terminating pod (deletionTimestamp only) still runs and keeps its share until it
+        # stops or is DELETED; compat releases at the deletionTimestamp, like the reference
+        completed = (pod.get("status") or {}).get("phase") in ("Succeeded", "Failed") or \
+            (self.state.options.compat and bool(m.get("deletionTimestamp")))
         if not node and not completed:
             return                             # pending: the extender's own business until bound
         if self.state.known(uid):
@@ -89,7 +103,7 @@ class PodController:
         pod = self.informer.get(key)
         if pod is None:
             return
-        if pu.is_completed(pod):
+        if pu.share_gone(pod, self.state.options.compat):
             if self.state.release(pod) and self.metrics:
                 self.metrics.pods_released.inc()
             return

@@ -49,6 +49,19 @@ def is_completed(pod: dict) -> bool:
     return ((pod.get("status") or {}).get("phase")) in ("Succeeded", "Failed")
 
 
+def is_terminated(pod: dict) -> bool:
+    """Its containers have stopped: phase Succeeded or Failed. A pod with only a
+    deletionTimestamp is still running through its grace period and holds its HBM and CUs;
+    kube-scheduler keeps such pods in its node accounting too. The reference releases at the
+    deletionTimestamp (is_completed); compat mode keeps that."""
+    return ((pod.get("status") or {}).get("phase")) in ("Succeeded", "Failed")
+
+
+def share_gone(pod: dict, compat: bool = False) -> bool:
+    """The pod no longer uses its devices: terminated, or (reference, compat) terminating."""
+    return is_completed(pod) if compat else is_terminated(pod)
+
+
 def _limit(c: dict, res: str):
     lim = ((c.get("resources") or {}).get("limits")) or {}
     return lim.get(res)

@@ -6,6 +6,7 @@ pkg/dealer/node.go (NodeInfo + PlanCache). Differences by design (SURVEY Appendi
     plan cache is keyed by generation instead of being wiped on every filter (node.go:96-98);
   * bind is reserve -> (API I/O, no lock) -> commit | rollback (fixes D1/D2);
   * delete events release (fixes D3); completed pods are skipped at rebuild (fixes D14);
+    terminating pods keep their share until they stop (compat: reference release at deletion);
   * G = 0 nodes are unfit instead of a divide-by-zero panic (fixes D6);
   * nodes re-register when capacity/topology change (fixes D20).
 """
@@ -361,7 +362,7 @@ class ClusterState:
         """Checkpoint/resume: the API server is the checkpoint (dealer.go:58-72, 279-299)."""
         n = 0
         for p in pods:
-            if pu.is_assumed(p) and pu.node_name_of(p) and not pu.is_completed(p):
+            if pu.is_assumed(p) and pu.node_name_of(p) and not pu.share_gone(p, self.options.compat):
                 n += int(self.allocate_existing(p))
         return n
 

@@ -309,6 +309,9 @@ struct PodWatchFilter {
   std::shared_ptr<Ledger> ledger;
   std::unordered_set<std::string> forwarded;   // "ns/name" in the Python store
   uint64_t released = 0, dropped = 0;
+  // compat (reference pod.go:15-24): a deletionTimestamp alone ends the share; otherwise a
+  // terminating pod keeps it until Succeeded/Failed or DELETED (controller/pods.py)
+  bool release_on_terminating = false;
 };
 
 static py::list decode_pod_events(const py::bytes& data, PodWatchFilter* f) {
@@ -351,8 +354,8 @@ static py::list decode_pod_events(const py::bytes& data, PodWatchFilter* f) {
         // what the controller ignores: a pending pod, or a bound, running one the ledger holds
         const std::string_view node = field(sp, "nodeName"), phase = field(st, "phase");
         const int32_t dts = d.is(md, json::Type::kObj) ? d.get(md, "deletionTimestamp") : -1;
-        const bool completed =
-            (dts >= 0 && !d.is(dts, json::Type::kNull)) || phase == "Succeeded" || phase == "Failed";
+        const bool completed = (f->release_on_terminating && dts >= 0 && !d.is(dts, json::Type::kNull)) ||
+                               phase == "Succeeded" || phase == "Failed";
         if (!completed && node.empty()) {
           drop = true;
         } else if (!completed) {
@@ -1050,6 +1053,7 @@ PYBIND11_MODULE(_native, m) {
             f.forwarded.insert(keys.begin(), keys.end());
           },
           py::arg("keys"), "After a relist: the keys now in the informer's store.")
+      .def_readwrite("release_on_terminating", &PodWatchFilter::release_on_terminating)
       .def_property_readonly("released", [](const PodWatchFilter& f) { return f.released; })
       .def_property_readonly("dropped", [](const PodWatchFilter& f) { return f.dropped; })
       .def_property_readonly("forwarded", [](const PodWatchFilter& f) { return f.forwarded.size(); });
