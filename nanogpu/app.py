@@ -162,7 +162,8 @@ class Runtime:
             from .telemetry.prom import PromClient
 
             self.poller = LoadPoller(self.state, PromClient(self.cfg.prometheus_url), self.node_informer.list,
-                                     selectors=self.cfg.gpu_node_selectors, metrics=self.metrics)
+                                     selectors=self.cfg.gpu_node_selectors, metrics=self.metrics,
+                                     get_node=self.node_informer.get)
             self.watcher.subscribe(self.poller.on_policy)
         self.watcher.load_now()
         if os.path.exists(self.cfg.policy_config_path):

@@ -76,6 +76,15 @@ class MetricQuery:
     cluster: str | None = None
     node_labels: tuple[str, ...] = ("node",)
 
+    def window_s(self) -> float:
+        """The longest range selector in the query (`avg_over_time(...[1m])` -> 60 s): how far
+        back the samples behind one answer reach. 0 for an instant query."""
+        best = 0.0
+        for q in (self.query, self.batch, self.cluster):
+            for n, unit in re.findall(r"\[(\d+(?:\.\d+)?)(ms|s|m|h)\]", q or ""):
+                best = max(best, float(n) * {"ms": 1e-3, "s": 1.0, "m": 60.0, "h": 3600.0}[unit])
+        return best
+
 
 # Reference query shapes (prometheus.go:70-76) as the default templates.
 REFERENCE_QUERY = '{metric}{{node=~"{node}",card="{card}"}} /100'

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import asyncio
 import logging
+import time
 
 from .. import types as T
 from ..config.policy import PolicySpec
@@ -34,10 +35,17 @@ class LoadPoller:
     def __init__(self, state, prom, list_nodes, spec: PolicySpec | None = None,
                  selectors: list[tuple[str, str]] | None = None, concurrency: int = 32,
                  max_retries: int = 5, base_backoff_s: float = 10.0, max_backoff_s: float = 360.0,
-                 metrics=None):
+                 metrics=None, get_node=None, forget_after: int = 3):
         self.state = state
         self.prom = prom
         self.list_nodes = list_nodes          # () -> list[node dict]
+        # name -> node dict (the node informer's store lookup). Without it, a name index is
+        # rebuilt once per period tick: never a scan of every node per node/metric key.
+        self.get_node = get_node
+        self._by_name: dict[str, dict] = {}
+        # a learned streaming owner is forgotten only after this many passes in a row in which
+        # every lone replica of it was measured cool
+        self.forget_after = max(1, int(forget_after))
         self.spec = spec or PolicySpec()
         self.selectors = selectors or [T.AMD_GPU_NODE_LABEL, T.LEGACY_GPU_NODE_LABEL]
         self.store = TelemetryStore()
@@ -97,16 +105,25 @@ class LoadPoller:
         if self.metrics is not None:
             self.metrics.child(self.metrics.metric_polls, result).inc()
 
-    def _learn_pass(self) -> tuple[int, int]:
-        return self.state.ledger.learn_stream_owners(True)
+    def attribution_cutoff(self, now: float | None = None) -> float:
+        """Pods recorded after this (time.monotonic) may postdate the samples behind the
+        current HBM-hot marks: the marks come from the previous tick's query (one period ago),
+        which averages `window` seconds before that. Such a pod is not blamed for a mark
+        measured on the tenant it replaced."""
+        q = self.spec.query_for(T.GPU_HBM_ACTIVITY_METRIC)
+        period = self.spec.period_of(T.GPU_HBM_ACTIVITY_METRIC)
+        return (time.monotonic() if now is None else now) - (q.window_s() + period)
 
-    def learn_owners(self, counts: tuple[int, int] | None = None) -> tuple[int, int]:
+    def _learn_pass(self, now: float | None = None) -> tuple[int, int]:
+        return self.state.ledger.learn_stream_owners(True, self.attribution_cutoff(now), self.forget_after)
+
+    def learn_owners(self, counts: tuple[int, int] | None = None, now: float | None = None) -> tuple[int, int]:
         """Streaming owners from the last period's marks (Ledger::learn_stream_owners): a
         device measured HBM-hot while it held one pod alone makes that pod's controlling owner
         (ReplicaSet, Job, ...) streaming, so the owner's next unannotated pods are placed as
         memory-bound; an owner alone on a device that is no longer hot is forgotten. One pass
         over the ledger per HBM-activity period, off the GIL."""
-        learned, forgotten = counts if counts is not None else self._learn_pass()
+        learned, forgotten = counts if counts is not None else self._learn_pass(now)
         self.owners_learned += learned
         self.owners_forgotten += forgotten
         if self.metrics is not None:
@@ -124,11 +141,20 @@ class LoadPoller:
             self.queue.add(f"{CLUSTER_KEY}/{metric}")
             return 1
         n = 0
+        by_name = {}
         for node in self.list_nodes():
+            name = pu.meta(node).get("name", "")
+            by_name[name] = node
             if is_gpu_node(node, self.selectors):
-                self.queue.add(f"{pu.meta(node).get('name', '')}/{metric}")
+                self.queue.add(f"{name}/{metric}")
                 n += 1
+        self._by_name = by_name
         return n
+
+    def _node(self, name: str) -> dict | None:
+        if self.get_node is not None:
+            return self.get_node(name)
+        return self._by_name.get(name)
 
     async def sync_metric(self, metric: str) -> None:
         """Polls `metric` on every GPU node now (no retries): tests and one-shot use."""
@@ -143,7 +169,7 @@ class LoadPoller:
         if name == CLUSTER_KEY:
             await self.sync_cluster(metric)
             return
-        node = next((n for n in self.list_nodes() if pu.meta(n).get("name") == name), None)
+        node = self._node(name)
         if node is None or not is_gpu_node(node, self.selectors):
             return                                   # node gone or no longer a GPU node
         await self.sync_node(node, metric)

@@ -229,11 +229,14 @@ class Ledger {
   bool is_stream_owner(uint64_t owner) const;
   // records the controlling owner of a pod the ledger holds (what learn_stream_owners reads)
   int32_t set_pod_owner(const std::string& key, uint64_t owner);
-  // One pass over the committed pods: a device marked mem_hot (measured HBM activity) that
-  // holds exactly one pod with a known owner makes that owner a streaming owner; with
-  // `forget_cool`, an owner alone on a device that is not hot is forgotten. Returns
-  // {owners learned, owners forgotten}.
-  std::pair<int32_t, int32_t> learn_stream_owners(bool forget_cool);
+  // One pass over the committed pods. A device that holds exactly one pod is that pod's "lone"
+  // device; only pods recorded at or before `reserved_before` (CLOCK_MONOTONIC: the start of
+  // the HBM metric's averaging window, so the mark was measured on this pod and not on a
+  // tenant it replaced) count. Per owner: learned if any of its lone pods sits on a device
+  // marked mem_hot; with `forget_cool`, forgotten once every lone pod of it was cool (and none
+  // hot) in `forget_after` consecutive passes. Returns {owners learned, owners forgotten}.
+  std::pair<int32_t, int32_t> learn_stream_owners(bool forget_cool, double reserved_before = 1e300,
+                                                  int32_t forget_after = 1);
   SizeSet learned_sizes() const;
   // The options a placement runs with: native binpack gets the request-size set (fixed |
   // learned | this demand's sizes) and its waste table; everything else is unchanged.
@@ -305,6 +308,9 @@ class Ledger {
   bool cache_get(const CacheKey& k, int32_t* rc, Plan* plan) const;
   bool cache_get_score(const CacheKey& k, int32_t* rc, int32_t* score) const;
   void cache_put(const CacheKey& k, int32_t rc, const Plan& plan);
+  // learner (one telemetry worker per replica): consecutive all-cool passes per learned owner
+  std::mutex learn_mu_;
+  std::unordered_map<uint64_t, int32_t> cool_streak_;
   mutable std::mutex names_mu_;
   mutable std::unordered_map<std::string, int32_t> names_;  // process-local name index
 };

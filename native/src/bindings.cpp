@@ -727,15 +727,15 @@ PYBIND11_MODULE(_native, m) {
           py::arg("key"), py::arg("owner_uid"))
       .def(
           "learn_stream_owners",
-          [](Ledger& l, bool forget_cool) {
+          [](Ledger& l, bool forget_cool, double reserved_before, int32_t forget_after) {
             std::pair<int32_t, int32_t> r;
             {
               py::gil_scoped_release nogil;
-              r = l.learn_stream_owners(forget_cool);
+              r = l.learn_stream_owners(forget_cool, reserved_before, forget_after);
             }
             return r;
           },
-          py::arg("forget_cool") = true)
+          py::arg("forget_cool") = true, py::arg("reserved_before") = 1e300, py::arg("forget_after") = 1)
       .def_static("owner_hash", [](const std::string& uid) { return owner_hash(uid); })
       .def("frag", [](const Ledger& l, int32_t min_request) { return frag_dict(l.frag(min_request)); },
            py::arg("min_request") = 0)

@@ -841,11 +841,13 @@ int32_t Ledger::set_pod_owner(const std::string& key, uint64_t owner) {
   return kOk;
 }
 
-std::pair<int32_t, int32_t> Ledger::learn_stream_owners(bool forget_cool) {
-  // (node, device) -> tenant pods and the owner of the last one seen
+std::pair<int32_t, int32_t> Ledger::learn_stream_owners(bool forget_cool, double reserved_before,
+                                                        int32_t forget_after) {
+  // (node, device) -> tenant pods, and the owner / record time of the last one seen
   struct Tenancy {
     int32_t pods = 0;
     uint64_t owner = 0;
+    double t = 0;
   };
   std::unordered_map<uint64_t, Tenancy> dev;
   for (int s = 0; s < kPodShards; ++s) {
@@ -864,12 +866,18 @@ std::pair<int32_t, int32_t> Ledger::learn_stream_owners(bool forget_cool) {
         Tenancy& te = dev[(static_cast<uint64_t>(p.node) << 16) | static_cast<uint16_t>(x)];
         ++te.pods;
         te.owner = p.owner;
+        te.t = p.t_reserved;
       }
     }
   }
-  int32_t learned = 0, forgotten = 0;
+  // per owner: any lone replica on a hot device / any on a cool one (a decision per owner, not
+  // per device, so one replica on a hot and one on a cool device cannot flip it back and forth)
+  struct Verdict {
+    bool hot = false, cool = false;
+  };
+  std::unordered_map<uint64_t, Verdict> owners;
   for (const auto& [key, te] : dev) {
-    if (te.pods != 1 || te.owner == 0) continue;
+    if (te.pods != 1 || te.owner == 0 || te.t > reserved_before) continue;
     const int32_t id = static_cast<int32_t>(key >> 16);
     const int x = static_cast<int>(key & 0xffff);
     NodeSlot* n = node(id);
@@ -881,14 +889,30 @@ std::pair<int32_t, int32_t> Ledger::learn_stream_owners(bool forget_cool) {
       if (x >= n->n_devs) continue;
       hot = n->devs[x].mem_hot != 0;
     }
-    if (hot && !is_stream_owner(te.owner)) {
-      set_stream_owner(te.owner, true);
-      ++learned;
-    } else if (!hot && forget_cool && is_stream_owner(te.owner)) {
-      set_stream_owner(te.owner, false);
-      ++forgotten;
+    Verdict& v = owners[te.owner];
+    (hot ? v.hot : v.cool) = true;
+  }
+  int32_t learned = 0, forgotten = 0;
+  std::lock_guard<std::mutex> g(learn_mu_);
+  for (const auto& [owner, v] : owners) {
+    if (v.hot) {
+      cool_streak_.erase(owner);
+      if (!is_stream_owner(owner)) {
+        set_stream_owner(owner, true);
+        ++learned;
+      }
+    } else if (forget_cool && is_stream_owner(owner)) {
+      if (++cool_streak_[owner] >= std::max(1, forget_after)) {
+        cool_streak_.erase(owner);
+        set_stream_owner(owner, false);
+        ++forgotten;
+      }
     }
   }
+  // an owner with no lone replica this pass keeps its streak where it was; owners no longer
+  // learned drop out of the map
+  for (auto it = cool_streak_.begin(); it != cool_streak_.end();)
+    it = is_stream_owner(it->first) ? std::next(it) : cool_streak_.erase(it);
   return {learned, forgotten};
 }
 

@@ -313,3 +313,47 @@ def test_stream_owner_learning_needs_a_lone_committed_tenant():
     assert L.release("p1") == N.OK
     assert L.allocate_plan(nid, "p1", [(30, 0)], [[0]], True) == N.OK
     assert L.lookup("p1")["owner"] == 0
+
+
+def test_stream_owner_learning_decides_per_owner_and_forgets_slowly():
+    """one owner with a lone replica on a hot device and another on a cool device is
+    learned and stays learned (the decision is per owner, not per device in hash order); a
+    learned owner is forgotten only after `forget_after` passes in a row with every lone
+    replica cool."""
+    t = synthetic_mi355x(4)
+    L, (nid,) = ledger_with(t)
+    for key, dev in (("r1", 0), ("r2", 1)):
+        assert L.allocate_plan(nid, key, [(30, 0)], [[dev]], True) == N.OK
+        assert L.set_pod_owner(key, "rs") == N.OK
+    assert L.set_mem_hot(nid, 0, True) == N.OK            # r1's device hot, r2's cool
+    for _ in range(5):
+        assert L.learn_stream_owners(True, forget_after=1) in ((1, 0), (0, 0))
+        assert L.is_stream_owner("rs")
+    assert L.set_mem_hot(nid, 0, False) == N.OK           # both cool now
+    assert L.learn_stream_owners(True, forget_after=3) == (0, 0) and L.is_stream_owner("rs")
+    assert L.learn_stream_owners(True, forget_after=3) == (0, 0) and L.is_stream_owner("rs")
+    assert L.set_mem_hot(nid, 1, True) == N.OK            # hot again: the streak starts over
+    assert L.learn_stream_owners(True, forget_after=3) == (0, 0)
+    assert L.set_mem_hot(nid, 1, False) == N.OK
+    for _ in range(2):
+        assert L.learn_stream_owners(True, forget_after=3) == (0, 0) and L.is_stream_owner("rs")
+    assert L.learn_stream_owners(True, forget_after=3) == (0, 1) and not L.is_stream_owner("rs")
+
+
+def test_a_pod_that_replaced_a_streaming_tenant_is_not_blamed_for_its_mark():
+    """the HBM-hot mark averages a window of past samples; a pod recorded after that
+    window began (it replaced the streaming tenant that heated the device) is not attributed."""
+    t = synthetic_mi355x(2)
+    L, (nid,) = ledger_with(t)
+    assert L.allocate_plan(nid, "streamer", [(50, 0)], [[0]], True) == N.OK
+    assert L.set_pod_owner("streamer", "hot-job") == N.OK
+    assert L.set_mem_hot(nid, 0, True) == N.OK
+    assert L.release("streamer") == N.OK                   # the tenant ends, the mark lingers
+    cutoff = N.mono_now()                                  # start of the mark's window
+    assert L.allocate_plan(nid, "newcomer", [(50, 0)], [[0]], True) == N.OK
+    assert L.set_pod_owner("newcomer", "compute-job") == N.OK
+    assert L.learn_stream_owners(True, reserved_before=cutoff) == (0, 0)
+    assert not L.is_stream_owner("compute-job")
+    # once a whole window has passed with it alone there, the mark is its own
+    assert L.learn_stream_owners(True, reserved_before=N.mono_now()) == (1, 0)
+    assert L.is_stream_owner("compute-job")
