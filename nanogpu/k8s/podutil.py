@@ -153,8 +153,15 @@ def pod_demand(pod: dict, is_stream_owner=None) -> Demand:
     return d
 
 
-# Containers one ledger record holds (native alloc.h kMaxContainers).
-LEDGER_MAX_CONTAINERS = 16
+# Containers one ledger record holds (native alloc.h kMaxContainers: one per plan index, 64;
+# the ledger keeps 16 inline and spills larger pods into overflow records).
+def _max_containers() -> int:
+    from ..native import core
+
+    return int(core().MAX_CONTAINERS)
+
+
+LEDGER_MAX_CONTAINERS = _max_containers()
 
 
 class TooManyGpuContainers(ValueError):
@@ -165,10 +172,11 @@ def ledger_view(demand: Demand) -> tuple[Demand, list[int] | None]:
     """The demand as the native ledger stores it, and the container each entry belongs to.
 
     The reference places any number of containers (allocate.go:54-62, rater.go:74-110); a
-    ledger record holds 16. A pod within that is passed as is (None: entries ARE containers,
+    ledger record holds 64 (every GPU container takes a plan index, and a node has at most
+    64 devices' worth of them). A pod within that is passed as is (None: entries ARE containers,
     so compat placements stay bit-exact with the reference). A larger pod keeps only its
     GPU-requesting containers, which is placement-neutral in native mode (zero-demand
-    containers take no device and sort last); more than 16 of those raises."""
+    containers take no device and sort last); more than 64 of those raises."""
     if len(demand) <= LEDGER_MAX_CONTAINERS:
         return demand, None
     idx = [i for i, d in enumerate(demand) if d[0] > 0 or d[1] > 0]

@@ -24,7 +24,10 @@ namespace nanogpu {
 
 constexpr int kMaxDevs = 64;         // 8 GPUs x CPX (8 XCD partitions each)
 constexpr int kMaxGpus = 16;         // physical GPUs per node
-constexpr int kMaxContainers = 16;   // containers per pod
+// containers per pod: every GPU-requesting container takes at least one plan index, so a pod
+// never needs more than kMaxPlanIdx (a ledger pod slot holds 16 inline, larger pods spill into
+// the ledger's overflow records)
+constexpr int kMaxContainers = 64;
 constexpr int kMaxPlanIdx = 64;      // device indices per pod plan
 constexpr int kNotNeedGPU = -1;      // reference NotNeedGPU, allocate.go:15
 constexpr int kLoadTotal = 2;        // reference LoadTotal, allocate.go:16

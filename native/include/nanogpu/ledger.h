@@ -62,15 +62,44 @@ struct alignas(64) PaddedMutex {   // one line per pod-shard lock (no false shar
   pthread_mutex_t m;
 };
 
+// A pod slot keeps up to kSlotContainers containers inline (the common case, and what keeps
+// the table small: it is scanned by the sweepers); a pod with more spills its demand and plan
+// into an overflow record (Ledger::put_record). Every pod is read through get_record.
+constexpr int kSlotContainers = 16;
+
+struct SlotDemand {
+  int32_t n;
+  int32_t pad;
+  ContainerDemand c[kSlotContainers];
+};
+
+struct SlotPlan {
+  int32_t n;
+  int32_t score;
+  int16_t off[kSlotContainers + 1];
+  int16_t idx[kMaxPlanIdx];
+};
+
 struct PodSlot {
   uint64_t hash;
   char key[kKeyLen];
   int32_t node;
   int32_t state;
   double t_reserved;   // CLOCK_MONOTONIC seconds at reservation
+  SlotDemand demand;   // inline record (ext == 0)
+  SlotPlan plan;
+  uint64_t owner;      // owner_hash of the pod's controlling owner (set_pod_owner), 0: unknown
+  int32_t ext;         // 0: inline; k > 0: overflow record k - 1
+  int32_t pad2;
+};
+
+// Overflow record of a pod with more than kSlotContainers containers (shared region, claimed
+// with a CAS on `used`, owned by exactly one pod slot).
+struct ExtRecord {
+  std::atomic<int32_t> used;
+  int32_t pad;
   Demand demand;
   Plan plan;
-  uint64_t owner;      // owner_hash of the pod's controlling owner (set_pod_owner), 0: unknown
 };
 
 struct LedgerHeader {
@@ -107,6 +136,9 @@ struct LedgerHeader {
   PaddedMutex shard_mu[kPodShards];
   int32_t shard_live[kPodShards];   // guarded by shard_mu[s]
   int32_t shard_tomb[kPodShards];
+  uint32_t ext_cap;                 // overflow records (pods over kSlotContainers containers)
+  std::atomic<uint32_t> ext_hint;   // where the next claim starts looking
+  std::atomic<int32_t> ext_used;
 };
 
 struct NodeSnapshot {
@@ -213,6 +245,7 @@ class Ledger {
   // Releases `key` only while it is Committed (reconcile racing a re-bind of the same key).
   int32_t drop_committed(const std::string& key);
   int64_t n_pods() const { return hdr_->n_pods.load(std::memory_order_acquire); }
+  int32_t overflow_records_used() const { return hdr_->ext_used.load(std::memory_order_relaxed); }
 
   // Load-aware telemetry (reference nodeusage.go + allocate.go:173-195).
   int32_t set_load(int32_t id, int dev, float usage);
@@ -258,6 +291,10 @@ class Ledger {
   int32_t release_if(const std::string& key, int32_t only_state);   // -1: any state
   PodSlot* find_pod_locked(int s, uint64_t h, const char* key) const;
   PodSlot* insert_pod_locked(int s, uint64_t h, const char* key);
+  // a slot's demand and plan, inline or in its overflow record (false: no record free)
+  bool put_record(PodSlot* p, const Demand& d, const Plan& plan);
+  void get_record(const PodSlot& p, Demand* d, Plan* plan) const;
+  void free_record(PodSlot* p);
 
   void lock_node(NodeSlot* n) const;
   void lock_mu(pthread_mutex_t* m) const;
@@ -270,6 +307,7 @@ class Ledger {
   LedgerHeader* hdr_ = nullptr;
   NodeSlot* nodes_ = nullptr;
   PodSlot* pods_ = nullptr;
+  ExtRecord* ext_ = nullptr;
 
   struct CacheKey {
     int32_t node;

@@ -25,7 +25,7 @@ namespace {
 // `flags` (nanogpu.k8s.podutil.Req: kFlagMemBound). Called with the GIL held.
 Demand to_demand(const py::sequence& v) {
   if (v.size() > static_cast<size_t>(kMaxContainers))
-    throw py::value_error("too many containers (max 16)");
+    throw py::value_error("too many containers (max " + std::to_string(kMaxContainers) + ")");
   Demand d;
   std::memset(&d, 0, sizeof(d));
   d.n = static_cast<int32_t>(v.size());
@@ -534,6 +534,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("bytes", &Ledger::bytes)
       .def_property_readonly("n_nodes", &Ledger::n_nodes)
       .def_property_readonly("n_pods", &Ledger::n_pods)
+      .def_property_readonly("overflow_records_used", &Ledger::overflow_records_used)
       .def_property_readonly("epoch", &Ledger::epoch)
       .def(
           "upsert_node",

@@ -19,7 +19,7 @@
 namespace nanogpu {
 
 static constexpr uint64_t kMagic = 0x4e414e4f47505531ULL;  // "NANOGPU1"
-static constexpr uint32_t kVersion = 9;  // 4: HBM pools; 5: cache lines; 6: sizes; 7: serving; 8: nominations; 9: stream owners
+static constexpr uint32_t kVersion = 10;  // 4: HBM pools; 5: cache lines; 6: sizes; 7: serving; 8: nominations; 9: stream owners; 10: overflow records
 
 static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -74,13 +74,16 @@ uint32_t pods_per_shard_for(uint32_t max_pods) {
   uint64_t per = (static_cast<uint64_t>(max_pods) * 3 / 2 + kPodShards - 1) / kPodShards;
   return static_cast<uint32_t>(std::max<uint64_t>(per, 16));
 }
+// pods with more than kSlotContainers containers are rare (one in 32 pods at most)
+uint32_t ext_records_for(uint32_t max_pods) { return std::max<uint32_t>(64, max_pods / 32); }
 }  // namespace
 
 size_t Ledger::region_bytes(uint32_t max_nodes, uint32_t max_pods) {
   const size_t h = align_up(sizeof(LedgerHeader), 4096);
   const size_t n = align_up(sizeof(NodeSlot) * max_nodes, 4096);
   const size_t p = align_up(sizeof(PodSlot) * kPodShards * pods_per_shard_for(max_pods), 4096);
-  return h + n + p;
+  const size_t e = align_up(sizeof(ExtRecord) * ext_records_for(max_pods), 4096);
+  return h + n + p + e;
 }
 
 Ledger::Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, bool create)
@@ -135,6 +138,9 @@ Ledger::Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, b
   nodes_ = reinterpret_cast<NodeSlot*>(base_ + align_up(sizeof(LedgerHeader), 4096));
   pods_ = reinterpret_cast<PodSlot*>(reinterpret_cast<char*>(nodes_) +
                                      align_up(sizeof(NodeSlot) * max_nodes, 4096));
+  ext_ = reinterpret_cast<ExtRecord*>(
+      reinterpret_cast<char*>(pods_) +
+      align_up(sizeof(PodSlot) * kPodShards * pods_per_shard_for(max_pods), 4096));
   if (init) {
     hdr_->version = kVersion;
     hdr_->max_nodes = max_nodes;
@@ -153,6 +159,9 @@ Ledger::Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, b
     hdr_->size_bits[1].store(0);
     for (auto& c : hdr_->size_hist) c.store(0);
     for (auto& o : hdr_->stream_owner) o.store(0);
+    hdr_->ext_cap = ext_records_for(max_pods);
+    hdr_->ext_hint.store(0);
+    hdr_->ext_used.store(0);
     init_mutex(&hdr_->registry_mu);
     for (int s = 0; s < kPodShards; ++s) {
       init_mutex(&hdr_->shard_mu[s].m);
@@ -263,6 +272,67 @@ PodSlot* Ledger::insert_pod_locked(int s, uint64_t h, const char* key) {
   std::strncpy(reuse->key, key, kKeyLen - 1);
   ++hdr_->shard_live[s];
   return reuse;
+}
+
+bool Ledger::put_record(PodSlot* p, const Demand& d, const Plan& plan) {
+  free_record(p);
+  if (d.n <= kSlotContainers && plan.n <= kSlotContainers) {
+    p->demand.n = d.n;
+    std::memcpy(p->demand.c, d.c, sizeof(ContainerDemand) * static_cast<size_t>(std::max(0, d.n)));
+    p->plan.n = plan.n;
+    p->plan.score = plan.score;
+    std::memcpy(p->plan.off, plan.off, sizeof(int16_t) * static_cast<size_t>(std::max(0, plan.n) + 1));
+    std::memcpy(p->plan.idx, plan.idx, sizeof(plan.idx));
+    return true;
+  }
+  const uint32_t cap = hdr_->ext_cap;
+  const uint32_t start = hdr_->ext_hint.load(std::memory_order_relaxed);
+  for (uint32_t k = 0; k < cap; ++k) {
+    const uint32_t i = (start + k) % cap;
+    int32_t free_ = 0;
+    if (ext_[i].used.load(std::memory_order_relaxed) == 0 &&
+        ext_[i].used.compare_exchange_strong(free_, 1, std::memory_order_acquire)) {
+      ext_[i].demand = d;
+      ext_[i].plan = plan;
+      p->ext = static_cast<int32_t>(i) + 1;
+      p->demand.n = d.n;
+      p->plan.n = plan.n;
+      p->plan.score = plan.score;
+      hdr_->ext_hint.store((i + 1) % cap, std::memory_order_relaxed);
+      hdr_->ext_used.fetch_add(1, std::memory_order_relaxed);
+      return true;
+    }
+  }
+  return false;
+}
+
+void Ledger::get_record(const PodSlot& p, Demand* d, Plan* plan) const {
+  if (p.ext > 0 && static_cast<uint32_t>(p.ext) <= hdr_->ext_cap) {
+    const ExtRecord& e = ext_[p.ext - 1];
+    if (d) *d = e.demand;
+    if (plan) *plan = e.plan;
+    return;
+  }
+  if (d) {
+    std::memset(d, 0, sizeof(Demand));
+    d->n = std::clamp(p.demand.n, 0, kSlotContainers);
+    std::memcpy(d->c, p.demand.c, sizeof(ContainerDemand) * static_cast<size_t>(d->n));
+  }
+  if (plan) {
+    std::memset(plan, 0, sizeof(Plan));
+    plan->n = std::clamp(p.plan.n, 0, kSlotContainers);
+    plan->score = p.plan.score;
+    std::memcpy(plan->off, p.plan.off, sizeof(int16_t) * static_cast<size_t>(plan->n + 1));
+    std::memcpy(plan->idx, p.plan.idx, sizeof(p.plan.idx));
+  }
+}
+
+void Ledger::free_record(PodSlot* p) {
+  if (p->ext > 0 && static_cast<uint32_t>(p->ext) <= hdr_->ext_cap) {
+    ext_[p->ext - 1].used.store(0, std::memory_order_release);
+    hdr_->ext_used.fetch_sub(1, std::memory_order_relaxed);
+  }
+  p->ext = 0;
 }
 
 int32_t Ledger::upsert_node(const std::string& name, const Device* devs, int n,
@@ -672,12 +742,12 @@ int32_t Ledger::reserve_as(int32_t id, const std::string& key, const Demand& d, 
         }
         p->state = state;
         p->t_reserved = mono_now();
-        *plan = p->plan;
+        get_record(*p, nullptr, plan);
         return state == kPodReserved ? kOk : kOkExisting;
       }
       if (state == kPodNominated) return kOkExisting;   // already bound or binding
       if (p->node != id) return kErrPodExists;
-      *plan = p->plan;
+      get_record(*p, nullptr, plan);
       return kOkExisting;
     }
   }
@@ -693,13 +763,17 @@ int32_t Ledger::reserve_as(int32_t id, const std::string& key, const Demand& d, 
     lock_mu(&hdr_->shard_mu[s].m);
     Unlock us{&hdr_->shard_mu[s].m};
     PodSlot* p = insert_pod_locked(s, h, key.c_str());
+    if (p && !put_record(p, d, *plan)) {
+      p->state = kPodTombstone;       // no overflow record free: give the slot back
+      --hdr_->shard_live[s];
+      ++hdr_->shard_tomb[s];
+      p = nullptr;
+    }
     if (!p) {
       unapply(n->devs, n->n_devs, d, *plan);
       return kErrTableFull;
     }
     p->node = id;
-    p->demand = d;
-    p->plan = *plan;
     p->t_reserved = mono_now();
     p->owner = 0;
     p->state = state;
@@ -743,13 +817,17 @@ int32_t Ledger::allocate_plan(int32_t id, const std::string& key, const Demand& 
     lock_mu(&hdr_->shard_mu[s].m);
     Unlock us{&hdr_->shard_mu[s].m};
     PodSlot* p = insert_pod_locked(s, h, key.c_str());
+    if (p && !put_record(p, d, plan)) {
+      p->state = kPodTombstone;
+      --hdr_->shard_live[s];
+      ++hdr_->shard_tomb[s];
+      p = nullptr;
+    }
     if (!p) {
       unapply(n->devs, n->n_devs, d, plan);
       return kErrTableFull;
     }
     p->node = id;
-    p->demand = d;
-    p->plan = plan;
     p->t_reserved = mono_now();
     p->owner = 0;
     p->state = committed ? kPodCommitted : kPodReserved;
@@ -801,7 +879,13 @@ int32_t Ledger::release_if(const std::string& key, int32_t only_state) {
   PodSlot* p = find_pod_locked(s, h, key.c_str());
   if (!p || p->node != id) return kErrUnknownPod;  // raced with another release
   if (only && p->state != only_state) return kOkExisting;   // adopted / committed meanwhile
-  unapply(n->devs, n->n_devs, p->demand, p->plan);
+  {
+    Demand pd;
+    Plan pp;
+    get_record(*p, &pd, &pp);
+    unapply(n->devs, n->n_devs, pd, pp);
+  }
+  free_record(p);
   p->state = kPodTombstone;
   --hdr_->shard_live[s];
   ++hdr_->shard_tomb[s];
@@ -823,8 +907,7 @@ bool Ledger::lookup(const std::string& key, PodRecord* out) const {
   out->node = p->node;
   out->state = p->state;
   out->t_reserved = p->t_reserved;
-  out->demand = p->demand;
-  out->plan = p->plan;
+  get_record(*p, &out->demand, &out->plan);
   out->owner = p->owner;
   return true;
 }
@@ -859,8 +942,10 @@ std::pair<int32_t, int32_t> Ledger::learn_stream_owners(bool forget_cool, double
       if (p.state != kPodCommitted || p.node < 0) continue;
       int16_t seen[kMaxPlanIdx];
       int n_seen = 0;
-      for (int k = 0; k < p.plan.off[p.plan.n] && k < kMaxPlanIdx; ++k) {
-        const int16_t x = p.plan.idx[k];
+      Plan pl;
+      get_record(p, nullptr, &pl);
+      for (int k = 0; k < pl.off[pl.n] && k < kMaxPlanIdx; ++k) {
+        const int16_t x = pl.idx[k];
         if (x < 0 || std::find(seen, seen + n_seen, x) != seen + n_seen) continue;
         seen[n_seen++] = x;
         Tenancy& te = dev[(static_cast<uint64_t>(p.node) << 16) | static_cast<uint16_t>(x)];
@@ -933,8 +1018,7 @@ int32_t Ledger::fits_without(int32_t id, const std::vector<std::string>& victims
       Unlock us{&hdr_->shard_mu[s].m};
       const PodSlot* p = find_pod_locked(s, h, key.c_str());
       if (!p || p->node != id) continue;
-      vd = p->demand;
-      vp = p->plan;
+      get_record(*p, &vd, &vp);
     }
     unapply(snap.devs, snap.n_devs, vd, vp);
   }
@@ -952,7 +1036,11 @@ std::vector<PodRecord> Ledger::pods_on(int32_t node_id) const {
       const PodSlot& p = t[i];
       if ((p.state == kPodReserved || p.state == kPodCommitted || p.state == kPodNominated) &&
           (node_id < 0 || p.node == node_id))
-        out.push_back(PodRecord{p.key, p.node, p.state, p.t_reserved, p.demand, p.plan, p.owner});
+      {
+        PodRecord r{p.key, p.node, p.state, p.t_reserved, {}, {}, p.owner};
+        get_record(p, &r.demand, &r.plan);
+        out.push_back(std::move(r));
+      }
     }
   }
   return out;

@@ -84,11 +84,12 @@ static void churn(Ledger& l, int n_nodes, int seed, int iters, std::atomic<int>*
     o.policy = static_cast<Policy>(rng() % 4);
     Demand d;
     std::memset(&d, 0, sizeof(d));
-    d.n = 1 + static_cast<int>(rng() % 3);
+    // one pod in 16 is wide (20 containers): its record spills into an overflow record
+    d.n = rng() % 16 == 0 ? 20 : 1 + static_cast<int>(rng() % 3);
     static const int pcts[] = {0, 10, 25, 50, 100, 200};
     for (int c = 0; c < d.n; ++c) {
-      d.c[c].pct = pcts[rng() % 6];
-      d.c[c].mib = static_cast<int64_t>(rng() % 4) * 8192;
+      d.c[c].pct = d.n > 16 ? 5 * static_cast<int>(rng() % 2) : pcts[rng() % 6];
+      d.c[c].mib = d.n > 16 ? 0 : static_cast<int64_t>(rng() % 4) * 8192;
     }
     const int node = static_cast<int>(rng() % n_nodes);
     const std::string key = "s" + std::to_string(seed) + "-" + std::to_string(it);
@@ -454,6 +455,7 @@ int main(int argc, char** argv) {
     }
   }
   CHECK(ledger->n_pods() == 0);
+  CHECK(ledger->overflow_records_used() == 0);
   const auto st = fe.filter_stats.count.load() + fe.prio_stats.count.load();
   std::printf("stress ok: %d threads x %d iters, %d reservations, %llu native verbs\n", threads, iters,
               reserved.load(), static_cast<unsigned long long>(st));

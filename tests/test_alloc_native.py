@@ -357,3 +357,29 @@ def test_a_pod_that_replaced_a_streaming_tenant_is_not_blamed_for_its_mark():
     # once a whole window has passed with it alone there, the mark is its own
     assert L.learn_stream_owners(True, reserved_before=N.mono_now()) == (1, 0)
     assert L.is_stream_owner("compute-job")
+
+
+def test_overflow_records_hold_wide_pods_and_are_reused():
+    """Pods over 16 containers spill into the ledger's overflow records: lookups return the
+    whole demand and plan, a release frees the record for the next wide pod."""
+    t = synthetic_mi355x(8)
+    L = N.Ledger("", 4, 64, True)           # 64 pods -> 64 overflow records
+    nid = L.upsert_node("n0", t.ledger_devices(True), t.ledger_topo())
+    wide = [(2, 0)] * 40
+    rc, plan = L.reserve(nid, "w0", wide, BIN)
+    assert rc == N.OK and len(plan) == 40
+    rec = L.lookup("w0")
+    assert rec["demand"] == [(2, 0)] * 40 and rec["plan"] == plan
+    assert L.overflow_records_used == 1
+    assert L.release("w0") == N.OK and L.overflow_records_used == 0
+    keys = []
+    for i in range(64):
+        rc, _ = L.reserve(nid, f"w{i}", [(1, 0)] * 17, BIN)
+        if rc != N.OK:
+            break
+        keys.append(f"w{i}")
+    assert L.overflow_records_used == len(keys) == 47      # 800 % / 17 % per pod
+    for k in keys:
+        assert L.release(k) == N.OK
+    assert L.overflow_records_used == 0 and L.n_pods == 0
+    assert all(d["pct_free"] == 100 for d in L.snapshot(nid)["devices"])

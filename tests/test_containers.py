@@ -1,8 +1,8 @@
 """Pods with any number of containers (reference allocate.go:54-62 and rater.go:74-110 place
 one demand slot per container, without a limit).
 
-A ledger record holds 16 containers; larger pods keep only their GPU-requesting containers
-there (podutil.ledger_view). Every verb answers in the extender protocol whatever the pod
+A ledger record holds 64 containers (16 inline in the pod's slot, more in an overflow record);
+larger pods keep only their GPU-requesting containers there (podutil.ledger_view). Every verb answers in the extender protocol whatever the pod
 looks like: filter reports unplaceable pods in FailedNodes, never as an HTTP error.
 """
 import asyncio
@@ -79,11 +79,11 @@ def test_too_many_gpu_containers_is_a_failed_node_not_an_error():
             store, rt = await _runtime(2, frontend=frontend)
             loop = asyncio.get_running_loop()
             try:
-                pod = store.create_pod(_sidecar_pod("huge", 30, set(range(20)), pct=5))
+                pod = store.create_pod(_sidecar_pod("huge", 70, set(range(66)), pct=1))
                 f, p, b = await loop.run_in_executor(None, _schedule, rt, store, pod, ["n0", "n1"])
                 body = json.loads(f[1])
                 assert f[0] == 200 and not body["NodeNames"] and body["Error"] == ""
-                assert all("at most 16" in r for r in body["FailedNodes"].values()), body
+                assert all("at most 64" in r for r in body["FailedNodes"].values()), body
                 assert p[0] == 200 and [h["Score"] for h in json.loads(p[1])] == [0, 0]
                 assert b is None
             finally:
@@ -99,19 +99,63 @@ def test_fuzz_container_counts_never_answer_5xx():
         rng = random.Random(11)
         try:
             for i in range(40):
-                n = rng.randint(0, 64)
-                gpu = set(rng.sample(range(n), min(n, rng.choice([0, 1, 2, 5, 17])))) if n else set()
-                pod = store.create_pod(_sidecar_pod(f"f{i}", n, gpu, pct=rng.choice([5, 10, 25])))
+                n = rng.randint(0, 80)
+                gpu = set(rng.sample(range(n), min(n, rng.choice([0, 1, 2, 5, 17, 24, 65])))) if n else set()
+                pod = store.create_pod(_sidecar_pod(f"f{i}", n, gpu, pct=rng.choice([1, 2, 5])))
                 f, p, b = await loop.run_in_executor(None, _schedule, rt, store, pod, ["n0", "n1", "n2", "n3"])
                 assert f[0] == 200 and p[0] == 200, (n, len(gpu), f, p)
                 fit = json.loads(f[1])["NodeNames"]
-                assert bool(fit) == (len(gpu) <= 16), (n, len(gpu), f)
+                # the pods are small (at most 65 x 5 % on four 8-GPU nodes): only the cap refuses
+                assert bool(fit) == (len(gpu) <= 64), (n, len(gpu), f)
                 if b is not None:
                     assert b == (200, b'{"Error":""}'), (n, len(gpu), b)
         finally:
             await rt.stop()
 
     asyncio.run(main())
+
+
+def test_twenty_four_gpu_containers_schedule_through_both_front_doors_and_rebuild():
+    """the reference places any number of GPU containers
+    (allocate.go:54-62). 24 containers of 5 % each (over the 16 a pod slot holds inline) take
+    an overflow record, schedule through the native and the Python front door, release on
+    delete and come back from their annotations after a restart."""
+    for frontend in ("native", "aiohttp"):
+        async def main():
+            store, rt = await _runtime(2, frontend=frontend)
+            loop = asyncio.get_running_loop()
+            try:
+                pod = store.create_pod(_sidecar_pod("wide24", 24, set(range(24)), pct=5))
+                f, p, b = await loop.run_in_executor(None, _schedule, rt, store, pod, ["n0", "n1"])
+                assert f[0] == 200 and json.loads(f[1])["NodeNames"], (frontend, f)
+                assert b == (200, b'{"Error":""}'), (frontend, b)
+                got = store.get_pod("default", "wide24")
+                ann = got["metadata"]["annotations"]
+                devs = [int(ann[T.container_annotation(f"c{k}")]) for k in range(24)]
+                node = pu.node_name_of(got)
+                used = {d: devs.count(d) * 5 for d in set(devs)}
+                gpus = rt.state.status()[node]["GPUs"]
+                assert all(gpus[d]["Percent"] == 100 - u for d, u in used.items())
+                led = rt.state.ledger
+                rec = led.lookup(pu.pod_uid(got))
+                assert len(rec["demand"]) == 24 and [x[0] for x in rec["plan"]] == devs
+                assert led.overflow_records_used == 1
+                # restart: a fresh runtime rebuilds the wide pod from its annotations
+                rt2 = await runtime(store)
+                try:
+                    g2 = rt2.state.status()[node]["GPUs"]
+                    assert all(g2[d]["Percent"] == 100 - u for d, u in used.items())
+                    assert rt2.state.ledger.lookup(pu.pod_uid(got))["plan"] == rec["plan"]
+                finally:
+                    await rt2.stop()
+                store.delete_pod("default", "wide24")
+                assert await wait_for(lambda: led.lookup(pu.pod_uid(got)) is None)
+                assert led.overflow_records_used == 0
+                assert all(g["Percent"] == 100 for g in rt.state.status()[node]["GPUs"])
+            finally:
+                await rt.stop()
+
+        asyncio.run(main())
 
 
 def test_restart_rebuilds_a_pod_with_more_than_16_containers():
