@@ -77,6 +77,18 @@ def parse_args():
                          "rank's extender talks REST to, with only rank 0 running the pod controller")
     ap.add_argument("--inproc-variant-steps", type=int, default=3,
                     help="after the timed steps, a pass with --inproc-api (0: none)")
+    ap.add_argument("--steady", action="store_true",
+                    help="steady-state churn instead of bursts: --pods fill the cluster once, then every step "
+                         "deletes 30 %% of the live pods and creates as many (nanogpu.sim.workload.steady)")
+    ap.add_argument("--steady-variant-steps", type=int, default=6,
+                    help="after the timed steps, a --steady pass with this many timed steps (0: none); "
+                         "frag_pct_steady is the mean of its second half")
+    ap.add_argument("--nodes-variant", type=int, default=1000,
+                    help="after the timed steps, a pass on this many nodes with kube-scheduler's node "
+                         "sampling (numFeasibleNodesToFind); 0: none")
+    ap.add_argument("--nodes-variant-pods", type=int, default=0,
+                    help="pods per burst of the --nodes-variant pass (0: --pods scaled to the same occupancy)")
+    ap.add_argument("--nodes-variant-steps", type=int, default=2)
     ap.add_argument("--apiserver-threads", type=int, default=0,
                     help="shared API server IO threads (0: one per rank, 4 to 16)")
     ap.add_argument("--bind-writer-threads", type=int, default=0,
@@ -309,20 +321,46 @@ HBM_GIB = (8, 16, 32, 64)
 
 
 def burst(rank: int, world: int, total: int, step: int, seed: int) -> list[dict]:
-    """Deterministic (sizes and UIDs), so the driver process rebuilds the same objects."""
+    """Deterministic (sizes, owners and UIDs), so the driver process rebuilds the same objects
+    (nanogpu.sim.workload: three pods in five belong to one of 16 ReplicaSets)."""
     import uuid
 
-    from nanogpu.k8s import podutil as pu
+    from nanogpu.sim import workload as W
 
-    rng = random.Random(seed * 1000003 + step)
     pods = []
-    for i in range(total):
-        pct, gib = rng.choice(SIZES), rng.choice(HBM_GIB)
+    for spec in W.burst_specs(step, total, seed):
+        i = spec.key
         if i % world != rank:
             continue
         uid = str(uuid.UUID(int=((step & 0xFFFFFFFF) << 64) | (rank << 32) | i))
-        pods.append(pu.make_pod(f"s{step}-p{i}", [("main", pct, gib * 1024)], namespace=f"bench-r{rank}", uid=uid))
+        pods.append(W.make_pod(spec, f"s{step}-p{i}", f"bench-r{rank}", uid))
     return pods
+
+
+STEADY_CHURN = 0.3
+STEADY_SEED = 11
+
+
+def steady_uid(key: int, rank: int) -> str:
+    import uuid
+
+    return str(uuid.UUID(int=(0x57EAD << 96) | (rank << 48) | key))
+
+
+def steady_pod(spec, rank: int) -> dict:
+    """A pod of the steady-state stream (nanogpu.sim.workload.steady), handled by rank
+    key % world: it lives across steps until the stream deletes it."""
+    from nanogpu.sim import workload as W
+
+    return W.make_pod(spec, f"k{spec.key}", f"bench-r{rank}", steady_uid(spec.key, rank))
+
+
+def steady_stream(args):
+    """Step 0 fills the cluster with --pods pods; each later step deletes 30 % of the live pods
+    and creates as many (warm-up steps first, then the timed ones)."""
+    from nanogpu.sim import workload as W
+
+    return W.steady(1 + args.warmup + args.steps, args.pods, STEADY_CHURN, STEADY_SEED)
 
 
 def apiserver_main(conn, avoid: list[int] | None = None, near: int = -1) -> None:
@@ -399,6 +437,16 @@ def apiserver_main(conn, avoid: list[int] | None = None, near: int = -1) -> None
             n = srv.delete_pods(keys.pop(msg[1]))
             conn.send((n, time.perf_counter() - t))
             conn.send(fut.result())
+        elif op == "churn_keys":
+            # steady-state churn: the given pods (created in earlier steps) are deleted, then
+            # this step's pods are created; one reply each
+            steps_keys = msg[1]
+            t = time.perf_counter()
+            n = srv.delete_pods(steps_keys) if steps_keys else 0
+            conn.send((n, time.perf_counter() - t))
+            t = time.perf_counter()
+            codes = srv.create_pods(steps.pop(msg[2])) if msg[2] in steps else []
+            conn.send((sum(1 for c in codes if c == 201), time.perf_counter() - t))
         elif op == "stats":
             conn.send(_json.loads(srv.stats()))
         elif op == "end":            # the pass is over
@@ -478,6 +526,12 @@ class ApiServerProc:
         deleted = await arecv(self.conn)
         return deleted, asyncio.ensure_future(arecv(self.conn))
 
+    async def churn_keys(self, dels: list[tuple[str, str]], create_step: int):
+        """Steady state: delete `dels` (namespace, name), then create `create_step`'s pods:
+        ((deleted, s), (created, s))."""
+        self.conn.send(("churn_keys", dels, create_step))
+        return await arecv(self.conn), await arecv(self.conn)
+
     def stats(self) -> dict:
         return self._rpc("stats")
 
@@ -503,14 +557,26 @@ def driver_main(conn) -> None:
     from nanogpu.sim.driver import NativeSchedulerDriver, ThreadedSchedulerDriver
     from nanogpu.sim.kubescore import KubeScoring
 
-    st = {"cfg": None, "work": {}, "session": None, "cls": NativeSchedulerDriver}
+    st = {"cfg": None, "work": {}, "session": None, "cls": NativeSchedulerDriver, "live": {}, "specs": {}}
 
     def configure(cfg: dict) -> None:
-        cls = ThreadedSchedulerDriver if cfg.get("driver") == "python" else NativeSchedulerDriver
+        # steady-state churn needs the stand-in's pod cache: the native stand-in only
+        cls = ThreadedSchedulerDriver if cfg.get("driver") == "python" and not cfg.get("steady") \
+            else NativeSchedulerDriver
         native = cls is NativeSchedulerDriver
+        cfg["name_index"] = {n: i for i, n in enumerate(cfg["names"])}
         # the pods of every step, built before the clock starts (the main process does the same)
         work = {}
-        for step in cfg["steps"]:
+        st["live"], st["specs"], st["stream"] = {}, {}, None
+        if cfg.get("steady"):
+            # steady-state churn: pods live across steps; the stand-in keeps kube-scheduler's
+            # cache of them (node, requests, owner) and hands it to every run
+            stream = st["stream"] = steady_stream(argparse.Namespace(**cfg["steady"]))
+            for step in cfg["steps"]:
+                specs = [s for s in stream[step].creates if s.key % cfg["world"] == cfg["rank"]]
+                st["specs"][step] = specs
+                work[step] = NativeSchedulerDriver.prepare_native([steady_pod(s, cfg["rank"]) for s in specs])
+        for step in ([] if cfg.get("steady") else cfg["steps"]):
             pods = burst(cfg["rank"], cfg["world"], cfg["pods"], step, 7)
             work[step] = NativeSchedulerDriver.prepare_native(pods) if native else pods
         cfg["kube_obj"] = KubeScoring() if cfg.get("kube") else None
@@ -539,7 +605,18 @@ def driver_main(conn) -> None:
                   else {"bind_threads": min(32, cfg["inflight"])})
             t0 = time.perf_counter()
             drv = cls("127.0.0.1", cfg["port"], cfg["names"], cfg["caps"], seed=step * 1009 + cfg["rank"], **kw)
-            stats = drv.run(prepared=work.pop(step)) if native else drv.run(work.pop(step))
+            if st["stream"] is not None:
+                live = st["live"]
+                for key in st["stream"][step].deletes:
+                    live.pop(key, None)
+                stats = drv.run(prepared=work.pop(step), live=list(live.values()))
+                args_k, node_of = drv._placed[-1]
+                idx = cfg["name_index"]
+                for spec, a, node in zip(st["specs"].pop(step), args_k, node_of):
+                    if node:
+                        live[spec.key] = (idx[node], a[4], a[5], a[6], a[7])
+            else:
+                stats = drv.run(prepared=work.pop(step)) if native else drv.run(work.pop(step))
             drv.close()
             t1 = time.perf_counter()
             sm = stats.summary()
@@ -614,7 +691,12 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     names = [pu.meta(n)["name"] for n in nodes]
     caps = node_capacities(nodes)
     api = InProcKube(store) if store is not None else None   # the workload's client (creates, deletes)
-    if apisrv is not None:
+    steady = bool(getattr(args, "steady", False))
+    stream = steady_stream(args) if steady else None
+    if apisrv is not None and steady:
+        for k, stp in enumerate(stream):
+            apisrv.load(k, [steady_pod(s, s.key % d.world) for s in stp.creates])
+    elif apisrv is not None:
         for st in all_steps_pre:
             apisrv.load(st, [p for r in range(d.world) for p in burst(r, d.world, args.pods, st, 7)])
     pod_ctrl = rt.controllers[-1] if rt.leader else None
@@ -623,13 +705,15 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     # synthetic pod objects are generated up front (client-side data, not scheduler work);
     # their creation in the API server, scheduling, deletion and release are all timed
     all_steps = [10_000 + w for w in range(args.warmup)] + list(range(args.steps))
-    bursts = {s: burst(d.rank, d.world, args.pods, s, 7) for s in all_steps}
+    bursts = {} if steady else {s: burst(d.rank, d.world, args.pods, s, 7) for s in all_steps}
 
     if conn is not None:
         conn.send({"port": rt.bound_port, "names": names, "caps": caps, "rank": d.rank, "world": d.world,
                    "pods": args.pods, "inflight": args.inflight_binds, "driver": args.driver,
                    "kube": not args.no_kube_combine,
-                   "steps": [10_000 + w for w in range(args.warmup)] + list(range(args.steps))})
+                   "steady": {"warmup": args.warmup, "steps": args.steps, "pods": args.pods} if steady else None,
+                   "steps": list(range(len(stream))) if steady else
+                   [10_000 + w for w in range(args.warmup)] + list(range(args.steps))})
         await loop.run_in_executor(None, conn.recv)   # the stand-in has built its pods
 
     # The workload's clients create the next burst while the pod controller releases this one
@@ -640,7 +724,43 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     created: dict = {}       # step -> its create, started during the previous step's release
     srv_ms: dict = {}        # step -> the API server's own create/delete time
 
+    async def one_step_steady(step: int, timed: bool) -> dict:
+        """Steady-state churn: this step's deletions (pods of earlier steps) and creations, the
+        controller's releases, then the stand-in schedules the new pods next to the live ones."""
+        t_step0 = time.perf_counter()
+        dels = stream[step].deletes
+        phases: dict = {}
+        if apisrv is not None:
+            (n_d, dt_d), (n_c, dt_c) = await apisrv.churn_keys(
+                [(f"bench-r{k % d.world}", f"k{k}") for k in dels], step)
+            phases.update(delete_srv_ms=1e3 * dt_d, create_srv_ms=1e3 * dt_c)
+        uids = [steady_uid(k, k % d.world) for k in dels]
+        lookup = rt.state.ledger.lookup
+        t_spin = time.perf_counter() + 0.003
+        for _ in range(50000):
+            if not uids or (not lookup(uids[-1]) and not any(lookup(u) for u in uids)):
+                break
+            await asyncio.sleep(0 if time.perf_counter() < t_spin else 0.0002)
+        phases["release_ms"] = 1e3 * (time.perf_counter() - t_step0)
+        if shared:
+            await barrier()
+        t_send = time.perf_counter()
+        conn.send(("step", step))
+        summary = await arecv(conn)
+        phases["schedule_wall_ms"] = 1e3 * (time.perf_counter() - t_send)
+        await barrier()
+        frag = rt.state.frag(min(SIZES))
+        phases.update(create_ms=0.0, schedule_ms=1e3 * summary["span_s"])
+        client_s = summary.pop("bind_s_all", [])
+        walls = rt.native.fe.take_bind_wall() if rt.native is not None else []
+        if timed:
+            results["client_bind_s"].extend(client_s)
+            results["frontdoor_bind_ms"].extend(1e3 * x for x in walls)
+        return {"stats": summary, "frag": frag, "phases": phases}
+
     async def one_step(step: int, timed: bool, nxt: int | None = None) -> dict:
+        if steady:
+            return await one_step_steady(step, timed)
         pods = bursts.pop(step)
         t_step0 = tc = time.perf_counter()
         if conn is not None:
@@ -760,8 +880,12 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
             gc_pause["n"] += 1
 
     gc.callbacks.append(on_gc)
-    for w in range(args.warmup):
-        await one_step(10_000 + w, False, 10_000 + w + 1 if w + 1 < args.warmup else None)
+    if steady:   # step 0 fills the cluster; then the warm-up churn steps; then the timed ones
+        warm_ids, timed_ids = list(range(1 + args.warmup)), list(range(1 + args.warmup, len(stream)))
+    else:
+        warm_ids, timed_ids = [10_000 + w for w in range(args.warmup)], list(range(args.steps))
+    for k, w in enumerate(warm_ids):
+        await one_step(w, False, warm_ids[k + 1] if k + 1 < len(warm_ids) else None)
     rt.tracer.buf.clear()
     await barrier()
     d.sync()
@@ -777,8 +901,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     t0 = time.perf_counter()
     if sampler is not None:
         sampler.on.set()
-    for s in range(args.steps):
-        r = await one_step(s, True, s + 1 if s + 1 < args.steps else None)
+    for k, s in enumerate(timed_ids):
+        r = await one_step(s, True, timed_ids[k + 1] if k + 1 < len(timed_ids) else None)
         results["steps"].append(r["stats"])
         results["frag"].append(r["frag"])
         results.setdefault("phases", []).append(r["phases"])
@@ -799,6 +923,9 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     results["nominations"] = {k: nom1[k] - nom0[k] for k in nom1}
     results["nomination_margin"] = rt.state.ledger.nomination_margin
     results["unschedulable_attempts"] = sum(st.get("unschedulable_attempts", 0) for st in results["steps"])
+    cycles = sum(st.get("cycles", 0) for st in results["steps"])
+    results["nodes_sent_per_filter"] = (round(sum(st.get("nodes_sent_filter", 0) for st in results["steps"]) / cycles, 1)
+                                        if cycles else None)
     n_sched = max(1, sum(st["scheduled"] for st in results["steps"]))
     results["cpu_us_per_pod"] = 1e6 * (time.process_time() - cpu0) / n_sched
     results["loop_cpu_us_per_pod"] = 1e6 * (time.thread_time() - loop_cpu0) / n_sched
@@ -877,9 +1004,31 @@ def main() -> int:
     d = Dist(args.gpus)
     d.init(use_gpu=not args.no_gpu)
     topo, gpu_info = node_template(d, args)
-    variant = inproc_v = None
+    variant = inproc_v = steady_v = nodes_v = None
     try:
         res = run_pass(d, args, topo, conn, "main", api_proc)
+        shared_api = not args.inproc_api and not args.inproc_driver
+        if args.steady_variant_steps > 0 and not args.steady and shared_api:
+            # steady-state churn (BASELINE config 5 at scale): the cluster is never emptied
+            s_args = argparse.Namespace(**{**vars(args), "steady": True, "steps": args.steady_variant_steps,
+                                           "warmup": 2, "profile_out": "", "stall_trace": "", "api_rtt_ms": 0.0})
+            try:
+                steady_v = (s_args, run_pass(d, s_args, topo, conn, "steady", api_proc))
+                steady_v = (s_args, steady_v[1], summarize(d, s_args, steady_v[1]))
+            except Exception as e:
+                steady_v = {"error": f"{type(e).__name__}: {e}"}
+        if args.nodes_variant > 0 and args.nodes_variant != args.nodes and not args.steady and shared_api:
+            # a large cluster behind kube-scheduler's node sampling: the extender sees only the
+            # share of feasible nodes numFeasibleNodesToFind lets through, from a rotating start
+            nv_pods = args.nodes_variant_pods or round(args.pods * args.nodes_variant / max(1, args.nodes))
+            n_args = argparse.Namespace(**{**vars(args), "nodes": args.nodes_variant, "pods": nv_pods,
+                                           "steps": args.nodes_variant_steps, "warmup": 1, "profile_out": "",
+                                           "stall_trace": "", "api_rtt_ms": 0.0})
+            try:
+                r = run_pass(d, n_args, topo, conn, "nodes", api_proc)
+                nodes_v = (n_args, r, summarize(d, n_args, r))
+            except Exception as e:
+                nodes_v = {"error": f"{type(e).__name__}: {e}"}
         if args.rtt_variant_ms > 0:
             # the same burst with a modelled API-server round trip on every API call (untimed
             # for `value`; its own clock): what the pods/s above excludes
@@ -988,6 +1137,8 @@ def main() -> int:
                 line[f"p50_bind_ms_{tag}"] = variant["p50_bind_ms"]
                 line[f"p99_bind_ms_{tag}"] = variant["p99_bind_ms"]
                 line[f"steps_{tag}"] = args.rtt_variant_steps
+        line.update(steady_keys(args, topo, steady_v))
+        line.update(nodes_variant_keys(args, topo, nodes_v))
         if inproc_v is not None:
             if "error" in inproc_v:
                 line["value_inproc_api"] = None
@@ -1061,6 +1212,66 @@ def summarize(d: Dist, args, res: dict) -> dict:
             "schedule_ms_by_rank": [round(v, 2) for v in d.gather_obj((res.get("phase_ms") or {}).get("schedule_ms", 0.0))]}
 
 
+def _frag_mean(frags: list[dict], key: str = "frag_pct"):
+    return round(statistics.mean(f[key] for f in frags), 3) if frags else None
+
+
+def steady_keys(args, topo, v) -> dict:
+    """frag% under steady-state churn, live (second half of the pass's timed steps), with the
+    reference algorithm and the native one replayed offline on the same stream."""
+    if v is None:
+        return {}
+    if isinstance(v, dict):
+        return {"value_steady": None, "error_steady": v["error"]}
+    s_args, res, out = v
+    half = res["frag"][len(res["frag"]) // 2:]
+    keys = {"value_steady": out["value"], "p50_bind_ms_steady": out["p50_bind_ms"],
+            "frag_pct_steady": _frag_mean(half), "frag_hbm_pct_steady": _frag_mean(half, "frag_mib"),
+            "steps_steady": s_args.steps, "failed_steady": out["failed"],
+            "steady_config": f"{s_args.pods} pods fill {s_args.nodes} nodes, then each step deletes "
+                             f"{int(100 * STEADY_CHURN)} % of the live pods and creates as many; frag = mean of "
+                             f"the last {len(half)} of {s_args.steps} timed steps"}
+    if args.partition == "SPX" and args.policy == "binpack" and not args.compat:
+        from nanogpu.sim import fragsim
+
+        hbm = topo.devices[0].hbm_mib if topo.devices else 288 * 1024
+        n_steps = 1 + s_args.warmup + s_args.steps
+        kw = dict(steps=n_steps, nodes=s_args.nodes, hbm_mib=hbm, initial=s_args.pods, churn=STEADY_CHURN,
+                  seed=STEADY_SEED, kube=True, first=1 + s_args.warmup + s_args.steps // 2)
+        ref, nat = fragsim.steady_state(True, **kw), fragsim.steady_state(False, **kw)
+        keys.update(frag_pct_steady_reference_model=ref["frag_pct"],
+                    frag_hbm_pct_steady_reference_model=ref["frag_hbm_pct"],
+                    frag_pct_steady_native_replay=nat["frag_pct"])
+    return keys
+
+
+def nodes_variant_keys(args, topo, v) -> dict:
+    """The --nodes-variant pass: pods/s, frag%, the reference model's frag% on the same bursts
+    and node sampling, and how often kube-scheduler's choice agreed with the nomination."""
+    if v is None:
+        return {}
+    tag = f"nodes{args.nodes_variant}"
+    if isinstance(v, dict):
+        return {f"value_{tag}": None, f"error_{tag}": v["error"]}
+    n_args, res, out = v
+    nom = res.get("nominations") or {}
+    keys = {f"value_{tag}": out["value"], f"p50_bind_ms_{tag}": out["p50_bind_ms"],
+            f"frag_pct_{tag}": _frag_mean(res["frag"]), f"failed_{tag}": out["failed"],
+            f"unschedulable_{tag}": out["unschedulable"], f"steps_{tag}": n_args.steps,
+            f"pods_per_burst_{tag}": n_args.pods,
+            f"nomination_adopt_pct_{tag}": round(100.0 * nom["adopted"] / nom["made"], 2) if nom.get("made") else None,
+            f"nominations_{tag}": nom,
+            f"nodes_sent_per_filter_{tag}": res.get("nodes_sent_per_filter")}
+    if args.partition == "SPX" and args.policy == "binpack" and not args.compat:
+        from nanogpu.sim import fragsim
+
+        hbm = topo.devices[0].hbm_mib if topo.devices else 288 * 1024
+        kw = dict(steps=n_args.steps, nodes=n_args.nodes, hbm_mib=hbm, pods=n_args.pods, kube=True)
+        keys[f"frag_pct_{tag}_reference_model"] = fragsim.headline(True, **kw)["frag_pct"]
+        keys[f"frag_pct_{tag}_native_replay"] = fragsim.headline(False, **kw)["frag_pct"]
+    return keys
+
+
 def reference_model_frag(args, topo) -> dict:
     """frag% of the reference algorithm (compat mode: the Go raters bit for bit) on the same
     bursts, replayed offline through the same ledger (nanogpu.sim.fragsim) — the reference
@@ -1071,11 +1282,13 @@ def reference_model_frag(args, topo) -> dict:
     from nanogpu.sim import fragsim
 
     hbm = topo.devices[0].hbm_mib if topo.devices else 288 * 1024
-    kw = dict(steps=args.steps, nodes=args.nodes, hbm_mib=hbm, pods=args.pods)
+    kw = dict(steps=args.steps, nodes=args.nodes, hbm_mib=hbm, pods=args.pods, kube=not args.no_kube_combine)
     ref, nat = fragsim.headline(True, **kw), fragsim.headline(False, **kw)
     return {"frag_pct_reference_model": ref["frag_pct"], "frag_hbm_pct_reference_model": ref["frag_hbm_pct"],
             "stranded_pct_reference_model": ref["stranded_pct"], "frag_pct_native_replay": nat["frag_pct"],
-            "frag_reference_model_source": "offline serial replay of the timed bursts, reference binpack "
+            "frag_reference_model_source": "offline serial replay of the timed bursts behind the same "
+                                           "kube-scheduler model (node sampling, NodeResourcesFit, plugin "
+                                           "scores, PodTopologySpread, 10 x extender), reference binpack "
                                            "(compat mode, bit-exact with rater.go) vs native binpack"}
 
 

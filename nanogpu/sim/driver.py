@@ -16,6 +16,7 @@ import asyncio
 import json
 import random
 import time
+import zlib
 from dataclasses import dataclass, field
 
 import aiohttp
@@ -215,6 +216,8 @@ class DriverStats:
     cycle_max_s: float = 0.0
     cycle_sum_s: float = 0.0
     cycle_wire_s: float = 0.0
+    nodes_sent_filter: int = 0     # node names sent to the extender's filter, summed over cycles
+    cycles: int = 0
 
     def summary(self) -> dict:
         span = max(1e-9, self.t_last_bind - self.t_first_filter)
@@ -237,6 +240,7 @@ class DriverStats:
                 "cycle_max_ms": 1e3 * self.cycle_max_s,
                 "cycle_sum_ms": 1e3 * self.cycle_sum_s,
                 "cycle_wire_ms": 1e3 * self.cycle_wire_s,
+                "nodes_sent_filter": self.nodes_sent_filter, "cycles": self.cycles,
                 "e2e_p50_ms": 1e3 * median(e2e),
                 # the burst's window on the monotonic clock (comparable across processes of a node)
                 "t_first_filter": self.t_first_filter, "t_last_bind": self.t_last_bind,
@@ -588,6 +592,17 @@ class ThreadedSchedulerDriver:
         self.cycle.close()
 
 
+def owner_index(pod: dict) -> int:
+    """The pod's controlling owner as the stand-in's int id (PodTopologySpread's selector),
+    -1 for none. kube-scheduler only applies its system default spread constraints to pods a
+    ReplicaSet / StatefulSet / ReplicationController / Service selects."""
+    refs = [r for r in (pu.meta(pod).get("ownerReferences") or []) if isinstance(r, dict)]
+    ctl = next((r for r in refs if r.get("controller") is True), None)
+    if ctl is None or ctl.get("kind") not in ("ReplicaSet", "StatefulSet", "ReplicationController"):
+        return -1
+    return zlib.crc32(str(ctl.get("uid", "")).encode()) & 0x7FFFFFFF
+
+
 class NativeSchedulerDriver:
     """ThreadedSchedulerDriver's protocol loop in C++ (native/src/schedsim.cpp): the same
     serial filter -> priorities -> select-host cycle and asynchronous bind pool, without
@@ -637,21 +652,32 @@ class NativeSchedulerDriver:
             ns, name = pu.pod_ns_name(p)
             d = pu.pod_demand(p)
             cpu, mem = ks.pod_requests(d)
-            args.append((enc.encode(p).encode(), ns, name, pu.pod_uid(p), sum(c for c, _ in d), cpu, mem))
+            args.append((enc.encode(p).encode(), ns, name, pu.pod_uid(p), sum(c for c, _ in d), cpu, mem,
+                         owner_index(p)))
         return args
 
-    def run(self, pods: list[dict] | None = None, prepared: list[tuple] | None = None) -> DriverStats:
+    def run(self, pods: list[dict] | None = None, prepared: list[tuple] | None = None,
+            live: list[tuple] | None = None) -> DriverStats:
+        """`live`: pods bound before this run, (node index, need, cpu_m, mem, owner) each, as
+        kube-scheduler's cache holds them (steady-state churn)."""
         from ..native import core
 
         args = prepared if prepared is not None else self.prepare(pods or [])
         native = None
         if isinstance(args, tuple):   # prepare_native: (pod tuples, SimBurst)
             args, native = args
+        k = self.kube
         r = core().drive_scheduler(self.host, self.port, native if native is not None else args,
                                    self.nodes, self.capacity, self.bind_threads,
                                    self.seed, self.max_attempts, self.backoff_s, self.session,
-                                   kube_combine=int(self.kube is not None),
-                                   extender_weight=self.kube.extender_weight if self.kube else 1)
+                                   kube_combine=int(k is not None),
+                                   extender_weight=k.extender_weight if k else 1,
+                                   sample_nodes=int(k.sample_nodes) if k else 1,
+                                   percentage_of_nodes_to_score=k.percentage_of_nodes_to_score if k else 0,
+                                   spread_weight=k.spread_weight if k else 0,
+                                   live=live or [])
+        self.stats.nodes_sent_filter = r["nodes_sent_filter"]
+        self.stats.cycles = r["cycles"]
         st = self.stats
         st.scheduled, st.failed = r["scheduled"], r["failed"]
         st.bind_errors, st.unschedulable_attempts = r["bind_errors"], r["unschedulable_attempts"]

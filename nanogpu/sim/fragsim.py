@@ -18,7 +18,8 @@ import statistics
 import sys
 
 from nanogpu.native import core
-from nanogpu.sim.kubescore import KubeScoring
+from nanogpu.sim import workload as W
+from nanogpu.sim.kubescore import KubeScoring, spread_scores
 from nanogpu.topology.model import synthetic_mi355x, synthetic_sriov_guest
 
 N = core()
@@ -36,18 +37,34 @@ class Cluster:
         self.rng = random.Random(seed)
         self.live: dict[str, int] = {}
         self.unsched = 0
-        # kube-scheduler combining (None: the extender's arg-max, random ties)
+        # kube-scheduler (None: the extender's arg-max over every node, random ties). With it:
+        # NodeResourcesFit on the gpu-percent capacity, node sampling from a rotating start,
+        # then LeastAllocated + BalancedAllocation + PodTopologySpread + 10 x extender
         self.kube = kube
         if kube is not None:
             kube.rng.seed(seed)
+            kube.next_start = 0
+        self.capacity = 100 * len(topo.devices)
+        self.pct_used = {i: 0 for i in self.ids}
         self.requested = {i: (0, 0) for i in self.ids}
-        self.pod_req: dict[str, tuple[int, int]] = {}
+        self.pod_req: dict[str, tuple[int, int, int, int]] = {}   # uid -> (cpu, mem, pct, owner)
+        self.owner_cnt: dict[tuple[int, int], int] = {}
+        self.nodes_sent = 0
+        self.cycles = 0
 
-    def place(self, uid: str, demand: list) -> bool:
+    def place(self, uid: str, demand: list, owner: int = -1) -> bool:
         if not self.track_hbm:
             demand = [(p, 0) for p, _ in demand]
-        rcs = self.L.filter(self.ids, demand, self.opts)
-        fit = [i for i, rc in zip(self.ids, rcs) if rc == 0]
+        need = sum(p for p, _ in demand)
+        if self.kube is not None:
+            cand = [self.ids[k] for k in self.kube.feasible(
+                len(self.ids), lambda k: self.pct_used[self.ids[k]] + need <= self.capacity)]
+        else:
+            cand = self.ids
+        self.cycles += 1
+        self.nodes_sent += len(cand)
+        rcs = self.L.filter(cand, demand, self.opts) if cand else []
+        fit = [i for i, rc in zip(cand, rcs) if rc == 0]
         if not fit:
             self.unsched += 1
             return False
@@ -56,7 +73,10 @@ class Cluster:
             host = fit[0]
         elif self.kube is not None:
             scores = self.L.score(fit, demand, self.opts)
-            host = fit[self.kube.select([self.kube.total(s, self.requested[i], req) for s, i in zip(scores, fit)])]
+            spread = spread_scores([self.owner_cnt.get((owner, i), 0) for i in fit], self.kube.spread_max_skew) \
+                if owner >= 0 else [0] * len(fit)
+            host = fit[self.kube.select([self.kube.total(s, self.requested[i], req, sp)
+                                         for s, i, sp in zip(scores, fit, spread)])]
         else:
             scores = self.L.score(fit, demand, self.opts)
             best = max(scores)
@@ -67,15 +87,22 @@ class Cluster:
         self.live[uid] = host
         u = self.requested[host]
         self.requested[host] = (u[0] + req[0], u[1] + req[1])
-        self.pod_req[uid] = req
+        self.pct_used[host] += need
+        if owner >= 0:
+            self.owner_cnt[(owner, host)] = self.owner_cnt.get((owner, host), 0) + 1
+        self.pod_req[uid] = (req[0], req[1], need, owner)
         return True
 
     def delete(self, uid: str) -> None:
         host = self.live.pop(uid, None)
         if host is not None:
             self.L.release(uid)
-            req, u = self.pod_req.pop(uid, (0, 0)), self.requested[host]
-            self.requested[host] = (u[0] - req[0], u[1] - req[1])
+            cpu, mem, need, owner = self.pod_req.pop(uid, (0, 0, 0, -1))
+            u = self.requested[host]
+            self.requested[host] = (u[0] - cpu, u[1] - mem)
+            self.pct_used[host] -= need
+            if owner >= 0:
+                self.owner_cnt[(owner, host)] -= 1
 
     def frag(self, min_req: int) -> dict:
         return self.L.frag(min_req)
@@ -98,17 +125,33 @@ def headline(compat: bool, steps: int = 20, nodes: int = 64, hbm_mib: int = 294_
     c = Cluster(topo, nodes, compat, track_hbm=True, seed=1, kube=KubeScoring() if kube else None)
     out = []
     for step in range(step0, step0 + steps):
-        rng = random.Random(7 * 1000003 + step)
         uids = []
-        for i in range(pods):
-            pct, gib = rng.choice((10, 25, 50)), rng.choice((8, 16, 32, 64))
-            uid = f"s{step}-{i}"
-            if c.place(uid, [(pct, gib * 1024)]):
+        for spec in W.burst_specs(step, pods):
+            uid = f"s{step}-{spec.key}"
+            if c.place(uid, [(spec.pct, spec.gib * 1024)], spec.owner):
                 uids.append(uid)
         out.append(c.frag(10))
         for u in uids:
             c.delete(u)
     return summarize(out, c)
+
+
+def steady_state(compat: bool, steps: int = 20, nodes: int = 64, hbm_mib: int = 294_896, initial: int = 1000,
+                 churn: float = 0.3, kube: bool = True, seed: int = 11, first: int | None = None, **_) -> dict:
+    """Steady-state churn (nanogpu.sim.workload.steady): an initial fill, then each step deletes
+    a random 30 % of the live pods and creates as many; frag measured after each step's creates,
+    averaged over the steps from `first` on (default: the second half; the cluster is never
+    emptied). bench.py's steady pass runs the same stream live."""
+    topo = synthetic_mi355x(8, "SPX", hbm_mib=hbm_mib)
+    c = Cluster(topo, nodes, compat, track_hbm=True, seed=seed, kube=KubeScoring() if kube else None)
+    out = []
+    for k, st in enumerate(W.steady(steps, initial, churn, seed)):
+        for key in st.deletes:
+            c.delete(f"k{key}")
+        for spec in st.creates:
+            c.place(f"k{spec.key}", [(spec.pct, spec.gib * 1024)], spec.owner)
+        out.append(c.frag(10))
+    return summarize(out[len(out) // 2 if first is None else first:], c)
 
 
 def config5(compat: bool, rounds: int = 5, pods_n: int = 1000, nodes_n: int = 8, sriov: bool = False,
@@ -149,6 +192,7 @@ def summarize(frs: list[dict], c: Cluster | None, unsched: int | None = None) ->
 
 SCENARIOS = {
     "headline": headline,
+    "steady": steady_state,
     "config5": config5,
     "config5_sriov": lambda compat, **kw: config5(compat, sriov=True, pods_n=125, **kw),
 }

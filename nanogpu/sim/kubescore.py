@@ -17,14 +17,50 @@ more than 10 points emptier. This is what makes a priorities-time nomination wro
 Pods here carry CPU / memory requests proportional to their GPU share (a GPU pod brings its
 host threads and staging memory): `cpu_per_gpu` cores and `mem_per_gpu` bytes per whole
 device, plus the HBM the pod requests mirrored in host memory.
+
+Two more parts of kube-scheduler decide which nodes an extender sees and which it gets:
+  * node sampling (generic_scheduler.go numFeasibleNodesToFind): with 100 nodes or more the
+    in-tree filters stop after an adaptive share of feasible nodes (50 % - nodes/125, at
+    least 5 % and 100 nodes; 42 % of 1,000), starting where the last cycle stopped, and only
+    those are sent to the extender's filter;
+  * PodTopologySpread's system default constraints for pods a ReplicaSet / StatefulSet /
+    ReplicationController / Service selects: hostname maxSkew 3 and zone maxSkew 5, both
+    ScheduleAnyway, plugin weight 2. Nodes without zone labels skip the zone term.
+The native stand-in (native/src/schedsim.cpp) implements the same three models.
 """
 from __future__ import annotations
 
+import math
 import random
 from dataclasses import dataclass, field
 
 MAX_NODE_SCORE = 100
 MAX_EXTENDER_PRIORITY = 10
+MIN_FEASIBLE_NODES = 100
+MIN_FEASIBLE_PERCENT = 5
+BASE_PERCENT = 50
+
+
+def num_feasible_nodes_to_find(all_nodes: int, percentage: int = 0) -> int:
+    """kube-scheduler's numFeasibleNodesToFind (percentageOfNodesToScore 0 = adaptive)."""
+    if all_nodes < MIN_FEASIBLE_NODES:
+        return all_nodes
+    pct = percentage if percentage > 0 else max(MIN_FEASIBLE_PERCENT, BASE_PERCENT - all_nodes // 125)
+    if pct >= 100:
+        return all_nodes
+    return max(MIN_FEASIBLE_NODES, all_nodes * pct // 100)
+
+
+def spread_scores(counts: list[int], max_skew: int = 3) -> list[int]:
+    """PodTopologySpread Score + NormalizeScore for the hostname constraint over the nodes
+    being scored: raw = int(matching pods on the node x log(nodes + 2) + maxSkew - 1), then
+    100 x (max + min - raw) / max (100 for every node when max is 0)."""
+    w = math.log(len(counts) + 2)
+    raw = [int(c * w + (max_skew - 1)) for c in counts]
+    lo, hi = min(raw, default=0), max(raw, default=0)
+    if hi == 0:
+        return [MAX_NODE_SCORE] * len(raw)
+    return [MAX_NODE_SCORE * (hi + lo - r) // hi for r in raw]
 
 
 @dataclass
@@ -36,7 +72,30 @@ class KubeScoring:
     mem_per_gpu: int = 96 << 30
     least_weight: int = 1
     balanced_weight: int = 1
+    spread_weight: int = 2                    # PodTopologySpread (system default constraints)
+    spread_max_skew: int = 3
+    sample_nodes: bool = True                 # numFeasibleNodesToFind
+    percentage_of_nodes_to_score: int = 0
     rng: random.Random = field(default_factory=lambda: random.Random(0))
+    next_start: int = 0                       # nextStartNodeIndex
+
+    def feasible(self, n_nodes: int, fits) -> list[int]:
+        """Indices of the nodes the in-tree filters pass to the extender: from nextStartNodeIndex,
+        node by node, until numFeasibleNodesToFind have passed `fits(i)`."""
+        if not n_nodes:
+            return []
+        want = num_feasible_nodes_to_find(n_nodes, self.percentage_of_nodes_to_score) if self.sample_nodes \
+            else n_nodes
+        out, processed = [], 0
+        for k in range(n_nodes):
+            if len(out) >= want:
+                break
+            i = (self.next_start + k) % n_nodes
+            processed += 1
+            if fits(i):
+                out.append(i)
+        self.next_start = (self.next_start + processed) % n_nodes
+        return out
 
     def pod_requests(self, demand) -> tuple[int, int]:
         """(cpu millicores, memory bytes) of a pod whose containers request `demand`
@@ -55,8 +114,9 @@ class KubeScoring:
         balanced = int((1 - abs(cf - mf)) * MAX_NODE_SCORE)
         return self.least_weight * least + self.balanced_weight * balanced
 
-    def total(self, ext_score: int, used: tuple[int, int], pod: tuple[int, int]) -> int:
-        return (self.plugin_score(used, pod) +
+    def total(self, ext_score: int, used: tuple[int, int], pod: tuple[int, int], spread: int = 0) -> int:
+        """`spread`: the node's normalised PodTopologySpread score (spread_scores), or 0."""
+        return (self.plugin_score(used, pod) + self.spread_weight * spread +
                 self.extender_weight * ext_score * (MAX_NODE_SCORE // MAX_EXTENDER_PRIORITY))
 
     def select(self, totals: list[int]) -> int:

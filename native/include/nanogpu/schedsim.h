@@ -12,7 +12,14 @@
 //   * binds leave as soon as their host is chosen (kube-scheduler's asynchronous binding
 //     cycle, a goroutine per pod): one epoll thread multiplexes up to `bind_threads`
 //     keep-alive connections, POST /scheduler/bind;
-//   * a failed attempt goes back to the queue with exponential backoff, up to max_attempts.
+//   * a failed attempt goes back to the queue with exponential backoff, up to max_attempts;
+//   * kube-scheduler's node sampling (numFeasibleNodesToFind, generic_scheduler.go): with 100
+//     nodes or more the in-tree filters stop after an adaptive share of feasible nodes
+//     (50 % - nodes/125, at least 5 %, at least 100 nodes), starting where the previous cycle
+//     stopped (nextStartNodeIndex), and only those reach the extender;
+//   * PodTopologySpread's system default for pods owned by a ReplicaSet / StatefulSet / ...:
+//     hostname, maxSkew 3, ScheduleAnyway, weight 2 (the zone constraint needs zone labels,
+//     which these nodes do not carry).
 // Times are steady_clock seconds (the clock of Python's time.perf_counter()).
 #pragma once
 
@@ -29,6 +36,14 @@ struct SimPod {
   int64_t need = 0;      // Σ container gpu-percent (the pre-filter's request)
   int64_t cpu_m = 0;     // CPU (millicores) and memory (bytes) requests: kube-scheduler's own
   int64_t mem = 0;       // score plugins see these (nanogpu/sim/kubescore.py)
+  int32_t owner = -1;    // controlling ReplicaSet (index), -1: none (no spread constraint)
+};
+
+// A pod already bound when a run starts (kube-scheduler's cache at a steady state).
+struct SimLive {
+  int32_t node = -1;
+  int64_t need = 0, cpu_m = 0, mem = 0;
+  int32_t owner = -1;
 };
 
 struct SimConfig {
@@ -47,7 +62,19 @@ struct SimConfig {
   int extender_weight = 1;
   int64_t node_cpu_m = 256000;
   int64_t node_mem = int64_t{3} << 40;
+  // numFeasibleNodesToFind: 1 = on (kube-scheduler always samples; below 100 nodes it keeps
+  // every node), 0 = every feasible node goes to the extender. percentage_of_nodes_to_score
+  // 0 = adaptive (the KubeSchedulerConfiguration default).
+  int sample_nodes = 1;
+  int percentage_of_nodes_to_score = 0;
+  // PodTopologySpread system default (owned pods only; needs kube_combine): weight, maxSkew
+  int spread_weight = 2;
+  int spread_max_skew = 3;
+  std::vector<SimLive> live;   // pods bound before this run (resource fit, spread counts)
 };
+
+// kube-scheduler's numFeasibleNodesToFind (v1.18+).
+int64_t num_feasible_nodes_to_find(int64_t all_nodes, int percentage);
 
 struct SimResult {
   int64_t scheduled = 0, failed = 0, bind_errors = 0, unschedulable_attempts = 0;
@@ -57,6 +84,8 @@ struct SimResult {
   std::vector<double> bind_latencies, e2e_latencies;
   std::vector<std::string> node_of;   // per pod; "" = not scheduled
   std::vector<std::string> last_error;
+  int64_t nodes_sent_filter = 0;      // node names sent to the extender's filter, summed
+  int64_t cycles = 0;
 };
 
 // Keep-alive connections carried from one drive() to the next (kube-scheduler's HTTP client

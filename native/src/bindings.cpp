@@ -4,6 +4,7 @@
 
 #include <cstring>
 #include <memory>
+#include <tuple>
 #include <unordered_set>
 #include <vector>
 
@@ -905,6 +906,8 @@ PYBIND11_MODULE(_native, m) {
            "Runs the native verb `iters` times in place (no socket): (ok, seconds per call, last body).")
       .def("reset_max", &Frontend::reset_max, "zero the per-verb and event-loop maxima");
   m.def("mono_now", &mono_now);
+  m.def("num_feasible_nodes_to_find", &sim::num_feasible_nodes_to_find, py::arg("all_nodes"),
+        py::arg("percentage") = 0, "kube-scheduler's numFeasibleNodesToFind (schedsim.h)");
   m.def("presize_fd_table", &presize_fd_table, py::arg("want") = 16384,
         "Grow the process fd table once up front (no RCU-synchronised growth under load).");
   py::class_<sim::Session, std::shared_ptr<sim::Session>>(m, "SchedulerSession")
@@ -917,18 +920,20 @@ PYBIND11_MODULE(_native, m) {
   auto to_sim_pods = [](const py::list& pods) {
     std::vector<sim::SimPod> ps(pods.size());
     for (size_t i = 0; i < pods.size(); ++i) {
-      // (json, ns, name, uid, need[, cpu_m, mem])
+      // (json, ns, name, uid, need[, cpu_m, mem[, owner]])
       auto t = pods[i].cast<py::tuple>();
-      if (t.size() != 5 && t.size() != 7) throw py::value_error("pod tuple: (json, ns, name, uid, need[, cpu_m, mem])");
+      if (t.size() != 5 && t.size() != 7 && t.size() != 8)
+        throw py::value_error("pod tuple: (json, ns, name, uid, need[, cpu_m, mem[, owner]])");
       ps[i].json = t[0].cast<std::string>();
       ps[i].ns = t[1].cast<std::string>();
       ps[i].name = t[2].cast<std::string>();
       ps[i].uid = t[3].cast<std::string>();
       ps[i].need = t[4].cast<int64_t>();
-      if (t.size() == 7) {
+      if (t.size() >= 7) {
         ps[i].cpu_m = t[5].cast<int64_t>();
         ps[i].mem = t[6].cast<int64_t>();
       }
+      if (t.size() == 8) ps[i].owner = t[7].cast<int32_t>();
     }
     return ps;
   };
@@ -945,7 +950,8 @@ PYBIND11_MODULE(_native, m) {
       [to_sim_pods](const std::string& host, int port, const py::object& pods,
          const std::vector<std::string>& nodes, const std::vector<int64_t>& capacity, int bind_threads, uint64_t seed,
          int max_attempts, double backoff_s, std::shared_ptr<sim::Session> session, int kube_combine,
-         int extender_weight) {
+         int extender_weight, int sample_nodes, int percentage_of_nodes_to_score, int spread_weight,
+         const std::vector<std::tuple<int32_t, int64_t, int64_t, int64_t, int32_t>>& live) {
         sim::SimConfig cfg;
         cfg.host = host;
         cfg.port = port;
@@ -957,6 +963,10 @@ PYBIND11_MODULE(_native, m) {
         cfg.backoff_s = backoff_s;
         cfg.kube_combine = kube_combine;
         cfg.extender_weight = extender_weight;
+        cfg.sample_nodes = sample_nodes;
+        cfg.percentage_of_nodes_to_score = percentage_of_nodes_to_score;
+        cfg.spread_weight = spread_weight;
+        for (const auto& [node, need, cpu, mem, owner] : live) cfg.live.push_back({node, need, cpu, mem, owner});
         if (!capacity.empty() && capacity.size() != nodes.size())
           throw py::value_error("capacity must be empty or one entry per node");
         std::shared_ptr<SimBurst> burst;
@@ -985,11 +995,15 @@ PYBIND11_MODULE(_native, m) {
         d["e2e_latencies"] = r.e2e_latencies;
         d["node_of"] = r.node_of;
         d["last_error"] = r.last_error;
+        d["nodes_sent_filter"] = r.nodes_sent_filter;
+        d["cycles"] = r.cycles;
         return d;
       },
       py::arg("host"), py::arg("port"), py::arg("pods"), py::arg("nodes"), py::arg("capacity"),
       py::arg("bind_threads") = 256, py::arg("seed") = 0, py::arg("max_attempts") = 8, py::arg("backoff_s") = 0.001,
       py::arg("session") = nullptr, py::arg("kube_combine") = 0, py::arg("extender_weight") = 1,
+      py::arg("sample_nodes") = 1, py::arg("percentage_of_nodes_to_score") = 0, py::arg("spread_weight") = 2,
+      py::arg("live") = std::vector<std::tuple<int32_t, int64_t, int64_t, int64_t, int32_t>>{},
       "kube-scheduler stand-in (native/src/schedsim.cpp): schedule `pods` through the extender at host:port");
 
   // ------------------------------------------------------------------ native API server

@@ -185,6 +185,7 @@ struct BindJob {
 struct SessionState {
   std::string host;
   int port = -1;
+  size_t next_start = 0;   // kube-scheduler's nextStartNodeIndex survives across cycles
   std::unique_ptr<Conn> cycle;
   std::vector<int> bind_fds;
   void reset() {
@@ -199,6 +200,15 @@ Session::Session() : st_(std::make_unique<SessionState>()) {
   presize_fd_table();   // a long-running scheduler's client pool: no fd-table growth mid-burst
 }
 Session::~Session() = default;
+
+int64_t num_feasible_nodes_to_find(int64_t all_nodes, int percentage) {
+  constexpr int64_t kMinFeasible = 100, kMinPercent = 5, kBasePercent = 50;
+  if (all_nodes < kMinFeasible) return all_nodes;
+  int64_t pct = percentage;
+  if (pct <= 0) pct = std::max(kMinPercent, kBasePercent - all_nodes / 125);
+  if (pct >= 100) return all_nodes;
+  return std::max(kMinFeasible, all_nodes * pct / 100);
+}
 
 SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* session_handle) {
   SessionState* session = session_handle ? session_handle->state() : nullptr;
@@ -233,6 +243,23 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* 
   const bool fit = !cfg.capacity.empty();
   std::vector<int64_t> requested(n_nodes, 0);
   std::vector<int64_t> req_cpu(n_nodes, 0), req_mem(n_nodes, 0);   // for kube_combine
+  // PodTopologySpread: pods of each owner per node, (owner << 32 | node) -> count
+  std::unordered_map<uint64_t, int32_t> owner_cnt;
+  auto owner_key = [](int32_t owner, int node) {
+    return (static_cast<uint64_t>(static_cast<uint32_t>(owner)) << 32) | static_cast<uint32_t>(node);
+  };
+  for (const SimLive& l : cfg.live) {
+    if (l.node < 0 || static_cast<size_t>(l.node) >= n_nodes) continue;
+    requested[l.node] += l.need;
+    req_cpu[l.node] += l.cpu_m;
+    req_mem[l.node] += l.mem;
+    if (l.owner >= 0) ++owner_cnt[owner_key(l.owner, l.node)];
+  }
+  size_t local_start = 0;
+  size_t& next_start = session ? session->next_start : local_start;
+  const int64_t want_feasible =
+      cfg.sample_nodes ? num_feasible_nodes_to_find(static_cast<int64_t>(n_nodes), cfg.percentage_of_nodes_to_score)
+                       : static_cast<int64_t>(n_nodes);
   // NodeResourcesLeastAllocated + NodeResourcesBalancedAllocation with the pod added
   auto plugin_score = [&](size_t n, const SimPod& p) {
     const double cf = std::min(1.0, static_cast<double>(req_cpu[n] + p.cpu_m) / static_cast<double>(cfg.node_cpu_m));
@@ -315,6 +342,7 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* 
       requested[job.node] -= pods[job.pod].need;
       req_cpu[job.node] -= pods[job.pod].cpu_m;
       req_mem[job.node] -= pods[job.pod].mem;
+      if (pods[job.pod].owner >= 0) --owner_cnt[owner_key(pods[job.pod].owner, job.node)];
       ++r.bind_errors;
       r.last_error[job.pod] = std::move(err);
       requeue(job.pod);
@@ -530,6 +558,8 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* 
   std::mt19937_64 rng(cfg.seed);
   std::string body, out, cands_json;
   std::vector<int> cands, fits, ties;
+  std::vector<int64_t> spread_raw;
+  int64_t spread_min = 0, spread_max = 0;
   json::Doc doc;
   for (;;) {
     size_t i;
@@ -549,11 +579,17 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* 
       i = ready.top().pod;
       ready.pop();
       ++attempts[i];
-      // resource-fit pre-filter on the scheduler's own accounting (requests of pods it bound)
+      // resource-fit pre-filter on the scheduler's own accounting (requests of pods it bound),
+      // from nextStartNodeIndex until numFeasibleNodesToFind nodes passed
       cands.clear();
-      if (fit) {
-        for (size_t n = 0; n < n_nodes; ++n)
+      if (fit && n_nodes) {
+        size_t processed = 0;
+        for (size_t k = 0; k < n_nodes && static_cast<int64_t>(cands.size()) < want_feasible; ++k) {
+          const size_t n = (next_start + k) % n_nodes;
+          ++processed;
           if (requested[n] + pods[i].need <= cfg.capacity[n]) cands.push_back(static_cast<int>(n));
+        }
+        next_start = (next_start + processed) % n_nodes;
       }
     }
     const double t_cycle = now_s();
@@ -566,6 +602,8 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* 
     }
     int host = -1;
     if (!fit || !cands.empty()) {
+      ++r.cycles;
+      r.nodes_sent_filter += static_cast<int64_t>(fit ? cands.size() : n_nodes);
       body.assign("{\"Pod\":").append(p.json).append(",\"Nodes\":null,\"NodeNames\":").append(*names).push_back('}');
       int status = 0;
       fits.clear();
@@ -599,6 +637,24 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* 
           // req_cpu / req_mem also change on the binder thread (a failed bind): read under mu
           std::unique_lock<std::mutex> plk(mu, std::defer_lock);
           if (cfg.kube_combine) plk.lock();
+          // PodTopologySpread (ScheduleAnyway, hostname) over the nodes priorities ran on:
+          // raw = matching pods on the node x log(nodes + 2) + maxSkew - 1, then normalised
+          // to 100 x (max + min - raw) / max (100 everywhere when max is 0), x weight
+          const bool spread = cfg.kube_combine && p.owner >= 0 && cfg.spread_weight > 0;
+          if (spread) {
+            spread_raw.resize(n_nodes);
+            const double w = std::log(static_cast<double>(psent->size()) + 2.0);
+            spread_min = INT64_MAX;
+            spread_max = 0;
+            for (int node : *psent) {
+              auto it = owner_cnt.find(owner_key(p.owner, node));
+              const int64_t cnt = it == owner_cnt.end() ? 0 : it->second;
+              const int64_t raw = static_cast<int64_t>(static_cast<double>(cnt) * w + (cfg.spread_max_skew - 1));
+              spread_raw[node] = raw;
+              spread_min = std::min(spread_min, raw);
+              spread_max = std::max(spread_max, raw);
+            }
+          }
           size_t cursor = 0;
           for (int32_t c = doc.at(doc.root()).first; c >= 0; c = doc.at(c).next) {
             int32_t h = doc.get(c, "Host", true), s = doc.get(c, "Score", true);
@@ -611,6 +667,10 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* 
               score = std::strtoll(std::string(st).c_str(), nullptr, 10);
             if (cfg.kube_combine)
               score = score * cfg.extender_weight * 10 + plugin_score(static_cast<size_t>(node), p);
+            if (spread) {
+              const int64_t s = spread_raw[node];
+              score += cfg.spread_weight * (spread_max == 0 ? 100 : 100 * (spread_max + spread_min - s) / spread_max);
+            }
             if (score > best) {
               best = score;
               ties.clear();
@@ -635,6 +695,7 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* 
     requested[host] += p.need;
     req_cpu[host] += p.cpu_m;
     req_mem[host] += p.mem;
+    if (p.owner >= 0) ++owner_cnt[owner_key(p.owner, host)];
     jobs.push_back({i, host});
     wake();
   }

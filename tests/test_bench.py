@@ -30,13 +30,21 @@ def _last_json(out: str) -> dict:
 
 def test_bench_single_rank_cpu():
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--no-gpu", "--steps", "2", "--warmup", "1",
-                        "--pods", "200", "--nodes", "8"], capture_output=True, text=True, timeout=300)
+                        "--pods", "200", "--nodes", "8", "--steady-variant-steps", "2", "--nodes-variant", "120",
+                        "--nodes-variant-steps", "1"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
     assert KEYS <= set(d)
     assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["higher_is_better"] is True
     assert d["scheduled"] == 400 and d["failed"] == 0 and d["value"] > 0
     assert d["p50_bind_ms"] is not None and 0 <= d["frag_pct"] <= 100
+    # steady-state churn pass: live frag next to the reference algorithm on the same stream
+    assert d["value_steady"] > 0 and d["failed_steady"] == 0
+    assert d["frag_pct_steady"] is not None and d["frag_pct_steady_reference_model"] is not None
+    # 120 nodes behind kube-scheduler's sampling: 100 feasible nodes reach the extender
+    assert d["value_nodes120"] > 0 and d["failed_nodes120"] == 0 and d["pods_per_burst_nodes120"] == 3000
+    assert d["nodes_sent_per_filter_nodes120"] == 100.0
+    assert d["frag_pct_nodes120_reference_model"] is not None
 
 
 @pytest.mark.parametrize("ranks", [2, 4])
@@ -45,13 +53,15 @@ def test_bench_multi_rank_gloo(ranks):
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
                         "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
                         "--gpus", str(ranks), "--no-gpu", "--steps", "2", "--warmup", "1", "--pods", "200",
-                        "--nodes", "8", "--rtt-variant-steps", "1"],
+                        "--nodes", "8", "--rtt-variant-steps", "1", "--steady-variant-steps", "2",
+                        "--nodes-variant", "0"],
                        capture_output=True, text=True, timeout=400, env=env, cwd="/tmp")
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
     assert d["n_gpus"] == ranks and d["scheduled"] == 400 and d["failed"] == 0
     assert f"{ranks} extender worker" in d["config"]["parallelism"]
     assert d["value_rtt2ms"] and d["p50_bind_ms"] is not None
+    assert d["value_steady"] > 0 and d["failed_steady"] == 0
 
 
 def test_link_weights_fall_back_to_the_reader_and_a_matrix_sets_the_mesh():

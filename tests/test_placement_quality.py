@@ -136,3 +136,38 @@ def test_learned_streaming_owner_stops_streamers_stacking():
     assert none >= 6
     assert learn == declared == 0
     assert _stacked_streamers("none", N.Options(N.Policy.BINPACK, compat=True)) == none   # the reference's
+
+
+def test_steady_state_churn_native_frag_at_most_the_reference_models():
+    """VERDICT r2 item 4 on a reduced stream: the cluster is filled once, then every step deletes
+    30 % of the live pods and creates as many (nanogpu.sim.workload.steady), behind the
+    kube-scheduler model. Native binpack's fragmentation stays at or below the reference
+    algorithm's (compat mode) on the same stream."""
+    from nanogpu.sim import fragsim
+
+    kw = dict(steps=10, nodes=16, initial=250, kube=True)
+    nat, ref = fragsim.steady_state(False, **kw), fragsim.steady_state(True, **kw)
+    assert nat["unschedulable"] == 0 and ref["unschedulable"] == 0
+    assert nat["frag_pct"] <= ref["frag_pct"], (nat, ref)
+    assert nat["frag_hbm_pct"] <= ref["frag_hbm_pct"], (nat, ref)
+
+
+def test_kube_scheduler_model_samples_nodes_and_spreads_owned_pods():
+    """numFeasibleNodesToFind (all nodes below 100; 42 % of 1,000; at least 100) with a rotating
+    start, and PodTopologySpread's normalised hostname score (fewer of the owner's pods on a
+    node scores higher)."""
+    from nanogpu import _native as NN
+    from nanogpu.sim.kubescore import KubeScoring, num_feasible_nodes_to_find, spread_scores
+
+    for n, want in ((64, 64), (99, 99), (100, 100), (200, 100), (1000, 420), (5000, 500), (10000, 500)):
+        assert num_feasible_nodes_to_find(n) == want == NN.num_feasible_nodes_to_find(n)
+    assert num_feasible_nodes_to_find(1000, 100) == 1000 and num_feasible_nodes_to_find(1000, 20) == 200
+    k = KubeScoring()
+    first = k.feasible(1000, lambda i: True)
+    second = k.feasible(1000, lambda i: True)
+    assert len(first) == len(second) == 420 and first[0] == 0 and second[0] == 420
+    odd = k.feasible(1000, lambda i: i % 2 == 1)         # processed nodes include the failures
+    assert len(odd) == 420 and odd[0] == 841 and k.next_start == (840 + 840) % 1000
+    assert spread_scores([0, 0, 0]) == [100, 100, 100]
+    s = spread_scores([3, 0, 1])
+    assert s[1] == max(s) and s[0] == min(s)
