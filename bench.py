@@ -89,6 +89,12 @@ def parse_args():
     ap.add_argument("--nodes-variant-pods", type=int, default=0,
                     help="pods per burst of the --nodes-variant pass (0: --pods scaled to the same occupancy)")
     ap.add_argument("--nodes-variant-steps", type=int, default=2)
+    ap.add_argument("--one-scheduler", action="store_true",
+                    help="with N ranks: ONE kube-scheduler stand-in (rank 0's) drives every pod, its cycle on "
+                         "rank 0's extender worker, its binds spread over all N workers (a cluster has one "
+                         "active kube-scheduler). Default: N independent stand-ins, one per rank")
+    ap.add_argument("--one-scheduler-variant-steps", type=int, default=5,
+                    help="with N > 1 ranks, after the timed steps, a --one-scheduler pass (0: none)")
     ap.add_argument("--apiserver-threads", type=int, default=0,
                     help="shared API server IO threads (0: one per rank, 4 to 16)")
     ap.add_argument("--bind-writer-threads", type=int, default=0,
@@ -577,7 +583,10 @@ def driver_main(conn) -> None:
                 st["specs"][step] = specs
                 work[step] = NativeSchedulerDriver.prepare_native([steady_pod(s, cfg["rank"]) for s in specs])
         for step in ([] if cfg.get("steady") else cfg["steps"]):
-            pods = burst(cfg["rank"], cfg["world"], cfg["pods"], step, 7)
+            if cfg.get("bind_ports"):   # the one scheduler of the job: every rank's pods
+                pods = [p for r in range(cfg["world"]) for p in burst(r, cfg["world"], cfg["pods"], step, 7)]
+            else:
+                pods = burst(cfg["rank"], cfg["world"], cfg["pods"], step, 7)
             work[step] = NativeSchedulerDriver.prepare_native(pods) if native else pods
         cfg["kube_obj"] = KubeScoring() if cfg.get("kube") else None
         session = None
@@ -601,7 +610,8 @@ def driver_main(conn) -> None:
             step = msg[1]
             # native: connections of the epoll binder (a bind leaves as soon as its host is
             # chosen, as kube-scheduler's per-pod bind goroutines); Python: pool threads
-            kw = ({"session": session, "bind_threads": 256, "kube": cfg["kube_obj"]} if native
+            kw = ({"session": session, "bind_threads": 256, "kube": cfg["kube_obj"],
+                   "bind_ports": cfg.get("bind_ports")} if native
                   else {"bind_threads": min(32, cfg["inflight"])})
             t0 = time.perf_counter()
             drv = cls("127.0.0.1", cfg["port"], cfg["names"], cfg["caps"], seed=step * 1009 + cfg["rank"], **kw)
@@ -707,8 +717,15 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     all_steps = [10_000 + w for w in range(args.warmup)] + list(range(args.steps))
     bursts = {} if steady else {s: burst(d.rank, d.world, args.pods, s, 7) for s in all_steps}
 
-    if conn is not None:
+    # --one-scheduler: ONE kube-scheduler stand-in for the job (rank 0's) drives every pod; its
+    # scheduling cycle stays on rank 0's worker, its binds spread over every rank's worker (the
+    # connections a Service spreads over an extender's workers)
+    one = bool(getattr(args, "one_scheduler", False)) and d.world > 1 and not steady
+    ports = d.gather_obj(rt.bound_port) if one else None
+    drives = conn is not None and (not one or d.rank == 0)
+    if conn is not None and drives:
         conn.send({"port": rt.bound_port, "names": names, "caps": caps, "rank": d.rank, "world": d.world,
+                   "bind_ports": ports,
                    "pods": args.pods, "inflight": args.inflight_binds, "driver": args.driver,
                    "kube": not args.no_kube_combine,
                    "steady": {"warmup": args.warmup, "steps": args.steps, "pods": args.pods} if steady else None,
@@ -783,8 +800,13 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                 await barrier()                     # every rank's pods exist
                 srv_ms.setdefault(step, {})["barrier_create_ms"] = 1e3 * (time.perf_counter() - tb)
             t_send = time.perf_counter()
-            conn.send(("step", step))
-            summary = await arecv(conn)
+            if drives:
+                conn.send(("step", step))
+                summary = await arecv(conn)
+            else:            # one scheduler: rank 0's stand-in schedules this rank's pods too
+                from nanogpu.sim.driver import DriverStats
+
+                summary = DriverStats().summary()
             # the stand-in's span is first filter -> last bind; this adds its per-step set-up,
             # summary and the pipe
             srv_ms.setdefault(step, {})["schedule_wall_ms"] = 1e3 * (time.perf_counter() - t_send)
@@ -1004,7 +1026,7 @@ def main() -> int:
     d = Dist(args.gpus)
     d.init(use_gpu=not args.no_gpu)
     topo, gpu_info = node_template(d, args)
-    variant = inproc_v = steady_v = nodes_v = None
+    variant = inproc_v = steady_v = nodes_v = one_v = None
     try:
         res = run_pass(d, args, topo, conn, "main", api_proc)
         shared_api = not args.inproc_api and not args.inproc_driver
@@ -1017,6 +1039,14 @@ def main() -> int:
                 steady_v = (s_args, steady_v[1], summarize(d, s_args, steady_v[1]))
             except Exception as e:
                 steady_v = {"error": f"{type(e).__name__}: {e}"}
+        if d.world > 1 and args.one_scheduler_variant_steps > 0 and not args.one_scheduler and not args.steady:
+            o_args = argparse.Namespace(**{**vars(args), "one_scheduler": True,
+                                           "steps": args.one_scheduler_variant_steps, "warmup": 1,
+                                           "profile_out": "", "stall_trace": "", "api_rtt_ms": 0.0})
+            try:
+                one_v = summarize(d, o_args, run_pass(d, o_args, topo, conn, "one", api_proc))
+            except Exception as e:
+                one_v = {"error": f"{type(e).__name__}: {e}"}
         if args.nodes_variant > 0 and args.nodes_variant != args.nodes and not args.steady and shared_api:
             # a large cluster behind kube-scheduler's node sampling: the extender sees only the
             # share of feasible nodes numFeasibleNodesToFind lets through, from a rotating start
@@ -1066,6 +1096,12 @@ def main() -> int:
             "metric": METRIC, "value": out["value"], "unit": "pods/s", "n_gpus": d.world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": out["ms_per_step"],
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "n/a",
+            # who drives the extender: a cluster runs ONE active kube-scheduler; with N ranks the
+            # headline runs one stand-in per rank unless --one-scheduler (value_one_scheduler is
+            # the one-scheduler figure of an N-rank job)
+            "value_mode": ("one kube-scheduler stand-in" if d.world == 1 or args.one_scheduler else
+                           f"{d.world} independent kube-scheduler stand-ins, one per extender worker, "
+                           f"each scheduling 1/{d.world} of the burst"),
             "data": "synthetic (pod bursts; simulated nodes cloned from the discovered MI355X)",
             "config": {"model": f"nano-gpu-scheduler extender ({args.policy}{', compat' if args.compat else ''})",
                        "global_batch": args.pods, "seq_len": None,
@@ -1137,6 +1173,18 @@ def main() -> int:
                 line[f"p50_bind_ms_{tag}"] = variant["p50_bind_ms"]
                 line[f"p99_bind_ms_{tag}"] = variant["p99_bind_ms"]
                 line[f"steps_{tag}"] = args.rtt_variant_steps
+        if one_v is not None:
+            if "error" in one_v:
+                line["value_one_scheduler"] = None
+                line["error_one_scheduler"] = one_v["error"]
+            else:
+                line["value_one_scheduler"] = one_v["value"]
+                line["p50_bind_ms_one_scheduler"] = one_v["p50_bind_ms"]
+                line["steps_one_scheduler"] = args.one_scheduler_variant_steps
+                line["one_scheduler_config"] = (f"one kube-scheduler stand-in: cycle on rank 0's worker, binds "
+                                                f"over all {d.world} workers")
+        elif d.world == 1 or args.one_scheduler:
+            line["value_one_scheduler"] = out["value"]      # the headline is already one scheduler
         line.update(steady_keys(args, topo, steady_v))
         line.update(nodes_variant_keys(args, topo, nodes_v))
         if inproc_v is not None:

@@ -612,8 +612,9 @@ class NativeSchedulerDriver:
 
     def __init__(self, host: str, port: int, node_names: list[str], node_capacity: dict[str, int] | None = None,
                  bind_threads: int = 256, seed: int = 0, max_attempts: int = 8, backoff_s: float = 0.001,
-                 session=None, kube: KubeScoring | None = None):
+                 session=None, kube: KubeScoring | None = None, bind_ports: list[int] | None = None):
         self.host, self.port = host, port
+        self.bind_ports = list(bind_ports or [])   # several extender workers behind one Service
         self.kube = kube     # combining in C++ (same model as nanogpu/sim/kubescore.py)
         self.session = session      # core().SchedulerSession(): keep-alive connections across runs
         self.nodes = list(node_names)
@@ -675,7 +676,7 @@ class NativeSchedulerDriver:
                                    sample_nodes=int(k.sample_nodes) if k else 1,
                                    percentage_of_nodes_to_score=k.percentage_of_nodes_to_score if k else 0,
                                    spread_weight=k.spread_weight if k else 0,
-                                   live=live or [])
+                                   live=live or [], bind_ports=self.bind_ports)
         self.stats.nodes_sent_filter = r["nodes_sent_filter"]
         self.stats.cycles = r["cycles"]
         st = self.stats

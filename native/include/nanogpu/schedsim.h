@@ -71,6 +71,10 @@ struct SimConfig {
   int spread_weight = 2;
   int spread_max_skew = 3;
   std::vector<SimLive> live;   // pods bound before this run (resource fit, spread counts)
+  // extender workers behind one Service: the scheduling cycle's keep-alive connection stays on
+  // `port`; bind connection k goes to bind_ports[k % size] (kube-proxy spreads connections).
+  // Empty: every bind to `port`.
+  std::vector<int> bind_ports;
 };
 
 // kube-scheduler's numFeasibleNodesToFind (v1.18+).

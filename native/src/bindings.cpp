@@ -951,7 +951,8 @@ PYBIND11_MODULE(_native, m) {
          const std::vector<std::string>& nodes, const std::vector<int64_t>& capacity, int bind_threads, uint64_t seed,
          int max_attempts, double backoff_s, std::shared_ptr<sim::Session> session, int kube_combine,
          int extender_weight, int sample_nodes, int percentage_of_nodes_to_score, int spread_weight,
-         const std::vector<std::tuple<int32_t, int64_t, int64_t, int64_t, int32_t>>& live) {
+         const std::vector<std::tuple<int32_t, int64_t, int64_t, int64_t, int32_t>>& live,
+         const std::vector<int>& bind_ports) {
         sim::SimConfig cfg;
         cfg.host = host;
         cfg.port = port;
@@ -966,6 +967,7 @@ PYBIND11_MODULE(_native, m) {
         cfg.sample_nodes = sample_nodes;
         cfg.percentage_of_nodes_to_score = percentage_of_nodes_to_score;
         cfg.spread_weight = spread_weight;
+        cfg.bind_ports = bind_ports;
         for (const auto& [node, need, cpu, mem, owner] : live) cfg.live.push_back({node, need, cpu, mem, owner});
         if (!capacity.empty() && capacity.size() != nodes.size())
           throw py::value_error("capacity must be empty or one entry per node");
@@ -1004,6 +1006,7 @@ PYBIND11_MODULE(_native, m) {
       py::arg("session") = nullptr, py::arg("kube_combine") = 0, py::arg("extender_weight") = 1,
       py::arg("sample_nodes") = 1, py::arg("percentage_of_nodes_to_score") = 0, py::arg("spread_weight") = 2,
       py::arg("live") = std::vector<std::tuple<int32_t, int64_t, int64_t, int64_t, int32_t>>{},
+      py::arg("bind_ports") = std::vector<int>{},
       "kube-scheduler stand-in (native/src/schedsim.cpp): schedule `pods` through the extender at host:port");
 
   // ------------------------------------------------------------------ native API server

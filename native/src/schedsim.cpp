@@ -447,7 +447,8 @@ SimResult drive(const SimConfig& cfg, const std::vector<SimPod>& pods, Session* 
         BindJob job = pending.front();
         pending.pop_front();
         if (c.fd < 0) {
-          c.fd = open_socket(cfg.host, cfg.port, true);
+          c.fd = open_socket(cfg.host, cfg.bind_ports.empty() ? cfg.port : cfg.bind_ports[k % cfg.bind_ports.size()],
+                             true);
           if (c.fd < 0) {
             c.job = job;
             c.busy = true;

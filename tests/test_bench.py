@@ -44,6 +44,7 @@ def test_bench_single_rank_cpu():
     # 120 nodes behind kube-scheduler's sampling: 100 feasible nodes reach the extender
     assert d["value_nodes120"] > 0 and d["failed_nodes120"] == 0 and d["pods_per_burst_nodes120"] == 3000
     assert d["nodes_sent_per_filter_nodes120"] == 100.0
+    assert d["value_mode"] == "one kube-scheduler stand-in" and d["value_one_scheduler"] == d["value"]
     assert d["frag_pct_nodes120_reference_model"] is not None
 
 
@@ -54,7 +55,7 @@ def test_bench_multi_rank_gloo(ranks):
                         "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
                         "--gpus", str(ranks), "--no-gpu", "--steps", "2", "--warmup", "1", "--pods", "200",
                         "--nodes", "8", "--rtt-variant-steps", "1", "--steady-variant-steps", "2",
-                        "--nodes-variant", "0"],
+                        "--nodes-variant", "0", "--one-scheduler-variant-steps", "1"],
                        capture_output=True, text=True, timeout=400, env=env, cwd="/tmp")
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
@@ -62,6 +63,9 @@ def test_bench_multi_rank_gloo(ranks):
     assert f"{ranks} extender worker" in d["config"]["parallelism"]
     assert d["value_rtt2ms"] and d["p50_bind_ms"] is not None
     assert d["value_steady"] > 0 and d["failed_steady"] == 0
+    # the headline's N stand-ins are labelled as such; one scheduler over N workers alongside
+    assert d["value_mode"].startswith(f"{ranks} independent kube-scheduler stand-ins")
+    assert d["value_one_scheduler"] > 0 and d["steps_one_scheduler"] == 1
 
 
 def test_link_weights_fall_back_to_the_reader_and_a_matrix_sets_the_mesh():
