@@ -244,6 +244,43 @@ class StallSampler:
         Path(path).write_text(json.dumps(out, indent=1))
 
 
+def thread_cpu() -> dict[str, float]:
+    """CPU seconds of this process's threads by group: the Python main thread (event loop:
+    informer, controller, Python routes), the native front door's epoll workers (ngpu-fe*,
+    busy polling included), the bind writers (ngpu-wr*), and the rest (executor threads, the
+    interpreter's helpers). From /proc/self/task/*/schedstat (ns on CPU), else stat ticks."""
+    pid = os.getpid()
+    hz = os.sysconf("SC_CLK_TCK")
+    out: dict[str, float] = {}
+    try:
+        tids = os.listdir(f"/proc/{pid}/task")
+    except OSError:
+        return out
+    for tid in tids:
+        base = f"/proc/{pid}/task/{tid}"
+        try:
+            with open(base + "/comm") as f:
+                comm = f.read().strip()
+            try:
+                with open(base + "/schedstat") as f:
+                    cpu = int(f.read().split()[0]) / 1e9
+            except (OSError, ValueError, IndexError):
+                with open(base + "/stat") as f:
+                    st = f.read()
+                fields = st[st.rindex(")") + 2:].split()
+                cpu = (int(fields[11]) + int(fields[12])) / hz
+        except (OSError, ValueError):
+            continue
+        if tid == str(pid):
+            group = "main"
+        elif comm.startswith("ngpu-"):
+            group = comm.rstrip("0123456789")
+        else:
+            group = "other"
+        out[group] = out.get(group, 0.0) + cpu
+    return out
+
+
 # --------------------------------------------------------------------------- node template
 def measured_links(d: Dist, host: dict, gpus_per_node: int) -> tuple[float, list | None, str]:
     """Per-link xGMI weights for the node model (per direction, GB/s): the peer-pull probe
@@ -920,6 +957,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     sampler = StallSampler() if args.stall_trace and d.rank == 0 else None
     nom0 = rt.state.ledger.nomination_counts()
     cpu0, loop_cpu0 = time.process_time(), time.thread_time()
+    threads0 = thread_cpu()
     t0 = time.perf_counter()
     if sampler is not None:
         sampler.on.set()
@@ -950,6 +988,9 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                                         if cycles else None)
     n_sched = max(1, sum(st["scheduled"] for st in results["steps"]))
     results["cpu_us_per_pod"] = 1e6 * (time.process_time() - cpu0) / n_sched
+    threads1 = thread_cpu()
+    results["cpu_us_per_pod_by_thread"] = {g: round(1e6 * (threads1[g] - threads0.get(g, 0.0)) / n_sched, 1)
+                                           for g in sorted(threads1)}
     results["loop_cpu_us_per_pod"] = 1e6 * (time.thread_time() - loop_cpu0) / n_sched
     # the Python part of each bind (API writes + commit): a sub-phase of the wall time
     binds = sorted(s["dur_ms"] for s in rt.tracer.dump(10 ** 9, "bind") if s["ok"])
@@ -1161,6 +1202,9 @@ def main() -> int:
             "extender_cpu_us_per_pod_rank0": round(res.get("cpu_us_per_pod", 0.0), 1),
             # of which the Python event-loop thread (binds' API writes, informer, controller)
             "extender_loop_cpu_us_per_pod_rank0": round(res.get("loop_cpu_us_per_pod", 0.0), 1),
+            # the same CPU by thread group: main (event loop), ngpu-fe (native front door epoll
+            # workers, busy polling included), ngpu-wr (native bind writers), other
+            "extender_cpu_us_per_pod_by_thread_rank0": res.get("cpu_us_per_pod_by_thread"),
         }
         line.update(reference_model_frag(args, topo))
         if variant is not None:

@@ -883,6 +883,7 @@ PYBIND11_MODULE(_native, m) {
         d["connections"] = f.connections.load();
         d["requests"] = f.requests.load();
         d["loop_max_s"] = static_cast<double>(f.loop_max_ns.load()) * 1e-9;
+        d["spin_hits"] = f.spin_hits.load();
         py::list ph;
         for (const auto& x : f.phase_max_ns) ph.append(static_cast<double>(x.load()) * 1e-9);
         d["phase_max_s"] = ph;

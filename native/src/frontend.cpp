@@ -360,7 +360,12 @@ Frontend::Frontend(std::shared_ptr<Ledger> ledger, const std::string& host, int 
     epoll_ctl(w->ep, EPOLL_CTL_ADD, w->efd, &ev);
     workers_.push_back(std::move(w));
   }
-  for (auto& w : workers_) w->th = std::thread([this, p = w.get()] { run(p); });
+  for (size_t i = 0; i < workers_.size(); ++i)
+    workers_[i]->th = std::thread([this, p = workers_[i].get(), i] {
+      // named for per-thread CPU accounting (bench.py thread_cpu, /proc/<pid>/task/<tid>/comm)
+      pthread_setname_np(pthread_self(), ("ngpu-fe" + std::to_string(i)).c_str());
+      run(p);
+    });
 }
 
 Frontend::~Frontend() { stop(); }
@@ -526,12 +531,26 @@ void Frontend::run(Worker* w) {
   epoll_event evs[128];
   std::vector<uint64_t> later;   // connections whose next request is a bind
   uint64_t last_event = 0;
+  // Adaptive busy polling: spin after an event only while spinning pays. Every event's gap to
+  // the previous one is a hit when it is shorter than the spin window (a spin would have
+  // caught it without a wake-up) and a miss otherwise; a worker spins while at least half of
+  // its last 16 gaps were hits. The worker that carries kube-scheduler's scheduling-cycle
+  // connection (filter, then priorities, then the next pod's filter a few microseconds
+  // later) stays hot during a burst; one that only sees the asynchronous binds, tens of
+  // microseconds apart, blocks in epoll_wait instead of burning a core.
+  uint32_t gaps = 0xffffu;   // 1 bits: hits among the last 16 gaps (start hot)
   while (!stop_.load(std::memory_order_acquire)) {
     const int64_t spin = busy_poll_ns_.load(std::memory_order_relaxed);
-    const bool polling = spin > 0 && now_ns() - last_event < static_cast<uint64_t>(spin);
+    const bool hot = __builtin_popcount(gaps & 0xffffu) >= 8;
+    const bool polling = spin > 0 && hot && now_ns() - last_event < static_cast<uint64_t>(spin);
     const int n = epoll_wait(w->ep, evs, 128, polling ? 0 : 200);
     const uint64_t t_batch = n > 0 ? now_ns() : 0;
-    if (n > 0) last_event = t_batch;
+    if (n > 0) {
+      if (spin > 0 && last_event)
+        gaps = (gaps << 1) | (t_batch - last_event < static_cast<uint64_t>(spin) ? 1u : 0u);
+      last_event = t_batch;
+      if (polling) spin_hits.fetch_add(1, std::memory_order_relaxed);   // caught without a wake-up
+    }
     struct BatchTimer {
       Frontend* f;
       uint64_t t0;

@@ -335,7 +335,11 @@ KubeWriter::KubeWriter(KubeTarget target, std::shared_ptr<Ledger> ledger, Respon
   }
   token_checked_ = mono_s();
   if (threads < 1) threads = 1;
-  for (int i = 0; i < threads; ++i) threads_.emplace_back([this] { run(); });
+  for (int i = 0; i < threads; ++i)
+    threads_.emplace_back([this, i] {
+      pthread_setname_np(pthread_self(), ("ngpu-wr" + std::to_string(i)).c_str());
+      run();
+    });
 }
 
 KubeWriter::~KubeWriter() {
