@@ -144,6 +144,14 @@ class PolicySpec:
     metrics_scope: str = "node"
     # HBM activity at or above which a device is marked streaming (types.HBM_HOT_THRESHOLD)
     hbm_hot_threshold: float | None = None
+    # (share %, mem_busy %) of a lone streaming tenant on this fleet's GPUs (types.HBM_STREAMING_CURVE)
+    hbm_streaming_curve: tuple[tuple[float, float], ...] | None = None
+
+    def learn_curve(self) -> list[tuple[float, float]]:
+        """The learner's per-share threshold (percent): HBM_LEARN_FRACTION of the streaming
+        curve, never above the device threshold."""
+        cap = 100.0 * (self.hbm_hot_threshold or T.HBM_HOT_THRESHOLD)
+        return [(s, min(cap, T.HBM_LEARN_FRACTION * b)) for s, b in (self.hbm_streaming_curve or T.HBM_STREAMING_CURVE)]
 
     def period_of(self, name: str) -> float:
         for p in self.sync_period:
@@ -191,6 +199,11 @@ def parse_policy(text: str) -> PolicySpec:
     hot = spec.get("hbmHotThreshold")
     if hot is not None and not 0.0 < float(hot) <= 1.0:
         raise ValueError(f"hbmHotThreshold {hot!r} outside (0, 1]")
+    curve = spec.get("hbmStreamingCurve")
+    if curve is not None:
+        curve = tuple(sorted((float(s), float(b)) for s, b in curve))
+        if not curve or any(not (0 < s <= 100 and 0 <= b <= 100) for s, b in curve):
+            raise ValueError(f"hbmStreamingCurve {spec.get('hbmStreamingCurve')!r}: [[share %, busy %], ...]")
     scope = spec.get("metricsScope", "node")
     if scope not in ("node", "cluster"):
         raise ValueError(f"unknown metricsScope {scope!r} (node or cluster)")
@@ -198,7 +211,7 @@ def parse_policy(text: str) -> PolicySpec:
         sync_period=tuple(periods), priority=prio, policy=pol,
         compat=sch.get("compat"), topology_weight=sch.get("topologyWeight"),
         score_normalize=sch.get("scoreNormalize"), metrics=tuple(metrics), metrics_scope=scope,
-        hbm_hot_threshold=None if hot is None else float(hot))
+        hbm_hot_threshold=None if hot is None else float(hot), hbm_streaming_curve=curve)
 
 
 def load_policy(path: str) -> PolicySpec:

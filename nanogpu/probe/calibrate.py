@@ -126,3 +126,98 @@ def ring_busbw(dist, device, nbytes: int = 256 << 20, iters: int = 5) -> float:
     t = torch.tensor([dt], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return 2.0 * (n - 1) / n * nbytes / float(t.item()) / 1e9
+
+
+# --------------------------------------------------------------------------- HBM activity
+_SAMPLER = r"""
+import json, sys, time
+f = open(sys.argv[1]); end = time.monotonic() + float(sys.argv[2]); out = []
+while time.monotonic() < end:
+    f.seek(0); out.append((time.monotonic(), int(f.read() or 0))); time.sleep(0.01)
+print(json.dumps(out))
+"""
+
+
+def mem_busy_file(host: dict | None = None):
+    """amdgpu's mem_busy_percent of the GPU this process sees first (None: not exposed)."""
+    from pathlib import Path
+
+    host = host if host is not None else json.loads(core().discover_topology("", True))
+    for g in host.get("gpus") or []:
+        p = Path(f"/sys/class/drm/renderD{int(g['render_minor'])}/device/mem_busy_percent")
+        if p.exists():
+            return p
+    return next(iter(sorted(Path("/sys/class/drm").glob("renderD*/device/mem_busy_percent"))), None)
+
+
+def cu_share_mask(share_pct: float, cus: int = 256, xcds: int = 8) -> list[int]:
+    """Mask words of the node agent's grant for a `share_pct` % tenant (nanogpu.agent.cumask)."""
+    from ..agent import cumask
+
+    if share_pct >= 100:
+        return cumask.mask_words(list(range(cus)), cus)
+    d = cumask.DeviceCUs(cus, xcds)
+    return cumask.mask_words(d.grant("t", int(round(share_pct))), cus)
+
+
+def tenant_call(P, kind: str, mask: list[int], device: int = 0, seconds: float = 1.0):
+    """A callable that runs about `seconds` of one CU-masked tenant: "stream" (HBM copy, returns
+    GB/s) or "mfma" (bf16 burn, returns TFLOP/s). Each probe launch is bounded, so long runs
+    call it back to back."""
+    n_cus = sum(bin(w).count("1") for w in mask)
+    if kind == "stream":
+        t = time.perf_counter()
+        P.hbm_colocated(device, [mask], 1 << 30, 4)
+        iters = max(4, min(1000, int(seconds / max((time.perf_counter() - t) / 4, 1e-5))))
+        return lambda: P.hbm_colocated(device, [mask], 1 << 30, iters)[0]
+    blocks = max(8, n_cus * 8)
+    t = time.perf_counter()
+    P.mfma_throughput(device, mask, blocks, 4096)
+    iters = max(4096, min(1 << 22, int(4096 * seconds / max(time.perf_counter() - t, 1e-6))))
+    return lambda: P.mfma_throughput(device, mask, blocks, iters)["tflops"]
+
+
+def mem_busy_while(busy_file, runs: list, seconds: float = 8.0, ramp_s: float = 0.3) -> list[dict]:
+    """Runs each (label, callable) of `runs` back to back for `seconds` while a child process
+    samples `busy_file` every 10 ms (a probe call may hold the GIL). Per run: the mean of ALL
+    samples in its window (what avg_over_time over scrapes converges to), the max, the mean of
+    the non-zero samples, and means at scrape-like spacing (1 s, 5 s); plus the call's rate."""
+    import subprocess
+    import sys
+
+    total = len(runs) * (seconds + 2.0) + 5.0
+    sampler = subprocess.Popen([sys.executable, "-c", _SAMPLER, str(busy_file), str(total)],
+                               stdout=subprocess.PIPE, text=True)
+    time.sleep(0.3)
+    windows = []
+    try:
+        for label, call in runs:
+            got = []
+            t0 = time.monotonic()
+            while time.monotonic() - t0 < seconds:
+                got.append(call())
+            windows.append((label, t0 + ramp_s, time.monotonic(), sum(got) / len(got), len(got)))
+            time.sleep(0.5)
+    finally:
+        out, _ = sampler.communicate(timeout=total + 30)
+    samples = json.loads(out)
+    res = []
+    for label, t0, t1, rate, calls in windows:
+        win = [(t, v) for t, v in samples if t0 <= t <= t1]
+        vals = [v for _, v in win]
+
+        def spaced(step: float):
+            picked, nxt = [], t0 + step / 2
+            for t, v in win:
+                if t >= nxt:
+                    picked.append(v)
+                    nxt += step
+            return round(sum(picked) / len(picked), 1) if picked else None
+
+        nz = [v for v in vals if v]
+        res.append({"label": label, "seconds": round(t1 - t0, 2), "rate": round(rate, 1), "calls": calls,
+                    "n": len(vals), "mean_all": round(sum(vals) / len(vals), 1) if vals else None,
+                    "max": max(vals) if vals else None,
+                    "mean_nonzero": round(sum(nz) / len(nz), 1) if nz else 0.0,
+                    "mean_1s": spaced(1.0), "mean_5s": spaced(5.0)})
+    return res

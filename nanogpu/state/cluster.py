@@ -390,6 +390,11 @@ class ClusterState:
         e = self._nodes.get(node_name)
         return bool(e) and self.ledger.set_mem_hot(e.id, device, bool(hot)) == N.OK
 
+    def set_mem_busy(self, node_name: str, device: int, activity: float) -> bool:
+        """The averaged HBM activity (0..1) the streaming-owner learner reads (Device::mem_busy)."""
+        e = self._nodes.get(node_name)
+        return bool(e) and self.ledger.set_mem_busy(e.id, device, int(round(100 * activity))) == N.OK
+
     # ------------------------------------------------------------------ introspection
     def frag(self, min_request: int = 0) -> dict:
         return self.ledger.frag(min_request)
@@ -410,7 +415,8 @@ class ClusterState:
                           "Partition": d["part"],
                           "Healthy": d["healthy"],
                           # streaming tenants: declared (nano-gpu/memory-bound) and measured
-                          "MemoryBoundTenants": d["mem_bound"], "HBMHot": d["mem_hot"]}
+                          "MemoryBoundTenants": d["mem_bound"], "HBMHot": d["mem_hot"],
+                          "HBMActivityPct": d["mem_busy"]}
                          for d in snap["devices"]],
                 "PlanCache": self._plan_cache(e.id),
                 "Generation": snap["generation"],

@@ -115,7 +115,8 @@ class LoadPoller:
         return (time.monotonic() if now is None else now) - (q.window_s() + period)
 
     def _learn_pass(self, now: float | None = None) -> tuple[int, int]:
-        return self.state.ledger.learn_stream_owners(True, self.attribution_cutoff(now), self.forget_after)
+        return self.state.ledger.learn_stream_owners(True, self.attribution_cutoff(now), self.forget_after,
+                                                     self.spec.learn_curve())
 
     def learn_owners(self, counts: tuple[int, int] | None = None, now: float | None = None) -> tuple[int, int]:
         """Streaming owners from the last period's marks (Ledger::learn_stream_owners): a
@@ -241,8 +242,9 @@ class LoadPoller:
         for card in range(n_dev):
             self.state.set_load(name, card, self.store.device_usage(name, card, periods, now))
             # unpolled (or no longer polled) metric: the mark clears
-            self.state.set_mem_hot(name, card, self.store.hbm_hot(
-                name, card, hbm_active, self.hbm_threshold, now))
+            busy = self.store.hbm_activity(name, card, hbm_active, now)
+            self.state.set_mem_hot(name, card, busy >= self.hbm_threshold)
+            self.state.set_mem_busy(name, card, busy)
 
     def sweep_stale(self) -> None:
         """Re-derives loads so samples that aged out stop counting (called periodically)."""

@@ -54,6 +54,13 @@ class TelemetryStore:
             total += math.ceil(10 * v) / 10
         return total
 
+    def hbm_activity(self, node: str, card: int, active_s: float, now: float | None = None) -> float:
+        """Fresh, valid HBM-activity sample in [0, 1]; 0.0 when stale, missing or invalid."""
+        if active_s <= 0:
+            return 0.0
+        exists, v, err = self.get(node, T.GPU_HBM_ACTIVITY_METRIC, card, active_s, now)
+        return v if exists and err is None else 0.0
+
     def hbm_hot(self, node: str, card: int, active_s: float, threshold: float, now: float | None = None
                 ) -> bool:
         """Fresh, valid HBM-activity sample at or above `threshold` (types.GPU_HBM_ACTIVITY_METRIC)."""

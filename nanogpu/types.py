@@ -45,7 +45,18 @@ FLAG_MEM_BOUND = 1
 # streaming tenant (alloc.h Device::mem_hot), declared or not. It feeds only that mark, not the
 # reference's load sum (RemainLoad), so the reference's load semantics are unchanged.
 GPU_HBM_ACTIVITY_METRIC = "gpu_hbm_activity_avg"
-HBM_HOT_THRESHOLD = 0.5
+# Measured on the MI355X box (tools/hbm_share_calibration.py, profiles/gpu_calibration.md):
+# amdgpu's mem_busy_percent averaged over 8 s of one tenant alone on the GPU. A streaming HBM
+# copy reads 10.9 / 30.1 / 48.8 / 54.4 % holding 12.5 / 25 / 50 / 100 % of the CUs; a bf16 MFMA
+# burn reads 0 % at 25, 75 and 100 %. The device mark fires for a streamer of a quarter of the
+# GPU or more (0.25); a full-chip streamer's 54 % would barely clear the old 0.5.
+HBM_HOT_THRESHOLD = 0.25
+# (share %, mem_busy %) of a lone streaming tenant, from the same calibration: the learner's
+# threshold for a pod alone on a device is HBM_LEARN_FRACTION of the curve at that pod's share
+# (capped at the device threshold), so a lone 25 % streamer (30 %) is learned while a lone MFMA
+# tenant of any size (0 %) is not.
+HBM_STREAMING_CURVE = ((12.5, 10.9), (25.0, 30.1), (50.0, 48.8), (100.0, 54.4))
+HBM_LEARN_FRACTION = 0.5
 AMD_GPU_NODE_LABEL = ("amd.com/gpu.present", "true")   # default telemetry node selector
 
 MI355X_CUS = 256

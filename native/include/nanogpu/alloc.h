@@ -70,8 +70,10 @@ struct Device {
   // mib_free/mib_total and every debit updates all members. -1: the device's own HBM.
   int16_t pool;
   int16_t mem_bound;    // memory-bound share containers placed here (see kFlagMemBound)
-  int32_t mem_hot;      // measured: the device's HBM activity is above the policy threshold
+  int16_t mem_hot;      // measured: the device's HBM activity is above the policy threshold
                         // (telemetry, Ledger::set_mem_hot), whatever its tenants declared
+  int16_t mem_busy;     // the averaged HBM activity itself, percent (Ledger::set_mem_busy): the
+                        // streaming-owner learner compares it with a threshold per tenant share
   int64_t mib_share;    // HBM a whole-device grant of a pooled member takes (pool / members)
 };
 

@@ -252,6 +252,8 @@ class Ledger {
   int32_t set_health(int32_t id, int dev, bool healthy);
   // measured HBM activity above the policy threshold (Device::mem_hot)
   int32_t set_mem_hot(int32_t id, int dev, bool hot);
+  // the averaged HBM activity in percent (what the learner reads; placement does not)
+  int32_t set_mem_busy(int32_t id, int dev, int32_t percent);
 
   FragStats frag(int32_t min_request) const;
 
@@ -268,8 +270,15 @@ class Ledger {
   // tenant it replaced) count. Per owner: learned if any of its lone pods sits on a device
   // marked mem_hot; with `forget_cool`, forgotten once every lone pod of it was cool (and none
   // hot) in `forget_after` consecutive passes. Returns {owners learned, owners forgotten}.
+  //
+  // `hot_curve` (share percent -> activity percent, ascending shares) makes the decision share
+  // aware: a lone pod holding share s of its device counts as streaming when the device's
+  // mem_busy is at least the curve at s (linear in between, flat outside). A streaming tenant
+  // alone moves more of the device's bandwidth the more CUs it holds, so one fixed threshold
+  // either misses small streamers or flags big non-streamers. Empty: the device's mem_hot mark.
   std::pair<int32_t, int32_t> learn_stream_owners(bool forget_cool, double reserved_before = 1e300,
-                                                  int32_t forget_after = 1);
+                                                  int32_t forget_after = 1,
+                                                  const std::vector<std::pair<float, float>>& hot_curve = {});
   SizeSet learned_sizes() const;
   // The options a placement runs with: native binpack gets the request-size set (fixed |
   // learned | this demand's sizes) and its waste table; everything else is unchanged.

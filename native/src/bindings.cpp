@@ -69,6 +69,7 @@ Device to_device(const py::dict& d) {
   v.pool = get<int16_t>(d, "pool", -1);
   v.mib_share = get<int64_t>(d, "mib_share", 0);
   v.mem_hot = get<bool>(d, "mem_hot", false) ? 1 : 0;
+  v.mem_busy = get<int16_t>(d, "mem_busy", 0);
   if (v.pool >= 0 && v.mib_share <= 0) v.mib_share = v.mib_total;
   return v;
 }
@@ -91,6 +92,7 @@ py::dict from_device(const Device& v) {
   d["mib_share"] = v.mib_share;
   d["mem_bound"] = v.mem_bound;
   d["mem_hot"] = v.mem_hot != 0;
+  d["mem_busy"] = v.mem_busy;
   return d;
 }
 
@@ -714,6 +716,7 @@ PYBIND11_MODULE(_native, m) {
       .def("set_load", &Ledger::set_load)
       .def("set_health", &Ledger::set_health)
       .def("set_mem_hot", &Ledger::set_mem_hot)
+      .def("set_mem_busy", &Ledger::set_mem_busy, py::arg("node"), py::arg("dev"), py::arg("percent"))
       .def(
           "set_stream_owner",
           [](Ledger& l, const std::string& uid, bool streaming) { l.set_stream_owner(owner_hash(uid), streaming); },
@@ -729,15 +732,17 @@ PYBIND11_MODULE(_native, m) {
           py::arg("key"), py::arg("owner_uid"))
       .def(
           "learn_stream_owners",
-          [](Ledger& l, bool forget_cool, double reserved_before, int32_t forget_after) {
+          [](Ledger& l, bool forget_cool, double reserved_before, int32_t forget_after,
+             const std::vector<std::pair<float, float>>& hot_curve) {
             std::pair<int32_t, int32_t> r;
             {
               py::gil_scoped_release nogil;
-              r = l.learn_stream_owners(forget_cool, reserved_before, forget_after);
+              r = l.learn_stream_owners(forget_cool, reserved_before, forget_after, hot_curve);
             }
             return r;
           },
-          py::arg("forget_cool") = true, py::arg("reserved_before") = 1e300, py::arg("forget_after") = 1)
+          py::arg("forget_cool") = true, py::arg("reserved_before") = 1e300, py::arg("forget_after") = 1,
+          py::arg("hot_curve") = std::vector<std::pair<float, float>>{})
       .def_static("owner_hash", [](const std::string& uid) { return owner_hash(uid); })
       .def("frag", [](const Ledger& l, int32_t min_request) { return frag_dict(l.frag(min_request)); },
            py::arg("min_request") = 0)

@@ -364,6 +364,7 @@ int32_t Ledger::upsert_node(const std::string& name, const Device* devs, int n,
       s.devs[i].mib_free = s.devs[i].mib_total;
       s.devs[i].mem_bound = 0;
       s.devs[i].mem_hot = 0;
+      s.devs[i].mem_busy = 0;
     }
     s.in_use = 1;
     hdr_->n_nodes.store(count + 1, std::memory_order_release);
@@ -385,11 +386,13 @@ int32_t Ledger::upsert_node(const std::string& name, const Device* devs, int n,
         merged[i].remain_load = old.remain_load;
         merged[i].mem_bound = old.mem_bound;
         merged[i].mem_hot = old.mem_hot;
+        merged[i].mem_busy = old.mem_busy;
       } else {
         merged[i].pct_free = merged[i].pct_total;
         merged[i].mib_free = merged[i].mib_total;
         merged[i].mem_bound = 0;
         merged[i].mem_hot = 0;
+        merged[i].mem_busy = 0;
       }
     }
     // Devices that vanished while still in use stay (unhealthy) until their pods release.
@@ -924,13 +927,27 @@ int32_t Ledger::set_pod_owner(const std::string& key, uint64_t owner) {
   return kOk;
 }
 
+static float curve_at(const std::vector<std::pair<float, float>>& c, float x) {
+  if (x <= c.front().first) return c.front().second;
+  if (x >= c.back().first) return c.back().second;
+  for (size_t i = 1; i < c.size(); ++i)
+    if (x <= c[i].first) {
+      const auto& [x0, y0] = c[i - 1];
+      const auto& [x1, y1] = c[i];
+      return x1 > x0 ? y0 + (y1 - y0) * (x - x0) / (x1 - x0) : y1;
+    }
+  return c.back().second;
+}
+
 std::pair<int32_t, int32_t> Ledger::learn_stream_owners(bool forget_cool, double reserved_before,
-                                                        int32_t forget_after) {
-  // (node, device) -> tenant pods, and the owner / record time of the last one seen
+                                                        int32_t forget_after,
+                                                        const std::vector<std::pair<float, float>>& hot_curve) {
+  // (node, device) -> tenant pods, and the owner / record time / share of the last one seen
   struct Tenancy {
     int32_t pods = 0;
     uint64_t owner = 0;
     double t = 0;
+    int32_t share = 0;   // percent of the device the last pod holds there
   };
   std::unordered_map<uint64_t, Tenancy> dev;
   for (int s = 0; s < kPodShards; ++s) {
@@ -941,17 +958,32 @@ std::pair<int32_t, int32_t> Ledger::learn_stream_owners(bool forget_cool, double
       const PodSlot& p = t[i];
       if (p.state != kPodCommitted || p.node < 0) continue;
       int16_t seen[kMaxPlanIdx];
+      int32_t share[kMaxPlanIdx];
       int n_seen = 0;
+      Demand dm;
       Plan pl;
-      get_record(p, nullptr, &pl);
-      for (int k = 0; k < pl.off[pl.n] && k < kMaxPlanIdx; ++k) {
-        const int16_t x = pl.idx[k];
-        if (x < 0 || std::find(seen, seen + n_seen, x) != seen + n_seen) continue;
-        seen[n_seen++] = x;
-        Tenancy& te = dev[(static_cast<uint64_t>(p.node) << 16) | static_cast<uint16_t>(x)];
+      get_record(p, &dm, &pl);
+      for (int c = 0; c < pl.n && c < dm.n; ++c) {
+        // a share container takes its percent of one device; a whole-device one all of each
+        const int32_t s = std::min(dm.c[c].pct, kPercentPerDevice);
+        for (int k = pl.off[c]; k < pl.off[c + 1] && k < kMaxPlanIdx; ++k) {
+          const int16_t x = pl.idx[k];
+          if (x < 0) continue;
+          int16_t* at = std::find(seen, seen + n_seen, x);
+          if (at != seen + n_seen) {
+            share[at - seen] = std::min(kPercentPerDevice, share[at - seen] + s);
+            continue;
+          }
+          share[n_seen] = s;
+          seen[n_seen++] = x;
+        }
+      }
+      for (int k = 0; k < n_seen; ++k) {
+        Tenancy& te = dev[(static_cast<uint64_t>(p.node) << 16) | static_cast<uint16_t>(seen[k])];
         ++te.pods;
         te.owner = p.owner;
         te.t = p.t_reserved;
+        te.share = share[k];
       }
     }
   }
@@ -972,7 +1004,8 @@ std::pair<int32_t, int32_t> Ledger::learn_stream_owners(bool forget_cool, double
       lock_node(n);
       Unlock un{&n->mu};
       if (x >= n->n_devs) continue;
-      hot = n->devs[x].mem_hot != 0;
+      hot = hot_curve.empty() ? n->devs[x].mem_hot != 0
+                              : n->devs[x].mem_busy >= curve_at(hot_curve, static_cast<float>(te.share));
     }
     Verdict& v = owners[te.owner];
     (hot ? v.hot : v.cool) = true;
@@ -1102,6 +1135,16 @@ int32_t Ledger::set_load(int32_t id, int dev, float usage) {
   n->generation.fetch_add(1, std::memory_order_release);
   hdr_->epoch.fetch_add(1);
   return kOk;
+}
+
+int32_t Ledger::set_mem_busy(int32_t id, int dev, int32_t percent) {
+  NodeSlot* n = node(id);
+  if (!n) return kErrUnknownNode;
+  lock_node(n);
+  Unlock un{&n->mu};
+  if (dev < 0 || dev >= n->n_devs) return kErrBadPlan;
+  n->devs[dev].mem_busy = static_cast<int16_t>(std::clamp(percent, 0, 100));
+  return kOk;   // read by the learner only: no generation bump, cached plans stay valid
 }
 
 int32_t Ledger::set_mem_hot(int32_t id, int dev, bool hot) {

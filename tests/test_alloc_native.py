@@ -383,3 +383,29 @@ def test_overflow_records_hold_wide_pods_and_are_reused():
         assert L.release(k) == N.OK
     assert L.overflow_records_used == 0 and L.n_pods == 0
     assert all(d["pct_free"] == 100 for d in L.snapshot(nid)["devices"])
+
+
+def test_share_aware_learner_threshold_follows_the_streaming_curve():
+    """with a curve the learner compares a lone pod's device activity with
+    the curve at that pod's share. The default curve (types.HBM_STREAMING_CURVE, measured on
+    the box) halved: 12.5 % -> 5.5, 25 % -> 15, 75 % -> 25 (capped at the device threshold)."""
+    from nanogpu.config.policy import PolicySpec
+
+    curve = PolicySpec().learn_curve()
+    t = synthetic_mi355x(4)
+    L, (nid,) = ledger_with(t)
+    for key, owner, pct, dev, busy in (("a", "o-small", 12, 0, 10), ("b", "o-quarter", 25, 1, 30),
+                                       ("c", "o-big-cool", 75, 2, 20), ("d", "o-big-hot", 75, 3, 40)):
+        assert L.allocate_plan(nid, key, [(pct, 0)], [[dev]], True) == N.OK
+        L.set_pod_owner(key, owner)
+        assert L.set_mem_busy(nid, dev, busy) == N.OK
+    assert [d["mem_busy"] for d in L.snapshot(nid)["devices"]] == [10, 30, 20, 40]
+    assert L.learn_stream_owners(True, N.mono_now(), 1, curve) == (3, 0)
+    assert [L.is_stream_owner(o) for o in ("o-small", "o-quarter", "o-big-cool", "o-big-hot")] == \
+        [True, True, False, True]
+    # without a curve the device mark decides (none set here)
+    L2, (nid2,) = ledger_with(t)
+    assert L2.allocate_plan(nid2, "b", [(25, 0)], [[1]], True) == N.OK
+    L2.set_pod_owner("b", "o-quarter")
+    L2.set_mem_busy(nid2, 1, 30)
+    assert L2.learn_stream_owners(True) == (0, 0)
