@@ -968,6 +968,10 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
       const std::string_view owner = controller_uid(d, d.get(md, "ownerReferences"));
       if (!owner.empty()) cached.owner = owner_hash(owner);
     }
+    // Read per request, not memoised per pod: a learning pass between a pod's priorities and
+    // its bind can change the flag. The bind then adopts the priorities-time nomination, whose
+    // plan and demand the ledger keeps (Ledger::reserve), so the pod lands where it was scored
+    // (tests/test_frontend.py::test_owner_learned_between_priorities_and_bind_is_tolerated).
     if (!d.is(mb, json::Type::kStr) && cached.owner && ledger_->is_stream_owner(cached.owner))
       for (int c = 0; c < dem.n; ++c) dem.c[c].flags |= kFlagMemBound;
   }

@@ -690,3 +690,43 @@ def test_learned_streaming_owner_marks_its_next_pods_memory_bound_on_the_native_
             await rt.stop()
 
     asyncio.run(main())
+
+
+def test_owner_learned_between_priorities_and_bind_is_tolerated():
+    """the owner-derived memory-bound flag is read per request, so a learning
+    pass between a pod's priorities and its bind gives the bind a different demand than the one
+    scored. That is tolerated by design: the bind adopts the priorities-time nomination (the
+    ledger keeps the nominated plan and its demand), so the pod lands where it was nominated and
+    commits; the next pods of the owner are the ones placed as memory-bound."""
+    async def main():
+        store, rt = await _runtime(1, "SPX")
+        loop = asyncio.get_running_loop()
+        led = rt.state.ledger
+        try:
+            pod = pu.make_pod("p", [("main", 25, 8192)])
+            pod["metadata"]["ownerReferences"] = [
+                {"apiVersion": "apps/v1", "kind": "ReplicaSet", "name": "rs", "uid": "rs-late", "controller": True}]
+            pod = store.create_pod(pod)
+            raw = _dumps({"Pod": pod, "Nodes": None, "NodeNames": ["n0"]})
+            got = await loop.run_in_executor(None, _http, rt.bound_port,
+                                             [("POST", "/scheduler/filter", raw), ("POST", "/scheduler/priorities", raw)])
+            assert [g[0] for g in got] == [200, 200]
+            uid = pu.pod_uid(pod)
+            nom = led.lookup(uid)
+            assert nom is not None and nom["state"] == "nominated"
+            led.set_stream_owner("rs-late", True)          # learned in between
+            m = pu.meta(pod)
+            bind = _dumps({"PodName": m["name"], "PodNamespace": m["namespace"], "PodUID": uid, "Node": "n0"})
+            got = await loop.run_in_executor(None, _http, rt.bound_port, [("POST", "/scheduler/bind", bind)])
+            assert got[0] == (200, b'{"Error":""}')
+            for _ in range(200):
+                rec = led.lookup(uid)
+                if rec and rec["state"] == "committed":
+                    break
+                await asyncio.sleep(0.01)
+            assert rec["state"] == "committed" and rec["plan"] == nom["plan"]
+            assert sum(d["pct_free"] for d in led.snapshot(led.find_node("n0"))["devices"]) == 8 * 100 - 25
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
