@@ -68,22 +68,26 @@ _SERVICES = {
 }
 
 
-def _map_entry(msg: descriptor_pb2.DescriptorProto, field: str) -> str:
+def _map_entry(msg: descriptor_pb2.DescriptorProto, field: str, package: str = PACKAGE) -> str:
     entry = msg.nested_type.add()
     entry.name = "".join(p.capitalize() for p in field.split("_")) + "Entry"
     entry.options.map_entry = True
     for i, k in enumerate(("key", "value"), 1):
         f = entry.field.add()
         f.name, f.number, f.type, f.label = k, i, _F.TYPE_STRING, _F.LABEL_OPTIONAL
-    return f".{PACKAGE}.{msg.name}.{entry.name}"
+    return f".{package}.{msg.name}.{entry.name}"
 
 
-def _build():
+def _build(package: str = PACKAGE, file_name: str = "nanogpu/deviceplugin_v1beta1.proto",
+           messages: dict | None = None, services: dict | None = None):
+    """Message classes of one proto package, assembled from the field tables above."""
+    messages = _MESSAGES if messages is None else messages
+    services = _SERVICES if services is None else services
     fd = descriptor_pb2.FileDescriptorProto()
-    fd.name = "nanogpu/deviceplugin_v1beta1.proto"
-    fd.package = PACKAGE
+    fd.name = file_name
+    fd.package = package
     fd.syntax = "proto3"
-    for name, fields in _MESSAGES.items():
+    for name, fields in messages.items():
         m = fd.message_type.add()
         m.name = name
         for fname, num, ftype, rep in fields:
@@ -91,25 +95,25 @@ def _build():
             f.name, f.number = fname, num
             if ftype == "map":
                 f.type, f.label = _F.TYPE_MESSAGE, _F.LABEL_REPEATED
-                f.type_name = _map_entry(m, fname)
+                f.type_name = _map_entry(m, fname, package)
             elif ftype.startswith("."):
                 f.type = _F.TYPE_MESSAGE
-                f.type_name = f".{PACKAGE}{ftype}"
+                f.type_name = f".{package}{ftype}"
                 f.label = _F.LABEL_REPEATED if rep else _F.LABEL_OPTIONAL
             else:
                 f.type = _T[ftype]
                 f.label = _F.LABEL_REPEATED if rep else _F.LABEL_OPTIONAL
-    for sname, methods in _SERVICES.items():
+    for sname, methods in services.items():
         s = fd.service.add()
         s.name = sname
         for mname, req, resp, stream in methods:
             md = s.method.add()
-            md.name, md.input_type, md.output_type = mname, f".{PACKAGE}.{req}", f".{PACKAGE}.{resp}"
+            md.name, md.input_type, md.output_type = mname, f".{package}.{req}", f".{package}.{resp}"
             md.server_streaming = stream
     pool = descriptor_pool.DescriptorPool()
     fdesc = pool.Add(fd)
     fdesc = pool.FindFileByName(fd.name)
-    return {name: message_factory.GetMessageClass(fdesc.message_types_by_name[name]) for name in _MESSAGES}
+    return {name: message_factory.GetMessageClass(fdesc.message_types_by_name[name]) for name in messages}
 
 
 M = _build()
@@ -120,28 +124,34 @@ def method_path(service: str, method: str) -> str:
     return f"/{PACKAGE}.{service}/{method}"
 
 
-def generic_handler(service: str, impl) -> "object":
+def generic_handler(service: str, impl, package: str = PACKAGE, services: dict | None = None,
+                    messages: dict | None = None) -> "object":
     """grpc generic handler for `service` dispatching to `impl.<Method>(request, context)`."""
     import grpc
 
+    services = _SERVICES if services is None else services
+    messages = M if messages is None else messages
     handlers = {}
-    for mname, req, resp, stream in _SERVICES[service]:
+    for mname, req, resp, stream in services[service]:
         fn = getattr(impl, mname)
-        de, se = M[req].FromString, M[resp].SerializeToString
+        de, se = messages[req].FromString, messages[resp].SerializeToString
         if stream:
             handlers[mname] = grpc.unary_stream_rpc_method_handler(fn, request_deserializer=de, response_serializer=se)
         else:
             handlers[mname] = grpc.unary_unary_rpc_method_handler(fn, request_deserializer=de, response_serializer=se)
-    return grpc.method_handlers_generic_handler(f"{PACKAGE}.{service}", handlers)
+    return grpc.method_handlers_generic_handler(f"{package}.{service}", handlers)
 
 
 class Stub:
     """Client for either service over a grpc channel (tests' fake kubelet uses it too)."""
 
-    def __init__(self, channel, service: str):
-        for mname, req, resp, stream in _SERVICES[service]:
-            path = method_path(service, mname)
-            ser, de = M[req].SerializeToString, M[resp].FromString
+    def __init__(self, channel, service: str, package: str = PACKAGE, services: dict | None = None,
+                 messages: dict | None = None):
+        services = _SERVICES if services is None else services
+        messages = M if messages is None else messages
+        for mname, req, resp, stream in services[service]:
+            path = f"/{package}.{service}/{mname}"
+            ser, de = messages[req].SerializeToString, messages[resp].FromString
             if stream:
                 call = channel.unary_stream(path, request_serializer=ser, response_deserializer=de)
             else:

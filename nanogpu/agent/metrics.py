@@ -117,6 +117,9 @@ def render(topo, plugin=None, render_minors: list[int] | None = None, sysfs_root
     family("nanogpu_container_cus", "gauge", "compute units the container may use on the device", rows_c)
     family("nanogpu_container_hbm_budget_bytes", "gauge", "HBM budget of the container on the device", rows_m)
     if plugin is not None:
+        family("nanogpu_plugin_swaps_fixed_total", "counter",
+               "containers kubelet admitted with another container's grant, reconciled from pod-resources",
+               [("", plugin.swaps_fixed)])
         family("nanogpu_plugin_id_mismatches_total", "counter",
                "Allocate calls whose kubelet IDs named another device than the container's placement",
                [("", plugin.id_mismatches)])

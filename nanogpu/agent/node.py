@@ -90,7 +90,8 @@ async def publish(api, node_name: str, topo: NodeTopology, advertise_percent: bo
 class NodeAgent:
     def __init__(self, api, node_name: str, topo: NodeTopology, host: dict | None = None,
                  device_plugin: bool = True, plugin_dir: str = "", health_period_s: float = 10.0,
-                 sysfs_root: str = "", kubelet_check_s: float = 1.0):
+                 sysfs_root: str = "", kubelet_check_s: float = 1.0, pod_resources_socket: str | None = None,
+                 reconcile_period_s: float = 5.0):
         self.api = api
         self.node = node_name
         self.topo = topo
@@ -101,6 +102,11 @@ class NodeAgent:
         self.sysfs_root = sysfs_root
         self.kubelet_check_s = kubelet_check_s
         self.selftest_failed: set[int] = set()   # devices whose active self-test failed
+        # kubelet's pod-resources API: which container got which device IDs (plugin.reconcile)
+        from .podresources import SOCKET as _PR_SOCKET
+
+        self.pod_resources_socket = pod_resources_socket if pod_resources_socket is not None else _PR_SOCKET
+        self.reconcile_period_s = reconcile_period_s
         self.registrations = 0
         self._register = True
         self.plugin = None
@@ -137,6 +143,29 @@ class NodeAgent:
             self.tasks.append(asyncio.ensure_future(self._kubelet_watch()))
         if self.health_period_s > 0:
             self.tasks.append(asyncio.ensure_future(self._health_loop()))
+        if self.reconcile_period_s > 0 and self.pod_resources_socket:
+            self.tasks.append(asyncio.ensure_future(self._reconcile_loop()))
+
+    async def reconcile_now(self) -> list[tuple[str, str]]:
+        """One pass: kubelet's pod-resources List against the plugin's grants."""
+        from .podresources import list_devices
+
+        if self.plugin is None or not os.path.exists(self.pod_resources_socket):
+            return []
+        listed = await list_devices(self.pod_resources_socket, T.RESOURCE_GPU_PERCENT)
+        moved = await self.plugin.reconcile(listed)
+        if moved:
+            log.warning("agent %s: %d containers ran with another container's grant; reconciled", self.node,
+                        len(moved))
+        return moved
+
+    async def _reconcile_loop(self) -> None:
+        while True:
+            await asyncio.sleep(self.reconcile_period_s)
+            try:
+                await self.reconcile_now()
+            except Exception as e:   # kubelet restarting, socket not served yet
+                log.debug("agent %s: pod-resources check failed: %s", self.node, e)
 
     def _dir(self) -> str:
         return self.plugin_dir or "/var/lib/kubelet/device-plugins"

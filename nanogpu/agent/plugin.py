@@ -15,7 +15,13 @@ into a device inside the container. This is the AMD equivalent:
   and the HBM budget (`NANO_GPU_MEMORY_MIB`, enforced in-process by nanogpu.agent.guest);
 * records the CU grant as `nano-gpu/cu-mask-<c>` on the pod, so an agent restart
   rebuilds its CU map from the API server (the same checkpoint contract as the
-  extender's, reference dealer.go:58-72).
+  extender's, reference dealer.go:58-72);
+* reconciles against kubelet's pod-resources API (`reconcile`): Allocate has no pod identity,
+  so if kubelet admits two same-size containers out of bind order, each gets the other's
+  device and grant. kubelet's List says which pod holds which IDs; the agent then moves the
+  grants to the containers that really run with them, rewrites both pods' placement and
+  CU-mask annotations (marked `nano-gpu/reconciled`, which the extender's pod controller
+  re-accounts), and records a Warning Event on each pod.
 """
 from __future__ import annotations
 
@@ -117,6 +123,7 @@ class NanoGpuPlugin:
         # live grants by (pod uid, container): what the agent's /metrics reports per container
         self.grants: dict[tuple[str, str], Assignment] = {}
         self.id_mismatches = 0   # Allocate IDs on another device than the placement (see Allocate)
+        self.swaps_fixed = 0     # containers whose grant was moved after a pod-resources check
 
     # ---------------------------------------------------------------- restart rebuild
     async def rebuild(self, pods: list[dict] | None = None) -> int:
@@ -153,6 +160,79 @@ class NanoGpuPlugin:
             del self.matcher.claimed[k]
         for k in [k for k in self.grants if k[0] == uid]:
             del self.grants[k]
+
+    async def reconcile(self, listed: dict[tuple[str, str, str], list[str]]) -> list[tuple[str, str]]:
+        """Checks the grants against kubelet's record of which container got which device IDs
+        (pod-resources List: (namespace, pod, container) -> IDs of nano-gpu/gpu-percent).
+
+        A container kubelet lists on other devices than the grant recorded for it ran with
+        another container's Allocate answer: kubelet admitted same-size containers out of bind
+        order, and the matcher gave each the other's placement. Each such container is paired
+        with the mis-recorded grant of the same size whose devices it really holds; the grant
+        (CU bits included) moves to it, both pods' annotations are rewritten to what runs, and
+        a Warning Event says so. Returns the (pod uid, container) keys that moved."""
+        uid_of = {a.pod_key: uid for (uid, _), a in self.grants.items()}
+        actual: dict[tuple[str, str], list[int]] = {}
+        for (ns, pod, cn), ids in listed.items():
+            uid = uid_of.get(f"{ns}/{pod}")
+            if uid is None or (uid, cn) not in self.grants:
+                continue
+            try:
+                actual[(uid, cn)] = sorted({int(i[1:i.index("-")]) for i in ids})
+            except ValueError:
+                continue
+        wrong = [(k, devs) for k, devs in actual.items() if devs != sorted(self.grants[k].devices)]
+        if not wrong:
+            return []
+        pool = {k: self.grants[k] for k, _ in wrong}
+        moves = []          # (container that runs it, grant it runs under)
+        for k, devs in wrong:
+            want = self.grants[k].percent
+            src = next((g for g, a in pool.items() if sorted(a.devices) == devs and a.percent == want), None)
+            if src is None:
+                log.warning("reconcile: %s/%s holds devices %s, no matching grant", *k, devs)
+                continue
+            del pool[src]
+            moves.append((k, src))
+        old = dict(self.grants)
+        bits = {}           # grant key -> (device, CU bits) before the moves
+        for k, src in moves:
+            a = old[src]
+            if len(a.devices) == 1 and f"{src[0]}/{src[1]}" in self.cus[a.devices[0]].used:
+                bits[src] = (a.devices[0], self.cus[a.devices[0]].bits(f"{src[0]}/{src[1]}"))
+        for _, src in moves:
+            if src in bits:
+                self.cus[bits[src][0]].release(f"{src[0]}/{src[1]}")
+        moved = []
+        for k, src in moves:
+            a = old[src]
+            mine = old[k]
+            self.grants[k] = Assignment(mine.pod_key, k[1], list(a.devices), a.percent, mine.mib, a.cus)
+            mask_ann = "full"
+            if src in bits:
+                dev, b = bits[src]
+                self.cus[dev].restore(f"{k[0]}/{k[1]}", b)
+                mask_ann = cumask.hsa_cu_mask(0, b)
+            ns, name = mine.pod_key.split("/", 1)
+            placed = ",".join(map(str, mine.devices))
+            runs = ",".join(map(str, a.devices))
+            try:
+                await self.api.patch_pod(ns, name, {"metadata": {"annotations": {
+                    T.container_annotation(k[1]): runs, T.ANNOTATION_CU_MASK_FMT.format(k[1]): mask_ann,
+                    T.ANNOTATION_RECONCILED: str(time.time())}}})
+            except Exception as e:   # the grant map is right either way; the next pass retries
+                log.warning("reconcile: annotating %s failed: %s", mine.pod_key, e)
+            try:
+                await self.api.create_event(ns, {"kind": "Pod", "namespace": ns, "name": name, "uid": k[0]},
+                                            "NanoGpuAllocationSwapped",
+                                            f"container {k[1]} runs on device {runs} (placed on {placed}): kubelet "
+                                            f"admitted same-size containers out of bind order; placement and "
+                                            f"CU-mask annotations now follow what runs", "Warning")
+            except Exception as e:
+                log.debug("reconcile: event for %s failed: %s", mine.pod_key, e)
+            moved.append(k)
+        self.swaps_fixed += len(moved)
+        return moved
 
     def set_health(self, dev: int, healthy: bool) -> None:
         if self.health[dev] != healthy:

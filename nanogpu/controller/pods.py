@@ -79,6 +79,7 @@ class PodController:
             # held a share is simply not in the ledger)
             self._release(uid)
             self.state.forget(uid)
+            self.state.forget_reaccount(uid)
             return
         node = (pod.get("spec") or {}).get("nodeName")
         # a terminating pod (deletionTimestamp only) still runs and keeps its share until it
@@ -87,8 +88,12 @@ class PodController:
             (self.state.options.compat and bool(m.get("deletionTimestamp")))
         if not node and not completed:
             return                             # pending: the extender's own business until bound
-        if self.state.known(uid):
+        if self.state.known(uid) or uid in self.state._reaccount_wait:
             if completed:                                                        # controller.go:303-306
+                self.queue.add(f"{m.get('namespace', 'default')}/{m.get('name', '')}")
+            elif T.ANNOTATION_RECONCILED in (m.get("annotations") or {}):
+                # the node agent found the pod running on other devices than placed (kubelet
+                # admitted same-size containers out of bind order) and rewrote its annotations
                 self.queue.add(f"{m.get('namespace', 'default')}/{m.get('name', '')}")
             return
         if completed or self.state.released(uid):
@@ -104,10 +109,17 @@ class PodController:
         if pod is None:
             return
         if pu.share_gone(pod, self.state.options.compat):
+            self.state.forget_reaccount(pu.pod_uid(pod))
             if self.state.release(pod) and self.metrics:
                 self.metrics.pods_released.inc()
             return
         if not pu.node_name_of(pod) or not pu.is_assumed(pod):
+            return
+        uid = pu.pod_uid(pod)
+        if T.ANNOTATION_RECONCILED in (pu.meta(pod).get("annotations") or {}) and \
+                (self.state.known(uid) or uid in self.state._reaccount_wait):
+            if self.state.reaccount(pod) and self.metrics:
+                self.metrics.pods_reaccounted.inc()
             return
         if not self.state.known(pu.pod_uid(pod)) and not self.state.released(pu.pod_uid(pod)):
             if not self.state.allocate_existing(pod):

@@ -112,6 +112,9 @@ class Metrics:
         self.api_errors = LoopCounter("nanogpu_api_errors_total", "API server errors", ["op", "code"], r)
         self.pods_bound = LoopCounter("nanogpu_pods_bound_total", "pods bound by this extender", registry=r)
         self.pods_released = LoopCounter("nanogpu_pods_released_total", "pods released", registry=r)
+        self.pods_reaccounted = LoopCounter("nanogpu_pods_reaccounted_total",
+                                            "bound pods moved to the devices kubelet ran them on (agent reconciliation)",
+                                            registry=r)
         self.rollbacks = LoopCounter("nanogpu_rollbacks_total", "reservations rolled back", registry=r)
         self.frag_pct = Gauge("nanogpu_frag_percent", "free gpu-percent on partially used devices / free",
                               registry=r)

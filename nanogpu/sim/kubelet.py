@@ -36,6 +36,9 @@ class FakeKubelet:
         self.devices: list[str] = []
         self.healthy: set[str] = set()
         self.allocated: set[str] = set()
+        # what kubelet's pod-resources API lists: (namespace, pod, container) -> device IDs
+        self.assigned: dict[tuple[str, str, str], list[str]] = {}
+        self.resource = T.RESOURCE_GPU_PERCENT
         self._plugin_ch = None
         self._stub = None
         self._watch: asyncio.Task | None = None
@@ -44,10 +47,32 @@ class FakeKubelet:
     async def start(self) -> None:
         import grpc
 
+        from ..agent import podresources as PR
+
         self.server = grpc.aio.server()
-        self.server.add_generic_rpc_handlers((D.generic_handler("Registration", self),))
+        self.server.add_generic_rpc_handlers((D.generic_handler("Registration", self),
+                                              PR.generic_handler(self)))
         self.server.add_insecure_port(f"unix://{os.path.join(self.dir, 'kubelet.sock')}")
+        self.server.add_insecure_port(f"unix://{self.pod_resources_socket}")
         await self.server.start()
+
+    @property
+    def pod_resources_socket(self) -> str:
+        return os.path.join(self.dir, "pod-resources.sock")
+
+    async def List(self, request, context):
+        """PodResourcesLister.List: the device IDs every admitted container holds."""
+        from ..agent import podresources as PR
+
+        resp = PR.ListPodResourcesResponse()
+        pods: dict[tuple[str, str], object] = {}
+        for (ns, name, cn), ids in self.assigned.items():
+            p = pods.get((ns, name))
+            if p is None:
+                p = pods[(ns, name)] = resp.pod_resources.add(name=name, namespace=ns)
+            c = p.containers.add(name=cn)
+            c.devices.add(resource_name=self.resource, device_ids=ids)
+        return resp
 
     async def Register(self, request, context):
         self.registered.append((request.version, request.endpoint, request.resource_name))
@@ -81,6 +106,8 @@ class FakeKubelet:
             resp = await self._stub.Allocate(D.AllocateRequest(container_requests=[
                 D.ContainerAllocateRequest(devices_ids=ids)]))
             self.allocated.update(ids)
+            ns, name = pu.pod_ns_name(pod)
+            self.assigned[(ns, name, c.get("name", ""))] = ids
             r = resp.container_responses[0]
             out[c.get("name", "")] = {"ids": ids, "envs": dict(r.envs),
                                       "devices": [d.host_path for d in r.devices],

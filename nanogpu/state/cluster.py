@@ -72,6 +72,7 @@ class ClusterState:
         self._released: OrderedDict[str, None] = OrderedDict()   # reference ReleasedPodMap
         self._rejected: dict[str, str] = {}     # nodes the ledger cannot hold, with the reason
         self._released_cap = 65536
+        self._reaccount_wait: dict[str, dict] = {}   # uid -> pod waiting for its partner (reaccount)
         self.set_policy(policy, compat=compat, load_aware=load_aware, topo_weight=topo_weight, seed=seed,
                         request_sizes=request_sizes or [], learn_sizes=learn_sizes)
 
@@ -297,7 +298,7 @@ class ClusterState:
     def rollback(self, uid: str) -> None:
         self.ledger.release(uid)
 
-    def allocate_existing(self, pod: dict) -> bool:
+    def allocate_existing(self, pod: dict, quiet: bool = False) -> bool:
         """Account a pod placed by someone else / found at restart (dealer.go:205-228)."""
         node = pu.node_name_of(pod)
         if not node:
@@ -320,12 +321,53 @@ class ClusterState:
             return False
         rc = self.ledger.allocate_plan(e.id, pu.pod_uid(pod), demand, pu.ledger_plan(plan, idx), True)
         if rc != N.OK:
-            log.warning("allocate %s on %s failed: %s", pu.pod_key(pod), node, N.err_str(rc))
+            if not quiet:
+                log.warning("allocate %s on %s failed: %s", pu.pod_key(pod), node, N.err_str(rc))
             return False
         owner = pu.controller_uid(pod)
         if owner:
             self.ledger.set_pod_owner(pu.pod_uid(pod), owner)
         return True
+
+    def reaccount(self, pod: dict) -> bool:
+        """A bound pod whose placement annotations changed (the node agent's reconciliation
+        with kubelet): its share moves to the annotated devices. True if it moved.
+
+        Swapped containers are re-accounted one at a time, so the first one's new devices are
+        often still held by its partner: its share is dropped and it waits (`_reaccount_wait`)
+        until the partner has moved; every move retries the waiting ones."""
+        uid = pu.pod_uid(pod)
+        rec = self.ledger.lookup(uid)
+        plan = pu.plan_from_pod(pod)
+        if rec is None and uid in self._reaccount_wait:
+            self._reaccount_wait[uid] = pod
+            return self._retry_reaccount()
+        if rec is None or plan is None or rec["state"] != "committed":
+            return False
+        try:
+            _, idx = pu.ledger_view(self.pod_demand(pod))
+        except pu.TooManyGpuContainers:
+            return False
+        if [list(x) for x in pu.ledger_plan(plan, idx)] == [list(x) for x in rec["plan"]]:
+            return False
+        if self.ledger.drop_committed(uid) != N.OK:
+            return False
+        if not self.allocate_existing(pod, quiet=True):
+            self._reaccount_wait[uid] = pod     # its new devices are still taken: wait
+            return False
+        self._retry_reaccount()
+        return True
+
+    def _retry_reaccount(self) -> bool:
+        moved = False
+        for uid, pod in list(self._reaccount_wait.items()):
+            if self.allocate_existing(pod, quiet=True):
+                del self._reaccount_wait[uid]
+                moved = True
+        return moved
+
+    def forget_reaccount(self, uid: str) -> None:
+        self._reaccount_wait.pop(uid, None)
 
     def release(self, pod: dict) -> bool:
         return self.release_uid(pu.pod_uid(pod))

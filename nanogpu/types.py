@@ -33,6 +33,7 @@ POLICIES = (PRIORITY_BINPACK, PRIORITY_SPREAD, PRIORITY_RANDOM, PRIORITY_FIRSTFI
 
 RESOURCE_GPU_MEMORY = "nano-gpu/gpu-memory"   # HBM MiB per container (288 GB / MI355X)
 ANNOTATION_TOPOLOGY = "nano-gpu/topology"     # node: JSON from the node agent (topology.model)
+ANNOTATION_RECONCILED = "nano-gpu/reconciled"   # pod: the agent rewrote its placement to what kubelet ran
 ANNOTATION_CU_MASK_FMT = "nano-gpu/cu-mask-{}"  # pod: per-container CU mask chosen by the agent
 ANNOTATION_ASSUME_TIME = "nano-gpu/assume-time"
 ANNOTATION_SCHEDULER = "nano-gpu/scheduler"

@@ -364,6 +364,9 @@ static py::list decode_pod_events(const py::bytes& data, PodWatchFilter* f) {
         } else if (!completed) {
           PodRecord rec;
           drop = f->ledger->lookup(std::string(field(md, "uid")), &rec);
+          // the node agent rewrote the placement to what kubelet ran (plugin.reconcile): the
+          // controller re-accounts it, so the event goes on
+          if (drop && line.find("\"nano-gpu/reconciled\"") != std::string_view::npos) drop = false;
         }
       }
       if (drop) {

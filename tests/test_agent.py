@@ -346,3 +346,91 @@ def test_agent_metrics_export_hbm_activity_from_sysfs(tmp_path):
     assert 'nanogpu_device_mem_busy_percent{device="0"} 85' in text
     assert 'nanogpu_device_mem_busy_percent{device="1"} 0' in text
     assert 'nanogpu_device_busy_percent{device="0"} 40' in text
+
+
+def test_out_of_bind_order_admission_is_reconciled_from_pod_resources(tmp_path):
+    """VERDICT r2 weak #8. Two 60 % pods with different HBM land on two GPUs; kubelet admits
+    the later-bound one first. Allocate carries no pod identity, so each container runs with
+    the other's device and CU grant. kubelet's pod-resources List shows it; the agent moves the
+    grants, rewrites both pods' placement and CU-mask annotations, records Warning Events, and
+    the extender (REST + native watch filter, its production path) re-accounts both pods, so
+    the HBM each GPU carries is what runs there."""
+    import json as _json
+
+    from nanogpu.app import Config, Runtime
+    from nanogpu.k8s.fake_apiserver import serve
+    from nanogpu.sim.kubelet import FakeKubelet as SimKubelet
+
+    import aiohttp
+
+    async def main():
+        store = FakeKubeStore()
+        topo = synthetic_mi355x(8)
+        store.add_node(pu.make_node("n0", 8, topo.to_json(), {"amd.com/gpu.present": "true"}))
+        runner, port = await serve(store)
+        url = f"http://127.0.0.1:{port}"
+        rt = Runtime(Config(kube_api=url, port=0, host="127.0.0.1", policy_config_path="/nonexistent"))
+        await rt.start()
+        api = InProcKube(store)
+        kl = SimKubelet(api, "n0", str(tmp_path))
+        await kl.start()
+        agent = NodeAgent(api, "n0", topo, device_plugin=True, plugin_dir=str(tmp_path), health_period_s=0,
+                          pod_resources_socket=kl.pod_resources_socket, reconcile_period_s=0)
+        await agent.start()
+        led = rt.state.ledger
+        try:
+            await asyncio.wait_for(kl.ready.wait(), 10)
+            assert rt.pod_informer.watch_filter is not None
+            a = store.create_pod(pu.make_pod("a", [("main", 60, 32 * 1024)]))
+            b = store.create_pod(pu.make_pod("b", [("main", 60, 64 * 1024)]))
+            async with aiohttp.ClientSession() as s:
+                for p in (a, b):
+                    m = pu.meta(p)
+                    body = {"PodName": m["name"], "PodNamespace": "default", "PodUID": m["uid"], "Node": "n0"}
+                    async with s.post(f"http://127.0.0.1:{rt.bound_port}/scheduler/bind", data=_json.dumps(body)) as r:
+                        assert (await r.json())["Error"] == ""
+                    await asyncio.sleep(0.01)       # distinct assume-times: a is bound first
+            for _ in range(300):
+                ra, rb = led.lookup(pu.pod_uid(a)), led.lookup(pu.pod_uid(b))
+                if ra and rb and ra["state"] == rb["state"] == "committed":
+                    break
+                await asyncio.sleep(0.01)
+            (dev_a,), (dev_b,) = ra["plan"][0], rb["plan"][0]
+            assert dev_a != dev_b
+            for _ in range(200):    # the agent's informer has both bound pods
+                if len(agent.informer.list()) == 2:
+                    break
+                await asyncio.sleep(0.01)
+            spec_b = await kl.admit(store.get_pod("default", "b"))    # out of bind order
+            spec_a = await kl.admit(store.get_pod("default", "a"))
+            # the swap v1beta1 cannot prevent: b runs on a's GPU and vice versa
+            assert spec_b["main"]["envs"]["NANO_GPU_DEVICES"] == str(dev_a)
+            assert spec_a["main"]["envs"]["NANO_GPU_DEVICES"] == str(dev_b)
+            moved = await agent.reconcile_now()
+            assert sorted(moved) == sorted([(pu.pod_uid(a), "main"), (pu.pod_uid(b), "main")])
+            assert agent.plugin.swaps_fixed == 2
+            ann_a = store.get_pod("default", "a")["metadata"]["annotations"]
+            ann_b = store.get_pod("default", "b")["metadata"]["annotations"]
+            assert ann_a[T.container_annotation("main")] == str(dev_b)
+            assert ann_b[T.container_annotation("main")] == str(dev_a)
+            assert ann_b[T.ANNOTATION_CU_MASK_FMT.format("main")] == spec_b["main"]["envs"]["HSA_CU_MASK"]
+            assert T.ANNOTATION_RECONCILED in ann_a and T.ANNOTATION_RECONCILED in ann_b
+            assert agent.plugin.cus[dev_a].used.keys() == {f"{pu.pod_uid(b)}/main"}
+            assert {e["reason"] for e in store.events} == {"NanoGpuAllocationSwapped"}
+            # the extender follows: b's 64 GiB now on dev_a, a's 32 GiB on dev_b
+            for _ in range(300):
+                if led.lookup(pu.pod_uid(a))["plan"] == [[dev_b]] and led.lookup(pu.pod_uid(b))["plan"] == [[dev_a]]:
+                    break
+                await asyncio.sleep(0.01)
+            assert led.lookup(pu.pod_uid(a))["plan"] == [[dev_b]] and led.lookup(pu.pod_uid(b))["plan"] == [[dev_a]]
+            gpus = rt.state.status()["n0"]["GPUs"]
+            assert gpus[dev_a]["MemoryMiBTotal"] - gpus[dev_a]["MemoryMiB"] == 64 * 1024
+            assert gpus[dev_b]["MemoryMiBTotal"] - gpus[dev_b]["MemoryMiB"] == 32 * 1024
+            assert await agent.reconcile_now() == []          # consistent now
+        finally:
+            await agent.stop()
+            await kl.stop()
+            await rt.stop()
+            await runner.cleanup()
+
+    asyncio.run(main())
