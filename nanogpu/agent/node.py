@@ -305,11 +305,16 @@ def build_parser():
                     help="run the HIP self-test (HBM copy + MFMA tile) on every device at start-up")
     ap.add_argument("--metrics-port", type=int, default=9410,
                     help="device / pod / container GPU metrics on :PORT/metrics (0: off)")
+    ap.add_argument("--pod-resources-socket", default="/var/lib/kubelet/pod-resources/kubelet.sock",
+                    help="kubelet's pod-resources API: the grants are checked against it ('' : off)")
+    ap.add_argument("--reconcile-period", type=float, default=5.0,
+                    help="seconds between pod-resources checks (0: off)")
     return ap
 
 
 def main(argv: list[str] | None = None) -> int:
-    a = build_parser().parse_args(argv)
+    ap = build_parser()
+    a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     topo, host = discover(a.sysfs_root, not a.no_amdsmi)
     if a.calibrate:
@@ -327,7 +332,8 @@ def main(argv: list[str] | None = None) -> int:
 
         api = KubeClient(KubeConfig.auto(a.kubeconfig, a.kube_api))
         agent = NodeAgent(api, a.node_name, topo, host, device_plugin=a.advertise == "device-plugin",
-                          plugin_dir=a.plugin_dir, sysfs_root=a.sysfs_root)
+                          plugin_dir=a.plugin_dir, sysfs_root=a.sysfs_root,
+                          pod_resources_socket=a.pod_resources_socket, reconcile_period_s=a.reconcile_period)
         await agent.start()
         if a.selftest:
             failed = await agent.selftest()
