@@ -290,6 +290,7 @@ struct Frontend::Worker {
   std::vector<std::pair<uint64_t, std::string>> mailbox;       // (conn id, response bytes)
   std::atomic<bool> unsignalled{false};                         // queued with notify=false
   uint64_t next_conn = 1;
+  uint64_t cycle_reply_ns = 0;   // last filter / priorities reply handed to the kernel
 };
 
 static uint64_t make_id(int worker, uint64_t conn) { return (conn << 8) | static_cast<uint64_t>(worker); }
@@ -530,25 +531,27 @@ void Frontend::prepare_bind(std::string_view body, PyRequest* r) {
 void Frontend::run(Worker* w) {
   epoll_event evs[128];
   std::vector<uint64_t> later;   // connections whose next request is a bind
-  uint64_t last_event = 0;
-  // Adaptive busy polling: spin after an event only while spinning pays. Every event's gap to
-  // the previous one is a hit when it is shorter than the spin window (a spin would have
-  // caught it without a wake-up) and a miss otherwise; a worker spins while at least half of
-  // its last 16 gaps were hits. The worker that carries kube-scheduler's scheduling-cycle
-  // connection (filter, then priorities, then the next pod's filter a few microseconds
-  // later) stays hot during a burst; one that only sees the asynchronous binds, tens of
-  // microseconds apart, blocks in epoll_wait instead of burning a core.
-  uint32_t gaps = 0xffffu;   // 1 bits: hits among the last 16 gaps (start hot)
+  // Busy polling only where a wake-up would sit on kube-scheduler's critical path: after this
+  // worker replied to a filter or priorities request. kube-scheduler's scheduling cycle is
+  // serial (filter, then priorities, then the next pod's filter a few microseconds later), so
+  // the next cycle request is due soon; a bind is asynchronous and its reply, or a writer's
+  // completion, never starts a spin. Adaptive on top: the first event after a cycle reply is a
+  // hit if it came within the spin window; a worker spins while at least half of its last 16
+  // were hits (a slow scheduler, tens of microseconds between verbs, is not spun for).
+  uint32_t gaps = 0xffffu;   // 1 bits: hits among the last 16 cycle replies (start hot)
+  uint64_t scored = 0;       // the cycle reply the last hit/miss was scored for
   while (!stop_.load(std::memory_order_acquire)) {
     const int64_t spin = busy_poll_ns_.load(std::memory_order_relaxed);
     const bool hot = __builtin_popcount(gaps & 0xffffu) >= 8;
-    const bool polling = spin > 0 && hot && now_ns() - last_event < static_cast<uint64_t>(spin);
+    const uint64_t since = w->cycle_reply_ns;
+    const bool polling = spin > 0 && hot && since && now_ns() - since < static_cast<uint64_t>(spin);
     const int n = epoll_wait(w->ep, evs, 128, polling ? 0 : 200);
     const uint64_t t_batch = n > 0 ? now_ns() : 0;
     if (n > 0) {
-      if (spin > 0 && last_event)
-        gaps = (gaps << 1) | (t_batch - last_event < static_cast<uint64_t>(spin) ? 1u : 0u);
-      last_event = t_batch;
+      if (spin > 0 && since && since != scored) {
+        gaps = (gaps << 1) | (t_batch - since < static_cast<uint64_t>(spin) ? 1u : 0u);
+        scored = since;
+      }
       if (polling) spin_hits.fetch_add(1, std::memory_order_relaxed);   // caught without a wake-up
     }
     struct BatchTimer {
@@ -751,6 +754,7 @@ void Frontend::process(Worker* w, Conn* c) {
     if (handle_native(w, c, method, path, body, &out)) {
       c->out += out;
       flush(w, c);
+      w->cycle_reply_ns = now_ns();   // the scheduling cycle's next request is due: spin for it
       if (!w->conns.count(id)) return;
     } else {
       defer(w, c, std::move(method), std::move(path), std::move(query), std::move(body));
