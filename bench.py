@@ -101,6 +101,8 @@ def parse_args():
                     help="extender's native bind writer threads per rank, 8 binds in flight each "
                          "(0: 16 split over the ranks, at least 2)")
     ap.add_argument("--inflight-binds", type=int, default=64)
+    ap.add_argument("--bind-writer-mode", choices=["evented", "threads"], default="evented",
+                    help="the extender's native bind writer: one epoll thread, or blocking threads")
     ap.add_argument("--no-overlap-create", action="store_true",
                     help="create the next burst only after this one is released (by default the "
                          "workload's clients create it while the pod controller releases)")
@@ -730,7 +732,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                  policy_config_path="/nonexistent/policy.yaml", reservation_ttl_s=3600,
                  busy_poll_us=args.busy_poll_us, frontend_threads=args.frontend_threads,
                  nominate=not args.no_nominate,
-                 bind_writer_threads=args.bind_writer_threads or max(2, 16 // d.world))
+                 bind_writer_threads=args.bind_writer_threads or max(2, 16 // d.world),
+                 bind_writer_mode=args.bind_writer_mode)
     all_steps_pre = [10_000 + w for w in range(args.warmup)] + list(range(args.steps))
     rt = Runtime(cfg, worker=d.rank if shared else 0, api=rt_api)
     await rt.start()

@@ -48,6 +48,7 @@ class Config:
     verify_pod_on_bind: bool = False
     native_bind_writes: bool = True             # C++ writer threads do the bind's API writes
     bind_writer_threads: int = 16               # x KubeWriter::kBatch (8) binds in flight
+    bind_writer_mode: str = "evented"           # evented (one epoll thread) | threads (blocking threads)
     reservation_ttl_s: float = 60.0
     nominate: bool = True              # priorities nominate the top node (Ledger::nominate)
     nomination_ttl_s: float = 5.0
@@ -204,7 +205,7 @@ class Runtime:
                 if self.cfg.native_bind_writes and not self.cfg.verify_pod_on_bind and api_cfg is not None:
                     ext = self.extender
                     if self.native.enable_native_writes(api_cfg, self.cfg.bind_writer_threads, ext.api_retries,
-                                                        ext.record_events):
+                                                        ext.record_events, self.cfg.bind_writer_mode == "evented"):
                         log.info("worker %d: bind API writes in native writer threads (%d)", self.worker,
                                  self.cfg.bind_writer_threads)
                 self.native.start()

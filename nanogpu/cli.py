@@ -59,7 +59,10 @@ def build_parser() -> argparse.ArgumentParser:
                    help="the native front door's C++ threads do each bind's PATCH + binding POST + commit "
                         "(native/src/kubewriter.cpp); --no-native-bind-writes keeps them in Python")
     p.add_argument("--bind-writer-threads", type=int, default=16,
-                   help="native bind writer threads; each pipelines up to 8 binds (16 x 8 = 128 in flight)")
+                   help="binds in flight / 8 for the native writer (16: 128 binds); in --bind-writer-mode "
+                        "threads, the number of blocking writer threads")
+    p.add_argument("--bind-writer-mode", choices=["evented", "threads"], default="evented",
+                   help="native bind writes on one epoll thread (evented) or on blocking threads")
     p.add_argument("--reservation-ttl", default="60s")
     p.add_argument("--no-nominate", action="store_true",
                    help="priorities do not tentatively reserve the top-scored node")
@@ -108,7 +111,7 @@ def parse(argv: list[str] | None = None) -> Config:
         topology_weight=a.topology_weight, track_hbm=not a.no_hbm, workers=max(1, a.workers),
         ledger_path=a.ledger_path, max_nodes=a.max_nodes, max_pods=a.max_pods,
         verify_pod_on_bind=a.bind_verify_pod, native_bind_writes=a.native_bind_writes,
-        bind_writer_threads=max(1, a.bind_writer_threads), reservation_ttl_s=parse_duration(a.reservation_ttl),
+        bind_writer_threads=max(1, a.bind_writer_threads), bind_writer_mode=a.bind_writer_mode, reservation_ttl_s=parse_duration(a.reservation_ttl),
         nominate=not a.no_nominate, nomination_ttl_s=parse_duration(a.nomination_ttl),
         fake_cluster=a.fake_cluster, fake_gpus_per_node=a.fake_gpus_per_node, fake_partition=a.fake_partition,
         seed=a.seed, frontend=a.frontend, frontend_threads=max(1, a.frontend_threads), busy_poll_us=a.busy_poll_us,

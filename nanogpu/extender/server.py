@@ -398,7 +398,8 @@ class NativeServer:
                       f"nanogpu_native_binds_inflight {kw['inflight']}"]
         return ("\n".join(lines) + "\n").encode()
 
-    def enable_native_writes(self, config, threads: int, retries: int, record_events: bool) -> bool:
+    def enable_native_writes(self, config, threads: int, retries: int, record_events: bool,
+                             evented: bool = True) -> bool:
         """Hands the bind's API writes to the front door's C++ writer threads (native/src/
         kubewriter.cpp) when the API server is a REST endpoint this process reaches with a
         bearer token or a client certificate; False (Python writes) otherwise."""
@@ -410,7 +411,8 @@ class NativeServer:
         tls = u.scheme == "https"
         self.fe.set_kube_writer(u.hostname, u.port or (443 if tls else 80), tls, config.token or "",
                                 config.token_file or "", config.ca_file or "", config.cert_file or "",
-                                config.key_file or "", bool(config.insecure), threads, retries, record_events)
+                                config.key_file or "", bool(config.insecure), threads, retries, record_events,
+                                evented)
         return True
 
     async def stop(self) -> None:

@@ -81,11 +81,19 @@ struct KubeWriterStats {
       label_failures{0};
 };
 
+// Two ways to run the writes:
+//   * evented (default): ONE epoll thread drives every bind's two requests on non-blocking
+//     keep-alive connections (plain or TLS), `threads` x kBatch binds in flight. A bind whose
+//     two answers are 2xx commits right there; anything else (a 5xx / 429 / 401 to retry, a
+//     409 to check, a failure to roll back) goes to a slow-path thread that finishes it with
+//     the blocking code below. One wake-up serves every answer that arrived together, where
+//     a thread per batch sleeps and wakes once per request (kubewriter_evented.cpp);
+//   * threads: `threads` blocking threads, each pipelining up to kBatch binds.
 class KubeWriter {
  public:
   using Respond = std::function<void(uint64_t id, int status, const std::string& body)>;
   KubeWriter(KubeTarget target, std::shared_ptr<Ledger> ledger, Respond respond, int threads, int retries,
-             bool record_events);
+             bool record_events, bool evented = true);
   ~KubeWriter();
   void submit(BindJob job);
   void stop();
@@ -103,6 +111,21 @@ class KubeWriter {
   int call(HttpConn* c, const char* method, const std::string& path, const std::string& ctype,
            const std::string& body, std::string* resp, bool retry);
   std::string auth();
+
+  // evented mode (kubewriter_evented.cpp)
+  struct SlowJob {
+    BindJob j;
+    std::string patch, binding, rp, rb;
+    int sp = 0, sb = 0;
+  };
+  void io_loop();
+  void run_slow();
+  bool evented_ = false;
+  int max_inflight_ = 0;
+  int efd_ = -1;                 // wakes the io thread (new jobs, stop)
+  std::thread io_;
+  std::atomic<bool> io_done_{false};   // the io thread has handed everything to the slow path
+  std::deque<SlowJob> slow_q_;   // under mu_, signalled on cv_
 
   KubeTarget t_;
   std::shared_ptr<Ledger> ledger_;

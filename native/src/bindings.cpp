@@ -789,7 +789,8 @@ PYBIND11_MODULE(_native, m) {
           "set_kube_writer",
           [](Frontend& f, const std::string& host, int port, bool tls, const std::string& token,
              const std::string& token_file, const std::string& ca_file, const std::string& cert_file,
-             const std::string& key_file, bool insecure, int threads, int retries, bool record_events) {
+             const std::string& key_file, bool insecure, int threads, int retries, bool record_events,
+             bool evented) {
             KubeTarget t;
             t.host = host;
             t.port = port;
@@ -800,14 +801,15 @@ PYBIND11_MODULE(_native, m) {
             t.cert_file = cert_file;
             t.key_file = key_file;
             t.insecure = insecure;
-            f.set_kube_writer(t, threads, retries, record_events);
+            f.set_kube_writer(t, threads, retries, record_events, evented);
           },
           py::arg("host"), py::arg("port"), py::arg("tls") = false, py::arg("token") = "",
           py::arg("token_file") = "", py::arg("ca_file") = "", py::arg("cert_file") = "", py::arg("key_file") = "",
           py::arg("insecure") = false, py::arg("threads") = 32, py::arg("retries") = 3,
-          py::arg("record_events") = true,
-          "Binds whose reservation succeeded natively are finished by C++ writer threads "
-          "(PATCH + binding + commit/rollback) on keep-alive connections to kube-apiserver.")
+          py::arg("record_events") = true, py::arg("evented") = true,
+          "Binds whose reservation succeeded natively are finished natively (PATCH + binding + "
+          "commit/rollback) on keep-alive connections to kube-apiserver: one epoll thread "
+          "(evented) or `threads` blocking threads; `threads` x 8 binds in flight.")
       .def("kube_writer_stats",
            [](const Frontend& f) -> py::object {
              const KubeWriter* w = f.kube_writer();

@@ -8,6 +8,7 @@
 #include <openssl/err.h>
 #include <openssl/ssl.h>
 #include <openssl/x509v3.h>
+#include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
 #include <sys/time.h>
@@ -304,9 +305,9 @@ int HttpConn::request(const char* method, const std::string& path, const std::st
 
 // ------------------------------------------------------------------------------ KubeWriter
 KubeWriter::KubeWriter(KubeTarget target, std::shared_ptr<Ledger> ledger, Respond respond, int threads, int retries,
-                       bool record_events)
+                       bool record_events, bool evented)
     : t_(std::move(target)), ledger_(std::move(ledger)), respond_(std::move(respond)), retries_(retries),
-      events_(record_events) {
+      events_(record_events), evented_(evented) {
   if (t_.tls) {
     SSL_CTX* ctx = SSL_CTX_new(TLS_client_method());
     if (!ctx) throw std::runtime_error("KubeWriter: SSL_CTX_new failed");
@@ -335,6 +336,22 @@ KubeWriter::KubeWriter(KubeTarget target, std::shared_ptr<Ledger> ledger, Respon
   }
   token_checked_ = mono_s();
   if (threads < 1) threads = 1;
+  if (evented_) {
+    max_inflight_ = threads * kBatch;
+    efd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
+    if (efd_ < 0) throw std::runtime_error("KubeWriter: eventfd failed");
+    io_ = std::thread([this] {
+      pthread_setname_np(pthread_self(), "ngpu-wr-io");
+      io_loop();
+    });
+    // the slow path: retries with backoff, conflict checks, rollbacks (rare; blocking is fine)
+    for (int i = 0; i < 2; ++i)
+      threads_.emplace_back([this, i] {
+        pthread_setname_np(pthread_self(), ("ngpu-wr-slow" + std::to_string(i)).c_str());
+        run_slow();
+      });
+    return;
+  }
   for (int i = 0; i < threads; ++i)
     threads_.emplace_back([this, i] {
       pthread_setname_np(pthread_self(), ("ngpu-wr" + std::to_string(i)).c_str());
@@ -344,6 +361,7 @@ KubeWriter::KubeWriter(KubeTarget target, std::shared_ptr<Ledger> ledger, Respon
 
 KubeWriter::~KubeWriter() {
   stop();
+  if (efd_ >= 0) ::close(efd_);
   if (ctx_) SSL_CTX_free(static_cast<SSL_CTX*>(ctx_));
 }
 
@@ -360,6 +378,12 @@ void KubeWriter::stop() {
     stop_ = true;
   }
   cv_.notify_all();
+  if (io_.joinable()) {
+    // the io thread finishes what it has in flight (bounded), hands failures to the slow path
+    uint64_t one = 1;
+    (void)!::write(efd_, &one, sizeof one);
+    io_.join();
+  }
   for (auto& t : threads_)
     if (t.joinable()) t.join();
   std::deque<BindJob> left;
@@ -374,16 +398,25 @@ void KubeWriter::stop() {
 }
 
 void KubeWriter::submit(BindJob job) {
+  bool accepted = false, wake = false;
   {
     std::lock_guard<std::mutex> g(mu_);
     if (!stop_) {
       stats.inflight.fetch_add(1, std::memory_order_relaxed);
+      wake = q_.empty();   // evented: the io thread drains the whole queue per wake-up
       q_.push_back(std::move(job));
-      cv_.notify_one();
-      return;
+      accepted = true;
+      if (!evented_) cv_.notify_one();
     }
   }
-  refuse(job);   // a bind that arrives while the writer shuts down
+  if (!accepted) {
+    refuse(job);   // a bind that arrives while the writer shuts down
+    return;
+  }
+  if (evented_ && wake) {
+    uint64_t one = 1;
+    (void)!::write(efd_, &one, sizeof one);
+  }
 }
 
 std::string KubeWriter::auth() {

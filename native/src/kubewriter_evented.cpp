@@ -1,0 +1,512 @@
+// Evented bind writer (see kubewriter.h): one epoll thread drives the two API requests of every
+// bind in flight on non-blocking keep-alive connections, plain HTTP or TLS.
+//
+// Why: the threaded writer keeps a thread per batch of binds that blocks in recv() for each
+// answer; at the bench's 40 binds per millisecond with a fast API server that is one sleep and
+// one wake-up per request (~17 us of CPU per bind on the MI355X box, profiles/). Here one
+// epoll_wait returns every answer that arrived together.
+//
+// Scope: the happy path only. A bind whose binding and label PATCH both answer 2xx is committed
+// on this thread and answered. Every other outcome (transport failure after the one reconnect a
+// stale keep-alive connection gets, 5xx / 429 / 401 to retry, 409 to check, a rollback) goes,
+// with the answers received, to a slow-path thread running KubeWriter::finish, the same code the
+// threaded writer uses, so retry and rollback semantics are identical in both modes.
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <openssl/err.h>
+#include <openssl/ssl.h>
+#include <openssl/x509v3.h>
+#include <sys/epoll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <chrono>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <vector>
+
+#include "nanogpu/kubewriter.h"
+
+namespace nanogpu {
+
+namespace {
+
+constexpr const char* kMergePatchE = "application/merge-patch+json";
+constexpr const char* kJsonE = "application/json";
+
+uint64_t ns_now() {
+  return static_cast<uint64_t>(
+      std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count());
+}
+
+// One HTTP/1.1 response at the front of `b`: 1 = complete, 0 = need more, -1 = malformed.
+// `eof`: the peer closed (completes a response without a length).
+int parse_response(const std::string& b, bool eof, int* status, std::string* body, size_t* consumed, bool* close) {
+  const size_t he = b.find("\r\n\r\n");
+  if (he == std::string::npos) return b.size() > (256u << 10) ? -1 : 0;
+  if (he < 12 || b.compare(0, 5, "HTTP/") != 0) return -1;
+  *status = std::atoi(b.c_str() + 9);
+  long clen = -1;
+  bool chunked = false;
+  *close = false;
+  size_t p = b.find("\r\n");
+  while (p < he) {
+    const size_t e = b.find("\r\n", p + 2);
+    const size_t end = e == std::string::npos || e > he ? he : e;
+    const size_t colon = b.find(':', p + 2);
+    if (colon != std::string::npos && colon < end) {
+      std::string k = b.substr(p + 2, colon - p - 2);
+      for (char& ch : k) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
+      size_t v0 = colon + 1;
+      while (v0 < end && b[v0] == ' ') ++v0;
+      const std::string v = b.substr(v0, end - v0);
+      if (k == "content-length") clen = std::atol(v.c_str());
+      else if (k == "transfer-encoding" && v.find("chunked") != std::string::npos) chunked = true;
+      else if (k == "connection" && (v == "close" || v == "Close")) *close = true;
+    }
+    if (end == he) break;
+    p = end;
+  }
+  size_t q = he + 4;
+  if (chunked) {
+    body->clear();
+    for (;;) {
+      const size_t le = b.find("\r\n", q);
+      if (le == std::string::npos) return 0;
+      const size_t sz = std::strtoul(b.c_str() + q, nullptr, 16);
+      if (b.size() < le + 2 + sz + 2) return 0;
+      body->append(b, le + 2, sz);
+      q = le + 2 + sz + 2;
+      if (sz == 0) break;
+    }
+    *consumed = q;
+    return 1;
+  }
+  if (clen >= 0) {
+    if (b.size() < q + static_cast<size_t>(clen)) return 0;
+    body->assign(b, q, static_cast<size_t>(clen));
+    *consumed = q + static_cast<size_t>(clen);
+    return 1;
+  }
+  if (!eof) return 0;   // the body runs to the end of the connection
+  body->assign(b, q, std::string::npos);
+  *consumed = b.size();
+  *close = true;
+  return 1;
+}
+
+enum ConnState { kIdle, kConnecting, kHandshake, kSending, kReceiving };
+
+struct AConn {
+  int fd = -1;
+  SSL* ssl = nullptr;
+  int st = kIdle;
+  bool reused = false;   // the request went out on a connection used before
+  bool got_any = false;  // response bytes seen for the current request
+  bool retried = false;  // the one fresh-connection retry is spent
+  std::string out, in;
+  size_t off = 0;
+  int64_t job = -1;      // in-flight job slot
+  int which = 0;         // 0: label PATCH, 1: binding
+};
+
+struct AJob {
+  BindJob j;
+  std::string patch, binding, rp, rb;
+  int sp = 0, sb = 0;
+  int left = 2;
+};
+
+}  // namespace
+
+void KubeWriter::io_loop() {
+  const int ep = epoll_create1(EPOLL_CLOEXEC);
+  if (ep < 0) throw std::runtime_error("KubeWriter: epoll_create1 failed");
+  {
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.u64 = UINT64_MAX;
+    epoll_ctl(ep, EPOLL_CTL_ADD, efd_, &ev);
+  }
+  std::vector<std::unique_ptr<AConn>> conns;   // index = epoll tag
+  std::vector<size_t> idle;
+  std::vector<std::unique_ptr<AJob>> slots(static_cast<size_t>(max_inflight_));
+  std::vector<int64_t> free_slots;
+  for (int64_t i = max_inflight_ - 1; i >= 0; --i) free_slots.push_back(i);
+  std::deque<BindJob> waiting;
+  sockaddr_storage addr{};
+  socklen_t addr_len = 0;
+  int family = AF_INET;
+  std::string a = auth();
+  uint64_t auth_at = ns_now();
+
+  auto resolve = [&]() -> bool {
+    if (addr_len) return true;
+    addrinfo hints{};
+    hints.ai_family = AF_UNSPEC;
+    hints.ai_socktype = SOCK_STREAM;
+    addrinfo* res = nullptr;
+    if (getaddrinfo(t_.host.c_str(), std::to_string(t_.port).c_str(), &hints, &res) != 0 || !res) return false;
+    std::memcpy(&addr, res->ai_addr, res->ai_addrlen);
+    addr_len = res->ai_addrlen;
+    family = res->ai_family;
+    freeaddrinfo(res);
+    return true;
+  };
+  auto close_conn = [&](AConn& c) {
+    if (c.ssl) SSL_free(c.ssl);
+    c.ssl = nullptr;
+    if (c.fd >= 0) {
+      epoll_ctl(ep, EPOLL_CTL_DEL, c.fd, nullptr);
+      ::close(c.fd);
+    }
+    c.fd = -1;
+    c.in.clear();
+    c.st = kIdle;
+  };
+  // a fresh non-blocking connection (connect in progress); false: cannot even start
+  auto open_conn = [&](size_t k) -> bool {
+    AConn& c = *conns[k];
+    close_conn(c);
+    if (!resolve()) return false;
+    const int fd = socket(family, SOCK_STREAM | SOCK_CLOEXEC | SOCK_NONBLOCK, 0);
+    if (fd < 0) return false;
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    const int cr = ::connect(fd, reinterpret_cast<sockaddr*>(&addr), addr_len);
+    if (cr != 0 && errno != EINPROGRESS) {
+      ::close(fd);
+      return false;
+    }
+    c.fd = fd;
+    c.st = cr == 0 ? (ctx_ ? kHandshake : kSending) : kConnecting;
+    if (ctx_) {
+      c.ssl = SSL_new(static_cast<SSL_CTX*>(ctx_));
+      if (!c.ssl) {
+        close_conn(c);
+        return false;
+      }
+      SSL_set_fd(c.ssl, fd);
+      in6_addr a6{};
+      const bool ip = inet_pton(AF_INET, t_.host.c_str(), &a6) == 1 || inet_pton(AF_INET6, t_.host.c_str(), &a6) == 1;
+      if (!ip) SSL_set_tlsext_host_name(c.ssl, t_.host.c_str());
+      if (!t_.insecure) {
+        if (ip) X509_VERIFY_PARAM_set1_ip_asc(SSL_get0_param(c.ssl), t_.host.c_str());
+        else SSL_set1_host(c.ssl, t_.host.c_str());
+      }
+    }
+    epoll_event ev{};
+    ev.events = EPOLLIN | EPOLLOUT | EPOLLRDHUP | EPOLLET;
+    ev.data.u64 = k;
+    epoll_ctl(ep, EPOLL_CTL_ADD, fd, &ev);
+    return true;
+  };
+  auto request = [&](const char* method, const std::string& path, const std::string& ctype, const std::string& body) {
+    std::string r;
+    r.reserve(256 + body.size());
+    r += method;
+    r += ' ';
+    r += path;
+    r += " HTTP/1.1\r\nHost: ";
+    r += t_.host;
+    r += "\r\nUser-Agent: nano-gpu-scheduler-amd/0.1\r\nAccept: application/json\r\n";
+    if (!a.empty()) r += "Authorization: Bearer " + a + "\r\n";
+    r += "Content-Type: ";
+    r += ctype;
+    r += "\r\nContent-Length: " + std::to_string(body.size()) + "\r\n\r\n";
+    r += body;
+    return r;
+  };
+
+  size_t inflight = 0;
+  // both answers of a slot are in: commit on the happy path, else the slow path finishes it
+  auto complete = [&](int64_t s) {
+    std::unique_ptr<AJob> jb = std::move(slots[static_cast<size_t>(s)]);
+    free_slots.push_back(s);
+    --inflight;
+    const bool ok2 = [](int st) { return st >= 200 && st < 300; }(jb->sb) && jb->sp >= 200 && jb->sp < 300;
+    stats.binding_ns.fetch_add(ns_now() - jb->j.t0_ns, std::memory_order_relaxed);
+    if (ok2) {
+      ledger_->commit(jb->j.uid);
+      stats.ok.fetch_add(1, std::memory_order_relaxed);
+      stats.inflight.fetch_sub(1, std::memory_order_relaxed);
+      respond_(jb->j.id, 200, "{\"Error\":\"\"}");
+      return;
+    }
+    SlowJob sj;
+    sj.j = std::move(jb->j);
+    sj.patch = std::move(jb->patch);
+    sj.binding = std::move(jb->binding);
+    sj.rp = std::move(jb->rp);
+    sj.rb = std::move(jb->rb);
+    sj.sp = jb->sp;
+    sj.sb = jb->sb;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      slow_q_.push_back(std::move(sj));
+    }
+    cv_.notify_one();
+  };
+  auto deliver = [&](AConn& c, int status, std::string body) {
+    AJob& jb = *slots[static_cast<size_t>(c.job)];
+    (c.which ? jb.sb : jb.sp) = status;
+    (c.which ? jb.rb : jb.rp) = std::move(body);
+    const int64_t s = c.job;
+    c.job = -1;
+    if (--jb.left == 0) complete(s);
+  };
+  std::vector<size_t> kick;   // connections to drive after this batch of events
+  // a transport failure: one retry on a fresh connection when a reused keep-alive connection
+  // failed before any answer byte (the server closed it while idle), else status 0
+  auto fail = [&](size_t k, const char* why) {
+    AConn& c = *conns[k];
+    if (c.job >= 0 && c.reused && !c.got_any && !c.retried) {
+      c.retried = true;
+      c.reused = false;
+      c.off = 0;
+      if (open_conn(k)) {
+        kick.push_back(k);
+        return;
+      }
+    }
+    close_conn(c);
+    if (c.job >= 0) deliver(c, 0, why);
+    idle.push_back(k);
+  };
+
+  // drives connection k as far as it goes without blocking (`events`: the epoll events that
+  // woke it, 0 when kicked)
+  auto drive = [&](size_t k, uint32_t events) {
+    AConn& c = *conns[k];
+    char tmp[16384];
+    for (;;) {
+      if (c.fd < 0) return;
+      if (c.st == kConnecting) {
+        // a non-blocking connect is done when the socket turns writable (or errors)
+        if (!(events & (EPOLLOUT | EPOLLERR | EPOLLHUP))) return;
+        int err = 0;
+        socklen_t len = sizeof err;
+        if (getsockopt(c.fd, SOL_SOCKET, SO_ERROR, &err, &len) != 0 || err != 0)
+          return fail(k, "cannot connect to the API server");
+        c.st = c.ssl ? kHandshake : kSending;
+        continue;
+      }
+      if (c.st == kHandshake) {
+        const int r = SSL_connect(c.ssl);
+        if (r == 1) {
+          c.st = kSending;
+          continue;
+        }
+        const int e = SSL_get_error(c.ssl, r);
+        if (e == SSL_ERROR_WANT_READ || e == SSL_ERROR_WANT_WRITE) return;
+        return fail(k, "TLS handshake with the API server failed");
+      }
+      if (c.st == kSending) {
+        while (c.off < c.out.size()) {
+          long w;
+          if (c.ssl) {
+            const int r = SSL_write(c.ssl, c.out.data() + c.off, static_cast<int>(c.out.size() - c.off));
+            if (r <= 0) {
+              const int e = SSL_get_error(c.ssl, r);
+              if (e == SSL_ERROR_WANT_WRITE || e == SSL_ERROR_WANT_READ) return;
+              return fail(k, "connection to the API server failed");
+            }
+            w = r;
+          } else {
+            w = ::send(c.fd, c.out.data() + c.off, c.out.size() - c.off, MSG_NOSIGNAL);
+            if (w < 0 && errno == EINTR) continue;
+            if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) return;
+            if (w <= 0) return fail(k, "connection to the API server failed");
+          }
+          c.off += static_cast<size_t>(w);
+        }
+        c.st = kReceiving;
+        continue;
+      }
+      if (c.st == kReceiving || c.st == kIdle) {
+        bool eof = false;
+        for (;;) {
+          long r;
+          if (c.ssl) {
+            r = SSL_read(c.ssl, tmp, sizeof tmp);
+            if (r <= 0) {
+              const int e = SSL_get_error(c.ssl, static_cast<int>(r));
+              if (e == SSL_ERROR_WANT_READ || e == SSL_ERROR_WANT_WRITE) break;
+              eof = true;
+              break;
+            }
+          } else {
+            r = ::recv(c.fd, tmp, sizeof tmp, 0);
+            if (r < 0 && errno == EINTR) continue;
+            if (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
+            if (r <= 0) {
+              eof = true;
+              break;
+            }
+          }
+          c.in.append(tmp, static_cast<size_t>(r));
+          c.got_any = true;
+        }
+        if (c.st == kIdle) {   // an idle keep-alive connection the server closed (or junk)
+          if (eof || !c.in.empty()) close_conn(c);
+          return;
+        }
+        int status = 0;
+        std::string body;
+        size_t used = 0;
+        bool close = false;
+        const int rc = parse_response(c.in, eof, &status, &body, &used, &close);
+        if (rc < 0) return fail(k, "bad answer from the API server");
+        if (rc == 0) {
+          if (eof) return fail(k, "connection to the API server failed");
+          return;
+        }
+        c.in.erase(0, used);
+        if (close || eof) close_conn(c);
+        c.st = kIdle;
+        deliver(c, status, std::move(body));
+        idle.push_back(k);
+        return;
+      }
+      return;
+    }
+  };
+  // starts request `which` of slot s on an idle (or new) connection
+  auto launch = [&](int64_t s, int which) {
+    AJob& jb = *slots[static_cast<size_t>(s)];
+    size_t k;
+    if (!idle.empty()) {
+      k = idle.back();
+      idle.pop_back();
+    } else {
+      k = conns.size();
+      conns.push_back(std::make_unique<AConn>());
+    }
+    AConn& c = *conns[k];
+    const std::string base = "/api/v1/namespaces/" + jb.j.ns + "/pods/" + jb.j.name;
+    c.out = which ? request("POST", base + "/binding", kJsonE, jb.binding)
+                  : request("PATCH", base, kMergePatchE, jb.patch);
+    c.off = 0;
+    c.in.clear();
+    c.job = s;
+    c.which = which;
+    c.got_any = false;
+    c.retried = false;
+    c.reused = c.fd >= 0;
+    if (c.fd >= 0) {
+      c.st = kSending;
+    } else if (!open_conn(k)) {
+      close_conn(c);
+      deliver(c, 0, "cannot connect to " + t_.host + ":" + std::to_string(t_.port));
+      idle.push_back(k);
+      return;
+    }
+    kick.push_back(k);
+  };
+
+  epoll_event evs[256];
+  uint64_t stop_at = 0;
+  for (;;) {
+    bool stopping;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stopping = stop_;
+      if (!stopping)
+        while (!q_.empty()) {
+          waiting.push_back(std::move(q_.front()));
+          q_.pop_front();
+        }
+    }
+    if (stopping && !stop_at) stop_at = ns_now() + 5'000'000'000ull;
+    if (stopping) {
+      for (BindJob& j : waiting) {
+        refuse(j);
+        stats.inflight.fetch_sub(1, std::memory_order_relaxed);
+      }
+      waiting.clear();
+      if (inflight == 0 || ns_now() > stop_at) break;
+    }
+    if (ns_now() - auth_at > 1'000'000'000ull) {   // a rotated token reaches new requests
+      a = auth();
+      auth_at = ns_now();
+    }
+    while (!waiting.empty() && !free_slots.empty()) {
+      const int64_t s = free_slots.back();
+      free_slots.pop_back();
+      auto jb = std::make_unique<AJob>();
+      jb->j = std::move(waiting.front());
+      waiting.pop_front();
+      build(jb->j, &jb->patch, &jb->binding);
+      slots[static_cast<size_t>(s)] = std::move(jb);
+      ++inflight;
+      // the binding first: it is the one kube-scheduler's bind waits on
+      launch(s, 1);
+      if (slots[static_cast<size_t>(s)]) launch(s, 0);
+    }
+    for (size_t i = 0; i < kick.size(); ++i) drive(kick[i], 0);   // fail() may append
+    kick.clear();
+    const int n = epoll_wait(ep, evs, 256, stopping ? 10 : 1000);
+    for (int e = 0; e < n; ++e) {
+      if (evs[e].data.u64 == UINT64_MAX) {
+        uint64_t v;
+        (void)!::read(efd_, &v, sizeof v);
+        continue;
+      }
+      const size_t k = evs[e].data.u64;
+      if (k < conns.size()) drive(k, evs[e].events);
+    }
+    for (size_t i = 0; i < kick.size(); ++i) drive(kick[i], 0);
+    kick.clear();
+  }
+  // what is still in flight after the grace period: the slow path answers it
+  for (auto& c : conns) close_conn(*c);
+  for (size_t s = 0; s < slots.size(); ++s) {
+    if (!slots[s]) continue;
+    AJob& jb = *slots[s];
+    if (jb.left > 0) {
+      if (jb.sb == 0) jb.rb = "extender shutting down";
+      if (jb.sp == 0) jb.rp = "extender shutting down";
+    }
+    SlowJob sj;
+    sj.j = std::move(jb.j);
+    sj.patch = std::move(jb.patch);
+    sj.binding = std::move(jb.binding);
+    sj.rp = std::move(jb.rp);
+    sj.rb = std::move(jb.rb);
+    sj.sp = jb.sp;
+    sj.sb = jb.sb;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      slow_q_.push_back(std::move(sj));
+    }
+    slots[s].reset();
+  }
+  io_done_.store(true);
+  {
+    std::lock_guard<std::mutex> g(mu_);   // the slow threads re-check under mu_
+  }
+  cv_.notify_all();
+  ::close(ep);
+}
+
+void KubeWriter::run_slow() {
+  HttpConn c(&t_, ctx_), c2(&t_, ctx_);
+  for (;;) {
+    SlowJob sj;
+    {
+      std::unique_lock<std::mutex> g(mu_);
+      cv_.wait(g, [this] { return !slow_q_.empty() || (stop_ && io_done_.load()); });
+      if (slow_q_.empty()) return;
+      sj = std::move(slow_q_.front());
+      slow_q_.pop_front();
+    }
+    finish(&c, &c2, sj.j, sj.patch, sj.binding, sj.sp, &sj.rp, sj.sb, &sj.rb);
+    stats.inflight.fetch_sub(1, std::memory_order_relaxed);
+  }
+}
+
+}  // namespace nanogpu

@@ -216,7 +216,7 @@ static void relist_gap(int iters) {
 }
 
 // Native API server + native bind writers under concurrency (see the header comment).
-static void apiserver_and_writers(int pods) {
+static void apiserver_and_writers(int pods, bool evented) {
   apisrv::Config cfg;
   cfg.threads = 2;
   apisrv::Server srv(cfg);
@@ -285,7 +285,7 @@ static void apiserver_and_writers(int pods) {
           if (status == 200 && body == "{\"Error\":\"\"}") ok.fetch_add(1);
           else bad.fetch_add(1);
         },
-        4, 2, false);
+        4, 2, false, evented);
     std::vector<std::thread> patchers;
     for (int t2 = 0; t2 < 2; ++t2)
       patchers.emplace_back([&, t2] {
@@ -461,7 +461,8 @@ int main(int argc, char** argv) {
               reserved.load(), static_cast<unsigned long long>(st));
   ledger.reset();
   unlink(path.c_str());
-  apiserver_and_writers(std::max(50, iters / 20));
+  apiserver_and_writers(std::max(50, iters / 20), true);    // one epoll writer thread
+  apiserver_and_writers(std::max(50, iters / 20), false);   // blocking writer threads
   relist_gap(std::max(200, iters / 4));
   return 0;
 }

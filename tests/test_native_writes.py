@@ -18,10 +18,12 @@ from nanogpu.k8s.fake_apiserver import Faults, FakeKubeStore, serve
 from nanogpu.topology.model import synthetic_mi355x
 
 
-async def _stack(store, native: bool):
+async def _stack(store, native):
+    """native: "evented" / "threads" (the C++ writer in that mode) or False (Python writes)."""
     runner, port = await serve(store)
     rt = Runtime(Config(kube_api=f"http://127.0.0.1:{port}", port=0, host="127.0.0.1",
-                        policy_config_path="/nonexistent", native_bind_writes=native))
+                        policy_config_path="/nonexistent", native_bind_writes=bool(native),
+                        bind_writer_mode=native or "evented"))
     await rt.start()
     return runner, rt
 
@@ -43,7 +45,7 @@ async def _metrics(base):
             return await r.text()
 
 
-@pytest.mark.parametrize("native", [True, False])
+@pytest.mark.parametrize("native", ["evented", "threads", False])
 def test_bind_writes_retry_transient_errors(native):
     async def main():
         store = FakeKubeStore(faults=Faults(patch_error_rate=0.3, bind_error_rate=0.3, seed=11))
@@ -71,7 +73,7 @@ def test_bind_writes_retry_transient_errors(native):
     asyncio.run(main())
 
 
-@pytest.mark.parametrize("native", [True, False])
+@pytest.mark.parametrize("native", ["evented", "threads", False])
 def test_failed_binding_rolls_back_and_unannotates(native):
     async def main():
         store = FakeKubeStore(faults=Faults(bind_error_rate=1.0))
@@ -103,7 +105,7 @@ def test_failed_binding_rolls_back_and_unannotates(native):
     asyncio.run(main())
 
 
-@pytest.mark.parametrize("native", [True, False])
+@pytest.mark.parametrize("native", ["evented", "threads", False])
 def test_binding_conflict_on_the_same_node_is_success(native):
     """A retried binding POST whose first attempt landed answers 409; the pod already sits on
     the requested node, so the bind succeeded."""
@@ -134,7 +136,8 @@ def test_binding_conflict_on_the_same_node_is_success(native):
     asyncio.run(main())
 
 
-def test_native_writer_speaks_tls_with_a_bearer_token(tmp_path):
+@pytest.mark.parametrize("mode", ["evented", "threads"])
+def test_native_writer_speaks_tls_with_a_bearer_token(tmp_path, mode):
     """https + token (how an in-cluster extender reaches kube-apiserver): a TLS proxy with a
     self-signed certificate in front of the fake API server checks the Authorization header.
     The certificate names the server the way kube-apiserver's does (CN kube-apiserver, the
@@ -183,7 +186,8 @@ def test_native_writer_speaks_tls_with_a_bearer_token(tmp_path):
 
         api = KubeClient(KubeConfig(server=f"https://127.0.0.1:{port}", ca_file=str(crt), token_file=str(tok),
                                     token="s3cret"))
-        rt = Runtime(Config(port=0, host="127.0.0.1", policy_config_path="/nonexistent"), api=api)
+        rt = Runtime(Config(port=0, host="127.0.0.1", policy_config_path="/nonexistent", bind_writer_mode=mode),
+                     api=api)
         await rt.start()
         try:
             assert rt.native.fe.kube_writer_stats() is not None
