@@ -115,15 +115,23 @@ def ring_busbw(dist, device, nbytes: int = 256 << 20, iters: int = 5) -> float:
     import torch
 
     n = dist.get_world_size()
-    buf = torch.ones(nbytes // 2, dtype=torch.bfloat16, device=device)
+    dev = torch.device(device)
+    # gloo (the CPU rehearsal) reduces float32; RCCL moves bf16, as a training job would
+    buf = torch.ones(nbytes // 2, dtype=torch.bfloat16 if dev.type == "cuda" else torch.float32, device=dev)
+    nbytes = buf.numel() * buf.element_size()
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
     dist.all_reduce(buf)   # warm-up (communicator setup)
-    torch.cuda.synchronize(device)
+    sync()
     t0 = time.perf_counter()
     for _ in range(iters):
         dist.all_reduce(buf)
-    torch.cuda.synchronize(device)
+    sync()
     dt = (time.perf_counter() - t0) / iters
-    t = torch.tensor([dt], dtype=torch.float64, device=device)
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return 2.0 * (n - 1) / n * nbytes / float(t.item()) / 1e9
 

@@ -70,3 +70,36 @@ def test_link_matrix_rounds_are_permutations_and_rows_gather(world):
 def test_a_failed_pair_fails_every_rank_without_a_hang():
     out = _run(2, fail_pair=(1, 0))
     assert [status for _, status, _, _ in out] == ["error", "error"]
+
+
+def _busbw_rank(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from nanogpu.probe.calibrate import ring_busbw
+
+    try:
+        q.put((rank, "ok", ring_busbw(dist, "cpu", nbytes=4 << 20, iters=2)))
+    except Exception as e:   # noqa: BLE001 - reported to the test
+        q.put((rank, "error", f"{type(e).__name__}: {e}"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ring_busbw_runs_on_the_cpu_rehearsal(world):
+    """The bench's N-GPU collective figure (RCCL all-reduce busBW) must not be able to abort a
+    driver run: the same code runs over gloo on the CPU, and every rank reports one number."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_busbw_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+    assert all(st == "ok" for _, st, _ in out), out
+    vals = {round(v, 6) for _, _, v in out}
+    assert len(vals) == 1 and next(iter(vals)) > 0      # the max over ranks, the same everywhere
