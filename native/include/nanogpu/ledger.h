@@ -112,6 +112,10 @@ struct LedgerHeader {
   std::atomic<int32_t> attached;    // processes attached
   pthread_mutex_t registry_mu;
   alignas(64) std::atomic<uint64_t> epoch;      // bumps on every mutation anywhere
+  // bumps when a node slot is created or removed: what caches of node ids (the front door's
+  // name -> id lists, assume_many's score memo) must re-check; every other change is visible
+  // through the node's own generation
+  std::atomic<uint64_t> node_epoch;
   // 1 while this replica may schedule: the worker running the leader elector writes it, every
   // worker (front door, Python router, /readyz) reads it. 1 without leader election.
   std::atomic<int32_t> serving;
@@ -187,6 +191,7 @@ class Ledger {
   std::vector<CachedPlan> cached_plans(int32_t id) const;
   uint64_t generation(int32_t id) const;
   uint64_t epoch() const { return hdr_->epoch.load(std::memory_order_acquire); }
+  uint64_t node_epoch() const { return hdr_->node_epoch.load(std::memory_order_acquire); }
   bool serving() const { return hdr_->serving.load(std::memory_order_acquire) != 0; }
   // Score lead over the runner-up a top node needs before priorities nominate it. Starts at
   // 0 (any unique top node); each nomination a bind moves elsewhere raises it by 2 (to 40),

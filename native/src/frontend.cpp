@@ -887,96 +887,129 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
       if (!other.parse(top.raw(c))) return false;
     }
   }
+  // priorities follows its cycle's filter with the same Pod text on the same connection, so
+  // on the same worker: the pod this thread parsed last is reused when the text is identical
+  // (demand, identity, containers); only the learned-owner flag is read again (below)
+  struct LastPod {
+    std::string raw, uid;
+    Demand dem{};
+    CachedPod cached;
+    bool mb_annotated = false;
+    bool valid = false;
+  };
+  thread_local LastPod last;
   int32_t pod = -1;
-  if (pod_top >= 0 && !top.is(pod_top, json::Type::kNull)) {
-    if (!top.is(pod_top, json::Type::kObj) || !d.parse(top.raw(pod_top))) return false;
-    pod = d.root();
-  }
   Demand dem;
   std::memset(&dem, 0, sizeof(dem));
   std::string_view uid;
   CachedPod cached;
-  if (pod >= 0 && !d.is(pod, json::Type::kNull)) {
-    if (!d.is(pod, json::Type::kObj)) return false;
-    const int32_t md = d.get(pod, "metadata");
-    if (md >= 0 && !d.is(md, json::Type::kNull)) {
-      if (!d.is(md, json::Type::kObj)) return false;
-      const int32_t u = d.get(md, "uid");
-      if (u >= 0) {
-        if (!d.is(u, json::Type::kStr)) return false;
-        uid = d.str(u);
-      }
-      const int32_t nm = d.get(md, "name"), ns = d.get(md, "namespace"), del = d.get(md, "deletionTimestamp");
-      if (d.is(nm, json::Type::kStr)) cached.name = std::string(d.str(nm));
-      cached.ns = d.is(ns, json::Type::kStr) ? std::string(d.str(ns)) : std::string("default");
-      if (del >= 0 && !d.is(del, json::Type::kNull) && !(d.is(del, json::Type::kStr) && d.str(del).empty()))
-        cached.completed = true;
+  bool mb_annotated = false;
+  const bool has_pod_text = pod_top >= 0 && !top.is(pod_top, json::Type::kNull);
+  const bool reused = has_pod_text && last.valid && top.is(pod_top, json::Type::kObj) && top.raw(pod_top) == last.raw;
+  if (reused) {
+    dem = last.dem;
+    uid = last.uid;
+    mb_annotated = last.mb_annotated;
+  } else {
+    if (has_pod_text) {
+      if (!top.is(pod_top, json::Type::kObj) || !d.parse(top.raw(pod_top))) return false;
+      pod = d.root();
     }
-    const int32_t stt = d.get(pod, "status");
-    if (d.is(stt, json::Type::kObj)) {
-      const int32_t ph = d.get(stt, "phase");
-      if (d.is(ph, json::Type::kStr) && (d.str(ph) == "Succeeded" || d.str(ph) == "Failed")) cached.completed = true;
-    }
-    const int32_t spec = d.get(pod, "spec");
-    int32_t cons = -1;
-    if (spec >= 0 && !d.is(spec, json::Type::kNull)) {
-      if (!d.is(spec, json::Type::kObj)) return false;
-      cons = d.get(spec, "containers");
-    }
-    if (cons >= 0 && !d.is(cons, json::Type::kNull)) {
-      if (!d.is(cons, json::Type::kArr)) return false;
-      if (d.at(cons).count > kMaxContainers) return false;
-      for (int32_t c = d.at(cons).first; c >= 0; c = d.at(c).next) {
-        if (!d.is(c, json::Type::kObj)) return false;
-        ContainerDemand& cd = dem.c[dem.n++];
-        const int32_t cn = d.get(c, "name");
-        cached.containers.emplace_back(d.is(cn, json::Type::kStr) ? std::string(d.str(cn)) : std::string());
-        const int32_t res = d.get(c, "resources");
-        int32_t lim = -1;
-        if (res >= 0 && !d.is(res, json::Type::kNull)) {
-          if (!d.is(res, json::Type::kObj)) return false;
-          lim = d.get(res, "limits");
+    if (pod >= 0 && !d.is(pod, json::Type::kNull)) {
+      if (!d.is(pod, json::Type::kObj)) return false;
+      const int32_t md = d.get(pod, "metadata");
+      if (md >= 0 && !d.is(md, json::Type::kNull)) {
+        if (!d.is(md, json::Type::kObj)) return false;
+        const int32_t u = d.get(md, "uid");
+        if (u >= 0) {
+          if (!d.is(u, json::Type::kStr)) return false;
+          uid = d.str(u);
         }
-        if (lim >= 0 && !d.is(lim, json::Type::kNull)) {
-          if (!d.is(lim, json::Type::kObj)) return false;
-          for (int k = 0; k < 2; ++k) {
-            const int32_t q = d.get(lim, k == 0 ? kPercent : kMemory);
-            if (q < 0 || d.is(q, json::Type::kNull)) continue;
-            if (!d.is(q, json::Type::kStr) && !d.is(q, json::Type::kNum)) return false;
-            int64_t v;
-            if (!quantity_value(d.str(q), k == 1, &v)) return false;  // Python logs + treats as 0
-            if (k == 0) {
-              if (v > INT32_MAX) return false;
-              cd.pct = static_cast<int32_t>(v);
-            } else {
-              cd.mib = v;
+        const int32_t nm = d.get(md, "name"), ns = d.get(md, "namespace"), del = d.get(md, "deletionTimestamp");
+        if (d.is(nm, json::Type::kStr)) cached.name = std::string(d.str(nm));
+        cached.ns = d.is(ns, json::Type::kStr) ? std::string(d.str(ns)) : std::string("default");
+        if (del >= 0 && !d.is(del, json::Type::kNull) && !(d.is(del, json::Type::kStr) && d.str(del).empty()))
+          cached.completed = true;
+      }
+      const int32_t stt = d.get(pod, "status");
+      if (d.is(stt, json::Type::kObj)) {
+        const int32_t ph = d.get(stt, "phase");
+        if (d.is(ph, json::Type::kStr) && (d.str(ph) == "Succeeded" || d.str(ph) == "Failed")) cached.completed = true;
+      }
+      const int32_t spec = d.get(pod, "spec");
+      int32_t cons = -1;
+      if (spec >= 0 && !d.is(spec, json::Type::kNull)) {
+        if (!d.is(spec, json::Type::kObj)) return false;
+        cons = d.get(spec, "containers");
+      }
+      if (cons >= 0 && !d.is(cons, json::Type::kNull)) {
+        if (!d.is(cons, json::Type::kArr)) return false;
+        if (d.at(cons).count > kMaxContainers) return false;
+        for (int32_t c = d.at(cons).first; c >= 0; c = d.at(c).next) {
+          if (!d.is(c, json::Type::kObj)) return false;
+          ContainerDemand& cd = dem.c[dem.n++];
+          const int32_t cn = d.get(c, "name");
+          cached.containers.emplace_back(d.is(cn, json::Type::kStr) ? std::string(d.str(cn)) : std::string());
+          const int32_t res = d.get(c, "resources");
+          int32_t lim = -1;
+          if (res >= 0 && !d.is(res, json::Type::kNull)) {
+            if (!d.is(res, json::Type::kObj)) return false;
+            lim = d.get(res, "limits");
+          }
+          if (lim >= 0 && !d.is(lim, json::Type::kNull)) {
+            if (!d.is(lim, json::Type::kObj)) return false;
+            for (int k = 0; k < 2; ++k) {
+              const int32_t q = d.get(lim, k == 0 ? kPercent : kMemory);
+              if (q < 0 || d.is(q, json::Type::kNull)) continue;
+              if (!d.is(q, json::Type::kStr) && !d.is(q, json::Type::kNum)) return false;
+              int64_t v;
+              if (!quantity_value(d.str(q), k == 1, &v)) return false;  // Python logs + treats as 0
+              if (k == 0) {
+                if (v > INT32_MAX) return false;
+                cd.pct = static_cast<int32_t>(v);
+              } else {
+                cd.mib = v;
+              }
             }
           }
         }
       }
     }
+    // nano-gpu/memory-bound: "true" (every container) or a comma list of container names. With
+    // no annotation, a pod whose controlling owner was measured streaming (Ledger stream owners,
+    // nanogpu.telemetry.poller.OwnerLearner) counts as memory-bound; "false" opts out.
+    if (pod >= 0 && d.is(pod, json::Type::kObj)) {
+      const int32_t md = d.get(pod, "metadata");
+      const int32_t ann = d.is(md, json::Type::kObj) ? d.get(md, "annotations") : -1;
+      const int32_t mb = d.is(ann, json::Type::kObj) ? d.get(ann, kMemBoundAnnotation) : -1;
+      if (d.is(mb, json::Type::kStr)) {
+        const std::string_view v = d.str(mb);
+        for (int c = 0; c < dem.n; ++c)
+          if (v == "true" || list_has(v, cached.containers[c])) dem.c[c].flags |= kFlagMemBound;
+      }
+      if (d.is(md, json::Type::kObj)) {
+        const std::string_view owner = controller_uid(d, d.get(md, "ownerReferences"));
+        if (!owner.empty()) cached.owner = owner_hash(owner);
+      }
+      mb_annotated = d.is(mb, json::Type::kStr);
+    }
+    if (pod >= 0 && !uid.empty()) {
+      last.raw.assign(top.raw(pod_top));
+      last.uid.assign(uid);
+      last.dem = dem;
+      last.cached = cached;
+      last.mb_annotated = mb_annotated;
+      last.valid = true;
+    }
   }
-  // nano-gpu/memory-bound: "true" (every container) or a comma list of container names. With
-  // no annotation, a pod whose controlling owner was measured streaming (Ledger stream owners,
-  // nanogpu.telemetry.poller.OwnerLearner) counts as memory-bound; "false" opts out.
-  if (pod >= 0 && d.is(pod, json::Type::kObj)) {
-    const int32_t md = d.get(pod, "metadata");
-    const int32_t ann = d.is(md, json::Type::kObj) ? d.get(md, "annotations") : -1;
-    const int32_t mb = d.is(ann, json::Type::kObj) ? d.get(ann, kMemBoundAnnotation) : -1;
-    if (d.is(mb, json::Type::kStr)) {
-      const std::string_view v = d.str(mb);
-      for (int c = 0; c < dem.n; ++c)
-        if (v == "true" || list_has(v, cached.containers[c])) dem.c[c].flags |= kFlagMemBound;
-    }
-    if (d.is(md, json::Type::kObj)) {
-      const std::string_view owner = controller_uid(d, d.get(md, "ownerReferences"));
-      if (!owner.empty()) cached.owner = owner_hash(owner);
-    }
-    // Read per request, not memoised per pod: a learning pass between a pod's priorities and
-    // its bind can change the flag. The bind then adopts the priorities-time nomination, whose
-    // plan and demand the ledger keeps (Ledger::reserve), so the pod lands where it was scored
-    // (tests/test_frontend.py::test_owner_learned_between_priorities_and_bind_is_tolerated).
-    if (!d.is(mb, json::Type::kStr) && cached.owner && ledger_->is_stream_owner(cached.owner))
+  // A learned streaming owner marks an unannotated pod memory-bound. Read per request, not
+  // memoised per pod: a learning pass between a pod's priorities and its bind can change the
+  // flag. The bind then adopts the priorities-time nomination, whose plan and demand the ledger
+  // keeps (Ledger::reserve), so the pod lands where it was scored
+  // (tests/test_frontend.py::test_owner_learned_between_priorities_and_bind_is_tolerated).
+  {
+    const uint64_t owner = reused ? last.cached.owner : cached.owner;
+    if (!mb_annotated && owner && ledger_->is_stream_owner(owner))
       for (int c = 0; c < dem.n; ++c) dem.c[c].flags |= kFlagMemBound;
   }
   // node ids: any unknown node goes to Python, which can register it from its informer.
@@ -999,7 +1032,7 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   thread_local IdCache idc;
   if (idc.owner != ledger_.get()) idc = IdCache{}, idc.owner = ledger_.get();
   const uint64_t nkey = text_hash(raw_names) | 1;   // 0 marks an empty slot
-  const uint64_t epoch = ledger_->epoch();
+  const uint64_t epoch = ledger_->node_epoch();
   int slot = -1;
   for (int k = 0; k < 4; ++k)
     if (idc.key[k] == nkey && idc.len[k] == raw_names.size()) slot = k;
@@ -1066,15 +1099,16 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     nominate = nominate_;
   }
   if (nominate && !uid.empty()) ledger_->drop_nomination(std::string(uid));   // not against itself
-  if (pod >= 0 && !uid.empty() && !(prioritize && has_pod(uid))) {
+  if ((pod >= 0 || reused) && !uid.empty() && !(prioritize && has_pod(uid))) {
     // filter caches the pod for its bind; priorities of the same cycle find it there
-    cached.raw.assign(d.raw(pod));
-    cached.demand = dem;
-    put_pod(uid, std::move(cached));
+    CachedPod cp = reused ? last.cached : std::move(cached);
+    cp.raw.assign(reused ? std::string_view(last.raw) : d.raw(pod));
+    cp.demand = dem;
+    put_pod(uid, std::move(cp));
   }
   Plan p;
   std::string& r = *out;
-  r.reserve(64 + 48 * static_cast<size_t>(nn));
+  r.reserve(64 + 128 * static_cast<size_t>(nn));   // room for a FailedNodes entry per node
   if (!prioritize) {
     rcs.resize(ids.size());
     scores.resize(ids.size());
@@ -1094,19 +1128,39 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     }
     r += "],\"FailedNodes\":{";
     if (any_failed) {
-      std::string dstr;
+      // "can't allocate <demand> on node <name>: <reason>" per failing node, written in place:
+      // the demand text, the reasons (alloc.cpp err_str) and an escape-free name (its request
+      // token is the name in quotes) need no escaping
+      thread_local std::string dstr;
+      dstr.clear();
+      char num[24];
       for (int i = 0; i < dem.n; ++i) {
-        dstr += "(" + std::to_string(dem.c[i].pct);
-        if (dem.c[i].mib) dstr += "," + std::to_string(dem.c[i].mib) + "Mi";
-        dstr += ")";
+        dstr += '(';
+        dstr.append(num, static_cast<size_t>(std::to_chars(num, num + sizeof num, dem.c[i].pct).ptr - num));
+        if (dem.c[i].mib) {
+          dstr += ',';
+          dstr.append(num, static_cast<size_t>(std::to_chars(num, num + sizeof num, dem.c[i].mib).ptr - num));
+          dstr += "Mi";
+        }
+        dstr += ')';
       }
       first = true;
       for (size_t i = 0; i < ids.size(); ++i) {
         if (rcs[i] == kOk) continue;
         if (!first) r += ',';
         r += nraw[i];
-        r += ':';
-        json::append_quoted(&r, "can't allocate " + dstr + " on node " + std::string(nv[i]) + ": " + err_str(rcs[i]));
+        if (nraw[i].size() == nv[i].size() + 2) {
+          r += ":\"can't allocate ";
+          r += dstr;
+          r += " on node ";
+          r += nv[i];
+          r += ": ";
+          r += err_str(rcs[i]);
+          r += '"';
+        } else {
+          r += ':';
+          json::append_quoted(&r, "can't allocate " + dstr + " on node " + std::string(nv[i]) + ": " + err_str(rcs[i]));
+        }
         first = false;
       }
     }

@@ -19,7 +19,7 @@
 namespace nanogpu {
 
 static constexpr uint64_t kMagic = 0x4e414e4f47505531ULL;  // "NANOGPU1"
-static constexpr uint32_t kVersion = 10;  // 4: HBM pools; 5: cache lines; 6: sizes; 7: serving; 8: nominations; 9: stream owners; 10: overflow records
+static constexpr uint32_t kVersion = 11;  // 4: HBM pools; 5: cache lines; 6: sizes; 7: serving; 8: nominations; 9: stream owners; 10: overflow records; 11: node epoch
 
 static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -147,6 +147,7 @@ Ledger::Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, b
     hdr_->pods_per_shard = pods_per_shard_for(max_pods);
     hdr_->n_nodes.store(0);
     hdr_->epoch.store(1);
+    hdr_->node_epoch.store(1);
     hdr_->serving.store(1);
     hdr_->nom_made.store(0);
     hdr_->nom_adopted.store(0);
@@ -368,6 +369,7 @@ int32_t Ledger::upsert_node(const std::string& name, const Device* devs, int n,
     }
     s.in_use = 1;
     hdr_->n_nodes.store(count + 1, std::memory_order_release);
+    hdr_->node_epoch.fetch_add(1, std::memory_order_release);
   } else {
     NodeSlot& s = nodes_[id];
     lock_node(&s);
@@ -445,6 +447,7 @@ bool Ledger::remove_node(int32_t id) {
   n->in_use = 0;
   n->generation.fetch_add(1);
   hdr_->epoch.fetch_add(1);
+  hdr_->node_epoch.fetch_add(1, std::memory_order_release);
   std::lock_guard<std::mutex> g(names_mu_);
   names_.erase(n->name);
   return true;
@@ -595,7 +598,8 @@ namespace {
 // indexed by node id, valid while the node's generation is the one it was computed at. A
 // filter or priorities request over 64 nodes then reads 64 generations and 64 contiguous
 // entries instead of probing 64 separately allocated plan-cache tables (~100 ns a node).
-// Any node added or removed (the ledger's epoch) clears it.
+// Any node added or removed (the ledger's node epoch) clears it; every other change shows in the
+// node's generation, which each entry carries.
 struct ScoreMemo {
   const void* owner = nullptr;
   uint64_t dh = 0, oh = 0, epoch = 0, used = 0;
@@ -638,7 +642,7 @@ void Ledger::assume_many(const int32_t* ids, int count, const Demand& d, const O
   const Options o = resolve(o_in, d);
   const uint64_t dh = d.hash(), oh = o.hash();
   const int32_t n_nodes = hdr_->n_nodes.load(std::memory_order_acquire);
-  ScoreMemo& memo = memo_for(this, dh, oh, hdr_->epoch.load(std::memory_order_acquire),
+  ScoreMemo& memo = memo_for(this, dh, oh, hdr_->node_epoch.load(std::memory_order_acquire),
                              static_cast<uint32_t>(std::max(0, n_nodes)));
   Plan plan;
   for (int i = 0; i < count; ++i) {
