@@ -1080,13 +1080,34 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   // name index) only when a node was added or removed since (the ledger's epoch moved).
   std::vector<int32_t>& ids = idc.ids[slot];
   if (idc.epoch[slot] != epoch) {
+    // names this worker resolved before, by a hash of the name (no string, no lock): with
+    // kube-scheduler's node sampling the list is a different window of the cluster every
+    // cycle, so the per-list cache above misses while every name in it is known
+    struct NameIds {
+      const Ledger* owner = nullptr;
+      uint64_t epoch = 0;
+      std::unordered_map<uint64_t, int32_t> by_hash;
+    };
+    thread_local NameIds nid;
+    if (nid.owner != ledger_.get() || nid.epoch != epoch) {
+      nid.by_hash.clear();
+      nid.owner = ledger_.get();
+      nid.epoch = epoch;
+    }
     for (size_t i = 0; i < nv.size(); ++i) {
       if (ids[i] >= 0 && ledger_->node_named(ids[i], nv[i])) continue;
+      const uint64_t h = text_hash(nv[i]);
+      auto it = nid.by_hash.find(h);
+      if (it != nid.by_hash.end() && ledger_->node_named(it->second, nv[i])) {
+        ids[i] = it->second;
+        continue;
+      }
       ids[i] = ledger_->find_node(std::string(nv[i]));
       if (ids[i] < 0) {
         idc.key[slot] = 0;
         return false;
       }
+      nid.by_hash[h] = ids[i];
     }
     idc.epoch[slot] = epoch;
   }
