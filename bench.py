@@ -1356,7 +1356,8 @@ def nodes_variant_keys(args, topo, v) -> dict:
             f"pods_per_burst_{tag}": n_args.pods,
             f"nomination_adopt_pct_{tag}": round(100.0 * nom["adopted"] / nom["made"], 2) if nom.get("made") else None,
             f"nominations_{tag}": nom,
-            f"nodes_sent_per_filter_{tag}": res.get("nodes_sent_per_filter")}
+            f"nodes_sent_per_filter_{tag}": res.get("nodes_sent_per_filter"),
+            f"native_verb_mean_us_{tag}": res.get("native")}
     if args.partition == "SPX" and args.policy == "binpack" and not args.compat:
         from nanogpu.sim import fragsim
 
