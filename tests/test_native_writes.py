@@ -202,3 +202,60 @@ def test_native_writer_speaks_tls_with_a_bearer_token(tmp_path, mode):
             await runner.cleanup()
 
     asyncio.run(main())
+
+
+@pytest.mark.parametrize("mode", ["evented", "threads"])
+def test_stop_with_binds_in_flight_answers_every_bind_and_leaves_the_ledger_clean(mode):
+    """A bind is in flight to a slow API server (0.3 s per answer) when the extender stops:
+    the writer finishes what it holds within its grace period, kube-scheduler gets an answer
+    for every bind, and no reservation is left behind (each pod is committed or rolled back)."""
+    from nanogpu import _native as NN
+
+    async def main():
+        srv = NN.ApiServer("127.0.0.1", 0, 2, 4096)
+        n0 = pu.make_node("n0", 8, synthetic_mi355x(8).to_json())
+        st, _ = srv.call("POST", "/api/v1/nodes", json.dumps(n0))
+        assert st in (200, 201)
+        url = f"http://127.0.0.1:{srv.port}"
+        rt = Runtime(Config(kube_api=url, port=0, host="127.0.0.1", policy_config_path="/nonexistent",
+                            bind_writer_mode=mode))
+        await rt.start()
+        base = f"http://127.0.0.1:{rt.bound_port}"
+        pods = []
+        for i in range(6):
+            p = pu.make_pod(f"s{i}", [("main", 10)])
+            st, _ = srv.call("POST", "/api/v1/namespaces/default/pods", json.dumps(p))
+            assert st == 201
+            pods.append(p)
+        srv.set_latency(0.3)
+        answers = []
+
+        async def bind(p):
+            m = pu.meta(p)
+            async with aiohttp.ClientSession() as s:
+                try:
+                    async with s.post(f"{base}/scheduler/bind", json={
+                            "PodName": m["name"], "PodNamespace": "default", "PodUID": m["uid"], "Node": "n0"},
+                            timeout=aiohttp.ClientTimeout(total=20)) as r:
+                        answers.append((r.status, await r.json()))
+                except Exception as e:   # noqa: BLE001
+                    answers.append((0, {"Error": repr(e)}))
+
+        tasks = [asyncio.ensure_future(bind(p)) for p in pods]
+        await asyncio.sleep(0.15)              # the writes are out, their answers not back yet
+        stopping = asyncio.ensure_future(rt.stop())
+        await asyncio.gather(*tasks)
+        await stopping
+        try:
+            assert len(answers) == len(pods)
+            assert all(st in (200, 500) for st, _ in answers), answers
+            led = rt.state.ledger
+            for p in pods:
+                rec = led.lookup(pu.pod_uid(p))
+                assert rec is None or rec["state"] == "committed", rec   # no reservation left
+            committed = sum(1 for p in pods if led.lookup(pu.pod_uid(p)) is not None)
+            assert committed == sum(1 for st, a in answers if st == 200 and a["Error"] == "")
+        finally:
+            srv.stop()
+
+    asyncio.run(main())
