@@ -103,6 +103,9 @@ def parse_args():
     ap.add_argument("--inflight-binds", type=int, default=64)
     ap.add_argument("--bind-writer-mode", choices=["evented", "threads"], default="evented",
                     help="the extender's native bind writer: one epoll thread, or blocking threads")
+    ap.add_argument("--no-native-pod-watch", action="store_true",
+                    help="the extender reads its pod watch with aiohttp on the event loop (A/B of the "
+                         "native watch thread)")
     ap.add_argument("--no-overlap-create", action="store_true",
                     help="create the next burst only after this one is released (by default the "
                          "workload's clients create it while the pod controller releases)")
@@ -720,7 +723,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         url = d.bcast_obj(url)
         from nanogpu.k8s.client import KubeClient, KubeConfig
 
-        rt_api = KubeClient(KubeConfig(server=url), pool=args.inflight_binds + 8)
+        rt_api = KubeClient(KubeConfig(server=url), pool=args.inflight_binds + 8,
+                            native_watch=not args.no_native_pod_watch)
     else:
         # the watch history a real API server keeps is a bounded cache, and not in our process
         store = FakeKubeStore(history=8192, faults=Faults(latency_s=args.api_rtt_ms / 1e3))

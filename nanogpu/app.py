@@ -49,6 +49,7 @@ class Config:
     native_bind_writes: bool = True             # C++ writer threads do the bind's API writes
     bind_writer_threads: int = 16               # x KubeWriter::kBatch (8) binds in flight
     bind_writer_mode: str = "evented"           # evented (one epoll thread) | threads (blocking threads)
+    native_pod_watch: bool = True               # a C++ thread reads and filters the pod watch (podwatch.cpp)
     reservation_ttl_s: float = 60.0
     nominate: bool = True              # priorities nominate the top node (Ledger::nominate)
     nomination_ttl_s: float = 5.0
@@ -128,7 +129,8 @@ class Runtime:
             return InProcKube(store)
         from .k8s.client import KubeClient, KubeConfig
 
-        return KubeClient(KubeConfig.auto(self.cfg.kubeconfig, self.cfg.kube_api))
+        return KubeClient(KubeConfig.auto(self.cfg.kubeconfig, self.cfg.kube_api),
+                          native_watch=self.cfg.native_pod_watch)
 
     async def start(self, serve: bool = True) -> None:
         from .config.policy import PolicyWatcher

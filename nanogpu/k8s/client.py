@@ -152,8 +152,13 @@ class KubeClient:
 
     supports_slim_watch = True   # watch_batches(slim=True): native slim pod decoding
 
-    def __init__(self, config: KubeConfig, timeout_s: float = 30.0, pool: int = 64, token_check_s: float = 60.0):
+    def __init__(self, config: KubeConfig, timeout_s: float = 30.0, pool: int = 64, token_check_s: float = 60.0,
+                 native_watch: bool = True):
         self.config = config
+        # a filtered pod watch (watch_batches with a watch_filter) is read by a native thread
+        # (nanogpu._native.PodWatchStream) rather than by aiohttp on the event loop
+        u = urllib.parse.urlsplit(config.server)
+        self.native_watch = native_watch and u.scheme in ("http", "https") and bool(u.hostname)
         self._timeout = aiohttp.ClientTimeout(total=timeout_s)
         self._pool = pool
         self._session: aiohttp.ClientSession | None = None
@@ -320,6 +325,42 @@ class KubeClient:
                 for ev in batch:
                     yield ev
 
+    async def _native_watch(self, path: str, watch_filter, read_timeout_s: int) -> AsyncIterator[list[dict]]:
+        """The filtered pod watch on a native thread (native/src/podwatch.cpp): the stream is
+        read, split and filtered off the event loop, which wakes only for the events the filter
+        keeps. Errors as in the aiohttp path: ApiError for an HTTP error answer, a transport
+        failure as an exception the informer relists on, a clean end as the end of the stream."""
+        from ..native import core
+
+        u = urllib.parse.urlsplit(self.config.server)
+        tls = u.scheme == "https"
+        hdr = self._auth() or {}
+        token = hdr.get("Authorization", "")[len("Bearer "):]
+        c = self.config
+        st = core().PodWatchStream(u.hostname, u.port or (443 if tls else 80), tls, token, c.ca_file or "",
+                                   c.cert_file or "", c.key_file or "", bool(c.insecure),
+                                   u.path.rstrip("/") + path, watch_filter, read_timeout_s)
+        loop = asyncio.get_running_loop()
+        ready = asyncio.Event()
+        fd = st.notify_fd()
+        loop.add_reader(fd, ready.set)
+        try:
+            while True:
+                await ready.wait()
+                ready.clear()
+                events, state, status, message = st.take()
+                if events:
+                    yield events
+                if state == 1:
+                    return
+                if state == 2:
+                    raise ApiError(status, message)
+                if state == 3:
+                    raise ConnectionError(f"pod watch: {message}")
+        finally:
+            loop.remove_reader(fd)
+            st.stop()   # shuts the socket down and joins the thread (no blocking read left)
+
     async def watch_batches(self, resource: str, resource_version: str, timeout_s: int = 300,
                             label_selector: str | None = None, slim: bool = False,
                             watch_filter=None) -> AsyncIterator[list[dict]]:
@@ -333,11 +374,16 @@ class KubeClient:
             from ..native import core
 
             decode = watch_filter.decode if watch_filter is not None else core().decode_pod_watch
-        s = await self._s()
         params = {"watch": "1", "resourceVersion": resource_version, "timeoutSeconds": str(timeout_s),
                   "allowWatchBookmarks": "true"}
         if label_selector:
             params["labelSelector"] = label_selector
+        if decode is not None and watch_filter is not None and self.native_watch:
+            async for batch in self._native_watch(f"/api/v1/{resource}?{urllib.parse.urlencode(params)}",
+                                                  watch_filter, timeout_s + 30):
+                yield batch
+            return
+        s = await self._s()
         url = f"{self.config.server}/api/v1/{resource}?{urllib.parse.urlencode(params)}"
         async with s.get(url, timeout=aiohttp.ClientTimeout(total=None, sock_read=timeout_s + 30),
                          headers=self._auth()) as r:

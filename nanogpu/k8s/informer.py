@@ -169,6 +169,16 @@ class Informer:
             stream = self.api.watch_batches(self.resource, self.rv, label_selector=self.label_selector, **kw)
         else:
             stream = _singletons(self.api.watch(self.resource, self.rv, label_selector=self.label_selector))
+        try:
+            await self._consume(stream)
+        finally:
+            # close the stream now, not when the generator is collected: a native watch thread
+            # (client.py::_native_watch) would go on filtering into the relist that follows
+            aclose = getattr(stream, "aclose", None)
+            if aclose is not None:
+                await aclose()
+
+    async def _consume(self, stream) -> None:
         store, key, handlers = self.store, self.key, self.handlers
         pop, get = store.pop, store.get
         async for batch in stream:

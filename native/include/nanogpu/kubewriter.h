@@ -36,10 +36,17 @@ struct KubeTarget {
   bool insecure = false;    // skip server certificate verification
 };
 
+// SSL_CTX* for the target's CA / client certificate (throws std::runtime_error); nullptr for
+// plain HTTP. The caller frees it with free_ssl_ctx.
+void* make_ssl_ctx(const KubeTarget& t);
+void free_ssl_ctx(void* ctx);
+// The bearer token now: the token file's contents when it has any, else the target's token.
+std::string kube_token(const KubeTarget& t);
+
 // One blocking HTTP/1.1 keep-alive connection (plain or TLS).
 class HttpConn {
  public:
-  HttpConn(const KubeTarget* t, void* ssl_ctx) : t_(t), ctx_(ssl_ctx) {}
+  HttpConn(const KubeTarget* t, void* ssl_ctx, int timeout_s = 30) : t_(t), ctx_(ssl_ctx), timeout_s_(timeout_s) {}
   ~HttpConn();
   // status 0 = transport failure (message in *body); reconnects once for a request that
   // failed on a connection the server had already closed.
@@ -50,18 +57,35 @@ class HttpConn {
   bool start(const char* method, const std::string& path, const std::string& content_type,
              const std::string& body, const std::string& auth);
   int finish(std::string* resp);
+  // A streamed answer (a watch): after start(), stream_head() reads the status line and
+  // headers; an answer other than 200 is read whole into *body. stream_read() then appends
+  // the next decoded body bytes (chunked or to the end of the connection) to *out: > 0 bytes,
+  // 0 at the end of the body, -1 on a transport failure or a read timeout (timeout_s).
+  int stream_head(std::string* body);
+  long stream_read(std::string* out);
+  int fd() const { return fd_; }
 
  private:
+  struct Head {
+    int status = 0;
+    long clen = -1;
+    bool chunked = false, close_after = false;
+  };
   bool connect_();
   void close_();
   bool send_all(const char* p, size_t n);
   long recv_some(char* p, size_t n);
   int receive(std::string* resp, bool* retryable);
+  bool read_head(Head* h, bool* retryable);
+  int read_body(const Head& h, std::string* resp);
+  bool stream_chunked_ = false, stream_end_ = false;
+  long chunk_left_ = -1;   // bytes of the current chunk still to read, its CRLF included; -1: a size line next
   std::string req_;
   bool reused_ = false, sent_ = false;
 
   const KubeTarget* t_;
   void* ctx_;               // SSL_CTX* (nullptr: plain HTTP)
+  int timeout_s_;           // send / receive timeout of the socket
   int fd_ = -1;
   void* ssl_ = nullptr;     // SSL*
   std::string buf_;

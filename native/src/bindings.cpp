@@ -14,6 +14,7 @@
 #include "nanogpu/gosort.h"
 #include "nanogpu/json.h"
 #include "nanogpu/ledger.h"
+#include "nanogpu/podwatch.h"
 #include "nanogpu/schedsim.h"
 #include "nanogpu/topo.h"
 
@@ -306,23 +307,37 @@ static py::dict slim_pod(const json::Doc& d, int32_t pod) {
 }
 
 
-// What the pod informer needs from the native side (nanogpu/k8s/informer.py): keys handed to
-// Python (its store) and the ledger the controller would only look up or release.
-struct PodWatchFilter {
-  std::shared_ptr<Ledger> ledger;
-  std::unordered_set<std::string> forwarded;   // "ns/name" in the Python store
-  uint64_t released = 0, dropped = 0;
-  // compat (reference pod.go:15-24): a deletionTimestamp alone ends the share; otherwise a
-  // terminating pod keeps it until Succeeded/Failed or DELETED (controller/pods.py)
-  bool release_on_terminating = false;
-};
+// One event line, parsed in full, as the informer's {type, object} (a Pod slimmed).
+static py::dict pod_event(json::Doc& d, std::string_view line) {
+  if (!d.parse(line) || !d.is(d.root(), json::Type::kObj)) throw py::value_error("bad watch event line");
+  const int32_t t = d.get(d.root(), "type");
+  const int32_t obj = d.get(d.root(), "object");
+  const std::string_view type = d.is(t, json::Type::kStr) ? d.str(t) : std::string_view();
+  py::dict ev;
+  ev["type"] = py::str(std::string(type));
+  const bool plain = type == "ERROR" || type == "BOOKMARK";
+  ev["object"] = d.is(obj, json::Type::kObj) ? (plain ? jnode(d, obj) : py::object(slim_pod(d, obj))) : py::dict();
+  return ev;
+}
 
+// events were dropped after the last one kept: a bookmark carries the resume point
+static py::dict bookmark(const std::string& rv) {
+  py::dict md, o, ev;
+  md["resourceVersion"] = rv;
+  o["metadata"] = md;
+  ev["type"] = "BOOKMARK";
+  ev["object"] = o;
+  return ev;
+}
+
+// The pod informer's decoder (nanogpu/k8s/informer.py); with a filter (podwatch.h) only what
+// the filter keeps is decoded.
 static py::list decode_pod_events(const py::bytes& data, PodWatchFilter* f) {
   std::string_view sv = data;
   py::list out;
   size_t p = 0;
   json::Doc d;
-  std::string last_rv;   // resourceVersion of dropped events after the last kept one
+  std::string rv, last_rv;   // resourceVersion of dropped events after the last kept one
   while (p < sv.size()) {
     size_t e = sv.find('\n', p);
     if (e == std::string_view::npos) e = sv.size();
@@ -330,76 +345,14 @@ static py::list decode_pod_events(const py::bytes& data, PodWatchFilter* f) {
     p = e + 1;
     while (!line.empty() && (line.back() == '\r' || line.back() == ' ')) line.remove_suffix(1);
     if (line.empty()) continue;
-    // with a filter most events are dropped on a few shallow fields (type, metadata's
-    // identity, nodeName, phase): parse to that depth first, in full only for what goes on
-    bool shallow = f != nullptr;
-    if (!(shallow ? d.parse_shallow(line, 3) : d.parse(line)) || !d.is(d.root(), json::Type::kObj))
-      throw py::value_error("bad watch event line");
-    int32_t t = d.get(d.root(), "type");
-    int32_t obj = d.get(d.root(), "object");
-    std::string_view type = d.is(t, json::Type::kStr) ? d.str(t) : std::string_view();
-    if (f && d.is(obj, json::Type::kObj) && (type == "ADDED" || type == "MODIFIED" || type == "DELETED")) {
-      const int32_t md = d.get(obj, "metadata"), sp = d.get(obj, "spec"), st = d.get(obj, "status");
-      auto field = [&](int32_t o, const char* k) -> std::string_view {
-        const int32_t v = d.is(o, json::Type::kObj) ? d.get(o, k) : -1;
-        return d.is(v, json::Type::kStr) ? d.str(v) : std::string_view();
-      };
-      std::string key(field(md, "namespace"));
-      key.push_back('/');
-      key.append(field(md, "name"));
-      const bool seen = f->forwarded.count(key) > 0;
-      bool drop = false;
-      if (!seen && type == "DELETED") {
-        // Python never held it: releasing is all the controller would do (pods.py::_on_event)
-        if (f->ledger->release(std::string(field(md, "uid"))) == kOk) ++f->released;
-        drop = true;
-      } else if (!seen) {
-        // what the controller ignores: a pending pod, or a bound, running one the ledger holds
-        const std::string_view node = field(sp, "nodeName"), phase = field(st, "phase");
-        const int32_t dts = d.is(md, json::Type::kObj) ? d.get(md, "deletionTimestamp") : -1;
-        const bool completed = (f->release_on_terminating && dts >= 0 && !d.is(dts, json::Type::kNull)) ||
-                               phase == "Succeeded" || phase == "Failed";
-        if (!completed && node.empty()) {
-          drop = true;
-        } else if (!completed) {
-          PodRecord rec;
-          drop = f->ledger->lookup(std::string(field(md, "uid")), &rec);
-          // the node agent rewrote the placement to what kubelet ran (plugin.reconcile): the
-          // controller re-accounts it, so the event goes on
-          if (drop && line.find("\"nano-gpu/reconciled\"") != std::string_view::npos) drop = false;
-        }
-      }
-      if (drop) {
-        ++f->dropped;
-        last_rv = std::string(field(md, "resourceVersion"));
-        continue;
-      }
-      if (type == "DELETED") f->forwarded.erase(key);
-      else f->forwarded.insert(std::move(key));
+    if (f && !filter_pod_event(*f, line, d, &rv)) {
+      last_rv = rv;
+      continue;
     }
-    if (shallow) {   // kept: the whole event is needed (slim_pod reads labels, containers)
-      if (!d.parse(line)) throw py::value_error("bad watch event line");
-      t = d.get(d.root(), "type");
-      obj = d.get(d.root(), "object");
-      type = d.is(t, json::Type::kStr) ? d.str(t) : std::string_view();
-      shallow = false;
-    }
-    py::dict ev;
-    ev["type"] = py::str(std::string(type));
-    const bool plain = type == "ERROR" || type == "BOOKMARK";
-    ev["object"] = d.is(obj, json::Type::kObj) ? (plain ? jnode(d, obj) : py::object(slim_pod(d, obj))) : py::dict();
-    out.append(ev);
+    out.append(pod_event(d, line));
     last_rv.clear();
   }
-  if (f && !last_rv.empty()) {
-    // events were dropped after the last one kept: a bookmark carries the resume point
-    py::dict md, o, ev;
-    md["resourceVersion"] = last_rv;
-    o["metadata"] = md;
-    ev["type"] = "BOOKMARK";
-    ev["object"] = o;
-    out.append(ev);
-  }
+  if (f && !last_rv.empty()) out.append(bookmark(last_rv));
   return out;
 }
 
@@ -1078,12 +1031,65 @@ PYBIND11_MODULE(_native, m) {
       .def(
           "reset",
           [](PodWatchFilter& f, const std::vector<std::string>& keys) {
+            std::lock_guard<std::mutex> g(f.mu);
             f.forwarded.clear();
             f.forwarded.insert(keys.begin(), keys.end());
           },
           py::arg("keys"), "After a relist: the keys now in the informer's store.")
       .def_readwrite("release_on_terminating", &PodWatchFilter::release_on_terminating)
-      .def_property_readonly("released", [](const PodWatchFilter& f) { return f.released; })
-      .def_property_readonly("dropped", [](const PodWatchFilter& f) { return f.dropped; })
-      .def_property_readonly("forwarded", [](const PodWatchFilter& f) { return f.forwarded.size(); });
+      .def_property_readonly("released",
+                             [](PodWatchFilter& f) {
+                               std::lock_guard<std::mutex> g(f.mu);
+                               return f.released;
+                             })
+      .def_property_readonly("dropped",
+                             [](PodWatchFilter& f) {
+                               std::lock_guard<std::mutex> g(f.mu);
+                               return f.dropped;
+                             })
+      .def_property_readonly("forwarded", [](PodWatchFilter& f) {
+        std::lock_guard<std::mutex> g(f.mu);
+        return f.forwarded.size();
+      });
+
+  py::class_<PodWatchStream>(
+      m, "PodWatchStream",
+      "A pod watch read by a native thread: the stream's event lines run through a PodWatchFilter "
+      "as they arrive and only the kept ones are queued; notify_fd() becomes readable when there "
+      "are some, or when the stream ended. take() -> (events, state, status, message): events "
+      "decoded as PodWatchFilter.decode does (a trailing BOOKMARK for dropped ones), state 0 "
+      "streaming, 1 ended cleanly, 2 HTTP error (status, body), 3 transport failure.")
+      .def(py::init([](const std::string& host, int port, bool tls, const std::string& token,
+                       const std::string& ca_file, const std::string& cert_file, const std::string& key_file,
+                       bool insecure, const std::string& path, std::shared_ptr<PodWatchFilter> filter,
+                       int read_timeout_s) {
+             KubeTarget t;
+             t.host = host;
+             t.port = port;
+             t.tls = tls;
+             t.token = token;
+             t.ca_file = ca_file;
+             t.cert_file = cert_file;
+             t.key_file = key_file;
+             t.insecure = insecure;
+             return std::make_unique<PodWatchStream>(std::move(t), path, std::move(filter), read_timeout_s);
+           }),
+           py::arg("host"), py::arg("port"), py::arg("tls"), py::arg("token"), py::arg("ca_file"),
+           py::arg("cert_file"), py::arg("key_file"), py::arg("insecure"), py::arg("path"), py::arg("filter"),
+           py::arg("read_timeout_s") = 330)
+      .def("notify_fd", &PodWatchStream::notify_fd)
+      .def("take",
+           [](PodWatchStream& s) {
+             PodWatchStream::Batch b;
+             {
+               py::gil_scoped_release nogil;
+               b = s.take();
+             }
+             py::list out;
+             json::Doc d;
+             for (const auto& l : b.lines) out.append(pod_event(d, l));
+             if (!b.last_rv.empty()) out.append(bookmark(b.last_rv));
+             return py::make_tuple(out, b.state, b.status, b.message);
+           })
+      .def("stop", &PodWatchStream::stop, py::call_guard<py::gil_scoped_release>());
 }

@@ -86,6 +86,42 @@ std::string pod_node(const std::string& body) {
 }  // namespace
 
 // ------------------------------------------------------------------------------ HttpConn
+void* make_ssl_ctx(const KubeTarget& t) {
+  if (!t.tls) return nullptr;
+  SSL_CTX* ctx = SSL_CTX_new(TLS_client_method());
+  if (!ctx) throw std::runtime_error("SSL_CTX_new failed");
+  if (!t.ca_file.empty()) {
+    if (SSL_CTX_load_verify_locations(ctx, t.ca_file.c_str(), nullptr) != 1) {
+      SSL_CTX_free(ctx);
+      throw std::runtime_error("cannot load CA file " + t.ca_file);
+    }
+  } else {
+    SSL_CTX_set_default_verify_paths(ctx);
+  }
+  SSL_CTX_set_verify(ctx, t.insecure ? SSL_VERIFY_NONE : SSL_VERIFY_PEER, nullptr);
+  if (!t.cert_file.empty() && !t.key_file.empty()) {
+    if (SSL_CTX_use_certificate_chain_file(ctx, t.cert_file.c_str()) != 1 ||
+        SSL_CTX_use_PrivateKey_file(ctx, t.key_file.c_str(), SSL_FILETYPE_PEM) != 1) {
+      SSL_CTX_free(ctx);
+      throw std::runtime_error("cannot load the client certificate / key");
+    }
+  }
+  return ctx;
+}
+
+void free_ssl_ctx(void* ctx) {
+  if (ctx) SSL_CTX_free(static_cast<SSL_CTX*>(ctx));
+}
+
+std::string kube_token(const KubeTarget& t) {
+  if (!t.token_file.empty()) {
+    int64_t mtime = 0;
+    std::string tok = read_token(t.token_file, &mtime);
+    if (!tok.empty()) return tok;
+  }
+  return t.token;
+}
+
 HttpConn::~HttpConn() { close_(); }
 
 void HttpConn::close_() {
@@ -108,7 +144,9 @@ bool HttpConn::connect_() {
   for (addrinfo* a = res; a; a = a->ai_next) {
     const int fd = socket(a->ai_family, a->ai_socktype | SOCK_CLOEXEC, a->ai_protocol);
     if (fd < 0) continue;
-    timeval tv{30, 0};
+    // connecting and the TLS handshake are bounded at 30 s whatever the read timeout (a
+    // watch's is the server's timeoutSeconds and more)
+    timeval tv{std::min(timeout_s_, 30), 0};
     setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
     setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
     int one = 1;
@@ -136,6 +174,10 @@ bool HttpConn::connect_() {
     }
     ssl_ = s;
     if (SSL_connect(s) != 1) return close_(), false;
+  }
+  if (timeout_s_ > 30) {
+    timeval tv{timeout_s_, 0};
+    setsockopt(fd_, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
   }
   return true;
 }
@@ -169,7 +211,7 @@ long HttpConn::recv_some(char* p, size_t n) {
   }
 }
 
-int HttpConn::receive(std::string* resp, bool* retryable) {
+bool HttpConn::read_head(Head* h, bool* retryable) {
   *retryable = false;
   char tmp[16384];
   size_t he;
@@ -178,17 +220,15 @@ int HttpConn::receive(std::string* resp, bool* retryable) {
     const long r = recv_some(tmp, sizeof tmp);
     if (r <= 0) {
       *retryable = !got_any;   // the server closed an idle keep-alive connection
-      return 0;
+      return false;
     }
     got_any = true;
     buf_.append(tmp, static_cast<size_t>(r));
   }
   const std::string head = buf_.substr(0, he);
   buf_.erase(0, he + 4);
-  int status = 0;
-  if (head.size() > 12) status = std::atoi(head.c_str() + 9);
-  long clen = -1;
-  bool chunked = false, close_after = false;
+  *h = Head();
+  if (head.size() > 12) h->status = std::atoi(head.c_str() + 9);
   size_t p = head.find("\r\n");
   while (p != std::string::npos && p + 2 < head.size()) {
     const size_t e = head.find("\r\n", p + 2);
@@ -199,14 +239,20 @@ int HttpConn::receive(std::string* resp, bool* retryable) {
       for (char& ch : k) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
       std::string v = line.substr(colon + 1);
       while (!v.empty() && v.front() == ' ') v.erase(0, 1);
-      if (k == "content-length") clen = std::atol(v.c_str());
-      else if (k == "transfer-encoding" && v.find("chunked") != std::string::npos) chunked = true;
-      else if (k == "connection" && (v == "close" || v == "Close")) close_after = true;
+      if (k == "content-length") h->clen = std::atol(v.c_str());
+      else if (k == "transfer-encoding" && v.find("chunked") != std::string::npos) h->chunked = true;
+      else if (k == "connection" && (v == "close" || v == "Close")) h->close_after = true;
     }
     p = e;
   }
+  return true;
+}
+
+int HttpConn::read_body(const Head& h, std::string* resp) {
+  char tmp[16384];
+  bool close_after = h.close_after;
   resp->clear();
-  if (chunked) {
+  if (h.chunked) {
     for (;;) {
       size_t le;
       while ((le = buf_.find("\r\n")) == std::string::npos) {
@@ -224,14 +270,14 @@ int HttpConn::receive(std::string* resp, bool* retryable) {
       buf_.erase(0, le + 2 + sz + 2);
       if (sz == 0) break;
     }
-  } else if (clen >= 0) {
-    while (buf_.size() < static_cast<size_t>(clen)) {
+  } else if (h.clen >= 0) {
+    while (buf_.size() < static_cast<size_t>(h.clen)) {
       const long r = recv_some(tmp, sizeof tmp);
       if (r <= 0) return close_(), 0;
       buf_.append(tmp, static_cast<size_t>(r));
     }
-    resp->assign(buf_, 0, static_cast<size_t>(clen));
-    buf_.erase(0, static_cast<size_t>(clen));
+    resp->assign(buf_, 0, static_cast<size_t>(h.clen));
+    buf_.erase(0, static_cast<size_t>(h.clen));
   } else {
     for (;;) {   // no length: the body runs to the end of the connection
       const long r = recv_some(tmp, sizeof tmp);
@@ -242,7 +288,64 @@ int HttpConn::receive(std::string* resp, bool* retryable) {
     close_after = true;
   }
   if (close_after) close_();
-  return status;
+  return h.status;
+}
+
+int HttpConn::receive(std::string* resp, bool* retryable) {
+  Head h;
+  if (!read_head(&h, retryable)) return 0;
+  return read_body(h, resp);
+}
+
+int HttpConn::stream_head(std::string* body) {
+  body->clear();
+  if (!sent_) return 0;
+  Head h;
+  bool retryable = false;
+  if (!read_head(&h, &retryable)) return close_(), 0;
+  if (h.status != 200) return read_body(h, body);
+  stream_chunked_ = h.chunked;
+  stream_end_ = false;
+  chunk_left_ = -1;
+  return h.status;
+}
+
+long HttpConn::stream_read(std::string* out) {
+  const size_t before = out->size();
+  char tmp[65536];
+  for (;;) {
+    if (!stream_chunked_) {
+      out->append(buf_);
+      buf_.clear();
+    } else {
+      while (!stream_end_) {
+        if (chunk_left_ < 0) {   // a chunk-size line next
+          const size_t le = buf_.find("\r\n");
+          if (le == std::string::npos) break;
+          const long sz = static_cast<long>(std::strtoul(buf_.c_str(), nullptr, 16));
+          buf_.erase(0, le + 2);
+          if (sz == 0) {
+            stream_end_ = true;
+            break;
+          }
+          chunk_left_ = sz + 2;
+        }
+        const size_t take = std::min(buf_.size(), static_cast<size_t>(chunk_left_));
+        const size_t data = chunk_left_ > 2 ? std::min(take, static_cast<size_t>(chunk_left_ - 2)) : 0;
+        out->append(buf_, 0, data);
+        buf_.erase(0, take);
+        chunk_left_ -= static_cast<long>(take);
+        if (chunk_left_ > 0) break;   // the rest of this chunk is still on the wire
+        chunk_left_ = -1;
+      }
+    }
+    if (out->size() > before) return static_cast<long>(out->size() - before);
+    if (stream_end_) return 0;
+    const long r = recv_some(tmp, sizeof tmp);
+    if (r == 0 && !stream_chunked_) return 0;   // a body without framing ends with the connection
+    if (r <= 0) return -1;                      // a chunked body cut short, an error, a timeout
+    buf_.append(tmp, static_cast<size_t>(r));
+  }
 }
 
 bool HttpConn::start(const char* method, const std::string& path, const std::string& content_type,
@@ -308,27 +411,7 @@ KubeWriter::KubeWriter(KubeTarget target, std::shared_ptr<Ledger> ledger, Respon
                        bool record_events, bool evented)
     : t_(std::move(target)), ledger_(std::move(ledger)), respond_(std::move(respond)), retries_(retries),
       events_(record_events), evented_(evented) {
-  if (t_.tls) {
-    SSL_CTX* ctx = SSL_CTX_new(TLS_client_method());
-    if (!ctx) throw std::runtime_error("KubeWriter: SSL_CTX_new failed");
-    if (!t_.ca_file.empty()) {
-      if (SSL_CTX_load_verify_locations(ctx, t_.ca_file.c_str(), nullptr) != 1) {
-        SSL_CTX_free(ctx);
-        throw std::runtime_error("KubeWriter: cannot load CA file " + t_.ca_file);
-      }
-    } else {
-      SSL_CTX_set_default_verify_paths(ctx);
-    }
-    SSL_CTX_set_verify(ctx, t_.insecure ? SSL_VERIFY_NONE : SSL_VERIFY_PEER, nullptr);
-    if (!t_.cert_file.empty() && !t_.key_file.empty()) {
-      if (SSL_CTX_use_certificate_chain_file(ctx, t_.cert_file.c_str()) != 1 ||
-          SSL_CTX_use_PrivateKey_file(ctx, t_.key_file.c_str(), SSL_FILETYPE_PEM) != 1) {
-        SSL_CTX_free(ctx);
-        throw std::runtime_error("KubeWriter: cannot load the client certificate / key");
-      }
-    }
-    ctx_ = ctx;
-  }
+  ctx_ = make_ssl_ctx(t_);
   token_ = t_.token;
   if (!t_.token_file.empty()) {
     const std::string tok = read_token(t_.token_file, &token_mtime_);
@@ -362,7 +445,7 @@ KubeWriter::KubeWriter(KubeTarget target, std::shared_ptr<Ledger> ledger, Respon
 KubeWriter::~KubeWriter() {
   stop();
   if (efd_ >= 0) ::close(efd_);
-  if (ctx_) SSL_CTX_free(static_cast<SSL_CTX*>(ctx_));
+  free_ssl_ctx(ctx_);
 }
 
 void KubeWriter::refuse(BindJob& j) {

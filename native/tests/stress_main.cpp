@@ -37,6 +37,7 @@
 #include "nanogpu/apiserver.h"
 #include "nanogpu/frontend.h"
 #include "nanogpu/kubewriter.h"
+#include "nanogpu/podwatch.h"
 #include "nanogpu/ledger.h"
 
 using namespace nanogpu;
@@ -194,11 +195,15 @@ static void relist_gap(int iters) {
       }
       // every pod still in the API server must still hold its share: reconcile never took it
       for (const auto& k : mine) {
+        PodRecord rec;
+        CHECK(l.lookup(k, &rec));
         {
           std::lock_guard<std::mutex> g(api_mu);
           api.erase(k);
         }
-        CHECK(l.release(k) == kOk);
+        // deleted from the API server first: a relist in between may release it before we do
+        const int32_t rc = l.release(k);
+        CHECK(rc == kOk || rc == kErrUnknownPod);
       }
     });
   for (auto& b : binders) b.join();
@@ -278,6 +283,20 @@ static void apiserver_and_writers(int pods, bool evented) {
   tgt.host = "127.0.0.1";
   tgt.port = port;
   tgt.tls = false;
+  // the pod informer's native watch on the same stream: every event here is one the filter
+  // drops (pending pods, bound pods the ledger holds, deletions of pods Python never saw,
+  // released right in the stream thread) while a consumer drains it as the event loop would
+  auto filter = std::make_shared<PodWatchFilter>();
+  filter->ledger = ledger;
+  PodWatchStream pw(tgt, "/api/v1/pods?watch=1&resourceVersion=" + rv0, filter, 30);
+  std::atomic<bool> stop_take{false};
+  std::atomic<int> kept{0};
+  std::thread taker([&] {
+    while (!stop_take.load()) {
+      kept.fetch_add(static_cast<int>(pw.take().lines.size()));
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+  });
   {
     KubeWriter kw(
         tgt, ledger,
@@ -349,6 +368,20 @@ static void apiserver_and_writers(int pods, bool evented) {
     patcher.join();
     deleter.join();
     CHECK(http(port, "GET", "/api/v1/namespaces/s/pods", "").find("\"items\":[]") != std::string::npos);
+  }
+  auto released = [&] {
+    std::lock_guard<std::mutex> g(filter->mu);
+    return filter->released;
+  };
+  for (int spin = 0; released() < static_cast<uint64_t>(pods) && spin < 2000; ++spin)
+    std::this_thread::sleep_for(std::chrono::milliseconds(2));
+  pw.stop();   // mid-stream: shuts the socket down under the reading thread
+  stop_take.store(true);
+  taker.join();
+  CHECK(released() == static_cast<uint64_t>(pods) && kept.load() == 0 && ledger->n_pods() == 0);
+  {
+    std::lock_guard<std::mutex> g(filter->mu);
+    CHECK(filter->dropped >= static_cast<uint64_t>(5 * pods));
   }
   srv.stop();
   std::printf("apiserver ok: %d pods bound by native writers, %d watch events\n", pods, events.load());

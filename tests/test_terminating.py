@@ -63,11 +63,13 @@ def test_terminating_pod_keeps_its_hbm_until_deleted(compat):
                 led = rt.state.ledger
                 assert await wait_for(lambda: (led.lookup(uid) or {}).get("state") == "committed")
                 store.set_phase("default", "a", "Running")
-                ev0 = rt.pod_informer.events
+                inf = rt.pod_informer
+                seen = lambda: inf.events + inf.watch_filter.dropped   # handed on or dropped natively
+                ev0 = seen()
                 # kubectl delete: the API server sets the deletionTimestamp, the pod runs on
                 store.patch_pod("default", "a", {"metadata": {"deletionTimestamp": TS,
                                                               "deletionGracePeriodSeconds": 30}})
-                assert await wait_for(lambda: rt.pod_informer.events >= ev0 + 1)
+                assert await wait_for(lambda: seen() >= ev0 + 1)
                 await asyncio.sleep(0.05)
                 b = store.create_pod(pu.make_pod("b", [("main", 30, big)]))
                 res = await _verb(s, base, "filter", {"Pod": b, "NodeNames": ["n0"]})
