@@ -188,6 +188,10 @@ class Dist:
     def gather_obj(self, obj):
         if self.dist is None:
             return [obj]
+        if self.cuda:
+            import torch
+
+            torch.cuda.set_device(self.local_rank)   # also when called from a helper thread
         out = [None] * self.world
         self.dist.all_gather_object(out, obj)
         return out
@@ -621,9 +625,12 @@ def driver_main(conn) -> None:
             # cache of them (node, requests, owner) and hands it to every run
             stream = st["stream"] = steady_stream(argparse.Namespace(**cfg["steady"]))
             for step in cfg["steps"]:
-                specs = [s for s in stream[step].creates if s.key % cfg["world"] == cfg["rank"]]
+                # the one scheduler of the job schedules every rank's pods
+                specs = [s for s in stream[step].creates
+                         if cfg.get("bind_ports") or s.key % cfg["world"] == cfg["rank"]]
                 st["specs"][step] = specs
-                work[step] = NativeSchedulerDriver.prepare_native([steady_pod(s, cfg["rank"]) for s in specs])
+                work[step] = NativeSchedulerDriver.prepare_native([steady_pod(s, s.key % cfg["world"])
+                                                                   for s in specs])
         for step in ([] if cfg.get("steady") else cfg["steps"]):
             if cfg.get("bind_ports"):   # the one scheduler of the job: every rank's pods
                 pods = [p for r in range(cfg["world"]) for p in burst(r, cfg["world"], cfg["pods"], step, 7)]
@@ -645,6 +652,11 @@ def driver_main(conn) -> None:
             if isinstance(msg, dict):
                 configure(msg)
                 continue
+            if msg[0] == "live":
+                # the pods the other ranks' stand-ins placed last step: a kube-scheduler's cache
+                # holds every bound pod (its informer), not only the ones it scheduled itself
+                st["live"].update(msg[1])
+                continue
             if msg[0] != "step":
                 break
             cfg, work, session, cls = st["cfg"], st["work"], st["session"], st["cls"]
@@ -664,14 +676,18 @@ def driver_main(conn) -> None:
                 stats = drv.run(prepared=work.pop(step), live=list(live.values()))
                 args_k, node_of = drv._placed[-1]
                 idx = cfg["name_index"]
+                placed = []
                 for spec, a, node in zip(st["specs"].pop(step), args_k, node_of):
                     if node:
                         live[spec.key] = (idx[node], a[4], a[5], a[6], a[7])
+                        placed.append((spec.key, live[spec.key]))
             else:
                 stats = drv.run(prepared=work.pop(step)) if native else drv.run(work.pop(step))
             drv.close()
             t1 = time.perf_counter()
             sm = stats.summary()
+            if st["stream"] is not None:
+                sm["live_placed"] = placed   # for the other ranks' stand-ins (their informers)
             t2 = time.perf_counter()
             conn.send(sm)
             if os.environ.get("NANOGPU_BENCH_DEBUG"):
@@ -764,7 +780,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     # --one-scheduler: ONE kube-scheduler stand-in for the job (rank 0's) drives every pod; its
     # scheduling cycle stays on rank 0's worker, its binds spread over every rank's worker (the
     # connections a Service spreads over an extender's workers)
-    one = bool(getattr(args, "one_scheduler", False)) and d.world > 1 and not steady
+    one = bool(getattr(args, "one_scheduler", False)) and d.world > 1
     ports = d.gather_obj(rt.bound_port) if one else None
     drives = conn is not None and (not one or d.rank == 0)
     if conn is not None and drives:
@@ -806,10 +822,23 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         if shared:
             await barrier()
         t_send = time.perf_counter()
-        conn.send(("step", step))
-        summary = await arecv(conn)
+        if drives:
+            conn.send(("step", step))
+            summary = await arecv(conn)
+        else:            # one scheduler: rank 0's stand-in schedules this rank's pods too
+            from nanogpu.sim.driver import DriverStats
+
+            summary = DriverStats().summary()
         phases["schedule_wall_ms"] = 1e3 * (time.perf_counter() - t_send)
-        await barrier()
+        placed = summary.pop("live_placed", [])
+        if shared and not one:
+            # the barrier, carrying each rank's placements to the other ranks' stand-ins
+            every = await loop.run_in_executor(None, d.gather_obj, placed)
+            others = [kv for r, lst in enumerate(every) if r != d.rank for kv in lst]
+            if others:
+                conn.send(("live", others))
+        else:
+            await barrier()
         frag = rt.state.frag(min(SIZES))
         phases.update(create_ms=0.0, schedule_ms=1e3 * summary["span_s"])
         client_s = summary.pop("bind_s_all", [])
@@ -1080,8 +1109,11 @@ def main() -> int:
         shared_api = not args.inproc_api and not args.inproc_driver
         if args.steady_variant_steps > 0 and not args.steady and shared_api:
             # steady-state churn (BASELINE config 5 at scale): the cluster is never emptied
+            # placement quality is a property of the deployment that exists: ONE kube-scheduler
+            # (with N > 1 ranks, its binds spread over every rank's worker)
             s_args = argparse.Namespace(**{**vars(args), "steady": True, "steps": args.steady_variant_steps,
-                                           "warmup": 2, "profile_out": "", "stall_trace": "", "api_rtt_ms": 0.0})
+                                           "warmup": 2, "profile_out": "", "stall_trace": "", "api_rtt_ms": 0.0,
+                                           "one_scheduler": d.world > 1})
             try:
                 steady_v = (s_args, run_pass(d, s_args, topo, conn, "steady", api_proc))
                 steady_v = (s_args, steady_v[1], summarize(d, s_args, steady_v[1]))
@@ -1101,7 +1133,7 @@ def main() -> int:
             nv_pods = args.nodes_variant_pods or round(args.pods * args.nodes_variant / max(1, args.nodes))
             n_args = argparse.Namespace(**{**vars(args), "nodes": args.nodes_variant, "pods": nv_pods,
                                            "steps": args.nodes_variant_steps, "warmup": 1, "profile_out": "",
-                                           "stall_trace": "", "api_rtt_ms": 0.0})
+                                           "stall_trace": "", "api_rtt_ms": 0.0, "one_scheduler": d.world > 1})
             try:
                 r = run_pass(d, n_args, topo, conn, "nodes", api_proc)
                 nodes_v = (n_args, r, summarize(d, n_args, r))
@@ -1326,10 +1358,14 @@ def steady_keys(args, topo, v) -> dict:
     half = res["frag"][len(res["frag"]) // 2:]
     keys = {"value_steady": out["value"], "p50_bind_ms_steady": out["p50_bind_ms"],
             "frag_pct_steady": _frag_mean(half), "frag_hbm_pct_steady": _frag_mean(half, "frag_mib"),
+            "frag_pct_steady_each_step": [round(f["frag_pct"], 3) for f in res["frag"]],
+            "nominations_steady": res.get("nominations"),
             "steps_steady": s_args.steps, "failed_steady": out["failed"],
             "steady_config": f"{s_args.pods} pods fill {s_args.nodes} nodes, then each step deletes "
                              f"{int(100 * STEADY_CHURN)} % of the live pods and creates as many; frag = mean of "
-                             f"the last {len(half)} of {s_args.steps} timed steps"}
+                             f"the last {len(half)} of {s_args.steps} timed steps"
+                             + ("; one kube-scheduler stand-in, binds over every rank's worker"
+                                if getattr(s_args, "one_scheduler", False) else "")}
     if args.partition == "SPX" and args.policy == "binpack" and not args.compat:
         from nanogpu.sim import fragsim
 
@@ -1361,6 +1397,8 @@ def nodes_variant_keys(args, topo, v) -> dict:
             f"nomination_adopt_pct_{tag}": round(100.0 * nom["adopted"] / nom["made"], 2) if nom.get("made") else None,
             f"nominations_{tag}": nom,
             f"nodes_sent_per_filter_{tag}": res.get("nodes_sent_per_filter"),
+            f"schedulers_{tag}": "one kube-scheduler stand-in, binds over every rank's worker"
+            if getattr(n_args, "one_scheduler", False) else "one kube-scheduler stand-in per rank",
             f"native_verb_mean_us_{tag}": res.get("native")}
     if args.partition == "SPX" and args.policy == "binpack" and not args.compat:
         from nanogpu.sim import fragsim

@@ -289,6 +289,7 @@ struct Frontend::Worker {
   std::mutex mb_mu;
   std::vector<std::pair<uint64_t, std::string>> mailbox;       // (conn id, response bytes)
   std::atomic<bool> unsignalled{false};                         // queued with notify=false
+  bool mb_signalled = false;   // under mb_mu: the eventfd was written for what the mailbox holds
   uint64_t next_conn = 1;
   uint64_t cycle_reply_ns = 0;   // last filter / priorities reply handed to the kernel
 };
@@ -424,16 +425,21 @@ void Frontend::respond(uint64_t id, int status, const std::string& content_type,
   r += "HTTP/1.1 " + std::to_string(status) + " " + reason(status) + "\r\nContent-Type: " + content_type +
        "\r\nContent-Length: " + std::to_string(body.size()) + "\r\n\r\n";
   r += body;
+  bool signal = false;
   {
     std::lock_guard<std::mutex> g(w->mb_mu);
     w->mailbox.emplace_back(id >> 8, std::move(r));
+    // one eventfd write per mailbox fill: the worker takes everything queued until it swaps
+    if (notify && !w->mb_signalled) signal = w->mb_signalled = true;
   }
   if (!notify) {
     w->unsignalled.store(true, std::memory_order_release);
     return;
   }
-  uint64_t one = 1;
-  (void)!write(w->efd, &one, sizeof(one));
+  if (signal) {
+    uint64_t one = 1;
+    (void)!write(w->efd, &one, sizeof(one));
+  }
 }
 
 void Frontend::wake_workers() {
@@ -588,6 +594,7 @@ void Frontend::run(Worker* w) {
         {
           std::lock_guard<std::mutex> g(w->mb_mu);
           mb.swap(w->mailbox);
+          w->mb_signalled = false;
         }
         for (auto& m : mb) {
           auto it = w->conns.find(m.first);
@@ -650,6 +657,9 @@ bool Frontend::read_in(Worker* w, Conn* c, bool* eof) {
         close_conn(w, c);
         return false;
       }
+      // a short read drained the socket: no second recv() just to see EAGAIN (the epoll is
+      // level-triggered, so bytes that arrive after this are reported again)
+      if (static_cast<size_t>(r) < sizeof(buf)) break;
       continue;
     }
     if (r == 0) *eof = true;

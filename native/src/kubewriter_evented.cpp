@@ -350,6 +350,9 @@ void KubeWriter::io_loop() {
           }
           c.in.append(tmp, static_cast<size_t>(r));
           c.got_any = true;
+          // plain TCP: a short read drained the socket, and edge-triggered epoll reports the
+          // next bytes as a new edge; TLS hands out a record at a time, so it reads on
+          if (!c.ssl && static_cast<size_t>(r) < sizeof tmp) break;
         }
         if (c.st == kIdle) {   // an idle keep-alive connection the server closed (or junk)
           if (eof || !c.in.empty()) close_conn(c);

@@ -55,7 +55,7 @@ def test_bench_multi_rank_gloo(ranks):
                         "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
                         "--gpus", str(ranks), "--no-gpu", "--steps", "2", "--warmup", "1", "--pods", "200",
                         "--nodes", "8", "--rtt-variant-steps", "1", "--steady-variant-steps", "2",
-                        "--nodes-variant", "0", "--one-scheduler-variant-steps", "1"],
+                        "--nodes-variant", "16", "--nodes-variant-steps", "1", "--one-scheduler-variant-steps", "1"],
                        capture_output=True, text=True, timeout=400, env=env, cwd="/tmp")
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
@@ -63,6 +63,9 @@ def test_bench_multi_rank_gloo(ranks):
     assert f"{ranks} extender worker" in d["config"]["parallelism"]
     assert d["value_rtt2ms"] and d["p50_bind_ms"] is not None
     assert d["value_steady"] > 0 and d["failed_steady"] == 0
+    # placement-quality passes run the deployment that exists: one kube-scheduler for the job
+    assert d["steady_config"].endswith("one kube-scheduler stand-in, binds over every rank's worker")
+    assert d["schedulers_nodes16"].startswith("one kube-scheduler") and d["failed_nodes16"] == 0
     # the headline's N stand-ins are labelled as such; one scheduler over N workers alongside
     assert d["value_mode"].startswith(f"{ranks} independent kube-scheduler stand-ins")
     assert d["value_one_scheduler"] > 0 and d["steps_one_scheduler"] == 1
