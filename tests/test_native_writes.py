@@ -197,6 +197,17 @@ def test_native_writer_speaks_tls_with_a_bearer_token(tmp_path, mode):
             assert status == 200 and res == {"Error": ""}, res
             assert store.get_pod("default", "t")["spec"]["nodeName"] == "n0"
             assert rt.native.fe.kube_writer_stats()["ok"] == 1
+            # the pod watch over the same TLS endpoint (the native watch thread): the deletion
+            # of a pod the filter kept from Python is released in that thread
+            assert api.native_watch and rt.pod_informer.watch_filter is not None
+            uid = pu.pod_uid(p)
+            store.delete_pod("default", "t")
+            for _ in range(500):
+                if rt.state.ledger.lookup(uid) is None:
+                    break
+                await asyncio.sleep(0.01)
+            assert rt.state.ledger.lookup(uid) is None
+            assert rt.pod_informer.watch_filter.released == 1
         finally:
             await rt.stop()
             await runner.cleanup()
