@@ -42,6 +42,8 @@ void* make_ssl_ctx(const KubeTarget& t);
 void free_ssl_ctx(void* ctx);
 // The bearer token now: the token file's contents when it has any, else the target's token.
 std::string kube_token(const KubeTarget& t);
+// The Host header's value: host:port, an IPv6 address in brackets.
+std::string host_header(const KubeTarget& t);
 
 // One blocking HTTP/1.1 keep-alive connection (plain or TLS).
 class HttpConn {

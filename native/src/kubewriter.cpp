@@ -113,6 +113,11 @@ void free_ssl_ctx(void* ctx) {
   if (ctx) SSL_CTX_free(static_cast<SSL_CTX*>(ctx));
 }
 
+std::string host_header(const KubeTarget& t) {
+  const bool v6 = t.host.find(':') != std::string::npos && t.host.front() != '[';
+  return (v6 ? "[" + t.host + "]" : t.host) + ":" + std::to_string(t.port);
+}
+
 std::string kube_token(const KubeTarget& t) {
   if (!t.token_file.empty()) {
     int64_t mtime = 0;
@@ -356,7 +361,7 @@ bool HttpConn::start(const char* method, const std::string& path, const std::str
   req_ += ' ';
   req_ += path;
   req_ += " HTTP/1.1\r\nHost: ";
-  req_ += t_->host;
+  req_ += host_header(*t_);
   req_ += "\r\nUser-Agent: nano-gpu-scheduler-amd/0.1\r\nAccept: application/json\r\n";
   if (!auth.empty()) req_ += "Authorization: Bearer " + auth + "\r\n";
   if (!body.empty() || std::strcmp(method, "POST") == 0 || std::strcmp(method, "PATCH") == 0) {

@@ -143,6 +143,7 @@ void KubeWriter::io_loop() {
   int family = AF_INET;
   std::string a = auth();
   uint64_t auth_at = ns_now();
+  const std::string host_hdr = host_header(t_);
 
   auto resolve = [&]() -> bool {
     if (addr_len) return true;
@@ -212,7 +213,7 @@ void KubeWriter::io_loop() {
     r += ' ';
     r += path;
     r += " HTTP/1.1\r\nHost: ";
-    r += t_.host;
+    r += host_hdr;
     r += "\r\nUser-Agent: nano-gpu-scheduler-amd/0.1\r\nAccept: application/json\r\n";
     if (!a.empty()) r += "Authorization: Bearer " + a + "\r\n";
     r += "Content-Type: ";

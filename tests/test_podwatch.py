@@ -61,15 +61,17 @@ def _events(st, n=120, seed=3):
     return b"\n".join(lines) + b"\n", str(rv)
 
 
-async def _serve(handler):
+async def _serve(handler, host="127.0.0.1", heads=None):
     async def conn(reader, writer):
-        await reader.readuntil(b"\r\n\r\n")
+        head = await reader.readuntil(b"\r\n\r\n")
+        if heads is not None:
+            heads.append(head.decode())
         try:
             await handler(writer)
         finally:
             writer.close()
 
-    srv = await asyncio.start_server(conn, "127.0.0.1", 0)
+    srv = await asyncio.start_server(conn, host, 0)
     return srv, srv.sockets[0].getsockname()[1]
 
 
@@ -201,5 +203,28 @@ def test_native_watch_errors_end_and_stop():
             finally:
                 await api.close()
                 srv.close()
+
+    asyncio.run(main())
+
+
+def test_native_watch_over_ipv6_sends_a_bracketed_host_header():
+    async def main():
+        st = _state()
+        data, last_rv = _events(st, n=20)
+        heads = []
+        try:
+            srv, port = await _serve(_chunked(data), host="::1", heads=heads)
+        except OSError:
+            pytest.skip("no IPv6 loopback")
+        api = KubeClient(KubeConfig(server=f"http://[::1]:{port}", token="t0k"))
+        try:
+            evs = await asyncio.wait_for(_collect(api, N.PodWatchFilter(st.ledger)), 20)
+        finally:
+            await api.close()
+            srv.close()
+        assert _shape(evs)[1] == last_rv
+        (head,) = heads
+        assert f"\r\nHost: [::1]:{port}\r\n" in head and "\r\nAuthorization: Bearer t0k\r\n" in head
+        assert head.startswith("GET /api/v1/pods?watch=1&resourceVersion=100&")
 
     asyncio.run(main())
