@@ -124,3 +124,19 @@ def test_config5_sriov_guests_churn():
     assert all(g.numa == -1 for g in t.gpus) and not any(any(row) for row in t.link_bw)
     r = asyncio.run(C.config5(rounds=5, pods_n=125, sriov=True))
     assert r["scheduled"] == 125 and r["max_hbm_overcommitted_gib"] == 0
+
+
+def test_bench_steady_main_pass_two_ranks_share_placements():
+    """`--steady` as the main pass with 2 independent stand-ins: each stand-in's kube-scheduler
+    cache gets the other rank's placements after every step (bench.py one_step_steady)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
+                        "--gpus", "2", "--no-gpu", "--steady", "--steps", "2", "--warmup", "1", "--pods", "200",
+                        "--nodes", "8", "--rtt-variant-steps", "0", "--inproc-variant-steps", "0",
+                        "--nodes-variant", "0", "--one-scheduler-variant-steps", "0"],
+                       capture_output=True, text=True, timeout=400, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert d["value"] > 0 and d["failed"] == 0 and d["scheduled"] > 0
+    assert d["value_mode"].startswith("2 independent kube-scheduler stand-ins")
