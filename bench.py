@@ -992,6 +992,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         prof.enable()
     sampler = StallSampler() if args.stall_trace and d.rank == 0 else None
     nom0 = rt.state.ledger.nomination_counts()
+    fe_stats = rt.native.fe.stats if rt.native is not None else (lambda: {})
+    handoffs0 = fe_stats().get("bind_handoffs", 0)
     cpu0, loop_cpu0 = time.process_time(), time.thread_time()
     threads0 = thread_cpu()
     t0 = time.perf_counter()
@@ -1017,6 +1019,9 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     elapsed = time.perf_counter() - t0
     nom1 = rt.state.ledger.nomination_counts()
     results["nominations"] = {k: nom1[k] - nom0[k] for k in nom1}
+    # binds a worker answered natively with the pod another worker's filter parsed (the
+    # shared ledger's bind handoff): the one-scheduler passes' binds on ranks other than 0
+    results["bind_handoffs"] = sum(d.gather_obj(fe_stats().get("bind_handoffs", 0) - handoffs0))
     results["nomination_margin"] = rt.state.ledger.nomination_margin
     results["unschedulable_attempts"] = sum(st.get("unschedulable_attempts", 0) for st in results["steps"])
     cycles = sum(st.get("cycles", 0) for st in results["steps"])
@@ -1263,6 +1268,7 @@ def main() -> int:
             else:
                 line["value_one_scheduler"] = one_v["value"]
                 line["p50_bind_ms_one_scheduler"] = one_v["p50_bind_ms"]
+                line["bind_handoffs_one_scheduler"] = one_v["bind_handoffs"]
                 line["steps_one_scheduler"] = args.one_scheduler_variant_steps
                 line["one_scheduler_config"] = (f"one kube-scheduler stand-in: cycle on rank 0's worker, binds "
                                                 f"over all {d.world} workers")
@@ -1339,6 +1345,7 @@ def summarize(d: Dist, args, res: dict) -> dict:
             "scheduled": scheduled, "failed": sum(d.gather_obj(res["failed"])),
             "unschedulable": sum(d.gather_obj(res["unschedulable_attempts"])),
             "bind_errors": sum(d.gather_obj(res["bind_errors"])),
+            "bind_handoffs": res.get("bind_handoffs"),
             # each rank's mean stand-in span per step: the slowest sets the peak barrier
             "schedule_ms_by_rank": [round(v, 2) for v in d.gather_obj((res.get("phase_ms") or {}).get("schedule_ms", 0.0))]}
 
@@ -1360,6 +1367,7 @@ def steady_keys(args, topo, v) -> dict:
             "frag_pct_steady": _frag_mean(half), "frag_hbm_pct_steady": _frag_mean(half, "frag_mib"),
             "frag_pct_steady_each_step": [round(f["frag_pct"], 3) for f in res["frag"]],
             "nominations_steady": res.get("nominations"),
+            "bind_handoffs_steady": res.get("bind_handoffs"),
             "steps_steady": s_args.steps, "failed_steady": out["failed"],
             "steady_config": f"{s_args.pods} pods fill {s_args.nodes} nodes, then each step deletes "
                              f"{int(100 * STEADY_CHURN)} % of the live pods and creates as many; frag = mean of "

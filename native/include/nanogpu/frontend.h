@@ -121,6 +121,9 @@ class Frontend {
   VerbStats filter_stats, prio_stats, py_stats, bind_stats;   // bind_stats: native reserve half
   std::atomic<uint64_t> connections{0}, requests{0};
   std::atomic<uint64_t> spin_hits{0};     // event batches a busy-polling worker caught
+  // binds this process answered natively with a pod another worker process's filter parsed
+  // (Ledger::take_pod_info), and pods it handed to the other workers that way
+  std::atomic<uint64_t> bind_handoffs{0}, pods_published{0};
   std::atomic<uint64_t> loop_max_ns{0};   // longest event-batch a worker spent between epoll_waits
   // longest single step of a batch: 0 accept, 1 mailbox, 2 read+cycle verbs, 3 deferred binds,
   // 4 pod-cache lock wait (bind), 5 node lookup (bind), 6 Python hand-off (defer)

@@ -102,6 +102,22 @@ struct ExtRecord {
   Plan plan;
 };
 
+// Bind handoff between the worker processes of a replica (Frontend): what a filter parsed
+// from a pod (namespace, name, containers, demand, owner), for its bind when another worker
+// process receives it. kube-scheduler sends binds from per-pod goroutines on other keep-alive
+// connections than its scheduling cycle's, and SO_REUSEPORT spreads connections over the
+// workers, so with several workers the bind usually lands on a worker whose own pod cache
+// never saw the pod. Direct-mapped by key hash; an entry a newer pod overwrote just sends
+// its bind the slow way (Python, which reads the pod from the API server).
+constexpr int kPodInfoBytes = 1008;
+struct PodInfoSlot {
+  uint64_t hash;   // key_hash(key), 0: empty
+  char key[kKeyLen];
+  uint32_t len;
+  uint32_t pad;
+  char data[kPodInfoBytes];
+};
+
 struct LedgerHeader {
   uint64_t magic;
   uint32_t version;
@@ -143,6 +159,8 @@ struct LedgerHeader {
   uint32_t ext_cap;                 // overflow records (pods over kSlotContainers containers)
   std::atomic<uint32_t> ext_hint;   // where the next claim starts looking
   std::atomic<int32_t> ext_used;
+  uint32_t info_cap;                // bind-handoff slots (PodInfoSlot)
+  PaddedMutex info_mu[kPodShards];  // slot i is guarded by info_mu[i % kPodShards]
 };
 
 struct NodeSnapshot {
@@ -250,6 +268,12 @@ class Ledger {
   // Releases `key` only while it is Committed (reconcile racing a re-bind of the same key).
   int32_t drop_committed(const std::string& key);
   int64_t n_pods() const { return hdr_->n_pods.load(std::memory_order_acquire); }
+  // processes attached to the region (more than one: worker processes share it)
+  int32_t attached() const { return hdr_->attached.load(std::memory_order_relaxed); }
+  // Bind handoff (PodInfoSlot): `blob` is the front door's packed pod. put: false when it does
+  // not fit a slot. take: the blob stored for `key`, removed (one bind per pod UID).
+  bool put_pod_info(const std::string& key, std::string_view blob);
+  bool take_pod_info(const std::string& key, std::string* blob);
   int32_t overflow_records_used() const { return hdr_->ext_used.load(std::memory_order_relaxed); }
 
   // Load-aware telemetry (reference nodeusage.go + allocate.go:173-195).
@@ -322,6 +346,7 @@ class Ledger {
   NodeSlot* nodes_ = nullptr;
   PodSlot* pods_ = nullptr;
   ExtRecord* ext_ = nullptr;
+  PodInfoSlot* info_ = nullptr;
 
   struct CacheKey {
     int32_t node;

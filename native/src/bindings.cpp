@@ -494,6 +494,18 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("n_nodes", &Ledger::n_nodes)
       .def_property_readonly("n_pods", &Ledger::n_pods)
       .def_property_readonly("overflow_records_used", &Ledger::overflow_records_used)
+      .def_property_readonly("attached", &Ledger::attached, "processes attached to the region")
+      .def("put_pod_info",
+           [](Ledger& l, const std::string& key, py::bytes blob) { return l.put_pod_info(key, std::string(blob)); },
+           py::arg("key"), py::arg("blob"))
+      .def(
+          "take_pod_info",
+          [](Ledger& l, const std::string& key) -> py::object {
+            std::string b;
+            if (!l.take_pod_info(key, &b)) return py::none();
+            return py::bytes(b);
+          },
+          py::arg("key"))
       .def_property_readonly("epoch", &Ledger::epoch)
       .def(
           "upsert_node",
@@ -847,6 +859,8 @@ PYBIND11_MODULE(_native, m) {
         d["requests"] = f.requests.load();
         d["loop_max_s"] = static_cast<double>(f.loop_max_ns.load()) * 1e-9;
         d["spin_hits"] = f.spin_hits.load();
+        d["bind_handoffs"] = f.bind_handoffs.load();
+        d["pods_published"] = f.pods_published.load();
         py::list ph;
         for (const auto& x : f.phase_max_ns) ph.append(static_cast<double>(x.load()) * 1e-9);
         d["phase_max_s"] = ph;

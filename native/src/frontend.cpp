@@ -460,6 +460,65 @@ size_t Frontend::pod_cache_size() const {
   return pods_.size();
 }
 
+namespace {
+// CachedPod <-> the bytes of a bind handoff (Ledger::put_pod_info): namespace, name, container
+// names, owner, completed flag and demand; not the pod's JSON text.
+template <typename T>
+void put_raw(std::string* o, const T& v) {
+  o->append(reinterpret_cast<const char*>(&v), sizeof(T));
+}
+void put_str(std::string* o, std::string_view v) {
+  put_raw(o, static_cast<uint16_t>(std::min<size_t>(v.size(), 0xffff)));
+  o->append(v.data(), std::min<size_t>(v.size(), 0xffff));
+}
+void pack_pod(const CachedPod& p, std::string* o) {
+  o->clear();
+  put_str(o, p.ns);
+  put_str(o, p.name);
+  put_raw(o, static_cast<uint16_t>(p.containers.size()));
+  for (const auto& c : p.containers) put_str(o, c);
+  put_raw(o, p.owner);
+  put_raw(o, static_cast<uint8_t>(p.completed));
+  put_raw(o, p.demand.n);
+  o->append(reinterpret_cast<const char*>(p.demand.c), sizeof(ContainerDemand) * static_cast<size_t>(p.demand.n));
+}
+struct Reader {
+  std::string_view b;
+  bool ok = true;
+  template <typename T>
+  T raw() {
+    T v{};
+    if (b.size() < sizeof(T)) return ok = false, v;
+    std::memcpy(&v, b.data(), sizeof(T));
+    b.remove_prefix(sizeof(T));
+    return v;
+  }
+  std::string str() {
+    const uint16_t n = raw<uint16_t>();
+    if (!ok || b.size() < n) return ok = false, std::string();
+    std::string v(b.substr(0, n));
+    b.remove_prefix(n);
+    return v;
+  }
+};
+bool unpack_pod(std::string_view b, CachedPod* p) {
+  Reader r{b};
+  p->ns = r.str();
+  p->name = r.str();
+  const uint16_t nc = r.raw<uint16_t>();
+  for (uint16_t i = 0; r.ok && i < nc; ++i) p->containers.push_back(r.str());
+  p->owner = r.raw<uint64_t>();
+  p->completed = r.raw<uint8_t>() != 0;
+  std::memset(&p->demand, 0, sizeof(p->demand));
+  p->demand.n = r.raw<int32_t>();
+  if (!r.ok || p->demand.n < 0 || p->demand.n > kMaxContainers ||
+      r.b.size() != sizeof(ContainerDemand) * static_cast<size_t>(p->demand.n))
+    return false;
+  std::memcpy(p->demand.c, r.b.data(), r.b.size());
+  return true;
+}
+}  // namespace
+
 void Frontend::put_pod(std::string_view uid, CachedPod pod) {
   if (uid.empty()) return;
   std::lock_guard<std::mutex> g(pod_mu_);
@@ -493,9 +552,16 @@ void Frontend::prepare_bind(std::string_view body, PyRequest* r) {
     std::lock_guard<std::mutex> g(pod_mu_);
     atomic_max(&phase_max_ns[4], now_ns() - tw);
     auto it = pods_.find(uid);
-    if (it == pods_.end()) return;
-    pod = std::move(it->second);
-    pods_.erase(it);  // one bind per pod UID (the deque entry expires lazily)
+    if (it != pods_.end()) {
+      pod = std::move(it->second);
+      pods_.erase(it);  // one bind per pod UID (the deque entry expires lazily)
+    }
+  }
+  if (pod.name.empty()) {
+    // another worker process's filter parsed it (its bind came over another connection)
+    std::string blob;
+    if (!ledger_->take_pod_info(uid, &blob) || !unpack_pod(blob, &pod)) return;
+    bind_handoffs.fetch_add(1, std::memory_order_relaxed);
   }
   if (pod.name != name || pod.ns != ns || pod.completed) {
     r->pod_json = std::move(pod.raw);   // unusual: Python decides (and reports) with the object
@@ -1135,6 +1201,12 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     CachedPod cp = reused ? last.cached : std::move(cached);
     cp.raw.assign(reused ? std::string_view(last.raw) : d.raw(pod));
     cp.demand = dem;
+    if (ledger_->attached() > 1) {
+      // other worker processes share the ledger: the bind may reach one of them
+      thread_local std::string blob;
+      pack_pod(cp, &blob);
+      if (ledger_->put_pod_info(std::string(uid), blob)) pods_published.fetch_add(1, std::memory_order_relaxed);
+    }
     put_pod(uid, std::move(cp));
   }
   Plan p;

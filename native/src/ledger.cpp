@@ -19,7 +19,7 @@
 namespace nanogpu {
 
 static constexpr uint64_t kMagic = 0x4e414e4f47505531ULL;  // "NANOGPU1"
-static constexpr uint32_t kVersion = 11;  // 4: HBM pools; 5: cache lines; 6: sizes; 7: serving; 8: nominations; 9: stream owners; 10: overflow records; 11: node epoch
+static constexpr uint32_t kVersion = 12;  // 4: HBM pools; 5: cache lines; 6: sizes; 7: serving; 8: nominations; 9: stream owners; 10: overflow records; 11: node epoch; 12: bind handoff
 
 static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -76,6 +76,8 @@ uint32_t pods_per_shard_for(uint32_t max_pods) {
 }
 // pods with more than kSlotContainers containers are rare (one in 32 pods at most)
 uint32_t ext_records_for(uint32_t max_pods) { return std::max<uint32_t>(64, max_pods / 32); }
+// bind handoffs in flight at once: pods between their filter and their bind
+uint32_t info_slots_for(uint32_t max_pods) { return std::clamp<uint32_t>(max_pods / 16, 1024, 16384); }
 }  // namespace
 
 size_t Ledger::region_bytes(uint32_t max_nodes, uint32_t max_pods) {
@@ -83,7 +85,8 @@ size_t Ledger::region_bytes(uint32_t max_nodes, uint32_t max_pods) {
   const size_t n = align_up(sizeof(NodeSlot) * max_nodes, 4096);
   const size_t p = align_up(sizeof(PodSlot) * kPodShards * pods_per_shard_for(max_pods), 4096);
   const size_t e = align_up(sizeof(ExtRecord) * ext_records_for(max_pods), 4096);
-  return h + n + p + e;
+  const size_t i = align_up(sizeof(PodInfoSlot) * info_slots_for(max_pods), 4096);
+  return h + n + p + e + i;
 }
 
 Ledger::Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, bool create)
@@ -141,6 +144,8 @@ Ledger::Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, b
   ext_ = reinterpret_cast<ExtRecord*>(
       reinterpret_cast<char*>(pods_) +
       align_up(sizeof(PodSlot) * kPodShards * pods_per_shard_for(max_pods), 4096));
+  info_ = reinterpret_cast<PodInfoSlot*>(reinterpret_cast<char*>(ext_) +
+                                         align_up(sizeof(ExtRecord) * ext_records_for(max_pods), 4096));
   if (init) {
     hdr_->version = kVersion;
     hdr_->max_nodes = max_nodes;
@@ -163,6 +168,8 @@ Ledger::Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, b
     hdr_->ext_cap = ext_records_for(max_pods);
     hdr_->ext_hint.store(0);
     hdr_->ext_used.store(0);
+    hdr_->info_cap = info_slots_for(max_pods);
+    for (auto& m : hdr_->info_mu) init_mutex(&m.m);
     init_mutex(&hdr_->registry_mu);
     for (int s = 0; s < kPodShards; ++s) {
       init_mutex(&hdr_->shard_mu[s].m);
@@ -1121,6 +1128,34 @@ std::vector<std::string> Ledger::reconcile(const std::vector<std::string>& live,
   for (const std::string& k : gone)
     if (drop_committed(k) == kOk) released.push_back(k);
   return released;
+}
+
+bool Ledger::put_pod_info(const std::string& key, std::string_view blob) {
+  if (key.empty() || key.size() >= static_cast<size_t>(kKeyLen) || blob.size() > static_cast<size_t>(kPodInfoBytes))
+    return false;
+  const uint64_t h = key_hash(key.c_str());
+  const uint32_t i = static_cast<uint32_t>(h % hdr_->info_cap);
+  lock_mu(&hdr_->info_mu[i % kPodShards].m);
+  Unlock u{&hdr_->info_mu[i % kPodShards].m};
+  PodInfoSlot& s = info_[i];
+  s.hash = h;
+  std::memcpy(s.key, key.c_str(), key.size() + 1);
+  s.len = static_cast<uint32_t>(blob.size());
+  std::memcpy(s.data, blob.data(), blob.size());
+  return true;
+}
+
+bool Ledger::take_pod_info(const std::string& key, std::string* blob) {
+  if (key.empty() || key.size() >= static_cast<size_t>(kKeyLen)) return false;
+  const uint64_t h = key_hash(key.c_str());
+  const uint32_t i = static_cast<uint32_t>(h % hdr_->info_cap);
+  lock_mu(&hdr_->info_mu[i % kPodShards].m);
+  Unlock u{&hdr_->info_mu[i % kPodShards].m};
+  PodInfoSlot& s = info_[i];
+  if (s.hash != h || std::strncmp(s.key, key.c_str(), kKeyLen) != 0) return false;
+  blob->assign(s.data, std::min<uint32_t>(s.len, kPodInfoBytes));
+  s.hash = 0;
+  return true;
 }
 
 std::vector<std::string> Ledger::expired_nominations(double older_than_s) const {

@@ -4,6 +4,7 @@ Compat mode is pinned bit-for-bit to the reference oracle in test_parity.py /
 test_alloc_golden.py; these tests pin what the native mode adds: the HBM dimension,
 partition / xGMI / NUMA-aware multi-container placement and the ledger invariants.
 """
+import os
 import random
 
 from hypothesis import given, settings
@@ -409,3 +410,26 @@ def test_share_aware_learner_threshold_follows_the_streaming_curve():
     L2.set_pod_owner("b", "o-quarter")
     L2.set_mem_busy(nid2, 1, 30)
     assert L2.learn_stream_owners(True) == (0, 0)
+
+
+def test_bind_handoff_slots_put_take_and_size_limit(tmp_path):
+    """Ledger::put_pod_info / take_pod_info: a blob stored under a pod key is taken once by any
+    process attached to the region; one too large for a slot is refused (the bind then goes
+    the slow way)."""
+    path = f"/dev/shm/nanogpu-test-info-{os.getpid()}"
+    try:
+        a = N.Ledger(path, 8, 1024, True)
+        b = N.Ledger(path, 8, 1024, True)        # a second worker attaching
+        assert a.attached == 2 and b.attached == 2
+        assert a.put_pod_info("uid-1", b"\x01\x02payload")
+        assert b.take_pod_info("uid-2") is None
+        assert b.take_pod_info("uid-1") == b"\x01\x02payload"
+        assert a.take_pod_info("uid-1") is None  # taken once
+        assert not a.put_pod_info("uid-3", b"x" * 5000)
+        del b
+        assert a.attached == 1
+    finally:
+        try:
+            os.unlink(path)
+        except FileNotFoundError:
+            pass

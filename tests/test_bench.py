@@ -69,6 +69,8 @@ def test_bench_multi_rank_gloo(ranks):
     # the headline's N stand-ins are labelled as such; one scheduler over N workers alongside
     assert d["value_mode"].startswith(f"{ranks} independent kube-scheduler stand-ins")
     assert d["value_one_scheduler"] > 0 and d["steps_one_scheduler"] == 1
+    # binds the cycle's worker did not see stay native on the other workers (ledger handoff)
+    assert d["bind_handoffs_one_scheduler"] > 0
 
 
 def test_link_weights_fall_back_to_the_reader_and_a_matrix_sets_the_mesh():

@@ -270,3 +270,60 @@ def test_stop_with_binds_in_flight_answers_every_bind_and_leaves_the_ledger_clea
             srv.stop()
 
     asyncio.run(main())
+
+
+def test_bind_on_another_worker_process_stays_native_through_the_ledger_handoff():
+    """Two extender workers on one shared ledger (what `--workers N` runs, and the bench's
+    ranks): kube-scheduler's filter reaches one worker and its bind, sent on another
+    connection, the other. The bind worker never saw the pod, so it takes the pod the filter
+    parsed from the ledger (Ledger::take_pod_info) and binds natively; a bind whose pod no
+    filter published goes to the Python path, which reads the pod from the API server."""
+    import os
+
+    async def main():
+        store = FakeKubeStore()
+        store.add_node(pu.make_node("n0", 8, synthetic_mi355x(8).to_json()))
+        runner, port = await serve(store)
+        path = f"/dev/shm/nanogpu-test-handoff-{os.getpid()}"
+        rts = []
+        try:
+            for w in range(2):
+                rt = Runtime(Config(kube_api=f"http://127.0.0.1:{port}", port=0, host="127.0.0.1",
+                                    policy_config_path="/nonexistent", ledger_path=path), worker=w)
+                await rt.start()
+                rts.append(rt)
+            a, b = (f"http://127.0.0.1:{rt.bound_port}" for rt in rts)
+            assert rts[0].state.ledger.attached >= 2
+            p = store.create_pod(pu.make_pod("h", [("main", 30, 4096)]))
+            m = pu.meta(p)
+            bind = {"PodName": "h", "PodNamespace": m["namespace"], "PodUID": m["uid"], "Node": "n0"}
+            async with aiohttp.ClientSession() as s:
+                async with s.post(f"{a}/scheduler/filter", json={"Pod": p, "NodeNames": ["n0"]}) as r:
+                    assert (await r.json())["NodeNames"] == ["n0"]
+                async with s.post(f"{b}/scheduler/bind", json=bind) as r:
+                    assert (await r.json()) == {"Error": ""}
+                fa, fb = rts[0].native.fe.stats(), rts[1].native.fe.stats()
+                assert fa["pods_published"] == 1 and fb["bind_handoffs"] == 1
+                assert rts[1].native.fe.kube_writer_stats()["ok"] == 1      # the native writer bound it
+                got = store.get_pod("default", "h")
+                assert got["spec"]["nodeName"] == "n0"
+                assert got["metadata"]["annotations"]["nano-gpu/container-main"]
+                rec = rts[0].state.ledger.lookup(m["uid"])
+                assert rec["state"] == "committed" and rec["demand"] == [(30, 4096)]
+                # no filter published this one: the Python path binds it from the API object
+                q = store.create_pod(pu.make_pod("q", [("main", 20)]))
+                mq = pu.meta(q)
+                async with s.post(f"{b}/scheduler/bind", json={**bind, "PodName": "q", "PodUID": mq["uid"]}) as r:
+                    assert (await r.json()) == {"Error": ""}
+                assert rts[1].native.fe.stats()["bind_handoffs"] == 1
+                assert store.get_pod("default", "q")["spec"]["nodeName"] == "n0"
+        finally:
+            for rt in rts:
+                await rt.stop()
+            await runner.cleanup()
+            try:
+                os.unlink(path)
+            except FileNotFoundError:
+                pass
+
+    asyncio.run(main())
