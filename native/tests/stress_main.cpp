@@ -220,6 +220,35 @@ static void relist_gap(int iters) {
   std::printf("relist ok: %d ghosts, %d reconciled\n", ghosts.load(), reconciled.load());
 }
 
+// Bind handoff slots (Ledger::put_pod_info / take_pod_info) under concurrency: writers and
+// takers on colliding slots never see a torn or foreign blob.
+static void handoff(int iters) {
+  Ledger l("", 8, 1024, true);   // 1024 slots: keys collide on purpose
+  std::atomic<int> taken{0};
+  std::vector<std::thread> ts;
+  for (int t = 0; t < 4; ++t)
+    ts.emplace_back([&, t] {
+      std::string blob;
+      for (int i = 0; i < iters; ++i) {
+        const std::string key = "h" + std::to_string(t) + "-" + std::to_string(i % 700);
+        const std::string want(64 + (i % 200), static_cast<char>('a' + t));
+        CHECK(l.put_pod_info(key, want + key));
+        const std::string other = "h" + std::to_string((t + 1) % 4) + "-" + std::to_string(i % 700);
+        for (const std::string* k : {&key, &other}) {
+          if (!l.take_pod_info(*k, &blob)) continue;
+          // a blob always ends with its own key and is one writer's byte repeated before it
+          CHECK(blob.size() > k->size() && blob.compare(blob.size() - k->size(), k->size(), *k) == 0);
+          const char c = blob[0];
+          for (size_t j = 0; j + k->size() < blob.size(); ++j) CHECK(blob[j] == c);
+          taken.fetch_add(1);
+        }
+      }
+    });
+  for (auto& t : ts) t.join();
+  CHECK(taken.load() > 0);
+  std::printf("handoff ok: %d taken\n", taken.load());
+}
+
 // Native API server + native bind writers under concurrency (see the header comment).
 static void apiserver_and_writers(int pods, bool evented) {
   apisrv::Config cfg;
@@ -497,5 +526,6 @@ int main(int argc, char** argv) {
   apiserver_and_writers(std::max(50, iters / 20), true);    // one epoll writer thread
   apiserver_and_writers(std::max(50, iters / 20), false);   // blocking writer threads
   relist_gap(std::max(200, iters / 4));
+  handoff(std::max(500, iters));
   return 0;
 }
