@@ -339,6 +339,15 @@ class NanoGpuPlugin:
             total = self.topo.devices[devs[0]].hbm_mib if devs else 0
             if total:
                 r.envs["NANO_GPU_MEMORY_FRACTION"] = f"{min(1.0, mib / total):.6f}"
+                if mib < total:
+                    # the HIP runtime's own view (ROCclr): the device reports this share of its
+                    # memory as its total (hipMemGetInfo, hipDeviceProp.totalGlobalMem) and
+                    # refuses any single allocation above it, so programs that size themselves
+                    # from the total fit the budget. Whole percents, rounded up: never below the
+                    # grant; the exact budget is the allocator cap guest.apply sets. Measured on
+                    # MI355X: the runtime does not cap the sum of allocations
+                    # (profiles/gpu_calibration.md).
+                    r.envs["GPU_MAX_HEAP_SIZE"] = str(min(100, -(-100 * mib // total)))
         r.annotations["nano-gpu/devices"] = r.envs["NANO_GPU_DEVICES"]
         ns, pname = pu.pod_ns_name(pod)
         try:

@@ -140,6 +140,9 @@ def test_device_plugin_end_to_end(tmp_path):
             # binpack put both shares on device 0: "a" (20%) gets 6 units = 48 CUs
             assert env["NANO_GPU_DEVICES"] == "0" and env["HSA_CU_MASK"] == "0:0-47"
             assert env["NANO_GPU_MEMORY_MIB"] == str(32 * 1024) and float(env["NANO_GPU_MEMORY_FRACTION"]) > 0.1
+            # the HIP runtime's view of the device: the budget in whole percents, rounded up
+            total = float(env["NANO_GPU_MEMORY_MIB"]) / float(env["NANO_GPU_MEMORY_FRACTION"])
+            assert int(env["GPU_MAX_HEAP_SIZE"]) == -(-100 * 32 * 1024 // round(total))
             paths = [d.container_path for d in ra.container_responses[0].devices]
             assert paths == ["/dev/kfd", "/dev/dri/renderD128"]
             rb = await stub.Allocate(D.AllocateRequest(container_requests=[
@@ -244,6 +247,13 @@ def test_guest_reads_grant(monkeypatch):
     monkeypatch.setenv("NANO_GPU_MEMORY_FRACTION", "0.25")
     g = guest.grant()
     assert g["percent"] == 20 and g["cu_mask"] == "0:0-47" and g["memory_fraction"] == 0.25
+    # with the exact budget, the allocator's fraction is relative to what the runtime reports
+    # (GPU_MAX_HEAP_SIZE already cut it to the rounded-up budget)
+    monkeypatch.setenv("NANO_GPU_MEMORY_MIB", "16384")
+    g = guest.grant()
+    assert abs(guest.allocator_fraction(g, 17693.0) - 16384 / 17693) < 1e-9
+    assert guest.allocator_fraction(g, 0.0) == 0.25
+    assert guest.allocator_fraction({"memory_mib": 0, "memory_fraction": 0.25}, 17693.0) == 0.25
 
 
 def test_ras_errors_make_devices_unhealthy_end_to_end(tmp_path):

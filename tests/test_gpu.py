@@ -231,6 +231,79 @@ def test_device_plugin_env_is_honoured_by_rocr():
     assert part["small_ok"] is True and part["big_ok"] is False
 
 
+_HEAP_CHILD = r'''
+import json, os, sys
+sys.path.insert(0, os.environ["REPO"])
+import torch
+from nanogpu.agent import guest
+applied = guest.apply(0) if os.environ.get("APPLY") == "1" else False
+free, total = torch.cuda.mem_get_info(0)
+out = {"applied": applied, "total_mib": total >> 20}
+def fits(mib):
+    try:
+        x = torch.empty(int(mib) << 20, dtype=torch.uint8, device="cuda")
+        del x
+        return True
+    except RuntimeError:
+        return False
+    finally:
+        torch.cuda.empty_cache()
+for k, v in json.loads(os.environ["SIZES"]).items():
+    out[k] = fits(v)
+if os.environ.get("SUM"):
+    blocks, got = [], 0
+    try:
+        while got < int(os.environ["SUM"]):
+            blocks.append(torch.empty(1024 << 20, dtype=torch.uint8, device="cuda"))
+            got += 1024
+    except RuntimeError:
+        pass
+    out["sum_mib"] = got
+print(json.dumps(out))
+'''
+
+
+def test_hbm_budget_reaches_the_hip_runtime():
+    """The device plugin's HBM budget (nanogpu/agent/plugin.py): GPU_MAX_HEAP_SIZE makes the
+    HIP runtime report the rounded-up budget as the device's total and refuse any single
+    allocation above it, for any HIP program; guest.apply then caps PyTorch's allocator at the
+    exact budget, relative to that reported total. What the runtime does NOT do is cap the sum
+    of allocations (pinned here, so the README's claim stays true)."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parent.parent
+
+    def child(env_extra):
+        env = dict(os.environ, REPO=str(root), **env_extra)
+        env.pop("PYTORCH_HIP_ALLOC_CONF", None)
+        r = subprocess.run([sys.executable, "-c", _HEAP_CHILD], env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        return json.loads(r.stdout.strip().splitlines()[-1])
+
+    import torch
+
+    device_mib = torch.cuda.get_device_properties(0).total_memory >> 20
+    budget = 16384
+    pct = -(-100 * budget // device_mib)
+    cap = device_mib * pct // 100
+    env = {"GPU_MAX_HEAP_SIZE": str(pct), "NANO_GPU_MEMORY_MIB": str(budget),
+           "NANO_GPU_MEMORY_FRACTION": f"{budget / device_mib:.6f}", "APPLY": "1",
+           "SIZES": json.dumps({"under_budget": budget * 0.85, "over_budget": budget * 1.05})}
+    a = child(env)
+    # runtime alone (no allocator cap, caching off: every tensor is its own hipMalloc)
+    b = child({"GPU_MAX_HEAP_SIZE": str(pct), "PYTORCH_NO_HIP_MEMORY_CACHING": "1",
+               "SIZES": json.dumps({"under_cap": cap * 0.9, "over_cap": cap * 1.1}), "SUM": str(int(1.5 * cap))})
+    record("hbm_budget_runtime", {"device_mib": device_mib, "budget_mib": budget, "gpu_max_heap_size": pct,
+                                  "reported_total_mib": a["total_mib"], "guest": a, "runtime_only": b})
+    assert abs(a["total_mib"] - cap) <= 2 and a["applied"]
+    assert a["under_budget"] and not a["over_budget"]            # the exact budget (allocator)
+    assert b["under_cap"] and not b["over_cap"]                  # one allocation over the cap
+    assert b["sum_mib"] > cap                                    # the sum is not capped
+
+
 def test_agent_metrics_read_real_amdgpu_sysfs(host, P):
     """The node agent's /metrics reads gpu_busy_percent and VRAM use from the real device; VRAM
     used grows by what a process allocates and the busy counter is a percentage."""
