@@ -376,7 +376,13 @@ class NativeServer:
                   "# TYPE nanogpu_native_deferred_total counter",
                   f"nanogpu_native_deferred_total {s['python']['deferred']}",
                   "# TYPE nanogpu_native_connections_total counter",
-                  f"nanogpu_native_connections_total {s['connections']}"]
+                  f"nanogpu_native_connections_total {s['connections']}",
+                  "# HELP nanogpu_native_bind_handoffs_total binds answered natively with the pod another "
+                  "worker process's filter parsed (shared-ledger handoff)",
+                  "# TYPE nanogpu_native_bind_handoffs_total counter",
+                  f"nanogpu_native_bind_handoffs_total {s.get('bind_handoffs', 0)}",
+                  "# TYPE nanogpu_native_pods_published_total counter",
+                  f"nanogpu_native_pods_published_total {s.get('pods_published', 0)}"]
         kw = self.fe.kube_writer_stats()
         if kw is not None:
             lines += ["# HELP nanogpu_native_binds_total binds finished by the native API writer",

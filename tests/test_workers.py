@@ -87,6 +87,18 @@ def test_two_workers_share_one_ledger():
             assert len(views) == 1
             free = json.loads(views.pop())
             assert sum(100 - x for v in free.values() for x in v) == 30 * bound
+            # with two workers on the ledger, every filter publishes its pod for a bind that
+            # lands on the other worker (the shared-ledger handoff)
+            published = 0
+            for _ in range(8):
+                r, w = await asyncio.open_connection("127.0.0.1", port)
+                w.write(b"GET /metrics HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n")
+                text = (await r.read()).decode()
+                w.close()
+                for line in text.splitlines():
+                    if line.startswith("nanogpu_native_pods_published_total "):
+                        published = max(published, float(line.split()[1]))
+            assert published > 0
         finally:
             os.killpg(proc.pid, signal.SIGTERM)
             try:
