@@ -103,6 +103,8 @@ def parse_args():
     ap.add_argument("--inflight-binds", type=int, default=64)
     ap.add_argument("--bind-writer-mode", choices=["evented", "threads"], default="evented",
                     help="the extender's native bind writer: one epoll thread, or blocking threads")
+    ap.add_argument("--no-assume-label", action="store_true",
+                    help="the extender binds with the binding alone (no label PATCH): one API write per bind")
     ap.add_argument("--no-native-pod-watch", action="store_true",
                     help="the extender reads its pod watch with aiohttp on the event loop (A/B of the "
                          "native watch thread)")
@@ -753,7 +755,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                  busy_poll_us=args.busy_poll_us, frontend_threads=args.frontend_threads,
                  nominate=not args.no_nominate,
                  bind_writer_threads=args.bind_writer_threads or max(2, 16 // d.world),
-                 bind_writer_mode=args.bind_writer_mode)
+                 bind_writer_mode=args.bind_writer_mode, assume_label=not args.no_assume_label)
     all_steps_pre = [10_000 + w for w in range(args.warmup)] + list(range(args.steps))
     rt = Runtime(cfg, worker=d.rank if shared else 0, api=rt_api)
     await rt.start()

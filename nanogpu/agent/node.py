@@ -130,8 +130,10 @@ class NodeAgent:
             return
         self.plugin = NanoGpuPlugin(self.topo, self.api, self.node, self.render_minors())
         # pods on this node: CU grants are rebuilt from the synced informer's view (the API
-        # server is the checkpoint), and released when pods finish or go away
-        self.informer = Informer(self.api, "pods", label_selector=f"{T.LABEL_GPU_ASSUME}=true")
+        # server is the checkpoint), and released when pods finish or go away. Selected by node
+        # (as kubelet watches), not by the assume label: each agent sees its own node's pods,
+        # not every GPU pod of the cluster, and a label that lands after the binding is no gap
+        self.informer = Informer(self.api, "pods", field_selector=f"{T.NODE_NAME_FIELD}={self.node}")
         self.informer.add_handler(self._on_pod)
         self.tasks.append(self.informer.start())
         await self.informer.synced.wait()

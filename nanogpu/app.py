@@ -50,6 +50,9 @@ class Config:
     bind_writer_threads: int = 16               # x KubeWriter::kBatch (8) binds in flight
     bind_writer_mode: str = "evented"           # evented (one epoll thread) | threads (blocking threads)
     native_pod_watch: bool = True               # a C++ thread reads and filters the pod watch (podwatch.cpp)
+    # the reference's `nano-gpu/assume` label, PATCHed beside the binding; off: one write a bind
+    # (the binding carries the annotations; this project's agent selects pods by node)
+    assume_label: bool = True
     reservation_ttl_s: float = 60.0
     nominate: bool = True              # priorities nominate the top node (Ledger::nominate)
     nomination_ttl_s: float = 5.0
@@ -156,7 +159,7 @@ class Runtime:
             await self.pod_informer.synced.wait()
             await self.controllers[-1].queue.drain(30.0)   # initial ADDs rebuild the ledger
         self.extender = Extender(self.state, self.api, self.metrics, self.tracer,
-                                 verify_pod_on_bind=self.cfg.verify_pod_on_bind)
+                                 verify_pod_on_bind=self.cfg.verify_pod_on_bind, assume_label=self.cfg.assume_label)
         # policy file: real hot reload
         self.watcher = PolicyWatcher(self.cfg.policy_config_path, self.cfg.policy_reload_s)
         self.watcher.subscribe(self._apply_policy)
@@ -207,7 +210,8 @@ class Runtime:
                 if self.cfg.native_bind_writes and not self.cfg.verify_pod_on_bind and api_cfg is not None:
                     ext = self.extender
                     if self.native.enable_native_writes(api_cfg, self.cfg.bind_writer_threads, ext.api_retries,
-                                                        ext.record_events, self.cfg.bind_writer_mode == "evented"):
+                                                        ext.record_events, self.cfg.bind_writer_mode == "evented",
+                                                        self.cfg.assume_label):
                         log.info("worker %d: bind API writes in native writer threads (%d)", self.worker,
                                  self.cfg.bind_writer_threads)
                 self.native.start()

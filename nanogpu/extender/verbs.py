@@ -53,8 +53,9 @@ class PodCache:
 class Extender:
     def __init__(self, state: ClusterState, api, metrics: Metrics | None = None,
                  tracer: Tracer | None = None, verify_pod_on_bind: bool = False,
-                 api_retries: int = 2, record_events: bool = True):
+                 api_retries: int = 2, record_events: bool = True, assume_label: bool = True):
         self.state = state
+        self.assume_label = assume_label   # PATCH the reference's assume label beside the binding
         self.api = api
         self.metrics = metrics or Metrics()
         self.tracer = tracer or Tracer()
@@ -299,7 +300,10 @@ class Extender:
                     if not e.conflict or pu.node_name_of(await self.api.get_pod(ns, name)) != node:
                         raise
 
-            if getattr(self.api, "completes_inline", False):
+            if not self.assume_label:
+                t3 = time.perf_counter()      # the binding alone carries the annotations
+                await write_binding()
+            elif getattr(self.api, "completes_inline", False):
                 await write_patch()
                 t3 = time.perf_counter()
                 await write_binding()

@@ -309,13 +309,15 @@ class KubeClient:
 
     # --------------------------------------------------------------------- watch
     async def watch(self, resource: str, resource_version: str, timeout_s: int = 300,
-                    label_selector: str | None = None) -> AsyncIterator[dict]:
+                    label_selector: str | None = None, field_selector: str | None = None) -> AsyncIterator[dict]:
         """Streams watch events ({type, object}) for `pods` or `nodes` cluster-wide."""
         s = await self._s()
         params = {"watch": "1", "resourceVersion": resource_version, "timeoutSeconds": str(timeout_s),
                   "allowWatchBookmarks": "true"}
         if label_selector:
             params["labelSelector"] = label_selector
+        if field_selector:
+            params["fieldSelector"] = field_selector
         url = f"{self.config.server}/api/v1/{resource}?{urllib.parse.urlencode(params)}"
         async with s.get(url, timeout=aiohttp.ClientTimeout(total=None, sock_read=timeout_s + 30),
                          headers=self._auth()) as r:
@@ -363,7 +365,7 @@ class KubeClient:
 
     async def watch_batches(self, resource: str, resource_version: str, timeout_s: int = 300,
                             label_selector: str | None = None, slim: bool = False,
-                            watch_filter=None) -> AsyncIterator[list[dict]]:
+                            watch_filter=None, field_selector: str | None = None) -> AsyncIterator[list[dict]]:
         """`watch`, one list per network read: every complete event line that arrived together.
         slim (pods): each Pod decoded natively down to what the pod informer reads
         (nanogpu._native.decode_pod_watch) instead of json.loads of the whole object; a
@@ -378,6 +380,8 @@ class KubeClient:
                   "allowWatchBookmarks": "true"}
         if label_selector:
             params["labelSelector"] = label_selector
+        if field_selector:
+            params["fieldSelector"] = field_selector
         if decode is not None and watch_filter is not None and self.native_watch:
             async for batch in self._native_watch(f"/api/v1/{resource}?{urllib.parse.urlencode(params)}",
                                                   watch_filter, timeout_s + 30):

@@ -303,8 +303,8 @@ class FakeKubeStore:
         return le
 
     # ------------------------------------------------------------------ watch
-    async def watch_batches(self, kind: str, resource_version: str, label_selector: str | None = None
-                            ) -> AsyncIterator[list[dict]]:
+    async def watch_batches(self, kind: str, resource_version: str, label_selector: str | None = None,
+                            field_selector: str | None = None) -> AsyncIterator[list[dict]]:
         """Watch stream delivered as batches: everything emitted since the consumer last ran
         arrives as one list (one wake-up per burst instead of one queue hop per event)."""
         try:
@@ -335,8 +335,9 @@ class FakeKubeStore:
                 end = None in batch
                 if end:
                     batch = batch[:batch.index(None)]
-                if label_selector:
-                    batch = [ev for ev in batch if ev["type"] == "ERROR" or _match_labels(ev["object"], label_selector)]
+                if label_selector or field_selector:
+                    batch = [ev for ev in batch if ev["type"] == "ERROR" or
+                             (_match_labels(ev["object"], label_selector) and _match_fields(ev["object"], field_selector))]
                 if batch:
                     yield batch
                 if end:
@@ -346,9 +347,9 @@ class FakeKubeStore:
                 timer.cancel()
             self.watchers[kind].remove(buf)
 
-    async def watch(self, kind: str, resource_version: str, label_selector: str | None = None
-                    ) -> AsyncIterator[dict]:
-        async for batch in self.watch_batches(kind, resource_version, label_selector):
+    async def watch(self, kind: str, resource_version: str, label_selector: str | None = None,
+                    field_selector: str | None = None) -> AsyncIterator[dict]:
+        async for batch in self.watch_batches(kind, resource_version, label_selector, field_selector):
             for ev in batch:
                 yield ev
 
@@ -459,11 +460,11 @@ class InProcKube:
         self.store.add_event({"namespace": ns, "involvedObject": involved, "reason": reason,
                               "message": message, "type": etype})
 
-    def watch(self, resource, resource_version, timeout_s=300, label_selector=None):
-        return self.store.watch(resource, resource_version, label_selector)   # no extra async-gen hop
+    def watch(self, resource, resource_version, timeout_s=300, label_selector=None, field_selector=None):
+        return self.store.watch(resource, resource_version, label_selector, field_selector)   # no extra async-gen hop
 
-    def watch_batches(self, resource, resource_version, timeout_s=300, label_selector=None):
-        return self.store.watch_batches(resource, resource_version, label_selector)
+    def watch_batches(self, resource, resource_version, timeout_s=300, label_selector=None, field_selector=None):
+        return self.store.watch_batches(resource, resource_version, label_selector, field_selector)
 
     async def get_lease(self, ns, name):
         await self._rtt()
@@ -495,10 +496,11 @@ def make_app(store: FakeKubeStore) -> web.Application:
         if store.faults.latency_s > 0:
             await asyncio.sleep(store.faults.latency_s)
 
-    async def stream_watch(request: web.Request, kind: str, label_selector=None) -> web.StreamResponse:
+    async def stream_watch(request: web.Request, kind: str, label_selector=None, field_selector=None
+                           ) -> web.StreamResponse:
         resp = web.StreamResponse(headers={"Content-Type": "application/json"})
         try:
-            gen = store.watch(kind, request.query.get("resourceVersion", "0"), label_selector)
+            gen = store.watch(kind, request.query.get("resourceVersion", "0"), label_selector, field_selector)
             await resp.prepare(request)
             async for ev in gen:
                 await resp.write(json.dumps(ev, separators=(",", ":")).encode() + b"\n")
@@ -526,7 +528,7 @@ def make_app(store: FakeKubeStore) -> web.Application:
         await lat()
         ls, fs = request.query.get("labelSelector"), request.query.get("fieldSelector")
         if request.query.get("watch") in ("1", "true"):
-            return await stream_watch(request, "pods", ls)
+            return await stream_watch(request, "pods", ls, fs)
         items, rv = store.list_pods(ls, fs)
         return listing("PodList", items, rv)
 

@@ -35,10 +35,12 @@ def _rv(o: dict) -> str:
 
 class Informer:
     def __init__(self, api, resource: str, label_selector: str | None = None,
-                 resync_s: float = 0.0, key=None, slim: bool = False, prefilter=None):
+                 resync_s: float = 0.0, key=None, slim: bool = False, prefilter=None,
+                 field_selector: str | None = None):
         self.api = api
         self.resource = resource               # "pods" | "nodes"
         self.label_selector = label_selector
+        self.field_selector = field_selector   # pods: e.g. spec.nodeName=<node> (a node agent)
         self.resync_s = resync_s
         self.key = key or (_pod_key if resource == "pods" else _node_key)
         self.store: dict[str, dict] = {}
@@ -89,7 +91,9 @@ class Informer:
 
     async def _list(self) -> None:
         before = time.monotonic()      # CLOCK_MONOTONIC, the ledger's clock (ledger.cpp mono_now)
-        if self.resource == "pods":
+        if self.resource == "pods" and self.field_selector:
+            items, rv = await self.api.list_pods(label_selector=self.label_selector, field_selector=self.field_selector)
+        elif self.resource == "pods":
             items, rv = await self.api.list_pods(label_selector=self.label_selector)
         else:
             items, rv = await self.api.list_nodes(label_selector=self.label_selector)
@@ -164,11 +168,13 @@ class Informer:
     async def _watch(self) -> None:
         # API objects that can (the in-process store, the REST client) deliver the stream in
         # batches: one loop wake-up per burst of events rather than one per event
+        kw = {"field_selector": self.field_selector} if self.field_selector else {}
         if hasattr(self.api, "watch_batches"):
-            kw = {"slim": True, "watch_filter": self.watch_filter} if self.slim else {}
+            if self.slim:
+                kw.update(slim=True, watch_filter=self.watch_filter)
             stream = self.api.watch_batches(self.resource, self.rv, label_selector=self.label_selector, **kw)
         else:
-            stream = _singletons(self.api.watch(self.resource, self.rv, label_selector=self.label_selector))
+            stream = _singletons(self.api.watch(self.resource, self.rv, label_selector=self.label_selector, **kw))
         try:
             await self._consume(stream)
         finally:

@@ -118,8 +118,10 @@ struct KubeWriterStats {
 class KubeWriter {
  public:
   using Respond = std::function<void(uint64_t id, int status, const std::string& body)>;
+  // `label`: also PATCH the assume label (and the annotations again) beside the binding, the
+  // reference's pod contract; false: the binding alone, which carries the annotations.
   KubeWriter(KubeTarget target, std::shared_ptr<Ledger> ledger, Respond respond, int threads, int retries,
-             bool record_events, bool evented = true);
+             bool record_events, bool evented = true, bool label = true);
   ~KubeWriter();
   void submit(BindJob job);
   void stop();
@@ -158,6 +160,7 @@ class KubeWriter {
   Respond respond_;
   int retries_;
   bool events_;
+  bool label_ = true;
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<BindJob> q_;

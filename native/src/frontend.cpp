@@ -372,11 +372,12 @@ Frontend::Frontend(std::shared_ptr<Ledger> ledger, const std::string& host, int 
 
 Frontend::~Frontend() { stop(); }
 
-void Frontend::set_kube_writer(const KubeTarget& t, int threads, int retries, bool record_events, bool evented) {
+void Frontend::set_kube_writer(const KubeTarget& t, int threads, int retries, bool record_events, bool evented,
+                               bool label) {
   if (writer_.load()) throw std::logic_error("Frontend: the kube writer is already set");
   writer_owner_ = std::make_unique<KubeWriter>(
       t, ledger_, [this](uint64_t id, int status, const std::string& body) { respond(id, status, "application/json", body); },
-      threads, retries, record_events, evented);
+      threads, retries, record_events, evented, label);
   writer_.store(writer_owner_.get(), std::memory_order_release);
 }
 

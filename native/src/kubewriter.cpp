@@ -413,9 +413,10 @@ int HttpConn::request(const char* method, const std::string& path, const std::st
 
 // ------------------------------------------------------------------------------ KubeWriter
 KubeWriter::KubeWriter(KubeTarget target, std::shared_ptr<Ledger> ledger, Respond respond, int threads, int retries,
-                       bool record_events, bool evented)
+                       bool record_events, bool evented, bool label)
     : t_(std::move(target)), ledger_(std::move(ledger)), respond_(std::move(respond)), retries_(retries),
       events_(record_events), evented_(evented) {
+  label_ = label;
   ctx_ = make_ssl_ctx(t_);
   token_ = t_.token;
   if (!t_.token_file.empty()) {
@@ -590,12 +591,12 @@ void KubeWriter::process_batch(std::vector<BindJob>& jobs, std::vector<std::uniq
   for (size_t i = 0; i < n; ++i) {
     build(jobs[i], &patch[i], &binding[i]);
     const std::string base = "/api/v1/namespaces/" + jobs[i].ns + "/pods/" + jobs[i].name;
-    conns[2 * i]->start("PATCH", base, kMergePatch, patch[i], a);
+    if (label_) conns[2 * i]->start("PATCH", base, kMergePatch, patch[i], a);
     conns[2 * i + 1]->start("POST", base + "/binding", kJson, binding[i], a);
   }
   for (size_t i = 0; i < n; ++i) {
     sb[i] = conns[2 * i + 1]->finish(&rb[i]);
-    sp[i] = conns[2 * i]->finish(&rp[i]);
+    sp[i] = label_ ? conns[2 * i]->finish(&rp[i]) : 200;   // no label: nothing else to write
   }
   stats.binding_ns.fetch_add(now_ns() - t1, std::memory_order_relaxed);   // the pairs, in flight together
   for (size_t i = 0; i < n; ++i) {

@@ -447,9 +447,13 @@ void KubeWriter::io_loop() {
       build(jb->j, &jb->patch, &jb->binding);
       slots[static_cast<size_t>(s)] = std::move(jb);
       ++inflight;
+      if (!label_) {   // the binding alone carries the annotations
+        slots[static_cast<size_t>(s)]->left = 1;
+        slots[static_cast<size_t>(s)]->sp = 200;
+      }
       // the binding first: it is the one kube-scheduler's bind waits on
       launch(s, 1);
-      if (slots[static_cast<size_t>(s)]) launch(s, 0);
+      if (label_ && slots[static_cast<size_t>(s)]) launch(s, 0);
     }
     for (size_t i = 0; i < kick.size(); ++i) drive(kick[i], 0);   // fail() may append
     kick.clear();

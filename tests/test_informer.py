@@ -242,3 +242,38 @@ def test_reconcile_leaves_reservations_nominations_and_late_commits_alone():
     for k in ("reserved", "nominated", "late", "after"):
         assert led.lookup(k) is not None, k
     assert led.reconcile([], before) == ["late"]     # a committed pod the LIST lacks goes
+
+
+@pytest.mark.parametrize("kind", ["python", "native"])
+def test_node_agent_informer_selects_its_node_by_field(kind):
+    """The node agent's pod informer (agent/node.py) selects `spec.nodeName=<node>` on the LIST
+    and the WATCH, as kubelet does: a pod appears once it is bound to this node, pods bound
+    elsewhere never arrive, and its deletion does."""
+    async def main():
+        srv = _PyApi() if kind == "python" else _NativeApi()
+        url = await srv.start([node("n0"), node("n1")])
+        api = KubeClient(KubeConfig(server=url))
+        early = await api.create_pod(pu.make_pod("early", [("c", 10)]))
+        await api.bind_pod("default", "early", pu.pod_uid(early), "n1", {"nano-gpu/assume": "true"})
+        inf = Informer(api, "pods", field_selector="spec.nodeName=n1")
+        inf.start()
+        try:
+            await asyncio.wait_for(inf.synced.wait(), 5)
+            assert [pu.meta(p)["name"] for p in inf.list()] == ["early"]      # the LIST is selected too
+            a = await api.create_pod(pu.make_pod("a", [("c", 10)]))
+            b = await api.create_pod(pu.make_pod("b", [("c", 10)]))
+            await asyncio.sleep(0.1)
+            assert inf.get("default/a") is None and inf.get("default/b") is None   # pending: no node yet
+            await api.bind_pod("default", "a", pu.pod_uid(a), "n0", {"nano-gpu/assume": "true"})
+            await api.bind_pod("default", "b", pu.pod_uid(b), "n1", {"nano-gpu/assume": "true"})
+            assert await wait_for(lambda: inf.get("default/b") is not None)
+            assert inf.get("default/a") is None
+            await api.delete_pod("default", "b")
+            assert await wait_for(lambda: inf.get("default/b") is None)
+            assert inf.get("default/a") is None
+        finally:
+            await inf.stop()
+            await api.close()
+            await srv.stop()
+
+    asyncio.run(main())

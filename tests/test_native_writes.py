@@ -327,3 +327,37 @@ def test_bind_on_another_worker_process_stays_native_through_the_ledger_handoff(
                 pass
 
     asyncio.run(main())
+
+
+@pytest.mark.parametrize("native", ["evented", "threads", False])
+def test_no_assume_label_binds_with_one_api_write(native):
+    """`--no-assume-label`: the binding alone (it carries the placement annotations, which
+    kube-apiserver sets with spec.nodeName) — one API write per bind instead of two, no label."""
+    async def main():
+        store = FakeKubeStore()
+        store.add_node(pu.make_node("n0", 8, synthetic_mi355x(8).to_json()))
+        runner, port = await serve(store)
+        rt = Runtime(Config(kube_api=f"http://127.0.0.1:{port}", port=0, host="127.0.0.1",
+                            policy_config_path="/nonexistent", native_bind_writes=bool(native),
+                            bind_writer_mode=native or "evented", assume_label=False))
+        await rt.start()
+        base = f"http://127.0.0.1:{rt.bound_port}"
+        try:
+            patches0 = store.counts.get("patch_pod", 0)
+            for i in range(3):
+                p = store.create_pod(pu.make_pod(f"p{i}", [("main", 20)]))
+                status, res = await _schedule(base, p, "n0")
+                assert status == 200 and res == {"Error": ""}, res
+                got = store.get_pod("default", f"p{i}")
+                assert got["spec"]["nodeName"] == "n0"
+                ann = got["metadata"]["annotations"]
+                assert ann["nano-gpu/assume"] == "true" and ann["nano-gpu/container-main"]
+                assert T.LABEL_GPU_ASSUME not in (got["metadata"].get("labels") or {})
+                assert rt.state.ledger.lookup(pu.pod_uid(p))["state"] == "committed"
+            assert store.counts.get("bind_pod", 0) == 3
+            assert store.counts.get("patch_pod", 0) == patches0     # no label PATCH
+        finally:
+            await rt.stop()
+            await runner.cleanup()
+
+    asyncio.run(main())
