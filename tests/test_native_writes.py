@@ -272,7 +272,8 @@ def test_stop_with_binds_in_flight_answers_every_bind_and_leaves_the_ledger_clea
     asyncio.run(main())
 
 
-def test_bind_on_another_worker_process_stays_native_through_the_ledger_handoff():
+@pytest.mark.parametrize("native_writes", [True, False])
+def test_bind_on_another_worker_process_stays_native_through_the_ledger_handoff(native_writes):
     """Two extender workers on one shared ledger (what `--workers N` runs, and the bench's
     ranks): kube-scheduler's filter reaches one worker and its bind, sent on another
     connection, the other. The bind worker never saw the pod, so it takes the pod the filter
@@ -289,7 +290,8 @@ def test_bind_on_another_worker_process_stays_native_through_the_ledger_handoff(
         try:
             for w in range(2):
                 rt = Runtime(Config(kube_api=f"http://127.0.0.1:{port}", port=0, host="127.0.0.1",
-                                    policy_config_path="/nonexistent", ledger_path=path), worker=w)
+                                    policy_config_path="/nonexistent", ledger_path=path,
+                                    native_bind_writes=native_writes), worker=w)
                 await rt.start()
                 rts.append(rt)
             a, b = (f"http://127.0.0.1:{rt.bound_port}" for rt in rts)
@@ -304,7 +306,8 @@ def test_bind_on_another_worker_process_stays_native_through_the_ledger_handoff(
                     assert (await r.json()) == {"Error": ""}
                 fa, fb = rts[0].native.fe.stats(), rts[1].native.fe.stats()
                 assert fa["pods_published"] == 1 and fb["bind_handoffs"] == 1
-                assert rts[1].native.fe.kube_writer_stats()["ok"] == 1      # the native writer bound it
+                if native_writes:
+                    assert rts[1].native.fe.kube_writer_stats()["ok"] == 1  # the native writer bound it
                 got = store.get_pod("default", "h")
                 assert got["spec"]["nodeName"] == "n0"
                 assert got["metadata"]["annotations"]["nano-gpu/container-main"]
