@@ -107,11 +107,14 @@ struct ExtRecord {
 // process receives it. kube-scheduler sends binds from per-pod goroutines on other keep-alive
 // connections than its scheduling cycle's, and SO_REUSEPORT spreads connections over the
 // workers, so with several workers the bind usually lands on a worker whose own pod cache
-// never saw the pod. Direct-mapped by key hash; an entry a newer pod overwrote just sends
-// its bind the slow way (Python, which reads the pod from the API server).
-constexpr int kPodInfoBytes = 1008;
+// never saw the pod. Buckets of kPodInfoWays slots by key hash, the oldest entry of a full
+// bucket replaced; an entry a newer pod replaced just sends its bind the slow way (Python,
+// which reads the pod from the API server).
+constexpr int kPodInfoBytes = 1000;
+constexpr int kPodInfoWays = 4;
 struct PodInfoSlot {
-  uint64_t hash;   // key_hash(key), 0: empty
+  uint64_t hash;    // key_hash(key), 0: empty
+  uint64_t stamp;   // insertion order within the region (the oldest of a full bucket goes)
   char key[kKeyLen];
   uint32_t len;
   uint32_t pad;
@@ -159,8 +162,9 @@ struct LedgerHeader {
   uint32_t ext_cap;                 // overflow records (pods over kSlotContainers containers)
   std::atomic<uint32_t> ext_hint;   // where the next claim starts looking
   std::atomic<int32_t> ext_used;
-  uint32_t info_cap;                // bind-handoff slots (PodInfoSlot)
-  PaddedMutex info_mu[kPodShards];  // slot i is guarded by info_mu[i % kPodShards]
+  uint32_t info_cap;                // bind-handoff slots (PodInfoSlot), a multiple of kPodInfoWays
+  std::atomic<uint64_t> info_stamp;
+  PaddedMutex info_mu[kPodShards];  // bucket b is guarded by info_mu[b % kPodShards]
 };
 
 struct NodeSnapshot {

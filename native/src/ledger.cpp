@@ -19,7 +19,7 @@
 namespace nanogpu {
 
 static constexpr uint64_t kMagic = 0x4e414e4f47505531ULL;  // "NANOGPU1"
-static constexpr uint32_t kVersion = 12;  // 4: HBM pools; 5: cache lines; 6: sizes; 7: serving; 8: nominations; 9: stream owners; 10: overflow records; 11: node epoch; 12: bind handoff
+static constexpr uint32_t kVersion = 13;  // 4: HBM pools; 5: cache lines; 6: sizes; 7: serving; 8: nominations; 9: stream owners; 10: overflow records; 11: node epoch; 12-13: bind handoff
 
 static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -77,7 +77,9 @@ uint32_t pods_per_shard_for(uint32_t max_pods) {
 // pods with more than kSlotContainers containers are rare (one in 32 pods at most)
 uint32_t ext_records_for(uint32_t max_pods) { return std::max<uint32_t>(64, max_pods / 32); }
 // bind handoffs in flight at once: pods between their filter and their bind
-uint32_t info_slots_for(uint32_t max_pods) { return std::clamp<uint32_t>(max_pods / 16, 1024, 16384); }
+uint32_t info_slots_for(uint32_t max_pods) {
+  return std::clamp<uint32_t>(max_pods / 16, 1024, 16384) / kPodInfoWays * kPodInfoWays;
+}
 }  // namespace
 
 size_t Ledger::region_bytes(uint32_t max_nodes, uint32_t max_pods) {
@@ -169,6 +171,7 @@ Ledger::Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, b
     hdr_->ext_hint.store(0);
     hdr_->ext_used.store(0);
     hdr_->info_cap = info_slots_for(max_pods);
+    hdr_->info_stamp.store(0);
     for (auto& m : hdr_->info_mu) init_mutex(&m.m);
     init_mutex(&hdr_->registry_mu);
     for (int s = 0; s < kPodShards; ++s) {
@@ -1134,28 +1137,43 @@ bool Ledger::put_pod_info(const std::string& key, std::string_view blob) {
   if (key.empty() || key.size() >= static_cast<size_t>(kKeyLen) || blob.size() > static_cast<size_t>(kPodInfoBytes))
     return false;
   const uint64_t h = key_hash(key.c_str());
-  const uint32_t i = static_cast<uint32_t>(h % hdr_->info_cap);
-  lock_mu(&hdr_->info_mu[i % kPodShards].m);
-  Unlock u{&hdr_->info_mu[i % kPodShards].m};
-  PodInfoSlot& s = info_[i];
-  s.hash = h;
-  std::memcpy(s.key, key.c_str(), key.size() + 1);
-  s.len = static_cast<uint32_t>(blob.size());
-  std::memcpy(s.data, blob.data(), blob.size());
+  const uint32_t bucket = static_cast<uint32_t>(h % (hdr_->info_cap / kPodInfoWays));
+  lock_mu(&hdr_->info_mu[bucket % kPodShards].m);
+  Unlock u{&hdr_->info_mu[bucket % kPodShards].m};
+  PodInfoSlot* b = &info_[bucket * kPodInfoWays];
+  PodInfoSlot* s = nullptr;
+  for (int w = 0; w < kPodInfoWays && !s; ++w)   // the key's own slot, else an empty one
+    if (b[w].hash == h && std::strncmp(b[w].key, key.c_str(), kKeyLen) == 0) s = &b[w];
+  for (int w = 0; w < kPodInfoWays && !s; ++w)
+    if (b[w].hash == 0) s = &b[w];
+  if (!s) {   // a full bucket: the oldest entry goes
+    s = &b[0];
+    for (int w = 1; w < kPodInfoWays; ++w)
+      if (b[w].stamp < s->stamp) s = &b[w];
+  }
+  s->hash = h;
+  s->stamp = hdr_->info_stamp.fetch_add(1, std::memory_order_relaxed) + 1;
+  std::memcpy(s->key, key.c_str(), key.size() + 1);
+  s->len = static_cast<uint32_t>(blob.size());
+  std::memcpy(s->data, blob.data(), blob.size());
   return true;
 }
 
 bool Ledger::take_pod_info(const std::string& key, std::string* blob) {
   if (key.empty() || key.size() >= static_cast<size_t>(kKeyLen)) return false;
   const uint64_t h = key_hash(key.c_str());
-  const uint32_t i = static_cast<uint32_t>(h % hdr_->info_cap);
-  lock_mu(&hdr_->info_mu[i % kPodShards].m);
-  Unlock u{&hdr_->info_mu[i % kPodShards].m};
-  PodInfoSlot& s = info_[i];
-  if (s.hash != h || std::strncmp(s.key, key.c_str(), kKeyLen) != 0) return false;
-  blob->assign(s.data, std::min<uint32_t>(s.len, kPodInfoBytes));
-  s.hash = 0;
-  return true;
+  const uint32_t bucket = static_cast<uint32_t>(h % (hdr_->info_cap / kPodInfoWays));
+  lock_mu(&hdr_->info_mu[bucket % kPodShards].m);
+  Unlock u{&hdr_->info_mu[bucket % kPodShards].m};
+  PodInfoSlot* b = &info_[bucket * kPodInfoWays];
+  for (int w = 0; w < kPodInfoWays; ++w) {
+    PodInfoSlot& s = b[w];
+    if (s.hash != h || std::strncmp(s.key, key.c_str(), kKeyLen) != 0) continue;
+    blob->assign(s.data, std::min<uint32_t>(s.len, kPodInfoBytes));
+    s.hash = 0;
+    return true;
+  }
+  return false;
 }
 
 std::vector<std::string> Ledger::expired_nominations(double older_than_s) const {

@@ -426,6 +426,13 @@ def test_bind_handoff_slots_put_take_and_size_limit(tmp_path):
         assert b.take_pod_info("uid-1") == b"\x01\x02payload"
         assert a.take_pod_info("uid-1") is None  # taken once
         assert not a.put_pod_info("uid-3", b"x" * 5000)
+        # 4-way buckets: 300 pods in flight over 1024 slots all survive but a handful (a
+        # direct-mapped table would lose about one in eight to collisions)
+        keys = [f"pod-{i:04d}" for i in range(300)]
+        for k in keys:
+            assert a.put_pod_info(k, k.encode())
+        got = sum(b.take_pod_info(k) == k.encode() for k in keys)
+        assert got >= 290, got
         del b
         assert a.attached == 1
     finally:
