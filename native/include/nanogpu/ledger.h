@@ -51,11 +51,21 @@ struct NodeSlot {
   char name[kNameLen];                              // written at registration only
   int32_t in_use;
   int32_t n_devs;
-  alignas(64) std::atomic<uint64_t> generation;
   alignas(64) pthread_mutex_t mu;
   int32_t n_pods;                                   // under mu
   alignas(64) Topology topo;
   Device devs[kMaxDevs];
+};
+
+// What a filter reads of every node it is sent: its generation (the plan cache's key) and
+// whether the slot is live. One dense array (16 bytes a node) instead of a line inside each
+// 20 KB node slot: a request over 420 nodes reads 105 consecutive cache lines, which the
+// hardware prefetches, instead of 420 scattered ones. A bind's write shares its line with three
+// other nodes' entries, a small cost against the reads (hundreds per bind).
+struct NodeHot {
+  std::atomic<uint64_t> gen;      // bumps on every change to the node (under its mutex)
+  std::atomic<int32_t> in_use;
+  int32_t pad;
 };
 
 struct alignas(64) PaddedMutex {   // one line per pod-shard lock (no false sharing)
@@ -325,6 +335,7 @@ class Ledger {
 
  private:
   NodeSlot* node(int32_t id) const;
+  std::atomic<uint64_t>& gen_of(const NodeSlot* n) const { return hot_[n - nodes_].gen; }
   PodSlot* shard(int s) const;
   int shard_of(uint64_t h) const { return static_cast<int>(h % kPodShards); }
   int32_t reserve_as(int32_t id, const std::string& key, const Demand& d, const Options& o, Plan* plan,
@@ -347,6 +358,7 @@ class Ledger {
   size_t bytes_ = 0;
   char* base_ = nullptr;
   LedgerHeader* hdr_ = nullptr;
+  NodeHot* hot_ = nullptr;
   NodeSlot* nodes_ = nullptr;
   PodSlot* pods_ = nullptr;
   ExtRecord* ext_ = nullptr;

@@ -222,6 +222,92 @@ static uint64_t text_hash(std::string_view s) {
   return h ^ (h >> 29);
 }
 
+// A JSON array of plain strings written compactly, `["a","b"]` (what kube-scheduler's Go encoder
+// sends), into name views and token views (quotes included). false: any other shape (spaces,
+// escapes, non-strings), which the caller hands to the JSON parser.
+static bool scan_string_array(std::string_view t, std::vector<std::string_view>* nv,
+                              std::vector<std::string_view>* nraw) {
+  if (t.size() < 2 || t.front() != '[' || t.back() != ']') return false;
+  size_t p = 1;
+  if (t.size() == 2) return true;
+  for (;;) {
+    if (p >= t.size() || t[p] != '"') return false;
+    const char* q = static_cast<const char*>(std::memchr(t.data() + p + 1, '"', t.size() - p - 1));
+    if (!q) return false;
+    const size_t e = static_cast<size_t>(q - t.data());
+    const std::string_view name = t.substr(p + 1, e - p - 1);
+    for (char ch : name)
+      if (ch == '\\' || static_cast<unsigned char>(ch) < 0x20) return false;
+    nv->push_back(name);
+    nraw->push_back(t.substr(p, e - p + 1));
+    p = e + 1;
+    if (p == t.size() - 1) return true;
+    if (t[p] != ',') return false;
+    ++p;
+  }
+}
+
+namespace {
+// name -> node id for this thread, valid for one node epoch: open addressing on the name's hash,
+// names kept in an arena so a lookup compares bytes in a few cache lines of its own
+struct NameTable {
+  const Ledger* owner = nullptr;
+  uint64_t epoch = 0;
+  struct Slot {
+    uint64_t h = 0;   // 0: empty
+    uint32_t off = 0, len = 0;
+    int32_t id = -1;
+  };
+  std::vector<Slot> slots;
+  std::string arena;
+  size_t used = 0;
+  void reset(const Ledger* o, uint64_t e) {
+    owner = o;
+    epoch = e;
+    slots.assign(1024, Slot{});
+    arena.clear();
+    used = 0;
+  }
+  int32_t find(std::string_view name) const {
+    if (slots.empty()) return -1;
+    const uint64_t h = text_hash(name) | 1;
+    const size_t mask = slots.size() - 1;
+    for (size_t i = h & mask;; i = (i + 1) & mask) {
+      const Slot& s = slots[i];
+      if (s.h == 0) return -1;
+      if (s.h == h && s.len == name.size() && std::memcmp(arena.data() + s.off, name.data(), name.size()) == 0)
+        return s.id;
+    }
+  }
+  void insert(std::string_view name, int32_t id) {
+    if ((used + 1) * 2 > slots.size()) {   // keep it at most half full
+      std::vector<Slot> old;
+      old.swap(slots);
+      slots.assign(old.size() * 2, Slot{});
+      used = 0;
+      for (const Slot& s : old)
+        if (s.h) place(s);
+    }
+    Slot s;
+    s.h = text_hash(name) | 1;
+    s.off = static_cast<uint32_t>(arena.size());
+    s.len = static_cast<uint32_t>(name.size());
+    s.id = id;
+    arena.append(name);
+    place(s);
+  }
+  void place(const Slot& s) {
+    const size_t mask = slots.size() - 1;
+    for (size_t i = s.h & mask;; i = (i + 1) & mask)
+      if (slots[i].h == 0) {
+        slots[i] = s;
+        ++used;
+        return;
+      }
+  }
+};
+}  // namespace
+
 static void atomic_max(std::atomic<uint64_t>* m, uint64_t v) {
   uint64_t cur = m->load(std::memory_order_relaxed);
   while (v > cur && !m->compare_exchange_weak(cur, v, std::memory_order_relaxed)) {
@@ -1097,61 +1183,90 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   thread_local std::vector<std::string_view> nraw;   // each name's JSON token, quotes included
   nv.clear();
   nraw.clear();
+  // The node lists of the last kListSlots distinct texts this thread resolved (LRU). With
+  // kube-scheduler's node sampling (numFeasibleNodesToFind from a rotating start) the list is
+  // a window of the cluster that moves every cycle, but the windows repeat: 1000 nodes sampled
+  // 420 at a time cycle through 50 of them, so a few dozen slots catch them all.
+  constexpr int kListSlots = 64;
   struct IdCache {
     const Ledger* owner = nullptr;
-    uint64_t key[4] = {};
-    uint64_t epoch[4] = {};     // the ledger's node epoch the ids were checked at
-    size_t len[4] = {};
-    std::vector<int32_t> ids[4];
-    std::vector<std::pair<uint32_t, uint32_t>> tok[4];   // token (offset, length) in the list text
-    unsigned next = 0;
+    uint64_t key[kListSlots] = {};
+    uint64_t epoch[kListSlots] = {};     // the ledger's node epoch the ids were checked at
+    uint64_t used[kListSlots] = {};
+    size_t len[kListSlots] = {};
+    bool compact[kListSlots] = {};       // the text is `["a","b",...]` exactly: a reply may copy it whole
+    std::vector<int32_t> ids[kListSlots];
+    std::vector<std::pair<uint32_t, uint32_t>> tok[kListSlots];   // token (offset, length) in the list text
+    uint64_t clock = 0;
   };
   thread_local IdCache idc;
   if (idc.owner != ledger_.get()) idc = IdCache{}, idc.owner = ledger_.get();
   const uint64_t nkey = text_hash(raw_names) | 1;   // 0 marks an empty slot
   const uint64_t epoch = ledger_->node_epoch();
   int slot = -1;
-  for (int k = 0; k < 4; ++k)
+  for (int k = 0; k < kListSlots && slot < 0; ++k)
     if (idc.key[k] == nkey && idc.len[k] == raw_names.size()) slot = k;
+  // a cached list's names are read through its token offsets into this request's text (no
+  // per-request copy of 2 x N views); a list parsed now fills nv / nraw
+  const std::vector<std::pair<uint32_t, uint32_t>>* toks = nullptr;
   if (slot >= 0) {
     // the same list text as before: its tokens sit at the same offsets (escape-free lists
     // only are cached); names and ids come from the cache
-    for (const auto& t : idc.tok[slot]) {
-      nraw.push_back(raw_names.substr(t.first, t.second));
-      nv.push_back(raw_names.substr(t.first + 1, t.second - 2));
-    }
+    toks = &idc.tok[slot];
   } else {
-    thread_local json::Doc dn;
-    if (!dn.parse(raw_names) || !dn.is(dn.root(), json::Type::kArr)) return false;
-    bool plain = true;
-    for (int32_t c = dn.at(dn.root()).first; c >= 0; c = dn.at(c).next) {
-      if (!dn.is(c, json::Type::kStr)) return false;
-      nv.push_back(dn.str(c));
-      // the token is reused as written unless it holds an escape (then it is re-quoted, so
-      // the reply stays byte-identical to the Python verb's json.dumps)
-      const std::string_view tok = dn.raw(c);
-      if (tok.size() == nv.back().size() + 2) {
-        nraw.push_back(tok);
-      } else {
-        plain = false;
-        thread_local std::deque<std::string> requoted;   // stable storage for this request
-        if (nraw.empty()) requoted.clear();
-        requoted.emplace_back();
-        json::append_quoted(&requoted.back(), nv.back());
-        nraw.push_back(requoted.back());
+    // the common shape first, scanned directly: ["a","b",...] with no escapes; anything else
+    // (whitespace, escapes, other types) goes through the JSON parser
+    bool plain = scan_string_array(raw_names, &nv, &nraw);
+    if (!plain) {
+      nv.clear();
+      nraw.clear();
+      thread_local json::Doc dn;
+      if (!dn.parse(raw_names) || !dn.is(dn.root(), json::Type::kArr)) return false;
+      plain = true;
+      for (int32_t c = dn.at(dn.root()).first; c >= 0; c = dn.at(c).next) {
+        if (!dn.is(c, json::Type::kStr)) return false;
+        nv.push_back(dn.str(c));
+        // the token is reused as written unless it holds an escape (then it is re-quoted, so
+        // the reply stays byte-identical to the Python verb's json.dumps)
+        const std::string_view tok = dn.raw(c);
+        if (tok.size() == nv.back().size() + 2) {
+          nraw.push_back(tok);
+        } else {
+          plain = false;
+          thread_local std::deque<std::string> requoted;   // stable storage for this request
+          if (nraw.empty()) requoted.clear();
+          requoted.emplace_back();
+          json::append_quoted(&requoted.back(), nv.back());
+          nraw.push_back(requoted.back());
+        }
       }
     }
-    slot = static_cast<int>(idc.next++ % 4);
+    slot = 0;
+    for (int k = 1; k < kListSlots; ++k)
+      if (idc.used[k] < idc.used[slot]) slot = k;
     idc.key[slot] = plain ? nkey : 0;   // a list with escapes is parsed every time
     idc.len[slot] = raw_names.size();
     idc.epoch[slot] = 0;                // ids checked below
     idc.ids[slot].assign(nv.size(), -1);
     idc.tok[slot].clear();
+    size_t joined = nraw.empty() ? 2 : 1 + nraw.size();   // brackets and commas
     if (plain)
-      for (const std::string_view t : nraw)
+      for (const std::string_view t : nraw) {
         idc.tok[slot].emplace_back(static_cast<uint32_t>(t.data() - raw_names.data()), static_cast<uint32_t>(t.size()));
+        joined += t.size();
+      }
+    idc.compact[slot] = plain && joined == raw_names.size();
   }
-  const int32_t nn = static_cast<int32_t>(nv.size());
+  idc.used[slot] = ++idc.clock;
+  auto raw_at = [&](size_t i) -> std::string_view {
+    return toks ? raw_names.substr((*toks)[i].first, (*toks)[i].second) : nraw[i];
+  };
+  auto name_at = [&](size_t i) -> std::string_view {
+    if (!toks) return nv[i];
+    const auto& t = (*toks)[i];
+    return raw_names.substr(t.first + 1, t.second - 2);
+  };
+  const int32_t nn = static_cast<int32_t>(toks ? toks->size() : nv.size());
   // node ids: any unknown node goes to Python, which can register it from its informer. The
   // ids of a cached list are re-checked (slot `id` still carries that name, else the ledger's
   // name index) only when a node was added or removed since (the ledger's epoch moved).
@@ -1160,31 +1275,22 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     // names this worker resolved before, by a hash of the name (no string, no lock): with
     // kube-scheduler's node sampling the list is a different window of the cluster every
     // cycle, so the per-list cache above misses while every name in it is known
-    struct NameIds {
-      const Ledger* owner = nullptr;
-      uint64_t epoch = 0;
-      std::unordered_map<uint64_t, int32_t> by_hash;
-    };
-    thread_local NameIds nid;
-    if (nid.owner != ledger_.get() || nid.epoch != epoch) {
-      nid.by_hash.clear();
-      nid.owner = ledger_.get();
-      nid.epoch = epoch;
-    }
-    for (size_t i = 0; i < nv.size(); ++i) {
-      if (ids[i] >= 0 && ledger_->node_named(ids[i], nv[i])) continue;
-      const uint64_t h = text_hash(nv[i]);
-      auto it = nid.by_hash.find(h);
-      if (it != nid.by_hash.end() && ledger_->node_named(it->second, nv[i])) {
-        ids[i] = it->second;
-        continue;
+    thread_local NameTable nid;
+    if (nid.owner != ledger_.get() || nid.epoch != epoch) nid.reset(ledger_.get(), epoch);
+    for (size_t i = 0; i < static_cast<size_t>(nn); ++i) {
+      const std::string_view name = name_at(i);
+      // the table holds its own copy of every name (a compact arena): a hit touches neither
+      // the ledger's node slots nor its lock, and is exact (names compared, not only hashed)
+      int32_t id = nid.find(name);
+      if (id < 0) {
+        id = ledger_->find_node(std::string(name));
+        if (id < 0) {
+          idc.key[slot] = 0;
+          return false;
+        }
+        nid.insert(name, id);
       }
-      ids[i] = ledger_->find_node(std::string(nv[i]));
-      if (ids[i] < 0) {
-        idc.key[slot] = 0;
-        return false;
-      }
-      nid.by_hash[h] = ids[i];
+      ids[i] = id;
     }
     idc.epoch[slot] = epoch;
   }
@@ -1219,18 +1325,23 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     ledger_->assume_many(ids.data(), static_cast<int>(ids.size()), dem, o, rcs.data(), scores.data());
     // written straight into the reply; a fitting node's name is its request token, as is
     r.clear();
-    r += "{\"Nodes\":null,\"NodeNames\":[";
-    bool first = true, any_failed = false;
-    for (size_t i = 0; i < ids.size(); ++i) {
-      if (rcs[i] != kOk) {
-        any_failed = true;
-        continue;
+    r += "{\"Nodes\":null,\"NodeNames\":";
+    bool any_failed = false;
+    for (size_t i = 0; i < ids.size() && !any_failed; ++i) any_failed = rcs[i] != kOk;
+    bool first = true;
+    if (!any_failed && toks && idc.compact[slot]) {
+      r += raw_names;   // every node fits: the request's own list is the answer
+    } else {
+      r += '[';
+      for (size_t i = 0; i < ids.size(); ++i) {
+        if (rcs[i] != kOk) continue;
+        if (!first) r += ',';
+        r += raw_at(i);
+        first = false;
       }
-      if (!first) r += ',';
-      r += nraw[i];
-      first = false;
+      r += ']';
     }
-    r += "],\"FailedNodes\":{";
+    r += ",\"FailedNodes\":{";
     if (any_failed) {
       // "can't allocate <demand> on node <name>: <reason>" per failing node, written in place:
       // the demand text, the reasons (alloc.cpp err_str) and an escape-free name (its request
@@ -1252,18 +1363,19 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
       for (size_t i = 0; i < ids.size(); ++i) {
         if (rcs[i] == kOk) continue;
         if (!first) r += ',';
-        r += nraw[i];
-        if (nraw[i].size() == nv[i].size() + 2) {
+        const std::string_view tok = raw_at(i), name = name_at(i);
+        r += tok;
+        if (tok.size() == name.size() + 2) {
           r += ":\"can't allocate ";
           r += dstr;
           r += " on node ";
-          r += nv[i];
+          r += name;
           r += ": ";
           r += err_str(rcs[i]);
           r += '"';
         } else {
           r += ':';
-          json::append_quoted(&r, "can't allocate " + dstr + " on node " + std::string(nv[i]) + ": " + err_str(rcs[i]));
+          json::append_quoted(&r, "can't allocate " + dstr + " on node " + std::string(name) + ": " + err_str(rcs[i]));
         }
         first = false;
       }
@@ -1310,19 +1422,28 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
       for (int32_t& s : scores) s = std::max(0, std::min(10, static_cast<int32_t>(std::nearbyint(s / 10.0))));
     }
   }
-  r.clear();
-  r += '[';
-  char num[16];
+  // [{"Host":<token>,"Score":<n>},...] written through a pointer into a buffer sized for the
+  // worst case (no per-append capacity checks: 420 nodes are 2,000 small writes)
+  constexpr std::string_view kHost = "{\"Host\":", kScore = ",\"Score\":";
+  size_t cap = 2;
+  for (size_t i = 0; i < ids.size(); ++i) cap += raw_at(i).size() + kHost.size() + kScore.size() + 14;
+  r.resize(cap);
+  char* w = r.data();
+  *w++ = '[';
   for (size_t i = 0; i < ids.size(); ++i) {
-    if (i) r += ',';
-    r += "{\"Host\":";
-    r += nraw[i];
-    r += ",\"Score\":";
-    const auto res = std::to_chars(num, num + sizeof num, scores[i]);
-    r.append(num, static_cast<size_t>(res.ptr - num));
-    r += '}';
+    if (i) *w++ = ',';
+    const std::string_view tok = raw_at(i);
+    std::memcpy(w, kHost.data(), kHost.size());
+    w += kHost.size();
+    std::memcpy(w, tok.data(), tok.size());
+    w += tok.size();
+    std::memcpy(w, kScore.data(), kScore.size());
+    w += kScore.size();
+    w = std::to_chars(w, w + 12, scores[i]).ptr;
+    *w++ = '}';
   }
-  r += ']';
+  *w++ = ']';
+  r.resize(static_cast<size_t>(w - r.data()));
   return true;
 }
 

@@ -19,7 +19,7 @@
 namespace nanogpu {
 
 static constexpr uint64_t kMagic = 0x4e414e4f47505531ULL;  // "NANOGPU1"
-static constexpr uint32_t kVersion = 13;  // 4: HBM pools; 5: cache lines; 6: sizes; 7: serving; 8: nominations; 9: stream owners; 10: overflow records; 11: node epoch; 12-13: bind handoff
+static constexpr uint32_t kVersion = 14;  // 4: HBM pools; 5: cache lines; 6: sizes; 7: serving; 8: nominations; 9: stream owners; 10: overflow records; 11: node epoch; 12-13: bind handoff; 14: dense node generations
 
 static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -83,7 +83,7 @@ uint32_t info_slots_for(uint32_t max_pods) {
 }  // namespace
 
 size_t Ledger::region_bytes(uint32_t max_nodes, uint32_t max_pods) {
-  const size_t h = align_up(sizeof(LedgerHeader), 4096);
+  const size_t h = align_up(sizeof(LedgerHeader), 4096) + align_up(sizeof(NodeHot) * max_nodes, 4096);
   const size_t n = align_up(sizeof(NodeSlot) * max_nodes, 4096);
   const size_t p = align_up(sizeof(PodSlot) * kPodShards * pods_per_shard_for(max_pods), 4096);
   const size_t e = align_up(sizeof(ExtRecord) * ext_records_for(max_pods), 4096);
@@ -140,7 +140,8 @@ Ledger::Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, b
     base_ = static_cast<char*>(p);
   }
   hdr_ = reinterpret_cast<LedgerHeader*>(base_);
-  nodes_ = reinterpret_cast<NodeSlot*>(base_ + align_up(sizeof(LedgerHeader), 4096));
+  hot_ = reinterpret_cast<NodeHot*>(base_ + align_up(sizeof(LedgerHeader), 4096));
+  nodes_ = reinterpret_cast<NodeSlot*>(reinterpret_cast<char*>(hot_) + align_up(sizeof(NodeHot) * max_nodes, 4096));
   pods_ = reinterpret_cast<PodSlot*>(reinterpret_cast<char*>(nodes_) +
                                      align_up(sizeof(NodeSlot) * max_nodes, 4096));
   ext_ = reinterpret_cast<ExtRecord*>(
@@ -365,7 +366,7 @@ int32_t Ledger::upsert_node(const std::string& name, const Device* devs, int n,
     std::memset(s.name, 0, kNameLen);
     std::strncpy(s.name, name.c_str(), kNameLen - 1);
     init_mutex(&s.mu);
-    s.generation.store(1);
+    hot_[id].gen.store(1);
     s.n_devs = n;
     s.n_pods = 0;
     s.topo = topo;
@@ -378,6 +379,7 @@ int32_t Ledger::upsert_node(const std::string& name, const Device* devs, int n,
       s.devs[i].mem_busy = 0;
     }
     s.in_use = 1;
+    hot_[id].in_use.store(1, std::memory_order_release);
     hdr_->n_nodes.store(count + 1, std::memory_order_release);
     hdr_->node_epoch.fetch_add(1, std::memory_order_release);
   } else {
@@ -417,7 +419,7 @@ int32_t Ledger::upsert_node(const std::string& name, const Device* devs, int n,
     std::memcpy(s.devs, merged, sizeof(Device) * m);
     s.n_devs = m;
     s.topo = topo;
-    s.generation.fetch_add(1);
+    gen_of(&s).fetch_add(1);
   }
   hdr_->epoch.fetch_add(1);
   {
@@ -455,7 +457,8 @@ bool Ledger::remove_node(int32_t id) {
   Unlock un{&n->mu};
   if (n->n_pods > 0) return false;
   n->in_use = 0;
-  n->generation.fetch_add(1);
+  hot_[id].in_use.store(0, std::memory_order_release);
+  gen_of(n).fetch_add(1);
   hdr_->epoch.fetch_add(1);
   hdr_->node_epoch.fetch_add(1, std::memory_order_release);
   std::lock_guard<std::mutex> g(names_mu_);
@@ -469,7 +472,7 @@ bool Ledger::snapshot(int32_t id, NodeSnapshot* out) const {
   lock_node(n);
   Unlock un{&n->mu};
   out->n_devs = n->n_devs;
-  out->generation = n->generation.load(std::memory_order_relaxed);
+  out->generation = gen_of(n).load(std::memory_order_relaxed);
   out->topo = n->topo;
   std::memcpy(out->devs, n->devs, sizeof(Device) * n->n_devs);
   return true;
@@ -477,7 +480,7 @@ bool Ledger::snapshot(int32_t id, NodeSnapshot* out) const {
 
 uint64_t Ledger::generation(int32_t id) const {
   NodeSlot* n = node(id);
-  return n ? n->generation.load(std::memory_order_acquire) : 0;
+  return n ? gen_of(n).load(std::memory_order_acquire) : 0;
 }
 
 namespace {
@@ -561,7 +564,7 @@ std::vector<Ledger::CachedPlan> Ledger::cached_plans(int32_t id) const {
   NodeSlot* n = node(id);
   NodeCache* cp = n ? node_cache(id, false) : nullptr;
   if (!cp) return out;
-  const uint64_t gen = n->generation.load(std::memory_order_acquire);
+  const uint64_t gen = gen_of(n).load(std::memory_order_acquire);
   cp->lock();
   for (const CacheEntry& e : cp->e)
     if (e.used.load(kRlx) && e.gen.load(kRlx) == gen)
@@ -657,13 +660,13 @@ void Ledger::assume_many(const int32_t* ids, int count, const Demand& d, const O
   Plan plan;
   for (int i = 0; i < count; ++i) {
     const int32_t id = ids[i];
-    NodeSlot* n = node(id);
     score[i] = 0;
-    if (!n || !n->in_use) {
+    // only the dense NodeHot array on a memo hit: the node slot is touched on a miss alone
+    if (id < 0 || id >= n_nodes || !hot_[id].in_use.load(std::memory_order_acquire)) {
       rc[i] = kErrUnknownNode;
       continue;
     }
-    const uint64_t gen = n->generation.load(std::memory_order_acquire);
+    const uint64_t gen = hot_[id].gen.load(std::memory_order_acquire);
     ScoreMemo::E* me = static_cast<size_t>(id) < memo.e.size() ? &memo.e[id] : nullptr;
     if (me && me->gen == gen + 1) {
       rc[i] = me->rc;
@@ -694,7 +697,7 @@ int32_t Ledger::assume(int32_t id, const Demand& d, const Options& o_in, Plan* p
   const Options o = resolve(o_in, d);
   const uint64_t dh = d.hash(), oh = o.hash();
   int32_t rc;
-  if (cache_get(CacheKey{id, n->generation.load(std::memory_order_acquire), dh, oh}, &rc, plan)) return rc;
+  if (cache_get(CacheKey{id, gen_of(n).load(std::memory_order_acquire), dh, oh}, &rc, plan)) return rc;
   NodeSnapshot snap;
   if (!snapshot(id, &snap)) return kErrUnknownNode;
   rc = choose(snap.devs, snap.n_devs, &snap.topo, d, o, plan);
@@ -768,7 +771,7 @@ int32_t Ledger::reserve_as(int32_t id, const std::string& key, const Demand& d, 
       return kOkExisting;
     }
   }
-  const uint64_t gen = n->generation.load(std::memory_order_relaxed);
+  const uint64_t gen = gen_of(n).load(std::memory_order_relaxed);
   const CacheKey k{id, gen, d.hash(), o.hash()};
   int32_t rc = kOk;
   const bool hit = cache_get(k, &rc, plan);
@@ -796,7 +799,7 @@ int32_t Ledger::reserve_as(int32_t id, const std::string& key, const Demand& d, 
     p->state = state;
   }
   ++n->n_pods;
-  n->generation.fetch_add(1, std::memory_order_release);
+  gen_of(n).fetch_add(1, std::memory_order_release);
   hdr_->n_pods.fetch_add(1);
   hdr_->epoch.fetch_add(1);
   if (state == kPodNominated) hdr_->nom_made.fetch_add(1, std::memory_order_relaxed);
@@ -850,7 +853,7 @@ int32_t Ledger::allocate_plan(int32_t id, const std::string& key, const Demand& 
     p->state = committed ? kPodCommitted : kPodReserved;
   }
   ++n->n_pods;
-  n->generation.fetch_add(1, std::memory_order_release);
+  gen_of(n).fetch_add(1, std::memory_order_release);
   hdr_->n_pods.fetch_add(1);
   hdr_->epoch.fetch_add(1);
   note_request(d);
@@ -907,7 +910,7 @@ int32_t Ledger::release_if(const std::string& key, int32_t only_state) {
   --hdr_->shard_live[s];
   ++hdr_->shard_tomb[s];
   --n->n_pods;
-  n->generation.fetch_add(1, std::memory_order_release);
+  gen_of(n).fetch_add(1, std::memory_order_release);
   hdr_->n_pods.fetch_sub(1);
   hdr_->epoch.fetch_add(1);
   return kOk;
@@ -1189,7 +1192,7 @@ int32_t Ledger::set_load(int32_t id, int dev, float usage) {
   Device& d = n->devs[dev];
   d.load_usage = usage;
   d.remain_load = static_cast<int16_t>(kLoadTotal - static_cast<int>(usage));
-  n->generation.fetch_add(1, std::memory_order_release);
+  gen_of(n).fetch_add(1, std::memory_order_release);
   hdr_->epoch.fetch_add(1);
   return kOk;
 }
@@ -1213,7 +1216,7 @@ int32_t Ledger::set_mem_hot(int32_t id, int dev, bool hot) {
   Device& d = n->devs[dev];
   if ((d.mem_hot != 0) == hot) return kOk;   // unchanged: cached plans stay valid
   d.mem_hot = hot ? 1 : 0;
-  n->generation.fetch_add(1, std::memory_order_release);
+  gen_of(n).fetch_add(1, std::memory_order_release);
   hdr_->epoch.fetch_add(1);
   return kOk;
 }
@@ -1225,7 +1228,7 @@ int32_t Ledger::set_health(int32_t id, int dev, bool healthy) {
   Unlock un{&n->mu};
   if (dev < 0 || dev >= n->n_devs) return kErrBadPlan;
   n->devs[dev].healthy = healthy ? 1 : 0;
-  n->generation.fetch_add(1, std::memory_order_release);
+  gen_of(n).fetch_add(1, std::memory_order_release);
   hdr_->epoch.fetch_add(1);
   return kOk;
 }

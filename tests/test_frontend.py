@@ -730,3 +730,51 @@ def test_owner_learned_between_priorities_and_bind_is_tolerated():
             await rt.stop()
 
     asyncio.run(main())
+
+
+def test_rotating_node_windows_answer_byte_identical_through_the_list_cache():
+    """kube-scheduler's node sampling sends a moving window of the cluster each cycle. The
+    native verbs cache the last 64 distinct lists (ids and token offsets), answer a fully
+    fitting filter with the request's own list text, and resolve new windows through a per-
+    thread name table. Every answer must still equal the Python verb's, across LRU evictions,
+    nodes that do not fit, a node added (the ledger's node epoch moves) and an unknown name."""
+    import random
+
+    from nanogpu.extender.verbs import Extender
+    from nanogpu.k8s.fake_apiserver import FakeKubeStore, InProcKube
+    from nanogpu.state.cluster import ClusterState
+
+    st = ClusterState()
+    names = [f"node-{i:02d}" for i in range(30)]
+    for n in names:
+        st.register_node(pu.make_node(n, 8, synthetic_mi355x(8).to_json()))
+    # some nodes nearly full: their FailedNodes entries interleave with the fitting ones
+    for k, n in enumerate(names[::3]):
+        nid = st.node_ids([n])[0]
+        for dev in range(8):
+            st.ledger.allocate_plan(nid, f"fill-{k}-{dev}", [(95, 0)], [[dev]], True)
+    ext = Extender(st, InProcKube(FakeKubeStore()))
+    fe = N.Frontend(st.ledger, "127.0.0.1", 0, 1)
+    rnd = random.Random(4)
+    try:
+        fe.set_options(st.options, False, False)
+        for step in range(160):
+            if step == 100:   # a new node: every cached list re-checks its ids
+                st.register_node(pu.make_node("node-new", 8, synthetic_mi355x(8).to_json()))
+                names.append("node-new")
+            start, size = rnd.randrange(len(names)), rnd.choice([5, 12, 25])
+            window = [names[(start + j) % len(names)] for j in range(size)]
+            pct = rnd.choice([10, 50])
+            raw = json.dumps({"Pod": pu.make_pod(f"p{step}", [("c", pct)]), "NodeNames": window},
+                             separators=(",", ":")).encode()
+            for prio, verb in ((False, ext.filter), (True, ext.prioritize)):
+                ok, _, out = fe.time_verb(raw, prio, 1)
+                assert ok and out == _dumps(verb(json.loads(raw))), (step, prio)
+        unknown = json.dumps({"Pod": pu.make_pod("u", [("c", 10)]), "NodeNames": names[:3] + ["ghost"]},
+                             separators=(",", ":")).encode()
+        assert fe.time_verb(unknown, False, 1)[0] is False     # Python registers or rejects it
+        ok, _, out = fe.time_verb(json.dumps({"Pod": pu.make_pod("v", [("c", 10)]), "NodeNames": names[:3]},
+                                             separators=(",", ":")).encode(), False, 1)
+        assert ok and json.loads(out)["NodeNames"] == [n for n in names[:3] if n != "node-00"]
+    finally:
+        fe.stop()
