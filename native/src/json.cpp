@@ -1,6 +1,8 @@
 // JSON DOM parser (see json.h).
 #include "nanogpu/json.h"
 
+#include <emmintrin.h>
+
 namespace nanogpu::json {
 
 namespace {
@@ -52,25 +54,46 @@ bool Doc::parse_shallow(std::string_view src, int max_depth) {
 
 // At an opening bracket: to just past its matching close. Strings are skipped whole (an
 // escaped quote does not end one); control characters inside them are rejected as parse()
-// would.
+// would. Sixteen bytes at a time (SSE2, the x86-64 baseline of the extender's host): only the
+// bytes that can change the state are looked at one by one. The bodies skipped this way are
+// kube-scheduler's node lists (6 KB for 420 sampled nodes) and the pod's deep parts.
 bool Doc::skip_container() {
   const char* s = src_.data();
   const size_t n = src_.size();
   int depth = 0;
+  bool in_str = false;
+  const __m128i quote = _mm_set1_epi8('"'), bslash = _mm_set1_epi8('\\'), ctl = _mm_set1_epi8(0x1f);
+  const __m128i lsq = _mm_set1_epi8('['), rsq = _mm_set1_epi8(']'), lcu = _mm_set1_epi8('{'), rcu = _mm_set1_epi8('}');
   while (p_ < n) {
-    const char c = s[p_++];
-    if (c == '"') {
-      for (;;) {
-        if (p_ >= n) return false;
-        const unsigned char ch = static_cast<unsigned char>(s[p_++]);
-        if (ch == '"') break;
-        if (ch == '\\') {
-          if (p_ >= n) return false;
-          ++p_;
-        } else if (ch < 0x20) {
-          return false;
-        }
+    if (p_ + 16 <= n) {
+      const __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + p_));
+      __m128i m;
+      if (in_str)   // a quote, a backslash, or a control character (x <= 0x1f unsigned)
+        m = _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(x, quote), _mm_cmpeq_epi8(x, bslash)),
+                         _mm_cmpeq_epi8(_mm_min_epu8(x, ctl), x));
+      else
+        m = _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(x, quote), _mm_cmpeq_epi8(x, lsq)),
+                         _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(x, rsq), _mm_cmpeq_epi8(x, lcu)),
+                                      _mm_cmpeq_epi8(x, rcu)));
+      const unsigned mask = static_cast<unsigned>(_mm_movemask_epi8(m));
+      if (!mask) {
+        p_ += 16;
+        continue;
       }
+      p_ += static_cast<size_t>(__builtin_ctz(mask));
+    }
+    const unsigned char c = static_cast<unsigned char>(s[p_++]);
+    if (in_str) {
+      if (c == '"') {
+        in_str = false;
+      } else if (c == '\\') {
+        if (p_ >= n) return false;
+        ++p_;
+      } else if (c < 0x20) {
+        return false;
+      }
+    } else if (c == '"') {
+      in_str = true;
     } else if (c == '{' || c == '[') {
       if (++depth > kMaxDepth) return false;
     } else if (c == '}' || c == ']') {

@@ -353,3 +353,41 @@ def test_watch_filter_shallow_parse_skips_deep_fields_exactly():
     unterminated = b'{"type":"ADDED","object":{"metadata":{"labels":{"a":"x\\"}}}}\n'
     with pytest.raises(ValueError):
         f.decode(unterminated)
+
+
+def test_shallow_skip_agrees_with_the_full_parser_at_every_alignment():
+    """The shallow parser skips deep containers sixteen bytes at a time (json.cpp
+    skip_container): quotes, escapes, brackets and control characters inside skipped text
+    must be seen wherever they fall in a 16-byte block. Random label text around those bytes,
+    at every offset: an event the filter keeps decodes exactly as the full parser decodes it,
+    and a corrupted one fails in both."""
+    import random
+
+    from nanogpu.state.cluster import ClusterState
+    from nanogpu.topology.model import synthetic_mi355x
+
+    st = ClusterState()
+    st.register_node(pu.make_node("n0", 8, synthetic_mi355x(8).to_json()))
+    rnd = random.Random(7)
+    alphabet = ['"', "\\", "[", "]", "{", "}", "a", "b", " ", ",", ":", "é", "\t", "\n"]
+    for i in range(400):
+        pod = pu.make_pod(f"p{i}", [("main", 10)])
+        pod["spec"]["nodeName"] = "n0"              # foreign bound pod: the filter keeps it
+        pod["metadata"]["labels"] = {f"k{j}": "x" * rnd.randrange(0, 17) + "".join(
+            rnd.choice(alphabet) for _ in range(rnd.randrange(0, 6))) for j in range(rnd.randrange(1, 4))}
+        pod["spec"]["extra"] = [["y" * rnd.randrange(0, 33), {"z": "[" * rnd.randrange(0, 3)}]]
+        line = json.dumps({"type": "ADDED", "object": pod}).encode() + b"\n"
+        f = N.PodWatchFilter(st.ledger)
+        assert f.decode(line) == N.decode_pod_watch(line)
+        # corrupt one byte inside the skipped part: both parsers must agree on failing or not
+        at = line.index(b'"extra"') + rnd.randrange(8, 30)
+        bad = line[:at] + rnd.choice([b'"', b"]", b"}", b"\x01"]) + line[at + 1:]
+        outcomes = []
+        for decode in (N.PodWatchFilter(st.ledger).decode, N.decode_pod_watch):
+            try:
+                decode(bad)
+                outcomes.append(True)
+            except ValueError:
+                outcomes.append(False)
+        if not outcomes[1]:
+            assert not outcomes[0], bad      # what the full parser rejects, the skip rejects
