@@ -143,8 +143,9 @@ class Frontend {
   bool read_in(Worker* w, Conn* c, bool* eof);      // false: connection closed
   void after_read(Worker* w, Conn* c, bool eof);    // parse + answer what is buffered
   void process(Worker* w, Conn* c);
-  bool handle_native(Worker* w, Conn* c, const std::string& method, const std::string& path,
-                     std::string_view body, std::string* out);
+  // the verb's whole HTTP answer appended to *out (false: not a native verb, nothing written)
+  bool handle_native(Worker* w, Conn* c, std::string_view method, std::string_view path, std::string_view body,
+                     std::string* out);
   void defer(Worker* w, Conn* c, std::string method, std::string path, std::string query, std::string body);
   void flush(Worker* w, Conn* c);
   void close_conn(Worker* w, Conn* c);

@@ -847,8 +847,8 @@ void Frontend::process(Worker* w, Conn* c) {
       close_conn(w, c);
       return;
     }
-    std::string method(line.substr(0, s1));
-    std::string target(line.substr(s1 + 1, s2 - s1 - 1));
+    const std::string_view method = line.substr(0, s1);
+    const std::string_view target = line.substr(s1 + 1, s2 - s1 - 1);
     const bool http10 = line.substr(s2 + 1) == "HTTP/1.0";
     size_t clen = 0;
     bool chunked = false, close = http10, keep = false;
@@ -872,9 +872,13 @@ void Frontend::process(Worker* w, Conn* c) {
       pos = e + 2;
     }
     if (http10 && keep) close = false;
-    std::string body;
+    // the body stays a view into the connection's input unless it came chunked; the input is
+    // consumed only after the request is handled (the views point into it)
+    thread_local std::string chunked_body;
+    std::string_view body;
     size_t consumed;
     if (chunked) {
+      chunked_body.clear();
       size_t p = he + 4;
       for (;;) {
         const size_t le2 = c->in.find("\r\n", p);
@@ -888,39 +892,40 @@ void Frontend::process(Worker* w, Conn* c) {
           consumed = end + 4;
           break;
         }
-        body.append(c->in, le2 + 2, n);
-        if (body.size() > kMaxBody) {
+        chunked_body.append(c->in, le2 + 2, n);
+        if (chunked_body.size() > kMaxBody) {
           close_conn(w, c);
           return;
         }
         p = le2 + 2 + n + 2;
       }
+      body = chunked_body;
     } else {
       if (clen > kMaxBody) {
         close_conn(w, c);
         return;
       }
       if (c->in.size() < he + 4 + clen) return;  // need more
-      body.assign(c->in, he + 4, clen);
+      body = std::string_view(c->in).substr(he + 4, clen);
       consumed = he + 4 + clen;
     }
-    c->in.erase(0, consumed);
     if (close) c->close_after = true;
     requests.fetch_add(1, std::memory_order_relaxed);
-    std::string path = target, query;
+    std::string_view path = target, query;
     const size_t qm = target.find('?');
-    if (qm != std::string::npos) {
+    if (qm != std::string_view::npos) {
       path = target.substr(0, qm);
       query = target.substr(qm + 1);
     }
-    std::string out;
-    if (handle_native(w, c, method, path, body, &out)) {
-      c->out += out;
+    if (handle_native(w, c, method, path, body, &c->out)) {   // the answer lands in c->out
+      c->in.erase(0, consumed);
       flush(w, c);
       w->cycle_reply_ns = now_ns();   // the scheduling cycle's next request is due: spin for it
       if (!w->conns.count(id)) return;
     } else {
-      defer(w, c, std::move(method), std::move(path), std::move(query), std::move(body));
+      std::string m(method), pth(path), q(query), b(body);   // owned: the Python side keeps them
+      c->in.erase(0, consumed);
+      defer(w, c, std::move(m), std::move(pth), std::move(q), std::move(b));
     }
   }
 }
@@ -1010,7 +1015,7 @@ void Frontend::close_conn(Worker* w, Conn* c) {
 }
 
 // ------------------------------------------------------------------------------ verbs
-bool Frontend::handle_native(Worker* w, Conn* c, const std::string& method, const std::string& path,
+bool Frontend::handle_native(Worker* w, Conn* c, std::string_view method, std::string_view path,
                              std::string_view body, std::string* out) {
   (void)w;
   (void)c;
@@ -1018,11 +1023,16 @@ bool Frontend::handle_native(Worker* w, Conn* c, const std::string& method, cons
   const bool prio = path == "/scheduler/priorities";
   if (!prio && path != "/scheduler/filter") return false;
   const uint64_t t0 = now_ns();
-  std::string resp;
+  thread_local std::string resp;   // keeps its capacity: no allocation per request
   if (!filter_verb(body, prio, &resp)) return false;
   (prio ? prio_stats : filter_stats).observe(now_ns() - t0);
-  *out = "HTTP/1.1 200 OK\r\nContent-Type: application/json; charset=utf-8\r\nContent-Length: " +
-         std::to_string(resp.size()) + "\r\n\r\n";
+  constexpr std::string_view kHead = "HTTP/1.1 200 OK\r\nContent-Type: application/json; charset=utf-8\r\nContent-Length: ";
+  char len[24];
+  const char* e = std::to_chars(len, len + sizeof len, resp.size()).ptr;
+  out->reserve(out->size() + kHead.size() + 24 + resp.size());
+  *out += kHead;
+  out->append(len, static_cast<size_t>(e - len));
+  *out += "\r\n\r\n";
   *out += resp;
   return true;
 }
