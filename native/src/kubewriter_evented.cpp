@@ -19,6 +19,8 @@
 #include <openssl/ssl.h>
 #include <openssl/x509v3.h>
 #include <sys/epoll.h>
+
+#include <charconv>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -45,41 +47,52 @@ uint64_t ns_now() {
 
 // One HTTP/1.1 response at the front of `b`: 1 = complete, 0 = need more, -1 = malformed.
 // `eof`: the peer closed (completes a response without a length).
+bool ieq_ascii(std::string_view a, std::string_view b) {
+  if (a.size() != b.size()) return false;
+  for (size_t i = 0; i < a.size(); ++i)
+    if (std::tolower(static_cast<unsigned char>(a[i])) != b[i]) return false;
+  return true;
+}
+
+// One answer at the front of `b`: 1 = complete (status, body, bytes consumed), 0 = more bytes
+// needed, -1 = not HTTP. Headers are read in place; the body is copied only for an answer
+// outside 2xx, the only one anybody reads (the slow path reports or inspects it).
 int parse_response(const std::string& b, bool eof, int* status, std::string* body, size_t* consumed, bool* close) {
   const size_t he = b.find("\r\n\r\n");
   if (he == std::string::npos) return b.size() > (256u << 10) ? -1 : 0;
   if (he < 12 || b.compare(0, 5, "HTTP/") != 0) return -1;
   *status = std::atoi(b.c_str() + 9);
+  const bool keep_body = *status < 200 || *status >= 300;
   long clen = -1;
   bool chunked = false;
   *close = false;
+  const std::string_view bv(b);
   size_t p = b.find("\r\n");
   while (p < he) {
     const size_t e = b.find("\r\n", p + 2);
     const size_t end = e == std::string::npos || e > he ? he : e;
     const size_t colon = b.find(':', p + 2);
     if (colon != std::string::npos && colon < end) {
-      std::string k = b.substr(p + 2, colon - p - 2);
-      for (char& ch : k) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
+      const std::string_view k = bv.substr(p + 2, colon - p - 2);
       size_t v0 = colon + 1;
       while (v0 < end && b[v0] == ' ') ++v0;
-      const std::string v = b.substr(v0, end - v0);
-      if (k == "content-length") clen = std::atol(v.c_str());
-      else if (k == "transfer-encoding" && v.find("chunked") != std::string::npos) chunked = true;
-      else if (k == "connection" && (v == "close" || v == "Close")) *close = true;
+      const std::string_view v = bv.substr(v0, end - v0);
+      if (ieq_ascii(k, "content-length")) clen = std::strtol(b.c_str() + v0, nullptr, 10);
+      else if (ieq_ascii(k, "transfer-encoding") && v.find("chunked") != std::string_view::npos) chunked = true;
+      else if (ieq_ascii(k, "connection") && (v == "close" || v == "Close")) *close = true;
     }
     if (end == he) break;
     p = end;
   }
   size_t q = he + 4;
+  body->clear();
   if (chunked) {
-    body->clear();
     for (;;) {
       const size_t le = b.find("\r\n", q);
       if (le == std::string::npos) return 0;
       const size_t sz = std::strtoul(b.c_str() + q, nullptr, 16);
       if (b.size() < le + 2 + sz + 2) return 0;
-      body->append(b, le + 2, sz);
+      if (keep_body) body->append(b, le + 2, sz);
       q = le + 2 + sz + 2;
       if (sz == 0) break;
     }
@@ -88,12 +101,12 @@ int parse_response(const std::string& b, bool eof, int* status, std::string* bod
   }
   if (clen >= 0) {
     if (b.size() < q + static_cast<size_t>(clen)) return 0;
-    body->assign(b, q, static_cast<size_t>(clen));
+    if (keep_body) body->assign(b, q, static_cast<size_t>(clen));
     *consumed = q + static_cast<size_t>(clen);
     return 1;
   }
   if (!eof) return 0;   // the body runs to the end of the connection
-  body->assign(b, q, std::string::npos);
+  if (keep_body) body->assign(b, q, std::string::npos);
   *consumed = b.size();
   *close = true;
   return 1;
@@ -206,21 +219,31 @@ void KubeWriter::io_loop() {
     epoll_ctl(ep, EPOLL_CTL_ADD, fd, &ev);
     return true;
   };
-  auto request = [&](const char* method, const std::string& path, const std::string& ctype, const std::string& body) {
-    std::string r;
-    r.reserve(256 + body.size());
-    r += method;
-    r += ' ';
-    r += path;
-    r += " HTTP/1.1\r\nHost: ";
-    r += host_hdr;
-    r += "\r\nUser-Agent: nano-gpu-scheduler-amd/0.1\r\nAccept: application/json\r\n";
-    if (!a.empty()) r += "Authorization: Bearer " + a + "\r\n";
-    r += "Content-Type: ";
-    r += ctype;
-    r += "\r\nContent-Length: " + std::to_string(body.size()) + "\r\n\r\n";
-    r += body;
-    return r;
+  // a request written into the connection's own buffer (its capacity is kept across binds)
+  auto request = [&](std::string* r, const char* method, const BindJob& j, bool binding, std::string_view ctype,
+                     const std::string& body) {
+    r->clear();
+    *r += method;
+    *r += " /api/v1/namespaces/";
+    *r += j.ns;
+    *r += "/pods/";
+    *r += j.name;
+    if (binding) *r += "/binding";
+    *r += " HTTP/1.1\r\nHost: ";
+    *r += host_hdr;
+    *r += "\r\nUser-Agent: nano-gpu-scheduler-amd/0.1\r\nAccept: application/json\r\n";
+    if (!a.empty()) {
+      *r += "Authorization: Bearer ";
+      *r += a;
+      *r += "\r\n";
+    }
+    *r += "Content-Type: ";
+    *r += ctype;
+    char len[24];
+    *r += "\r\nContent-Length: ";
+    r->append(len, static_cast<size_t>(std::to_chars(len, len + sizeof len, body.size()).ptr - len));
+    *r += "\r\n\r\n";
+    *r += body;
   };
 
   size_t inflight = 0;
@@ -391,9 +414,8 @@ void KubeWriter::io_loop() {
       conns.push_back(std::make_unique<AConn>());
     }
     AConn& c = *conns[k];
-    const std::string base = "/api/v1/namespaces/" + jb.j.ns + "/pods/" + jb.j.name;
-    c.out = which ? request("POST", base + "/binding", kJsonE, jb.binding)
-                  : request("PATCH", base, kMergePatchE, jb.patch);
+    if (which) request(&c.out, "POST", jb.j, true, kJsonE, jb.binding);
+    else request(&c.out, "PATCH", jb.j, false, kMergePatchE, jb.patch);
     c.off = 0;
     c.in.clear();
     c.job = s;
