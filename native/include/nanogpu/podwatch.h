@@ -13,6 +13,7 @@
 #pragma once
 
 #include <atomic>
+#include <condition_variable>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -77,6 +78,10 @@ class PodWatchStream {
   std::mutex sock_mu_;   // stop() shuts the socket down only while the thread holds it open
   int sock_ = -1;
   std::mutex mu_;        // pending_
+  // backpressure: with this many kept lines not taken yet the thread stops reading (the
+  // socket's buffers then push back on the API server) until the event loop catches up
+  static constexpr size_t kMaxPending = 65536;
+  std::condition_variable drained_;
 
   Batch pending_;
   std::thread th_;

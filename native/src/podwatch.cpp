@@ -93,6 +93,10 @@ void PodWatchStream::stop() {
     stop_ = true;
     if (sock_ >= 0) ::shutdown(sock_, SHUT_RDWR);   // wakes the thread's blocking read
   }
+  {
+    std::lock_guard<std::mutex> g(mu_);   // ... or its wait for the event loop
+  }
+  drained_.notify_all();
   if (th_.joinable()) th_.join();
 }
 
@@ -117,12 +121,16 @@ void PodWatchStream::push(std::vector<std::string>* lines, bool dropped, const s
 }
 
 PodWatchStream::Batch PodWatchStream::take() {
-  std::lock_guard<std::mutex> g(mu_);
-  uint64_t v;
-  (void)!::read(efd_, &v, sizeof v);
-  Batch b = std::move(pending_);
-  pending_ = Batch();
-  pending_.state = b.state;   // an end stays an end
+  Batch b;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    uint64_t v;
+    (void)!::read(efd_, &v, sizeof v);
+    b = std::move(pending_);
+    pending_ = Batch();
+    pending_.state = b.state;   // an end stays an end
+  }
+  drained_.notify_all();
   return b;
 }
 
@@ -180,6 +188,8 @@ void PodWatchStream::run() {
     }
     buf.erase(0, p);
     if (!kept.empty() || dropped) push(&kept, dropped, tail_rv, kStreaming, 0, "");
+    std::unique_lock<std::mutex> lk(mu_);
+    drained_.wait(lk, [&] { return pending_.lines.size() < kMaxPending || stop_.load(); });
   }
 }
 
