@@ -83,3 +83,12 @@ def test_busy_poll_guard_reads_the_cgroup_quota(tmp_path, monkeypatch):
     cfg = app.Config(workers=2, frontend_threads=2, busy_poll_us=20)
     app.guard_busy_poll(cfg)
     assert cfg.busy_poll_us == 20
+
+
+def test_extender_flags_reach_the_config():
+    """Round-3 switches: the label-less bind, the aiohttp pod watch, the writer mode; and their
+    defaults (the reference's label contract, the native watch thread, the evented writer)."""
+    base = cli.parse([])
+    assert base.assume_label and base.native_pod_watch and base.bind_writer_mode == "evented"
+    cfg = cli.parse(["--no-assume-label", "--no-native-pod-watch", "--bind-writer-mode", "threads"])
+    assert not cfg.assume_label and not cfg.native_pod_watch and cfg.bind_writer_mode == "threads"
