@@ -623,7 +623,7 @@ void Frontend::put_pod(std::string_view uid, CachedPod pod) {
 }
 
 void Frontend::prepare_bind(std::string_view body, PyRequest* r) {
-  json::Doc d;
+  thread_local json::Doc d;   // keeps its capacity across binds
   if (!d.parse(body) || !d.is(d.root(), json::Type::kObj)) return;
   auto str = [&](const char* k) -> std::string {
     const int32_t v = d.get(d.root(), k, true);
