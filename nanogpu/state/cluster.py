@@ -232,7 +232,7 @@ class ClusterState:
         ids = self.node_ids(node_names)
         scores = self.ledger.score(ids, demand, self.options)
         if self.nominate and scores:
-            self._nominate_best(pod, demand, ids, scores)
+            scores = self._nominate_best(pod, demand, ids, scores)
         if self.score_normalize and scores:
             scores = self._normalize(scores)
         return scores
@@ -242,21 +242,29 @@ class ClusterState:
         if uid:
             self.ledger.drop_nomination(uid)
 
-    def _nominate_best(self, pod: dict, demand, ids: list[int], scores: list[int]) -> None:
-        """Same rule as the native front door: a unique best fitting node is nominated."""
+    def _nominate_best(self, pod: dict, demand, ids: list[int], scores: list[int]) -> list[int]:
+        """Same rule as the native front door (frontend.cpp, priorities): a unique best fitting
+        node is nominated; a tie at the top is broken by one point for the first tied node in
+        the request's order while the nomination margin is 0. Returns the scores to answer."""
         uid = pu.pod_uid(pod)
-        if not uid or not any(p > 0 or m > 0 for p, m in demand):
-            return
         fits = self.ledger.filter(ids, demand, self.options)
-        cand = [(s, i) for s, i, rc in zip(scores, ids, fits) if rc == N.OK and i >= 0]
-        if not cand:
-            return
+        cand = [(s, k) for k, (s, i, rc) in enumerate(zip(scores, ids, fits)) if rc == N.OK and i >= 0]
+        if not cand or not uid:
+            return scores
         best = max(s for s, _ in cand)
-        top = [i for s, i in cand if s == best]
+        top = [k for s, k in cand if s == best]
         rest = [s for s, _ in cand if s != best]
+        margin = self.ledger.nomination_margin
+        if len(top) > 1 and margin == 0:
+            scores = list(scores)
+            scores[top[0]] += 1
+            rest, top = [best], top[:1]
+            best += 1
         # the lead must survive kube-scheduler's own plugins (Ledger::nomination_margin)
-        if len(top) == 1 and (not rest or best - max(rest) >= self.ledger.nomination_margin):
-            self.ledger.nominate(top[0], uid, demand, self.options)
+        if (len(top) == 1 and (not rest or best - max(rest) >= margin)
+                and any(p > 0 or m > 0 for p, m in demand)):
+            self.ledger.nominate(ids[top[0]], uid, demand, self.options)
+        return scores
 
     def _normalize(self, scores: list[int]) -> list[int]:
         """Maps to kube-scheduler's extender range [0, 10] (MaxExtenderPriority) [ext]."""

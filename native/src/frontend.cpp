@@ -1414,8 +1414,19 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     }
   }
   // a unique winner is the node kube-scheduler picks (ties are broken at random there) when
-  // its lead survives kube-scheduler's own score plugins (Ledger::nomination_margin)
-  const bool lead = n_best == 1 && (second < 0 || scores[best] - second >= ledger_->nomination_margin());
+  // its lead survives kube-scheduler's own score plugins (Ledger::nomination_margin). A tie at
+  // the top is broken here, for the first tied node in the request's order, by one point, and
+  // that node nominated: a pod without a nomination is invisible to the filters of the pods
+  // behind it until its bind reserves, and on identical nodes the top nearly always ties. Only
+  // while kube-scheduler has been following the nominations (margin 0): a moved one raises the
+  // margin and turns this off (cluster.py::score applies the same rule on the Python path).
+  const int32_t margin = ledger_->nomination_margin();
+  if (nominate && !o.compat && n_best > 1 && margin == 0 && !uid.empty()) {
+    ++scores[best];
+    second = scores[best] - 1;
+    n_best = 1;
+  }
+  const bool lead = n_best == 1 && (second < 0 || scores[best] - second >= margin);
   if (nominate && lead && !uid.empty() && dem.n > 0) {
     bool wants = false;
     for (int i = 0; i < dem.n; ++i) wants = wants || dem.c[i].pct > 0 || dem.c[i].mib > 0;

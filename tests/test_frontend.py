@@ -339,8 +339,9 @@ def test_inline_bind_failure_rolls_back():
 
 def test_priorities_nominate_unique_best_and_bind_adopts():
     """Native priorities nominate the unique top node, so the next pod's filter sees the
-    pod before its bind arrives; ties nominate nothing; compat mode never nominates; the
-    bind adopts the nomination (a failed bind rolls it back)."""
+    pod before its bind arrives; a tie at the top goes to the first tied node by one point
+    (while kube-scheduler follows the nominations); compat mode never nominates; the bind
+    adopts the nomination (a failed bind rolls it back)."""
     async def main():
         store, rt = await _runtime(2)
         loop = asyncio.get_running_loop()
@@ -375,12 +376,16 @@ def test_priorities_nominate_unique_best_and_bind_adopts():
                 ("POST", "/scheduler/bind", _dumps({"PodName": "a", "PodNamespace": "default",
                                                     "PodUID": pu.pod_uid(a), "Node": "n0"}))])
             assert res[1] == (200, b'{"Error":""}') and led.lookup(pu.pod_uid(a))["state"] == "committed"
-            # ties (two empty-equal candidates) nominate nothing
+            # a tie at the top (the same node twice) is broken for the first one, which is
+            # nominated and answered one point above the other
             c = store.create_pod(pu.make_pod("c", [("c", 10)]))
-            store2_nodes = ["n1"]
-            await loop.run_in_executor(None, _http, rt.bound_port, [
-                ("POST", "/scheduler/priorities", _dumps({"Pod": c, "NodeNames": store2_nodes + store2_nodes}))])
-            assert led.lookup(pu.pod_uid(c)) is None
+            res = await loop.run_in_executor(None, _http, rt.bound_port, [
+                ("POST", "/scheduler/priorities", _dumps({"Pod": c, "NodeNames": ["n1", "n1"]}))])
+            s0, s1 = (h["Score"] for h in json.loads(res[0][1]))
+            assert s0 == s1 + 1
+            rec = led.lookup(pu.pod_uid(c))
+            assert rec["state"] == "nominated" and rec["node"] == rt.state.node_entry("n1").id
+            led.drop_nomination(pu.pod_uid(c))
             # compat mode (the reference keeps no state between verbs): no nominations
             rt.state.set_policy("binpack", compat=True)
             d = store.create_pod(pu.make_pod("d", [("c", 10)]))
@@ -627,7 +632,7 @@ def test_escaped_node_names_still_answer_byte_identical():
     ext = Extender(st, InProcKube(FakeKubeStore()))
     fe = N.Frontend(st.ledger, "127.0.0.1", 0, 1)
     try:
-        fe.set_options(st.options, False, False)
+        fe.set_options(st.options, False, st.nominate)   # the same nomination rule as the Python verb
         raw = ('{"Pod":' + json.dumps(pu.make_pod("p", [("c", 20)])) + ',"NodeNames":["n\\u0030","n1"]}').encode()
         ok, _, out = fe.time_verb(raw, False, 1)
         assert ok and out == _dumps(ext.filter(json.loads(raw)))
@@ -757,7 +762,7 @@ def test_rotating_node_windows_answer_byte_identical_through_the_list_cache():
     fe = N.Frontend(st.ledger, "127.0.0.1", 0, 1)
     rnd = random.Random(4)
     try:
-        fe.set_options(st.options, False, False)
+        fe.set_options(st.options, False, st.nominate)   # the same nomination rule as the Python verb
         for step in range(160):
             if step == 100:   # a new node: every cached list re-checks its ids
                 st.register_node(pu.make_node("node-new", 8, synthetic_mi355x(8).to_json()))
