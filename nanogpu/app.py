@@ -253,6 +253,9 @@ class Runtime:
             gone = await loop.run_in_executor(None, self.state.sweep_nominations, self.cfg.nomination_ttl_s)
             if gone:
                 log.info("released %d nominations no bind adopted", len(gone))
+            removed = self.state.retry_removals()
+            if removed:
+                log.info("removed deleted nodes once their last shares went: %s", ", ".join(removed))
             if loop.time() < next_res:
                 continue
             next_res = loop.time() + max(1.0, self.cfg.reservation_ttl_s / 4)

@@ -71,6 +71,7 @@ class ClusterState:
         self._nodes_mu = threading.Lock()
         self._released: OrderedDict[str, None] = OrderedDict()   # reference ReleasedPodMap
         self._rejected: dict[str, str] = {}     # nodes the ledger cannot hold, with the reason
+        self._pending_removal: dict[str, int] = {}   # deleted nodes whose slot still holds shares
         self._released_cap = 65536
         self._reaccount_wait: dict[str, dict] = {}   # uid -> pod waiting for its partner (reaccount)
         self.set_policy(policy, compat=compat, load_aware=load_aware, topo_weight=topo_weight, seed=seed,
@@ -161,9 +162,38 @@ class ClusterState:
         return e
 
     def forget_node(self, name: str) -> bool:
+        """A deleted Node: its ledger slot goes once nothing holds a share on it. Nominations
+        there are dropped at once (nobody will bind to a deleted node); reservations and
+        committed pods keep the slot until they are released, and `retry_removals` (the
+        sweeper) finishes the removal then, so the slot is not left behind."""
         with self._nodes_mu:
             e = self._nodes.pop(name, None)
-        return bool(e) and self.ledger.remove_node(e.id)
+        if not e:
+            return False
+        if self._remove_slot(e.id):
+            self._pending_removal.pop(name, None)
+            return True
+        self._pending_removal[name] = e.id
+        return False
+
+    def _remove_slot(self, node_id: int) -> bool:
+        for rec in self.ledger.pods_on(node_id):
+            if rec["state"] == "nominated":
+                self.ledger.drop_nomination(rec["key"])
+        return self.ledger.remove_node(node_id)
+
+    def retry_removals(self) -> list[str]:
+        """Deleted nodes whose slot could not go yet (pods held shares): removed now if they
+        are empty; a node registered again under the same name meanwhile is left alone."""
+        done = []
+        for name, nid in list(self._pending_removal.items()):
+            if name in self._nodes or self.ledger.node_name(nid) != name:
+                self._pending_removal.pop(name, None)
+                continue
+            if self._remove_slot(nid):
+                self._pending_removal.pop(name, None)
+                done.append(name)
+        return done
 
     def node_entry(self, name: str) -> NodeEntry | None:
         e = self._nodes.get(name)
@@ -244,8 +274,9 @@ class ClusterState:
 
     def _nominate_best(self, pod: dict, demand, ids: list[int], scores: list[int]) -> list[int]:
         """Same rule as the native front door (frontend.cpp, priorities): a unique best fitting
-        node is nominated; a tie at the top is broken by one point for the first tied node in
-        the request's order while the nomination margin is 0. Returns the scores to answer."""
+        node is nominated; a tie at the top is broken by one point, for the tied node (in the
+        request's order) that the pod's UID hash picks, while the nomination margin is 0.
+        Returns the scores to answer."""
         uid = pu.pod_uid(pod)
         fits = self.ledger.filter(ids, demand, self.options)
         cand = [(s, k) for k, (s, i, rc) in enumerate(zip(scores, ids, fits)) if rc == N.OK and i >= 0]
@@ -256,9 +287,10 @@ class ClusterState:
         rest = [s for s, _ in cand if s != best]
         margin = self.ledger.nomination_margin
         if len(top) > 1 and margin == 0:
+            pick = top[N.Ledger.owner_hash(uid) % len(top)]
             scores = list(scores)
-            scores[top[0]] += 1
-            rest, top = [best], top[:1]
+            scores[pick] += 1
+            rest, top = [best], [pick]
             best += 1
         # the lead must survive kube-scheduler's own plugins (Ledger::nomination_margin)
         if (len(top) == 1 and (not rest or best - max(rest) >= margin)

@@ -1415,13 +1415,23 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   }
   // a unique winner is the node kube-scheduler picks (ties are broken at random there) when
   // its lead survives kube-scheduler's own score plugins (Ledger::nomination_margin). A tie at
-  // the top is broken here, for the first tied node in the request's order, by one point, and
-  // that node nominated: a pod without a nomination is invisible to the filters of the pods
+  // the top is broken here by one point, for the tied node the pod's UID hash picks, and that
+  // node nominated: a pod without a nomination is invisible to the filters of the pods
   // behind it until its bind reserves, and on identical nodes the top nearly always ties. Only
   // while kube-scheduler has been following the nominations (margin 0): a moved one raises the
   // margin and turns this off (cluster.py::score applies the same rule on the Python path).
   const int32_t margin = ledger_->nomination_margin();
   if (nominate && !o.compat && n_best > 1 && margin == 0 && !uid.empty()) {
+    // which tied node: one picked by the pod's UID hash, as even over the tied nodes as
+    // kube-scheduler's random pick among equal scores, but the same for every worker
+    int64_t pick = static_cast<int64_t>(owner_hash(uid) % static_cast<uint64_t>(n_best));
+    for (size_t i = 0; i < scores.size(); ++i) {
+      if (rcs[i] != kOk || scores[i] != scores[best]) continue;
+      if (pick-- == 0) {
+        best = static_cast<int64_t>(i);
+        break;
+      }
+    }
     ++scores[best];
     second = scores[best] - 1;
     n_best = 1;

@@ -744,3 +744,34 @@ def test_hbm_hot_threshold_is_a_policy_knob():
     with pytest.raises(ValueError):
         parse_policy("spec:\n  hbmHotThreshold: 1.5\n")
     assert LoadPoller(st, None, lambda: []).hbm_threshold == T.HBM_HOT_THRESHOLD
+
+
+def test_deleted_node_slot_goes_when_its_last_share_does():
+    """A deleted Node: nominations on it are dropped at once; a committed pod keeps the slot
+    until it is released, then the sweeper's retry removes it; a node registered again under
+    the same name meanwhile is left alone."""
+    from nanogpu import _native as NN
+    from nanogpu.state.cluster import ClusterState
+    from nanogpu.topology.model import synthetic_mi355x
+
+    st = ClusterState()
+    for n in ("a", "b"):
+        st.register_node(pu.make_node(n, 8, synthetic_mi355x(8).to_json()))
+    ida, idb = st.node_ids(["a", "b"])
+    assert st.ledger.nominate(ida, "nom", [(10, 0)], st.options) == NN.OK
+    assert st.forget_node("a") and st.ledger.find_node("a") < 0          # nomination dropped
+    assert st.ledger.lookup("nom") is None
+    assert st.ledger.reserve(idb, "held", [(10, 0)], st.options)[0] == NN.OK
+    st.ledger.commit("held")
+    assert not st.forget_node("b") and st.ledger.find_node("b") == idb    # still holds a share
+    assert st.retry_removals() == []
+    st.ledger.release("held")
+    assert st.retry_removals() == ["b"] and st.ledger.find_node("b") < 0
+    # re-registered before the retry: not removed
+    st.register_node(pu.make_node("c", 8, synthetic_mi355x(8).to_json()))
+    idc = st.node_ids(["c"])[0]
+    assert st.ledger.reserve(idc, "held2", [(10, 0)], st.options)[0] == NN.OK
+    assert not st.forget_node("c")
+    st.register_node(pu.make_node("c", 8, synthetic_mi355x(8).to_json()))
+    st.ledger.release("held2")
+    assert st.retry_removals() == [] and st.ledger.find_node("c") >= 0
