@@ -121,6 +121,7 @@ class Frontend {
   VerbStats filter_stats, prio_stats, py_stats, bind_stats;   // bind_stats: native reserve half
   std::atomic<uint64_t> connections{0}, requests{0};
   std::atomic<uint64_t> spin_hits{0};     // event batches a busy-polling worker caught
+  std::atomic<uint64_t> mb_wakeups{0};    // posted responses that had to wake a parked worker
   // binds this process answered natively with a pod another worker process's filter parsed
   // (Ledger::take_pod_info), and pods it handed to the other workers that way
   std::atomic<uint64_t> bind_handoffs{0}, pods_published{0};

@@ -859,6 +859,7 @@ PYBIND11_MODULE(_native, m) {
         d["requests"] = f.requests.load();
         d["loop_max_s"] = static_cast<double>(f.loop_max_ns.load()) * 1e-9;
         d["spin_hits"] = f.spin_hits.load();
+        d["mailbox_wakeups"] = f.mb_wakeups.load();
         d["bind_handoffs"] = f.bind_handoffs.load();
         d["pods_published"] = f.pods_published.load();
         py::list ph;

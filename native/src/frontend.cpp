@@ -376,6 +376,13 @@ struct Frontend::Worker {
   std::vector<std::pair<uint64_t, std::string>> mailbox;       // (conn id, response bytes)
   std::atomic<bool> unsignalled{false};                         // queued with notify=false
   bool mb_signalled = false;   // under mb_mu: the eventfd was written for what the mailbox holds
+  // An awake worker (busy polling, or handling a batch) looks at the mailbox itself after
+  // every epoll round, so a response posted then needs no eventfd write and no wake-up. Only
+  // a worker about to block is signalled: it sets `parked` and then re-reads `mb_pending`, the
+  // poster sets `mb_pending` and then reads `parked` (both seq_cst), so one of the two always
+  // sees the other.
+  std::atomic<bool> parked{false};
+  std::atomic<bool> mb_pending{false};
   uint64_t next_conn = 1;
   uint64_t cycle_reply_ns = 0;   // last filter / priorities reply handed to the kernel
 };
@@ -516,14 +523,18 @@ void Frontend::respond(uint64_t id, int status, const std::string& content_type,
   {
     std::lock_guard<std::mutex> g(w->mb_mu);
     w->mailbox.emplace_back(id >> 8, std::move(r));
-    // one eventfd write per mailbox fill: the worker takes everything queued until it swaps
-    if (notify && !w->mb_signalled) signal = w->mb_signalled = true;
+    w->mb_pending.store(true, std::memory_order_seq_cst);
+    // one eventfd write per mailbox fill, and only to a worker that may be blocked in
+    // epoll_wait: the worker takes everything queued until it swaps
+    if (notify && !w->mb_signalled && w->parked.load(std::memory_order_seq_cst))
+      signal = w->mb_signalled = true;
   }
   if (!notify) {
     w->unsignalled.store(true, std::memory_order_release);
     return;
   }
   if (signal) {
+    mb_wakeups.fetch_add(1, std::memory_order_relaxed);
     uint64_t one = 1;
     (void)!write(w->efd, &one, sizeof(one));
   }
@@ -699,12 +710,45 @@ void Frontend::run(Worker* w) {
   // were hits (a slow scheduler, tens of microseconds between verbs, is not spun for).
   uint32_t gaps = 0xffffu;   // 1 bits: hits among the last 16 cycle replies (start hot)
   uint64_t scored = 0;       // the cycle reply the last hit/miss was scored for
+  // responses posted by the bind writer or Python: sent, then the connection's next request
+  auto drain_mailbox = [&] {
+    PhaseTimer pt{&phase_max_ns[1]};
+    std::vector<std::pair<uint64_t, std::string>> mb;
+    {
+      std::lock_guard<std::mutex> g(w->mb_mu);
+      mb.swap(w->mailbox);
+      w->mb_signalled = false;
+      w->mb_pending.store(false, std::memory_order_relaxed);
+    }
+    for (auto& m : mb) {
+      auto it = w->conns.find(m.first);
+      if (it == w->conns.end()) continue;
+      Conn* c = it->second.get();
+      c->out += m.second;
+      c->waiting = false;
+      const bool was_bind = c->bind_waiting;
+      const uint64_t t_req = c->t_req_ns;
+      c->bind_waiting = false;
+      flush(w, c);   // may close the connection (Connection: close, a peer reset): c is gone then
+      if (was_bind) note_bind_wall(now_ns() - t_req);   // handed to the kernel: extender-side wall time
+      if (w->conns.count(m.first)) process(w, c);
+    }
+  };
   while (!stop_.load(std::memory_order_acquire)) {
     const int64_t spin = busy_poll_ns_.load(std::memory_order_relaxed);
     const bool hot = __builtin_popcount(gaps & 0xffffu) >= 8;
     const uint64_t since = w->cycle_reply_ns;
     const bool polling = spin > 0 && hot && since && now_ns() - since < static_cast<uint64_t>(spin);
+    if (!polling) {
+      w->parked.store(true, std::memory_order_seq_cst);
+      if (w->mb_pending.load(std::memory_order_seq_cst)) {   // posted before we parked
+        w->parked.store(false, std::memory_order_relaxed);
+        drain_mailbox();
+        continue;
+      }
+    }
     const int n = epoll_wait(w->ep, evs, 128, polling ? 0 : 200);
+    w->parked.store(false, std::memory_order_relaxed);
     const uint64_t t_batch = n > 0 ? now_ns() : 0;
     if (n > 0) {
       if (spin > 0 && since && since != scored) {
@@ -740,28 +784,9 @@ void Frontend::run(Worker* w) {
           w->conns.emplace(c->id, std::move(c));
         }
       } else if (tag == 1) {
-        PhaseTimer pt{&phase_max_ns[1]};
         uint64_t v;
         (void)!read(w->efd, &v, sizeof(v));
-        std::vector<std::pair<uint64_t, std::string>> mb;
-        {
-          std::lock_guard<std::mutex> g(w->mb_mu);
-          mb.swap(w->mailbox);
-          w->mb_signalled = false;
-        }
-        for (auto& m : mb) {
-          auto it = w->conns.find(m.first);
-          if (it == w->conns.end()) continue;
-          Conn* c = it->second.get();
-          c->out += m.second;
-          c->waiting = false;
-          flush(w, c);
-          if (c->bind_waiting) {   // response handed to the kernel: the extender-side wall time
-            c->bind_waiting = false;
-            note_bind_wall(now_ns() - c->t_req_ns);
-          }
-          if (w->conns.count(m.first)) process(w, c);
-        }
+        drain_mailbox();
       } else {
         PhaseTimer pt{&phase_max_ns[2]};
         const uint64_t cid = (tag & ~(1ull << 63)) >> 1;
@@ -795,6 +820,7 @@ void Frontend::run(Worker* w) {
       if (it != w->conns.end()) after_read(w, it->second.get(), false);
     }
     later.clear();
+    if (w->mb_pending.load(std::memory_order_acquire)) drain_mailbox();   // posted while awake
   }
 }
 

@@ -17,6 +17,7 @@
 // Exit code 0 = pass. Usage: nanogpu-stress [threads] [iterations]
 #include <arpa/inet.h>
 #include <netinet/in.h>
+#include <poll.h>
 #include <sys/socket.h>
 #include <sys/wait.h>
 #include <unistd.h>
@@ -437,6 +438,50 @@ static std::string post(int port, const std::string& path, const std::string& bo
   return out;
 }
 
+// Responses posted from another thread (the bind writer's and Python's path) while front-door
+// workers alternate between busy polling, handling batches and blocking in epoll_wait: every
+// request must be answered whether the poster saw its worker parked (eventfd) or awake (the
+// worker's own mailbox check). Pauses of random length let the workers park between posts.
+static void mailbox_wakeups(int requests) {
+  auto ledger = std::make_shared<Ledger>("", 4, 1024, true);
+  Frontend fe(ledger, "127.0.0.1", 0, 2);
+  fe.set_busy_poll_us(20);
+  std::atomic<bool> stop{false};
+  std::atomic<int> answered{0};
+  std::thread py([&] {
+    std::mt19937_64 rng(5);
+    pollfd pf{fe.notify_fd(), POLLIN, 0};
+    while (!stop.load()) {
+      if (poll(&pf, 1, 20) <= 0) continue;
+      std::vector<PyRequest> rs = fe.take();
+      for (size_t i = 0; i < rs.size(); ++i) {
+        if (rng() % 4 == 0) std::this_thread::sleep_for(std::chrono::microseconds(rng() % 300));
+        const bool notify = rng() % 3 != 0;
+        fe.respond(rs[i].id, 200, "application/json", "{\"ok\":" + std::to_string(i) + "}", notify);
+        answered.fetch_add(1);
+      }
+      fe.wake_workers();
+    }
+  });
+  std::vector<std::thread> clients;
+  for (int c = 0; c < 4; ++c)
+    clients.emplace_back([&, c] {
+      std::mt19937_64 rng(100 + c);
+      for (int i = 0; i < requests / 4; ++i) {
+        if (rng() % 8 == 0) std::this_thread::sleep_for(std::chrono::microseconds(rng() % 500));
+        const std::string r = post(fe.port(), "/not-native", "{}");
+        CHECK(r.rfind("HTTP/1.1 200", 0) == 0 && r.find("{\"ok\":") != std::string::npos);
+      }
+    });
+  for (auto& c : clients) c.join();
+  stop.store(true);
+  py.join();
+  CHECK(answered.load() == requests / 4 * 4);
+  fe.stop();
+  std::printf("mailbox ok: %d posted responses, %llu needed a wake-up\n", answered.load(),
+              static_cast<unsigned long long>(fe.mb_wakeups.load()));
+}
+
 int main(int argc, char** argv) {
   const int threads = argc > 1 ? std::atoi(argv[1]) : 4;
   const int iters = argc > 2 ? std::atoi(argv[2]) : 2000;
@@ -527,5 +572,6 @@ int main(int argc, char** argv) {
   apiserver_and_writers(std::max(50, iters / 20), false);   // blocking writer threads
   relist_gap(std::max(200, iters / 4));
   handoff(std::max(500, iters));
+  mailbox_wakeups(std::max(400, iters / 2));
   return 0;
 }
