@@ -255,6 +255,31 @@ class StallSampler:
         Path(path).write_text(json.dumps(out, indent=1))
 
 
+def thread_ticks() -> dict[str, list[int]]:
+    """[user, kernel] clock ticks of this process's threads by group (thread_cpu's groups),
+    from /proc/self/task/*/stat utime and stime: what share of each group's CPU is kernel
+    time (syscalls, and on loopback the receiving side's TCP path a send runs)."""
+    pid = os.getpid()
+    out: dict[str, list[int]] = {}
+    try:
+        tids = os.listdir(f"/proc/{pid}/task")
+    except OSError:
+        return out
+    for tid in tids:
+        try:
+            with open(f"/proc/{pid}/task/{tid}/stat") as f:
+                st = f.read()
+        except OSError:
+            continue
+        comm = st[st.index("(") + 1:st.rindex(")")]
+        fields = st[st.rindex(")") + 2:].split()
+        group = "main" if tid == str(pid) else comm.rstrip("0123456789") if comm.startswith("ngpu-") else "other"
+        acc = out.setdefault(group, [0, 0])
+        acc[0] += int(fields[11])
+        acc[1] += int(fields[12])
+    return out
+
+
 def thread_cpu() -> dict[str, float]:
     """CPU seconds of this process's threads by group: the Python main thread (event loop:
     informer, controller, Python routes), the native front door's epoll workers (ngpu-fe*,
@@ -997,7 +1022,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     fe_stats = rt.native.fe.stats if rt.native is not None else (lambda: {})
     handoffs0 = fe_stats().get("bind_handoffs", 0)
     cpu0, loop_cpu0 = time.process_time(), time.thread_time()
-    threads0 = thread_cpu()
+    threads0, ticks0, times0 = thread_cpu(), thread_ticks(), os.times()
     t0 = time.perf_counter()
     if sampler is not None:
         sampler.on.set()
@@ -1031,9 +1056,18 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                                         if cycles else None)
     n_sched = max(1, sum(st["scheduled"] for st in results["steps"]))
     results["cpu_us_per_pod"] = 1e6 * (time.process_time() - cpu0) / n_sched
-    threads1 = thread_cpu()
+    threads1, ticks1, times1 = thread_cpu(), thread_ticks(), os.times()
     results["cpu_us_per_pod_by_thread"] = {g: round(1e6 * (threads1[g] - threads0.get(g, 0.0)) / n_sched, 1)
                                            for g in sorted(threads1)}
+    # user / kernel split (10 ms ticks: about 1 % resolution over a 20-step run)
+    results["cpu_us_per_pod_user_kernel"] = [round(1e6 * (times1.user - times0.user) / n_sched, 1),
+                                             round(1e6 * (times1.system - times0.system) / n_sched, 1)]
+    kshare = {}
+    for g, (u1, k1) in ticks1.items():
+        u0, k0 = ticks0.get(g, [0, 0])
+        if (u1 - u0) + (k1 - k0) >= 5:
+            kshare[g] = round(100.0 * (k1 - k0) / ((u1 - u0) + (k1 - k0)), 1)
+    results["kernel_pct_by_thread"] = kshare
     results["loop_cpu_us_per_pod"] = 1e6 * (time.thread_time() - loop_cpu0) / n_sched
     # the Python part of each bind (API writes + commit): a sub-phase of the wall time
     binds = sorted(s["dur_ms"] for s in rt.tracer.dump(10 ** 9, "bind") if s["ok"])
@@ -1251,6 +1285,9 @@ def main() -> int:
             # the same CPU by thread group: main (event loop), ngpu-fe (native front door epoll
             # workers, busy polling included), ngpu-wr (native bind writers), other
             "extender_cpu_us_per_pod_by_thread_rank0": res.get("cpu_us_per_pod_by_thread"),
+            # [user, kernel] µs a pod, and each thread group's kernel share of its CPU
+            "extender_cpu_us_per_pod_user_kernel_rank0": res.get("cpu_us_per_pod_user_kernel"),
+            "extender_kernel_pct_by_thread_rank0": res.get("kernel_pct_by_thread"),
         }
         line.update(reference_model_frag(args, topo))
         if variant is not None:

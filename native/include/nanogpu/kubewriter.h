@@ -151,6 +151,10 @@ class KubeWriter {
   bool evented_ = false;
   int max_inflight_ = 0;
   int efd_ = -1;                 // wakes the io thread (new jobs, stop)
+  // the io thread is about to block in epoll_wait: only then does a submit write efd_ (it sets
+  // io_parked_ and re-reads q_len_; a submit stores q_len_ and reads io_parked_, both seq_cst)
+  std::atomic<bool> io_parked_{false};
+  std::atomic<size_t> q_len_{0};
   std::thread io_;
   std::atomic<bool> io_done_{false};   // the io thread has handed everything to the slow path
   std::deque<SlowJob> slow_q_;   // under mu_, signalled on cv_

@@ -492,8 +492,10 @@ void KubeWriter::submit(BindJob job) {
     std::lock_guard<std::mutex> g(mu_);
     if (!stop_) {
       stats.inflight.fetch_add(1, std::memory_order_relaxed);
-      wake = q_.empty();   // evented: the io thread drains the whole queue per wake-up
+      const bool first = q_.empty();   // evented: the io thread drains the whole queue per wake-up
       q_.push_back(std::move(job));
+      q_len_.store(q_.size(), std::memory_order_seq_cst);
+      wake = first && io_parked_.load(std::memory_order_seq_cst);   // an awake io thread looks itself
       accepted = true;
       if (!evented_) cv_.notify_one();
     }

@@ -441,11 +441,13 @@ void KubeWriter::io_loop() {
     {
       std::lock_guard<std::mutex> g(mu_);
       stopping = stop_;
-      if (!stopping)
+      if (!stopping) {
         while (!q_.empty()) {
           waiting.push_back(std::move(q_.front()));
           q_.pop_front();
         }
+        q_len_.store(0, std::memory_order_relaxed);
+      }
     }
     if (stopping && !stop_at) stop_at = ns_now() + 5'000'000'000ull;
     if (stopping) {
@@ -479,7 +481,11 @@ void KubeWriter::io_loop() {
     }
     for (size_t i = 0; i < kick.size(); ++i) drive(kick[i], 0);   // fail() may append
     kick.clear();
-    const int n = epoll_wait(ep, evs, 256, stopping ? 10 : 1000);
+    // park: a bind submitted from here on writes efd_; one submitted before is picked up now
+    io_parked_.store(true, std::memory_order_seq_cst);
+    const bool queued = !stopping && q_len_.load(std::memory_order_seq_cst) > 0;
+    const int n = epoll_wait(ep, evs, 256, queued ? 0 : stopping ? 10 : 1000);
+    io_parked_.store(false, std::memory_order_relaxed);
     for (int e = 0; e < n; ++e) {
       if (evs[e].data.u64 == UINT64_MAX) {
         uint64_t v;
