@@ -74,6 +74,8 @@ class Faults:
     patch_error_rate: float = 0.0     # 500 on pod PATCH
     bind_error_rate: float = 0.0      # 500 on binding POST
     conflict_rate: float = 0.0        # 409 on binding POST
+    close_after_binding: bool = False  # answer a binding with Connection: close (requests
+                                       # pipelined behind it on the connection go unanswered)
     seed: int = 0
     rng: random.Random = field(default_factory=random.Random)
 
@@ -592,7 +594,10 @@ def make_app(store: FakeKubeStore) -> web.Application:
             store.bind_pod(request.match_info["ns"], request.match_info["name"],
                            (body.get("metadata") or {}).get("uid", ""), (body.get("target") or {}).get("name", ""),
                            (body.get("metadata") or {}).get("annotations"))
-            return web.json_response({"kind": "Status", "status": "Success"}, status=201)
+            resp = web.json_response({"kind": "Status", "status": "Success"}, status=201)
+            if store.faults.close_after_binding:
+                resp.force_close()
+            return resp
         except ApiError as e:
             return _err(e)
 

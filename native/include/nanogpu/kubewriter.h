@@ -135,6 +135,8 @@ class KubeWriter {
   void process_batch(std::vector<BindJob>& jobs, std::vector<std::unique_ptr<HttpConn>>& conns);
   void finish(HttpConn* c, HttpConn* c2, BindJob& j, const std::string& patch, const std::string& binding, int sp,
               std::string* rp, int sb, std::string* rb);
+  // a bound pod's label PATCH that failed transiently: retried; a lasting failure is counted
+  void finish_label(HttpConn* c, const BindJob& j, const std::string& patch, int sp, std::string* rp);
   void refuse(BindJob& j);
   int call(HttpConn* c, const char* method, const std::string& path, const std::string& ctype,
            const std::string& body, std::string* resp, bool retry);
@@ -145,6 +147,7 @@ class KubeWriter {
     BindJob j;
     std::string patch, binding, rp, rb;
     int sp = 0, sb = 0;
+    bool answered = false;   // bound and answered already: only the label is left
   };
   void io_loop();
   void run_slow();

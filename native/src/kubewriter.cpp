@@ -607,6 +607,14 @@ void KubeWriter::process_batch(std::vector<BindJob>& jobs, std::vector<std::uniq
   }
 }
 
+void KubeWriter::finish_label(HttpConn* c, const BindJob& j, const std::string& patch, int sp, std::string* rp) {
+  auto transient = [](int st) { return st == 0 || st == 401 || st == 429 || st >= 500; };
+  const uint64_t t3 = now_ns();
+  if (transient(sp)) sp = call(c, "PATCH", "/api/v1/namespaces/" + j.ns + "/pods/" + j.name, kMergePatch, patch, rp, true);
+  stats.patch_ns.fetch_add(now_ns() - t3, std::memory_order_relaxed);
+  if (sp < 200 || sp >= 300) stats.label_failures.fetch_add(1, std::memory_order_relaxed);
+}
+
 void KubeWriter::finish(HttpConn* c, HttpConn* c2, BindJob& j, const std::string& patch, const std::string& b,
                         int sp, std::string* rp, int sb, std::string* rb) {
   const std::string base = "/api/v1/namespaces/" + j.ns + "/pods/" + j.name;
@@ -622,11 +630,7 @@ void KubeWriter::finish(HttpConn* c, HttpConn* c2, BindJob& j, const std::string
   if (sb < 200 || sb >= 300) {
     err = api_error(sb, *rb);
   } else if (sp < 200 || sp >= 300) {
-    // bound, with its annotations (they came with the binding): only the label is missing
-    const uint64_t t3 = now_ns();
-    if (transient(sp)) sp = call(c, "PATCH", base, kMergePatch, patch, rp, true);
-    stats.patch_ns.fetch_add(now_ns() - t3, std::memory_order_relaxed);
-    if (sp < 200 || sp >= 300) stats.label_failures.fetch_add(1, std::memory_order_relaxed);
+    finish_label(c, j, patch, sp, rp);   // bound, with its annotations: only the label is missing
   }
   if (err.empty()) {
     ledger_->commit(j.uid);

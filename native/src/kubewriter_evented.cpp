@@ -114,17 +114,25 @@ int parse_response(const std::string& b, bool eof, int* status, std::string* bod
 
 enum ConnState { kIdle, kConnecting, kHandshake, kSending, kReceiving };
 
+// A bind's two requests go out pipelined on ONE connection, the binding first: one send and,
+// usually, one read for both answers (HTTP/1.1 answers come back in request order; kube-
+// apiserver's Go server and the bench's API server both serve pipelined requests in order).
+struct Pending {
+  int64_t job;   // in-flight job slot
+  int which;     // 0: label PATCH, 1: binding
+};
+
 struct AConn {
   int fd = -1;
   SSL* ssl = nullptr;
   int st = kIdle;
-  bool reused = false;   // the request went out on a connection used before
-  bool got_any = false;  // response bytes seen for the current request
+  bool reused = false;   // the requests went out on a connection used before
+  bool got_any = false;  // response bytes seen since the requests went out
   bool retried = false;  // the one fresh-connection retry is spent
   std::string out, in;
   size_t off = 0;
-  int64_t job = -1;      // in-flight job slot
-  int which = 0;         // 0: label PATCH, 1: binding
+  Pending pend[2];       // answers still due, in request order
+  int npend = 0;
 };
 
 struct AJob {
@@ -132,6 +140,7 @@ struct AJob {
   std::string patch, binding, rp, rb;
   int sp = 0, sb = 0;
   int left = 2;
+  bool answered = false;   // kube-scheduler has its answer (the binding landed; the label may follow)
 };
 
 }  // namespace
@@ -247,13 +256,18 @@ void KubeWriter::io_loop() {
   };
 
   size_t inflight = 0;
+  auto ok2xx = [](int st) { return st >= 200 && st < 300; };
   // both answers of a slot are in: commit on the happy path, else the slow path finishes it
   auto complete = [&](int64_t s) {
     std::unique_ptr<AJob> jb = std::move(slots[static_cast<size_t>(s)]);
     free_slots.push_back(s);
     --inflight;
-    const bool ok2 = [](int st) { return st >= 200 && st < 300; }(jb->sb) && jb->sp >= 200 && jb->sp < 300;
-    stats.binding_ns.fetch_add(ns_now() - jb->j.t0_ns, std::memory_order_relaxed);
+    if (jb->answered && ok2xx(jb->sp)) {   // bound and answered earlier; the label landed too
+      stats.inflight.fetch_sub(1, std::memory_order_relaxed);
+      return;
+    }
+    const bool ok2 = ok2xx(jb->sb) && ok2xx(jb->sp);
+    if (!jb->answered) stats.binding_ns.fetch_add(ns_now() - jb->j.t0_ns, std::memory_order_relaxed);
     if (ok2) {
       ledger_->commit(jb->j.uid);
       stats.ok.fetch_add(1, std::memory_order_relaxed);
@@ -262,6 +276,7 @@ void KubeWriter::io_loop() {
       return;
     }
     SlowJob sj;
+    sj.answered = jb->answered;   // then only the label is left to retry
     sj.j = std::move(jb->j);
     sj.patch = std::move(jb->patch);
     sj.binding = std::move(jb->binding);
@@ -275,21 +290,38 @@ void KubeWriter::io_loop() {
     }
     cv_.notify_one();
   };
+  // the answer to connection c's oldest pending request
   auto deliver = [&](AConn& c, int status, std::string body) {
-    AJob& jb = *slots[static_cast<size_t>(c.job)];
-    (c.which ? jb.sb : jb.sp) = status;
-    (c.which ? jb.rb : jb.rp) = std::move(body);
-    const int64_t s = c.job;
-    c.job = -1;
-    if (--jb.left == 0) complete(s);
+    const Pending p = c.pend[0];
+    c.pend[0] = c.pend[1];
+    --c.npend;
+    AJob& jb = *slots[static_cast<size_t>(p.job)];
+    (p.which ? jb.sb : jb.sp) = status;
+    (p.which ? jb.rb : jb.rp) = std::move(body);
+    if (--jb.left == 0) {
+      complete(p.job);
+    } else if (p.which == 1 && ok2xx(status)) {
+      // bound, with the placement annotations: kube-scheduler's bind is answered now; the
+      // label PATCH behind it is the reference's selector contract only (a failure there goes
+      // to the slow path's label retry, never to a rollback)
+      jb.answered = true;
+      stats.binding_ns.fetch_add(ns_now() - jb.j.t0_ns, std::memory_order_relaxed);
+      ledger_->commit(jb.j.uid);
+      stats.ok.fetch_add(1, std::memory_order_relaxed);
+      respond_(jb.j.id, 200, "{\"Error\":\"\"}");
+    }
+  };
+  // every answer still due on connection c fails with `why` (status 0: the slow path retries)
+  auto deliver_rest = [&](AConn& c, const char* why) {
+    while (c.npend > 0) deliver(c, 0, why);
   };
   std::vector<size_t> kick;   // connections to drive after this batch of events
   // a transport failure: one retry on a fresh connection when a reused keep-alive connection
   // failed before any answer byte (the server closed it while idle), else status 0
   auto fail = [&](size_t k, const char* why) {
     AConn& c = *conns[k];
-    if (c.job >= 0 && c.reused && !c.got_any && !c.retried) {
-      c.retried = true;
+    if (c.npend > 0 && c.reused && !c.got_any && !c.retried) {
+      c.retried = true;   // nothing was answered: the whole pipeline goes out again
       c.reused = false;
       c.off = 0;
       if (open_conn(k)) {
@@ -298,7 +330,7 @@ void KubeWriter::io_loop() {
       }
     }
     close_conn(c);
-    if (c.job >= 0) deliver(c, 0, why);
+    deliver_rest(c, why);
     idle.push_back(k);
   };
 
@@ -382,28 +414,41 @@ void KubeWriter::io_loop() {
           if (eof || !c.in.empty()) close_conn(c);
           return;
         }
-        int status = 0;
-        std::string body;
-        size_t used = 0;
-        bool close = false;
-        const int rc = parse_response(c.in, eof, &status, &body, &used, &close);
-        if (rc < 0) return fail(k, "bad answer from the API server");
-        if (rc == 0) {
-          if (eof) return fail(k, "connection to the API server failed");
-          return;
+        // every complete answer in order; a pipeline cut short leaves its later answers to
+        // the slow path (the label PATCH there is idempotent)
+        while (c.npend > 0) {
+          int status = 0;
+          std::string body;
+          size_t used = 0;
+          bool close = false;
+          const int rc = parse_response(c.in, eof && c.npend == 1, &status, &body, &used, &close);
+          if (rc < 0) return fail(k, "bad answer from the API server");
+          if (rc == 0) {
+            if (!eof) return;   // more bytes to come
+            if (c.got_any && c.in.empty() && c.npend < 2) break;   // answered some, then closed
+            return fail(k, "connection to the API server failed");
+          }
+          c.in.erase(0, used);
+          deliver(c, status, std::move(body));
+          if (close) {
+            eof = true;
+            break;
+          }
         }
-        c.in.erase(0, used);
-        if (close || eof) close_conn(c);
+        if (c.npend > 0 || eof) {
+          close_conn(c);
+          deliver_rest(c, "connection to the API server closed before every answer");
+        }
         c.st = kIdle;
-        deliver(c, status, std::move(body));
         idle.push_back(k);
         return;
       }
       return;
     }
   };
-  // starts request `which` of slot s on an idle (or new) connection
-  auto launch = [&](int64_t s, int which) {
+  // starts slot s's requests on an idle (or new) connection: the binding, then (label mode)
+  // the label PATCH pipelined behind it
+  auto launch = [&](int64_t s) {
     AJob& jb = *slots[static_cast<size_t>(s)];
     size_t k;
     if (!idle.empty()) {
@@ -414,12 +459,18 @@ void KubeWriter::io_loop() {
       conns.push_back(std::make_unique<AConn>());
     }
     AConn& c = *conns[k];
-    if (which) request(&c.out, "POST", jb.j, true, kJsonE, jb.binding);
-    else request(&c.out, "PATCH", jb.j, false, kMergePatchE, jb.patch);
+    request(&c.out, "POST", jb.j, true, kJsonE, jb.binding);
+    c.pend[0] = Pending{s, 1};
+    c.npend = 1;
+    if (label_) {
+      thread_local std::string second;
+      request(&second, "PATCH", jb.j, false, kMergePatchE, jb.patch);
+      c.out += second;
+      c.pend[1] = Pending{s, 0};
+      c.npend = 2;
+    }
     c.off = 0;
     c.in.clear();
-    c.job = s;
-    c.which = which;
     c.got_any = false;
     c.retried = false;
     c.reused = c.fd >= 0;
@@ -427,7 +478,7 @@ void KubeWriter::io_loop() {
       c.st = kSending;
     } else if (!open_conn(k)) {
       close_conn(c);
-      deliver(c, 0, "cannot connect to " + t_.host + ":" + std::to_string(t_.port));
+      deliver_rest(c, "cannot connect to the API server");
       idle.push_back(k);
       return;
     }
@@ -475,9 +526,7 @@ void KubeWriter::io_loop() {
         slots[static_cast<size_t>(s)]->left = 1;
         slots[static_cast<size_t>(s)]->sp = 200;
       }
-      // the binding first: it is the one kube-scheduler's bind waits on
-      launch(s, 1);
-      if (label_ && slots[static_cast<size_t>(s)]) launch(s, 0);
+      launch(s);
     }
     for (size_t i = 0; i < kick.size(); ++i) drive(kick[i], 0);   // fail() may append
     kick.clear();
@@ -515,6 +564,7 @@ void KubeWriter::io_loop() {
     sj.rb = std::move(jb.rb);
     sj.sp = jb.sp;
     sj.sb = jb.sb;
+    sj.answered = jb.answered;
     {
       std::lock_guard<std::mutex> g(mu_);
       slow_q_.push_back(std::move(sj));
@@ -540,7 +590,11 @@ void KubeWriter::run_slow() {
       sj = std::move(slow_q_.front());
       slow_q_.pop_front();
     }
-    finish(&c, &c2, sj.j, sj.patch, sj.binding, sj.sp, &sj.rp, sj.sb, &sj.rb);
+    if (sj.answered) {   // bound and answered: only the label PATCH is left to retry
+      finish_label(&c, sj.j, sj.patch, sj.sp, &sj.rp);
+    } else {
+      finish(&c, &c2, sj.j, sj.patch, sj.binding, sj.sp, &sj.rp, sj.sb, &sj.rb);
+    }
     stats.inflight.fetch_sub(1, std::memory_order_relaxed);
   }
 }

@@ -364,3 +364,48 @@ def test_no_assume_label_binds_with_one_api_write(native):
             await runner.cleanup()
 
     asyncio.run(main())
+
+
+@pytest.mark.parametrize("faults", [dict(patch_error_rate=1.0), dict(close_after_binding=True),
+                                    dict(patch_error_rate=0.5, seed=3)])
+def test_pipelined_label_after_the_binding(faults):
+    """The evented writer pipelines the label PATCH behind the binding on one connection and
+    answers kube-scheduler when the binding lands. A label PATCH that fails (5xx), or never gets
+    an answer because the server closed the connection after the binding's, is retried on the
+    slow path: the bind stays a success and is never rolled back; a lasting label failure is
+    counted, never turned into a failed bind."""
+    async def main():
+        store = FakeKubeStore(faults=Faults(**faults))
+        store.add_node(pu.make_node("n0", 8, synthetic_mi355x(8).to_json()))
+        runner, rt = await _stack(store, "evented")
+        base = f"http://127.0.0.1:{rt.bound_port}"
+        try:
+            for i in range(6):
+                p = store.create_pod(pu.make_pod(f"p{i}", [("main", 10)]))
+                status, res = await _schedule(base, p, "n0")
+                assert status == 200 and res == {"Error": ""}, res
+                got = store.get_pod("default", f"p{i}")
+                assert got["spec"]["nodeName"] == "n0"
+                assert got["metadata"]["annotations"][T.container_annotation("main")]
+                assert rt.state.ledger.lookup(pu.pod_uid(p))["state"] == "committed"
+            assert rt.state.status()["n0"]["GPUs"][0]["Percent"] == 40
+            labelled = lambda: sum((store.get_pod("default", f"p{i}")["metadata"].get("labels") or {})
+                                   .get(T.LABEL_GPU_ASSUME) == "true" for i in range(6))
+            for _ in range(300):   # the label lands after the answer, through the slow path's retry
+                if labelled() == 6 or rt.native.fe.kube_writer_stats()["inflight"] == 0:
+                    break
+                await asyncio.sleep(0.01)
+            text = await _metrics(base)
+            assert 'nanogpu_native_binds_total{result="ok"} 6' in text
+            failures = int(next(ln.split()[1] for ln in text.splitlines()
+                                if ln.startswith("nanogpu_native_label_failures_total ")))
+            if faults.get("patch_error_rate") == 1.0:
+                assert labelled() == 0 and failures == 6
+                assert store.events == []                           # no rollback, no FailedBinding
+            else:   # a 50 % 5xx rate can outlast the retries: every label lands or is counted
+                assert labelled() + failures == 6
+        finally:
+            await rt.stop()
+            await runner.cleanup()
+
+    asyncio.run(main())
