@@ -114,6 +114,9 @@ def parse_args():
     ap.add_argument("--no-gpu", action="store_true", help="skip GPU discovery (CPU-only rehearsal)")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--profile-out", default="", help="cProfile the timed steps (rank 0) into this file")
+    ap.add_argument("--cpu-profile-out", default="",
+                    help="native CPU sampling profile of the headline pass's timed steps (rank 0's "
+                         "extender process, every thread, symbolized) as JSON into this file")
     ap.add_argument("--no-nominate", action="store_true", help="priorities do not nominate (Ledger::nominate)")
     ap.add_argument("--no-kube-combine", action="store_true",
                     help="the stand-in takes the extender's arg-max instead of kube-scheduler's plugin + "
@@ -1018,6 +1021,11 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         prof = cProfile.Profile()
         prof.enable()
     sampler = StallSampler() if args.stall_trace and d.rank == 0 else None
+    native_prof = bool(args.cpu_profile_out and d.rank == 0 and getattr(args, "_headline", False))
+    if native_prof:
+        from nanogpu import _native
+
+        native_prof = _native.sampler_start(1000)
     nom0 = rt.state.ledger.nomination_counts()
     fe_stats = rt.native.fe.stats if rt.native is not None else (lambda: {})
     handoffs0 = fe_stats().get("bind_handoffs", 0)
@@ -1033,6 +1041,11 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         results.setdefault("phases", []).append(r["phases"])
     if sampler is not None:
         sampler.report(args.stall_trace)
+    if native_prof:
+        from nanogpu import _native
+        from nanogpu.obs import cpu_profile
+
+        Path(args.cpu_profile_out).write_text(json.dumps(cpu_profile(_native.sampler_stop()), indent=1))
     if prof is not None:
         import io
         import pstats
@@ -1146,7 +1159,9 @@ def main() -> int:
     topo, gpu_info = node_template(d, args)
     variant = inproc_v = steady_v = nodes_v = one_v = None
     try:
+        args._headline = True    # the native CPU profile covers this pass only
         res = run_pass(d, args, topo, conn, "main", api_proc)
+        args._headline = False
         shared_api = not args.inproc_api and not args.inproc_driver
         if args.steady_variant_steps > 0 and not args.steady and shared_api:
             # steady-state churn (BASELINE config 5 at scale): the cluster is never emptied

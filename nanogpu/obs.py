@@ -216,3 +216,84 @@ def sample_profile(seconds: float = 5.0, interval: float = 0.005, top: int = 40)
     for stack, n in counts.most_common(top):
         lines.append(f"{n:6d} {stack}")
     return "\n".join(lines)
+
+
+def _maps() -> list[tuple[int, int, int, str]]:
+    """(start, end, file offset, path) of this process's file-backed executable mappings."""
+    out = []
+    with open("/proc/self/maps") as f:
+        for ln in f:
+            parts = ln.split(None, 5)
+            if len(parts) < 6 or "x" not in parts[1]:
+                continue
+            a, b = (int(x, 16) for x in parts[0].split("-"))
+            out.append((a, b, int(parts[2], 16), parts[5].strip()))
+    out.sort()
+    return out
+
+
+def _symbolize(pcs: set[int]) -> dict[int, str]:
+    """pc -> "function (object)" through /proc/self/maps and addr2line (llvm-symbolizer when
+    binutils is missing); unmapped or anonymous code keeps its address."""
+    import os
+    import shutil
+    import subprocess
+
+    maps = _maps()
+    starts = [m[0] for m in maps]
+    by_obj: dict[str, list[tuple[int, int]]] = collections.defaultdict(list)
+    names: dict[int, str] = {}
+    for pc in pcs:
+        i = bisect.bisect_right(starts, pc) - 1
+        if i < 0 or pc >= maps[i][1]:
+            names[pc] = hex(pc)               # anonymous code (a JIT, a trampoline)
+            continue
+        if not maps[i][3].startswith("/"):
+            names[pc] = maps[i][3]            # [vdso]: a clock read or its syscall fallback
+            continue
+        a, _b, off, path = maps[i]
+        by_obj[path].append((pc, pc - a + off))
+    tool = shutil.which("addr2line") or shutil.which("llvm-addr2line") or "/opt/rocm/lib/llvm/bin/llvm-addr2line"
+    for path, items in by_obj.items():
+        obj = os.path.basename(path)
+        fns = []
+        if os.path.exists(tool):
+            try:
+                r = subprocess.run([tool, "-f", "-C", "-e", path] + [hex(o) for _pc, o in items],
+                                   capture_output=True, text=True, timeout=60)
+                lines = r.stdout.splitlines()
+                fns = lines[0::2] if len(lines) == 2 * len(items) else []
+            except (OSError, subprocess.SubprocessError):
+                fns = []
+        for k, (pc, o) in enumerate(items):
+            fn = fns[k] if k < len(fns) and fns[k] != "??" else f"+{o:#x}"
+            names[pc] = f"{fn.split('(')[0][:90]} ({obj})"
+    return names
+
+
+def cpu_profile(samples: list[tuple[int, int, int]], top: int = 25) -> dict:
+    """Per thread group (the bench's groups: main, ngpu-fe, ngpu-wr-io, ...), the share of
+    samples in each function, from the native sampler (nanogpu._native.sampler_stop). A leaf in
+    a libc system-call stub (send, recv, epoll_wait, ...) is the kernel time of that call. libc's
+    internal routines (memcpy, memchr, malloc's) have no exported symbol: addr2line names them
+    after the nearest exported one (e.g. __nss_database_lookup)."""
+    import os
+
+    comm: dict[int, str] = {}
+    pid = os.getpid()
+    for tid in {s[2] for s in samples}:
+        try:
+            with open(f"/proc/{pid}/task/{tid}/comm") as f:
+                c = f.read().strip()
+        except OSError:
+            c = "exited"
+        comm[tid] = "main" if tid == pid else (c.rstrip("0123456789") if c.startswith("ngpu-") else "other")
+    names = _symbolize({s[0] for s in samples})
+    groups: dict[str, collections.Counter] = collections.defaultdict(collections.Counter)
+    for pc, _caller, tid in samples:
+        groups[comm[tid]][names[pc]] += 1
+    out = {"samples": len(samples)}
+    for g, cnt in sorted(groups.items(), key=lambda kv: -sum(kv[1].values())):
+        n = sum(cnt.values())
+        out[g] = {"samples": n, "top": [[name, round(100.0 * k / n, 1)] for name, k in cnt.most_common(top)]}
+    return out

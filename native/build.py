@@ -28,7 +28,7 @@ EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 ARCH = os.environ.get("NANOGPU_OFFLOAD_ARCH", "gfx950")
 
 CORE_SOURCES = ["alloc.cpp", "ledger.cpp", "topo.cpp", "json.cpp", "frontend.cpp", "schedsim.cpp", "apiserver.cpp",
-                "kubewriter.cpp", "kubewriter_evented.cpp", "podwatch.cpp"]
+                "kubewriter.cpp", "kubewriter_evented.cpp", "podwatch.cpp", "sampler.cpp"]
 
 
 def _pybind_includes() -> list[str]:

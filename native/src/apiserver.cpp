@@ -1141,6 +1141,13 @@ void Server::Impl::on_readable(IoThread* t, const std::shared_ptr<Conn>& c) {
       c->out += resp;
     }
     if (close_req) c->close_after = true;
+    // a pipelined request behind this one: its answer goes out first, as Go's net/http (kube-
+    // apiserver) flushes every response when its handler returns; an answer never waits for
+    // the next request's handling
+    if (!c->in.empty() && !c->close_after && lat <= 0 && t->delayed.empty() && !write_out(c.get())) {
+      close_conn(t, c);
+      return;
+    }
   }
   if (!write_out(c.get())) {
     close_conn(t, c);

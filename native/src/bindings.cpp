@@ -15,6 +15,7 @@
 #include "nanogpu/json.h"
 #include "nanogpu/ledger.h"
 #include "nanogpu/podwatch.h"
+#include "nanogpu/sampler.h"
 #include "nanogpu/schedsim.h"
 #include "nanogpu/topo.h"
 
@@ -885,6 +886,14 @@ PYBIND11_MODULE(_native, m) {
            "Runs the native verb `iters` times in place (no socket): (ok, seconds per call, last body).")
       .def("reset_max", &Frontend::reset_max, "zero the per-verb and event-loop maxima");
   m.def("mono_now", &mono_now);
+  m.def("sampler_start", &sampler::start, py::arg("hz") = 1000,
+        "CPU sampling profiler: SIGPROF every 1/hz s of process CPU time (false: already running).");
+  m.def("sampler_stop", []() {
+    const std::vector<sampler::Sample> v = sampler::stop();
+    py::list out;
+    for (const auto& x : v) out.append(py::make_tuple(x.pc, x.caller, x.tid));
+    return out;
+  }, "Stops the sampler: [(pc, caller pc or 0, tid)] (nanogpu.obs.cpu_profile symbolizes them).");
   m.def("num_feasible_nodes_to_find", &sim::num_feasible_nodes_to_find, py::arg("all_nodes"),
         py::arg("percentage") = 0, "kube-scheduler's numFeasibleNodesToFind (schedsim.h)");
   m.def("presize_fd_table", &presize_fd_table, py::arg("want") = 16384,
