@@ -116,6 +116,26 @@ bool Doc::parse(std::string_view src) {
   return p_ == src_.size();
 }
 
+// The first quote, backslash or control character at or after q (n if none): sixteen bytes at
+// a time, the bytes of a string that need no look one by one.
+static inline size_t plain_run_end(const char* s, size_t q, size_t n) {
+  const __m128i quote = _mm_set1_epi8('"'), bslash = _mm_set1_epi8('\\'), ctl = _mm_set1_epi8(0x1f);
+  while (q + 16 <= n) {
+    const __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + q));
+    const __m128i m = _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(x, quote), _mm_cmpeq_epi8(x, bslash)),
+                                   _mm_cmpeq_epi8(_mm_min_epu8(x, ctl), x));
+    const unsigned mask = static_cast<unsigned>(_mm_movemask_epi8(m));
+    if (mask) return q + static_cast<size_t>(__builtin_ctz(mask));
+    q += 16;
+  }
+  while (q < n) {
+    const unsigned char ch = static_cast<unsigned char>(s[q]);
+    if (ch == '"' || ch == '\\' || ch < 0x20) break;
+    ++q;
+  }
+  return q;
+}
+
 bool Doc::string(uint32_t* off, uint32_t* len) {
   if (p_ >= src_.size() || src_[p_] != '"') return false;
   ++p_;
@@ -123,12 +143,7 @@ bool Doc::string(uint32_t* off, uint32_t* len) {
   const size_t n = src_.size();
   {
     // common case: no escape before the closing quote -> the text stays in the source
-    size_t q = p_;
-    while (q < n) {
-      const unsigned char ch = static_cast<unsigned char>(s[q]);
-      if (ch == '"' || ch == '\\' || ch < 0x20) break;
-      ++q;
-    }
+    const size_t q = plain_run_end(s, p_, n);
     if (q < n && s[q] == '"') {
       *off = static_cast<uint32_t>(p_);
       *len = static_cast<uint32_t>(q - p_) | kInSrc;
@@ -141,11 +156,7 @@ bool Doc::string(uint32_t* off, uint32_t* len) {
     // a run of plain characters is copied in one go; only quotes, escapes and control
     // characters need a look
     const size_t run = p_;
-    while (p_ < n) {
-      const unsigned char ch = static_cast<unsigned char>(s[p_]);
-      if (ch == '"' || ch == '\\' || ch < 0x20) break;
-      ++p_;
-    }
+    p_ = plain_run_end(s, p_, n);
     if (p_ > run) arena_.append(s + run, p_ - run);
     if (p_ >= n) return false;
     const char c = s[p_++];

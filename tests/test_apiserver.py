@@ -391,3 +391,30 @@ def test_shallow_skip_agrees_with_the_full_parser_at_every_alignment():
                 outcomes.append(False)
         if not outcomes[1]:
             assert not outcomes[0], bad      # what the full parser rejects, the skip rejects
+
+
+def test_native_json_strings_match_python_at_every_alignment():
+    """json.cpp scans strings sixteen bytes at a time for the first quote, backslash or control
+    character: escapes and multi-byte UTF-8 at every offset of a 16-byte block decode exactly
+    as Python's json does, in plain and ensure_ascii encodings, and a raw control character
+    inside a string is rejected wherever it falls."""
+    import random
+
+    rnd = random.Random(11)
+    pieces = ['"', "\\", "/", "\n", "\t", "é", "€", "😀", "a", "b", " ", "\u0001"]
+    for i in range(300):
+        labels = {f"k{j}": "x" * rnd.randrange(0, 18) + "".join(rnd.choice(pieces) for _ in range(rnd.randrange(0, 12)))
+                  + "y" * rnd.randrange(0, 18) for j in range(rnd.randrange(1, 4))}
+        pod = pu.make_pod(f"p{i}", [("main", 10)])
+        pod["metadata"]["labels"] = labels
+        for ascii_only in (False, True):
+            line = json.dumps({"type": "MODIFIED", "object": pod}, ensure_ascii=ascii_only).encode() + b"\n"
+            got = N.decode_pod_watch(line)
+            assert got[0]["object"]["metadata"]["labels"] == labels
+    # a raw control byte inside a string, at each offset of a block
+    for k in range(20):
+        pod = pu.make_pod("c", [("main", 10)])
+        pod["metadata"]["labels"] = {"k": "z" * k + "CTL" + "w" * 20}
+        line = json.dumps({"type": "ADDED", "object": pod}).encode().replace(b"CTL", b"\x01") + b"\n"
+        with pytest.raises(ValueError):
+            N.decode_pod_watch(line)
