@@ -345,17 +345,27 @@ def test_agent_metrics_read_real_amdgpu_sysfs(host, P):
             prev = cur
         return prev
 
-    torch.cuda.synchronize()
-    torch.cuda.empty_cache()
-    before = settled()
-    x = torch.empty(4 << 30, dtype=torch.uint8, device="cuda:0")
-    x.fill_(1)
-    torch.cuda.synchronize()
-    grew = settled() - before
-    del x
-    torch.cuda.empty_cache()
-    record("agent_metrics_vram_delta_for_4GiB", grew)
-    assert grew >= (3 << 30), grew
+    # the counter is the whole device's: memory another process frees (or takes) during a
+    # reading moves it too (one box run read -40 GB across our 4 GiB allocation). Our 4 GiB
+    # must show as a rise on allocation or as a fall on free; up to 3 attempts
+    deltas = []
+    for _attempt in range(3):
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        before = settled()
+        x = torch.empty(4 << 30, dtype=torch.uint8, device="cuda:0")
+        x.fill_(1)
+        torch.cuda.synchronize()
+        during = settled()
+        del x
+        torch.cuda.empty_cache()
+        torch.cuda.synchronize()
+        after = settled()
+        deltas.append((during - before, during - after))
+        if max(deltas[-1]) >= (3 << 30):
+            break
+    record("agent_metrics_vram_delta_for_4GiB", deltas[-1][0])
+    assert any(max(d) >= (3 << 30) for d in deltas), deltas
 
 
 def test_hbm_bandwidth_under_cu_mask_sharing(P):
