@@ -46,6 +46,10 @@ def test_bench_single_rank_cpu():
     assert d["nodes_sent_per_filter_nodes120"] == 100.0
     assert d["value_mode"] == "one kube-scheduler stand-in" and d["value_one_scheduler"] == d["value"]
     assert d["frag_pct_nodes120_reference_model"] is not None
+    # extender CPU a pod: by thread group, and split into user / kernel time
+    assert d["extender_cpu_us_per_pod_rank0"] > 0 and "ngpu-fe" in d["extender_cpu_us_per_pod_by_thread_rank0"]
+    user, kernel = d["extender_cpu_us_per_pod_user_kernel_rank0"]
+    assert user >= 0 and kernel >= 0 and user + kernel > 0
 
 
 @pytest.mark.parametrize("ranks", [2, 4])
