@@ -24,7 +24,7 @@ namespace sampler {
 
 namespace {
 
-constexpr size_t kCap = 1 << 20;   // ~1M samples: 17 minutes of one core at 1 kHz
+constexpr size_t kCap = 1 << 18;   // 262k samples: over 15 minutes at the tick-bound rate
 Sample g_buf[kCap];
 std::atomic<size_t> g_n{0};
 std::atomic<bool> g_on{false};

@@ -489,3 +489,49 @@ def test_share_aware_learner_learns_a_lone_25pct_streamer_not_a_lone_75pct_mfma_
     curve = PolicySpec().learn_curve()
     assert L.learn_stream_owners(True, N.mono_now(), 3, curve) == (1, 0)
     assert L.is_stream_owner("rs-stream") and not L.is_stream_owner("rs-mfma")
+
+
+_RCCL_SCRIPT = r"""
+import json, os, sys
+import torch
+import torch.distributed as dist
+sys.path.insert(0, os.environ["NANOGPU_ROOT"])
+from nanogpu.probe.calibrate import link_matrix, ring_busbw
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+out = {"backend": dist.get_backend()}
+out["busbw"] = ring_busbw(dist, "cuda:0", nbytes=64 << 20, iters=3)   # one rank: 0 by definition
+t = torch.full((1 << 20,), 2.0, dtype=torch.bfloat16, device="cuda:0")
+dist.all_reduce(t)
+out["allreduce_ok"] = bool((t == 2.0).all().item())
+out["matrix"] = link_matrix(1, dist=dist, rank=0)                      # the all-gathered rows
+dist.barrier(device_ids=[0])
+got = [None]
+dist.all_gather_object(got, {"rank": 0})
+lst = ["url"]
+dist.broadcast_object_list(lst, src=0)
+out["objects"] = [got[0]["rank"], lst[0]]
+dist.destroy_process_group()
+print(json.dumps(out))
+"""
+
+
+def test_rccl_paths_of_the_multi_rank_bench_run_on_the_device(tmp_path):
+    """The collectives a driver N-GPU bench run uses (torch.distributed backend "nccl" = RCCL
+    on ROCm): RCCL all-reduce (ring_busbw), the peer-matrix all-gather, the device barrier and
+    the object collectives, on the box's one MI355X with a one-rank group. A 2-rank group
+    needs two GPUs (RCCL refuses two ranks on one device)."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parent.parent
+    env = dict(os.environ, NANOGPU_ROOT=str(root), MASTER_ADDR="127.0.0.1", MASTER_PORT="29613",
+               HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-c", _RCCL_SCRIPT], capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    record("rccl_one_rank", out)
+    assert out["backend"] == "nccl" and out["allreduce_ok"]
+    assert out["busbw"] == 0.0 and out["matrix"] == [[0.0]] and out["objects"] == [0, "url"]
