@@ -16,7 +16,6 @@
 #include <cerrno>
 #include <chrono>
 #include <cmath>
-#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -709,10 +708,6 @@ void Frontend::run(Worker* w) {
   // completion, never starts a spin. Adaptive on top: the first event after a cycle reply is a
   // hit if it came within the spin window; a worker spins while at least half of its last 16
   // were hits (a slow scheduler, tens of microseconds between verbs, is not spun for).
-  // NANOGPU_FE_NAP=1: within the spin window, sleep in epoll with a timeout instead of
-  // polling (experiment: profiles/ab_results.md)
-  const char* nap_env = std::getenv("NANOGPU_FE_NAP");
-  const bool nap = nap_env && nap_env[0] == '1';
   uint32_t gaps = 0xffffu;   // 1 bits: hits among the last 16 cycle replies (start hot)
   uint64_t scored = 0;       // the cycle reply the last hit/miss was scored for
   // responses posted by the bind writer or Python: sent, then the connection's next request
@@ -752,25 +747,7 @@ void Frontend::run(Worker* w) {
         continue;
       }
     }
-    int n;
-    if (polling && nap) {
-      // nap instead of spinning: a wait bounded by what is left of the spin window. An event
-      // wakes the thread at once either way; the short timer keeps the CPU's idle governor in
-      // a shallow state, so the wake-up stays cheap while no CPU time is burnt polling
-      w->parked.store(true, std::memory_order_seq_cst);
-      if (w->mb_pending.load(std::memory_order_seq_cst)) {
-        w->parked.store(false, std::memory_order_relaxed);
-        drain_mailbox();
-        continue;
-      }
-      const uint64_t gone = now_ns() - since;
-      const uint64_t left = gone < static_cast<uint64_t>(spin) ? static_cast<uint64_t>(spin) - gone : 0;
-      timespec ts{0, static_cast<long>(std::min<uint64_t>(left, 999999999ull))};
-      n = epoll_pwait2(w->ep, evs, 128, &ts, nullptr);
-      if (n < 0 && errno == ENOSYS) n = epoll_wait(w->ep, evs, 128, 0);
-    } else {
-      n = epoll_wait(w->ep, evs, 128, polling ? 0 : 200);
-    }
+    const int n = epoll_wait(w->ep, evs, 128, polling ? 0 : 200);
     w->parked.store(false, std::memory_order_relaxed);
     const uint64_t t_batch = n > 0 ? now_ns() : 0;
     if (n > 0) {
