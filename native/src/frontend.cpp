@@ -887,7 +887,8 @@ void Frontend::process(Worker* w, Conn* c) {
       if (colon != std::string_view::npos) {
         const std::string_view k = trim(h.substr(0, colon)), v = trim(h.substr(colon + 1));
         if (ieq(k, "content-length")) {
-          clen = std::strtoull(std::string(v).c_str(), nullptr, 10);
+          // no allocation per request; a malformed length reads as too large (refused below)
+          if (std::from_chars(v.data(), v.data() + v.size(), clen).ec != std::errc()) clen = SIZE_MAX;
         } else if (ieq(k, "transfer-encoding")) {
           chunked = v.find("chunked") != std::string_view::npos;
         } else if (ieq(k, "connection")) {
