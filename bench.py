@@ -89,12 +89,14 @@ def parse_args():
     ap.add_argument("--nodes-variant-pods", type=int, default=0,
                     help="pods per burst of the --nodes-variant pass (0: --pods scaled to the same occupancy)")
     ap.add_argument("--nodes-variant-steps", type=int, default=2)
-    ap.add_argument("--one-scheduler", action="store_true",
-                    help="with N ranks: ONE kube-scheduler stand-in (rank 0's) drives every pod, its cycle on "
-                         "rank 0's extender worker, its binds spread over all N workers (a cluster has one "
-                         "active kube-scheduler). Default: N independent stand-ins, one per rank")
-    ap.add_argument("--one-scheduler-variant-steps", type=int, default=5,
-                    help="with N > 1 ranks, after the timed steps, a --one-scheduler pass (0: none)")
+    ap.add_argument("--independent-schedulers", action="store_true",
+                    help="with N ranks: N independent kube-scheduler stand-ins, one per extender worker, each "
+                         "scheduling 1/N of the burst. Default: ONE stand-in (rank 0's) drives every pod, its "
+                         "cycle on rank 0's extender worker, its binds spread over all N workers (a cluster "
+                         "runs one active kube-scheduler)")
+    ap.add_argument("--independent-variant-steps", type=int, default=3,
+                    help="with N > 1 ranks, after the timed steps, an --independent-schedulers pass "
+                         "(value_independent_schedulers; 0: none)")
     ap.add_argument("--apiserver-threads", type=int, default=0,
                     help="shared API server IO threads (0: one per rank, 4 to 16)")
     ap.add_argument("--bind-writer-threads", type=int, default=0,
@@ -807,7 +809,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     all_steps = [10_000 + w for w in range(args.warmup)] + list(range(args.steps))
     bursts = {} if steady else {s: burst(d.rank, d.world, args.pods, s, 7) for s in all_steps}
 
-    # --one-scheduler: ONE kube-scheduler stand-in for the job (rank 0's) drives every pod; its
+    # one scheduler (the default with N ranks): ONE kube-scheduler stand-in for the job (rank 0's) drives every pod; its
     # scheduling cycle stays on rank 0's worker, its binds spread over every rank's worker (the
     # connections a Service spreads over an extender's workers)
     one = bool(getattr(args, "one_scheduler", False)) and d.world > 1
@@ -1031,6 +1033,9 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     handoffs0 = fe_stats().get("bind_handoffs", 0)
     cpu0, loop_cpu0 = time.process_time(), time.thread_time()
     threads0, ticks0, times0 = thread_cpu(), thread_ticks(), os.times()
+    from nanogpu import affinity
+
+    snap0 = affinity.cpu_snapshot()
     t0 = time.perf_counter()
     if sampler is not None:
         sampler.on.set()
@@ -1057,6 +1062,14 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     await barrier()
     d.sync()
     elapsed = time.perf_counter() - t0
+    # how busy this rank's cores, their SMT siblings, the API server's and the whole host were
+    # while the clock ran (other tenants on the siblings slow every hand-off)
+    mine = sorted(os.sched_getaffinity(0))
+    groups = {"rank": mine, "rank_smt_siblings": affinity.smt_siblings(mine)} \
+        if len(mine) < (os.cpu_count() or 1) else {}
+    if apisrv is not None and apisrv.cpus:
+        groups.update(apiserver=apisrv.cpus, apiserver_smt_siblings=affinity.smt_siblings(apisrv.cpus))
+    results["cpu_busy_pct"] = affinity.busy_report(snap0, affinity.cpu_snapshot(), groups)
     nom1 = rt.state.ledger.nomination_counts()
     results["nominations"] = {k: nom1[k] - nom0[k] for k in nom1}
     # binds a worker answered natively with the pod another worker's filter parsed (the
@@ -1113,6 +1126,127 @@ def _cpulist(cpus: list[int]) -> str:
     return ",".join(map(str, cpus)) if cpus else "unpinned"
 
 
+# printed last on the line, in this order: what BASELINE's metric is made of
+HEADLINE_LAST = ("value_independent_schedulers", "frag_pct_steady_reference_model", "frag_pct_steady",
+                 "extender_cpu_us_per_pod_rank0", "frag_pct_reference_model", "frag_hbm_pct", "frag_pct",
+                 "p99_bind_ms", "p50_bind_ms", "pods_per_s_first_filter_to_last_bind", "value")
+# bulky per-step / per-thread records: --json-out only
+DIAG_KEYS = ("step_diag_rank0", "schedule_ms_each_step_rank0", "phase_ms_per_step_rank0",
+             "extender_cpu_us_per_pod_by_thread_rank0", "extender_kernel_pct_by_thread_rank0",
+             "extender_cpu_us_per_pod_user_kernel_rank0", "frag_pct_steady_each_step", "nominations",
+             "nominations_steady", "native_verb_mean_us", "frag_reference_model_source", "host_selection",
+             "one_scheduler_config", "steady_config", "cpu_layout")
+
+
+def order_line(full: dict) -> tuple[dict, dict]:
+    """(the printed line, the diagnostics): diagnostics and every `nominations_*` /
+    `native_verb_mean_us_*` map move out; the headline keys go last."""
+    diag = {k: full[k] for k in full
+            if k in DIAG_KEYS or k.startswith(("nominations_", "native_verb_mean_us_"))}
+    line = {k: v for k, v in full.items() if k not in diag and k not in HEADLINE_LAST}
+    for k in HEADLINE_LAST:
+        if k in full:
+            line[k] = full[k]
+    return line, diag
+
+
+def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc, gpu_info: dict, topo,
+                  variant, one_v, steady_v, nodes_v, inproc_v) -> tuple[dict, dict]:
+    from nanogpu import affinity
+
+    fr = res["frag"]
+    full = {
+        "metric": METRIC, "value": out["value"], "unit": "pods/s", "n_gpus": d.world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": out["ms_per_step"],
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "n/a",
+        # who drives the extender: a cluster runs ONE active kube-scheduler, so with N ranks the
+        # headline is one stand-in whose binds spread over every worker
+        # (--independent-schedulers: one per rank, value_independent_schedulers)
+        "value_mode": ("one kube-scheduler stand-in" if d.world == 1 else
+                       f"one kube-scheduler stand-in, binds over all {d.world} extender workers"
+                       if args.one_scheduler else
+                       f"{d.world} independent kube-scheduler stand-ins, one per extender worker"),
+        "data": "synthetic (pod bursts; simulated nodes cloned from the discovered MI355X)",
+        "config": {"model": f"nano-gpu-scheduler extender ({args.policy}{', compat' if args.compat else ''})",
+                   "global_batch": args.pods, "seq_len": None,
+                   "parallelism": f"{d.world} extender worker(s), shared native ledger",
+                   "cluster": f"{args.nodes} nodes x {args.gpus_per_node} MI355X ({args.partition})",
+                   "api_rtt_ms": args.api_rtt_ms,
+                   # one native HTTP API server in its own process shared by all ranks (default),
+                   # or --inproc-api's per-rank in-process store (value_inproc_api)
+                   "api_server": ("in-process store per rank" if args.inproc_api else
+                                  f"one native HTTP API server, own process "
+                                  f"({args.apiserver_threads or min(16, max(4, d.world))} IO threads)"),
+                   "cpus_rank0": _cpulist(cpus),
+                   "cpus_apiserver": _cpulist(api_proc.cpus) if api_proc is not None else None,
+                   "frontend": f"{args.frontend_threads} threads, busy-poll {args.busy_poll_us} us"},
+        # physical cores vs SMT siblings of the pinned CPUs, and how busy the siblings were
+        "cpu_layout": {"rank0": affinity.cpu_layout(cpus),
+                       "apiserver": affinity.cpu_layout(api_proc.cpus) if api_proc is not None else None},
+        "cpu_busy_pct_rank0": res.get("cpu_busy_pct"),
+        "pods_per_s_first_filter_to_last_bind": out["value_burst_window"],
+        # POST /scheduler/bind wall time as kube-scheduler's stand-in sees it (request written ->
+        # reply read), every bind of the timed steps on all ranks
+        "p50_bind_ms": out["p50_bind_ms"], "p99_bind_ms": out["p99_bind_ms"],
+        # extender side of the same binds: request bytes read -> reply handed to the kernel
+        "p50_bind_frontdoor_ms": out["p50_bind_frontdoor_ms"],
+        "p99_bind_frontdoor_ms": out["p99_bind_frontdoor_ms"],
+        "frag_pct": round(statistics.mean(f["frag_pct"] for f in fr), 3) if fr else None,
+        "frag_hbm_pct": round(statistics.mean(f["frag_mib"] for f in fr), 3) if fr else None,
+        "stranded_pct": round(statistics.mean(f["stranded_pct"] for f in fr), 3) if fr else None,
+        "scheduled": out["scheduled"], "failed": out["failed"], "bind_retries": out["bind_errors"],
+        "host_selection": "extender arg-max" if args.no_kube_combine else
+                          "kube-scheduler combining (LeastAllocated + BalancedAllocation + 10 x extender)",
+        "nominations": res["nominations"],
+        "nomination_adopt_pct": (round(100.0 * res["nominations"]["adopted"] / res["nominations"]["made"], 2)
+                                 if res["nominations"]["made"] else None),
+        "p50_queue_to_bound_ms_rank0": (round(statistics.mean(st.get("e2e_p50_ms", 0.0) for st in res["steps"]), 3)
+                                        if res["steps"] else None),
+        "unschedulable_attempts": out["unschedulable"],
+        "gpu": gpu_info,
+        "native_verb_mean_us": res.get("native"),
+        "phase_ms_per_step_rank0": res.get("phase_ms"),
+        "schedule_ms_each_step_rank0": res.get("schedule_ms_steps"),
+        "schedule_ms_by_rank": out["schedule_ms_by_rank"],
+        "bind_handoffs": out["bind_handoffs"],
+        "step_diag_rank0": res.get("step_diag"),
+        # CPU time of the rank-0 extender process (all its threads) per pod it handled
+        "extender_cpu_us_per_pod_rank0": round(res.get("cpu_us_per_pod", 0.0), 1),
+        "extender_loop_cpu_us_per_pod_rank0": round(res.get("loop_cpu_us_per_pod", 0.0), 1),
+        "extender_cpu_us_per_pod_by_thread_rank0": res.get("cpu_us_per_pod_by_thread"),
+        "extender_cpu_us_per_pod_user_kernel_rank0": res.get("cpu_us_per_pod_user_kernel"),
+        "extender_kernel_pct_by_thread_rank0": res.get("kernel_pct_by_thread"),
+    }
+    full.update(reference_model_frag(args, topo))
+    if variant is not None:
+        tag = f"rtt{args.rtt_variant_ms:g}ms"
+        if "error" in variant:
+            full[f"value_{tag}"] = None
+            full[f"error_{tag}"] = variant["error"]
+        else:
+            full[f"value_{tag}"] = variant["value"]
+            full[f"p50_bind_ms_{tag}"] = variant["p50_bind_ms"]
+            full[f"p99_bind_ms_{tag}"] = variant["p99_bind_ms"]
+    if one_v is not None:
+        if "error" in one_v:
+            full["value_independent_schedulers"] = None
+            full["error_independent_schedulers"] = one_v["error"]
+        else:
+            full["value_independent_schedulers"] = one_v["value"]
+            full["p50_bind_ms_independent_schedulers"] = one_v["p50_bind_ms"]
+            full["steps_independent_schedulers"] = args.independent_variant_steps
+    full.update(steady_keys(args, topo, steady_v))
+    full.update(nodes_variant_keys(args, topo, nodes_v))
+    if inproc_v is not None:
+        if "error" in inproc_v:
+            full["value_inproc_api"] = None
+            full["error_inproc_api"] = inproc_v["error"]
+        else:
+            full["value_inproc_api"] = inproc_v["value"]
+            full["p50_bind_ms_inproc_api"] = inproc_v["p50_bind_ms"]
+    return order_line(full)
+
+
 def main() -> int:
     args = parse_args()
     cpus: list[int] = []
@@ -1156,6 +1290,8 @@ def main() -> int:
         api_proc = ApiServerProc(avoid=rank_cpus, near=rank0_numa)
     d = Dist(args.gpus)
     d.init(use_gpu=not args.no_gpu)
+    # the deployment that exists: one active kube-scheduler in front of every extender worker
+    args.one_scheduler = d.world > 1 and not args.independent_schedulers
     topo, gpu_info = node_template(d, args)
     variant = inproc_v = steady_v = nodes_v = one_v = None
     try:
@@ -1175,9 +1311,11 @@ def main() -> int:
                 steady_v = (s_args, steady_v[1], summarize(d, s_args, steady_v[1]))
             except Exception as e:
                 steady_v = {"error": f"{type(e).__name__}: {e}"}
-        if d.world > 1 and args.one_scheduler_variant_steps > 0 and not args.one_scheduler and not args.steady:
-            o_args = argparse.Namespace(**{**vars(args), "one_scheduler": True,
-                                           "steps": args.one_scheduler_variant_steps, "warmup": 1,
+        if d.world > 1 and args.independent_variant_steps > 0 and args.one_scheduler and not args.steady:
+            # N kube-schedulers, one per worker: what the workers sustain when the one
+            # scheduler's serial cycle is not the limit (a deployment nobody runs; labelled)
+            o_args = argparse.Namespace(**{**vars(args), "one_scheduler": False,
+                                           "steps": args.independent_variant_steps, "warmup": 1,
                                            "profile_out": "", "stall_trace": "", "api_rtt_ms": 0.0})
             try:
                 one_v = summarize(d, o_args, run_pass(d, o_args, topo, conn, "one", api_proc))
@@ -1207,7 +1345,8 @@ def main() -> int:
                 variant = {"error": f"{type(e).__name__}: {e}"}
         if args.inproc_variant_steps > 0 and not args.inproc_api and not args.inproc_driver:
             # round 1's extender-isolated setup: an in-process store per rank, no HTTP
-            i_args = argparse.Namespace(**{**vars(args), "inproc_api": True, "api_rtt_ms": 0.0,
+            # (each rank its own store: a stand-in per rank, each binding on its own worker)
+            i_args = argparse.Namespace(**{**vars(args), "inproc_api": True, "api_rtt_ms": 0.0, "one_scheduler": False,
                                            "steps": args.inproc_variant_steps, "warmup": 1,
                                            "profile_out": "", "stall_trace": ""})
             try:
@@ -1227,121 +1366,13 @@ def main() -> int:
             api_proc.close()
     out = summarize(d, args, res)
     if d.rank == 0:
-        fr = res["frag"]
-        line = {
-            "metric": METRIC, "value": out["value"], "unit": "pods/s", "n_gpus": d.world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": out["ms_per_step"],
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "n/a",
-            # who drives the extender: a cluster runs ONE active kube-scheduler; with N ranks the
-            # headline runs one stand-in per rank unless --one-scheduler (value_one_scheduler is
-            # the one-scheduler figure of an N-rank job)
-            "value_mode": ("one kube-scheduler stand-in" if d.world == 1 or args.one_scheduler else
-                           f"{d.world} independent kube-scheduler stand-ins, one per extender worker, "
-                           f"each scheduling 1/{d.world} of the burst"),
-            "data": "synthetic (pod bursts; simulated nodes cloned from the discovered MI355X)",
-            "config": {"model": f"nano-gpu-scheduler extender ({args.policy}{', compat' if args.compat else ''})",
-                       "global_batch": args.pods, "seq_len": None,
-                       "parallelism": f"{d.world} extender worker(s), shared native ledger",
-                       "cluster": f"{args.nodes} nodes x {args.gpus_per_node} MI355X ({args.partition})",
-                       "api_rtt_ms": args.api_rtt_ms,
-                       # the API server every bind writes to and the pod controller watches:
-                       # one native HTTP API server in its own process shared by all ranks
-                       # (default), or --inproc-api's per-rank in-process store (value_inproc_api)
-                       "api_server": ("in-process store per rank, extender-isolated" if args.inproc_api else
-                                      f"one native HTTP API server for all ranks, own process "
-                                      f"({args.apiserver_threads or min(16, max(4, d.world))} IO threads), REST + watch"),
-                       "cpus_rank0": _cpulist(cpus),
-                       "cpus_apiserver": _cpulist(api_proc.cpus) if api_proc is not None else None,
-                       # next burst created by the clients while this one is released
-                       "create_overlaps_release": not (args.inproc_api or args.no_overlap_create),
-                       "frontend": f"{args.frontend_threads} threads, busy-poll {args.busy_poll_us} us"},
-            # POST /scheduler/bind wall time as kube-scheduler's stand-in sees it (request
-            # written -> reply read), over every bind of the timed steps on all ranks
-            # BASELINE.md's pods/s definition: bound / (last bind - first filter) of each burst;
-            # `value` also counts each step's pod creation and delete + release
-            "pods_per_s_first_filter_to_last_bind": out["value_burst_window"],
-            "p50_bind_ms": out["p50_bind_ms"], "p99_bind_ms": out["p99_bind_ms"],
-            # extender side of the same binds: request bytes read -> reply handed to the kernel
-            "p50_bind_frontdoor_ms": out["p50_bind_frontdoor_ms"],
-            "p99_bind_frontdoor_ms": out["p99_bind_frontdoor_ms"],
-            # sub-phase: the Python half (API writes + ledger commit)
-            "p50_bind_python_ms": out["p50_bind_python_ms"],
-            "frag_pct": round(statistics.mean(f["frag_pct"] for f in fr), 3) if fr else None,
-            "frag_hbm_pct": round(statistics.mean(f["frag_mib"] for f in fr), 3) if fr else None,
-            "stranded_pct": round(statistics.mean(f["stranded_pct"] for f in fr), 3) if fr else None,
-            "scheduled": out["scheduled"], "failed": out["failed"], "bind_retries": out["bind_errors"],
-            # how kube-scheduler's stand-in picks among the extender's scores: its plugin +
-            # weight x 10 x extender sum ("kube", nanogpu/sim/kubescore.py) or the arg-max
-            "host_selection": "extender arg-max" if args.no_kube_combine else
-                              "kube-scheduler combining (LeastAllocated + BalancedAllocation + 10 x extender)",
-            # priorities-time nominations (shared ledger, timed steps): share adopted by the bind,
-            # moved elsewhere by kube-scheduler's own scores, and the adaptive score lead
-            "nominations": res["nominations"],
-            "nomination_adopt_pct": (round(100.0 * res["nominations"]["adopted"] / res["nominations"]["made"], 2)
-                                     if res["nominations"]["made"] else None),
-            "nomination_margin": res["nomination_margin"],
-            # also end to end, from the pod entering the stand-in's queue (the burst
-            # is created at once) to its bind answered; rank 0, mean of the per-step medians
-            "p50_queue_to_bound_ms_rank0": (round(statistics.mean(st.get("e2e_p50_ms", 0.0) for st in res["steps"]), 3)
-                                            if res["steps"] else None),
-            "unschedulable_attempts": out["unschedulable"],
-            "gpu": gpu_info,
-            "native_verb_mean_us": res.get("native"),
-            "phase_ms_per_step_rank0": res.get("phase_ms"),
-            "schedule_ms_each_step_rank0": res.get("schedule_ms_steps"),
-            "schedule_ms_by_rank": out["schedule_ms_by_rank"],
-            # per timed step (rank 0): slowest scheduling cycle and bind seen by the stand-in,
-            # pods the cycle found no host for, cyclic-GC pause time of the extender process
-            "step_diag_rank0": res.get("step_diag"),
-            # CPU time of the rank-0 extender process (all its threads) per pod it handled
-            "extender_cpu_us_per_pod_rank0": round(res.get("cpu_us_per_pod", 0.0), 1),
-            # of which the Python event-loop thread (binds' API writes, informer, controller)
-            "extender_loop_cpu_us_per_pod_rank0": round(res.get("loop_cpu_us_per_pod", 0.0), 1),
-            # the same CPU by thread group: main (event loop), ngpu-fe (native front door epoll
-            # workers, busy polling included), ngpu-wr (native bind writers), other
-            "extender_cpu_us_per_pod_by_thread_rank0": res.get("cpu_us_per_pod_by_thread"),
-            # [user, kernel] µs a pod, and each thread group's kernel share of its CPU
-            "extender_cpu_us_per_pod_user_kernel_rank0": res.get("cpu_us_per_pod_user_kernel"),
-            "extender_kernel_pct_by_thread_rank0": res.get("kernel_pct_by_thread"),
-        }
-        line.update(reference_model_frag(args, topo))
-        if variant is not None:
-            tag = f"rtt{args.rtt_variant_ms:g}ms"
-            if "error" in variant:
-                line[f"value_{tag}"] = None
-                line[f"error_{tag}"] = variant["error"]
-            else:
-                line[f"value_{tag}"] = variant["value"]
-                line[f"p50_bind_ms_{tag}"] = variant["p50_bind_ms"]
-                line[f"p99_bind_ms_{tag}"] = variant["p99_bind_ms"]
-                line[f"steps_{tag}"] = args.rtt_variant_steps
-        if one_v is not None:
-            if "error" in one_v:
-                line["value_one_scheduler"] = None
-                line["error_one_scheduler"] = one_v["error"]
-            else:
-                line["value_one_scheduler"] = one_v["value"]
-                line["p50_bind_ms_one_scheduler"] = one_v["p50_bind_ms"]
-                line["bind_handoffs_one_scheduler"] = one_v["bind_handoffs"]
-                line["steps_one_scheduler"] = args.one_scheduler_variant_steps
-                line["one_scheduler_config"] = (f"one kube-scheduler stand-in: cycle on rank 0's worker, binds "
-                                                f"over all {d.world} workers")
-        elif d.world == 1 or args.one_scheduler:
-            line["value_one_scheduler"] = out["value"]      # the headline is already one scheduler
-        line.update(steady_keys(args, topo, steady_v))
-        line.update(nodes_variant_keys(args, topo, nodes_v))
-        if inproc_v is not None:
-            if "error" in inproc_v:
-                line["value_inproc_api"] = None
-                line["error_inproc_api"] = inproc_v["error"]
-            else:
-                line["value_inproc_api"] = inproc_v["value"]
-                line["p50_bind_ms_inproc_api"] = inproc_v["p50_bind_ms"]
-                line["p99_bind_ms_inproc_api"] = inproc_v["p99_bind_ms"]
-                line["steps_inproc_api"] = args.inproc_variant_steps
+        line, diag = headline_line(d, args, res, out, cpus, api_proc, gpu_info, topo,
+                                   variant, one_v, steady_v, nodes_v, inproc_v)
+        # the driver keeps the last 8 KB of stdout: ONE compact line (< 4 KB) with the
+        # headline keys last; the per-step diagnostics go to --json-out only
         print(json.dumps(line), flush=True)
         if args.json_out:
-            Path(args.json_out).write_text(json.dumps(line, indent=1))
+            Path(args.json_out).write_text(json.dumps({**line, "diagnostics": diag}, indent=1))
     d.close()
     return 0
 

@@ -71,26 +71,64 @@ def numa_of_cpu(cpu: int, root: Path = SYS_CPU) -> int:
     return -1
 
 
-def _busy(cpus: list[int], window_s: float) -> dict[int, float]:
-    def snap() -> dict[int, tuple[int, int]]:
-        out = {}
-        for line in _read(Path("/proc/stat")).splitlines():
-            if line.startswith("cpu") and line[3:4].isdigit():
-                f = line.split()
-                v = [int(x) for x in f[1:]]
-                idle = v[3] + (v[4] if len(v) > 4 else 0)
-                out[int(f[0][3:])] = (sum(v), idle)
-        return out
+def cpu_snapshot(stat: Path = Path("/proc/stat")) -> dict[int, tuple[int, int]]:
+    """Per CPU (total, idle) jiffies since boot."""
+    out = {}
+    for line in _read(stat).splitlines():
+        if line.startswith("cpu") and line[3:4].isdigit():
+            f = line.split()
+            v = [int(x) for x in f[1:]]
+            idle = v[3] + (v[4] if len(v) > 4 else 0)
+            out[int(f[0][3:])] = (sum(v), idle)
+    return out
 
-    a = snap()
-    time.sleep(window_s)
-    b = snap()
+
+def busy_between(a: dict, b: dict, cpus) -> dict[int, float]:
+    """Busy fraction of each CPU between two cpu_snapshot()s."""
     res = {}
     for c in cpus:
         if c in a and c in b:
             tot = b[c][0] - a[c][0]
             res[c] = 1.0 - (b[c][1] - a[c][1]) / tot if tot > 0 else 0.0
     return res
+
+
+def _busy(cpus: list[int], window_s: float) -> dict[int, float]:
+    a = cpu_snapshot()
+    time.sleep(window_s)
+    return busy_between(a, cpu_snapshot(), cpus)
+
+
+def smt_siblings(cpus: list[int], root: Path = SYS_CPU) -> list[int]:
+    """The other hardware threads of the cores `cpus` sit on (not in `cpus` themselves)."""
+    mine = set(cpus)
+    out: set[int] = set()
+    for c in cpus:
+        out.update(_parse_list(_read(root / f"cpu{c}" / "topology" / "thread_siblings_list")))
+    return sorted(out - mine)
+
+
+def cpu_layout(cpus: list[int], root: Path = SYS_CPU) -> dict | None:
+    """Physical-core / SMT layout of a pinned CPU set: the cores, their sibling threads,
+    the L3 domains and NUMA nodes they span."""
+    if not cpus:
+        return None
+    cores = {tuple(_parse_list(_read(root / f"cpu{c}" / "topology" / "thread_siblings_list")) or [c])
+             for c in cpus}
+    return {"cpus": len(cpus), "physical_cores": len(cores), "smt_siblings": smt_siblings(cpus, root),
+            "whole_cores": all(set(core) <= set(cpus) for core in cores),
+            "numa": sorted({numa_of_cpu(c, root) for c in cpus})}
+
+
+def busy_report(a: dict, b: dict, groups: dict[str, list[int]]) -> dict[str, float | None]:
+    """Mean busy % of each named CPU group between two snapshots, plus the whole host."""
+    out: dict[str, float | None] = {}
+    for name, cs in groups.items():
+        v = busy_between(a, b, cs)
+        out[name] = round(100.0 * sum(v.values()) / len(v), 1) if v else None
+    v = busy_between(a, b, list(b))
+    out["host"] = round(100.0 * sum(v.values()) / len(v), 1) if v else None
+    return out
 
 
 def pick_cpus(numa: int = -1, local_rank: int = 0, local_ranks_numa: list[int] | None = None,
