@@ -53,6 +53,7 @@ class Config:
     # the reference's `nano-gpu/assume` label, PATCHed beside the binding; off: one write a bind
     # (the binding carries the annotations; this project's agent selects pods by node)
     assume_label: bool = True
+    api_write_timeout_s: float = 30.0           # native bind writer: an API answer due within this
     reservation_ttl_s: float = 60.0
     nominate: bool = True              # priorities nominate the top node (Ledger::nominate)
     nomination_ttl_s: float = 5.0
@@ -211,7 +212,7 @@ class Runtime:
                     ext = self.extender
                     if self.native.enable_native_writes(api_cfg, self.cfg.bind_writer_threads, ext.api_retries,
                                                         ext.record_events, self.cfg.bind_writer_mode == "evented",
-                                                        self.cfg.assume_label):
+                                                        self.cfg.assume_label, self.cfg.api_write_timeout_s):
                         log.info("worker %d: bind API writes in native writer threads (%d)", self.worker,
                                  self.cfg.bind_writer_threads)
                 self.native.start()

@@ -63,6 +63,9 @@ def build_parser() -> argparse.ArgumentParser:
                         "threads, the number of blocking writer threads")
     p.add_argument("--bind-writer-mode", choices=["evented", "threads"], default="evented",
                    help="native bind writes on one epoll thread (evented) or on blocking threads")
+    p.add_argument("--api-write-timeout", default="30s",
+                   help="native bind writer: an API request unanswered this long fails over to the slow "
+                        "path (a half-open connection never answers)")
     p.add_argument("--no-assume-label", action="store_true",
                    help="bind with the binding alone (it carries the placement annotations) instead of also "
                         "PATCHing the reference's nano-gpu/assume label: one API write per bind; for clusters "
@@ -119,7 +122,8 @@ def parse(argv: list[str] | None = None) -> Config:
         ledger_path=a.ledger_path, max_nodes=a.max_nodes, max_pods=a.max_pods,
         verify_pod_on_bind=a.bind_verify_pod, native_bind_writes=a.native_bind_writes,
         bind_writer_threads=max(1, a.bind_writer_threads), bind_writer_mode=a.bind_writer_mode,
-        native_pod_watch=not a.no_native_pod_watch, assume_label=not a.no_assume_label, reservation_ttl_s=parse_duration(a.reservation_ttl),
+        native_pod_watch=not a.no_native_pod_watch, assume_label=not a.no_assume_label,
+        api_write_timeout_s=parse_duration(a.api_write_timeout), reservation_ttl_s=parse_duration(a.reservation_ttl),
         nominate=not a.no_nominate, nomination_ttl_s=parse_duration(a.nomination_ttl),
         fake_cluster=a.fake_cluster, fake_gpus_per_node=a.fake_gpus_per_node, fake_partition=a.fake_partition,
         seed=a.seed, frontend=a.frontend, frontend_threads=max(1, a.frontend_threads), busy_poll_us=a.busy_poll_us,

@@ -394,10 +394,14 @@ class NativeServer:
                       "# TYPE nanogpu_native_api_retries_total counter",
                       f"nanogpu_native_api_retries_total {kw['retries']}",
                       "# HELP nanogpu_native_api_write_seconds_total time in the bind's API writes: the "
-                      "binding and the label PATCH in flight together, then label-PATCH retries",
+                      "binding and the label PATCH behind it, then label-PATCH retries",
                       "# TYPE nanogpu_native_api_write_seconds_total counter",
                       f'nanogpu_native_api_write_seconds_total{{op="binding+patch"}} {kw["binding_seconds_total"]:.9f}',
                       f'nanogpu_native_api_write_seconds_total{{op="patch_retry"}} {kw["patch_seconds_total"]:.9f}',
+                      "# HELP nanogpu_native_api_timeouts_total bind API requests unanswered within the "
+                      "writer's timeout (failed over to the slow path)",
+                      "# TYPE nanogpu_native_api_timeouts_total counter",
+                      f"nanogpu_native_api_timeouts_total {kw.get('timeouts', 0)}",
                       "# TYPE nanogpu_native_label_failures_total counter",
                       f"nanogpu_native_label_failures_total {kw['label_failures']}",
                       "# TYPE nanogpu_native_binds_inflight gauge",
@@ -405,7 +409,7 @@ class NativeServer:
         return ("\n".join(lines) + "\n").encode()
 
     def enable_native_writes(self, config, threads: int, retries: int, record_events: bool,
-                             evented: bool = True, label: bool = True) -> bool:
+                             evented: bool = True, label: bool = True, timeout_s: float = 30.0) -> bool:
         """Hands the bind's API writes to the front door's C++ writer threads (native/src/
         kubewriter.cpp) when the API server is a REST endpoint this process reaches with a
         bearer token or a client certificate; False (Python writes) otherwise."""
@@ -418,7 +422,7 @@ class NativeServer:
         self.fe.set_kube_writer(u.hostname, u.port or (443 if tls else 80), tls, config.token or "",
                                 config.token_file or "", config.ca_file or "", config.cert_file or "",
                                 config.key_file or "", bool(config.insecure), threads, retries, record_events,
-                                evented, label)
+                                evented, label, timeout_s)
         return True
 
     async def stop(self) -> None:

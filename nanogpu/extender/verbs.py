@@ -5,8 +5,8 @@ dealer calls behind them (dealer.go:89-203). The reference holds ONE mutex acros
 filter, score and the API writes of bind; here filter/prioritize are lock-free reads of
 per-node snapshots and bind is
 
-    reserve (native ledger, µs)  ->  PATCH annotations  ->  POST binding  ->  commit
-                                  \\-> any failure: rollback + best-effort un-annotate
+    reserve (native ledger, µs)  ->  POST binding (+ annotations)  ->  commit  ->  PATCH label
+                                  \\-> binding refused: rollback
 
 so binds for different pods overlap their API round trips (the reference's
 bind rate is bounded by 1 / (2 x RTT)).
@@ -269,72 +269,62 @@ class Extender:
 
     async def _write(self, ns: str, name: str, uid: str, node: str, names: list[str], plan, fresh: bool, sp,
                      pod_ns_name: tuple[str, str]) -> None:
-        """Second half of bind: the placement annotations and the binding, then commit; on
-        any failure roll the reservation back and un-annotate (fixes reference D1/D2).
+        """Second half of bind: the binding, commit, then the assume label (fixes reference
+        D1/D2: a failed binding rolls the reservation back and reports the error).
 
         The Binding itself carries the placement annotations, which kube-apiserver sets on
         the pod together with spec.nodeName (setPodHostAndAnnotations): a bound pod never
-        lacks them, whichever write lands first. The PATCH (annotations + the assume label)
-        is sent at the same time, so a bind costs one API round trip, not two. In-process
-        APIs that complete inline keep the writes sequential (no Tasks)."""
+        lacks them, and a refused binding writes nothing. The label follows as a PATCH that
+        restates spec.nodeName (pu.label_patch), so it lands only on a pod bound to `node`.
+        Nothing is ever un-annotated: no write of this bind can have landed on a pod that is
+        not bound here (a pod bound elsewhere keeps its placement untouched)."""
+        t2 = time.perf_counter()
+        ann = pu.placement_annotations(names, plan, {T.ANNOTATION_ASSUME_TIME: f"{time.time():.6f}"})
         try:
-            t2 = time.perf_counter()
-            extra = {T.ANNOTATION_ASSUME_TIME: f"{time.time():.6f}"}
-            patch = pu.placement_patch_names(names, plan, extra)
-            ann = patch["metadata"]["annotations"]
-
-            async def write_patch() -> None:
-                try:   # first attempt inline; the retry loop only after an API error
-                    await self.api.patch_pod(ns, name, patch)
-                except ApiError as e:
-                    await self._retry_after(e, "patch", self.api.patch_pod, ns, name, patch)
-
-            async def write_binding() -> None:
+            try:
                 try:
-                    try:
-                        await self.api.bind_pod(ns, name, uid, node, ann)
-                    except ApiError as e0:
-                        await self._retry_after(e0, "bind", self.api.bind_pod, ns, name, uid, node, ann)
-                except ApiError as e:
-                    # A retried bind whose first attempt landed: already bound to this node is success.
-                    if not e.conflict or pu.node_name_of(await self.api.get_pod(ns, name)) != node:
-                        raise
-
-            if not self.assume_label:
-                t3 = time.perf_counter()      # the binding alone carries the annotations
-                await write_binding()
-            elif getattr(self.api, "completes_inline", False):
-                await write_patch()
-                t3 = time.perf_counter()
-                await write_binding()
-            else:
-                pe, be = await asyncio.gather(write_patch(), write_binding(), return_exceptions=True)
-                t3 = time.perf_counter()
-                if isinstance(be, BaseException):
-                    raise be
-                if isinstance(pe, BaseException):
-                    # bound, annotations on the pod with the binding: only the label is late
-                    log.warning("bind %s/%s: label PATCH failed (%s); retrying in the background", ns, name, pe)
-                    self._background(self._relabel(ns, name, patch))
-            t4 = time.perf_counter()
-            sp.phases["patch"], sp.phases["binding"] = t3 - t2, t4 - t3
-            self._m_patch.observe(t3 - t2)
-            self._m_binding.observe(t4 - t3)
+                    await self.api.bind_pod(ns, name, uid, node, ann)
+                except ApiError as e0:
+                    await self._retry_after(e0, "bind", self.api.bind_pod, ns, name, uid, node, ann)
+            except (ApiError, OSError, asyncio.TimeoutError) as e:
+                # a retried POST whose first attempt landed (409), or an answer lost to a 5xx or
+                # the transport: the pod already on this node means the bind succeeded
+                if isinstance(e, ApiError) and not (e.conflict or e.status >= 500 or e.status == 429):
+                    raise
+                try:
+                    landed = pu.node_name_of(await self.api.get_pod(ns, name)) == node
+                except (ApiError, OSError, asyncio.TimeoutError):
+                    landed = False
+                if not landed:
+                    raise
         except BaseException as e:
-            # D2: the reference leaves the cache debited when the binding POST fails.
-            if not fresh:
-                raise
-            self.state.rollback(uid)
-            self.metrics.rollbacks.inc()
-            if not isinstance(e, asyncio.CancelledError):
-                self._background(self._unannotate(*pod_ns_name, names))
+            # D2: the reference leaves the cache debited when the binding POST fails
+            if fresh:
+                self.state.rollback(uid)
+                self.metrics.rollbacks.inc()
                 if self.record_events and isinstance(e, ApiError):
                     self._background(self.api.create_event(
                         ns, {"kind": "Pod", "name": name, "namespace": ns, "uid": uid}, "FailedBinding",
                         f"nano-gpu bind failed: {e}"))
             raise
+        t3 = time.perf_counter()
         self.state.commit(uid)
         self.metrics.pods_bound.inc()
+        if self.assume_label:
+            patch = pu.label_patch(node)
+            try:
+                try:   # first attempt inline; the retry loop only after an API error
+                    await self.api.patch_pod(ns, name, patch)
+                except ApiError as e:
+                    await self._retry_after(e, "patch", self.api.patch_pod, ns, name, patch)
+            except (ApiError, OSError, asyncio.TimeoutError) as e:
+                # bound, annotations on the pod with the binding: only the label is late
+                log.warning("bind %s/%s: label PATCH failed (%s); retrying in the background", ns, name, e)
+                self._background(self._relabel(ns, name, patch))
+        t4 = time.perf_counter()
+        sp.phases["binding"], sp.phases["patch"] = t3 - t2, t4 - t3
+        self._m_binding.observe(t3 - t2)
+        self._m_patch.observe(t4 - t3)
 
     async def _relabel(self, ns: str, name: str, patch: dict) -> None:
         for attempt in range(6):
@@ -343,19 +333,10 @@ class Extender:
                 await self.api.patch_pod(ns, name, patch)
                 return
             except ApiError as e:
-                if e.not_found:
+                if e.not_found or e.status == 422:   # gone, or no longer on this node
                     return
             except (OSError, asyncio.TimeoutError):
                 pass
-
-    async def _unannotate(self, ns: str, name: str, names: list[str]) -> None:
-        ann = {T.container_annotation(n): None for n in names}
-        ann[T.ANNOTATION_GPU_ASSUME] = None
-        try:
-            await self.api.patch_pod(ns, name, {"metadata": {"annotations": ann,
-                                                             "labels": {T.LABEL_GPU_ASSUME: None}}})
-        except (ApiError, OSError, asyncio.TimeoutError):
-            pass
 
     def _background(self, coro) -> None:
         t = asyncio.ensure_future(coro)

@@ -175,6 +175,13 @@ class FakeKubeStore:
         if p is None:
             raise ApiError(404, f'pods "{name}" not found', "NotFound")
         np_ = pu.apply_patch(p, patch)
+        if "spec" in patch and (np_.get("spec") or {}) != (p.get("spec") or {}):
+            # kube-apiserver's pod update validation: the spec is immutable but for a few
+            # fields, spec.nodeName included (a Binding sets it); restating it is a no-op
+            raise ApiError(422, f'Pod "{name}" is invalid: spec: Forbidden: pod updates may not change fields '
+                                f'other than `spec.containers[*].image`, `spec.initContainers[*].image`, '
+                                f'`spec.activeDeadlineSeconds`, `spec.tolerations` (only additions to existing '
+                                f'tolerations) or `spec.terminationGracePeriodSeconds`', "Invalid")
         np_ = self._stamp(np_) if np_.get("metadata") is not p.get("metadata") else self._bump(np_)
         self.pods[(ns, name)] = np_
         self._emit("pods", "MODIFIED", np_)

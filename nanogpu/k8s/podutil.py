@@ -243,11 +243,25 @@ def placement_patch(pod: dict, plan: Plan, extra: dict | None = None) -> dict:
 
 
 def placement_patch_names(names: list[str], plan: Plan, extra: dict | None = None) -> dict:
+    return {"metadata": {"annotations": placement_annotations(names, plan, extra),
+                         "labels": {T.LABEL_GPU_ASSUME: "true"}}}
+
+
+def placement_annotations(names: list[str], plan: Plan, extra: dict | None = None) -> dict:
+    """The reference's placement annotations (pod.go:65-79): what the Binding carries."""
     ann = {T.container_annotation(n): ",".join(str(i) for i in plan[k]) for k, n in enumerate(names)}
     ann[T.ANNOTATION_GPU_ASSUME] = "true"
     if extra:
         ann.update(extra)
-    return {"metadata": {"annotations": ann, "labels": {T.LABEL_GPU_ASSUME: "true"}}}
+    return ann
+
+
+def label_patch(node: str) -> dict:
+    """The bind's second write: the assume label only (the Binding carried the annotations),
+    guarded by spec.nodeName. kube-apiserver refuses a pod patch that would change
+    spec.nodeName (422), and restating an unchanged value is a no-op, so the label lands only
+    on a pod that is bound to `node`: never on one bound elsewhere or still unbound."""
+    return {"metadata": {"labels": {T.LABEL_GPU_ASSUME: "true"}}, "spec": {"nodeName": node}}
 
 
 def apply_patch(obj: dict, patch: dict) -> dict:

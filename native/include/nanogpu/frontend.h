@@ -112,7 +112,7 @@ class Frontend {
   // Native bind writes: from now on a bind whose reservation succeeded here is finished by
   // KubeWriter threads (PATCH + binding + commit / rollback) without Python. Set once.
   void set_kube_writer(const KubeTarget& t, int threads, int retries, bool record_events,
-                       bool evented = true, bool label = true);
+                       bool evented = true, bool label = true, double timeout_s = 30.0);
   const KubeWriter* kube_writer() const { return writer_.load(std::memory_order_acquire); }
   // The native filter / priorities verb on a request body (what a worker runs per request);
   // false = the request needs the Python path.

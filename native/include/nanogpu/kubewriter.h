@@ -1,6 +1,7 @@
-// Native second half of the extender's bind: the two API writes (placement PATCH, then the
-// pods/binding POST) and the ledger commit / rollback, done by C++ threads on keep-alive
-// connections to kube-apiserver instead of the Python event loop.
+// Native second half of the extender's bind: the two API writes (the pods/binding POST, which
+// carries the placement annotations, then the assume-label PATCH guarded by spec.nodeName) and
+// the ledger commit / rollback, done by C++ threads on keep-alive connections to
+// kube-apiserver instead of the Python event loop.
 //
 // Reference: pkg/dealer/dealer.go:155-203 (Bind: the plan annotated on the pod, the binding
 // posted, the node's cache debited; the reference holds its global lock across both writes)
@@ -8,7 +9,7 @@
 // which stays the fallback and the spec for the tests: 5xx / 429 are retried with backoff,
 // a binding 409 whose pod already sits on the requested node is success (a retried POST
 // whose first attempt landed), and any failure of a fresh reservation rolls the ledger back
-// and un-annotates the pod (the reference's defects D1/D2 fixed).
+// (the reference's defects D1/D2 fixed). No write of a refused bind lands on the pod.
 #pragma once
 
 #include <atomic>
@@ -42,6 +43,8 @@ void* make_ssl_ctx(const KubeTarget& t);
 void free_ssl_ctx(void* ctx);
 // The bearer token now: the token file's contents when it has any, else the target's token.
 std::string kube_token(const KubeTarget& t);
+// TCP keepalive probes and TCP_USER_TIMEOUT (timeout_s) on an API server connection.
+void tcp_liveness(int fd, double timeout_s);
 // The Host header's value: host:port, an IPv6 address in brackets.
 std::string host_header(const KubeTarget& t);
 
@@ -104,24 +107,26 @@ struct BindJob {
 
 struct KubeWriterStats {
   std::atomic<uint64_t> ok{0}, failed{0}, rollbacks{0}, retries{0}, patch_ns{0}, binding_ns{0}, inflight{0},
-      label_failures{0};
+      label_failures{0}, timeouts{0};
 };
 
 // Two ways to run the writes:
 //   * evented (default): ONE epoll thread drives every bind's two requests on non-blocking
 //     keep-alive connections (plain or TLS), `threads` x kBatch binds in flight. A bind whose
 //     two answers are 2xx commits right there; anything else (a 5xx / 429 / 401 to retry, a
-//     409 to check, a failure to roll back) goes to a slow-path thread that finishes it with
+//     409 to check, a failure to roll back, no answer within timeout_s) goes to a slow-path
+//     thread that finishes it with
 //     the blocking code below. One wake-up serves every answer that arrived together, where
 //     a thread per batch sleeps and wakes once per request (kubewriter_evented.cpp);
 //   * threads: `threads` blocking threads, each pipelining up to kBatch binds.
 class KubeWriter {
  public:
   using Respond = std::function<void(uint64_t id, int status, const std::string& body)>;
-  // `label`: also PATCH the assume label (and the annotations again) beside the binding, the
-  // reference's pod contract; false: the binding alone, which carries the annotations.
+  // `label`: also PATCH the assume label behind the binding, the reference's pod contract;
+  // false: the binding alone, which carries the annotations. `timeout_s`: an API request
+  // unanswered this long fails (a half-open connection never answers, nor resets).
   KubeWriter(KubeTarget target, std::shared_ptr<Ledger> ledger, Respond respond, int threads, int retries,
-             bool record_events, bool evented = true, bool label = true);
+             bool record_events, bool evented = true, bool label = true, double timeout_s = 30.0);
   ~KubeWriter();
   void submit(BindJob job);
   void stop();
@@ -135,7 +140,11 @@ class KubeWriter {
   void process_batch(std::vector<BindJob>& jobs, std::vector<std::unique_ptr<HttpConn>>& conns);
   void finish(HttpConn* c, HttpConn* c2, BindJob& j, const std::string& patch, const std::string& binding, int sp,
               std::string* rp, int sb, std::string* rb);
-  // a bound pod's label PATCH that failed transiently: retried; a lasting failure is counted
+  // the binding's outcome (retried, checked): committed and answered (true), or rolled back
+  // and answered with the error
+  bool finish_binding(HttpConn* c2, BindJob& j, const std::string& binding, int sb, std::string* rb);
+  // a bound pod's label PATCH that failed (transiently, or refused by its nodeName guard
+  // before the binding had landed): sent again; a lasting failure is counted
   void finish_label(HttpConn* c, const BindJob& j, const std::string& patch, int sp, std::string* rp);
   void refuse(BindJob& j);
   int call(HttpConn* c, const char* method, const std::string& path, const std::string& ctype,
@@ -166,6 +175,7 @@ class KubeWriter {
   std::shared_ptr<Ledger> ledger_;
   Respond respond_;
   int retries_;
+  double timeout_s_ = 30.0;
   bool events_;
   bool label_ = true;
   std::mutex mu_;

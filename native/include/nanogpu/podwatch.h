@@ -34,7 +34,7 @@ struct PodWatchFilter {
   uint64_t released = 0, dropped = 0;
   // compat (reference pod.go:15-24): a deletionTimestamp alone ends the share; otherwise a
   // terminating pod keeps it until Succeeded/Failed or DELETED (controller/pods.py)
-  bool release_on_terminating = false;
+  std::atomic<bool> release_on_terminating{false};   // set from Python while the watch thread reads it
   std::mutex mu;   // a stream thread and the Python loop (reset, counters) share it
 };
 

@@ -615,7 +615,18 @@ struct Server::Impl {
     }
   }
   ObjP patch_pod(std::string_view ns, std::string_view name, const JV& patch) {
-    return write_pod(ns, name, [&](const Obj&, JV* v) { merge_patch(v, patch); });
+    return write_pod(ns, name, [&](const Obj& cur, JV* v) {
+      merge_patch(v, patch);
+      // kube-apiserver's pod update validation: spec.nodeName is set by a Binding only, so a
+      // patch that would change it is refused (and one that restates it is a precondition)
+      const JV* sp = v->get("spec");
+      if ((sp ? str_of(sp->get("nodeName")) : std::string()) != cur.node)
+        throw ApiErr{422, "Invalid",
+                     "Pod \"" + std::string(name) + "\" is invalid: spec: Forbidden: pod updates may not change "
+                     "fields other than `spec.containers[*].image`, `spec.initContainers[*].image`, "
+                     "`spec.activeDeadlineSeconds`, `spec.tolerations` (only additions to existing tolerations) "
+                     "or `spec.terminationGracePeriodSeconds`"};
+    });
   }
   // pods/binding; the Binding's metadata.annotations land on the pod with spec.nodeName, as
   // kube-apiserver's setPodHostAndAnnotations does

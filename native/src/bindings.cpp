@@ -756,7 +756,7 @@ PYBIND11_MODULE(_native, m) {
           [](Frontend& f, const std::string& host, int port, bool tls, const std::string& token,
              const std::string& token_file, const std::string& ca_file, const std::string& cert_file,
              const std::string& key_file, bool insecure, int threads, int retries, bool record_events,
-             bool evented, bool label) {
+             bool evented, bool label, double timeout_s) {
             KubeTarget t;
             t.host = host;
             t.port = port;
@@ -767,12 +767,13 @@ PYBIND11_MODULE(_native, m) {
             t.cert_file = cert_file;
             t.key_file = key_file;
             t.insecure = insecure;
-            f.set_kube_writer(t, threads, retries, record_events, evented, label);
+            f.set_kube_writer(t, threads, retries, record_events, evented, label, timeout_s);
           },
           py::arg("host"), py::arg("port"), py::arg("tls") = false, py::arg("token") = "",
           py::arg("token_file") = "", py::arg("ca_file") = "", py::arg("cert_file") = "", py::arg("key_file") = "",
           py::arg("insecure") = false, py::arg("threads") = 32, py::arg("retries") = 3,
           py::arg("record_events") = true, py::arg("evented") = true, py::arg("label") = true,
+          py::arg("timeout_s") = 30.0,
           "Binds whose reservation succeeded natively are finished natively (PATCH + binding + "
           "commit/rollback) on keep-alive connections to kube-apiserver: one epoll thread "
           "(evented) or `threads` blocking threads; `threads` x 8 binds in flight.")
@@ -789,6 +790,7 @@ PYBIND11_MODULE(_native, m) {
              d["patch_seconds_total"] = static_cast<double>(w->stats.patch_ns.load()) * 1e-9;
              d["binding_seconds_total"] = static_cast<double>(w->stats.binding_ns.load()) * 1e-9;
              d["label_failures"] = w->stats.label_failures.load();
+             d["timeouts"] = w->stats.timeouts.load();
              return d;
            })
       .def("take",
@@ -1060,7 +1062,10 @@ PYBIND11_MODULE(_native, m) {
             f.forwarded.insert(keys.begin(), keys.end());
           },
           py::arg("keys"), "After a relist: the keys now in the informer's store.")
-      .def_readwrite("release_on_terminating", &PodWatchFilter::release_on_terminating)
+      .def_property(
+          "release_on_terminating",
+          [](const PodWatchFilter& f) { return f.release_on_terminating.load(std::memory_order_relaxed); },
+          [](PodWatchFilter& f, bool v) { f.release_on_terminating.store(v, std::memory_order_relaxed); })
       .def_property_readonly("released",
                              [](PodWatchFilter& f) {
                                std::lock_guard<std::mutex> g(f.mu);

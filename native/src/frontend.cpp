@@ -466,11 +466,11 @@ Frontend::Frontend(std::shared_ptr<Ledger> ledger, const std::string& host, int 
 Frontend::~Frontend() { stop(); }
 
 void Frontend::set_kube_writer(const KubeTarget& t, int threads, int retries, bool record_events, bool evented,
-                               bool label) {
+                               bool label, double timeout_s) {
   if (writer_.load()) throw std::logic_error("Frontend: the kube writer is already set");
   writer_owner_ = std::make_unique<KubeWriter>(
       t, ledger_, [this](uint64_t id, int status, const std::string& body) { respond(id, status, "application/json", body); },
-      threads, retries, record_events, evented, label);
+      threads, retries, record_events, evented, label, timeout_s);
   writer_.store(writer_owner_.get(), std::memory_order_release);
 }
 
@@ -877,7 +877,7 @@ void Frontend::process(Worker* w, Conn* c) {
     const std::string_view target = line.substr(s1 + 1, s2 - s1 - 1);
     const bool http10 = line.substr(s2 + 1) == "HTTP/1.0";
     size_t clen = 0;
-    bool chunked = false, close = http10, keep = false;
+    bool chunked = false, close = http10, keep = false, have_clen = false;
     size_t pos = le == std::string_view::npos ? head.size() : le + 2;
     while (pos < head.size()) {
       size_t e = head.find("\r\n", pos);
@@ -887,8 +887,14 @@ void Frontend::process(Worker* w, Conn* c) {
       if (colon != std::string_view::npos) {
         const std::string_view k = trim(h.substr(0, colon)), v = trim(h.substr(colon + 1));
         if (ieq(k, "content-length")) {
-          // no allocation per request; a malformed length reads as too large (refused below)
-          if (std::from_chars(v.data(), v.data() + v.size(), clen).ec != std::errc()) clen = SIZE_MAX;
+          // no allocation per request; a malformed length (trailing bytes included: "12abc",
+          // "12, 34") or a repeated header that disagrees reads as too large (refused below)
+          size_t v_len = 0;
+          const auto r = std::from_chars(v.data(), v.data() + v.size(), v_len);
+          if (r.ec != std::errc() || r.ptr != v.data() + v.size() || v.empty() || (have_clen && v_len != clen))
+            v_len = SIZE_MAX;
+          clen = have_clen && clen == SIZE_MAX ? SIZE_MAX : v_len;
+          have_clen = true;
         } else if (ieq(k, "transfer-encoding")) {
           chunked = v.find("chunked") != std::string_view::npos;
         } else if (ieq(k, "connection")) {
@@ -899,6 +905,10 @@ void Frontend::process(Worker* w, Conn* c) {
       pos = e + 2;
     }
     if (http10 && keep) close = false;
+    if (chunked && have_clen) {   // both framings: request smuggling territory, refused
+      close_conn(w, c);
+      return;
+    }
     // the body stays a view into the connection's input unless it came chunked; the input is
     // consumed only after the request is handled (the views point into it)
     thread_local std::string chunked_body;
@@ -1234,6 +1244,7 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     bool compact[kListSlots] = {};       // the text is `["a","b",...]` exactly: a reply may copy it whole
     std::vector<int32_t> ids[kListSlots];
     std::vector<std::pair<uint32_t, uint32_t>> tok[kListSlots];   // token (offset, length) in the list text
+    std::string text[kListSlots];        // the list text itself: a hash hit is confirmed byte for byte
     uint64_t clock = 0;
   };
   thread_local IdCache idc;
@@ -1242,7 +1253,7 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   const uint64_t epoch = ledger_->node_epoch();
   int slot = -1;
   for (int k = 0; k < kListSlots && slot < 0; ++k)
-    if (idc.key[k] == nkey && idc.len[k] == raw_names.size()) slot = k;
+    if (idc.key[k] == nkey && idc.len[k] == raw_names.size() && idc.text[k] == raw_names) slot = k;
   // a cached list's names are read through its token offsets into this request's text (no
   // per-request copy of 2 x N views); a list parsed now fills nv / nraw
   const std::vector<std::pair<uint32_t, uint32_t>>* toks = nullptr;
@@ -1283,6 +1294,8 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
       if (idc.used[k] < idc.used[slot]) slot = k;
     idc.key[slot] = plain ? nkey : 0;   // a list with escapes is parsed every time
     idc.len[slot] = raw_names.size();
+    if (plain) idc.text[slot].assign(raw_names.data(), raw_names.size());
+    else idc.text[slot].clear();
     idc.epoch[slot] = 0;                // ids checked below
     idc.ids[slot].assign(nv.size(), -1);
     idc.tok[slot].clear();

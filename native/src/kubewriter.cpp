@@ -113,6 +113,18 @@ void free_ssl_ctx(void* ctx) {
   if (ctx) SSL_CTX_free(static_cast<SSL_CTX*>(ctx));
 }
 
+void tcp_liveness(int fd, double timeout_s) {
+  // a peer that vanished (no FIN, no RST: a rebooted node, a dropped NAT / LB entry) is
+  // noticed: keepalive probes on an idle connection, and unacknowledged sends time out
+  int one = 1, idle = 10, intvl = 5, cnt = 3;
+  setsockopt(fd, SOL_SOCKET, SO_KEEPALIVE, &one, sizeof one);
+  setsockopt(fd, IPPROTO_TCP, TCP_KEEPIDLE, &idle, sizeof idle);
+  setsockopt(fd, IPPROTO_TCP, TCP_KEEPINTVL, &intvl, sizeof intvl);
+  setsockopt(fd, IPPROTO_TCP, TCP_KEEPCNT, &cnt, sizeof cnt);
+  const unsigned ms = static_cast<unsigned>(std::min(timeout_s, 3600.0) * 1000.0);
+  setsockopt(fd, IPPROTO_TCP, TCP_USER_TIMEOUT, &ms, sizeof ms);
+}
+
 std::string host_header(const KubeTarget& t) {
   const bool v6 = t.host.find(':') != std::string::npos && t.host.front() != '[';
   return (v6 ? "[" + t.host + "]" : t.host) + ":" + std::to_string(t.port);
@@ -156,6 +168,7 @@ bool HttpConn::connect_() {
     setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
     int one = 1;
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    tcp_liveness(fd, timeout_s_);
     if (::connect(fd, a->ai_addr, a->ai_addrlen) == 0) {
       fd_ = fd;
       break;
@@ -413,9 +426,9 @@ int HttpConn::request(const char* method, const std::string& path, const std::st
 
 // ------------------------------------------------------------------------------ KubeWriter
 KubeWriter::KubeWriter(KubeTarget target, std::shared_ptr<Ledger> ledger, Respond respond, int threads, int retries,
-                       bool record_events, bool evented, bool label)
+                       bool record_events, bool evented, bool label, double timeout_s)
     : t_(std::move(target)), ledger_(std::move(ledger)), respond_(std::move(respond)), retries_(retries),
-      events_(record_events), evented_(evented) {
+      timeout_s_(timeout_s > 0 ? timeout_s : 30.0), events_(record_events), evented_(evented) {
   label_ = label;
   ctx_ = make_ssl_ctx(t_);
   token_ = t_.token;
@@ -545,10 +558,12 @@ int KubeWriter::call(HttpConn* c, const char* method, const std::string& path, c
   }
 }
 
-// The two request bodies of one bind. Placement annotations (pu.placement_patch_names): the
-// Binding carries them, so they land on the pod atomically with spec.nodeName (kube-apiserver
-// setPodHostAndAnnotations); the PATCH, in flight at the same time on a second connection,
-// adds the assume label.
+// The two request bodies of one bind. The Binding carries the placement annotations
+// (pu.placement_annotations), so they land on the pod atomically with spec.nodeName
+// (kube-apiserver setPodHostAndAnnotations) and a refused binding writes nothing. The PATCH
+// adds the assume label only, and restates spec.nodeName: kube-apiserver refuses a pod patch
+// that would change it (422), so the label lands only on a pod bound to this node
+// (pu.label_patch), never on one bound elsewhere or still unbound.
 void KubeWriter::build(BindJob& j, std::string* patch, std::string* binding) {
   std::string ann = "{";
   for (size_t k = 0; k < j.containers.size() && k < j.plan.size(); ++k) {
@@ -569,7 +584,11 @@ void KubeWriter::build(BindJob& j, std::string* patch, std::string* binding) {
   ann += "\":\"";
   ann += ts;
   ann += "\"}";
-  *patch = "{\"metadata\":{\"annotations\":" + ann + ",\"labels\":{\"" + kAssume + "\":\"true\"}}}";
+  *patch = "{\"metadata\":{\"labels\":{\"";
+  *patch += kAssume;
+  *patch += "\":\"true\"}},\"spec\":{\"nodeName\":";
+  json::append_quoted(patch, j.node);
+  *patch += "}}";
   std::string& b = *binding;
   b = "{\"apiVersion\":\"v1\",\"kind\":\"Binding\",\"metadata\":{\"name\":";
   json::append_quoted(&b, j.name);
@@ -582,79 +601,76 @@ void KubeWriter::build(BindJob& j, std::string* patch, std::string* binding) {
   b += "}}";
 }
 
-// A batch of binds taken together: every bind's PATCH and binding are sent first (two
-// connections per bind), then the answers are read and each bind is finished in turn.
+// A batch of binds taken together: every bind's binding is sent first, then the answers
+// are read and each bind is finished (committed and answered, or rolled back); the label
+// PATCHes of the bound pods go out after that, together.
 void KubeWriter::process_batch(std::vector<BindJob>& jobs, std::vector<std::unique_ptr<HttpConn>>& conns) {
   const size_t n = jobs.size();
   std::vector<std::string> patch(n), binding(n), rp(n), rb(n);
-  std::vector<int> sp(n), sb(n);
+  std::vector<int> sb(n);
+  std::vector<char> bound(n, 0);
   const std::string a = auth();
   const uint64_t t1 = now_ns();
   for (size_t i = 0; i < n; ++i) {
     build(jobs[i], &patch[i], &binding[i]);
-    const std::string base = "/api/v1/namespaces/" + jobs[i].ns + "/pods/" + jobs[i].name;
-    if (label_) conns[2 * i]->start("PATCH", base, kMergePatch, patch[i], a);
-    conns[2 * i + 1]->start("POST", base + "/binding", kJson, binding[i], a);
+    conns[2 * i + 1]->start("POST", "/api/v1/namespaces/" + jobs[i].ns + "/pods/" + jobs[i].name + "/binding", kJson,
+                            binding[i], a);
   }
-  for (size_t i = 0; i < n; ++i) {
-    sb[i] = conns[2 * i + 1]->finish(&rb[i]);
-    sp[i] = label_ ? conns[2 * i]->finish(&rp[i]) : 200;   // no label: nothing else to write
+  for (size_t i = 0; i < n; ++i) sb[i] = conns[2 * i + 1]->finish(&rb[i]);
+  stats.binding_ns.fetch_add(now_ns() - t1, std::memory_order_relaxed);   // in flight together
+  for (size_t i = 0; i < n; ++i) bound[i] = finish_binding(conns[2 * i + 1].get(), jobs[i], binding[i], sb[i], &rb[i]);
+  if (label_) {
+    const uint64_t t3 = now_ns();
+    for (size_t i = 0; i < n; ++i)
+      if (bound[i])
+        conns[2 * i]->start("PATCH", "/api/v1/namespaces/" + jobs[i].ns + "/pods/" + jobs[i].name, kMergePatch,
+                            patch[i], a);
+    for (size_t i = 0; i < n; ++i) {
+      if (!bound[i]) continue;
+      const int sp = conns[2 * i]->finish(&rp[i]);
+      if (sp < 200 || sp >= 300) finish_label(conns[2 * i].get(), jobs[i], patch[i], sp, &rp[i]);
+    }
+    stats.patch_ns.fetch_add(now_ns() - t3, std::memory_order_relaxed);
   }
-  stats.binding_ns.fetch_add(now_ns() - t1, std::memory_order_relaxed);   // the pairs, in flight together
-  for (size_t i = 0; i < n; ++i) {
-    finish(conns[2 * i].get(), conns[2 * i + 1].get(), jobs[i], patch[i], binding[i], sp[i], &rp[i], sb[i], &rb[i]);
-    stats.inflight.fetch_sub(1, std::memory_order_relaxed);
-  }
+  for (size_t i = 0; i < n; ++i) stats.inflight.fetch_sub(1, std::memory_order_relaxed);
 }
 
 void KubeWriter::finish_label(HttpConn* c, const BindJob& j, const std::string& patch, int sp, std::string* rp) {
-  auto transient = [](int st) { return st == 0 || st == 401 || st == 429 || st >= 500; };
+  // the pod is bound here by now: a PATCH refused by its nodeName guard (it reached the server
+  // before the binding had landed) or lost in transport goes out again, with the transient
+  // retries; a pod that is gone is left alone
   const uint64_t t3 = now_ns();
-  if (transient(sp)) sp = call(c, "PATCH", "/api/v1/namespaces/" + j.ns + "/pods/" + j.name, kMergePatch, patch, rp, true);
+  if (sp != 404) sp = call(c, "PATCH", "/api/v1/namespaces/" + j.ns + "/pods/" + j.name, kMergePatch, patch, rp, true);
   stats.patch_ns.fetch_add(now_ns() - t3, std::memory_order_relaxed);
   if (sp < 200 || sp >= 300) stats.label_failures.fetch_add(1, std::memory_order_relaxed);
 }
 
-void KubeWriter::finish(HttpConn* c, HttpConn* c2, BindJob& j, const std::string& patch, const std::string& b,
-                        int sp, std::string* rp, int sb, std::string* rb) {
+bool KubeWriter::finish_binding(HttpConn* c2, BindJob& j, const std::string& b, int sb, std::string* rb) {
   const std::string base = "/api/v1/namespaces/" + j.ns + "/pods/" + j.name;
-  std::string err;
   auto transient = [](int st) { return st == 0 || st == 401 || st == 429 || st >= 500; };
   if (transient(sb)) sb = call(c2, "POST", base + "/binding", kJson, b, rb, true);
-  if (sb == 409) {
-    // a retried POST whose first attempt landed: already on this node is success
+  if (sb == 409 || transient(sb)) {
+    // a retried POST whose first attempt landed (409), or an answer lost to a 5xx or the
+    // transport: the pod already on this node means the bind succeeded
     std::string got;
     const int gs = call(c2, "GET", base, kJson, std::string(), &got, true);
     if (gs == 200 && pod_node(got) == j.node) sb = 201;
   }
-  if (sb < 200 || sb >= 300) {
-    err = api_error(sb, *rb);
-  } else if (sp < 200 || sp >= 300) {
-    finish_label(c, j, patch, sp, rp);   // bound, with its annotations: only the label is missing
-  }
-  if (err.empty()) {
+  if (sb >= 200 && sb < 300) {
     ledger_->commit(j.uid);
     stats.ok.fetch_add(1, std::memory_order_relaxed);
     respond_(j.id, 200, "{\"Error\":\"\"}");
-    return;
+    return true;
   }
+  const std::string err = api_error(sb, *rb);
   stats.failed.fetch_add(1, std::memory_order_relaxed);
   if (j.fresh) {
-    // D2: roll the reservation back, then un-annotate (best effort) and record the event
+    // D2: roll the reservation back and record the event. Nothing is un-annotated: the
+    // Binding, which carries the annotations, was refused, and the label PATCH's nodeName
+    // guard keeps it off a pod not bound here. No write of this bind landed; a pod bound
+    // elsewhere keeps its own placement untouched.
     ledger_->release(j.uid);
     stats.rollbacks.fetch_add(1, std::memory_order_relaxed);
-    std::string un = "{\"metadata\":{\"annotations\":{";
-    for (const std::string& nm : j.containers) {
-      json::append_quoted(&un, kContainerPrefix + nm);
-      un += ":null,";
-    }
-    un += "\"";
-    un += kAssume;
-    un += "\":null},\"labels\":{\"";
-    un += kAssume;
-    un += "\":null}}}";
-    std::string ignored;
-    call(c, "PATCH", base, kMergePatch, un, &ignored, false);
     if (events_ && sb > 0) {
       char tbuf[32];
       const std::time_t now = std::time(nullptr);
@@ -680,18 +696,27 @@ void KubeWriter::finish(HttpConn* c, HttpConn* c2, BindJob& j, const std::string
       ev += "\",\"lastTimestamp\":\"";
       ev += tbuf;
       ev += "\",\"count\":1}";
-      call(c, "POST", "/api/v1/namespaces/" + j.ns + "/events", kJson, ev, &ignored, false);
+      std::string ignored;
+      call(c2, "POST", "/api/v1/namespaces/" + j.ns + "/events", kJson, ev, &ignored, false);
     }
   }
   std::string body = "{\"Error\":";
   json::append_quoted(&body, err);
   body += "}";
   respond_(j.id, 500, body);
+  return false;
+}
+
+// the slow path of the evented writer: the binding's outcome, then (bound) the label
+void KubeWriter::finish(HttpConn* c, HttpConn* c2, BindJob& j, const std::string& patch, const std::string& b,
+                        int sp, std::string* rp, int sb, std::string* rb) {
+  if (finish_binding(c2, j, b, sb, rb) && label_ && (sp < 200 || sp >= 300)) finish_label(c, j, patch, sp, rp);
 }
 
 void KubeWriter::run() {
   std::vector<std::unique_ptr<HttpConn>> conns;
-  for (int i = 0; i < 2 * kBatch; ++i) conns.push_back(std::make_unique<HttpConn>(&t_, ctx_));
+  const int tmo = std::max(1, static_cast<int>(timeout_s_ + 0.5));
+  for (int i = 0; i < 2 * kBatch; ++i) conns.push_back(std::make_unique<HttpConn>(&t_, ctx_, tmo));
   std::vector<BindJob> jobs;
   for (;;) {
     jobs.clear();

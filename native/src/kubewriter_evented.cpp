@@ -133,6 +133,7 @@ struct AConn {
   size_t off = 0;
   Pending pend[2];       // answers still due, in request order
   int npend = 0;
+  uint64_t deadline_ns = 0;   // the answers are due by then (KubeWriter timeout_s)
 };
 
 struct AJob {
@@ -200,6 +201,7 @@ void KubeWriter::io_loop() {
     if (fd < 0) return false;
     int one = 1;
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    tcp_liveness(fd, timeout_s_);
     const int cr = ::connect(fd, reinterpret_cast<sockaddr*>(&addr), addr_len);
     if (cr != 0 && errno != EINPROGRESS) {
       ::close(fd);
@@ -256,6 +258,8 @@ void KubeWriter::io_loop() {
   };
 
   size_t inflight = 0;
+  const uint64_t timeout_ns = static_cast<uint64_t>(timeout_s_ * 1e9);
+  uint64_t scanned_at = ns_now();
   auto ok2xx = [](int st) { return st >= 200 && st < 300; };
   // both answers of a slot are in: commit on the happy path, else the slow path finishes it
   auto complete = [&](int64_t s) {
@@ -473,6 +477,7 @@ void KubeWriter::io_loop() {
     c.in.clear();
     c.got_any = false;
     c.retried = false;
+    c.deadline_ns = ns_now() + timeout_ns;
     c.reused = c.fd >= 0;
     if (c.fd >= 0) {
       c.st = kSending;
@@ -533,7 +538,8 @@ void KubeWriter::io_loop() {
     // park: a bind submitted from here on writes efd_; one submitted before is picked up now
     io_parked_.store(true, std::memory_order_seq_cst);
     const bool queued = !stopping && q_len_.load(std::memory_order_seq_cst) > 0;
-    const int n = epoll_wait(ep, evs, 256, queued ? 0 : stopping ? 10 : 1000);
+    // with answers due, wake for the deadline scan
+    const int n = epoll_wait(ep, evs, 256, queued ? 0 : stopping ? 10 : inflight ? 100 : 1000);
     io_parked_.store(false, std::memory_order_relaxed);
     for (int e = 0; e < n; ++e) {
       if (evs[e].data.u64 == UINT64_MAX) {
@@ -546,6 +552,23 @@ void KubeWriter::io_loop() {
     }
     for (size_t i = 0; i < kick.size(); ++i) drive(kick[i], 0);
     kick.clear();
+    // a request unanswered past its deadline (a half-open connection: no answer, no reset)
+    // fails to the slow path with status 0, never re-sent on this connection; at most one
+    // scan per 100 ms
+    const uint64_t now = ns_now();
+    if (inflight > 0 && now - scanned_at > 100'000'000ull) {
+      scanned_at = now;
+      for (size_t k = 0; k < conns.size(); ++k) {
+        AConn& c = *conns[k];
+        if (c.npend > 0 && c.fd >= 0 && now > c.deadline_ns) {
+          stats.timeouts.fetch_add(static_cast<uint64_t>(c.npend), std::memory_order_relaxed);
+          c.retried = true;
+          fail(k, "the API server did not answer in time");
+        }
+      }
+      for (size_t i = 0; i < kick.size(); ++i) drive(kick[i], 0);
+      kick.clear();
+    }
   }
   // what is still in flight after the grace period: the slow path answers it
   for (auto& c : conns) close_conn(*c);
@@ -580,7 +603,8 @@ void KubeWriter::io_loop() {
 }
 
 void KubeWriter::run_slow() {
-  HttpConn c(&t_, ctx_), c2(&t_, ctx_);
+  const int tmo = std::max(1, static_cast<int>(timeout_s_ + 0.5));
+  HttpConn c(&t_, ctx_, tmo), c2(&t_, ctx_, tmo);
   for (;;) {
     SlowJob sj;
     {

@@ -43,7 +43,7 @@ bool filter_pod_event(PodWatchFilter& f, std::string_view line, json::Doc& d, st
     // what the controller ignores: a pending pod, or a bound, running one the ledger holds
     const std::string_view node = field(d, sp, "nodeName"), phase = field(d, st, "phase");
     const int32_t dts = d.is(md, json::Type::kObj) ? d.get(md, "deletionTimestamp") : -1;
-    const bool completed = (f.release_on_terminating && dts >= 0 && !d.is(dts, json::Type::kNull)) ||
+    const bool completed = (f.release_on_terminating.load(std::memory_order_relaxed) && dts >= 0 && !d.is(dts, json::Type::kNull)) ||
                            phase == "Succeeded" || phase == "Failed";
     if (!completed && node.empty()) {
       drop = true;

@@ -16,6 +16,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <cerrno>
 #include <cstring>
 #include <mutex>
 
@@ -31,7 +32,17 @@ std::atomic<bool> g_on{false};
 std::mutex g_mu;                   // start / stop
 struct sigaction g_old{};
 
+void sample_into(void* uc_);
+
 void on_prof(int, siginfo_t*, void* uc_) {
+  // the interrupted code may sit between a failed syscall and its errno check: keep its errno
+  // (process_vm_readv and gettid below can set it)
+  const int saved_errno = errno;
+  sample_into(uc_);
+  errno = saved_errno;
+}
+
+void sample_into(void* uc_) {
   if (!g_on.load(std::memory_order_relaxed)) return;
   const size_t i = g_n.fetch_add(1, std::memory_order_relaxed);
   if (i >= kCap) return;

@@ -316,10 +316,11 @@ def test_native_scheduler_standin_binds_everything(latency_s):
 
 
 def test_inline_bind_failure_rolls_back():
-    """A patch failure inside the in-place bind: 500 with the error, reservation rolled back."""
+    """A binding failure inside the in-place bind: 500 with the error, reservation rolled back
+    (a failing label PATCH alone never fails a bind: the Binding carried the placement)."""
     async def main():
         store, rt = await _runtime(1)
-        store.faults.patch_error_rate = 1.0
+        store.faults.bind_error_rate = 1.0
         loop = asyncio.get_running_loop()
         try:
             p = store.create_pod(pu.make_pod("x", [("c", 30)]))
@@ -328,7 +329,7 @@ def test_inline_bind_failure_rolls_back():
                 ("POST", "/scheduler/filter", _dumps({"Pod": p, "NodeNames": ["n0"]})),
                 ("POST", "/scheduler/bind", _dumps({"PodName": "x", "PodNamespace": "default", "PodUID": m["uid"],
                                                     "Node": "n0"}))])
-            assert res[1][0] == 500 and "injected patch failure" in json.loads(res[1][1])["Error"]
+            assert res[1][0] == 500 and "injected binding failure" in json.loads(res[1][1])["Error"]
             assert rt.state.ledger.lookup(m["uid"]) is None
             assert all(g["Percent"] == 100 for g in rt.state.status()["n0"]["GPUs"])
         finally:
@@ -395,7 +396,7 @@ def test_priorities_nominate_unique_best_and_bind_adopts():
             assert led.lookup(pu.pod_uid(d)) is None
             # a failed bind of an adopted nomination rolls it back
             rt.state.set_policy("binpack", compat=False)
-            store.faults.patch_error_rate = 1.0
+            store.faults.bind_error_rate = 1.0
             e = store.create_pod(pu.make_pod("e", [("c", 10)]))
             res = await loop.run_in_executor(None, _http, rt.bound_port, [
                 ("POST", "/scheduler/priorities", _dumps({"Pod": e, "NodeNames": both})),

@@ -1,9 +1,10 @@
 """Native bind writes (native/src/kubewriter.cpp): the front door's C++ threads do the
 bind's PATCH + binding POST + ledger commit. Same contract as the Python path
 (nanogpu/extender/verbs.py::Extender._write, the reference's Bind at dealer.go:155-203 with
-D1/D2 fixed): transient 5xx retried, a failed binding rolls the reservation back, takes the
-placement annotations off again and records a FailedBinding event; kube-scheduler gets
-{"Error": ...}. Each test runs with the writer on and off and expects the same outcome."""
+D1/D2 fixed): transient 5xx retried, a failed binding rolls the reservation back and records a
+FailedBinding event; kube-scheduler gets {"Error": ...}. The Binding carries the placement
+annotations and the label PATCH is guarded by spec.nodeName, so a refused bind writes nothing
+on the pod. Each test runs with the writer on and off and expects the same outcome."""
 import asyncio
 import json
 
@@ -74,7 +75,7 @@ def test_bind_writes_retry_transient_errors(native):
 
 
 @pytest.mark.parametrize("native", ["evented", "threads", False])
-def test_failed_binding_rolls_back_and_unannotates(native):
+def test_failed_binding_rolls_back_and_writes_nothing(native):
     async def main():
         store = FakeKubeStore(faults=Faults(bind_error_rate=1.0))
         store.add_node(pu.make_node("n0", 8, synthetic_mi355x(8).to_json()))
@@ -409,3 +410,199 @@ def test_pipelined_label_after_the_binding(faults):
             await runner.cleanup()
 
     asyncio.run(main())
+
+
+class _NativeServer:
+    """The native API server (native/src/apiserver.cpp) behind the same calls the tests make
+    on FakeKubeStore."""
+
+    def __init__(self):
+        from nanogpu import _native as NN
+
+        self.srv = NN.ApiServer("127.0.0.1", 0, 2, 4096)
+        self.url = f"http://127.0.0.1:{self.srv.port}"
+
+    def call(self, method, path, body=None):
+        st, text = self.srv.call(method, path, json.dumps(body) if body is not None else "")
+        return st, (json.loads(text) if text else None)
+
+    def stats(self):
+        return json.loads(self.srv.stats())
+
+
+def _bound_elsewhere_pod(name):
+    """A pod another scheduler bound to a node this extender does not manage, with that
+    scheduler's placement annotations and label."""
+    p = pu.make_pod(name, [("main", 40)])
+    p["spec"]["nodeName"] = "other-node"
+    p["metadata"]["annotations"] = {T.container_annotation("main"): "5", T.ANNOTATION_GPU_ASSUME: "true",
+                                    T.ANNOTATION_ASSUME_TIME: "1700000000.000001"}
+    p["metadata"]["labels"] = {T.LABEL_GPU_ASSUME: "true", "app": "x"}
+    return p
+
+
+@pytest.mark.parametrize("server", ["python", "native"])
+@pytest.mark.parametrize("native", ["evented", "threads", False])
+def test_binding_refused_for_a_pod_bound_elsewhere_leaves_its_placement_alone(native, server):
+    """The pod is already bound to another node (with that placement's annotations) when this
+    extender binds it to n0: the binding is refused (409, the GET shows the other node), the
+    ledger holds nothing for n0, and the pod's annotations and labels are byte-identical."""
+    async def main():
+        runner = ns = None
+        if server == "python":
+            store = FakeKubeStore()
+            store.add_node(pu.make_node("n0", 8, synthetic_mi355x(8).to_json()))
+            runner, port = await serve(store)
+            url = f"http://127.0.0.1:{port}"
+            p = store.create_pod(_bound_elsewhere_pod("taken"))
+            get = lambda: store.get_pod("default", "taken")
+        else:
+            ns = _NativeServer()
+            url = ns.url
+            assert ns.call("POST", "/api/v1/nodes", pu.make_node("n0", 8, synthetic_mi355x(8).to_json()))[0] in (200, 201)
+            st, p = ns.call("POST", "/api/v1/namespaces/default/pods", _bound_elsewhere_pod("taken"))
+            assert st == 201
+            get = lambda: ns.call("GET", "/api/v1/namespaces/default/pods/taken")[1]
+        before = json.dumps(get()["metadata"].get("annotations"), sort_keys=True), \
+            json.dumps(get()["metadata"].get("labels"), sort_keys=True)
+        rt = Runtime(Config(kube_api=url, port=0, host="127.0.0.1", policy_config_path="/nonexistent",
+                            native_bind_writes=bool(native), bind_writer_mode=native or "evented"))
+        await rt.start()
+        base = f"http://127.0.0.1:{rt.bound_port}"
+        try:
+            status, res = await _schedule(base, p, "n0")
+            assert status == 500 and "409" in res["Error"], res
+            assert rt.state.ledger.lookup(pu.pod_uid(p)) is None
+            assert rt.state.status()["n0"]["GPUs"][0]["Percent"] == 100
+            if native:   # the writer made the reservation, and rolled it back
+                assert rt.native.fe.kube_writer_stats()["rollbacks"] == 1
+            await asyncio.sleep(0.2)   # anything still in flight would have landed by now
+            got = get()
+            assert got["spec"]["nodeName"] == "other-node"
+            after = json.dumps(got["metadata"].get("annotations"), sort_keys=True), \
+                json.dumps(got["metadata"].get("labels"), sort_keys=True)
+            assert after == before
+        finally:
+            await rt.stop()
+            if runner is not None:
+                await runner.cleanup()
+            if ns is not None:
+                ns.srv.stop()
+
+    asyncio.run(main())
+
+
+@pytest.mark.parametrize("server", ["python", "native"])
+@pytest.mark.parametrize("native", ["evented", "threads", False])
+def test_binding_refused_for_a_deleted_pod_sends_no_cleanup_patch(native, server):
+    """The pod is deleted between filter and bind: the binding answers 404, the reservation is
+    rolled back, and no PATCH follows (the evented writer's guarded label PATCH, pipelined
+    behind the binding, is the only one that may go out; it finds no pod)."""
+    async def main():
+        runner = ns = None
+        if server == "python":
+            store = FakeKubeStore()
+            store.add_node(pu.make_node("n0", 8, synthetic_mi355x(8).to_json()))
+            runner, port = await serve(store)
+            url = f"http://127.0.0.1:{port}"
+            p = store.create_pod(pu.make_pod("gone", [("main", 30)]))
+            patches = lambda: store.counts.get("patch_pod", 0)
+            delete = lambda: store.delete_pod("default", "gone")
+        else:
+            ns = _NativeServer()
+            url = ns.url
+            assert ns.call("POST", "/api/v1/nodes", pu.make_node("n0", 8, synthetic_mi355x(8).to_json()))[0] in (200, 201)
+            st, p = ns.call("POST", "/api/v1/namespaces/default/pods", pu.make_pod("gone", [("main", 30)]))
+            assert st == 201
+            patches = lambda: ns.stats()["calls"]["patch_pod"]
+            delete = lambda: ns.call("DELETE", "/api/v1/namespaces/default/pods/gone")
+        rt = Runtime(Config(kube_api=url, port=0, host="127.0.0.1", policy_config_path="/nonexistent",
+                            native_bind_writes=bool(native), bind_writer_mode=native or "evented"))
+        await rt.start()
+        base = f"http://127.0.0.1:{rt.bound_port}"
+        try:
+            async with aiohttp.ClientSession() as s:
+                async with s.post(f"{base}/scheduler/filter", json={"Pod": p, "NodeNames": ["n0"]}) as r:
+                    assert (await r.json())["NodeNames"] == ["n0"]
+                delete()
+                p0 = patches()
+                m = pu.meta(p)
+                async with s.post(f"{base}/scheduler/bind", json={"PodName": "gone", "PodNamespace": "default",
+                                                                    "PodUID": m["uid"], "Node": "n0"}) as r:
+                    status, res = r.status, await r.json()
+            assert status == 500 and "404" in res["Error"], res
+            assert rt.state.ledger.lookup(pu.pod_uid(p)) is None
+            await asyncio.sleep(0.2)
+            assert patches() - p0 <= (1 if native == "evented" else 0)
+        finally:
+            await rt.stop()
+            if runner is not None:
+                await runner.cleanup()
+            if ns is not None:
+                ns.srv.stop()
+
+    asyncio.run(main())
+
+
+@pytest.mark.parametrize("mode", ["evented", "threads"])
+def test_an_api_server_that_never_answers_times_the_bind_out(mode):
+    """A half-open API server (accepts, reads, never answers nor resets): every bind still gets
+    an answer (an error) within a few writer timeouts, the reservation is rolled back, and the
+    evented writer counts the timeouts (its requests had no deadline)."""
+    import socket
+    import threading
+    import time as _time
+
+    lsock = socket.socket()
+    lsock.bind(("127.0.0.1", 0))
+    lsock.listen(64)
+    held, stop = [], threading.Event()
+
+    def accept():
+        lsock.settimeout(0.1)
+        while not stop.is_set():
+            try:
+                c, _ = lsock.accept()
+                held.append(c)   # read nothing back, answer nothing
+            except OSError:
+                pass
+
+    th = threading.Thread(target=accept, daemon=True)
+    th.start()
+
+    async def main():
+        from nanogpu.k8s.fake_apiserver import InProcKube
+
+        store = FakeKubeStore()
+        store.add_node(pu.make_node("n0", 8, synthetic_mi355x(8).to_json()))
+        rt = Runtime(Config(port=0, host="127.0.0.1", policy_config_path="/nonexistent", bind_writer_mode=mode,
+                            api_write_timeout_s=0.5), api=InProcKube(store))
+        await rt.start()
+        base = f"http://127.0.0.1:{rt.bound_port}"
+        from nanogpu.k8s.client import KubeConfig
+
+        # the bind writes go to the silent server (the informers stay on the in-process store)
+        assert rt.native.enable_native_writes(KubeConfig(server=f"http://127.0.0.1:{lsock.getsockname()[1]}"),
+                                              2, 1, False, mode == "evented", True, 0.5)
+        try:
+            pods = [store.create_pod(pu.make_pod(f"h{i}", [("main", 10)])) for i in range(3)]
+            t0 = _time.monotonic()
+            res = await asyncio.gather(*(_schedule(base, p, "n0") for p in pods))
+            took = _time.monotonic() - t0
+            assert all(st == 500 and r["Error"] for st, r in res), res
+            assert took < 15, took
+            for p in pods:
+                assert rt.state.ledger.lookup(pu.pod_uid(p)) is None
+            if mode == "evented":
+                assert rt.native.fe.kube_writer_stats()["timeouts"] >= 1
+        finally:
+            await rt.stop()
+
+    try:
+        asyncio.run(main())
+    finally:
+        stop.set()
+        th.join(2)
+        for c in held:
+            c.close()
+        lsock.close()
