@@ -136,6 +136,10 @@ def parse_args():
                          "GPU's NUMA node (nanogpu.affinity)")
     ap.add_argument("--stall-trace", default="",
                     help="sample the extender's Python threads every ms in the timed steps; write gaps/stalls here")
+    ap.add_argument("--probe-pair-timeout", type=float, default=30.0,
+                    help="time box of each GPU pair's peer-copy probe (s); the RCCL ring gets 4x")
+    ap.add_argument("--probe-standin", default="",
+                    help="tests: a stand-in peer probe (hang:SRC-DST never finishes that pair)")
     ap.add_argument("--inproc-driver", action="store_true",
                     help="run the kube-scheduler stand-in inside the extender process (default: own process)")
     return ap.parse_args()
@@ -323,28 +327,54 @@ def thread_cpu() -> dict[str, float]:
 
 
 # --------------------------------------------------------------------------- node template
-def measured_links(d: Dist, host: dict, gpus_per_node: int) -> tuple[float, list | None, str]:
+class StandinProbe:
+    """`--probe-standin hang:SRC-DST` (tests): a peer probe over `world` stand-in GPUs whose
+    SRC -> DST copy never completes (and ignores its own deadline); every other pair 100 GB/s."""
+
+    def __init__(self, spec: str, n: int):
+        kind, _, pair = spec.partition(":")
+        if kind != "hang":
+            raise ValueError(f"--probe-standin: unknown stand-in {spec!r}")
+        a, b = pair.split("-")
+        self.hang = (int(a), int(b))
+        self.n = n
+
+    def peer_bandwidth(self, src, dst, nbytes, iters, deadline_s=30.0):
+        if (src, dst) == self.hang:
+            time.sleep(3600)
+        return {"gbs": 100.0, "pull_gbs": 100.0, "dma_gbs": 0.0, "peer_access": True}
+
+
+def measured_links(d: Dist, host: dict, gpus_per_node: int, group=None, standin: str = "",
+                   pair_timeout_s: float = 30.0) -> tuple[float, list | None, str]:
     """Per-link xGMI weights for the node model (per direction, GB/s): the peer-pull probe
     over every visible pair when this job sees the node's GPUs (all ranks take part), else
     the rate KFD publishes for this GPU's links (a 1-GPU container still sees them), else
-    the placeholder. A probe failure is recorded and never aborts the bench."""
+    the placeholder. Every pair is time-boxed and the ranks agree on the outcome
+    (calibrate.link_matrix over the CPU `group`): a failed or timed-out probe is recorded in
+    the source and never aborts or hangs the bench."""
     from nanogpu.probe.calibrate import link_matrix, reader_link_gbs
 
     link, src = 153.0, "placeholder (no xGMI link visible)"
     rd = reader_link_gbs(host)
     if rd > 0:
         link, src = rd, "kfd io_link max_bandwidth (native topology reader)"
-    if not d.cuda:
+    P = None
+    if standin:
+        ndev = d.world if d.dist is not None else 2
+        P = StandinProbe(standin, ndev)
+    elif not d.cuda:
         return link, None, src
-    import torch
+    else:
+        import torch
 
-    ndev = torch.cuda.device_count()
+        ndev = torch.cuda.device_count()
     try:
         m = None
         if d.dist is not None and d.world == ndev and d.world > 1:
-            m = link_matrix(ndev, dist=d.dist, rank=d.local_rank)
+            m = link_matrix(ndev, dist=d.dist, rank=d.local_rank, P=P, group=group, pair_timeout_s=pair_timeout_s)
         elif d.dist is None and ndev > 1:
-            m = link_matrix(ndev)
+            m = link_matrix(ndev, P=P, pair_timeout_s=pair_timeout_s)
         if m is not None:
             off = [v for a, r in enumerate(m) for b, v in enumerate(r) if a != b]
             src = f"peer-pull probe, {ndev} GPUs, every pair (copy kernel over xGMI)"
@@ -378,17 +408,28 @@ def node_template(d: Dist, args) -> tuple[object, dict]:
 
             info["gpu"]["hbm_copy_gbs"] = round(hbm_bandwidth(d.local_rank, 1 << 30, 10), 1)
     link, matrix = 153.0, None
-    if not args.no_gpu:
-        link, matrix, src = measured_links(d, facts["host"], args.gpus_per_node)
+    # the calibration's own CPU group: its barriers, row exchange and agreements carry a
+    # timeout and cannot queue behind a wedged GPU stream
+    cal = None
+    if d.dist is not None and (not args.no_gpu or args.probe_standin):
+        from datetime import timedelta
+
+        cal = d.dist.new_group(backend="gloo", timeout=timedelta(seconds=max(60.0, 4 * args.probe_pair_timeout)))
+    if not args.no_gpu or args.probe_standin:
+        link, matrix, src = measured_links(d, facts["host"] if not args.no_gpu else {}, args.gpus_per_node,
+                                           group=cal, standin=args.probe_standin,
+                                           pair_timeout_s=args.probe_pair_timeout)
         info["link_bw_source"] = src
         if matrix is not None:
             info["link_bw_matrix_gbs"] = [[round(v, 1) for v in r] for r in matrix]
-        if d.dist is not None and d.cuda:
-            # RCCL all-reduce busBW over all ranks: a collective aggregate, labelled as such
-            try:
-                from nanogpu.probe.calibrate import ring_busbw
+        if d.dist is not None and d.cuda and "failed" not in src:
+            # RCCL all-reduce busBW over all ranks: a collective aggregate, labelled as such;
+            # time-boxed on a communicator of its own, the outcome agreed by every rank
+            from nanogpu.probe.calibrate import ring_busbw_bounded
 
-                info["rccl_allreduce_busbw_gbs"] = round(ring_busbw(d.dist, d.device), 1)
+            try:
+                v, why = ring_busbw_bounded(d.dist, d.device, cal, timeout_s=4 * args.probe_pair_timeout)
+                info["rccl_allreduce_busbw_gbs"] = round(v, 1) if v is not None else why
             except Exception as e:
                 info["rccl_allreduce_busbw_gbs"] = f"error: {type(e).__name__}: {e}"
     info["link_bw_gbs"] = round(link, 1)

@@ -70,48 +70,99 @@ def reader_link_gbs(host: dict) -> float:
     return float(gpus[0].get("xgmi_min_bw_mbs", 0)) / 1000.0 if gpus else 0.0
 
 
+class ProbeTimeout(RuntimeError):
+    """A calibration step that did not finish in its time box (a wedged link, peer or RCCL
+    ring); the node model falls back to the rates KFD publishes."""
+
+
+def bounded(fn, timeout_s: float):
+    """Runs `fn()` on a daemon thread for at most `timeout_s`: ("ok", value), ("error", exc)
+    or ("timeout", None). A call stuck inside the HIP runtime or RCCL is abandoned, not
+    joined, so the rank reaches its next collective and the job agrees on the outcome."""
+    import threading
+
+    box: dict = {}
+
+    def run():
+        try:
+            box["v"] = fn()
+        except BaseException as e:   # noqa: BLE001 - reported to the caller
+            box["e"] = e
+
+    th = threading.Thread(target=run, daemon=True, name="ngpu-probe")
+    th.start()
+    th.join(timeout_s)
+    if th.is_alive():
+        return "timeout", None
+    if "e" in box:
+        return ("timeout" if isinstance(box["e"], TimeoutError) else "error"), box["e"]
+    return "ok", box["v"]
+
+
+_TIMEOUT, _ERROR = -2.0, -1.0
+
+
 def link_matrix(n: int, nbytes: int = 64 << 20, iters: int = 3, dist=None, rank: int = 0,
-                P=None) -> list[list[float]]:
+                P=None, group=None, pair_timeout_s: float = 30.0) -> list[list[float]]:
     """n x n per-direction GB/s, m[src][dst], from the peer-pull probe (0 on the diagonal).
-    `P`: the probe module (tests pass a stand-in)."""
+    `P`: the probe module (tests pass a stand-in). Every pair is time-boxed (`bounded`, and the
+    probe's own event deadline): after a timeout a rank probes nothing more on its GPU. With
+    `dist`, rounds are kept in step and the rows exchanged over `group` (a gloo group with a
+    timeout: CPU-side, so a wedged GPU stream cannot hold it); every rank then holds the same
+    matrix and raises the same ProbeTimeout / RuntimeError, so they all fall back together."""
     P = P or probe(required=True)
     m = [[0.0] * n for _ in range(n)]
+
+    def pair(src: int, dst: int) -> float:
+        kind, v = bounded(lambda: P.peer_bandwidth(src, dst, nbytes, iters, pair_timeout_s), pair_timeout_s + 5.0)
+        return v["gbs"] if kind == "ok" else _TIMEOUT if kind == "timeout" else _ERROR
+
     if dist is None:
+        wedged = False
         for dst in range(n):
             for src in range(n):
                 if src != dst:
-                    m[src][dst] = P.peer_bandwidth(src, dst, nbytes, iters)["gbs"]
-        return m
-    import torch
+                    m[src][dst] = _TIMEOUT if wedged else pair(src, dst)
+                    wedged = wedged or m[src][dst] == _TIMEOUT
+    else:
+        import torch
 
-    row = [0.0] * n                      # this rank's GPU as the destination
-    for k in range(1, n):
-        src = (rank + k) % n
-        dist.barrier()
-        try:                             # a failed pair must not leave the other ranks waiting
-            row[src] = P.peer_bandwidth(src, rank, nbytes, iters)["gbs"]
-        except Exception:
-            row[src] = -1.0
-    if torch.cuda.is_available():
-        torch.cuda.set_device(rank)
-        dev = torch.device("cuda", rank)
-    else:                                # gloo rehearsal of the same exchange
-        dev = torch.device("cpu")
-    t = torch.tensor(row, dtype=torch.float64, device=dev)
-    rows = [torch.zeros_like(t) for _ in range(n)]
-    dist.all_gather(rows, t)
-    for dst, r in enumerate(rows):
-        for src, v in enumerate(r.tolist()):
-            m[src][dst] = v
+        row = [0.0] * n                      # this rank's GPU as the destination
+        wedged = False
+        for k in range(1, n):
+            src = (rank + k) % n
+            dist.barrier(group=group)
+            row[src] = _TIMEOUT if wedged else pair(src, rank)
+            wedged = wedged or row[src] == _TIMEOUT
+        t = torch.tensor(row, dtype=torch.float64)
+        rows = [torch.zeros_like(t) for _ in range(n)]
+        dist.all_gather(rows, t, group=group)
+        for dst, r in enumerate(rows):
+            for src, v in enumerate(r.tolist()):
+                m[src][dst] = v
+    late = [f"{s}->{d}" for s in range(n) for d in range(n) if m[s][d] == _TIMEOUT]
+    if late:
+        raise ProbeTimeout(f"peer copy timed out ({pair_timeout_s:g} s per pair): {', '.join(late[:8])}"
+                           + (f" and {len(late) - 8} more" if len(late) > 8 else ""))
     if any(v < 0 for r in m for v in r):  # every rank sees the same gathered matrix
         raise RuntimeError("peer_bandwidth failed on some pair")
     return m
 
 
-def ring_busbw(dist, device, nbytes: int = 256 << 20, iters: int = 5) -> float:
-    """RCCL all-reduce bus bandwidth (GB/s) over all ranks of the job, one collective on the
-    default group: busBW = 2(n-1)/n x bytes / t. A collective aggregate (several xGMI links
-    at once on a full mesh), not a per-link rate."""
+def agree(dist, ok: bool, group=None) -> bool:
+    """True on every rank iff `ok` on every rank (one MIN all-reduce over `group`)."""
+    import torch
+
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item())
+
+
+def ring_busbw(dist, device, nbytes: int = 256 << 20, iters: int = 5, group=None) -> float:
+    """RCCL all-reduce bus bandwidth (GB/s) over all ranks of the job: busBW = 2(n-1)/n x
+    bytes / t. A collective aggregate (several xGMI links at once on a full mesh), not a
+    per-link rate. `group`: the communicator to measure on (the bench gives it one of its own,
+    so a ring that wedges cannot hold the job's default group)."""
     import torch
 
     n = dist.get_world_size()
@@ -124,16 +175,42 @@ def ring_busbw(dist, device, nbytes: int = 256 << 20, iters: int = 5) -> float:
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
-    dist.all_reduce(buf)   # warm-up (communicator setup)
+    dist.all_reduce(buf, group=group)   # warm-up (communicator setup)
     sync()
     t0 = time.perf_counter()
     for _ in range(iters):
-        dist.all_reduce(buf)
+        dist.all_reduce(buf, group=group)
     sync()
     dt = (time.perf_counter() - t0) / iters
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return 2.0 * (n - 1) / n * nbytes / float(t.item()) / 1e9
+
+
+def ring_busbw_bounded(dist, device, agree_group, timeout_s: float = 60.0, **kw) -> tuple[float | None, str]:
+    """`ring_busbw` in a time box on a communicator of its own, then one agreement over the
+    CPU `agree_group`: (GB/s, "") when every rank finished, else (None, why) on every rank."""
+    import torch
+
+    if torch.device(device).type == "cuda":
+        torch.cuda.set_device(torch.device(device))
+    from datetime import timedelta
+
+    ring = dist.new_group(backend="nccl" if torch.device(device).type == "cuda" else "gloo",
+                          timeout=timedelta(seconds=max(1.0, timeout_s)))
+
+    def run():
+        if torch.device(device).type == "cuda":
+            torch.cuda.set_device(torch.device(device))   # this thread's current device
+        return ring_busbw(dist, device, group=ring, **kw)
+
+    kind, v = bounded(run, timeout_s)
+    ok = agree(dist, kind == "ok", group=agree_group)
+    if ok:
+        return v, ""
+    return None, ("RCCL all-reduce timed out" if kind == "timeout" else
+                  f"RCCL all-reduce failed: {type(v).__name__}: {v}" if kind == "error" else
+                  "RCCL all-reduce failed or timed out on another rank")
 
 
 # --------------------------------------------------------------------------- HBM activity

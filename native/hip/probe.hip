@@ -17,11 +17,13 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace py = pybind11;
@@ -429,17 +431,41 @@ struct PeerRate {
   bool peer_access;
 };
 
+// A peer transfer that did not finish by its deadline (a wedged link or peer). Its stream,
+// events and buffers are abandoned, never freed: hipFree / hipStreamDestroy would wait on the
+// work that never completes.
+struct PeerTimeout : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+using Clock = std::chrono::steady_clock;
+
+// Polls `e` until it completes (true) or `deadline` passes (false); never blocks in the runtime.
+bool wait_event(hipEvent_t e, Clock::time_point deadline) {
+  for (;;) {
+    const hipError_t q = hipEventQuery(e);
+    if (q == hipSuccess) return true;
+    if (q != hipErrorNotReady) HIP_OK(q);
+    if (Clock::now() > deadline) return false;
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+}
+
 // Per-pair link rate for the topology scorer. The copy kernel runs on the destination GPU and
 // loads straight from the peer's memory (peer access enabled), so every byte crosses the one
 // xGMI link between the pair in one direction; its grid (n / 4096 WGs, >> 256 CUs) keeps
-// enough loads in flight to saturate the link rather than one SDMA engine.
-PeerRate peer_bandwidth(int src, int dst, size_t bytes, int iters) {
+// enough loads in flight to saturate the link rather than one SDMA engine. Every wait polls an
+// event against `deadline_s` (from the call): a transfer that never completes throws
+// PeerTimeout instead of blocking the rank (and, through the next collective, the whole job).
+PeerRate peer_bandwidth(int src, int dst, size_t bytes, int iters, double deadline_s) {
   int n_dev = 0;
   HIP_OK(hipGetDeviceCount(&n_dev));
   if (src < 0 || dst < 0 || src >= n_dev || dst >= n_dev || src == dst)
     throw std::invalid_argument("peer_bandwidth: need two distinct visible devices");
   const size_t n = bytes / sizeof(float4);
   if (n == 0 || iters <= 0) throw std::invalid_argument("peer_bandwidth: bytes/iters must be positive");
+  const Clock::time_point deadline =
+      Clock::now() + std::chrono::microseconds(static_cast<int64_t>((deadline_s > 0 ? deadline_s : 30.0) * 1e6));
   PeerRate r{0.0, 0.0, false};
   int prev = 0;   // the caller's current device comes back on return (torch tracks it)
   HIP_OK(hipGetDevice(&prev));
@@ -456,34 +482,73 @@ PeerRate peer_bandwidth(int src, int dst, size_t bytes, int iters) {
     (void)hipGetLastError();
     r.peer_access = true;
   }
-  HIP_OK(hipSetDevice(src));
-  DevBuf<float4> a(n);
-  HIP_OK(hipMemset(a.p, 0, n * sizeof(float4)));
-  HIP_OK(hipDeviceSynchronize());
-  HIP_OK(hipSetDevice(dst));
-  DevBuf<float4> b(n);
-  {
-    Stream st({});
-    Events ev;
-    HIP_OK(hipMemcpyPeerAsync(b.p, dst, a.p, src, n * sizeof(float4), st.s));   // warm-up
-    HIP_OK(hipEventRecord(ev.a, st.s));
-    for (int i = 0; i < iters; ++i) HIP_OK(hipMemcpyPeerAsync(b.p, dst, a.p, src, n * sizeof(float4), st.s));
-    HIP_OK(hipEventRecord(ev.b, st.s));
-    r.dma_gbs = static_cast<double>(n * sizeof(float4)) * iters / (ev.ms() * 1e-3) / 1e9;
+  // owned until a timeout abandons them
+  hipStream_t ss = nullptr, st = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  float4 *a = nullptr, *b = nullptr;
+  bool abandoned = false;
+  auto cleanup = [&] {
+    if (abandoned) return;
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (ss) (void)hipStreamDestroy(ss);
+    if (st) (void)hipStreamDestroy(st);
+    if (a) (void)hipFree(a);
+    if (b) (void)hipFree(b);
+  };
+  auto timed = [&](const char* what, auto&& enqueue) -> double {   // seconds of `enqueue`'s work
+    HIP_OK(hipEventRecord(e0, st));
+    enqueue();
+    HIP_OK(hipEventRecord(e1, st));
+    if (!wait_event(e1, deadline)) {
+      abandoned = true;
+      throw PeerTimeout(std::string("peer_bandwidth ") + std::to_string(src) + "->" + std::to_string(dst) + ": " +
+                        what + " did not finish within " + std::to_string(deadline_s) + " s");
+    }
+    float ms = 0.f;
+    HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+    return ms * 1e-3;
+  };
+  try {
+    HIP_OK(hipSetDevice(src));
+    HIP_OK(hipMalloc(&a, n * sizeof(float4)));
+    HIP_OK(hipStreamCreateWithFlags(&ss, hipStreamNonBlocking));
+    HIP_OK(hipMemsetAsync(a, 0, n * sizeof(float4), ss));
+    hipEvent_t fill = nullptr;
+    HIP_OK(hipEventCreateWithFlags(&fill, hipEventDisableTiming));
+    HIP_OK(hipEventRecord(fill, ss));
+    const bool filled = wait_event(fill, deadline);
+    (void)hipEventDestroy(fill);
+    if (!filled) {
+      abandoned = true;
+      throw PeerTimeout("peer_bandwidth: the source fill on GPU " + std::to_string(src) + " did not finish");
+    }
+    HIP_OK(hipSetDevice(dst));
+    HIP_OK(hipMalloc(&b, n * sizeof(float4)));
+    HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    HIP_OK(hipEventCreate(&e0));
+    HIP_OK(hipEventCreate(&e1));
+    const double nb = static_cast<double>(n * sizeof(float4));
+    timed("SDMA warm-up", [&] { HIP_OK(hipMemcpyPeerAsync(b, dst, a, src, n * sizeof(float4), st)); });
+    r.dma_gbs = nb * iters / timed("SDMA copies", [&] {
+      for (int i = 0; i < iters; ++i) HIP_OK(hipMemcpyPeerAsync(b, dst, a, src, n * sizeof(float4), st));
+    }) / 1e9;
+    if (r.peer_access) {
+      const dim3 grid(copy_grid(n));
+      timed("pull warm-up", [&] {
+        hipLaunchKernelGGL(hbm_copy, grid, dim3(kCopyBlock), 0, st, a, b, n);
+        HIP_OK(hipGetLastError());
+      });
+      r.pull_gbs = nb * iters / timed("pull copies", [&] {
+        for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(hbm_copy, grid, dim3(kCopyBlock), 0, st, a, b, n);
+        HIP_OK(hipGetLastError());
+      }) / 1e9;
+    }
+  } catch (...) {
+    cleanup();
+    throw;
   }
-  if (r.peer_access) {
-    Stream st({});
-    Events ev;
-    const dim3 grid(copy_grid(n));
-    hipLaunchKernelGGL(hbm_copy, grid, dim3(kCopyBlock), 0, st.s, a.p, b.p, n);   // warm-up
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(ev.a, st.s));
-    for (int i = 0; i < iters; ++i) hipLaunchKernelGGL(hbm_copy, grid, dim3(kCopyBlock), 0, st.s, a.p, b.p, n);
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(ev.b, st.s));
-    r.pull_gbs = static_cast<double>(n * sizeof(float4)) * iters / (ev.ms() * 1e-3) / 1e9;
-  }
-  HIP_OK(hipDeviceSynchronize());
+  cleanup();
   return r;
 }
 
@@ -522,11 +587,11 @@ PYBIND11_MODULE(_probe, m) {
         "Concurrent MFMA burns on CU-masked streams; per-stream TFLOP/s.");
   m.def(
       "peer_bandwidth",
-      [](int src, int dst, size_t bytes, int iters) {
+      [](int src, int dst, size_t bytes, int iters, double deadline_s) {
         PeerRate r;
         {
           py::gil_scoped_release nogil;
-          r = peer_bandwidth(src, dst, bytes, iters);
+          r = peer_bandwidth(src, dst, bytes, iters, deadline_s);
         }
         py::dict d;
         d["pull_gbs"] = r.pull_gbs;
@@ -536,5 +601,8 @@ PYBIND11_MODULE(_probe, m) {
         return d;
       },
       py::arg("src"), py::arg("dst"), py::arg("bytes") = size_t(256) << 20, py::arg("iters") = 10,
-      "One-direction xGMI rate src -> dst in GB/s: copy kernel pulling over peer access, and SDMA.");
+      py::arg("deadline_s") = 30.0,
+      "One-direction xGMI rate src -> dst in GB/s: copy kernel pulling over peer access, and SDMA. "
+      "Raises TimeoutError when the transfers do not finish within deadline_s (the work is abandoned).");
+  py::register_exception<PeerTimeout>(m, "PeerTimeout", PyExc_TimeoutError);
 }

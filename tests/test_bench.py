@@ -160,3 +160,22 @@ def test_bench_steady_main_pass_two_ranks_share_placements():
     d = _last_json(r.stdout)
     assert d["value"] > 0 and d["failed"] == 0 and d["scheduled"] > 0
     assert d["value_mode"].startswith("2 independent kube-scheduler stand-ins")
+
+
+def test_bench_multi_rank_survives_a_hung_peer_probe():
+    """One GPU pair's peer copy never completes (a stand-in probe): every rank gives up on it
+    within the pair's time box, they agree, the node model falls back to the KFD / placeholder
+    link rate with the timeout named in `link_bw_source`, and the bench finishes."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
+                        "--gpus", "4", "--no-gpu", "--steps", "1", "--warmup", "1", "--pods", "100",
+                        "--nodes", "8", "--rtt-variant-ms", "0", "--steady-variant-steps", "0", "--nodes-variant", "0",
+                        "--inproc-variant-steps", "0", "--independent-variant-steps", "0",
+                        "--probe-standin", "hang:1-2", "--probe-pair-timeout", "1"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    src = d["gpu"]["link_bw_source"]
+    assert "ProbeTimeout" in src and "1->2" in src, src
+    assert d["gpu"]["link_bw_gbs"] == 153.0 and d["scheduled"] == 100 and d["failed"] == 0

@@ -109,6 +109,10 @@ def test_agent_node_model_from_real_device(host):
 
 
 def test_peer_bandwidth_multi_gpu(P):
+    # the deadline-bounded probe: a wedged transfer raises PeerTimeout (a TimeoutError)
+    assert issubclass(P.PeerTimeout, TimeoutError)
+    with pytest.raises(ValueError):
+        P.peer_bandwidth(0, 0, 1 << 20, 1, 5.0)
     if P.device_count() < 2:
         pytest.skip("single visible GPU")
     r = P.peer_bandwidth(0, 1, 64 << 20, 3)
@@ -496,15 +500,19 @@ import json, os, sys
 import torch
 import torch.distributed as dist
 sys.path.insert(0, os.environ["NANOGPU_ROOT"])
-from nanogpu.probe.calibrate import link_matrix, ring_busbw
+from datetime import timedelta
+from nanogpu.probe.calibrate import link_matrix, ring_busbw, ring_busbw_bounded
 torch.cuda.set_device(0)
 dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
 out = {"backend": dist.get_backend()}
 out["busbw"] = ring_busbw(dist, "cuda:0", nbytes=64 << 20, iters=3)   # one rank: 0 by definition
+# the bench's calibration: a gloo group for agreement, the ring on a communicator of its own
+cal = dist.new_group(backend="gloo", timeout=timedelta(seconds=60))
+out["busbw_bounded"] = list(ring_busbw_bounded(dist, "cuda:0", cal, timeout_s=60, nbytes=64 << 20, iters=3))
 t = torch.full((1 << 20,), 2.0, dtype=torch.bfloat16, device="cuda:0")
 dist.all_reduce(t)
 out["allreduce_ok"] = bool((t == 2.0).all().item())
-out["matrix"] = link_matrix(1, dist=dist, rank=0)                      # the all-gathered rows
+out["matrix"] = link_matrix(1, dist=dist, rank=0, group=cal)           # the all-gathered rows
 dist.barrier(device_ids=[0])
 got = [None]
 dist.all_gather_object(got, {"rank": 0})
@@ -535,3 +543,4 @@ def test_rccl_paths_of_the_multi_rank_bench_run_on_the_device(tmp_path):
     record("rccl_one_rank", out)
     assert out["backend"] == "nccl" and out["allreduce_ok"]
     assert out["busbw"] == 0.0 and out["matrix"] == [[0.0]] and out["objects"] == [0, "url"]
+    assert out["busbw_bounded"] == [0.0, ""]

@@ -11,39 +11,51 @@ import torch.multiprocessing as mp
 
 
 class FakeProbe:
-    def __init__(self, fail_pair=None):
+    def __init__(self, fail_pair=None, hang_pair=None):
         self.calls = []
         self.fail_pair = fail_pair
+        self.hang_pair = hang_pair
 
-    def peer_bandwidth(self, src, dst, nbytes, iters):
+    def peer_bandwidth(self, src, dst, nbytes, iters, deadline_s=30.0):
+        import time
+
         self.calls.append((src, dst))
         if (src, dst) == self.fail_pair:
             raise RuntimeError("peer access denied")
+        if (src, dst) == self.hang_pair:
+            time.sleep(3600)          # a copy that never completes (and ignores its deadline)
         return {"gbs": 10.0 * src + dst + 1, "pull_gbs": 0.0, "dma_gbs": 0.0, "peer_access": True}
 
 
-def _rank(rank, world, port, fail_pair, q):
+def _rank(rank, world, port, fail_pair, q, hang_pair=None):
+    import time
+    from datetime import timedelta
+
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from nanogpu.probe.calibrate import link_matrix
+    from nanogpu.probe.calibrate import ProbeTimeout, link_matrix
 
-    fp = FakeProbe(fail_pair)
+    group = dist.new_group(backend="gloo", timeout=timedelta(seconds=60))
+    fp = FakeProbe(fail_pair, hang_pair)
+    t0 = time.monotonic()
     try:
-        m = link_matrix(world, dist=dist, rank=rank, P=fp)
+        m = link_matrix(world, dist=dist, rank=rank, P=fp, group=group, pair_timeout_s=0.5)
         q.put((rank, "ok", m, fp.calls))
+    except ProbeTimeout as e:
+        q.put((rank, "timeout", (str(e), time.monotonic() - t0), fp.calls))
     except RuntimeError as e:
         q.put((rank, "error", str(e), fp.calls))
     dist.destroy_process_group()
 
 
-def _run(world, fail_pair=None):
+def _run(world, fail_pair=None, hang_pair=None):
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_rank, args=(r, world, port, fail_pair, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank, args=(r, world, port, fail_pair, q, hang_pair)) for r in range(world)]
     for p in procs:
         p.start()
     out = [q.get(timeout=120) for _ in range(world)]
@@ -70,6 +82,18 @@ def test_link_matrix_rounds_are_permutations_and_rows_gather(world):
 def test_a_failed_pair_fails_every_rank_without_a_hang():
     out = _run(2, fail_pair=(1, 0))
     assert [status for _, status, _, _ in out] == ["error", "error"]
+
+
+def test_a_hung_pair_times_out_on_every_rank():
+    """One peer copy never completes: its rank gives up on it after the pair's time box and
+    probes nothing more; every rank gets the same ProbeTimeout naming the pair, within a
+    few time boxes (no rank blocks in a collective)."""
+    out = _run(4, hang_pair=(1, 2))
+    assert [status for _, status, _, _ in out] == ["timeout"] * 4, out
+    for rank, _, (msg, took), calls in out:
+        assert "1->2" in msg and took < 30
+        if rank == 2:   # after the hung pull from GPU 1, GPU 2 pulls from no other peer
+            assert calls == [(3, 2), (0, 2), (1, 2)][: calls.index((1, 2)) + 1]
 
 
 def _busbw_rank(rank, world, port, q):
@@ -103,3 +127,39 @@ def test_ring_busbw_runs_on_the_cpu_rehearsal(world):
     assert all(st == "ok" for _, st, _ in out), out
     vals = {round(v, 6) for _, _, v in out}
     assert len(vals) == 1 and next(iter(vals)) > 0      # the max over ranks, the same everywhere
+
+
+def _busbw_hang_rank(rank, world, port, q):
+    import time
+    from datetime import timedelta
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from nanogpu.probe import calibrate
+
+    if rank == 1:   # this rank's ring never finishes
+        calibrate.ring_busbw = lambda *a, **k: time.sleep(3600)
+    agree = dist.new_group(backend="gloo", timeout=timedelta(seconds=60))
+    t0 = time.monotonic()
+    v, why = calibrate.ring_busbw_bounded(dist, "cpu", agree, timeout_s=2.0, nbytes=1 << 20, iters=1)
+    q.put((rank, v, why, time.monotonic() - t0))
+    dist.destroy_process_group()
+
+
+def test_a_hung_ring_is_agreed_on_by_every_rank():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_busbw_hang_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(30)
+        if p.is_alive():
+            p.kill()
+    for rank, v, why, took in out:
+        assert v is None and why and took < 30, out
