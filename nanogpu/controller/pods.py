@@ -51,14 +51,18 @@ class PodController:
         if self.state.release_uid(uid) and self.metrics:
             self.metrics.pods_released.inc()
 
-    def _on_relist(self, pods: list[dict], before: float) -> None:
+    async def _on_relist(self, pods: list[dict], before: float) -> None:
         """client-go's reflector turns every key missing from a relist into a delete, and the
         reference's informer handlers rely on it (controller.go:89-136, 337-357). The store's
         own diff (informer.py::_list) covers the pods Python held; pods the native watch filter
         kept away from Python (bound by this extender, held only by the ledger) are reconciled
-        here: a committed share whose pod the LIST no longer returns is released."""
-        uids = [(p.get("metadata") or {}).get("uid", "") for p in pods]
-        gone = self.state.reconcile([u for u in uids if u], before)
+        here: a committed share whose pod the LIST no longer returns is released. The ledger
+        walk runs on an executor thread without the GIL (the UIDs cross as one string), so the
+        event loop keeps serving while a 100k-pod relist is reconciled."""
+        joined = "\n".join(u for u in ((p.get("metadata") or {}).get("uid", "") for p in pods) if u)
+        loop = asyncio.get_running_loop()
+        gone = await loop.run_in_executor(None, self.state.reconcile_native, joined, before)
+        self.state.note_released(gone)
         if gone:
             self.reconciled += len(gone)
             if self.metrics:

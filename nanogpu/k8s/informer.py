@@ -71,7 +71,8 @@ class Informer:
         self.handlers.append(h)
 
     def add_relist_hook(self, h: Callable[[list[dict], float], None]) -> None:
-        """`h(items, before)` runs after each LIST. The native watch filter keeps the pods this
+        """`h(items, before)` runs after each LIST (awaited when it is a coroutine function; the
+        watch resumes after it). The native watch filter keeps the pods this
         extender bound out of the store, so the store's diff below cannot see them vanish;
         the hook lets the ledger reconcile against the listed objects directly."""
         self.relist_hooks.append(h)
@@ -114,7 +115,9 @@ class Informer:
             self.watch_filter.reset(list(self.store))   # everything listed is in the store now
         for h in self.relist_hooks:
             try:
-                h(items, before)
+                r = h(items, before)
+                if asyncio.iscoroutine(r):   # a hook that moves its work off the loop
+                    await r
             except Exception:  # a hook bug must not kill the informer
                 log.exception("%s informer relist hook failed", self.resource)
 

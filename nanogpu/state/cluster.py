@@ -424,12 +424,20 @@ class ClusterState:
     def reconcile(self, live_uids: list[str], before: float) -> list[str]:
         """After a pod LIST: releases committed shares recorded before `before` whose pod is
         not among `live_uids` (Ledger::reconcile). Returns the UIDs released."""
-        gone = self.ledger.reconcile(live_uids, float(before))
-        for uid in gone:
+        gone = self.reconcile_native("\n".join(live_uids), before)
+        self.note_released(gone)
+        return gone
+
+    def reconcile_native(self, joined_uids: str, before: float) -> list[str]:
+        """The ledger half of `reconcile` (thread-safe, runs without the GIL: the pod
+        controller calls it from an executor thread); `joined_uids` newline-separated."""
+        return self.ledger.reconcile_joined(joined_uids, float(before))
+
+    def note_released(self, uids: list[str]) -> None:
+        for uid in uids:
             self._released[uid] = None
         while len(self._released) > self._released_cap:
             self._released.popitem(last=False)
-        return gone
 
     def known(self, uid: str) -> bool:
         return self.ledger.lookup(uid) is not None

@@ -279,6 +279,8 @@ class Ledger {
   // after `before` may postdate the LIST's snapshot and is left alone too. Returns the keys
   // released.
   std::vector<std::string> reconcile(const std::vector<std::string>& live, double before);
+  // The same over views (the binding hands the LIST's UIDs as one newline-joined string)
+  std::vector<std::string> reconcile_views(const std::vector<std::string_view>& live, double before);
   // Releases `key` only while it is Committed (reconcile racing a re-bind of the same key).
   int32_t drop_committed(const std::string& key);
   int64_t n_pods() const { return hdr_->n_pods.load(std::memory_order_acquire); }

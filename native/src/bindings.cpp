@@ -668,6 +668,24 @@ PYBIND11_MODULE(_native, m) {
       .def("expired_nominations", &Ledger::expired_nominations, py::call_guard<py::gil_scoped_release>())
       .def("drop_reservation", &Ledger::drop_reservation, py::call_guard<py::gil_scoped_release>())
       .def("drop_committed", &Ledger::drop_committed, py::call_guard<py::gil_scoped_release>())
+      .def(
+          "reconcile_joined",
+          [](Ledger& l, const std::string& joined, double before) {
+            py::gil_scoped_release nogil;
+            std::vector<std::string_view> v;
+            v.reserve(joined.size() / 37 + 1);
+            size_t a = 0;
+            while (a < joined.size()) {
+              size_t b = joined.find('\n', a);
+              if (b == std::string::npos) b = joined.size();
+              if (b > a) v.emplace_back(joined.data() + a, b - a);
+              a = b + 1;
+            }
+            return l.reconcile_views(v, before);
+          },
+          py::arg("joined"), py::arg("before"),
+          "reconcile() with the listed UIDs as one newline-joined string: one copy across the "
+          "binding, the split and the walk without the GIL")
       .def("reconcile", &Ledger::reconcile, py::arg("live"), py::arg("before"),
            py::call_guard<py::gil_scoped_release>(),
            "Relist: release Committed pods recorded before `before` (mono_now) whose key is not in "

@@ -1116,9 +1116,42 @@ std::vector<std::string> Ledger::expired_reservations(double older_than_s) const
 int32_t Ledger::drop_committed(const std::string& key) { return release_if(key, kPodCommitted); }
 
 std::vector<std::string> Ledger::reconcile(const std::vector<std::string>& live, double before) {
-  std::unordered_set<std::string_view> alive;
-  alive.reserve(live.size() * 2);
-  for (const std::string& k : live) alive.insert(k);
+  std::vector<std::string_view> v(live.begin(), live.end());
+  return reconcile_views(v, before);
+}
+
+// Cost at 100k listed pods: one hash set of the views, one pass over every pod slot with each
+// shard's lock held for that shard's slots only (a reserve waits for at most one shard's pass),
+// then the releases one by one (native/tests/stress_main.cpp relist_scale pins both).
+std::vector<std::string> Ledger::reconcile_views(const std::vector<std::string_view>& live, double before) {
+  // the listed keys in a flat open-addressing table keyed by the hash every pod slot already
+  // stores (key_hash): one probe per committed slot, the key bytes compared only on a match
+  size_t cap = 64;
+  while (cap < live.size() * 2) cap <<= 1;
+  std::vector<uint64_t> th(cap, 0);
+  std::vector<uint32_t> ti(cap, 0);
+  for (size_t i = 0; i < live.size(); ++i) {
+    const std::string_view k = live[i];
+    uint64_t h = 0xcbf29ce484222325ULL;   // key_hash over the view's bytes
+    for (const unsigned char c : k) {
+      h ^= c;
+      h *= 0x100000001b3ULL;
+    }
+    h ^= h >> 33;
+    h *= 0xff51afd7ed558ccdULL;
+    h ^= h >> 33;
+    h |= 1;   // 0 marks an empty cell
+    size_t j = h & (cap - 1);
+    while (th[j]) j = (j + 1) & (cap - 1);
+    th[j] = h;
+    ti[j] = static_cast<uint32_t>(i);
+  }
+  auto listed = [&](const PodSlot& p) {
+    const uint64_t h = p.hash | 1;
+    for (size_t j = h & (cap - 1); th[j]; j = (j + 1) & (cap - 1))
+      if (th[j] == h && live[ti[j]] == std::string_view(p.key)) return true;
+    return false;
+  };
   std::vector<std::string> gone;
   for (int s = 0; s < kPodShards; ++s) {
     lock_mu(&hdr_->shard_mu[s].m);
@@ -1126,8 +1159,7 @@ std::vector<std::string> Ledger::reconcile(const std::vector<std::string>& live,
     const PodSlot* t = shard(s);
     for (uint32_t i = 0; i < hdr_->pods_per_shard; ++i) {
       const PodSlot& p = t[i];
-      if (p.state == kPodCommitted && p.t_reserved < before && !alive.count(std::string_view(p.key)))
-        gone.emplace_back(p.key);
+      if (p.state == kPodCommitted && p.t_reserved < before && !listed(p)) gone.emplace_back(p.key);
     }
   }
   std::vector<std::string> released;

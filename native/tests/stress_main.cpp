@@ -221,6 +221,81 @@ static void relist_gap(int iters) {
   std::printf("relist ok: %d ghosts, %d reconciled\n", ghosts.load(), reconciled.load());
 }
 
+// Relist reconciliation at cluster scale: `pods` committed pods on 256 nodes, a LIST that
+// returns all but 1 %, reconciled while a front-door stand-in reserves and releases on the same
+// ledger. Prints the best-of-3 reconcile time and the slowest reserve seen during the walks
+// (tests/test_relist_scale.py pins both). Usage: nanogpu-stress relist-scale [pods]
+static void relist_scale(int pods) {
+  const int n_nodes = 256;
+  Ledger l("", n_nodes, std::max(131072, pods + 4096), true);
+  for (int k = 0; k < n_nodes; ++k) {
+    Device devs[8];
+    std::memset(devs, 0, sizeof(devs));
+    for (int i = 0; i < 8; ++i) {
+      devs[i].pct_total = 100;
+      devs[i].mib_total = 294896;
+      devs[i].gpu = static_cast<int16_t>(i);
+      devs[i].healthy = 1;
+      devs[i].xcds = 8;
+      devs[i].cus = 256;
+    }
+    Topology t;
+    std::memset(&t, 0, sizeof(t));
+    t.n_gpus = 8;
+    CHECK(l.upsert_node("node-" + std::to_string(k), devs, 8, t) == k);
+  }
+  double best_ms = 1e9, reserve_max_ms = 0.0;
+  size_t released_total = 0;
+  for (int round = 0; round < 3; ++round) {
+    std::vector<std::string> keys;
+    keys.reserve(static_cast<size_t>(pods));
+    Options o;
+    Demand d;
+    std::memset(&d, 0, sizeof(d));
+    d.n = 1;
+    d.c[0].pct = 0;
+    d.c[0].mib = 1;   // HBM only: 100k pods fit 256 nodes
+    for (int i = 0; i < pods; ++i) {
+      char uid[48];
+      std::snprintf(uid, sizeof uid, "%08x-0000-4000-8000-%012d", round, i);
+      keys.emplace_back(uid);
+      Plan p;
+      CHECK(l.reserve(i % n_nodes, keys.back(), d, o, &p) == kOk);
+      CHECK(l.commit(keys.back()) == kOk);
+    }
+    const double before = mono_now() + 1.0;
+    std::vector<std::string_view> live;
+    for (int i = 0; i < pods; ++i)
+      if (i % 100 != 0) live.emplace_back(keys[static_cast<size_t>(i)]);
+    std::atomic<bool> walking{true};
+    double worst = 0.0;
+    std::thread fd([&] {   // the front door: reserve + release while the walk runs
+      int n = 0;
+      while (walking.load(std::memory_order_relaxed)) {
+        const std::string k = "fd-" + std::to_string(n++);
+        Plan p;
+        const auto t0 = std::chrono::steady_clock::now();
+        const int32_t rc = l.reserve(n % n_nodes, k, d, o, &p);
+        worst = std::max(worst, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        if (rc == kOk) CHECK(l.release(k) == kOk);
+      }
+    });
+    const auto t0 = std::chrono::steady_clock::now();
+    const std::vector<std::string> gone = l.reconcile_views(live, before);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    walking.store(false);
+    fd.join();
+    CHECK(gone.size() == static_cast<size_t>((pods + 99) / 100));
+    best_ms = std::min(best_ms, ms);
+    reserve_max_ms = std::max(reserve_max_ms, worst);
+    released_total += gone.size();
+    for (const std::string_view k : live) CHECK(l.release(std::string(k)) == kOk);
+    CHECK(l.n_pods() == 0);
+  }
+  std::printf("relist_scale {\"pods\": %d, \"reconcile_ms\": %.3f, \"reserve_max_ms\": %.3f, \"released\": %zu}\n",
+              pods, best_ms, reserve_max_ms, released_total);
+}
+
 // Bind handoff slots (Ledger::put_pod_info / take_pod_info) under concurrency: writers and
 // takers on colliding slots never see a torn or foreign blob.
 static void handoff(int iters) {
@@ -483,6 +558,10 @@ static void mailbox_wakeups(int requests) {
 }
 
 int main(int argc, char** argv) {
+  if (argc > 1 && std::strcmp(argv[1], "relist-scale") == 0) {
+    relist_scale(argc > 2 ? std::atoi(argv[2]) : 100000);
+    return 0;
+  }
   const int threads = argc > 1 ? std::atoi(argv[1]) : 4;
   const int iters = argc > 2 ? std::atoi(argv[2]) : 2000;
   const int n_nodes = 6;
