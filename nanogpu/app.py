@@ -48,7 +48,7 @@ class Config:
     verify_pod_on_bind: bool = False
     native_bind_writes: bool = True             # C++ writer threads do the bind's API writes
     bind_writer_threads: int = 16               # x KubeWriter::kBatch (8) binds in flight
-    bind_writer_mode: str = "evented"           # evented (one epoll thread) | threads (blocking threads)
+    bind_writer_mode: str = "evented"           # inline (front-door workers) | evented (one epoll thread) | threads
     native_pod_watch: bool = True               # a C++ thread reads and filters the pod watch (podwatch.cpp)
     # the reference's `nano-gpu/assume` label, PATCHed beside the binding; off: one write a bind
     # (the binding carries the annotations; this project's agent selects pods by node)
@@ -211,8 +211,9 @@ class Runtime:
                 if self.cfg.native_bind_writes and not self.cfg.verify_pod_on_bind and api_cfg is not None:
                     ext = self.extender
                     if self.native.enable_native_writes(api_cfg, self.cfg.bind_writer_threads, ext.api_retries,
-                                                        ext.record_events, self.cfg.bind_writer_mode == "evented",
-                                                        self.cfg.assume_label, self.cfg.api_write_timeout_s):
+                                                        ext.record_events, self.cfg.bind_writer_mode != "threads",
+                                                        self.cfg.assume_label, self.cfg.api_write_timeout_s,
+                                                        self.cfg.bind_writer_mode == "inline"):
                         log.info("worker %d: bind API writes in native writer threads (%d)", self.worker,
                                  self.cfg.bind_writer_threads)
                 self.native.start()

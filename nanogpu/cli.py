@@ -61,8 +61,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--bind-writer-threads", type=int, default=16,
                    help="binds in flight / 8 for the native writer (16: 128 binds); in --bind-writer-mode "
                         "threads, the number of blocking writer threads")
-    p.add_argument("--bind-writer-mode", choices=["evented", "threads"], default="evented",
-                   help="native bind writes on one epoll thread (evented) or on blocking threads")
+    p.add_argument("--bind-writer-mode", choices=["inline", "evented", "threads"], default="evented",
+                   help="native bind writes: from each front-door worker's own epoll loop (inline), on one "
+                        "epoll thread (evented) or on blocking threads")
     p.add_argument("--api-write-timeout", default="30s",
                    help="native bind writer: an API request unanswered this long fails over to the slow "
                         "path (a half-open connection never answers)")

@@ -1,0 +1,84 @@
+// The evented half of the native bind writer (see kubewriter.h): the API requests of every bind
+// in flight on non-blocking keep-alive connections (plain or TLS), driven by an epoll set that
+// belongs to whoever owns the BindIo:
+//   * the writer's own io thread (KubeWriter evented mode: ngpu-wr-io), or
+//   * a front-door worker (inline mode): the worker that parsed the bind sends its binding
+//     from its own epoll loop, takes the API answer there and writes kube-scheduler's reply
+//     on the same thread. No hand-off to a writer thread and back (eventfd, two wake-ups and
+//     a mailbox per bind); a busy-polling worker catches the API answer in its spin.
+// Happy path only: a bind whose binding (and label PATCH) answer 2xx is committed and answered
+// here. Every other outcome goes to the writer's slow-path threads (KubeWriter::finish).
+#pragma once
+
+#include <cstdint>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <string>
+#include <sys/socket.h>
+#include <vector>
+
+#include "nanogpu/kubewriter.h"
+
+namespace nanogpu {
+
+class BindIo {
+ public:
+  using Reply = std::function<void(uint64_t id, int status, const std::string& body)>;
+  // Registers its sockets in `ep` with epoll data `tag_bit | k` (k: connection index); `reply`
+  // answers a bind that completed on the happy path (from the owning thread).
+  BindIo(KubeWriter* kw, int ep, uint64_t tag_bit, int max_inflight, Reply reply);
+  ~BindIo();
+  BindIo(const BindIo&) = delete;
+  BindIo& operator=(const BindIo&) = delete;
+
+  void submit(BindJob j);                      // launches it now, or when a slot frees up
+  void on_event(uint64_t k, uint32_t events);  // an epoll event of connection k
+  void pump();                                 // after a batch of events: drive what is due
+  size_t inflight() const { return inflight_; }
+  size_t waiting() const { return waiting_.size(); }
+  // Stop: every bind still in flight or waiting goes to the slow path with what it got
+  // (`why` for answers that never came). The connections are closed.
+  void abandon(const char* why);
+  uint64_t timeouts() const { return timeouts_; }
+
+ private:
+  struct Conn;
+  struct Job;
+  bool resolve();
+  void close_conn(Conn& c);
+  bool open_conn(size_t k);
+  void request(std::string* r, const char* method, const BindJob& j, bool binding, std::string_view ctype,
+               const std::string& body);
+  void complete(int64_t s);
+  void deliver(Conn& c, int status, std::string body);
+  void deliver_rest(Conn& c, const char* why);
+  void fail(size_t k, const char* why);
+  void drive(size_t k, uint32_t events);
+  void launch(int64_t s);
+  void start_waiting();
+  void scan_deadlines(uint64_t now);
+
+  KubeWriter* kw_;
+  int ep_;
+  uint64_t tag_bit_;
+  Reply reply_;
+  std::vector<std::unique_ptr<Conn>> conns_;   // index = epoll tag (without tag_bit)
+  std::vector<size_t> idle_;
+  std::vector<std::unique_ptr<Job>> slots_;
+  std::vector<int64_t> free_slots_;
+  std::deque<BindJob> waiting_;
+  std::vector<size_t> kick_;                   // connections to drive in pump()
+  sockaddr_storage addr_{};
+  socklen_t addr_len_ = 0;
+  int family_ = 0;
+  std::string auth_;
+  uint64_t auth_at_ = 0;
+  std::string host_hdr_;
+  size_t inflight_ = 0;
+  uint64_t timeout_ns_ = 0;
+  uint64_t scanned_at_ = 0;
+  uint64_t timeouts_ = 0;
+};
+
+}  // namespace nanogpu

@@ -111,8 +111,10 @@ class Frontend {
   void stop();
   // Native bind writes: from now on a bind whose reservation succeeded here is finished by
   // KubeWriter threads (PATCH + binding + commit / rollback) without Python. Set once.
+  // `inline_io`: each worker drives the API requests of the binds it parsed from its own epoll
+  // loop and answers them itself (BindIo, bindio.h); else the writer's own io thread does.
   void set_kube_writer(const KubeTarget& t, int threads, int retries, bool record_events,
-                       bool evented = true, bool label = true, double timeout_s = 30.0);
+                       bool evented = true, bool label = true, double timeout_s = 30.0, bool inline_io = false);
   const KubeWriter* kube_writer() const { return writer_.load(std::memory_order_acquire); }
   // The native filter / priorities verb on a request body (what a worker runs per request);
   // false = the request needs the Python path.
@@ -154,13 +156,18 @@ class Frontend {
   bool has_pod(std::string_view uid) const;
   void prepare_bind(std::string_view body, PyRequest* r);
   void note_bind_wall(uint64_t ns);
+  // a response for connection `conn` of worker w, on w's thread: sent, then its next request
+  void deliver_reply(Worker* w, uint64_t conn, std::string&& bytes);
+  void drain_local(Worker* w);   // the replies w's BindIo queued during its last call
+  static std::string http_response(int status, const std::string& content_type, const std::string& body);
 
   std::shared_ptr<Ledger> ledger_;
   std::unique_ptr<KubeWriter> writer_owner_;
   std::atomic<KubeWriter*> writer_{nullptr};
   int port_ = 0;
   int py_efd_ = -1;
-  std::atomic<bool> stop_{false};
+  std::atomic<bool> stopping_{false};   // stop() entered (idempotence)
+  std::atomic<bool> stop_{false};       // the workers leave their loops
   std::atomic<bool> serving_{true};
   std::atomic<int64_t> busy_poll_ns_{0};
   std::vector<std::unique_ptr<Worker>> workers_;

@@ -119,17 +119,26 @@ struct KubeWriterStats {
 //     the blocking code below. One wake-up serves every answer that arrived together, where
 //     a thread per batch sleeps and wakes once per request (kubewriter_evented.cpp);
 //   * threads: `threads` blocking threads, each pipelining up to kBatch binds.
+class BindIo;
+
 class KubeWriter {
  public:
   using Respond = std::function<void(uint64_t id, int status, const std::string& body)>;
   // `label`: also PATCH the assume label behind the binding, the reference's pod contract;
   // false: the binding alone, which carries the annotations. `timeout_s`: an API request
   // unanswered this long fails (a half-open connection never answers, nor resets).
+  // `inline_io` (evented only): no io thread; the owners of epoll loops (front-door workers)
+  // drive the requests themselves through make_io(), and submit() is not used.
   KubeWriter(KubeTarget target, std::shared_ptr<Ledger> ledger, Respond respond, int threads, int retries,
-             bool record_events, bool evented = true, bool label = true, double timeout_s = 30.0);
+             bool record_events, bool evented = true, bool label = true, double timeout_s = 30.0,
+             bool inline_io = false);
   ~KubeWriter();
   void submit(BindJob job);
   void stop();
+  // An evented request driver on the caller's epoll set `ep` (tags `tag_bit | k`); `reply`
+  // answers its happy-path binds on the caller's thread. Failures go to this writer's slow path.
+  std::unique_ptr<BindIo> make_io(int ep, uint64_t tag_bit, Respond reply);
+  bool inline_io() const { return inline_io_; }
   KubeWriterStats stats;
 
  private:
@@ -151,6 +160,7 @@ class KubeWriter {
            const std::string& body, std::string* resp, bool retry);
   std::string auth();
 
+  friend class BindIo;
   // evented mode (kubewriter_evented.cpp)
   struct SlowJob {
     BindJob j;
@@ -160,6 +170,9 @@ class KubeWriter {
   };
   void io_loop();
   void run_slow();
+  void to_slow(SlowJob&& sj);    // the slow path takes it (or, once its threads are gone, the caller)
+  bool inline_io_ = false;
+  bool slow_gone_ = false;       // under mu_: the slow-path threads have exited
   bool evented_ = false;
   int max_inflight_ = 0;
   int efd_ = -1;                 // wakes the io thread (new jobs, stop)

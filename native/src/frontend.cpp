@@ -1,6 +1,8 @@
 // Native extender front door (see frontend.h).
 #include "nanogpu/frontend.h"
 
+#include "nanogpu/bindio.h"
+
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <netinet/in.h>
@@ -370,6 +372,11 @@ struct Frontend::Conn {
 struct Frontend::Worker {
   int idx = 0;
   int lfd = -1, ep = -1, efd = -1;
+  // inline bind writes (set_kube_writer inline_io): this worker's request driver, published
+  // once from the setting thread, then used by this worker's thread only
+  std::unique_ptr<BindIo> bio_owner;
+  std::atomic<BindIo*> bio{nullptr};
+  std::vector<std::pair<uint64_t, std::string>> local_replies;   // (conn id, response bytes)
   std::thread th;
   std::unordered_map<uint64_t, std::unique_ptr<Conn>> conns;   // by conn id
   std::mutex mb_mu;
@@ -388,6 +395,8 @@ struct Frontend::Worker {
 };
 
 static uint64_t make_id(int worker, uint64_t conn) { return (conn << 8) | static_cast<uint64_t>(worker); }
+// epoll tags: 0 listen socket, 1 mailbox, bit 63 a client connection, bit 62 a BindIo connection
+static constexpr uint64_t kBioTag = 1ull << 62;
 
 int presize_fd_table(int want) {
   rlimit rl{};
@@ -466,23 +475,37 @@ Frontend::Frontend(std::shared_ptr<Ledger> ledger, const std::string& host, int 
 Frontend::~Frontend() { stop(); }
 
 void Frontend::set_kube_writer(const KubeTarget& t, int threads, int retries, bool record_events, bool evented,
-                               bool label, double timeout_s) {
+                               bool label, double timeout_s, bool inline_io) {
   if (writer_.load()) throw std::logic_error("Frontend: the kube writer is already set");
   writer_owner_ = std::make_unique<KubeWriter>(
       t, ledger_, [this](uint64_t id, int status, const std::string& body) { respond(id, status, "application/json", body); },
-      threads, retries, record_events, evented, label, timeout_s);
+      threads, retries, record_events, evented, label, timeout_s, inline_io);
+  if (inline_io) {
+    for (auto& wp : workers_) {
+      Worker* w = wp.get();
+      // happy-path answers from w's own BindIo, on w's thread: queued, sent after the call
+      w->bio_owner = writer_owner_->make_io(w->ep, kBioTag, [w](uint64_t id, int status, const std::string& body) {
+        w->local_replies.emplace_back(id >> 8, http_response(status, "application/json", body));
+      });
+      w->bio.store(w->bio_owner.get(), std::memory_order_release);
+    }
+  }
   writer_.store(writer_owner_.get(), std::memory_order_release);
 }
 
 void Frontend::stop() {
-  if (stop_.exchange(true)) return;
-  if (writer_owner_) writer_owner_->stop();   // answers what it still holds through the workers
+  if (stopping_.exchange(true)) return;
+  // the workers still run while the writer stops: what it answers reaches kube-scheduler
+  if (writer_owner_) writer_owner_->stop();
+  stop_.store(true, std::memory_order_release);
   for (auto& w : workers_) {
     uint64_t one = 1;
     (void)!write(w->efd, &one, sizeof(one));
   }
   for (auto& w : workers_) {
     if (w->th.joinable()) w->th.join();
+    w->bio.store(nullptr, std::memory_order_relaxed);
+    w->bio_owner.reset();   // its sockets leave w->ep before the epoll fd closes
     for (auto& kv : w->conns) close(kv.second->fd);
     w->conns.clear();
     close(w->lfd);
@@ -509,16 +532,21 @@ std::vector<PyRequest> Frontend::take() {
   return out;
 }
 
-void Frontend::respond(uint64_t id, int status, const std::string& content_type, const std::string& body,
-                       bool notify) {
-  const int widx = static_cast<int>(id & 0xff);
-  if (widx < 0 || widx >= static_cast<int>(workers_.size())) return;
-  Worker* w = workers_[widx].get();
+std::string Frontend::http_response(int status, const std::string& content_type, const std::string& body) {
   std::string r;
   r.reserve(body.size() + 128);
   r += "HTTP/1.1 " + std::to_string(status) + " " + reason(status) + "\r\nContent-Type: " + content_type +
        "\r\nContent-Length: " + std::to_string(body.size()) + "\r\n\r\n";
   r += body;
+  return r;
+}
+
+void Frontend::respond(uint64_t id, int status, const std::string& content_type, const std::string& body,
+                       bool notify) {
+  const int widx = static_cast<int>(id & 0xff);
+  if (widx < 0 || widx >= static_cast<int>(workers_.size())) return;
+  Worker* w = workers_[widx].get();
+  std::string r = http_response(status, content_type, body);
   bool signal = false;
   {
     std::lock_guard<std::mutex> g(w->mb_mu);
@@ -720,19 +748,7 @@ void Frontend::run(Worker* w) {
       w->mb_signalled = false;
       w->mb_pending.store(false, std::memory_order_relaxed);
     }
-    for (auto& m : mb) {
-      auto it = w->conns.find(m.first);
-      if (it == w->conns.end()) continue;
-      Conn* c = it->second.get();
-      c->out += m.second;
-      c->waiting = false;
-      const bool was_bind = c->bind_waiting;
-      const uint64_t t_req = c->t_req_ns;
-      c->bind_waiting = false;
-      flush(w, c);   // may close the connection (Connection: close, a peer reset): c is gone then
-      if (was_bind) note_bind_wall(now_ns() - t_req);   // handed to the kernel: extender-side wall time
-      if (w->conns.count(m.first)) process(w, c);
-    }
+    for (auto& m : mb) deliver_reply(w, m.first, std::move(m.second));
   };
   while (!stop_.load(std::memory_order_acquire)) {
     const int64_t spin = busy_poll_ns_.load(std::memory_order_relaxed);
@@ -747,7 +763,9 @@ void Frontend::run(Worker* w) {
         continue;
       }
     }
-    const int n = epoll_wait(w->ep, evs, 128, polling ? 0 : 200);
+    BindIo* bio = w->bio.load(std::memory_order_acquire);
+    // with bind answers due, wake at least for the BindIo's deadline scan
+    const int n = epoll_wait(w->ep, evs, 128, polling ? 0 : bio && bio->inflight() ? 100 : 200);
     w->parked.store(false, std::memory_order_relaxed);
     const uint64_t t_batch = n > 0 ? now_ns() : 0;
     if (n > 0) {
@@ -787,6 +805,8 @@ void Frontend::run(Worker* w) {
         uint64_t v;
         (void)!read(w->efd, &v, sizeof(v));
         drain_mailbox();
+      } else if (!(tag >> 63) && (tag & kBioTag)) {
+        if (bio) bio->on_event(tag & ~kBioTag, evs[i].events);
       } else {
         PhaseTimer pt{&phase_max_ns[2]};
         const uint64_t cid = (tag & ~(1ull << 63)) >> 1;
@@ -820,7 +840,53 @@ void Frontend::run(Worker* w) {
       if (it != w->conns.end()) after_read(w, it->second.get(), false);
     }
     later.clear();
+    if (bio) {   // the binds this batch parsed go out now; answers that came in are replied
+      bio->pump();
+      drain_local(w);
+    }
     if (w->mb_pending.load(std::memory_order_acquire)) drain_mailbox();   // posted while awake
+  }
+  // stopping: the binds this worker has in flight finish (bounded), else the slow path takes
+  // them; their answers still reach kube-scheduler on the open connections
+  if (BindIo* bio = w->bio.load(std::memory_order_acquire)) {
+    const uint64_t until = now_ns() + 5'000'000'000ull;
+    while (bio->inflight() + bio->waiting() > 0 && now_ns() < until) {
+      const int n = epoll_wait(w->ep, evs, 128, 10);
+      for (int i = 0; i < n; ++i) {
+        const uint64_t tag = evs[i].data.u64;
+        if (!(tag >> 63) && (tag & kBioTag)) bio->on_event(tag & ~kBioTag, evs[i].events);
+      }
+      bio->pump();
+      drain_local(w);
+    }
+    bio->abandon("extender shutting down");
+    drain_local(w);
+  }
+  drain_mailbox();
+}
+
+void Frontend::deliver_reply(Worker* w, uint64_t conn, std::string&& bytes) {
+  auto it = w->conns.find(conn);
+  if (it == w->conns.end()) return;
+  Conn* c = it->second.get();
+  c->out += bytes;
+  c->waiting = false;
+  const bool was_bind = c->bind_waiting;
+  const uint64_t t_req = c->t_req_ns;
+  c->bind_waiting = false;
+  flush(w, c);   // may close the connection (Connection: close, a peer reset): c is gone then
+  if (was_bind) note_bind_wall(now_ns() - t_req);   // handed to the kernel: extender-side wall time
+  if (w->conns.count(conn)) process(w, c);
+}
+
+void Frontend::drain_local(Worker* w) {
+  // process() below may parse the next bind and queue more: swap first, loop until empty
+  thread_local std::vector<std::pair<uint64_t, std::string>> batch;
+  while (!w->local_replies.empty()) {
+    batch.clear();
+    batch.swap(w->local_replies);
+    for (auto& r : batch) deliver_reply(w, r.first, std::move(r.second));
+    if (BindIo* bio = w->bio.load(std::memory_order_relaxed)) bio->pump();
   }
 }
 
@@ -973,7 +1039,8 @@ void Frontend::defer(Worker* w, Conn* c, std::string method, std::string path, s
   if (method == "POST" && path == "/scheduler/bind" && serving()) {
     prepare_bind(body, &r);
     KubeWriter* kw = writer_.load(std::memory_order_acquire);
-    if (kw && r.bind.ok && (r.bind.rc == kOk || r.bind.rc == kOkExisting)) {
+    BindIo* bio = w->bio.load(std::memory_order_acquire);
+    if (kw && r.bind.ok && (r.bind.rc == kOk || r.bind.rc == kOkExisting) && (bio || !kw->inline_io())) {
       // the whole bind stays native: API writes and commit on the writer's threads
       BindJob j;
       j.id = r.id;
@@ -989,7 +1056,8 @@ void Frontend::defer(Worker* w, Conn* c, std::string method, std::string path, s
       c->bind_waiting = true;
       c->t_req_ns = c->t_in_ns ? c->t_in_ns : now_ns();
       c->t_in_ns = c->in.empty() ? 0 : now_ns();
-      kw->submit(std::move(j));
+      if (bio) bio->submit(std::move(j));   // sent by pump() after this batch of events
+      else kw->submit(std::move(j));
       return;
     }
   }

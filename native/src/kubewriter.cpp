@@ -426,9 +426,10 @@ int HttpConn::request(const char* method, const std::string& path, const std::st
 
 // ------------------------------------------------------------------------------ KubeWriter
 KubeWriter::KubeWriter(KubeTarget target, std::shared_ptr<Ledger> ledger, Respond respond, int threads, int retries,
-                       bool record_events, bool evented, bool label, double timeout_s)
+                       bool record_events, bool evented, bool label, double timeout_s, bool inline_io)
     : t_(std::move(target)), ledger_(std::move(ledger)), respond_(std::move(respond)), retries_(retries),
-      timeout_s_(timeout_s > 0 ? timeout_s : 30.0), events_(record_events), evented_(evented) {
+      timeout_s_(timeout_s > 0 ? timeout_s : 30.0), events_(record_events), evented_(evented || inline_io) {
+  inline_io_ = inline_io;
   label_ = label;
   ctx_ = make_ssl_ctx(t_);
   token_ = t_.token;
@@ -440,12 +441,16 @@ KubeWriter::KubeWriter(KubeTarget target, std::shared_ptr<Ledger> ledger, Respon
   if (threads < 1) threads = 1;
   if (evented_) {
     max_inflight_ = threads * kBatch;
-    efd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
-    if (efd_ < 0) throw std::runtime_error("KubeWriter: eventfd failed");
-    io_ = std::thread([this] {
-      pthread_setname_np(pthread_self(), "ngpu-wr-io");
-      io_loop();
-    });
+    if (inline_io_) {
+      io_done_.store(true);   // no io thread: the owners of the BindIo drivers hand off themselves
+    } else {
+      efd_ = eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
+      if (efd_ < 0) throw std::runtime_error("KubeWriter: eventfd failed");
+      io_ = std::thread([this] {
+        pthread_setname_np(pthread_self(), "ngpu-wr-io");
+        io_loop();
+      });
+    }
     // the slow path: retries with backoff, conflict checks, rollbacks (rare; blocking is fine)
     for (int i = 0; i < 2; ++i)
       threads_.emplace_back([this, i] {
@@ -488,6 +493,20 @@ void KubeWriter::stop() {
   }
   for (auto& t : threads_)
     if (t.joinable()) t.join();
+  std::deque<SlowJob> late;   // handed over while the slow threads were already leaving
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    slow_gone_ = true;
+    late.swap(slow_q_);
+  }
+  if (!late.empty()) {
+    HttpConn c(&t_, ctx_, 5), c2(&t_, ctx_, 5);
+    for (SlowJob& sj : late) {
+      if (sj.answered) finish_label(&c, sj.j, sj.patch, sj.sp, &sj.rp);
+      else finish(&c, &c2, sj.j, sj.patch, sj.binding, sj.sp, &sj.rp, sj.sb, &sj.rb);
+      stats.inflight.fetch_sub(1, std::memory_order_relaxed);
+    }
+  }
   std::deque<BindJob> left;
   {
     std::lock_guard<std::mutex> g(mu_);

@@ -492,6 +492,80 @@ static void apiserver_and_writers(int pods, bool evented) {
   std::printf("apiserver ok: %d pods bound by native writers, %d watch events\n", pods, events.load());
 }
 
+static std::string post(int port, const std::string& path, const std::string& body);
+
+// Inline bind writes (Frontend::set_kube_writer inline_io): client threads send filter + bind
+// over HTTP to a 2-worker front door whose workers drive the binds' API requests to the native
+// API server from their own epoll loops; every bind must be answered, bound and committed, and
+// the front door must stop cleanly with the writer.
+static void inline_binds(int pods) {
+  apisrv::Config cfg;
+  cfg.threads = 2;
+  apisrv::Server srv(cfg);
+  const int port = srv.port();
+  CHECK(http(port, "POST", "/api/v1/nodes", "{\"metadata\":{\"name\":\"n0\"}}").rfind("HTTP/1.1 201", 0) == 0);
+  std::vector<std::string> texts;
+  for (int i = 0; i < pods; ++i)
+    texts.push_back("{\"metadata\":{\"name\":\"q" + std::to_string(i) + "\",\"namespace\":\"s\",\"uid\":\"iq" +
+                    std::to_string(i) + "\"},\"spec\":{\"containers\":[{\"name\":\"c\",\"resources\":{\"limits\":"
+                    "{\"nano-gpu/gpu-percent\":\"1\"}}}]},\"status\":{\"phase\":\"Pending\"}}");
+  for (int c : srv.create_pods(texts)) CHECK(c == 201);
+  auto ledger = std::make_shared<Ledger>("", 8, 4096, true);
+  Device devs[8];
+  std::memset(devs, 0, sizeof(devs));
+  for (int i = 0; i < 8; ++i) {
+    devs[i].pct_total = 100;
+    devs[i].mib_total = 294896;
+    devs[i].gpu = static_cast<int16_t>(i);
+    devs[i].healthy = 1;
+    devs[i].xcds = 8;
+    devs[i].cus = 256;
+  }
+  Topology t;
+  std::memset(&t, 0, sizeof(t));
+  t.n_gpus = 8;
+  CHECK(ledger->upsert_node("n0", devs, 8, t) == 0);
+  {
+    Frontend fe(ledger, "127.0.0.1", 0, 2);
+    fe.set_busy_poll_us(20);
+    Options fo;
+    fe.set_options(fo, true);
+    KubeTarget tgt;
+    tgt.host = "127.0.0.1";
+    tgt.port = port;
+    tgt.tls = false;
+    fe.set_kube_writer(tgt, 2, 2, false, true, true, 30.0, true);
+    std::vector<std::thread> clients;
+    std::atomic<int> ok{0};
+    for (int c = 0; c < 4; ++c)
+      clients.emplace_back([&, c] {
+        for (int i = c; i < pods; i += 4) {
+          const std::string pod = texts[static_cast<size_t>(i)];
+          CHECK(post(fe.port(), "/scheduler/filter", "{\"Pod\":" + pod + ",\"NodeNames\":[\"n0\"]}")
+                    .rfind("HTTP/1.1 200", 0) == 0);
+          const std::string r = post(fe.port(), "/scheduler/bind",
+                                     "{\"PodName\":\"q" + std::to_string(i) + "\",\"PodNamespace\":\"s\",\"PodUID\":\"iq" +
+                                         std::to_string(i) + "\",\"Node\":\"n0\"}");
+          CHECK(r.rfind("HTTP/1.1 200", 0) == 0 && r.find("{\"Error\":\"\"}") != std::string::npos);
+          ok.fetch_add(1);
+        }
+      });
+    for (auto& c : clients) c.join();
+    CHECK(ok.load() == pods);
+    const KubeWriter* kw = fe.kube_writer();
+    CHECK(kw && kw->stats.ok.load() == static_cast<uint64_t>(pods));
+    fe.stop();
+  }
+  for (int i = 0; i < pods; ++i) {
+    const std::string r = http(port, "GET", "/api/v1/namespaces/s/pods/q" + std::to_string(i), "");
+    CHECK(r.find("\"nodeName\":\"n0\"") != std::string::npos);
+    PodRecord rec;
+    CHECK(ledger->lookup("iq" + std::to_string(i), &rec) && rec.state == kPodCommitted);
+  }
+  srv.stop();
+  std::printf("inline ok: %d binds written from the front-door workers\n", pods);
+}
+
 static std::string post(int port, const std::string& path, const std::string& body) {
   const int fd = socket(AF_INET, SOCK_STREAM, 0);
   sockaddr_in a{};
@@ -649,6 +723,7 @@ int main(int argc, char** argv) {
   unlink(path.c_str());
   apiserver_and_writers(std::max(50, iters / 20), true);    // one epoll writer thread
   apiserver_and_writers(std::max(50, iters / 20), false);   // blocking writer threads
+  inline_binds(std::max(100, iters / 10));
   relist_gap(std::max(200, iters / 4));
   handoff(std::max(500, iters));
   mailbox_wakeups(std::max(400, iters / 2));
