@@ -140,6 +140,9 @@ def parse_args():
                     help="time box of each GPU pair's peer-copy probe (s); the RCCL ring gets 4x")
     ap.add_argument("--probe-standin", default="",
                     help="tests: a stand-in peer probe (hang:SRC-DST never finishes that pair)")
+    ap.add_argument("--no-relocate", action="store_true",
+                    help="keep the rank on the L3 domain picked at start even when other tenants load it "
+                         "(by default, after the warm-up, a busy domain is left for a quieter one)")
     ap.add_argument("--inproc-driver", action="store_true",
                     help="run the kube-scheduler stand-in inside the extender process (default: own process)")
     return ap.parse_args()
@@ -808,6 +811,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         if d.rank == 0:
             apisrv = api_proc
             url = apisrv.start(args.apiserver_threads or min(16, max(4, d.world)), args.api_rtt_ms / 1e3)
+            if getattr(args, "_placement", None):
+                args._placement["apiserver"] = list(apisrv.cpus)
             apisrv.add_nodes(nodes)
         url = d.bcast_obj(url)
         from nanogpu.k8s.client import KubeClient, KubeConfig
@@ -1054,6 +1059,19 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         warm_ids, timed_ids = [10_000 + w for w in range(args.warmup)], list(range(args.steps))
     for k, w in enumerate(warm_ids):
         await one_step(w, False, warm_ids[k + 1] if k + 1 < len(warm_ids) else None)
+    moved = None
+    if d.world == 1 and getattr(args, "_placement", None) and not getattr(args, "no_relocate", False):
+        # the job is idle here: if other tenants have moved onto this domain (cores or SMT
+        # siblings) since it was picked, move the extender and its stand-in to a quieter one
+        from nanogpu import affinity
+
+        pl = args._placement
+        to = affinity.quieter_domain(pl["cpus"], pl["numa"], exclude=pl.get("apiserver") or [])
+        if to is not None:
+            affinity.relocate(pl["pids"], to)
+            moved = {"from": pl["cpus"], "to": to}
+            pl["cpus"] = to
+    results["relocated"] = moved
     rt.tracer.buf.clear()
     await barrier()
     d.sync()
@@ -1225,6 +1243,7 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
         "cpu_layout": {"rank0": affinity.cpu_layout(cpus),
                        "apiserver": affinity.cpu_layout(api_proc.cpus) if api_proc is not None else None},
         "cpu_busy_pct_rank0": res.get("cpu_busy_pct"),
+        "relocated_rank0": res.get("relocated"),
         "pods_per_s_first_filter_to_last_bind": out["value_burst_window"],
         # POST /scheduler/bind wall time as kube-scheduler's stand-in sees it (request written ->
         # reply read), every bind of the timed steps on all ranks
@@ -1329,6 +1348,11 @@ def main() -> int:
     if int(os.environ.get("RANK", "0")) == 0 and not args.inproc_driver:
         # the shared API server's process, like the stand-in's: before anything touches the GPU
         api_proc = ApiServerProc(avoid=rank_cpus, near=rank0_numa)
+    args._placement = None
+    if cpus and int(os.environ.get("LOCAL_WORLD_SIZE", "1")) == 1:
+        args._placement = {"cpus": list(cpus), "numa": rank0_numa,
+                           "pids": [os.getpid()] + ([drv_proc.pid] if drv_proc is not None else []),
+                           "apiserver": None}
     d = Dist(args.gpus)
     d.init(use_gpu=not args.no_gpu)
     # the deployment that exists: one active kube-scheduler in front of every extender worker
@@ -1407,7 +1431,8 @@ def main() -> int:
             api_proc.close()
     out = summarize(d, args, res)
     if d.rank == 0:
-        line, diag = headline_line(d, args, res, out, cpus, api_proc, gpu_info, topo,
+        final_cpus = args._placement["cpus"] if getattr(args, "_placement", None) else cpus
+        line, diag = headline_line(d, args, res, out, final_cpus, api_proc, gpu_info, topo,
                                    variant, one_v, steady_v, nodes_v, inproc_v)
         # the driver keeps the last 8 KB of stdout: ONE compact line (< 4 KB) with the
         # headline keys last; the per-step diagnostics go to --json-out only

@@ -10,7 +10,8 @@ pods/s, two CCDs 23.1k, one CCD 25.3k.
 `pick_cpus()` returns the physical cores (first SMT sibling) of one L3 domain:
   * on the NUMA node of the GPU this process is paired with (the node agent / bench rank),
   * distinct per local rank when several ranks share a node,
-  * otherwise the least busy domain (a shared host), skipping the one serving CPU 0.
+  * otherwise the least busy domain (a shared host), counting the SMT siblings' load with the
+    cores' own (another tenant on a sibling slows the core), skipping the one serving CPU 0.
 Everything is read from sysfs / procfs; nothing here touches the GPU, so it can run before
 worker processes are spawned.
 """
@@ -99,8 +100,9 @@ def _busy(cpus: list[int], window_s: float) -> dict[int, float]:
     return busy_between(a, cpu_snapshot(), cpus)
 
 
-def smt_siblings(cpus: list[int], root: Path = SYS_CPU) -> list[int]:
+def smt_siblings(cpus: list[int], root: Path | None = None) -> list[int]:
     """The other hardware threads of the cores `cpus` sit on (not in `cpus` themselves)."""
+    root = root or SYS_CPU
     mine = set(cpus)
     out: set[int] = set()
     for c in cpus:
@@ -108,11 +110,12 @@ def smt_siblings(cpus: list[int], root: Path = SYS_CPU) -> list[int]:
     return sorted(out - mine)
 
 
-def cpu_layout(cpus: list[int], root: Path = SYS_CPU) -> dict | None:
+def cpu_layout(cpus: list[int], root: Path | None = None) -> dict | None:
     """Physical-core / SMT layout of a pinned CPU set: the cores, their sibling threads,
     the L3 domains and NUMA nodes they span."""
     if not cpus:
         return None
+    root = root or SYS_CPU
     cores = {tuple(_parse_list(_read(root / f"cpu{c}" / "topology" / "thread_siblings_list")) or [c])
              for c in cpus}
     return {"cpus": len(cpus), "physical_cores": len(cores), "smt_siblings": smt_siblings(cpus, root),
@@ -131,8 +134,16 @@ def busy_report(a: dict, b: dict, groups: dict[str, list[int]]) -> dict[str, flo
     return out
 
 
+def _domain_busy(dom: list[int], load: dict[int, float]) -> float:
+    """A domain's load for placement: its cores and their SMT siblings alike. Another tenant
+    on a sibling takes half of the core's issue slots; on the MI355X box runs whose siblings
+    were 25-40 % busy lost 20-35 % of their pods/s (profiles/variance_r04.md)."""
+    cpus = list(dom) + smt_siblings(dom)
+    return sum(load.get(c, 0.0) for c in cpus) / len(cpus)
+
+
 def pick_cpus(numa: int = -1, local_rank: int = 0, local_ranks_numa: list[int] | None = None,
-              window_s: float = 0.1) -> list[int]:
+              window_s: float = 0.25) -> list[int]:
     """Cores of one L3 domain for this process (see module docstring); [] when the host gives
     no usable topology (then leave the affinity alone)."""
     doms = l3_domains()
@@ -147,11 +158,11 @@ def pick_cpus(numa: int = -1, local_rank: int = 0, local_ranks_numa: list[int] |
         # several ranks on this node: the k-th rank of a NUMA node takes its k-th domain
         k = sum(1 for r in range(local_rank) if local_ranks_numa[r] == numa)
         return doms[k % len(doms)]
-    load = _busy([c for d in doms for c in d], window_s)
-    return min(doms, key=lambda d: (sum(load.get(c, 0.0) for c in d) / len(d), d[0]))
+    load = _busy([c for d in doms for c in list(d) + smt_siblings(d)], window_s)
+    return min(doms, key=lambda d: (round(_domain_busy(d, load), 3), d[0]))
 
 
-def pick_cpus_avoiding(taken: list[int], near: int = -1, window_s: float = 0.1) -> list[int]:
+def pick_cpus_avoiding(taken: list[int], near: int = -1, window_s: float = 0.25) -> list[int]:
     """An L3 domain for a helper process (the bench's shared API server) that shares no core
     with `taken` (the ranks' domains, which may not be busy yet when the helper starts):
     a domain on NUMA node `near` that is less than half busy (every request and watch event
@@ -167,13 +178,62 @@ def pick_cpus_avoiding(taken: list[int], near: int = -1, window_s: float = 0.1) 
         free = [d for d in free if 0 not in d] or free   # CPU 0 carries housekeeping work
     if not free:
         return pick_cpus()
-    load = _busy([c for d in free for c in d], window_s)
+    load = _busy([c for d in free for c in list(d) + smt_siblings(d)], window_s)
+
     def key(d):
-        busy = sum(load.get(c, 0.0) for c in d) / len(d)
+        busy = _domain_busy(d, load)
         far = near >= 0 and numa_of_cpu(d[0]) != near
         return (busy >= 0.5, far, round(busy, 1), d[0])
 
     return min(free, key=key)
+
+
+def domain_of(cpus: list[int]) -> list[int] | None:
+    """The L3 domain (physical cores) `cpus` belong to, when they are one domain's cores."""
+    for d in l3_domains():
+        if set(cpus) <= set(d):
+            return d
+    return None
+
+
+def quieter_domain(current: list[int], numa: int = -1, exclude: list[int] | None = None,
+                   window_s: float = 0.2, threshold: float = 0.15) -> list[int] | None:
+    """While this process group is idle (all of its CPU load is someone else's): when the
+    domain `current` sits on is at least `threshold` busy with other tenants' work, cores and
+    SMT siblings alike, the least busy other domain on NUMA node `numa` (none of `exclude`)
+    that is under half as busy; else None. Moving away from contention, never holding CPUs."""
+    doms = l3_domains()
+    if numa >= 0:
+        doms = [d for d in doms if numa_of_cpu(d[0]) == numa] or doms
+    cur = next((d for d in doms if set(current) <= set(d)), None)
+    if cur is None:
+        return None
+    avoid = set(exclude or [])
+    others = [d for d in doms if d is not cur and 0 not in d and not avoid.intersection(d)]
+    load = _busy([c for d in [cur] + others for c in list(d) + smt_siblings(d)], window_s)
+    here = _domain_busy(cur, load)
+    if here < threshold or not others:
+        return None
+    best = min(others, key=lambda d: (_domain_busy(d, load), d[0]))
+    return best if _domain_busy(best, load) < here / 2 else None
+
+
+def relocate(pids: list[int], cpus: list[int]) -> int:
+    """Pins every thread of the processes `pids` to `cpus` (threads of a running process keep
+    their own masks: each is set). Returns the threads moved."""
+    n = 0
+    for pid in pids:
+        try:
+            tids = os.listdir(f"/proc/{pid}/task")
+        except OSError:
+            continue
+        for tid in tids:
+            try:
+                os.sched_setaffinity(int(tid), cpus)
+                n += 1
+            except OSError:
+                pass
+    return n
 
 
 def apply(cpus: list[int]) -> bool:

@@ -55,7 +55,7 @@ def test_single_rank_takes_the_least_busy_domain(tmp_path, monkeypatch):
     monkeypatch.setattr(A, "numa_of_cpu", lambda cpu, root=tmp_path: real_numa(cpu, root))
     busy = {c: 0.9 for c in range(24)}
     busy.update({c: 0.1 for c in (8, 9, 10, 11)})
-    monkeypatch.setattr(A, "_busy", lambda cpus, w: {c: busy[c] for c in cpus})
+    monkeypatch.setattr(A, "_busy", lambda cpus, w: {c: busy.get(c, 0.0) for c in cpus})
     assert A.pick_cpus(0) == [8, 9, 10, 11]
     assert A.pick_cpus(1) in ([12, 13, 14, 15], [16, 17, 18, 19], [20, 21, 22, 23])
 
@@ -87,9 +87,44 @@ def test_bench_api_server_stays_on_rank0s_socket_unless_it_is_busy(tmp_path, mon
     monkeypatch.setattr(A, "numa_of_cpu", lambda cpu, root=tmp_path: real_numa(cpu, root))
     busy = {c: 0.0 for c in range(24)}
     busy.update({c: 0.2 for c in (8, 9, 10, 11)})          # socket 0's free domain: lightly used
-    monkeypatch.setattr(A, "_busy", lambda cpus, w: {c: busy[c] for c in cpus})
+    monkeypatch.setattr(A, "_busy", lambda cpus, w: {c: busy.get(c, 0.0) for c in cpus})
     taken = A.pick_cpus(0, 0, [0])                          # rank 0 on socket 0
     assert A.numa_of_cpu(taken[0]) == 0
     assert A.pick_cpus_avoiding(taken, near=0) == [8, 9, 10, 11]
     busy.update({c: 0.7 for c in (8, 9, 10, 11)})           # now mostly busy: go far
     assert A.numa_of_cpu(A.pick_cpus_avoiding(taken, near=0)[0]) == 1
+
+
+def test_a_domain_whose_smt_siblings_are_busy_loses(tmp_path, monkeypatch):
+    """Two idle domains on the GPU's socket; another tenant keeps the SMT siblings of one of
+    them busy: the rank takes the other (the siblings' load counts with the cores')."""
+    allowed = make_tree(tmp_path)
+    monkeypatch.setattr(A, "SYS_CPU", tmp_path)
+    real_l3, real_numa = A.l3_domains, A.numa_of_cpu
+    monkeypatch.setattr(A.os, "sched_getaffinity", lambda pid: allowed)
+    monkeypatch.setattr(A, "l3_domains", lambda allowed=None, root=tmp_path: real_l3(allowed, root))
+    monkeypatch.setattr(A, "numa_of_cpu", lambda cpu, root=tmp_path: real_numa(cpu, root))
+    busy = {c: 0.0 for c in range(48)}
+    busy.update({c + 24: 0.8 for c in (4, 5, 6, 7)})       # siblings of domain [4..7]
+    monkeypatch.setattr(A, "_busy", lambda cpus, w: {c: busy.get(c, 0.0) for c in cpus})
+    assert A.smt_siblings([4, 5]) == [28, 29]
+    assert A.pick_cpus(0) == [8, 9, 10, 11]
+    layout = A.cpu_layout([8, 9, 10, 11])
+    assert layout["physical_cores"] == 4 and layout["smt_siblings"] == [32, 33, 34, 35] and not layout["whole_cores"]
+
+
+def test_an_idle_job_leaves_a_domain_other_tenants_moved_onto(tmp_path, monkeypatch):
+    allowed = make_tree(tmp_path)
+    monkeypatch.setattr(A, "SYS_CPU", tmp_path)
+    real_l3, real_numa = A.l3_domains, A.numa_of_cpu
+    monkeypatch.setattr(A.os, "sched_getaffinity", lambda pid: allowed)
+    monkeypatch.setattr(A, "l3_domains", lambda allowed=None, root=tmp_path: real_l3(allowed, root))
+    monkeypatch.setattr(A, "numa_of_cpu", lambda cpu, root=tmp_path: real_numa(cpu, root))
+    busy = {c: 0.0 for c in range(48)}
+    monkeypatch.setattr(A, "_busy", lambda cpus, w: {c: busy.get(c, 0.0) for c in cpus})
+    assert A.quieter_domain([4, 5, 6, 7], 0) is None                # nobody else there: stay
+    busy.update({c + 24: 0.6 for c in (4, 5, 6, 7)})                 # a tenant on the siblings
+    assert A.quieter_domain([4, 5, 6, 7], 0) == [8, 9, 10, 11]
+    assert A.quieter_domain([4, 5, 6, 7], 0, exclude=[8]) is None    # the API server's domain: not that one
+    busy.update({c: 0.5 for c in (8, 9, 10, 11)})                    # the alternative is no better
+    assert A.quieter_domain([4, 5, 6, 7], 0) is None
