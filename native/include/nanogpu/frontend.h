@@ -100,6 +100,9 @@ class Frontend {
   // After any event a worker keeps polling (epoll timeout 0) for this long before it
   // blocks again: trades a little CPU during bursts for no wake-up latency per request.
   void set_busy_poll_us(int us) { busy_poll_ns_.store(static_cast<int64_t>(us) * 1000, std::memory_order_relaxed); }
+  // Binds read in the same batch as a filter / priorities request are reserved first (placement
+  // quality: the next pod's filter sees the pod just bound) instead of after (cycle latency).
+  void set_bind_first(bool on) { bind_first_.store(on, std::memory_order_relaxed); }
   // Drains requests waiting for Python (non-blocking).
   std::vector<PyRequest> take();
   // Completes request `id` (any thread). Unknown ids (connection gone) are dropped.
@@ -170,6 +173,7 @@ class Frontend {
   std::atomic<bool> stop_{false};       // the workers leave their loops
   std::atomic<bool> serving_{true};
   std::atomic<int64_t> busy_poll_ns_{0};
+  std::atomic<bool> bind_first_{false};
   std::vector<std::unique_ptr<Worker>> workers_;
 
   mutable std::mutex opt_mu_;

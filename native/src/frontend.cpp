@@ -824,9 +824,13 @@ void Frontend::run(Worker* w) {
         if (evs[i].events & (EPOLLIN | EPOLLRDHUP)) {
           bool eof = false;
           if (!read_in(w, c, &eof)) continue;
-          // scheduling-cycle verbs first: kube-scheduler's next pod waits on filter /
-          // priorities, while a bind's reply only ends an asynchronous binding goroutine
-          if (!eof && c->in.compare(0, 20, "POST /scheduler/bind") == 0) {
+          // Which verb of a batch goes first. Cycle first: kube-scheduler's next pod waits on
+          // filter / priorities, while a bind's reply only ends an asynchronous binding
+          // goroutine. Binds first (set_bind_first): the bind of pod i is reserved before
+          // pod i+1's filter reads the ledger, so a pod kube-scheduler placed off its
+          // nomination (or never nominated) is not invisible to the next pod's placement.
+          const bool is_bind = c->in.compare(0, 20, "POST /scheduler/bind") == 0;
+          if (!eof && is_bind != bind_first_.load(std::memory_order_relaxed)) {
             later.push_back(cid);
             continue;
           }
