@@ -54,6 +54,7 @@ class Config:
     # (the binding carries the annotations; this project's agent selects pods by node)
     assume_label: bool = True
     bind_first: bool = False                    # front door: a batch's binds before its filters
+    spin_nap: bool = False                      # front door: sleep the busy-poll window, not poll it
     api_write_timeout_s: float = 30.0           # native bind writer: an API answer due within this
     reservation_ttl_s: float = 60.0
     nominate: bool = True              # priorities nominate the top node (Ledger::nominate)
@@ -209,6 +210,7 @@ class Runtime:
                 self.native.fe.set_serving(True)   # the ledger's shared flag gates it as well
                 self.native.fe.set_busy_poll_us(self.cfg.busy_poll_us)
                 self.native.fe.set_bind_first(self.cfg.bind_first)
+                self.native.fe.set_spin_nap(self.cfg.spin_nap)
                 api_cfg = getattr(self.api, "config", None)
                 if self.cfg.native_bind_writes and not self.cfg.verify_pod_on_bind and api_cfg is not None:
                     ext = self.extender

@@ -103,6 +103,8 @@ class Frontend {
   // Binds read in the same batch as a filter / priorities request are reserved first (placement
   // quality: the next pod's filter sees the pod just bound) instead of after (cycle latency).
   void set_bind_first(bool on) { bind_first_.store(on, std::memory_order_relaxed); }
+  // The busy-poll window is slept (epoll_pwait2 with a microsecond timeout) instead of polled.
+  void set_spin_nap(bool on) { spin_nap_.store(on, std::memory_order_relaxed); }
   // Drains requests waiting for Python (non-blocking).
   std::vector<PyRequest> take();
   // Completes request `id` (any thread). Unknown ids (connection gone) are dropped.
@@ -174,6 +176,7 @@ class Frontend {
   std::atomic<bool> serving_{true};
   std::atomic<int64_t> busy_poll_ns_{0};
   std::atomic<bool> bind_first_{false};
+  std::atomic<bool> spin_nap_{false};
   std::vector<std::unique_ptr<Worker>> workers_;
 
   mutable std::mutex opt_mu_;

@@ -770,6 +770,7 @@ PYBIND11_MODULE(_native, m) {
       .def("set_serving", &Frontend::set_serving)
       .def("set_busy_poll_us", &Frontend::set_busy_poll_us)
       .def("set_bind_first", &Frontend::set_bind_first)
+      .def("set_spin_nap", &Frontend::set_spin_nap)
       .def(
           "set_kube_writer",
           [](Frontend& f, const std::string& host, int port, bool tls, const std::string& token,

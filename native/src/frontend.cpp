@@ -754,8 +754,14 @@ void Frontend::run(Worker* w) {
     const int64_t spin = busy_poll_ns_.load(std::memory_order_relaxed);
     const bool hot = __builtin_popcount(gaps & 0xffffu) >= 8;
     const uint64_t since = w->cycle_reply_ns;
-    const bool polling = spin > 0 && hot && since && now_ns() - since < static_cast<uint64_t>(spin);
-    if (!polling) {
+    const uint64_t t_now = now_ns();
+    const bool polling = spin > 0 && hot && since && t_now - since < static_cast<uint64_t>(spin);
+    // nap: the spin window is slept in the kernel (epoll_pwait2 with the window's remaining
+    // microseconds) instead of polled: a request that arrives wakes the worker, and idle
+    // periods that short keep the core in its shallowest idle state (fast exit), while the
+    // window costs no CPU time
+    const bool nap = polling && spin_nap_.load(std::memory_order_relaxed);
+    if (!polling || nap) {
       w->parked.store(true, std::memory_order_seq_cst);
       if (w->mb_pending.load(std::memory_order_seq_cst)) {   // posted before we parked
         w->parked.store(false, std::memory_order_relaxed);
@@ -764,8 +770,14 @@ void Frontend::run(Worker* w) {
       }
     }
     BindIo* bio = w->bio.load(std::memory_order_acquire);
-    // with bind answers due, wake at least for the BindIo's deadline scan
-    const int n = epoll_wait(w->ep, evs, 128, polling ? 0 : bio && bio->inflight() ? 100 : 200);
+    int n;
+    if (nap) {
+      const timespec ts{0, static_cast<long>(static_cast<uint64_t>(spin) - (t_now - since))};
+      n = epoll_pwait2(w->ep, evs, 128, &ts, nullptr);
+    } else {
+      // with bind answers due, wake at least for the BindIo's deadline scan
+      n = epoll_wait(w->ep, evs, 128, polling ? 0 : bio && bio->inflight() ? 100 : 200);
+    }
     w->parked.store(false, std::memory_order_relaxed);
     const uint64_t t_batch = n > 0 ? now_ns() : 0;
     if (n > 0) {
