@@ -176,7 +176,8 @@ def ledger_view(demand: Demand) -> tuple[Demand, list[int] | None]:
     64 devices' worth of them). A pod within that is passed as is (None: entries ARE containers,
     so compat placements stay bit-exact with the reference). A larger pod keeps only its
     GPU-requesting containers, which is placement-neutral in native mode (zero-demand
-    containers take no device and sort last); more than 64 of those raises."""
+    containers take no device and sort last); more than 64 of those raises (the caller places
+    such a pod with `wide_place` and accounts it with `fold_plan`)."""
     if len(demand) <= LEDGER_MAX_CONTAINERS:
         return demand, None
     idx = [i for i, d in enumerate(demand) if d[0] > 0 or d[1] > 0]
@@ -184,6 +185,84 @@ def ledger_view(demand: Demand) -> tuple[Demand, list[int] | None]:
         raise TooManyGpuContainers(f"pod requests GPUs in {len(idx)} containers; at most "
                                    f"{LEDGER_MAX_CONTAINERS} per pod are supported")
     return [demand[i] for i in idx], idx
+
+
+def gpu_container_count(demand: Demand) -> int:
+    return sum(1 for d in demand if d[0] > 0 or d[1] > 0)
+
+
+def is_wide(demand: Demand) -> bool:
+    """More GPU-requesting containers than one ledger record holds (wide_place / fold_plan)."""
+    return len(demand) > LEDGER_MAX_CONTAINERS and gpu_container_count(demand) > LEDGER_MAX_CONTAINERS
+
+
+def wide_place(devices: list[dict], demand: Demand, spread: bool = False) -> Plan | None:
+    """Placement of a pod with more GPU containers than a ledger record holds (the reference
+    places any count: allocate.go:54-62, rater.go:74-110). Containers largest first, as the
+    reference's Choose does; a share goes to the fitting device with the least free percent
+    (binpack: best fit) or the most (spread), HBM checked per memory pool; a k x 100 % container
+    takes k devices with nothing used. Returns one entry per container ([-1]: no GPU), or None
+    when the pod does not fit. The result is accounted through `fold_plan`."""
+    free = [int(d["pct_free"]) if d.get("healthy", True) else -1 for d in devices]
+    total = [int(d["pct_total"]) for d in devices]
+    pool_of = [int(d.get("pool", -1)) if int(d.get("pool", -1)) >= 0 else -(k + 1) for k, d in enumerate(devices)]
+    mib: dict[int, int] = {}
+    for k, d in enumerate(devices):
+        mib[pool_of[k]] = int(d["mib_free"]) if int(d.get("mib_total", 0)) > 0 else 1 << 62
+    plan: Plan = [[-1] for _ in demand]
+    order = sorted(range(len(demand)), key=lambda i: (demand[i][0], demand[i][1]), reverse=True)
+    for i in order:
+        pct, m = int(demand[i][0]), int(demand[i][1])
+        if pct <= 0 and m <= 0:
+            continue
+        if pct >= 100 and pct % 100 == 0:
+            k = pct // 100
+            cand = [j for j in range(len(devices)) if free[j] == total[j] > 0]
+            if len(cand) < k:
+                return None
+            take = cand[:k]
+            for j in take:
+                free[j] = 0
+                mib[pool_of[j]] = 0 if pool_of[j] < 0 else mib[pool_of[j]]
+            plan[i] = take
+            continue
+        fit = [j for j in range(len(devices)) if free[j] >= pct and mib[pool_of[j]] >= m]
+        if not fit:
+            return None
+        j = (max if spread else min)(fit, key=lambda x: (free[x], -x if spread else x))
+        free[j] -= pct
+        mib[pool_of[j]] -= m
+        if free[j] == 0 and pool_of[j] < 0:
+            mib[pool_of[j]] = 0   # folded, a device filled to 100 % is held whole (fold_plan)
+        plan[i] = [j]
+    return plan
+
+
+def fold_plan(demand: Demand, plan: Plan) -> tuple[Demand, Plan]:
+    """A wide pod as one ledger record: one entry per device it uses, holding the sum of the
+    shares placed there (a device its containers fill to 100 % is held whole, HBM included),
+    so any container count fits the record's 64 entries (a node has at most 64 devices)."""
+    per: dict[int, list[int]] = {}
+    for k, idx in enumerate(plan):
+        pct, m = int(demand[k][0]), int(demand[k][1])
+        flags = getattr(demand[k], "flags", 0)
+        if pct <= 0 and m <= 0:
+            continue
+        whole = pct >= 100 and pct % 100 == 0
+        for j in idx:
+            if j < 0:
+                continue
+            acc = per.setdefault(j, [0, 0, 0])
+            acc[0] += 100 if whole else pct
+            acc[1] += 0 if whole else m
+            acc[2] |= flags
+    folded: Demand = []
+    fplan: Plan = []
+    for j in sorted(per):
+        pct, m, flags = per[j]
+        folded.append(Req(min(pct, 100), m, flags) if flags else (min(pct, 100), m))
+        fplan.append([j])
+    return folded, fplan
 
 
 def full_plan(plan: Plan, idx: list[int] | None, n_containers: int) -> Plan:

@@ -74,6 +74,7 @@ class ClusterState:
         self._pending_removal: dict[str, int] = {}   # deleted nodes whose slot still holds shares
         self._released_cap = 65536
         self._reaccount_wait: dict[str, dict] = {}   # uid -> pod waiting for its partner (reaccount)
+        self._wide_plans: dict[str, list] = {}        # uid -> per-container plan of a wide pod
         self.set_policy(policy, compat=compat, load_aware=load_aware, topo_weight=topo_weight, seed=seed,
                         request_sizes=request_sizes or [], learn_sizes=learn_sizes)
 
@@ -233,10 +234,10 @@ class ClusterState:
         """Reference Dealer.Assume (dealer.go:89-136) + Predicate.Handler (predicate.go:19-41)."""
         if self.nominate:
             self._drop_own_nomination(pod)
-        try:
-            demand, _ = pu.ledger_view(self.pod_demand(pod))
-        except pu.TooManyGpuContainers as e:
-            return [], {name: f"nano-gpu: {e}" for name in node_names}
+        full = self.pod_demand(pod)
+        if pu.is_wide(full):
+            return self._wide_filter(full, node_names)
+        demand, _ = pu.ledger_view(full)
         ids = self.node_ids(node_names)
         rcs = self.ledger.filter(ids, demand, self.options)
         ok, failed = [], {}
@@ -255,10 +256,10 @@ class ClusterState:
         """Reference Dealer.Score (dealer.go:138-153); ScoreMin (0) for unknown/unfit nodes."""
         if self.nominate:
             self._drop_own_nomination(pod)
-        try:
-            demand, _ = pu.ledger_view(self.pod_demand(pod))
-        except pu.TooManyGpuContainers:
-            return [0] * len(node_names)             # filter already failed every node
+        full = self.pod_demand(pod)
+        if pu.is_wide(full):
+            return self._wide_scores(full, node_names)
+        demand, _ = pu.ledger_view(full)
         ids = self.node_ids(node_names)
         scores = self.ledger.score(ids, demand, self.options)
         if self.nominate and scores:
@@ -317,10 +318,9 @@ class ClusterState:
             raise SchedulingError(f"node {node_name} not found")
         uid = pu.pod_uid(pod)
         full = self.pod_demand(pod)
-        try:
-            demand, idx = pu.ledger_view(full)
-        except pu.TooManyGpuContainers as e:
-            raise SchedulingError(str(e)) from None
+        if pu.is_wide(full):
+            return self._wide_reserve(e, uid, full)
+        demand, idx = pu.ledger_view(full)
         rc, plan = self.ledger.reserve(e.id, uid, demand, self.options)
         if rc not in (N.OK, N.OK_EXISTING):
             raise self.reserve_error(demand, node_name, rc)
@@ -328,6 +328,65 @@ class ClusterState:
         if owner:                     # what the streaming-owner learner reads (learn_stream_owners)
             self.ledger.set_pod_owner(uid, owner)
         return pu.full_plan(plan, idx, len(full)), rc == N.OK
+
+    # ------------------------------------------------------------------ wide pods
+    # More GPU containers than a ledger record holds (pu.is_wide): placed in Python on the
+    # node's snapshot (pu.wide_place), accounted as one record folded per device (pu.fold_plan).
+    # The native front door hands such pods to this path (its demand parser stops at 64).
+    def _wide_plan(self, nid: int, full) -> list | None:
+        if nid < 0:
+            return None
+        snap = self.ledger.snapshot(nid)
+        return pu.wide_place(snap["devices"], full, spread=self.policy == "spread")
+
+    def _wide_filter(self, full, node_names: list[str]) -> tuple[list[str], dict[str, str]]:
+        ok, failed = [], {}
+        n = pu.gpu_container_count(full)
+        for name, nid in zip(node_names, self.node_ids(node_names)):
+            if nid < 0:
+                failed[name] = f"nano gpu scheduler get node failed: node {name} not found"
+            elif self._wide_plan(nid, full) is None:
+                failed[name] = f"can't allocate {n} GPU containers on node {name}: {N.err_str(N.ERR_NO_FIT)}"
+            else:
+                ok.append(name)
+        return ok, failed
+
+    def _wide_scores(self, full, node_names: list[str]) -> list[int]:
+        """Utilisation after the placement (binpack: fuller is better; spread: emptier)."""
+        out = []
+        for nid in self.node_ids(node_names):
+            plan = self._wide_plan(nid, full)
+            if plan is None:
+                out.append(0)
+                continue
+            devs = self.ledger.snapshot(nid)["devices"]
+            total = sum(int(d["pct_total"]) for d in devs) or 1
+            used = total - sum(int(d["pct_free"]) for d in devs)
+            folded, _ = pu.fold_plan(full, plan)
+            u = int(100 * (used + sum(p for p, _ in folded)) / total)
+            out.append(100 - u if self.policy == "spread" else u)
+        if self.score_normalize and out:
+            out = self._normalize(out)
+        return out
+
+    def _wide_reserve(self, e, uid: str, full) -> tuple[list[list[int]], bool]:
+        rec = self.ledger.lookup(uid)
+        if rec is not None and uid in self._wide_plans:
+            if rec["node"] != e.id:
+                raise SchedulingError(f"pod {uid} is already placed on another node")
+            return self._wide_plans[uid], False        # a retried bind
+        plan = self._wide_plan(e.id, full)
+        if plan is None:
+            raise SchedulingError(f"assume {pu.gpu_container_count(full)} GPU containers on {e.name} failed: "
+                                  f"{N.err_str(N.ERR_NO_FIT)}")
+        folded, fplan = pu.fold_plan(full, plan)
+        rc = self.ledger.allocate_plan(e.id, uid, folded, fplan, False)
+        if rc != N.OK:
+            raise self.reserve_error(folded, e.name, rc)
+        self._wide_plans[uid] = plan
+        if len(self._wide_plans) > 4096:
+            self._wide_plans.pop(next(iter(self._wide_plans)))
+        return plan, True
 
     def reserve_error(self, demand, node_name: str, rc: int) -> SchedulingError:
         return SchedulingError(f"assume {self._demand_str(demand)} on {node_name} failed: {N.err_str(rc)}")
@@ -350,16 +409,17 @@ class ClusterState:
         if e is None:
             log.warning("allocate %s: node %s unknown", pu.pod_key(pod), node)
             return False
-        try:
-            demand, idx = pu.ledger_view(self.pod_demand(pod))
-        except pu.TooManyGpuContainers as err:
-            log.warning("allocate %s: %s", pu.pod_key(pod), err)
+        full = self.pod_demand(pod)
+        if len(plan) != len(full):
+            log.warning("allocate %s: %d assignments for %d containers", pu.pod_key(pod), len(plan), len(full))
             return False
-        if len(plan) != len(self.pod_demand(pod)):
-            log.warning("allocate %s: %d assignments for %d containers", pu.pod_key(pod), len(plan),
-                        len(self.pod_demand(pod)))
-            return False
-        rc = self.ledger.allocate_plan(e.id, pu.pod_uid(pod), demand, pu.ledger_plan(plan, idx), True)
+        if pu.is_wide(full):
+            demand, lplan = pu.fold_plan(full, plan)
+            self._wide_plans[pu.pod_uid(pod)] = plan
+        else:
+            demand, idx = pu.ledger_view(full)
+            lplan = pu.ledger_plan(plan, idx)
+        rc = self.ledger.allocate_plan(e.id, pu.pod_uid(pod), demand, lplan, True)
         if rc != N.OK:
             if not quiet:
                 log.warning("allocate %s on %s failed: %s", pu.pod_key(pod), node, N.err_str(rc))
@@ -384,11 +444,13 @@ class ClusterState:
             return self._retry_reaccount()
         if rec is None or plan is None or rec["state"] != "committed":
             return False
-        try:
-            _, idx = pu.ledger_view(self.pod_demand(pod))
-        except pu.TooManyGpuContainers:
-            return False
-        if [list(x) for x in pu.ledger_plan(plan, idx)] == [list(x) for x in rec["plan"]]:
+        full = self.pod_demand(pod)
+        if pu.is_wide(full):
+            _, lplan = pu.fold_plan(full, plan) if len(plan) == len(full) else (None, None)
+        else:
+            _, idx = pu.ledger_view(full)
+            lplan = pu.ledger_plan(plan, idx)
+        if lplan is None or [list(x) for x in lplan] == [list(x) for x in rec["plan"]]:
             return False
         if self.ledger.drop_committed(uid) != N.OK:
             return False

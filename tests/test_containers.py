@@ -14,6 +14,7 @@ from nanogpu.k8s import podutil as pu
 
 from nanogpu.app import Config, Runtime
 from nanogpu.k8s.fake_apiserver import FakeKubeStore, InProcKube
+from nanogpu.topology.model import synthetic_mi355x
 from test_control_plane import annotated, runtime, wait_for
 from test_control_plane import node as mknode
 from test_frontend import _dumps, _http
@@ -73,7 +74,12 @@ def test_forty_container_pod_schedules_through_both_front_doors():
         asyncio.run(main())
 
 
-def test_too_many_gpu_containers_is_a_failed_node_not_an_error():
+def test_pods_with_more_gpu_containers_than_a_ledger_record_place():
+    """The reference places any container count (allocate.go:54-62, rater.go:74-110). A pod with
+    66 GPU containers (more than the ledger record's 64 entries) is placed in Python
+    (podutil.wide_place) and accounted folded per device (podutil.fold_plan): every container
+    gets its device, the device's share is their sum, and deleting the pod gives it all back.
+    One that cannot fit fails its nodes with the reason, never a 5xx."""
     for frontend in ("native", "aiohttp"):
         async def main():
             store, rt = await _runtime(2, frontend=frontend)
@@ -82,14 +88,54 @@ def test_too_many_gpu_containers_is_a_failed_node_not_an_error():
                 pod = store.create_pod(_sidecar_pod("huge", 70, set(range(66)), pct=1))
                 f, p, b = await loop.run_in_executor(None, _schedule, rt, store, pod, ["n0", "n1"])
                 body = json.loads(f[1])
+                assert f[0] == 200 and body["NodeNames"] == ["n0", "n1"] and body["Error"] == "", body
+                assert p[0] == 200 and all(h["Score"] > 0 for h in json.loads(p[1]))
+                assert b == (200, b'{"Error":""}'), (frontend, b)
+                got = store.get_pod("default", "huge")
+                ann = got["metadata"]["annotations"]
+                devs = [int(ann[T.container_annotation(f"c{k}")]) for k in range(66)]
+                assert all(ann[T.container_annotation(f"c{k}")] == "-1" for k in range(66, 70))
+                node = pu.node_name_of(got)
+                gpus = rt.state.status()[node]["GPUs"]
+                used = [100 - g["Percent"] for g in gpus]
+                assert sum(used) == 66 and all(used[d] > 0 for d in devs)   # binpack: on as few as fit
+                assert rt.state.ledger.lookup(pu.pod_uid(pod))["state"] == "committed"
+                store.delete_pod("default", "huge")
+                assert await wait_for(lambda: all(g["Percent"] == 100 for g in rt.state.status()[node]["GPUs"]))
+                # more than the node holds: 200 x 10 % on 8-GPU nodes
+                big = store.create_pod(_sidecar_pod("toobig", 200, set(range(200)), pct=10))
+                f, p, b = await loop.run_in_executor(None, _schedule, rt, store, big, ["n0", "n1"])
+                body = json.loads(f[1])
                 assert f[0] == 200 and not body["NodeNames"] and body["Error"] == ""
-                assert all("at most 64" in r for r in body["FailedNodes"].values()), body
-                assert p[0] == 200 and [h["Score"] for h in json.loads(p[1])] == [0, 0]
-                assert b is None
+                assert all("can't allocate 200 GPU containers" in r for r in body["FailedNodes"].values()), body
+                assert p[0] == 200 and [h["Score"] for h in json.loads(p[1])] == [0, 0] and b is None
             finally:
                 await rt.stop()
 
         asyncio.run(main())
+
+
+def test_a_wide_pod_found_at_restart_is_accounted_from_its_annotations():
+    """Checkpoint/resume for a wide pod: the annotations written at bind fold into one ledger
+    record on a fresh extender (allocate_existing), the same per-device shares as before."""
+    from nanogpu.state.cluster import ClusterState
+
+    st = ClusterState()
+    st.register_node(pu.make_node("n0", 8, synthetic_mi355x(8).to_json()))
+    pod = _sidecar_pod("wide", 80, set(range(80)), pct=5)
+    pod["metadata"]["uid"] = "wide-uid"
+    plan, fresh = st.reserve(pod, "n0")
+    assert fresh and len(plan) == 80 and all(len(x) == 1 and x[0] >= 0 for x in plan)
+    st.commit("wide-uid")
+    before = [g["Percent"] for g in st.status()["n0"]["GPUs"]]
+    assert sum(100 - x for x in before) == 400
+    pod["spec"]["nodeName"] = "n0"
+    pod["metadata"]["annotations"] = dict(pu.placement_annotations([f"c{k}" for k in range(80)], plan))
+    fresh_state = ClusterState()
+    fresh_state.register_node(pu.make_node("n0", 8, synthetic_mi355x(8).to_json()))
+    assert fresh_state.allocate_existing(pod)
+    assert [g["Percent"] for g in fresh_state.status()["n0"]["GPUs"]] == before
+    assert fresh_state.release(pod) and all(g["Percent"] == 100 for g in fresh_state.status()["n0"]["GPUs"])
 
 
 def test_fuzz_container_counts_never_answer_5xx():
@@ -105,8 +151,9 @@ def test_fuzz_container_counts_never_answer_5xx():
                 f, p, b = await loop.run_in_executor(None, _schedule, rt, store, pod, ["n0", "n1", "n2", "n3"])
                 assert f[0] == 200 and p[0] == 200, (n, len(gpu), f, p)
                 fit = json.loads(f[1])["NodeNames"]
-                # the pods are small (at most 65 x 5 % on four 8-GPU nodes): only the cap refuses
-                assert bool(fit) == (len(gpu) <= 64), (n, len(gpu), f)
+                # the pods are small (at most 65 x 5 % on four 8-GPU nodes): every one fits, the
+                # ones with more GPU containers than a ledger record included
+                assert fit, (n, len(gpu), f)
                 if b is not None:
                     assert b == (200, b'{"Error":""}'), (n, len(gpu), b)
         finally:
