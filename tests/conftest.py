@@ -41,3 +41,18 @@ def tmp_shm(tmp_path):
         p.unlink()
     except FileNotFoundError:
         pass
+
+
+@pytest.fixture
+def cpu_exclusive():
+    """Multi-process bench jobs (several ranks, each with busy front-door threads, plus the API
+    server and the stand-ins) measure timing-sensitive things; under `pytest -n` they take turns
+    (an exclusive lock across the xdist workers) instead of starving each other."""
+    import fcntl
+
+    with open("/tmp/nanogpu-tests-cpu-exclusive.lock", "w") as f:
+        fcntl.flock(f, fcntl.LOCK_EX)
+        try:
+            yield
+        finally:
+            fcntl.flock(f, fcntl.LOCK_UN)
