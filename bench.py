@@ -140,6 +140,8 @@ def parse_args():
                     help="time box of each GPU pair's peer-copy probe (s); the RCCL ring gets 4x")
     ap.add_argument("--probe-standin", default="",
                     help="tests: a stand-in peer probe (hang:SRC-DST never finishes that pair)")
+    ap.add_argument("--no-batch-labels", action="store_true",
+                    help="the extender's writer pipelines each label PATCH behind its binding (no batches)")
     ap.add_argument("--spin-nap", action="store_true",
                     help="the extender's front door sleeps its busy-poll window instead of polling it")
     ap.add_argument("--bind-first", action="store_true",
@@ -836,7 +838,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                  nominate=not args.no_nominate,
                  bind_writer_threads=args.bind_writer_threads or max(2, 16 // d.world),
                  bind_writer_mode=args.bind_writer_mode, assume_label=not args.no_assume_label,
-                 bind_first=args.bind_first, spin_nap=args.spin_nap)
+                 bind_first=args.bind_first, spin_nap=args.spin_nap, batch_labels=not args.no_batch_labels)
     all_steps_pre = [10_000 + w for w in range(args.warmup)] + list(range(args.steps))
     rt = Runtime(cfg, worker=d.rank if shared else 0, api=rt_api)
     await rt.start()

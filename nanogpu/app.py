@@ -55,6 +55,7 @@ class Config:
     assume_label: bool = True
     bind_first: bool = False                    # front door: a batch's binds before its filters
     spin_nap: bool = False                      # front door: sleep the busy-poll window, not poll it
+    batch_labels: bool = True                   # native writer: label PATCHes batched after bindings
     api_write_timeout_s: float = 30.0           # native bind writer: an API answer due within this
     reservation_ttl_s: float = 60.0
     nominate: bool = True              # priorities nominate the top node (Ledger::nominate)
@@ -217,7 +218,8 @@ class Runtime:
                     if self.native.enable_native_writes(api_cfg, self.cfg.bind_writer_threads, ext.api_retries,
                                                         ext.record_events, self.cfg.bind_writer_mode != "threads",
                                                         self.cfg.assume_label, self.cfg.api_write_timeout_s,
-                                                        self.cfg.bind_writer_mode == "inline"):
+                                                        self.cfg.bind_writer_mode == "inline",
+                                                        self.cfg.batch_labels):
                         log.info("worker %d: bind API writes in native writer threads (%d)", self.worker,
                                  self.cfg.bind_writer_threads)
                 self.native.start()

@@ -410,7 +410,7 @@ class NativeServer:
 
     def enable_native_writes(self, config, threads: int, retries: int, record_events: bool,
                              evented: bool = True, label: bool = True, timeout_s: float = 30.0,
-                             inline_io: bool = False) -> bool:
+                             inline_io: bool = False, batch_labels: bool = True) -> bool:
         """Hands the bind's API writes to the front door's C++ writer threads (native/src/
         kubewriter.cpp) when the API server is a REST endpoint this process reaches with a
         bearer token or a client certificate; False (Python writes) otherwise."""
@@ -423,7 +423,7 @@ class NativeServer:
         self.fe.set_kube_writer(u.hostname, u.port or (443 if tls else 80), tls, config.token or "",
                                 config.token_file or "", config.ca_file or "", config.cert_file or "",
                                 config.key_file or "", bool(config.insecure), threads, retries, record_events,
-                                evented, label, timeout_s, inline_io)
+                                evented, label, timeout_s, inline_io, batch_labels)
         return True
 
     async def stop(self) -> None:

@@ -35,8 +35,11 @@ class BindIo {
   void submit(BindJob j);                      // launches it now, or when a slot frees up
   void on_event(uint64_t k, uint32_t events);  // an epoll event of connection k
   void pump();                                 // after a batch of events: drive what is due
-  size_t inflight() const { return inflight_; }
+  // binds and batched label PATCHes not finished yet
+  size_t inflight() const { return inflight_ + labels_out_ + label_wait_.size(); }
   size_t waiting() const { return waiting_.size(); }
+  // label PATCHes held for a batch: the owner's loop must come back within about a millisecond
+  bool labels_waiting() const { return !label_wait_.empty(); }
   // Stop: every bind still in flight or waiting goes to the slow path with what it got
   // (`why` for answers that never came). The connections are closed.
   void abandon(const char* why);
@@ -45,6 +48,7 @@ class BindIo {
  private:
   struct Conn;
   struct Job;
+  struct Label;
   bool resolve();
   void close_conn(Conn& c);
   bool open_conn(size_t k);
@@ -58,6 +62,9 @@ class BindIo {
   void launch(int64_t s);
   void start_waiting();
   void scan_deadlines(uint64_t now);
+  void queue_label(BindJob&& j, std::string&& patch);
+  void label_done(int64_t ls, int status, std::string body);
+  void launch_labels();
 
   KubeWriter* kw_;
   int ep_;
@@ -79,6 +86,16 @@ class BindIo {
   uint64_t timeout_ns_ = 0;
   uint64_t scanned_at_ = 0;
   uint64_t timeouts_ = 0;
+  // Label PATCHes (the reference's assume label, guarded by spec.nodeName) go out after their
+  // binding answered, batched: up to kLabelBatch pipelined on one connection, one send and a
+  // read or two for all of them, held at most kLabelHoldNs for the batch to fill.
+  static constexpr size_t kLabelBatch = 32;
+  static constexpr uint64_t kLabelHoldNs = 500'000;
+  std::vector<std::unique_ptr<Label>> lslots_;
+  std::vector<int64_t> lfree_;
+  std::deque<int64_t> label_wait_;
+  uint64_t label_oldest_ns_ = 0;
+  size_t labels_out_ = 0;   // sent, answer due
 };
 
 }  // namespace nanogpu

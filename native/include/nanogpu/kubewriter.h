@@ -139,6 +139,8 @@ class KubeWriter {
   // answers its happy-path binds on the caller's thread. Failures go to this writer's slow path.
   std::unique_ptr<BindIo> make_io(int ep, uint64_t tag_bit, Respond reply);
   bool inline_io() const { return inline_io_; }
+  // evented / inline: false pipelines each label PATCH behind its binding instead of batching
+  void set_batch_labels(bool on) { batch_labels_.store(on, std::memory_order_relaxed); }
   KubeWriterStats stats;
 
  private:
@@ -172,6 +174,7 @@ class KubeWriter {
   void run_slow();
   void to_slow(SlowJob&& sj);    // the slow path takes it (or, once its threads are gone, the caller)
   bool inline_io_ = false;
+  std::atomic<bool> batch_labels_{true};   // evented: label PATCHes batched after their bindings (BindIo)
   bool slow_gone_ = false;       // under mu_: the slow-path threads have exited
   bool evented_ = false;
   int max_inflight_ = 0;

@@ -776,7 +776,7 @@ PYBIND11_MODULE(_native, m) {
           [](Frontend& f, const std::string& host, int port, bool tls, const std::string& token,
              const std::string& token_file, const std::string& ca_file, const std::string& cert_file,
              const std::string& key_file, bool insecure, int threads, int retries, bool record_events,
-             bool evented, bool label, double timeout_s, bool inline_io) {
+             bool evented, bool label, double timeout_s, bool inline_io, bool batch_labels) {
             KubeTarget t;
             t.host = host;
             t.port = port;
@@ -787,13 +787,13 @@ PYBIND11_MODULE(_native, m) {
             t.cert_file = cert_file;
             t.key_file = key_file;
             t.insecure = insecure;
-            f.set_kube_writer(t, threads, retries, record_events, evented, label, timeout_s, inline_io);
+            f.set_kube_writer(t, threads, retries, record_events, evented, label, timeout_s, inline_io, batch_labels);
           },
           py::arg("host"), py::arg("port"), py::arg("tls") = false, py::arg("token") = "",
           py::arg("token_file") = "", py::arg("ca_file") = "", py::arg("cert_file") = "", py::arg("key_file") = "",
           py::arg("insecure") = false, py::arg("threads") = 32, py::arg("retries") = 3,
           py::arg("record_events") = true, py::arg("evented") = true, py::arg("label") = true,
-          py::arg("timeout_s") = 30.0, py::arg("inline_io") = false,
+          py::arg("timeout_s") = 30.0, py::arg("inline_io") = false, py::arg("batch_labels") = true,
           "Binds whose reservation succeeded natively are finished natively (PATCH + binding + "
           "commit/rollback) on keep-alive connections to kube-apiserver: one epoll thread "
           "(evented) or `threads` blocking threads; `threads` x 8 binds in flight.")

@@ -475,11 +475,12 @@ Frontend::Frontend(std::shared_ptr<Ledger> ledger, const std::string& host, int 
 Frontend::~Frontend() { stop(); }
 
 void Frontend::set_kube_writer(const KubeTarget& t, int threads, int retries, bool record_events, bool evented,
-                               bool label, double timeout_s, bool inline_io) {
+                               bool label, double timeout_s, bool inline_io, bool batch_labels) {
   if (writer_.load()) throw std::logic_error("Frontend: the kube writer is already set");
   writer_owner_ = std::make_unique<KubeWriter>(
       t, ledger_, [this](uint64_t id, int status, const std::string& body) { respond(id, status, "application/json", body); },
       threads, retries, record_events, evented, label, timeout_s, inline_io);
+  writer_owner_->set_batch_labels(batch_labels);
   if (inline_io) {
     for (auto& wp : workers_) {
       Worker* w = wp.get();
@@ -776,7 +777,7 @@ void Frontend::run(Worker* w) {
       n = epoll_pwait2(w->ep, evs, 128, &ts, nullptr);
     } else {
       // with bind answers due, wake at least for the BindIo's deadline scan
-      n = epoll_wait(w->ep, evs, 128, polling ? 0 : bio && bio->inflight() ? 100 : 200);
+      n = epoll_wait(w->ep, evs, 128, polling ? 0 : bio && bio->labels_waiting() ? 1 : bio && bio->inflight() ? 100 : 200);
     }
     w->parked.store(false, std::memory_order_relaxed);
     const uint64_t t_batch = n > 0 ? now_ns() : 0;

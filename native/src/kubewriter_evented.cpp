@@ -120,8 +120,8 @@ enum ConnState { kIdle, kConnecting, kHandshake, kSending, kReceiving };
 // usually, one read for both answers (HTTP/1.1 answers come back in request order; kube-
 // apiserver's Go server and the bench's API server both serve pipelined requests in order).
 struct Pending {
-  int64_t job;   // in-flight job slot
-  int which;     // 0: label PATCH, 1: binding
+  int64_t job;   // in-flight job slot (label slot for a batched label)
+  int which;     // 0: label PATCH pipelined behind its binding, 1: binding, 2: batched label PATCH
 };
 
 }  // namespace
@@ -135,9 +135,10 @@ struct BindIo::Conn {
   bool retried = false;  // the one fresh-connection retry is spent
   std::string out, in;
   size_t off = 0;
-  Pending pend[2];       // answers still due, in request order
-  int npend = 0;
+  std::vector<Pending> pend;   // answers still due, in request order, from `head`
+  size_t head = 0;
   uint64_t deadline_ns = 0;   // the answers are due by then (KubeWriter timeout_s)
+  int npend() const { return static_cast<int>(pend.size() - head); }
 };
 
 struct BindIo::Job {
@@ -146,6 +147,12 @@ struct BindIo::Job {
   int sp = 0, sb = 0;
   int left = 2;
   bool answered = false;   // kube-scheduler has its answer (the binding landed; the label may follow)
+  bool batch_label = false;   // the label goes in a later batch (queue_label), not behind the binding
+};
+
+struct BindIo::Label {
+  BindJob j;
+  std::string patch;
 };
 
 namespace {
@@ -270,13 +277,17 @@ void BindIo::complete(int64_t s) {
     st.inflight.fetch_sub(1, std::memory_order_relaxed);
     return;
   }
-  const bool ok2 = ok2xx(jb->sb) && ok2xx(jb->sp);
+  const bool ok2 = ok2xx(jb->sb) && (jb->batch_label || ok2xx(jb->sp));
   if (!jb->answered) st.binding_ns.fetch_add(ns_now() - jb->j.t0_ns, std::memory_order_relaxed);
   if (ok2) {
     kw_->ledger_->commit(jb->j.uid);
     st.ok.fetch_add(1, std::memory_order_relaxed);
-    st.inflight.fetch_sub(1, std::memory_order_relaxed);
     reply_(jb->j.id, 200, "{\"Error\":\"\"}");
+    if (jb->batch_label) {   // bound: the label follows in a batch (stats.inflight until then)
+      queue_label(std::move(jb->j), std::move(jb->patch));
+      return;
+    }
+    st.inflight.fetch_sub(1, std::memory_order_relaxed);
     return;
   }
   KubeWriter::SlowJob sj;
@@ -293,9 +304,12 @@ void BindIo::complete(int64_t s) {
 
 // the answer to connection c's oldest pending request
 void BindIo::deliver(Conn& c, int status, std::string body) {
-  const Pending p = c.pend[0];
-  c.pend[0] = c.pend[1];
-  --c.npend;
+  const Pending p = c.pend[c.head++];
+  if (c.head == c.pend.size()) {
+    c.pend.clear();
+    c.head = 0;
+  }
+  if (p.which == 2) return label_done(p.job, status, std::move(body));
   Job& jb = *slots_[static_cast<size_t>(p.job)];
   (p.which ? jb.sb : jb.sp) = status;
   (p.which ? jb.rb : jb.rp) = std::move(body);
@@ -316,14 +330,14 @@ void BindIo::deliver(Conn& c, int status, std::string body) {
 
 // every answer still due on connection c fails with `why` (status 0: the slow path retries)
 void BindIo::deliver_rest(Conn& c, const char* why) {
-  while (c.npend > 0) deliver(c, 0, why);
+  while (c.npend() > 0) deliver(c, 0, why);
 }
 
 // a transport failure: one retry on a fresh connection when a reused keep-alive connection
 // failed before any answer byte (the server closed it while idle), else status 0
 void BindIo::fail(size_t k, const char* why) {
   Conn& c = *conns_[k];
-  if (c.npend > 0 && c.reused && !c.got_any && !c.retried) {
+  if (c.npend() > 0 && c.reused && !c.got_any && !c.retried) {
     c.retried = true;   // nothing was answered: the whole pipeline goes out again
     c.reused = false;
     c.off = 0;
@@ -422,26 +436,28 @@ void BindIo::drive(size_t k, uint32_t events) {
       }
       // every complete answer in order; a pipeline cut short leaves its later answers to
       // the slow path (the label PATCH there is idempotent)
-      while (c.npend > 0) {
+      bool delivered = false;
+      while (c.npend() > 0) {
         int status = 0;
         std::string body;
         size_t used = 0;
         bool close = false;
-        const int rc = parse_response(c.in, eof && c.npend == 1, &status, &body, &used, &close);
+        const int rc = parse_response(c.in, eof && c.npend() == 1, &status, &body, &used, &close);
         if (rc < 0) return fail(k, "bad answer from the API server");
         if (rc == 0) {
           if (!eof) return;   // more bytes to come
-          if (c.got_any && c.in.empty() && c.npend < 2) break;   // answered some, then closed
+          if (c.got_any && c.in.empty() && (delivered || c.head > 0)) break;   // answered some, then closed
           return fail(k, "connection to the API server failed");
         }
         c.in.erase(0, used);
+        delivered = true;
         deliver(c, status, std::move(body));
         if (close) {
           eof = true;
           break;
         }
       }
-      if (c.npend > 0 || eof) {
+      if (c.npend() > 0 || eof) {
         close_conn(c);
         deliver_rest(c, "connection to the API server closed before every answer");
       }
@@ -467,14 +483,14 @@ void BindIo::launch(int64_t s) {
   }
   Conn& c = *conns_[k];
   request(&c.out, "POST", jb.j, true, kJsonE, jb.binding);
-  c.pend[0] = Pending{s, 1};
-  c.npend = 1;
-  if (kw_->label_) {
+  c.pend.clear();
+  c.head = 0;
+  c.pend.push_back(Pending{s, 1});
+  if (kw_->label_ && !jb.batch_label) {
     thread_local std::string second;
     request(&second, "PATCH", jb.j, false, kMergePatchE, jb.patch);
     c.out += second;
-    c.pend[1] = Pending{s, 0};
-    c.npend = 2;
+    c.pend.push_back(Pending{s, 0});
   }
   c.off = 0;
   c.in.clear();
@@ -508,6 +524,9 @@ void BindIo::start_waiting() {
     if (!kw_->label_) {   // the binding alone carries the annotations
       jb->left = 1;
       jb->sp = 200;
+    } else if (kw_->batch_labels_.load(std::memory_order_relaxed)) {   // the binding alone now, its label later
+      jb->left = 1;
+      jb->batch_label = true;
     }
     slots_[static_cast<size_t>(s)] = std::move(jb);
     ++inflight_;
@@ -528,17 +547,95 @@ void BindIo::on_event(uint64_t k, uint32_t events) {
 // a request unanswered past its deadline (a half-open connection: no answer, no reset) fails
 // to the slow path with status 0, never re-sent on this connection; one scan per 100 ms
 void BindIo::scan_deadlines(uint64_t now) {
-  if (inflight_ == 0 || now - scanned_at_ < 100'000'000ull) return;
+  if (inflight_ + labels_out_ == 0 || now - scanned_at_ < 100'000'000ull) return;
   scanned_at_ = now;
   for (size_t k = 0; k < conns_.size(); ++k) {
     Conn& c = *conns_[k];
-    if (c.npend > 0 && c.fd >= 0 && now > c.deadline_ns) {
-      timeouts_ += static_cast<uint64_t>(c.npend);
-      kw_->stats.timeouts.fetch_add(static_cast<uint64_t>(c.npend), std::memory_order_relaxed);
+    if (c.npend() > 0 && c.fd >= 0 && now > c.deadline_ns) {
+      timeouts_ += static_cast<uint64_t>(c.npend());
+      kw_->stats.timeouts.fetch_add(static_cast<uint64_t>(c.npend()), std::memory_order_relaxed);
       c.retried = true;
       fail(k, "the API server did not answer in time");
     }
   }
+}
+
+void BindIo::queue_label(BindJob&& j, std::string&& patch) {
+  int64_t ls;
+  if (!lfree_.empty()) {
+    ls = lfree_.back();
+    lfree_.pop_back();
+  } else {
+    ls = static_cast<int64_t>(lslots_.size());
+    lslots_.emplace_back();
+  }
+  auto l = std::make_unique<Label>();
+  l->j = std::move(j);
+  l->patch = std::move(patch);
+  lslots_[static_cast<size_t>(ls)] = std::move(l);
+  if (label_wait_.empty()) label_oldest_ns_ = ns_now();
+  label_wait_.push_back(ls);
+}
+
+void BindIo::label_done(int64_t ls, int status, std::string body) {
+  std::unique_ptr<Label> l = std::move(lslots_[static_cast<size_t>(ls)]);
+  lfree_.push_back(ls);
+  --labels_out_;
+  if (ok2xx(status)) {
+    kw_->stats.inflight.fetch_sub(1, std::memory_order_relaxed);
+    return;
+  }
+  // refused by its nodeName guard cannot happen here (its binding answered 2xx): a 5xx, a
+  // lost answer, a timeout: the slow path retries it
+  KubeWriter::SlowJob sj;
+  sj.answered = true;
+  sj.j = std::move(l->j);
+  sj.patch = std::move(l->patch);
+  sj.sp = status;
+  sj.rp = std::move(body);
+  kw_->to_slow(std::move(sj));
+}
+
+// up to kLabelBatch waiting label PATCHes, pipelined on one idle (or new) connection
+void BindIo::launch_labels() {
+  size_t k;
+  if (!idle_.empty()) {
+    k = idle_.back();
+    idle_.pop_back();
+  } else {
+    k = conns_.size();
+    conns_.push_back(std::make_unique<Conn>());
+  }
+  Conn& c = *conns_[k];
+  c.out.clear();
+  c.pend.clear();
+  c.head = 0;
+  thread_local std::string one;
+  while (!label_wait_.empty() && c.pend.size() < kLabelBatch) {
+    const int64_t ls = label_wait_.front();
+    label_wait_.pop_front();
+    const Label& l = *lslots_[static_cast<size_t>(ls)];
+    request(&one, "PATCH", l.j, false, kMergePatchE, l.patch);
+    c.out += one;
+    c.pend.push_back(Pending{ls, 2});
+    ++labels_out_;
+  }
+  label_oldest_ns_ = label_wait_.empty() ? 0 : ns_now();
+  c.off = 0;
+  c.in.clear();
+  c.got_any = false;
+  c.retried = false;
+  c.deadline_ns = ns_now() + timeout_ns_;
+  c.reused = c.fd >= 0;
+  if (c.fd >= 0) {
+    c.st = kSending;
+  } else if (!open_conn(k)) {
+    close_conn(c);
+    deliver_rest(c, "cannot connect to the API server");
+    idle_.push_back(k);
+    return;
+  }
+  kick_.push_back(k);
 }
 
 void BindIo::pump() {
@@ -547,13 +644,30 @@ void BindIo::pump() {
     for (size_t i = 0; i < kick_.size(); ++i) drive(kick_[i], 0);   // fail() may append
     kick_.clear();
   }
+  if (!label_wait_.empty()) {
+    const uint64_t now = ns_now();
+    while (label_wait_.size() >= kLabelBatch || (!label_wait_.empty() && now - label_oldest_ns_ >= kLabelHoldNs))
+      launch_labels();
+    for (size_t i = 0; i < kick_.size(); ++i) drive(kick_[i], 0);
+    kick_.clear();
+  }
   scan_deadlines(ns_now());
   for (size_t i = 0; i < kick_.size(); ++i) drive(kick_[i], 0);
   kick_.clear();
 }
 
 void BindIo::abandon(const char* why) {
-  for (auto& c : conns_) close_conn(*c);
+  // answers still due: failed with `why` (binds and labels go to the slow path that way)
+  for (auto& c : conns_) {
+    close_conn(*c);
+    deliver_rest(*c, why);
+  }
+  while (!label_wait_.empty()) {   // labels never sent: the slow path writes them
+    const int64_t ls = label_wait_.front();
+    label_wait_.pop_front();
+    ++labels_out_;
+    label_done(ls, 0, why);
+  }
   for (size_t s = 0; s < slots_.size(); ++s) {
     if (!slots_[s]) continue;
     Job& jb = *slots_[s];
@@ -626,7 +740,8 @@ void KubeWriter::io_loop() {
     io_parked_.store(true, std::memory_order_seq_cst);
     const bool queued = !stopping && q_len_.load(std::memory_order_seq_cst) > 0;
     // with answers due, wake for the deadline scan
-    const int n = epoll_wait(ep, evs, 256, queued ? 0 : stopping ? 10 : io.inflight() ? 100 : 1000);
+    const int n = epoll_wait(ep, evs, 256,
+                             queued ? 0 : stopping || io.labels_waiting() ? 1 : io.inflight() ? 100 : 1000);
     io_parked_.store(false, std::memory_order_relaxed);
     for (int e = 0; e < n; ++e) {
       if (evs[e].data.u64 == UINT64_MAX) {

@@ -55,6 +55,12 @@ def test_minimum_slice_one_pod_binpack():
             ann = got["metadata"]["annotations"]
             assert ann[T.container_annotation("main")] == "0"
             assert ann[T.ANNOTATION_GPU_ASSUME] == "true"
+            # the assume label follows the binding in the writer's next label batch (<= ~1 ms)
+            for _ in range(200):
+                if (store.get_pod("default", "p1")["metadata"].get("labels") or {}).get(T.LABEL_GPU_ASSUME):
+                    break
+                await asyncio.sleep(0.005)
+            got = store.get_pod("default", "p1")
             assert got["metadata"]["labels"][T.LABEL_GPU_ASSUME] == "true"
             assert got["spec"]["nodeName"] == "mi355x-0"
             assert ("default", "p1", "mi355x-0") in store.bindings

@@ -17,7 +17,7 @@ sys.path.insert(0, str(ROOT / "native"))
 
 
 @pytest.mark.parametrize("kind,threads,iters", [("plain", 4, 3000), ("asan", 4, 1500), ("tsan", 3, 800)])
-def test_native_stress(kind, threads, iters):
+def test_native_stress(kind, threads, iters, cpu_exclusive):
     import build
 
     exe = build.build_stress(kind)

@@ -12,7 +12,7 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "native"))
 
 
-def test_reconcile_of_100k_listed_pods_is_fast_and_never_stalls_a_reserve():
+def test_reconcile_of_100k_listed_pods_is_fast_and_never_stalls_a_reserve(cpu_exclusive):
     import build
 
     exe = build.build_stress("plain")
