@@ -1078,6 +1078,14 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
             affinity.relocate(pl["pids"], to)
             moved = {"from": pl["cpus"], "to": to}
             pl["cpus"] = to
+        if pl.get("apiserver") and pl.get("api_pid"):   # the shared API server's domain likewise
+            to = affinity.quieter_domain(pl["apiserver"], pl["numa"], exclude=pl["cpus"])
+            if to is not None:
+                affinity.relocate([pl["api_pid"]], to)
+                moved = dict(moved or {}, apiserver_from=pl["apiserver"], apiserver_to=to)
+                pl["apiserver"] = to
+                if apisrv is not None:
+                    apisrv.cpus = to
     results["relocated"] = moved
     rt.tracer.buf.clear()
     await barrier()
@@ -1359,7 +1367,7 @@ def main() -> int:
     if cpus and int(os.environ.get("LOCAL_WORLD_SIZE", "1")) == 1:
         args._placement = {"cpus": list(cpus), "numa": rank0_numa,
                            "pids": [os.getpid()] + ([drv_proc.pid] if drv_proc is not None else []),
-                           "apiserver": None}
+                           "apiserver": None, "api_pid": api_proc.proc.pid if api_proc is not None else None}
     d = Dist(args.gpus)
     d.init(use_gpu=not args.no_gpu)
     # the deployment that exists: one active kube-scheduler in front of every extender worker

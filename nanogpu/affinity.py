@@ -197,11 +197,13 @@ def domain_of(cpus: list[int]) -> list[int] | None:
 
 
 def quieter_domain(current: list[int], numa: int = -1, exclude: list[int] | None = None,
-                   window_s: float = 0.2, threshold: float = 0.15) -> list[int] | None:
-    """While this process group is idle (all of its CPU load is someone else's): when the
-    domain `current` sits on is at least `threshold` busy with other tenants' work, cores and
-    SMT siblings alike, the least busy other domain on NUMA node `numa` (none of `exclude`)
-    that is under half as busy; else None. Moving away from contention, never holding CPUs."""
+                   window_s: float = 0.3, threshold_cpus: float = 0.5) -> list[int] | None:
+    """While this process group is idle (all of its CPU load is someone else's): when other
+    tenants keep at least `threshold_cpus` CPUs' worth of the domain `current` sits on busy
+    (its cores and their SMT siblings), the least busy other domain on NUMA node `numa` (none
+    of `exclude`) with under half that load; else None. Moving away from contention, never
+    holding CPUs. On the MI355X box one CPU of foreign work on the rank's cores cost 11 % of
+    pods/s (profiles/variance_r04.md)."""
     doms = l3_domains()
     if numa >= 0:
         doms = [d for d in doms if numa_of_cpu(d[0]) == numa] or doms
@@ -211,11 +213,15 @@ def quieter_domain(current: list[int], numa: int = -1, exclude: list[int] | None
     avoid = set(exclude or [])
     others = [d for d in doms if d is not cur and 0 not in d and not avoid.intersection(d)]
     load = _busy([c for d in [cur] + others for c in list(d) + smt_siblings(d)], window_s)
-    here = _domain_busy(cur, load)
-    if here < threshold or not others:
+
+    def cpus_busy(d: list[int]) -> float:   # CPUs' worth of work on the domain's hw threads
+        return sum(load.get(c, 0.0) for c in list(d) + smt_siblings(d))
+
+    here = cpus_busy(cur)
+    if here < threshold_cpus or not others:
         return None
-    best = min(others, key=lambda d: (_domain_busy(d, load), d[0]))
-    return best if _domain_busy(best, load) < here / 2 else None
+    best = min(others, key=lambda d: (cpus_busy(d), d[0]))
+    return best if cpus_busy(best) < here / 2 else None
 
 
 def relocate(pids: list[int], cpus: list[int]) -> int:

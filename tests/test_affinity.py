@@ -125,6 +125,12 @@ def test_an_idle_job_leaves_a_domain_other_tenants_moved_onto(tmp_path, monkeypa
     assert A.quieter_domain([4, 5, 6, 7], 0) is None                # nobody else there: stay
     busy.update({c + 24: 0.6 for c in (4, 5, 6, 7)})                 # a tenant on the siblings
     assert A.quieter_domain([4, 5, 6, 7], 0) == [8, 9, 10, 11]
+    busy.update({c + 24: 0.0 for c in (4, 5, 6, 7)})
+    busy[5] = 0.9                                                    # one CPU's worth on a core of ours
+    assert A.quieter_domain([4, 5, 6, 7], 0) == [8, 9, 10, 11]
+    busy[5] = 0.3                                                    # a little: not worth moving
+    assert A.quieter_domain([4, 5, 6, 7], 0) is None
+    busy.update({c + 24: 0.6 for c in (4, 5, 6, 7)})
     assert A.quieter_domain([4, 5, 6, 7], 0, exclude=[8]) is None    # the API server's domain: not that one
     busy.update({c: 0.5 for c in (8, 9, 10, 11)})                    # the alternative is no better
     assert A.quieter_domain([4, 5, 6, 7], 0) is None
