@@ -33,6 +33,8 @@ def test_extender_deployment_args_parse():
     assert cfg.frontend_threads == 2 and cfg.busy_poll_us == 20 and cfg.cpu_affinity == "auto"
     # the CPU request holds every busy-polling thread (else the server turns polling off)
     cpu = float(c["resources"]["requests"]["cpu"])
+    # Guaranteed QoS, whole CPUs: what the static CPU manager needs to give the pod exclusive cores
+    assert c["resources"]["limits"] == c["resources"]["requests"] and cpu == int(cpu)
     assert busy_poll_fits(cfg.workers, cfg.frontend_threads, cpu)
     ports = {p["containerPort"] for p in c.get("ports", [])}
     env = {e["name"]: e.get("value") for e in c.get("env", [])}
