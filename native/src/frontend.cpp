@@ -13,6 +13,9 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <cpuid.h>
+#include <x86intrin.h>
+
 #include <algorithm>
 #include <charconv>
 #include <cerrno>
@@ -38,6 +41,46 @@ double now_s() {
 uint64_t now_ns() {
   return static_cast<uint64_t>(
       std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count());
+}
+
+// The front door's own timers (busy-poll windows, phase and verb timings, the extender-side
+// bind wall): durations measured on one worker thread, read several times a request. The
+// invariant TSC (CPUID 8000_0007h EDX bit 8) scaled to nanoseconds costs a few cycles where
+// the vDSO clock read costs tens (6.5 % of the front door's samples, profiles/extender_cpu_profile.md).
+// Values handed to other threads (BindJob::t0_ns) stay on now_ns().
+struct TscClock {
+  double ns_per_tick = 0.0;   // 0: no invariant TSC, fast_ns() is now_ns()
+  uint64_t tick0 = 0, ns0 = 0;
+};
+
+TscClock calibrate_tsc() {
+  TscClock c;
+  unsigned a = 0, b = 0, cx = 0, d = 0;
+  if (!__get_cpuid(0x80000007u, &a, &b, &cx, &d) || !((d >> 8) & 1u)) return c;
+  const uint64_t n0 = now_ns(), t0 = __rdtsc();
+  uint64_t n1;
+  do {
+    n1 = now_ns();
+  } while (n1 - n0 < 2'000'000);   // 2 ms
+  const uint64_t t1 = __rdtsc();
+  if (t1 <= t0) return c;
+  const double r = static_cast<double>(n1 - n0) / static_cast<double>(t1 - t0);
+  if (r < 0.05 || r > 2.0) return c;   // 0.5-20 GHz, else not a clock to trust
+  c.ns_per_tick = r;
+  c.tick0 = t1;
+  c.ns0 = n1;
+  return c;
+}
+
+const TscClock& tsc_clock() {
+  static const TscClock c = calibrate_tsc();
+  return c;
+}
+
+uint64_t fast_ns() {
+  const TscClock& c = tsc_clock();
+  if (c.ns_per_tick == 0.0) return now_ns();
+  return c.ns0 + static_cast<uint64_t>(static_cast<double>(__rdtsc() - c.tick0) * c.ns_per_tick);
 }
 
 bool ieq(std::string_view a, std::string_view b) {
@@ -350,8 +393,8 @@ void Frontend::reset_max() {
 namespace {
 struct PhaseTimer {
   std::atomic<uint64_t>* m;
-  uint64_t t0 = now_ns();
-  ~PhaseTimer() { atomic_max(m, now_ns() - t0); }
+  uint64_t t0 = fast_ns();
+  ~PhaseTimer() { atomic_max(m, fast_ns() - t0); }
 };
 }  // namespace
 
@@ -422,6 +465,7 @@ int presize_fd_table(int want) {
 Frontend::Frontend(std::shared_ptr<Ledger> ledger, const std::string& host, int port, int threads)
     : ledger_(std::move(ledger)) {
   if (!ledger_) throw std::invalid_argument("Frontend: ledger required");
+  (void)tsc_clock();   // calibrated here (2 ms), not on the first request
   presize_fd_table();
   if (threads < 1) threads = 1;
   if (threads > 64) threads = 64;
@@ -675,9 +719,9 @@ void Frontend::prepare_bind(std::string_view body, PyRequest* r) {
   if (uid.empty() || name.empty() || node.empty()) return;
   CachedPod pod;
   {
-    const uint64_t tw = now_ns();
+    const uint64_t tw = fast_ns();
     std::lock_guard<std::mutex> g(pod_mu_);
-    atomic_max(&phase_max_ns[4], now_ns() - tw);
+    atomic_max(&phase_max_ns[4], fast_ns() - tw);
     auto it = pods_.find(uid);
     if (it != pods_.end()) {
       pod = std::move(it->second);
@@ -708,13 +752,13 @@ void Frontend::prepare_bind(std::string_view body, PyRequest* r) {
     std::lock_guard<std::mutex> g(opt_mu_);
     o = opt_;
   }
-  const uint64_t t0 = now_ns();
+  const uint64_t t0 = fast_ns();
   Plan plan;
   std::memset(&plan, 0, sizeof(plan));
   PreparedBind& b = r->bind;
   b.rc = ledger_->reserve(id, uid, pod.demand, o, &plan);
   if ((b.rc == kOk || b.rc == kOkExisting) && pod.owner) ledger_->set_pod_owner(uid, pod.owner);
-  bind_stats.observe(now_ns() - t0);
+  bind_stats.observe(fast_ns() - t0);
   b.ok = true;
   b.ns = std::move(ns);
   b.name = name;
@@ -755,7 +799,7 @@ void Frontend::run(Worker* w) {
     const int64_t spin = busy_poll_ns_.load(std::memory_order_relaxed);
     const bool hot = __builtin_popcount(gaps & 0xffffu) >= 8;
     const uint64_t since = w->cycle_reply_ns;
-    const uint64_t t_now = now_ns();
+    const uint64_t t_now = fast_ns();
     const bool polling = spin > 0 && hot && since && t_now - since < static_cast<uint64_t>(spin);
     // nap: the spin window is slept in the kernel (epoll_pwait2 with the window's remaining
     // microseconds) instead of polled: a request that arrives wakes the worker, and idle
@@ -780,7 +824,7 @@ void Frontend::run(Worker* w) {
       n = epoll_wait(w->ep, evs, 128, polling ? 0 : bio && bio->labels_waiting() ? 1 : bio && bio->inflight() ? 100 : 200);
     }
     w->parked.store(false, std::memory_order_relaxed);
-    const uint64_t t_batch = n > 0 ? now_ns() : 0;
+    const uint64_t t_batch = n > 0 ? fast_ns() : 0;
     if (n > 0) {
       if (spin > 0 && since && since != scored) {
         gaps = (gaps << 1) | (t_batch - since < static_cast<uint64_t>(spin) ? 1u : 0u);
@@ -792,7 +836,7 @@ void Frontend::run(Worker* w) {
       Frontend* f;
       uint64_t t0;
       ~BatchTimer() {
-        if (t0) atomic_max(&f->loop_max_ns, now_ns() - t0);
+        if (t0) atomic_max(&f->loop_max_ns, fast_ns() - t0);
       }
     } batch_timer{this, t_batch};
     for (int i = 0; i < n; ++i) {
@@ -866,8 +910,8 @@ void Frontend::run(Worker* w) {
   // stopping: the binds this worker has in flight finish (bounded), else the slow path takes
   // them; their answers still reach kube-scheduler on the open connections
   if (BindIo* bio = w->bio.load(std::memory_order_acquire)) {
-    const uint64_t until = now_ns() + 5'000'000'000ull;
-    while (bio->inflight() + bio->waiting() > 0 && now_ns() < until) {
+    const uint64_t until = fast_ns() + 5'000'000'000ull;
+    while (bio->inflight() + bio->waiting() > 0 && fast_ns() < until) {
       const int n = epoll_wait(w->ep, evs, 128, 10);
       for (int i = 0; i < n; ++i) {
         const uint64_t tag = evs[i].data.u64;
@@ -892,7 +936,7 @@ void Frontend::deliver_reply(Worker* w, uint64_t conn, std::string&& bytes) {
   const uint64_t t_req = c->t_req_ns;
   c->bind_waiting = false;
   flush(w, c);   // may close the connection (Connection: close, a peer reset): c is gone then
-  if (was_bind) note_bind_wall(now_ns() - t_req);   // handed to the kernel: extender-side wall time
+  if (was_bind) note_bind_wall(fast_ns() - t_req);   // handed to the kernel: extender-side wall time
   if (w->conns.count(conn)) process(w, c);
 }
 
@@ -913,7 +957,7 @@ bool Frontend::read_in(Worker* w, Conn* c, bool* eof) {
   for (;;) {
     const ssize_t r = recv(c->fd, buf, sizeof(buf), 0);
     if (r > 0) {
-      if (c->in.empty()) c->t_in_ns = now_ns();
+      if (c->in.empty()) c->t_in_ns = fast_ns();
       c->in.append(buf, static_cast<size_t>(r));
       if (c->in.size() > kMaxBody + kMaxHeader) {
         close_conn(w, c);
@@ -1040,7 +1084,7 @@ void Frontend::process(Worker* w, Conn* c) {
     if (handle_native(w, c, method, path, body, &c->out)) {   // the answer lands in c->out
       c->in.erase(0, consumed);
       flush(w, c);
-      w->cycle_reply_ns = now_ns();   // the scheduling cycle's next request is due: spin for it
+      w->cycle_reply_ns = fast_ns();   // the scheduling cycle's next request is due: spin for it
       if (!w->conns.count(id)) return;
     } else {
       std::string m(method), pth(path), q(query), b(body);   // owned: the Python side keeps them
@@ -1068,11 +1112,11 @@ void Frontend::defer(Worker* w, Conn* c, std::string method, std::string path, s
       j.containers = std::move(r.bind.containers);
       j.plan = std::move(r.bind.plan);
       j.fresh = r.bind.rc == kOk;
-      j.t0_ns = now_ns();
+      j.t0_ns = now_ns();   // read by the writer's threads: the shared clock
       c->waiting = true;
       c->bind_waiting = true;
-      c->t_req_ns = c->t_in_ns ? c->t_in_ns : now_ns();
-      c->t_in_ns = c->in.empty() ? 0 : now_ns();
+      c->t_req_ns = c->t_in_ns ? c->t_in_ns : fast_ns();
+      c->t_in_ns = c->in.empty() ? 0 : fast_ns();
       if (bio) bio->submit(std::move(j));   // sent by pump() after this batch of events
       else kw->submit(std::move(j));
       return;
@@ -1085,8 +1129,8 @@ void Frontend::defer(Worker* w, Conn* c, std::string method, std::string path, s
   r.t_arrival = now_s();
   c->waiting = true;
   c->bind_waiting = r.path == "/scheduler/bind";
-  c->t_req_ns = c->t_in_ns ? c->t_in_ns : now_ns();
-  c->t_in_ns = c->in.empty() ? 0 : now_ns();   // pipelined bytes behind it: their clock starts now
+  c->t_req_ns = c->t_in_ns ? c->t_in_ns : fast_ns();
+  c->t_in_ns = c->in.empty() ? 0 : fast_ns();   // pipelined bytes behind it: their clock starts now
   py_stats.deferred.fetch_add(1, std::memory_order_relaxed);
   PhaseTimer pt{&phase_max_ns[6]};
   {
@@ -1144,10 +1188,10 @@ bool Frontend::handle_native(Worker* w, Conn* c, std::string_view method, std::s
   if (method != "POST" || !serving()) return false;
   const bool prio = path == "/scheduler/priorities";
   if (!prio && path != "/scheduler/filter") return false;
-  const uint64_t t0 = now_ns();
+  const uint64_t t0 = fast_ns();
   thread_local std::string resp;   // keeps its capacity: no allocation per request
   if (!filter_verb(body, prio, &resp)) return false;
-  (prio ? prio_stats : filter_stats).observe(now_ns() - t0);
+  (prio ? prio_stats : filter_stats).observe(fast_ns() - t0);
   constexpr std::string_view kHead = "HTTP/1.1 200 OK\r\nContent-Type: application/json; charset=utf-8\r\nContent-Length: ";
   char len[24];
   const char* e = std::to_chars(len, len + sizeof len, resp.size()).ptr;
