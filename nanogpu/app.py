@@ -56,6 +56,7 @@ class Config:
     bind_first: bool = False                    # front door: a batch's binds before its filters
     spin_nap: bool = False                      # front door: sleep the busy-poll window, not poll it
     batch_labels: bool = True                   # native writer: label PATCHes batched after bindings
+    watch_assigned_only: bool = True            # pod informer: bound pods only (spec.nodeName!=)
     api_write_timeout_s: float = 30.0           # native bind writer: an API answer due within this
     reservation_ttl_s: float = 60.0
     nominate: bool = True              # priorities nominate the top node (Ledger::nominate)
@@ -153,7 +154,11 @@ class Runtime:
         if self.leader:
             # the controllers read a pod's identity, nano-gpu/* annotations and limits, node
             # and phase: the REST watch decodes just those (native), not the whole object
-            self.pod_informer = Informer(self.api, "pods", slim=True, prefilter=self.state.ledger)
+            # assigned pods only (`spec.nodeName!=`, the selector kube-scheduler's own informer
+            # uses for them): a pending pod is the extender's business through its verbs, not
+            # the controller's, and an unschedulable pod's condition updates never reach us
+            self.pod_informer = Informer(self.api, "pods", slim=True, prefilter=self.state.ledger,
+                                         field_selector=T.ASSIGNED_PODS if self.cfg.watch_assigned_only else None)
             pc = PodController(self.state, self.pod_informer, workers=self.cfg.threadness, metrics=self.metrics)
             self.controllers.append(pc)
             pc.start()

@@ -51,18 +51,20 @@ def _match_labels(obj: dict, selector: str | None) -> bool:
 
 
 def _match_fields(obj: dict, selector: str | None) -> bool:
+    """kube-apiserver's pod field selectors: `k=v` / `k==v` and `k!=v` on spec.nodeName,
+    metadata.name, metadata.namespace and status.phase (`spec.nodeName!=`: assigned pods)."""
     if not selector:
         return True
     for term in selector.split(","):
-        k, _, v = term.partition("=")
+        term = term.strip()
+        neg = "!=" in term
+        k, _, v = term.partition("!=" if neg else "=")
         v = v.lstrip("=")
-        if k == "spec.nodeName" and pu.node_name_of(obj) != v:
-            return False
-        if k == "metadata.name" and pu.meta(obj).get("name") != v:
-            return False
-        if k == "metadata.namespace" and pu.meta(obj).get("namespace") != v:
-            return False
-        if k == "status.phase" and (obj.get("status") or {}).get("phase") != v:
+        have = {"spec.nodeName": lambda: pu.node_name_of(obj) or "",
+                "metadata.name": lambda: pu.meta(obj).get("name") or "",
+                "metadata.namespace": lambda: pu.meta(obj).get("namespace") or "",
+                "status.phase": lambda: (obj.get("status") or {}).get("phase") or ""}.get(k.strip())
+        if have is not None and (have() == v) == neg:
             return False
     return True
 

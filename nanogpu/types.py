@@ -73,3 +73,7 @@ FILTER_NODE_CACHE_ERROR = ("nano-gpu-scheduler extender must be configured with 
 
 def container_annotation(name: str) -> str:
     return ANNOTATION_CONTAINER_FMT.format(name)
+
+# the pod informer's field selector: assigned pods only (kube-scheduler's own assigned-pod
+# informer uses the same selector)
+ASSIGNED_PODS = "spec.nodeName!="

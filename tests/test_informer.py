@@ -277,3 +277,59 @@ def test_node_agent_informer_selects_its_node_by_field(kind):
             await srv.stop()
 
     asyncio.run(main())
+
+
+@pytest.mark.parametrize("kind", ["inproc", "rest-native-server"])
+def test_extender_pod_informer_sees_assigned_pods_only(kind):
+    """The extender's pod informer watches `spec.nodeName!=` (types.ASSIGNED_PODS): a pending
+    pod, and every update of it, never reaches the controller; it appears when it is bound and
+    leaves when it is deleted. On the REST path the selector crosses URL-encoded to the native
+    API server."""
+    from nanogpu import types as T
+
+    async def main():
+        srv = None
+        if kind == "inproc":
+            store = FakeKubeStore()
+            api = InProcKube(store)
+            create = store.create_pod
+            bind = lambda name: store.bind_pod("default", name, "", "n0")
+            delete = lambda name: store.delete_pod("default", name)
+            store.add_node(pu.make_node("n0", 8))
+        else:
+            srv = N.ApiServer("127.0.0.1", 0, 2, 4096)
+            srv.call("POST", "/api/v1/nodes", json.dumps(pu.make_node("n0", 8)))
+            api = KubeClient(KubeConfig(server=f"http://127.0.0.1:{srv.port}"))
+            create = lambda p: srv.call("POST", "/api/v1/namespaces/default/pods", json.dumps(p))
+            bind = lambda name: srv.call("POST", f"/api/v1/namespaces/default/pods/{name}/binding", json.dumps(
+                {"metadata": {"name": name}, "target": {"kind": "Node", "name": "n0"}}))
+            delete = lambda name: srv.call("DELETE", f"/api/v1/namespaces/default/pods/{name}", "")
+        create(pu.make_pod("early", [("c", 10)]))
+        bind("early")
+        create(pu.make_pod("waiting", [("c", 10)]))
+        inf = Informer(api, "pods", field_selector=T.ASSIGNED_PODS)
+        seen = []
+        inf.add_handler(lambda et, o, old: seen.append((et, pu.meta(o)["name"])))
+        task = inf.start()
+        try:
+            await asyncio.wait_for(inf.synced.wait(), 10)
+            assert set(inf.store) == {"default/early"}                  # LIST: assigned only
+            create(pu.make_pod("later", [("c", 10)]))
+            await asyncio.sleep(0.2)
+            assert "default/later" not in inf.store and all(n != "later" for _, n in seen)
+            bind("later")
+            assert await wait_for(lambda: "default/later" in inf.store)
+            delete("later")
+            assert await wait_for(lambda: "default/later" not in inf.store)
+            assert all(n != "waiting" for _, n in seen)
+        finally:
+            task.cancel()
+            try:
+                await task
+            except (asyncio.CancelledError, Exception):
+                pass
+            if srv is not None:
+                await api.close()
+                srv.stop()
+
+    asyncio.run(main())
