@@ -774,6 +774,7 @@ void Frontend::prepare_bind(std::string_view body, PyRequest* r) {
 void Frontend::run(Worker* w) {
   epoll_event evs[128];
   std::vector<uint64_t> later;   // connections whose next request is a bind
+  std::vector<std::pair<uint64_t, uint32_t>> bio_later;   // BindIo events of this batch
   // Busy polling only where a wake-up would sit on kube-scheduler's critical path: after this
   // worker replied to a filter or priorities request. kube-scheduler's scheduling cycle is
   // serial (filter, then priorities, then the next pod's filter a few microseconds later), so
@@ -863,7 +864,10 @@ void Frontend::run(Worker* w) {
         (void)!read(w->efd, &v, sizeof(v));
         drain_mailbox();
       } else if (!(tag >> 63) && (tag & kBioTag)) {
-        if (bio) bio->on_event(tag & ~kBioTag, evs[i].events);
+        // API answers after this batch's scheduling-cycle requests: a bind's answer only ends
+        // an asynchronous binding, the cycle's next pod waits on filter / priorities
+        const uint32_t ev = evs[i].events;   // epoll_event is packed: no reference into it
+        bio_later.emplace_back(tag & ~kBioTag, ev);
       } else {
         PhaseTimer pt{&phase_max_ns[2]};
         const uint64_t cid = (tag & ~(1ull << 63)) >> 1;
@@ -901,6 +905,9 @@ void Frontend::run(Worker* w) {
       if (it != w->conns.end()) after_read(w, it->second.get(), false);
     }
     later.clear();
+    if (bio)
+      for (const auto& e : bio_later) bio->on_event(e.first, e.second);
+    bio_later.clear();
     if (bio) {   // the binds this batch parsed go out now; answers that came in are replied
       bio->pump();
       drain_local(w);
@@ -1495,7 +1502,6 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     }
     put_pod(uid, std::move(cp));
   }
-  Plan p;
   std::string& r = *out;
   r.reserve(64 + 128 * static_cast<size_t>(nn));   // room for a FailedNodes entry per node
   if (!prioritize) {
