@@ -595,6 +595,23 @@ def apiserver_main(conn, avoid: list[int] | None = None, near: int = -1) -> None
             return
 
 
+async def wait_released(lookup, uids: list[str], timeout_s: float = 10.0) -> bool:
+    """Until the ledger holds none of `uids` (the pod controller's releases). Polled every
+    20 µs from an executor thread: the event loop stays free for the watch (the in-process
+    and aiohttp watches deliver the DELETED events on it), and the harness's waiting does not
+    spin the extender process's event loop, whose CPU time the bench reports. Deletions arrive
+    in order: the last pod first, then all of them once."""
+    def poll() -> bool:
+        end = time.perf_counter() + timeout_s
+        while time.perf_counter() < end:
+            if not lookup(uids[-1]) and not any(lookup(u) for u in uids):
+                return True
+            time.sleep(20e-6)
+        return False
+
+    return await asyncio.get_running_loop().run_in_executor(None, poll)
+
+
 async def arecv(conn):
     """conn.recv() awaited on the event loop (the pipe's fd in the selector): no executor
     thread, whose start can wait milliseconds for the GIL while the loop is busy."""
@@ -897,12 +914,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                 [(f"bench-r{k % d.world}", f"k{k}") for k in dels], step)
             phases.update(delete_srv_ms=1e3 * dt_d, create_srv_ms=1e3 * dt_c)
         uids = [steady_uid(k, k % d.world) for k in dels]
-        lookup = rt.state.ledger.lookup
-        t_spin = time.perf_counter() + 0.003
-        for _ in range(50000):
-            if not uids or (not lookup(uids[-1]) and not any(lookup(u) for u in uids)):
-                break
-            await asyncio.sleep(0 if time.perf_counter() < t_spin else 0.0002)
+        if uids:
+            await wait_released(rt.state.ledger.lookup, uids)
         phases["release_ms"] = 1e3 * (time.perf_counter() - t_step0)
         if shared:
             await barrier()
@@ -997,18 +1010,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
             srv_ms.setdefault(step, {}).update(delete_srv_ms=1e3 * dt_d, peak_ms=1e3 * (t_frag - ts),
                                                delete_rpc_ms=1e3 * (time.perf_counter() - t_frag))
         # the pod controller releases on DELETED; wait until our shares are gone
-        # (the in-process watch delivers the DELETED events on the next loop iterations: yield
-        # first, and only then back off to short sleeps)
-        # Deletions are delivered in order: wait for the last pod, then check them all once.
-        # (yield-only polling for the first 3 ms, so noticing the last release costs no
-        # sleep quantum; then 0.2 ms naps)
-        uids = [pu.pod_uid(p) for p in pods]
-        lookup = rt.state.ledger.lookup
-        t_spin = time.perf_counter() + 0.003
-        for i in range(50000):
-            if not lookup(uids[-1]) and not any(lookup(u) for u in uids):
-                break
-            await asyncio.sleep(0 if time.perf_counter() < t_spin else 0.0002)
+        await wait_released(rt.state.ledger.lookup, [pu.pod_uid(p) for p in pods])
         t_rel = time.perf_counter()
         if pod_ctrl is not None:
             await pod_ctrl.queue.drain(5.0)
