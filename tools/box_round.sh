@@ -5,6 +5,8 @@
 set -o pipefail
 out=$1; shift
 mkdir -p "$out"
+timeout -k 10 420 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$out/gputest.log" 2>&1 || exit $?
+tail -2 "$out/gputest.log"
 OUT="$out/arms" REPS=${REPS:-3} tools/bench_arms.sh "$@" || exit $?
 tools/box_variance.sh "$out/var" ${VAR_RUNS:-4} || exit $?
 export TMPDIR=/tmp
