@@ -1220,6 +1220,10 @@ def order_line(full: dict) -> tuple[dict, dict]:
     diag = {k: full[k] for k in full
             if k in DIAG_KEYS or k.startswith(("nominations_", "native_verb_mean_us_"))}
     line = {k: v for k, v in full.items() if k not in diag and k not in HEADLINE_LAST}
+    gpu = full.get("gpu")
+    if isinstance(gpu, dict) and "link_bw_matrix_gbs" in gpu:   # 8 x 8 rates: diagnostics
+        diag["link_bw_matrix_gbs"] = gpu["link_bw_matrix_gbs"]
+        line["gpu"] = {k: v for k, v in gpu.items() if k != "link_bw_matrix_gbs"}
     for k in HEADLINE_LAST:
         if k in full:
             line[k] = full[k]
