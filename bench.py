@@ -1224,6 +1224,16 @@ def order_line(full: dict) -> tuple[dict, dict]:
     if isinstance(gpu, dict) and "link_bw_matrix_gbs" in gpu:   # 8 x 8 rates: diagnostics
         diag["link_bw_matrix_gbs"] = gpu["link_bw_matrix_gbs"]
         line["gpu"] = {k: v for k, v in gpu.items() if k != "link_bw_matrix_gbs"}
+    # whatever else the line carries, it stays under ~3.8 KB: the largest side keys move out
+    keep = {"metric", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config", "value_mode", "scheduled", "failed"}
+    budget = 3800 - sum(len(json.dumps({k: full[k]})) for k in HEADLINE_LAST if k in full)
+    while len(json.dumps(line)) > budget:
+        side = [k for k in line if k not in keep]
+        if not side:
+            break
+        big = max(side, key=lambda k: len(json.dumps(line[k])))
+        diag[big] = line.pop(big)
     for k in HEADLINE_LAST:
         if k in full:
             line[k] = full[k]
