@@ -785,3 +785,50 @@ def test_rotating_node_windows_answer_byte_identical_through_the_list_cache():
         assert ok and json.loads(out)["NodeNames"] == [n for n in names[:3] if n != "node-00"]
     finally:
         fe.stop()
+
+
+def test_ambiguous_request_framing_is_refused():
+    """`Content-Length: 12abc` (a numeric prefix), a second Content-Length that
+    disagrees, or Content-Length together with chunked encoding would let the front door and a
+    proxy in front of it frame the same bytes differently (request smuggling): each closes the
+    connection without an answer. Well-framed requests, a repeated equal Content-Length
+    included, are answered."""
+    def send(port, data):
+        s = socket.create_connection(("127.0.0.1", port))
+        s.settimeout(2.0)
+        try:
+            s.sendall(data)
+            s.shutdown(socket.SHUT_WR)
+            out = b""
+            while True:
+                got = s.recv(65536)
+                if not got:
+                    return out
+                out += got
+        except (socket.timeout, ConnectionResetError):
+            return b"<timeout>"
+        finally:
+            s.close()
+
+    async def main():
+        store, rt = await _runtime(2)
+        loop = asyncio.get_running_loop()
+        pod = store.create_pod(_pods(random.Random(1), 1)[0])
+        body = _dumps({"Pod": pod, "NodeNames": ["n0"]})
+        head = b"POST /scheduler/filter HTTP/1.1\r\nHost: x\r\n"
+        n = str(len(body)).encode()
+        try:
+            for extra, answered in [(b"Content-Length: " + n + b"\r\n", True),
+                                    (b"Content-Length: " + n + b"\r\nContent-Length: " + n + b"\r\n", True),
+                                    (b"Content-Length: " + n + b"abc\r\n", False),
+                                    (b"Content-Length: " + n + b", " + n + b"\r\n", False),
+                                    (b"Content-Length: " + n + b"\r\nContent-Length: 3\r\n", False),
+                                    (b"Content-Length: " + n + b"\r\nTransfer-Encoding: chunked\r\n", False)]:
+                got = await loop.run_in_executor(None, send, rt.bound_port, head + extra + b"\r\n" + body)
+                assert got.startswith(b"HTTP/1.1 200") == answered, (extra, got[:80])
+                if not answered:
+                    assert got == b"", (extra, got[:80])
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
