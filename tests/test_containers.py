@@ -247,3 +247,58 @@ def test_node_with_more_devices_than_a_slot_holds_fails_alone():
             await rt.stop()
 
     asyncio.run(main())
+
+
+from hypothesis import given, settings   # noqa: E402
+from hypothesis import strategies as st   # noqa: E402
+
+
+@settings(max_examples=150, deadline=None)
+@given(st.lists(st.tuples(st.sampled_from([0, 1, 2, 5, 10, 25, 100, 200]), st.sampled_from([0, 512, 4096])),
+                min_size=65, max_size=160),
+       st.booleans(), st.lists(st.integers(0, 100), min_size=8, max_size=8))
+def test_wide_placement_never_overcommits_and_folds_exactly(demand, spread, used):
+    """podutil.wide_place / fold_plan on any wide demand over a partly used 8-device node: a
+    placement never overcommits a device's percent or HBM, whole-device containers get devices
+    nobody else uses, and the folded record holds each device's exact sum (a device filled to
+    100 % is held whole); the ledger accepts the folded record and gives everything back."""
+    devs = [{"pct_free": 100 - u, "pct_total": 100, "mib_free": 262144 - 1024 * u, "mib_total": 262144,
+             "healthy": True, "pool": -1} for u in used]
+    plan = pu.wide_place(devs, demand, spread=spread)
+    if plan is None:
+        return
+    assert len(plan) == len(demand)
+    pct = [0] * 8
+    mib = [0] * 8
+    whole = set()
+    for (p, m), idx in zip(demand, plan):
+        if p <= 0 and m <= 0:
+            assert idx == [-1]
+            continue
+        if p >= 100 and p % 100 == 0:
+            assert len(idx) == p // 100 and not whole.intersection(idx)
+            whole.update(idx)
+            for j in idx:
+                pct[j] += 100
+        else:
+            (j,) = idx
+            pct[j] += p
+            mib[j] += m
+    for j in range(8):
+        assert pct[j] <= devs[j]["pct_free"] and mib[j] <= devs[j]["mib_free"]
+        if j in whole:
+            assert pct[j] == 100 and devs[j]["pct_free"] == 100
+    folded, fplan = pu.fold_plan(demand, plan)
+    assert len(folded) <= 8 and sorted(x[0] for x in fplan) == [j for j in range(8) if pct[j] or mib[j]]
+    for (fp, fm), (j,) in zip(folded, fplan):
+        assert fp == min(100, pct[j]) and (fm == mib[j] or j in whole)
+    from nanogpu.state.cluster import ClusterState
+
+    st_ = ClusterState()
+    node = pu.make_node("n0", 8, synthetic_mi355x(8, hbm_mib=262144).to_json())
+    e = st_.register_node(node)
+    for j, u in enumerate(used):    # the same pre-existing load
+        if u:
+            assert st_.ledger.allocate_plan(e.id, f"pre{j}", [(u, 1024 * u)], [[j]], True) == 0
+    assert st_.ledger.allocate_plan(e.id, "wide", folded, fplan, True) == 0
+    assert st_.ledger.release("wide") == 0
