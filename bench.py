@@ -140,8 +140,9 @@ def parse_args():
                     help="time box of each GPU pair's peer-copy probe (s); the RCCL ring gets 4x")
     ap.add_argument("--probe-standin", default="",
                     help="tests: a stand-in peer probe (hang:SRC-DST never finishes that pair)")
-    ap.add_argument("--no-batch-labels", action="store_true",
-                    help="the extender's writer pipelines each label PATCH behind its binding (no batches)")
+    ap.add_argument("--batch-labels", action="store_true",
+                    help="the extender's writer batches the label PATCHes of bound pods (default: each pipelined "
+                         "behind its binding)")
     ap.add_argument("--spin-nap", action="store_true",
                     help="the extender's front door sleeps its busy-poll window instead of polling it")
     ap.add_argument("--bind-first", action="store_true",
@@ -855,7 +856,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                  nominate=not args.no_nominate,
                  bind_writer_threads=args.bind_writer_threads or max(2, 16 // d.world),
                  bind_writer_mode=args.bind_writer_mode, assume_label=not args.no_assume_label,
-                 bind_first=args.bind_first, spin_nap=args.spin_nap, batch_labels=not args.no_batch_labels)
+                 bind_first=args.bind_first, spin_nap=args.spin_nap, batch_labels=args.batch_labels)
     all_steps_pre = [10_000 + w for w in range(args.warmup)] + list(range(args.steps))
     rt = Runtime(cfg, worker=d.rank if shared else 0, api=rt_api)
     await rt.start()
@@ -1115,11 +1116,27 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     t0 = time.perf_counter()
     if sampler is not None:
         sampler.on.set()
+    # other tenants moving onto the rank's domain mid-run: checked every 4 steps (~0.1 s), the
+    # job moves to a quieter domain when they keep half a CPU or more of it busy
+    watch = None
+    if d.world == 1 and getattr(args, "_placement", None) and not getattr(args, "no_relocate", False):
+        pl = args._placement
+        watch = affinity.ContentionWatch(pl["cpus"], pl["pids"], pl["numa"], exclude=pl.get("apiserver") or [])
+        watch.check()
+        results["foreign_cpus"] = []
     for k, s in enumerate(timed_ids):
         r = await one_step(s, True, timed_ids[k + 1] if k + 1 < len(timed_ids) else None)
         results["steps"].append(r["stats"])
         results["frag"].append(r["frag"])
         results.setdefault("phases", []).append(r["phases"])
+        if watch is not None and k % 4 == 3:
+            foreign, to = watch.check()
+            results["foreign_cpus"].append(round(foreign, 2))
+            if to is not None:
+                affinity.relocate(pl["pids"], to)
+                results["relocated"] = dict(results.get("relocated") or {}, mid_run_from=pl["cpus"], mid_run_to=to,
+                                            at_step=k + 1)
+                pl["cpus"] = watch.cpus = to
     if sampler is not None:
         sampler.report(args.stall_trace)
     if native_prof:
@@ -1275,6 +1292,8 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
                        "apiserver": affinity.cpu_layout(api_proc.cpus) if api_proc is not None else None},
         "cpu_busy_pct_rank0": res.get("cpu_busy_pct"),
         "relocated_rank0": res.get("relocated"),
+        # other tenants' CPUs on the rank's domain, every 4 timed steps (ContentionWatch)
+        "foreign_cpus_rank0": res.get("foreign_cpus"),
         "pods_per_s_first_filter_to_last_bind": out["value_burst_window"],
         # POST /scheduler/bind wall time as kube-scheduler's stand-in sees it (request written ->
         # reply read), every bind of the timed steps on all ranks

@@ -224,6 +224,73 @@ def quieter_domain(current: list[int], numa: int = -1, exclude: list[int] | None
     return best if cpus_busy(best) < here / 2 else None
 
 
+def proc_cpu_ns(pid: int) -> int:
+    """CPU time of every thread of process `pid`, ns (/proc/<pid>/task/*/schedstat)."""
+    total = 0
+    try:
+        tids = os.listdir(f"/proc/{pid}/task")
+    except OSError:
+        return 0
+    for tid in tids:
+        try:
+            with open(f"/proc/{pid}/task/{tid}/schedstat") as f:
+                total += int(f.read().split()[0])
+        except (OSError, ValueError, IndexError):
+            pass
+    return total
+
+
+class ContentionWatch:
+    """Other tenants' load on a process group's L3 domain while the group is busy: the
+    domain's hardware threads' busy time minus the group's own CPU time, between two calls
+    of `check()`. When it reaches `threshold_cpus`, `check()` returns the quietest other domain
+    on the same NUMA node (all of whose load is someone else's) if it carries under half as
+    much; the caller moves there (`relocate`). Cooperative: it never holds CPUs."""
+
+    def __init__(self, cpus: list[int], pids: list[int], numa: int = -1, exclude: list[int] | None = None,
+                 threshold_cpus: float = 0.5):
+        self.cpus, self.pids, self.numa = list(cpus), list(pids), numa
+        self.exclude = list(exclude or [])
+        self.threshold = threshold_cpus
+        self.last = None
+        self.hot = 0        # consecutive windows at or over the threshold (two are needed to move)
+        self.moves = 0      # at most two moves per run: no chasing a tenant around the node
+
+    def _sample(self):
+        return cpu_snapshot(), sum(proc_cpu_ns(p) for p in self.pids), time.perf_counter()
+
+    def check(self) -> tuple[float, list[int] | None]:
+        """(other tenants' CPUs on our domain since the last call, a domain to move to or None)."""
+        now = self._sample()
+        prev, self.last = self.last, now
+        if prev is None:
+            return 0.0, None
+        (a, own_a, t_a), (b, own_b, t_b) = prev, now
+        wall = t_b - t_a
+        if wall <= 0:
+            return 0.0, None
+        cur = domain_of(self.cpus) or list(self.cpus)
+        hw = list(cur) + smt_siblings(cur)
+        busy = busy_between(a, b, hw)
+        foreign = max(0.0, sum(busy.values()) - (own_b - own_a) / 1e9 / wall)
+        self.hot = self.hot + 1 if foreign >= self.threshold else 0
+        if self.hot < 2 or self.moves >= 2:
+            return foreign, None
+        doms = l3_domains()
+        if self.numa >= 0:
+            doms = [d for d in doms if numa_of_cpu(d[0]) == self.numa] or doms
+        avoid = set(self.exclude) | set(cur)
+        others = [d for d in doms if 0 not in d and not avoid.intersection(d)]
+        if not others:
+            return foreign, None
+        load = busy_between(a, b, [c for d in others for c in list(d) + smt_siblings(d)])
+        best = min(others, key=lambda d: (sum(load.get(c, 0.0) for c in list(d) + smt_siblings(d)), d[0]))
+        if sum(load.get(c, 0.0) for c in list(best) + smt_siblings(best)) >= foreign / 2:
+            return foreign, None
+        self.hot, self.moves = 0, self.moves + 1
+        return foreign, best
+
+
 def relocate(pids: list[int], cpus: list[int]) -> int:
     """Pins every thread of the processes `pids` to `cpus` (threads of a running process keep
     their own masks: each is set). Returns the threads moved."""

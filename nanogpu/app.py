@@ -55,7 +55,7 @@ class Config:
     assume_label: bool = True
     bind_first: bool = False                    # front door: a batch's binds before its filters
     spin_nap: bool = False                      # front door: sleep the busy-poll window, not poll it
-    batch_labels: bool = True                   # native writer: label PATCHes batched after bindings
+    batch_labels: bool = False                  # native writer: batch label PATCHes after bindings (off: pipelined)
     watch_assigned_only: bool = True            # pod informer: bound pods only (spec.nodeName!=)
     api_write_timeout_s: float = 30.0           # native bind writer: an API answer due within this
     reservation_ttl_s: float = 60.0

@@ -410,7 +410,7 @@ class NativeServer:
 
     def enable_native_writes(self, config, threads: int, retries: int, record_events: bool,
                              evented: bool = True, label: bool = True, timeout_s: float = 30.0,
-                             inline_io: bool = False, batch_labels: bool = True) -> bool:
+                             inline_io: bool = False, batch_labels: bool = False) -> bool:
         """Hands the bind's API writes to the front door's C++ writer threads (native/src/
         kubewriter.cpp) when the API server is a REST endpoint this process reaches with a
         bearer token or a client certificate; False (Python writes) otherwise."""

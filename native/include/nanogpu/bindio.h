@@ -86,9 +86,10 @@ class BindIo {
   uint64_t timeout_ns_ = 0;
   uint64_t scanned_at_ = 0;
   uint64_t timeouts_ = 0;
-  // Label PATCHes (the reference's assume label, guarded by spec.nodeName) go out after their
-  // binding answered, batched: up to kLabelBatch pipelined on one connection, one send and a
-  // read or two for all of them, held at most kLabelHoldNs for the batch to fill.
+  // Label PATCHes (the reference's assume label, guarded by spec.nodeName): pipelined behind
+  // their binding on its connection by default; with KubeWriter::set_batch_labels they go out
+  // after their binding answered, batched: up to kLabelBatch pipelined on one connection, one
+  // send and a read or two for all of them, held at most kLabelHoldNs for the batch to fill.
   static constexpr size_t kLabelBatch = 32;
   static constexpr uint64_t kLabelHoldNs = 500'000;
   std::vector<std::unique_ptr<Label>> lslots_;

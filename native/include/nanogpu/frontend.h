@@ -120,7 +120,7 @@ class Frontend {
   // loop and answers them itself (BindIo, bindio.h); else the writer's own io thread does.
   void set_kube_writer(const KubeTarget& t, int threads, int retries, bool record_events,
                        bool evented = true, bool label = true, double timeout_s = 30.0, bool inline_io = false,
-                       bool batch_labels = true);
+                       bool batch_labels = false);
   const KubeWriter* kube_writer() const { return writer_.load(std::memory_order_acquire); }
   // The native filter / priorities verb on a request body (what a worker runs per request);
   // false = the request needs the Python path.

@@ -174,7 +174,7 @@ class KubeWriter {
   void run_slow();
   void to_slow(SlowJob&& sj);    // the slow path takes it (or, once its threads are gone, the caller)
   bool inline_io_ = false;
-  std::atomic<bool> batch_labels_{true};   // evented: label PATCHes batched after their bindings (BindIo)
+  std::atomic<bool> batch_labels_{false};  // evented: label PATCHes batched after their bindings (BindIo)
   bool slow_gone_ = false;       // under mu_: the slow-path threads have exited
   bool evented_ = false;
   int max_inflight_ = 0;

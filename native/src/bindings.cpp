@@ -793,7 +793,7 @@ PYBIND11_MODULE(_native, m) {
           py::arg("token_file") = "", py::arg("ca_file") = "", py::arg("cert_file") = "", py::arg("key_file") = "",
           py::arg("insecure") = false, py::arg("threads") = 32, py::arg("retries") = 3,
           py::arg("record_events") = true, py::arg("evented") = true, py::arg("label") = true,
-          py::arg("timeout_s") = 30.0, py::arg("inline_io") = false, py::arg("batch_labels") = true,
+          py::arg("timeout_s") = 30.0, py::arg("inline_io") = false, py::arg("batch_labels") = false,
           "Binds whose reservation succeeded natively are finished natively (PATCH + binding + "
           "commit/rollback) on keep-alive connections to kube-apiserver: one epoll thread "
           "(evented) or `threads` blocking threads; `threads` x 8 binds in flight.")

@@ -134,3 +134,48 @@ def test_an_idle_job_leaves_a_domain_other_tenants_moved_onto(tmp_path, monkeypa
     assert A.quieter_domain([4, 5, 6, 7], 0, exclude=[8]) is None    # the API server's domain: not that one
     busy.update({c: 0.5 for c in (8, 9, 10, 11)})                    # the alternative is no better
     assert A.quieter_domain([4, 5, 6, 7], 0) is None
+
+
+def test_a_busy_job_moves_when_other_tenants_share_its_domain(tmp_path, monkeypatch):
+    """Mid-run: the domain's busy time minus the job's own CPU time is other tenants' load.
+    Two windows in a row at half a CPU or more and a domain carrying under half as much: move;
+    the job's own load never counts; at most two moves."""
+    import types
+
+    allowed = make_tree(tmp_path)
+    monkeypatch.setattr(A, "SYS_CPU", tmp_path)
+    real_l3, real_numa = A.l3_domains, A.numa_of_cpu
+    monkeypatch.setattr(A.os, "sched_getaffinity", lambda pid: allowed)
+    monkeypatch.setattr(A, "l3_domains", lambda allowed=None, root=tmp_path: real_l3(allowed, root))
+    monkeypatch.setattr(A, "numa_of_cpu", lambda cpu, root=tmp_path: real_numa(cpu, root))
+    clock = {"t": 0.0, "own": 0}
+    busy = {c: 0.0 for c in range(48)}
+    monkeypatch.setattr(A, "time", types.SimpleNamespace(perf_counter=lambda: clock["t"]))
+    monkeypatch.setattr(A, "cpu_snapshot", lambda: None)
+    monkeypatch.setattr(A, "busy_between", lambda a, b, cpus: {c: busy.get(c, 0.0) for c in cpus})
+    monkeypatch.setattr(A, "proc_cpu_ns", lambda pid: clock["own"])
+
+    w = A.ContentionWatch([4, 5, 6, 7], [1], numa=0, exclude=[12])
+
+    def window(own_cpus: float):     # 0.1 s in which the job itself used `own_cpus` CPUs
+        clock["t"] += 0.1
+        clock["own"] += int(own_cpus * 0.1e9)
+        return w.check()
+
+    assert w.check() == (0.0, None)
+    busy.update({c: 0.9 for c in (4, 5, 6, 7)})                       # the job's own 3.6 CPUs
+    f, to = window(3.6)
+    assert abs(f) < 1e-6 and to is None
+    busy.update({c + 24: 0.5 for c in (4, 5)})                         # a tenant on two siblings
+    f, to = window(3.6)
+    assert abs(f - 1.0) < 1e-6 and to is None                          # one window: not yet
+    f, to = window(3.6)
+    assert to == [8, 9, 10, 11]                                        # second: move (not CPU 0's, not the API server's)
+    busy.update({c: 0.3 for c in (8, 9, 10, 11)})                      # the job is there now (own load only)
+    w.cpus = to
+    for _ in range(3):
+        assert window(1.2)[1] is None
+    busy.update({c: 0.6 for c in (8, 9, 10, 11)})                      # 1.2 CPUs of foreign load...
+    busy.update({c: 0.4 for c in (16, 17, 18, 19, 20, 21, 22, 23)})    # ...and the rest of the socket
+    busy.update({c: 0.4 for c in (4, 5, 6, 7)})                        # is no quieter: stay
+    assert window(1.2)[1] is None and window(1.2)[1] is None

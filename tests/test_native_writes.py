@@ -19,12 +19,13 @@ from nanogpu.k8s.fake_apiserver import Faults, FakeKubeStore, serve
 from nanogpu.topology.model import synthetic_mi355x
 
 
-async def _stack(store, native):
-    """native: "evented" / "threads" (the C++ writer in that mode) or False (Python writes)."""
+async def _stack(store, native, batch_labels=False):
+    """native: "inline" / "evented" / "threads" (the C++ writer in that mode) or False (Python
+    writes); batch_labels: the evented driver's batched label PATCHes instead of pipelined ones."""
     runner, port = await serve(store)
     rt = Runtime(Config(kube_api=f"http://127.0.0.1:{port}", port=0, host="127.0.0.1",
                         policy_config_path="/nonexistent", native_bind_writes=bool(native),
-                        bind_writer_mode=native or "evented"))
+                        bind_writer_mode=native or "evented", batch_labels=batch_labels))
     await rt.start()
     return runner, rt
 
@@ -370,8 +371,10 @@ def test_no_assume_label_binds_with_one_api_write(native):
 @pytest.mark.parametrize("faults", [dict(patch_error_rate=1.0), dict(close_after_binding=True),
                                     dict(patch_error_rate=0.5, seed=3)])
 @pytest.mark.parametrize("mode", ["inline", "evented"])
-def test_pipelined_label_after_the_binding(faults, mode):
-    """The evented writer pipelines the label PATCH behind the binding on one connection and
+@pytest.mark.parametrize("batch", [False, True])
+def test_pipelined_label_after_the_binding(faults, mode, batch):
+    """The evented writer pipelines the label PATCH behind the binding on one connection (or,
+    batched, sends the label PATCHes of bound pods together after their bindings) and
     answers kube-scheduler when the binding lands. A label PATCH that fails (5xx), or never gets
     an answer because the server closed the connection after the binding's, is retried on the
     slow path: the bind stays a success and is never rolled back; a lasting label failure is
@@ -379,7 +382,7 @@ def test_pipelined_label_after_the_binding(faults, mode):
     async def main():
         store = FakeKubeStore(faults=Faults(**faults))
         store.add_node(pu.make_node("n0", 8, synthetic_mi355x(8).to_json()))
-        runner, rt = await _stack(store, mode)
+        runner, rt = await _stack(store, mode, batch)
         base = f"http://127.0.0.1:{rt.bound_port}"
         try:
             for i in range(6):
