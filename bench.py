@@ -149,7 +149,8 @@ def parse_args():
                     help="the extender's front door reserves a batch's binds before its filters")
     ap.add_argument("--no-relocate", action="store_true",
                     help="keep the rank on the L3 domain picked at start even when other tenants load it "
-                         "(by default, after the warm-up, a busy domain is left for a quieter one)")
+                         "(by default a busy domain is left for a quieter one after the warm-up, and during "
+                         "the timed steps when other tenants keep half a CPU of it busy)")
     ap.add_argument("--inproc-driver", action="store_true",
                     help="run the kube-scheduler stand-in inside the extender process (default: own process)")
     return ap.parse_args()
