@@ -1,6 +1,7 @@
 // The pod informer's watch, native side (see podwatch.h).
 #include "nanogpu/podwatch.h"
 
+#include <string.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <unistd.h>
@@ -52,7 +53,9 @@ bool filter_pod_event(PodWatchFilter& f, std::string_view line, json::Doc& d, st
       drop = f.ledger->lookup(std::string(field(d, md, "uid")), &rec);
       // the node agent rewrote the placement to what kubelet ran (plugin.reconcile): the
       // controller re-accounts it, so the event goes on
-      if (drop && line.find("\"nano-gpu/reconciled\"") != std::string_view::npos) drop = false;
+      // (memmem: string_view::find stops at every '"' of the event to compare the rest)
+      static constexpr char kReconciled[] = "\"nano-gpu/reconciled\"";
+      if (drop && memmem(line.data(), line.size(), kReconciled, sizeof kReconciled - 1) != nullptr) drop = false;
     }
   }
   if (drop) {

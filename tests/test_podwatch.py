@@ -228,3 +228,25 @@ def test_native_watch_over_ipv6_sends_a_bracketed_host_header():
         assert head.startswith("GET /api/v1/pods?watch=1&resourceVersion=100&")
 
     asyncio.run(main())
+
+
+def test_a_held_pod_the_node_agent_reconciled_goes_on_to_the_controller():
+    """A bound pod the ledger holds is dropped natively, unless the node agent rewrote its
+    placement (`nano-gpu/reconciled` annotation, agent/plugin.py): then the controller must
+    re-account it. The annotation can sit anywhere in a long event line."""
+    st = _state()
+    nid = st.node_ids(["n0"])[0]
+    wf = N.PodWatchFilter(st.ledger)
+    lines = []
+    for i, reconciled in enumerate([False, True, False, True]):
+        p = pu.make_pod(f"h{i}", [("main", 5)])
+        assert st.ledger.reserve(nid, pu.pod_uid(p), [(5, 0)], st.options)[0] == N.OK
+        p["spec"]["nodeName"] = "n0"
+        p["metadata"]["resourceVersion"] = str(200 + i)
+        p["metadata"]["labels"] = {"k\"q": "\"" * 200}            # many quotes before the annotations
+        p["metadata"]["annotations"] = {"a": "nano-gpu/reconciled-not"}
+        if reconciled:
+            p["metadata"]["annotations"]["nano-gpu/reconciled"] = "1"
+        lines.append(json.dumps({"type": "MODIFIED", "object": p}).encode())
+    kept = [e["object"]["metadata"]["name"] for e in wf.decode(b"\n".join(lines) + b"\n") if e["type"] == "MODIFIED"]
+    assert kept == ["h1", "h3"] and wf.dropped == 2
