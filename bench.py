@@ -614,7 +614,26 @@ async def wait_released(lookup, uids: list[str], timeout_s: float = 10.0) -> boo
     return await asyncio.get_running_loop().run_in_executor(None, poll)
 
 
-async def arecv(conn):
+class HarnessCpu:
+    """CPU the bench harness itself spends on the extender process's main thread (the stand-in's
+    step summary off the pipe, the frag measurement, the per-step records, the contention
+    watch): `with hc:` around synchronous harness code only. The extender's CPU per pod is
+    reported without it (a deployed extender runs none of it) and it is reported on its own."""
+
+    def __init__(self):
+        self.s = 0.0
+        self.t = 0.0
+
+    def __enter__(self):
+        self.t = time.thread_time()
+        return self
+
+    def __exit__(self, *exc):
+        self.s += time.thread_time() - self.t
+        return False
+
+
+async def arecv(conn, hc: HarnessCpu | None = None):
     """conn.recv() awaited on the event loop (the pipe's fd in the selector): no executor
     thread, whose start can wait milliseconds for the GIL while the loop is busy."""
     if not conn.poll():
@@ -631,7 +650,10 @@ async def arecv(conn):
             await fut
         finally:
             loop.remove_reader(fd)
-    return conn.recv()
+    if hc is None:
+        return conn.recv()
+    with hc:
+        return conn.recv()
 
 
 class ApiServerProc:
@@ -904,6 +926,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     overlap = apisrv is not None and not getattr(args, "no_overlap_create", False)
     created: dict = {}       # step -> its create, started during the previous step's release
     srv_ms: dict = {}        # step -> the API server's own create/delete time
+    hc = HarnessCpu()        # the harness's own CPU on the main thread (not the extender's)
 
     async def one_step_steady(step: int, timed: bool) -> dict:
         """Steady-state churn: this step's deletions (pods of earlier steps) and creations, the
@@ -915,7 +938,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
             (n_d, dt_d), (n_c, dt_c) = await apisrv.churn_keys(
                 [(f"bench-r{k % d.world}", f"k{k}") for k in dels], step)
             phases.update(delete_srv_ms=1e3 * dt_d, create_srv_ms=1e3 * dt_c)
-        uids = [steady_uid(k, k % d.world) for k in dels]
+        with hc:
+            uids = [steady_uid(k, k % d.world) for k in dels]
         if uids:
             await wait_released(rt.state.ledger.lookup, uids)
         phases["release_ms"] = 1e3 * (time.perf_counter() - t_step0)
@@ -923,8 +947,9 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
             await barrier()
         t_send = time.perf_counter()
         if drives:
-            conn.send(("step", step))
-            summary = await arecv(conn)
+            with hc:
+                conn.send(("step", step))
+            summary = await arecv(conn, hc)
         else:            # one scheduler: rank 0's stand-in schedules this rank's pods too
             from nanogpu.sim.driver import DriverStats
 
@@ -939,13 +964,14 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                 conn.send(("live", others))
         else:
             await barrier()
-        frag = rt.state.frag(min(SIZES))
-        phases.update(create_ms=0.0, schedule_ms=1e3 * summary["span_s"])
-        client_s = summary.pop("bind_s_all", [])
-        walls = rt.native.fe.take_bind_wall() if rt.native is not None else []
-        if timed:
-            results["client_bind_s"].extend(client_s)
-            results["frontdoor_bind_ms"].extend(1e3 * x for x in walls)
+        with hc:
+            frag = rt.state.frag(min(SIZES))
+            phases.update(create_ms=0.0, schedule_ms=1e3 * summary["span_s"])
+            client_s = summary.pop("bind_s_all", [])
+            walls = rt.native.fe.take_bind_wall() if rt.native is not None else []
+            if timed:
+                results["client_bind_s"].extend(client_s)
+                results["frontdoor_bind_ms"].extend(1e3 * x for x in walls)
         return {"stats": summary, "frag": frag, "phases": phases}
 
     async def one_step(step: int, timed: bool, nxt: int | None = None) -> dict:
@@ -974,8 +1000,9 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                 srv_ms.setdefault(step, {})["barrier_create_ms"] = 1e3 * (time.perf_counter() - tb)
             t_send = time.perf_counter()
             if drives:
-                conn.send(("step", step))
-                summary = await arecv(conn)
+                with hc:
+                    conn.send(("step", step))
+                summary = await arecv(conn, hc)
             else:            # one scheduler: rank 0's stand-in schedules this rank's pods too
                 from nanogpu.sim.driver import DriverStats
 
@@ -995,7 +1022,9 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         # all ranks finished their share of the burst: peak occupancy
         await barrier()
         srv_ms.setdefault(step, {})["barrier_peak_ms"] = 1e3 * (time.perf_counter() - ts)
-        frag = rt.state.frag(min(SIZES))
+        with hc:
+            frag = rt.state.frag(min(SIZES))
+            uids = [pu.pod_uid(p) for p in pods]
         t_frag = time.perf_counter()
         if store is not None:
             for p in pods:
@@ -1012,13 +1041,14 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
             srv_ms.setdefault(step, {}).update(delete_srv_ms=1e3 * dt_d, peak_ms=1e3 * (t_frag - ts),
                                                delete_rpc_ms=1e3 * (time.perf_counter() - t_frag))
         # the pod controller releases on DELETED; wait until our shares are gone
-        await wait_released(rt.state.ledger.lookup, [pu.pod_uid(p) for p in pods])
+        await wait_released(rt.state.ledger.lookup, uids)
         t_rel = time.perf_counter()
         if pod_ctrl is not None:
             await pod_ctrl.queue.drain(5.0)
         srv_ms.setdefault(step, {})["drain_ms"] = 1e3 * (time.perf_counter() - t_rel)
         if os.environ.get("NANOGPU_BENCH_DEBUG"):
             print(f"step {step} start {t_step0:.4f} release {ts:.4f} end {time.perf_counter():.4f}", file=sys.stderr)
+        hc.__enter__()
         phases = {"create_ms": 1e3 * tc, "schedule_ms": 1e3 * summary["span_s"],
                   "release_ms": 1e3 * (time.perf_counter() - ts)}
         phases.update(srv_ms.pop(step, {}))
@@ -1045,6 +1075,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
             diag["gc_max_ms"] = round(1e3 * gc_pause["max"], 2)
             gc_pause.update(sum=0.0, max=0.0, n=0)
             results.setdefault("diag", []).append(diag)
+        hc.__exit__(None, None, None)
         return {"stats": summary, "frag": frag, "phases": phases}
 
     from nanogpu.app import tune_gc
@@ -1109,6 +1140,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     nom0 = rt.state.ledger.nomination_counts()
     fe_stats = rt.native.fe.stats if rt.native is not None else (lambda: {})
     handoffs0 = fe_stats().get("bind_handoffs", 0)
+    hc.s = 0.0
     cpu0, loop_cpu0 = time.process_time(), time.thread_time()
     threads0, ticks0, times0 = thread_cpu(), thread_ticks(), os.times()
     from nanogpu import affinity
@@ -1131,7 +1163,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         results["frag"].append(r["frag"])
         results.setdefault("phases", []).append(r["phases"])
         if watch is not None and k % 4 == 3:
-            foreign, to = watch.check()
+            with hc:
+                foreign, to = watch.check()
             results["foreign_cpus"].append(round(foreign, 2))
             if to is not None:
                 affinity.relocate(pl["pids"], to)
@@ -1175,9 +1208,12 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     results["nodes_sent_per_filter"] = (round(sum(st.get("nodes_sent_filter", 0) for st in results["steps"]) / cycles, 1)
                                         if cycles else None)
     n_sched = max(1, sum(st["scheduled"] for st in results["steps"]))
-    results["cpu_us_per_pod"] = 1e6 * (time.process_time() - cpu0) / n_sched
+    harness_s = hc.s
+    results["cpu_us_per_pod"] = 1e6 * (time.process_time() - cpu0 - harness_s) / n_sched
+    results["harness_cpu_us_per_pod"] = 1e6 * harness_s / n_sched
     threads1, ticks1, times1 = thread_cpu(), thread_ticks(), os.times()
-    results["cpu_us_per_pod_by_thread"] = {g: round(1e6 * (threads1[g] - threads0.get(g, 0.0)) / n_sched, 1)
+    results["cpu_us_per_pod_by_thread"] = {g: round(1e6 * (threads1[g] - threads0.get(g, 0.0)
+                                                           - (harness_s if g == "main" else 0.0)) / n_sched, 1)
                                            for g in sorted(threads1)}
     # user / kernel split (10 ms ticks: about 1 % resolution over a 20-step run)
     results["cpu_us_per_pod_user_kernel"] = [round(1e6 * (times1.user - times0.user) / n_sched, 1),
@@ -1188,7 +1224,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         if (u1 - u0) + (k1 - k0) >= 5:
             kshare[g] = round(100.0 * (k1 - k0) / ((u1 - u0) + (k1 - k0)), 1)
     results["kernel_pct_by_thread"] = kshare
-    results["loop_cpu_us_per_pod"] = 1e6 * (time.thread_time() - loop_cpu0) / n_sched
+    results["loop_cpu_us_per_pod"] = 1e6 * (time.thread_time() - loop_cpu0 - harness_s) / n_sched
     # the Python part of each bind (API writes + commit): a sub-phase of the wall time
     binds = sorted(s["dur_ms"] for s in rt.tracer.dump(10 ** 9, "bind") if s["ok"])
     results["elapsed_s"] = elapsed
@@ -1321,8 +1357,10 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
         "schedule_ms_by_rank": out["schedule_ms_by_rank"],
         "bind_handoffs": out["bind_handoffs"],
         "step_diag_rank0": res.get("step_diag"),
-        # CPU time of the rank-0 extender process (all its threads) per pod it handled
+        # CPU time of the rank-0 extender process (all its threads) per pod it handled, without
+        # the bench harness's own work on its main thread (HarnessCpu, reported next to it)
         "extender_cpu_us_per_pod_rank0": round(res.get("cpu_us_per_pod", 0.0), 1),
+        "bench_harness_cpu_us_per_pod_rank0": round(res.get("harness_cpu_us_per_pod", 0.0), 2),
         "extender_loop_cpu_us_per_pod_rank0": round(res.get("loop_cpu_us_per_pod", 0.0), 1),
         "extender_cpu_us_per_pod_by_thread_rank0": res.get("cpu_us_per_pod_by_thread"),
         "extender_cpu_us_per_pod_user_kernel_rank0": res.get("cpu_us_per_pod_user_kernel"),
