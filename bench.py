@@ -119,6 +119,10 @@ def parse_args():
     ap.add_argument("--cpu-profile-out", default="",
                     help="native CPU sampling profile of the headline pass's timed steps (rank 0's "
                          "extender process, every thread, symbolized) as JSON into this file")
+    ap.add_argument("--io-tally", action="store_true",
+                    help="count and time the extender's system calls and hot phases by call site "
+                         "(native/include/nanogpu/iotally.h) over the headline pass's timed steps: "
+                         "io_per_pod_rank0 in the diagnostics (calls a pod, us a pod, ns a call)")
     ap.add_argument("--no-nominate", action="store_true", help="priorities do not nominate (Ledger::nominate)")
     ap.add_argument("--no-kube-combine", action="store_true",
                     help="the stand-in takes the extender's arg-max instead of kube-scheduler's plugin + "
@@ -1137,6 +1141,12 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         from nanogpu import _native
 
         native_prof = _native.sampler_start(1000)
+    io_tally = bool(args.io_tally and getattr(args, "_headline", False))
+    if io_tally:
+        from nanogpu import _native
+
+        _native.io_tally_reset()
+        _native.io_tally_enable(True)
     nom0 = rt.state.ledger.nomination_counts()
     fe_stats = rt.native.fe.stats if rt.native is not None else (lambda: {})
     handoffs0 = fe_stats().get("bind_handoffs", 0)
@@ -1173,6 +1183,11 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                 pl["cpus"] = watch.cpus = to
     if sampler is not None:
         sampler.report(args.stall_trace)
+    if io_tally:
+        from nanogpu import _native
+
+        _native.io_tally_enable(False)
+        results["io_tally"] = _native.io_tally()
     if native_prof:
         from nanogpu import _native
         from nanogpu.obs import cpu_profile
@@ -1210,6 +1225,9 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     n_sched = max(1, sum(st["scheduled"] for st in results["steps"]))
     harness_s = hc.s
     results["cpu_us_per_pod"] = 1e6 * (time.process_time() - cpu0 - harness_s) / n_sched
+    if "io_tally" in results:   # (calls, s) by call site -> calls a pod, us a pod, ns a call
+        results["io_per_pod"] = {k: [round(n / n_sched, 3), round(1e6 * sec / n_sched, 2), round(1e9 * sec / max(1, n))]
+                                 for k, (n, sec) in sorted(results.pop("io_tally").items())}
     results["harness_cpu_us_per_pod"] = 1e6 * harness_s / n_sched
     threads1, ticks1, times1 = thread_cpu(), thread_ticks(), os.times()
     results["cpu_us_per_pod_by_thread"] = {g: round(1e6 * (threads1[g] - threads0.get(g, 0.0)
@@ -1261,7 +1279,7 @@ HEADLINE_LAST = ("value_independent_schedulers", "frag_pct_steady_reference_mode
                  "extender_cpu_us_per_pod_rank0", "frag_pct_reference_model", "frag_hbm_pct", "frag_pct",
                  "p99_bind_ms", "p50_bind_ms", "pods_per_s_first_filter_to_last_bind", "value")
 # bulky per-step / per-thread records: --json-out only
-DIAG_KEYS = ("step_diag_rank0", "schedule_ms_each_step_rank0", "phase_ms_per_step_rank0",
+DIAG_KEYS = ("step_diag_rank0", "io_per_pod_rank0", "schedule_ms_each_step_rank0", "phase_ms_per_step_rank0",
              "extender_cpu_us_per_pod_by_thread_rank0", "extender_kernel_pct_by_thread_rank0",
              "extender_cpu_us_per_pod_user_kernel_rank0", "frag_pct_steady_each_step", "nominations",
              "nominations_steady", "native_verb_mean_us", "frag_reference_model_source", "host_selection",
@@ -1366,6 +1384,8 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
         "extender_cpu_us_per_pod_user_kernel_rank0": res.get("cpu_us_per_pod_user_kernel"),
         "extender_kernel_pct_by_thread_rank0": res.get("kernel_pct_by_thread"),
     }
+    if res.get("io_per_pod") is not None:
+        full["io_per_pod_rank0"] = res["io_per_pod"]
     full.update(reference_model_frag(args, topo))
     if variant is not None:
         tag = f"rtt{args.rtt_variant_ms:g}ms"

@@ -23,6 +23,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "nanogpu/iotally.h"
 #include "nanogpu/alloc.h"
 #include "nanogpu/kubewriter.h"
 #include "nanogpu/ledger.h"
@@ -156,7 +157,7 @@ class Frontend {
   bool handle_native(Worker* w, Conn* c, std::string_view method, std::string_view path, std::string_view body,
                      std::string* out);
   void defer(Worker* w, Conn* c, std::string method, std::string path, std::string query, std::string body);
-  void flush(Worker* w, Conn* c);
+  void flush(Worker* w, Conn* c, int io_kind = kFeSendOther);
   void close_conn(Worker* w, Conn* c);
   void put_pod(std::string_view uid, CachedPod pod);
   bool has_pod(std::string_view uid) const;

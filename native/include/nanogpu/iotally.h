@@ -1,0 +1,88 @@
+// Per-call-site tally of the extender's system calls and hot phases: how many times each ran
+// and how long it took (TSC ticks), process-wide. The sampler (sampler.h) says which functions
+// the CPU time lands in; this says how much each kind of call costs on the box and how many of
+// them a pod takes, which is what separates the protocol's floor (the HTTP exchanges and API
+// writes every pod needs) from work that can go. Off unless switched on (bench.py
+// --io-tally); when off a site costs one relaxed load.
+#pragma once
+
+#include <x86intrin.h>
+
+#include <atomic>
+#include <cstdint>
+
+namespace nanogpu {
+
+enum IoKind : int {
+  // front-door worker threads
+  kFeSpinEmpty,     // polling epoll_wait that found nothing (the busy poll)
+  kFeSpinHit,       // polling epoll_wait that returned events
+  kFeWait,          // blocking epoll_wait (time includes sleep: count only is CPU-meaningful)
+  kFeRecv,          // recv() of a kube-scheduler request
+  kFeSendCycle,     // send() of a filter / priorities answer
+  kFeSendOther,     // send() of any other answer (binds, Python's)
+  kFeEfdRead,       // mailbox eventfd read
+  kFeSubmit,        // bind handed to the writer (queue + eventfd write when it sleeps)
+  kFeParseBind,     // bind arguments parsed, pod looked up, reserve
+  kFeVerb,          // filter / priorities verb (JSON in, answer out)
+  // bind writer thread (evented) / BindIo
+  kWrWait,          // epoll_wait (count only)
+  kWrEfdRead,
+  kWrSend,          // one send() of a bind's pipelined binding + label PATCH
+  kWrRecv,          // recv() of API answers
+  kWrBuild,         // binding / label request bodies built
+  kWrCommit,        // ledger commit + answer posted to the front door
+  // pod watch thread
+  kPwRecv,          // blocking read of watch bytes (count only)
+  kPwFilter,        // one event line through the filter
+  kIoKinds
+};
+
+inline const char* io_kind_name(int k) {
+  static const char* const names[kIoKinds] = {
+      "fe_spin_empty", "fe_spin_hit", "fe_wait", "fe_recv", "fe_send_cycle", "fe_send_other", "fe_efd_read",
+      "fe_submit", "fe_parse_bind", "fe_verb", "wr_wait", "wr_efd_read", "wr_send", "wr_recv",
+      "wr_build", "wr_commit", "pw_recv", "pw_filter"};
+  return k >= 0 && k < kIoKinds ? names[k] : "?";
+}
+
+struct IoTally {
+  std::atomic<bool> on{false};
+  // one cache line per kind: the kinds belong to different threads
+  struct alignas(64) Slot {
+    std::atomic<uint64_t> n{0}, ticks{0};
+  };
+  Slot s[kIoKinds];
+  void add(int k, uint64_t ticks) {
+    s[k].n.fetch_add(1, std::memory_order_relaxed);
+    s[k].ticks.fetch_add(ticks, std::memory_order_relaxed);
+  }
+  void reset() {
+    for (auto& x : s) x.n.store(0, std::memory_order_relaxed), x.ticks.store(0, std::memory_order_relaxed);
+  }
+};
+
+inline IoTally g_io;
+
+// RAII: times the enclosing scope into kind k when the tally is on
+struct IoTimer {
+  int k;
+  uint64_t t0;
+  explicit IoTimer(int kind) : k(kind), t0(g_io.on.load(std::memory_order_relaxed) ? __rdtsc() : 0) {}
+  ~IoTimer() {
+    if (t0) g_io.add(k, __rdtsc() - t0);
+  }
+  IoTimer(const IoTimer&) = delete;
+  IoTimer& operator=(const IoTimer&) = delete;
+};
+
+// the same by hand, where the kind is known only afterwards
+inline uint64_t io_t0() { return g_io.on.load(std::memory_order_relaxed) ? __rdtsc() : 0; }
+inline void io_end(int k, uint64_t t0) {
+  if (t0) g_io.add(k, __rdtsc() - t0);
+}
+
+// ns per TSC tick (calibrated by the front door; 0 when the TSC is not invariant)
+double io_ns_per_tick();
+
+}  // namespace nanogpu

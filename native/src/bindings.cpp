@@ -8,6 +8,7 @@
 #include <unordered_set>
 #include <vector>
 
+#include "nanogpu/iotally.h"
 #include "nanogpu/alloc.h"
 #include "nanogpu/apiserver.h"
 #include "nanogpu/frontend.h"
@@ -908,6 +909,18 @@ PYBIND11_MODULE(_native, m) {
            "Runs the native verb `iters` times in place (no socket): (ok, seconds per call, last body).")
       .def("reset_max", &Frontend::reset_max, "zero the per-verb and event-loop maxima");
   m.def("mono_now", &mono_now);
+  m.def("io_tally_enable", [](bool on) { g_io.on.store(on, std::memory_order_relaxed); }, py::arg("on"),
+        "Switches the per-call-site system-call / phase tally (iotally.h) on or off.");
+  m.def("io_tally_reset", []() { g_io.reset(); }, "Zeroes the tally.");
+  m.def("io_tally", []() {
+    const double r = io_ns_per_tick();
+    py::dict out;
+    for (int k = 0; k < kIoKinds; ++k) {
+      const uint64_t n = g_io.s[k].n.load(std::memory_order_relaxed);
+      if (n) out[io_kind_name(k)] = py::make_tuple(n, 1e-9 * r * static_cast<double>(g_io.s[k].ticks.load(std::memory_order_relaxed)));
+    }
+    return out;
+  }, "{kind: (calls, seconds)} since the last reset (kinds with calls only).");
   m.def("sampler_start", &sampler::start, py::arg("hz") = 1000,
         "CPU sampling profiler: SIGPROF every 1/hz s of process CPU time (false: already running).");
   m.def("sampler_stop", []() {

@@ -2,6 +2,7 @@
 #include "nanogpu/frontend.h"
 
 #include "nanogpu/bindio.h"
+#include "nanogpu/iotally.h"
 
 #include <arpa/inet.h>
 #include <fcntl.h>
@@ -82,6 +83,15 @@ uint64_t fast_ns() {
   if (c.ns_per_tick == 0.0) return now_ns();
   return c.ns0 + static_cast<uint64_t>(static_cast<double>(__rdtsc() - c.tick0) * c.ns_per_tick);
 }
+
+}  // namespace
+
+double io_ns_per_tick() {
+  const double r = tsc_clock().ns_per_tick;
+  return r > 0.0 ? r : 1.0;
+}
+
+namespace {
 
 bool ieq(std::string_view a, std::string_view b) {
   if (a.size() != b.size()) return false;
@@ -817,6 +827,7 @@ void Frontend::run(Worker* w) {
     }
     BindIo* bio = w->bio.load(std::memory_order_acquire);
     int n;
+    const uint64_t io0 = io_t0();
     if (nap) {
       const timespec ts{0, static_cast<long>(static_cast<uint64_t>(spin) - (t_now - since))};
       n = epoll_pwait2(w->ep, evs, 128, &ts, nullptr);
@@ -824,6 +835,7 @@ void Frontend::run(Worker* w) {
       // with bind answers due, wake at least for the BindIo's deadline scan
       n = epoll_wait(w->ep, evs, 128, polling ? 0 : bio && bio->labels_waiting() ? 1 : bio && bio->inflight() ? 100 : 200);
     }
+    io_end(polling && !nap ? (n > 0 ? kFeSpinHit : kFeSpinEmpty) : kFeWait, io0);
     w->parked.store(false, std::memory_order_relaxed);
     const uint64_t t_batch = n > 0 ? fast_ns() : 0;
     if (n > 0) {
@@ -861,7 +873,10 @@ void Frontend::run(Worker* w) {
         }
       } else if (tag == 1) {
         uint64_t v;
-        (void)!read(w->efd, &v, sizeof(v));
+        {
+          IoTimer it{kFeEfdRead};
+          (void)!read(w->efd, &v, sizeof(v));
+        }
         drain_mailbox();
       } else if (!(tag >> 63) && (tag & kBioTag)) {
         // API answers after this batch's scheduling-cycle requests: a bind's answer only ends
@@ -962,7 +977,11 @@ bool Frontend::read_in(Worker* w, Conn* c, bool* eof) {
   char buf[65536];
   *eof = false;
   for (;;) {
-    const ssize_t r = recv(c->fd, buf, sizeof(buf), 0);
+    ssize_t r;
+    {
+      IoTimer it{kFeRecv};
+      r = recv(c->fd, buf, sizeof(buf), 0);
+    }
     if (r > 0) {
       if (c->in.empty()) c->t_in_ns = fast_ns();
       c->in.append(buf, static_cast<size_t>(r));
@@ -1090,7 +1109,7 @@ void Frontend::process(Worker* w, Conn* c) {
     }
     if (handle_native(w, c, method, path, body, &c->out)) {   // the answer lands in c->out
       c->in.erase(0, consumed);
-      flush(w, c);
+      flush(w, c, kFeSendCycle);
       w->cycle_reply_ns = fast_ns();   // the scheduling cycle's next request is due: spin for it
       if (!w->conns.count(id)) return;
     } else {
@@ -1105,7 +1124,10 @@ void Frontend::defer(Worker* w, Conn* c, std::string method, std::string path, s
   PyRequest r;
   r.id = make_id(w->idx, c->id);
   if (method == "POST" && path == "/scheduler/bind" && serving()) {
-    prepare_bind(body, &r);
+    {
+      IoTimer it{kFeParseBind};
+      prepare_bind(body, &r);
+    }
     KubeWriter* kw = writer_.load(std::memory_order_acquire);
     BindIo* bio = w->bio.load(std::memory_order_acquire);
     if (kw && r.bind.ok && (r.bind.rc == kOk || r.bind.rc == kOkExisting) && (bio || !kw->inline_io())) {
@@ -1124,6 +1146,7 @@ void Frontend::defer(Worker* w, Conn* c, std::string method, std::string path, s
       c->bind_waiting = true;
       c->t_req_ns = c->t_in_ns ? c->t_in_ns : fast_ns();
       c->t_in_ns = c->in.empty() ? 0 : fast_ns();
+      IoTimer it{kFeSubmit};
       if (bio) bio->submit(std::move(j));   // sent by pump() after this batch of events
       else kw->submit(std::move(j));
       return;
@@ -1148,9 +1171,13 @@ void Frontend::defer(Worker* w, Conn* c, std::string method, std::string path, s
   (void)!write(py_efd_, &one, sizeof(one));
 }
 
-void Frontend::flush(Worker* w, Conn* c) {
+void Frontend::flush(Worker* w, Conn* c, int io_kind) {
   while (c->out_off < c->out.size()) {
-    const ssize_t n = send(c->fd, c->out.data() + c->out_off, c->out.size() - c->out_off, MSG_NOSIGNAL);
+    ssize_t n;
+    {
+      IoTimer it{io_kind};
+      n = send(c->fd, c->out.data() + c->out_off, c->out.size() - c->out_off, MSG_NOSIGNAL);
+    }
     if (n > 0) {
       c->out_off += static_cast<size_t>(n);
       continue;
@@ -1197,6 +1224,7 @@ bool Frontend::handle_native(Worker* w, Conn* c, std::string_view method, std::s
   if (!prio && path != "/scheduler/filter") return false;
   const uint64_t t0 = fast_ns();
   thread_local std::string resp;   // keeps its capacity: no allocation per request
+  IoTimer it{kFeVerb};
   if (!filter_verb(body, prio, &resp)) return false;
   (prio ? prio_stats : filter_stats).observe(fast_ns() - t0);
   constexpr std::string_view kHead = "HTTP/1.1 200 OK\r\nContent-Type: application/json; charset=utf-8\r\nContent-Length: ";

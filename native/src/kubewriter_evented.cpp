@@ -33,6 +33,7 @@
 #include <vector>
 
 #include "nanogpu/bindio.h"
+#include "nanogpu/iotally.h"
 #include "nanogpu/kubewriter.h"
 
 namespace nanogpu {
@@ -277,6 +278,7 @@ void BindIo::complete(int64_t s) {
     st.inflight.fetch_sub(1, std::memory_order_relaxed);
     return;
   }
+  IoTimer it{kWrCommit};
   const bool ok2 = ok2xx(jb->sb) && (jb->batch_label || ok2xx(jb->sp));
   if (!jb->answered) st.binding_ns.fetch_add(ns_now() - jb->j.t0_ns, std::memory_order_relaxed);
   if (ok2) {
@@ -319,6 +321,7 @@ void BindIo::deliver(Conn& c, int status, std::string body) {
     // bound, with the placement annotations: kube-scheduler's bind is answered now; the
     // label PATCH behind it is the reference's selector contract only (a failure there goes
     // to the slow path's label retry, never to a rollback)
+    IoTimer it{kWrCommit};
     jb.answered = true;
     KubeWriterStats& st = kw_->stats;
     st.binding_ns.fetch_add(ns_now() - jb.j.t0_ns, std::memory_order_relaxed);
@@ -390,7 +393,10 @@ void BindIo::drive(size_t k, uint32_t events) {
           }
           w = r;
         } else {
-          w = ::send(c.fd, c.out.data() + c.off, c.out.size() - c.off, MSG_NOSIGNAL);
+          {
+            IoTimer it{kWrSend};
+            w = ::send(c.fd, c.out.data() + c.off, c.out.size() - c.off, MSG_NOSIGNAL);
+          }
           if (w < 0 && errno == EINTR) continue;
           if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) return;
           if (w <= 0) return fail(k, "connection to the API server failed");
@@ -416,7 +422,10 @@ void BindIo::drive(size_t k, uint32_t events) {
             break;
           }
         } else {
-          r = ::recv(c.fd, tmp, sizeof tmp, 0);
+          {
+            IoTimer it{kWrRecv};
+            r = ::recv(c.fd, tmp, sizeof tmp, 0);
+          }
           if (r < 0 && errno == EINTR) continue;
           if (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
           if (r <= 0) {
@@ -520,7 +529,10 @@ void BindIo::start_waiting() {
     auto jb = std::make_unique<Job>();
     jb->j = std::move(waiting_.front());
     waiting_.pop_front();
-    kw_->build(jb->j, &jb->patch, &jb->binding);
+    {
+      IoTimer it{kWrBuild};
+      kw_->build(jb->j, &jb->patch, &jb->binding);
+    }
     if (!kw_->label_) {   // the binding alone carries the annotations
       jb->left = 1;
       jb->sp = 200;
@@ -740,12 +752,15 @@ void KubeWriter::io_loop() {
     io_parked_.store(true, std::memory_order_seq_cst);
     const bool queued = !stopping && q_len_.load(std::memory_order_seq_cst) > 0;
     // with answers due, wake for the deadline scan
+    const uint64_t io0 = io_t0();
     const int n = epoll_wait(ep, evs, 256,
                              queued ? 0 : stopping || io.labels_waiting() ? 1 : io.inflight() ? 100 : 1000);
+    io_end(kWrWait, io0);
     io_parked_.store(false, std::memory_order_relaxed);
     for (int e = 0; e < n; ++e) {
       if (evs[e].data.u64 == UINT64_MAX) {
         uint64_t v;
+        IoTimer it{kWrEfdRead};
         (void)!::read(efd_, &v, sizeof v);
         continue;
       }

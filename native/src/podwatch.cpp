@@ -1,6 +1,8 @@
 // The pod informer's watch, native side (see podwatch.h).
 #include "nanogpu/podwatch.h"
 
+#include "nanogpu/iotally.h"
+
 #include <string.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
@@ -164,7 +166,12 @@ void PodWatchStream::run() {
   json::Doc d;
   for (;;) {
     const size_t had = buf.size();
-    const long r = c.stream_read(&buf);
+    long r;
+    {
+      const uint64_t io0 = io_t0();
+      r = c.stream_read(&buf);
+      io_end(kPwRecv, io0);
+    }
     if (r == 0) return finish(kEnded, 200, "");
     if (r < 0) return finish(stop_ ? kEnded : kTransportError, 0, "watch stream failed");
     bool dropped = false;
@@ -177,6 +184,7 @@ void PodWatchStream::run() {
       if (line.empty()) continue;
       bool keep;
       try {
+        IoTimer it{kPwFilter};
         keep = filter_pod_event(*f_, line, d, &rv);
       } catch (const std::invalid_argument&) {
         return finish(kTransportError, 0, "bad watch event line");

@@ -832,3 +832,31 @@ def test_ambiguous_request_framing_is_refused():
             await rt.stop()
 
     asyncio.run(main())
+
+
+def test_io_tally_counts_the_front_door_calls_of_a_cycle():
+    """bench.py --io-tally: with the tally on, one filter + priorities exchange shows up as
+    recv / verb / cycle-send calls at their sites; off, nothing is counted."""
+    async def main():
+        store, rt = await _runtime(2)
+        loop = asyncio.get_running_loop()
+        try:
+            pod = store.create_pod(pu.make_pod("t0", [("c0", 25, 0)]))
+            raw = _dumps({"Pod": pod, "Nodes": None, "NodeNames": ["n0", "n1"]})
+            reqs = [("POST", "/scheduler/filter", raw), ("POST", "/scheduler/priorities", raw)]
+            N.io_tally_reset()
+            await loop.run_in_executor(None, _http, rt.bound_port, reqs)
+            assert N.io_tally() == {}
+            N.io_tally_enable(True)
+            try:
+                got = await loop.run_in_executor(None, _http, rt.bound_port, reqs)
+            finally:
+                N.io_tally_enable(False)
+            assert [s for s, _ in got] == [200, 200]
+            t = N.io_tally()
+            assert t["fe_verb"][0] == 2 and t["fe_send_cycle"][0] == 2, t
+            assert t["fe_recv"][0] >= 1 and all(sec >= 0.0 for _, sec in t.values()), t
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
