@@ -126,6 +126,8 @@ class Frontend {
   // The native filter / priorities verb on a request body (what a worker runs per request);
   // false = the request needs the Python path.
   bool filter_verb(std::string_view body, bool prioritize, std::string* out);
+  struct VerbScratch;   // a worker's per-request scratch (frontend.cpp)
+  bool filter_verb(std::string_view body, bool prioritize, std::string* out, VerbScratch& s);
 
   VerbStats filter_stats, prio_stats, py_stats, bind_stats;   // bind_stats: native reserve half
   std::atomic<uint64_t> connections{0}, requests{0};

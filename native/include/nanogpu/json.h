@@ -31,6 +31,9 @@ struct Node {
 class Doc {
  public:
   bool parse(std::string_view src);
+  // One value at the start of `src` (leading whitespace skipped); `*end` gets the offset just
+  // past it. Whatever follows is the caller's business (a member of an enclosing document).
+  bool parse_prefix(std::string_view src, size_t* end);
   // Objects and arrays nested deeper than `max_depth` (the root is depth 0) are checked for
   // balanced brackets and well-formed strings but get no child nodes: they read as empty,
   // and raw() still spans their text. For readers that need a few shallow fields of a large

@@ -891,6 +891,19 @@ PYBIND11_MODULE(_native, m) {
         d["phase_max_s"] = ph;
         return d;
       })
+      .def("verb",
+           [](Frontend& f, const py::bytes& body, bool prioritize) {
+             const std::string b = body;
+             std::string out;
+             bool ok;
+             {
+               py::gil_scoped_release nogil;
+               ok = f.filter_verb(b, prioritize, &out);
+             }
+             return py::make_tuple(ok, ok ? out : std::string());
+           },
+           py::arg("body"), py::arg("prioritize"),
+           "The native filter / priorities verb on one body: (answered natively, answer JSON).")
       .def("time_verb",
            [](Frontend& f, const py::bytes& body, bool prioritize, int iters) {
              const std::string b = body;

@@ -408,6 +408,62 @@ struct PhaseTimer {
 };
 }  // namespace
 
+namespace {
+// priorities follows its cycle's filter with the same Pod text on the same connection, so on
+// the same worker: the pod a worker parsed last is reused when the text is identical (demand,
+// identity, containers); only the learned-owner flag is read again
+struct LastPod {
+  std::string raw, uid;
+  Demand dem{};
+  CachedPod cached;
+  bool mb_annotated = false;
+  bool valid = false;
+};
+
+// The node lists of the last kListSlots distinct texts a worker resolved (LRU). With
+// kube-scheduler's node sampling (numFeasibleNodesToFind from a rotating start) the list is a
+// window of the cluster that moves every cycle, but the windows repeat: 1000 nodes sampled 420
+// at a time cycle through 50 of them, so a few dozen slots catch them all. A slot is found by
+// its text alone (length, then bytes; the last slot used is tried first): no hash pass over the
+// list.
+constexpr int kListSlots = 64;
+struct IdCache {
+  const Ledger* owner = nullptr;
+  bool valid[kListSlots] = {};         // an escape-free list whose ids can be reused
+  uint64_t epoch[kListSlots] = {};     // the ledger's node epoch the ids were checked at
+  uint64_t used[kListSlots] = {};
+  size_t len[kListSlots] = {};
+  bool compact[kListSlots] = {};       // the text is `["a","b",...]` exactly: a reply may copy it whole
+  std::vector<int32_t> ids[kListSlots];
+  std::vector<std::pair<uint32_t, uint32_t>> tok[kListSlots];   // token (offset, length) in the list text
+  std::string text[kListSlots];        // the list text itself
+  int mru = 0;
+  uint64_t clock = 0;
+  int find(std::string_view t) const {
+    if (valid[mru] && len[mru] == t.size() && std::memcmp(text[mru].data(), t.data(), t.size()) == 0) return mru;
+    for (int k = 0; k < kListSlots; ++k)
+      if (valid[k] && len[k] == t.size() && std::memcmp(text[k].data(), t.data(), t.size()) == 0) return k;
+    return -1;
+  }
+};
+}  // namespace
+
+// A front-door worker's scratch for the verbs: DOMs, name views, result arrays, the last pod
+// and the node-list cache keep their capacity from one request to the next (every cycle of a
+// burst sends the same-sized bodies). Owned by the worker and handed down, not thread_local:
+// in a shared library every thread_local access is a __tls_get_addr call (10 % of the verbs'
+// samples when they were thread_local).
+struct Frontend::VerbScratch {
+  json::Doc top, d, other, dn;
+  std::vector<std::string_view> nv, nraw;
+  std::vector<int32_t> rcs, scores;
+  LastPod last;
+  IdCache idc;
+  NameTable nid;
+  std::deque<std::string> requoted;
+  std::string blob, dstr, resp;
+};
+
 // ------------------------------------------------------------------------------ plumbing
 struct Frontend::Conn {
   int fd = -1;
@@ -445,6 +501,7 @@ struct Frontend::Worker {
   std::atomic<bool> mb_pending{false};
   uint64_t next_conn = 1;
   uint64_t cycle_reply_ns = 0;   // last filter / priorities reply handed to the kernel
+  VerbScratch scratch;           // the verbs' per-request scratch (this worker's thread only)
 };
 
 static uint64_t make_id(int worker, uint64_t conn) { return (conn << 8) | static_cast<uint64_t>(worker); }
@@ -1217,15 +1274,14 @@ void Frontend::close_conn(Worker* w, Conn* c) {
 // ------------------------------------------------------------------------------ verbs
 bool Frontend::handle_native(Worker* w, Conn* c, std::string_view method, std::string_view path,
                              std::string_view body, std::string* out) {
-  (void)w;
   (void)c;
   if (method != "POST" || !serving()) return false;
   const bool prio = path == "/scheduler/priorities";
   if (!prio && path != "/scheduler/filter") return false;
   const uint64_t t0 = fast_ns();
-  thread_local std::string resp;   // keeps its capacity: no allocation per request
+  std::string& resp = w->scratch.resp;   // keeps its capacity: no allocation per request
   IoTimer it{kFeVerb};
-  if (!filter_verb(body, prio, &resp)) return false;
+  if (!filter_verb(body, prio, &resp, w->scratch)) return false;
   (prio ? prio_stats : filter_stats).observe(fast_ns() - t0);
   constexpr std::string_view kHead = "HTTP/1.1 200 OK\r\nContent-Type: application/json; charset=utf-8\r\nContent-Length: ";
   char len[24];
@@ -1239,56 +1295,103 @@ bool Frontend::handle_native(Worker* w, Conn* c, std::string_view method, std::s
 }
 
 bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* out) {
-  // per-thread scratch: the DOM, the name views and the result arrays keep their capacity
-  // from one request to the next (every cycle of a burst sends the same-sized bodies)
-  thread_local json::Doc top, d;
-  thread_local std::vector<std::string_view> nv;
-  thread_local std::vector<int32_t> rcs, scores;
-  // The body's top level only (Pod and NodeNames stay unparsed text), then the Pod on its own
-  // (`d`); the node-name list is parsed only when this worker has not seen that exact text.
-  if (body.empty() || !top.parse_shallow(body, 1)) return false;
-  const int32_t root = top.root();
-  if (!top.is(root, json::Type::kObj)) return false;
-  const int32_t names = top.get(root, "NodeNames", true);
-  if (!top.is(names, json::Type::kArr)) return false;     // null / Nodes-only: Python path
-  const int32_t pod_top = top.get(root, "Pod", true);
-  // any other member that is an object or array was only bracket-checked: the whole body
-  // must be valid JSON, as for the Python verb (which answers 400 otherwise)
-  for (int32_t c = top.at(root).first; c >= 0; c = top.at(c).next) {
-    if (c == names || c == pod_top) continue;
-    if (top.is(c, json::Type::kObj) || top.is(c, json::Type::kArr)) {
-      thread_local json::Doc other;
-      if (!other.parse(top.raw(c))) return false;
+  thread_local VerbScratch s;   // callers off the workers (tests, time_verb)
+  return filter_verb(body, prioritize, out, s);
+}
+
+bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* out, VerbScratch& s) {
+  json::Doc& top = s.top;
+  json::Doc& d = s.d;
+  std::vector<std::string_view>& nv = s.nv;
+  std::vector<std::string_view>& nraw = s.nraw;
+  std::vector<int32_t>& rcs = s.rcs;
+  std::vector<int32_t>& scores = s.scores;
+  LastPod& last = s.last;
+  IdCache& idc = s.idc;
+  if (idc.owner != ledger_.get()) idc = IdCache{}, idc.owner = ledger_.get();
+  if (body.empty()) return false;
+  // kube-scheduler's ExtenderArgs as Go's encoding/json writes them (struct field order, no
+  // spaces): {"Pod":{...},"Nodes":null,"NodeNames":[...]}. In that exact layout the pod's text
+  // is found by comparing it with the last pod's (priorities, and every retry, sends the same
+  // text) or by parsing it where it starts, and the node list runs to the closing brace: no
+  // pass over the body just to find where its members end. Any other layout takes the general
+  // path below (a shallow parse of the top level, then the members).
+  constexpr std::string_view kHead = "{\"Pod\":", kMid = ",\"Nodes\":null,\"NodeNames\":";
+  std::string_view pod_text, raw_names;
+  bool framed = false, reused = false, has_pod_text = false;
+  bool scanned = false;   // nv / nraw hold raw_names' names (a list not in the cache)
+  int found = -2;         // the list's cache slot when the framing looked it up (-1: none)
+  int32_t pod = -1;
+  nv.clear();
+  nraw.clear();
+  if (body.size() > kHead.size() + kMid.size() + 4 && body.compare(0, kHead.size(), kHead) == 0 &&
+      body[kHead.size()] == '{' && body.back() == '}') {
+    const std::string_view rest = body.substr(kHead.size());
+    size_t pe = 0;
+    bool same = false;
+    if (last.valid && rest.size() > last.raw.size() && std::memcmp(rest.data(), last.raw.data(), last.raw.size()) == 0) {
+      pe = last.raw.size();
+      same = true;
+    } else if (!d.parse_prefix(rest, &pe) || !d.is(d.root(), json::Type::kObj)) {
+      pe = 0;
+    }
+    if (pe) {
+      const std::string_view tail = rest.substr(pe);
+      if (tail.size() > kMid.size() + 2 && tail.compare(0, kMid.size(), kMid) == 0 && tail[kMid.size()] == '[' &&
+          tail[tail.size() - 2] == ']') {
+        raw_names = tail.substr(kMid.size(), tail.size() - kMid.size() - 1);
+        // the list must be one: a cached text, or a compact string array scanned whole
+        // (anything else, members after it included, goes the general way)
+        found = idc.find(raw_names);
+        framed = found >= 0 || (scanned = scan_string_array(raw_names, &nv, &nraw));
+        if (framed) {
+          has_pod_text = true;
+          pod_text = rest.substr(0, pe);
+          reused = same;
+          if (!same) pod = d.root();
+        } else {
+          nv.clear();
+          nraw.clear();
+        }
+      }
     }
   }
-  // priorities follows its cycle's filter with the same Pod text on the same connection, so
-  // on the same worker: the pod this thread parsed last is reused when the text is identical
-  // (demand, identity, containers); only the learned-owner flag is read again (below)
-  struct LastPod {
-    std::string raw, uid;
-    Demand dem{};
-    CachedPod cached;
-    bool mb_annotated = false;
-    bool valid = false;
-  };
-  thread_local LastPod last;
-  int32_t pod = -1;
+  if (!framed) {
+    // The body's top level only (Pod and NodeNames stay unparsed text), then the Pod on its own
+    // (`d`); the node-name list is parsed only when this worker has not seen that exact text.
+    if (!top.parse_shallow(body, 1)) return false;
+    const int32_t root = top.root();
+    if (!top.is(root, json::Type::kObj)) return false;
+    const int32_t names = top.get(root, "NodeNames", true);
+    if (!top.is(names, json::Type::kArr)) return false;     // null / Nodes-only: Python path
+    const int32_t pod_top = top.get(root, "Pod", true);
+    // any other member that is an object or array was only bracket-checked: the whole body
+    // must be valid JSON, as for the Python verb (which answers 400 otherwise)
+    for (int32_t c = top.at(root).first; c >= 0; c = top.at(c).next) {
+      if (c == names || c == pod_top) continue;
+      if (top.is(c, json::Type::kObj) || top.is(c, json::Type::kArr)) {
+        if (!s.other.parse(top.raw(c))) return false;
+      }
+    }
+    raw_names = top.raw(names);
+    has_pod_text = pod_top >= 0 && !top.is(pod_top, json::Type::kNull);
+    if (has_pod_text) pod_text = top.raw(pod_top);
+    reused = has_pod_text && last.valid && top.is(pod_top, json::Type::kObj) && pod_text == last.raw;
+    if (has_pod_text && !reused) {
+      if (!top.is(pod_top, json::Type::kObj) || !d.parse(pod_text)) return false;
+      pod = d.root();
+    }
+  }
   Demand dem;
   std::memset(&dem, 0, sizeof(dem));
   std::string_view uid;
   CachedPod cached;
   bool mb_annotated = false;
-  const bool has_pod_text = pod_top >= 0 && !top.is(pod_top, json::Type::kNull);
-  const bool reused = has_pod_text && last.valid && top.is(pod_top, json::Type::kObj) && top.raw(pod_top) == last.raw;
   if (reused) {
     dem = last.dem;
     uid = last.uid;
     mb_annotated = last.mb_annotated;
   } else {
-    if (has_pod_text) {
-      if (!top.is(pod_top, json::Type::kObj) || !d.parse(top.raw(pod_top))) return false;
-      pod = d.root();
-    }
     if (pod >= 0 && !d.is(pod, json::Type::kNull)) {
       if (!d.is(pod, json::Type::kObj)) return false;
       const int32_t md = d.get(pod, "metadata");
@@ -1368,12 +1471,13 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
       mb_annotated = d.is(mb, json::Type::kStr);
     }
     if (pod >= 0 && !uid.empty()) {
-      last.raw.assign(top.raw(pod_top));
+      last.raw.assign(pod_text);
       last.uid.assign(uid);
       last.dem = dem;
       last.cached = cached;
       last.mb_annotated = mb_annotated;
       last.valid = true;
+      uid = last.uid;   // `d` is reparsed by the next request; the uid outlives it here
     }
   }
   // A learned streaming owner marks an unannotated pod memory-bound. Read per request, not
@@ -1390,34 +1494,8 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   // kube-scheduler sends the same node list over and over, so each worker remembers the ids
   // of the last lists it resolved (keyed by the array's raw text) and only checks that slot
   // `id` still carries that name; a miss falls back to the ledger's name index.
-  const std::string_view raw_names = top.raw(names);
-  thread_local std::vector<std::string_view> nraw;   // each name's JSON token, quotes included
-  nv.clear();
-  nraw.clear();
-  // The node lists of the last kListSlots distinct texts this thread resolved (LRU). With
-  // kube-scheduler's node sampling (numFeasibleNodesToFind from a rotating start) the list is
-  // a window of the cluster that moves every cycle, but the windows repeat: 1000 nodes sampled
-  // 420 at a time cycle through 50 of them, so a few dozen slots catch them all.
-  constexpr int kListSlots = 64;
-  struct IdCache {
-    const Ledger* owner = nullptr;
-    uint64_t key[kListSlots] = {};
-    uint64_t epoch[kListSlots] = {};     // the ledger's node epoch the ids were checked at
-    uint64_t used[kListSlots] = {};
-    size_t len[kListSlots] = {};
-    bool compact[kListSlots] = {};       // the text is `["a","b",...]` exactly: a reply may copy it whole
-    std::vector<int32_t> ids[kListSlots];
-    std::vector<std::pair<uint32_t, uint32_t>> tok[kListSlots];   // token (offset, length) in the list text
-    std::string text[kListSlots];        // the list text itself: a hash hit is confirmed byte for byte
-    uint64_t clock = 0;
-  };
-  thread_local IdCache idc;
-  if (idc.owner != ledger_.get()) idc = IdCache{}, idc.owner = ledger_.get();
-  const uint64_t nkey = text_hash(raw_names) | 1;   // 0 marks an empty slot
   const uint64_t epoch = ledger_->node_epoch();
-  int slot = -1;
-  for (int k = 0; k < kListSlots && slot < 0; ++k)
-    if (idc.key[k] == nkey && idc.len[k] == raw_names.size() && idc.text[k] == raw_names) slot = k;
+  int slot = scanned ? -1 : framed && found != -2 ? found : idc.find(raw_names);
   // a cached list's names are read through its token offsets into this request's text (no
   // per-request copy of 2 x N views); a list parsed now fills nv / nraw
   const std::vector<std::pair<uint32_t, uint32_t>>* toks = nullptr;
@@ -1428,11 +1506,11 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   } else {
     // the common shape first, scanned directly: ["a","b",...] with no escapes; anything else
     // (whitespace, escapes, other types) goes through the JSON parser
-    bool plain = scan_string_array(raw_names, &nv, &nraw);
+    bool plain = scanned || scan_string_array(raw_names, &nv, &nraw);
     if (!plain) {
       nv.clear();
       nraw.clear();
-      thread_local json::Doc dn;
+      json::Doc& dn = s.dn;
       if (!dn.parse(raw_names) || !dn.is(dn.root(), json::Type::kArr)) return false;
       plain = true;
       for (int32_t c = dn.at(dn.root()).first; c >= 0; c = dn.at(c).next) {
@@ -1445,7 +1523,7 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
           nraw.push_back(tok);
         } else {
           plain = false;
-          thread_local std::deque<std::string> requoted;   // stable storage for this request
+          std::deque<std::string>& requoted = s.requoted;   // stable storage for this request
           if (nraw.empty()) requoted.clear();
           requoted.emplace_back();
           json::append_quoted(&requoted.back(), nv.back());
@@ -1456,7 +1534,7 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     slot = 0;
     for (int k = 1; k < kListSlots; ++k)
       if (idc.used[k] < idc.used[slot]) slot = k;
-    idc.key[slot] = plain ? nkey : 0;   // a list with escapes is parsed every time
+    idc.valid[slot] = plain;   // a list with escapes is parsed every time
     idc.len[slot] = raw_names.size();
     if (plain) idc.text[slot].assign(raw_names.data(), raw_names.size());
     else idc.text[slot].clear();
@@ -1472,6 +1550,7 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     idc.compact[slot] = plain && joined == raw_names.size();
   }
   idc.used[slot] = ++idc.clock;
+  idc.mru = slot;
   auto raw_at = [&](size_t i) -> std::string_view {
     return toks ? raw_names.substr((*toks)[i].first, (*toks)[i].second) : nraw[i];
   };
@@ -1489,7 +1568,7 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     // names this worker resolved before, by a hash of the name (no string, no lock): with
     // kube-scheduler's node sampling the list is a different window of the cluster every
     // cycle, so the per-list cache above misses while every name in it is known
-    thread_local NameTable nid;
+    NameTable& nid = s.nid;
     if (nid.owner != ledger_.get() || nid.epoch != epoch) nid.reset(ledger_.get(), epoch);
     for (size_t i = 0; i < static_cast<size_t>(nn); ++i) {
       const std::string_view name = name_at(i);
@@ -1499,7 +1578,7 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
       if (id < 0) {
         id = ledger_->find_node(std::string(name));
         if (id < 0) {
-          idc.key[slot] = 0;
+          idc.valid[slot] = false;
           return false;
         }
         nid.insert(name, id);
@@ -1524,7 +1603,7 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     cp.demand = dem;
     if (ledger_->attached() > 1) {
       // other worker processes share the ledger: the bind may reach one of them
-      thread_local std::string blob;
+      std::string& blob = s.blob;
       pack_pod(cp, &blob);
       if (ledger_->put_pod_info(std::string(uid), blob)) pods_published.fetch_add(1, std::memory_order_relaxed);
     }
@@ -1559,7 +1638,7 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
       // "can't allocate <demand> on node <name>: <reason>" per failing node, written in place:
       // the demand text, the reasons (alloc.cpp err_str) and an escape-free name (its request
       // token is the name in quotes) need no escaping
-      thread_local std::string dstr;
+      std::string& dstr = s.dstr;
       dstr.clear();
       char num[24];
       for (int i = 0; i < dem.n; ++i) {

@@ -116,6 +116,20 @@ bool Doc::parse(std::string_view src) {
   return p_ == src_.size();
 }
 
+bool Doc::parse_prefix(std::string_view src, size_t* end) {
+  src_ = src;
+  p_ = 0;
+  nodes_.clear();
+  arena_.clear();
+  nodes_.reserve(src.size() / 8 + 16);
+  arena_.reserve(src.size());
+  max_depth_ = 1 << 30;
+  ws();
+  if (value(0) < 0) return false;
+  *end = p_;
+  return true;
+}
+
 // The first quote, backslash or control character at or after q (n if none): sixteen bytes at
 // a time, the bytes of a string that need no look one by one.
 static inline size_t plain_run_end(const char* s, size_t q, size_t n) {

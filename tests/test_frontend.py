@@ -860,3 +860,43 @@ def test_io_tally_counts_the_front_door_calls_of_a_cycle():
             await rt.stop()
 
     asyncio.run(main())
+
+
+def test_compact_args_layout_and_general_layout_answer_alike():
+    """The verbs' fast framing (kube-scheduler's exact {"Pod":..,"Nodes":null,"NodeNames":[..]}
+    layout, the pod found by comparison with the last one or parsed in place) and the general
+    path (any other layout: spaces, member order) give the same answers, and a body that only
+    looks framed (trailing members, a list that is not one) still gets the general path's
+    verdict."""
+    async def main():
+        store, rt = await _runtime(4)
+        fe = rt.native.fe
+        ext = rt.extender
+        names = [f"n{i}" for i in range(4)]
+        rng = random.Random(3)
+        try:
+            for pod in _pods(rng, 12):
+                pod = store.create_pod(pod)
+                compact = _dumps({"Pod": pod, "Nodes": None, "NodeNames": names})
+                spaced = json.dumps({"NodeNames": names, "Pod": pod, "Nodes": None}).encode()
+                for prio in (False, True):
+                    want = _dumps(ext.prioritize(json.loads(compact)) if prio else ext.filter(json.loads(compact)))
+                    for body in (compact, spaced, compact):   # framed + parsed, general, framed + reused
+                        ok, got = fe.verb(body, prio)
+                        assert ok and got == want.decode(), (prio, body[:40], got)
+            pod = _pods(rng, 1)[0]
+            pod["metadata"]["name"] = "framing-edge"
+            pod = store.create_pod(pod)
+            base = _dumps({"Pod": pod, "Nodes": None, "NodeNames": names})
+            want = _dumps(ext.filter(json.loads(base))).decode()
+            assert fe.verb(base, False) == (True, want)
+            # valid JSON with a member after the list: not the framed layout, answered alike
+            for extra in (base[:-1] + b',"x":["y"]}', base[:-1] + b',"x":1}'):
+                assert fe.verb(extra, False) == (True, want), extra[-20:]
+            # not JSON (a stray bracket after the list): never answered natively
+            assert fe.verb(base[:-1] + b']}', False)[0] is False
+            assert fe.verb(base.replace(b'"NodeNames":["n0"', b'"NodeNames":["n0"]]', 1), False)[0] is False
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
