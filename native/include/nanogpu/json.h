@@ -55,6 +55,8 @@ class Doc {
   int32_t get(int32_t obj, std::string_view k, bool ci = false) const;
   bool is(int32_t i, Type t) const { return i >= 0 && nodes_[i].type == t; }
   size_t size() const { return nodes_.size(); }
+  // skip_container (or its scalar fallback) from offset 0 of `src`: the end offset, -1 = fails
+  static long skip_for_test(std::string_view src, bool scalar);
 
  private:
   std::string_view text(uint32_t off, uint32_t len) const {
@@ -63,6 +65,7 @@ class Doc {
   int32_t value(int depth);
   bool string(uint32_t* off, uint32_t* len);
   bool skip_container();
+  bool skip_scalar();   // SSE2 fallback of skip_container (and its reference in the tests)
   int max_depth_ = 1 << 30;
   void ws() {
     while (p_ < src_.size() && (src_[p_] == ' ' || src_[p_] == '\n' || src_[p_] == '\r' || src_[p_] == '\t')) ++p_;

@@ -266,6 +266,8 @@ class Ledger {
   int32_t commit(const std::string& key);
   int32_t release(const std::string& key);
   bool lookup(const std::string& key, PodRecord* out) const;
+  // whether the ledger holds a record for `key` (no copy of it; the pod watch's drop test)
+  bool holds(std::string_view key) const;
   std::vector<PodRecord> pods_on(int32_t node) const;
   // Preemption check (extender preemptVerb): does demand `d` fit on node `id` once the
   // shares of `victims` (pod keys) are released? Simulated on a copy; nothing changes.

@@ -36,6 +36,7 @@ struct PodWatchFilter {
   // terminating pod keeps it until Succeeded/Failed or DELETED (controller/pods.py)
   std::atomic<bool> release_on_terminating{false};   // set from Python while the watch thread reads it
   std::mutex mu;   // a stream thread and the Python loop (reset, counters) share it
+  std::string key_buf;   // under mu: the event's "ns/name" (no allocation per event)
 };
 
 // Runs one event line through the filter. `d` is parsed (shallow) by the call. Returns true

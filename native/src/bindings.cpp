@@ -922,6 +922,9 @@ PYBIND11_MODULE(_native, m) {
            "Runs the native verb `iters` times in place (no socket): (ok, seconds per call, last body).")
       .def("reset_max", &Frontend::reset_max, "zero the per-verb and event-loop maxima");
   m.def("mono_now", &mono_now);
+  m.def("json_skip", [](const py::bytes& src, bool scalar) { return json::Doc::skip_for_test(std::string(src), scalar); },
+        py::arg("src"), py::arg("scalar") = false,
+        "The JSON container skipper from offset 0 (AVX2, or the scalar fallback): end offset, -1 = refused.");
   m.def("io_tally_enable", [](bool on) { g_io.on.store(on, std::memory_order_relaxed); }, py::arg("on"),
         "Switches the per-call-site system-call / phase tally (iotally.h) on or off.");
   m.def("io_tally_reset", []() { g_io.reset(); }, "Zeroes the tally.");

@@ -916,6 +916,33 @@ int32_t Ledger::release_if(const std::string& key, int32_t only_state) {
   return kOk;
 }
 
+bool Ledger::holds(std::string_view key) const {
+  if (key.empty() || key.size() >= kKeyLen) return false;
+  uint64_t h = 0xcbf29ce484222325ULL;   // key_hash over the view's bytes
+  for (const char c : key) {
+    if (c == '\0') return false;
+    h ^= static_cast<unsigned char>(c);
+    h *= 0x100000001b3ULL;
+  }
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdULL;
+  h ^= h >> 33;
+  const int s = shard_of(h);
+  lock_mu(&hdr_->shard_mu[s].m);
+  Unlock us{&hdr_->shard_mu[s].m};
+  const PodSlot* t = shard(s);
+  const uint32_t cap = hdr_->pods_per_shard;
+  uint32_t i = static_cast<uint32_t>((h / kPodShards) % cap);
+  for (uint32_t probe = 0; probe < cap; ++probe, i = (i + 1) % cap) {
+    const PodSlot& p = t[i];
+    if (p.state == kPodEmpty) return false;
+    if (p.state != kPodTombstone && p.hash == h && std::memcmp(p.key, key.data(), key.size()) == 0 &&
+        p.key[key.size()] == '\0')
+      return true;
+  }
+  return false;
+}
+
 bool Ledger::lookup(const std::string& key, PodRecord* out) const {
   const uint64_t h = key_hash(key.c_str());
   const int s = shard_of(h);

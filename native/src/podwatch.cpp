@@ -32,11 +32,22 @@ bool filter_pod_event(PodWatchFilter& f, std::string_view line, json::Doc& d, st
     return true;   // ERROR, BOOKMARK: the informer's own business
   const int32_t md = d.get(obj, "metadata"), sp = d.get(obj, "spec"), st = d.get(obj, "status");
   rv->assign(field(d, md, "resourceVersion"));
-  std::string key(field(d, md, "namespace"));
-  key.push_back('/');
-  key.append(field(d, md, "name"));
   std::lock_guard<std::mutex> g(f.mu);
-  const bool seen = f.forwarded.count(key) > 0;
+  // "ns/name" in the filter's own buffer (its capacity kept): built for the forwarded set only
+  std::string& key = f.key_buf;
+  bool have_key = false;
+  auto make_key = [&] {
+    if (have_key) return;
+    key.assign(field(d, md, "namespace"));
+    key.push_back('/');
+    key.append(field(d, md, "name"));
+    have_key = true;
+  };
+  bool seen = false;
+  if (!f.forwarded.empty()) {
+    make_key();
+    seen = f.forwarded.count(key) > 0;
+  }
   bool drop = false;
   if (!seen && type == "DELETED") {
     // Python never held it: releasing is all the controller would do (pods.py::_on_event)
@@ -51,21 +62,26 @@ bool filter_pod_event(PodWatchFilter& f, std::string_view line, json::Doc& d, st
     if (!completed && node.empty()) {
       drop = true;
     } else if (!completed) {
-      PodRecord rec;
-      drop = f.ledger->lookup(std::string(field(d, md, "uid")), &rec);
+      drop = f.ledger->holds(field(d, md, "uid"));
       // the node agent rewrote the placement to what kubelet ran (plugin.reconcile): the
-      // controller re-accounts it, so the event goes on
-      // (memmem: string_view::find stops at every '"' of the event to compare the rest)
+      // controller re-accounts it, so the event goes on. Looked for in the annotations'
+      // text only (a depth-3 object the shallow parse spans without parsing)
+      // (memmem: string_view::find stops at every '"' of the text to compare the rest)
       static constexpr char kReconciled[] = "\"nano-gpu/reconciled\"";
-      if (drop && memmem(line.data(), line.size(), kReconciled, sizeof kReconciled - 1) != nullptr) drop = false;
+      const int32_t ann = d.is(md, json::Type::kObj) ? d.get(md, "annotations") : -1;
+      if (drop && d.is(ann, json::Type::kObj)) {
+        const std::string_view a = d.raw(ann);
+        if (memmem(a.data(), a.size(), kReconciled, sizeof kReconciled - 1) != nullptr) drop = false;
+      }
     }
   }
   if (drop) {
     ++f.dropped;
     return false;
   }
+  make_key();
   if (type == "DELETED") f.forwarded.erase(key);
-  else f.forwarded.insert(std::move(key));
+  else f.forwarded.insert(key);
   return true;
 }
 
