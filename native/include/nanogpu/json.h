@@ -78,5 +78,7 @@ class Doc {
 
 // Appends `s` as a JSON string literal (quotes included).
 void append_quoted(std::string* out, std::string_view s);
+// The same without the quotes.
+void append_escaped(std::string* out, std::string_view s);
 
 }  // namespace nanogpu::json

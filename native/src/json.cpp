@@ -417,6 +417,11 @@ int32_t Doc::get(int32_t obj, std::string_view k, bool ci) const {
 
 void append_quoted(std::string* out, std::string_view s) {
   out->push_back('"');
+  append_escaped(out, s);
+  out->push_back('"');
+}
+
+void append_escaped(std::string* out, std::string_view s) {
   size_t run = 0;
   for (size_t i = 0; i < s.size(); ++i) {
     const char c = s[i];
@@ -440,7 +445,6 @@ void append_quoted(std::string* out, std::string_view s) {
     }
   }
   out->append(s.data() + run, s.size() - run);
-  out->push_back('"');
 }
 
 }  // namespace nanogpu::json

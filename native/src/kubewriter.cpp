@@ -1,6 +1,8 @@
 // Native bind writes to kube-apiserver (see kubewriter.h).
 #include "nanogpu/kubewriter.h"
 
+#include <charconv>
+
 #include <arpa/inet.h>
 #include <netdb.h>
 #include <netinet/in.h>
@@ -584,38 +586,49 @@ int KubeWriter::call(HttpConn* c, const char* method, const std::string& path, c
 // that would change it (422), so the label lands only on a pod bound to this node
 // (pu.label_patch), never on one bound elsewhere or still unbound.
 void KubeWriter::build(BindJob& j, std::string* patch, std::string* binding) {
-  std::string ann = "{";
-  for (size_t k = 0; k < j.containers.size() && k < j.plan.size(); ++k) {
-    json::append_quoted(&ann, kContainerPrefix + j.containers[k]);
-    ann += ":\"";
-    for (size_t i = 0; i < j.plan[k].size(); ++i) {
-      if (i) ann += ',';
-      ann += std::to_string(j.plan[k][i]);
-    }
-    ann += "\",";
-  }
-  char ts[48];
-  std::snprintf(ts, sizeof ts, "%.6f", wall_s());
-  ann += "\"";
-  ann += kAssume;
-  ann += "\":\"true\",\"";
-  ann += kAssumeTime;
-  ann += "\":\"";
-  ann += ts;
-  ann += "\"}";
-  *patch = "{\"metadata\":{\"labels\":{\"";
-  *patch += kAssume;
-  *patch += "\":\"true\"}},\"spec\":{\"nodeName\":";
-  json::append_quoted(patch, j.node);
-  *patch += "}}";
+  // written in place, one buffer each (no temporaries: this runs once a bind on the writer)
+  std::string& p = *patch;
+  p.clear();
+  p.reserve(96 + j.node.size());
+  p += "{\"metadata\":{\"labels\":{\"";
+  p += kAssume;
+  p += "\":\"true\"}},\"spec\":{\"nodeName\":";
+  json::append_quoted(&p, j.node);
+  p += "}}";
   std::string& b = *binding;
-  b = "{\"apiVersion\":\"v1\",\"kind\":\"Binding\",\"metadata\":{\"name\":";
+  b.clear();
+  size_t est = 320 + j.name.size() + j.ns.size() + j.uid.size() + j.node.size();
+  for (size_t k = 0; k < j.containers.size(); ++k) est += 40 + j.containers[k].size() + 4 * (k < j.plan.size() ? j.plan[k].size() : 0);
+  b.reserve(est);
+  b += "{\"apiVersion\":\"v1\",\"kind\":\"Binding\",\"metadata\":{\"name\":";
   json::append_quoted(&b, j.name);
   b += ",\"namespace\":";
   json::append_quoted(&b, j.ns);
   b += ",\"uid\":";
   json::append_quoted(&b, j.uid);
-  b += ",\"annotations\":" + ann + "},\"target\":{\"apiVersion\":\"v1\",\"kind\":\"Node\",\"name\":";
+  b += ",\"annotations\":{";
+  char num[24];
+  for (size_t k = 0; k < j.containers.size() && k < j.plan.size(); ++k) {
+    b += '"';
+    b += kContainerPrefix;
+    json::append_escaped(&b, j.containers[k]);
+    b += '"';
+    b += ":\"";
+    for (size_t i = 0; i < j.plan[k].size(); ++i) {
+      if (i) b += ',';
+      b.append(num, static_cast<size_t>(std::to_chars(num, num + sizeof num, j.plan[k][i]).ptr - num));
+    }
+    b += "\",";
+  }
+  char ts[48];
+  const int tl = std::snprintf(ts, sizeof ts, "%.6f", wall_s());
+  b += "\"";
+  b += kAssume;
+  b += "\":\"true\",\"";
+  b += kAssumeTime;
+  b += "\":\"";
+  b.append(ts, static_cast<size_t>(std::max(0, tl)));
+  b += "\"}},\"target\":{\"apiVersion\":\"v1\",\"kind\":\"Node\",\"name\":";
   json::append_quoted(&b, j.node);
   b += "}}";
 }
