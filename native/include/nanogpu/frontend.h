@@ -166,9 +166,10 @@ class Frontend {
   void prepare_bind(std::string_view body, PyRequest* r);
   void note_bind_wall(uint64_t ns);
   // a response for connection `conn` of worker w, on w's thread: sent, then its next request
-  void deliver_reply(Worker* w, uint64_t conn, std::string&& bytes);
+  struct Reply;
+  void deliver_reply(Worker* w, const Reply& r);
   void drain_local(Worker* w);   // the replies w's BindIo queued during its last call
-  static std::string http_response(int status, const std::string& content_type, const std::string& body);
+  static void append_http(std::string* out, int status, std::string_view content_type, std::string_view body);
 
   std::shared_ptr<Ledger> ledger_;
   std::unique_ptr<KubeWriter> writer_owner_;

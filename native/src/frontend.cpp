@@ -478,6 +478,16 @@ struct Frontend::Conn {
   uint64_t t_req_ns = 0;     // ... of the request now with Python
 };
 
+// An answer posted to a worker (bind writer, Python, inline BindIo): formatted into the
+// connection's output by the worker itself, so posting one allocates nothing for a short
+// JSON body (a bind's {"Error":""} fits the string's inline buffer).
+struct Frontend::Reply {
+  uint64_t conn = 0;
+  int status = 200;
+  std::string ctype;   // empty: application/json
+  std::string body;
+};
+
 struct Frontend::Worker {
   int idx = 0;
   int lfd = -1, ep = -1, efd = -1;
@@ -485,11 +495,13 @@ struct Frontend::Worker {
   // once from the setting thread, then used by this worker's thread only
   std::unique_ptr<BindIo> bio_owner;
   std::atomic<BindIo*> bio{nullptr};
-  std::vector<std::pair<uint64_t, std::string>> local_replies;   // (conn id, response bytes)
+  std::vector<Reply> local_replies;   // inline BindIo answers, sent after the call
+  std::vector<Reply> local_spare;
   std::thread th;
   std::unordered_map<uint64_t, std::unique_ptr<Conn>> conns;   // by conn id
   std::mutex mb_mu;
-  std::vector<std::pair<uint64_t, std::string>> mailbox;       // (conn id, response bytes)
+  std::vector<Reply> mailbox;        // posted by other threads (under mb_mu)
+  std::vector<Reply> mb_spare;       // the worker's side of the swap (keeps its capacity)
   std::atomic<bool> unsignalled{false};                         // queued with notify=false
   bool mb_signalled = false;   // under mb_mu: the eventfd was written for what the mailbox holds
   // An awake worker (busy polling, or handling a batch) looks at the mailbox itself after
@@ -597,7 +609,11 @@ void Frontend::set_kube_writer(const KubeTarget& t, int threads, int retries, bo
       Worker* w = wp.get();
       // happy-path answers from w's own BindIo, on w's thread: queued, sent after the call
       w->bio_owner = writer_owner_->make_io(w->ep, kBioTag, [w](uint64_t id, int status, const std::string& body) {
-        w->local_replies.emplace_back(id >> 8, http_response(status, "application/json", body));
+        Reply r;
+        r.conn = id >> 8;
+        r.status = status;
+        r.body = body;
+        w->local_replies.push_back(std::move(r));
       });
       w->bio.store(w->bio_owner.get(), std::memory_order_release);
     }
@@ -644,13 +660,19 @@ std::vector<PyRequest> Frontend::take() {
   return out;
 }
 
-std::string Frontend::http_response(int status, const std::string& content_type, const std::string& body) {
-  std::string r;
-  r.reserve(body.size() + 128);
-  r += "HTTP/1.1 " + std::to_string(status) + " " + reason(status) + "\r\nContent-Type: " + content_type +
-       "\r\nContent-Length: " + std::to_string(body.size()) + "\r\n\r\n";
-  r += body;
-  return r;
+void Frontend::append_http(std::string* out, int status, std::string_view content_type, std::string_view body) {
+  char num[24];
+  out->reserve(out->size() + body.size() + 96 + content_type.size());
+  *out += "HTTP/1.1 ";
+  out->append(num, static_cast<size_t>(std::to_chars(num, num + sizeof num, status).ptr - num));
+  *out += ' ';
+  *out += reason(status);
+  *out += "\r\nContent-Type: ";
+  *out += content_type;
+  *out += "\r\nContent-Length: ";
+  out->append(num, static_cast<size_t>(std::to_chars(num, num + sizeof num, body.size()).ptr - num));
+  *out += "\r\n\r\n";
+  *out += body;
 }
 
 void Frontend::respond(uint64_t id, int status, const std::string& content_type, const std::string& body,
@@ -658,11 +680,15 @@ void Frontend::respond(uint64_t id, int status, const std::string& content_type,
   const int widx = static_cast<int>(id & 0xff);
   if (widx < 0 || widx >= static_cast<int>(workers_.size())) return;
   Worker* w = workers_[widx].get();
-  std::string r = http_response(status, content_type, body);
+  Reply r;
+  r.conn = id >> 8;
+  r.status = status;
+  if (content_type != "application/json") r.ctype = content_type;
+  r.body = body;
   bool signal = false;
   {
     std::lock_guard<std::mutex> g(w->mb_mu);
-    w->mailbox.emplace_back(id >> 8, std::move(r));
+    w->mailbox.push_back(std::move(r));
     w->mb_pending.store(true, std::memory_order_seq_cst);
     // one eventfd write per mailbox fill, and only to a worker that may be blocked in
     // epoll_wait: the worker takes everything queued until it swaps
@@ -854,14 +880,16 @@ void Frontend::run(Worker* w) {
   // responses posted by the bind writer or Python: sent, then the connection's next request
   auto drain_mailbox = [&] {
     PhaseTimer pt{&phase_max_ns[1]};
-    std::vector<std::pair<uint64_t, std::string>> mb;
+    std::vector<Reply>& mb = w->mb_spare;
+    mb.clear();
     {
       std::lock_guard<std::mutex> g(w->mb_mu);
       mb.swap(w->mailbox);
       w->mb_signalled = false;
       w->mb_pending.store(false, std::memory_order_relaxed);
     }
-    for (auto& m : mb) deliver_reply(w, m.first, std::move(m.second));
+    for (Reply& m : mb) deliver_reply(w, m);
+    mb.clear();
   };
   while (!stop_.load(std::memory_order_acquire)) {
     const int64_t spin = busy_poll_ns_.load(std::memory_order_relaxed);
@@ -1005,11 +1033,12 @@ void Frontend::run(Worker* w) {
   drain_mailbox();
 }
 
-void Frontend::deliver_reply(Worker* w, uint64_t conn, std::string&& bytes) {
+void Frontend::deliver_reply(Worker* w, const Reply& r) {
+  const uint64_t conn = r.conn;
   auto it = w->conns.find(conn);
   if (it == w->conns.end()) return;
   Conn* c = it->second.get();
-  c->out += bytes;
+  append_http(&c->out, r.status, r.ctype.empty() ? std::string_view("application/json") : std::string_view(r.ctype), r.body);
   c->waiting = false;
   const bool was_bind = c->bind_waiting;
   const uint64_t t_req = c->t_req_ns;
@@ -1021,11 +1050,11 @@ void Frontend::deliver_reply(Worker* w, uint64_t conn, std::string&& bytes) {
 
 void Frontend::drain_local(Worker* w) {
   // process() below may parse the next bind and queue more: swap first, loop until empty
-  thread_local std::vector<std::pair<uint64_t, std::string>> batch;
+  std::vector<Reply>& batch = w->local_spare;
   while (!w->local_replies.empty()) {
     batch.clear();
     batch.swap(w->local_replies);
-    for (auto& r : batch) deliver_reply(w, r.first, std::move(r.second));
+    for (const Reply& r : batch) deliver_reply(w, r);
     if (BindIo* bio = w->bio.load(std::memory_order_relaxed)) bio->pump();
   }
 }
