@@ -161,7 +161,7 @@ class Frontend {
   void defer(Worker* w, Conn* c, std::string method, std::string path, std::string query, std::string body);
   void flush(Worker* w, Conn* c, int io_kind = kFeSendOther);
   void close_conn(Worker* w, Conn* c);
-  void put_pod(std::string_view uid, CachedPod pod);
+  void put_pod(std::string_view uid, const CachedPod& meta, std::string_view raw, const Demand& dem);
   bool has_pod(std::string_view uid) const;
   void prepare_bind(std::string_view body, PyRequest* r);
   void note_bind_wall(uint64_t ns);
@@ -196,9 +196,20 @@ class Frontend {
   std::vector<uint64_t> bind_wall_ns_;
 
   mutable std::mutex pod_mu_;
-  std::unordered_map<std::string, CachedPod> pods_;
-  std::deque<std::string> pod_order_;
-  size_t pod_cap_ = 16384;
+  // filter -> bind pod cache: kPodWays-way buckets by UID hash whose entries keep their
+  // strings' capacity from pod to pod (no allocation per pod once warm); a full bucket gives
+  // up its oldest entry (a pod filtered long ago and never bound)
+  struct PodEntry {
+    uint64_t h = 0;   // 0: empty
+    uint64_t stamp = 0;
+    std::string uid;
+    CachedPod pod;
+  };
+  static constexpr size_t kPodWays = 4;
+  std::vector<PodEntry> pod_slots_ = std::vector<PodEntry>(16384);
+  uint64_t pod_stamp_ = 0;
+  size_t pod_live_ = 0;
+  PodEntry* find_pod_locked(std::string_view uid, uint64_t h);
 };
 
 }  // namespace nanogpu

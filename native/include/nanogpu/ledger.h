@@ -246,26 +246,26 @@ class Ledger {
   // pod as Reserved. Idempotent for the same key on the same node. A nomination of the
   // key on this node is adopted (kOk: the caller owns it, e.g. rolls it back on failure);
   // one on another node is released first.
-  int32_t reserve(int32_t id, const std::string& key, const Demand& d, const Options& o, Plan* plan);
+  int32_t reserve(int32_t id, std::string_view key, const Demand& d, const Options& o, Plan* plan);
   // Priorities: takes `d` tentatively on node `id` for pod `key` (state Nominated), the node
   // kube-scheduler is about to pick, so the filters of the pods scheduled right behind it
   // (kube-scheduler's cycle does not wait for the bind) already see it — the extender-side
   // counterpart of kube-scheduler's assume cache. Moves an older nomination of the key;
   // leaves a Reserved/Committed key alone (kOkExisting). Unbound ones expire (below).
-  int32_t nominate(int32_t id, const std::string& key, const Demand& d, const Options& o);
+  int32_t nominate(int32_t id, std::string_view key, const Demand& d, const Options& o);
   std::vector<std::string> expired_nominations(double older_than_s) const;
   // Releases `key` only while it is a nomination: every scheduling attempt of a pod starts
   // by dropping its own nomination, so its filter and scores never count it against itself.
   // kOk = dropped, kOkExisting = reserved/committed (left alone), kErrUnknownPod = none.
-  int32_t drop_nomination(const std::string& key);
+  int32_t drop_nomination(std::string_view key);
   // Releases `key` only while it is still a reservation (a sweep racing a commit).
-  int32_t drop_reservation(const std::string& key);
+  int32_t drop_reservation(std::string_view key);
   // Allocates an explicit plan (pods bound by someone else / rebuild from annotations).
-  int32_t allocate_plan(int32_t id, const std::string& key, const Demand& d, const Plan& plan,
+  int32_t allocate_plan(int32_t id, std::string_view key, const Demand& d, const Plan& plan,
                         bool committed);
-  int32_t commit(const std::string& key);
-  int32_t release(const std::string& key);
-  bool lookup(const std::string& key, PodRecord* out) const;
+  int32_t commit(std::string_view key);
+  int32_t release(std::string_view key);
+  bool lookup(std::string_view key, PodRecord* out) const;
   // whether the ledger holds a record for `key` (no copy of it; the pod watch's drop test)
   bool holds(std::string_view key) const;
   std::vector<PodRecord> pods_on(int32_t node) const;
@@ -284,14 +284,14 @@ class Ledger {
   // The same over views (the binding hands the LIST's UIDs as one newline-joined string)
   std::vector<std::string> reconcile_views(const std::vector<std::string_view>& live, double before);
   // Releases `key` only while it is Committed (reconcile racing a re-bind of the same key).
-  int32_t drop_committed(const std::string& key);
+  int32_t drop_committed(std::string_view key);
   int64_t n_pods() const { return hdr_->n_pods.load(std::memory_order_acquire); }
   // processes attached to the region (more than one: worker processes share it)
   int32_t attached() const { return hdr_->attached.load(std::memory_order_relaxed); }
   // Bind handoff (PodInfoSlot): `blob` is the front door's packed pod. put: false when it does
   // not fit a slot. take: the blob stored for `key`, removed (one bind per pod UID).
-  bool put_pod_info(const std::string& key, std::string_view blob);
-  bool take_pod_info(const std::string& key, std::string* blob);
+  bool put_pod_info(std::string_view key, std::string_view blob);
+  bool take_pod_info(std::string_view key, std::string* blob);
   int32_t overflow_records_used() const { return hdr_->ext_used.load(std::memory_order_relaxed); }
 
   // Load-aware telemetry (reference nodeusage.go + allocate.go:173-195).
@@ -310,7 +310,7 @@ class Ledger {
   void set_stream_owner(uint64_t owner, bool streaming);
   bool is_stream_owner(uint64_t owner) const;
   // records the controlling owner of a pod the ledger holds (what learn_stream_owners reads)
-  int32_t set_pod_owner(const std::string& key, uint64_t owner);
+  int32_t set_pod_owner(std::string_view key, uint64_t owner);
   // One pass over the committed pods. A device that holds exactly one pod is that pod's "lone"
   // device; only pods recorded at or before `reserved_before` (CLOCK_MONOTONIC: the start of
   // the HBM metric's averaging window, so the mark was measured on this pod and not on a
@@ -342,10 +342,10 @@ class Ledger {
   std::atomic<uint64_t>& gen_of(const NodeSlot* n) const { return hot_[n - nodes_].gen; }
   PodSlot* shard(int s) const;
   int shard_of(uint64_t h) const { return static_cast<int>(h % kPodShards); }
-  int32_t reserve_as(int32_t id, const std::string& key, const Demand& d, const Options& o, Plan* plan,
+  int32_t reserve_as(int32_t id, std::string_view key, const Demand& d, const Options& o, Plan* plan,
                      int32_t state);
   std::vector<std::string> expired(int32_t state, double older_than_s) const;
-  int32_t release_if(const std::string& key, int32_t only_state);   // -1: any state
+  int32_t release_if(std::string_view key, int32_t only_state);   // -1: any state
   PodSlot* find_pod_locked(int s, uint64_t h, const char* key) const;
   PodSlot* insert_pod_locked(int s, uint64_t h, const char* key);
   // a slot's demand and plan, inline or in its overflow record (false: no record free)

@@ -714,14 +714,30 @@ void Frontend::wake_workers() {
   }
 }
 
+namespace {
+uint64_t uid_hash(std::string_view uid) {   // FNV-1a, never 0 (0 marks an empty slot)
+  uint64_t h = 0xcbf29ce484222325ULL;
+  for (const char c : uid) h = (h ^ static_cast<unsigned char>(c)) * 0x100000001b3ULL;
+  return h | 1;
+}
+}  // namespace
+
+Frontend::PodEntry* Frontend::find_pod_locked(std::string_view uid, uint64_t h) {
+  const size_t nb = pod_slots_.size() / kPodWays;
+  PodEntry* b = &pod_slots_[((h >> 7) % nb) * kPodWays];
+  for (size_t w = 0; w < kPodWays; ++w)
+    if (b[w].h == h && b[w].uid == uid) return &b[w];
+  return nullptr;
+}
+
 bool Frontend::has_pod(std::string_view uid) const {
   std::lock_guard<std::mutex> g(pod_mu_);
-  return pods_.find(std::string(uid)) != pods_.end();
+  return const_cast<Frontend*>(this)->find_pod_locked(uid, uid_hash(uid)) != nullptr;
 }
 
 size_t Frontend::pod_cache_size() const {
   std::lock_guard<std::mutex> g(pod_mu_);
-  return pods_.size();
+  return pod_live_;
 }
 
 namespace {
@@ -735,7 +751,7 @@ void put_str(std::string* o, std::string_view v) {
   put_raw(o, static_cast<uint16_t>(std::min<size_t>(v.size(), 0xffff)));
   o->append(v.data(), std::min<size_t>(v.size(), 0xffff));
 }
-void pack_pod(const CachedPod& p, std::string* o) {
+void pack_pod(const CachedPod& p, const Demand& dem, std::string* o) {
   o->clear();
   put_str(o, p.ns);
   put_str(o, p.name);
@@ -743,8 +759,8 @@ void pack_pod(const CachedPod& p, std::string* o) {
   for (const auto& c : p.containers) put_str(o, c);
   put_raw(o, p.owner);
   put_raw(o, static_cast<uint8_t>(p.completed));
-  put_raw(o, p.demand.n);
-  o->append(reinterpret_cast<const char*>(p.demand.c), sizeof(ContainerDemand) * static_cast<size_t>(p.demand.n));
+  put_raw(o, dem.n);
+  o->append(reinterpret_cast<const char*>(dem.c), sizeof(ContainerDemand) * static_cast<size_t>(dem.n));
 }
 struct Reader {
   std::string_view b;
@@ -783,20 +799,37 @@ bool unpack_pod(std::string_view b, CachedPod* p) {
 }
 }  // namespace
 
-void Frontend::put_pod(std::string_view uid, CachedPod pod) {
+void Frontend::put_pod(std::string_view uid, const CachedPod& meta, std::string_view raw, const Demand& dem) {
   if (uid.empty()) return;
+  const uint64_t h = uid_hash(uid);
   std::lock_guard<std::mutex> g(pod_mu_);
-  auto it = pods_.find(std::string(uid));
-  if (it != pods_.end()) {
-    it->second = std::move(pod);
-    return;
+  PodEntry* e = find_pod_locked(uid, h);
+  if (!e) {   // an empty way of the bucket, else its oldest entry (a pod filtered but never bound)
+    const size_t nb = pod_slots_.size() / kPodWays;
+    PodEntry* b = &pod_slots_[((h >> 7) % nb) * kPodWays];
+    e = &b[0];
+    for (size_t w = 0; w < kPodWays; ++w) {
+      if (b[w].h == 0) {
+        e = &b[w];
+        break;
+      }
+      if (b[w].stamp < e->stamp) e = &b[w];
+    }
+    if (e->h == 0) ++pod_live_;
+    e->h = h;
+    e->uid.assign(uid);
   }
-  pods_.emplace(std::string(uid), std::move(pod));
-  pod_order_.emplace_back(uid);
-  while (pods_.size() > pod_cap_ && !pod_order_.empty()) {
-    pods_.erase(pod_order_.front());
-    pod_order_.pop_front();
-  }
+  // assigned member by member: the entry's strings keep their capacity from pod to pod
+  e->stamp = ++pod_stamp_;
+  CachedPod& p = e->pod;
+  p.raw.assign(raw);
+  p.ns.assign(meta.ns);
+  p.name.assign(meta.name);
+  p.containers.resize(meta.containers.size());
+  for (size_t i = 0; i < meta.containers.size(); ++i) p.containers[i].assign(meta.containers[i]);
+  p.demand = dem;
+  p.completed = meta.completed;
+  p.owner = meta.owner;
 }
 
 void Frontend::prepare_bind(std::string_view body, PyRequest* r) {
@@ -810,35 +843,39 @@ void Frontend::prepare_bind(std::string_view body, PyRequest* r) {
   std::string ns = str("PodNamespace");
   if (ns.empty()) ns = "default";
   if (uid.empty() || name.empty() || node.empty()) return;
-  CachedPod pod;
-  {
-    const uint64_t tw = fast_ns();
-    std::lock_guard<std::mutex> g(pod_mu_);
-    atomic_max(&phase_max_ns[4], fast_ns() - tw);
-    auto it = pods_.find(uid);
-    if (it != pods_.end()) {
-      pod = std::move(it->second);
-      pods_.erase(it);  // one bind per pod UID (the deque entry expires lazily)
-    }
-  }
-  if (pod.name.empty()) {
-    // another worker process's filter parsed it (its bind came over another connection)
-    std::string blob;
-    if (!ledger_->take_pod_info(uid, &blob) || !unpack_pod(blob, &pod)) return;
-    bind_handoffs.fetch_add(1, std::memory_order_relaxed);
-  }
-  if (pod.name != name || pod.ns != ns || pod.completed) {
-    r->pod_json = std::move(pod.raw);   // unusual: Python decides (and reports) with the object
-    return;
-  }
   int32_t id;
   {
     PhaseTimer pt{&phase_max_ns[5]};
     id = ledger_->find_node(node);
   }
-  if (id < 0) {
-    r->pod_json = std::move(pod.raw);
-    return;
+  CachedPod pod;
+  bool cached = false;
+  {
+    const uint64_t h = uid_hash(uid);
+    const uint64_t tw = fast_ns();
+    std::lock_guard<std::mutex> g(pod_mu_);
+    atomic_max(&phase_max_ns[4], fast_ns() - tw);
+    if (PodEntry* e = find_pod_locked(uid, h)) {   // one bind per pod UID: the entry is freed
+      const CachedPod& c = e->pod;
+      cached = true;
+      if (c.name != name || c.ns != ns || c.completed || id < 0) {
+        r->pod_json = c.raw;   // unusual: Python decides (and reports) with the object
+      } else {
+        pod.containers = c.containers;
+        pod.demand = c.demand;
+        pod.owner = c.owner;
+      }
+      e->h = 0;
+      --pod_live_;
+    }
+  }
+  if (cached && !r->pod_json.empty()) return;
+  if (!cached) {
+    // another worker process's filter parsed it (its bind came over another connection)
+    std::string blob;
+    if (!ledger_->take_pod_info(uid, &blob) || !unpack_pod(blob, &pod)) return;
+    bind_handoffs.fetch_add(1, std::memory_order_relaxed);
+    if (pod.name != name || pod.ns != ns || pod.completed || id < 0) return;   // Python reads the pod itself
   }
   Options o;
   {
@@ -1414,13 +1451,21 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   Demand dem;
   std::memset(&dem, 0, sizeof(dem));
   std::string_view uid;
-  CachedPod cached;
+  // the pod's identity and containers are parsed into the last-pod record itself (its strings
+  // keep their capacity); it is valid again only once the parse succeeded with a UID
+  CachedPod& cached = last.cached;
   bool mb_annotated = false;
   if (reused) {
     dem = last.dem;
     uid = last.uid;
     mb_annotated = last.mb_annotated;
   } else {
+    last.valid = false;
+    cached.ns.clear();
+    cached.name.clear();
+    cached.containers.clear();
+    cached.completed = false;
+    cached.owner = 0;
     if (pod >= 0 && !d.is(pod, json::Type::kNull)) {
       if (!d.is(pod, json::Type::kObj)) return false;
       const int32_t md = d.get(pod, "metadata");
@@ -1432,8 +1477,8 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
           uid = d.str(u);
         }
         const int32_t nm = d.get(md, "name"), ns = d.get(md, "namespace"), del = d.get(md, "deletionTimestamp");
-        if (d.is(nm, json::Type::kStr)) cached.name = std::string(d.str(nm));
-        cached.ns = d.is(ns, json::Type::kStr) ? std::string(d.str(ns)) : std::string("default");
+        if (d.is(nm, json::Type::kStr)) cached.name.assign(d.str(nm));
+        cached.ns.assign(d.is(ns, json::Type::kStr) ? d.str(ns) : std::string_view("default"));
         if (del >= 0 && !d.is(del, json::Type::kNull) && !(d.is(del, json::Type::kStr) && d.str(del).empty()))
           cached.completed = true;
       }
@@ -1455,7 +1500,7 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
           if (!d.is(c, json::Type::kObj)) return false;
           ContainerDemand& cd = dem.c[dem.n++];
           const int32_t cn = d.get(c, "name");
-          cached.containers.emplace_back(d.is(cn, json::Type::kStr) ? std::string(d.str(cn)) : std::string());
+          cached.containers.emplace_back(d.is(cn, json::Type::kStr) ? d.str(cn) : std::string_view());
           const int32_t res = d.get(c, "resources");
           int32_t lim = -1;
           if (res >= 0 && !d.is(res, json::Type::kNull)) {
@@ -1503,7 +1548,6 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
       last.raw.assign(pod_text);
       last.uid.assign(uid);
       last.dem = dem;
-      last.cached = cached;
       last.mb_annotated = mb_annotated;
       last.valid = true;
       uid = last.uid;   // `d` is reparsed by the next request; the uid outlives it here
@@ -1624,19 +1668,17 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     normalize = normalize_;
     nominate = nominate_;
   }
-  if (nominate && !uid.empty()) ledger_->drop_nomination(std::string(uid));   // not against itself
+  if (nominate && !uid.empty()) ledger_->drop_nomination(uid);   // not against itself
   if ((pod >= 0 || reused) && !uid.empty() && !(prioritize && has_pod(uid))) {
     // filter caches the pod for its bind; priorities of the same cycle find it there
-    CachedPod cp = reused ? last.cached : std::move(cached);
-    cp.raw.assign(reused ? std::string_view(last.raw) : d.raw(pod));
-    cp.demand = dem;
+    const std::string_view raw = reused ? std::string_view(last.raw) : d.raw(pod);
     if (ledger_->attached() > 1) {
       // other worker processes share the ledger: the bind may reach one of them
       std::string& blob = s.blob;
-      pack_pod(cp, &blob);
-      if (ledger_->put_pod_info(std::string(uid), blob)) pods_published.fetch_add(1, std::memory_order_relaxed);
+      pack_pod(cached, dem, &blob);
+      if (ledger_->put_pod_info(uid, blob)) pods_published.fetch_add(1, std::memory_order_relaxed);
     }
-    put_pod(uid, std::move(cp));
+    put_pod(uid, cached, raw, dem);
   }
   std::string& r = *out;
   r.reserve(64 + 128 * static_cast<size_t>(nn));   // room for a FailedNodes entry per node
@@ -1751,7 +1793,7 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   if (nominate && lead && !uid.empty() && dem.n > 0) {
     bool wants = false;
     for (int i = 0; i < dem.n; ++i) wants = wants || dem.c[i].pct > 0 || dem.c[i].mib > 0;
-    if (wants) ledger_->nominate(ids[best], std::string(uid), dem, o);
+    if (wants) ledger_->nominate(ids[best], uid, dem, o);
   }
   if (normalize && !scores.empty()) {
     // nanogpu/state/cluster.py::_normalize (Python round(): half to even)

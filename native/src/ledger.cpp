@@ -35,6 +35,19 @@ uint64_t key_hash(const char* key) {
   return h;
 }
 
+// A pod key as the C string the table stores (NUL-terminated, < kKeyLen bytes) on the stack:
+// the key APIs take a view, so the front door's UIDs reach the table without a heap copy. A
+// key no slot can hold (empty, too long) reads as the empty key, which no slot holds either.
+struct KeyBuf {
+  char b[kKeyLen];
+  explicit KeyBuf(std::string_view k) {
+    const size_t n = k.size() < static_cast<size_t>(kKeyLen) ? k.size() : 0;
+    std::memcpy(b, k.data(), n);
+    b[n] = '\0';
+  }
+  const char* c_str() const { return b; }
+};
+
 double mono_now() {
   timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -709,7 +722,7 @@ namespace {
 constexpr int32_t kNominatedElsewhere = -1000;   // internal: release the nomination, retry
 }
 
-int32_t Ledger::reserve(int32_t id, const std::string& key, const Demand& d, const Options& o,
+int32_t Ledger::reserve(int32_t id, std::string_view key, const Demand& d, const Options& o,
                         Plan* plan) {
   int32_t rc = reserve_as(id, key, d, o, plan, kPodReserved);
   if (rc == kNominatedElsewhere) {
@@ -725,7 +738,7 @@ int32_t Ledger::reserve(int32_t id, const std::string& key, const Demand& d, con
   return rc;
 }
 
-int32_t Ledger::nominate(int32_t id, const std::string& key, const Demand& d, const Options& o) {
+int32_t Ledger::nominate(int32_t id, std::string_view key, const Demand& d, const Options& o) {
   Plan plan;
   int32_t rc = reserve_as(id, key, d, o, &plan, kPodNominated);
   if (rc == kNominatedElsewhere) {
@@ -736,20 +749,21 @@ int32_t Ledger::nominate(int32_t id, const std::string& key, const Demand& d, co
   return rc;
 }
 
-int32_t Ledger::reserve_as(int32_t id, const std::string& key, const Demand& d, const Options& o_in, Plan* plan,
+int32_t Ledger::reserve_as(int32_t id, std::string_view key, const Demand& d, const Options& o_in, Plan* plan,
                            int32_t state) {
   NodeSlot* n = node(id);
   const Options o = resolve(o_in, d);
   if (!n || !n->in_use) return kErrUnknownNode;
   if (key.empty() || key.size() >= kKeyLen) return kErrBadDemand;
-  const uint64_t h = key_hash(key.c_str());
+  const KeyBuf kb(key);
+  const uint64_t h = key_hash(kb.c_str());
   const int s = shard_of(h);
   lock_node(n);
   Unlock un{&n->mu};
   {
     lock_mu(&hdr_->shard_mu[s].m);
     Unlock us{&hdr_->shard_mu[s].m};
-    PodSlot* p = find_pod_locked(s, h, key.c_str());
+    PodSlot* p = find_pod_locked(s, h, kb.c_str());
     if (p) {
       if (p->state == kPodNominated) {
         if (p->node != id) return kNominatedElsewhere;
@@ -782,7 +796,7 @@ int32_t Ledger::reserve_as(int32_t id, const std::string& key, const Demand& d, 
   {
     lock_mu(&hdr_->shard_mu[s].m);
     Unlock us{&hdr_->shard_mu[s].m};
-    PodSlot* p = insert_pod_locked(s, h, key.c_str());
+    PodSlot* p = insert_pod_locked(s, h, kb.c_str());
     if (p && !put_record(p, d, *plan)) {
       p->state = kPodTombstone;       // no overflow record free: give the slot back
       --hdr_->shard_live[s];
@@ -807,7 +821,7 @@ int32_t Ledger::reserve_as(int32_t id, const std::string& key, const Demand& d, 
   return kOk;
 }
 
-int32_t Ledger::allocate_plan(int32_t id, const std::string& key, const Demand& d,
+int32_t Ledger::allocate_plan(int32_t id, std::string_view key, const Demand& d,
                               const Plan& plan, bool committed) {
   NodeSlot* n = node(id);
   if (!n || !n->in_use) return kErrUnknownNode;
@@ -817,14 +831,15 @@ int32_t Ledger::allocate_plan(int32_t id, const std::string& key, const Demand& 
     PodRecord r;
     if (lookup(key, &r) && r.state == kPodNominated) release(key);
   }
-  const uint64_t h = key_hash(key.c_str());
+  const KeyBuf kb(key);
+  const uint64_t h = key_hash(kb.c_str());
   const int s = shard_of(h);
   lock_node(n);
   Unlock un{&n->mu};
   {
     lock_mu(&hdr_->shard_mu[s].m);
     Unlock us{&hdr_->shard_mu[s].m};
-    PodSlot* p = find_pod_locked(s, h, key.c_str());
+    PodSlot* p = find_pod_locked(s, h, kb.c_str());
     if (p) {
       if (p->node != id) return kErrPodExists;
       if (committed) p->state = kPodCommitted;
@@ -836,7 +851,7 @@ int32_t Ledger::allocate_plan(int32_t id, const std::string& key, const Demand& 
   {
     lock_mu(&hdr_->shard_mu[s].m);
     Unlock us{&hdr_->shard_mu[s].m};
-    PodSlot* p = insert_pod_locked(s, h, key.c_str());
+    PodSlot* p = insert_pod_locked(s, h, kb.c_str());
     if (p && !put_record(p, d, plan)) {
       p->state = kPodTombstone;
       --hdr_->shard_live[s];
@@ -860,32 +875,34 @@ int32_t Ledger::allocate_plan(int32_t id, const std::string& key, const Demand& 
   return kOk;
 }
 
-int32_t Ledger::commit(const std::string& key) {
-  const uint64_t h = key_hash(key.c_str());
+int32_t Ledger::commit(std::string_view key) {
+  const KeyBuf kb(key);
+  const uint64_t h = key_hash(kb.c_str());
   const int s = shard_of(h);
   lock_mu(&hdr_->shard_mu[s].m);
   Unlock us{&hdr_->shard_mu[s].m};
-  PodSlot* p = find_pod_locked(s, h, key.c_str());
+  PodSlot* p = find_pod_locked(s, h, kb.c_str());
   if (!p) return kErrUnknownPod;
   p->state = kPodCommitted;
   return kOk;
 }
 
-int32_t Ledger::release(const std::string& key) { return release_if(key, -1); }
+int32_t Ledger::release(std::string_view key) { return release_if(key, -1); }
 
-int32_t Ledger::drop_nomination(const std::string& key) { return release_if(key, kPodNominated); }
+int32_t Ledger::drop_nomination(std::string_view key) { return release_if(key, kPodNominated); }
 
-int32_t Ledger::drop_reservation(const std::string& key) { return release_if(key, kPodReserved); }
+int32_t Ledger::drop_reservation(std::string_view key) { return release_if(key, kPodReserved); }
 
-int32_t Ledger::release_if(const std::string& key, int32_t only_state) {
+int32_t Ledger::release_if(std::string_view key, int32_t only_state) {
+  const KeyBuf kb(key);
   const bool only = only_state >= 0;
-  const uint64_t h = key_hash(key.c_str());
+  const uint64_t h = key_hash(kb.c_str());
   const int s = shard_of(h);
   int32_t id;
   {
     lock_mu(&hdr_->shard_mu[s].m);
     Unlock us{&hdr_->shard_mu[s].m};
-    PodSlot* p = find_pod_locked(s, h, key.c_str());
+    PodSlot* p = find_pod_locked(s, h, kb.c_str());
     if (!p) return kErrUnknownPod;
     if (only && p->state != only_state) return kOkExisting;
     id = p->node;
@@ -896,7 +913,7 @@ int32_t Ledger::release_if(const std::string& key, int32_t only_state) {
   Unlock un{&n->mu};
   lock_mu(&hdr_->shard_mu[s].m);
   Unlock us{&hdr_->shard_mu[s].m};
-  PodSlot* p = find_pod_locked(s, h, key.c_str());
+  PodSlot* p = find_pod_locked(s, h, kb.c_str());
   if (!p || p->node != id) return kErrUnknownPod;  // raced with another release
   if (only && p->state != only_state) return kOkExisting;   // adopted / committed meanwhile
   {
@@ -943,12 +960,13 @@ bool Ledger::holds(std::string_view key) const {
   return false;
 }
 
-bool Ledger::lookup(const std::string& key, PodRecord* out) const {
-  const uint64_t h = key_hash(key.c_str());
+bool Ledger::lookup(std::string_view key, PodRecord* out) const {
+  const KeyBuf kb(key);
+  const uint64_t h = key_hash(kb.c_str());
   const int s = shard_of(h);
   lock_mu(&hdr_->shard_mu[s].m);
   Unlock us{&hdr_->shard_mu[s].m};
-  PodSlot* p = find_pod_locked(s, h, key.c_str());
+  PodSlot* p = find_pod_locked(s, h, kb.c_str());
   if (!p) return false;
   out->key = p->key;
   out->node = p->node;
@@ -959,13 +977,14 @@ bool Ledger::lookup(const std::string& key, PodRecord* out) const {
   return true;
 }
 
-int32_t Ledger::set_pod_owner(const std::string& key, uint64_t owner) {
+int32_t Ledger::set_pod_owner(std::string_view key, uint64_t owner) {
+  const KeyBuf kb(key);
   if (key.empty() || key.size() >= kKeyLen) return kErrUnknownPod;
-  const uint64_t h = key_hash(key.c_str());
+  const uint64_t h = key_hash(kb.c_str());
   const int s = shard_of(h);
   lock_mu(&hdr_->shard_mu[s].m);
   Unlock us{&hdr_->shard_mu[s].m};
-  PodSlot* p = find_pod_locked(s, h, key.c_str());
+  PodSlot* p = find_pod_locked(s, h, kb.c_str());
   if (!p) return kErrUnknownPod;
   p->owner = owner;
   return kOk;
@@ -1086,14 +1105,15 @@ int32_t Ledger::fits_without(int32_t id, const std::vector<std::string>& victims
   // or holds on another node, frees nothing here)
   for (const std::string& key : victims) {
     if (key.empty() || key.size() >= kKeyLen) continue;
-    const uint64_t h = key_hash(key.c_str());
+    const KeyBuf kb(key);
+    const uint64_t h = key_hash(kb.c_str());
     const int s = shard_of(h);
     Demand vd;
     Plan vp;
     {
       lock_mu(&hdr_->shard_mu[s].m);
       Unlock us{&hdr_->shard_mu[s].m};
-      const PodSlot* p = find_pod_locked(s, h, key.c_str());
+      const PodSlot* p = find_pod_locked(s, h, kb.c_str());
       if (!p || p->node != id) continue;
       get_record(*p, &vd, &vp);
     }
@@ -1140,7 +1160,7 @@ std::vector<std::string> Ledger::expired_reservations(double older_than_s) const
   return expired(kPodReserved, older_than_s);
 }
 
-int32_t Ledger::drop_committed(const std::string& key) { return release_if(key, kPodCommitted); }
+int32_t Ledger::drop_committed(std::string_view key) { return release_if(key, kPodCommitted); }
 
 std::vector<std::string> Ledger::reconcile(const std::vector<std::string>& live, double before) {
   std::vector<std::string_view> v(live.begin(), live.end());
@@ -1195,17 +1215,18 @@ std::vector<std::string> Ledger::reconcile_views(const std::vector<std::string_v
   return released;
 }
 
-bool Ledger::put_pod_info(const std::string& key, std::string_view blob) {
+bool Ledger::put_pod_info(std::string_view key, std::string_view blob) {
+  const KeyBuf kb(key);
   if (key.empty() || key.size() >= static_cast<size_t>(kKeyLen) || blob.size() > static_cast<size_t>(kPodInfoBytes))
     return false;
-  const uint64_t h = key_hash(key.c_str());
+  const uint64_t h = key_hash(kb.c_str());
   const uint32_t bucket = static_cast<uint32_t>(h % (hdr_->info_cap / kPodInfoWays));
   lock_mu(&hdr_->info_mu[bucket % kPodShards].m);
   Unlock u{&hdr_->info_mu[bucket % kPodShards].m};
   PodInfoSlot* b = &info_[bucket * kPodInfoWays];
   PodInfoSlot* s = nullptr;
   for (int w = 0; w < kPodInfoWays && !s; ++w)   // the key's own slot, else an empty one
-    if (b[w].hash == h && std::strncmp(b[w].key, key.c_str(), kKeyLen) == 0) s = &b[w];
+    if (b[w].hash == h && std::strncmp(b[w].key, kb.c_str(), kKeyLen) == 0) s = &b[w];
   for (int w = 0; w < kPodInfoWays && !s; ++w)
     if (b[w].hash == 0) s = &b[w];
   if (!s) {   // a full bucket: the oldest entry goes
@@ -1215,22 +1236,23 @@ bool Ledger::put_pod_info(const std::string& key, std::string_view blob) {
   }
   s->hash = h;
   s->stamp = hdr_->info_stamp.fetch_add(1, std::memory_order_relaxed) + 1;
-  std::memcpy(s->key, key.c_str(), key.size() + 1);
+  std::memcpy(s->key, kb.c_str(), key.size() + 1);
   s->len = static_cast<uint32_t>(blob.size());
   std::memcpy(s->data, blob.data(), blob.size());
   return true;
 }
 
-bool Ledger::take_pod_info(const std::string& key, std::string* blob) {
+bool Ledger::take_pod_info(std::string_view key, std::string* blob) {
+  const KeyBuf kb(key);
   if (key.empty() || key.size() >= static_cast<size_t>(kKeyLen)) return false;
-  const uint64_t h = key_hash(key.c_str());
+  const uint64_t h = key_hash(kb.c_str());
   const uint32_t bucket = static_cast<uint32_t>(h % (hdr_->info_cap / kPodInfoWays));
   lock_mu(&hdr_->info_mu[bucket % kPodShards].m);
   Unlock u{&hdr_->info_mu[bucket % kPodShards].m};
   PodInfoSlot* b = &info_[bucket * kPodInfoWays];
   for (int w = 0; w < kPodInfoWays; ++w) {
     PodInfoSlot& s = b[w];
-    if (s.hash != h || std::strncmp(s.key, key.c_str(), kKeyLen) != 0) continue;
+    if (s.hash != h || std::strncmp(s.key, kb.c_str(), kKeyLen) != 0) continue;
     blob->assign(s.data, std::min<uint32_t>(s.len, kPodInfoBytes));
     s.hash = 0;
     return true;
