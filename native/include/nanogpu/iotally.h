@@ -24,7 +24,12 @@ enum IoKind : int {
   kFeEfdRead,       // mailbox eventfd read
   kFeSubmit,        // bind handed to the writer (queue + eventfd write when it sleeps)
   kFeParseBind,     // bind arguments parsed, pod looked up, reserve
-  kFeVerb,          // filter / priorities verb (JSON in, answer out)
+  kFeVerb,          // filter / priorities verb (JSON in, answer out); its parts:
+  kFeVerbPod,       //   the args framed, the pod parsed (or matched with the last one)
+  kFeVerbNames,     //   the node list matched / scanned, ids resolved
+  kFeVerbCache,     //   nomination dropped, the pod cached for its bind
+  kFeVerbAssume,    //   Ledger::assume_many
+  kFeVerbNominate,  //   Ledger::nominate (priorities)
   // bind writer thread (evented) / BindIo
   kWrWait,          // epoll_wait (count only)
   kWrEfdRead,
@@ -41,7 +46,8 @@ enum IoKind : int {
 inline const char* io_kind_name(int k) {
   static const char* const names[kIoKinds] = {
       "fe_spin_empty", "fe_spin_hit", "fe_wait", "fe_recv", "fe_send_cycle", "fe_send_other", "fe_efd_read",
-      "fe_submit", "fe_parse_bind", "fe_verb", "wr_wait", "wr_efd_read", "wr_send", "wr_recv",
+      "fe_submit", "fe_parse_bind", "fe_verb", "fe_verb_pod", "fe_verb_names", "fe_verb_cache",
+      "fe_verb_assume", "fe_verb_nominate", "wr_wait", "wr_efd_read", "wr_send", "wr_recv",
       "wr_build", "wr_commit", "pw_recv", "pw_filter"};
   return k >= 0 && k < kIoKinds ? names[k] : "?";
 }

@@ -1374,6 +1374,7 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   std::vector<int32_t>& scores = s.scores;
   LastPod& last = s.last;
   IdCache& idc = s.idc;
+  uint64_t io0 = io_t0();
   if (idc.owner != ledger_.get()) idc = IdCache{}, idc.owner = ledger_.get();
   if (body.empty()) return false;
   // kube-scheduler's ExtenderArgs as Go's encoding/json writes them (struct field order, no
@@ -1567,6 +1568,8 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   // kube-scheduler sends the same node list over and over, so each worker remembers the ids
   // of the last lists it resolved (keyed by the array's raw text) and only checks that slot
   // `id` still carries that name; a miss falls back to the ledger's name index.
+  io_end(kFeVerbPod, io0);
+  io0 = io_t0();
   const uint64_t epoch = ledger_->node_epoch();
   int slot = scanned ? -1 : framed && found != -2 ? found : idc.find(raw_names);
   // a cached list's names are read through its token offsets into this request's text (no
@@ -1668,6 +1671,8 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     normalize = normalize_;
     nominate = nominate_;
   }
+  io_end(kFeVerbNames, io0);
+  io0 = io_t0();
   if (nominate && !uid.empty()) ledger_->drop_nomination(uid);   // not against itself
   if ((pod >= 0 || reused) && !uid.empty() && !(prioritize && has_pod(uid))) {
     // filter caches the pod for its bind; priorities of the same cycle find it there
@@ -1685,7 +1690,11 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   if (!prioritize) {
     rcs.resize(ids.size());
     scores.resize(ids.size());
-    ledger_->assume_many(ids.data(), static_cast<int>(ids.size()), dem, o, rcs.data(), scores.data());
+    io_end(kFeVerbCache, io0);
+    {
+      IoTimer it{kFeVerbAssume};
+      ledger_->assume_many(ids.data(), static_cast<int>(ids.size()), dem, o, rcs.data(), scores.data());
+    }
     // written straight into the reply; a fitting node's name is its request token, as is
     r.clear();
     r += "{\"Nodes\":null,\"NodeNames\":";
@@ -1748,7 +1757,11 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   }
   scores.resize(ids.size());
   rcs.resize(ids.size());
-  ledger_->assume_many(ids.data(), static_cast<int>(ids.size()), dem, o, rcs.data(), scores.data());
+  io_end(kFeVerbCache, io0);
+  {
+    IoTimer it{kFeVerbAssume};
+    ledger_->assume_many(ids.data(), static_cast<int>(ids.size()), dem, o, rcs.data(), scores.data());
+  }
   int64_t best = -1;
   int n_best = 0;
   int32_t second = -1;   // best score among the other fitting nodes
@@ -1793,7 +1806,10 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   if (nominate && lead && !uid.empty() && dem.n > 0) {
     bool wants = false;
     for (int i = 0; i < dem.n; ++i) wants = wants || dem.c[i].pct > 0 || dem.c[i].mib > 0;
-    if (wants) ledger_->nominate(ids[best], uid, dem, o);
+    if (wants) {
+      IoTimer it{kFeVerbNominate};
+      ledger_->nominate(ids[best], uid, dem, o);
+    }
   }
   if (normalize && !scores.empty()) {
     // nanogpu/state/cluster.py::_normalize (Python round(): half to even)
