@@ -139,6 +139,8 @@ struct BindIo::Conn {
   std::vector<Pending> pend;   // answers still due, in request order, from `head`
   size_t head = 0;
   uint64_t deadline_ns = 0;   // the answers are due by then (KubeWriter timeout_s)
+  bool lowat = false;         // SO_RCVLOWAT raised: arriving bytes do not wake the loop
+  uint64_t lazy_since = 0;    // in lazy_ since (0: not lazy)
   int npend() const { return static_cast<int>(pend.size() - head); }
 };
 
@@ -192,6 +194,8 @@ bool BindIo::resolve() {
 void BindIo::close_conn(Conn& c) {
   if (c.ssl) SSL_free(c.ssl);
   c.ssl = nullptr;
+  c.lowat = false;
+  c.lazy_since = 0;   // drain_lazy drops it from lazy_
   if (c.fd >= 0) {
     epoll_ctl(ep_, EPOLL_CTL_DEL, c.fd, nullptr);
     ::close(c.fd);
@@ -454,7 +458,7 @@ void BindIo::drive(size_t k, uint32_t events) {
         const int rc = parse_response(c.in, eof && c.npend() == 1, &status, &body, &used, &close);
         if (rc < 0) return fail(k, "bad answer from the API server");
         if (rc == 0) {
-          if (!eof) return;   // more bytes to come
+          if (!eof) return go_lazy(k);   // more bytes to come
           if (c.got_any && c.in.empty() && (delivered || c.head > 0)) break;   // answered some, then closed
           return fail(k, "connection to the API server failed");
         }
@@ -476,6 +480,53 @@ void BindIo::drive(size_t k, uint32_t events) {
     }
     return;
   }
+}
+
+// Only label answers of answered binds are due on connection k: they are read by a later
+// pass (drain_lazy) instead of waking the loop when they arrive.
+void BindIo::go_lazy(size_t k) {
+  Conn& c = *conns_[k];
+  if (c.ssl || c.fd < 0 || c.npend() <= 0) return;
+  for (size_t i = c.head; i < c.pend.size(); ++i) {
+    const Pending& p = c.pend[i];
+    if (p.which != 0 || !slots_[static_cast<size_t>(p.job)] || !slots_[static_cast<size_t>(p.job)]->answered) return;
+  }
+  if (!c.lowat) {
+    const int big = 1 << 30;
+    if (setsockopt(c.fd, SOL_SOCKET, SO_RCVLOWAT, &big, sizeof big) != 0) return;
+    c.lowat = true;
+  }
+  if (!c.lazy_since) {
+    c.lazy_since = ns_now();
+    lazy_.push_back(k);
+  }
+}
+
+// the lazy connections whose label answers are due by now are read (one recv each; an answer
+// still on its way leaves the connection lazy for the next pass)
+void BindIo::drain_lazy(uint64_t now) {
+  size_t keep = 0;
+  for (size_t i = 0; i < lazy_.size(); ++i) {
+    const size_t k = lazy_[i];
+    Conn& c = *conns_[k];
+    if (!c.lazy_since || c.fd < 0) {
+      c.lazy_since = 0;
+      continue;   // closed (or failed) meanwhile
+    }
+    if (now - c.lazy_since < kLazyNs) {
+      lazy_[keep++] = k;
+      continue;
+    }
+    c.lazy_since = 0;
+    drive(k, EPOLLIN);   // delivers what came; go_lazy() re-queues it if nothing did
+    if (c.lazy_since) {
+      // re-queued at the end of lazy_ by go_lazy (now past i): keep one entry only
+      lazy_.pop_back();
+      c.lazy_since = now;
+      lazy_[keep++] = k;
+    }
+  }
+  lazy_.resize(keep);
 }
 
 // starts slot s's requests on an idle (or new) connection: the binding, then (label mode)
@@ -507,6 +558,11 @@ void BindIo::launch(int64_t s) {
   c.retried = false;
   c.deadline_ns = ns_now() + timeout_ns_;
   c.reused = c.fd >= 0;
+  if (c.fd >= 0 && c.lowat) {   // idle again after lazy answers: answers wake the loop again
+    const int one = 1;
+    setsockopt(c.fd, SOL_SOCKET, SO_RCVLOWAT, &one, sizeof one);
+    c.lowat = false;
+  }
   if (c.fd >= 0) {
     c.st = kSending;
   } else if (!open_conn(k)) {
@@ -639,6 +695,11 @@ void BindIo::launch_labels() {
   c.retried = false;
   c.deadline_ns = ns_now() + timeout_ns_;
   c.reused = c.fd >= 0;
+  if (c.fd >= 0 && c.lowat) {
+    const int one = 1;
+    setsockopt(c.fd, SOL_SOCKET, SO_RCVLOWAT, &one, sizeof one);
+    c.lowat = false;
+  }
   if (c.fd >= 0) {
     c.st = kSending;
   } else if (!open_conn(k)) {
@@ -663,6 +724,7 @@ void BindIo::pump() {
     for (size_t i = 0; i < kick_.size(); ++i) drive(kick_[i], 0);
     kick_.clear();
   }
+  if (!lazy_.empty()) drain_lazy(ns_now());
   scan_deadlines(ns_now());
   for (size_t i = 0; i < kick_.size(); ++i) drive(kick_[i], 0);
   kick_.clear();
