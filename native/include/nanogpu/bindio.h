@@ -103,9 +103,11 @@ class BindIo {
   // Lazy label answers: once a bind's binding has answered (and kube-scheduler has its reply),
   // the label PATCH's answer behind it on the connection is not worth a wake-up of its own. The
   // connection's receive low-water mark goes up (SO_RCVLOWAT: the kernel does not signal the
-  // answer's arrival) and the answer is read by a later pass of the loop, which runs for the
-  // next bind anyway, kLazyNs or more after the binding answered. Plain TCP only.
-  static constexpr uint64_t kLazyNs = 20'000;
+  // answer's arrival). The next bind launched goes out on that connection behind it, and the
+  // read of its binding answer takes the label answer along; a connection no bind reuses within
+  // kLazyNs is read by a pass of the loop (the loop comes back within a millisecond while any is
+  // lazy). Plain TCP only.
+  static constexpr uint64_t kLazyNs = 1'000'000;
   std::vector<size_t> lazy_;
 };
 

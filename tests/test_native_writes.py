@@ -610,3 +610,57 @@ def test_an_api_server_that_never_answers_times_the_bind_out(mode):
         for c in held:
             c.close()
         lsock.close()
+
+
+@pytest.mark.parametrize("mode", ["evented", "inline"])
+def test_many_concurrent_binds_with_lazy_label_answers_all_complete(mode):
+    """The evented writer reads a label PATCH's answer lazily (the connection's low-water mark
+    raised once the binding answered) and pipelines the next bind behind it. Driven by the
+    native kube-scheduler stand-in (binds back to back, many in flight) against the native API
+    server, every bind is answered once, every pod is bound with its label, and the writer ends
+    with nothing in flight."""
+    from nanogpu import _native as NN
+    from nanogpu.sim.driver import NativeSchedulerDriver, node_capacities
+
+    async def main():
+        srv = NN.ApiServer("127.0.0.1", 0, 2, 8192)
+        nodes = []
+        for i in range(8):
+            st, body = srv.call("POST", "/api/v1/nodes", json.dumps(pu.make_node(f"n{i}", 8, synthetic_mi355x(8).to_json())))
+            nodes.append(json.loads(body))
+        rt = Runtime(Config(kube_api=f"http://127.0.0.1:{srv.port}", port=0, host="127.0.0.1",
+                            policy_config_path="/nonexistent", bind_writer_mode=mode))
+        await rt.start()
+        loop = asyncio.get_running_loop()
+        try:
+            for rnd in range(3):
+                pods = []
+                for i in range(400):
+                    p = pu.make_pod(f"r{rnd}-c{i}", [("main", 5)])
+                    st, body = srv.call("POST", "/api/v1/namespaces/default/pods", json.dumps(p))
+                    assert st == 201
+                    pods.append(json.loads(body))
+                drv = NativeSchedulerDriver("127.0.0.1", rt.bound_port, [n["metadata"]["name"] for n in nodes],
+                                            node_capacities(nodes), bind_threads=16)
+                res = await asyncio.wait_for(loop.run_in_executor(None, drv.run, pods), 60)
+                assert res.scheduled == len(pods) and res.failed == 0, (res.scheduled, res.failed)
+                for _ in range(300):   # the last label answers: read within a few milliseconds
+                    if rt.native.fe.kube_writer_stats()["inflight"] == 0:
+                        break
+                    await asyncio.sleep(0.01)
+                assert rt.native.fe.kube_writer_stats()["inflight"] == 0
+                for p in pods:
+                    st, body = srv.call("GET", f"/api/v1/namespaces/default/pods/{pu.meta(p)['name']}", "")
+                    got = json.loads(body)
+                    assert got["spec"].get("nodeName") and got["metadata"]["labels"].get(T.GPU_ASSUME) == "true", got
+                for p in pods:   # room for the next round
+                    srv.call("DELETE", f"/api/v1/namespaces/default/pods/{pu.meta(p)['name']}", "")
+                for _ in range(300):
+                    if rt.state.ledger.n_pods == 0:
+                        break
+                    await asyncio.sleep(0.01)
+        finally:
+            await rt.stop()
+            srv.stop()
+
+    asyncio.run(main())
