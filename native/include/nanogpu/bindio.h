@@ -38,9 +38,8 @@ class BindIo {
   // binds and batched label PATCHes not finished yet
   size_t inflight() const { return inflight_ + labels_out_ + label_wait_.size(); }
   size_t waiting() const { return waiting_.size(); }
-  // label PATCHes held for a batch, or label answers read lazily: the owner's loop must come
-  // back within about a millisecond
-  bool labels_waiting() const { return !label_wait_.empty() || !lazy_.empty(); }
+  // label PATCHes held for a batch: the owner's loop must come back within about a millisecond
+  bool labels_waiting() const { return !label_wait_.empty(); }
   // Stop: every bind still in flight or waiting goes to the slow path with what it got
   // (`why` for answers that never came). The connections are closed.
   void abandon(const char* why);
@@ -66,8 +65,6 @@ class BindIo {
   void queue_label(BindJob&& j, std::string&& patch);
   void label_done(int64_t ls, int status, std::string body);
   void launch_labels();
-  void go_lazy(size_t k);
-  void drain_lazy(uint64_t now);
 
   KubeWriter* kw_;
   int ep_;
@@ -100,15 +97,6 @@ class BindIo {
   std::deque<int64_t> label_wait_;
   uint64_t label_oldest_ns_ = 0;
   size_t labels_out_ = 0;   // sent, answer due
-  // Lazy label answers: once a bind's binding has answered (and kube-scheduler has its reply),
-  // the label PATCH's answer behind it on the connection is not worth a wake-up of its own. The
-  // connection's receive low-water mark goes up (SO_RCVLOWAT: the kernel does not signal the
-  // answer's arrival). The next bind launched goes out on that connection behind it, and the
-  // read of its binding answer takes the label answer along; a connection no bind reuses within
-  // kLazyNs is read by a pass of the loop (the loop comes back within a millisecond while any is
-  // lazy). Plain TCP only.
-  static constexpr uint64_t kLazyNs = 1'000'000;
-  std::vector<size_t> lazy_;
 };
 
 }  // namespace nanogpu

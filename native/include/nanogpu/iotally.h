@@ -17,6 +17,7 @@ enum IoKind : int {
   // front-door worker threads
   kFeSpinEmpty,     // polling epoll_wait that found nothing (the busy poll)
   kFeSpinHit,       // polling epoll_wait that returned events
+  kFeSpinAfterPrio, // the part of fe_spin_empty spent after a priorities answer (the rest: after a filter's)
   kFeWait,          // blocking epoll_wait (time includes sleep: count only is CPU-meaningful)
   kFeRecv,          // recv() of a kube-scheduler request
   kFeSendCycle,     // send() of a filter / priorities answer
@@ -45,7 +46,7 @@ enum IoKind : int {
 
 inline const char* io_kind_name(int k) {
   static const char* const names[kIoKinds] = {
-      "fe_spin_empty", "fe_spin_hit", "fe_wait", "fe_recv", "fe_send_cycle", "fe_send_other", "fe_efd_read",
+      "fe_spin_empty", "fe_spin_hit", "fe_spin_after_prio", "fe_wait", "fe_recv", "fe_send_cycle", "fe_send_other", "fe_efd_read",
       "fe_submit", "fe_parse_bind", "fe_verb", "fe_verb_pod", "fe_verb_names", "fe_verb_cache",
       "fe_verb_assume", "fe_verb_nominate", "wr_wait", "wr_efd_read", "wr_send", "wr_recv",
       "wr_build", "wr_commit", "pw_recv", "pw_filter"};

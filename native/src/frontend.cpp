@@ -513,6 +513,7 @@ struct Frontend::Worker {
   std::atomic<bool> mb_pending{false};
   uint64_t next_conn = 1;
   uint64_t cycle_reply_ns = 0;   // last filter / priorities reply handed to the kernel
+  bool cycle_was_prio = false;   // ... and whether it was a priorities answer (io tally)
   VerbScratch scratch;           // the verbs' per-request scratch (this worker's thread only)
 };
 
@@ -957,6 +958,7 @@ void Frontend::run(Worker* w) {
       // with bind answers due, wake at least for the BindIo's deadline scan
       n = epoll_wait(w->ep, evs, 128, polling ? 0 : bio && bio->labels_waiting() ? 1 : bio && bio->inflight() ? 100 : 200);
     }
+    if (io0 && polling && !nap && n <= 0 && w->cycle_was_prio) g_io.add(kFeSpinAfterPrio, __rdtsc() - io0);
     io_end(polling && !nap ? (n > 0 ? kFeSpinHit : kFeSpinEmpty) : kFeWait, io0);
     w->parked.store(false, std::memory_order_relaxed);
     const uint64_t t_batch = n > 0 ? fast_ns() : 0;
@@ -1234,6 +1236,7 @@ void Frontend::process(Worker* w, Conn* c) {
       c->in.erase(0, consumed);
       flush(w, c, kFeSendCycle);
       w->cycle_reply_ns = fast_ns();   // the scheduling cycle's next request is due: spin for it
+      w->cycle_was_prio = path == "/scheduler/priorities";
       if (!w->conns.count(id)) return;
     } else {
       std::string m(method), pth(path), q(query), b(body);   // owned: the Python side keeps them

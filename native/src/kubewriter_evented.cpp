@@ -20,13 +20,11 @@
 #include <openssl/ssl.h>
 #include <openssl/x509v3.h>
 #include <sys/epoll.h>
-#include <sys/ioctl.h>
 
 #include <charconv>
 #include <sys/socket.h>
 #include <unistd.h>
 
-#include <algorithm>
 #include <cerrno>
 #include <chrono>
 #include <cstring>
@@ -141,8 +139,6 @@ struct BindIo::Conn {
   std::vector<Pending> pend;   // answers still due, in request order, from `head`
   size_t head = 0;
   uint64_t deadline_ns = 0;   // the answers are due by then (KubeWriter timeout_s)
-  int lowat = 1;              // the socket's SO_RCVLOWAT (kLowatLazy: arriving bytes do not wake the loop)
-  uint64_t lazy_since = 0;    // in lazy_ since (0: not lazy)
   int npend() const { return static_cast<int>(pend.size() - head); }
 };
 
@@ -196,8 +192,6 @@ bool BindIo::resolve() {
 void BindIo::close_conn(Conn& c) {
   if (c.ssl) SSL_free(c.ssl);
   c.ssl = nullptr;
-  c.lowat = 1;
-  c.lazy_since = 0;   // drain_lazy drops it from lazy_
   if (c.fd >= 0) {
     epoll_ctl(ep_, EPOLL_CTL_DEL, c.fd, nullptr);
     ::close(c.fd);
@@ -460,7 +454,7 @@ void BindIo::drive(size_t k, uint32_t events) {
         const int rc = parse_response(c.in, eof && c.npend() == 1, &status, &body, &used, &close);
         if (rc < 0) return fail(k, "bad answer from the API server");
         if (rc == 0) {
-          if (!eof) return go_lazy(k);   // more bytes to come
+          if (!eof) return;   // more bytes to come
           if (c.got_any && c.in.empty() && (delivered || c.head > 0)) break;   // answered some, then closed
           return fail(k, "connection to the API server failed");
         }
@@ -477,7 +471,6 @@ void BindIo::drive(size_t k, uint32_t events) {
         deliver_rest(c, "connection to the API server closed before every answer");
       }
       c.st = kIdle;
-      c.lazy_since = 0;   // every answer is in: no longer lazy (launch / drain_lazy skip its entry)
       idle_.push_back(k);
       return;
     }
@@ -485,114 +478,22 @@ void BindIo::drive(size_t k, uint32_t events) {
   }
 }
 
-namespace {
-constexpr int kLowatLazy = 1 << 30;
-bool set_lowat(int fd, int* cur, int v) {
-  if (*cur == v) return true;
-  if (setsockopt(fd, SOL_SOCKET, SO_RCVLOWAT, &v, sizeof v) != 0) return false;
-  *cur = v;
-  return true;
-}
-}  // namespace
-
-// More bytes are due on connection k. When they are only label answers of answered binds, they
-// are read later (a bind pipelined behind them, or drain_lazy) instead of waking the loop when
-// they arrive; otherwise whatever arrives wakes it (a low-water mark a launch raised is reset).
-void BindIo::go_lazy(size_t k) {
-  Conn& c = *conns_[k];
-  if (c.fd < 0) return;
-  bool lazy = !c.ssl && c.npend() > 0;
-  for (size_t i = c.head; lazy && i < c.pend.size(); ++i) {
-    const Pending& p = c.pend[i];
-    lazy = p.which == 0 && slots_[static_cast<size_t>(p.job)] && slots_[static_cast<size_t>(p.job)]->answered;
-  }
-  if (!lazy || !set_lowat(c.fd, &c.lowat, kLowatLazy)) {
-    if (!set_lowat(c.fd, &c.lowat, 1)) fail(k, "connection to the API server failed");
-    return;
-  }
-  if (!c.lazy_since) {
-    c.lazy_since = ns_now();
-    lazy_.push_back(k);
-  }
-}
-
-// the lazy connections whose label answers are due by now are read (one recv each; an answer
-// still on its way leaves the connection lazy for the next pass)
-void BindIo::drain_lazy(uint64_t now) {
-  size_t keep = 0;
-  for (size_t i = 0; i < lazy_.size(); ++i) {
-    const size_t k = lazy_[i];
-    Conn& c = *conns_[k];
-    if (!c.lazy_since || c.fd < 0 || c.st != kReceiving || c.npend() <= 0) {
-      c.lazy_since = 0;
-      continue;   // answered, closed or failed meanwhile
-    }
-    if (now - c.lazy_since < kLazyNs) {
-      lazy_[keep++] = k;
-      continue;
-    }
-    c.lazy_since = 0;
-    drive(k, EPOLLIN);   // delivers what came; go_lazy() re-queues it if nothing did
-    if (c.lazy_since) {
-      // re-queued at the end of lazy_ by go_lazy (now past i): keep one entry only
-      lazy_.pop_back();
-      c.lazy_since = now;
-      lazy_[keep++] = k;
-    }
-  }
-  lazy_.resize(keep);
-}
-
 // starts slot s's requests on an idle (or new) connection: the binding, then (label mode)
 // the label PATCH pipelined behind it
 void BindIo::launch(int64_t s) {
   Job& jb = *slots_[static_cast<size_t>(s)];
   size_t k;
-  // A connection whose only due answers are lazy label answers is used first: the new bind is
-  // pipelined behind them, and the read that takes its binding answer takes theirs too (one
-  // read, no drain of its own). Its low-water mark is set just above the bytes already waiting,
-  // so the binding answer, and nothing before it, wakes the loop.
-  bool behind_lazy = false;
-  while (!lazy_.empty()) {
-    k = lazy_.back();
-    lazy_.pop_back();
-    Conn& lc = *conns_[k];
-    if (!lc.lazy_since || lc.fd < 0 || lc.st != kReceiving || lc.npend() <= 0) {
-      lc.lazy_since = 0;
-      continue;
-    }
-    lc.lazy_since = 0;
-    int queued = 0;
-    if (ioctl(lc.fd, FIONREAD, &queued) == 0 && queued >= 0 && queued < kLowatLazy - 1 &&
-        set_lowat(lc.fd, &lc.lowat, queued + 1)) {
-      behind_lazy = true;
-      break;
-    }
-    // no way to set the mark: the connection goes on as an ordinary one once drained
-    set_lowat(lc.fd, &lc.lowat, 1);
-    kick_.push_back(k);   // drive() reads what is there
-  }
-  if (!behind_lazy) {
-    if (!idle_.empty()) {
-      k = idle_.back();
-      idle_.pop_back();
-    } else {
-      k = conns_.size();
-      conns_.push_back(std::make_unique<Conn>());
-    }
+  if (!idle_.empty()) {
+    k = idle_.back();
+    idle_.pop_back();
+  } else {
+    k = conns_.size();
+    conns_.push_back(std::make_unique<Conn>());
   }
   Conn& c = *conns_[k];
   request(&c.out, "POST", jb.j, true, kJsonE, jb.binding);
-  if (!behind_lazy) {
-    c.pend.clear();
-    c.head = 0;
-    c.in.clear();
-    c.got_any = false;
-    c.retried = false;
-  } else {
-    // the answers due ahead of this bind were never re-sendable: no fresh-connection retry
-    c.retried = true;
-  }
+  c.pend.clear();
+  c.head = 0;
   c.pend.push_back(Pending{s, 1});
   if (kw_->label_ && !jb.batch_label) {
     thread_local std::string second;
@@ -601,9 +502,10 @@ void BindIo::launch(int64_t s) {
     c.pend.push_back(Pending{s, 0});
   }
   c.off = 0;
+  c.in.clear();
+  c.got_any = false;
+  c.retried = false;
   c.deadline_ns = ns_now() + timeout_ns_;
-  // idle after lazy answers: answers wake the loop again (a mark that cannot be set: a new one)
-  if (!behind_lazy && c.fd >= 0 && !set_lowat(c.fd, &c.lowat, 1)) close_conn(c);
   c.reused = c.fd >= 0;
   if (c.fd >= 0) {
     c.st = kSending;
@@ -737,7 +639,6 @@ void BindIo::launch_labels() {
   c.retried = false;
   c.deadline_ns = ns_now() + timeout_ns_;
   c.reused = c.fd >= 0;
-  if (c.fd >= 0 && !set_lowat(c.fd, &c.lowat, 1)) close_conn(c);
   if (c.fd >= 0) {
     c.st = kSending;
   } else if (!open_conn(k)) {
@@ -762,7 +663,6 @@ void BindIo::pump() {
     for (size_t i = 0; i < kick_.size(); ++i) drive(kick_[i], 0);
     kick_.clear();
   }
-  if (!lazy_.empty()) drain_lazy(ns_now());
   scan_deadlines(ns_now());
   for (size_t i = 0; i < kick_.size(); ++i) drive(kick_[i], 0);
   kick_.clear();

@@ -613,12 +613,11 @@ def test_an_api_server_that_never_answers_times_the_bind_out(mode):
 
 
 @pytest.mark.parametrize("mode", ["evented", "inline"])
-def test_many_concurrent_binds_with_lazy_label_answers_all_complete(mode):
-    """The evented writer reads a label PATCH's answer lazily (the connection's low-water mark
-    raised once the binding answered) and pipelines the next bind behind it. Driven by the
-    native kube-scheduler stand-in (binds back to back, many in flight) against the native API
-    server, every bind is answered once, every pod is bound with its label, and the writer ends
-    with nothing in flight."""
+def test_many_concurrent_binds_with_label_patches_all_complete(mode):
+    """Driven by the native kube-scheduler stand-in (binds back to back, many in flight) against
+    the native API server, every bind is answered once, every pod is bound with its label
+    (pipelined behind its binding on a connection the writer keeps), and the writer ends with
+    nothing in flight."""
     from nanogpu import _native as NN
     from nanogpu.sim.driver import NativeSchedulerDriver, node_capacities
 
