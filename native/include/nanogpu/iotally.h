@@ -31,6 +31,8 @@ enum IoKind : int {
   kFeVerbCache,     //   nomination dropped, the pod cached for its bind
   kFeVerbAssume,    //   Ledger::assume_many
   kFeVerbNominate,  //   Ledger::nominate (priorities)
+  kLedgerChoose,    // a node's plan computed (snapshot + choose) on a score-memo and plan-cache miss
+  kLedgerCacheHit,  // a node's score taken from the plan cache on a memo miss
   // bind writer thread (evented) / BindIo
   kWrWait,          // epoll_wait (count only)
   kWrEfdRead,
@@ -48,7 +50,7 @@ inline const char* io_kind_name(int k) {
   static const char* const names[kIoKinds] = {
       "fe_spin_empty", "fe_spin_hit", "fe_spin_after_prio", "fe_wait", "fe_recv", "fe_send_cycle", "fe_send_other", "fe_efd_read",
       "fe_submit", "fe_parse_bind", "fe_verb", "fe_verb_pod", "fe_verb_names", "fe_verb_cache",
-      "fe_verb_assume", "fe_verb_nominate", "wr_wait", "wr_efd_read", "wr_send", "wr_recv",
+      "fe_verb_assume", "fe_verb_nominate", "ledger_choose", "ledger_cache_hit", "wr_wait", "wr_efd_read", "wr_send", "wr_recv",
       "wr_build", "wr_commit", "pw_recv", "pw_filter"};
   return k >= 0 && k < kIoKinds ? names[k] : "?";
 }

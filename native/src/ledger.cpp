@@ -1,6 +1,7 @@
 // Native cluster ledger (see ledger.h). Reference parity: pkg/dealer/dealer.go
 // (Assume :89-136, Score :138-153, Bind :155-203, Allocate :205-228, Release :230-255,
 // KnownPod :257-262, getNodeInfo :271-301) and pkg/dealer/node.go (PlanCache :18-98).
+#include "nanogpu/iotally.h"
 #include "nanogpu/ledger.h"
 
 #include <errno.h>
@@ -686,10 +687,13 @@ void Ledger::assume_many(const int32_t* ids, int count, const Demand& d, const O
       score[i] = me->score;
       continue;
     }
+    const uint64_t io0 = io_t0();
     if (cache_get_score(CacheKey{id, gen, dh, oh}, &rc[i], &score[i])) {
       if (me) *me = ScoreMemo::E{gen + 1, rc[i], score[i]};
+      io_end(kLedgerCacheHit, io0);
       continue;
     }
+    IoTimer it{kLedgerChoose};
     NodeSnapshot snap;
     if (!snapshot(id, &snap)) {
       rc[i] = kErrUnknownNode;
