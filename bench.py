@@ -133,6 +133,8 @@ def parse_args():
     ap.add_argument("--frontend-threads", type=int, default=1, help="native front door epoll workers")
     ap.add_argument("--busy-poll-us", type=int, default=int(os.environ.get("NANOGPU_BUSY_POLL_US", "20")),
                     help="native front door busy-poll window")
+    ap.add_argument("--busy-poll-prio-us", type=int, default=int(os.environ.get("NANOGPU_BUSY_POLL_PRIO_US", "-1")),
+                    help="the busy-poll window after a priorities answer (-1: --busy-poll-us, 0: sleep)")
     ap.add_argument("--driver", default="native", choices=["native", "python"],
                     help="kube-scheduler stand-in: C++ (native/src/schedsim.cpp) or the Python threaded one")
     ap.add_argument("--cpu-affinity", default="auto", choices=["auto", "none"],
@@ -879,7 +881,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     cfg = Config(port=0, host="127.0.0.1", priority=args.policy, compat=args.compat, ledger_path=ledger_path,
                  max_nodes=max(1024, args.nodes), max_pods=max(65536, 4 * args.pods),
                  policy_config_path="/nonexistent/policy.yaml", reservation_ttl_s=3600,
-                 busy_poll_us=args.busy_poll_us, frontend_threads=args.frontend_threads,
+                 busy_poll_us=args.busy_poll_us, busy_poll_prio_us=args.busy_poll_prio_us,
+                 frontend_threads=args.frontend_threads,
                  nominate=not args.no_nominate,
                  bind_writer_threads=args.bind_writer_threads or max(2, 16 // d.world),
                  bind_writer_mode=args.bind_writer_mode, assume_label=not args.no_assume_label,
@@ -1341,7 +1344,8 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
                                   f"({args.apiserver_threads or min(16, max(4, d.world))} IO threads)"),
                    "cpus_rank0": _cpulist(cpus),
                    "cpus_apiserver": _cpulist(api_proc.cpus) if api_proc is not None else None,
-                   "frontend": f"{args.frontend_threads} threads, busy-poll {args.busy_poll_us} us"},
+                   "frontend": f"{args.frontend_threads} threads, busy-poll {args.busy_poll_us} us"
+                               + (f" ({args.busy_poll_prio_us} us after priorities)" if args.busy_poll_prio_us >= 0 else "")},
         # physical cores vs SMT siblings of the pinned CPUs, and how busy the siblings were
         "cpu_layout": {"rank0": affinity.cpu_layout(cpus),
                        "apiserver": affinity.cpu_layout(api_proc.cpus) if api_proc is not None else None},
@@ -1444,6 +1448,7 @@ def main() -> int:
         # a rank keeps ~6 threads busy (2 front-door workers, its Python loop and executor, the
         # stand-in's cycle and binder): with fewer cores, spinning workers would steal them
         args.busy_poll_us = 0
+        args.busy_poll_prio_us = 0
     drv_proc, conn = None, None
     if not args.inproc_driver:
         # started before anything touches the GPU: a fresh interpreter, no HIP state

@@ -76,6 +76,7 @@ class Config:
     identity: str = ""
     frontend_threads: int = 4
     busy_poll_us: int = 0                       # native workers spin this long after an event
+    busy_poll_prio_us: int = -1                 # ... after a priorities answer (-1: busy_poll_us)
     cpu_affinity: str = "none"                  # none | auto (one L3 domain per worker) | cpu list
     request_sizes: list = field(default_factory=list)   # share sizes binpack's waste model fixes
     learn_sizes: bool = True                    # ...plus the sizes the ledger sees requested
@@ -215,6 +216,7 @@ class Runtime:
                 self.native = server.NativeServer(router, self.cfg.host, self.cfg.port, self.cfg.frontend_threads)
                 self.native.fe.set_serving(True)   # the ledger's shared flag gates it as well
                 self.native.fe.set_busy_poll_us(self.cfg.busy_poll_us)
+                self.native.fe.set_busy_poll_prio_us(self.cfg.busy_poll_prio_us)
                 self.native.fe.set_bind_first(self.cfg.bind_first)
                 self.native.fe.set_spin_nap(self.cfg.spin_nap)
                 api_cfg = getattr(self.api, "config", None)
@@ -378,6 +380,7 @@ def guard_busy_poll(cfg: Config) -> None:
         log.warning("busy-poll off: %d worker(s) x %d front-door threads + loops need %d cores, %.1f available",
                     cfg.workers, cfg.frontend_threads, cfg.workers * (cfg.frontend_threads + 1), cores)
         cfg.busy_poll_us = 0
+        cfg.busy_poll_prio_us = 0
 
 
 def run(cfg: Config) -> int:

@@ -101,6 +101,9 @@ class Frontend {
   // After any event a worker keeps polling (epoll timeout 0) for this long before it
   // blocks again: trades a little CPU during bursts for no wake-up latency per request.
   void set_busy_poll_us(int us) { busy_poll_ns_.store(static_cast<int64_t>(us) * 1000, std::memory_order_relaxed); }
+  // the window after a priorities answer (kube-scheduler then picks the host, sends the bind and
+  // builds the next pod's filter: a longer gap than after a filter answer); < 0: the same window
+  void set_busy_poll_prio_us(int us) { busy_poll_prio_ns_.store(us < 0 ? -1 : static_cast<int64_t>(us) * 1000, std::memory_order_relaxed); }
   // Binds read in the same batch as a filter / priorities request are reserved first (placement
   // quality: the next pod's filter sees the pod just bound) instead of after (cycle latency).
   void set_bind_first(bool on) { bind_first_.store(on, std::memory_order_relaxed); }
@@ -180,6 +183,7 @@ class Frontend {
   std::atomic<bool> stop_{false};       // the workers leave their loops
   std::atomic<bool> serving_{true};
   std::atomic<int64_t> busy_poll_ns_{0};
+  std::atomic<int64_t> busy_poll_prio_ns_{-1};
   std::atomic<bool> bind_first_{false};
   std::atomic<bool> spin_nap_{false};
   std::vector<std::unique_ptr<Worker>> workers_;

@@ -57,6 +57,7 @@ class Doc {
   size_t size() const { return nodes_.size(); }
   // skip_container (or its scalar fallback) from offset 0 of `src`: the end offset, -1 = fails
   static long skip_for_test(std::string_view src, bool scalar);
+  static bool skip_uses_avx2();   // the AVX2 walk is the one skip_container runs
 
  private:
   std::string_view text(uint32_t off, uint32_t len) const {

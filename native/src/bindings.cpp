@@ -770,6 +770,7 @@ PYBIND11_MODULE(_native, m) {
            py::arg("nominate") = false)
       .def("set_serving", &Frontend::set_serving)
       .def("set_busy_poll_us", &Frontend::set_busy_poll_us)
+      .def("set_busy_poll_prio_us", &Frontend::set_busy_poll_prio_us)
       .def("set_bind_first", &Frontend::set_bind_first)
       .def("set_spin_nap", &Frontend::set_spin_nap)
       .def(
@@ -925,6 +926,7 @@ PYBIND11_MODULE(_native, m) {
   m.def("json_skip", [](const py::bytes& src, bool scalar) { return json::Doc::skip_for_test(std::string(src), scalar); },
         py::arg("src"), py::arg("scalar") = false,
         "The JSON container skipper from offset 0 (AVX2, or the scalar fallback): end offset, -1 = refused.");
+  m.def("json_skip_uses_avx2", &json::Doc::skip_uses_avx2, "Whether the JSON skipper runs its AVX2 walk on this host.");
   m.def("io_tally_enable", [](bool on) { g_io.on.store(on, std::memory_order_relaxed); }, py::arg("on"),
         "Switches the per-call-site system-call / phase tally (iotally.h) on or off.");
   m.def("io_tally_reset", []() { g_io.reset(); }, "Zeroes the tally.");

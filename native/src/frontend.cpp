@@ -930,7 +930,8 @@ void Frontend::run(Worker* w) {
     mb.clear();
   };
   while (!stop_.load(std::memory_order_acquire)) {
-    const int64_t spin = busy_poll_ns_.load(std::memory_order_relaxed);
+    const int64_t prio_spin = busy_poll_prio_ns_.load(std::memory_order_relaxed);
+    const int64_t spin = w->cycle_was_prio && prio_spin >= 0 ? prio_spin : busy_poll_ns_.load(std::memory_order_relaxed);
     const bool hot = __builtin_popcount(gaps & 0xffffu) >= 8;
     const uint64_t since = w->cycle_reply_ns;
     const uint64_t t_now = fast_ns();

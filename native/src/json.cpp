@@ -129,13 +129,19 @@ __attribute__((target("avx2,pclmul,popcnt,bmi"))) bool skip_avx2(const char* s, 
   return false;
 }
 
-const bool kHaveAvx2 = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("pclmul");
+// a static initializer of a shared library may run before libgcc's own CPU-model constructor
+const bool kHaveAvx2 = [] {
+  __builtin_cpu_init();
+  return __builtin_cpu_supports("avx2") && __builtin_cpu_supports("pclmul");
+}();
 }  // namespace
 
 bool Doc::skip_container() {
   if (kHaveAvx2) return skip_avx2(src_.data(), src_.size(), &p_, kMaxDepth);
   return skip_scalar();
 }
+
+bool Doc::skip_uses_avx2() { return kHaveAvx2; }
 
 long Doc::skip_for_test(std::string_view src, bool scalar) {
   Doc d;

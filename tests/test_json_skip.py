@@ -40,6 +40,11 @@ def test_avx2_skip_never_accepts_what_the_scalar_walk_refuses_or_ends_elsewhere(
         assert a == s
 
 
+def test_the_avx2_walk_is_the_one_in_use_where_the_host_has_avx2():
+    flags = open("/proc/cpuinfo").read().split()
+    assert N.json_skip_uses_avx2() == ("avx2" in flags and "pclmulqdq" in flags)
+
+
 def test_long_documents_cross_many_blocks():
     rng = random.Random(5)
     for n in (1, 63, 64, 65, 127, 128, 129, 1000, 5000):
