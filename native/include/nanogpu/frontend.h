@@ -190,6 +190,7 @@ class Frontend {
 
   mutable std::mutex opt_mu_;
   Options opt_;
+  std::atomic<uint64_t> opt_version_{1};   // bumped by every set_options (workers re-copy then)
   bool normalize_ = false;
   bool nominate_ = false;
 

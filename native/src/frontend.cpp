@@ -462,6 +462,9 @@ struct Frontend::VerbScratch {
   NameTable nid;
   std::deque<std::string> requoted;
   std::string blob, dstr, resp;
+  uint64_t opt_seen = 0;   // Frontend::opt_version_ of the copy below
+  Options opt;
+  bool normalize = false, nominate = false;
 };
 
 // ------------------------------------------------------------------------------ plumbing
@@ -647,6 +650,7 @@ void Frontend::stop() {
 
 void Frontend::set_options(const Options& o, bool score_normalize, bool nominate) {
   std::lock_guard<std::mutex> g(opt_mu_);
+  opt_version_.fetch_add(1, std::memory_order_release);
   opt_ = o;
   normalize_ = score_normalize;
   nominate_ = nominate;
@@ -1667,14 +1671,17 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     }
     idc.epoch[slot] = epoch;
   }
-  Options o;
-  bool normalize, nominate;
-  {
+  // the options as of the last policy change this worker saw (one atomic load a request; the
+  // lock and the copy only after a change)
+  if (s.opt_seen != opt_version_.load(std::memory_order_acquire)) {
     std::lock_guard<std::mutex> g(opt_mu_);
-    o = opt_;
-    normalize = normalize_;
-    nominate = nominate_;
+    s.opt = opt_;
+    s.normalize = normalize_;
+    s.nominate = nominate_;
+    s.opt_seen = opt_version_.load(std::memory_order_relaxed);
   }
+  const Options& o = s.opt;
+  const bool normalize = s.normalize, nominate = s.nominate;
   io_end(kFeVerbNames, io0);
   io0 = io_t0();
   if (nominate && !uid.empty()) ledger_->drop_nomination(uid);   // not against itself
