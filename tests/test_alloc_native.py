@@ -440,3 +440,20 @@ def test_bind_handoff_slots_put_take_and_size_limit(tmp_path):
             os.unlink(path)
         except FileNotFoundError:
             pass
+
+
+def test_pod_keys_are_views_and_keys_no_slot_holds_never_match():
+    """The ledger's key APIs take string views (a stack copy of the key, no heap string): a
+    63-character key is held and found; an empty key or one of 64 characters or more is refused
+    by reserve and, where a call does not check sizes, reads as the empty key, which no slot
+    holds. A longer key that starts with a held key's text never finds that pod."""
+    L, (nid,) = ledger_with(synthetic_mi355x(8))
+    k63 = "u" * 63
+    rc, _ = L.reserve(nid, k63, [(10, 0)], BIN)
+    assert rc == N.OK and L.lookup(k63) is not None
+    assert L.lookup(k63 + "x") is None and L.lookup(k63 + "x" * 40) is None
+    assert L.release(k63 + "x") != N.OK and L.lookup(k63) is not None
+    for bad in ("", "v" * 64, "w" * 200):
+        rc, _ = L.reserve(nid, bad, [(10, 0)], BIN)
+        assert rc != N.OK and L.lookup(bad) is None
+    assert L.release(k63) == N.OK and L.lookup(k63) is None

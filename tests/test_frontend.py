@@ -900,3 +900,33 @@ def test_compact_args_layout_and_general_layout_answer_alike():
             await rt.stop()
 
     asyncio.run(main())
+
+
+def test_filter_to_bind_pod_cache_stays_bounded_and_evicted_pods_still_bind():
+    """The filter -> bind pod cache is 4-way buckets of fixed size: filtering more pods than it
+    holds keeps it at its size, a recent pod's bind stays native, and a pod whose entry was
+    given up still binds (Python reads the pod itself)."""
+    async def main():
+        store, rt = await _runtime(4)
+        fe = rt.native.fe
+        ext = rt.extender
+        loop = asyncio.get_running_loop()
+        try:
+            first = store.create_pod(pu.make_pod("evict-first", [("c0", 10, 0)]))
+            fe.verb(_dumps({"Pod": first, "Nodes": None, "NodeNames": ["n0"]}), False)
+            for i in range(17000):   # more pods than the cache holds (16384)
+                p = pu.make_pod(f"f{i}", [("c0", 10, 0)])
+                assert fe.verb(_dumps({"Pod": p, "Nodes": None, "NodeNames": ["n1"]}), False)[0]
+            assert fe.pod_cache_size() <= 16384
+            last = store.create_pod(pu.make_pod("evict-last", [("c0", 10, 0)]))
+            fe.verb(_dumps({"Pod": last, "Nodes": None, "NodeNames": ["n2"]}), False)
+            for pod, node in ((last, "n2"), (first, "n0")):
+                m = pu.meta(pod)
+                body = _dumps({"PodName": m["name"], "PodNamespace": m["namespace"], "PodUID": m["uid"], "Node": node})
+                got = await loop.run_in_executor(None, _http, rt.bound_port, [("POST", "/scheduler/bind", body)])
+                assert got[0] == (200, b'{"Error":""}'), got
+                assert rt.state.ledger.lookup(m["uid"]) is not None
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
