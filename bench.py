@@ -103,8 +103,10 @@ def parse_args():
                     help="extender's native bind writer threads per rank, 8 binds in flight each "
                          "(0: 16 split over the ranks, at least 2)")
     ap.add_argument("--inflight-binds", type=int, default=64)
-    ap.add_argument("--bind-writer-mode", choices=["inline", "evented", "threads"], default="evented",
-                    help="the extender's native bind writer: one epoll thread, or blocking threads")
+    ap.add_argument("--bind-writer-mode", choices=["inline", "evented", "frontdoor", "threads"], default="evented",
+                    help="the extender's native bind writer: one epoll thread (evented), the front door sending "
+                         "and one epoll thread reading the answers (frontdoor), the front door alone (inline), "
+                         "or blocking threads")
     ap.add_argument("--no-assume-label", action="store_true",
                     help="the extender binds with the binding alone (no label PATCH): one API write per bind")
     ap.add_argument("--no-native-pod-watch", action="store_true",

@@ -48,7 +48,8 @@ class Config:
     verify_pod_on_bind: bool = False
     native_bind_writes: bool = True             # C++ writer threads do the bind's API writes
     bind_writer_threads: int = 16               # x KubeWriter::kBatch (8) binds in flight
-    bind_writer_mode: str = "evented"           # inline (front-door workers) | evented (one epoll thread) | threads
+    bind_writer_mode: str = "evented"           # inline (front-door workers) | evented (one epoll thread) |
+    #                                             frontdoor (front-door workers send, one epoll thread reads) | threads
     native_pod_watch: bool = True               # a C++ thread reads and filters the pod watch (podwatch.cpp)
     # the reference's `nano-gpu/assume` label, PATCHed beside the binding; off: one write a bind
     # (the binding carries the annotations; this project's agent selects pods by node)
@@ -229,6 +230,7 @@ class Runtime:
                                                         self.cfg.batch_labels):
                         log.info("worker %d: bind API writes in native writer threads (%d)", self.worker,
                                  self.cfg.bind_writer_threads)
+                        self.native.fe.set_fe_send(self.cfg.bind_writer_mode == "frontdoor")
                 self.native.start()
                 self.bound_port = self.native.port
             else:

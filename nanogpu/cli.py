@@ -61,9 +61,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--bind-writer-threads", type=int, default=16,
                    help="binds in flight / 8 for the native writer (16: 128 binds); in --bind-writer-mode "
                         "threads, the number of blocking writer threads")
-    p.add_argument("--bind-writer-mode", choices=["inline", "evented", "threads"], default="evented",
+    p.add_argument("--bind-writer-mode", choices=["inline", "evented", "frontdoor", "threads"], default="evented",
                    help="native bind writes: from each front-door worker's own epoll loop (inline), on one "
-                        "epoll thread (evented) or on blocking threads")
+                        "epoll thread (evented), sent by the front-door worker with the answers read on one "
+                        "epoll thread (frontdoor), or on blocking threads")
     p.add_argument("--bind-first", action="store_true",
                    help="front door: reserve the binds of an event batch before answering its filter / "
                         "priorities requests (the next pod's filter sees the pod just bound)")

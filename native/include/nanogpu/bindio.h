@@ -43,6 +43,11 @@ class BindIo {
   // Stop: every bind still in flight or waiting goes to the slow path with what it got
   // (`why` for answers that never came). The connections are closed.
   void abandon(const char* why);
+  // front-door sends (KubeWriter::send_from_caller): takes over the binds handed over since
+  // the last call (their connections are in this loop's epoll set already)
+  void adopt_handoffs();
+  // connection k is handed out for front-door sends instead of waiting in idle_
+  bool publish(size_t k);
   uint64_t timeouts() const { return timeouts_; }
 
  private:

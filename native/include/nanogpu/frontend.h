@@ -126,6 +126,10 @@ class Frontend {
                        bool evented = true, bool label = true, double timeout_s = 30.0, bool inline_io = false,
                        bool batch_labels = false);
   const KubeWriter* kube_writer() const { return writer_.load(std::memory_order_acquire); }
+  // evented writer: workers send each bind's requests themselves (KubeWriter::send_from_caller)
+  void set_fe_send(bool on) {
+    if (KubeWriter* w = writer_.load(std::memory_order_acquire)) w->set_fe_send(on);
+  }
   // The native filter / priorities verb on a request body (what a worker runs per request);
   // false = the request needs the Python path.
   bool filter_verb(std::string_view body, bool prioritize, std::string* out);

@@ -141,6 +141,14 @@ class KubeWriter {
   bool inline_io() const { return inline_io_; }
   // evented / inline: false pipelines each label PATCH behind its binding instead of batching
   void set_batch_labels(bool on) { batch_labels_.store(on, std::memory_order_relaxed); }
+  // Front-door sends (evented mode with its io thread, plain TCP, labels pipelined): the
+  // calling thread (a front-door worker, inside the poll window it would otherwise spin
+  // through) writes the bind's requests itself on an idle connection the io thread published,
+  // adds the connection to the io thread's epoll set and hands it over; the io thread reads
+  // the answers, commits and answers kube-scheduler as for any bind, and is not woken for the
+  // submission. false: nothing was sent (mode off, no connection idle): submit() the job.
+  bool send_from_caller(BindJob& job);
+  void set_fe_send(bool on) { fe_send_.store(on, std::memory_order_relaxed); }
   KubeWriterStats stats;
 
  private:
@@ -185,6 +193,23 @@ class KubeWriter {
   std::atomic<size_t> q_len_{0};
   std::thread io_;
   std::atomic<bool> io_done_{false};   // the io thread has handed everything to the slow path
+  // front-door sends (send_from_caller): connections the io thread published (taken out of its
+  // epoll set), the binds sent on them waiting to be adopted, all under fe_mu_
+  struct Handoff {
+    size_t k = 0;                 // BindIo connection index
+    BindJob j;
+    std::string patch, binding, out;
+    size_t sent = 0;              // bytes of `out` the caller's send took
+    bool broken = false;          // the send failed: the io thread retries on a fresh connection
+  };
+  std::atomic<bool> fe_send_{false};
+  std::mutex fe_mu_;
+  std::vector<std::pair<size_t, int>> fe_idle_;   // (connection index, fd)
+  std::vector<Handoff> adopt_;
+  bool fe_closed_ = true;        // no io thread to hand over to (not started, or stopping)
+  int fe_busy_ = 0;              // front-door threads between taking a connection and its handoff
+  int io_ep_ = -1;               // the io thread's epoll set (under fe_mu_)
+  std::string host_hdr_;
   std::deque<SlowJob> slow_q_;   // under mu_, signalled on cv_
 
   KubeTarget t_;

@@ -1279,7 +1279,7 @@ void Frontend::defer(Worker* w, Conn* c, std::string method, std::string path, s
       c->t_in_ns = c->in.empty() ? 0 : fast_ns();
       IoTimer it{kFeSubmit};
       if (bio) bio->submit(std::move(j));   // sent by pump() after this batch of events
-      else kw->submit(std::move(j));
+      else if (!kw->send_from_caller(j)) kw->submit(std::move(j));   // sent here, or by the writer
       return;
     }
   }

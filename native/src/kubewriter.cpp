@@ -440,6 +440,7 @@ KubeWriter::KubeWriter(KubeTarget target, std::shared_ptr<Ledger> ledger, Respon
     if (!tok.empty()) token_ = tok;
   }
   token_checked_ = mono_s();
+  host_hdr_ = host_header(t_);
   if (threads < 1) threads = 1;
   if (evented_) {
     max_inflight_ = threads * kBatch;

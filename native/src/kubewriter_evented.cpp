@@ -115,7 +115,36 @@ int parse_response(const std::string& b, bool eof, int* status, std::string* bod
   return 1;
 }
 
-enum ConnState { kIdle, kConnecting, kHandshake, kSending, kReceiving };
+// kPublished: handed out for front-door sends (KubeWriter::send_from_caller), out of this
+// loop's epoll set until a handoff brings it back
+enum ConnState { kIdle, kConnecting, kHandshake, kSending, kReceiving, kPublished };
+
+// One API request: method, the pod's path, headers, body (`r`'s capacity is kept).
+void compose_request(std::string* r, const char* method, const BindJob& j, bool binding, std::string_view ctype,
+                     const std::string& body, const std::string& host_hdr, const std::string& auth) {
+  r->clear();
+  *r += method;
+  *r += " /api/v1/namespaces/";
+  *r += j.ns;
+  *r += "/pods/";
+  *r += j.name;
+  if (binding) *r += "/binding";
+  *r += " HTTP/1.1\r\nHost: ";
+  *r += host_hdr;
+  *r += "\r\nUser-Agent: nano-gpu-scheduler-amd/0.1\r\nAccept: application/json\r\n";
+  if (!auth.empty()) {
+    *r += "Authorization: Bearer ";
+    *r += auth;
+    *r += "\r\n";
+  }
+  *r += "Content-Type: ";
+  *r += ctype;
+  char len[24];
+  *r += "\r\nContent-Length: ";
+  r->append(len, static_cast<size_t>(std::to_chars(len, len + sizeof len, body.size()).ptr - len));
+  *r += "\r\n\r\n";
+  *r += body;
+}
 
 // A bind's two requests go out pipelined on ONE connection, the binding first: one send and,
 // usually, one read for both answers (HTTP/1.1 answers come back in request order; kube-
@@ -139,6 +168,7 @@ struct BindIo::Conn {
   std::vector<Pending> pend;   // answers still due, in request order, from `head`
   size_t head = 0;
   uint64_t deadline_ns = 0;   // the answers are due by then (KubeWriter timeout_s)
+  bool missed = false;        // kPublished: an arrival's edge came before the handoff was adopted
   int npend() const { return static_cast<int>(pend.size() - head); }
 };
 
@@ -244,28 +274,7 @@ bool BindIo::open_conn(size_t k) {
 // a request written into the connection's own buffer (its capacity is kept across binds)
 void BindIo::request(std::string* r, const char* method, const BindJob& j, bool binding, std::string_view ctype,
                      const std::string& body) {
-  r->clear();
-  *r += method;
-  *r += " /api/v1/namespaces/";
-  *r += j.ns;
-  *r += "/pods/";
-  *r += j.name;
-  if (binding) *r += "/binding";
-  *r += " HTTP/1.1\r\nHost: ";
-  *r += host_hdr_;
-  *r += "\r\nUser-Agent: nano-gpu-scheduler-amd/0.1\r\nAccept: application/json\r\n";
-  if (!auth_.empty()) {
-    *r += "Authorization: Bearer ";
-    *r += auth_;
-    *r += "\r\n";
-  }
-  *r += "Content-Type: ";
-  *r += ctype;
-  char len[24];
-  *r += "\r\nContent-Length: ";
-  r->append(len, static_cast<size_t>(std::to_chars(len, len + sizeof len, body.size()).ptr - len));
-  *r += "\r\n\r\n";
-  *r += body;
+  compose_request(r, method, j, binding, ctype, body, host_hdr_, auth_);
 }
 
 // both answers of a slot are in: commit on the happy path, else the slow path finishes it
@@ -359,6 +368,10 @@ void BindIo::fail(size_t k, const char* why) {
 void BindIo::drive(size_t k, uint32_t events) {
   Conn& c = *conns_[k];
   char tmp[16384];
+  if (c.st == kPublished) {   // a front-door thread owns it until its handoff is adopted
+    if (events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) c.missed = true;   // read at adoption
+    return;
+  }
   for (;;) {
     if (c.fd < 0) return;
     if (c.st == kConnecting) {
@@ -410,6 +423,8 @@ void BindIo::drive(size_t k, uint32_t events) {
       continue;
     }
     if (c.st == kReceiving || c.st == kIdle) {
+      // a writable edge alone brings no bytes (every arrival is an EPOLLIN edge of its own)
+      if (events && !(events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR))) return;
       bool eof = false;
       for (;;) {
         long r;
@@ -471,10 +486,83 @@ void BindIo::drive(size_t k, uint32_t events) {
         deliver_rest(c, "connection to the API server closed before every answer");
       }
       c.st = kIdle;
-      idle_.push_back(k);
+      if (!publish(k)) idle_.push_back(k);
       return;
     }
     return;
+  }
+}
+
+bool BindIo::publish(size_t k) {
+  Conn& c = *conns_[k];
+  if (kw_->inline_io_ || tag_bit_ != 0 || c.ssl || c.fd < 0 || !kw_->fe_send_.load(std::memory_order_relaxed) ||
+      kw_->batch_labels_.load(std::memory_order_relaxed))
+    return false;
+  // out of this loop's epoll set first: the front door adds it back when it has sent on it
+  if (epoll_ctl(ep_, EPOLL_CTL_DEL, c.fd, nullptr) != 0) return false;
+  {
+    std::lock_guard<std::mutex> g(kw_->fe_mu_);
+    if (!kw_->fe_closed_) {
+      c.st = kPublished;
+      c.missed = false;
+      kw_->fe_idle_.emplace_back(k, c.fd);
+      return true;
+    }
+  }
+  epoll_event ev{};
+  ev.events = EPOLLIN | EPOLLOUT | EPOLLRDHUP | EPOLLET;
+  ev.data.u64 = tag_bit_ | k;
+  epoll_ctl(ep_, EPOLL_CTL_ADD, c.fd, &ev);
+  return false;
+}
+
+void BindIo::adopt_handoffs() {
+  std::vector<KubeWriter::Handoff> hs;
+  {
+    std::lock_guard<std::mutex> g(kw_->fe_mu_);
+    if (kw_->adopt_.empty()) return;
+    hs.swap(kw_->adopt_);
+  }
+  for (KubeWriter::Handoff& h : hs) {
+    int64_t s;
+    if (!free_slots_.empty()) {
+      s = free_slots_.back();
+      free_slots_.pop_back();
+    } else {
+      s = static_cast<int64_t>(slots_.size());   // sent already: always taken on
+      slots_.emplace_back();
+    }
+    auto jb = std::make_unique<Job>();
+    jb->j = std::move(h.j);
+    jb->patch = std::move(h.patch);
+    jb->binding = std::move(h.binding);
+    if (!kw_->label_) {
+      jb->left = 1;
+      jb->sp = 200;
+    }
+    slots_[static_cast<size_t>(s)] = std::move(jb);
+    ++inflight_;
+    Conn& c = *conns_[h.k];
+    c.out = std::move(h.out);
+    c.off = h.sent;
+    c.pend.clear();
+    c.head = 0;
+    c.pend.push_back(Pending{s, 1});
+    if (kw_->label_) c.pend.push_back(Pending{s, 0});
+    c.in.clear();
+    c.got_any = false;
+    c.retried = false;
+    c.reused = true;
+    c.deadline_ns = ns_now() + timeout_ns_;
+    c.st = c.off < c.out.size() ? kSending : kReceiving;
+    if (h.broken) {   // a stale keep-alive connection: the whole pipeline again on a fresh one
+      c.missed = false;
+      fail(h.k, "connection to the API server failed");
+      continue;
+    }
+    // the rest of a short send, or bytes whose edge came before the adoption (ignored then)
+    if (c.st == kSending || c.missed) kick_.push_back(h.k);
+    c.missed = false;
   }
 }
 
@@ -483,6 +571,24 @@ void BindIo::drive(size_t k, uint32_t events) {
 void BindIo::launch(int64_t s) {
   Job& jb = *slots_[static_cast<size_t>(s)];
   size_t k;
+  if (idle_.empty()) {   // one the front door is not using: back into this loop's epoll set
+    std::pair<size_t, int> pub{0, -1};
+    {
+      std::lock_guard<std::mutex> g(kw_->fe_mu_);
+      if (!kw_->fe_idle_.empty()) {
+        pub = kw_->fe_idle_.back();
+        kw_->fe_idle_.pop_back();
+      }
+    }
+    if (pub.second >= 0) {
+      epoll_event ev{};
+      ev.events = EPOLLIN | EPOLLOUT | EPOLLRDHUP | EPOLLET;
+      ev.data.u64 = tag_bit_ | pub.first;
+      epoll_ctl(ep_, EPOLL_CTL_ADD, pub.second, &ev);
+      conns_[pub.first]->st = kIdle;
+      idle_.push_back(pub.first);
+    }
+  }
   if (!idle_.empty()) {
     k = idle_.back();
     idle_.pop_back();
@@ -718,6 +824,11 @@ void KubeWriter::io_loop() {
     epoll_ctl(ep, EPOLL_CTL_ADD, efd_, &ev);
   }
   BindIo io(this, ep, 0, max_inflight_, respond_);
+  {
+    std::lock_guard<std::mutex> g(fe_mu_);
+    io_ep_ = ep;
+    fe_closed_ = false;
+  }
   epoll_event evs[256];
   uint64_t stop_at = 0;
   for (;;) {
@@ -734,8 +845,13 @@ void KubeWriter::io_loop() {
         q_len_.store(0, std::memory_order_relaxed);
       }
     }
-    if (stopping && !stop_at) stop_at = ns_now() + 5'000'000'000ull;
+    if (stopping && !stop_at) {
+      stop_at = ns_now() + 5'000'000'000ull;
+      std::lock_guard<std::mutex> g(fe_mu_);   // no more front-door sends from here on
+      fe_closed_ = true;
+    }
     if (stopping) {
+      io.adopt_handoffs();
       std::deque<BindJob> left;
       {
         std::lock_guard<std::mutex> g(mu_);
@@ -757,6 +873,7 @@ void KubeWriter::io_loop() {
                              queued ? 0 : stopping || io.labels_waiting() ? 1 : io.inflight() ? 100 : 1000);
     io_end(kWrWait, io0);
     io_parked_.store(false, std::memory_order_relaxed);
+    io.adopt_handoffs();   // before their connections' events: those are only read once adopted
     for (int e = 0; e < n; ++e) {
       if (evs[e].data.u64 == UINT64_MAX) {
         uint64_t v;
@@ -768,6 +885,21 @@ void KubeWriter::io_loop() {
     }
     io.pump();
   }
+  // a front-door thread between taking a connection and handing it over finishes first (its
+  // send uses the connection's fd and this loop's epoll set, both closed below)
+  for (int i = 0; i < 100000; ++i) {
+    {
+      std::lock_guard<std::mutex> g(fe_mu_);
+      fe_closed_ = true;
+      if (fe_busy_ == 0) {
+        io_ep_ = -1;
+        fe_idle_.clear();
+        break;
+      }
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(10));
+  }
+  io.adopt_handoffs();
   // what is still in flight after the grace period: the slow path answers it
   io.abandon("extender shutting down");
   io_done_.store(true);
@@ -780,6 +912,52 @@ void KubeWriter::io_loop() {
 
 std::unique_ptr<BindIo> KubeWriter::make_io(int ep, uint64_t tag_bit, Respond reply) {
   return std::make_unique<BindIo>(this, ep, tag_bit, max_inflight_, std::move(reply));
+}
+
+bool KubeWriter::send_from_caller(BindJob& j) {
+  if (!fe_send_.load(std::memory_order_relaxed) || !evented_ || inline_io_ || ctx_ ||
+      batch_labels_.load(std::memory_order_relaxed))
+    return false;
+  std::pair<size_t, int> conn;
+  int ep;
+  {
+    std::lock_guard<std::mutex> g(fe_mu_);
+    if (fe_closed_ || fe_idle_.empty() || io_ep_ < 0) return false;
+    conn = fe_idle_.back();
+    fe_idle_.pop_back();
+    ep = io_ep_;
+    ++fe_busy_;   // the io thread closes neither this fd nor its epoll set until the handoff
+  }
+  Handoff h;
+  h.k = conn.first;
+  build(j, &h.patch, &h.binding);
+  const std::string a = auth();
+  compose_request(&h.out, "POST", j, true, kJsonE, h.binding, host_hdr_, a);
+  if (label_) {
+    thread_local std::string second;
+    compose_request(&second, "PATCH", j, false, kMergePatchE, h.patch, host_hdr_, a);
+    h.out += second;
+  }
+  ssize_t n;
+  do {
+    IoTimer it{kWrSend};
+    n = ::send(conn.second, h.out.data(), h.out.size(), MSG_NOSIGNAL | MSG_DONTWAIT);
+  } while (n < 0 && errno == EINTR);
+  h.sent = n > 0 ? static_cast<size_t>(n) : 0;
+  h.broken = n < 0 && errno != EAGAIN && errno != EWOULDBLOCK;
+  h.j = std::move(j);
+  stats.inflight.fetch_add(1, std::memory_order_relaxed);
+  // into the io thread's epoll set before the handoff is visible: the answer's edge may come
+  // first (the io thread then ignores it and reads the connection when it adopts the handoff)
+  epoll_event ev{};
+  // EPOLLOUT only for the rest of a short send: otherwise the writable edge is a wasted wake-up
+  ev.events = EPOLLIN | EPOLLRDHUP | EPOLLET | (h.sent < h.out.size() ? EPOLLOUT : 0u);
+  ev.data.u64 = conn.first;   // the io thread's BindIo tags its connections with no tag bit
+  epoll_ctl(ep, EPOLL_CTL_ADD, conn.second, &ev);
+  std::lock_guard<std::mutex> g(fe_mu_);
+  adopt_.push_back(std::move(h));
+  --fe_busy_;
+  return true;
 }
 
 void KubeWriter::to_slow(SlowJob&& sj) {

@@ -47,7 +47,7 @@ async def _metrics(base):
             return await r.text()
 
 
-@pytest.mark.parametrize("native", ["inline", "evented", "threads", False])
+@pytest.mark.parametrize("native", ["inline", "evented", "frontdoor", "threads", False])
 def test_bind_writes_retry_transient_errors(native):
     async def main():
         store = FakeKubeStore(faults=Faults(patch_error_rate=0.3, bind_error_rate=0.3, seed=11))
@@ -75,7 +75,7 @@ def test_bind_writes_retry_transient_errors(native):
     asyncio.run(main())
 
 
-@pytest.mark.parametrize("native", ["inline", "evented", "threads", False])
+@pytest.mark.parametrize("native", ["inline", "evented", "frontdoor", "threads", False])
 def test_failed_binding_rolls_back_and_writes_nothing(native):
     async def main():
         store = FakeKubeStore(faults=Faults(bind_error_rate=1.0))
@@ -107,7 +107,7 @@ def test_failed_binding_rolls_back_and_writes_nothing(native):
     asyncio.run(main())
 
 
-@pytest.mark.parametrize("native", ["inline", "evented", "threads", False])
+@pytest.mark.parametrize("native", ["inline", "evented", "frontdoor", "threads", False])
 def test_binding_conflict_on_the_same_node_is_success(native):
     """A retried binding POST whose first attempt landed answers 409; the pod already sits on
     the requested node, so the bind succeeded."""
@@ -138,7 +138,7 @@ def test_binding_conflict_on_the_same_node_is_success(native):
     asyncio.run(main())
 
 
-@pytest.mark.parametrize("mode", ["inline", "evented", "threads"])
+@pytest.mark.parametrize("mode", ["inline", "evented", "frontdoor", "threads"])
 def test_native_writer_speaks_tls_with_a_bearer_token(tmp_path, mode):
     """https + token (how an in-cluster extender reaches kube-apiserver): a TLS proxy with a
     self-signed certificate in front of the fake API server checks the Authorization header.
@@ -217,7 +217,7 @@ def test_native_writer_speaks_tls_with_a_bearer_token(tmp_path, mode):
     asyncio.run(main())
 
 
-@pytest.mark.parametrize("mode", ["inline", "evented", "threads"])
+@pytest.mark.parametrize("mode", ["inline", "evented", "frontdoor", "threads"])
 def test_stop_with_binds_in_flight_answers_every_bind_and_leaves_the_ledger_clean(mode):
     """A bind is in flight to a slow API server (0.3 s per answer) when the extender stops:
     the writer finishes what it holds within its grace period, kube-scheduler gets an answer
@@ -334,7 +334,7 @@ def test_bind_on_another_worker_process_stays_native_through_the_ledger_handoff(
     asyncio.run(main())
 
 
-@pytest.mark.parametrize("native", ["inline", "evented", "threads", False])
+@pytest.mark.parametrize("native", ["inline", "evented", "frontdoor", "threads", False])
 def test_no_assume_label_binds_with_one_api_write(native):
     """`--no-assume-label`: the binding alone (it carries the placement annotations, which
     kube-apiserver sets with spec.nodeName) — one API write per bind instead of two, no label."""
@@ -370,7 +370,7 @@ def test_no_assume_label_binds_with_one_api_write(native):
 
 @pytest.mark.parametrize("faults", [dict(patch_error_rate=1.0), dict(close_after_binding=True),
                                     dict(patch_error_rate=0.5, seed=3)])
-@pytest.mark.parametrize("mode", ["inline", "evented"])
+@pytest.mark.parametrize("mode", ["inline", "evented", "frontdoor"])
 @pytest.mark.parametrize("batch", [False, True])
 def test_pipelined_label_after_the_binding(faults, mode, batch):
     """The evented writer pipelines the label PATCH behind the binding on one connection (or,
@@ -446,7 +446,7 @@ def _bound_elsewhere_pod(name):
 
 
 @pytest.mark.parametrize("server", ["python", "native"])
-@pytest.mark.parametrize("native", ["inline", "evented", "threads", False])
+@pytest.mark.parametrize("native", ["inline", "evented", "frontdoor", "threads", False])
 def test_binding_refused_for_a_pod_bound_elsewhere_leaves_its_placement_alone(native, server):
     """The pod is already bound to another node (with that placement's annotations) when this
     extender binds it to n0: the binding is refused (409, the GET shows the other node), the
@@ -497,7 +497,7 @@ def test_binding_refused_for_a_pod_bound_elsewhere_leaves_its_placement_alone(na
 
 
 @pytest.mark.parametrize("server", ["python", "native"])
-@pytest.mark.parametrize("native", ["inline", "evented", "threads", False])
+@pytest.mark.parametrize("native", ["inline", "evented", "frontdoor", "threads", False])
 def test_binding_refused_for_a_deleted_pod_sends_no_cleanup_patch(native, server):
     """The pod is deleted between filter and bind: the binding answers 404, the reservation is
     rolled back, and no PATCH follows (the evented writer's guarded label PATCH, pipelined
@@ -537,7 +537,7 @@ def test_binding_refused_for_a_deleted_pod_sends_no_cleanup_patch(native, server
             assert status == 500 and "404" in res["Error"], res
             assert rt.state.ledger.lookup(pu.pod_uid(p)) is None
             await asyncio.sleep(0.2)
-            assert patches() - p0 <= (1 if native in ("evented", "inline") else 0)
+            assert patches() - p0 <= (1 if native in ("evented", "inline", "frontdoor") else 0)
         finally:
             await rt.stop()
             if runner is not None:
@@ -548,7 +548,7 @@ def test_binding_refused_for_a_deleted_pod_sends_no_cleanup_patch(native, server
     asyncio.run(main())
 
 
-@pytest.mark.parametrize("mode", ["inline", "evented", "threads"])
+@pytest.mark.parametrize("mode", ["inline", "evented", "frontdoor", "threads"])
 def test_an_api_server_that_never_answers_times_the_bind_out(mode):
     """A half-open API server (accepts, reads, never answers nor resets): every bind still gets
     an answer (an error) within a few writer timeouts, the reservation is rolled back, and the
@@ -612,7 +612,7 @@ def test_an_api_server_that_never_answers_times_the_bind_out(mode):
         lsock.close()
 
 
-@pytest.mark.parametrize("mode", ["evented", "inline"])
+@pytest.mark.parametrize("mode", ["evented", "inline", "frontdoor"])
 def test_many_concurrent_binds_with_label_patches_all_complete(mode):
     """Driven by the native kube-scheduler stand-in (binds back to back, many in flight) against
     the native API server, every bind is answered once, every pod is bound with its label
