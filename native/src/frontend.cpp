@@ -1237,11 +1237,12 @@ void Frontend::process(Worker* w, Conn* c) {
       path = target.substr(0, qm);
       query = target.substr(qm + 1);
     }
+    const bool prio = path == "/scheduler/priorities";   // `path` views c->in, erased below
     if (handle_native(w, c, method, path, body, &c->out)) {   // the answer lands in c->out
       c->in.erase(0, consumed);
       flush(w, c, kFeSendCycle);
       w->cycle_reply_ns = fast_ns();   // the scheduling cycle's next request is due: spin for it
-      w->cycle_was_prio = path == "/scheduler/priorities";
+      w->cycle_was_prio = prio;
       if (!w->conns.count(id)) return;
     } else {
       std::string m(method), pth(path), q(query), b(body);   // owned: the Python side keeps them

@@ -500,7 +500,7 @@ static std::string post(int port, const std::string& path, const std::string& bo
 // over HTTP to a 2-worker front door whose workers drive the binds' API requests to the native
 // API server from their own epoll loops; every bind must be answered, bound and committed, and
 // the front door must stop cleanly with the writer.
-static void inline_binds(int pods) {
+static void inline_binds(int pods, bool frontdoor = false) {
   apisrv::Config cfg;
   cfg.threads = 2;
   apisrv::Server srv(cfg);
@@ -536,7 +536,9 @@ static void inline_binds(int pods) {
     tgt.host = "127.0.0.1";
     tgt.port = port;
     tgt.tls = false;
-    fe.set_kube_writer(tgt, 2, 2, false, true, true, 30.0, true);
+    // frontdoor: the evented writer's io thread reads the answers, the workers send the binds
+    fe.set_kube_writer(tgt, 2, 2, false, true, true, 30.0, !frontdoor);
+    if (frontdoor) fe.set_fe_send(true);
     std::vector<std::thread> clients;
     std::atomic<int> ok{0};
     for (int c = 0; c < 4; ++c)
@@ -565,7 +567,7 @@ static void inline_binds(int pods) {
     CHECK(ledger->lookup("iq" + std::to_string(i), &rec) && rec.state == kPodCommitted);
   }
   srv.stop();
-  std::printf("inline ok: %d binds written from the front-door workers\n", pods);
+  std::printf("%s ok: %d binds written from the front-door workers\n", frontdoor ? "frontdoor" : "inline", pods);
 }
 
 static std::string post(int port, const std::string& path, const std::string& body) {
@@ -726,6 +728,7 @@ int main(int argc, char** argv) {
   apiserver_and_writers(std::max(50, iters / 20), true);    // one epoll writer thread
   apiserver_and_writers(std::max(50, iters / 20), false);   // blocking writer threads
   inline_binds(std::max(100, iters / 10));
+  inline_binds(std::max(100, iters / 10), true);   // sent by the workers, answers on the io thread
   relist_gap(std::max(200, iters / 4));
   handoff(std::max(500, iters));
   mailbox_wakeups(std::max(400, iters / 2));

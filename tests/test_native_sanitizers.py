@@ -24,5 +24,5 @@ def test_native_stress(kind, threads, iters, cpu_exclusive):
     r = subprocess.run([str(exe), str(threads), str(iters)], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
     assert "stress ok" in r.stdout and "relist ok" in r.stdout and "handoff ok" in r.stdout
-    assert "mailbox ok" in r.stdout and "inline ok" in r.stdout
+    assert "mailbox ok" in r.stdout and "inline ok" in r.stdout and "frontdoor ok" in r.stdout
     assert "ERROR: AddressSanitizer" not in r.stderr and "WARNING: ThreadSanitizer" not in r.stderr
