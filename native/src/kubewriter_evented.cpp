@@ -498,22 +498,14 @@ bool BindIo::publish(size_t k) {
   if (kw_->inline_io_ || tag_bit_ != 0 || c.ssl || c.fd < 0 || !kw_->fe_send_.load(std::memory_order_relaxed) ||
       kw_->batch_labels_.load(std::memory_order_relaxed))
     return false;
-  // out of this loop's epoll set first: the front door adds it back when it has sent on it
-  if (epoll_ctl(ep_, EPOLL_CTL_DEL, c.fd, nullptr) != 0) return false;
-  {
-    std::lock_guard<std::mutex> g(kw_->fe_mu_);
-    if (!kw_->fe_closed_) {
-      c.st = kPublished;
-      c.missed = false;
-      kw_->fe_idle_.emplace_back(k, c.fd);
-      return true;
-    }
-  }
-  epoll_event ev{};
-  ev.events = EPOLLIN | EPOLLOUT | EPOLLRDHUP | EPOLLET;
-  ev.data.u64 = tag_bit_ | k;
-  epoll_ctl(ep_, EPOLL_CTL_ADD, c.fd, &ev);
-  return false;
+  // it stays in this loop's epoll set: an edge that comes while a front-door thread holds it is
+  // only noted (drive), and read once the handoff is adopted
+  std::lock_guard<std::mutex> g(kw_->fe_mu_);
+  if (kw_->fe_closed_) return false;
+  c.st = kPublished;
+  c.missed = false;
+  kw_->fe_idle_.emplace_back(k, c.fd);
+  return true;
 }
 
 void BindIo::adopt_handoffs() {
@@ -581,12 +573,13 @@ void BindIo::launch(int64_t s) {
       }
     }
     if (pub.second >= 0) {
-      epoll_event ev{};
-      ev.events = EPOLLIN | EPOLLOUT | EPOLLRDHUP | EPOLLET;
-      ev.data.u64 = tag_bit_ | pub.first;
-      epoll_ctl(ep_, EPOLL_CTL_ADD, pub.second, &ev);
-      conns_[pub.first]->st = kIdle;
-      idle_.push_back(pub.first);
+      Conn& pc = *conns_[pub.first];
+      pc.st = kIdle;
+      if (pc.missed) {   // the server closed it (or sent junk) while it was out: see to it now
+        pc.missed = false;
+        drive(pub.first, EPOLLIN);
+      }
+      if (pc.fd >= 0 && pc.st == kIdle) idle_.push_back(pub.first);
     }
   }
   if (!idle_.empty()) {
@@ -919,14 +912,12 @@ bool KubeWriter::send_from_caller(BindJob& j) {
       batch_labels_.load(std::memory_order_relaxed))
     return false;
   std::pair<size_t, int> conn;
-  int ep;
   {
     std::lock_guard<std::mutex> g(fe_mu_);
     if (fe_closed_ || fe_idle_.empty() || io_ep_ < 0) return false;
     conn = fe_idle_.back();
     fe_idle_.pop_back();
-    ep = io_ep_;
-    ++fe_busy_;   // the io thread closes neither this fd nor its epoll set until the handoff
+    ++fe_busy_;   // the io thread does not close this fd until the handoff
   }
   Handoff h;
   h.k = conn.first;
@@ -947,13 +938,8 @@ bool KubeWriter::send_from_caller(BindJob& j) {
   h.broken = n < 0 && errno != EAGAIN && errno != EWOULDBLOCK;
   h.j = std::move(j);
   stats.inflight.fetch_add(1, std::memory_order_relaxed);
-  // into the io thread's epoll set before the handoff is visible: the answer's edge may come
-  // first (the io thread then ignores it and reads the connection when it adopts the handoff)
-  epoll_event ev{};
-  // EPOLLOUT only for the rest of a short send: otherwise the writable edge is a wasted wake-up
-  ev.events = EPOLLIN | EPOLLRDHUP | EPOLLET | (h.sent < h.out.size() ? EPOLLOUT : 0u);
-  ev.data.u64 = conn.first;   // the io thread's BindIo tags its connections with no tag bit
-  epoll_ctl(ep, EPOLL_CTL_ADD, conn.second, &ev);
+  // the connection never left the io thread's epoll set: the answer's edge may come before the
+  // handoff is adopted (the io thread then notes it and reads the connection at the adoption)
   std::lock_guard<std::mutex> g(fe_mu_);
   adopt_.push_back(std::move(h));
   --fe_busy_;
