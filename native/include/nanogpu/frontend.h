@@ -219,6 +219,7 @@ class Frontend {
   uint64_t pod_stamp_ = 0;
   size_t pod_live_ = 0;
   PodEntry* find_pod_locked(std::string_view uid, uint64_t h);
+  const PodEntry* find_pod_locked(std::string_view uid, uint64_t h) const;
 };
 
 }  // namespace nanogpu

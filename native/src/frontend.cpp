@@ -727,17 +727,21 @@ uint64_t uid_hash(std::string_view uid) {   // FNV-1a, never 0 (0 marks an empty
 }
 }  // namespace
 
-Frontend::PodEntry* Frontend::find_pod_locked(std::string_view uid, uint64_t h) {
+const Frontend::PodEntry* Frontend::find_pod_locked(std::string_view uid, uint64_t h) const {
   const size_t nb = pod_slots_.size() / kPodWays;
-  PodEntry* b = &pod_slots_[((h >> 7) % nb) * kPodWays];
+  const PodEntry* b = &pod_slots_[((h >> 7) % nb) * kPodWays];
   for (size_t w = 0; w < kPodWays; ++w)
     if (b[w].h == h && b[w].uid == uid) return &b[w];
   return nullptr;
 }
 
+Frontend::PodEntry* Frontend::find_pod_locked(std::string_view uid, uint64_t h) {
+  return const_cast<PodEntry*>(static_cast<const Frontend*>(this)->find_pod_locked(uid, h));
+}
+
 bool Frontend::has_pod(std::string_view uid) const {
   std::lock_guard<std::mutex> g(pod_mu_);
-  return const_cast<Frontend*>(this)->find_pod_locked(uid, uid_hash(uid)) != nullptr;
+  return find_pod_locked(uid, uid_hash(uid)) != nullptr;
 }
 
 size_t Frontend::pod_cache_size() const {
