@@ -1153,8 +1153,10 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         _native.io_tally_reset()
         _native.io_tally_enable(True)
     nom0 = rt.state.ledger.nomination_counts()
+    ctrl0 = pod_ctrl.queue.processed if pod_ctrl is not None else 0
     fe_stats = rt.native.fe.stats if rt.native is not None else (lambda: {})
     handoffs0 = fe_stats().get("bind_handoffs", 0)
+    py0 = fe_stats().get("python", {}).get("count", 0)
     hc.s = 0.0
     cpu0, loop_cpu0 = time.process_time(), time.thread_time()
     threads0, ticks0, times0 = thread_cpu(), thread_ticks(), os.times()
@@ -1223,6 +1225,9 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     # shared ledger's bind handoff): the one-scheduler passes' binds on ranks other than 0
     results["bind_handoffs"] = sum(d.gather_obj(fe_stats().get("bind_handoffs", 0) - handoffs0))
     results["nomination_margin"] = rt.state.ledger.nomination_margin
+    # pods the Python pod controller processed (the native watch keeps the rest from it)
+    results["controller_keys"] = (pod_ctrl.queue.processed - ctrl0) if pod_ctrl is not None else None
+    results["python_requests"] = fe_stats().get("python", {}).get("count", 0) - py0   # routed to Python
     results["unschedulable_attempts"] = sum(st.get("unschedulable_attempts", 0) for st in results["steps"])
     cycles = sum(st.get("cycles", 0) for st in results["steps"])
     results["nodes_sent_per_filter"] = (round(sum(st.get("nodes_sent_filter", 0) for st in results["steps"]) / cycles, 1)
@@ -1284,7 +1289,7 @@ HEADLINE_LAST = ("value_independent_schedulers", "frag_pct_steady_reference_mode
                  "extender_cpu_us_per_pod_rank0", "frag_pct_reference_model", "frag_hbm_pct", "frag_pct",
                  "p99_bind_ms", "p50_bind_ms", "pods_per_s_first_filter_to_last_bind", "value")
 # bulky per-step / per-thread records: --json-out only
-DIAG_KEYS = ("step_diag_rank0", "io_per_pod_rank0", "schedule_ms_each_step_rank0", "phase_ms_per_step_rank0",
+DIAG_KEYS = ("step_diag_rank0", "io_per_pod_rank0", "controller_keys_per_pod_rank0", "python_requests_per_pod_rank0", "schedule_ms_each_step_rank0", "phase_ms_per_step_rank0",
              "extender_cpu_us_per_pod_by_thread_rank0", "extender_kernel_pct_by_thread_rank0",
              "extender_cpu_us_per_pod_user_kernel_rank0", "frag_pct_steady_each_step", "nominations",
              "nominations_steady", "native_verb_mean_us", "frag_reference_model_source", "host_selection",
@@ -1369,6 +1374,9 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
         "host_selection": "extender arg-max" if args.no_kube_combine else
                           "kube-scheduler combining (LeastAllocated + BalancedAllocation + 10 x extender)",
         "nominations": res["nominations"],
+        "controller_keys_per_pod_rank0": (round(res["controller_keys"] / max(1, res["scheduled"]), 3)
+                                          if res.get("controller_keys") is not None else None),
+        "python_requests_per_pod_rank0": round(res.get("python_requests", 0) / max(1, res["scheduled"]), 3),
         "nomination_adopt_pct": (round(100.0 * res["nominations"]["adopted"] / res["nominations"]["made"], 2)
                                  if res["nominations"]["made"] else None),
         "p50_queue_to_bound_ms_rank0": (round(statistics.mean(st.get("e2e_p50_ms", 0.0) for st in res["steps"]), 3)
