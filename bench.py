@@ -135,6 +135,8 @@ def parse_args():
     ap.add_argument("--frontend-threads", type=int, default=1, help="native front door epoll workers")
     ap.add_argument("--busy-poll-us", type=int, default=int(os.environ.get("NANOGPU_BUSY_POLL_US", "20")),
                     help="native front door busy-poll window")
+    ap.add_argument("--lazy-label-answers", action="store_true",
+                    help="native writer: label PATCH answers read lazily (nanogpu --lazy-label-answers)")
     ap.add_argument("--busy-poll-prio-us", type=int, default=int(os.environ.get("NANOGPU_BUSY_POLL_PRIO_US", "-1")),
                     help="the busy-poll window after a priorities answer (-1: --busy-poll-us, 0: sleep)")
     ap.add_argument("--driver", default="native", choices=["native", "python"],
@@ -883,7 +885,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     cfg = Config(port=0, host="127.0.0.1", priority=args.policy, compat=args.compat, ledger_path=ledger_path,
                  max_nodes=max(1024, args.nodes), max_pods=max(65536, 4 * args.pods),
                  policy_config_path="/nonexistent/policy.yaml", reservation_ttl_s=3600,
-                 busy_poll_us=args.busy_poll_us, busy_poll_prio_us=args.busy_poll_prio_us,
+                 busy_poll_us=args.busy_poll_us, busy_poll_prio_us=args.busy_poll_prio_us, lazy_label_answers=args.lazy_label_answers,
                  frontend_threads=args.frontend_threads,
                  nominate=not args.no_nominate,
                  bind_writer_threads=args.bind_writer_threads or max(2, 16 // d.world),

@@ -57,6 +57,7 @@ class Config:
     bind_first: bool = False                    # front door: a batch's binds before its filters
     spin_nap: bool = False                      # front door: sleep the busy-poll window, not poll it
     batch_labels: bool = False                  # native writer: batch label PATCHes after bindings (off: pipelined)
+    lazy_label_answers: bool = False            # native writer: read label PATCH answers lazily (no wake-up each)
     watch_assigned_only: bool = True            # pod informer: bound pods only (spec.nodeName!=)
     api_write_timeout_s: float = 30.0           # native bind writer: an API answer due within this
     reservation_ttl_s: float = 60.0
@@ -231,6 +232,7 @@ class Runtime:
                         log.info("worker %d: bind API writes in native writer threads (%d)", self.worker,
                                  self.cfg.bind_writer_threads)
                         self.native.fe.set_fe_send(self.cfg.bind_writer_mode == "frontdoor")
+                        self.native.fe.set_lazy_labels(self.cfg.lazy_label_answers)
                 self.native.start()
                 self.bound_port = self.native.port
             else:

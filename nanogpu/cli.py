@@ -97,6 +97,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--frontend-threads", type=int, default=4)
     p.add_argument("--busy-poll-us", type=int, default=0,
                    help="native workers keep polling this long after an event (lower latency, more CPU)")
+    p.add_argument("--lazy-label-answers", action="store_true",
+                   help="native writer: a label PATCH's answer is read by a later pass of the writer's loop "
+                        "instead of waking it (the connection's SO_RCVLOWAT raised once its binding answered)")
     p.add_argument("--busy-poll-prio-us", type=int, default=-1,
                    help="the polling window after a priorities answer (kube-scheduler then picks the host, "
                         "sends the bind and builds the next pod's filter); -1: --busy-poll-us, 0: sleep")
@@ -141,6 +144,6 @@ def parse(argv: list[str] | None = None) -> Config:
         nominate=not a.no_nominate, nomination_ttl_s=parse_duration(a.nomination_ttl),
         fake_cluster=a.fake_cluster, fake_gpus_per_node=a.fake_gpus_per_node, fake_partition=a.fake_partition,
         seed=a.seed, frontend=a.frontend, frontend_threads=max(1, a.frontend_threads), busy_poll_us=a.busy_poll_us,
-        busy_poll_prio_us=a.busy_poll_prio_us,
+        busy_poll_prio_us=a.busy_poll_prio_us, lazy_label_answers=a.lazy_label_answers,
         leader_elect=a.leader_elect, lease_name=a.lease_name, lease_namespace=a.lease_namespace, identity=a.identity,
         cpu_affinity=a.cpu_affinity, request_sizes=_sizes(a.request_sizes), learn_sizes=not a.no_learn_sizes)

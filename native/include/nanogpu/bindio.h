@@ -39,13 +39,16 @@ class BindIo {
   size_t inflight() const { return inflight_ + labels_out_ + label_wait_.size(); }
   size_t waiting() const { return waiting_.size(); }
   // label PATCHes held for a batch: the owner's loop must come back within about a millisecond
-  bool labels_waiting() const { return !label_wait_.empty(); }
+  bool labels_waiting() const { return !label_wait_.empty() || !lazy_.empty(); }
   // Stop: every bind still in flight or waiting goes to the slow path with what it got
   // (`why` for answers that never came). The connections are closed.
   void abandon(const char* why);
   // front-door sends (KubeWriter::send_from_caller): takes over the binds handed over since
   // the last call (their connections are in this loop's epoll set already)
   void adopt_handoffs();
+  // lazy label answers (KubeWriter::set_lazy_labels)
+  void go_lazy(size_t k);
+  void drain_lazy(uint64_t now);
   // connection k is handed out for front-door sends instead of waiting in idle_
   bool publish(size_t k);
   uint64_t timeouts() const { return timeouts_; }
@@ -102,6 +105,11 @@ class BindIo {
   std::deque<int64_t> label_wait_;
   uint64_t label_oldest_ns_ = 0;
   size_t labels_out_ = 0;   // sent, answer due
+  // lazy label answers: connections whose only due answers are label answers of answered binds
+  // (their low-water mark raised), read kLazyNs or more after they went lazy
+  static constexpr uint64_t kLazyNs = 20'000;
+  std::vector<size_t> lazy_;
+  void reset_lowat(Conn& c);
 };
 
 }  // namespace nanogpu

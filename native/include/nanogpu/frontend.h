@@ -130,6 +130,9 @@ class Frontend {
   void set_fe_send(bool on) {
     if (KubeWriter* w = writer_.load(std::memory_order_acquire)) w->set_fe_send(on);
   }
+  void set_lazy_labels(bool on) {
+    if (KubeWriter* w = writer_.load(std::memory_order_acquire)) w->set_lazy_labels(on);
+  }
   // The native filter / priorities verb on a request body (what a worker runs per request);
   // false = the request needs the Python path.
   bool filter_verb(std::string_view body, bool prioritize, std::string* out);

@@ -149,6 +149,9 @@ class KubeWriter {
   // submission. false: nothing was sent (mode off, no connection idle): submit() the job.
   bool send_from_caller(BindJob& job);
   void set_fe_send(bool on) { fe_send_.store(on, std::memory_order_relaxed); }
+  // evented / inline: a label PATCH's answer is read by a later pass of the loop instead of
+  // waking it (the connection's SO_RCVLOWAT raised once its binding answered)
+  void set_lazy_labels(bool on) { lazy_labels_.store(on, std::memory_order_relaxed); }
   KubeWriterStats stats;
 
  private:
@@ -203,6 +206,7 @@ class KubeWriter {
     bool broken = false;          // the send failed: the io thread retries on a fresh connection
   };
   std::atomic<bool> fe_send_{false};
+  std::atomic<bool> lazy_labels_{false};
   std::mutex fe_mu_;
   std::vector<std::pair<size_t, int>> fe_idle_;   // (connection index, fd)
   std::vector<Handoff> adopt_;

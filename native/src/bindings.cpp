@@ -771,6 +771,8 @@ PYBIND11_MODULE(_native, m) {
       .def("set_serving", &Frontend::set_serving)
       .def("set_busy_poll_us", &Frontend::set_busy_poll_us)
       .def("set_busy_poll_prio_us", &Frontend::set_busy_poll_prio_us)
+      .def("set_lazy_labels", &Frontend::set_lazy_labels, py::arg("on"),
+           "Evented / inline writer: label PATCH answers read by a later pass of the loop, not woken for.")
       .def("set_fe_send", &Frontend::set_fe_send, py::arg("on"),
            "Evented writer: front-door workers send each bind's requests themselves; the writer "
            "thread reads the answers (KubeWriter::send_from_caller).")

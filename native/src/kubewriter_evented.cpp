@@ -169,6 +169,8 @@ struct BindIo::Conn {
   size_t head = 0;
   uint64_t deadline_ns = 0;   // the answers are due by then (KubeWriter timeout_s)
   bool missed = false;        // kPublished: an arrival's edge came before the handoff was adopted
+  bool lowat = false;         // SO_RCVLOWAT raised (lazy label answers): arrivals do not wake the loop
+  uint64_t lazy_since = 0;    // in lazy_ since (0: not lazy)
   int npend() const { return static_cast<int>(pend.size() - head); }
 };
 
@@ -222,6 +224,8 @@ bool BindIo::resolve() {
 void BindIo::close_conn(Conn& c) {
   if (c.ssl) SSL_free(c.ssl);
   c.ssl = nullptr;
+  c.lowat = false;
+  c.lazy_since = 0;   // drain_lazy drops its entry
   if (c.fd >= 0) {
     epoll_ctl(ep_, EPOLL_CTL_DEL, c.fd, nullptr);
     ::close(c.fd);
@@ -469,7 +473,7 @@ void BindIo::drive(size_t k, uint32_t events) {
         const int rc = parse_response(c.in, eof && c.npend() == 1, &status, &body, &used, &close);
         if (rc < 0) return fail(k, "bad answer from the API server");
         if (rc == 0) {
-          if (!eof) return;   // more bytes to come
+          if (!eof) return go_lazy(k);   // more bytes to come
           if (c.got_any && c.in.empty() && (delivered || c.head > 0)) break;   // answered some, then closed
           return fail(k, "connection to the API server failed");
         }
@@ -486,11 +490,66 @@ void BindIo::drive(size_t k, uint32_t events) {
         deliver_rest(c, "connection to the API server closed before every answer");
       }
       c.st = kIdle;
+      c.lazy_since = 0;   // every answer is in: its lazy_ entry (if any) is stale
       if (!publish(k)) idle_.push_back(k);
       return;
     }
     return;
   }
+}
+
+// More bytes are due on connection k. When they are only label answers of binds already
+// answered (--lazy-label-answers), the connection's receive low-water mark goes up, so their
+// arrival wakes nobody, and a later pass of the loop reads them (drain_lazy).
+void BindIo::go_lazy(size_t k) {
+  Conn& c = *conns_[k];
+  if (!kw_->lazy_labels_.load(std::memory_order_relaxed) || c.ssl || c.fd < 0 || c.npend() <= 0) return;
+  for (size_t i = c.head; i < c.pend.size(); ++i) {
+    const Pending& p = c.pend[i];
+    if (p.which != 0 || !slots_[static_cast<size_t>(p.job)] || !slots_[static_cast<size_t>(p.job)]->answered) return;
+  }
+  if (!c.lowat) {
+    const int big = 1 << 30;
+    if (setsockopt(c.fd, SOL_SOCKET, SO_RCVLOWAT, &big, sizeof big) != 0) return;
+    c.lowat = true;
+  }
+  if (!c.lazy_since) {
+    c.lazy_since = ns_now();
+    lazy_.push_back(k);
+  }
+}
+
+// lazy connections whose label answers are due by now are read (one recv each; an answer still
+// on its way leaves the connection lazy for the next pass)
+void BindIo::drain_lazy(uint64_t now) {
+  size_t keep = 0;
+  for (size_t i = 0; i < lazy_.size(); ++i) {
+    const size_t k = lazy_[i];
+    Conn& c = *conns_[k];
+    if (!c.lazy_since || c.fd < 0 || c.st != kReceiving) {
+      c.lazy_since = 0;
+      continue;   // answered, closed or failed meanwhile
+    }
+    if (now - c.lazy_since < kLazyNs) {
+      lazy_[keep++] = k;
+      continue;
+    }
+    c.lazy_since = 0;
+    drive(k, EPOLLIN);   // delivers what came; go_lazy() re-queues it if nothing did
+    if (c.lazy_since) {   // re-queued at the end of lazy_ (past i): one entry only
+      lazy_.pop_back();
+      c.lazy_since = now;
+      lazy_[keep++] = k;
+    }
+  }
+  lazy_.resize(keep);
+}
+
+void BindIo::reset_lowat(Conn& c) {
+  if (c.fd < 0 || !c.lowat) return;
+  const int one = 1;
+  setsockopt(c.fd, SOL_SOCKET, SO_RCVLOWAT, &one, sizeof one);
+  c.lowat = false;
 }
 
 bool BindIo::publish(size_t k) {
@@ -500,6 +559,7 @@ bool BindIo::publish(size_t k) {
     return false;
   // it stays in this loop's epoll set: an edge that comes while a front-door thread holds it is
   // only noted (drive), and read once the handoff is adopted
+  reset_lowat(c);   // after lazy label answers: the next binding's answer must wake the loop
   std::lock_guard<std::mutex> g(kw_->fe_mu_);
   if (kw_->fe_closed_) return false;
   c.st = kPublished;
@@ -606,6 +666,7 @@ void BindIo::launch(int64_t s) {
   c.retried = false;
   c.deadline_ns = ns_now() + timeout_ns_;
   c.reused = c.fd >= 0;
+  reset_lowat(c);   // idle again after lazy answers: answers wake the loop again
   if (c.fd >= 0) {
     c.st = kSending;
   } else if (!open_conn(k)) {
@@ -738,6 +799,7 @@ void BindIo::launch_labels() {
   c.retried = false;
   c.deadline_ns = ns_now() + timeout_ns_;
   c.reused = c.fd >= 0;
+  reset_lowat(c);   // idle again after lazy answers: answers wake the loop again
   if (c.fd >= 0) {
     c.st = kSending;
   } else if (!open_conn(k)) {
@@ -750,6 +812,8 @@ void BindIo::launch_labels() {
 }
 
 void BindIo::pump() {
+  // lazy label answers due by now first: their connections are free for the binds below
+  if (!lazy_.empty()) drain_lazy(ns_now());
   for (int round = 0; round < 4 && (!kick_.empty() || !waiting_.empty()); ++round) {
     start_waiting();
     for (size_t i = 0; i < kick_.size(); ++i) drive(kick_[i], 0);   // fail() may append

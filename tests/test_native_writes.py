@@ -612,8 +612,9 @@ def test_an_api_server_that_never_answers_times_the_bind_out(mode):
         lsock.close()
 
 
+@pytest.mark.parametrize("lazy", [False, True])
 @pytest.mark.parametrize("mode", ["evented", "inline", "frontdoor"])
-def test_many_concurrent_binds_with_label_patches_all_complete(mode):
+def test_many_concurrent_binds_with_label_patches_all_complete(mode, lazy):
     """Driven by the native kube-scheduler stand-in (binds back to back, many in flight) against
     the native API server, every bind is answered once, every pod is bound with its label
     (pipelined behind its binding on a connection the writer keeps), and the writer ends with
@@ -628,7 +629,7 @@ def test_many_concurrent_binds_with_label_patches_all_complete(mode):
             st, body = srv.call("POST", "/api/v1/nodes", json.dumps(pu.make_node(f"n{i}", 8, synthetic_mi355x(8).to_json())))
             nodes.append(json.loads(body))
         rt = Runtime(Config(kube_api=f"http://127.0.0.1:{srv.port}", port=0, host="127.0.0.1",
-                            policy_config_path="/nonexistent", bind_writer_mode=mode))
+                            policy_config_path="/nonexistent", bind_writer_mode=mode, lazy_label_answers=lazy))
         await rt.start()
         loop = asyncio.get_running_loop()
         try:
