@@ -439,10 +439,18 @@ struct IdCache {
   std::string text[kListSlots];        // the list text itself
   int mru = 0;
   uint64_t clock = 0;
+  // equal-length lists are told apart by their last bytes first (sampled windows of one
+  // cluster's names are mostly the same length), then compared whole
+  bool same(int k, std::string_view t) const {
+    if (!valid[k] || len[k] != t.size()) return false;
+    const size_t tail = std::min<size_t>(16, t.size());
+    return std::memcmp(text[k].data() + t.size() - tail, t.data() + t.size() - tail, tail) == 0 &&
+           std::memcmp(text[k].data(), t.data(), t.size()) == 0;
+  }
   int find(std::string_view t) const {
-    if (valid[mru] && len[mru] == t.size() && std::memcmp(text[mru].data(), t.data(), t.size()) == 0) return mru;
+    if (same(mru, t)) return mru;
     for (int k = 0; k < kListSlots; ++k)
-      if (valid[k] && len[k] == t.size() && std::memcmp(text[k].data(), t.data(), t.size()) == 0) return k;
+      if (k != mru && same(k, t)) return k;
     return -1;
   }
 };
