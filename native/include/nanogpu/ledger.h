@@ -229,6 +229,8 @@ class Ledger {
   // 0 (any unique top node); each nomination a bind moves elsewhere raises it by 2 (to 40),
   // every 16 adopted ones lower it by 1: nominations stay where kube-scheduler agrees.
   int32_t nomination_margin() const { return hdr_->nom_margin.load(std::memory_order_relaxed); }
+  // nominations made so far, anywhere in the region (a change marker)
+  uint64_t nominations_made() const { return hdr_->nom_made.load(std::memory_order_acquire); }
   void nomination_counts(uint64_t* made, uint64_t* adopted, uint64_t* moved) const {
     *made = hdr_->nom_made.load(std::memory_order_relaxed);
     *adopted = hdr_->nom_adopted.load(std::memory_order_relaxed);

@@ -470,6 +470,8 @@ struct Frontend::VerbScratch {
   NameTable nid;
   std::deque<std::string> requoted;
   std::string blob, dstr, resp;
+  bool nom_dropped = false;   // the last pod's own nomination was dropped ...
+  uint64_t nom_mark = 0;      // ... when Ledger::nominations_made() read this
   uint64_t opt_seen = 0;   // Frontend::opt_version_ of the copy below
   Options opt;
   bool normalize = false, nominate = false;
@@ -1697,7 +1699,15 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   const bool normalize = s.normalize, nominate = s.nominate;
   io_end(kFeVerbNames, io0);
   io0 = io_t0();
-  if (nominate && !uid.empty()) ledger_->drop_nomination(uid);   // not against itself
+  // not against itself; priorities right behind this worker's filter of the same pod text
+  // (`reused`) with no nomination made anywhere since find it dropped already: no second trip
+  // to the pod table
+  if (nominate && !uid.empty() &&
+      !(prioritize && reused && s.nom_dropped && ledger_->nominations_made() == s.nom_mark)) {
+    s.nom_mark = ledger_->nominations_made();
+    ledger_->drop_nomination(uid);
+    s.nom_dropped = reused || (pod >= 0 && last.valid);   // about the pod `last` holds
+  }
   if ((pod >= 0 || reused) && !uid.empty() && !(prioritize && has_pod(uid))) {
     // filter caches the pod for its bind; priorities of the same cycle find it there
     const std::string_view raw = reused ? std::string_view(last.raw) : d.raw(pod);
@@ -1833,6 +1843,7 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     if (wants) {
       IoTimer it{kFeVerbNominate};
       ledger_->nominate(ids[best], uid, dem, o);
+      s.nom_dropped = false;
     }
   }
   if (normalize && !scores.empty()) {
