@@ -133,8 +133,9 @@ def parse_args():
     # thread that polls 20 us after each event; `--busy-poll-us 0 --frontend-threads 4` is the
     # server's plain default (about 10 % lower here, README "Results")
     ap.add_argument("--frontend-threads", type=int, default=1, help="native front door epoll workers")
-    ap.add_argument("--busy-poll-us", type=int, default=int(os.environ.get("NANOGPU_BUSY_POLL_US", "20")),
-                    help="native front door busy-poll window")
+    ap.add_argument("--busy-poll-us", type=int, default=int(os.environ.get("NANOGPU_BUSY_POLL_US", "8")),
+                    help="native front door busy-poll window (the deployment's: 8 us catches kube-scheduler's "
+                         "next request at 64 nodes and stops polling through the long gaps of big clusters)")
     ap.add_argument("--lazy-label-answers", action="store_true",
                     help="native writer: label PATCH answers read lazily (nanogpu --lazy-label-answers)")
     ap.add_argument("--busy-poll-prio-us", type=int, default=int(os.environ.get("NANOGPU_BUSY_POLL_PRIO_US", "-1")),

@@ -30,7 +30,7 @@ def test_extender_deployment_args_parse():
     assert c["command"][-2:] == ["-m", "nanogpu"]
     cfg = cli.parse(c["args"])
     assert cfg.priority == "binpack" and cfg.workers == 2 and cfg.leader_elect
-    assert cfg.frontend_threads == 1 and cfg.busy_poll_us == 20 and cfg.cpu_affinity == "auto"
+    assert cfg.frontend_threads == 1 and cfg.busy_poll_us == 8 and cfg.cpu_affinity == "auto"
     # the CPU request holds every busy-polling thread (else the server turns polling off)
     cpu = float(c["resources"]["requests"]["cpu"])
     # Guaranteed QoS, whole CPUs: what the static CPU manager needs to give the pod exclusive cores
