@@ -130,7 +130,7 @@ def parse_args():
                     help="the stand-in takes the extender's arg-max instead of kube-scheduler's plugin + "
                          "weighted-extender sum (nanogpu/sim/kubescore.py)")
     # the deployment's front-door settings (deploy/nano-gpu-scheduler-amd.yaml): 1 epoll
-    # thread that polls 20 us after each event; `--busy-poll-us 0 --frontend-threads 4` is the
+    # thread that polls 8 us after each event; `--busy-poll-us 0 --frontend-threads 4` is the
     # server's plain default (about 10 % lower here, README "Results")
     ap.add_argument("--frontend-threads", type=int, default=1, help="native front door epoll workers")
     ap.add_argument("--busy-poll-us", type=int, default=int(os.environ.get("NANOGPU_BUSY_POLL_US", "8")),
