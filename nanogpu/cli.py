@@ -74,6 +74,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--spin-nap", action="store_true",
                    help="front door: sleep the busy-poll window in the kernel (microsecond epoll timeout) "
                         "instead of polling it")
+    p.add_argument("--spin-recv", action="store_true",
+                   help="front door: each busy-poll pass first tries a non-blocking recv on the connection the "
+                        "last filter / priorities answer went out on, then epoll_wait(0)")
     p.add_argument("--api-write-timeout", default="30s",
                    help="native bind writer: an API request unanswered this long fails over to the slow "
                         "path (a half-open connection never answers)")
@@ -140,7 +143,7 @@ def parse(argv: list[str] | None = None) -> Config:
         verify_pod_on_bind=a.bind_verify_pod, native_bind_writes=a.native_bind_writes,
         bind_writer_threads=max(1, a.bind_writer_threads), bind_writer_mode=a.bind_writer_mode,
         native_pod_watch=not a.no_native_pod_watch, assume_label=not a.no_assume_label,
-        api_write_timeout_s=parse_duration(a.api_write_timeout), bind_first=a.bind_first, spin_nap=a.spin_nap, batch_labels=a.batch_labels, reservation_ttl_s=parse_duration(a.reservation_ttl),
+        api_write_timeout_s=parse_duration(a.api_write_timeout), bind_first=a.bind_first, spin_nap=a.spin_nap, spin_recv=a.spin_recv, batch_labels=a.batch_labels, reservation_ttl_s=parse_duration(a.reservation_ttl),
         nominate=not a.no_nominate, nomination_ttl_s=parse_duration(a.nomination_ttl),
         fake_cluster=a.fake_cluster, fake_gpus_per_node=a.fake_gpus_per_node, fake_partition=a.fake_partition,
         seed=a.seed, frontend=a.frontend, frontend_threads=max(1, a.frontend_threads), busy_poll_us=a.busy_poll_us,

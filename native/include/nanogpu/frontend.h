@@ -109,6 +109,9 @@ class Frontend {
   void set_bind_first(bool on) { bind_first_.store(on, std::memory_order_relaxed); }
   // The busy-poll window is slept (epoll_pwait2 with a microsecond timeout) instead of polled.
   void set_spin_nap(bool on) { spin_nap_.store(on, std::memory_order_relaxed); }
+  // busy poll: probe the connection the last cycle answer went out on with a non-blocking
+  // recv before each epoll_wait(0) (the request that follows usually comes back on it)
+  void set_spin_recv(bool on) { spin_recv_.store(on, std::memory_order_relaxed); }
   // Drains requests waiting for Python (non-blocking).
   std::vector<PyRequest> take();
   // Completes request `id` (any thread). Unknown ids (connection gone) are dropped.
@@ -164,6 +167,7 @@ class Frontend {
   void run(Worker* w);
   bool read_in(Worker* w, Conn* c, bool* eof);      // false: connection closed
   void after_read(Worker* w, Conn* c, bool eof);    // parse + answer what is buffered
+  bool spin_recv_hot(Worker* w);                     // true: a request was read and handled
   void process(Worker* w, Conn* c);
   // the verb's whole HTTP answer appended to *out (false: not a native verb, nothing written)
   bool handle_native(Worker* w, Conn* c, std::string_view method, std::string_view path, std::string_view body,
@@ -193,6 +197,7 @@ class Frontend {
   std::atomic<int64_t> busy_poll_prio_ns_{-1};
   std::atomic<bool> bind_first_{false};
   std::atomic<bool> spin_nap_{false};
+  std::atomic<bool> spin_recv_{false};
   std::vector<std::unique_ptr<Worker>> workers_;
 
   mutable std::mutex opt_mu_;

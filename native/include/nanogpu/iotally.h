@@ -43,6 +43,7 @@ enum IoKind : int {
   // pod watch thread
   kPwRecv,          // blocking read of watch bytes (count only)
   kPwFilter,        // one event line through the filter
+  kFeSpinRecv,      // busy poll: non-blocking recv on the last cycle answer's connection (set_spin_recv)
   kIoKinds
 };
 
@@ -51,7 +52,7 @@ inline const char* io_kind_name(int k) {
       "fe_spin_empty", "fe_spin_hit", "fe_spin_after_prio", "fe_wait", "fe_recv", "fe_send_cycle", "fe_send_other", "fe_efd_read",
       "fe_submit", "fe_parse_bind", "fe_verb", "fe_verb_pod", "fe_verb_names", "fe_verb_cache",
       "fe_verb_assume", "fe_verb_nominate", "ledger_choose", "ledger_cache_hit", "wr_wait", "wr_efd_read", "wr_send", "wr_recv",
-      "wr_build", "wr_commit", "pw_recv", "pw_filter"};
+      "wr_build", "wr_commit", "pw_recv", "pw_filter", "fe_spin_recv"};
   return k >= 0 && k < kIoKinds ? names[k] : "?";
 }
 

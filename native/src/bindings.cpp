@@ -778,6 +778,7 @@ PYBIND11_MODULE(_native, m) {
            "thread reads the answers (KubeWriter::send_from_caller).")
       .def("set_bind_first", &Frontend::set_bind_first)
       .def("set_spin_nap", &Frontend::set_spin_nap)
+      .def("set_spin_recv", &Frontend::set_spin_recv)
       .def(
           "set_kube_writer",
           [](Frontend& f, const std::string& host, int port, bool tls, const std::string& token,

@@ -527,6 +527,7 @@ struct Frontend::Worker {
   uint64_t next_conn = 1;
   uint64_t cycle_reply_ns = 0;   // last filter / priorities reply handed to the kernel
   bool cycle_was_prio = false;   // ... and whether it was a priorities answer (io tally)
+  uint64_t cycle_cid = 0;        // ... and the connection it went out on (set_spin_recv)
   VerbScratch scratch;           // the verbs' per-request scratch (this worker's thread only)
 };
 
@@ -968,6 +969,19 @@ void Frontend::run(Worker* w) {
       }
     }
     BindIo* bio = w->bio.load(std::memory_order_acquire);
+    if (polling && !nap && spin_recv_.load(std::memory_order_relaxed) && spin_recv_hot(w)) {
+      if (since != scored) {   // caught inside the window
+        gaps = (gaps << 1) | 1u;
+        scored = since;
+      }
+      spin_hits.fetch_add(1, std::memory_order_relaxed);
+      if (bio) {
+        bio->pump();
+        drain_local(w);
+      }
+      if (w->mb_pending.load(std::memory_order_acquire)) drain_mailbox();
+      continue;
+    }
     int n;
     const uint64_t io0 = io_t0();
     if (nap) {
@@ -1146,6 +1160,36 @@ bool Frontend::read_in(Worker* w, Conn* c, bool* eof) {
   return true;
 }
 
+bool Frontend::spin_recv_hot(Worker* w) {
+  // one non-blocking recv on the connection the last cycle answer went out on: a request
+  // found there is handled without the epoll_wait that would report it and the recv after it
+  auto it = w->conns.find(w->cycle_cid);
+  if (it == w->conns.end()) return false;
+  Conn* c = it->second.get();
+  if (c->waiting || c->close_after) return false;
+  char buf[16384];
+  ssize_t r;
+  {
+    IoTimer t{kFeSpinRecv};
+    r = recv(c->fd, buf, sizeof(buf), MSG_DONTWAIT);
+  }
+  if (r < 0) return false;   // EAGAIN (nothing yet) or an error epoll reports next
+  if (r == 0) {
+    after_read(w, c, true);
+    return true;
+  }
+  if (c->in.empty()) c->t_in_ns = fast_ns();
+  c->in.append(buf, static_cast<size_t>(r));
+  if (static_cast<size_t>(r) == sizeof(buf)) {   // more behind it: the usual reader takes it
+    bool eof = false;
+    if (!read_in(w, c, &eof)) return true;
+    after_read(w, c, eof);
+    return true;
+  }
+  after_read(w, c, false);
+  return true;
+}
+
 void Frontend::after_read(Worker* w, Conn* c, bool eof) {
   const uint64_t id = c->id;
   process(w, c);
@@ -1257,6 +1301,7 @@ void Frontend::process(Worker* w, Conn* c) {
       flush(w, c, kFeSendCycle);
       w->cycle_reply_ns = fast_ns();   // the scheduling cycle's next request is due: spin for it
       w->cycle_was_prio = prio;
+      w->cycle_cid = id;
       if (!w->conns.count(id)) return;
     } else {
       std::string m(method), pth(path), q(query), b(body);   // owned: the Python side keeps them
