@@ -154,8 +154,9 @@ def parse_args():
     ap.add_argument("--batch-labels", action="store_true",
                     help="the extender's writer batches the label PATCHes of bound pods (default: each pipelined "
                          "behind its binding)")
-    ap.add_argument("--spin-recv", action="store_true",
-                    help="front door busy poll tries a non-blocking recv on the last cycle answer's connection first")
+    ap.add_argument("--spin-recv", action=argparse.BooleanOptionalAction, default=True,
+                    help="front door busy poll tries a non-blocking recv on the last cycle answer's connection "
+                         "first (the deployment's default; --no-spin-recv: epoll_wait(0) alone)")
     ap.add_argument("--spin-nap", action="store_true",
                     help="the extender's front door sleeps its busy-poll window instead of polling it")
     ap.add_argument("--bind-first", action="store_true",

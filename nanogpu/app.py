@@ -56,7 +56,7 @@ class Config:
     assume_label: bool = True
     bind_first: bool = False                    # front door: a batch's binds before its filters
     spin_nap: bool = False                      # front door: sleep the busy-poll window, not poll it
-    spin_recv: bool = False                     # front door: poll the last cycle answer's connection with recv first
+    spin_recv: bool = True                      # front door: poll the last cycle answer's connection with recv first
     batch_labels: bool = False                  # native writer: batch label PATCHes after bindings (off: pipelined)
     lazy_label_answers: bool = False            # native writer: read label PATCH answers lazily (no wake-up each)
     watch_assigned_only: bool = True            # pod informer: bound pods only (spec.nodeName!=)

@@ -74,9 +74,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--spin-nap", action="store_true",
                    help="front door: sleep the busy-poll window in the kernel (microsecond epoll timeout) "
                         "instead of polling it")
-    p.add_argument("--spin-recv", action="store_true",
+    p.add_argument("--spin-recv", action=argparse.BooleanOptionalAction, default=True,
                    help="front door: each busy-poll pass first tries a non-blocking recv on the connection the "
-                        "last filter / priorities answer went out on, then epoll_wait(0)")
+                        "last filter / priorities answer went out on, then epoll_wait(0) (--no-spin-recv: "
+                        "epoll_wait(0) alone)")
     p.add_argument("--api-write-timeout", default="30s",
                    help="native bind writer: an API request unanswered this long fails over to the slow "
                         "path (a half-open connection never answers)")

@@ -110,7 +110,8 @@ class Frontend {
   // The busy-poll window is slept (epoll_pwait2 with a microsecond timeout) instead of polled.
   void set_spin_nap(bool on) { spin_nap_.store(on, std::memory_order_relaxed); }
   // busy poll: probe the connection the last cycle answer went out on with a non-blocking
-  // recv before each epoll_wait(0) (the request that follows usually comes back on it)
+  // recv before each epoll_wait(0) (the request that follows usually comes back on it;
+  // profiles/ab_results_r04.md r04sr: +6 % pods/s, -1.3 us a pod). Off while binds go first.
   void set_spin_recv(bool on) { spin_recv_.store(on, std::memory_order_relaxed); }
   // Drains requests waiting for Python (non-blocking).
   std::vector<PyRequest> take();

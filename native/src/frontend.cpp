@@ -969,7 +969,8 @@ void Frontend::run(Worker* w) {
       }
     }
     BindIo* bio = w->bio.load(std::memory_order_acquire);
-    if (polling && !nap && spin_recv_.load(std::memory_order_relaxed) && spin_recv_hot(w)) {
+    if (polling && !nap && spin_recv_.load(std::memory_order_relaxed) && !bind_first_.load(std::memory_order_relaxed) &&
+        spin_recv_hot(w)) {   // (binds first: a bind on another connection must not wait behind it)
       if (since != scored) {   // caught inside the window
         gaps = (gaps << 1) | 1u;
         scored = since;
