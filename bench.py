@@ -157,6 +157,8 @@ def parse_args():
     ap.add_argument("--spin-recv", action=argparse.BooleanOptionalAction, default=True,
                     help="front door busy poll tries a non-blocking recv on the last cycle answer's connection "
                          "first (the deployment's default; --no-spin-recv: epoll_wait(0) alone)")
+    ap.add_argument("--spin-recv-binds", action="store_true",
+                    help="... and, when that finds nothing, the connection the last bind answer went out on")
     ap.add_argument("--spin-nap", action="store_true",
                     help="the extender's front door sleeps its busy-poll window instead of polling it")
     ap.add_argument("--bind-first", action="store_true",
@@ -894,7 +896,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                  nominate=not args.no_nominate,
                  bind_writer_threads=args.bind_writer_threads or max(2, 16 // d.world),
                  bind_writer_mode=args.bind_writer_mode, assume_label=not args.no_assume_label,
-                 bind_first=args.bind_first, spin_nap=args.spin_nap, spin_recv=args.spin_recv, batch_labels=args.batch_labels)
+                 bind_first=args.bind_first, spin_nap=args.spin_nap, spin_recv=args.spin_recv, spin_recv_binds=args.spin_recv_binds, batch_labels=args.batch_labels)
     all_steps_pre = [10_000 + w for w in range(args.warmup)] + list(range(args.steps))
     rt = Runtime(cfg, worker=d.rank if shared else 0, api=rt_api)
     await rt.start()

@@ -57,6 +57,7 @@ class Config:
     bind_first: bool = False                    # front door: a batch's binds before its filters
     spin_nap: bool = False                      # front door: sleep the busy-poll window, not poll it
     spin_recv: bool = True                      # front door: poll the last cycle answer's connection with recv first
+    spin_recv_binds: bool = False               # ... then the last bind answer's
     batch_labels: bool = False                  # native writer: batch label PATCHes after bindings (off: pipelined)
     lazy_label_answers: bool = False            # native writer: read label PATCH answers lazily (no wake-up each)
     watch_assigned_only: bool = True            # pod informer: bound pods only (spec.nodeName!=)
@@ -223,6 +224,7 @@ class Runtime:
                 self.native.fe.set_bind_first(self.cfg.bind_first)
                 self.native.fe.set_spin_nap(self.cfg.spin_nap)
                 self.native.fe.set_spin_recv(self.cfg.spin_recv)
+                self.native.fe.set_spin_recv_binds(self.cfg.spin_recv_binds)
                 api_cfg = getattr(self.api, "config", None)
                 if self.cfg.native_bind_writes and not self.cfg.verify_pod_on_bind and api_cfg is not None:
                     ext = self.extender

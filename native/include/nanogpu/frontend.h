@@ -113,6 +113,8 @@ class Frontend {
   // recv before each epoll_wait(0) (the request that follows usually comes back on it;
   // profiles/ab_results_r04.md r04sr: +6 % pods/s, -1.3 us a pod). Off while binds go first.
   void set_spin_recv(bool on) { spin_recv_.store(on, std::memory_order_relaxed); }
+  // ... and, when that finds nothing, the connection the last bind answer went out on
+  void set_spin_recv_binds(bool on) { spin_recv_binds_.store(on, std::memory_order_relaxed); }
   // Drains requests waiting for Python (non-blocking).
   std::vector<PyRequest> take();
   // Completes request `id` (any thread). Unknown ids (connection gone) are dropped.
@@ -169,6 +171,7 @@ class Frontend {
   bool read_in(Worker* w, Conn* c, bool* eof);      // false: connection closed
   void after_read(Worker* w, Conn* c, bool eof);    // parse + answer what is buffered
   bool spin_recv_hot(Worker* w);                     // true: a request was read and handled
+  bool spin_recv_conn(Worker* w, uint64_t cid);
   void process(Worker* w, Conn* c);
   // the verb's whole HTTP answer appended to *out (false: not a native verb, nothing written)
   bool handle_native(Worker* w, Conn* c, std::string_view method, std::string_view path, std::string_view body,
@@ -199,6 +202,7 @@ class Frontend {
   std::atomic<bool> bind_first_{false};
   std::atomic<bool> spin_nap_{false};
   std::atomic<bool> spin_recv_{false};
+  std::atomic<bool> spin_recv_binds_{false};
   std::vector<std::unique_ptr<Worker>> workers_;
 
   mutable std::mutex opt_mu_;

@@ -779,6 +779,7 @@ PYBIND11_MODULE(_native, m) {
       .def("set_bind_first", &Frontend::set_bind_first)
       .def("set_spin_nap", &Frontend::set_spin_nap)
       .def("set_spin_recv", &Frontend::set_spin_recv)
+      .def("set_spin_recv_binds", &Frontend::set_spin_recv_binds)
       .def(
           "set_kube_writer",
           [](Frontend& f, const std::string& host, int port, bool tls, const std::string& token,

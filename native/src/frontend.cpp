@@ -528,6 +528,7 @@ struct Frontend::Worker {
   uint64_t cycle_reply_ns = 0;   // last filter / priorities reply handed to the kernel
   bool cycle_was_prio = false;   // ... and whether it was a priorities answer (io tally)
   uint64_t cycle_cid = 0;        // ... and the connection it went out on (set_spin_recv)
+  uint64_t bind_cid = 0;         // the connection the last bind answer went out on (set_spin_recv_binds)
   VerbScratch scratch;           // the verbs' per-request scratch (this worker's thread only)
 };
 
@@ -1117,7 +1118,10 @@ void Frontend::deliver_reply(Worker* w, const Reply& r) {
   const uint64_t t_req = c->t_req_ns;
   c->bind_waiting = false;
   flush(w, c);   // may close the connection (Connection: close, a peer reset): c is gone then
-  if (was_bind) note_bind_wall(fast_ns() - t_req);   // handed to the kernel: extender-side wall time
+  if (was_bind) {
+    note_bind_wall(fast_ns() - t_req);   // handed to the kernel: extender-side wall time
+    w->bind_cid = conn;   // back in kube-scheduler's idle pool, the next bind's likeliest (LIFO)
+  }
   if (w->conns.count(conn)) process(w, c);
 }
 
@@ -1162,9 +1166,15 @@ bool Frontend::read_in(Worker* w, Conn* c, bool* eof) {
 }
 
 bool Frontend::spin_recv_hot(Worker* w) {
+  if (spin_recv_conn(w, w->cycle_cid)) return true;
+  return spin_recv_binds_.load(std::memory_order_relaxed) && w->bind_cid != w->cycle_cid &&
+         spin_recv_conn(w, w->bind_cid);
+}
+
+bool Frontend::spin_recv_conn(Worker* w, uint64_t cid) {
   // one non-blocking recv on the connection the last cycle answer went out on: a request
   // found there is handled without the epoll_wait that would report it and the recv after it
-  auto it = w->conns.find(w->cycle_cid);
+  auto it = w->conns.find(cid);
   if (it == w->conns.end()) return false;
   Conn* c = it->second.get();
   if (c->waiting || c->close_after) return false;

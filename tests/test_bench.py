@@ -63,13 +63,14 @@ def test_bench_single_rank_cpu(tmp_path, cpu_exclusive):
     assert user >= 0 and kernel >= 0 and user + kernel > 0
 
 
-def test_bench_spin_recv_catches_requests_on_the_hot_connection(tmp_path, cpu_exclusive):
+@pytest.mark.parametrize("binds", [False, True])
+def test_bench_spin_recv_catches_requests_on_the_hot_connection(binds, tmp_path, cpu_exclusive):
     # a 500 us window: on this host too kube-scheduler's next request lands inside it
     full = tmp_path / "full.json"
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--no-gpu", "--steps", "2", "--warmup", "1",
                         "--pods", "200", "--nodes", "8", "--steady-variant-steps", "0", "--nodes-variant", "0",
                         "--rtt-variant-ms", "0", "--inproc-variant-steps", "0", "--busy-poll-us", "500",
-                        "--spin-recv", "--io-tally", "--json-out", str(full)],
+                        "--spin-recv", "--io-tally", "--json-out", str(full)] + (["--spin-recv-binds"] if binds else []),
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _last_json(r.stdout)
