@@ -26,7 +26,8 @@ interpreter time per pod exceeded the extender's and capped the rate): `--driver
 selects the Python one, `--inproc-driver` runs a Python stand-in inside the extender's
 event loop.
 
-Scaling (`--gpus N`, one torchrun rank per GPU): every rank is one extender worker; all
+Scaling (`--gpus N`, one torchrun rank per GPU; plain `python bench.py --gpus N` starts the N
+ranks itself through torch.distributed.run, `launch_ranks`): every rank is one extender worker; all
 workers share ONE native ledger in /dev/shm (the SO_REUSEPORT replica design of
 nanogpu.app) and ONE API server, each drives 1/N of the burst through its own HTTP
 endpoint, so the burst and the cluster are fixed while workers are added ("strong" scaling). The GPUs are used for the
@@ -169,7 +170,41 @@ def parse_args():
                          "the timed steps when other tenants keep half a CPU of it busy)")
     ap.add_argument("--inproc-driver", action="store_true",
                     help="run the kube-scheduler stand-in inside the extender process (default: own process)")
+    ap.add_argument("--sysfs-root", default="",
+                    help="tests: the KFD sysfs tree the launcher counts visible GPUs in (default: /sys)")
     return ap.parse_args()
+
+
+# --------------------------------------------------------------------------- launcher
+def launch_ranks(args) -> int:
+    """`--gpus N` (N > 1) without a torchrun environment: this process starts the N ranks
+    itself, `python -m torch.distributed.run --nproc-per-node N bench.py <same args>` as a
+    child, and exits with its return code. The ranks write the JSON line to the stdout they
+    inherit. Nothing here touches the GPU (no HIP call, no exec): the visible GPUs are
+    counted from KFD sysfs and the visibility variables (nanogpu.topology.visible), and
+    fewer than N is an error, never a silent 1-rank run."""
+    import socket
+    import subprocess
+
+    if not args.no_gpu:
+        from nanogpu.topology.visible import visible_gpu_count
+
+        seen = visible_gpu_count(args.sysfs_root)
+        if seen < args.gpus:
+            print(f"bench: --gpus {args.gpus} needs {args.gpus} visible GPUs; {seen} visible "
+                  f"(KFD sysfs{' under ' + args.sysfs_root if args.sysfs_root else ''}, "
+                  f"ROCR/HIP_VISIBLE_DEVICES)", file=sys.stderr)
+            return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # RCCL's dmabuf IPC on this host driver
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve()), *sys.argv[1:]]
+    print(f"bench: starting {args.gpus} ranks: {' '.join(cmd[1:8])} ...", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
 
 
 # --------------------------------------------------------------------------- distributed
@@ -181,8 +216,10 @@ class Dist:
         self.dist = None
         self.device = None
         self.cuda = False
-        if want > 1 and self.world == 1:
-            print(f"bench: --gpus {want} requested without torchrun; running 1 rank", file=sys.stderr)
+        if want > 1 and self.world != want:
+            # main() launches the ranks itself when WORLD_SIZE is unset; a torchrun job whose
+            # size disagrees with --gpus would report a curve point it did not measure
+            raise SystemExit(f"bench: --gpus {want} but WORLD_SIZE={self.world}")
 
     def init(self, use_gpu: bool):
         import torch
@@ -913,7 +950,10 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         for st in all_steps_pre:
             apisrv.load(st, [p for r in range(d.world) for p in burst(r, d.world, args.pods, st, 7)])
     pod_ctrl = rt.controllers[-1] if rt.leader else None
-    results = {"steps": [], "frag": [], "client_bind_s": [], "frontdoor_bind_ms": []}
+    results = {"steps": [], "frag": [], "client_bind_s": [], "frontdoor_bind_ms": [], "bind_hops_ns": []}
+    if rt.native is not None:
+        # each native bind's hop split (front door -> writer -> API server -> front door)
+        rt.native.fe.set_bind_hops(True)
 
     # synthetic pod objects are generated up front (client-side data, not scheduler work);
     # their creation in the API server, scheduling, deletion and release are all timed
@@ -986,9 +1026,11 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
             phases.update(create_ms=0.0, schedule_ms=1e3 * summary["span_s"])
             client_s = summary.pop("bind_s_all", [])
             walls = rt.native.fe.take_bind_wall() if rt.native is not None else []
+            hops = rt.native.fe.take_bind_hops() if rt.native is not None else []
             if timed:
                 results["client_bind_s"].extend(client_s)
                 results["frontdoor_bind_ms"].extend(1e3 * x for x in walls)
+                results["bind_hops_ns"].extend(hops)
         return {"stats": summary, "frag": frag, "phases": phases}
 
     async def one_step(step: int, timed: bool, nxt: int | None = None) -> dict:
@@ -1070,10 +1112,12 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                   "release_ms": 1e3 * (time.perf_counter() - ts)}
         phases.update(srv_ms.pop(step, {}))
         walls = rt.native.fe.take_bind_wall() if rt.native is not None else []
+        hops = rt.native.fe.take_bind_hops() if rt.native is not None else []
         client_s = summary.pop("bind_s_all", [])
         if timed:
             results["client_bind_s"].extend(client_s)
             results["frontdoor_bind_ms"].extend(1e3 * x for x in walls)
+            results["bind_hops_ns"].extend(hops)
             diag = {"t0": round(t_step0, 4), "t1": round(time.perf_counter(), 4)}
             diag.update({k: round(summary.get(k, 0.0), 2) for k in ("cycle_max_ms", "cycle_sum_ms", "cycle_wire_ms", "bind_max_ms")})
             diag["unschedulable"] = summary.get("unschedulable_attempts", 0)
@@ -1176,12 +1220,17 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         sampler.on.set()
     # other tenants moving onto the rank's domain mid-run: checked every 4 steps (~0.1 s), the
     # job moves to a quieter domain when they keep half a CPU or more of it busy
-    watch = None
+    watch = api_watch = None
     if d.world == 1 and getattr(args, "_placement", None) and not getattr(args, "no_relocate", False):
         pl = args._placement
         watch = affinity.ContentionWatch(pl["cpus"], pl["pids"], pl["numa"], exclude=pl.get("apiserver") or [])
         watch.check()
         results["foreign_cpus"] = []
+        if pl.get("apiserver") and pl.get("api_pid"):
+            # the shared API server's domain too: read only (it is never moved mid-run)
+            api_watch = affinity.ContentionWatch(pl["apiserver"], [pl["api_pid"]], pl["numa"])
+            api_watch.check()
+            results["foreign_cpus_api"] = []
     for k, s in enumerate(timed_ids):
         r = await one_step(s, True, timed_ids[k + 1] if k + 1 < len(timed_ids) else None)
         results["steps"].append(r["stats"])
@@ -1190,6 +1239,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         if watch is not None and k % 4 == 3:
             with hc:
                 foreign, to = watch.check()
+                if api_watch is not None:
+                    results["foreign_cpus_api"].append(round(api_watch.check()[0], 2))
             results["foreign_cpus"].append(round(foreign, 2))
             if to is not None:
                 affinity.relocate(pl["pids"], to)
@@ -1316,7 +1367,8 @@ def order_line(full: dict) -> tuple[dict, dict]:
         line["gpu"] = {k: v for k, v in gpu.items() if k != "link_bw_matrix_gbs"}
     # whatever else the line carries, it stays under ~3.8 KB: the largest side keys move out
     keep = {"metric", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
-            "vs_baseline", "dtype", "data", "config", "value_mode", "scheduled", "failed"}
+            "vs_baseline", "dtype", "data", "config", "value_mode", "scheduled", "failed", "bind_hops_us",
+            "bind_tail_hop"}
     budget = 3800 - sum(len(json.dumps({k: full[k]})) for k in HEADLINE_LAST if k in full)
     while len(json.dumps(line)) > budget:
         side = [k for k in line if k not in keep]
@@ -1368,6 +1420,8 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
         "relocated_rank0": res.get("relocated"),
         # other tenants' CPUs on the rank's domain, every 4 timed steps (ContentionWatch)
         "foreign_cpus_rank0": res.get("foreign_cpus"),
+        # ... and on the shared API server's domain (its own threads' CPU time taken out)
+        "foreign_cpus_apiserver": res.get("foreign_cpus_api"),
         "pods_per_s_first_filter_to_last_bind": out["value_burst_window"],
         # POST /scheduler/bind wall time as kube-scheduler's stand-in sees it (request written ->
         # reply read), every bind of the timed steps on all ranks
@@ -1375,6 +1429,10 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
         # extender side of the same binds: request bytes read -> reply handed to the kernel
         "p50_bind_frontdoor_ms": out["p50_bind_frontdoor_ms"],
         "p99_bind_frontdoor_ms": out["p99_bind_frontdoor_ms"],
+        # the same binds split by hop (p50, p99, mean of the slowest 1 %; us) and the hop whose
+        # slowest-1 % mean exceeds its median most: where the p99 bind's time goes
+        "bind_hops_us": (out.get("bind_hops") or {}).get("us"),
+        "bind_tail_hop": (out.get("bind_hops") or {}).get("tail_hop"),
         "frag_pct": round(statistics.mean(f["frag_pct"] for f in fr), 3) if fr else None,
         "frag_hbm_pct": round(statistics.mean(f["frag_mib"] for f in fr), 3) if fr else None,
         "stranded_pct": round(statistics.mean(f["stranded_pct"] for f in fr), 3) if fr else None,
@@ -1440,6 +1498,8 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
 
 def main() -> int:
     args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args)
     cpus: list[int] = []
     rank_cpus: list[int] = []
     rank0_numa = -1
@@ -1601,9 +1661,34 @@ def _pct(a: list, q: float):
     return round(a[min(len(a) - 1, int(q * len(a)))], 4) if a else None
 
 
+# the hops of a native bind (nanogpu/bindhops.h), in order: parse + ledger reserve, hand-off to
+# the writer's loop, request built and sent, the API server's answer, commit + reply posted to
+# the front door, reply written to kube-scheduler's connection
+BIND_HOPS = ("reserve", "handoff", "send", "api", "commit", "reply")
+
+
+def hop_summary(rows: list) -> dict | None:
+    """{hop: [p50, p99, mean over the slowest 1 % of binds]} in us, and the hop that owns the
+    tail (largest excess of its tail mean over its p50)."""
+    n = len(rows)
+    if not n:
+        return None
+    cols = [sorted(c) for c in zip(*rows)]
+    by_total = sorted(range(n), key=lambda i: sum(rows[i]))
+    tail = by_total[min(n - 1, int(0.99 * n)):]
+    out = {}
+    for h, name in enumerate(BIND_HOPS):
+        t = sum(rows[i][h] for i in tail) / len(tail)
+        out[name] = [round(cols[h][n // 2] / 1e3, 1), round(cols[h][min(n - 1, int(0.99 * n))] / 1e3, 1),
+                     round(t / 1e3, 1)]
+    owner = max(BIND_HOPS, key=lambda k: out[k][2] - out[k][0])
+    return {"us": out, "tail_hop": owner, "n": n}
+
+
 def summarize(d: Dist, args, res: dict) -> dict:
     """Whole-job numbers of one pass (collective: every rank calls it)."""
     elapsed = d.max(res["elapsed_s"])
+    hops = hop_summary([h for r in d.gather_obj(res.get("bind_hops_ns", [])) for h in r])
     client = sorted(b for r in d.gather_obj(res["client_bind_ms"]) for b in r)
     front = sorted(b for r in d.gather_obj(res["frontdoor_bind_ms"]) for b in r)
     py = sorted(b for r in d.gather_obj(res["bind_ms"]) for b in r)
@@ -1629,6 +1714,7 @@ def summarize(d: Dist, args, res: dict) -> dict:
             "unschedulable": sum(d.gather_obj(res["unschedulable_attempts"])),
             "bind_errors": sum(d.gather_obj(res["bind_errors"])),
             "bind_handoffs": res.get("bind_handoffs"),
+            "bind_hops": hops,
             # each rank's mean stand-in span per step: the slowest sets the peak barrier
             "schedule_ms_by_rank": [round(v, 2) for v in d.gather_obj((res.get("phase_ms") or {}).get("schedule_ms", 0.0))]}
 

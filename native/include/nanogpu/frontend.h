@@ -12,6 +12,7 @@
 // remain the fallback and the reference implementation for the tests.
 #pragma once
 
+#include <array>
 #include <atomic>
 #include <cstdint>
 #include <deque>
@@ -163,6 +164,12 @@ class Frontend {
   // latency"). Bounded at kMaxWallSamples between calls.
   std::vector<uint64_t> take_bind_wall();
   static constexpr size_t kMaxWallSamples = 1u << 20;
+  // Per-hop split of the native binds answered since the last call (bindhops.h), each the six
+  // durations in ns between its seven stamps: parse+reserve, hand-off to the writer, build+send,
+  // API answer, commit+post, reply. Recorded only while switched on (off by default; false
+  // when this host has no invariant TSC to stamp with).
+  bool set_bind_hops(bool on);
+  std::vector<std::array<uint32_t, 6>> take_bind_hops();
 
  private:
   struct Conn;
@@ -216,6 +223,7 @@ class Frontend {
 
   std::mutex wall_mu_;
   std::vector<uint64_t> bind_wall_ns_;
+  std::vector<std::array<uint32_t, 6>> bind_hops_;
 
   mutable std::mutex pod_mu_;
   // filter -> bind pod cache: kPodWays-way buckets by UID hash whose entries keep their

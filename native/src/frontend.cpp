@@ -1,6 +1,7 @@
 // Native extender front door (see frontend.h).
 #include "nanogpu/frontend.h"
 
+#include "nanogpu/bindhops.h"
 #include "nanogpu/bindio.h"
 #include "nanogpu/iotally.h"
 
@@ -82,6 +83,13 @@ uint64_t fast_ns() {
   const TscClock& c = tsc_clock();
   if (c.ns_per_tick == 0.0) return now_ns();
   return c.ns0 + static_cast<uint64_t>(static_cast<double>(__rdtsc() - c.tick0) * c.ns_per_tick);
+}
+
+// the TSC reading a fast_ns() value was taken at (the bind hop stamps are raw TSC)
+uint64_t tsc_of(uint64_t fast) {
+  const TscClock& c = tsc_clock();
+  if (c.ns_per_tick == 0.0 || fast < c.ns0) return __rdtsc();
+  return c.tick0 + static_cast<uint64_t>(static_cast<double>(fast - c.ns0) / c.ns_per_tick);
 }
 
 }  // namespace
@@ -391,6 +399,19 @@ std::vector<uint64_t> Frontend::take_bind_wall() {
   std::lock_guard<std::mutex> g(wall_mu_);
   std::vector<uint64_t> out;
   out.swap(bind_wall_ns_);
+  return out;
+}
+
+bool Frontend::set_bind_hops(bool on) {
+  on = on && tsc_clock().ns_per_tick > 0.0;
+  g_hops.on.store(on, std::memory_order_relaxed);
+  return on;
+}
+
+std::vector<std::array<uint32_t, 6>> Frontend::take_bind_hops() {
+  std::lock_guard<std::mutex> g(wall_mu_);
+  std::vector<std::array<uint32_t, 6>> out;
+  out.swap(bind_hops_);
   return out;
 }
 
@@ -1121,6 +1142,15 @@ void Frontend::deliver_reply(Worker* w, const Reply& r) {
   if (was_bind) {
     note_bind_wall(fast_ns() - t_req);   // handed to the kernel: extender-side wall time
     w->bind_cid = conn;   // back in kube-scheduler's idle pool, the next bind's likeliest (LIFO)
+    uint64_t hv[kBindHops];
+    if (g_hops.close(make_id(w->idx, conn), hv)) {
+      const double k = io_ns_per_tick();
+      std::array<uint32_t, 6> d{};
+      for (int h = 0; h < 6; ++h)
+        d[h] = static_cast<uint32_t>(std::min(4.0e9, static_cast<double>(hv[h + 1] - hv[h]) * k));
+      std::lock_guard<std::mutex> g(wall_mu_);
+      if (bind_hops_.size() < kMaxWallSamples) bind_hops_.push_back(d);
+    }
   }
   if (w->conns.count(conn)) process(w, c);
 }
@@ -1348,6 +1378,7 @@ void Frontend::defer(Worker* w, Conn* c, std::string method, std::string path, s
       c->bind_waiting = true;
       c->t_req_ns = c->t_in_ns ? c->t_in_ns : fast_ns();
       c->t_in_ns = c->in.empty() ? 0 : fast_ns();
+      g_hops.open(j.id, tsc_of(c->t_req_ns));
       IoTimer it{kFeSubmit};
       if (bio) bio->submit(std::move(j));   // sent by pump() after this batch of events
       else if (!kw->send_from_caller(j)) kw->submit(std::move(j));   // sent here, or by the writer

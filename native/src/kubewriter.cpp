@@ -1,6 +1,8 @@
 // Native bind writes to kube-apiserver (see kubewriter.h).
 #include "nanogpu/kubewriter.h"
 
+#include "nanogpu/bindhops.h"
+
 #include <charconv>
 
 #include <arpa/inet.h>
@@ -645,11 +647,16 @@ void KubeWriter::process_batch(std::vector<BindJob>& jobs, std::vector<std::uniq
   const std::string a = auth();
   const uint64_t t1 = now_ns();
   for (size_t i = 0; i < n; ++i) {
+    g_hops.stamp(jobs[i].id, kHopPickup);
     build(jobs[i], &patch[i], &binding[i]);
     conns[2 * i + 1]->start("POST", "/api/v1/namespaces/" + jobs[i].ns + "/pods/" + jobs[i].name + "/binding", kJson,
                             binding[i], a);
+    g_hops.stamp(jobs[i].id, kHopSent);
   }
-  for (size_t i = 0; i < n; ++i) sb[i] = conns[2 * i + 1]->finish(&rb[i]);
+  for (size_t i = 0; i < n; ++i) {
+    sb[i] = conns[2 * i + 1]->finish(&rb[i]);
+    g_hops.stamp(jobs[i].id, kHopAnswer);
+  }
   stats.binding_ns.fetch_add(now_ns() - t1, std::memory_order_relaxed);   // in flight together
   for (size_t i = 0; i < n; ++i) bound[i] = finish_binding(conns[2 * i + 1].get(), jobs[i], binding[i], sb[i], &rb[i]);
   if (label_) {
@@ -689,9 +696,11 @@ bool KubeWriter::finish_binding(HttpConn* c2, BindJob& j, const std::string& b, 
     const int gs = call(c2, "GET", base, kJson, std::string(), &got, true);
     if (gs == 200 && pod_node(got) == j.node) sb = 201;
   }
+  g_hops.stamp(j.id, kHopAnswer);   // the outcome is known (after any retry)
   if (sb >= 200 && sb < 300) {
     ledger_->commit(j.uid);
     stats.ok.fetch_add(1, std::memory_order_relaxed);
+    g_hops.stamp(j.id, kHopPosted);
     respond_(j.id, 200, "{\"Error\":\"\"}");
     return true;
   }
@@ -736,6 +745,7 @@ bool KubeWriter::finish_binding(HttpConn* c2, BindJob& j, const std::string& b, 
   std::string body = "{\"Error\":";
   json::append_quoted(&body, err);
   body += "}";
+  g_hops.stamp(j.id, kHopPosted);
   respond_(j.id, 500, body);
   return false;
 }

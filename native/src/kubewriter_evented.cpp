@@ -32,6 +32,7 @@
 #include <memory>
 #include <vector>
 
+#include "nanogpu/bindhops.h"
 #include "nanogpu/bindio.h"
 #include "nanogpu/iotally.h"
 #include "nanogpu/kubewriter.h"
@@ -297,6 +298,7 @@ void BindIo::complete(int64_t s) {
   if (ok2) {
     kw_->ledger_->commit(jb->j.uid);
     st.ok.fetch_add(1, std::memory_order_relaxed);
+    g_hops.stamp(jb->j.id, kHopPosted);
     reply_(jb->j.id, 200, "{\"Error\":\"\"}");
     if (jb->batch_label) {   // bound: the label follows in a batch (stats.inflight until then)
       queue_label(std::move(jb->j), std::move(jb->patch));
@@ -326,6 +328,7 @@ void BindIo::deliver(Conn& c, int status, std::string body) {
   }
   if (p.which == 2) return label_done(p.job, status, std::move(body));
   Job& jb = *slots_[static_cast<size_t>(p.job)];
+  if (p.which == 1) g_hops.stamp(jb.j.id, kHopAnswer);
   (p.which ? jb.sb : jb.sp) = status;
   (p.which ? jb.rb : jb.rp) = std::move(body);
   if (--jb.left == 0) {
@@ -340,6 +343,7 @@ void BindIo::deliver(Conn& c, int status, std::string body) {
     st.binding_ns.fetch_add(ns_now() - jb.j.t0_ns, std::memory_order_relaxed);
     kw_->ledger_->commit(jb.j.uid);
     st.ok.fetch_add(1, std::memory_order_relaxed);
+    g_hops.stamp(jb.j.id, kHopPosted);
     reply_(jb.j.id, 200, "{\"Error\":\"\"}");
   }
 }
@@ -420,6 +424,10 @@ void BindIo::drive(size_t k, uint32_t events) {
         }
         c.off += static_cast<size_t>(w);
       }
+      if (g_hops.enabled())
+        for (size_t i = c.head; i < c.pend.size(); ++i)
+          if (c.pend[i].which == 1 && slots_[static_cast<size_t>(c.pend[i].job)])
+            g_hops.stamp(slots_[static_cast<size_t>(c.pend[i].job)]->j.id, kHopSent);
       c.st = kReceiving;
       // the answer cannot be there yet: wait for its edge (edge-triggered epoll reports
       // the bytes that arrive from now on) instead of a recv() that would see EAGAIN
@@ -707,6 +715,7 @@ void BindIo::start_waiting() {
 }
 
 void BindIo::submit(BindJob j) {
+  g_hops.stamp(j.id, kHopPickup);
   kw_->stats.inflight.fetch_add(1, std::memory_order_relaxed);
   waiting_.push_back(std::move(j));
   start_waiting();
@@ -985,6 +994,7 @@ bool KubeWriter::send_from_caller(BindJob& j) {
   }
   Handoff h;
   h.k = conn.first;
+  g_hops.stamp(j.id, kHopPickup);
   build(j, &h.patch, &h.binding);
   const std::string a = auth();
   compose_request(&h.out, "POST", j, true, kJsonE, h.binding, host_hdr_, a);
@@ -999,6 +1009,7 @@ bool KubeWriter::send_from_caller(BindJob& j) {
     n = ::send(conn.second, h.out.data(), h.out.size(), MSG_NOSIGNAL | MSG_DONTWAIT);
   } while (n < 0 && errno == EINTR);
   h.sent = n > 0 ? static_cast<size_t>(n) : 0;
+  if (h.sent == h.out.size()) g_hops.stamp(j.id, kHopSent);
   h.broken = n < 0 && errno != EAGAIN && errno != EWOULDBLOCK;
   h.j = std::move(j);
   stats.inflight.fetch_add(1, std::memory_order_relaxed);

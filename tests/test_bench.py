@@ -61,6 +61,12 @@ def test_bench_single_rank_cpu(tmp_path, cpu_exclusive):
     assert d["extender_cpu_us_per_pod_rank0"] > 0 and "ngpu-fe" in diag["extender_cpu_us_per_pod_by_thread_rank0"]
     user, kernel = diag["extender_cpu_us_per_pod_user_kernel_rank0"]
     assert user >= 0 and kernel >= 0 and user + kernel > 0
+    # every native bind split by hop: p50 <= p99 per hop; the median binds' hops add up to about
+    # the front door's median wall (each hop's median is taken alone, so only roughly)
+    hops = d["bind_hops_us"]
+    assert list(hops) == ["reserve", "handoff", "send", "api", "commit", "reply"] and d["bind_tail_hop"] in hops
+    assert all(len(v) == 3 and 0 <= v[0] <= v[1] for v in hops.values())
+    assert 0.2 * d["p50_bind_frontdoor_ms"] <= sum(v[0] for v in hops.values()) / 1e3 <= 3 * d["p50_bind_frontdoor_ms"]
 
 
 @pytest.mark.parametrize("binds", [False, True])
@@ -108,6 +114,66 @@ def test_bench_multi_rank_gloo(ranks, tmp_path, cpu_exclusive):
     assert d["value_independent_schedulers"] > 0 and d["steps_independent_schedulers"] == 1
     # binds the cycle's worker did not see stay native on the other workers (ledger handoff)
     assert d["bind_handoffs"] > 0
+
+
+def test_plain_gpus_n_starts_n_ranks_itself(tmp_path, cpu_exclusive):
+    """`python bench.py --gpus 4` without torchrun must not measure one rank.
+    The launcher starts torch.distributed.run as a child (no GPU touched with --no-gpu) and the
+    line reports the 4-worker job."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "4", "--no-gpu", "--steps", "1",
+                        "--warmup", "1", "--pods", "200", "--nodes", "8", "--rtt-variant-ms", "0",
+                        "--steady-variant-steps", "0", "--nodes-variant", "0", "--inproc-variant-steps", "0",
+                        "--independent-variant-steps", "0"],
+                       capture_output=True, text=True, timeout=400, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _last_json(r.stdout)
+    assert d["n_gpus"] == 4 and d["config"]["parallelism"].startswith("4 extender worker")
+    assert d["value_mode"] == "one kube-scheduler stand-in, binds over all 4 extender workers"
+    assert d["scheduled"] == 200 and d["failed"] == 0
+
+
+def test_plain_gpus_n_refuses_when_fewer_gpus_are_visible(tmp_path):
+    """`--gpus 2` on the real box's one-GPU sysfs view exits non-zero before starting ranks."""
+    env = {k: v for k, v in os.environ.items() if k != "WORLD_SIZE"}
+    real = ROOT / "tests/fixtures/sysfs/mi355x_real"
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
+                        "--sysfs-root", str(real)],
+                       capture_output=True, text=True, timeout=120, env=env, cwd="/tmp")
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert "needs 2 visible GPUs; 1 visible" in r.stderr and not r.stdout.strip()
+
+
+def test_visible_gpu_count_applies_the_visibility_variables(tmp_path):
+    from nanogpu.topology.fixtures import write_mi355x_sysfs
+    from nanogpu.topology.visible import visible_gpu_count
+
+    write_mi355x_sysfs(tmp_path / "spx", 8, "SPX")
+    write_mi355x_sysfs(tmp_path / "cpx", 8, "CPX")
+    spx, cpx = str(tmp_path / "spx"), str(tmp_path / "cpx")
+    assert visible_gpu_count(spx, env={}) == 8
+    assert visible_gpu_count(cpx, env={}) == 64          # HIP enumerates every partition
+    assert visible_gpu_count(spx, env={"HIP_VISIBLE_DEVICES": "0,3"}) == 2
+    assert visible_gpu_count(spx, env={"CUDA_VISIBLE_DEVICES": "5"}) == 1
+    assert visible_gpu_count(spx, env={"ROCR_VISIBLE_DEVICES": "0,1,2", "HIP_VISIBLE_DEVICES": "0,1,2,3"}) == 3
+    assert visible_gpu_count(spx, env={"HIP_VISIBLE_DEVICES": "1,9,2"}) == 1   # stops at an invalid ordinal
+    assert visible_gpu_count(spx, env={"HIP_VISIBLE_DEVICES": ""}) == 8   # set but empty: unset
+    assert visible_gpu_count(spx, env={"ROCR_VISIBLE_DEVICES": "GPU-aa,GPU-bb"}) == 2
+    assert visible_gpu_count(str(ROOT / "tests/fixtures/sysfs/mi355x_real"), env={}) == 1
+    assert visible_gpu_count(str(tmp_path / "none"), env={}) == 0
+
+
+def test_hop_summary_names_the_hop_that_owns_the_tail():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", ROOT / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert bench.hop_summary([]) is None
+    rows = [[1000, 2000, 3000, 40000, 500, 4000]] * 990 + [[1000, 2000, 3000, 40000, 500, 300000]] * 10
+    h = bench.hop_summary(rows)
+    assert h["n"] == 1000 and h["tail_hop"] == "reply"
+    assert h["us"]["api"] == [40.0, 40.0, 40.0] and h["us"]["reply"] == [4.0, 300.0, 300.0]
 
 
 def test_link_weights_fall_back_to_the_reader_and_a_matrix_sets_the_mesh():
