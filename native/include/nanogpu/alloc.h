@@ -33,6 +33,7 @@ constexpr int kNotNeedGPU = -1;      // reference NotNeedGPU, allocate.go:15
 constexpr int kLoadTotal = 2;        // reference LoadTotal, allocate.go:16
 constexpr int kPercentPerDevice = 100;
 constexpr int kWasteSlots = kPercentPerDevice + 1;
+constexpr int32_t kRevalidateNoMemo = -2;   // ShareMemo::rc of a memo entry that cannot be re-validated
 
 enum class Policy : int32_t { kBinpack = 0, kSpread = 1, kRandom = 2, kFirstFit = 3 };
 
@@ -157,6 +158,33 @@ int32_t choose(const Device* devs, int n, const Topology* topo, const Demand& d,
 // Node score for `d` on the pre-placement state (reference semantics: rater.go:59-70,
 // 113-123 in compat mode; 0..100 utilisation/fragmentation score in native mode).
 int32_t rate(const Device* devs, int n, const Demand& d, const Options& o, const Plan* plan);
+
+// Devices a plan's debit changes: its device indices and, for pooled HBM, every member of
+// their pools (a debit mirrors the pool's free MiB onto each member).
+uint64_t plan_touch_mask(const Device* devs, int n, const Plan& p);
+
+// Single-share fast path and re-validation of a memoised placement (Ledger::assume_many). A
+// placement decided device by device (native binpack, one container asking a share of one
+// device, no load awareness: share_fast_path) is pick_share's least (key, index) pair over the
+// devices that fit, each key read from that device alone. scan_share computes it over every
+// device, as choose() would (same device, same score), and keeps the runner-up pair;
+// revalidate answers a node that changed from its memo (ShareMemo), the devices that changed
+// (`changed`: bit i = device i) and the runner-up bound alone, or says kRevalidateNo when an
+// unchanged device could now be the best.
+struct ShareMemo {
+  int32_t rc = kRevalidateNoMemo;   // kOk / kErrNoFit for a memo that can be re-validated
+  int32_t dev = -1;                 // the chosen device (kOk)
+  int32_t score = 0;
+  int32_t runner_idx = kMaxDevs;    // kMaxDevs: no other device fitted
+  uint64_t runner_key = ~0ull;      // every other fitting device's pair is at or above this one
+  bool runner_exact = false;        // ... which is device runner_idx's own pair
+};
+constexpr int32_t kRevalidateNo = -1;
+bool share_fast_path(const Demand& d, const Options& o, int n);
+// kOk (*plan with its score) or kErrNoFit, *next set; kRevalidateNo when not covered
+int32_t scan_share(const Device* devs, int n, const Demand& d, const Options& o, Plan* plan, ShareMemo* next);
+int32_t revalidate(const Device* devs, int n, const Demand& d, const Options& o, const ShareMemo& prev,
+                   uint64_t changed, Plan* plan, ShareMemo* next);
 
 // Debits the plan; on any misfit restores what was taken and returns an error.
 // (Fixes reference allocate.go:108-113, which restores Demand[i] instead of Demand[j].)

@@ -44,6 +44,13 @@ enum IoKind : int {
   kPwRecv,          // blocking read of watch bytes (count only)
   kPwFilter,        // one event line through the filter
   kFeSpinRecv,      // busy poll: non-blocking recv on the last cycle answer's connection (set_spin_recv)
+  kLedgerRevalidate,  // a node's memoised answer re-validated against the devices changed since (no choose)
+  kLedgerScan,        // a one-share binpack pod's placement computed by the fast full scan (scan_share)
+  // why a memo miss ran choose() (counts): no memo entry to re-validate, more bumps since it than
+  // the change ring holds, re-validation undecided (an unchanged device may now be the best)
+  kLedgerMemoCold,
+  kLedgerRingGap,
+  kLedgerRevalUndecided,
   kIoKinds
 };
 
@@ -52,7 +59,8 @@ inline const char* io_kind_name(int k) {
       "fe_spin_empty", "fe_spin_hit", "fe_spin_after_prio", "fe_wait", "fe_recv", "fe_send_cycle", "fe_send_other", "fe_efd_read",
       "fe_submit", "fe_parse_bind", "fe_verb", "fe_verb_pod", "fe_verb_names", "fe_verb_cache",
       "fe_verb_assume", "fe_verb_nominate", "ledger_choose", "ledger_cache_hit", "wr_wait", "wr_efd_read", "wr_send", "wr_recv",
-      "wr_build", "wr_commit", "pw_recv", "pw_filter", "fe_spin_recv"};
+      "wr_build", "wr_commit", "pw_recv", "pw_filter", "fe_spin_recv", "ledger_revalidate", "ledger_scan",
+      "ledger_memo_cold", "ledger_ring_gap", "ledger_reval_undecided"};
   return k >= 0 && k < kIoKinds ? names[k] : "?";
 }
 
@@ -90,6 +98,10 @@ struct IoTimer {
 inline uint64_t io_t0() { return g_io.on.load(std::memory_order_relaxed) ? __rdtsc() : 0; }
 inline void io_end(int k, uint64_t t0) {
   if (t0) g_io.add(k, __rdtsc() - t0);
+}
+// an event counted, not timed
+inline void io_count(int k) {
+  if (g_io.on.load(std::memory_order_relaxed)) g_io.add(k, 0);
 }
 
 // ns per TSC tick (calibrated by the front door; 0 when the TSC is not invariant)

@@ -47,12 +47,21 @@ enum PodState : int32_t { kPodEmpty = 0, kPodReserved = 1, kPodCommitted = 2, kP
 // whose line every lock/unlock by any worker process dirties, so lock traffic on a node does
 // not turn the filters of the other workers into cross-CCD misses; the generation has a
 // line of its own as it changes on every mutation.
+// The devices each of a node's last kChangeRing generation bumps touched (Ledger::bump): a
+// placement memoised at an older generation is re-validated against the devices that changed
+// since (Ledger::assume_many) instead of being recomputed from scratch.
+constexpr int kChangeRing = 64;
+
 struct NodeSlot {
   char name[kNameLen];                              // written at registration only
   int32_t in_use;
   int32_t n_devs;
   alignas(64) pthread_mutex_t mu;
   int32_t n_pods;                                   // under mu
+  // entry g % kChangeRing: the bump from generation g to g + 1 (tag chg_gen = g) changed the
+  // devices in chg_mask (bit i: device i; every bit: the node as a whole). Written under mu.
+  alignas(64) std::atomic<uint64_t> chg_gen[kChangeRing];
+  std::atomic<uint64_t> chg_mask[kChangeRing];
   alignas(64) Topology topo;
   Device devs[kMaxDevs];
 };
@@ -342,6 +351,12 @@ class Ledger {
  private:
   NodeSlot* node(int32_t id) const;
   std::atomic<uint64_t>& gen_of(const NodeSlot* n) const { return hot_[n - nodes_].gen; }
+  // under n->mu: records which devices this change touched (~0: all, or not device-local), then
+  // bumps the node's generation
+  void bump(NodeSlot* n, uint64_t devices_touched);
+  // the devices changed between generations `from` and `to` (false: the ring no longer holds
+  // every bump in between)
+  bool changed_since(const NodeSlot* n, uint64_t from, uint64_t to, uint64_t* mask) const;
   PodSlot* shard(int s) const;
   int shard_of(uint64_t h) const { return static_cast<int>(h % kPodShards); }
   int32_t reserve_as(int32_t id, std::string_view key, const Demand& d, const Options& o, Plan* plan,
@@ -359,6 +374,8 @@ class Ledger {
   void lock_mu(pthread_mutex_t* m) const;
 
   std::string path_;
+  // this object's identity for per-thread caches (a later Ledger can reuse a freed address)
+  uint64_t instance_ = 0;
   bool owner_;
   int fd_ = -1;
   size_t bytes_ = 0;

@@ -548,6 +548,165 @@ static int32_t place_all(Work& w, const Topology* topo, const Demand& d, const O
   return kOk;
 }
 
+namespace {
+// pick_share's ordering key of a device for the first container of a pod (nothing chosen yet,
+// so the affinity term is 0), packed so that unsigned order is pick_share's order: mem-bound
+// neighbours, waste, leftover percent, leftover HBM share (smaller is better; equal keys go to
+// the lower index). kNoKey: a component out of the packed range (not covered).
+constexpr uint64_t kNoKey = ~0ull;
+
+uint64_t binpack_key(const Device& d, const ContainerDemand& c, const Options& o) {
+  const bool membound = (c.flags & kFlagMemBound) != 0;
+  const int64_t k0 = membound ? d.mem_bound + (d.mem_hot ? 1 : 0) : 0;
+  const int64_t kw = (o.waste_aware() ? waste_delta(o, d.pct_free, c.pct) : 0) + 32768;
+  const int64_t k1 = d.pct_free - c.pct;
+  const int64_t k2 = d.mib_total > 0 && c.mib > 0 ? (d.mib_free - c.mib) * 1000 / d.mib_total : 0;
+  if (k0 < 0 || k0 > 0xfffe || kw < 0 || kw > 0xffff || k1 < 0 || k1 > 0xffff || k2 < 0 || k2 > 0xffff) return kNoKey;
+  return (static_cast<uint64_t>(k0) << 48) | (static_cast<uint64_t>(kw) << 32) | (static_cast<uint64_t>(k1) << 16) |
+         static_cast<uint64_t>(k2);
+}
+
+bool covered(const Demand& d, const Options& o, int n) {
+  return !o.compat && o.policy == Policy::kBinpack && !o.load_aware && d.n == 1 && n > 0 && n <= kMaxDevs &&
+         d.c[0].pct > 0 && d.c[0].pct <= kPercentPerDevice;
+}
+}  // namespace
+
+uint64_t plan_touch_mask(const Device* devs, int n, const Plan& p) {
+  uint64_t m = 0;
+  const int total = p.n > 0 ? p.off[p.n] : 0;
+  for (int a = 0; a < total && a < kMaxPlanIdx; ++a) {
+    const int i = p.idx[a];
+    if (i < 0 || i >= n) continue;
+    m |= 1ull << i;
+    if (devs[i].pool >= 0)
+      for (int k = 0; k < n; ++k)
+        if (devs[k].pool == devs[i].pool) m |= 1ull << k;
+  }
+  return m;
+}
+
+namespace {
+// (key, index) pairs: pick_share's choice is the least pair among the devices that fit
+inline bool pair_less(uint64_t ka, int ia, uint64_t kb, int ib) { return ka < kb || (ka == kb && ia < ib); }
+}  // namespace
+
+bool share_fast_path(const Demand& d, const Options& o, int n) { return covered(d, o, n); }
+
+int32_t scan_share(const Device* devs, int n, const Demand& d, const Options& o, Plan* plan, ShareMemo* next) {
+  // pick_share for the first container, every device compared: the least (key, index) pair of
+  // the devices that fit (what choose() places on), and the runner-up for re-validation
+  if (!covered(d, o, n)) return kRevalidateNo;
+  const ContainerDemand& c = d.c[0];
+  uint64_t k1 = kNoKey, k2 = kNoKey;
+  int i1 = kMaxDevs, i2 = kMaxDevs;
+  for (int j = 0; j < n; ++j) {
+    if (!share_fits(devs[j], c)) continue;
+    const uint64_t k = binpack_key(devs[j], c, o);
+    if (k == kNoKey) return kRevalidateNo;
+    if (pair_less(k, j, k1, i1)) {
+      k2 = k1;
+      i2 = i1;
+      k1 = k;
+      i1 = j;
+    } else if (pair_less(k, j, k2, i2)) {
+      k2 = k;
+      i2 = j;
+    }
+  }
+  next->runner_key = k2;
+  next->runner_idx = i2;
+  next->runner_exact = i2 != kMaxDevs;
+  if (i1 == kMaxDevs) {
+    next->rc = kErrNoFit;
+    next->dev = -1;
+    next->score = 0;
+    return kErrNoFit;
+  }
+  plan_init(plan, 1);
+  plan->off[0] = 0;
+  plan->idx[0] = static_cast<int16_t>(i1);
+  plan->off[1] = 1;
+  plan->score = rate(devs, n, d, o, plan);
+  next->rc = kOk;
+  next->dev = i1;
+  next->score = plan->score;
+  return kOk;
+}
+
+int32_t revalidate(const Device* devs, int n, const Demand& d, const Options& o, const ShareMemo& prev,
+                   uint64_t changed, Plan* plan, ShareMemo* next) {
+  // covered: native binpack, no load term, one container asking a share of one device. Its
+  // device is pick_share's least (key, index) pair over the devices that fit, each device's key
+  // read from that device alone, and its score (binpack_penalty, crowding) reads the chosen
+  // device alone. A device that did not change kept its pair (or still does not fit), so:
+  //   * prev.dev and the changed devices are compared exactly;
+  //   * so is the runner-up device when its pair is exact (it was that device's pair when the
+  //     memo was made, and the device has not changed since);
+  //   * every other device is bounded below by the runner-up pair (a device that did not fit
+  //     then still does not).
+  // The least exact pair wins when it is below that bound (or is the runner-up itself); else an
+  // unchanged device might: kRevalidateNo.
+  if (!covered(d, o, n)) return kRevalidateNo;
+  if (prev.rc != kOk && prev.rc != kErrNoFit) return kRevalidateNo;
+  const ContainerDemand& c = d.c[0];
+  const bool have_runner = prev.rc == kOk && prev.runner_idx != kMaxDevs;
+  const bool runner_exact = have_runner && prev.runner_exact && !((changed >> prev.runner_idx) & 1u);
+  uint64_t k1 = kNoKey, k2 = kNoKey;   // least and second least exact pairs
+  int i1 = kMaxDevs, i2 = kMaxDevs;
+  for (int j = 0; j < n; ++j) {
+    const bool exact = ((changed >> j) & 1u) || (prev.rc == kOk && j == prev.dev) || (runner_exact && j == prev.runner_idx);
+    if (!exact || !share_fits(devs[j], c)) continue;
+    const uint64_t k = binpack_key(devs[j], c, o);
+    if (k == kNoKey) return kRevalidateNo;
+    if (pair_less(k, j, k1, i1)) {
+      k2 = k1;
+      i2 = i1;
+      k1 = k;
+      i1 = j;
+    } else if (pair_less(k, j, k2, i2)) {
+      k2 = k;
+      i2 = j;
+    }
+  }
+  // The devices not compared exactly: none fits (no runner-up), or every one is above the
+  // runner-up pair when that is an exact device's (compared above, so the least exact pair is at
+  // or below it), else at or above the bound, so the least exact pair must be below it.
+  if (have_runner && !runner_exact && (i1 == kMaxDevs || !pair_less(k1, i1, prev.runner_key, prev.runner_idx)))
+    return kRevalidateNo;
+  if (i1 == kMaxDevs) {
+    next->rc = kErrNoFit;
+    next->dev = -1;
+    next->score = 0;
+    next->runner_key = kNoKey;
+    next->runner_idx = kMaxDevs;
+    next->runner_exact = false;
+    return kErrNoFit;
+  }
+  // the new runner-up: the second exact pair when it is below the old bound (exact), else the
+  // old bound, which still bounds the devices it covered (exact only while its device is not the
+  // new choice)
+  if (!have_runner || (i2 != kMaxDevs && pair_less(k2, i2, prev.runner_key, prev.runner_idx))) {
+    next->runner_key = k2;
+    next->runner_idx = i2;
+    next->runner_exact = i2 != kMaxDevs;
+  } else {
+    next->runner_key = prev.runner_key;
+    next->runner_idx = prev.runner_idx;
+    next->runner_exact = runner_exact && i1 != prev.runner_idx;
+  }
+  plan_init(plan, 1);
+  plan->off[0] = 0;
+  plan->idx[0] = static_cast<int16_t>(i1);
+  plan->off[1] = 1;
+  // the score reads the chosen device: unchanged, or computed as choose() does
+  plan->score = prev.rc == kOk && i1 == prev.dev && !((changed >> i1) & 1u) ? prev.score : rate(devs, n, d, o, plan);
+  next->rc = kOk;
+  next->dev = i1;
+  next->score = plan->score;
+  return kOk;
+}
+
 static int32_t native_choose(const Device* devs, int n, const Topology* topo, const Demand& d,
                              const Options& o, Plan* plan) {
   Work w0;

@@ -595,6 +595,19 @@ PYBIND11_MODULE(_native, m) {
             }
             return scores;
           })
+      .def(
+          "assume_many",
+          [](Ledger& l, const std::vector<int32_t>& ids, const py::sequence& demand, const Options& o) {
+            Demand d = to_demand(demand);
+            std::vector<int32_t> rcs(ids.size()), scores(ids.size());
+            {
+              py::gil_scoped_release nogil;
+              l.assume_many(ids.data(), static_cast<int>(ids.size()), d, o, rcs.data(), scores.data());
+            }
+            return py::make_tuple(rcs, scores);
+          },
+          "The front door's filter / priorities path over node ids (this thread's score memo, memo "
+          "entries re-validated against the devices changed since): (error codes, scores).")
       .def("assume",
            [](Ledger& l, int32_t id, const py::sequence& demand,
               const Options& o) -> py::tuple {

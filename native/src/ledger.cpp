@@ -20,7 +20,7 @@
 namespace nanogpu {
 
 static constexpr uint64_t kMagic = 0x4e414e4f47505531ULL;  // "NANOGPU1"
-static constexpr uint32_t kVersion = 14;  // 4: HBM pools; 5: cache lines; 6: sizes; 7: serving; 8: nominations; 9: stream owners; 10: overflow records; 11: node epoch; 12-13: bind handoff; 14: dense node generations
+static constexpr uint32_t kVersion = 15;  // 4: HBM pools; 5: cache lines; 6: sizes; 7: serving; 8: nominations; 9: stream owners; 10: overflow records; 11: node epoch; 12-13: bind handoff; 14: dense node generations; 15: device change ring
 
 static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -107,6 +107,8 @@ size_t Ledger::region_bytes(uint32_t max_nodes, uint32_t max_pods) {
 
 Ledger::Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, bool create)
     : path_(path), owner_(false) {
+  static std::atomic<uint64_t> instances{0};
+  instance_ = instances.fetch_add(1, std::memory_order_relaxed) + 1;
   if (max_nodes == 0 || max_pods == 0) throw std::invalid_argument("ledger: zero capacity");
   bytes_ = region_bytes(max_nodes, max_pods);
   bool init = false;
@@ -433,7 +435,7 @@ int32_t Ledger::upsert_node(const std::string& name, const Device* devs, int n,
     std::memcpy(s.devs, merged, sizeof(Device) * m);
     s.n_devs = m;
     s.topo = topo;
-    gen_of(&s).fetch_add(1);
+    bump(&s, ~0ull);
   }
   hdr_->epoch.fetch_add(1);
   {
@@ -472,7 +474,7 @@ bool Ledger::remove_node(int32_t id) {
   if (n->n_pods > 0) return false;
   n->in_use = 0;
   hot_[id].in_use.store(0, std::memory_order_release);
-  gen_of(n).fetch_add(1);
+  bump(n, ~0ull);
   hdr_->epoch.fetch_add(1);
   hdr_->node_epoch.fetch_add(1, std::memory_order_release);
   std::lock_guard<std::mutex> g(names_mu_);
@@ -495,6 +497,33 @@ bool Ledger::snapshot(int32_t id, NodeSnapshot* out) const {
 uint64_t Ledger::generation(int32_t id) const {
   NodeSlot* n = node(id);
   return n ? gen_of(n).load(std::memory_order_acquire) : 0;
+}
+
+void Ledger::bump(NodeSlot* n, uint64_t devices_touched) {
+  const uint64_t g = gen_of(n).load(std::memory_order_relaxed);
+  const int k = static_cast<int>(g % kChangeRing);
+  // the tag is cleared while the mask is rewritten: a reader that sees the tag before and after
+  // its mask read equal to g read the mask of this bump
+  n->chg_gen[k].store(0, std::memory_order_relaxed);
+  std::atomic_thread_fence(std::memory_order_release);
+  n->chg_mask[k].store(devices_touched, std::memory_order_relaxed);
+  n->chg_gen[k].store(g, std::memory_order_release);
+  gen_of(n).fetch_add(1, std::memory_order_release);
+}
+
+bool Ledger::changed_since(const NodeSlot* n, uint64_t from, uint64_t to, uint64_t* mask) const {
+  if (to < from || to - from > static_cast<uint64_t>(kChangeRing)) return false;
+  uint64_t m = 0;
+  for (uint64_t g = from; g < to; ++g) {
+    const int k = static_cast<int>(g % kChangeRing);
+    if (n->chg_gen[k].load(std::memory_order_acquire) != g) return false;
+    const uint64_t x = n->chg_mask[k].load(std::memory_order_relaxed);
+    std::atomic_thread_fence(std::memory_order_acquire);
+    if (n->chg_gen[k].load(std::memory_order_relaxed) != g) return false;
+    m |= x;
+  }
+  *mask = m;
+  return true;
 }
 
 namespace {
@@ -628,11 +657,12 @@ namespace {
 // Any node added or removed (the ledger's node epoch) clears it; every other change shows in the
 // node's generation, which each entry carries.
 struct ScoreMemo {
-  const void* owner = nullptr;
+  uint64_t owner = 0;   // Ledger::instance_ (0: unused)
   uint64_t dh = 0, oh = 0, epoch = 0, used = 0;
   struct E {
     uint64_t gen;   // generation + 1; 0 = empty
     int32_t rc, score;
+    ShareMemo sm;   // what re-validates it after the node changed (sm.rc kRevalidateNoMemo: nothing)
   };
   std::vector<E> e;
 };
@@ -640,15 +670,15 @@ constexpr int kMemoSlots = 16;
 thread_local ScoreMemo t_memo[kMemoSlots];
 thread_local uint64_t t_memo_clock = 0;
 
-ScoreMemo& memo_for(const void* owner, uint64_t dh, uint64_t oh, uint64_t epoch, uint32_t n_nodes) {
+ScoreMemo& memo_for(uint64_t owner, uint64_t dh, uint64_t oh, uint64_t epoch, uint32_t n_nodes) {
   ScoreMemo* lru = &t_memo[0];
   for (ScoreMemo& m : t_memo) {
     if (m.owner == owner && m.dh == dh && m.oh == oh) {
       if (m.epoch != epoch) {
-        m.e.assign(n_nodes, ScoreMemo::E{0, 0, 0});
+        m.e.assign(n_nodes, ScoreMemo::E{0, 0, 0, ShareMemo{}});
         m.epoch = epoch;
       }
-      if (m.e.size() < n_nodes) m.e.resize(n_nodes, ScoreMemo::E{0, 0, 0});
+      if (m.e.size() < n_nodes) m.e.resize(n_nodes, ScoreMemo::E{0, 0, 0, ShareMemo{}});
       m.used = ++t_memo_clock;
       return m;
     }
@@ -658,7 +688,7 @@ ScoreMemo& memo_for(const void* owner, uint64_t dh, uint64_t oh, uint64_t epoch,
   lru->dh = dh;
   lru->oh = oh;
   lru->epoch = epoch;
-  lru->e.assign(n_nodes, ScoreMemo::E{0, 0, 0});
+  lru->e.assign(n_nodes, ScoreMemo::E{0, 0, 0, ShareMemo{}});
   lru->used = ++t_memo_clock;
   return *lru;
 }
@@ -669,9 +699,10 @@ void Ledger::assume_many(const int32_t* ids, int count, const Demand& d, const O
   const Options o = resolve(o_in, d);
   const uint64_t dh = d.hash(), oh = o.hash();
   const int32_t n_nodes = hdr_->n_nodes.load(std::memory_order_acquire);
-  ScoreMemo& memo = memo_for(this, dh, oh, hdr_->node_epoch.load(std::memory_order_acquire),
+  ScoreMemo& memo = memo_for(instance_, dh, oh, hdr_->node_epoch.load(std::memory_order_acquire),
                              static_cast<uint32_t>(std::max(0, n_nodes)));
   Plan plan;
+  const bool fast = share_fast_path(d, o, kMaxDevs);
   for (int i = 0; i < count; ++i) {
     const int32_t id = ids[i];
     score[i] = 0;
@@ -689,9 +720,50 @@ void Ledger::assume_many(const int32_t* ids, int count, const Demand& d, const O
     }
     const uint64_t io0 = io_t0();
     if (cache_get_score(CacheKey{id, gen, dh, oh}, &rc[i], &score[i])) {
-      if (me) *me = ScoreMemo::E{gen + 1, rc[i], score[i]};
+      if (me) *me = ScoreMemo::E{gen + 1, rc[i], score[i], ShareMemo{}};
       io_end(kLedgerCacheHit, io0);
       continue;
+    }
+    // One share container under native binpack (the common pod): answered in place under the
+    // node's lock, no snapshot copy. From an older memo entry and the devices changed since when
+    // that decides it (alloc.h revalidate), else by the fast full scan (scan_share: what
+    // choose() computes for such a pod).
+    if (fast) {
+      const uint64_t io1 = io_t0();
+      NodeSlot* ns = node(id);
+      int32_t r = kRevalidateNo;
+      int kind = kLedgerRevalidate;
+      uint64_t g = 0, changed;
+      ShareMemo next;
+      if (ns) {
+        lock_node(ns);
+        Unlock un{&ns->mu};
+        g = gen_of(ns).load(std::memory_order_relaxed);
+        if (!ns->in_use) {
+          r = kErrUnknownNode;
+        } else {
+          if (!me || !me->gen || me->sm.rc == kRevalidateNoMemo || me->gen - 1 >= g) io_count(kLedgerMemoCold);
+          else if (!changed_since(ns, me->gen - 1, g, &changed)) io_count(kLedgerRingGap);
+          else if ((r = revalidate(ns->devs, ns->n_devs, d, o, me->sm, changed, &plan, &next)) == kRevalidateNo)
+            io_count(kLedgerRevalUndecided);
+          if (r == kRevalidateNo) {
+            r = scan_share(ns->devs, ns->n_devs, d, o, &plan, &next);
+            kind = kLedgerScan;
+          }
+        }
+      }
+      if (r == kErrUnknownNode || !ns) {
+        rc[i] = kErrUnknownNode;
+        continue;
+      }
+      if (r != kRevalidateNo) {
+        rc[i] = r;
+        score[i] = r == kOk ? plan.score : 0;
+        cache_put(CacheKey{id, g, dh, oh}, r, plan);
+        if (me) *me = ScoreMemo::E{g + 1, r, score[i], next};
+        io_end(kind, io1);
+        continue;
+      }
     }
     IoTimer it{kLedgerChoose};
     NodeSnapshot snap;
@@ -702,7 +774,7 @@ void Ledger::assume_many(const int32_t* ids, int count, const Demand& d, const O
     rc[i] = choose(snap.devs, snap.n_devs, &snap.topo, d, o, &plan);
     score[i] = rc[i] == kOk ? plan.score : 0;
     cache_put(CacheKey{id, snap.generation, dh, oh}, rc[i], plan);
-    if (me) *me = ScoreMemo::E{snap.generation + 1, rc[i], score[i]};
+    if (me) *me = ScoreMemo::E{snap.generation + 1, rc[i], score[i], ShareMemo{}};
   }
 }
 
@@ -817,7 +889,7 @@ int32_t Ledger::reserve_as(int32_t id, std::string_view key, const Demand& d, co
     p->state = state;
   }
   ++n->n_pods;
-  gen_of(n).fetch_add(1, std::memory_order_release);
+  bump(n, plan_touch_mask(n->devs, n->n_devs, *plan));
   hdr_->n_pods.fetch_add(1);
   hdr_->epoch.fetch_add(1);
   if (state == kPodNominated) hdr_->nom_made.fetch_add(1, std::memory_order_relaxed);
@@ -872,7 +944,7 @@ int32_t Ledger::allocate_plan(int32_t id, std::string_view key, const Demand& d,
     p->state = committed ? kPodCommitted : kPodReserved;
   }
   ++n->n_pods;
-  gen_of(n).fetch_add(1, std::memory_order_release);
+  bump(n, plan_touch_mask(n->devs, n->n_devs, plan));
   hdr_->n_pods.fetch_add(1);
   hdr_->epoch.fetch_add(1);
   note_request(d);
@@ -920,18 +992,20 @@ int32_t Ledger::release_if(std::string_view key, int32_t only_state) {
   PodSlot* p = find_pod_locked(s, h, kb.c_str());
   if (!p || p->node != id) return kErrUnknownPod;  // raced with another release
   if (only && p->state != only_state) return kOkExisting;   // adopted / committed meanwhile
+  uint64_t touched;
   {
     Demand pd;
     Plan pp;
     get_record(*p, &pd, &pp);
     unapply(n->devs, n->n_devs, pd, pp);
+    touched = plan_touch_mask(n->devs, n->n_devs, pp);
   }
   free_record(p);
   p->state = kPodTombstone;
   --hdr_->shard_live[s];
   ++hdr_->shard_tomb[s];
   --n->n_pods;
-  gen_of(n).fetch_add(1, std::memory_order_release);
+  bump(n, touched);
   hdr_->n_pods.fetch_sub(1);
   hdr_->epoch.fetch_add(1);
   return kOk;
@@ -1277,7 +1351,7 @@ int32_t Ledger::set_load(int32_t id, int dev, float usage) {
   Device& d = n->devs[dev];
   d.load_usage = usage;
   d.remain_load = static_cast<int16_t>(kLoadTotal - static_cast<int>(usage));
-  gen_of(n).fetch_add(1, std::memory_order_release);
+  bump(n, 1ull << dev);
   hdr_->epoch.fetch_add(1);
   return kOk;
 }
@@ -1301,7 +1375,7 @@ int32_t Ledger::set_mem_hot(int32_t id, int dev, bool hot) {
   Device& d = n->devs[dev];
   if ((d.mem_hot != 0) == hot) return kOk;   // unchanged: cached plans stay valid
   d.mem_hot = hot ? 1 : 0;
-  gen_of(n).fetch_add(1, std::memory_order_release);
+  bump(n, 1ull << dev);
   hdr_->epoch.fetch_add(1);
   return kOk;
 }
@@ -1313,7 +1387,7 @@ int32_t Ledger::set_health(int32_t id, int dev, bool healthy) {
   Unlock un{&n->mu};
   if (dev < 0 || dev >= n->n_devs) return kErrBadPlan;
   n->devs[dev].healthy = healthy ? 1 : 0;
-  gen_of(n).fetch_add(1, std::memory_order_release);
+  bump(n, 1ull << dev);
   hdr_->epoch.fetch_add(1);
   return kOk;
 }

@@ -457,3 +457,85 @@ def test_pod_keys_are_views_and_keys_no_slot_holds_never_match():
         rc, _ = L.reserve(nid, bad, [(10, 0)], BIN)
         assert rc != N.OK and L.lookup(bad) is None
     assert L.release(k63) == N.OK and L.lookup(k63) is None
+
+
+# ----------------------------------------------------------------------------- memo re-validation
+_share = st.tuples(st.sampled_from([5, 10, 25, 50, 100]), st.sampled_from([0, 0, 8192, 32768, 100 * 1024]),
+                   st.sampled_from([0, 0, 1]))
+
+
+@settings(max_examples=120, deadline=None)
+@given(st.lists(st.tuples(st.sampled_from(["reserve", "reserve", "reserve", "release", "hot", "health"]),
+                          _share, st.integers(0, 3), st.integers(0, 63)), min_size=5, max_size=80),
+       st.lists(_share, min_size=1, max_size=4), st.sampled_from(["SPX", "CPX", "QPX"]),
+       st.sampled_from([N.Policy.BINPACK, N.Policy.SPREAD]), st.booleans())
+def test_memo_revalidation_agrees_with_a_fresh_choose(ops, probes, mode, policy, hbm):
+    """assume_many (the front door's filter path) keeps a per-thread memo of each node's answer
+    and, when the node changed, re-validates it against the devices the changes touched
+    (Ledger::changed_since + alloc revalidate) instead of re-running choose(). Whatever the
+    history of reserves, releases, health and HBM-activity flips, its (rc, score) per node is
+    what a fresh choose() on the node's current state gives (the plan cache cleared)."""
+    t = synthetic_mi355x(2, mode)
+    L, ids = ledger_with(t, 4, track_hbm=hbm)
+    o = N.Options(policy)
+    live = []
+    N.io_tally_reset()
+    N.io_tally_enable(True)   # (the timers only; the paths are the same either way)
+    try:
+        for k, (op, d, node, dev) in enumerate(ops):
+            nid = ids[node]
+            if op == "reserve":
+                if L.reserve(nid, f"p{k}", [d], o)[0] == N.OK:
+                    live.append(f"p{k}")
+            elif op == "release" and live:
+                L.release(live.pop(dev % len(live)))
+            elif op == "hot":
+                L.set_mem_hot(nid, dev % len(t.devices), bool(k % 2))
+            elif op == "health":
+                L.set_health(nid, dev % len(t.devices), dev % 5 != 0)
+            for p in probes:
+                rcs, scores = L.assume_many(ids, [p], o)
+                dh = N.demand_hash([p])
+                # the plan each node's answer was cached with (by the memo path: the device too)
+                plans = {nid2: [pl for h, _, rc_, pl, _ in L.cached_plans(nid2) if h == dh and rc_ == N.OK]
+                         for nid2 in ids}
+                L.clear_cache()
+                for nid2, rc, sc in zip(ids, rcs, scores):
+                    rc2, plan2, sc2 = L.assume(nid2, [p], o)
+                    assert (rc, sc if rc == N.OK else 0) == (rc2, sc2 if rc2 == N.OK else 0), (k, op, p, nid2)
+                    if rc == N.OK and plans[nid2]:
+                        assert plans[nid2][0] == plan2, (k, op, p, nid2)
+                L.clear_cache()
+    finally:
+        N.io_tally_enable(False)
+
+
+def test_memo_revalidation_skips_most_recomputation_on_a_binpack_burst():
+    """A burst like the bench's: 1-container pods of a dozen shapes reserved one after another
+    on 64 nodes, every pod's filter over all nodes. Once each shape has been seen (the first
+    filter of a shape computes every node), a node that changed is answered from its memo entry
+    and the devices the change touched, not by choose() (5.7 plan computations a
+    pod; at most 2 wanted)."""
+    t = synthetic_mi355x(8)
+    L = N.Ledger("", 64, 4096, True)
+    ids = [L.upsert_node(f"n{i}", t.ledger_devices(True), t.ledger_topo()) for i in range(64)]
+    o = N.Options(N.Policy.BINPACK)
+    rng = random.Random(5)
+    shapes = [(p, m) for p in (10, 25, 50) for m in (8192, 16384, 32768, 65536)]
+    N.io_tally_enable(True)
+    try:
+        for k in range(700):
+            if k == 100:
+                N.io_tally_reset()
+            d = [rng.choice(shapes)]
+            rcs, scores = L.assume_many(ids, d, o)
+            best = max((s, -i) for i, (rc, s) in enumerate(zip(rcs, scores)) if rc == N.OK)
+            assert L.reserve(ids[-best[1]], f"p{k}", d, o)[0] == N.OK
+        tally = N.io_tally()
+    finally:
+        N.io_tally_enable(False)
+    # full placement computations (the general choose() and the one-share fast scan) against
+    # answers re-validated from the memo and the changed devices alone
+    full = tally.get("ledger_choose", (0, 0))[0] + tally.get("ledger_scan", (0, 0))[0]
+    reval = tally.get("ledger_revalidate", (0, 0))[0]
+    assert reval > 0 and full / 600 <= 2.0, (full, reval, tally)
