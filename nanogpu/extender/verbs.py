@@ -311,20 +311,23 @@ class Extender:
         self.state.commit(uid)
         self.metrics.pods_bound.inc()
         if self.assume_label:
-            patch = pu.label_patch(node)
-            try:
-                try:   # first attempt inline; the retry loop only after an API error
-                    await self.api.patch_pod(ns, name, patch)
-                except ApiError as e:
-                    await self._retry_after(e, "patch", self.api.patch_pod, ns, name, patch)
-            except (ApiError, OSError, asyncio.TimeoutError) as e:
-                # bound, annotations on the pod with the binding: only the label is late
-                log.warning("bind %s/%s: label PATCH failed (%s); retrying in the background", ns, name, e)
-                self._background(self._relabel(ns, name, patch))
-        t4 = time.perf_counter()
-        sp.phases["binding"], sp.phases["patch"] = t3 - t2, t4 - t3
+            # bound, annotations on the pod with the binding: kube-scheduler is answered now and
+            # the label follows (as the native writer does), retried in the background
+            self._background(self._label(ns, name, pu.label_patch(node)))
+        sp.phases["binding"] = t3 - t2
         self._m_binding.observe(t3 - t2)
-        self._m_patch.observe(t4 - t3)
+
+    async def _label(self, ns: str, name: str, patch: dict) -> None:
+        t = time.perf_counter()
+        try:
+            try:   # first attempt at once; the retry loop only after an API error
+                await self.api.patch_pod(ns, name, patch)
+            except ApiError as e:
+                await self._retry_after(e, "patch", self.api.patch_pod, ns, name, patch)
+        except (ApiError, OSError, asyncio.TimeoutError) as e:
+            log.warning("bind %s/%s: label PATCH failed (%s); retrying in the background", ns, name, e)
+            await self._relabel(ns, name, patch)
+        self._m_patch.observe(time.perf_counter() - t)
 
     async def _relabel(self, ns: str, name: str, patch: dict) -> None:
         for attempt in range(6):

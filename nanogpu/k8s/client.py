@@ -252,16 +252,66 @@ class KubeClient:
     async def delete_pod(self, ns: str, name: str) -> None:
         await self.request("DELETE", f"/api/v1/namespaces/{ns}/pods/{name}")
 
+    async def request_bytes(self, method: str, path: str, params: dict | None = None) -> bytes:
+        """`request` without decoding: the body as bytes (raises ApiError as `request` does)."""
+        s = await self._s()
+        for attempt in (0, 1):
+            self.calls += 1
+            headers = dict(self._auth(force=attempt == 1) or {})
+            async with s.request(method, self.config.server + path, params=params, headers=headers or None) as r:
+                body = await r.read()
+                status = r.status
+            if status == 401 and attempt == 0 and self.config.token_file:
+                continue
+            break
+        if status >= 400:
+            text = body.decode("utf-8", "replace")
+            try:
+                st = json.loads(text)
+                raise ApiError(status, st.get("message", text), st.get("reason", ""))
+            except (ValueError, AttributeError):
+                raise ApiError(status, text) from None
+        return body
+
     async def list_pods(self, label_selector: str | None = None, field_selector: str | None = None,
-                        namespace: str | None = None) -> tuple[list[dict], str]:
+                        namespace: str | None = None, slim: bool = False, page: int = 500) -> tuple[list[dict], str]:
+        """All pods matching the selectors, read `page` at a time (`limit` / `continue`, as
+        client-go's pager: a 100k-pod LIST is never one body in memory); a continue token that
+        expired meanwhile (410) restarts as one unpaged LIST. `slim`: each page decoded natively
+        down to what the pod informer reads (nanogpu._native.decode_pod_list), the rest of every
+        pod never becomes a Python object."""
         params = {}
         if label_selector:
             params["labelSelector"] = label_selector
         if field_selector:
             params["fieldSelector"] = field_selector
         path = f"/api/v1/namespaces/{namespace}/pods" if namespace else "/api/v1/pods"
-        r = await self.request("GET", path, params=params or None)
-        return r.get("items") or [], (r.get("metadata") or {}).get("resourceVersion", "")
+        decode = None
+        if slim:
+            from ..native import core
+
+            decode = core().decode_pod_list
+        items: list[dict] = []
+        rv, cont = "", ""
+        try:
+            while True:
+                q = dict(params, limit=str(page)) if page > 0 else dict(params)
+                if cont:
+                    q["continue"] = cont
+                if decode is not None:
+                    got, rv, cont = decode(await self.request_bytes("GET", path, params=q))
+                else:
+                    r = await self.request("GET", path, params=q or None)
+                    got = r.get("items") or []
+                    md = r.get("metadata") or {}
+                    rv, cont = md.get("resourceVersion", ""), md.get("continue", "")
+                items.extend(got)
+                if not cont or page <= 0:
+                    return items, rv
+        except ApiError as e:
+            if e.status != 410 or page <= 0:
+                raise
+            return await self.list_pods(label_selector, field_selector, namespace, slim=slim, page=0)
 
     # --------------------------------------------------------------------- nodes
     async def get_node(self, name: str) -> dict:

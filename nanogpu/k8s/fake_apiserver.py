@@ -530,9 +530,27 @@ def make_app(store: FakeKubeStore) -> web.Application:
             pass
         return resp
 
-    def listing(kind: str, items: list, rv: str) -> web.Response:
-        return web.json_response({"kind": kind, "apiVersion": "v1", "metadata": {"resourceVersion": rv},
-                                  "items": items})
+    def listing(kind: str, items: list, rv: str, request: web.Request | None = None) -> web.Response:
+        md = {"resourceVersion": rv}
+        limit = int(request.query.get("limit", "0") or 0) if request is not None else 0
+        if limit > 0:
+            # `limit` / `continue` pages over the list in key order. A token is good for the
+            # resourceVersion it was issued at; one the store has moved past is 410 Expired (a real
+            # API server keeps the snapshot until etcd compacts it: the client's fallback is the
+            # same either way)
+            items = sorted(items, key=lambda p: (pu.meta(p).get("namespace", ""), pu.meta(p).get("name", "")))
+            start = 0
+            tok = request.query.get("continue", "")
+            if tok:
+                t_rv, _, off = tok.partition(":")
+                if t_rv != rv:
+                    return _err(ApiError(410, "The provided continue parameter is too old", "Expired"))
+                start = int(off or 0)
+            page = items[start:start + limit]
+            if start + limit < len(items):
+                md["continue"] = f"{rv}:{start + limit}"
+            items = page
+        return web.json_response({"kind": kind, "apiVersion": "v1", "metadata": md, "items": items})
 
     @routes.get("/api/v1/pods")
     async def list_all_pods(request):
@@ -541,14 +559,14 @@ def make_app(store: FakeKubeStore) -> web.Application:
         if request.query.get("watch") in ("1", "true"):
             return await stream_watch(request, "pods", ls, fs)
         items, rv = store.list_pods(ls, fs)
-        return listing("PodList", items, rv)
+        return listing("PodList", items, rv, request)
 
     @routes.get("/api/v1/namespaces/{ns}/pods")
     async def list_ns_pods(request):
         await lat()
         items, rv = store.list_pods(request.query.get("labelSelector"), request.query.get("fieldSelector"),
                                     request.match_info["ns"])
-        return listing("PodList", items, rv)
+        return listing("PodList", items, rv, request)
 
     @routes.post("/api/v1/namespaces/{ns}/pods")
     async def create_pod(request):

@@ -92,10 +92,12 @@ class Informer:
 
     async def _list(self) -> None:
         before = time.monotonic()      # CLOCK_MONOTONIC, the ledger's clock (ledger.cpp mono_now)
-        if self.resource == "pods" and self.field_selector:
-            items, rv = await self.api.list_pods(label_selector=self.label_selector, field_selector=self.field_selector)
-        elif self.resource == "pods":
-            items, rv = await self.api.list_pods(label_selector=self.label_selector)
+        if self.resource == "pods":
+            # slim: the LIST decoded natively to what the watch events carry too
+            kw = {"slim": True} if self.slim else {}
+            if self.field_selector:
+                kw["field_selector"] = self.field_selector
+            items, rv = await self.api.list_pods(label_selector=self.label_selector, **kw)
         else:
             items, rv = await self.api.list_nodes(label_selector=self.label_selector)
         fresh = {self.key(o): o for o in items}

@@ -74,7 +74,6 @@ class ClusterState:
         self._pending_removal: dict[str, int] = {}   # deleted nodes whose slot still holds shares
         self._released_cap = 65536
         self._reaccount_wait: dict[str, dict] = {}   # uid -> pod waiting for its partner (reaccount)
-        self._wide_plans: dict[str, list] = {}        # uid -> per-container plan of a wide pod
         self.set_policy(policy, compat=compat, load_aware=load_aware, topo_weight=topo_weight, seed=seed,
                         request_sizes=request_sizes or [], learn_sizes=learn_sizes)
 
@@ -331,7 +330,10 @@ class ClusterState:
 
     # ------------------------------------------------------------------ wide pods
     # More GPU containers than a ledger record holds (pu.is_wide): placed in Python on the
-    # node's snapshot (pu.wide_place), accounted as one record folded per device (pu.fold_plan).
+    # node's snapshot (pu.wide_place), accounted as one record folded per device (pu.fold_plan)
+    # with the per-container plan beside it in the shared ledger (Ledger::reserve_wide), so any
+    # worker process answers a retried bind with the plan the ledger holds (reference
+    # dealer.go:200 keeps every pod's plan in its dealer; allocate.go:29-50).
     # The native front door hands such pods to this path (its demand parser stops at 64).
     def _wide_plan(self, nid: int, full) -> list | None:
         if nid < 0:
@@ -371,22 +373,28 @@ class ClusterState:
 
     def _wide_reserve(self, e, uid: str, full) -> tuple[list[list[int]], bool]:
         rec = self.ledger.lookup(uid)
-        if rec is not None and uid in self._wide_plans:
-            if rec["node"] != e.id:
-                raise SchedulingError(f"pod {uid} is already placed on another node")
-            return self._wide_plans[uid], False        # a retried bind
+        if rec is not None and rec["state"] != "nominated":
+            # a retried bind (on this worker or another): the plan the ledger holds, never a new one
+            return self._wide_held(e, uid, rec), False
         plan = self._wide_plan(e.id, full)
         if plan is None:
             raise SchedulingError(f"assume {pu.gpu_container_count(full)} GPU containers on {e.name} failed: "
                                   f"{N.err_str(N.ERR_NO_FIT)}")
         folded, fplan = pu.fold_plan(full, plan)
-        rc = self.ledger.allocate_plan(e.id, uid, folded, fplan, False)
+        rc, held = self.ledger.reserve_wide(e.id, uid, folded, fplan, plan, False)
+        if rc == N.OK_EXISTING:          # another worker reserved it meanwhile
+            return self._wide_held(e, uid, self.ledger.lookup(uid), held), False
         if rc != N.OK:
             raise self.reserve_error(folded, e.name, rc)
-        self._wide_plans[uid] = plan
-        if len(self._wide_plans) > 4096:
-            self._wide_plans.pop(next(iter(self._wide_plans)))
         return plan, True
+
+    def _wide_held(self, e, uid: str, rec: dict | None, held: list | None = None) -> list[list[int]]:
+        if rec is None or rec["node"] != e.id:
+            raise SchedulingError(f"pod {uid} is already placed on another node")
+        held = held if held is not None else self.ledger.wide_plan(uid)
+        if held is None:
+            raise SchedulingError(f"pod {uid} is reserved on {e.name} without its per-container plan")
+        return [list(x) for x in held]
 
     def reserve_error(self, demand, node_name: str, rc: int) -> SchedulingError:
         return SchedulingError(f"assume {self._demand_str(demand)} on {node_name} failed: {N.err_str(rc)}")
@@ -415,11 +423,12 @@ class ClusterState:
             return False
         if pu.is_wide(full):
             demand, lplan = pu.fold_plan(full, plan)
-            self._wide_plans[pu.pod_uid(pod)] = plan
+            rc, _ = self.ledger.reserve_wide(e.id, pu.pod_uid(pod), demand, lplan, plan, True)
+            rc = N.OK if rc == N.OK_EXISTING else rc   # already accounted (dealer.go:214-216)
         else:
             demand, idx = pu.ledger_view(full)
             lplan = pu.ledger_plan(plan, idx)
-        rc = self.ledger.allocate_plan(e.id, pu.pod_uid(pod), demand, lplan, True)
+            rc = self.ledger.allocate_plan(e.id, pu.pod_uid(pod), demand, lplan, True)
         if rc != N.OK:
             if not quiet:
                 log.warning("allocate %s on %s failed: %s", pu.pod_key(pod), node, N.err_str(rc))

@@ -23,6 +23,8 @@
 #include <thread>
 #include <vector>
 
+#include <sys/socket.h>
+
 #include "nanogpu/ledger.h"
 
 namespace nanogpu {
@@ -214,6 +216,11 @@ class KubeWriter {
   int fe_busy_ = 0;              // front-door threads between taking a connection and its handoff
   int io_ep_ = -1;               // the io thread's epoll set (under fe_mu_)
   std::string host_hdr_;
+  // the API server's address, resolved at construction (evented / inline); addr_len_ 0: not
+  // resolved then, each BindIo resolves it itself
+  sockaddr_storage addr_{};
+  socklen_t addr_len_ = 0;
+  int family_ = 0;
   std::deque<SlowJob> slow_q_;   // under mu_, signalled on cv_
 
   KubeTarget t_;

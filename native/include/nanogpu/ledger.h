@@ -109,7 +109,7 @@ struct PodSlot {
   SlotPlan plan;
   uint64_t owner;      // owner_hash of the pod's controlling owner (set_pod_owner), 0: unknown
   int32_t ext;         // 0: inline; k > 0: overflow record k - 1
-  int32_t pad2;
+  int32_t wide;        // 0: none; k > 0: wide record k - 1 (a wide pod's per-container plan)
 };
 
 // Overflow record of a pod with more than kSlotContainers containers (shared region, claimed
@@ -120,6 +120,21 @@ struct ExtRecord {
   Demand demand;
   Plan plan;
 };
+
+// A wide pod (more GPU containers than a Demand holds, pu.is_wide) is accounted as one record
+// folded per device; its per-container plan, what its bind answers and its annotations carry,
+// lives beside it in a wide record (shared region, claimed with a CAS on `used`, owned by one
+// pod slot), so every worker answers a retried bind with the plan the ledger holds and a
+// restart rebuilds it from the ledger or the annotations alike.
+constexpr int kWideContainers = 1024;   // GPU containers a wide record holds
+constexpr int kWideIdx = 2048;          // device indices (whole-device containers take several)
+struct WideRecord {
+  std::atomic<int32_t> used;
+  int32_t n;                            // containers
+  int16_t off[kWideContainers + 1];     // container c: idx[off[c] .. off[c+1])
+  int16_t idx[kWideIdx];
+};
+using WidePlan = std::vector<std::vector<int32_t>>;   // per container, its device indices (-1: none)
 
 // Bind handoff between the worker processes of a replica (Frontend): what a filter parsed
 // from a pod (namespace, name, containers, demand, owner), for its bind when another worker
@@ -181,6 +196,9 @@ struct LedgerHeader {
   uint32_t ext_cap;                 // overflow records (pods over kSlotContainers containers)
   std::atomic<uint32_t> ext_hint;   // where the next claim starts looking
   std::atomic<int32_t> ext_used;
+  uint32_t wide_cap;                // wide records (WideRecord)
+  std::atomic<uint32_t> wide_hint;
+  std::atomic<int32_t> wide_used;
   uint32_t info_cap;                // bind-handoff slots (PodInfoSlot), a multiple of kPodInfoWays
   std::atomic<uint64_t> info_stamp;
   PaddedMutex info_mu[kPodShards];  // bucket b is guarded by info_mu[b % kPodShards]
@@ -274,6 +292,16 @@ class Ledger {
   // Allocates an explicit plan (pods bound by someone else / rebuild from annotations).
   int32_t allocate_plan(int32_t id, std::string_view key, const Demand& d, const Plan& plan,
                         bool committed);
+  // A wide pod: its folded record (demand / plan, as allocate_plan) and its per-container plan
+  // `wide`. kOk: accounted now; kOkExisting: the pod is already on node `id` and *held is the
+  // per-container plan the ledger holds for it (empty if it has none), nothing changed (a
+  // `committed` call still marks it committed); kErrPodExists: it is on another node;
+  // kErrTableFull: no slot or wide record free; kErrBadDemand: more than the record holds.
+  int32_t reserve_wide(int32_t id, std::string_view key, const Demand& folded, const Plan& fplan,
+                       const WidePlan& wide, bool committed, WidePlan* held);
+  // the per-container plan of wide pod `key` (false: not a wide pod of this ledger)
+  bool wide_plan(std::string_view key, WidePlan* out) const;
+  int32_t wide_records_used() const { return hdr_->wide_used.load(std::memory_order_relaxed); }
   int32_t commit(std::string_view key);
   int32_t release(std::string_view key);
   bool lookup(std::string_view key, PodRecord* out) const;
@@ -369,6 +397,8 @@ class Ledger {
   bool put_record(PodSlot* p, const Demand& d, const Plan& plan);
   void get_record(const PodSlot& p, Demand* d, Plan* plan) const;
   void free_record(PodSlot* p);
+  bool put_wide(PodSlot* p, const WidePlan& w);
+  void get_wide(const PodSlot& p, WidePlan* w) const;
 
   void lock_node(NodeSlot* n) const;
   void lock_mu(pthread_mutex_t* m) const;
@@ -385,6 +415,7 @@ class Ledger {
   NodeSlot* nodes_ = nullptr;
   PodSlot* pods_ = nullptr;
   ExtRecord* ext_ = nullptr;
+  WideRecord* wide_ = nullptr;
   PodInfoSlot* info_ = nullptr;
 
   struct CacheKey {

@@ -649,6 +649,33 @@ PYBIND11_MODULE(_native, m) {
            py::arg("committed") = true)
       .def("commit", &Ledger::commit, py::call_guard<py::gil_scoped_release>())
       .def("release", &Ledger::release, py::call_guard<py::gil_scoped_release>())
+      .def("reserve_wide",
+           [](Ledger& l, int32_t id, const std::string& key, const py::sequence& folded,
+              const std::vector<std::vector<int>>& fplan, const WidePlan& wide, bool committed) -> py::tuple {
+             Demand d = to_demand(folded);
+             Plan p = to_plan(fplan);
+             WidePlan held;
+             int32_t rc;
+             {
+               py::gil_scoped_release nogil;
+               rc = l.reserve_wide(id, key, d, p, wide, committed, &held);
+             }
+             if (rc == kOkExisting) return py::make_tuple(rc, held.empty() ? py::object(py::none()) : py::cast(held));
+             return py::make_tuple(rc, py::none());
+           },
+           py::arg("node"), py::arg("key"), py::arg("folded"), py::arg("fplan"), py::arg("wide"),
+           py::arg("committed") = false,
+           "A wide pod: its folded record and its per-container plan, in the shared ledger. (rc, held): "
+           "OK; OK_EXISTING with the per-container plan the ledger already holds for the pod on that node "
+           "(None if it holds none); or an error")
+      .def("wide_plan",
+           [](const Ledger& l, const std::string& key) -> py::object {
+             WidePlan w;
+             if (!l.wide_plan(key, &w)) return py::none();
+             return py::cast(w);
+           },
+           "The per-container plan of wide pod `key` held in the ledger (None: not a wide pod here)")
+      .def_property_readonly("wide_records_used", &Ledger::wide_records_used)
       .def("lookup",
            [](const Ledger& l, const std::string& key) -> py::object {
              PodRecord r;
@@ -1122,6 +1149,30 @@ PYBIND11_MODULE(_native, m) {
       "decode_pod_watch", [](py::bytes data) { return decode_pod_events(data, nullptr); }, py::arg("data"),
       "Newline-delimited pod watch events -> [{type, object}] with each Pod reduced to the fields the "
       "pod informer reads (identity, labels, nano-gpu/* annotations and resources, nodeName, phase).");
+
+  m.def(
+      "decode_pod_list",
+      [](py::bytes data) {
+        const std::string_view sv = data;
+        json::Doc d;
+        if (!d.parse(sv) || !d.is(d.root(), json::Type::kObj)) throw py::value_error("bad PodList");
+        py::list items;
+        const int32_t arr = d.get(d.root(), "items");
+        if (d.is(arr, json::Type::kArr))
+          for (int32_t c = d.at(arr).first; c >= 0; c = d.at(c).next)
+            if (d.is(c, json::Type::kObj)) items.append(slim_pod(d, c));
+        std::string rv, cont;
+        const int32_t md = d.get(d.root(), "metadata");
+        if (d.is(md, json::Type::kObj)) {
+          const int32_t r = d.get(md, "resourceVersion"), k = d.get(md, "continue");
+          if (d.is(r, json::Type::kStr)) rv = std::string(d.str(r));
+          if (d.is(k, json::Type::kStr)) cont = std::string(d.str(k));
+        }
+        return py::make_tuple(items, rv, cont);
+      },
+      py::arg("data"),
+      "A PodList page -> (pods reduced as decode_pod_watch reduces them, resourceVersion, continue token): "
+      "what the pod informer keeps of a LIST, without decoding every field of every pod in Python.");
 
   py::class_<PodWatchFilter, std::shared_ptr<PodWatchFilter>>(
       m, "PodWatchFilter",

@@ -443,6 +443,22 @@ KubeWriter::KubeWriter(KubeTarget target, std::shared_ptr<Ledger> ledger, Respon
   }
   token_checked_ = mono_s();
   host_hdr_ = host_header(t_);
+  if (evented_) {
+    // the API server's address resolved here, on the thread that sets the writer up: an inline
+    // BindIo runs on a front-door worker, whose epoll loop must not wait on a DNS lookup (a name
+    // that does not resolve yet is looked up by the BindIo when it first connects)
+    addrinfo hints{};
+    hints.ai_family = AF_UNSPEC;
+    hints.ai_socktype = SOCK_STREAM;
+    addrinfo* res = nullptr;
+    if (getaddrinfo(t_.host.c_str(), std::to_string(t_.port).c_str(), &hints, &res) == 0 && res &&
+        res->ai_addrlen <= sizeof(addr_)) {
+      std::memcpy(&addr_, res->ai_addr, res->ai_addrlen);
+      addr_len_ = res->ai_addrlen;
+      family_ = res->ai_family;
+    }
+    if (res) freeaddrinfo(res);
+  }
   if (threads < 1) threads = 1;
   if (evented_) {
     max_inflight_ = threads * kBatch;

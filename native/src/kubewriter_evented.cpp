@@ -210,6 +210,12 @@ BindIo::~BindIo() {
 
 bool BindIo::resolve() {
   if (addr_len_) return true;
+  if (kw_->addr_len_) {   // resolved when the writer was set up (not on this loop)
+    std::memcpy(&addr_, &kw_->addr_, kw_->addr_len_);
+    addr_len_ = kw_->addr_len_;
+    family_ = kw_->family_;
+    return true;
+  }
   addrinfo hints{};
   hints.ai_family = AF_UNSPEC;
   hints.ai_socktype = SOCK_STREAM;

@@ -20,7 +20,7 @@
 namespace nanogpu {
 
 static constexpr uint64_t kMagic = 0x4e414e4f47505531ULL;  // "NANOGPU1"
-static constexpr uint32_t kVersion = 15;  // 4: HBM pools; 5: cache lines; 6: sizes; 7: serving; 8: nominations; 9: stream owners; 10: overflow records; 11: node epoch; 12-13: bind handoff; 14: dense node generations; 15: device change ring
+static constexpr uint32_t kVersion = 16;  // 4: HBM pools; 5: cache lines; 6: sizes; 7: serving; 8: nominations; 9: stream owners; 10: overflow records; 11: node epoch; 12-13: bind handoff; 14: dense node generations; 15: device change ring; 16: wide records
 
 static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -90,6 +90,8 @@ uint32_t pods_per_shard_for(uint32_t max_pods) {
 }
 // pods with more than kSlotContainers containers are rare (one in 32 pods at most)
 uint32_t ext_records_for(uint32_t max_pods) { return std::max<uint32_t>(64, max_pods / 32); }
+// pods with more GPU containers than a Demand holds are rarer still
+uint32_t wide_records_for(uint32_t max_pods) { return std::max<uint32_t>(16, max_pods / 512); }
 // bind handoffs in flight at once: pods between their filter and their bind
 uint32_t info_slots_for(uint32_t max_pods) {
   return std::clamp<uint32_t>(max_pods / 16, 1024, 16384) / kPodInfoWays * kPodInfoWays;
@@ -101,8 +103,9 @@ size_t Ledger::region_bytes(uint32_t max_nodes, uint32_t max_pods) {
   const size_t n = align_up(sizeof(NodeSlot) * max_nodes, 4096);
   const size_t p = align_up(sizeof(PodSlot) * kPodShards * pods_per_shard_for(max_pods), 4096);
   const size_t e = align_up(sizeof(ExtRecord) * ext_records_for(max_pods), 4096);
+  const size_t w = align_up(sizeof(WideRecord) * wide_records_for(max_pods), 4096);
   const size_t i = align_up(sizeof(PodInfoSlot) * info_slots_for(max_pods), 4096);
-  return h + n + p + e + i;
+  return h + n + p + e + w + i;
 }
 
 Ledger::Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, bool create)
@@ -163,8 +166,10 @@ Ledger::Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, b
   ext_ = reinterpret_cast<ExtRecord*>(
       reinterpret_cast<char*>(pods_) +
       align_up(sizeof(PodSlot) * kPodShards * pods_per_shard_for(max_pods), 4096));
-  info_ = reinterpret_cast<PodInfoSlot*>(reinterpret_cast<char*>(ext_) +
-                                         align_up(sizeof(ExtRecord) * ext_records_for(max_pods), 4096));
+  wide_ = reinterpret_cast<WideRecord*>(reinterpret_cast<char*>(ext_) +
+                                        align_up(sizeof(ExtRecord) * ext_records_for(max_pods), 4096));
+  info_ = reinterpret_cast<PodInfoSlot*>(reinterpret_cast<char*>(wide_) +
+                                         align_up(sizeof(WideRecord) * wide_records_for(max_pods), 4096));
   if (init) {
     hdr_->version = kVersion;
     hdr_->max_nodes = max_nodes;
@@ -187,6 +192,9 @@ Ledger::Ledger(const std::string& path, uint32_t max_nodes, uint32_t max_pods, b
     hdr_->ext_cap = ext_records_for(max_pods);
     hdr_->ext_hint.store(0);
     hdr_->ext_used.store(0);
+    hdr_->wide_cap = wide_records_for(max_pods);
+    hdr_->wide_hint.store(0);
+    hdr_->wide_used.store(0);
     hdr_->info_cap = info_slots_for(max_pods);
     hdr_->info_stamp.store(0);
     for (auto& m : hdr_->info_mu) init_mutex(&m.m);
@@ -361,6 +369,51 @@ void Ledger::free_record(PodSlot* p) {
     hdr_->ext_used.fetch_sub(1, std::memory_order_relaxed);
   }
   p->ext = 0;
+  if (p->wide > 0 && static_cast<uint32_t>(p->wide) <= hdr_->wide_cap) {
+    wide_[p->wide - 1].used.store(0, std::memory_order_release);
+    hdr_->wide_used.fetch_sub(1, std::memory_order_relaxed);
+  }
+  p->wide = 0;
+}
+
+bool Ledger::put_wide(PodSlot* p, const WidePlan& w) {
+  size_t total = 0;
+  for (const auto& c : w) total += c.size();
+  if (w.size() > static_cast<size_t>(kWideContainers) || total > static_cast<size_t>(kWideIdx)) return false;
+  const uint32_t cap = hdr_->wide_cap;
+  const uint32_t start = hdr_->wide_hint.load(std::memory_order_relaxed);
+  for (uint32_t k = 0; k < cap; ++k) {
+    const uint32_t i = (start + k) % cap;
+    int32_t free_ = 0;
+    if (wide_[i].used.load(std::memory_order_relaxed) == 0 &&
+        wide_[i].used.compare_exchange_strong(free_, 1, std::memory_order_acquire)) {
+      WideRecord& r = wide_[i];
+      r.n = static_cast<int32_t>(w.size());
+      int pos = 0;
+      for (size_t c = 0; c < w.size(); ++c) {
+        r.off[c] = static_cast<int16_t>(pos);
+        for (int32_t x : w[c]) r.idx[pos++] = static_cast<int16_t>(x);
+      }
+      r.off[w.size()] = static_cast<int16_t>(pos);
+      p->wide = static_cast<int32_t>(i) + 1;
+      hdr_->wide_hint.store((i + 1) % cap, std::memory_order_relaxed);
+      hdr_->wide_used.fetch_add(1, std::memory_order_relaxed);
+      return true;
+    }
+  }
+  return false;
+}
+
+void Ledger::get_wide(const PodSlot& p, WidePlan* w) const {
+  w->clear();
+  if (p.wide <= 0 || static_cast<uint32_t>(p.wide) > hdr_->wide_cap) return;
+  const WideRecord& r = wide_[p.wide - 1];
+  const int n = std::clamp(r.n, 0, kWideContainers);
+  w->resize(static_cast<size_t>(n));
+  for (int c = 0; c < n; ++c) {
+    const int a = std::clamp<int>(r.off[c], 0, kWideIdx), b = std::clamp<int>(r.off[c + 1], a, kWideIdx);
+    (*w)[static_cast<size_t>(c)].assign(r.idx + a, r.idx + b);
+  }
 }
 
 int32_t Ledger::upsert_node(const std::string& name, const Device* devs, int n,
@@ -949,6 +1002,78 @@ int32_t Ledger::allocate_plan(int32_t id, std::string_view key, const Demand& d,
   hdr_->epoch.fetch_add(1);
   note_request(d);
   return kOk;
+}
+
+int32_t Ledger::reserve_wide(int32_t id, std::string_view key, const Demand& folded, const Plan& fplan,
+                             const WidePlan& wide, bool committed, WidePlan* held) {
+  NodeSlot* n = node(id);
+  if (!n || !n->in_use) return kErrUnknownNode;
+  if (key.empty() || key.size() >= kKeyLen) return kErrBadDemand;
+  {
+    // the annotations are the truth: a nomination of ours yields (as in allocate_plan)
+    PodRecord r;
+    if (lookup(key, &r) && r.state == kPodNominated) release(key);
+  }
+  const KeyBuf kb(key);
+  const uint64_t h = key_hash(kb.c_str());
+  const int s = shard_of(h);
+  lock_node(n);
+  Unlock un{&n->mu};
+  {
+    lock_mu(&hdr_->shard_mu[s].m);
+    Unlock us{&hdr_->shard_mu[s].m};
+    PodSlot* p = find_pod_locked(s, h, kb.c_str());
+    if (p) {
+      if (p->node != id) return kErrPodExists;
+      if (committed) p->state = kPodCommitted;
+      if (held) get_wide(*p, held);
+      return kOkExisting;   // a retried bind, another worker's reservation, an informer replay
+    }
+  }
+  size_t total = 0;
+  for (const auto& c : wide) total += c.size();
+  if (wide.size() > static_cast<size_t>(kWideContainers) || total > static_cast<size_t>(kWideIdx)) return kErrBadDemand;
+  int32_t rc = apply(n->devs, n->n_devs, folded, fplan);
+  if (rc != kOk) return rc;
+  {
+    lock_mu(&hdr_->shard_mu[s].m);
+    Unlock us{&hdr_->shard_mu[s].m};
+    PodSlot* p = insert_pod_locked(s, h, kb.c_str());
+    if (p && (!put_record(p, folded, fplan) || !put_wide(p, wide))) {
+      free_record(p);
+      p->state = kPodTombstone;
+      --hdr_->shard_live[s];
+      ++hdr_->shard_tomb[s];
+      p = nullptr;
+    }
+    if (!p) {
+      unapply(n->devs, n->n_devs, folded, fplan);
+      return kErrTableFull;
+    }
+    p->node = id;
+    p->t_reserved = mono_now();
+    p->owner = 0;
+    p->state = committed ? kPodCommitted : kPodReserved;
+  }
+  ++n->n_pods;
+  bump(n, plan_touch_mask(n->devs, n->n_devs, fplan));
+  hdr_->n_pods.fetch_add(1);
+  hdr_->epoch.fetch_add(1);
+  note_request(folded);
+  return kOk;
+}
+
+bool Ledger::wide_plan(std::string_view key, WidePlan* out) const {
+  if (key.empty() || key.size() >= kKeyLen) return false;
+  const KeyBuf kb(key);
+  const uint64_t h = key_hash(kb.c_str());
+  const int s = shard_of(h);
+  lock_mu(&hdr_->shard_mu[s].m);
+  Unlock us{&hdr_->shard_mu[s].m};
+  const PodSlot* p = find_pod_locked(s, h, kb.c_str());
+  if (!p || p->wide <= 0) return false;
+  get_wide(*p, out);
+  return true;
 }
 
 int32_t Ledger::commit(std::string_view key) {

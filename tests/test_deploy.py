@@ -25,6 +25,32 @@ def _container(name, kind):
     return obj["spec"]["template"]["spec"]["containers"][0]
 
 
+def _mib(q: str) -> float:
+    units = {"Ki": 1 / 1024, "Mi": 1, "Gi": 1024}
+    for u, f in units.items():
+        if q.endswith(u):
+            return float(q[:-2]) * f
+    return float(q) / 2 ** 20
+
+
+def test_extender_memory_covers_the_shm_ledger_and_the_workers():
+    """the /dev/shm emptyDir (Memory medium) is charged to the container's memory
+    limit. The ledger at the deployment's geometry must fit the emptyDir's sizeLimit, and the
+    limit must hold the sizeLimit plus the workers' own memory (~200 MiB each, plus the pod
+    informer's reduced store: 200 MiB at 100k pods)."""
+    from nanogpu import _native as N
+
+    dep = next(d for d in _docs("nano-gpu-scheduler-amd.yaml") if d["kind"] == "Deployment")
+    pod = dep["spec"]["template"]["spec"]
+    c = pod["containers"][0]
+    cfg = cli.parse(c["args"])
+    ledger_mib = N.Ledger("", cfg.max_nodes, cfg.max_pods, True).bytes / 2 ** 20
+    shm = next(v for v in pod["volumes"] if v["name"] == "shm")["emptyDir"]
+    assert shm["medium"] == "Memory" and ledger_mib <= _mib(shm["sizeLimit"])
+    limit = _mib(c["resources"]["limits"]["memory"])
+    assert limit >= _mib(shm["sizeLimit"]) + cfg.workers * 200 + 200 + 512
+
+
 def test_extender_deployment_args_parse():
     c = _container("nano-gpu-scheduler-amd.yaml", "Deployment")
     assert c["command"][-2:] == ["-m", "nanogpu"]

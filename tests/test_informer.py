@@ -333,3 +333,47 @@ def test_extender_pod_informer_sees_assigned_pods_only(kind):
                 srv.stop()
 
     asyncio.run(main())
+
+
+def test_pod_list_is_paged_and_slim_decoded():
+    """ADVICE r04 (deploy memory): the pod informer's LIST goes `limit` pods a page with
+    `continue` tokens (client-go's pager), each page decoded natively down to what the informer
+    reads (the same reduction as the watch events): a 100k-pod relist is never one body nor a
+    full Python object per pod. A token the server expired (410) restarts as one unpaged LIST."""
+    async def main():
+        store = FakeKubeStore()
+        for i in range(23):
+            p = annotated(f"p{i:02d}", f"n{i % 3}", [[i % 8]], pct=10)
+            p["metadata"]["managedFields"] = [{"manager": "kubelet", "fieldsV1": {"f:status": {}}}]
+            p["spec"]["containers"][0]["env"] = [{"name": "X", "value": "y" * 100}]
+            store.create_pod(p)
+        runner, port = await serve(store)
+        api = KubeClient(KubeConfig(server=f"http://127.0.0.1:{port}"))
+        try:
+            calls = api.calls
+            items, rv = await api.list_pods(page=5, slim=True)
+            assert api.calls - calls == 5 and rv == str(store.rv)          # 23 pods: 5 pages
+            assert sorted(pu.meta(p)["name"] for p in items) == [f"p{i:02d}" for i in range(23)]
+            p = next(x for x in items if pu.meta(x)["name"] == "p07")
+            assert "managedFields" not in p["metadata"] and "env" not in p["spec"]["containers"][0]
+            assert pu.node_name_of(p) == "n1" and pu.plan_from_pod(p) == [[7]]
+            full, _ = await api.list_pods(page=5)
+            assert len(full) == 23 and "managedFields" in full[0]["metadata"]
+            # the store moves between two pages: the token expires, the client lists unpaged
+            real = api.request_bytes
+            n = {"k": 0}
+
+            async def moving(method, path, params=None):
+                n["k"] += 1
+                if n["k"] == 2:
+                    store.create_pod(annotated("late", "n0", [[0]], pct=10))
+                return await real(method, path, params)
+
+            api.request_bytes = moving
+            items, rv = await api.list_pods(page=5, slim=True)
+            assert len(items) == 24 and rv == str(store.rv)
+        finally:
+            await api.close()
+            await runner.cleanup()
+
+    asyncio.run(main())
