@@ -232,7 +232,16 @@ class Dist:
             import torch.distributed as dist
 
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("nccl" if self.cuda else "gloo")
+            # gloo reports its connections on stdout ("[Gloo] Rank 0 is connected ..."): the job's
+            # stdout stays the one JSON line, so the group is set up with fd 1 pointed at stderr
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                dist.init_process_group("nccl" if self.cuda else "gloo")
+            finally:
+                os.dup2(saved, 1)
+                os.close(saved)
             self.dist = dist
 
     def barrier(self):
@@ -1431,6 +1440,7 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
         "p99_bind_frontdoor_ms": out["p99_bind_frontdoor_ms"],
         # the same binds split by hop (p50, p99, mean of the slowest 1 %; us) and the hop whose
         # slowest-1 % mean exceeds its median most: where the p99 bind's time goes
+        "extender_share_of_cycle": cycle_share(res)[0],
         "bind_hops_us": (out.get("bind_hops") or {}).get("us"),
         "bind_tail_hop": (out.get("bind_hops") or {}).get("tail_hop"),
         "frag_pct": round(statistics.mean(f["frag_pct"] for f in fr), 3) if fr else None,
@@ -1757,6 +1767,22 @@ def steady_keys(args, topo, v) -> dict:
     return keys
 
 
+def cycle_share(res: dict) -> tuple[float | None, float | None]:
+    """Who owns kube-scheduler's serial cycle (filter -> priorities -> host chosen), over the
+    pass's timed steps: (share of the cycle the stand-in waited on the extender, request sent ->
+    answer read; share the extender's native verbs computed). The rest is the stand-in's own
+    work (node sampling, plugin scores, host selection) and the loopback round trips."""
+    steps = res.get("steps") or []
+    cyc = sum(st.get("cycle_sum_ms", 0.0) for st in steps)
+    wire = sum(st.get("cycle_wire_ms", 0.0) for st in steps)
+    n = sum(st.get("cycles", 0) for st in steps)
+    nat = res.get("native") or {}
+    if cyc <= 0:
+        return None, None
+    verbs_ms = n * (nat.get("filter", 0.0) + nat.get("priorities", 0.0)) / 1e3
+    return round(wire / cyc, 3), round(verbs_ms / cyc, 3)
+
+
 def nodes_variant_keys(args, topo, v) -> dict:
     """The --nodes-variant pass: pods/s, frag%, the reference model's frag% on the same bursts
     and node sampling, and how often kube-scheduler's choice agreed with the nomination."""
@@ -1777,6 +1803,11 @@ def nodes_variant_keys(args, topo, v) -> dict:
             f"schedulers_{tag}": "one kube-scheduler stand-in, binds over every rank's worker"
             if getattr(n_args, "one_scheduler", False) else "one kube-scheduler stand-in per rank",
             f"native_verb_mean_us_{tag}": res.get("native")}
+    keys[f"extender_share_of_cycle_{tag}"], keys[f"extender_verb_share_of_cycle_{tag}"] = cycle_share(res)
+    st = res.get("steps") or []
+    if st and sum(x.get("cycles", 0) for x in st):
+        keys[f"cycle_us_{tag}"] = round(1e3 * sum(x.get("cycle_sum_ms", 0.0) for x in st)
+                                        / sum(x.get("cycles", 0) for x in st), 1)
     if args.partition == "SPX" and args.policy == "binpack" and not args.compat:
         from nanogpu.sim import fragsim
 
