@@ -339,6 +339,15 @@ class ClusterState:
         if nid < 0:
             return None
         snap = self.ledger.snapshot(nid)
+        if self.options.compat and self.policy in ("binpack", "spread"):
+            # the reference's Choose places any container count (rater.go:74-163): its executable
+            # spec (nanogpu.sim.oracle, bit-exact with Go 1.16's sort) on the node's percents
+            from ..sim import oracle
+
+            gpus = [oracle.G(int(d["pct_free"]) if d.get("healthy", True) else -1, int(d["pct_total"]))
+                    for d in snap["devices"]]
+            idx = oracle.choose(gpus, [int(pct) for pct, _ in full], spread=self.policy == "spread")
+            return None if idx is None else [[i] for i in idx]
         return pu.wide_place(snap["devices"], full, spread=self.policy == "spread")
 
     def _wide_filter(self, full, node_names: list[str]) -> tuple[list[str], dict[str, str]]:
@@ -354,8 +363,19 @@ class ClusterState:
         return ok, failed
 
     def _wide_scores(self, full, node_names: list[str]) -> list[int]:
-        """Utilisation after the placement (binpack: fuller is better; spread: emptier)."""
+        """Utilisation after the placement (binpack: fuller is better; spread: emptier); in
+        compat mode the reference's Rate on the node as it is (rater.go:59-70, 113-123)."""
         out = []
+        if self.options.compat and self.policy in ("binpack", "spread"):
+            from ..sim import oracle
+
+            for nid in self.node_ids(node_names):
+                if nid < 0 or self._wide_plan(nid, full) is None:
+                    out.append(0)
+                    continue
+                gpus = [oracle.G(int(d["pct_free"]), int(d["pct_total"])) for d in self.ledger.snapshot(nid)["devices"]]
+                out.append((oracle.rate_spread if self.policy == "spread" else oracle.rate_binpack)(gpus))
+            return self._normalize(out) if self.score_normalize and out else out
         for nid in self.node_ids(node_names):
             plan = self._wide_plan(nid, full)
             if plan is None:

@@ -186,6 +186,35 @@ def test_a_wide_pods_retried_bind_on_another_worker_gets_the_ledger_plan(tmp_shm
     assert [100 - g["Percent"] for g in c.status()["n0"]["GPUs"]] == [30] + [0] * 7
 
 
+def test_wide_pods_in_compat_mode_follow_the_reference_choose():
+    """`--compat` keeps the reference's placement for every pod: a wide pod (more GPU containers
+    than a ledger record) is placed by the reference's Choose (its executable spec,
+    nanogpu.sim.oracle, Go 1.16 sort included) and scored by its Rate on the node as it is."""
+    from nanogpu.sim import oracle
+    from nanogpu.state.cluster import ClusterState
+
+    for policy in ("binpack", "spread"):
+        st = ClusterState(policy=policy, compat=True)
+        st.register_node(pu.make_node("n0", 8, synthetic_mi355x(8).to_json()))
+        st.register_node(pu.make_node("n1", 8, synthetic_mi355x(8).to_json()))
+        pre = _sidecar_pod("pre", 3, {0, 1, 2}, pct=30)
+        pre["metadata"]["uid"] = f"pre-{policy}"
+        st.reserve(pre, "n0")
+        pod = _sidecar_pod(f"wide-{policy}", 100, set(range(0, 100, 4)) | set(range(1, 100, 2)), pct=3)
+        pod["metadata"]["uid"] = f"wide-{policy}"
+        full = st.pod_demand(pod)
+        assert pu.is_wide(full)
+        devs = st.ledger.snapshot(st.node_entry("n0").id)["devices"]
+        gpus = [oracle.G(int(d["pct_free"]), int(d["pct_total"])) for d in devs]
+        want = oracle.choose(gpus, [p for p, _ in full], spread=policy == "spread")
+        scores = st.score(pod, ["n0", "n1"])
+        assert scores[0] == (oracle.rate_spread if policy == "spread" else oracle.rate_binpack)(gpus)
+        plan, fresh = st.reserve(pod, "n0")
+        assert fresh and plan == [[i] for i in want], policy
+        used = [100 - g["Percent"] for g in st.status()["n0"]["GPUs"]]
+        assert sum(used) == 90 + 3 * sum(1 for p, _ in full if p)
+
+
 def test_fuzz_container_counts_never_answer_5xx():
     async def main():
         store, rt = await _runtime(4)
