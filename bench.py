@@ -1040,6 +1040,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                 results["client_bind_s"].extend(client_s)
                 results["frontdoor_bind_ms"].extend(1e3 * x for x in walls)
                 results["bind_hops_ns"].extend(hops)
+                results.setdefault("bind_hops_steps", []).append(hops)
         return {"stats": summary, "frag": frag, "phases": phases}
 
     async def one_step(step: int, timed: bool, nxt: int | None = None) -> dict:
@@ -1127,6 +1128,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
             results["client_bind_s"].extend(client_s)
             results["frontdoor_bind_ms"].extend(1e3 * x for x in walls)
             results["bind_hops_ns"].extend(hops)
+            results.setdefault("bind_hops_steps", []).append(hops)
             diag = {"t0": round(t_step0, 4), "t1": round(time.perf_counter(), 4)}
             diag.update({k: round(summary.get(k, 0.0), 2) for k in ("cycle_max_ms", "cycle_sum_ms", "cycle_wire_ms", "bind_max_ms")})
             diag["unschedulable"] = summary.get("unschedulable_attempts", 0)
@@ -1357,7 +1359,7 @@ HEADLINE_LAST = ("value_independent_schedulers", "frag_pct_steady_reference_mode
                  "extender_cpu_us_per_pod_rank0", "frag_pct_reference_model", "frag_hbm_pct", "frag_pct",
                  "p99_bind_ms", "p50_bind_ms", "pods_per_s_first_filter_to_last_bind", "value")
 # bulky per-step / per-thread records: --json-out only
-DIAG_KEYS = ("step_diag_rank0", "io_per_pod_rank0", "controller_keys_per_pod_rank0", "python_requests_per_pod_rank0", "schedule_ms_each_step_rank0", "phase_ms_per_step_rank0",
+DIAG_KEYS = ("step_diag_rank0", "bind_hops_us_by_decile_rank0", "io_per_pod_rank0", "controller_keys_per_pod_rank0", "python_requests_per_pod_rank0", "schedule_ms_each_step_rank0", "phase_ms_per_step_rank0",
              "extender_cpu_us_per_pod_by_thread_rank0", "extender_kernel_pct_by_thread_rank0",
              "extender_cpu_us_per_pod_user_kernel_rank0", "frag_pct_steady_each_step", "nominations",
              "nominations_steady", "native_verb_mean_us", "frag_reference_model_source", "host_selection",
@@ -1443,6 +1445,7 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
         "extender_share_of_cycle": cycle_share(res)[0],
         "bind_hops_us": (out.get("bind_hops") or {}).get("us"),
         "bind_tail_hop": (out.get("bind_hops") or {}).get("tail_hop"),
+        "bind_hops_us_by_decile_rank0": hops_by_decile(res.get("bind_hops_steps") or []),
         "frag_pct": round(statistics.mean(f["frag_pct"] for f in fr), 3) if fr else None,
         "frag_hbm_pct": round(statistics.mean(f["frag_mib"] for f in fr), 3) if fr else None,
         "stranded_pct": round(statistics.mean(f["stranded_pct"] for f in fr), 3) if fr else None,
@@ -1693,6 +1696,23 @@ def hop_summary(rows: list) -> dict | None:
                      round(t / 1e3, 1)]
     owner = max(BIND_HOPS, key=lambda k: out[k][2] - out[k][0])
     return {"us": out, "tail_hop": owner, "n": n}
+
+
+def hops_by_decile(steps: list) -> dict | None:
+    """Each hop's mean (us) over the binds of each tenth of a step, in the order they were
+    answered, averaged over the steps: whether a hop's tail sits at the start of a burst (cores
+    that slept through the gap between steps) or spreads over it."""
+    rows = [[] for _ in range(10)]
+    for hops in steps:
+        n = len(hops)
+        if n < 10:
+            continue
+        for k, h in enumerate(hops):
+            rows[min(9, 10 * k // n)].append(h)
+    if not rows[0]:
+        return None
+    return {name: [round(sum(r[h] for r in rows[dc]) / len(rows[dc]) / 1e3, 1) for dc in range(10)]
+            for h, name in enumerate(BIND_HOPS)}
 
 
 def summarize(d: Dist, args, res: dict) -> dict:
