@@ -98,6 +98,8 @@ def parse_args():
     ap.add_argument("--independent-variant-steps", type=int, default=3,
                     help="with N > 1 ranks, after the timed steps, an --independent-schedulers pass "
                          "(value_independent_schedulers; 0: none)")
+    ap.add_argument("--apiserver-keep-heap", action="store_true",
+                    help="the shared API server's process keeps freed heap memory (no trim / unmap)")
     ap.add_argument("--apiserver-threads", type=int, default=0,
                     help="shared API server IO threads (0: one per rank, 4 to 16)")
     ap.add_argument("--bind-writer-threads", type=int, default=0,
@@ -583,7 +585,16 @@ def apiserver_main(conn, avoid: list[int] | None = None, near: int = -1) -> None
     while True:
         msg = conn.recv()
         op = msg[0]
-        if op == "start":            # a fresh server: (threads, modelled RTT in seconds)
+        if op == "start":            # a fresh server: (threads, modelled RTT in seconds[, keep heap])
+            if len(msg) > 3 and msg[3]:
+                # glibc keeps freed memory instead of trimming / unmapping it: a burst's writes
+                # after the previous burst's bulk delete then reuse pages instead of faulting
+                # them back in (M_TRIM_THRESHOLD -1, M_MMAP_THRESHOLD -3)
+                import ctypes
+
+                libc = ctypes.CDLL("libc.so.6")
+                libc.mallopt(-1, 1 << 30)
+                libc.mallopt(-3, 32 << 20)
             if srv is not None:
                 srv.stop()
             steps.clear()
@@ -736,8 +747,8 @@ class ApiServerProc:
         self.conn.send(msg)
         return self.conn.recv()
 
-    def start(self, threads: int, latency_s: float = 0.0) -> str:
-        port, self.cpus = self._rpc("start", threads, latency_s)
+    def start(self, threads: int, latency_s: float = 0.0, keep_heap: bool = False) -> str:
+        port, self.cpus = self._rpc("start", threads, latency_s, keep_heap)
         self.url = f"http://127.0.0.1:{port}"
         return self.url
 
@@ -919,7 +930,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         url = None
         if d.rank == 0:
             apisrv = api_proc
-            url = apisrv.start(args.apiserver_threads or min(16, max(4, d.world)), args.api_rtt_ms / 1e3)
+            url = apisrv.start(args.apiserver_threads or min(16, max(4, d.world)), args.api_rtt_ms / 1e3,
+                               args.apiserver_keep_heap)
             if getattr(args, "_placement", None):
                 args._placement["apiserver"] = list(apisrv.cpus)
             apisrv.add_nodes(nodes)
