@@ -51,7 +51,7 @@ bool filter_pod_event(PodWatchFilter& f, std::string_view line, json::Doc& d, st
   bool drop = false;
   if (!seen && type == "DELETED") {
     // Python never held it: releasing is all the controller would do (pods.py::_on_event)
-    if (f.ledger->release(std::string(field(d, md, "uid"))) == kOk) ++f.released;
+    if (f.ledger->release(field(d, md, "uid")) == kOk) ++f.released;
     drop = true;
   } else if (!seen) {
     // what the controller ignores: a pending pod, or a bound, running one the ledger holds

@@ -635,6 +635,105 @@ static void mailbox_wakeups(int requests) {
               static_cast<unsigned long long>(fe.mb_wakeups.load()));
 }
 
+// Filter-path memo re-validation (Ledger::assume_many: change ring, runner-up bound, fast scan)
+// and wide records (Ledger::reserve_wide) under concurrency: reader threads run assume_many over
+// every node while writer threads reserve, release and account wide pods. Quiescent at the end,
+// every memoised answer must equal a fresh choose() on the node's state, and every wide record
+// must be free again.
+static void memo_and_wide(int iters) {
+  Ledger l("", 16, 65536, true);
+  const int n_nodes = 6;
+  add_nodes(l, n_nodes);
+  std::atomic<bool> stop{false};
+  Options bin;
+  std::vector<std::thread> ts;
+  std::vector<int32_t> ids(n_nodes);
+  for (int k = 0; k < n_nodes; ++k) ids[k] = k;
+  auto shape = [](std::mt19937_64& rng) {
+    Demand d;
+    std::memset(&d, 0, sizeof(d));
+    static const int pcts[] = {5, 10, 25, 50, 100};
+    d.n = 1;
+    d.c[0].pct = pcts[rng() % 5];
+    d.c[0].mib = static_cast<int64_t>(rng() % 3) * 16384;
+    d.c[0].flags = rng() % 4 == 0 ? kFlagMemBound : 0;
+    return d;
+  };
+  for (int r = 0; r < 2; ++r)
+    ts.emplace_back([&, r] {
+      std::mt19937_64 rng(100 + r);
+      std::vector<int32_t> rc(n_nodes), sc(n_nodes);
+      while (!stop.load()) {
+        const Demand d = shape(rng);
+        l.assume_many(ids.data(), n_nodes, d, bin, rc.data(), sc.data());
+        for (int k = 0; k < n_nodes; ++k) CHECK(rc[k] != kErrUnknownNode);
+      }
+    });
+  std::vector<std::thread> ws;
+  for (int w = 0; w < 3; ++w)
+    ws.emplace_back([&, w] {
+      std::mt19937_64 rng(200 + w);
+      std::vector<std::string> live;
+      for (int it = 0; it < iters; ++it) {
+        const std::string key = "m" + std::to_string(w) + "-" + std::to_string(it);
+        const int node = static_cast<int>(rng() % n_nodes);
+        if (rng() % 8 == 0) {
+          // a wide pod: 70 x 1 % on the first devices, folded per device
+          WidePlan wide(70);
+          Demand folded;
+          std::memset(&folded, 0, sizeof(folded));
+          folded.n = 2;
+          folded.c[0].pct = 35;
+          folded.c[1].pct = 35;
+          for (int c = 0; c < 70; ++c) wide[static_cast<size_t>(c)] = {c % 2};
+          Plan fp;
+          std::memset(&fp, 0, sizeof(fp));
+          fp.n = 2;
+          fp.off[0] = 0, fp.off[1] = 1, fp.off[2] = 2;
+          fp.idx[0] = 0, fp.idx[1] = 1;
+          WidePlan held;
+          const int32_t rc = l.reserve_wide(node, key, folded, fp, wide, rng() % 2 == 0, &held);
+          if (rc == kOk) {
+            WidePlan got;
+            CHECK(l.wide_plan(key, &got) && got == wide);
+            CHECK(l.reserve_wide(node, key, folded, fp, wide, true, &held) == kOkExisting && held == wide);
+            live.push_back(key);
+          }
+        } else {
+          const Demand d = shape(rng);
+          Plan p;
+          if (l.reserve(node, key, d, bin, &p) == kOk) live.push_back(key);
+        }
+        if (!live.empty() && rng() % 3 == 0) {
+          const size_t i = rng() % live.size();
+          CHECK(l.release(live[i]) == kOk);
+          live.erase(live.begin() + static_cast<long>(i));
+        }
+      }
+      for (const auto& k : live) CHECK(l.release(k) == kOk);
+    });
+  for (auto& w : ws) w.join();
+  stop.store(true);
+  for (auto& t : ts) t.join();
+  CHECK(l.n_pods() == 0 && l.wide_records_used() == 0);
+  // quiescent: memoised (and re-validated) answers equal fresh placements
+  std::mt19937_64 rng(300);
+  std::vector<int32_t> rc(n_nodes), sc(n_nodes);
+  for (int q = 0; q < 200; ++q) {
+    const Demand d = shape(rng);
+    Plan p;
+    l.reserve(static_cast<int32_t>(rng() % n_nodes), "q" + std::to_string(q), d, bin, &p);
+    l.assume_many(ids.data(), n_nodes, d, bin, rc.data(), sc.data());
+    l.clear_cache();
+    for (int k = 0; k < n_nodes; ++k) {
+      const int32_t r2 = l.assume(k, d, bin, &p);
+      CHECK(rc[k] == r2);
+      if (r2 == kOk) CHECK(sc[k] == p.score);
+    }
+  }
+  std::printf("memo + wide ok: %d iterations x 3 writers, 2 readers\n", iters);
+}
+
 int main(int argc, char** argv) {
   if (argc > 1 && std::strcmp(argv[1], "relist-scale") == 0) {
     relist_scale(argc > 2 ? std::atoi(argv[2]) : 100000);
@@ -732,5 +831,6 @@ int main(int argc, char** argv) {
   relist_gap(std::max(200, iters / 4));
   handoff(std::max(500, iters));
   mailbox_wakeups(std::max(400, iters / 2));
+  memo_and_wide(std::max(1000, iters));
   return 0;
 }
