@@ -1458,6 +1458,10 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
         "bind_hops_us": (out.get("bind_hops") or {}).get("us"),
         "bind_tail_hop": (out.get("bind_hops") or {}).get("tail_hop"),
         "bind_hops_us_by_decile_rank0": hops_by_decile(res.get("bind_hops_steps") or []),
+        # the API hop's mean over the first tenth of each burst vs the median tenth: a tail at
+        # the burst start (the API server's cores waking) or spread over it
+        "bind_api_us_first_tenth_vs_median_tenth": _first_vs_median(hops_by_decile(res.get("bind_hops_steps") or []),
+                                                                     "api"),
         "frag_pct": round(statistics.mean(f["frag_pct"] for f in fr), 3) if fr else None,
         "frag_hbm_pct": round(statistics.mean(f["frag_mib"] for f in fr), 3) if fr else None,
         "stranded_pct": round(statistics.mean(f["stranded_pct"] for f in fr), 3) if fr else None,
@@ -1725,6 +1729,13 @@ def hops_by_decile(steps: list) -> dict | None:
         return None
     return {name: [round(sum(r[h] for r in rows[dc]) / len(rows[dc]) / 1e3, 1) for dc in range(10)]
             for h, name in enumerate(BIND_HOPS)}
+
+
+def _first_vs_median(dec: dict | None, hop: str):
+    if not dec or hop not in dec:
+        return None
+    v = dec[hop]
+    return [v[0], sorted(v)[len(v) // 2]]
 
 
 def summarize(d: Dist, args, res: dict) -> dict:
