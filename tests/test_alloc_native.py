@@ -465,7 +465,7 @@ _share = st.tuples(st.sampled_from([5, 10, 25, 50, 100]), st.sampled_from([0, 0,
 
 
 @settings(max_examples=120, deadline=None)
-@given(st.lists(st.tuples(st.sampled_from(["reserve", "reserve", "reserve", "release", "hot", "health"]),
+@given(st.lists(st.tuples(st.sampled_from(["reserve", "reserve", "reserve", "release", "hot", "health", "reup"]),
                           _share, st.integers(0, 3), st.integers(0, 63)), min_size=5, max_size=80),
        st.lists(_share, min_size=1, max_size=4), st.sampled_from(["SPX", "CPX", "QPX"]),
        st.sampled_from([N.Policy.BINPACK, N.Policy.SPREAD]), st.booleans())
@@ -493,6 +493,8 @@ def test_memo_revalidation_agrees_with_a_fresh_choose(ops, probes, mode, policy,
                 L.set_mem_hot(nid, dev % len(t.devices), bool(k % 2))
             elif op == "health":
                 L.set_health(nid, dev % len(t.devices), dev % 5 != 0)
+            elif op == "reup":   # the node registered again (every device marked changed)
+                assert L.upsert_node(f"n{node}", t.ledger_devices(hbm), t.ledger_topo()) == nid
             for p in probes:
                 rcs, scores = L.assume_many(ids, [p], o)
                 dh = N.demand_hash([p])
