@@ -496,6 +496,16 @@ struct Frontend::VerbScratch {
   uint64_t opt_seen = 0;   // Frontend::opt_version_ of the copy below
   Options opt;
   bool normalize = false, nominate = false;
+  // A worker's verbs leave two pieces of work for after their answer is on the wire
+  // (Frontend::run_deferred, before the worker reads anything else): the pod cached for its bind
+  // (filter) and the priorities-time nomination. Neither changes the answer, and kube-scheduler's
+  // next request of the cycle no longer waits on them. Off for callers off the workers (tests,
+  // time_verb), which get the work done in the verb.
+  bool defer = false;
+  bool defer_put = false;
+  bool defer_nominate = false;
+  int32_t defer_node = -1;
+  Demand defer_dem{};
 };
 
 // ------------------------------------------------------------------------------ plumbing
@@ -597,6 +607,10 @@ Frontend::Frontend(std::shared_ptr<Ledger> ledger, const std::string& host, int 
   }
   for (int i = 0; i < threads; ++i) {
     auto w = std::make_unique<Worker>();
+    // the verbs' pod caching / nomination run after their answer (run_deferred);
+    // NANOGPU_FE_NO_DEFER=1 keeps them inside the verb (A/B measurements)
+    const char* nd = std::getenv("NANOGPU_FE_NO_DEFER");
+    w->scratch.defer = !(nd && nd[0] == '1');
     w->idx = i;
     w->lfd = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
     int one = 1;
@@ -1343,6 +1357,7 @@ void Frontend::process(Worker* w, Conn* c) {
       w->cycle_reply_ns = fast_ns();   // the scheduling cycle's next request is due: spin for it
       w->cycle_was_prio = prio;
       w->cycle_cid = id;
+      run_deferred(w->scratch);        // the answer is out: the pod cache / nomination now
       if (!w->conns.count(id)) return;
     } else {
       std::string m(method), pth(path), q(query), b(body);   // owned: the Python side keeps them
@@ -1448,6 +1463,31 @@ void Frontend::close_conn(Worker* w, Conn* c) {
 }
 
 // ------------------------------------------------------------------------------ verbs
+void Frontend::cache_pod(VerbScratch& s, std::string_view uid, const CachedPod& cached, std::string_view raw,
+                         const Demand& dem) {
+  if (ledger_->attached() > 1) {
+    // other worker processes share the ledger: the bind may reach one of them
+    std::string& blob = s.blob;
+    pack_pod(cached, dem, &blob);
+    if (ledger_->put_pod_info(uid, blob)) pods_published.fetch_add(1, std::memory_order_relaxed);
+  }
+  put_pod(uid, cached, raw, dem);
+}
+
+void Frontend::run_deferred(VerbScratch& s) {
+  if (!s.defer_put && !s.defer_nominate) return;
+  const LastPod& last = s.last;
+  if (s.defer_put) {
+    IoTimer it{kFeVerbCache};
+    cache_pod(s, last.uid, last.cached, last.raw, s.defer_dem);
+  }
+  if (s.defer_nominate) {
+    IoTimer it{kFeVerbNominate};
+    ledger_->nominate(s.defer_node, last.uid, s.defer_dem, s.opt);
+  }
+  s.defer_put = s.defer_nominate = false;
+}
+
 bool Frontend::handle_native(Worker* w, Conn* c, std::string_view method, std::string_view path,
                              std::string_view body, std::string* out) {
   (void)c;
@@ -1797,14 +1837,12 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   }
   if ((pod >= 0 || reused) && !uid.empty() && !(prioritize && has_pod(uid))) {
     // filter caches the pod for its bind; priorities of the same cycle find it there
-    const std::string_view raw = reused ? std::string_view(last.raw) : d.raw(pod);
-    if (ledger_->attached() > 1) {
-      // other worker processes share the ledger: the bind may reach one of them
-      std::string& blob = s.blob;
-      pack_pod(cached, dem, &blob);
-      if (ledger_->put_pod_info(uid, blob)) pods_published.fetch_add(1, std::memory_order_relaxed);
+    if (s.defer && last.valid && uid.data() == last.uid.data()) {
+      s.defer_put = true;   // the pod is last.raw / last.uid / last.cached: stable until the next request
+      s.defer_dem = dem;
+    } else {
+      cache_pod(s, uid, cached, reused ? std::string_view(last.raw) : d.raw(pod), dem);
     }
-    put_pod(uid, cached, raw, dem);
   }
   std::string& r = *out;
   r.reserve(64 + 128 * static_cast<size_t>(nn));   // room for a FailedNodes entry per node
@@ -1928,8 +1966,14 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     bool wants = false;
     for (int i = 0; i < dem.n; ++i) wants = wants || dem.c[i].pct > 0 || dem.c[i].mib > 0;
     if (wants) {
-      IoTimer it{kFeVerbNominate};
-      ledger_->nominate(ids[best], uid, dem, o);
+      if (s.defer && last.valid && uid.data() == last.uid.data()) {
+        s.defer_nominate = true;
+        s.defer_node = ids[best];
+        s.defer_dem = dem;
+      } else {
+        IoTimer it{kFeVerbNominate};
+        ledger_->nominate(ids[best], uid, dem, o);
+      }
       s.nom_dropped = false;
     }
   }
