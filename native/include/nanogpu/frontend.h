@@ -188,7 +188,7 @@ class Frontend {
   void close_conn(Worker* w, Conn* c);
   void put_pod(std::string_view uid, const CachedPod& meta, std::string_view raw, const Demand& dem);
   bool has_pod(std::string_view uid) const;
-  void prepare_bind(std::string_view body, PyRequest* r);
+  void prepare_bind(std::string_view body, PyRequest* r, VerbScratch& s);
   void cache_pod(VerbScratch& s, std::string_view uid, const CachedPod& cached, std::string_view raw, const Demand& dem);
   void run_deferred(VerbScratch& s);   // a worker verb's work left for after its answer went out
   void note_bind_wall(uint64_t ns);

@@ -888,14 +888,14 @@ void Frontend::put_pod(std::string_view uid, const CachedPod& meta, std::string_
   p.owner = meta.owner;
 }
 
-void Frontend::prepare_bind(std::string_view body, PyRequest* r) {
+void Frontend::prepare_bind(std::string_view body, PyRequest* r, VerbScratch& s) {
   thread_local json::Doc d;   // keeps its capacity across binds
   if (!d.parse(body) || !d.is(d.root(), json::Type::kObj)) return;
   auto str = [&](const char* k) -> std::string {
     const int32_t v = d.get(d.root(), k, true);
     return d.is(v, json::Type::kStr) ? std::string(d.str(v)) : std::string();
   };
-  const std::string uid = str("PodUID"), name = str("PodName"), node = str("Node");
+  std::string uid = str("PodUID"), name = str("PodName"), node = str("Node");
   std::string ns = str("PodNamespace");
   if (ns.empty()) ns = "default";
   if (uid.empty() || name.empty() || node.empty()) return;
@@ -933,11 +933,15 @@ void Frontend::prepare_bind(std::string_view body, PyRequest* r) {
     bind_handoffs.fetch_add(1, std::memory_order_relaxed);
     if (pod.name != name || pod.ns != ns || pod.completed || id < 0) return;   // Python reads the pod itself
   }
-  Options o;
-  {
+  // the options as of the last policy change this worker saw (as the verbs read them)
+  if (s.opt_seen != opt_version_.load(std::memory_order_acquire)) {
     std::lock_guard<std::mutex> g(opt_mu_);
-    o = opt_;
+    s.opt = opt_;
+    s.normalize = normalize_;
+    s.nominate = nominate_;
+    s.opt_seen = opt_version_.load(std::memory_order_relaxed);
   }
+  const Options& o = s.opt;
   const uint64_t t0 = fast_ns();
   Plan plan;
   std::memset(&plan, 0, sizeof(plan));
@@ -947,9 +951,9 @@ void Frontend::prepare_bind(std::string_view body, PyRequest* r) {
   bind_stats.observe(fast_ns() - t0);
   b.ok = true;
   b.ns = std::move(ns);
-  b.name = name;
-  b.uid = uid;
-  b.node = node;
+  b.name = std::move(name);
+  b.uid = std::move(uid);
+  b.node = std::move(node);
   b.containers = std::move(pod.containers);
   for (int c = 0; c < pod.demand.n; ++c) b.demand.emplace_back(pod.demand.c[c].pct, pod.demand.c[c].mib);
   if (b.rc == kOk || b.rc == kOkExisting)
@@ -1373,7 +1377,7 @@ void Frontend::defer(Worker* w, Conn* c, std::string method, std::string path, s
   if (method == "POST" && path == "/scheduler/bind" && serving()) {
     {
       IoTimer it{kFeParseBind};
-      prepare_bind(body, &r);
+      prepare_bind(body, &r, w->scratch);
     }
     KubeWriter* kw = writer_.load(std::memory_order_acquire);
     BindIo* bio = w->bio.load(std::memory_order_acquire);
