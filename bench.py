@@ -206,7 +206,19 @@ def launch_ranks(args) -> int:
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(args.gpus),
            "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve()), *sys.argv[1:]]
     print(f"bench: starting {args.gpus} ranks: {' '.join(cmd[1:8])} ...", file=sys.stderr, flush=True)
-    return subprocess.run(cmd, env=env).returncode
+    import signal
+
+    child = subprocess.Popen(cmd, env=env)
+
+    def forward(signum, _frame):   # a timeout's TERM (or ^C) reaches the ranks: no orphaned job
+        try:
+            child.send_signal(signum)
+        except OSError:
+            pass
+
+    for sig in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP):
+        signal.signal(sig, forward)
+    return child.wait()
 
 
 # --------------------------------------------------------------------------- distributed

@@ -326,3 +326,25 @@ def test_one_scheduler_over_four_workers_keeps_steady_churn_placement_quality(tm
         if d["frag_pct_steady"] <= d["frag_pct_steady_reference_model"]:
             break
     assert seen[-1][0] <= seen[-1][1], seen
+
+
+def test_launcher_forwards_a_term_to_its_ranks(tmp_path):
+    """A timeout that TERMs `python bench.py --gpus 2` must not orphan the rank job it started."""
+    import signal
+    import time
+
+    env = {k: v for k, v in os.environ.items() if k != "WORLD_SIZE"}
+    p = subprocess.Popen([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--no-gpu", "--steps", "50",
+                          "--warmup", "1", "--pods", "1000"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         env=env, cwd="/tmp", start_new_session=True)
+    try:
+        time.sleep(8)                      # the ranks are up (torch imported, extenders started)
+        p.send_signal(signal.SIGTERM)      # to the launcher only
+        p.wait(timeout=60)
+        time.sleep(2)
+        # nothing of the job is left in the launcher's session
+        left = subprocess.run(["pgrep", "-s", str(p.pid)], capture_output=True, text=True).stdout.split()
+        assert not left, left
+    finally:
+        if p.poll() is None:
+            os.killpg(p.pid, signal.SIGKILL)
