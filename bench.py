@@ -509,6 +509,9 @@ def node_template(d: Dist, args) -> tuple[object, dict]:
         info["link_bw_source"] = src
         if matrix is not None:
             info["link_bw_matrix_gbs"] = [[round(v, 1) for v in r] for r in matrix]
+            # the matrix goes to the diagnostics; its spread stays on the line
+            off = sorted(v for a, r in enumerate(matrix) for b, v in enumerate(r) if a != b)
+            info["link_bw_gbs_min_median_max"] = [round(off[0], 1), round(off[len(off) // 2], 1), round(off[-1], 1)]
         if d.dist is not None and d.cuda and "failed" not in src:
             # RCCL all-reduce busBW over all ranks: a collective aggregate, labelled as such;
             # time-boxed on a communicator of its own, the outcome agreed by every rank
