@@ -246,16 +246,7 @@ class Dist:
             import torch.distributed as dist
 
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            # gloo reports its connections on stdout ("[Gloo] Rank 0 is connected ..."): the job's
-            # stdout stays the one JSON line, so the group is set up with fd 1 pointed at stderr
-            sys.stdout.flush()
-            saved = os.dup(1)
-            os.dup2(2, 1)
-            try:
-                dist.init_process_group("nccl" if self.cuda else "gloo")
-            finally:
-                os.dup2(saved, 1)
-                os.close(saved)
+            dist.init_process_group("nccl" if self.cuda else "gloo")
             self.dist = dist
 
     def barrier(self):
@@ -1544,6 +1535,12 @@ def main() -> int:
     args = parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(args)
+    # stdout carries the one JSON line and nothing else: everything else this process and its
+    # children write there (gloo's connection reports on every group created, library chatter)
+    # goes to stderr; the line is written to the original stdout at the end
+    sys.stdout.flush()
+    line_fd = os.dup(1)
+    os.dup2(2, 1)
     cpus: list[int] = []
     rank_cpus: list[int] = []
     rank0_numa = -1
@@ -1672,7 +1669,7 @@ def main() -> int:
                                    variant, one_v, steady_v, nodes_v, inproc_v)
         # the driver keeps the last 8 KB of stdout: ONE compact line (< 4 KB) with the
         # headline keys last; the per-step diagnostics go to --json-out only
-        print(json.dumps(line), flush=True)
+        os.write(line_fd, (json.dumps(line) + "\n").encode())
         if args.json_out:
             Path(args.json_out).write_text(json.dumps({**line, "diagnostics": diag}, indent=1))
     d.close()
