@@ -1349,7 +1349,9 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     if rt.native is not None:
         ns = rt.native.fe.stats()
         results["native"] = {v: round(1e6 * ns[v]["seconds_total"] / max(1, ns[v]["count"]), 2)
-                             for v in ("filter", "priorities")}
+                             for v in ("filter", "priorities", "filter_wall", "priorities_wall")}
+        # priorities runs only when more than one node passed the filter
+        results["native"]["prio_per_filter"] = round(ns["priorities"]["count"] / max(1, ns["filter"]["count"]), 4)
     results["phase_ms"] = {k: round(statistics.mean(p[k] for p in results["phases"]), 2)
                            for k in ("create_ms", "schedule_ms", "release_ms", "create_srv_ms", "delete_srv_ms")
                            if all(k in p for p in results["phases"])} if results.get("phases") else None
@@ -1822,20 +1824,24 @@ def steady_keys(args, topo, v) -> dict:
     return keys
 
 
-def cycle_share(res: dict) -> tuple[float | None, float | None]:
+def cycle_share(res: dict) -> tuple[float | None, float | None, float | None]:
     """Who owns kube-scheduler's serial cycle (filter -> priorities -> host chosen), over the
     pass's timed steps: (share of the cycle the stand-in waited on the extender, request sent ->
-    answer read; share the extender's native verbs computed). The rest is the stand-in's own
-    work (node sampling, plugin scores, host selection) and the loopback round trips."""
+    answer read; share the extender held the requests, first byte read -> answer handed to the
+    kernel; share its native verbs computed, body parse -> answer built). wire - held is the
+    loopback transit plus the stand-in's own send / wake-up / recv; 1 - wire is the stand-in's
+    own work (node sampling, request building, plugin scores, host selection)."""
     steps = res.get("steps") or []
     cyc = sum(st.get("cycle_sum_ms", 0.0) for st in steps)
     wire = sum(st.get("cycle_wire_ms", 0.0) for st in steps)
     n = sum(st.get("cycles", 0) for st in steps)
     nat = res.get("native") or {}
     if cyc <= 0:
-        return None, None
-    verbs_ms = n * (nat.get("filter", 0.0) + nat.get("priorities", 0.0)) / 1e3
-    return round(wire / cyc, 3), round(verbs_ms / cyc, 3)
+        return None, None, None
+    pp = nat.get("prio_per_filter", 1.0)
+    verbs_ms = n * (nat.get("filter", 0.0) + pp * nat.get("priorities", 0.0)) / 1e3
+    held_ms = n * (nat.get("filter_wall", 0.0) + pp * nat.get("priorities_wall", 0.0)) / 1e3
+    return round(wire / cyc, 3), round(held_ms / cyc, 3), round(verbs_ms / cyc, 3)
 
 
 def nodes_variant_keys(args, topo, v) -> dict:
@@ -1858,7 +1864,8 @@ def nodes_variant_keys(args, topo, v) -> dict:
             f"schedulers_{tag}": "one kube-scheduler stand-in, binds over every rank's worker"
             if getattr(n_args, "one_scheduler", False) else "one kube-scheduler stand-in per rank",
             f"native_verb_mean_us_{tag}": res.get("native")}
-    keys[f"extender_share_of_cycle_{tag}"], keys[f"extender_verb_share_of_cycle_{tag}"] = cycle_share(res)
+    (keys[f"extender_share_of_cycle_{tag}"], keys[f"extender_held_share_of_cycle_{tag}"],
+     keys[f"extender_verb_share_of_cycle_{tag}"]) = cycle_share(res)
     st = res.get("steps") or []
     if st and sum(x.get("cycles", 0) for x in st):
         keys[f"cycle_us_{tag}"] = round(1e3 * sum(x.get("cycle_sum_ms", 0.0) for x in st)

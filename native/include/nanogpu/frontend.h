@@ -147,6 +147,8 @@ class Frontend {
   bool filter_verb(std::string_view body, bool prioritize, std::string* out, VerbScratch& s);
 
   VerbStats filter_stats, prio_stats, py_stats, bind_stats;   // bind_stats: native reserve half
+  // a native verb's residence: first request byte read -> whole answer handed to the kernel
+  VerbStats filter_wall_stats, prio_wall_stats;
   std::atomic<uint64_t> connections{0}, requests{0};
   std::atomic<uint64_t> spin_hits{0};     // event batches a busy-polling worker caught
   std::atomic<uint64_t> mb_wakeups{0};    // posted responses that had to wake a parked worker

@@ -936,6 +936,8 @@ PYBIND11_MODULE(_native, m) {
         py::dict d;
         d["filter"] = one(f.filter_stats);
         d["priorities"] = one(f.prio_stats);
+        d["filter_wall"] = one(f.filter_wall_stats);
+        d["priorities_wall"] = one(f.prio_wall_stats);
         d["python"] = one(f.py_stats);
         d["bind_reserve"] = one(f.bind_stats);
         d["connections"] = f.connections.load();

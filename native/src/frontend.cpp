@@ -416,7 +416,8 @@ std::vector<std::array<uint32_t, 6>> Frontend::take_bind_hops() {
 }
 
 void Frontend::reset_max() {
-  for (VerbStats* v : {&filter_stats, &prio_stats, &py_stats, &bind_stats}) v->max_ns.store(0);
+  for (VerbStats* v : {&filter_stats, &prio_stats, &py_stats, &bind_stats, &filter_wall_stats, &prio_wall_stats})
+    v->max_ns.store(0);
   loop_max_ns.store(0);
   for (auto& p : phase_max_ns) p.store(0);
 }
@@ -1356,9 +1357,12 @@ void Frontend::process(Worker* w, Conn* c) {
     }
     const bool prio = path == "/scheduler/priorities";   // `path` views c->in, erased below
     if (handle_native(w, c, method, path, body, &c->out)) {   // the answer lands in c->out
+      const uint64_t t_in = c->t_in_ns;
       c->in.erase(0, consumed);
+      if (!c->in.empty()) c->t_in_ns = fast_ns();   // a pipelined request behind it: its own clock
       flush(w, c, kFeSendCycle);
       w->cycle_reply_ns = fast_ns();   // the scheduling cycle's next request is due: spin for it
+      if (t_in) (prio ? prio_wall_stats : filter_wall_stats).observe(w->cycle_reply_ns - t_in);
       w->cycle_was_prio = prio;
       w->cycle_cid = id;
       run_deferred(w->scratch);        // the answer is out: the pod cache / nomination now
