@@ -166,6 +166,9 @@ def parse_args():
                     help="the extender's front door sleeps its busy-poll window instead of polling it")
     ap.add_argument("--bind-first", action="store_true",
                     help="the extender's front door reserves a batch's binds before its filters")
+    ap.add_argument("--one-loop", action="store_true",
+                    help="run the harness's step driving on the extender's asyncio loop (its CPU then "
+                         "bracketed and subtracted) instead of giving the extender a loop thread of its own")
     ap.add_argument("--no-relocate", action="store_true",
                     help="keep the rank on the L3 domain picked at start even when other tenants load it "
                          "(by default a busy domain is left for a quieter one after the warm-up, and during "
@@ -342,6 +345,14 @@ class StallSampler:
         Path(path).write_text(json.dumps(out, indent=1))
 
 
+def _thread_group(is_main: bool, comm: str) -> str:
+    if is_main:
+        return "main"
+    if comm.startswith("ngpu-"):
+        return comm.rstrip("0123456789")
+    return "bench-harness" if comm.startswith("bench-") else "other"
+
+
 def thread_ticks() -> dict[str, list[int]]:
     """[user, kernel] clock ticks of this process's threads by group (thread_cpu's groups),
     from /proc/self/task/*/stat utime and stime: what share of each group's CPU is kernel
@@ -360,8 +371,7 @@ def thread_ticks() -> dict[str, list[int]]:
             continue
         comm = st[st.index("(") + 1:st.rindex(")")]
         fields = st[st.rindex(")") + 2:].split()
-        group = "main" if tid == str(pid) else comm.rstrip("0123456789") if comm.startswith("ngpu-") else "other"
-        acc = out.setdefault(group, [0, 0])
+        acc = out.setdefault(_thread_group(tid == str(pid), comm), [0, 0])
         acc[0] += int(fields[11])
         acc[1] += int(fields[12])
     return out
@@ -394,12 +404,7 @@ def thread_cpu() -> dict[str, float]:
                 cpu = (int(fields[11]) + int(fields[12])) / hz
         except (OSError, ValueError):
             continue
-        if tid == str(pid):
-            group = "main"
-        elif comm.startswith("ngpu-"):
-            group = comm.rstrip("0123456789")
-        else:
-            group = "other"
+        group = _thread_group(tid == str(pid), comm)
         out[group] = out.get(group, 0.0) + cpu
     return out
 
@@ -712,6 +717,50 @@ class HarnessCpu:
         return False
 
 
+def set_thread_comm(name: str) -> None:
+    """Names the calling OS thread (/proc/self/task/<tid>/comm, 15 bytes): thread_cpu() groups
+    the process's CPU by these names."""
+    import ctypes
+
+    try:
+        ctypes.CDLL(None, use_errno=True).prctl(15, name.encode()[:15], 0, 0, 0)   # PR_SET_NAME
+    except (OSError, AttributeError):
+        pass
+
+
+class ExtenderLoop:
+    """The extender's asyncio loop on a thread of its own ("ngpu-loop"), as in a deployment,
+    where `python -m nanogpu` runs nothing else on it: the harness drives the steps from the
+    main thread, so the extender's CPU a pod is its own threads' CPU, measured, instead of the
+    main thread's minus the harness parts that can be bracketed."""
+
+    def __init__(self):
+        import threading
+
+        self.loop = asyncio.new_event_loop()
+        started = threading.Event()
+
+        def run():
+            set_thread_comm("ngpu-loop")
+            asyncio.set_event_loop(self.loop)
+            started.set()
+            self.loop.run_forever()
+
+        self.th = threading.Thread(target=run, name="ngpu-loop", daemon=True)
+        self.th.start()
+        started.wait()
+
+    async def run(self, coro):
+        """Awaits `coro` run on the extender's loop."""
+        return await asyncio.wrap_future(asyncio.run_coroutine_threadsafe(coro, self.loop))
+
+    def close(self) -> None:
+        self.loop.call_soon_threadsafe(self.loop.stop)
+        self.th.join(10.0)
+        if not self.th.is_alive():
+            self.loop.close()
+
+
 async def arecv(conn, hc: HarnessCpu | None = None):
     """conn.recv() awaited on the event loop (the pipe's fd in the selector): no executor
     thread, whose start can wait milliseconds for the GIL while the loop is busy."""
@@ -920,6 +969,19 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     # rank's pods. Without it each rank has an in-process store of its own (extender-isolated).
     shared = not getattr(args, "inproc_api", False) and conn is not None and (api_proc is not None or d.rank != 0)
     loop = asyncio.get_running_loop()
+    # with the API server in its own process nothing the harness touches lives on the
+    # extender's loop: the extender gets a loop thread of its own (the in-process store's
+    # watches do, so that pass keeps one loop and brackets the harness's CPU instead)
+    ext = ExtenderLoop() if shared and not getattr(args, "one_loop", False) else None
+    if ext is not None:
+        from concurrent.futures import ThreadPoolExecutor
+
+        # the harness's executor threads (barriers, release polls) named as the harness's
+        loop.set_default_executor(ThreadPoolExecutor(4, initializer=set_thread_comm,
+                                                     initargs=("bench-harness",)))
+
+    async def on_ext(coro):
+        return await (ext.run(coro) if ext is not None else coro)
 
     async def barrier() -> None:
         if shared:   # keep the loop turning (watch, controller) while other ranks catch up
@@ -944,14 +1006,18 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         url = d.bcast_obj(url)
         from nanogpu.k8s.client import KubeClient, KubeConfig
 
-        rt_api = KubeClient(KubeConfig(server=url), pool=args.inflight_binds + 8,
-                            native_watch=not args.no_native_pod_watch)
+        def rt_api_make():
+            return KubeClient(KubeConfig(server=url), pool=args.inflight_binds + 8,
+                              native_watch=not args.no_native_pod_watch)
     else:
         # the watch history a real API server keeps is a bounded cache, and not in our process
         store = FakeKubeStore(history=8192, faults=Faults(latency_s=args.api_rtt_ms / 1e3))
         for n in nodes:
             store.add_node(n)
         rt_api = InProcKube(store)
+
+        def rt_api_make():
+            return rt_api
     cfg = Config(port=0, host="127.0.0.1", priority=args.policy, compat=args.compat, ledger_path=ledger_path,
                  max_nodes=max(1024, args.nodes), max_pods=max(65536, 4 * args.pods),
                  policy_config_path="/nonexistent/policy.yaml", reservation_ttl_s=3600,
@@ -962,8 +1028,13 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                  bind_writer_mode=args.bind_writer_mode, assume_label=not args.no_assume_label,
                  bind_first=args.bind_first, spin_nap=args.spin_nap, spin_recv=args.spin_recv, spin_recv_binds=args.spin_recv_binds, batch_labels=args.batch_labels)
     all_steps_pre = [10_000 + w for w in range(args.warmup)] + list(range(args.steps))
-    rt = Runtime(cfg, worker=d.rank if shared else 0, api=rt_api)
-    await rt.start()
+
+    async def start_runtime():   # built and started on the extender's loop
+        r = Runtime(cfg, worker=d.rank if shared else 0, api=rt_api_make())
+        await r.start()
+        return r
+
+    rt = await on_ext(start_runtime())
     client = FastExtenderClient("127.0.0.1", rt.bound_port, pool=args.inflight_binds + 8)
     names = [pu.meta(n)["name"] for n in nodes]
     caps = node_capacities(nodes)
@@ -1131,7 +1202,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         await wait_released(rt.state.ledger.lookup, uids)
         t_rel = time.perf_counter()
         if pod_ctrl is not None:
-            await pod_ctrl.queue.drain(5.0)
+            await on_ext(pod_ctrl.queue.drain(5.0))
         srv_ms.setdefault(step, {})["drain_ms"] = 1e3 * (time.perf_counter() - t_rel)
         if os.environ.get("NANOGPU_BENCH_DEBUG"):
             print(f"step {step} start {t_step0:.4f} release {ts:.4f} end {time.perf_counter():.4f}", file=sys.stderr)
@@ -1321,16 +1392,26 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     results["nodes_sent_per_filter"] = (round(sum(st.get("nodes_sent_filter", 0) for st in results["steps"]) / cycles, 1)
                                         if cycles else None)
     n_sched = max(1, sum(st["scheduled"] for st in results["steps"]))
-    harness_s = hc.s
-    results["cpu_us_per_pod"] = 1e6 * (time.process_time() - cpu0 - harness_s) / n_sched
+    cpu1, loop_cpu1 = time.process_time(), time.thread_time()
+    threads1, ticks1, times1 = thread_cpu(), thread_ticks(), os.times()
+    dthr = {g: threads1[g] - threads0.get(g, 0.0) for g in threads1}
+    if ext is not None:
+        # the main thread and its executor threads are the harness's alone; the extender's
+        # Python loop is the "ngpu-loop" thread
+        harness_s = dthr.pop("main", 0.0) + dthr.pop("bench-harness", 0.0)
+        dthr["main"] = dthr.pop("ngpu-loop", 0.0)
+        loop_s = dthr["main"]
+    else:
+        harness_s = hc.s
+        dthr["main"] = dthr.get("main", 0.0) - harness_s
+        loop_s = loop_cpu1 - loop_cpu0 - harness_s
+    results["cpu_us_per_pod"] = 1e6 * (cpu1 - cpu0 - harness_s) / n_sched
     if "io_tally" in results:   # (calls, s) by call site -> calls a pod, us a pod, ns a call
         results["io_per_pod"] = {k: [round(n / n_sched, 3), round(1e6 * sec / n_sched, 2), round(1e9 * sec / max(1, n))]
                                  for k, (n, sec) in sorted(results.pop("io_tally").items())}
     results["harness_cpu_us_per_pod"] = 1e6 * harness_s / n_sched
-    threads1, ticks1, times1 = thread_cpu(), thread_ticks(), os.times()
-    results["cpu_us_per_pod_by_thread"] = {g: round(1e6 * (threads1[g] - threads0.get(g, 0.0)
-                                                           - (harness_s if g == "main" else 0.0)) / n_sched, 1)
-                                           for g in sorted(threads1)}
+    results["extender_loop_thread"] = ext is not None
+    results["cpu_us_per_pod_by_thread"] = {g: round(1e6 * dthr[g] / n_sched, 1) for g in sorted(dthr)}
     # user / kernel split (10 ms ticks: about 1 % resolution over a 20-step run)
     results["cpu_us_per_pod_user_kernel"] = [round(1e6 * (times1.user - times0.user) / n_sched, 1),
                                              round(1e6 * (times1.system - times0.system) / n_sched, 1)]
@@ -1339,8 +1420,13 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         u0, k0 = ticks0.get(g, [0, 0])
         if (u1 - u0) + (k1 - k0) >= 5:
             kshare[g] = round(100.0 * (k1 - k0) / ((u1 - u0) + (k1 - k0)), 1)
+    if ext is not None:   # the extender's Python loop reported as "main", as without the split
+        kshare.pop("main", None)
+        kshare.pop("bench-harness", None)
+        if "ngpu-loop" in kshare:
+            kshare["main"] = kshare.pop("ngpu-loop")
     results["kernel_pct_by_thread"] = kshare
-    results["loop_cpu_us_per_pod"] = 1e6 * (time.thread_time() - loop_cpu0 - harness_s) / n_sched
+    results["loop_cpu_us_per_pod"] = 1e6 * loop_s / n_sched
     # the Python part of each bind (API writes + commit): a sub-phase of the wall time
     binds = sorted(s["dur_ms"] for s in rt.tracer.dump(10 ** 9, "bind") if s["ok"])
     results["elapsed_s"] = elapsed
@@ -1364,7 +1450,9 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     if apisrv is not None:
         results["apiserver"] = apisrv.stats()
     await barrier()          # no rank still talks to the shared API server
-    await rt.stop()
+    await on_ext(rt.stop())
+    if ext is not None:
+        ext.close()
     if apisrv is not None:
         apisrv.end()
     return results
@@ -1621,7 +1709,8 @@ def main() -> int:
                 one_v = summarize(d, o_args, run_pass(d, o_args, topo, conn, "one", api_proc))
             except Exception as e:
                 one_v = {"error": f"{type(e).__name__}: {e}"}
-        if args.nodes_variant > 0 and args.nodes_variant != args.nodes and not args.steady and shared_api:
+        if (args.nodes_variant > 0 and args.nodes_variant_steps > 0 and args.nodes_variant != args.nodes
+                and not args.steady and shared_api):
             # a large cluster behind kube-scheduler's node sampling: the extender sees only the
             # share of feasible nodes numFeasibleNodesToFind lets through, from a rotating start
             nv_pods = args.nodes_variant_pods or round(args.pods * args.nodes_variant / max(1, args.nodes))
