@@ -71,6 +71,11 @@ def parse_args():
     ap.add_argument("--rtt-variant-ms", type=float, default=2.0,
                     help="after the timed steps, a second pass with this API round trip (0: none)")
     ap.add_argument("--rtt-variant-steps", type=int, default=3)
+    ap.add_argument("--decisive-filter", action="store_true",
+                    help="the extender's filter answers only the node priorities would rank first (one "
+                         "round trip a pod; nanogpu --decisive-filter)")
+    ap.add_argument("--decisive-variant-steps", type=int, default=5,
+                    help="after the timed steps, a pass with --decisive-filter (0: none)")
     ap.add_argument("--inproc-api", action="store_true",
                     help="each rank gets an in-process API store of its own (round 1's extender-isolated "
                          "setup) instead of the default: ONE API server for the whole job over HTTP (the "
@@ -1026,7 +1031,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                  nominate=not args.no_nominate,
                  bind_writer_threads=args.bind_writer_threads or max(2, 16 // d.world),
                  bind_writer_mode=args.bind_writer_mode, assume_label=not args.no_assume_label,
-                 bind_first=args.bind_first, spin_nap=args.spin_nap, spin_recv=args.spin_recv, spin_recv_binds=args.spin_recv_binds, batch_labels=args.batch_labels)
+                 bind_first=args.bind_first, spin_nap=args.spin_nap, spin_recv=args.spin_recv, spin_recv_binds=args.spin_recv_binds, batch_labels=args.batch_labels,
+                 decisive_filter=getattr(args, "decisive_filter", False))
     all_steps_pre = [10_000 + w for w in range(args.warmup)] + list(range(args.steps))
 
     async def start_runtime():   # built and started on the extender's loop
@@ -1309,6 +1315,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     fe_stats = rt.native.fe.stats if rt.native is not None else (lambda: {})
     handoffs0 = fe_stats().get("bind_handoffs", 0)
     py0 = fe_stats().get("python", {}).get("count", 0)
+    prio0 = fe_stats().get("priorities", {}).get("count", 0)
     hc.s = 0.0
     cpu0, loop_cpu0 = time.process_time(), time.thread_time()
     threads0, ticks0, times0 = thread_cpu(), thread_ticks(), os.times()
@@ -1437,6 +1444,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         results["native"] = {v: round(1e6 * ns[v]["seconds_total"] / max(1, ns[v]["count"]), 2)
                              for v in ("filter", "priorities", "filter_wall", "priorities_wall")}
         # priorities runs only when more than one node passed the filter
+        results["prio_per_pod"] = round((ns["priorities"]["count"] - prio0) / max(1, results["scheduled"]), 3)
         results["native"]["prio_per_filter"] = round(ns["priorities"]["count"] / max(1, ns["filter"]["count"]), 4)
     results["phase_ms"] = {k: round(statistics.mean(p[k] for p in results["phases"]), 2)
                            for k in ("create_ms", "schedule_ms", "release_ms", "create_srv_ms", "delete_srv_ms")
@@ -1502,7 +1510,7 @@ def order_line(full: dict) -> tuple[dict, dict]:
 
 
 def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc, gpu_info: dict, topo,
-                  variant, one_v, steady_v, nodes_v, inproc_v) -> tuple[dict, dict]:
+                  variant, one_v, steady_v, nodes_v, inproc_v, dec_v=None) -> tuple[dict, dict]:
     from nanogpu import affinity
 
     fr = res["frag"]
@@ -1611,6 +1619,18 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
             full["steps_independent_schedulers"] = args.independent_variant_steps
     full.update(steady_keys(args, topo, steady_v))
     full.update(nodes_variant_keys(args, topo, nodes_v))
+    if dec_v is not None:
+        # the same bursts with the decisive filter (kube-scheduler left one feasible node: no
+        # scoring, no priorities call); its own score plugins have no say in this mode
+        if "error" in dec_v:
+            full["value_decisive_filter"] = None
+            full["error_decisive_filter"] = dec_v["error"]
+        else:
+            dres, dout = dec_v["res"], dec_v["out"]
+            full["value_decisive_filter"] = dout["value"]
+            full["p50_bind_ms_decisive_filter"] = dout["p50_bind_ms"]
+            full["frag_pct_decisive_filter"] = _frag_mean(dres["frag"])
+            full["priorities_calls_per_pod_decisive_filter"] = dres.get("prio_per_pod")
     if inproc_v is not None:
         if "error" in inproc_v:
             full["value_inproc_api"] = None
@@ -1681,7 +1701,7 @@ def main() -> int:
     # the deployment that exists: one active kube-scheduler in front of every extender worker
     args.one_scheduler = d.world > 1 and not args.independent_schedulers
     topo, gpu_info = node_template(d, args)
-    variant = inproc_v = steady_v = nodes_v = one_v = None
+    variant = inproc_v = steady_v = nodes_v = one_v = dec_v = None
     try:
         args._headline = True    # the native CPU profile covers this pass only
         res = run_pass(d, args, topo, conn, "main", api_proc)
@@ -1732,6 +1752,15 @@ def main() -> int:
                 variant = summarize(d, v_args, run_pass(d, v_args, topo, conn, "rtt", api_proc))
             except Exception as e:   # the headline result stands; say what failed
                 variant = {"error": f"{type(e).__name__}: {e}"}
+        if args.decisive_variant_steps > 0 and not args.decisive_filter and not args.steady and not args.compat:
+            x_args = argparse.Namespace(**{**vars(args), "decisive_filter": True,
+                                           "steps": args.decisive_variant_steps, "warmup": 1,
+                                           "profile_out": "", "stall_trace": "", "api_rtt_ms": 0.0})
+            try:
+                r = run_pass(d, x_args, topo, conn, "decisive", api_proc)
+                dec_v = {"res": r, "out": summarize(d, x_args, r)}
+            except Exception as e:
+                dec_v = {"error": f"{type(e).__name__}: {e}"}
         if args.inproc_variant_steps > 0 and not args.inproc_api and not args.inproc_driver:
             # round 1's extender-isolated setup: an in-process store per rank, no HTTP
             # (each rank its own store: a stand-in per rank, each binding on its own worker)
@@ -1757,7 +1786,7 @@ def main() -> int:
     if d.rank == 0:
         final_cpus = args._placement["cpus"] if getattr(args, "_placement", None) else cpus
         line, diag = headline_line(d, args, res, out, final_cpus, api_proc, gpu_info, topo,
-                                   variant, one_v, steady_v, nodes_v, inproc_v)
+                                   variant, one_v, steady_v, nodes_v, inproc_v, dec_v)
         # the driver keeps the last 8 KB of stdout: ONE compact line (< 4 KB) with the
         # headline keys last; the per-step diagnostics go to --json-out only
         os.write(line_fd, (json.dumps(line) + "\n").encode())

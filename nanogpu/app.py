@@ -64,6 +64,7 @@ class Config:
     api_write_timeout_s: float = 30.0           # native bind writer: an API answer due within this
     reservation_ttl_s: float = 60.0
     nominate: bool = True              # priorities nominate the top node (Ledger::nominate)
+    decisive_filter: bool = False      # filter answers only the top node (one round trip a pod)
     nomination_ttl_s: float = 5.0
     policy_reload_s: float = 3.0
     fake_cluster: int = 0                       # >0: serve against an in-process fake cluster of N nodes
@@ -106,7 +107,7 @@ class Runtime:
             topo_weight=cfg.topology_weight, seed=cfg.seed, ledger_path=cfg.ledger_path,
             max_nodes=cfg.max_nodes, max_pods=cfg.max_pods, track_hbm=cfg.track_hbm,
             node_source=self._node_from_cache, score_normalize=cfg.score_normalize, nominate=cfg.nominate,
-            request_sizes=cfg.request_sizes, learn_sizes=cfg.learn_sizes)
+            request_sizes=cfg.request_sizes, learn_sizes=cfg.learn_sizes, decisive_filter=cfg.decisive_filter)
         self.metrics = Metrics()
         self.tracer = Tracer()
         self.extender: Extender | None = None

@@ -60,9 +60,10 @@ class ClusterState:
                  ledger_path: str = "", max_nodes: int = 4096, max_pods: int = 131072,
                  track_hbm: bool = True, node_source: Callable[[str], dict | None] | None = None,
                  score_normalize: bool = False, nominate: bool = True, request_sizes: list[int] | None = None,
-                 learn_sizes: bool = True):
+                 learn_sizes: bool = True, decisive_filter: bool = False):
         self.ledger = N.Ledger(ledger_path, max_nodes, max_pods, True)
         self._nominate = bool(nominate)
+        self._decisive = bool(decisive_filter)
         self.track_hbm = track_hbm
         self._listeners: list[Callable[[], None]] = []
         self._score_normalize = bool(score_normalize)
@@ -108,6 +109,20 @@ class ClusterState:
     @nominate.setter
     def nominate(self, v: bool) -> None:
         self._nominate = bool(v)
+        self._changed()
+
+    @property
+    def decisive_filter(self) -> bool:
+        """Filter answers only the node priorities would rank first (and nominates it), so
+        kube-scheduler, left one feasible node, skips scoring and the priorities call: one
+        round trip a pod instead of two. Its own score plugins then have no say. Off in compat
+        mode and for wide pods. Off by default (the reference's filter answers every fitting
+        node)."""
+        return self._decisive and not self.options.compat
+
+    @decisive_filter.setter
+    def decisive_filter(self, v: bool) -> None:
+        self._decisive = bool(v)
         self._changed()
 
     def set_policy(self, policy: str, compat: bool | None = None, load_aware: bool | None = None,
@@ -239,8 +254,16 @@ class ClusterState:
         demand, _ = pu.ledger_view(full)
         ids = self.node_ids(node_names)
         rcs = self.ledger.filter(ids, demand, self.options)
+        if self.decisive_filter and any(rc == N.OK for rc in rcs):
+            scores = self.ledger.score(ids, demand, self.options)
+            pick = self._top_pick(pu.pod_uid(pod), scores, rcs)
+            if self.nominate and pu.pod_uid(pod) and any(p > 0 or m > 0 for p, m in demand):
+                self.ledger.nominate(ids[pick], pu.pod_uid(pod), demand, self.options)
+            rcs = [rc if rc != N.OK or k == pick else None for k, rc in enumerate(rcs)]
         ok, failed = [], {}
         for name, nid, rc in zip(node_names, ids, rcs):
+            if rc is None:    # fits, not the decisive pick: neither answered nor failed
+                continue
             if rc == N.OK:
                 ok.append(name)
             elif nid < 0:
@@ -271,6 +294,15 @@ class ClusterState:
         uid = pu.pod_uid(pod)
         if uid:
             self.ledger.drop_nomination(uid)
+
+    @staticmethod
+    def _top_pick(uid: str, scores: list[int], rcs: list[int]) -> int:
+        """frontend.cpp top_pick: the fitting node with the top score; a tie goes to the tied
+        node (in the request's order) the pod's UID hash picks."""
+        cand = [k for k, rc in enumerate(rcs) if rc == N.OK]
+        best = max(scores[k] for k in cand)
+        top = [k for k in cand if scores[k] == best]
+        return top[N.Ledger.owner_hash(uid) % len(top)] if len(top) > 1 and uid else top[0]
 
     def _nominate_best(self, pod: dict, demand, ids: list[int], scores: list[int]) -> list[int]:
         """Same rule as the native front door (frontend.cpp, priorities): a unique best fitting

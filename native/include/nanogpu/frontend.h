@@ -93,7 +93,10 @@ class Frontend {
   int notify_fd() const { return py_efd_; }
   // nominate: priorities tentatively reserve the pod on its unique top-scored node
   // (Ledger::nominate) so the next pods' filters see it before the bind arrives.
-  void set_options(const Options& o, bool score_normalize, bool nominate = false);
+  // decisive: filter answers the one node priorities would rank first (ties broken by the pod's
+  // UID hash, as priorities breaks them) and nominates it; kube-scheduler skips scoring for a
+  // single feasible node, so a pod's cycle is one round trip (off: the reference's filter)
+  void set_options(const Options& o, bool score_normalize, bool nominate = false, bool decisive = false);
   // false: every request goes to Python (a standby replica answers 503 from there).
   void set_serving(bool on) { serving_.store(on, std::memory_order_release); }
   // this process's switch AND the replica's shared flag in the ledger (leader election runs
@@ -221,6 +224,7 @@ class Frontend {
   std::atomic<uint64_t> opt_version_{1};   // bumped by every set_options (workers re-copy then)
   bool normalize_ = false;
   bool nominate_ = false;
+  bool decisive_ = false;
 
   std::mutex py_mu_;
   std::deque<PyRequest> py_q_;

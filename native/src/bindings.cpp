@@ -807,7 +807,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("port", &Frontend::port)
       .def("notify_fd", &Frontend::notify_fd)
       .def("set_options", &Frontend::set_options, py::arg("options"), py::arg("score_normalize") = false,
-           py::arg("nominate") = false)
+           py::arg("nominate") = false, py::arg("decisive") = false)
       .def("set_serving", &Frontend::set_serving)
       .def("set_busy_poll_us", &Frontend::set_busy_poll_us)
       .def("set_busy_poll_prio_us", &Frontend::set_busy_poll_prio_us)

@@ -371,6 +371,35 @@ struct NameTable {
 };
 }  // namespace
 
+// The fitting node with the top score; a tie at the top goes to the tied node (in the
+// request's order) the pod's UID hash picks: as even over the tied nodes as kube-scheduler's
+// random pick among equal scores, but the same on every worker. -1: nothing fits.
+static int64_t top_pick(const std::vector<int32_t>& scores, const std::vector<int32_t>& rcs, std::string_view uid) {
+  int64_t best = -1;
+  uint64_t n_best = 0;
+  for (size_t i = 0; i < scores.size(); ++i) {
+    if (rcs[i] != kOk) continue;
+    if (best < 0 || scores[i] > scores[best]) {
+      best = static_cast<int64_t>(i);
+      n_best = 1;
+    } else if (scores[i] == scores[best]) {
+      ++n_best;
+    }
+  }
+  if (n_best < 2 || uid.empty()) return best;
+  uint64_t k = owner_hash(uid) % n_best;
+  const int32_t top = scores[best];
+  for (size_t i = static_cast<size_t>(best); i < scores.size(); ++i)
+    if (rcs[i] == kOk && scores[i] == top && k-- == 0) return static_cast<int64_t>(i);
+  return best;
+}
+
+static bool wants_devices(const Demand& d) {
+  for (int i = 0; i < d.n; ++i)
+    if (d.c[i].pct > 0 || d.c[i].mib > 0) return true;
+  return false;
+}
+
 static void atomic_max(std::atomic<uint64_t>* m, uint64_t v) {
   uint64_t cur = m->load(std::memory_order_relaxed);
   while (v > cur && !m->compare_exchange_weak(cur, v, std::memory_order_relaxed)) {
@@ -496,13 +525,14 @@ struct Frontend::VerbScratch {
   uint64_t nom_mark = 0;      // ... when Ledger::nominations_made() read this
   uint64_t opt_seen = 0;   // Frontend::opt_version_ of the copy below
   Options opt;
-  bool normalize = false, nominate = false;
+  bool normalize = false, nominate = false, decisive = false;
   // A worker's verbs leave two pieces of work for after their answer is on the wire
   // (Frontend::run_deferred, before the worker reads anything else): the pod cached for its bind
   // (filter) and the priorities-time nomination. Neither changes the answer, and kube-scheduler's
   // next request of the cycle no longer waits on them. Off for callers off the workers (tests,
   // time_verb), which get the work done in the verb.
   bool defer = false;
+  bool defer_cache = false;   // the pod-cache put too: only with one worker thread (see filter_verb)
   bool defer_put = false;
   bool defer_nominate = false;
   int32_t defer_node = -1;
@@ -612,6 +642,7 @@ Frontend::Frontend(std::shared_ptr<Ledger> ledger, const std::string& host, int 
     // NANOGPU_FE_NO_DEFER=1 keeps them inside the verb (A/B measurements)
     const char* nd = std::getenv("NANOGPU_FE_NO_DEFER");
     w->scratch.defer = !(nd && nd[0] == '1');
+    w->scratch.defer_cache = w->scratch.defer && threads == 1;
     w->idx = i;
     w->lfd = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
     int one = 1;
@@ -696,12 +727,13 @@ void Frontend::stop() {
   py_efd_ = -1;
 }
 
-void Frontend::set_options(const Options& o, bool score_normalize, bool nominate) {
+void Frontend::set_options(const Options& o, bool score_normalize, bool nominate, bool decisive) {
   std::lock_guard<std::mutex> g(opt_mu_);
   opt_version_.fetch_add(1, std::memory_order_release);
   opt_ = o;
   normalize_ = score_normalize;
   nominate_ = nominate;
+  decisive_ = decisive;
 }
 
 std::vector<PyRequest> Frontend::take() {
@@ -940,6 +972,7 @@ void Frontend::prepare_bind(std::string_view body, PyRequest* r, VerbScratch& s)
     s.opt = opt_;
     s.normalize = normalize_;
     s.nominate = nominate_;
+    s.decisive = decisive_;
     s.opt_seen = opt_version_.load(std::memory_order_relaxed);
   }
   const Options& o = s.opt;
@@ -1828,10 +1861,11 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     s.opt = opt_;
     s.normalize = normalize_;
     s.nominate = nominate_;
+    s.decisive = decisive_;
     s.opt_seen = opt_version_.load(std::memory_order_relaxed);
   }
   const Options& o = s.opt;
-  const bool normalize = s.normalize, nominate = s.nominate;
+  const bool normalize = s.normalize, nominate = s.nominate, decisive = s.decisive && !o.compat;
   io_end(kFeVerbNames, io0);
   io0 = io_t0();
   // not against itself; priorities right behind this worker's filter of the same pod text
@@ -1844,8 +1878,11 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     s.nom_dropped = reused || (pod >= 0 && last.valid);   // about the pod `last` holds
   }
   if ((pod >= 0 || reused) && !uid.empty() && !(prioritize && has_pod(uid))) {
-    // filter caches the pod for its bind; priorities of the same cycle find it there
-    if (s.defer && last.valid && uid.data() == last.uid.data()) {
+    // filter caches the pod for its bind; priorities of the same cycle find it there. After
+    // the answer only when no other worker can read the bind first: kube-scheduler sends it
+    // on another connection, which another thread or worker process may serve (a miss there
+    // goes to the Python path); a late nomination is harmless (a reserved pod ignores it)
+    if (s.defer_cache && ledger_->attached() <= 1 && last.valid && uid.data() == last.uid.data()) {
       s.defer_put = true;   // the pod is last.raw / last.uid / last.cached: stable until the next request
       s.defer_dem = dem;
     } else {
@@ -1862,13 +1899,30 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
       IoTimer it{kFeVerbAssume};
       ledger_->assume_many(ids.data(), static_cast<int>(ids.size()), dem, o, rcs.data(), scores.data());
     }
+    // decisive: the node priorities would rank first is the only one answered (and nominated)
+    const int64_t pick = decisive ? top_pick(scores, rcs, uid) : -1;
+    if (pick >= 0 && nominate && !uid.empty() && wants_devices(dem)) {
+      if (s.defer && last.valid && uid.data() == last.uid.data()) {
+        s.defer_nominate = true;
+        s.defer_node = ids[pick];
+        s.defer_dem = dem;
+      } else {
+        IoTimer it{kFeVerbNominate};
+        ledger_->nominate(ids[pick], uid, dem, o);
+      }
+      s.nom_dropped = false;
+    }
     // written straight into the reply; a fitting node's name is its request token, as is
     r.clear();
     r += "{\"Nodes\":null,\"NodeNames\":";
     bool any_failed = false;
     for (size_t i = 0; i < ids.size() && !any_failed; ++i) any_failed = rcs[i] != kOk;
     bool first = true;
-    if (!any_failed && toks && idc.compact[slot]) {
+    if (pick >= 0) {
+      r += '[';
+      r += raw_at(static_cast<size_t>(pick));
+      r += ']';
+    } else if (!any_failed && toks && idc.compact[slot]) {
       r += raw_names;   // every node fits: the request's own list is the answer
     } else {
       r += '[';
@@ -1955,25 +2009,14 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   // margin and turns this off (cluster.py::score applies the same rule on the Python path).
   const int32_t margin = ledger_->nomination_margin();
   if (nominate && !o.compat && n_best > 1 && margin == 0 && !uid.empty()) {
-    // which tied node: one picked by the pod's UID hash, as even over the tied nodes as
-    // kube-scheduler's random pick among equal scores, but the same for every worker
-    int64_t pick = static_cast<int64_t>(owner_hash(uid) % static_cast<uint64_t>(n_best));
-    for (size_t i = 0; i < scores.size(); ++i) {
-      if (rcs[i] != kOk || scores[i] != scores[best]) continue;
-      if (pick-- == 0) {
-        best = static_cast<int64_t>(i);
-        break;
-      }
-    }
+    best = top_pick(scores, rcs, uid);
     ++scores[best];
     second = scores[best] - 1;
     n_best = 1;
   }
   const bool lead = n_best == 1 && (second < 0 || scores[best] - second >= margin);
   if (nominate && lead && !uid.empty() && dem.n > 0) {
-    bool wants = false;
-    for (int i = 0; i < dem.n; ++i) wants = wants || dem.c[i].pct > 0 || dem.c[i].mib > 0;
-    if (wants) {
+    if (wants_devices(dem)) {
       if (s.defer && last.valid && uid.data() == last.uid.data()) {
         s.defer_nominate = true;
         s.defer_node = ids[best];

@@ -496,6 +496,33 @@ static void apiserver_and_writers(int pods, bool evented) {
 
 static std::string post(int port, const std::string& path, const std::string& body);
 
+// A scenario step that has not finished within `secs` prints `what()` (the step's progress)
+// and aborts: a hang names itself instead of running into the test's timeout.
+class Watchdog {
+ public:
+  template <class F>
+  Watchdog(const char* step, int secs, F what) : th_([this, step, secs, what] {
+    // polls a flag (no mutex: a std::mutex reused at a stack address confuses TSan)
+    const auto end = std::chrono::steady_clock::now() + std::chrono::seconds(secs);
+    while (!done_.load()) {
+      if (std::chrono::steady_clock::now() >= end) {
+        std::fprintf(stderr, "WATCHDOG: %s still running after %d s: %s\n", step, secs, what().c_str());
+        std::fflush(stderr);
+        std::abort();
+      }
+      std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    }
+  }) {}
+  ~Watchdog() {
+    done_.store(true);
+    th_.join();
+  }
+
+ private:
+  std::atomic<bool> done_{false};
+  std::thread th_;
+};
+
 // Inline bind writes (Frontend::set_kube_writer inline_io): client threads send filter + bind
 // over HTTP to a 2-worker front door whose workers drive the binds' API requests to the native
 // API server from their own epoll loops; every bind must be answered, bound and committed, and
@@ -541,9 +568,22 @@ static void inline_binds(int pods, bool frontdoor = false) {
     if (frontdoor) fe.set_fe_send(true);
     std::vector<std::thread> clients;
     std::atomic<int> ok{0};
+    std::atomic<int> sent[4] = {{-1}, {-1}, {-1}, {-1}};
+    const KubeWriter* kw0 = fe.kube_writer();
+    auto progress = [&] {
+      std::string m = "answered " + std::to_string(ok.load()) + "/" + std::to_string(pods) + "; client's last bind";
+      for (auto& x : sent) m += " " + std::to_string(x.load());
+      if (kw0)
+        m += "; writer ok " + std::to_string(kw0->stats.ok.load()) + " failed " + std::to_string(kw0->stats.failed.load()) +
+             " inflight " + std::to_string(kw0->stats.inflight.load()) + " retries " + std::to_string(kw0->stats.retries.load()) +
+             " timeouts " + std::to_string(kw0->stats.timeouts.load());
+      return m;
+    };
+    Watchdog wd(frontdoor ? "frontdoor binds" : "inline binds", 45, progress);
     for (int c = 0; c < 4; ++c)
       clients.emplace_back([&, c] {
         for (int i = c; i < pods; i += 4) {
+          sent[c].store(i);
           const std::string pod = texts[static_cast<size_t>(i)];
           CHECK(post(fe.port(), "/scheduler/filter", "{\"Pod\":" + pod + ",\"NodeNames\":[\"n0\"]}")
                     .rfind("HTTP/1.1 200", 0) == 0);
@@ -735,6 +775,7 @@ static void memo_and_wide(int iters) {
 }
 
 int main(int argc, char** argv) {
+  std::setvbuf(stdout, nullptr, _IOLBF, 0);   // each scenario's line out as it passes (a hang names its scenario)
   if (argc > 1 && std::strcmp(argv[1], "relist-scale") == 0) {
     relist_scale(argc > 2 ? std::atoi(argv[2]) : 100000);
     return 0;

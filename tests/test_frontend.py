@@ -409,6 +409,96 @@ def test_priorities_nominate_unique_best_and_bind_adopts():
     asyncio.run(main())
 
 
+@pytest.mark.parametrize("policy,partition", [("binpack", "SPX"), ("spread", "CPX")])
+def test_decisive_filter_answers_the_priorities_winner_byte_identical(policy, partition):
+    """--decisive-filter: the native filter answers the one node the Python filter answers,
+    byte for byte, which is the node priorities would rank first (ties broken by the pod's UID
+    hash, as priorities breaks them), and nominates it; failed nodes keep their reasons."""
+    async def main():
+        store, rt = await _runtime(4, partition, priority=policy, decisive_filter=True)
+        ext = rt.extender
+        led = rt.state.ledger
+        rng = random.Random(11)
+        names = [f"n{i}" for i in range(4)]
+        loop = asyncio.get_running_loop()
+        try:
+            for k, pod in enumerate(_pods(rng, 40)):
+                pod = store.create_pod(pod)
+                uid = pu.pod_uid(pod)
+                body = {"Pod": pod, "Nodes": None, "NodeNames": rng.sample(names, rng.randint(1, 4))}
+                raw = _dumps(body)
+                got = await loop.run_in_executor(None, _http, rt.bound_port, [("POST", "/scheduler/filter", raw)])
+                assert got[0] == (200, _dumps(ext.filter(json.loads(raw)))), got[0]
+                ans = json.loads(got[0][1])
+                fit = ans["NodeNames"]
+                assert len(fit) <= 1
+                # with the decisive answer's nomination dropped, priorities rank it first
+                led.drop_nomination(uid)
+                rt.state.decisive_filter = False
+                full = ext.filter(json.loads(raw))
+                prio = ext.prioritize(json.loads(raw))
+                rt.state.decisive_filter = True
+                assert set(full["FailedNodes"]) == set(ans["FailedNodes"])
+                if full["NodeNames"]:
+                    top = max(h["Score"] for h in prio if h["Host"] in full["NodeNames"])
+                    winners = [h["Host"] for h in prio if h["Host"] in full["NodeNames"] and h["Score"] == top]
+                    assert fit and fit[0] in winners, (fit, prio)
+                else:
+                    assert fit == []
+                led.drop_nomination(uid)
+                if fit and k % 2 == 0:
+                    got = await loop.run_in_executor(None, _http, rt.bound_port, [("POST", "/scheduler/filter", raw)])
+                    rec = led.lookup(uid)
+                    wants = any(p > 0 or m > 0 for p, m in pu.ledger_view(rt.state.pod_demand(pod))[0])
+                    if wants:
+                        assert rec["state"] == "nominated" and rec["node"] == rt.state.node_entry(fit[0]).id
+                    m = pu.meta(pod)
+                    r = await ext.bind({"PodName": m["name"], "PodNamespace": m["namespace"],
+                                        "PodUID": m["uid"], "Node": fit[0]})
+                    assert r["Error"] == ""
+            # compat mode (the reference's verbs): every fitting node again
+            rt.state.set_policy(policy, compat=True)
+            pod = store.create_pod(pu.make_pod("cmp", [("c", 10)]))
+            raw = _dumps({"Pod": pod, "Nodes": None, "NodeNames": names})
+            got = await loop.run_in_executor(None, _http, rt.bound_port, [("POST", "/scheduler/filter", raw)])
+            assert len(json.loads(got[0][1])["NodeNames"]) > 1
+            assert got[0] == (200, _dumps(ext.filter(json.loads(raw))))
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
+
+
+def test_decisive_filter_takes_one_round_trip_a_pod_through_the_standin():
+    """With one feasible node kube-scheduler (the stand-in) skips scoring: every pod bound
+    after a filter alone, no priorities call, no device over-committed."""
+    from nanogpu.sim.driver import NativeSchedulerDriver, node_capacities
+
+    async def main():
+        store, rt = await _runtime(4, decisive_filter=True)
+        loop = asyncio.get_running_loop()
+        try:
+            rng = random.Random(5)
+            pods = [store.create_pod(pu.make_pod(f"p{i}", [("c", rng.choice([10, 25, 50]))])) for i in range(80)]
+            nodes = [f"n{i}" for i in range(4)]
+            drv = NativeSchedulerDriver("127.0.0.1", rt.bound_port, nodes,
+                                        node_capacities([store.get_node(n) for n in nodes]), bind_threads=16)
+            st = await loop.run_in_executor(None, drv.run, pods)
+            assert st.scheduled == 80
+            fs = rt.native.fe.stats()
+            assert fs["priorities"]["count"] == 0 and fs["filter"]["count"] >= 80
+            used = {}
+            for p in store.pods.values():
+                if pu.node_name_of(p):
+                    k = (pu.node_name_of(p), pu.container_assignment(p, "c")[0])
+                    used[k] = used.get(k, 0) + pu.pod_demand(p)[0][0]
+            assert max(used.values()) <= 100
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
+
+
 def _fd_slots() -> int:
     for line in open("/proc/self/status"):
         if line.startswith("FDSize:"):
