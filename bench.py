@@ -105,6 +105,9 @@ def parse_args():
                          "(value_independent_schedulers; 0: none)")
     ap.add_argument("--apiserver-keep-heap", action="store_true",
                     help="the shared API server's process keeps freed heap memory (no trim / unmap)")
+    ap.add_argument("--apiserver-spin-us", type=float, default=0.0,
+                    help="the shared API server's IO threads poll this long after their last event before "
+                         "sleeping (a diagnostic: are a burst's first answers slow because its cores slept?)")
     ap.add_argument("--apiserver-threads", type=int, default=0,
                     help="shared API server IO threads (0: one per rank, 4 to 16)")
     ap.add_argument("--bind-writer-threads", type=int, default=0,
@@ -617,6 +620,8 @@ def apiserver_main(conn, avoid: list[int] | None = None, near: int = -1) -> None
             keys.clear()
             srv = core().ApiServer("127.0.0.1", 0, msg[1], 1 << 16)   # watch cache: 64k events per kind
             srv.set_latency(msg[2])
+            if len(msg) > 4 and msg[4] > 0:
+                srv.set_spin(msg[4])
             conn.send((srv.port, sorted(os.sched_getaffinity(0))))
         elif op == "nodes":
             for n in msg[1]:
@@ -807,8 +812,8 @@ class ApiServerProc:
         self.conn.send(msg)
         return self.conn.recv()
 
-    def start(self, threads: int, latency_s: float = 0.0, keep_heap: bool = False) -> str:
-        port, self.cpus = self._rpc("start", threads, latency_s, keep_heap)
+    def start(self, threads: int, latency_s: float = 0.0, keep_heap: bool = False, spin_s: float = 0.0) -> str:
+        port, self.cpus = self._rpc("start", threads, latency_s, keep_heap, spin_s)
         self.url = f"http://127.0.0.1:{port}"
         return self.url
 
@@ -1004,7 +1009,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         if d.rank == 0:
             apisrv = api_proc
             url = apisrv.start(args.apiserver_threads or min(16, max(4, d.world)), args.api_rtt_ms / 1e3,
-                               args.apiserver_keep_heap)
+                               args.apiserver_keep_heap, args.apiserver_spin_us / 1e6)
             if getattr(args, "_placement", None):
                 args._placement["apiserver"] = list(apisrv.cpus)
             apisrv.add_nodes(nodes)

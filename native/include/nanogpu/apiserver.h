@@ -84,6 +84,8 @@ class Server {
   // Modelled API round trip: every HTTP response is held this long after its request was
   // handled (watch events are not delayed). 0 = none.
   void set_latency(double seconds);
+  // IO threads poll for `seconds` after their last event before sleeping (0: sleep at once)
+  void set_spin(double seconds);
   // Watch-cache control for tests: forget history (a resumed watch gets 410 Gone), end every
   // open watch of `kind` ("pods" | "nodes" | "" = both).
   void compact(std::string_view kind);

@@ -471,6 +471,7 @@ struct IoThread {
   // modelled round trip: responses held until due, in arrival order (one latency for all)
   std::deque<std::tuple<double, std::weak_ptr<Conn>, std::string>> delayed;
   double last_flush = 0, flush_due = 0;   // watch output coalescing (Impl::flush_watches)
+  double last_event = 0;                  // the spin window (set_spin) runs from here
   std::atomic<bool> urgent{false};        // flush now, without the linger (a bulk write ended)
   std::mutex mu;
   std::vector<std::shared_ptr<Conn>> flush;   // watch conns with pending output
@@ -491,6 +492,7 @@ struct Server::Impl {
   Config cfg;
   int lfd = -1;
   std::atomic<double> latency_s{0.0};
+  std::atomic<double> spin_s{0.0};   // poll this long after the last event before sleeping (0: never)
   double linger_s = 200e-6;   // watch output coalescing window under load
   std::atomic<bool> stopping{false};
   std::vector<std::unique_ptr<IoThread>> io;
@@ -1224,7 +1226,18 @@ void Server::Impl::io_loop(IoThread* t) {
     if (!t->delayed.empty()) wait_s = std::min(wait_s, std::get<0>(t->delayed.front()) - steady_s());
     if (t->flush_due > 0) wait_s = std::min(wait_s, t->flush_due - steady_s());
     wait_s = std::max(0.0, wait_s);
-    const int n = wait_events(t->ep, evs, 256, wait_s);
+    int n = 0;
+    const double spin = spin_s.load(std::memory_order_relaxed);
+    if (spin > 0 && wait_s > 0) {
+      // a diagnostic: the thread polls instead of sleeping for `spin` after its last event,
+      // so its core never idles between a burst's requests (or across a short gap)
+      const double until = t->last_event + spin;
+      while ((n = wait_events(t->ep, evs, 256, 0.0)) == 0 && steady_s() < until &&
+             !stopping.load(std::memory_order_relaxed)) {
+      }
+    }
+    if (n == 0) n = wait_events(t->ep, evs, 256, wait_s);
+    if (n > 0 && spin > 0) t->last_event = steady_s();
     for (int i = 0; i < n; ++i) {
       const int fd = evs[i].data.fd;
       if (fd == lfd) {
@@ -1488,6 +1501,7 @@ std::string Server::stats_json() const {
 }
 
 void Server::set_latency(double seconds) { impl_->latency_s.store(seconds > 0 ? seconds : 0.0); }
+void Server::set_spin(double seconds) { impl_->spin_s.store(seconds > 0 ? seconds : 0.0); }
 
 void Server::compact(std::string_view kind) {
   std::lock_guard<std::mutex> g(impl_->mu);

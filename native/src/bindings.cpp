@@ -1144,6 +1144,8 @@ PYBIND11_MODULE(_native, m) {
            "Deletes (namespace, name) pods; returns how many existed.")
       .def("stats", [](const apisrv::Server& s) { return s.stats_json(); })
       .def("set_latency", &apisrv::Server::set_latency, py::arg("seconds"))
+      .def("set_spin", &apisrv::Server::set_spin, py::arg("seconds"),
+           "IO threads poll this long after their last event before sleeping (a diagnostic)")
       .def("compact", &apisrv::Server::compact, py::arg("kind") = "")
       .def("drop_watches", &apisrv::Server::drop_watches, py::arg("kind") = "");
 

@@ -240,6 +240,36 @@ def test_native_bulk_create_delete_and_timeout_ends_the_stream():
         srv.stop()
 
 
+def test_native_spinning_io_threads_still_answer_and_stop():
+    """set_spin (bench --apiserver-spin-us, a diagnostic): IO threads poll for a window after
+    their last event instead of sleeping; requests over HTTP are answered, timeouts and watch
+    deadlines still fire, and stop() returns while they spin."""
+    import time
+
+    srv = N.ApiServer("127.0.0.1", 0, 2, 1000)
+    srv.set_spin(0.05)
+    try:
+        async def main():
+            api = KubeClient(KubeConfig(server=f"http://127.0.0.1:{srv.port}"))
+            try:
+                for i in range(20):
+                    await api.create_pod(pu.make_pod(f"s{i}", [("main", 10)], namespace="s"))
+                items, rv = await api.list_pods()
+                assert len(items) == 20
+                t0 = asyncio.get_running_loop().time()
+                async for _ in api.watch("pods", rv, timeout_s=1):
+                    pass
+                assert 0.8 < asyncio.get_running_loop().time() - t0 < 3.0
+            finally:
+                await api.close()
+
+        asyncio.run(main())
+    finally:
+        t0 = time.perf_counter()
+        srv.stop()
+        assert time.perf_counter() - t0 < 2.0
+
+
 def test_slim_pod_decoding_keeps_what_the_controllers_read():
     """decode_pod_watch (the pod informer's native decoder) drops everything but identity,
     labels, nano-gpu/* annotations and resources, nodeName and phase; every podutil reading
