@@ -5,7 +5,7 @@
 set -o pipefail
 out=${OUT:-gpurun_out/arms}; reps=${REPS:-3}
 mkdir -p "$out"
-base="--gpus 1 --steps 20 --warmup 5 --rtt-variant-ms 0 --steady-variant-steps 0 --nodes-variant 0 --inproc-variant-steps 0"
+base="--gpus 1 --steps 20 --warmup 5 --rtt-variant-ms 0 --steady-variant-steps 0 --nodes-variant 0 --inproc-variant-steps 0 --decisive-variant-steps 0"
 for i in $(seq 1 "$reps"); do
   k=0
   for flags in "$@"; do
