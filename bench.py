@@ -1500,7 +1500,7 @@ def order_line(full: dict) -> tuple[dict, dict]:
     # whatever else the line carries, it stays under ~3.8 KB: the largest side keys move out
     keep = {"metric", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
             "vs_baseline", "dtype", "data", "config", "value_mode", "scheduled", "failed", "bind_hops_us",
-            "bind_tail_hop"}
+            "bind_tail_hop", "gpu"}
     budget = 3800 - sum(len(json.dumps({k: full[k]})) for k in HEADLINE_LAST if k in full)
     while len(json.dumps(line)) > budget:
         side = [k for k in line if k not in keep]
@@ -1636,6 +1636,7 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
             full["p50_bind_ms_decisive_filter"] = dout["p50_bind_ms"]
             full["frag_pct_decisive_filter"] = _frag_mean(dres["frag"])
             full["priorities_calls_per_pod_decisive_filter"] = dres.get("prio_per_pod")
+            full["extender_cpu_us_per_pod_decisive_filter"] = round(dres.get("cpu_us_per_pod", 0.0), 1)
     if inproc_v is not None:
         if "error" in inproc_v:
             full["value_inproc_api"] = None
