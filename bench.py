@@ -1564,6 +1564,7 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
         # the same binds split by hop (p50, p99, mean of the slowest 1 %; us) and the hop whose
         # slowest-1 % mean exceeds its median most: where the p99 bind's time goes
         "extender_share_of_cycle": cycle_share(res)[0],
+        "extender_held_share_of_cycle": cycle_share(res)[1],
         "bind_hops_us": (out.get("bind_hops") or {}).get("us"),
         "bind_tail_hop": (out.get("bind_hops") or {}).get("tail_hop"),
         "bind_hops_us_by_decile_rank0": hops_by_decile(res.get("bind_hops_steps") or []),
