@@ -14,6 +14,8 @@ import sys
 import time
 from pathlib import Path
 
+import pytest
+
 from nanogpu.k8s import podutil as pu
 from nanogpu.k8s.fake_apiserver import FakeKubeStore, serve
 from nanogpu.sim.driver import FastExtenderClient, SchedulerDriver, node_capacities
@@ -30,7 +32,11 @@ def _free_port():
     return p
 
 
-def test_two_workers_share_one_ledger():
+@pytest.mark.parametrize("decisive", [False, True])
+def test_two_workers_share_one_ledger(decisive):
+    """(decisive: --decisive-filter, filter answers one node and kube-scheduler binds it at
+    once; with two workers the filter publishes its pod before answering, so a bind on the
+    other worker finds it)"""
     async def main():
         store = FakeKubeStore()
         nodes = [pu.make_node(f"n{i}", 2, synthetic_mi355x(2).to_json()) for i in range(3)]
@@ -41,7 +47,7 @@ def test_two_workers_share_one_ledger():
         ledger = f"/dev/shm/nanogpu-test-workers-{os.getpid()}"
         proc = subprocess.Popen([sys.executable, "-m", "nanogpu", "--kube-api", f"http://127.0.0.1:{api_port}",
                                  "--workers", "2", "--host", "127.0.0.1", "--ledger-path", ledger,
-                                 "--policyConfigPath", "/nonexistent"],
+                                 "--policyConfigPath", "/nonexistent"] + (["--decisive-filter"] if decisive else []),
                                 env=dict(os.environ, PORT=str(port)), cwd=str(ROOT),
                                 stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
         try:
