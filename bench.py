@@ -691,16 +691,16 @@ def apiserver_main(conn, avoid: list[int] | None = None, near: int = -1) -> None
             return
 
 
-async def wait_released(lookup, uids: list[str], timeout_s: float = 10.0) -> bool:
+async def wait_released(ledger, uids: list[str], timeout_s: float = 10.0) -> bool:
     """Until the ledger holds none of `uids` (the pod controller's releases). Polled every
     20 µs from an executor thread: the event loop stays free for the watch (the in-process
     and aiohttp watches deliver the DELETED events on it), and the harness's waiting does not
     spin the extender process's event loop, whose CPU time the bench reports. Deletions arrive
-    in order: the last pod first, then all of them once."""
+    in order: the last pod first, then all of them once (one native call for the lot)."""
     def poll() -> bool:
         end = time.perf_counter() + timeout_s
         while time.perf_counter() < end:
-            if not lookup(uids[-1]) and not any(lookup(u) for u in uids):
+            if not ledger.holds_any(uids[-1:]) and not ledger.holds_any(uids):
                 return True
             time.sleep(20e-6)
         return False
@@ -994,6 +994,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         return await (ext.run(coro) if ext is not None else coro)
 
     async def barrier() -> None:
+        if d.world == 1:
+            return
         if shared:   # keep the loop turning (watch, controller) while other ranks catch up
             await loop.run_in_executor(None, d.barrier)
         else:
@@ -1068,6 +1070,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     # their creation in the API server, scheduling, deletion and release are all timed
     all_steps = [10_000 + w for w in range(args.warmup)] + list(range(args.steps))
     bursts = {} if steady else {s: burst(d.rank, d.world, args.pods, s, 7) for s in all_steps}
+    # their UIDs too (deterministic, set by burst()): the release check's keys, not scheduler work
+    burst_uids = {s: [pu.pod_uid(p) for p in ps] for s, ps in bursts.items()}
 
     # one scheduler (the default with N ranks): ONE kube-scheduler stand-in for the job (rank 0's) drives every pod; its
     # scheduling cycle stays on rank 0's worker, its binds spread over every rank's worker (the
@@ -1107,7 +1111,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         with hc:
             uids = [steady_uid(k, k % d.world) for k in dels]
         if uids:
-            await wait_released(rt.state.ledger.lookup, uids)
+            await wait_released(rt.state.ledger, uids)
         phases["release_ms"] = 1e3 * (time.perf_counter() - t_step0)
         if shared:
             await barrier()
@@ -1190,11 +1194,13 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         ts = time.perf_counter()
         # all ranks finished their share of the burst: peak occupancy
         await barrier()
-        srv_ms.setdefault(step, {})["barrier_peak_ms"] = 1e3 * (time.perf_counter() - ts)
+        tb = time.perf_counter()
+        srv_ms.setdefault(step, {})["barrier_peak_ms"] = 1e3 * (tb - ts)
         with hc:
             frag = rt.state.frag(min(SIZES))
-            uids = [pu.pod_uid(p) for p in pods]
+        uids = burst_uids.pop(step)
         t_frag = time.perf_counter()
+        srv_ms[step]["frag_ms"] = 1e3 * (t_frag - tb)
         if store is not None:
             for p in pods:
                 m = pu.meta(p)
@@ -1210,9 +1216,10 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
             srv_ms.setdefault(step, {}).update(delete_srv_ms=1e3 * dt_d, peak_ms=1e3 * (t_frag - ts),
                                                delete_rpc_ms=1e3 * (time.perf_counter() - t_frag))
         # the pod controller releases on DELETED; wait until our shares are gone
-        await wait_released(rt.state.ledger.lookup, uids)
+        await wait_released(rt.state.ledger, uids)
         t_rel = time.perf_counter()
-        if pod_ctrl is not None:
+        if pod_ctrl is not None and (pod_ctrl.queue.depth() or pod_ctrl.queue.processing):
+            # (read across threads: an empty queue now is what drain() would return at once on)
             await on_ext(pod_ctrl.queue.drain(5.0))
         srv_ms.setdefault(step, {})["drain_ms"] = 1e3 * (time.perf_counter() - t_rel)
         if os.environ.get("NANOGPU_BENCH_DEBUG"):

@@ -682,6 +682,15 @@ PYBIND11_MODULE(_native, m) {
              if (!l.lookup(key, &r)) return py::none();
              return record_dict(r);
            })
+      .def(
+          "holds_any",
+          [](const Ledger& l, const std::vector<std::string>& keys) {
+            py::gil_scoped_release nogil;
+            for (const std::string& k : keys)
+              if (l.holds(k)) return true;
+            return false;
+          },
+          py::arg("keys"), "Whether the ledger holds a record of any of `keys` (one call for many)")
       .def("pods_on",
            [](const Ledger& l, int32_t node) {
              py::list out;
