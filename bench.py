@@ -738,6 +738,42 @@ def set_thread_comm(name: str) -> None:
         pass
 
 
+class ContentionMonitor:
+    """The contention watches (affinity.ContentionWatch) on a harness thread of their own,
+    every `period_s` while the timed steps run: their /proc and sysfs reads (3-4 ms a round on
+    a 256-CPU host) stay off the steps' path, where they used to sit between every 4th step.
+    A relocation it decides is made from this thread (sched_setaffinity of every thread)."""
+
+    def __init__(self, watch, api_watch, pl: dict, results: dict, period_s: float = 0.1):
+        import threading
+
+        self.watch, self.api_watch, self.pl, self.results = watch, api_watch, pl, results
+        self.period_s = period_s
+        self.steps_done = 0            # the step loop's progress, for the relocation record
+        self.stop_ev = threading.Event()
+        self.th = threading.Thread(target=self._run, name="bench-harness", daemon=True)
+        self.th.start()
+
+    def _run(self) -> None:
+        from nanogpu import affinity
+
+        set_thread_comm("bench-harness")
+        while not self.stop_ev.wait(self.period_s):
+            foreign, to = self.watch.check()
+            if self.api_watch is not None:
+                self.results["foreign_cpus_api"].append(round(self.api_watch.check()[0], 2))
+            self.results["foreign_cpus"].append(round(foreign, 2))
+            if to is not None:
+                affinity.relocate(self.pl["pids"], to)
+                self.results["relocated"] = dict(self.results.get("relocated") or {}, mid_run_from=self.pl["cpus"],
+                                                 mid_run_to=to, at_step=self.steps_done)
+                self.pl["cpus"] = self.watch.cpus = to
+
+    def close(self) -> None:
+        self.stop_ev.set()
+        self.th.join(5.0)
+
+
 class ExtenderLoop:
     """The extender's asyncio loop on a thread of its own ("ngpu-loop"), as in a deployment,
     where `python -m nanogpu` runs nothing else on it: the harness drives the steps from the
@@ -911,6 +947,7 @@ def driver_main(conn) -> None:
         while True:
             msg = conn.recv()
             if isinstance(msg, dict):
+                st.pop("spent", None)
                 configure(msg)
                 continue
             if msg[0] == "live":
@@ -944,13 +981,16 @@ def driver_main(conn) -> None:
                         placed.append((spec.key, live[spec.key]))
             else:
                 stats = drv.run(prepared=work.pop(step)) if native else drv.run(work.pop(step))
-            drv.close()
             t1 = time.perf_counter()
             sm = stats.summary()
             if st["stream"] is not None:
                 sm["live_placed"] = placed   # for the other ranks' stand-ins (their informers)
             t2 = time.perf_counter()
             conn.send(sm)
+            # the step's driver and pod records are freed at the next configure, not inside the
+            # next step's clock (thousands of objects)
+            drv.close()
+            st.setdefault("spent", []).append(drv)
             if os.environ.get("NANOGPU_BENCH_DEBUG"):
                 print(f"drv step {step}: pre {1e3*(stats.t_first_filter-t0):.3f} run {1e3*(t1-t0):.3f} "
                       f"post {1e3*(t1-stats.t_last_bind):.3f} summary {1e3*(t2-t1):.3f} send {1e3*(time.perf_counter()-t2):.3f}",
@@ -1098,6 +1138,27 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     srv_ms: dict = {}        # step -> the API server's own create/delete time
     hc = HarnessCpu()        # the harness's own CPU on the main thread (not the extender's)
 
+    # the front door's per-bind records (wall time, hop split) are taken once, after the timed
+    # steps (no per-step copy inside the clock): each step only marks how many there are
+    bind_marks: list = []
+    spent: list = []   # finished steps' pod objects, freed after the timed steps
+
+    def mark_binds() -> None:
+        if rt.native is not None:
+            bind_marks.append(rt.native.fe.bind_samples_waiting())
+
+    def take_binds() -> None:
+        if rt.native is None:
+            return
+        walls, hops = rt.native.fe.take_bind_wall(), rt.native.fe.take_bind_hops()
+        results["frontdoor_bind_ms"] = [1e3 * x for x in walls]
+        results["bind_hops_ns"] = hops
+        steps_h, prev = [], 0
+        for _, nh in bind_marks:
+            steps_h.append(hops[prev:nh])
+            prev = nh
+        results["bind_hops_steps"] = steps_h
+
     async def one_step_steady(step: int, timed: bool) -> dict:
         """Steady-state churn: this step's deletions (pods of earlier steps) and creations, the
         controller's releases, then the stand-in schedules the new pods next to the live ones."""
@@ -1138,19 +1199,18 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
             frag = rt.state.frag(min(SIZES))
             phases.update(create_ms=0.0, schedule_ms=1e3 * summary["span_s"])
             client_s = summary.pop("bind_s_all", [])
-            walls = rt.native.fe.take_bind_wall() if rt.native is not None else []
-            hops = rt.native.fe.take_bind_hops() if rt.native is not None else []
             if timed:
                 results["client_bind_s"].extend(client_s)
-                results["frontdoor_bind_ms"].extend(1e3 * x for x in walls)
-                results["bind_hops_ns"].extend(hops)
-                results.setdefault("bind_hops_steps", []).append(hops)
+                mark_binds()
         return {"stats": summary, "frag": frag, "phases": phases}
 
     async def one_step(step: int, timed: bool, nxt: int | None = None) -> dict:
         if steady:
             return await one_step_steady(step, timed)
         pods = bursts.pop(step)
+        # the step's pod objects (client-side data) are kept until the timed steps are over:
+        # dropped here, their ~30k Python objects would be freed inside the clock (~1 ms a step)
+        spent.append(pods)
         t_step0 = tc = time.perf_counter()
         if conn is not None:
             # the pods are created in the API server (this process), then the scheduler
@@ -1228,14 +1288,10 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         phases = {"create_ms": 1e3 * tc, "schedule_ms": 1e3 * summary["span_s"],
                   "release_ms": 1e3 * (time.perf_counter() - ts)}
         phases.update(srv_ms.pop(step, {}))
-        walls = rt.native.fe.take_bind_wall() if rt.native is not None else []
-        hops = rt.native.fe.take_bind_hops() if rt.native is not None else []
         client_s = summary.pop("bind_s_all", [])
         if timed:
             results["client_bind_s"].extend(client_s)
-            results["frontdoor_bind_ms"].extend(1e3 * x for x in walls)
-            results["bind_hops_ns"].extend(hops)
-            results.setdefault("bind_hops_steps", []).append(hops)
+            mark_binds()
             diag = {"t0": round(t_step0, 4), "t1": round(time.perf_counter(), 4)}
             diag.update({k: round(summary.get(k, 0.0), 2) for k in ("cycle_max_ms", "cycle_sum_ms", "cycle_wire_ms", "bind_max_ms")})
             diag["unschedulable"] = summary.get("unschedulable_attempts", 0)
@@ -1253,6 +1309,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
             diag["gc_ms"] = round(1e3 * gc_pause["sum"], 2)
             diag["gc_max_ms"] = round(1e3 * gc_pause["max"], 2)
             gc_pause.update(sum=0.0, max=0.0, n=0)
+            diag["t2"] = round(time.perf_counter(), 4)
             results.setdefault("diag", []).append(diag)
         hc.__exit__(None, None, None)
         return {"stats": summary, "frag": frag, "phases": phases}
@@ -1302,6 +1359,9 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                     apisrv.cpus = to
     results["relocated"] = moved
     rt.tracer.buf.clear()
+    if rt.native is not None:   # the warm-up steps' bind records
+        rt.native.fe.take_bind_wall()
+        rt.native.fe.take_bind_hops()
     await barrier()
     d.sync()
     prof = None
@@ -1337,35 +1397,32 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     t0 = time.perf_counter()
     if sampler is not None:
         sampler.on.set()
-    # other tenants moving onto the rank's domain mid-run: checked every 4 steps (~0.1 s), the
-    # job moves to a quieter domain when they keep half a CPU or more of it busy
-    watch = api_watch = None
+    # other tenants moving onto the rank's domain mid-run: checked every 0.1 s by a harness
+    # thread, the job moves to a quieter domain when they keep half a CPU or more of it busy
+    monitor = None
     if d.world == 1 and getattr(args, "_placement", None) and not getattr(args, "no_relocate", False):
         pl = args._placement
         watch = affinity.ContentionWatch(pl["cpus"], pl["pids"], pl["numa"], exclude=pl.get("apiserver") or [])
         watch.check()
         results["foreign_cpus"] = []
+        api_watch = None
         if pl.get("apiserver") and pl.get("api_pid"):
             # the shared API server's domain too: read only (it is never moved mid-run)
             api_watch = affinity.ContentionWatch(pl["apiserver"], [pl["api_pid"]], pl["numa"])
             api_watch.check()
             results["foreign_cpus_api"] = []
+        monitor = ContentionMonitor(watch, api_watch, pl, results)
     for k, s in enumerate(timed_ids):
         r = await one_step(s, True, timed_ids[k + 1] if k + 1 < len(timed_ids) else None)
         results["steps"].append(r["stats"])
         results["frag"].append(r["frag"])
         results.setdefault("phases", []).append(r["phases"])
-        if watch is not None and k % 4 == 3:
-            with hc:
-                foreign, to = watch.check()
-                if api_watch is not None:
-                    results["foreign_cpus_api"].append(round(api_watch.check()[0], 2))
-            results["foreign_cpus"].append(round(foreign, 2))
-            if to is not None:
-                affinity.relocate(pl["pids"], to)
-                results["relocated"] = dict(results.get("relocated") or {}, mid_run_from=pl["cpus"], mid_run_to=to,
-                                            at_step=k + 1)
-                pl["cpus"] = watch.cpus = to
+        if monitor is not None:
+            monitor.steps_done = k + 1
+    if monitor is not None:
+        monitor.close()
+    take_binds()
+    spent.clear()
     if sampler is not None:
         sampler.report(args.stall_trace)
     if io_tally:
@@ -1421,9 +1478,9 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         dthr["main"] = dthr.pop("ngpu-loop", 0.0)
         loop_s = dthr["main"]
     else:
-        harness_s = hc.s
-        dthr["main"] = dthr.get("main", 0.0) - harness_s
-        loop_s = loop_cpu1 - loop_cpu0 - harness_s
+        dthr["main"] = dthr.get("main", 0.0) - hc.s
+        loop_s = loop_cpu1 - loop_cpu0 - hc.s
+        harness_s = hc.s + dthr.pop("bench-harness", 0.0)   # the contention monitor's thread
     results["cpu_us_per_pod"] = 1e6 * (cpu1 - cpu0 - harness_s) / n_sched
     if "io_tally" in results:   # (calls, s) by call site -> calls a pod, us a pod, ns a call
         results["io_per_pod"] = {k: [round(n / n_sched, 3), round(1e6 * sec / n_sched, 2), round(1e9 * sec / max(1, n))]

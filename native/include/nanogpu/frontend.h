@@ -175,6 +175,8 @@ class Frontend {
   // when this host has no invariant TSC to stamp with).
   bool set_bind_hops(bool on);
   std::vector<std::array<uint32_t, 6>> take_bind_hops();
+  // how many of each are waiting to be taken (a marker between steps, no copy)
+  std::pair<size_t, size_t> bind_samples_waiting();
 
  private:
   struct Conn;

@@ -918,6 +918,8 @@ PYBIND11_MODULE(_native, m) {
              return s;
            },
            "seconds from request read to response written, per bind since the last call")
+      .def("bind_samples_waiting", &Frontend::bind_samples_waiting,
+           "(bind wall times, bind hop splits) recorded and not yet taken")
       .def("set_bind_hops", &Frontend::set_bind_hops, py::arg("on"),
            "record each native bind's hop split (false: off, or no invariant TSC on this host)")
       .def("take_bind_hops", [](Frontend& f) {

@@ -437,6 +437,11 @@ bool Frontend::set_bind_hops(bool on) {
   return on;
 }
 
+std::pair<size_t, size_t> Frontend::bind_samples_waiting() {
+  std::lock_guard<std::mutex> g(wall_mu_);
+  return {bind_wall_ns_.size(), bind_hops_.size()};
+}
+
 std::vector<std::array<uint32_t, 6>> Frontend::take_bind_hops() {
   std::lock_guard<std::mutex> g(wall_mu_);
   std::vector<std::array<uint32_t, 6>> out;
