@@ -459,6 +459,20 @@ def test_pod_keys_are_views_and_keys_no_slot_holds_never_match():
     assert L.release(k63) == N.OK and L.lookup(k63) is None
 
 
+def test_holds_any_matches_lookup_over_a_key_list():
+    """holds_any (the bench's release check: one call for a burst's keys) is true exactly when
+    lookup finds one of the keys; bad keys never match."""
+    L, (nid,) = ledger_with(synthetic_mi355x(8))
+    keys = [f"h{i}" for i in range(40)]
+    for k in keys[::3]:
+        assert L.reserve(nid, k, [(5, 0)], BIN)[0] == N.OK
+    assert L.holds_any(keys) and L.holds_any(keys[:1]) and not L.holds_any(keys[1:3])
+    assert not L.holds_any([]) and not L.holds_any(["", "z" * 64])
+    for k in keys[::3]:
+        assert L.release(k) == N.OK
+    assert not L.holds_any(keys) and all(L.lookup(k) is None for k in keys)
+
+
 # ----------------------------------------------------------------------------- memo re-validation
 _share = st.tuples(st.sampled_from([5, 10, 25, 50, 100]), st.sampled_from([0, 0, 8192, 32768, 100 * 1024]),
                    st.sampled_from([0, 0, 1]))

