@@ -835,6 +835,10 @@ int main(int argc, char** argv) {
             "\"NodeNames\":[\"node-0\",\"node-1\",\"node-2\",\"node-3\",\"node-4\",\"node-5\"]}";
         const std::string r = post(fe.port(), i % 2 ? "/scheduler/priorities" : "/scheduler/filter", body);
         CHECK(r.rfind("HTTP/1.1 200", 0) == 0);
+        // the options change under the workers now and then: the decisive filter (one node
+        // answered) on and off, picked up by each worker's next request (no nominations: the
+        // devices must all be free at the end)
+        if (c == 1 && i % 7 == 3) fe.set_options(fo, true, false, (i / 7) % 2 == 0);
       }
     });
 
