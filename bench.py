@@ -727,6 +727,17 @@ class HarnessCpu:
         return False
 
 
+def rss_mib() -> float:
+    """This process's resident memory, MiB (/proc/self/status VmRSS)."""
+    try:
+        for line in open("/proc/self/status"):
+            if line.startswith("VmRSS:"):
+                return round(int(line.split()[1]) / 1024, 1)
+    except OSError:
+        pass
+    return 0.0
+
+
 def set_thread_comm(name: str) -> None:
     """Names the calling OS thread (/proc/self/task/<tid>/comm, 15 bytes): thread_cpu() groups
     the process's CPU by these names."""
@@ -1358,6 +1369,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                 if apisrv is not None:
                     apisrv.cpus = to
     results["relocated"] = moved
+    results["rss_mib"] = [rss_mib()]   # the extender process's resident memory, before / after the timed steps
     rt.tracer.buf.clear()
     if rt.native is not None:   # the warm-up steps' bind records
         rt.native.fe.take_bind_wall()
@@ -1423,6 +1435,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         monitor.close()
     take_binds()
     spent.clear()
+    results["rss_mib"].append(rss_mib())
     if sampler is not None:
         sampler.report(args.stall_trace)
     if io_tally:
@@ -1662,6 +1675,7 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
         # the bench harness's own work on its main thread (HarnessCpu, reported next to it)
         "extender_cpu_us_per_pod_rank0": round(res.get("cpu_us_per_pod", 0.0), 1),
         "bench_harness_cpu_us_per_pod_rank0": round(res.get("harness_cpu_us_per_pod", 0.0), 2),
+        "extender_rss_mib_before_after_rank0": res.get("rss_mib"),
         "extender_loop_cpu_us_per_pod_rank0": round(res.get("loop_cpu_us_per_pod", 0.0), 1),
         "extender_cpu_us_per_pod_by_thread_rank0": res.get("cpu_us_per_pod_by_thread"),
         "extender_cpu_us_per_pod_user_kernel_rank0": res.get("cpu_us_per_pod_user_kernel"),
