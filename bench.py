@@ -1431,6 +1431,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         results.setdefault("phases", []).append(r["phases"])
         if monitor is not None:
             monitor.steps_done = k + 1
+        if k % 100 == 99 and d.rank == 0:   # a long run's heartbeat (one line per 100 steps)
+            print(f"bench: {k + 1} timed steps", file=sys.stderr, flush=True)
     if monitor is not None:
         monitor.close()
     take_binds()
@@ -1883,6 +1885,9 @@ def main() -> int:
 
 def run_pass(d: Dist, args, topo, conn, tag: str, api_proc=None) -> dict:
     """One bench pass on a fresh shared ledger (all ranks)."""
+    if d.rank == 0:   # progress on stderr (a long run is seen to be alive)
+        print(f"bench: pass {tag}: {args.steps} steps of {args.pods} pods on {args.nodes} nodes",
+              file=sys.stderr, flush=True)
     ledger_path = d.bcast_obj(f"/dev/shm/nanogpu-bench-{os.environ.get('MASTER_PORT', os.getpid())}-{tag}-"
                               f"{int(time.time())}" if d.rank == 0 else None)
     from nanogpu.native import core
