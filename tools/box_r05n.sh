@@ -17,3 +17,6 @@ print({k: d.get(k) for k in ("value", "p50_bind_ms", "p99_bind_ms", "frag_pct", 
                              "value_decisive_filter", "extender_cpu_us_per_pod_rank0", "extender_rss_mib_before_after_rank0")})
 print("step ms by 50-step block:", [round(sum(c) / len(c), 2) for c in chunks])
 PY
+# the decisive filter with one front-door thread (filters queue behind binds on it) vs two
+OUT="$out/arms" REPS=2 tools/bench_arms.sh "--decisive-filter" "--decisive-filter --frontend-threads 2" || exit $?
+echo done
