@@ -618,7 +618,11 @@ def apiserver_main(conn, avoid: list[int] | None = None, near: int = -1) -> None
                 srv.stop()
             steps.clear()
             keys.clear()
-            srv = core().ApiServer("127.0.0.1", 0, msg[1], 1 << 16)   # watch cache: 64k events per kind
+            # watch cache: 16k events per kind. A burst makes about 4k (create, bind, label,
+            # delete), so the warm-up steps fill it and every timed step runs in the steady
+            # state, evicting as many old versions as it adds (with 64k the first ~16 steps
+            # evicted nothing and ran faster than the ones after them: profiles/soak_r05.md)
+            srv = core().ApiServer("127.0.0.1", 0, msg[1], 1 << 14)
             srv.set_latency(msg[2])
             if len(msg) > 4 and msg[4] > 0:
                 srv.set_spin(msg[4])

@@ -393,6 +393,8 @@ class Ledger {
   int32_t release_if(std::string_view key, int32_t only_state);   // -1: any state
   PodSlot* find_pod_locked(int s, uint64_t h, const char* key) const;
   PodSlot* insert_pod_locked(int s, uint64_t h, const char* key);
+  // frees slot `p` of shard `s` (shard lock held): a tombstone only where a probe may pass
+  void erase_pod_locked(int s, PodSlot* p);
   // a slot's demand and plan, inline or in its overflow record (false: no record free)
   bool put_record(PodSlot* p, const Demand& d, const Plan& plan);
   void get_record(const PodSlot& p, Demand* d, Plan* plan) const;

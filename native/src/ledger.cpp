@@ -268,9 +268,33 @@ PodSlot* Ledger::find_pod_locked(int s, uint64_t h, const char* key) const {
   return nullptr;
 }
 
+void Ledger::erase_pod_locked(int s, PodSlot* p) {
+  // Linear probing needs a tombstone only where a later entry's probe may run through the
+  // slot. With the next slot empty none can; nor then through the tombstones right before
+  // this one (a cluster's dead tail): they all become empty (no live entry moves, so slot
+  // pointers stay valid). Churn then leaves no tombstones to lengthen every miss's probe.
+  PodSlot* t = shard(s);
+  const uint32_t cap = hdr_->pods_per_shard;
+  const uint32_t i = static_cast<uint32_t>(p - t);
+  --hdr_->shard_live[s];
+  if (t[(i + 1) % cap].state != kPodEmpty) {
+    p->state = kPodTombstone;
+    ++hdr_->shard_tomb[s];
+    return;
+  }
+  p->state = kPodEmpty;
+  for (uint32_t k = (i + cap - 1) % cap; k != i && t[k].state == kPodTombstone; k = (k + cap - 1) % cap) {
+    t[k].state = kPodEmpty;
+    --hdr_->shard_tomb[s];
+  }
+}
+
 PodSlot* Ledger::insert_pod_locked(int s, uint64_t h, const char* key) {
   const uint32_t cap = hdr_->pods_per_shard;
-  if (hdr_->shard_live[s] + hdr_->shard_tomb[s] + 1 > static_cast<int32_t>(cap * 9 / 10)) {
+  // rehash when the table is nearly full, or when tombstones alone are a quarter of it (the
+  // probe of every miss runs through them)
+  if (hdr_->shard_live[s] + hdr_->shard_tomb[s] + 1 > static_cast<int32_t>(cap * 9 / 10) ||
+      hdr_->shard_tomb[s] > static_cast<int32_t>(cap / 4)) {
     if (hdr_->shard_tomb[s] == 0) return nullptr;  // genuinely full
     // compact: rehash live entries, dropping tombstones
     PodSlot* t = shard(s);
@@ -927,9 +951,7 @@ int32_t Ledger::reserve_as(int32_t id, std::string_view key, const Demand& d, co
     Unlock us{&hdr_->shard_mu[s].m};
     PodSlot* p = insert_pod_locked(s, h, kb.c_str());
     if (p && !put_record(p, d, *plan)) {
-      p->state = kPodTombstone;       // no overflow record free: give the slot back
-      --hdr_->shard_live[s];
-      ++hdr_->shard_tomb[s];
+      erase_pod_locked(s, p);       // no overflow record free: give the slot back
       p = nullptr;
     }
     if (!p) {
@@ -982,9 +1004,7 @@ int32_t Ledger::allocate_plan(int32_t id, std::string_view key, const Demand& d,
     Unlock us{&hdr_->shard_mu[s].m};
     PodSlot* p = insert_pod_locked(s, h, kb.c_str());
     if (p && !put_record(p, d, plan)) {
-      p->state = kPodTombstone;
-      --hdr_->shard_live[s];
-      ++hdr_->shard_tomb[s];
+      erase_pod_locked(s, p);
       p = nullptr;
     }
     if (!p) {
@@ -1041,9 +1061,7 @@ int32_t Ledger::reserve_wide(int32_t id, std::string_view key, const Demand& fol
     PodSlot* p = insert_pod_locked(s, h, kb.c_str());
     if (p && (!put_record(p, folded, fplan) || !put_wide(p, wide))) {
       free_record(p);
-      p->state = kPodTombstone;
-      --hdr_->shard_live[s];
-      ++hdr_->shard_tomb[s];
+      erase_pod_locked(s, p);
       p = nullptr;
     }
     if (!p) {
@@ -1126,9 +1144,7 @@ int32_t Ledger::release_if(std::string_view key, int32_t only_state) {
     touched = plan_touch_mask(n->devs, n->n_devs, pp);
   }
   free_record(p);
-  p->state = kPodTombstone;
-  --hdr_->shard_live[s];
-  ++hdr_->shard_tomb[s];
+  erase_pod_locked(s, p);
   --n->n_pods;
   bump(n, touched);
   hdr_->n_pods.fetch_sub(1);
