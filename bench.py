@@ -108,6 +108,8 @@ def parse_args():
     ap.add_argument("--apiserver-spin-us", type=float, default=0.0,
                     help="the shared API server's IO threads poll this long after their last event before "
                          "sleeping (a diagnostic: are a burst's first answers slow because its cores slept?)")
+    ap.add_argument("--apiserver-history", type=int, default=0,
+                    help="the shared API server's watch cache, events per kind (0: 65536)")
     ap.add_argument("--apiserver-threads", type=int, default=0,
                     help="shared API server IO threads (0: one per rank, 4 to 16)")
     ap.add_argument("--bind-writer-threads", type=int, default=0,
@@ -618,11 +620,10 @@ def apiserver_main(conn, avoid: list[int] | None = None, near: int = -1) -> None
                 srv.stop()
             steps.clear()
             keys.clear()
-            # watch cache: 16k events per kind. A burst makes about 4k (create, bind, label,
-            # delete), so the warm-up steps fill it and every timed step runs in the steady
-            # state, evicting as many old versions as it adds (with 64k the first ~16 steps
-            # evicted nothing and ran faster than the ones after them: profiles/soak_r05.md)
-            srv = core().ApiServer("127.0.0.1", 0, msg[1], 1 << 14)
+            # watch cache: 64k events per kind (--apiserver-history). A burst makes about 4k
+            # (create, bind, label, delete): from the ~16th step on every event evicts an old
+            # version, freed under the store's lock (profiles/soak_r05.md)
+            srv = core().ApiServer("127.0.0.1", 0, msg[1], msg[5] if len(msg) > 5 and msg[5] else 1 << 16)
             srv.set_latency(msg[2])
             if len(msg) > 4 and msg[4] > 0:
                 srv.set_spin(msg[4])
@@ -863,8 +864,9 @@ class ApiServerProc:
         self.conn.send(msg)
         return self.conn.recv()
 
-    def start(self, threads: int, latency_s: float = 0.0, keep_heap: bool = False, spin_s: float = 0.0) -> str:
-        port, self.cpus = self._rpc("start", threads, latency_s, keep_heap, spin_s)
+    def start(self, threads: int, latency_s: float = 0.0, keep_heap: bool = False, spin_s: float = 0.0,
+              history: int = 0) -> str:
+        port, self.cpus = self._rpc("start", threads, latency_s, keep_heap, spin_s, history)
         self.url = f"http://127.0.0.1:{port}"
         return self.url
 
@@ -1066,7 +1068,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         if d.rank == 0:
             apisrv = api_proc
             url = apisrv.start(args.apiserver_threads or min(16, max(4, d.world)), args.api_rtt_ms / 1e3,
-                               args.apiserver_keep_heap, args.apiserver_spin_us / 1e6)
+                               args.apiserver_keep_heap, args.apiserver_spin_us / 1e6, args.apiserver_history)
             if getattr(args, "_placement", None):
                 args._placement["apiserver"] = list(apisrv.cpus)
             apisrv.add_nodes(nodes)
