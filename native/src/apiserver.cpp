@@ -416,6 +416,14 @@ struct Ev {
   std::shared_ptr<const std::string> line;   // {"type":..,"object":..}\n
 };
 
+// Versions a thread's writes evicted from the watch history (a full history evicts one per
+// event: its text, its parsed tree, a few hundred frees). They are freed by the same thread
+// once it has left the store's lock (release_evicted), not while every other request waits on
+// that lock: a soak of 300 bursts had its bulk creates 60 % slower once the history was full.
+thread_local std::vector<Ev> tl_evicted;
+
+void release_evicted() { tl_evicted.clear(); }
+
 std::shared_ptr<const std::string> ev_line(const char* type, const std::string& obj_json) {
   auto s = std::make_shared<std::string>();
   s->reserve(obj_json.size() + 32);
@@ -545,7 +553,10 @@ struct Server::Impl {
     }
     auto& h = hist[kind];
     h.push_back(std::move(e));
-    while (h.size() > cfg.history) h.pop_front();
+    while (h.size() > cfg.history) {
+      tl_evicted.push_back(std::move(h.front()));   // freed after the lock (release_evicted)
+      h.pop_front();
+    }
   }
 
   // -- pods
@@ -736,11 +747,14 @@ struct Server::Impl {
 
   std::pair<int, std::string> handle(const Req& r) {
     n_requests.fetch_add(1, std::memory_order_relaxed);
+    std::pair<int, std::string> out;
     try {
-      return route(r);
+      out = route(r);
     } catch (const ApiErr& e) {
-      return {e.code, status_body(e.code, e.reason, e.message)};
+      out = {e.code, status_body(e.code, e.reason, e.message)};
     }
+    release_evicted();   // no lock held here
+    return out;
   }
 
   std::pair<int, std::string> route(const Req& r) {
@@ -1452,18 +1466,21 @@ std::vector<int> Server::create_pods(const std::vector<std::string>& texts, int 
     }
   });
   const auto t1 = std::chrono::steady_clock::now();
-  std::lock_guard<std::mutex> g(impl_->mu);
-  for (size_t i = 0; i < texts.size(); ++i) {
-    if (codes[i] != 201) continue;
-    try {
-      if (fast[i].ok) impl_->create_fast_locked(fast[i]);
-      else impl_->create_pod_locked(std::move(vs[i]), "");
-      impl_->n_create.fetch_add(1, std::memory_order_relaxed);
-    } catch (const ApiErr& e) {
-      codes[i] = e.code;
+  {
+    std::lock_guard<std::mutex> g(impl_->mu);
+    for (size_t i = 0; i < texts.size(); ++i) {
+      if (codes[i] != 201) continue;
+      try {
+        if (fast[i].ok) impl_->create_fast_locked(fast[i]);
+        else impl_->create_pod_locked(std::move(vs[i]), "");
+        impl_->n_create.fetch_add(1, std::memory_order_relaxed);
+      } catch (const ApiErr& e) {
+        codes[i] = e.code;
+      }
     }
+    impl_->flush_now();
   }
-  impl_->flush_now();
+  release_evicted();
   const auto t2 = std::chrono::steady_clock::now();
   auto ns = [](auto d) { return static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(d).count()); };
   impl_->bulk_parse_ns.fetch_add(ns(t1 - t0), std::memory_order_relaxed);
@@ -1473,12 +1490,15 @@ std::vector<int> Server::create_pods(const std::vector<std::string>& texts, int 
 
 int Server::delete_pods(const std::vector<std::pair<std::string, std::string>>& keys) {
   const auto t0 = std::chrono::steady_clock::now();
-  std::lock_guard<std::mutex> g(impl_->mu);
-  // serial: measured on the box, building the final versions on several threads was slower
-  // than one thread (allocator contention outweighs ~1 us of work per pod)
   int n = 0;
-  for (const auto& k : keys) n += impl_->delete_pod_locked(k.first, k.second) ? 1 : 0;
-  impl_->flush_now();
+  {
+    std::lock_guard<std::mutex> g(impl_->mu);
+    // serial: measured on the box, building the final versions on several threads was slower
+    // than one thread (allocator contention outweighs ~1 us of work per pod)
+    for (const auto& k : keys) n += impl_->delete_pod_locked(k.first, k.second) ? 1 : 0;
+    impl_->flush_now();
+  }
+  release_evicted();
   impl_->n_delete.fetch_add(static_cast<uint64_t>(keys.size()), std::memory_order_relaxed);
   impl_->bulk_delete_ns.fetch_add(
       static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count()),
