@@ -1453,6 +1453,8 @@ void parallel_for(size_t n, size_t workers, size_t min_parallel, Fn&& fn) {
 }
 }  // namespace
 
+constexpr size_t kBulkChunk = 128;   // pods a bulk create / delete writes per hold of the store's lock
+
 std::vector<int> Server::create_pods(const std::vector<std::string>& texts, int threads) {
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<FastCreate> fast(texts.size());
@@ -1466,21 +1468,25 @@ std::vector<int> Server::create_pods(const std::vector<std::string>& texts, int 
     }
   });
   const auto t1 = std::chrono::steady_clock::now();
-  {
-    std::lock_guard<std::mutex> g(impl_->mu);
-    for (size_t i = 0; i < texts.size(); ++i) {
-      if (codes[i] != 201) continue;
-      try {
-        if (fast[i].ok) impl_->create_fast_locked(fast[i]);
-        else impl_->create_pod_locked(std::move(vs[i]), "");
-        impl_->n_create.fetch_add(1, std::memory_order_relaxed);
-      } catch (const ApiErr& e) {
-        codes[i] = e.code;
+  // in chunks: the store's lock is let go (and what the chunk evicted freed) every kBulkChunk
+  // pods, so a bind or a label patch waits for one chunk, not for the whole burst
+  for (size_t b = 0; b < texts.size(); b += kBulkChunk) {
+    {
+      std::lock_guard<std::mutex> g(impl_->mu);
+      for (size_t i = b; i < std::min(texts.size(), b + kBulkChunk); ++i) {
+        if (codes[i] != 201) continue;
+        try {
+          if (fast[i].ok) impl_->create_fast_locked(fast[i]);
+          else impl_->create_pod_locked(std::move(vs[i]), "");
+          impl_->n_create.fetch_add(1, std::memory_order_relaxed);
+        } catch (const ApiErr& e) {
+          codes[i] = e.code;
+        }
       }
+      impl_->flush_now();
     }
-    impl_->flush_now();
+    release_evicted();
   }
-  release_evicted();
   const auto t2 = std::chrono::steady_clock::now();
   auto ns = [](auto d) { return static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(d).count()); };
   impl_->bulk_parse_ns.fetch_add(ns(t1 - t0), std::memory_order_relaxed);
@@ -1491,14 +1497,18 @@ std::vector<int> Server::create_pods(const std::vector<std::string>& texts, int 
 int Server::delete_pods(const std::vector<std::pair<std::string, std::string>>& keys) {
   const auto t0 = std::chrono::steady_clock::now();
   int n = 0;
-  {
-    std::lock_guard<std::mutex> g(impl_->mu);
-    // serial: measured on the box, building the final versions on several threads was slower
-    // than one thread (allocator contention outweighs ~1 us of work per pod)
-    for (const auto& k : keys) n += impl_->delete_pod_locked(k.first, k.second) ? 1 : 0;
-    impl_->flush_now();
+  // serial: measured on the box, building the final versions on several threads was slower
+  // than one thread (allocator contention outweighs ~1 us of work per pod); in chunks, as the
+  // bulk create
+  for (size_t b = 0; b < keys.size(); b += kBulkChunk) {
+    {
+      std::lock_guard<std::mutex> g(impl_->mu);
+      for (size_t i = b; i < std::min(keys.size(), b + kBulkChunk); ++i)
+        n += impl_->delete_pod_locked(keys[i].first, keys[i].second) ? 1 : 0;
+      impl_->flush_now();
+    }
+    release_evicted();
   }
-  release_evicted();
   impl_->n_delete.fetch_add(static_cast<uint64_t>(keys.size()), std::memory_order_relaxed);
   impl_->bulk_delete_ns.fetch_add(
       static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count()),
