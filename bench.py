@@ -1406,17 +1406,11 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     handoffs0 = fe_stats().get("bind_handoffs", 0)
     py0 = fe_stats().get("python", {}).get("count", 0)
     prio0 = fe_stats().get("priorities", {}).get("count", 0)
-    hc.s = 0.0
-    cpu0, loop_cpu0 = time.process_time(), time.thread_time()
-    threads0, ticks0, times0 = thread_cpu(), thread_ticks(), os.times()
     from nanogpu import affinity
 
-    snap0 = affinity.cpu_snapshot()
-    t0 = time.perf_counter()
-    if sampler is not None:
-        sampler.on.set()
     # other tenants moving onto the rank's domain mid-run: checked every 0.1 s by a harness
     # thread, the job moves to a quieter domain when they keep half a CPU or more of it busy
+    # (set up before the clock and the CPU snapshots)
     monitor = None
     if d.world == 1 and getattr(args, "_placement", None) and not getattr(args, "no_relocate", False):
         pl = args._placement
@@ -1430,6 +1424,13 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
             api_watch.check()
             results["foreign_cpus_api"] = []
         monitor = ContentionMonitor(watch, api_watch, pl, results)
+    hc.s = 0.0
+    cpu0, loop_cpu0 = time.process_time(), time.thread_time()
+    threads0, ticks0, times0 = thread_cpu(), thread_ticks(), os.times()
+    snap0 = affinity.cpu_snapshot()
+    t0 = time.perf_counter()
+    if sampler is not None:
+        sampler.on.set()
     for k, s in enumerate(timed_ids):
         r = await one_step(s, True, timed_ids[k + 1] if k + 1 < len(timed_ids) else None)
         results["steps"].append(r["stats"])
@@ -1439,18 +1440,23 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
             monitor.steps_done = k + 1
         if k % 100 == 99 and d.rank == 0:   # a long run's heartbeat (one line per 100 steps)
             print(f"bench: {k + 1} timed steps", file=sys.stderr, flush=True)
-    if monitor is not None:
-        monitor.close()
-    take_binds()
-    spent.clear()
-    results["rss_mib"].append(rss_mib())
-    if sampler is not None:
-        sampler.report(args.stall_trace)
     if io_tally:
         from nanogpu import _native
 
         _native.io_tally_enable(False)
         results["io_tally"] = _native.io_tally()
+    await barrier()
+    d.sync()
+    elapsed = time.perf_counter() - t0
+    # the clock has stopped: the harness's own records from here (off the timed steps)
+    with hc:
+        if monitor is not None:
+            monitor.close()
+        take_binds()
+        spent.clear()
+        results["rss_mib"].append(rss_mib())
+    if sampler is not None:
+        sampler.report(args.stall_trace)
     if native_prof:
         from nanogpu import _native
         from nanogpu.obs import cpu_profile
@@ -1464,9 +1470,6 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         buf = io.StringIO()
         pstats.Stats(prof, stream=buf).sort_stats(os.environ.get("NANOGPU_PROF_SORT", "tottime")).print_stats(45)
         Path(args.profile_out).write_text(buf.getvalue())
-    await barrier()
-    d.sync()
-    elapsed = time.perf_counter() - t0
     # how busy this rank's cores, their SMT siblings, the API server's and the whole host were
     # while the clock ran (other tenants on the siblings slow every hand-off)
     mine = sorted(os.sched_getaffinity(0))
