@@ -254,12 +254,16 @@ class ClusterState:
         demand, _ = pu.ledger_view(full)
         ids = self.node_ids(node_names)
         rcs = self.ledger.filter(ids, demand, self.options)
+        wants = self.nominate and pu.pod_uid(pod) and any(p > 0 or m > 0 for p, m in demand)
         if self.decisive_filter and any(rc == N.OK for rc in rcs):
             scores = self.ledger.score(ids, demand, self.options)
             pick = self._top_pick(pu.pod_uid(pod), scores, rcs)
-            if self.nominate and pu.pod_uid(pod) and any(p > 0 or m > 0 for p, m in demand):
+            if wants:
                 self.ledger.nominate(ids[pick], pu.pod_uid(pod), demand, self.options)
             rcs = [rc if rc != N.OK or k == pick else None for k, rc in enumerate(rcs)]
+        elif wants and sum(1 for rc in rcs if rc == N.OK) == 1:
+            # one fitting node: kube-scheduler binds it without a priorities call (frontend.cpp)
+            self.ledger.nominate(ids[rcs.index(N.OK)], pu.pod_uid(pod), demand, self.options)
         ok, failed = [], {}
         for name, nid, rc in zip(node_names, ids, rcs):
             if rc is None:    # fits, not the decisive pick: neither answered nor failed

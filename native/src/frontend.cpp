@@ -1906,14 +1906,28 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     }
     // decisive: the node priorities would rank first is the only one answered (and nominated)
     const int64_t pick = decisive ? top_pick(scores, rcs, uid) : -1;
-    if (pick >= 0 && nominate && !uid.empty() && wants_devices(dem)) {
+    // one fitting node: kube-scheduler binds it without a priorities call, so the filter
+    // nominates it (otherwise the pod is invisible to the next filters until its bind reserves)
+    int64_t only = -1;
+    if (!decisive && nominate && !o.compat) {
+      for (size_t i = 0; i < ids.size(); ++i) {
+        if (rcs[i] != kOk) continue;
+        if (only >= 0) {
+          only = -1;
+          break;
+        }
+        only = static_cast<int64_t>(i);
+      }
+    }
+    const int64_t nom = pick >= 0 ? pick : only;
+    if (nom >= 0 && nominate && !uid.empty() && wants_devices(dem)) {
       if (s.defer && last.valid && uid.data() == last.uid.data()) {
         s.defer_nominate = true;
-        s.defer_node = ids[pick];
+        s.defer_node = ids[nom];
         s.defer_dem = dem;
       } else {
         IoTimer it{kFeVerbNominate};
-        ledger_->nominate(ids[pick], uid, dem, o);
+        ledger_->nominate(ids[nom], uid, dem, o);
       }
       s.nom_dropped = false;
     }

@@ -385,6 +385,7 @@ def test_status_dumps_the_plan_cache_valid_at_the_current_generation():
     store = FakeKubeStore()
     store.add_node(node("n0", 2))
     st, ext = _ext(store)
+    st.nominate = False   # (a one-node filter nominates: the node would change under the dump)
     p = store.create_pod(pu.make_pod("a", [("c", 30)]))
     ext.filter({"Pod": p, "NodeNames": ["n0"]})
     big = store.create_pod(pu.make_pod("b", [("c", 100), ("d", 100), ("e", 100)]))

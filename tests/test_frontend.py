@@ -239,8 +239,9 @@ def test_native_quantity_matches_python(q, mib):
 
 
 def test_native_prepared_bind_and_its_error_text():
+    # (no nominations: with them the late pod's one-node filter would hold its GPU for its bind)
     async def main():
-        store, rt = await _runtime(1)
+        store, rt = await _runtime(1, nominate=False)
         loop = asyncio.get_running_loop()
         try:
             big = store.create_pod(pu.make_pod("big", [("c", 100)] * 8))     # fills the node
@@ -493,6 +494,41 @@ def test_decisive_filter_takes_one_round_trip_a_pod_through_the_standin():
                     k = (pu.node_name_of(p), pu.container_assignment(p, "c")[0])
                     used[k] = used.get(k, 0) + pu.pod_demand(p)[0][0]
             assert max(used.values()) <= 100
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
+
+
+def test_a_filter_with_one_fitting_node_nominates_it():
+    """kube-scheduler binds a pod whose filter left one node without calling priorities: that
+    filter nominates the node (native and Python alike), so the next pods' filters see the pod
+    before its bind lands; with two fitting nodes the filter nominates nothing."""
+    async def main():
+        store, rt = await _runtime(2)
+        ext, led = rt.extender, rt.state.ledger
+        loop = asyncio.get_running_loop()
+        try:
+            a = store.create_pod(pu.make_pod("one", [("c", 30)]))
+            res = await loop.run_in_executor(None, _http, rt.bound_port, [
+                ("POST", "/scheduler/filter", _dumps({"Pod": a, "NodeNames": ["n1"]}))])
+            assert json.loads(res[0][1])["NodeNames"] == ["n1"]
+            rec = led.lookup(pu.pod_uid(a))
+            assert rec["state"] == "nominated" and rec["node"] == rt.state.node_entry("n1").id
+            b = store.create_pod(pu.make_pod("two", [("c", 30)]))
+            await loop.run_in_executor(None, _http, rt.bound_port, [
+                ("POST", "/scheduler/filter", _dumps({"Pod": b, "NodeNames": ["n0", "n1"]}))])
+            assert led.lookup(pu.pod_uid(b)) is None
+            # the Python verb does the same
+            c = store.create_pod(pu.make_pod("three", [("c", 30)]))
+            ext.filter({"Pod": c, "NodeNames": ["n0"]})
+            assert led.lookup(pu.pod_uid(c))["state"] == "nominated"
+            # and the bind adopts the nomination
+            m = pu.meta(a)
+            res = await loop.run_in_executor(None, _http, rt.bound_port, [
+                ("POST", "/scheduler/bind", _dumps({"PodName": m["name"], "PodNamespace": "default",
+                                                    "PodUID": m["uid"], "Node": "n1"}))])
+            assert res[0] == (200, b'{"Error":""}') and led.lookup(pu.pod_uid(a))["state"] == "committed"
         finally:
             await rt.stop()
 
