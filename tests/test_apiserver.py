@@ -240,6 +240,46 @@ def test_native_bulk_create_delete_and_timeout_ends_the_stream():
         srv.stop()
 
 
+def test_native_bulk_writes_in_chunks_keep_every_pod_and_event():
+    """Bulk create / delete take the store's lock 128 pods at a time (a bind waits for one
+    chunk): a 300-pod burst still lands whole, a watcher sees each pod's ADDED and DELETED once,
+    in resourceVersion order, and a small watch cache evicting under them loses nothing live."""
+    import socket
+    import threading
+
+    srv = N.ApiServer("127.0.0.1", 0, 2, 256)
+    got = bytearray()
+    s = socket.create_connection(("127.0.0.1", srv.port))
+    try:
+        s.sendall(b"GET /api/v1/pods?watch=true&resourceVersion=0 HTTP/1.1\r\nHost: x\r\n\r\n")
+
+        def reader():
+            while True:
+                b = s.recv(1 << 20)
+                if not b:
+                    return
+                got.extend(b)
+
+        threading.Thread(target=reader, daemon=True).start()
+        pods = [json.dumps(pu.make_pod(f"c{i}", [("main", 10)], namespace="k")) for i in range(300)]
+        assert srv.create_pods(pods) == [201] * 300
+        code, body = srv.call("GET", "/api/v1/namespaces/k/pods")
+        assert code == 200 and len(json.loads(body)["items"]) == 300
+        assert srv.delete_pods([("k", f"c{i}") for i in range(300)]) == 300
+        import time
+
+        end = time.time() + 5
+        while got.count(b'"type":"DELETED"') < 300 and time.time() < end:
+            time.sleep(0.02)
+        assert got.count(b'"type":"ADDED"') == 300 and got.count(b'"type":"DELETED"') == 300
+        rvs = [int(x) for x in __import__("re").findall(rb'"resourceVersion":"(\d+)"', bytes(got))]
+        assert rvs == sorted(rvs)
+        assert json.loads(srv.stats())["pods"] == 0
+    finally:
+        s.close()
+        srv.stop()
+
+
 def test_native_spinning_io_threads_still_answer_and_stop():
     """set_spin (bench --apiserver-spin-us, a diagnostic): IO threads poll for a window after
     their last event instead of sleeping; requests over HTTP are answered, timeouts and watch
