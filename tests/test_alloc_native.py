@@ -473,6 +473,31 @@ def test_holds_any_matches_lookup_over_a_key_list():
     assert not L.holds_any(keys) and all(L.lookup(k) is None for k in keys)
 
 
+@settings(max_examples=60, deadline=None)
+@given(st.lists(st.tuples(st.booleans(), st.integers(0, 199)), min_size=50, max_size=600))
+def test_pod_table_stays_exact_under_churn_with_tombstone_cleanup(ops):
+    """The pod table is open addressing with linear probing per shard: a freed slot becomes
+    empty when the next one is (with the dead tombstones before it), and a shard rehashes once
+    tombstones are a quarter of it. Over any reserve / release sequence on a table small enough
+    to collide constantly (4 slots a shard: chains wrap round), every key is found exactly when
+    it is held (a full shard refuses the reserve; the model follows)."""
+    L = N.Ledger("", 2, 256, True)
+    nid = L.upsert_node("n0", synthetic_mi355x(8).ledger_devices(False), synthetic_mi355x(8).ledger_topo())
+    live = set()
+    for add, k in ops:
+        key = f"p{k}"
+        if add and key not in live:
+            if L.reserve(nid, key, [(0, 0)], BIN)[0] == N.OK:
+                live.add(key)
+        elif not add and key in live:
+            assert L.release(key) == N.OK
+            live.discard(key)
+    for k in range(200):
+        key = f"p{k}"
+        assert (L.lookup(key) is not None) == (key in live), key
+    assert L.holds_any(sorted(live)) == bool(live) and L.n_pods == len(live)
+
+
 # ----------------------------------------------------------------------------- memo re-validation
 _share = st.tuples(st.sampled_from([5, 10, 25, 50, 100]), st.sampled_from([0, 0, 8192, 32768, 100 * 1024]),
                    st.sampled_from([0, 0, 1]))
