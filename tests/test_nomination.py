@@ -76,7 +76,8 @@ def test_wrong_nominations_are_counted_and_raise_the_margin():
 
 def test_a_wrong_nomination_never_blocks_a_pod_after_its_ttl():
     async def main():
-        store, rt = await _runtime(2, nomination_ttl_s=0.2)
+        # (a TTL of 1 s: a slow shared host must not expire it between two requests)
+        store, rt = await _runtime(2, nomination_ttl_s=1.0)
         loop = asyncio.get_running_loop()
         try:
             # n0 has one 40 % hole left on its last GPU; n1 is empty
@@ -98,7 +99,7 @@ def test_a_wrong_nomination_never_blocks_a_pod_after_its_ttl():
             res = await loop.run_in_executor(None, _http, rt.bound_port, [
                 ("POST", "/scheduler/filter", _dumps({"Pod": b, "NodeNames": both}))])
             assert json.loads(res[0][1])["NodeNames"] == ["n1"]           # held for a while...
-            assert await wait_for(lambda: rt.state.ledger.lookup(pu.pod_uid(a)) is None, timeout=3)
+            assert await wait_for(lambda: rt.state.ledger.lookup(pu.pod_uid(a)) is None, timeout=6)
             res = await loop.run_in_executor(None, _http, rt.bound_port, [
                 ("POST", "/scheduler/filter", _dumps({"Pod": b, "NodeNames": both}))])
             assert json.loads(res[0][1])["NodeNames"] == both             # ...never longer than the TTL
