@@ -451,13 +451,15 @@ def test_streaming_tenant_drives_mem_busy_percent_over_the_hot_threshold(busy):
     """The signal behind Device::mem_hot: while the HBM copy streams on the whole GPU, the mean
     of every sample of amdgpu's mem_busy_percent (exported by the agent as
     nanogpu_device_mem_busy_percent and polled as gpu_hbm_activity_avg), and the mean of
-    samples 5 s apart like Prometheus scrapes, are at or above types.HBM_HOT_THRESHOLD."""
+    samples 1 s apart like scrapes, are at or above types.HBM_HOT_THRESHOLD. (Samples 5 s
+    apart are one reading in a 6 s run: a single instantaneous value, 19 % on one box whose
+    mean was 33 %, says nothing about the average the poller reads.)"""
     from nanogpu import types as T
 
     s = busy["stream100"]
     assert s["rate"] > 1000, s                      # GB/s: the copy really streamed
     assert s["mean_all"] >= 100 * T.HBM_HOT_THRESHOLD, s
-    assert s["mean_5s"] >= 100 * T.HBM_HOT_THRESHOLD, s
+    assert s["mean_1s"] >= 100 * T.HBM_HOT_THRESHOLD, s
 
 
 def test_compute_bound_tenant_stays_under_the_hot_threshold(busy):
@@ -469,7 +471,7 @@ def test_compute_bound_tenant_stays_under_the_hot_threshold(busy):
     m = busy["mfma100"]
     assert m["rate"] > 500, m                       # TFLOP/s: the burn really ran
     assert m["mean_all"] < 100 * T.HBM_HOT_THRESHOLD, m
-    assert m["mean_5s"] < 100 * T.HBM_HOT_THRESHOLD, m
+    assert m["mean_1s"] < 100 * T.HBM_HOT_THRESHOLD, m
 
 
 def test_share_aware_learner_learns_a_lone_25pct_streamer_not_a_lone_75pct_mfma_tenant(busy):
