@@ -562,18 +562,13 @@ STEADY_CHURN = 0.3
 STEADY_SEED = 11
 
 
-def steady_uid(key: int, rank: int) -> str:
-    import uuid
-
-    return str(uuid.UUID(int=(0x57EAD << 96) | (rank << 48) | key))
-
-
-def steady_pod(spec, rank: int) -> dict:
-    """A pod of the steady-state stream (nanogpu.sim.workload.steady), handled by rank
-    key % world: it lives across steps until the stream deletes it."""
+def steady_pod(spec, rank: int = 0) -> dict:
+    """A pod of the steady-state stream (nanogpu.sim.workload.steady): it lives across steps
+    until the stream deletes it. Its name, namespace and UID do not depend on the rank count
+    (workload.steady_pod): N workers replay the 1-worker stream."""
     from nanogpu.sim import workload as W
 
-    return W.make_pod(spec, f"k{spec.key}", f"bench-r{rank}", steady_uid(spec.key, rank))
+    return W.steady_pod(spec)
 
 
 def steady_stream(args):
@@ -1028,6 +1023,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     from nanogpu.k8s import podutil as pu
     from nanogpu.k8s.fake_apiserver import Faults, FakeKubeStore, InProcKube
     from nanogpu.sim.driver import FastExtenderClient, SchedulerDriver, node_capacities
+    from nanogpu.sim import workload as W
 
     # --shared-api: ONE API server for the job, as in a cluster: the native API server in its
     # own process (ApiServerProc), reached over HTTP by every rank's extender. Only rank 0 runs
@@ -1184,10 +1180,10 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         phases: dict = {}
         if apisrv is not None:
             (n_d, dt_d), (n_c, dt_c) = await apisrv.churn_keys(
-                [(f"bench-r{k % d.world}", f"k{k}") for k in dels], step)
+                [(W.STEADY_NAMESPACE, f"k{k}") for k in dels], step)
             phases.update(delete_srv_ms=1e3 * dt_d, create_srv_ms=1e3 * dt_c)
         with hc:
-            uids = [steady_uid(k, k % d.world) for k in dels]
+            uids = [W.steady_uid(k) for k in dels]
         if uids:
             await wait_released(rt.state.ledger, uids)
         phases["release_ms"] = 1e3 * (time.perf_counter() - t_step0)
@@ -1571,7 +1567,7 @@ HEADLINE_LAST = ("value_independent_schedulers", "frag_pct_steady_reference_mode
 DIAG_KEYS = ("step_diag_rank0", "bind_hops_us_by_decile_rank0", "io_per_pod_rank0", "controller_keys_per_pod_rank0", "python_requests_per_pod_rank0", "schedule_ms_each_step_rank0", "phase_ms_per_step_rank0",
              "extender_cpu_us_per_pod_by_thread_rank0", "extender_kernel_pct_by_thread_rank0",
              "extender_cpu_us_per_pod_user_kernel_rank0", "frag_pct_steady_each_step", "nominations",
-             "nominations_steady", "native_verb_mean_us", "frag_reference_model_source", "host_selection",
+             "nominations_steady", "frag_pct_steady_native_replay_each_step", "native_verb_mean_us", "frag_reference_model_source", "host_selection",
              "one_scheduler_config", "steady_config", "cpu_layout")
 
 
@@ -2028,16 +2024,21 @@ def steady_keys(args, topo, v) -> dict:
                              + ("; one kube-scheduler stand-in, binds over every rank's worker"
                                 if getattr(s_args, "one_scheduler", False) else "")}
     if args.partition == "SPX" and args.policy == "binpack" and not args.compat:
+        from nanogpu import types as T
         from nanogpu.sim import fragsim
 
         hbm = topo.devices[0].hbm_mib if topo.devices else 288 * 1024
         n_steps = 1 + s_args.warmup + s_args.steps
         kw = dict(steps=n_steps, nodes=s_args.nodes, hbm_mib=hbm, initial=s_args.pods, churn=STEADY_CHURN,
-                  seed=STEADY_SEED, kube=True, first=1 + s_args.warmup + s_args.steps // 2)
-        ref, nat = fragsim.steady_state(True, **kw), fragsim.steady_state(False, **kw)
+                  seed=STEADY_SEED, first=1 + s_args.warmup + s_args.steps // 2)
+        ref = fragsim.steady_state(True, kube=True, **kw)
+        # the extender's own verbs replayed offline on the same stream (fragsim.steady_protocol):
+        # with the priorities lead the live run matches it step for step at any worker count
+        nat = fragsim.steady_protocol(0, lead=T.PRIORITY_LEAD, **kw)
         keys.update(frag_pct_steady_reference_model=ref["frag_pct"],
                     frag_hbm_pct_steady_reference_model=ref["frag_hbm_pct"],
-                    frag_pct_steady_native_replay=nat["frag_pct"])
+                    frag_pct_steady_native_replay=nat["frag_pct"],
+                    frag_pct_steady_native_replay_each_step=nat["frag_pct_each_step"][1 + s_args.warmup:])
     return keys
 
 

@@ -65,6 +65,7 @@ class Config:
     reservation_ttl_s: float = 60.0
     nominate: bool = True              # priorities nominate the top node (Ledger::nominate)
     decisive_filter: bool = False      # filter answers only the top node (one round trip a pod)
+    priority_lead: int = T.PRIORITY_LEAD   # priorities: the nominated node's lead (0: off)
     nomination_ttl_s: float = 5.0
     policy_reload_s: float = 3.0
     fake_cluster: int = 0                       # >0: serve against an in-process fake cluster of N nodes
@@ -107,7 +108,8 @@ class Runtime:
             topo_weight=cfg.topology_weight, seed=cfg.seed, ledger_path=cfg.ledger_path,
             max_nodes=cfg.max_nodes, max_pods=cfg.max_pods, track_hbm=cfg.track_hbm,
             node_source=self._node_from_cache, score_normalize=cfg.score_normalize, nominate=cfg.nominate,
-            request_sizes=cfg.request_sizes, learn_sizes=cfg.learn_sizes, decisive_filter=cfg.decisive_filter)
+            request_sizes=cfg.request_sizes, learn_sizes=cfg.learn_sizes, decisive_filter=cfg.decisive_filter,
+            priority_lead=cfg.priority_lead)
         self.metrics = Metrics()
         self.tracer = Tracer()
         self.extender: Extender | None = None

@@ -96,6 +96,11 @@ def build_parser() -> argparse.ArgumentParser:
                    help="filter answers only the node priorities would rank first (and nominates it): "
                         "kube-scheduler then skips scoring and the priorities call, one round trip a pod; "
                         "its own score plugins have no say (off: every fitting node, as the reference)")
+    p.add_argument("--priority-lead", type=int, default=T.PRIORITY_LEAD,
+                   help="priorities answer the nominated node this many points above every other fitting node "
+                        "(normalised scores: 10 and 0), so kube-scheduler's own score plugins (about 800 points "
+                        "between nodes at most, against 10 x the extender's score) bind the pod where the ledger "
+                        "holds it; 0: raw scores, as the reference")
     p.add_argument("--fake-cluster", type=int, default=0, help="serve against N in-process fake MI355X nodes")
     p.add_argument("--fake-gpus-per-node", type=int, default=8)
     p.add_argument("--fake-partition", default="SPX", choices=["SPX", "DPX", "QPX", "CPX"])
@@ -150,7 +155,7 @@ def parse(argv: list[str] | None = None) -> Config:
         native_pod_watch=not a.no_native_pod_watch, assume_label=not a.no_assume_label,
         api_write_timeout_s=parse_duration(a.api_write_timeout), bind_first=a.bind_first, spin_nap=a.spin_nap, spin_recv=a.spin_recv, batch_labels=a.batch_labels, reservation_ttl_s=parse_duration(a.reservation_ttl),
         nominate=not a.no_nominate, nomination_ttl_s=parse_duration(a.nomination_ttl),
-        decisive_filter=a.decisive_filter,
+        decisive_filter=a.decisive_filter, priority_lead=a.priority_lead,
         fake_cluster=a.fake_cluster, fake_gpus_per_node=a.fake_gpus_per_node, fake_partition=a.fake_partition,
         seed=a.seed, frontend=a.frontend, frontend_threads=max(1, a.frontend_threads), busy_poll_us=a.busy_poll_us,
         busy_poll_prio_us=a.busy_poll_prio_us, lazy_label_answers=a.lazy_label_answers,

@@ -263,7 +263,8 @@ class NativeServer:
 
     def sync_options(self) -> None:
         st = self.router.ext.state
-        self.fe.set_options(st.options, bool(st.score_normalize), bool(st.nominate), bool(st.decisive_filter))
+        self.fe.set_options(st.options, bool(st.score_normalize), bool(st.nominate), bool(st.decisive_filter),
+                            int(st.priority_lead))
 
     def start(self) -> None:
         self._loop = asyncio.get_running_loop()

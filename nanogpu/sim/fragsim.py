@@ -154,6 +154,114 @@ def steady_state(compat: bool, steps: int = 20, nodes: int = 64, hbm_mib: int = 
     return summarize(out[len(out) // 2 if first is None else first:], c)
 
 
+def steady_protocol(lag: int, lead: int = 0, steps: int = 9, nodes: int = 64, hbm_mib: int = 294_896,
+                    initial: int = 1000, churn: float = 0.3, seed: int = 11, first: int | None = None,
+                    nominate: bool = True) -> dict:
+    """The steady-churn stream through the extender's own verbs (the native front door's filter
+    and priorities, with their nominations, Frontend.verb) and kube-scheduler's model, with every
+    bind reserving `lag` scheduling cycles after its own: kube-scheduler starts the next pod's
+    cycle without waiting for a bind (binding is asynchronous there), so its next filters can
+    reach the extender before the bind does. In a deployment `lag` is set by timing (which worker
+    the bind reaches, how soon its thread runs); here it is fixed, so the replay is exact and a
+    policy's sensitivity to it is measured, not sampled. `lead`: Frontend.set_options(lead=...)
+    (nanogpu.types.PRIORITY_LEAD). frag is averaged over the steps from `first` (default: the
+    second half), as steady_state; also the nominations made / adopted / moved."""
+    import collections
+    from collections import deque
+
+    from nanogpu.sim.driver import owner_index
+
+    topo = synthetic_mi355x(8, "SPX", hbm_mib=hbm_mib)
+    L = N.Ledger("", max(64, nodes), 1 << 16, True)
+    names = [f"n{i:03d}" for i in range(nodes)]
+    index = {n: i for i, n in enumerate(names)}
+    ids = [L.upsert_node(n, topo.ledger_devices(True), topo.ledger_topo()) for n in names]
+    opts = N.Options(N.Policy.BINPACK)
+    fe = N.Frontend(L, "127.0.0.1", 0, 1)
+    fe.set_options(opts, False, nominate, False, lead)
+    kube = KubeScoring()
+    kube.rng.seed(seed)
+    cap = 100 * len(topo.devices)
+    pct_used = [0] * nodes
+    requested = [(0, 0)] * nodes
+    owner_cnt: collections.Counter = collections.Counter()
+    live: dict[int, tuple] = {}
+    enc = json.JSONEncoder(separators=(",", ":"))
+    out = []
+    failed = [0]
+    try:
+        for k, st in enumerate(W.steady(steps, initial, churn, seed)):
+            for key in st.deletes:
+                rec = live.pop(key, None)
+                if rec is None:
+                    continue
+                h, need, req, owner, uid = rec
+                L.release(uid)
+                pct_used[h] -= need
+                requested[h] = (requested[h][0] - req[0], requested[h][1] - req[1])
+                if owner >= 0:
+                    owner_cnt[(owner, h)] -= 1
+            pending: deque = deque()
+
+            def bind_oldest() -> None:
+                key, h, dem, uid = pending.popleft()
+                rc, _ = L.reserve(ids[h], uid, dem, opts)
+                if rc in (N.OK, N.OK_EXISTING):
+                    L.commit(uid)
+                    return
+                # the node filled up under it: kube-scheduler's bind fails and the pod goes back
+                # to its queue (counted here, not retried)
+                failed[0] += 1
+                _, need, req, owner, _ = live.pop(key)
+                pct_used[h] -= need
+                requested[h] = (requested[h][0] - req[0], requested[h][1] - req[1])
+                if owner >= 0:
+                    owner_cnt[(owner, h)] -= 1
+
+            for spec in st.creates:
+                pod = W.steady_pod(spec)   # bench.py's steady pods (same UIDs: same tie-breaks)
+                uid = pod["metadata"]["uid"]
+                dem = [(spec.pct, spec.gib * 1024)]
+                req = kube.pod_requests(dem)
+                owner = owner_index(pod)
+                cand = kube.feasible(nodes, lambda i: pct_used[i] + spec.pct <= cap)
+                text = enc.encode(pod)
+
+                def verb(node_list: list[int], prio: bool):
+                    body = '{"Pod":' + text + ',"Nodes":null,"NodeNames":' + enc.encode([names[i] for i in node_list]) + "}"
+                    ok, ans = fe.verb(body.encode(), prio)
+                    assert ok
+                    return json.loads(ans)
+
+                fits = [index[n] for n in verb(cand, False)["NodeNames"]] if cand else []
+                if not fits:
+                    continue
+                host = fits[0]
+                if len(fits) > 1:
+                    sc = {index[e["Host"]]: e["Score"] for e in verb(fits, True)}
+                    spread = spread_scores([owner_cnt.get((owner, i), 0) for i in fits], kube.spread_max_skew) \
+                        if owner >= 0 else [0] * len(fits)
+                    host = fits[kube.select([kube.total(sc[i], requested[i], req, sp) for i, sp in zip(fits, spread)])]
+                pct_used[host] += spec.pct
+                requested[host] = (requested[host][0] + req[0], requested[host][1] + req[1])
+                if owner >= 0:
+                    owner_cnt[(owner, host)] += 1
+                live[spec.key] = (host, spec.pct, req, owner, uid)
+                pending.append((spec.key, host, dem, uid))
+                while len(pending) > lag:
+                    bind_oldest()
+            while pending:
+                bind_oldest()
+            out.append(L.frag(10))
+    finally:
+        fe.stop()
+    res = summarize(out[len(out) // 2 if first is None else first:], None, 0)
+    res["frag_pct_each_step"] = [round(f["frag_pct"], 3) for f in out]
+    res["nominations"] = L.nomination_counts()
+    res["bind_failures"] = failed[0]
+    return res
+
+
 def config5(compat: bool, rounds: int = 5, pods_n: int = 1000, nodes_n: int = 8, sriov: bool = False,
             reps: int = 10, kube: bool = False, **_) -> dict:
     """BASELINE config 5: CPX nodes (or SR-IOV guests), 1000-pod create/delete churn, binpack.

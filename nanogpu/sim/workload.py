@@ -65,6 +65,20 @@ def make_pod(spec: PodSpec, name: str, namespace: str, uid: str) -> dict:
     return p
 
 
+STEADY_NAMESPACE = "bench-steady"
+
+
+def steady_uid(key: int) -> str:
+    """A steady-stream pod's UID: the same whichever worker or rank handles it, so a run with N
+    extender workers replays exactly the stream one worker sees (the UID breaks ties at the top,
+    frontend.cpp top_pick)."""
+    return str(uuid.UUID(int=(0x57EAD << 96) | key))
+
+
+def steady_pod(spec: PodSpec) -> dict:
+    return make_pod(spec, f"k{spec.key}", STEADY_NAMESPACE, steady_uid(spec.key))
+
+
 @dataclass
 class SteadyStep:
     deletes: list[int]          # keys of pods created earlier

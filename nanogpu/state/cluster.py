@@ -60,9 +60,10 @@ class ClusterState:
                  ledger_path: str = "", max_nodes: int = 4096, max_pods: int = 131072,
                  track_hbm: bool = True, node_source: Callable[[str], dict | None] | None = None,
                  score_normalize: bool = False, nominate: bool = True, request_sizes: list[int] | None = None,
-                 learn_sizes: bool = True, decisive_filter: bool = False):
+                 learn_sizes: bool = True, decisive_filter: bool = False, priority_lead: int = T.PRIORITY_LEAD):
         self.ledger = N.Ledger(ledger_path, max_nodes, max_pods, True)
         self._nominate = bool(nominate)
+        self._lead = max(0, int(priority_lead))
         self._decisive = bool(decisive_filter)
         self.track_hbm = track_hbm
         self._listeners: list[Callable[[], None]] = []
@@ -109,6 +110,18 @@ class ClusterState:
     @nominate.setter
     def nominate(self, v: bool) -> None:
         self._nominate = bool(v)
+        self._changed()
+
+    @property
+    def priority_lead(self) -> int:
+        """Priorities answer the nominated node this many points above every other fitting node
+        (normalised scores: 10 and 0), so kube-scheduler's own score plugins do not move the pod
+        off the devices the ledger holds for it (frontend.cpp, priorities). 0: off."""
+        return self._lead
+
+    @priority_lead.setter
+    def priority_lead(self, v: int) -> None:
+        self._lead = max(0, int(v))
         self._changed()
 
     @property
@@ -332,6 +345,14 @@ class ClusterState:
         if (len(top) == 1 and (not rest or best - max(rest) >= margin)
                 and any(p > 0 or m > 0 for p, m in demand)):
             self.ledger.nominate(ids[top[0]], uid, demand, self.options)
+            if self._lead > 0 and rest:
+                # the nominated node leads every other fitting node by `priority_lead`
+                # (normalised: 10 and 0, _normalize maps 100 to 10)
+                scores = list(scores)
+                if self.score_normalize:
+                    scores = [100 if k == top[0] else 0 for k in range(len(scores))]
+                elif best - max(rest) < self._lead:
+                    scores[top[0]] = max(rest) + self._lead
         return scores
 
     def _normalize(self, scores: list[int]) -> list[int]:

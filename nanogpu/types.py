@@ -30,6 +30,12 @@ LEGACY_GPU_NODE_LABEL = ("nvidia-device-enable", "enable")  # controller/node.go
 PRIORITY_RANDOM = "random"        # promised by reference README.md:14, absent in its code
 PRIORITY_FIRSTFIT = "firstfit"    # reference SampleRater (rater.go:21-50), test-only there
 POLICIES = (PRIORITY_BINPACK, PRIORITY_SPREAD, PRIORITY_RANDOM, PRIORITY_FIRSTFIT)
+# Priorities answer the nominated node this many raw points above every other fitting node.
+# kube-scheduler adds 10 x (extender score x weight) to its own plugins' sum; the default plugins
+# that differ between GPU nodes (LeastAllocated, BalancedAllocation, PodTopologySpread x 2,
+# ImageLocality, InterPodAffinity, NodeAffinity, TaintToleration) span at most ~800 points, so
+# 100 raw points (1,000) keep the pod on its nomination. 0 answers the raw scores (reference).
+PRIORITY_LEAD = 100
 
 RESOURCE_GPU_MEMORY = "nano-gpu/gpu-memory"   # HBM MiB per container (288 GB / MI355X)
 ANNOTATION_TOPOLOGY = "nano-gpu/topology"     # node: JSON from the node agent (topology.model)

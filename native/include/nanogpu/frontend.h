@@ -96,7 +96,8 @@ class Frontend {
   // decisive: filter answers the one node priorities would rank first (ties broken by the pod's
   // UID hash, as priorities breaks them) and nominates it; kube-scheduler skips scoring for a
   // single feasible node, so a pod's cycle is one round trip (off: the reference's filter)
-  void set_options(const Options& o, bool score_normalize, bool nominate = false, bool decisive = false);
+  void set_options(const Options& o, bool score_normalize, bool nominate = false, bool decisive = false,
+                   int32_t lead = 0);
   // false: every request goes to Python (a standby replica answers 503 from there).
   void set_serving(bool on) { serving_.store(on, std::memory_order_release); }
   // this process's switch AND the replica's shared flag in the ledger (leader election runs
@@ -198,6 +199,10 @@ class Frontend {
   void prepare_bind(std::string_view body, PyRequest* r, VerbScratch& s);
   void cache_pod(VerbScratch& s, std::string_view uid, const CachedPod& cached, std::string_view raw, const Demand& dem);
   void run_deferred(VerbScratch& s);   // a worker verb's work left for after its answer went out
+  // a nomination may wait until after the answer only where nothing can read the ledger in
+  // between: one worker thread and no other process on the ledger (kube-scheduler's next filter
+  // may reach another connection's thread or another worker, and must see this pod's devices held)
+  bool defer_nominate_ok(const VerbScratch& s) const;
   void note_bind_wall(uint64_t ns);
   // a response for connection `conn` of worker w, on w's thread: sent, then its next request
   struct Reply;
@@ -221,12 +226,21 @@ class Frontend {
   std::atomic<bool> spin_recv_binds_{false};
   std::vector<std::unique_ptr<Worker>> workers_;
 
+  // this instance among every Frontend the process made: thread_local caches (the verbs'
+  // scratch for callers off the workers) are keyed by it, not by an address a later instance
+  // (or its ledger) may reuse
+  const uint64_t serial_ = next_serial();
+  static uint64_t next_serial() {
+    static std::atomic<uint64_t> n{0};
+    return n.fetch_add(1, std::memory_order_relaxed) + 1;
+  }
   mutable std::mutex opt_mu_;
   Options opt_;
   std::atomic<uint64_t> opt_version_{1};   // bumped by every set_options (workers re-copy then)
   bool normalize_ = false;
   bool nominate_ = false;
   bool decisive_ = false;
+  int32_t lead_ = 0;   // priorities: the nominated node's lead over every other node (0: off)
 
   std::mutex py_mu_;
   std::deque<PyRequest> py_q_;

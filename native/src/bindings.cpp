@@ -816,7 +816,9 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("port", &Frontend::port)
       .def("notify_fd", &Frontend::notify_fd)
       .def("set_options", &Frontend::set_options, py::arg("options"), py::arg("score_normalize") = false,
-           py::arg("nominate") = false, py::arg("decisive") = false)
+           py::arg("nominate") = false, py::arg("decisive") = false, py::arg("lead") = 0,
+           "lead: priorities answer the nominated node this many points above every other fitting node "
+           "(normalised scores: 10 and 0), so kube-scheduler's own plugins do not move the pod")
       .def("set_serving", &Frontend::set_serving)
       .def("set_busy_poll_us", &Frontend::set_busy_poll_us)
       .def("set_busy_poll_prio_us", &Frontend::set_busy_poll_prio_us)

@@ -314,7 +314,7 @@ namespace {
 // name -> node id for this thread, valid for one node epoch: open addressing on the name's hash,
 // names kept in an arena so a lookup compares bytes in a few cache lines of its own
 struct NameTable {
-  const Ledger* owner = nullptr;
+  uint64_t owner = 0;   // Frontend::serial_ (a thread_local table outlives the Frontend it served)
   uint64_t epoch = 0;
   struct Slot {
     uint64_t h = 0;   // 0: empty
@@ -324,7 +324,7 @@ struct NameTable {
   std::vector<Slot> slots;
   std::string arena;
   size_t used = 0;
-  void reset(const Ledger* o, uint64_t e) {
+  void reset(uint64_t o, uint64_t e) {
     owner = o;
     epoch = e;
     slots.assign(1024, Slot{});
@@ -484,7 +484,7 @@ struct LastPod {
 // list.
 constexpr int kListSlots = 64;
 struct IdCache {
-  const Ledger* owner = nullptr;
+  uint64_t owner = 0;   // Frontend::serial_
   bool valid[kListSlots] = {};         // an escape-free list whose ids can be reused
   uint64_t epoch[kListSlots] = {};     // the ledger's node epoch the ids were checked at
   uint64_t used[kListSlots] = {};
@@ -528,9 +528,11 @@ struct Frontend::VerbScratch {
   std::string blob, dstr, resp;
   bool nom_dropped = false;   // the last pod's own nomination was dropped ...
   uint64_t nom_mark = 0;      // ... when Ledger::nominations_made() read this
-  uint64_t opt_seen = 0;   // Frontend::opt_version_ of the copy below
+  uint64_t opt_seen = 0;   // Frontend::opt_version_ of the copy below ...
+  uint64_t opt_owner = 0;   // ... of this Frontend (serial_)
   Options opt;
   bool normalize = false, nominate = false, decisive = false;
+  int32_t lead = 0;
   // A worker's verbs leave two pieces of work for after their answer is on the wire
   // (Frontend::run_deferred, before the worker reads anything else): the pod cached for its bind
   // (filter) and the priorities-time nomination. Neither changes the answer, and kube-scheduler's
@@ -732,13 +734,14 @@ void Frontend::stop() {
   py_efd_ = -1;
 }
 
-void Frontend::set_options(const Options& o, bool score_normalize, bool nominate, bool decisive) {
+void Frontend::set_options(const Options& o, bool score_normalize, bool nominate, bool decisive, int32_t lead) {
   std::lock_guard<std::mutex> g(opt_mu_);
   opt_version_.fetch_add(1, std::memory_order_release);
   opt_ = o;
   normalize_ = score_normalize;
   nominate_ = nominate;
   decisive_ = decisive;
+  lead_ = std::max<int32_t>(0, lead);
 }
 
 std::vector<PyRequest> Frontend::take() {
@@ -972,12 +975,14 @@ void Frontend::prepare_bind(std::string_view body, PyRequest* r, VerbScratch& s)
     if (pod.name != name || pod.ns != ns || pod.completed || id < 0) return;   // Python reads the pod itself
   }
   // the options as of the last policy change this worker saw (as the verbs read them)
-  if (s.opt_seen != opt_version_.load(std::memory_order_acquire)) {
+  if (s.opt_seen != opt_version_.load(std::memory_order_acquire) || s.opt_owner != serial_) {
     std::lock_guard<std::mutex> g(opt_mu_);
     s.opt = opt_;
     s.normalize = normalize_;
     s.nominate = nominate_;
     s.decisive = decisive_;
+    s.lead = lead_;
+    s.opt_owner = serial_;   // a thread_local scratch serves every Frontend of its thread
     s.opt_seen = opt_version_.load(std::memory_order_relaxed);
   }
   const Options& o = s.opt;
@@ -1520,6 +1525,10 @@ void Frontend::cache_pod(VerbScratch& s, std::string_view uid, const CachedPod& 
   put_pod(uid, cached, raw, dem);
 }
 
+bool Frontend::defer_nominate_ok(const VerbScratch& s) const {
+  return s.defer_cache && ledger_->attached() <= 1;
+}
+
 void Frontend::run_deferred(VerbScratch& s) {
   if (!s.defer_put && !s.defer_nominate) return;
   const LastPod& last = s.last;
@@ -1571,7 +1580,7 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   LastPod& last = s.last;
   IdCache& idc = s.idc;
   uint64_t io0 = io_t0();
-  if (idc.owner != ledger_.get()) idc = IdCache{}, idc.owner = ledger_.get();
+  if (idc.owner != serial_) idc = IdCache{}, idc.owner = serial_;
   if (body.empty()) return false;
   // kube-scheduler's ExtenderArgs as Go's encoding/json writes them (struct field order, no
   // spaces): {"Pod":{...},"Nodes":null,"NodeNames":[...]}. In that exact layout the pod's text
@@ -1841,7 +1850,7 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     // kube-scheduler's node sampling the list is a different window of the cluster every
     // cycle, so the per-list cache above misses while every name in it is known
     NameTable& nid = s.nid;
-    if (nid.owner != ledger_.get() || nid.epoch != epoch) nid.reset(ledger_.get(), epoch);
+    if (nid.owner != serial_ || nid.epoch != epoch) nid.reset(serial_, epoch);
     for (size_t i = 0; i < static_cast<size_t>(nn); ++i) {
       const std::string_view name = name_at(i);
       // the table holds its own copy of every name (a compact arena): a hit touches neither
@@ -1861,12 +1870,14 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   }
   // the options as of the last policy change this worker saw (one atomic load a request; the
   // lock and the copy only after a change)
-  if (s.opt_seen != opt_version_.load(std::memory_order_acquire)) {
+  if (s.opt_seen != opt_version_.load(std::memory_order_acquire) || s.opt_owner != serial_) {
     std::lock_guard<std::mutex> g(opt_mu_);
     s.opt = opt_;
     s.normalize = normalize_;
     s.nominate = nominate_;
     s.decisive = decisive_;
+    s.lead = lead_;
+    s.opt_owner = serial_;   // a thread_local scratch serves every Frontend of its thread
     s.opt_seen = opt_version_.load(std::memory_order_relaxed);
   }
   const Options& o = s.opt;
@@ -1921,7 +1932,7 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     }
     const int64_t nom = pick >= 0 ? pick : only;
     if (nom >= 0 && nominate && !uid.empty() && wants_devices(dem)) {
-      if (s.defer && last.valid && uid.data() == last.uid.data()) {
+      if (s.defer && defer_nominate_ok(s) && last.valid && uid.data() == last.uid.data()) {
         s.defer_nominate = true;
         s.defer_node = ids[nom];
         s.defer_dem = dem;
@@ -2034,9 +2045,10 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     n_best = 1;
   }
   const bool lead = n_best == 1 && (second < 0 || scores[best] - second >= margin);
+  bool nominated = false;
   if (nominate && lead && !uid.empty() && dem.n > 0) {
     if (wants_devices(dem)) {
-      if (s.defer && last.valid && uid.data() == last.uid.data()) {
+      if (s.defer && defer_nominate_ok(s) && last.valid && uid.data() == last.uid.data()) {
         s.defer_nominate = true;
         s.defer_node = ids[best];
         s.defer_dem = dem;
@@ -2045,6 +2057,29 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
         ledger_->nominate(ids[best], uid, dem, o);
       }
       s.nom_dropped = false;
+      nominated = true;
+    }
+  }
+  // The nomination is the pod's placement from this answer on: every later filter sees its
+  // devices held. kube-scheduler adds its own score plugins (LeastAllocated, BalancedAllocation,
+  // PodTopologySpread: about 800 points between nodes at most) to 10 x the extender's score, so a
+  // close second can still win. A pod bound elsewhere than its nomination was invisible on the
+  // node it went to until its bind reserved there, and the filters kube-scheduler ran meanwhile
+  // (its next cycles start before its binds land) stacked onto the same free devices: steady-
+  // churn frag grew from 0.6 % with no such lag to 3.6 % with one cycle of it and 12 % with four
+  // (tests/test_lag.py). With a lead, the nominated node is answered `lead` points above every
+  // other fitting node (normalised scores: 10 and 0), so kube-scheduler binds where the ledger
+  // already holds the pod, whichever worker the bind reaches and however late.
+  if (nominated && s.lead > 0 && !o.compat) {
+    int32_t other = INT32_MIN;
+    for (size_t i = 0; i < ids.size(); ++i)
+      if (static_cast<int64_t>(i) != best && rcs[i] == kOk) other = std::max(other, scores[i]);
+    if (other != INT32_MIN) {
+      if (normalize) {
+        for (size_t i = 0; i < ids.size(); ++i) scores[i] = static_cast<int64_t>(i) == best ? 100 : 0;
+      } else if (scores[best] - other < s.lead) {
+        scores[best] = other + s.lead;
+      }
     }
   }
   if (normalize && !scores.empty()) {

@@ -55,7 +55,9 @@ def test_bench_single_rank_cpu(tmp_path, cpu_exclusive):
     # 120 nodes behind kube-scheduler's sampling: 100 feasible nodes reach the extender
     assert d["value_nodes120"] > 0 and d["failed_nodes120"] == 0 and d["pods_per_burst_nodes120"] == 3000
     # (a pod that found no host in a cycle is retried over the nodes that were feasible then)
-    assert 99.0 <= d["nodes_sent_per_filter_nodes120"] <= 100.0
+    # (binpack fills nodes to kube-scheduler's resource fit, so late in a burst fewer than 100
+    # nodes are feasible in a cycle)
+    assert 80.0 <= d["nodes_sent_per_filter_nodes120"] <= 100.0
     assert d["value_mode"] == "one kube-scheduler stand-in" and "value_independent_schedulers" not in d
     assert d["frag_pct_nodes120_reference_model"] is not None
     # extender CPU a pod: by thread group, and split into user / kernel time
@@ -309,37 +311,38 @@ def test_bench_multi_rank_survives_a_hung_peer_probe(cpu_exclusive):
     assert d["gpu"]["link_bw_gbs"] == 153.0 and d["scheduled"] == 100 and d["failed"] == 0
 
 
-def test_one_scheduler_over_four_workers_keeps_steady_churn_placement_quality(tmp_path, cpu_exclusive):
-    """one kube-scheduler's binds over 4 extender workers (the headline's
-    N-rank mode) on the headline's steady-churn pass (1,000 pods on 64 nodes, 30 % replaced a
-    step). Timing makes frag_pct_steady vary run to run with one worker as with four
-    (profiles/steady_frag_workers_r04.md: 0.29-1.31 % either way, serial replay 0.43 %), so it
-    is bounded against the reference algorithm on the same stream, not against a 1-worker run."""
-    full = tmp_path / "full.json"
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
-    seen = []
-    for _attempt in range(2):   # a second run only when other work starved the first (see below)
-        r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
-                            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
-                            "--gpus", "4", "--no-gpu", "--steps", "1", "--warmup", "1", "--pods", "1000", "--nodes", "64",
-                            "--rtt-variant-ms", "0", "--steady-variant-steps", "6", "--nodes-variant", "0",
-                            "--inproc-variant-steps", "0", "--independent-variant-steps", "0", "--busy-poll-us", "0",
-                            "--json-out", str(full)],
+def test_steady_churn_frag_is_the_same_at_1_2_and_4_workers(tmp_path, cpu_exclusive):
+    """steady-churn frag must not grow with extender workers. One kube-scheduler
+    (the stand-in) drives the headline's steady pass (1,000 pods on 64 nodes, 30 % replaced a
+    step), its binds over 1, 2 and 4 workers. The cause was the bind landing after the next
+    filters (tests/test_lag.py); with the priorities lead (nanogpu.types.PRIORITY_LEAD) every pod
+    is held where it binds from its priorities answer on, so the frag of every step is the same
+    at every worker count and equals the offline replay of the extender's verbs. No skip, no
+    retry: timing no longer enters."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    got = {}
+    for n in (1, 2, 4):
+        full = tmp_path / f"w{n}.json"
+        r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(n), "--no-gpu", "--steps", "1",
+                            "--warmup", "1", "--rtt-variant-ms", "0", "--steady-variant-steps", "6",
+                            "--nodes-variant", "0", "--inproc-variant-steps", "0", "--independent-variant-steps", "0",
+                            "--decisive-variant-steps", "0", "--json-out", str(full)],
                            capture_output=True, text=True, timeout=600, env=env, cwd="/tmp")
         assert r.returncode == 0, r.stderr[-3000:]
         d = _last_json(r.stdout)
         diag = json.loads(full.read_text())["diagnostics"]
-        assert d["value_mode"] == "one kube-scheduler stand-in, binds over all 4 extender workers"
-        assert diag["steady_config"].endswith("one kube-scheduler stand-in, binds over every rank's worker")
-        assert d["failed_steady"] == 0 and d["bind_handoffs_steady"] > 0
-        seen.append((d["frag_pct_steady"], d["frag_pct_steady_reference_model"]))
-        # quiet host: 0.29-1.31 % against 3.80 % (the bound also holds for two such jobs sharing 8
-        # CPUs). A host starved by more than that can do worse (binds trail kube-scheduler's cycle
-        # and the filters behind them see the ledger without their pods, see the profile): that
-        # is timing, and a second run decides
-        if d["frag_pct_steady"] <= d["frag_pct_steady_reference_model"]:
-            break
-    assert seen[-1][0] <= seen[-1][1], seen
+        assert d["failed_steady"] == 0
+        if n > 1:
+            assert diag["steady_config"].endswith("one kube-scheduler stand-in, binds over every rank's worker")
+            assert d["bind_handoffs_steady"] > 0
+        nom = diag["nominations_steady"]
+        assert nom["moved"] == 0 and nom["adopted"] == nom["made"] > 0
+        got[n] = (d["frag_pct_steady"], diag["frag_pct_steady_each_step"], diag["frag_pct_steady_native_replay_each_step"])
+    for n in (2, 4):
+        assert got[n][0] <= 1.2 * got[1][0], got
+        assert got[n][1] == got[1][1], got
+    assert got[1][1] == got[1][2], got    # the live run is the replay, step for step
+    assert got[1][0] < 1.0   # the reference algorithm reads 3.80 on this stream
 
 
 def test_launcher_forwards_a_term_to_its_ranks(tmp_path):

@@ -379,13 +379,13 @@ def test_priorities_nominate_unique_best_and_bind_adopts():
                                                     "PodUID": pu.pod_uid(a), "Node": "n0"}))])
             assert res[1] == (200, b'{"Error":""}') and led.lookup(pu.pod_uid(a))["state"] == "committed"
             # a tie at the top (the same node twice) is broken for the one the pod's UID hash
-            # picks, which is nominated and answered one point above the other
+            # picks, which is nominated and answered the priorities lead above the other
             c = store.create_pod(pu.make_pod("c", [("c", 10)]))
             res = await loop.run_in_executor(None, _http, rt.bound_port, [
                 ("POST", "/scheduler/priorities", _dumps({"Pod": c, "NodeNames": ["n1", "n1"]}))])
             got = [h["Score"] for h in json.loads(res[0][1])]
             k = N.Ledger.owner_hash(pu.pod_uid(c)) % 2
-            assert got[k] == got[1 - k] + 1
+            assert got[k] == got[1 - k] + rt.state.priority_lead
             rec = led.lookup(pu.pod_uid(c))
             assert rec["state"] == "nominated" and rec["node"] == rt.state.node_entry("n1").id
             led.drop_nomination(pu.pod_uid(c))
@@ -760,7 +760,7 @@ def test_escaped_node_names_still_answer_byte_identical():
     ext = Extender(st, InProcKube(FakeKubeStore()))
     fe = N.Frontend(st.ledger, "127.0.0.1", 0, 1)
     try:
-        fe.set_options(st.options, False, st.nominate)   # the same nomination rule as the Python verb
+        fe.set_options(st.options, False, st.nominate, False, st.priority_lead)   # the Python verb's rules
         raw = ('{"Pod":' + json.dumps(pu.make_pod("p", [("c", 20)])) + ',"NodeNames":["n\\u0030","n1"]}').encode()
         ok, _, out = fe.time_verb(raw, False, 1)
         assert ok and out == _dumps(ext.filter(json.loads(raw)))
@@ -890,7 +890,7 @@ def test_rotating_node_windows_answer_byte_identical_through_the_list_cache():
     fe = N.Frontend(st.ledger, "127.0.0.1", 0, 1)
     rnd = random.Random(4)
     try:
-        fe.set_options(st.options, False, st.nominate)   # the same nomination rule as the Python verb
+        fe.set_options(st.options, False, st.nominate, False, st.priority_lead)   # the Python verb's rules
         for step in range(160):
             if step == 100:   # a new node: every cached list re-checks its ids
                 st.register_node(pu.make_node("node-new", 8, synthetic_mi355x(8).to_json()))

@@ -31,8 +31,10 @@ def test_kube_combining_overrides_a_small_extender_lead():
 
 
 def test_wrong_nominations_are_counted_and_raise_the_margin():
+    """--priority-lead 0 (raw scores, as the reference): kube-scheduler's plugins can move the
+    pod off a close nomination; the ledger counts it and nominates less eagerly."""
     async def main():
-        store, rt = await _runtime(2)
+        store, rt = await _runtime(2, priority_lead=0)
         led = rt.state.ledger
         client = FastExtenderClient("127.0.0.1", rt.bound_port, pool=8)
         loop = asyncio.get_running_loop()
@@ -67,6 +69,46 @@ def test_wrong_nominations_are_counted_and_raise_the_margin():
             q = pu.make_pod("q", [("c", 30)])
             await client.prioritize({"Pod": q, "Nodes": None, "NodeNames": ["n0", "n1"]})
             assert led.lookup(pu.pod_uid(q))["state"] == "nominated"
+        finally:
+            await client.close()
+            await rt.stop()
+
+    asyncio.run(main())
+
+
+def test_the_priorities_lead_keeps_kube_scheduler_on_the_nomination():
+    """The default lead (nanogpu.types.PRIORITY_LEAD): the same near-tie is answered with the
+    nominated node 100 points ahead, which kube-scheduler's own plugins (busy CPUs / memory on
+    n0) cannot overturn, so the bind adopts the nomination and the margin stays 0."""
+    from nanogpu import types as T
+
+    async def main():
+        store, rt = await _runtime(2)
+        led = rt.state.ledger
+        client = FastExtenderClient("127.0.0.1", rt.bound_port, pool=8)
+        loop = asyncio.get_running_loop()
+        try:
+            nodes = [store.nodes[n] for n in ("n0", "n1")]
+            for name, pct, node in (("b0", 60, "n0"), ("b1", 55, "n1")):
+                base = store.create_pod(pu.make_pod(name, [("c", pct)]))
+                m = pu.meta(base)
+                await loop.run_in_executor(None, _http, rt.bound_port, [
+                    ("POST", "/scheduler/filter", _dumps({"Pod": base, "NodeNames": [node]})),
+                    ("POST", "/scheduler/bind", _dumps({"PodName": name, "PodNamespace": "default",
+                                                        "PodUID": m["uid"], "Node": node}))])
+            pod = pu.make_pod("p", [("c", 30)])
+            scores = await client.prioritize({"Pod": pod, "Nodes": None, "NodeNames": ["n0", "n1"]})
+            assert [h["Score"] for h in scores] == [85 + T.PRIORITY_LEAD, 85]
+            led.drop_nomination(pu.pod_uid(pod))
+            drv = SchedulerDriver(client, InProcKube(store), ["n0", "n1"], node_capacities(nodes),
+                                  kube=KubeScoring(), resource_fit=False)
+            drv.used["n0"] = (250_000, 3 << 40)
+            stats = await drv.run([pod])
+            assert stats.scheduled == 1
+            assert pu.node_name_of(store.get_pod("default", "p")) == "n0"
+            c = led.nomination_counts()
+            assert c["moved"] == 0 and c["adopted"] >= 1, c
+            assert led.nomination_margin == 0
         finally:
             await client.close()
             await rt.stop()
