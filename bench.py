@@ -622,6 +622,8 @@ def apiserver_main(conn, avoid: list[int] | None = None, near: int = -1) -> None
             srv.set_latency(msg[2])
             if len(msg) > 4 and msg[4] > 0:
                 srv.set_spin(msg[4])
+            # kube-apiserver's default --max-mutating-requests-inflight: over it, 429 + Retry-After
+            srv.set_max_mutating_inflight(msg[6] if len(msg) > 6 else 0)
             conn.send((srv.port, sorted(os.sched_getaffinity(0))))
         elif op == "nodes":
             for n in msg[1]:
@@ -860,8 +862,8 @@ class ApiServerProc:
         return self.conn.recv()
 
     def start(self, threads: int, latency_s: float = 0.0, keep_heap: bool = False, spin_s: float = 0.0,
-              history: int = 0) -> str:
-        port, self.cpus = self._rpc("start", threads, latency_s, keep_heap, spin_s, history)
+              history: int = 0, max_inflight: int = 0) -> str:
+        port, self.cpus = self._rpc("start", threads, latency_s, keep_heap, spin_s, history, max_inflight)
         self.url = f"http://127.0.0.1:{port}"
         return self.url
 
@@ -1064,7 +1066,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         if d.rank == 0:
             apisrv = api_proc
             url = apisrv.start(args.apiserver_threads or min(16, max(4, d.world)), args.api_rtt_ms / 1e3,
-                               args.apiserver_keep_heap, args.apiserver_spin_us / 1e6, args.apiserver_history)
+                               args.apiserver_keep_heap, args.apiserver_spin_us / 1e6, args.apiserver_history,
+                               T.API_MAX_MUTATING_INFLIGHT)
             if getattr(args, "_placement", None):
                 args._placement["apiserver"] = list(apisrv.cpus)
             apisrv.add_nodes(nodes)
@@ -1091,6 +1094,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
                  nominate=not args.no_nominate,
                  bind_writer_threads=args.bind_writer_threads or max(2, 16 // d.world),
                  bind_writer_mode=args.bind_writer_mode, assume_label=not args.no_assume_label,
+                 # every rank's extender writes to the one API server: they share its in-flight limit
+                 api_inflight_share=d.world if shared else 1,
                  bind_first=args.bind_first, spin_nap=args.spin_nap, spin_recv=args.spin_recv, spin_recv_binds=args.spin_recv_binds, batch_labels=args.batch_labels,
                  decisive_filter=getattr(args, "decisive_filter", False))
     all_steps_pre = [10_000 + w for w in range(args.warmup)] + list(range(args.steps))
@@ -1601,6 +1606,7 @@ def order_line(full: dict) -> tuple[dict, dict]:
 def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc, gpu_info: dict, topo,
                   variant, one_v, steady_v, nodes_v, inproc_v, dec_v=None) -> tuple[dict, dict]:
     from nanogpu import affinity
+    from nanogpu import types as T
 
     fr = res["frag"]
     full = {
@@ -1624,7 +1630,8 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
                    # or --inproc-api's per-rank in-process store (value_inproc_api)
                    "api_server": ("in-process store per rank" if args.inproc_api else
                                   f"one native HTTP API server, own process "
-                                  f"({args.apiserver_threads or min(16, max(4, d.world))} IO threads)"),
+                                  f"({args.apiserver_threads or min(16, max(4, d.world))} IO threads, "
+                                  f"max {T.API_MAX_MUTATING_INFLIGHT} mutating requests in flight: 429 over it)"),
                    "cpus_rank0": _cpulist(cpus),
                    "cpus_apiserver": _cpulist(api_proc.cpus) if api_proc is not None else None,
                    "frontend": f"{args.frontend_threads} threads, busy-poll {args.busy_poll_us} us"
@@ -1660,6 +1667,7 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
         "frag_hbm_pct": round(statistics.mean(f["frag_mib"] for f in fr), 3) if fr else None,
         "stranded_pct": round(statistics.mean(f["stranded_pct"] for f in fr), 3) if fr else None,
         "scheduled": out["scheduled"], "failed": out["failed"], "bind_retries": out["bind_errors"],
+        "api_429s": out.get("api_429s"),
         "host_selection": "extender arg-max" if args.no_kube_combine else
                           "kube-scheduler combining (LeastAllocated + BalancedAllocation + 10 x extender)",
         "nominations": res["nominations"],
@@ -1700,6 +1708,7 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
             full[f"value_{tag}"] = variant["value"]
             full[f"p50_bind_ms_{tag}"] = variant["p50_bind_ms"]
             full[f"p99_bind_ms_{tag}"] = variant["p99_bind_ms"]
+            full[f"api_429s_{tag}"] = variant.get("api_429s")
     if one_v is not None:
         if "error" in one_v:
             full["value_independent_schedulers"] = None
@@ -1897,15 +1906,17 @@ def run_pass(d: Dist, args, topo, conn, tag: str, api_proc=None) -> dict:
                               f"{int(time.time())}" if d.rank == 0 else None)
     from nanogpu.native import core
 
-    led = None
     if d.rank == 0:
+        # the shared region is laid out before any rank attaches; the harness keeps no handle
+        # on it (Ledger::attached counts the extender processes: one worker defers its
+        # nominations past the answer, several do not)
         led = core().Ledger(ledger_path, max(1024, args.nodes), max(65536, 4 * args.pods), True)
+        del led
     d.barrier()
     try:
         return asyncio.run(run_rank(d, args, topo, ledger_path, conn, api_proc))
     finally:
         d.barrier()
-        del led
         if d.rank == 0:
             try:
                 os.unlink(ledger_path)
@@ -1995,6 +2006,8 @@ def summarize(d: Dist, args, res: dict) -> dict:
             "bind_errors": sum(d.gather_obj(res["bind_errors"])),
             "bind_handoffs": res.get("bind_handoffs"),
             "bind_hops": hops,
+            # the API server's max-in-flight admission: 429s answered in this pass (rank 0 holds it)
+            "api_429s": ((res.get("apiserver") or {}).get("admission") or {}).get("too_many_requests"),
             # each rank's mean stand-in span per step: the slowest sets the peak barrier
             "schedule_ms_by_rank": [round(v, 2) for v in d.gather_obj((res.get("phase_ms") or {}).get("schedule_ms", 0.0))]}
 

@@ -47,7 +47,10 @@ class Config:
     max_pods: int = 131072
     verify_pod_on_bind: bool = False
     native_bind_writes: bool = True             # C++ writer threads do the bind's API writes
-    bind_writer_threads: int = 16               # x KubeWriter::kBatch (8) binds in flight
+    bind_writer_threads: int = 16               # x KubeWriter::kBatch (8) binds in flight (threads mode,
+    #                                             and evented / inline when api_max_inflight is 0)
+    api_max_inflight: int = T.API_MAX_MUTATING_INFLIGHT   # kube-apiserver's mutating in-flight limit
+    api_inflight_share: int = 0                 # extender processes sharing it (0: `workers`)
     bind_writer_mode: str = "evented"           # inline (front-door workers) | evented (one epoll thread) |
     #                                             frontdoor (front-door workers send, one epoll thread reads) | threads
     native_pod_watch: bool = True               # a C++ thread reads and filters the pod watch (podwatch.cpp)
@@ -87,6 +90,17 @@ class Config:
     request_sizes: list = field(default_factory=list)   # share sizes binpack's waste model fixes
     learn_sizes: bool = True                    # ...plus the sizes the ledger sees requested
     gpu_node_selectors: list = field(default_factory=lambda: [T.AMD_GPU_NODE_LABEL, T.LEGACY_GPU_NODE_LABEL])
+
+    def writer_max_binds(self) -> int:
+        """Binds one worker's native writer keeps in flight at most (its admission window's start
+        and ceiling): 3/4 of kube-apiserver's mutating in-flight limit, shared by the extender's
+        processes, a bind being two mutating requests with the label PATCH (one without). The
+        rest of the limit is left to the cluster's other clients. 0: bind_writer_threads x 8."""
+        if self.api_max_inflight <= 0:
+            return 0
+        share = self.api_inflight_share or max(1, self.workers)
+        per_bind = 2 if self.assume_label else 1
+        return max(2, (3 * self.api_max_inflight // 4) // (share * per_bind))
 
 
 class Runtime:
@@ -235,7 +249,7 @@ class Runtime:
                                                         ext.record_events, self.cfg.bind_writer_mode != "threads",
                                                         self.cfg.assume_label, self.cfg.api_write_timeout_s,
                                                         self.cfg.bind_writer_mode == "inline",
-                                                        self.cfg.batch_labels):
+                                                        self.cfg.batch_labels, self.cfg.writer_max_binds()):
                         log.info("worker %d: bind API writes in native writer threads (%d)", self.worker,
                                  self.cfg.bind_writer_threads)
                         self.native.fe.set_fe_send(self.cfg.bind_writer_mode == "frontdoor")

@@ -59,8 +59,13 @@ def build_parser() -> argparse.ArgumentParser:
                    help="the native front door's C++ threads do each bind's PATCH + binding POST + commit "
                         "(native/src/kubewriter.cpp); --no-native-bind-writes keeps them in Python")
     p.add_argument("--bind-writer-threads", type=int, default=16,
-                   help="binds in flight / 8 for the native writer (16: 128 binds); in --bind-writer-mode "
-                        "threads, the number of blocking writer threads")
+                   help="--bind-writer-mode threads: the number of blocking writer threads (8 binds in flight "
+                        "each); evented / inline: the binds in flight when --api-max-inflight is 0 (x 8)")
+    p.add_argument("--api-max-inflight", type=int, default=T.API_MAX_MUTATING_INFLIGHT,
+                   help="kube-apiserver's --max-mutating-requests-inflight (its default 200). The native writer "
+                        "starts each worker at 3/4 of it over --workers (a bind is its binding + label PATCH), "
+                        "and on a 429 halves its window and re-sends after Retry-After (+1 per clean window); "
+                        "0: --bind-writer-threads x 8 binds, no sizing")
     p.add_argument("--bind-writer-mode", choices=["inline", "evented", "frontdoor", "threads"], default="evented",
                    help="native bind writes: from each front-door worker's own epoll loop (inline), on one "
                         "epoll thread (evented), sent by the front-door worker with the answers read on one "
@@ -151,7 +156,7 @@ def parse(argv: list[str] | None = None) -> Config:
         topology_weight=a.topology_weight, track_hbm=not a.no_hbm, workers=max(1, a.workers),
         ledger_path=a.ledger_path, max_nodes=a.max_nodes, max_pods=a.max_pods,
         verify_pod_on_bind=a.bind_verify_pod, native_bind_writes=a.native_bind_writes,
-        bind_writer_threads=max(1, a.bind_writer_threads), bind_writer_mode=a.bind_writer_mode,
+        bind_writer_threads=max(1, a.bind_writer_threads), api_max_inflight=max(0, a.api_max_inflight), bind_writer_mode=a.bind_writer_mode,
         native_pod_watch=not a.no_native_pod_watch, assume_label=not a.no_assume_label,
         api_write_timeout_s=parse_duration(a.api_write_timeout), bind_first=a.bind_first, spin_nap=a.spin_nap, spin_recv=a.spin_recv, batch_labels=a.batch_labels, reservation_ttl_s=parse_duration(a.reservation_ttl),
         nominate=not a.no_nominate, nomination_ttl_s=parse_duration(a.nomination_ttl),

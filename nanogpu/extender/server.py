@@ -406,12 +406,21 @@ class NativeServer:
                       "# TYPE nanogpu_native_label_failures_total counter",
                       f"nanogpu_native_label_failures_total {kw['label_failures']}",
                       "# TYPE nanogpu_native_binds_inflight gauge",
-                      f"nanogpu_native_binds_inflight {kw['inflight']}"]
+                      f"nanogpu_native_binds_inflight {kw['inflight']}",
+                      "# HELP nanogpu_native_api_throttled_total API answers 429 TooManyRequests (kube-apiserver's "
+                      "max-in-flight admission); each was re-sent after its Retry-After",
+                      "# TYPE nanogpu_native_api_throttled_total counter",
+                      f"nanogpu_native_api_throttled_total {kw.get('throttled', 0)}",
+                      "# TYPE nanogpu_native_bind_window_cuts_total counter",
+                      f"nanogpu_native_bind_window_cuts_total {kw.get('window_cuts', 0)}",
+                      "# HELP nanogpu_native_bind_window binds the writer keeps in flight at most now",
+                      "# TYPE nanogpu_native_bind_window gauge",
+                      f"nanogpu_native_bind_window {kw.get('window', 0)}"]
         return ("\n".join(lines) + "\n").encode()
 
     def enable_native_writes(self, config, threads: int, retries: int, record_events: bool,
                              evented: bool = True, label: bool = True, timeout_s: float = 30.0,
-                             inline_io: bool = False, batch_labels: bool = False) -> bool:
+                             inline_io: bool = False, batch_labels: bool = False, max_binds: int = 0) -> bool:
         """Hands the bind's API writes to the front door's C++ writer threads (native/src/
         kubewriter.cpp) when the API server is a REST endpoint this process reaches with a
         bearer token or a client certificate; False (Python writes) otherwise."""
@@ -424,7 +433,7 @@ class NativeServer:
         self.fe.set_kube_writer(u.hostname, u.port or (443 if tls else 80), tls, config.token or "",
                                 config.token_file or "", config.ca_file or "", config.cert_file or "",
                                 config.key_file or "", bool(config.insecure), threads, retries, record_events,
-                                evented, label, timeout_s, inline_io, batch_labels)
+                                evented, label, timeout_s, inline_io, batch_labels, max_binds)
         return True
 
     async def stop(self) -> None:

@@ -193,6 +193,13 @@ class Extender:
                                       f"{pu.pod_uid(pod)}, and it's not equal with expected {args.pod_uid}")
         return pod
 
+    @staticmethod
+    def _backoff(e: ApiError, attempt: int) -> float:
+        """5 ms x 2^k, or a 429's Retry-After when it asks for longer (kube-apiserver: 1 s)."""
+        b = 0.005 * (2 ** attempt)
+        ra = getattr(e, "retry_after", None)
+        return min(30.0, max(b, ra)) if e.status == 429 and ra else b
+
     async def _retry(self, op: str, fn, *a):
         for attempt in range(self.api_retries + 1):
             try:
@@ -201,14 +208,15 @@ class Extender:
                 self.metrics.child(self.metrics.api_errors, op, str(e.status)).inc()
                 if e.status < 500 and e.status != 429 or attempt == self.api_retries:
                     raise
-            await asyncio.sleep(0.005 * (2 ** attempt))
+                wait = self._backoff(e, attempt)
+            await asyncio.sleep(wait)
 
     async def _retry_after(self, first: ApiError, op: str, fn, *a):
         """`_retry` for a call whose first attempt already failed with `first`."""
         self.metrics.child(self.metrics.api_errors, op, str(first.status)).inc()
         if first.status < 500 and first.status != 429 or self.api_retries == 0:
             raise first
-        await asyncio.sleep(0.005)
+        await asyncio.sleep(self._backoff(first, 0))
         for attempt in range(1, self.api_retries + 1):
             try:
                 return await fn(*a)
@@ -216,7 +224,8 @@ class Extender:
                 self.metrics.child(self.metrics.api_errors, op, str(e.status)).inc()
                 if e.status < 500 and e.status != 429 or attempt == self.api_retries:
                     raise
-            await asyncio.sleep(0.005 * (2 ** attempt))
+                wait = self._backoff(e, attempt)
+            await asyncio.sleep(wait)
 
     async def _bind(self, args: BindingArgs, sp) -> None:
         pod = None if self.verify_pod_on_bind else self.pods.pop(args.pod_uid)

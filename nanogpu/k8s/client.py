@@ -28,11 +28,17 @@ SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
 
 
 class ApiError(Exception):
-    def __init__(self, status: int, message: str, reason: str = ""):
+    def __init__(self, status: int, message: str, reason: str = "", retry_after: float | None = None):
         super().__init__(f"{status} {reason}: {message}")
         self.status = status
         self.reason = reason
         self.message = message
+        self.retry_after = retry_after   # seconds, from a 429's Retry-After header
+
+    @property
+    def throttled(self) -> bool:
+        """kube-apiserver's max-in-flight admission refused the request (nothing was done)."""
+        return self.status == 429
 
     @property
     def not_found(self) -> bool:
@@ -41,6 +47,14 @@ class ApiError(Exception):
     @property
     def conflict(self) -> bool:
         return self.status == 409
+
+
+def _retry_after(headers) -> float | None:
+    v = headers.get("Retry-After") if headers is not None else None
+    try:
+        return float(v) if v is not None else None
+    except ValueError:
+        return None
 
 
 @dataclass
@@ -217,15 +231,16 @@ class KubeClient:
             async with s.request(method, url, data=data, params=params, headers=headers or None) as r:
                 text = await r.text()
                 status = r.status
+                ra = _retry_after(r.headers) if status == 429 else None
             if status == 401 and attempt == 0 and self.config.token_file:
                 continue                      # the token may have rotated under us: re-read once
             break
         if status >= 400:
             try:
                 st = json.loads(text)
-                raise ApiError(status, st.get("message", text), st.get("reason", ""))
+                raise ApiError(status, st.get("message", text), st.get("reason", ""), ra)
             except (ValueError, AttributeError):
-                raise ApiError(status, text) from None
+                raise ApiError(status, text, "", ra) from None
         return json.loads(text) if text else None
 
     # --------------------------------------------------------------------- pods
@@ -261,6 +276,7 @@ class KubeClient:
             async with s.request(method, self.config.server + path, params=params, headers=headers or None) as r:
                 body = await r.read()
                 status = r.status
+                ra = _retry_after(r.headers) if status == 429 else None
             if status == 401 and attempt == 0 and self.config.token_file:
                 continue
             break
@@ -268,9 +284,9 @@ class KubeClient:
             text = body.decode("utf-8", "replace")
             try:
                 st = json.loads(text)
-                raise ApiError(status, st.get("message", text), st.get("reason", ""))
+                raise ApiError(status, st.get("message", text), st.get("reason", ""), ra)
             except (ValueError, AttributeError):
-                raise ApiError(status, text) from None
+                raise ApiError(status, text, "", ra) from None
         return body
 
     async def list_pods(self, label_selector: str | None = None, field_selector: str | None = None,

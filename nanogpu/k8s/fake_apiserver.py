@@ -78,6 +78,10 @@ class Faults:
     conflict_rate: float = 0.0        # 409 on binding POST
     close_after_binding: bool = False  # answer a binding with Connection: close (requests
                                        # pipelined behind it on the connection go unanswered)
+    # kube-apiserver's --max-mutating-requests-inflight (0: none): a POST / PUT / PATCH / DELETE
+    # over it is answered 429 TooManyRequests with `Retry-After: retry_after_s`, not handled
+    max_mutating_inflight: int = 0
+    retry_after_s: int = 1
     seed: int = 0
     rng: random.Random = field(default_factory=random.Random)
 
@@ -689,7 +693,29 @@ def make_app(store: FakeKubeStore) -> web.Application:
         store.add_event(await request.json())
         return web.json_response({}, status=201)
 
-    app = web.Application(client_max_size=16 * 1024 * 1024)
+    mutating = {"inflight": 0, "peak": 0}
+
+    @web.middleware
+    async def admission(request, handler):
+        # kube-apiserver's max-in-flight filter: over the limit, refused before any handling
+        limit = store.faults.max_mutating_inflight
+        if limit <= 0 or request.method not in ("POST", "PUT", "PATCH", "DELETE"):
+            return await handler(request)
+        if mutating["inflight"] >= limit:
+            store._count("throttled")
+            return web.json_response({"kind": "Status", "apiVersion": "v1", "status": "Failure",
+                                      "message": "Too many requests, please try again later.",
+                                      "reason": "TooManyRequests", "code": 429},
+                                     status=429, headers={"Retry-After": str(store.faults.retry_after_s)})
+        mutating["inflight"] += 1
+        mutating["peak"] = max(mutating["peak"], mutating["inflight"])
+        store.counts["peak_mutating_inflight"] = mutating["peak"]
+        try:
+            return await handler(request)
+        finally:
+            mutating["inflight"] -= 1
+
+    app = web.Application(client_max_size=16 * 1024 * 1024, middlewares=[admission])
     app.add_routes(routes)
     app[STORE_KEY] = store
 

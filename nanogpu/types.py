@@ -36,6 +36,9 @@ POLICIES = (PRIORITY_BINPACK, PRIORITY_SPREAD, PRIORITY_RANDOM, PRIORITY_FIRSTFI
 # ImageLocality, InterPodAffinity, NodeAffinity, TaintToleration) span at most ~800 points, so
 # 100 raw points (1,000) keep the pod on its nomination. 0 answers the raw scores (reference).
 PRIORITY_LEAD = 100
+# kube-apiserver's --max-mutating-requests-inflight default: the native bind writer sizes its
+# window under it (nanogpu.app.Config.writer_max_binds) and backs off on its 429s
+API_MAX_MUTATING_INFLIGHT = 200
 
 RESOURCE_GPU_MEMORY = "nano-gpu/gpu-memory"   # HBM MiB per container (288 GB / MI355X)
 ANNOTATION_TOPOLOGY = "nano-gpu/topology"     # node: JSON from the node agent (topology.model)

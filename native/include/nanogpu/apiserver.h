@@ -86,6 +86,11 @@ class Server {
   void set_latency(double seconds);
   // IO threads poll for `seconds` after their last event before sleeping (0: sleep at once)
   void set_spin(double seconds);
+  // kube-apiserver's --max-mutating-requests-inflight (its default 200; 0: no limit): a
+  // POST / PUT / PATCH / DELETE arriving while this many are in flight (handled, answer not yet
+  // written: with a modelled round trip, until it is due) is answered 429 TooManyRequests with
+  // `Retry-After: 1`, as kube-apiserver's max-in-flight filter does, without being handled.
+  void set_max_mutating_inflight(int n);
   // Watch-cache control for tests: forget history (a resumed watch gets 410 Gone), end every
   // open watch of `kind` ("pods" | "nodes" | "" = both).
   void compact(std::string_view kind);

@@ -36,10 +36,10 @@ class BindIo {
   void on_event(uint64_t k, uint32_t events);  // an epoll event of connection k
   void pump();                                 // after a batch of events: drive what is due
   // binds and batched label PATCHes not finished yet
-  size_t inflight() const { return inflight_ + labels_out_ + label_wait_.size(); }
+  size_t inflight() const { return inflight_ + labels_out_ + label_wait_.size() + deferred_.size(); }
   size_t waiting() const { return waiting_.size(); }
   // label PATCHes held for a batch: the owner's loop must come back within about a millisecond
-  bool labels_waiting() const { return !label_wait_.empty() || !lazy_.empty(); }
+  bool labels_waiting() const { return !label_wait_.empty() || !lazy_.empty() || !deferred_.empty(); }
   // Stop: every bind still in flight or waiting goes to the slow path with what it got
   // (`why` for answers that never came). The connections are closed.
   void abandon(const char* why);
@@ -52,6 +52,7 @@ class BindIo {
   // connection k is handed out for front-door sends instead of waiting in idle_
   bool publish(size_t k);
   uint64_t timeouts() const { return timeouts_; }
+  double window() const { return window_; }
 
  private:
   struct Conn;
@@ -63,7 +64,7 @@ class BindIo {
   void request(std::string* r, const char* method, const BindJob& j, bool binding, std::string_view ctype,
                const std::string& body);
   void complete(int64_t s);
-  void deliver(Conn& c, int status, std::string body);
+  void deliver(Conn& c, int status, std::string body, double retry_after = -1);
   void deliver_rest(Conn& c, const char* why);
   void fail(size_t k, const char* why);
   void drive(size_t k, uint32_t events);
@@ -73,6 +74,26 @@ class BindIo {
   void queue_label(BindJob&& j, std::string&& patch);
   void label_done(int64_t ls, int status, std::string body);
   void launch_labels();
+  // kube-apiserver's max-in-flight admission (429 TooManyRequests, Retry-After): the binds in
+  // flight are capped by an AIMD window, halved on a 429 (once per window: only an answer to a
+  // request sent after the last cut cuts again), one bind wider after a window's worth of clean
+  // binds, never above the configured maximum. A throttled bind (its binding refused before any
+  // handling, so nothing of it landed) or label goes out again after the Retry-After, from this
+  // loop; after kMaxThrottled refusals the slow path finishes it (retries, then rollback).
+  void throttle(uint64_t seq);
+  void widen();
+  void defer(BindJob&& j, std::string&& patch, bool label_only, double retry_after);
+  void resend_due(uint64_t now);
+  static constexpr int kMaxThrottled = 8;
+  double window_ = 1, max_window_ = 1, clean_ = 0;
+  uint64_t launch_seq_ = 0, cut_seq_ = 0;
+  struct Deferred {
+    uint64_t due_ns;
+    BindJob j;
+    std::string patch;
+    bool label_only;
+  };
+  std::deque<Deferred> deferred_;
 
   KubeWriter* kw_;
   int ep_;

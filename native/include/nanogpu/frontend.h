@@ -135,7 +135,7 @@ class Frontend {
   // loop and answers them itself (BindIo, bindio.h); else the writer's own io thread does.
   void set_kube_writer(const KubeTarget& t, int threads, int retries, bool record_events,
                        bool evented = true, bool label = true, double timeout_s = 30.0, bool inline_io = false,
-                       bool batch_labels = false);
+                       bool batch_labels = false, int max_binds = 0);
   const KubeWriter* kube_writer() const { return writer_.load(std::memory_order_acquire); }
   // evented writer: workers send each bind's requests themselves (KubeWriter::send_from_caller)
   void set_fe_send(bool on) {

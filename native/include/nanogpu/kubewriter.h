@@ -71,13 +71,17 @@ class HttpConn {
   int stream_head(std::string* body);
   long stream_read(std::string* out);
   int fd() const { return fd_; }
+  // the last answer's Retry-After (seconds; -1: none), as kube-apiserver sends with a 429
+  double retry_after() const { return retry_after_; }
 
  private:
   struct Head {
     int status = 0;
     long clen = -1;
     bool chunked = false, close_after = false;
+    double retry_after = -1;
   };
+  double retry_after_ = -1;
   bool connect_();
   void close_();
   bool send_all(const char* p, size_t n);
@@ -105,11 +109,17 @@ struct BindJob {
   std::vector<std::vector<int32_t>> plan;
   bool fresh = true;                     // this bind made the reservation (rollback on failure)
   uint64_t t0_ns = 0;
+  int throttled = 0;                     // times kube-apiserver answered it 429 (re-sent after Retry-After)
 };
 
 struct KubeWriterStats {
   std::atomic<uint64_t> ok{0}, failed{0}, rollbacks{0}, retries{0}, patch_ns{0}, binding_ns{0}, inflight{0},
       label_failures{0}, timeouts{0};
+  // kube-apiserver's max-in-flight admission: answers 429 TooManyRequests, the binds and labels
+  // re-sent after their Retry-After, the window cuts, and the bind window now (evented: the
+  // smallest over the writer's BindIo drivers)
+  std::atomic<uint64_t> throttled{0}, throttle_resends{0}, window_cuts{0};
+  std::atomic<int64_t> window{0};
 };
 
 // Two ways to run the writes:
@@ -131,9 +141,12 @@ class KubeWriter {
   // unanswered this long fails (a half-open connection never answers, nor resets).
   // `inline_io` (evented only): no io thread; the owners of epoll loops (front-door workers)
   // drive the requests themselves through make_io(), and submit() is not used.
+  // `max_binds` (evented / inline): binds in flight per request driver, the start and the ceiling
+  // of its admission window (0: threads x kBatch); size it under kube-apiserver's
+  // --max-mutating-requests-inflight (each bind is 2 mutating requests with the label PATCH).
   KubeWriter(KubeTarget target, std::shared_ptr<Ledger> ledger, Respond respond, int threads, int retries,
              bool record_events, bool evented = true, bool label = true, double timeout_s = 30.0,
-             bool inline_io = false);
+             bool inline_io = false, int max_binds = 0);
   ~KubeWriter();
   void submit(BindJob job);
   void stop();

@@ -231,6 +231,7 @@ const char* reason_phrase(int code) {
     case 410: return "Gone";
     case 413: return "Payload Too Large";
     case 422: return "Unprocessable Entity";
+    case 429: return "Too Many Requests";
     default: return "Status";
   }
 }
@@ -477,7 +478,8 @@ struct IoThread {
   int ep = -1, efd = -1;
   std::thread th;
   // modelled round trip: responses held until due, in arrival order (one latency for all)
-  std::deque<std::tuple<double, std::weak_ptr<Conn>, std::string>> delayed;
+  // (due, connection, bytes, a mutating request's answer: its in-flight slot is freed when written)
+  std::deque<std::tuple<double, std::weak_ptr<Conn>, std::string, bool>> delayed;
   double last_flush = 0, flush_due = 0;   // watch output coalescing (Impl::flush_watches)
   double last_event = 0;                  // the spin window (set_spin) runs from here
   std::atomic<bool> urgent{false};        // flush now, without the linger (a bulk write ended)
@@ -501,6 +503,12 @@ struct Server::Impl {
   int lfd = -1;
   std::atomic<double> latency_s{0.0};
   std::atomic<double> spin_s{0.0};   // poll this long after the last event before sleeping (0: never)
+  // max-in-flight admission (set_max_mutating_inflight): mutating requests handled whose answer
+  // is not written yet, the limit (0: none) and the 429s answered
+  std::atomic<int> mutating_inflight{0};
+  std::atomic<int> max_mutating{0};
+  std::atomic<uint64_t> n_429{0};
+  std::atomic<int> peak_mutating{0};
   double linger_s = 200e-6;   // watch output coalescing window under load
   std::atomic<bool> stopping{false};
   std::vector<std::unique_ptr<IoThread>> io;
@@ -1004,6 +1012,7 @@ namespace {
 std::string head(int code, size_t len, bool chunked = false) {
   std::string h = "HTTP/1.1 " + std::to_string(code) + " " + reason_phrase(code) +
                   "\r\nContent-Type: application/json\r\n";
+  if (code == 429) h += "Retry-After: 1\r\n";   // kube-apiserver's max-in-flight rejection
   if (chunked)
     h += "Transfer-Encoding: chunked\r\n\r\n";
   else
@@ -1157,15 +1166,36 @@ void Server::Impl::on_readable(IoThread* t, const std::shared_ptr<Conn>& c) {
       c->in.swap(rest);
       break;
     }
-    auto [code, resp] = handle(req);
+    // kube-apiserver's max-in-flight filter: a mutating request over the limit is refused before
+    // any handling (429, Retry-After: 1); one admitted holds its slot until its answer is written
+    const bool mutating = req.method == "POST" || req.method == "PUT" || req.method == "PATCH" ||
+                          req.method == "DELETE";
+    const int limit = max_mutating.load(std::memory_order_relaxed);
+    bool admitted = false;
+    std::pair<int, std::string> answer;
+    if (mutating && limit > 0) {
+      const int now_in = mutating_inflight.fetch_add(1, std::memory_order_relaxed) + 1;
+      if (now_in > limit) {
+        mutating_inflight.fetch_sub(1, std::memory_order_relaxed);
+        n_429.fetch_add(1, std::memory_order_relaxed);
+        answer = {429, status_body(429, "TooManyRequests", "Too many requests, please try again later.")};
+      } else {
+        admitted = true;
+        int pk = peak_mutating.load(std::memory_order_relaxed);
+        while (now_in > pk && !peak_mutating.compare_exchange_weak(pk, now_in, std::memory_order_relaxed)) {
+        }
+      }
+    }
+    auto [code, resp] = admitted || !(mutating && limit > 0) ? handle(req) : std::move(answer);
     c->in.erase(0, consumed);
-    const double lat = latency_s.load(std::memory_order_relaxed);
+    const double lat = code == 429 ? 0.0 : latency_s.load(std::memory_order_relaxed);
     if (lat > 0 || !t->delayed.empty()) {
       // earlier responses of this thread may still be held: keep every connection's order
-      t->delayed.emplace_back(steady_s() + lat, c, head(code, resp.size()) + resp);
+      t->delayed.emplace_back(steady_s() + lat, c, head(code, resp.size()) + resp, admitted);
     } else {
       c->out += head(code, resp.size());
       c->out += resp;
+      if (admitted) mutating_inflight.fetch_sub(1, std::memory_order_relaxed);
     }
     if (close_req) c->close_after = true;
     // a pipelined request behind this one: its answer goes out first, as Go's net/http (kube-
@@ -1312,6 +1342,7 @@ void Server::Impl::io_loop(IoThread* t) {
     while (!t->delayed.empty() && std::get<0>(t->delayed.front()) <= now) {
       auto c = std::get<1>(t->delayed.front()).lock();
       std::string bytes = std::move(std::get<2>(t->delayed.front()));
+      if (std::get<3>(t->delayed.front())) mutating_inflight.fetch_sub(1, std::memory_order_relaxed);
       t->delayed.pop_front();
       if (!c || !t->conns.count(c->fd) || t->conns[c->fd] != c) continue;
       c->out += bytes;
@@ -1527,11 +1558,14 @@ std::string Server::stats_json() const {
          ld(m.n_patch) + ",\"bind_pod\":" + ld(m.n_bind) + ",\"delete_pod\":" + ld(m.n_delete) + ",\"list\":" +
          ld(m.n_list) + ",\"watch\":" + ld(m.n_watch) + ",\"events\":" + ld(m.n_events) + ",\"lease\":" +
          ld(m.n_lease) + "},\"bulk_ns\":{\"parse\":" + ld(m.bulk_parse_ns) + ",\"insert\":" +
-         ld(m.bulk_insert_ns) + ",\"delete\":" + ld(m.bulk_delete_ns) + "}}";
+         ld(m.bulk_insert_ns) + ",\"delete\":" + ld(m.bulk_delete_ns) + "},\"admission\":{\"max_mutating_inflight\":" +
+         std::to_string(m.max_mutating.load()) + ",\"peak_mutating_inflight\":" + std::to_string(m.peak_mutating.load()) +
+         ",\"too_many_requests\":" + ld(m.n_429) + "}}";
 }
 
 void Server::set_latency(double seconds) { impl_->latency_s.store(seconds > 0 ? seconds : 0.0); }
 void Server::set_spin(double seconds) { impl_->spin_s.store(seconds > 0 ? seconds : 0.0); }
+void Server::set_max_mutating_inflight(int n) { impl_->max_mutating.store(n > 0 ? n : 0); }
 
 void Server::compact(std::string_view kind) {
   std::lock_guard<std::mutex> g(impl_->mu);

@@ -836,7 +836,7 @@ PYBIND11_MODULE(_native, m) {
           [](Frontend& f, const std::string& host, int port, bool tls, const std::string& token,
              const std::string& token_file, const std::string& ca_file, const std::string& cert_file,
              const std::string& key_file, bool insecure, int threads, int retries, bool record_events,
-             bool evented, bool label, double timeout_s, bool inline_io, bool batch_labels) {
+             bool evented, bool label, double timeout_s, bool inline_io, bool batch_labels, int max_binds) {
             KubeTarget t;
             t.host = host;
             t.port = port;
@@ -847,13 +847,15 @@ PYBIND11_MODULE(_native, m) {
             t.cert_file = cert_file;
             t.key_file = key_file;
             t.insecure = insecure;
-            f.set_kube_writer(t, threads, retries, record_events, evented, label, timeout_s, inline_io, batch_labels);
+            f.set_kube_writer(t, threads, retries, record_events, evented, label, timeout_s, inline_io, batch_labels,
+                              max_binds);
           },
           py::arg("host"), py::arg("port"), py::arg("tls") = false, py::arg("token") = "",
           py::arg("token_file") = "", py::arg("ca_file") = "", py::arg("cert_file") = "", py::arg("key_file") = "",
           py::arg("insecure") = false, py::arg("threads") = 32, py::arg("retries") = 3,
           py::arg("record_events") = true, py::arg("evented") = true, py::arg("label") = true,
           py::arg("timeout_s") = 30.0, py::arg("inline_io") = false, py::arg("batch_labels") = false,
+          py::arg("max_binds") = 0,
           "Binds whose reservation succeeded natively are finished natively (PATCH + binding + "
           "commit/rollback) on keep-alive connections to kube-apiserver: one epoll thread "
           "(evented) or `threads` blocking threads; `threads` x 8 binds in flight.")
@@ -871,6 +873,10 @@ PYBIND11_MODULE(_native, m) {
              d["binding_seconds_total"] = static_cast<double>(w->stats.binding_ns.load()) * 1e-9;
              d["label_failures"] = w->stats.label_failures.load();
              d["timeouts"] = w->stats.timeouts.load();
+             d["throttled"] = w->stats.throttled.load();
+             d["throttle_resends"] = w->stats.throttle_resends.load();
+             d["window_cuts"] = w->stats.window_cuts.load();
+             d["window"] = w->stats.window.load();
              return d;
            })
       .def("take",
@@ -1159,6 +1165,9 @@ PYBIND11_MODULE(_native, m) {
       .def("set_latency", &apisrv::Server::set_latency, py::arg("seconds"))
       .def("set_spin", &apisrv::Server::set_spin, py::arg("seconds"),
            "IO threads poll this long after their last event before sleeping (a diagnostic)")
+      .def("set_max_mutating_inflight", &apisrv::Server::set_max_mutating_inflight, py::arg("n"),
+           "kube-apiserver's --max-mutating-requests-inflight (0: none): mutating requests over it get 429 "
+           "with Retry-After: 1")
       .def("compact", &apisrv::Server::compact, py::arg("kind") = "")
       .def("drop_watches", &apisrv::Server::drop_watches, py::arg("kind") = "");
 

@@ -688,11 +688,11 @@ Frontend::Frontend(std::shared_ptr<Ledger> ledger, const std::string& host, int 
 Frontend::~Frontend() { stop(); }
 
 void Frontend::set_kube_writer(const KubeTarget& t, int threads, int retries, bool record_events, bool evented,
-                               bool label, double timeout_s, bool inline_io, bool batch_labels) {
+                               bool label, double timeout_s, bool inline_io, bool batch_labels, int max_binds) {
   if (writer_.load()) throw std::logic_error("Frontend: the kube writer is already set");
   writer_owner_ = std::make_unique<KubeWriter>(
       t, ledger_, [this](uint64_t id, int status, const std::string& body) { respond(id, status, "application/json", body); },
-      threads, retries, record_events, evented, label, timeout_s, inline_io);
+      threads, retries, record_events, evented, label, timeout_s, inline_io, max_binds);
   writer_owner_->set_batch_labels(batch_labels);
   if (inline_io) {
     for (auto& wp : workers_) {

@@ -264,9 +264,11 @@ bool HttpConn::read_head(Head* h, bool* retryable) {
       if (k == "content-length") h->clen = std::atol(v.c_str());
       else if (k == "transfer-encoding" && v.find("chunked") != std::string::npos) h->chunked = true;
       else if (k == "connection" && (v == "close" || v == "Close")) h->close_after = true;
+      else if (k == "retry-after") h->retry_after = std::atof(v.c_str());
     }
     p = e;
   }
+  retry_after_ = h->retry_after;
   return true;
 }
 
@@ -430,7 +432,7 @@ int HttpConn::request(const char* method, const std::string& path, const std::st
 
 // ------------------------------------------------------------------------------ KubeWriter
 KubeWriter::KubeWriter(KubeTarget target, std::shared_ptr<Ledger> ledger, Respond respond, int threads, int retries,
-                       bool record_events, bool evented, bool label, double timeout_s, bool inline_io)
+                       bool record_events, bool evented, bool label, double timeout_s, bool inline_io, int max_binds)
     : t_(std::move(target)), ledger_(std::move(ledger)), respond_(std::move(respond)), retries_(retries),
       timeout_s_(timeout_s > 0 ? timeout_s : 30.0), events_(record_events), evented_(evented || inline_io) {
   inline_io_ = inline_io;
@@ -461,7 +463,8 @@ KubeWriter::KubeWriter(KubeTarget target, std::shared_ptr<Ledger> ledger, Respon
   }
   if (threads < 1) threads = 1;
   if (evented_) {
-    max_inflight_ = threads * kBatch;
+    max_inflight_ = max_binds > 0 ? max_binds : threads * kBatch;
+    stats.window.store(max_inflight_, std::memory_order_relaxed);
     if (inline_io_) {
       io_done_.store(true);   // no io thread: the owners of the BindIo drivers hand off themselves
     } else {
@@ -594,7 +597,13 @@ int KubeWriter::call(HttpConn* c, const char* method, const std::string& path, c
     const bool transient = st >= 500 || st == 429;
     if (!retry || !transient || attempt >= retries_) return st;
     stats.retries.fetch_add(1, std::memory_order_relaxed);
-    std::this_thread::sleep_for(std::chrono::microseconds(5000LL << attempt));
+    // kube-apiserver's 429 says when to come back (Retry-After, seconds); else 5 ms x 2^k
+    int64_t wait_us = 5000LL << attempt;
+    if (st == 429) {
+      stats.throttled.fetch_add(1, std::memory_order_relaxed);
+      if (c->retry_after() > 0) wait_us = std::max<int64_t>(wait_us, static_cast<int64_t>(c->retry_after() * 1e6));
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(std::min<int64_t>(wait_us, 30'000'000)));
   }
 }
 

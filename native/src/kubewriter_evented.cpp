@@ -61,7 +61,9 @@ bool ieq_ascii(std::string_view a, std::string_view b) {
 // One answer at the front of `b`: 1 = complete (status, body, bytes consumed), 0 = more bytes
 // needed, -1 = not HTTP. Headers are read in place; the body is copied only for an answer
 // outside 2xx, the only one anybody reads (the slow path reports or inspects it).
-int parse_response(const std::string& b, bool eof, int* status, std::string* body, size_t* consumed, bool* close) {
+int parse_response(const std::string& b, bool eof, int* status, std::string* body, size_t* consumed, bool* close,
+                   double* retry_after) {
+  *retry_after = -1;
   const size_t he = b.find("\r\n\r\n");
   if (he == std::string::npos) return b.size() > (256u << 10) ? -1 : 0;
   if (he < 12 || b.compare(0, 5, "HTTP/") != 0) return -1;
@@ -84,6 +86,7 @@ int parse_response(const std::string& b, bool eof, int* status, std::string* bod
       if (ieq_ascii(k, "content-length")) clen = std::strtol(b.c_str() + v0, nullptr, 10);
       else if (ieq_ascii(k, "transfer-encoding") && v.find("chunked") != std::string_view::npos) chunked = true;
       else if (ieq_ascii(k, "connection") && (v == "close" || v == "Close")) *close = true;
+      else if (*status == 429 && ieq_ascii(k, "retry-after")) *retry_after = std::strtod(b.c_str() + v0, nullptr);
     }
     if (end == he) break;
     p = end;
@@ -180,6 +183,8 @@ struct BindIo::Job {
   std::string patch, binding, rp, rb;
   int sp = 0, sb = 0;
   int left = 2;
+  uint64_t seq = 0;           // launch order (the admission window's cut rule)
+  double retry_after = -1;    // a 429's Retry-After (seconds)
   bool answered = false;   // kube-scheduler has its answer (the binding landed; the label may follow)
   bool batch_label = false;   // the label goes in a later batch (queue_label), not behind the binding
 };
@@ -187,6 +192,8 @@ struct BindIo::Job {
 struct BindIo::Label {
   BindJob j;
   std::string patch;
+  uint64_t seq = 0;
+  double retry_after = -1;   // a 429's Retry-After (seconds)
 };
 
 namespace {
@@ -197,6 +204,7 @@ BindIo::BindIo(KubeWriter* kw, int ep, uint64_t tag_bit, int max_inflight, Reply
     : kw_(kw), ep_(ep), tag_bit_(tag_bit), reply_(std::move(reply)) {
   slots_.resize(static_cast<size_t>(std::max(1, max_inflight)));
   for (int64_t i = static_cast<int64_t>(slots_.size()) - 1; i >= 0; --i) free_slots_.push_back(i);
+  window_ = max_window_ = static_cast<double>(slots_.size());
   auth_ = kw_->auth();
   auth_at_ = ns_now();
   host_hdr_ = host_header(kw_->t_);
@@ -295,11 +303,27 @@ void BindIo::complete(int64_t s) {
   --inflight_;
   KubeWriterStats& st = kw_->stats;
   if (jb->answered && ok2xx(jb->sp)) {   // bound and answered earlier; the label landed too
+    widen();
     st.inflight.fetch_sub(1, std::memory_order_relaxed);
+    return;
+  }
+  // kube-apiserver refused the binding at admission (429): nothing of this bind landed (the
+  // label PATCH behind it was refused by its nodeName guard, or throttled too); the whole bind
+  // goes out again after the Retry-After, on its reservation
+  if (!jb->answered && jb->sb == 429 && jb->j.throttled < kMaxThrottled) {
+    ++jb->j.throttled;
+    defer(std::move(jb->j), std::string(), false, jb->retry_after);
+    return;   // still in flight for the writer's stats
+  }
+  // bound and answered; only its label PATCH was throttled
+  if (jb->answered && jb->sp == 429 && jb->j.throttled < kMaxThrottled) {
+    ++jb->j.throttled;
+    defer(std::move(jb->j), std::move(jb->patch), true, jb->retry_after);
     return;
   }
   IoTimer it{kWrCommit};
   const bool ok2 = ok2xx(jb->sb) && (jb->batch_label || ok2xx(jb->sp));
+  if (ok2) widen();
   if (!jb->answered) st.binding_ns.fetch_add(ns_now() - jb->j.t0_ns, std::memory_order_relaxed);
   if (ok2) {
     kw_->ledger_->commit(jb->j.uid);
@@ -326,14 +350,21 @@ void BindIo::complete(int64_t s) {
 }
 
 // the answer to connection c's oldest pending request
-void BindIo::deliver(Conn& c, int status, std::string body) {
+void BindIo::deliver(Conn& c, int status, std::string body, double retry_after) {
   const Pending p = c.pend[c.head++];
   if (c.head == c.pend.size()) {
     c.pend.clear();
     c.head = 0;
   }
-  if (p.which == 2) return label_done(p.job, status, std::move(body));
+  if (p.which == 2) {
+    if (status == 429) lslots_[static_cast<size_t>(p.job)]->retry_after = retry_after;
+    return label_done(p.job, status, std::move(body));
+  }
   Job& jb = *slots_[static_cast<size_t>(p.job)];
+  if (status == 429) {
+    throttle(jb.seq);
+    jb.retry_after = std::max(jb.retry_after, retry_after);
+  }
   if (p.which == 1) g_hops.stamp(jb.j.id, kHopAnswer);
   (p.which ? jb.sb : jb.sp) = status;
   (p.which ? jb.rb : jb.rp) = std::move(body);
@@ -484,7 +515,8 @@ void BindIo::drive(size_t k, uint32_t events) {
         std::string body;
         size_t used = 0;
         bool close = false;
-        const int rc = parse_response(c.in, eof && c.npend() == 1, &status, &body, &used, &close);
+        double retry_after = -1;
+        const int rc = parse_response(c.in, eof && c.npend() == 1, &status, &body, &used, &close, &retry_after);
         if (rc < 0) return fail(k, "bad answer from the API server");
         if (rc == 0) {
           if (!eof) return go_lazy(k);   // more bytes to come
@@ -493,7 +525,7 @@ void BindIo::drive(size_t k, uint32_t events) {
         }
         c.in.erase(0, used);
         delivered = true;
-        deliver(c, status, std::move(body));
+        deliver(c, status, std::move(body), retry_after);
         if (close) {
           eof = true;
           break;
@@ -606,6 +638,7 @@ void BindIo::adopt_handoffs() {
       jb->left = 1;
       jb->sp = 200;
     }
+    jb->seq = ++launch_seq_;
     slots_[static_cast<size_t>(s)] = std::move(jb);
     ++inflight_;
     Conn& c = *conns_[h.k];
@@ -697,7 +730,7 @@ void BindIo::start_waiting() {
     auth_ = kw_->auth();
     auth_at_ = ns_now();
   }
-  while (!waiting_.empty() && !free_slots_.empty()) {
+  while (!waiting_.empty() && !free_slots_.empty() && static_cast<double>(inflight_) < window_) {
     const int64_t s = free_slots_.back();
     free_slots_.pop_back();
     auto jb = std::make_unique<Job>();
@@ -714,6 +747,7 @@ void BindIo::start_waiting() {
       jb->left = 1;
       jb->batch_label = true;
     }
+    jb->seq = ++launch_seq_;
     slots_[static_cast<size_t>(s)] = std::move(jb);
     ++inflight_;
     launch(s);
@@ -769,7 +803,14 @@ void BindIo::label_done(int64_t ls, int status, std::string body) {
   lfree_.push_back(ls);
   --labels_out_;
   if (ok2xx(status)) {
+    widen();
     kw_->stats.inflight.fetch_sub(1, std::memory_order_relaxed);
+    return;
+  }
+  if (status == 429 && l->j.throttled < kMaxThrottled) {
+    throttle(l->seq);
+    ++l->j.throttled;
+    defer(std::move(l->j), std::move(l->patch), true, l->retry_after);
     return;
   }
   // refused by its nodeName guard cannot happen here (its binding answered 2xx): a 5xx, a
@@ -801,7 +842,8 @@ void BindIo::launch_labels() {
   while (!label_wait_.empty() && c.pend.size() < kLabelBatch) {
     const int64_t ls = label_wait_.front();
     label_wait_.pop_front();
-    const Label& l = *lslots_[static_cast<size_t>(ls)];
+    Label& l = *lslots_[static_cast<size_t>(ls)];
+    l.seq = ++launch_seq_;
     request(&one, "PATCH", l.j, false, kMergePatchE, l.patch);
     c.out += one;
     c.pend.push_back(Pending{ls, 2});
@@ -827,6 +869,7 @@ void BindIo::launch_labels() {
 }
 
 void BindIo::pump() {
+  if (!deferred_.empty()) resend_due(ns_now());   // throttled binds / labels whose Retry-After passed
   // lazy label answers due by now first: their connections are free for the binds below
   if (!lazy_.empty()) drain_lazy(ns_now());
   for (int round = 0; round < 4 && (!kick_.empty() || !waiting_.empty()); ++round) {
@@ -878,11 +921,72 @@ void BindIo::abandon(const char* why) {
     kw_->to_slow(std::move(sj));
   }
   inflight_ = 0;
+  while (!deferred_.empty()) {   // throttled, not re-sent yet: the slow path's retries finish them
+    Deferred d = std::move(deferred_.front());
+    deferred_.pop_front();
+    KubeWriter::SlowJob sj;
+    sj.answered = d.label_only;
+    if (d.label_only) {
+      sj.sp = 429;
+      sj.patch = std::move(d.patch);
+    } else {
+      kw_->build(d.j, &sj.patch, &sj.binding);
+      sj.sb = 429;
+      sj.rb = why;
+    }
+    sj.j = std::move(d.j);
+    kw_->to_slow(std::move(sj));
+  }
   for (BindJob& j : waiting_) {
     kw_->refuse(j);
     kw_->stats.inflight.fetch_sub(1, std::memory_order_relaxed);
   }
   waiting_.clear();
+}
+
+// ------------------------------------------------------------------------------ admission
+void BindIo::throttle(uint64_t seq) {
+  KubeWriterStats& st = kw_->stats;
+  st.throttled.fetch_add(1, std::memory_order_relaxed);
+  if (seq <= cut_seq_) return;   // sent before the last cut: that cut answered it already
+  window_ = std::max(1.0, window_ / 2);
+  cut_seq_ = launch_seq_;
+  clean_ = 0;
+  st.window_cuts.fetch_add(1, std::memory_order_relaxed);
+  st.window.store(static_cast<int64_t>(window_), std::memory_order_relaxed);
+}
+
+void BindIo::widen() {
+  if (window_ >= max_window_) return;
+  clean_ += 1;
+  if (clean_ < window_) return;   // one bind wider per window of clean binds
+  clean_ = 0;
+  window_ = std::min(max_window_, window_ + 1);
+  kw_->stats.window.store(static_cast<int64_t>(window_), std::memory_order_relaxed);
+}
+
+void BindIo::defer(BindJob&& j, std::string&& patch, bool label_only, double retry_after) {
+  // the server's Retry-After (kube-apiserver: 1 s), else 5 ms x 2^k as the slow path's retries
+  const double wait_s = retry_after > 0 ? std::min(retry_after, 30.0)
+                                        : 0.005 * static_cast<double>(1u << std::min(j.throttled, 12));
+  const uint64_t due = ns_now() + static_cast<uint64_t>(wait_s * 1e9);
+  Deferred d{due, std::move(j), std::move(patch), label_only};
+  auto at = deferred_.end();
+  while (at != deferred_.begin() && std::prev(at)->due_ns > due) --at;   // due order (nearly always the end)
+  deferred_.insert(at, std::move(d));
+}
+
+void BindIo::resend_due(uint64_t now) {
+  while (!deferred_.empty() && deferred_.front().due_ns <= now) {
+    Deferred d = std::move(deferred_.front());
+    deferred_.pop_front();
+    kw_->stats.throttle_resends.fetch_add(1, std::memory_order_relaxed);
+    if (d.label_only) {
+      queue_label(std::move(d.j), std::move(d.patch));   // batched with any other waiting label
+    } else {
+      waiting_.push_front(std::move(d.j));   // first in line for the window (start_waiting rebuilds it)
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------ io thread
