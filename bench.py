@@ -105,9 +105,10 @@ def parse_args():
                          "(value_independent_schedulers; 0: none)")
     ap.add_argument("--apiserver-keep-heap", action="store_true",
                     help="the shared API server's process keeps freed heap memory (no trim / unmap)")
-    ap.add_argument("--apiserver-spin-us", type=float, default=0.0,
+    ap.add_argument("--apiserver-spin-us", type=float, default=5000.0,
                     help="the shared API server's IO threads poll this long after their last event before "
-                         "sleeping (a diagnostic: are a burst's first answers slow because its cores slept?)")
+                         "sleeping (default 5 ms: a kube-apiserver serving a cluster is never idle between one "
+                         "scheduler's bursts; its CPU is reported, apiserver_cpu_us_per_pod; 0: sleep at once)")
     ap.add_argument("--apiserver-history", type=int, default=0,
                     help="the shared API server's watch cache, events per kind (0: 65536)")
     ap.add_argument("--apiserver-threads", type=int, default=0,
@@ -620,11 +621,14 @@ def apiserver_main(conn, avoid: list[int] | None = None, near: int = -1) -> None
             # version, freed under the store's lock (profiles/soak_r05.md)
             srv = core().ApiServer("127.0.0.1", 0, msg[1], msg[5] if len(msg) > 5 and msg[5] else 1 << 16)
             srv.set_latency(msg[2])
-            if len(msg) > 4 and msg[4] > 0:
-                srv.set_spin(msg[4])
+            # polling only on CPUs of its own: on the ranks' cores it would take them from the extender
+            own = not (set(os.sched_getaffinity(0)) & set(avoid or []))
+            spin = msg[4] if len(msg) > 4 and msg[4] > 0 and own else 0.0
+            if spin > 0:
+                srv.set_spin(spin)
             # kube-apiserver's default --max-mutating-requests-inflight: over it, 429 + Retry-After
             srv.set_max_mutating_inflight(msg[6] if len(msg) > 6 else 0)
-            conn.send((srv.port, sorted(os.sched_getaffinity(0))))
+            conn.send((srv.port, sorted(os.sched_getaffinity(0)), spin))
         elif op == "nodes":
             for n in msg[1]:
                 srv.call("POST", "/api/v1/nodes", n)
@@ -681,6 +685,8 @@ def apiserver_main(conn, avoid: list[int] | None = None, near: int = -1) -> None
             conn.send((sum(1 for c in codes if c == 201), time.perf_counter() - t))
         elif op == "stats":
             conn.send(_json.loads(srv.stats()))
+        elif op == "cpu":            # this process's CPU seconds (IO threads, polling included)
+            conn.send(time.process_time())
         elif op == "end":            # the pass is over
             if srv is not None:
                 srv.stop()
@@ -856,6 +862,7 @@ class ApiServerProc:
         self.proc.start()
         self.url = ""
         self.cpus: list[int] = []
+        self.spin_s = 0.0   # the IO threads' polling window in effect (0 when it shares the ranks' CPUs)
 
     def _rpc(self, *msg):
         self.conn.send(msg)
@@ -863,7 +870,7 @@ class ApiServerProc:
 
     def start(self, threads: int, latency_s: float = 0.0, keep_heap: bool = False, spin_s: float = 0.0,
               history: int = 0, max_inflight: int = 0) -> str:
-        port, self.cpus = self._rpc("start", threads, latency_s, keep_heap, spin_s, history, max_inflight)
+        port, self.cpus, self.spin_s = self._rpc("start", threads, latency_s, keep_heap, spin_s, history, max_inflight)
         self.url = f"http://127.0.0.1:{port}"
         return self.url
 
@@ -897,6 +904,9 @@ class ApiServerProc:
 
     def stats(self) -> dict:
         return self._rpc("stats")
+
+    def cpu_s(self) -> float:
+        return self._rpc("cpu")
 
     def end(self) -> None:
         self._rpc("end")
@@ -1426,6 +1436,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
             results["foreign_cpus_api"] = []
         monitor = ContentionMonitor(watch, api_watch, pl, results)
     hc.s = 0.0
+    api_cpu0 = apisrv.cpu_s() if apisrv is not None else None   # the shared API server's process
     cpu0, loop_cpu0 = time.process_time(), time.thread_time()
     threads0, ticks0, times0 = thread_cpu(), thread_ticks(), os.times()
     snap0 = affinity.cpu_snapshot()
@@ -1450,6 +1461,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
     d.sync()
     elapsed = time.perf_counter() - t0
     # the clock has stopped: the harness's own records from here (off the timed steps)
+    if api_cpu0 is not None:
+        results["apiserver_cpu_s"] = apisrv.cpu_s() - api_cpu0
     with hc:
         if monitor is not None:
             monitor.close()
@@ -1567,7 +1580,8 @@ def _cpulist(cpus: list[int]) -> str:
 # printed last on the line, in this order: what BASELINE's metric is made of
 HEADLINE_LAST = ("value_independent_schedulers", "frag_pct_steady_reference_model", "frag_pct_steady",
                  "extender_cpu_us_per_pod_rank0", "frag_pct_reference_model", "frag_hbm_pct", "frag_pct",
-                 "p99_bind_ms", "p50_bind_ms", "pods_per_s_first_filter_to_last_bind", "value")
+                 "p99_bind_extender_ms", "p99_bind_ms", "p50_bind_ms", "pods_per_s_first_filter_to_last_bind",
+                 "value")
 # bulky per-step / per-thread records: --json-out only
 DIAG_KEYS = ("step_diag_rank0", "bind_hops_us_by_decile_rank0", "io_per_pod_rank0", "controller_keys_per_pod_rank0", "python_requests_per_pod_rank0", "schedule_ms_each_step_rank0", "phase_ms_per_step_rank0",
              "extender_cpu_us_per_pod_by_thread_rank0", "extender_kernel_pct_by_thread_rank0",
@@ -1631,7 +1645,10 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
                    "api_server": ("in-process store per rank" if args.inproc_api else
                                   f"one native HTTP API server, own process "
                                   f"({args.apiserver_threads or min(16, max(4, d.world))} IO threads, "
-                                  f"max {T.API_MAX_MUTATING_INFLIGHT} mutating requests in flight: 429 over it)"),
+                                  f"max {T.API_MAX_MUTATING_INFLIGHT} mutating requests in flight: 429 over it; "
+                                  + (f"IO threads poll {1e6 * api_proc.spin_s:g} us after their last event)"
+                                     if api_proc is not None and api_proc.spin_s > 0 else "IO threads sleep when idle)")),
+                   "apiserver_cpu_us_per_pod": out.get("apiserver_cpu_us_per_pod"),
                    "cpus_rank0": _cpulist(cpus),
                    "cpus_apiserver": _cpulist(api_proc.cpus) if api_proc is not None else None,
                    "frontend": f"{args.frontend_threads} threads, busy-poll {args.busy_poll_us} us"
@@ -1649,6 +1666,9 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
         # POST /scheduler/bind wall time as kube-scheduler's stand-in sees it (request written ->
         # reply read), every bind of the timed steps on all ranks
         "p50_bind_ms": out["p50_bind_ms"], "p99_bind_ms": out["p99_bind_ms"],
+        # the same binds without the API server's answer time (bind_hops' `api` hop): the part of
+        # a bind's latency the extender owns (`bind_tail_hop` names who owns the rest of the tail)
+        "p50_bind_extender_ms": out["p50_bind_extender_ms"], "p99_bind_extender_ms": out["p99_bind_extender_ms"],
         # extender side of the same binds: request bytes read -> reply handed to the kernel
         "p50_bind_frontdoor_ms": out["p50_bind_frontdoor_ms"],
         "p99_bind_frontdoor_ms": out["p99_bind_frontdoor_ms"],
@@ -1774,6 +1794,16 @@ def main() -> int:
         cores = len(cpus) / max(1, sharing) if cpus else (os.cpu_count() or 1) / max(1, lws)
     else:
         cores = (os.cpu_count() or 1) / max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 and not args.independent_schedulers:
+        # one kube-scheduler for the job: rank 0's worker serves its cycle, the others only its
+        # binds (whose latency is the API server's), so rank 0 is the one front door that polls
+        # for the next request, on the cores the ranks share
+        if int(os.environ.get("RANK", "0")) != 0:
+            args.busy_poll_us = 0
+            args.busy_poll_prio_us = 0
+        else:
+            cores = len(cpus) if cpus else (os.cpu_count() or 1)
     if cores < 6 and args.busy_poll_us:
         # a rank keeps ~6 threads busy (2 front-door workers, its Python loop and executor, the
         # stand-in's cycle and binder): with fewer cores, spinning workers would steal them
@@ -1979,7 +2009,13 @@ def _first_vs_median(dec: dict | None, hop: str):
 def summarize(d: Dist, args, res: dict) -> dict:
     """Whole-job numbers of one pass (collective: every rank calls it)."""
     elapsed = d.max(res["elapsed_s"])
-    hops = hop_summary([h for r in d.gather_obj(res.get("bind_hops_ns", [])) for h in r])
+    rows = [h for r in d.gather_obj(res.get("bind_hops_ns", [])) for h in r]
+    hops = hop_summary(rows)
+    # the extender's own part of each bind: its wall time (request read -> reply handed to the
+    # kernel) without the API server's answer time (the `api` hop)
+    ext = sorted(sum(h) - h[BIND_HOPS.index("api")] for h in rows)
+    scheduled_all = sum(d.gather_obj(res["scheduled"]))
+    api_cpu = res.get("apiserver_cpu_s")
     client = sorted(b for r in d.gather_obj(res["client_bind_ms"]) for b in r)
     front = sorted(b for r in d.gather_obj(res["frontdoor_bind_ms"]) for b in r)
     py = sorted(b for r in d.gather_obj(res["bind_ms"]) for b in r)
@@ -1994,6 +2030,9 @@ def summarize(d: Dist, args, res: dict) -> dict:
         if firsts and lasts:
             win += max(lasts) - min(firsts)
     return {"value": round(scheduled / elapsed, 2) if elapsed > 0 else 0.0,
+            "p50_bind_extender_ms": round(ext[len(ext) // 2] / 1e6, 4) if ext else None,
+            "p99_bind_extender_ms": round(ext[min(len(ext) - 1, int(0.99 * len(ext)))] / 1e6, 4) if ext else None,
+            "apiserver_cpu_us_per_pod": round(1e6 * api_cpu / scheduled_all, 1) if api_cpu is not None and scheduled_all else None,
             "value_burst_window": round(scheduled / win, 2) if win > 0 else None,
             "ms_per_step": round(1e3 * elapsed / max(1, args.steps), 3),
             "p50_bind_ms": round(statistics.median(client), 4) if client else None,

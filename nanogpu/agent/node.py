@@ -31,9 +31,13 @@ def discover(sysfs_root: str = "", use_amdsmi: bool = True) -> tuple[NodeTopolog
     return from_host_json(host), host
 
 
-def calibrate(topo: NodeTopology, device: int = 0) -> dict:
-    """Measures what the annotation cannot read from sysfs, on the real device (HIP probe)."""
-    from ..probe.calibrate import hbm_bandwidth, local_gpu_facts
+def calibrate(topo: NodeTopology, device: int = 0, host: dict | None = None, busy_s: float = 3.0) -> dict:
+    """Measures what the annotation cannot read from sysfs, on the real devices (HIP probe):
+    the HBM copy rate, and each GPU's own mem_busy_percent scale (GpuSpec.hbm_busy_cal) under
+    the probe's stream at 25 % and 100 % of its CUs, which the extender's poller reads HBM
+    activity through (telemetry.store.normalize_hbm_activity)."""
+    from ..native import probe
+    from ..probe.calibrate import hbm_bandwidth, hbm_busy_calibration, local_gpu_facts, mem_busy_files
 
     out: dict = {}
     facts = local_gpu_facts(device)
@@ -41,6 +45,27 @@ def calibrate(topo: NodeTopology, device: int = 0) -> dict:
     if props:
         out["gcn_arch"] = props.get("gcn_arch")
         out["hbm_copy_gbs"] = round(hbm_bandwidth(device, 1 << 30, 10), 1)
+        P = probe()
+        h = host if host is not None else facts.get("host") or {}
+        files = mem_busy_files(h)
+        by_index = {g.index: g for g in topo.gpus}
+        cals, seen = {}, set()
+        # HIP ordinal k is the k-th device the reader lists (KFD order). Whole GPUs (SPX) only:
+        # the probe's CU masks assume the full chip
+        for k, hg in enumerate((h.get("gpus") or [])[:P.device_count()]):
+            parent = int(hg.get("parent", k))
+            g = by_index.get(parent)
+            if g is None or parent in seen or (hg.get("compute_partition") or "SPX").upper() != "SPX":
+                continue
+            seen.add(parent)
+            try:
+                g.hbm_busy_cal = hbm_busy_calibration(P, k, files.get(parent), seconds=busy_s)
+            except Exception:   # a probe failure leaves that GPU on the reference scale
+                log.exception("mem_busy calibration of GPU %d failed", parent)
+                g.hbm_busy_cal = []
+            if g.hbm_busy_cal:
+                cals[parent] = g.hbm_busy_cal
+        out["hbm_busy_cal"] = cals
     topo.calibration.update(out)
     return out
 
@@ -320,7 +345,7 @@ def main(argv: list[str] | None = None) -> int:
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     topo, host = discover(a.sysfs_root, not a.no_amdsmi)
     if a.calibrate:
-        calibrate(topo)
+        calibrate(topo, host=host)
     if a.print:
         print(json.dumps(topo.to_dict(), indent=1))
         return 0 if topo.devices else 1

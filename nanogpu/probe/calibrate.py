@@ -235,6 +235,36 @@ def mem_busy_file(host: dict | None = None):
     return next(iter(sorted(Path("/sys/class/drm").glob("renderD*/device/mem_busy_percent"))), None)
 
 
+def mem_busy_files(host: dict | None = None) -> dict:
+    """Physical GPU index (topology GpuSpec.index: the reader's `parent`) -> its amdgpu
+    mem_busy_percent file, for the GPUs that expose one."""
+    from pathlib import Path
+
+    host = host if host is not None else json.loads(core().discover_topology("", True))
+    out = {}
+    for k, g in enumerate(host.get("gpus") or []):
+        p = Path(f"/sys/class/drm/renderD{int(g['render_minor'])}/device/mem_busy_percent")
+        if p.exists():
+            out.setdefault(int(g.get("parent", k)), p)
+    return out
+
+
+def hbm_busy_calibration(P, device: int, busy_file, shares=(25, 100), seconds: float = 3.0) -> list:
+    """This GPU's own mem_busy_percent scale (topology GpuSpec.hbm_busy_cal): the probe's HBM
+    stream alone on `device` under a CU mask of each share for `seconds`, with every 10 ms
+    sample of `busy_file` averaged. The same kernels at the same GB/s read 54.4 / 30.1 % on one
+    box and 28.7 / 20.7 % on another, so the classifier (types.HBM_HOT_THRESHOLD, the learner's
+    curve) compares a device's readings with its own scale (telemetry.store.normalize_hbm_activity)
+    instead of one box's constants. [[share %, mean mem_busy %], ...]; [] when the counter
+    never moved (not exposed, or an idle-reading device)."""
+    if busy_file is None:
+        return []
+    runs = [(f"stream{s}", tenant_call(P, "stream", cu_share_mask(s), device)) for s in shares]
+    res = mem_busy_while(busy_file, runs, seconds=seconds)
+    cal = [[float(s), float(r["mean_all"] or 0.0)] for s, r in zip(shares, res)]
+    return cal if all(b > 0 for _, b in cal) else []
+
+
 def cu_share_mask(share_pct: float, cus: int = 256, xcds: int = 8) -> list[int]:
     """Mask words of the node agent's grant for a `share_pct` % tenant (nanogpu.agent.cumask)."""
     from ..agent import cumask

@@ -20,7 +20,7 @@ from .. import types as T
 from ..config.policy import PolicySpec
 from ..k8s import podutil as pu
 from ..k8s.informer import WorkQueue
-from .store import TelemetryStore
+from .store import TelemetryStore, normalize_hbm_activity
 
 log = logging.getLogger(__name__)
 CLUSTER_KEY = "*"          # queue key prefix of a cluster-scoped metric (never a node name)
@@ -239,12 +239,23 @@ class LoadPoller:
         periods = [(p.name, self.spec.active_duration(p.name)) for p in self.spec.sync_period
                    if p.name != T.GPU_HBM_ACTIVITY_METRIC]
         hbm_active = self.spec.active_duration(T.GPU_HBM_ACTIVITY_METRIC)
+        cal = self._hbm_cal(name)
         for card in range(n_dev):
             self.state.set_load(name, card, self.store.device_usage(name, card, periods, now))
-            # unpolled (or no longer polled) metric: the mark clears
-            busy = self.store.hbm_activity(name, card, hbm_active, now)
+            # unpolled (or no longer polled) metric: the mark clears. The reading is put on the
+            # classifier's scale through the device's own calibration (its agent's probe)
+            busy = normalize_hbm_activity(self.store.hbm_activity(name, card, hbm_active, now), cal.get(card))
             self.state.set_mem_hot(name, card, busy >= self.hbm_threshold)
             self.state.set_mem_busy(name, card, busy)
+
+    def _hbm_cal(self, name: str) -> dict[int, list]:
+        """card -> its physical GPU's mem_busy calibration (GpuSpec.hbm_busy_cal), from the
+        node's published topology; a partition shares its GPU's."""
+        e = self.state.node_entry(name)
+        if e is None or e.topology is None:
+            return {}
+        by_gpu = {g.index: g.hbm_busy_cal for g in e.topology.gpus if g.hbm_busy_cal}
+        return {k: by_gpu[d.gpu] for k, d in enumerate(e.topology.devices) if d.gpu in by_gpu}
 
     def sweep_stale(self) -> None:
         """Re-derives loads so samples that aged out stop counting (called periodically)."""

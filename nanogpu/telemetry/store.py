@@ -71,3 +71,37 @@ class TelemetryStore:
 
     def nodes(self) -> set[str]:
         return {k[0] for k in self.data}
+
+
+def normalize_hbm_activity(v: float, cal: list | None) -> float:
+    """A device's HBM activity (0..1, amdgpu mem_busy_percent / 100) on the scale of the
+    calibration box the classifier's constants come from (types.HBM_STREAMING_CURVE,
+    HBM_HOT_THRESHOLD). `cal` is that device's own curve, [[CU share %, mem_busy %], ...] of a
+    lone streaming probe (GpuSpec.hbm_busy_cal): the reading is mapped piecewise-linearly through
+    (0, 0) and each calibrated point onto the reference curve at the same share, so a quarter-GPU
+    streamer reads as one on every box (one box: 20.7 % where the calibration box read 30.1 %).
+    The reference (prometheus.go:70-76, allocate.go:173-195) likewise normalises load values
+    before bucketing them. No calibration: the reading as it is."""
+    pts = sorted((float(s), float(b)) for s, b in (cal or []) if b > 0)
+    if not pts or v <= 0:
+        return max(0.0, v)
+    ref = T.HBM_STREAMING_CURVE
+
+    def ref_at(share: float) -> float:
+        if share <= ref[0][0]:
+            return ref[0][1] * share / ref[0][0]
+        for (s0, b0), (s1, b1) in zip(ref, ref[1:]):
+            if share <= s1:
+                return b0 + (b1 - b0) * (share - s0) / (s1 - s0)
+        return ref[-1][1]
+
+    xs = [0.0] + [b for _, b in pts]
+    ys = [0.0] + [ref_at(s) for s, _ in pts]
+    x = 100.0 * v
+    for k in range(1, len(xs)):
+        if x <= xs[k] or k == len(xs) - 1:
+            x0, x1, y0, y1 = xs[k - 1], xs[k], ys[k - 1], ys[k]
+            y = y0 + (y1 - y0) * (x - x0) / (x1 - x0) if x1 > x0 else y1
+            return max(0.0, min(1.0, y / 100.0))
+    return max(0.0, min(1.0, v))
+

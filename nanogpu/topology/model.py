@@ -13,7 +13,8 @@ Schema (version 1):
   "version": 1, "model": "AMD Instinct MI355X", "gfx": "gfx950",
   "virtualization": "BAREMETAL",
   "gpus":    [{"index": 0, "numa": 0, "cus": 256, "xcds": 8, "hbm_mib": 294912,
-               "compute_partition": "SPX", "memory_partition": "NPS1", "bdf": "0000:05:00.0"}],
+               "compute_partition": "SPX", "memory_partition": "NPS1", "bdf": "0000:05:00.0",
+               "hbm_busy_cal": [[25, 20.7], [100, 28.7]]}],   # optional (agent --calibrate)
   "devices": [{"gpu": 0, "part": 0, "cus": 256, "xcds": 8, "hbm_mib": 294912}],
   "link_bw": [[0.0, 153.0, ...], ...],     # GB/s between physical GPUs (0 = no direct link)
   "calibration": {...}                      # optional probe results (HBM GB/s, CU map)
@@ -44,6 +45,11 @@ class GpuSpec:
     ras_ce: int = 0
     xgmi_peers: int = 0          # xGMI links of this GPU (visible or not from the agent's cgroup)
     xgmi_link_gbs: float = 0.0   # slowest of them, GB/s (KFD io_link max_bandwidth)
+    # this GPU's own mem_busy_percent scale: [[CU share %, mem_busy %], ...] of the agent's
+    # streaming probe alone on it (agent --calibrate, probe.calibrate.hbm_busy_calibration);
+    # the poller maps readings through it onto types.HBM_STREAMING_CURVE (telemetry.store
+    # normalize_hbm_activity). Empty: readings are taken as they are.
+    hbm_busy_cal: list = field(default_factory=list)
 
 
 @dataclass

@@ -55,12 +55,16 @@ FLAG_MEM_BOUND = 1
 # streaming tenant (alloc.h Device::mem_hot), declared or not. It feeds only that mark, not the
 # reference's load sum (RemainLoad), so the reference's load semantics are unchanged.
 GPU_HBM_ACTIVITY_METRIC = "gpu_hbm_activity_avg"
-# Measured on the MI355X box (tools/hbm_share_calibration.py, profiles/gpu_calibration.md):
-# amdgpu's mem_busy_percent averaged over 8 s of one tenant alone on the GPU. A streaming HBM
-# copy reads 10.9 / 30.1 / 48.8 / 54.4 % holding 12.5 / 25 / 50 / 100 % of the CUs; a bf16 MFMA
-# burn reads 0 % at 25, 75 and 100 %. The device mark fires for a streamer of a quarter of the
-# GPU or more (0.25); a full-chip streamer's 54 % would barely clear the old 0.5.
-HBM_HOT_THRESHOLD = 0.25
+# Measured on the MI355X calibration box (tools/hbm_share_calibration.py,
+# profiles/gpu_calibration.md): amdgpu's mem_busy_percent averaged over 8 s of one tenant alone
+# on the GPU. A streaming HBM copy reads 10.9 / 30.1 / 48.8 / 54.4 % holding 12.5 / 25 / 50 / 100 %
+# of the CUs; a bf16 MFMA burn reads 0 % at 25, 75 and 100 %. Other boxes read the same kernels at
+# the same GB/s on another scale (20.7 / 28.7 % for 25 / 100 % on one): the poller maps every
+# reading onto this box's scale through the device's own calibration (GpuSpec.hbm_busy_cal,
+# telemetry.store.normalize_hbm_activity) before these constants apply. The device mark fires
+# for a streamer of a quarter of the GPU or more (30.1 on this scale): 0.20 leaves a single
+# reading a third of margin under that mean, and stays over an eighth-GPU streamer (10.9).
+HBM_HOT_THRESHOLD = 0.20
 # (share %, mem_busy %) of a lone streaming tenant, from the same calibration: the learner's
 # threshold for a pod alone on a device is HBM_LEARN_FRACTION of the curve at that pod's share
 # (capped at the device threshold), so a lone 25 % streamer (30 %) is learned while a lone MFMA

@@ -159,6 +159,10 @@ class Frontend {
   // binds this process answered natively with a pod another worker process's filter parsed
   // (Ledger::take_pod_info), and pods it handed to the other workers that way
   std::atomic<uint64_t> bind_handoffs{0}, pods_published{0};
+  // binds whose pod another worker had not published yet when they came (they waited for it)
+  std::atomic<uint64_t> handoff_waits{0};
+  static constexpr uint64_t kHandoffWaitNs = 200'000;
+  static constexpr uint64_t kDeferredNominationWaitNs = 100'000;
   std::atomic<uint64_t> loop_max_ns{0};   // longest event-batch a worker spent between epoll_waits
   // longest single step of a batch: 0 accept, 1 mailbox, 2 read+cycle verbs, 3 deferred binds,
   // 4 pod-cache lock wait (bind), 5 node lookup (bind), 6 Python hand-off (defer)
@@ -199,9 +203,10 @@ class Frontend {
   void prepare_bind(std::string_view body, PyRequest* r, VerbScratch& s);
   void cache_pod(VerbScratch& s, std::string_view uid, const CachedPod& cached, std::string_view raw, const Demand& dem);
   void run_deferred(VerbScratch& s);   // a worker verb's work left for after its answer went out
-  // a nomination may wait until after the answer only where nothing can read the ledger in
-  // between: one worker thread and no other process on the ledger (kube-scheduler's next filter
-  // may reach another connection's thread or another worker, and must see this pod's devices held)
+  // a nomination may wait until after the answer with one worker thread (this worker reads
+  // nothing in between). kube-scheduler's next filter may reach another worker process: the
+  // ledger counts the deferred nominations, and that filter waits until they are made
+  // (Ledger::wait_deferred_nominations), so it never sees the ledger without this pod's devices
   bool defer_nominate_ok(const VerbScratch& s) const;
   void note_bind_wall(uint64_t ns);
   // a response for connection `conn` of worker w, on w's thread: sent, then its next request

@@ -179,6 +179,11 @@ struct LedgerHeader {
   std::atomic<uint64_t> nom_adopted;
   std::atomic<uint64_t> nom_moved;
   std::atomic<int32_t> nom_margin;
+  // nominations a worker left for after its answer (Frontend::run_deferred): begun before the
+  // answer went out, done once made; a filter on another worker waits while they differ
+  // (wait_deferred_nominations), so it never reads the ledger without a pod answered before it
+  alignas(64) std::atomic<uint64_t> nom_deferred_begun;
+  std::atomic<uint64_t> nom_deferred_done;
   alignas(64) std::atomic<int64_t> n_pods;
   // learned request-size mix (Ledger::note_request): decayed counts of share sizes and the
   // set of the common ones, which native binpack's waste model uses (alloc.h SizeSet)
@@ -256,6 +261,14 @@ class Ledger {
   // 0 (any unique top node); each nomination a bind moves elsewhere raises it by 2 (to 40),
   // every 16 adopted ones lower it by 1: nominations stay where kube-scheduler agrees.
   int32_t nomination_margin() const { return hdr_->nom_margin.load(std::memory_order_relaxed); }
+  // a nomination this worker makes after its answer: begin() before the answer is written,
+  // end() once Ledger::nominate ran (Frontend::run_deferred)
+  void deferred_nomination_begin() { hdr_->nom_deferred_begun.fetch_add(1, std::memory_order_release); }
+  void deferred_nomination_end() { hdr_->nom_deferred_done.fetch_add(1, std::memory_order_release); }
+  // before a filter reads the ledger: until every nomination another worker deferred past its
+  // answer is made, at most `max_ns` (a worker that died in between cannot hold filters up for
+  // longer). False: it timed out.
+  bool wait_deferred_nominations(uint64_t max_ns) const;
   // nominations made so far, anywhere in the region (a change marker)
   uint64_t nominations_made() const { return hdr_->nom_made.load(std::memory_order_acquire); }
   void nomination_counts(uint64_t* made, uint64_t* adopted, uint64_t* moved) const {

@@ -1275,7 +1275,8 @@ void Server::Impl::io_loop(IoThread* t) {
     if (spin > 0 && wait_s > 0) {
       // a diagnostic: the thread polls instead of sleeping for `spin` after its last event,
       // so its core never idles between a burst's requests (or across a short gap)
-      const double until = t->last_event + spin;
+      // not past the next held answer's due time or the watch flush: those go out on time
+      const double until = std::min(t->last_event + spin, steady_s() + wait_s);
       while ((n = wait_events(t->ep, evs, 256, 0.0)) == 0 && steady_s() < until &&
              !stopping.load(std::memory_order_relaxed)) {
       }

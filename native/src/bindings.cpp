@@ -741,6 +741,11 @@ PYBIND11_MODULE(_native, m) {
            "Relist: release Committed pods recorded before `before` (mono_now) whose key is not in "
            "`live`; returns the keys released")
       .def("drop_nomination", &Ledger::drop_nomination, py::call_guard<py::gil_scoped_release>())
+      .def("deferred_nomination_begin", &Ledger::deferred_nomination_begin)
+      .def("deferred_nomination_end", &Ledger::deferred_nomination_end)
+      .def("wait_deferred_nominations", &Ledger::wait_deferred_nominations, py::arg("max_ns"),
+           py::call_guard<py::gil_scoped_release>(),
+           "Until every nomination a worker deferred past its answer is made (False: `max_ns` passed).")
       .def(
           "nominate",
           [](Ledger& l, int32_t id, const std::string& key, const py::sequence& demand,
@@ -966,6 +971,7 @@ PYBIND11_MODULE(_native, m) {
         d["mailbox_wakeups"] = f.mb_wakeups.load();
         d["bind_handoffs"] = f.bind_handoffs.load();
         d["pods_published"] = f.pods_published.load();
+        d["handoff_waits"] = f.handoff_waits.load();
         py::list ph;
         for (const auto& x : f.phase_max_ns) ph.append(static_cast<double>(x.load()) * 1e-9);
         d["phase_max_s"] = ph;

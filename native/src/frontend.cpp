@@ -968,9 +968,20 @@ void Frontend::prepare_bind(std::string_view body, PyRequest* r, VerbScratch& s)
   }
   if (cached && !r->pod_json.empty()) return;
   if (!cached) {
-    // another worker process's filter parsed it (its bind came over another connection)
+    // another worker process's filter parsed it (its bind came over another connection). That
+    // worker publishes it just after its filter answer (Frontend::run_deferred): a bind that
+    // overtook the publish waits for it a little, then goes to Python (which reads the pod)
     std::string blob;
-    if (!ledger_->take_pod_info(uid, &blob) || !unpack_pod(blob, &pod)) return;
+    bool got = ledger_->take_pod_info(uid, &blob);
+    if (!got && ledger_->attached() > 1) {
+      const uint64_t t_end = fast_ns() + kHandoffWaitNs;
+      while (!got && fast_ns() < t_end) {
+        for (int k = 0; k < 64; ++k) __builtin_ia32_pause();
+        got = ledger_->take_pod_info(uid, &blob);
+      }
+      if (got) handoff_waits.fetch_add(1, std::memory_order_relaxed);
+    }
+    if (!got || !unpack_pod(blob, &pod)) return;
     bind_handoffs.fetch_add(1, std::memory_order_relaxed);
     if (pod.name != name || pod.ns != ns || pod.completed || id < 0) return;   // Python reads the pod itself
   }
@@ -1525,9 +1536,7 @@ void Frontend::cache_pod(VerbScratch& s, std::string_view uid, const CachedPod& 
   put_pod(uid, cached, raw, dem);
 }
 
-bool Frontend::defer_nominate_ok(const VerbScratch& s) const {
-  return s.defer_cache && ledger_->attached() <= 1;
-}
+bool Frontend::defer_nominate_ok(const VerbScratch& s) const { return s.defer_cache; }
 
 void Frontend::run_deferred(VerbScratch& s) {
   if (!s.defer_put && !s.defer_nominate) return;
@@ -1539,6 +1548,7 @@ void Frontend::run_deferred(VerbScratch& s) {
   if (s.defer_nominate) {
     IoTimer it{kFeVerbNominate};
     ledger_->nominate(s.defer_node, last.uid, s.defer_dem, s.opt);
+    ledger_->deferred_nomination_end();
   }
   s.defer_put = s.defer_nominate = false;
 }
@@ -1883,6 +1893,9 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   const Options& o = s.opt;
   const bool normalize = s.normalize, nominate = s.nominate, decisive = s.decisive && !o.compat;
   io_end(kFeVerbNames, io0);
+  // a nomination another worker left for after its answer is made before this verb reads the
+  // ledger (this worker's own ran before it read this request); bounded
+  if (nominate && ledger_->attached() > 1) ledger_->wait_deferred_nominations(kDeferredNominationWaitNs);
   io0 = io_t0();
   // not against itself; priorities right behind this worker's filter of the same pod text
   // (`reused`) with no nomination made anywhere since find it dropped already: no second trip
@@ -1894,11 +1907,12 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     s.nom_dropped = reused || (pod >= 0 && last.valid);   // about the pod `last` holds
   }
   if ((pod >= 0 || reused) && !uid.empty() && !(prioritize && has_pod(uid))) {
-    // filter caches the pod for its bind; priorities of the same cycle find it there. After
-    // the answer only when no other worker can read the bind first: kube-scheduler sends it
-    // on another connection, which another thread or worker process may serve (a miss there
-    // goes to the Python path); a late nomination is harmless (a reserved pod ignores it)
-    if (s.defer_cache && ledger_->attached() <= 1 && last.valid && uid.data() == last.uid.data()) {
+    // filter caches the pod for its bind (and, with other worker processes on the ledger,
+    // publishes it for their binds); priorities of the same cycle find it there. After the
+    // answer with one worker thread: the pod's own bind is the only reader, and it follows the
+    // answer. A bind on another worker process that comes before the deferred publish waits
+    // for it (prepare_bind, kHandoffWaitNs); one on this thread comes after it
+    if (s.defer_cache && last.valid && uid.data() == last.uid.data()) {
       s.defer_put = true;   // the pod is last.raw / last.uid / last.cached: stable until the next request
       s.defer_dem = dem;
     } else {
@@ -1936,6 +1950,7 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
         s.defer_nominate = true;
         s.defer_node = ids[nom];
         s.defer_dem = dem;
+        ledger_->deferred_nomination_begin();   // other workers' filters wait for it
       } else {
         IoTimer it{kFeVerbNominate};
         ledger_->nominate(ids[nom], uid, dem, o);
@@ -2052,6 +2067,7 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
         s.defer_nominate = true;
         s.defer_node = ids[best];
         s.defer_dem = dem;
+        ledger_->deferred_nomination_begin();   // other workers' filters wait for it
       } else {
         IoTimer it{kFeVerbNominate};
         ledger_->nominate(ids[best], uid, dem, o);

@@ -20,7 +20,7 @@
 namespace nanogpu {
 
 static constexpr uint64_t kMagic = 0x4e414e4f47505531ULL;  // "NANOGPU1"
-static constexpr uint32_t kVersion = 16;  // 4: HBM pools; 5: cache lines; 6: sizes; 7: serving; 8: nominations; 9: stream owners; 10: overflow records; 11: node epoch; 12-13: bind handoff; 14: dense node generations; 15: device change ring; 16: wide records
+static constexpr uint32_t kVersion = 17;  // 4: HBM pools; 5: cache lines; 6: sizes; 7: serving; 8: nominations; 9: stream owners; 10: overflow records; 11: node epoch; 12-13: bind handoff; 14: dense node generations; 15: device change ring; 16: wide records; 17: deferred nominations
 
 static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -1109,6 +1109,20 @@ int32_t Ledger::commit(std::string_view key) {
 int32_t Ledger::release(std::string_view key) { return release_if(key, -1); }
 
 int32_t Ledger::drop_nomination(std::string_view key) { return release_if(key, kPodNominated); }
+
+bool Ledger::wait_deferred_nominations(uint64_t max_ns) const {
+  if (hdr_->nom_deferred_done.load(std::memory_order_acquire) ==
+      hdr_->nom_deferred_begun.load(std::memory_order_acquire))
+    return true;
+  const auto t_end = std::chrono::steady_clock::now() + std::chrono::nanoseconds(max_ns);
+  for (;;) {
+    for (int k = 0; k < 32; ++k) __builtin_ia32_pause();
+    if (hdr_->nom_deferred_done.load(std::memory_order_acquire) >=
+        hdr_->nom_deferred_begun.load(std::memory_order_acquire))
+      return true;
+    if (std::chrono::steady_clock::now() > t_end) return false;
+  }
+}
 
 int32_t Ledger::drop_reservation(std::string_view key) { return release_if(key, kPodReserved); }
 

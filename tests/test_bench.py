@@ -137,45 +137,46 @@ def test_plain_gpus_n_starts_n_ranks_itself(tmp_path, cpu_exclusive):
     assert d["scheduled"] == 200 and d["failed"] == 0
 
 
-def test_one_scheduler_over_two_workers_keeps_the_one_worker_rate(cpu_exclusive):
-    """one kube-scheduler's binds spread over 2 extender workers (the driver's
-    N = 2 headline) run at the 1-worker rate on the same CPUs: the bind handoff through the
-    shared ledger costs the cycle nothing. Interleaved runs, best of each (this host's noise is
-    other tenants'); the same front-door settings on both (no busy poll: with 2 ranks on 8 CPUs
-    the bench turns it off). On the MI355X box's CPUs: 42.7k (1) vs 42.5k / 44.1k / 42.3k pods/s
-    at 2 / 4 / 8 ranks (profiles/scaling_rehearsal.md, round 5)."""
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_one_scheduler_over_n_workers_keeps_the_one_worker_rate(ranks, cpu_exclusive):
+    """one kube-scheduler's binds spread over N extender workers (the
+    driver's N-GPU headline) schedule at >= 0.9x the 1-worker rate on the same CPUs. The cycle
+    stays on rank 0's worker; the binds the other workers answer take their pod from the shared
+    ledger's handoff, which the cycle's worker publishes after its filter answer
+    (Frontend::run_deferred), so the handoff costs the cycle nothing. Measured: the extender's
+    ledger operations per pod are the same at 1 and 4 workers, each 40 % slower when other
+    processes' binds wrote the node state (cache lines from other cores), and the publish was
+    2.6 us a pod inside the filter before it moved past the answer (profiles/scaling_rehearsal.md).
+    The scheduling rate of each run's fastest step (pods / the stand-in's first filter -> last
+    bind span: the harness's per-step barriers are outside it), best of interleaved runs (this
+    host's other tenants swing whole runs). The front door that serves the cycle polls 8 us for
+    its next request on both sides (with N ranks only rank 0's does: the others serve binds
+    alone); without it, rank 0's thread, which at N > 1 no longer serves most binds between two
+    cycle requests, sleeps between them and every request pays a wake-up (0.83-0.88x here with
+    polling off on both sides, 0.97x with it on). No skip: a shortfall fails."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
-    base = ["--no-gpu", "--steps", "6", "--warmup", "2", "--busy-poll-us", "0", "--rtt-variant-ms", "0",
+    base = ["--no-gpu", "--steps", "8", "--warmup", "2", "--rtt-variant-ms", "0",
             "--steady-variant-steps", "0", "--nodes-variant", "0", "--inproc-variant-steps", "0",
             "--independent-variant-steps", "0", "--decisive-variant-steps", "0"]
-    # the scheduling rate of each run's fastest step (pods a step / the stand-in's first filter ->
-    # last bind span): this host's other tenants swing whole runs 3x, a quiet step of each side is
-    # the comparable one; the span leaves out the harness's per-step gloo barriers, which only
-    # the 2-rank job has
-    got = {1: [], 2: []}
+    got = {1: [], ranks: []}
     with tempfile.TemporaryDirectory() as tmp:
-        for rnd in range(8):
-            for n in (1, 2):
+        for rnd in range(6):
+            for n in (1, ranks):
                 out = Path(tmp) / f"r{n}_{rnd}.json"
                 r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(n), "--json-out", str(out)]
                                    + base, capture_output=True, text=True, timeout=400, env=env, cwd="/tmp")
                 assert r.returncode == 0, r.stderr[-3000:]
                 d = _last_json(r.stdout)
                 assert d["n_gpus"] == n and d["failed"] == 0
-                if n == 2:
+                if n > 1:
                     assert d["bind_handoffs"] > 0 and d["value_mode"].startswith("one kube-scheduler stand-in")
-                spans = json.loads(out.read_text())["diagnostics"]["schedule_ms_each_step_rank0"]
-                per_step = d["scheduled"] / len(spans)
-                got[n].append(round(1e3 * per_step / min(spans), 1))
-            # four pairs decide unless other work on the host starved one side; then four more
-            if rnd >= 3 and max(got[2]) >= 0.9 * max(got[1]):
+                diag = json.loads(out.read_text())["diagnostics"]
+                assert diag["python_requests_per_pod_rank0"] == 0.0   # every bind stayed native
+                spans = diag["schedule_ms_each_step_rank0"]
+                got[n].append(round(1e3 * d["scheduled"] / len(spans) / min(spans), 1))
+            if rnd >= 1 and max(got[ranks]) >= 0.9 * max(got[1]):
                 break
-    if max(got[2]) < 0.9 * max(got[1]) and max(got[1]) > 1.4 * min(got[1]):
-        # the 1-rank runs alone swing by more than the margin tested: other tenants on this
-        # shared host, which the 2-rank job (one more extender process) feels more. The box's
-        # rehearsal on CPUs of its own is the measurement (profiles/scaling_rehearsal.md)
-        pytest.skip(f"host too noisy to compare rates: 1-rank runs {sorted(got[1])}")
-    assert max(got[2]) >= 0.9 * max(got[1]), got
+    assert max(got[ranks]) >= 0.9 * max(got[1]), got
 
 
 def test_plain_gpus_n_refuses_when_fewer_gpus_are_visible(tmp_path):

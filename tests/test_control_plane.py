@@ -776,3 +776,78 @@ def test_deleted_node_slot_goes_when_its_last_share_does():
     st.register_node(pu.make_node("c", 8, synthetic_mi355x(8).to_json()))
     st.ledger.release("held2")
     assert st.retry_removals() == [] and st.ledger.find_node("c") >= 0
+
+
+def test_hbm_activity_is_read_through_the_devices_own_calibration():
+    """the same quarter-GPU streamer reads 30.1 % on the calibration box and
+    20.7 % on another (28.7 % for the whole chip there). The agent publishes each GPU's own scale
+    (GpuSpec.hbm_busy_cal, probe.calibrate.hbm_busy_calibration); the poller maps readings through
+    it onto the reference curve, so the same tenant is classified the same on both boxes."""
+    from nanogpu.telemetry.store import normalize_hbm_activity as norm
+
+    cal = [[25, 20.7], [100, 28.7]]
+    assert norm(0.207, cal) == pytest.approx(0.301, abs=1e-3)      # the box's 25 % streamer -> reference's
+    assert norm(0.287, cal) == pytest.approx(0.544, abs=1e-3)      # its whole-chip streamer
+    assert norm(0.0, cal) == 0.0 and norm(0.9, cal) <= 1.0
+    assert norm(0.207, []) == 0.207 and norm(0.207, None) == 0.207   # no calibration: as read
+    xs = [i / 100 for i in range(101)]
+    assert all(norm(a, cal) <= norm(b, cal) for a, b in zip(xs, xs[1:]))   # monotone
+    # the calibration box's own scale is the identity at its points
+    assert norm(0.301, [[25, 30.1], [100, 54.4]]) == pytest.approx(0.301, abs=1e-3)
+
+    async def main():
+        # a 17 % reading: under the hot threshold as read, a quarter-GPU streamer's on this box
+        series = {T.GPU_HBM_ACTIVITY_METRIC: {("n0", 0): [0.17], ("n0", 1): [0.17], ("n1", 0): [0.17]}}
+        runner, port, _ = await fake_prometheus(series)
+        st = ClusterState(policy="binpack", load_aware=True)
+        t = synthetic_mi355x(2)
+        t.gpus[0].hbm_busy_cal = cal          # GPU 0 calibrated, GPU 1 not
+        t2 = synthetic_mi355x(2)
+        n0 = pu.make_node("n0", 2, t.to_json(), {"amd.com/gpu.present": "true"})
+        n1 = pu.make_node("n1", 2, t2.to_json(), {"amd.com/gpu.present": "true"})
+        st.register_node(n0)
+        st.register_node(n1)
+        assert st.node_entry("n0").topology.gpus[0].hbm_busy_cal == cal   # through the annotation
+        spec = PolicySpec(sync_period=(Period(T.GPU_HBM_ACTIVITY_METRIC, 15),))
+        poller = LoadPoller(st, PromClient(f"http://127.0.0.1:{port}"), lambda: [n0, n1], spec=spec)
+        try:
+            await poller.sync_metric(T.GPU_HBM_ACTIVITY_METRIC)
+            d0 = st.ledger.snapshot(st.node_entry("n0").id)["devices"]
+            d1 = st.ledger.snapshot(st.node_entry("n1").id)["devices"]
+            assert [d["mem_hot"] for d in d0] == [True, False]
+            assert d0[0]["mem_busy"] == 25 and d0[1]["mem_busy"] == 17
+            assert not d1[0]["mem_hot"]
+        finally:
+            await poller.prom.close()
+            await runner.cleanup()
+
+    asyncio.run(main())
+
+
+def test_agent_calibration_lands_on_each_whole_gpu(monkeypatch):
+    """agent.node.calibrate measures each SPX GPU's scale on its own HIP ordinal and mem_busy
+    file and publishes it in the topology annotation (probe calls stubbed: no GPU here)."""
+    from nanogpu.agent import node as A
+    from nanogpu.probe import calibrate as C
+    from nanogpu.topology.model import NodeTopology
+
+    class P:
+        @staticmethod
+        def device_count():
+            return 2
+
+    calls = []
+    monkeypatch.setattr(C, "local_gpu_facts", lambda device=0, use_probe=True: {"props": {"gcn_arch": "gfx950"}})
+    monkeypatch.setattr(C, "hbm_bandwidth", lambda *a, **k: 5994.0)
+    monkeypatch.setattr(C, "mem_busy_files", lambda h: {0: "busy0", 1: "busy1"})
+    monkeypatch.setattr(C, "hbm_busy_calibration",
+                        lambda P_, k, f, seconds=3.0: calls.append((k, f)) or [[25, 20.0 + k], [100, 28.0 + k]])
+    import nanogpu.native as NV
+    monkeypatch.setattr(NV, "probe", lambda *a, **k: P)
+    host = {"gpus": [{"parent": 0, "compute_partition": "SPX"}, {"parent": 1, "compute_partition": "SPX"}]}
+    topo = synthetic_mi355x(2)
+    out = A.calibrate(topo, host=host, busy_s=0.0)
+    assert calls == [(0, "busy0"), (1, "busy1")]
+    assert out["hbm_busy_cal"] == {0: [[25, 20.0], [100, 28.0]], 1: [[25, 21.0], [100, 29.0]]}
+    back = NodeTopology.from_json(topo.to_json())
+    assert back.gpus[1].hbm_busy_cal == [[25, 21.0], [100, 29.0]]

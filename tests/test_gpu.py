@@ -497,6 +497,44 @@ def test_share_aware_learner_learns_a_lone_25pct_streamer_not_a_lone_75pct_mfma_
     assert L.is_stream_owner("rs-stream") and not L.is_stream_owner("rs-mfma")
 
 
+@pytest.fixture(scope="module")
+def busy_cal(host, P):
+    """This device's own mem_busy scale (the agent's --calibrate: the probe's stream alone at
+    25 % and 100 % of the CUs, every 10 ms sample averaged), then a 25 % streamer and a 75 % MFMA
+    tenant alone for 16 s each, sampled as the original assertion did (readings 5 s apart)."""
+    from nanogpu.probe import calibrate as C
+
+    f = C.mem_busy_file(host)
+    if f is None:
+        pytest.skip("mem_busy_percent not exposed")
+    cal = C.hbm_busy_calibration(P, 0, f, seconds=3.0)
+    runs = [(label, C.tenant_call(P, kind, C.cu_share_mask(share)))
+            for label, kind, share in (("stream25", "stream", 25), ("mfma75", "mfma", 75))]
+    res = {r["label"]: r for r in C.mem_busy_while(f, runs, seconds=16.0)}
+    record("mem_busy_calibration", {"cal": cal, "tenants": res})
+    print(json.dumps({"cal": cal, "tenants": res}, indent=1))
+    return cal, res
+
+
+def test_calibrated_hbm_classifier_on_5s_samples(busy_cal):
+    """with this device's own calibration the classifier tells a quarter-GPU
+    streamer (hot) from a 75 % MFMA tenant (not) on samples 5 s apart, on a box whose scale is
+    not the calibration box's (one read 20.7 / 28.7 % where the constants' box read 30.1 / 54.4)."""
+    from nanogpu import types as T
+    from nanogpu.telemetry.store import normalize_hbm_activity as norm
+
+    cal, res = busy_cal
+    assert len(cal) == 2 and all(b > 0 for _, b in cal), cal
+    assert cal[0][1] < cal[1][1], cal                 # a quarter of the CUs streams less than all
+    s, m = res["stream25"], res["mfma75"]
+    assert s["rate"] > 500 and m["rate"] > 300, (s, m)   # GB/s, TFLOP/s: both tenants really ran
+    assert s["mean_5s"] is not None and m["mean_5s"] is not None, (s, m)
+    assert norm(s["mean_5s"] / 100, cal) >= T.HBM_HOT_THRESHOLD, (cal, s)
+    assert norm(m["mean_5s"] / 100, cal) < T.HBM_HOT_THRESHOLD, (cal, m)
+    # and the averages the poller converges to
+    assert norm(s["mean_all"] / 100, cal) >= T.HBM_HOT_THRESHOLD > norm(m["mean_all"] / 100, cal)
+
+
 _RCCL_SCRIPT = r"""
 import json, os, sys
 import torch
