@@ -327,6 +327,8 @@ class Runtime:
         for inf in (self.node_informer, self.pod_informer):
             if inf is not None:
                 await inf.stop()
+        if self.extender is not None:
+            await self.extender.drain()
         if self.api is not None and hasattr(self.api, "close"):
             await self.api.close()
 
@@ -408,8 +410,32 @@ def guard_busy_poll(cfg: Config) -> None:
         cfg.busy_poll_prio_us = 0
 
 
+def check_region_space(path: str, max_nodes: int, max_pods: int) -> None:
+    """The shared ledger is a file on a tmpfs (/dev/shm, an emptyDir with medium Memory in the
+    deployment): a region larger than the filesystem's free space maps fine and then raises
+    SIGBUS on the first page past it. Refuse to start instead, naming the sizes (the region
+    grows with --max-nodes and --max-pods: Ledger::region_bytes)."""
+    from .native import core
+
+    need = int(core().Ledger.region_bytes(max_nodes, max_pods))
+    d = os.path.dirname(os.path.abspath(path)) or "/"
+    try:
+        st = os.statvfs(d)
+    except OSError:
+        return
+    free = st.f_bavail * st.f_frsize
+    if os.path.exists(path):
+        free += os.path.getsize(path)   # a stale region of ours is replaced
+    if need > free:
+        raise SystemExit(f"nano-gpu: the shared ledger needs {need >> 20} MiB (--max-nodes {max_nodes}, "
+                         f"--max-pods {max_pods}) but {d} has {free >> 20} MiB free: raise the /dev/shm "
+                         f"emptyDir sizeLimit or lower the flags")
+
+
 def run(cfg: Config) -> int:
     guard_busy_poll(cfg)
+    if cfg.ledger_path or cfg.workers > 1:
+        check_region_space(cfg.ledger_path or "/dev/shm/nanogpu-ledger", cfg.max_nodes, cfg.max_pods)
     if cfg.workers <= 1:
         if cfg.ledger_path:
             _drop_stale_region(cfg.ledger_path)

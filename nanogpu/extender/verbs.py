@@ -354,3 +354,17 @@ class Extender:
         t = asyncio.ensure_future(coro)
         self._bg.add(t)
         t.add_done_callback(self._bg.discard)
+
+    async def drain(self, timeout_s: float = 2.0) -> None:
+        """Stop: the label PATCHes and events still in the background get `timeout_s` to land
+        (a graceful shutdown leaves no bound pod without its label), then are cancelled, before
+        the API client closes. The label is eventual: a process killed in between leaves a bound
+        pod without it; its placement annotations came with the binding, and this extender's
+        own rebuild reads those (the reference's label selector is the only reader of it)."""
+        if not self._bg:
+            return
+        _, pending = await asyncio.wait(list(self._bg), timeout=timeout_s)
+        for t in pending:
+            t.cancel()
+        if pending:
+            await asyncio.gather(*pending, return_exceptions=True)

@@ -851,3 +851,18 @@ def test_agent_calibration_lands_on_each_whole_gpu(monkeypatch):
     assert out["hbm_busy_cal"] == {0: [[25, 20.0], [100, 28.0]], 1: [[25, 21.0], [100, 29.0]]}
     back = NodeTopology.from_json(topo.to_json())
     assert back.gpus[1].hbm_busy_cal == [[25, 21.0], [100, 29.0]]
+
+
+def test_a_ledger_larger_than_the_tmpfs_is_refused_at_start(tmp_path, monkeypatch):
+    """a region past the /dev/shm emptyDir's size would SIGBUS on first touch; the
+    extender refuses to start and names the sizes instead."""
+    import os as _os
+
+    from nanogpu import app as A
+
+    class St:
+        f_bavail, f_frsize = 16, 1 << 20      # 16 MiB free
+    monkeypatch.setattr(_os, "statvfs", lambda d: St)
+    with pytest.raises(SystemExit, match="needs .* MiB"):
+        A.check_region_space(str(tmp_path / "ledger"), 4096, 1 << 20)
+    A.check_region_space(str(tmp_path / "ledger"), 8, 64)   # a small one fits

@@ -1,6 +1,6 @@
 import sys, json, asyncio
 sys.path.insert(0, __import__('os').path.dirname(__import__('os').path.dirname(__import__('os').path.abspath(__file__))))
-import bench
+from nanogpu.sim import benchlib
 from nanogpu.app import Config, Runtime
 from nanogpu.k8s import podutil as pu
 from nanogpu.k8s.fake_apiserver import FakeKubeStore, InProcKube
@@ -14,7 +14,7 @@ async def scan():
     rt = Runtime(Config(port=0, host="127.0.0.1", policy_config_path="/nonexistent", ledger_path=f"/dev/shm/vb3-{id(store)}", nominate=False), api=InProcKube(store))
     await rt.start()
     fe = rt.native.fe
-    p = bench.burst(0, 1, 12, 0, 7)[0]
+    p = benchlib.burst(0, 1, 12, 0, 7)[0]
     for k in (1, 64):
         names = [f"mi355x-{i:03d}" for i in range(k)]
         body = json.dumps({"Pod": p, "Nodes": None, "NodeNames": names}, separators=(",", ":")).encode()
