@@ -389,18 +389,18 @@ def test_overflow_records_hold_wide_pods_and_are_reused():
 def test_share_aware_learner_threshold_follows_the_streaming_curve():
     """with a curve the learner compares a lone pod's device activity with
     the curve at that pod's share. The default curve (types.HBM_STREAMING_CURVE, measured on
-    the box) halved: 12.5 % -> 5.5, 25 % -> 15, 75 % -> 25 (capped at the device threshold)."""
+    the box) halved: 12.5 % -> 5.5, 25 % -> 15, 75 % -> 20 (capped at the device threshold, 0.20)."""
     from nanogpu.config.policy import PolicySpec
 
     curve = PolicySpec().learn_curve()
     t = synthetic_mi355x(4)
     L, (nid,) = ledger_with(t)
     for key, owner, pct, dev, busy in (("a", "o-small", 12, 0, 10), ("b", "o-quarter", 25, 1, 30),
-                                       ("c", "o-big-cool", 75, 2, 20), ("d", "o-big-hot", 75, 3, 40)):
+                                       ("c", "o-big-cool", 75, 2, 18), ("d", "o-big-hot", 75, 3, 40)):
         assert L.allocate_plan(nid, key, [(pct, 0)], [[dev]], True) == N.OK
         L.set_pod_owner(key, owner)
         assert L.set_mem_busy(nid, dev, busy) == N.OK
-    assert [d["mem_busy"] for d in L.snapshot(nid)["devices"]] == [10, 30, 20, 40]
+    assert [d["mem_busy"] for d in L.snapshot(nid)["devices"]] == [10, 30, 18, 40]
     assert L.learn_stream_owners(True, N.mono_now(), 1, curve) == (3, 0)
     assert [L.is_stream_owner(o) for o in ("o-small", "o-quarter", "o-big-cool", "o-big-hot")] == \
         [True, True, False, True]
