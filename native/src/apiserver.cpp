@@ -1270,18 +1270,18 @@ void Server::Impl::io_loop(IoThread* t) {
     if (!t->delayed.empty()) wait_s = std::min(wait_s, std::get<0>(t->delayed.front()) - steady_s());
     if (t->flush_due > 0) wait_s = std::min(wait_s, t->flush_due - steady_s());
     wait_s = std::max(0.0, wait_s);
+    const double deadline = steady_s() + wait_s;   // the next held answer / watch flush is due
     int n = 0;
     const double spin = spin_s.load(std::memory_order_relaxed);
     if (spin > 0 && wait_s > 0) {
-      // a diagnostic: the thread polls instead of sleeping for `spin` after its last event,
-      // so its core never idles between a burst's requests (or across a short gap)
-      // not past the next held answer's due time or the watch flush: those go out on time
-      const double until = std::min(t->last_event + spin, steady_s() + wait_s);
+      // the thread polls instead of sleeping for `spin` after its last event, so its core never
+      // idles between a burst's requests (or across a short gap); never past `deadline`
+      const double until = std::min(t->last_event + spin, deadline);
       while ((n = wait_events(t->ep, evs, 256, 0.0)) == 0 && steady_s() < until &&
              !stopping.load(std::memory_order_relaxed)) {
       }
     }
-    if (n == 0) n = wait_events(t->ep, evs, 256, wait_s);
+    if (n == 0) n = wait_events(t->ep, evs, 256, std::max(0.0, deadline - steady_s()));
     if (n > 0 && spin > 0) t->last_event = steady_s();
     for (int i = 0; i < n; ++i) {
       const int fd = evs[i].data.fd;
