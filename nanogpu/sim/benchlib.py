@@ -149,7 +149,10 @@ def node_template(d: Dist, args) -> tuple[object, dict]:
     from nanogpu.topology.model import synthetic_mi355x
 
     info = {"gpu": None, "link_bw_source": "placeholder"}
-    hbm_mib = 288 * 1024
+    # without a GPU (--no-gpu rehearsals) the node is the MI355X the box reports: amdgpu's VRAM
+    # size there is 294,896 MiB (tests/fixtures/sysfs/mi355x_real), 16 MiB under 288 GiB, which
+    # moves HBM fits at the margin: the rehearsal and the GPU run then schedule the same node
+    hbm_mib = MI355X_VRAM_MIB
     if not args.no_gpu:
         from nanogpu.probe.calibrate import local_gpu_facts
 
@@ -206,6 +209,7 @@ def node_template(d: Dist, args) -> tuple[object, dict]:
 
 # --------------------------------------------------------------------------- workload
 SIZES = (10, 25, 50)
+MI355X_VRAM_MIB = 294_896   # amdgpu's VRAM of one MI355X as the box reports it (mem_info_vram_total)
 INFLIGHT_BINDS = 64   # the stand-in's binds in flight in Python mode, and the harness's API client pool
 HBM_GIB = (8, 16, 32, 64)
 
@@ -1252,7 +1256,7 @@ def steady_keys(args, topo, v) -> dict:
         from nanogpu import types as T
         from nanogpu.sim import fragsim
 
-        hbm = topo.devices[0].hbm_mib if topo.devices else 288 * 1024
+        hbm = topo.devices[0].hbm_mib if topo.devices else MI355X_VRAM_MIB
         n_steps = 1 + s_args.warmup + s_args.steps
         kw = dict(steps=n_steps, nodes=s_args.nodes, hbm_mib=hbm, initial=s_args.pods, churn=STEADY_CHURN,
                   seed=STEADY_SEED, first=1 + s_args.warmup + s_args.steps // 2)
@@ -1316,7 +1320,7 @@ def nodes_variant_keys(args, topo, v) -> dict:
     if args.partition == "SPX" and args.policy == "binpack" and not args.compat:
         from nanogpu.sim import fragsim
 
-        hbm = topo.devices[0].hbm_mib if topo.devices else 288 * 1024
+        hbm = topo.devices[0].hbm_mib if topo.devices else MI355X_VRAM_MIB
         kw = dict(steps=n_args.steps, nodes=n_args.nodes, hbm_mib=hbm, pods=n_args.pods, kube=True)
         keys[f"frag_pct_{tag}_reference_model"] = fragsim.headline(True, **kw)["frag_pct"]
         keys[f"frag_pct_{tag}_native_replay"] = fragsim.headline(False, **kw)["frag_pct"]
@@ -1332,7 +1336,7 @@ def reference_model_frag(args, topo) -> dict:
         return {"frag_pct_reference_model": None}
     from nanogpu.sim import fragsim
 
-    hbm = topo.devices[0].hbm_mib if topo.devices else 288 * 1024
+    hbm = topo.devices[0].hbm_mib if topo.devices else MI355X_VRAM_MIB
     kw = dict(steps=args.steps, nodes=args.nodes, hbm_mib=hbm, pods=args.pods, kube=True)
     ref, nat = fragsim.headline(True, **kw), fragsim.headline(False, **kw)
     return {"frag_pct_reference_model": ref["frag_pct"], "frag_hbm_pct_reference_model": ref["frag_hbm_pct"],
