@@ -112,7 +112,7 @@ def parse_args():
                          "sleeping (default 5 ms: a kube-apiserver serving a cluster is never idle between one "
                          "scheduler's bursts; its CPU is reported, apiserver_cpu_us_per_pod; 0: sleep at once)")
     ap.add_argument("--apiserver-threads", type=int, default=0,
-                    help="shared API server IO threads (0: one per rank, 4 to 16)")
+                    help="shared API server IO threads (0: 4; more spinning threads starve its bulk create at 8 ranks)")
     ap.add_argument("--bind-writer-mode", choices=["inline", "evented", "frontdoor", "threads"], default="evented",
                     help="the extender's native bind writer: one epoll thread (evented), the front door sending "
                          "and one epoll thread reading the answers (frontdoor), the front door alone (inline), "
@@ -394,7 +394,7 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
                    # or --inproc-api's per-rank in-process store (value_inproc_api)
                    "api_server": ("in-process store per rank" if args.inproc_api else
                                   f"one native HTTP API server, own process "
-                                  f"({args.apiserver_threads or min(16, max(4, d.world))} IO threads, "
+                                  f"({args.apiserver_threads or 4} IO threads, "
                                   f"max {T.API_MAX_MUTATING_INFLIGHT} mutating requests in flight: 429 over it; "
                                   + (f"IO threads poll {1e6 * api_proc.spin_s:g} us after their last event)"
                                      if api_proc is not None and api_proc.spin_s > 0 else "IO threads sleep when idle)")),

@@ -710,7 +710,7 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         url = None
         if d.rank == 0:
             apisrv = api_proc
-            url = apisrv.start(args.apiserver_threads or min(16, max(4, d.world)), args.api_rtt_ms / 1e3,
+            url = apisrv.start(args.apiserver_threads or 4, args.api_rtt_ms / 1e3,
                                args.apiserver_spin_us / 1e6,
                                T.API_MAX_MUTATING_INFLIGHT)
             if getattr(args, "_placement", None):

@@ -176,9 +176,10 @@ struct LedgerHeader {
   // (the bind went to another node: kube-scheduler's own scores overrode ours), and the score
   // lead a node needs over the runner-up before priorities nominate it (adaptive)
   alignas(64) std::atomic<uint64_t> nom_made;
-  std::atomic<uint64_t> nom_adopted;
+  std::atomic<int32_t> nom_margin;   // read by every priorities call
+  // written by the binds, which land on any worker: a line apart from what priorities read
+  alignas(64) std::atomic<uint64_t> nom_adopted;
   std::atomic<uint64_t> nom_moved;
-  std::atomic<int32_t> nom_margin;
   // nominations a worker left for after its answer (Frontend::run_deferred): begun before the
   // answer went out, done once made; a filter on another worker waits while they differ
   // (wait_deferred_nominations), so it never reads the ledger without a pod answered before it

@@ -20,7 +20,7 @@
 namespace nanogpu {
 
 static constexpr uint64_t kMagic = 0x4e414e4f47505531ULL;  // "NANOGPU1"
-static constexpr uint32_t kVersion = 17;  // 4: HBM pools; 5: cache lines; 6: sizes; 7: serving; 8: nominations; 9: stream owners; 10: overflow records; 11: node epoch; 12-13: bind handoff; 14: dense node generations; 15: device change ring; 16: wide records; 17: deferred nominations
+static constexpr uint32_t kVersion = 18;  // 4: HBM pools; 5: cache lines; 6: sizes; 7: serving; 8: nominations; 9: stream owners; 10: overflow records; 11: node epoch; 12-13: bind handoff; 14: dense node generations; 15: device change ring; 16: wide records; 17: deferred nominations; 18: adoption counters on a line of their own
 
 static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -873,7 +873,15 @@ int32_t Ledger::assume(int32_t id, const Demand& d, const Options& o_in, Plan* p
 
 namespace {
 constexpr int32_t kNominatedElsewhere = -1000;   // internal: release the nomination, retry
+
+// a bind adopted its pod's nomination: every 16th lowers the nomination margin by one
+void note_adopted(LedgerHeader* h) {
+  if ((h->nom_adopted.fetch_add(1, std::memory_order_relaxed) + 1) % 16 != 0) return;
+  int32_t m = h->nom_margin.load(std::memory_order_relaxed);
+  while (m > 0 && !h->nom_margin.compare_exchange_weak(m, m - 1, std::memory_order_relaxed)) {
+  }
 }
+}  // namespace
 
 int32_t Ledger::reserve(int32_t id, std::string_view key, const Demand& d, const Options& o,
                         Plan* plan) {
@@ -911,6 +919,22 @@ int32_t Ledger::reserve_as(int32_t id, std::string_view key, const Demand& d, co
   const KeyBuf kb(key);
   const uint64_t h = key_hash(kb.c_str());
   const int s = shard_of(h);
+  if (state == kPodReserved) {
+    // A bind adopting its nomination changes the pod's state only, never the node's devices:
+    // under the pod shard's lock alone (a pod's state is written under it; release_if re-checks
+    // under node + shard lock). The node's lock line then stays with the worker that runs the
+    // scheduling cycle instead of moving to whichever worker took the bind.
+    lock_mu(&hdr_->shard_mu[s].m);
+    Unlock us{&hdr_->shard_mu[s].m};
+    PodSlot* p = find_pod_locked(s, h, kb.c_str());
+    if (p && p->state == kPodNominated && p->node == id) {
+      note_adopted(hdr_);
+      p->state = state;
+      p->t_reserved = mono_now();
+      get_record(*p, nullptr, plan);
+      return kOk;
+    }
+  }
   lock_node(n);
   Unlock un{&n->mu};
   {
@@ -921,12 +945,7 @@ int32_t Ledger::reserve_as(int32_t id, std::string_view key, const Demand& d, co
       if (p->state == kPodNominated) {
         if (p->node != id) return kNominatedElsewhere;
         // adopt (bind) or refresh (a repeated priorities call) the nomination
-        if (state == kPodReserved &&
-            (hdr_->nom_adopted.fetch_add(1, std::memory_order_relaxed) + 1) % 16 == 0) {
-          int32_t m = hdr_->nom_margin.load(std::memory_order_relaxed);
-          while (m > 0 && !hdr_->nom_margin.compare_exchange_weak(m, m - 1, std::memory_order_relaxed)) {
-          }
-        }
+        if (state == kPodReserved) note_adopted(hdr_);
         p->state = state;
         p->t_reserved = mono_now();
         get_record(*p, nullptr, plan);

@@ -138,7 +138,7 @@ def test_plain_gpus_n_starts_n_ranks_itself(tmp_path, cpu_exclusive):
 
 
 @pytest.mark.parametrize("ranks", [2, 4])
-def test_one_scheduler_over_n_workers_keeps_the_one_worker_rate(ranks, cpu_exclusive):
+def test_one_scheduler_over_n_workers_keeps_the_one_worker_rate(ranks, cpu_alone):
     """one kube-scheduler's binds spread over N extender workers (the
     driver's N-GPU headline) schedule at >= 0.9x the 1-worker rate on the same CPUs. The cycle
     stays on rank 0's worker; the binds the other workers answer take their pod from the shared
@@ -155,7 +155,7 @@ def test_one_scheduler_over_n_workers_keeps_the_one_worker_rate(ranks, cpu_exclu
     cycle requests, sleeps between them and every request pays a wake-up (0.83-0.88x here with
     polling off on both sides, 0.97x with it on). No skip: a shortfall fails."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
-    base = ["--no-gpu", "--steps", "8", "--warmup", "2", "--rtt-variant-ms", "0",
+    base = ["--no-gpu", "--steps", "24", "--warmup", "2", "--rtt-variant-ms", "0",
             "--steady-variant-steps", "0", "--nodes-variant", "0", "--inproc-variant-steps", "0",
             "--independent-variant-steps", "0", "--decisive-variant-steps", "0"]
     got = {1: [], ranks: []}

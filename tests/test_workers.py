@@ -144,12 +144,22 @@ def test_ledger_refuses_a_short_or_foreign_region(tmp_path):
                 os.unlink(p)
 
 
+def _die_with_parent():
+    """The replica runs in a session of its own (the test signals its whole group); if the test
+    process is killed before its `finally` (an interrupted `pytest -x -n`), the replica gets
+    SIGTERM instead of living on as an orphan."""
+    import ctypes
+
+    ctypes.CDLL(None, use_errno=True).prctl(1, signal.SIGTERM)   # PR_SET_PDEATHSIG
+
+
 async def _start_replica(api_port, port, ledger, *extra):
     proc = subprocess.Popen([sys.executable, "-m", "nanogpu", "--kube-api", f"http://127.0.0.1:{api_port}",
                              "--workers", "2", "--host", "127.0.0.1", "--ledger-path", ledger,
                              "--policyConfigPath", "/nonexistent", *extra],
                             env=dict(os.environ, PORT=str(port)), cwd=str(ROOT),
-                            stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True)
+                            stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True,
+                            preexec_fn=_die_with_parent)
     deadline = time.time() + 60
     while True:
         try:
