@@ -181,7 +181,8 @@ class Runtime:
             # the controller's, and an unschedulable pod's condition updates never reach us
             self.pod_informer = Informer(self.api, "pods", slim=True, prefilter=self.state.ledger,
                                          field_selector=T.ASSIGNED_PODS if self.cfg.watch_assigned_only else None)
-            pc = PodController(self.state, self.pod_informer, workers=self.cfg.threadness, metrics=self.metrics)
+            pc = PodController(self.state, self.pod_informer, workers=self.cfg.threadness, metrics=self.metrics,
+                               relabel=self._relabel if self.cfg.assume_label else None)
             self.controllers.append(pc)
             pc.start()
             self.tasks.append(self.pod_informer.start())
@@ -262,6 +263,12 @@ class Runtime:
                                                                   reuse_port=self.cfg.workers > 1)
             log.info("worker %d serving on :%d (%s front door, policy=%s compat=%s)", self.worker, self.bound_port,
                      self.cfg.frontend, self.state.policy, self.state.options.compat)
+
+    async def _relabel(self, ns: str, name: str, node: str) -> None:
+        """The assume label of a placed pod, guarded by its node (podutil.label_patch)."""
+        from .k8s import podutil as pu
+
+        await self.api.patch_pod(ns, name, pu.label_patch(node))
 
     def _informer_metrics(self) -> bytes:
         f = self.pod_informer.watch_filter if self.pod_informer is not None else None

@@ -27,14 +27,21 @@ log = logging.getLogger(__name__)
 
 
 class PodController:
-    def __init__(self, state: ClusterState, informer: Informer, workers: int = 1, metrics=None):
+    def __init__(self, state: ClusterState, informer: Informer, workers: int = 1, metrics=None,
+                 relabel=None):
         self.state = state
         self.informer = informer
         self.queue = WorkQueue("podQueue")
         self.workers = max(1, workers)
         self.metrics = metrics
+        # async (namespace, name, node): PATCHes the assume label onto a bound pod. The bind
+        # answers kube-scheduler once the binding (which carries the placement annotations)
+        # landed and the label follows; a process killed in between leaves a placed pod
+        # without it, which the next relist (every start begins with one) puts back
+        self.relabel = relabel
         self._tasks: list[asyncio.Task] = []
         self.reconciled = 0        # shares released because a relist no longer held their pod
+        self.relabeled = 0         # assume labels re-applied after a relist
         informer.add_handler(self._on_event)
         informer.add_relist_hook(self._on_relist)
         if getattr(informer, "watch_filter", None) is not None:
@@ -68,6 +75,29 @@ class PodController:
             if self.metrics:
                 self.metrics.pods_released.inc(len(gone))
             log.info("relist: released %d pods deleted while the watch was down", len(gone))
+        if self.relabel is not None:
+            missing = [(m.get("namespace", "default"), m.get("name", ""), pu.node_name_of(p))
+                       for p in pods for m in (pu.meta(p),)
+                       if pu.node_name_of(p) and pu.is_assumed(p)
+                       and (m.get("labels") or {}).get(T.LABEL_GPU_ASSUME) != "true"
+                       and not pu.share_gone(p, self.state.options.compat)]
+            if missing:
+                self._tasks.append(asyncio.ensure_future(self._relabel_all(missing)))
+
+    async def _relabel_all(self, missing: list[tuple[str, str, str]]) -> None:
+        sem = asyncio.Semaphore(8)
+
+        async def one(ns: str, name: str, node: str) -> None:
+            async with sem:
+                try:
+                    await self.relabel(ns, name, node)
+                    self.relabeled += 1
+                except Exception as e:   # gone, moved, or the API down: the next relist retries
+                    log.warning("relist: assume label of %s/%s not re-applied: %s", ns, name, e)
+
+        await asyncio.gather(*(one(*m) for m in missing))
+        log.info("relist: re-applied the assume label to %d of %d placed pods without it",
+                 self.relabeled, len(missing))
 
     def _on_event(self, etype: str, pod: dict, old: dict | None) -> None:
         # hot: every pod event of the cluster passes here (four per scheduled pod), so the

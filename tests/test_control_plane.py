@@ -109,6 +109,39 @@ def test_restart_rebuilds_ledger_from_annotations_skipping_completed():
     asyncio.run(main())
 
 
+def test_restart_puts_back_an_assume_label_the_last_incarnation_did_not_write():
+    """the bind answers once the binding (placement annotations) landed and the
+    reference's `nano-gpu/assume` label follows; a process killed in between leaves a placed pod
+    without the label, which the reference lists assumed pods by (dealer.go:59, 280). The next
+    start's relist re-applies it, guarded by the pod's node; a completed pod, a pod without the
+    placement and a pod already labelled are left alone."""
+    async def main():
+        store = FakeKubeStore()
+        store.add_node(node())
+        for name, phase in (("placed", "Running"), ("done", "Succeeded")):
+            p = annotated(name, "n0", [[2]], 40, phase=phase)
+            del p["metadata"]["labels"][T.LABEL_GPU_ASSUME]
+            store.create_pod(p)
+        store.create_pod(annotated("labelled", "n0", [[3]], 40))
+        foreign = pu.make_pod("foreign", [("c", 10)])
+        foreign["spec"]["nodeName"] = "n0"
+        store.create_pod(foreign)
+        patches_before = store.counts.get("patch_pod", 0)
+        rt = await runtime(store)
+        try:
+            ctl = rt.controllers[-1]
+            assert await wait_for(lambda: ctl.relabeled == 1)
+            labels = {n: (store.get_pod("default", n)["metadata"].get("labels") or {}).get(T.LABEL_GPU_ASSUME)
+                      for n in ("placed", "done", "labelled", "foreign")}
+            assert labels == {"placed": "true", "done": None, "labelled": "true", "foreign": None}, labels
+            assert store.counts.get("patch_pod", 0) - patches_before == 1
+            assert free(rt)[2] == 60 and free(rt)[3] == 60      # the rebuild itself is unchanged
+        finally:
+            await rt.stop()
+
+    asyncio.run(main())
+
+
 def test_node_capacity_change_and_delete():
     async def main():
         store = FakeKubeStore()
