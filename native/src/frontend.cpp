@@ -286,28 +286,53 @@ static uint64_t text_hash(std::string_view s) {
 }
 
 // A JSON array of plain strings written compactly, `["a","b"]` (what kube-scheduler's Go encoder
-// sends), into name views and token views (quotes included). false: any other shape (spaces,
-// escapes, non-strings), which the caller hands to the JSON parser.
-static bool scan_string_array(std::string_view t, std::vector<std::string_view>* nv,
-                              std::vector<std::string_view>* nraw) {
-  if (t.size() < 2 || t.front() != '[' || t.back() != ']') return false;
-  size_t p = 1;
-  if (t.size() == 2) return true;
-  for (;;) {
-    if (p >= t.size() || t[p] != '"') return false;
-    const char* q = static_cast<const char*>(std::memchr(t.data() + p + 1, '"', t.size() - p - 1));
-    if (!q) return false;
-    const size_t e = static_cast<size_t>(q - t.data());
-    const std::string_view name = t.substr(p + 1, e - p - 1);
-    for (char ch : name)
-      if (ch == '\\' || static_cast<unsigned char>(ch) < 0x20) return false;
-    nv->push_back(name);
-    nraw->push_back(t.substr(p, e - p + 1));
-    p = e + 1;
-    if (p == t.size() - 1) return true;
-    if (t[p] != ',') return false;
-    ++p;
+// sends), into its tokens' (offset, length), quotes included. false: any other shape (spaces,
+// escapes, non-strings), which the caller hands to the JSON parser. One pass, 16 bytes a step:
+// the quotes' positions from a byte compare, and any backslash or control byte anywhere sends
+// the list the parser's way (sampled windows of 420 names are 5 KB: a window not seen before
+// is scanned whole on the scheduling cycle's path).
+static bool scan_string_array(std::string_view t, std::vector<std::pair<uint32_t, uint32_t>>* toks) {
+  const size_t n = t.size();
+  if (n < 2 || t.front() != '[' || t.back() != ']') return false;
+  if (n == 2) return true;
+  const char* b = t.data();
+  const __m128i quote = _mm_set1_epi8('"'), bslash = _mm_set1_epi8('\\'), space = _mm_set1_epi8(0x20);
+  size_t expect = 1;   // where the next name's opening quote must be
+  size_t open = 0;
+  bool in_str = false, closed = false;
+  for (size_t base = 0; base < n; base += 16) {
+    __m128i v;
+    if (base + 16 <= n) {
+      v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(b + base));
+    } else {
+      alignas(16) char tail[16];
+      std::memset(tail, ' ', sizeof tail);
+      std::memcpy(tail, b + base, n - base);
+      v = _mm_load_si128(reinterpret_cast<const __m128i*>(tail));
+    }
+    // a byte below 0x20 (unsigned) or a backslash: not the plain shape
+    const __m128i ctl = _mm_andnot_si128(_mm_cmpeq_epi8(_mm_max_epu8(v, space), v), _mm_set1_epi8(-1));
+    if (_mm_movemask_epi8(_mm_or_si128(ctl, _mm_cmpeq_epi8(v, bslash)))) return false;
+    for (uint32_t m = static_cast<uint32_t>(_mm_movemask_epi8(_mm_cmpeq_epi8(v, quote))); m; m &= m - 1) {
+      const size_t q = base + static_cast<size_t>(__builtin_ctz(m));
+      if (closed) return false;
+      if (!in_str) {
+        if (q != expect) return false;
+        open = q;
+        in_str = true;
+        continue;
+      }
+      in_str = false;
+      toks->emplace_back(static_cast<uint32_t>(open), static_cast<uint32_t>(q - open + 1));
+      if (q + 2 == n) {
+        closed = true;
+      } else {
+        if (b[q + 1] != ',') return false;
+        expect = q + 2;
+      }
+    }
   }
+  return closed;
 }
 
 namespace {
@@ -324,12 +349,43 @@ struct NameTable {
   std::vector<Slot> slots;
   std::string arena;
   size_t used = 0;
+  // by node id: its name in the arena, and the id that followed it in the last list resolved.
+  // kube-scheduler's lists are windows of its own node order, so the next name is nearly always
+  // the successor seen before (one compare of bytes laid out in id order, no hash); a node that
+  // filled up, left out of the window, costs one lookup and moves the successor
+  std::vector<std::pair<uint32_t, uint32_t>> at;
+  std::vector<int32_t> succ;
   void reset(uint64_t o, uint64_t e) {
     owner = o;
     epoch = e;
     slots.assign(1024, Slot{});
     arena.clear();
     used = 0;
+    at.clear();
+    succ.clear();
+  }
+  bool is(int32_t id, std::string_view name) const {
+    if (id < 0 || static_cast<size_t>(id) >= at.size()) return false;
+    const auto& [off, len] = at[static_cast<size_t>(id)];
+    if (len != name.size() || len == 0) return false;
+    const char* a = arena.data() + off;
+    if (len >= 8 && len <= 16) {   // node names: two overlapping 8-byte words, no call
+      uint64_t x0, y0, x1, y1;
+      std::memcpy(&x0, a, 8);
+      std::memcpy(&y0, name.data(), 8);
+      std::memcpy(&x1, a + len - 8, 8);
+      std::memcpy(&y1, name.data() + len - 8, 8);
+      return ((x0 ^ y0) | (x1 ^ y1)) == 0;
+    }
+    return std::memcmp(a, name.data(), len) == 0;
+  }
+  int32_t next_of(int32_t id) const {
+    return id >= 0 && static_cast<size_t>(id) < succ.size() ? succ[static_cast<size_t>(id)] : -1;
+  }
+  void set_next(int32_t id, int32_t next) {
+    if (id < 0) return;
+    if (static_cast<size_t>(id) >= succ.size()) succ.resize(static_cast<size_t>(id) + 1, -1);
+    succ[static_cast<size_t>(id)] = next;
   }
   int32_t find(std::string_view name) const {
     if (slots.empty()) return -1;
@@ -358,6 +414,10 @@ struct NameTable {
     s.id = id;
     arena.append(name);
     place(s);
+    if (id >= 0) {
+      if (static_cast<size_t>(id) >= at.size()) at.resize(static_cast<size_t>(id) + 1, {0u, 0u});
+      at[static_cast<size_t>(id)] = {s.off, s.len};
+    }
   }
   void place(const Slot& s) {
     const size_t mask = slots.size() - 1;
@@ -509,6 +569,37 @@ struct IdCache {
       if (k != mru && same(k, t)) return k;
     return -1;
   }
+  // The nodes of list `src` that a filter answered as fitting (`rcs[i] == kOk`), kept as a list
+  // of its own: kube-scheduler sends priorities exactly that list, in that order, re-encoded the
+  // way a compact escape-free list is written. Once nodes fill up, the answer is a subset of the
+  // request's window, so without this every priorities call would scan and resolve its whole
+  // list again (6 us at 420 nodes).
+  void remember_subset(int src, const std::vector<int32_t>& rcs) {
+    if (src < 0 || !valid[src] || tok[src].size() != rcs.size()) return;
+    int k = src == 0 ? 1 : 0;
+    for (int j = 0; j < kListSlots; ++j)
+      if (j != src && used[j] < used[k]) k = j;
+    std::string& t = text[k];
+    t.clear();
+    t += '[';
+    tok[k].clear();
+    ids[k].clear();
+    for (size_t i = 0; i < rcs.size(); ++i) {
+      if (rcs[i] != kOk) continue;
+      if (t.size() > 1) t += ',';
+      const auto& [off, n] = tok[src][i];
+      tok[k].emplace_back(static_cast<uint32_t>(t.size()), n);
+      t.append(text[src], off, n);
+      ids[k].push_back(ids[src][i]);
+    }
+    t += ']';
+    valid[k] = true;
+    compact[k] = true;
+    len[k] = t.size();
+    epoch[k] = epoch[src];
+    used[k] = ++clock;
+    mru = k;   // the next request is this pod's priorities
+  }
 };
 }  // namespace
 
@@ -519,7 +610,8 @@ struct IdCache {
 // samples when they were thread_local).
 struct Frontend::VerbScratch {
   json::Doc top, d, other, dn;
-  std::vector<std::string_view> nv, nraw;
+  std::vector<std::string_view> nv, nraw;                // a list in another shape (the JSON parser's)
+  std::vector<std::pair<uint32_t, uint32_t>> ntok;       // a compact list scanned now: its tokens
   std::vector<int32_t> rcs, scores;
   LastPod last;
   IdCache idc;
@@ -542,6 +634,7 @@ struct Frontend::VerbScratch {
   bool defer_cache = false;   // the pod-cache put too: only with one worker thread (see filter_verb)
   bool defer_put = false;
   bool defer_nominate = false;
+  int defer_list = -1;   // the filter's node-list slot whose fitting subset priorities will send
   int32_t defer_node = -1;
   Demand defer_dem{};
 };
@@ -1539,6 +1632,11 @@ void Frontend::cache_pod(VerbScratch& s, std::string_view uid, const CachedPod& 
 bool Frontend::defer_nominate_ok(const VerbScratch& s) const { return s.defer_cache; }
 
 void Frontend::run_deferred(VerbScratch& s) {
+  if (s.defer_list >= 0) {
+    IoTimer it{kFeVerbNames};
+    s.idc.remember_subset(s.defer_list, s.rcs);
+    s.defer_list = -1;
+  }
   if (!s.defer_put && !s.defer_nominate) return;
   const LastPod& last = s.last;
   if (s.defer_put) {
@@ -1601,7 +1699,7 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   constexpr std::string_view kHead = "{\"Pod\":", kMid = ",\"Nodes\":null,\"NodeNames\":";
   std::string_view pod_text, raw_names;
   bool framed = false, reused = false, has_pod_text = false;
-  bool scanned = false;   // nv / nraw hold raw_names' names (a list not in the cache)
+  bool scanned = false;   // s.ntok holds raw_names' tokens (a list not in the cache)
   int found = -2;         // the list's cache slot when the framing looked it up (-1: none)
   int32_t pod = -1;
   nv.clear();
@@ -1625,7 +1723,8 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
         // the list must be one: a cached text, or a compact string array scanned whole
         // (anything else, members after it included, goes the general way)
         found = idc.find(raw_names);
-        framed = found >= 0 || (scanned = scan_string_array(raw_names, &nv, &nraw));
+        if (found < 0) s.ntok.clear();
+        framed = found >= 0 || (scanned = scan_string_array(raw_names, &s.ntok));
         if (framed) {
           has_pod_text = true;
           pod_text = rest.substr(0, pe);
@@ -1787,8 +1886,8 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   io0 = io_t0();
   const uint64_t epoch = ledger_->node_epoch();
   int slot = scanned ? -1 : framed && found != -2 ? found : idc.find(raw_names);
-  // a cached list's names are read through its token offsets into this request's text (no
-  // per-request copy of 2 x N views); a list parsed now fills nv / nraw
+  // a list's names are read through its token offsets into this request's text (no per-request
+  // copy of 2 x N views); only a list in another shape fills nv / nraw
   const std::vector<std::pair<uint32_t, uint32_t>>* toks = nullptr;
   if (slot >= 0) {
     // the same list text as before: its tokens sit at the same offsets (escape-free lists
@@ -1797,7 +1896,9 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   } else {
     // the common shape first, scanned directly: ["a","b",...] with no escapes; anything else
     // (whitespace, escapes, other types) goes through the JSON parser
-    bool plain = scanned || scan_string_array(raw_names, &nv, &nraw);
+    if (!scanned) s.ntok.clear();
+    const bool compact = scanned || scan_string_array(raw_names, &s.ntok);
+    bool plain = compact;
     if (!plain) {
       nv.clear();
       nraw.clear();
@@ -1830,15 +1931,21 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     if (plain) idc.text[slot].assign(raw_names.data(), raw_names.size());
     else idc.text[slot].clear();
     idc.epoch[slot] = 0;                // ids checked below
-    idc.ids[slot].assign(nv.size(), -1);
-    idc.tok[slot].clear();
-    size_t joined = nraw.empty() ? 2 : 1 + nraw.size();   // brackets and commas
-    if (plain)
-      for (const std::string_view t : nraw) {
-        idc.tok[slot].emplace_back(static_cast<uint32_t>(t.data() - raw_names.data()), static_cast<uint32_t>(t.size()));
-        joined += t.size();
-      }
-    idc.compact[slot] = plain && joined == raw_names.size();
+    if (compact) {
+      idc.tok[slot].swap(s.ntok);       // the scan's tokens become the slot's (no copy)
+      idc.compact[slot] = true;
+    } else {
+      idc.tok[slot].clear();
+      size_t joined = nraw.empty() ? 2 : 1 + nraw.size();   // brackets and commas
+      if (plain)
+        for (const std::string_view t : nraw) {
+          idc.tok[slot].emplace_back(static_cast<uint32_t>(t.data() - raw_names.data()), static_cast<uint32_t>(t.size()));
+          joined += t.size();
+        }
+      idc.compact[slot] = plain && joined == raw_names.size();
+    }
+    idc.ids[slot].assign(plain ? idc.tok[slot].size() : nv.size(), -1);
+    if (plain) toks = &idc.tok[slot];   // names through the slot's offsets from here on
   }
   idc.used[slot] = ++idc.clock;
   idc.mru = slot;
@@ -1861,20 +1968,27 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     // cycle, so the per-list cache above misses while every name in it is known
     NameTable& nid = s.nid;
     if (nid.owner != serial_ || nid.epoch != epoch) nid.reset(serial_, epoch);
+    int32_t prev = -1;
     for (size_t i = 0; i < static_cast<size_t>(nn); ++i) {
       const std::string_view name = name_at(i);
-      // the table holds its own copy of every name (a compact arena): a hit touches neither
-      // the ledger's node slots nor its lock, and is exact (names compared, not only hashed)
-      int32_t id = nid.find(name);
-      if (id < 0) {
-        id = ledger_->find_node(std::string(name));
+      // the successor of the previous name last time, else the table (its own copy of every
+      // name in a compact arena): a hit touches neither the ledger's node slots nor its lock,
+      // and is exact (names compared, not only hashed)
+      int32_t id = nid.next_of(prev);
+      if (!nid.is(id, name)) {
+        id = nid.find(name);
         if (id < 0) {
-          idc.valid[slot] = false;
-          return false;
+          id = ledger_->find_node(std::string(name));
+          if (id < 0) {
+            idc.valid[slot] = false;
+            return false;
+          }
+          nid.insert(name, id);
         }
-        nid.insert(name, id);
+        nid.set_next(prev, id);
       }
       ids[i] = id;
+      prev = id;
     }
     idc.epoch[slot] = epoch;
   }
@@ -2019,6 +2133,14 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
       }
     }
     r += "},\"Error\":\"\"}";
+    if (any_failed && pick < 0 && slot >= 0 && idc.valid[slot] && idc.epoch[slot] == epoch) {
+      size_t n_ok = 0;
+      for (const int32_t rc : rcs) n_ok += rc == kOk;
+      if (n_ok > 1) {   // one node: kube-scheduler skips priorities
+        if (s.defer) s.defer_list = slot;
+        else idc.remember_subset(slot, rcs);
+      }
+    }
     return true;
   }
   scores.resize(ids.size());

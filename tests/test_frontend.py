@@ -770,6 +770,55 @@ def test_escaped_node_names_still_answer_byte_identical():
         fe.stop()
 
 
+def test_sampled_windows_and_their_fitting_subsets_answer_byte_identical():
+    """kube-scheduler sends windows of its node order (nodes it counts as full left out) and then
+    priorities over exactly the nodes filter answered. The native verbs scan a list 16 bytes at
+    a time, resolve names by their predecessor's last successor, and keep a filter's fitting
+    subset as a list of its own for that priorities call: names of every length across the
+    16-byte blocks, windows that skip filled nodes and lists in other shapes (spaces: the JSON
+    parser's path) must all answer what the Python verbs answer."""
+    from nanogpu.extender.verbs import Extender
+    from nanogpu.state.cluster import ClusterState
+
+    st = ClusterState()
+    names = [("n" * (1 + i % 23)) + f"-{i}" for i in range(30)] + ["x", "gpu.rack-2.example.com", "mi355x-node-0000000000000017"]
+    for n in names:
+        st.register_node(pu.make_node(n, 8, synthetic_mi355x(8).to_json()))
+    ext = Extender(st, InProcKube(FakeKubeStore()))
+    fe = N.Frontend(st.ledger, "127.0.0.1", 0, 1)
+    rng = random.Random(5)
+    opts = st.options
+    try:
+        fe.set_options(opts, False, st.nominate, False, st.priority_lead)
+        n_subsets = 0
+        for k in range(300):
+            if k % 10 == 0:   # fill a node whole, free another: the windows change
+                full = rng.choice(names)
+                for d in range(8):
+                    st.ledger.reserve(st.ledger.find_node(full), f"fill-{k}-{d}", [(100, 0)], opts)
+                if k >= 20:
+                    for d in range(8):
+                        st.ledger.release(f"fill-{k - 20}-{d}")
+            start, size = rng.randrange(len(names)), rng.randint(2, len(names))
+            window = [names[(start + j) % len(names)] for j in range(size)]
+            pod = pu.make_pod(f"p{k}", [("c", rng.choice([10, 25, 50, 100]))])
+            body = {"Pod": pod, "Nodes": None, "NodeNames": window}
+            raw = _dumps(body) if k % 7 else json.dumps(body).encode()   # spaces: the general path
+            ok, _, out = fe.time_verb(raw, False, 1)
+            want = _dumps(ext.filter(json.loads(raw)))
+            assert ok and out == want, (k, out, want)
+            fit = json.loads(out)["NodeNames"]
+            if len(fit) < 2:
+                continue
+            n_subsets += len(fit) < len(window)
+            praw = _dumps({"Pod": pod, "Nodes": None, "NodeNames": fit})
+            ok, _, out = fe.time_verb(praw, True, 1)
+            assert ok and out == _dumps(ext.prioritize(json.loads(praw))), (k, out)
+        assert n_subsets > 20
+    finally:
+        fe.stop()
+
+
 def test_learned_streaming_owner_marks_its_next_pods_memory_bound_on_the_native_path():
     """A device measured HBM-hot while it holds one pod alone makes that pod's controlling
     owner a streaming owner (Ledger::learn_stream_owners). The owner's next unannotated pods
