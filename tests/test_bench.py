@@ -1,6 +1,7 @@
 """bench.py contract (single rank and 2- and 4-rank gloo jobs) and the BASELINE config harness."""
 import asyncio
 import json
+import statistics
 import os
 import socket
 import subprocess
@@ -148,8 +149,9 @@ def test_one_scheduler_over_n_workers_keeps_the_one_worker_rate(ranks, cpu_alone
     processes' binds wrote the node state (cache lines from other cores), and the publish was
     2.6 us a pod inside the filter before it moved past the answer (profiles/scaling_rehearsal.md).
     The scheduling rate of each run's fastest step (pods / the stand-in's first filter -> last
-    bind span: the harness's per-step barriers are outside it), best of interleaved runs (this
-    host's other tenants swing whole runs). The front door that serves the cycle polls 8 us for
+    bind span: the harness's per-step barriers are outside it), N workers against 1 in
+    interleaved pairs (this host's other tenants swing whole runs, and a pair shares the host's
+    state of the moment): the median of the pairs' ratios, over 3 to 8 pairs. The front door that serves the cycle polls 8 us for
     its next request on both sides (with N ranks only rank 0's does: the others serve binds
     alone); without it, rank 0's thread, which at N > 1 no longer serves most binds between two
     cycle requests, sleeps between them and every request pays a wake-up (0.83-0.88x here with
@@ -159,8 +161,9 @@ def test_one_scheduler_over_n_workers_keeps_the_one_worker_rate(ranks, cpu_alone
             "--steady-variant-steps", "0", "--nodes-variant", "0", "--inproc-variant-steps", "0",
             "--independent-variant-steps", "0", "--decisive-variant-steps", "0"]
     got = {1: [], ranks: []}
+    ratios: list[float] = []
     with tempfile.TemporaryDirectory() as tmp:
-        for rnd in range(6):
+        for rnd in range(8):
             for n in (1, ranks):
                 out = Path(tmp) / f"r{n}_{rnd}.json"
                 r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(n), "--json-out", str(out)]
@@ -174,9 +177,10 @@ def test_one_scheduler_over_n_workers_keeps_the_one_worker_rate(ranks, cpu_alone
                 assert diag["python_requests_per_pod_rank0"] == 0.0   # every bind stayed native
                 spans = diag["schedule_ms_each_step_rank0"]
                 got[n].append(round(1e3 * d["scheduled"] / len(spans) / min(spans), 1))
-            if rnd >= 1 and max(got[ranks]) >= 0.9 * max(got[1]):
+            ratios.append(got[ranks][-1] / got[1][-1])
+            if len(ratios) >= 3 and statistics.median(ratios) >= 0.9:
                 break
-    assert max(got[ranks]) >= 0.9 * max(got[1]), got
+    assert statistics.median(ratios) >= 0.9, (got, ratios)
 
 
 def test_plain_gpus_n_refuses_when_fewer_gpus_are_visible(tmp_path):
