@@ -195,10 +195,12 @@ class Extender:
 
     @staticmethod
     def _backoff(e: ApiError, attempt: int) -> float:
-        """5 ms x 2^k, or a 429's Retry-After when it asks for longer (kube-apiserver: 1 s)."""
+        """5 ms x 2^k, or a 429's Retry-After when it asks for longer (kube-apiserver: 1 s), at
+        most 2 s a wait: the bind holds kube-scheduler's request, which times out at 30 s (the
+        native writer waits the same way, BindIo::kMaxRetryAfterS)."""
         b = 0.005 * (2 ** attempt)
         ra = getattr(e, "retry_after", None)
-        return min(30.0, max(b, ra)) if e.status == 429 and ra else b
+        return min(2.0, max(b, ra)) if e.status == 429 and ra else b
 
     async def _retry(self, op: str, fn, *a):
         for attempt in range(self.api_retries + 1):

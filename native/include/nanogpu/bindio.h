@@ -85,6 +85,7 @@ class BindIo {
   void defer(BindJob&& j, std::string&& patch, bool label_only, double retry_after);
   void resend_due(uint64_t now);
   static constexpr int kMaxThrottled = 8;
+  static constexpr double kMaxRetryAfterS = 2.0;
   double window_ = 1, max_window_ = 1, clean_ = 0;
   uint64_t launch_seq_ = 0, cut_seq_ = 0;
   struct Deferred {

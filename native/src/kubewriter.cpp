@@ -603,7 +603,8 @@ int KubeWriter::call(HttpConn* c, const char* method, const std::string& path, c
       stats.throttled.fetch_add(1, std::memory_order_relaxed);
       if (c->retry_after() > 0) wait_us = std::max<int64_t>(wait_us, static_cast<int64_t>(c->retry_after() * 1e6));
     }
-    std::this_thread::sleep_for(std::chrono::microseconds(std::min<int64_t>(wait_us, 30'000'000)));
+    // at most 2 s a wait (BindIo::kMaxRetryAfterS): kube-scheduler's bind times out at 30 s
+    std::this_thread::sleep_for(std::chrono::microseconds(std::min<int64_t>(wait_us, 2'000'000)));
   }
 }
 

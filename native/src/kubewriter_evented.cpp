@@ -966,9 +966,11 @@ void BindIo::widen() {
 }
 
 void BindIo::defer(BindJob&& j, std::string&& patch, bool label_only, double retry_after) {
-  // the server's Retry-After (kube-apiserver: 1 s), else 5 ms x 2^k as the slow path's retries
-  const double wait_s = retry_after > 0 ? std::min(retry_after, 30.0)
-                                        : 0.005 * static_cast<double>(1u << std::min(j.throttled, 12));
+  // the server's Retry-After (kube-apiserver: 1 s), else 5 ms x 2^k as the slow path's retries;
+  // at most kMaxRetryAfterS each, so kMaxThrottled waits stay inside kube-scheduler's 30 s
+  // extender timeout and the ledger's 60 s reservation TTL (the bind holds its reservation)
+  const double wait_s = std::min(kMaxRetryAfterS, retry_after > 0 ? retry_after
+                                                                  : 0.005 * static_cast<double>(1u << std::min(j.throttled, 12)));
   const uint64_t due = ns_now() + static_cast<uint64_t>(wait_s * 1e9);
   Deferred d{due, std::move(j), std::move(patch), label_only};
   auto at = deferred_.end();

@@ -152,6 +152,8 @@ def test_python_writer_honours_retry_after():
     assert e.throttled and Extender._backoff(e, 0) == 1.0
     assert Extender._backoff(ApiError(500, "x"), 2) == pytest.approx(0.02)
     assert Extender._backoff(ApiError(429, "x"), 0) == pytest.approx(0.005)   # no header: the backoff
+    # a long Retry-After is cut to 2 s: the bind holds kube-scheduler's 30 s extender request
+    assert Extender._backoff(ApiError(429, "x", "TooManyRequests", 60.0), 0) == 2.0
 
     from nanogpu.k8s.client import KubeClient, KubeConfig
     from nanogpu.k8s.fake_apiserver import Faults, FakeKubeStore, serve
