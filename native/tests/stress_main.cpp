@@ -28,6 +28,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <random>
 #include <string>
@@ -774,6 +775,107 @@ static void memo_and_wide(int iters) {
   std::printf("memo + wide ok: %d iterations x 3 writers, 2 readers\n", iters);
 }
 
+// Nominations adopted by binds on other threads while sweepers drop them: a bind adopts its
+// pod's nomination under the pod shard's lock alone (Ledger::reserve_as), a sweep releases a
+// nomination under node + shard lock only while it is still one (release_if re-checks), and a
+// bind to another node than the nomination releases it and reserves afresh. Whatever wins each
+// race, every device is whole again once every pod is released, and no pod is counted twice.
+static void nominate_adopt(int iters) {
+  Ledger l("", 8, 65536, true);
+  add_nodes(l, 4);
+  std::mutex mu;
+  std::deque<std::pair<std::string, int>> nominated;   // (key, node) waiting for a bind
+  std::atomic<bool> done{false};
+  std::thread nominator([&] {
+    std::mt19937_64 rng(5);
+    Options o;
+    for (int i = 0; i < iters; ++i) {
+      Demand d;
+      std::memset(&d, 0, sizeof(d));
+      d.n = 1;
+      d.c[0].pct = 10 * (1 + static_cast<int>(rng() % 5));
+      d.c[0].mib = static_cast<int64_t>(rng() % 3) * 8192;
+      const int node = static_cast<int>(rng() % 4);
+      const std::string key = "nom-" + std::to_string(i);
+      const int32_t rc = l.nominate(node, key, d, o);
+      CHECK(rc == kOk || rc == kOkExisting || rc == kErrNoFit || rc == kErrNoDevices);
+      std::lock_guard<std::mutex> g(mu);
+      nominated.emplace_back(key, node);
+    }
+    done.store(true);
+  });
+  std::vector<std::thread> binders;
+  std::mutex live_mu;
+  std::vector<std::string> live;
+  for (int t = 0; t < 2; ++t)
+    binders.emplace_back([&, t] {
+      std::mt19937_64 rng(100 + t);
+      Options o;
+      for (;;) {
+        std::pair<std::string, int> job;
+        {
+          std::lock_guard<std::mutex> g(mu);
+          if (nominated.empty()) {
+            if (done.load()) break;
+            continue;
+          }
+          job = nominated.front();
+          nominated.pop_front();
+        }
+        Demand d;
+        std::memset(&d, 0, sizeof(d));
+        d.n = 1;
+        d.c[0].pct = 10;
+        // one bind in five goes to another node than its nomination (kube-scheduler's pick)
+        const int node = rng() % 5 == 0 ? (job.second + 1) % 4 : job.second;
+        Plan p;
+        const int32_t rc = l.reserve(node, job.first, d, o, &p);
+        if (rc == kOk || rc == kOkExisting) {
+          if (l.commit(job.first) == kOk) {
+            std::lock_guard<std::mutex> g(live_mu);
+            live.push_back(job.first);
+          }
+        }
+        {   // an older pod deleted (the cluster stays about half full)
+          std::string k;
+          {
+            std::lock_guard<std::mutex> g(live_mu);
+            if (live.size() > 24 || (!live.empty() && rng() % 3 == 0)) {
+              const size_t i = rng() % live.size();
+              k = live[i];
+              live.erase(live.begin() + static_cast<long>(i));
+            }
+          }
+          if (!k.empty()) CHECK(l.release(k) == kOk);
+        }
+      }
+    });
+  std::thread sweeper([&] {   // the nomination TTL sweep, at TTL 0: every nomination is fair game
+    while (!done.load()) {
+      for (const std::string& k : l.expired_nominations(0.0)) l.drop_nomination(k);
+    }
+  });
+  nominator.join();
+  for (auto& b : binders) b.join();
+  sweeper.join();
+  for (const std::string& k : l.expired_nominations(-1.0)) CHECK(l.drop_nomination(k) == kOk);
+  for (const std::string& k : live) CHECK(l.release(k) == kOk);
+  for (int k = 0; k < 4; ++k) {
+    NodeSnapshot s;
+    CHECK(l.snapshot(k, &s));
+    for (int i = 0; i < s.n_devs; ++i) {
+      CHECK(s.devs[i].pct_free == s.devs[i].pct_total);
+      CHECK(s.devs[i].mib_free == s.devs[i].mib_total);
+    }
+  }
+  CHECK(l.n_pods() == 0);
+  uint64_t made = 0, adopted = 0, moved = 0;
+  l.nomination_counts(&made, &adopted, &moved);
+  std::printf("nominate/adopt ok: %d pods, %llu nominated, %llu adopted, %llu moved\n", iters,
+              static_cast<unsigned long long>(made), static_cast<unsigned long long>(adopted),
+              static_cast<unsigned long long>(moved));
+}
+
 int main(int argc, char** argv) {
   std::setvbuf(stdout, nullptr, _IOLBF, 0);   // each scenario's line out as it passes (a hang names its scenario)
   if (argc > 1 && std::strcmp(argv[1], "relist-scale") == 0) {
@@ -877,5 +979,6 @@ int main(int argc, char** argv) {
   handoff(std::max(500, iters));
   mailbox_wakeups(std::max(400, iters / 2));
   memo_and_wide(std::max(1000, iters));
+  nominate_adopt(std::max(2000, iters));
   return 0;
 }
