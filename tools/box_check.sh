@@ -4,7 +4,7 @@
 set -o pipefail
 out=${1:-gpurun_out/check}
 mkdir -p "$out"
-timeout -k 10 420 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$out/gputest.log" 2>&1 || exit $?
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$out/gputest.log" 2>&1 || exit $?
 tail -2 "$out/gputest.log"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 || exit $?
 tail -2 "$out/smoke.log"
