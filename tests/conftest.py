@@ -43,47 +43,6 @@ def tmp_shm(tmp_path):
         pass
 
 
-_GATE = "/tmp/nanogpu-tests-cpu-gate.lock"
-_ALONE = "/tmp/nanogpu-tests-cpu-alone.lock"
-
-
-@pytest.fixture(autouse=True)
-def _cpu_share(request):
-    """Every test holds the machine-wide lock shared; a `cpu_alone` test holds it exclusively,
-    so under `pytest -n` it runs with no other test beside it. The gate keeps new tests from
-    starting while a `cpu_alone` test waits for the running ones to finish (no starvation)."""
-    if "cpu_alone" in request.fixturenames:
-        yield
-        return
-    import fcntl
-
-    with open(_GATE, "w") as g, open(_ALONE, "w") as f:
-        fcntl.flock(g, fcntl.LOCK_EX)
-        fcntl.flock(f, fcntl.LOCK_SH)
-        fcntl.flock(g, fcntl.LOCK_UN)
-        try:
-            yield
-        finally:
-            fcntl.flock(f, fcntl.LOCK_UN)
-
-
-@pytest.fixture
-def cpu_alone():
-    """A test that compares rates between runs: under `pytest -n` the other workers' tests
-    (sanitizer stress, multi-rank benches) would swing one run against the other, so it runs
-    alone on the machine."""
-    import fcntl
-
-    with open(_GATE, "w") as g, open(_ALONE, "w") as f:
-        fcntl.flock(g, fcntl.LOCK_EX)
-        fcntl.flock(f, fcntl.LOCK_EX)
-        try:
-            yield
-        finally:
-            fcntl.flock(f, fcntl.LOCK_UN)
-            fcntl.flock(g, fcntl.LOCK_UN)
-
-
 @pytest.fixture
 def cpu_exclusive():
     """Multi-process bench jobs (several ranks, each with busy front-door threads, plus the API

@@ -145,34 +145,50 @@ def _host_steal() -> tuple[int, int]:
     return v[7], sum(v)
 
 
-@pytest.mark.parametrize("ranks,floor", [(2, 0.85), (4, 0.75)])
-def test_one_scheduler_over_n_workers_keeps_the_one_worker_rate(ranks, floor, cpu_alone):
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_one_scheduler_over_n_workers_does_the_one_worker_cycle_work(ranks, cpu_exclusive):
     """one kube-scheduler's binds spread over N extender workers (the
-    driver's N-GPU headline) schedule at the 1-worker rate on the same CPUs. The cycle stays on
-    rank 0's worker; the binds the other workers answer take their pod from the shared ledger's
-    handoff, which the cycle's worker publishes after its filter answer (Frontend::run_deferred),
-    and adopt their nomination under the pod shard's lock only, so neither costs the cycle.
-    Measured: the extender's ledger operations per pod are the same at 1 and 4 workers, each
-    40 % slower when other processes' binds wrote the node state (cache lines from other cores),
-    and the publish was 2.6 us a pod inside the filter before it moved past the answer
-    (profiles/scaling_rehearsal.md). On the MI355X box's 16 CPUs: 1.03x at 4 workers, 0.98x at 8
-    (profiles/raw/r06f).
-    The scheduling rate of each run's fastest step (pods / the stand-in's first filter -> last
-    bind span: the harness's per-step barriers are outside it), N workers against 1 in
-    interleaved pairs (this host's other tenants swing whole runs, and a pair shares the host's
-    state of the moment): the median of the pairs' ratios, over 3 to 8 pairs. The floors, 0.85x
-    at 2 workers and 0.75x at 4, are this container's: it is a VM whose hypervisor takes CPU
-    time (steal) in proportion to the vCPUs a job keeps busy, 0.6-1.2 % of it during a 1-worker
-    run and 4-8 % during a 4-worker one; single runs of one build swing 2x (3.4-17k pods/s) and
-    pair ratios 0.56-1.84, with medians of 1.0 at 2 workers and 0.82-0.9 at 4 (the rates, ratios
-    and steal of every run are in the failure message). The box, whose 16 CPUs are the job's,
-    is where the 0.9x bar is read: 1.03x at 4 workers, 0.98x at 8. The front door that serves the cycle polls 8 us for
-    its next request on both sides (with N ranks only rank 0's does: the others serve binds
-    alone); without it, rank 0's thread, which at N > 1 no longer serves most binds between two
-    cycle requests, sleeps between them and every request pays a wake-up (0.83-0.88x here with
-    polling off on both sides, 0.97x with it on). No skip: a shortfall fails."""
-    med, info = _rate_pairs(ranks, floor, max_pairs=8, steps=24)
-    assert med >= floor, info
+    driver's N-GPU headline) leave the scheduling cycle's worker the work it has with one: the
+    same verbs, sends, pod-cache puts, nominations and ledger scans / memo re-validations a pod
+    (`--io-tally` counts, exact to the stream), no bind through Python, and binds answered by the
+    other workers through the ledger's handoff. The cycle stays on rank 0's worker; the handoff
+    is published after its filter answer (Frontend::run_deferred) and a bind adopts its
+    nomination under the pod shard's lock only, so neither sits on the cycle.
+    The rate itself, >= 0.9x the 1-worker rate at 4 workers, is asserted in the GPU tier
+    (test_one_scheduler_over_four_workers_keeps_the_rate_on_the_box) because this container
+    cannot time it: it is a VM whose hypervisor takes CPU time (steal) in proportion to the
+    vCPUs a job keeps busy, 0.6-1.2 % during a 1-worker run and 4-9 % during a 4-worker one;
+    single runs of one build swing 3x (4-13k pods/s) and interleaved 1/N pair ratios 0.56-1.84.
+    Here the rate gets a floor only for gross breakage (0.5x, fastest steps)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    base = ["--no-gpu", "--steps", "8", "--warmup", "2", "--rtt-variant-ms", "0", "--io-tally",
+            "--steady-variant-steps", "0", "--nodes-variant", "0", "--inproc-variant-steps", "0",
+            "--independent-variant-steps", "0", "--decisive-variant-steps", "0"]
+    io, rate = {}, {}
+    with tempfile.TemporaryDirectory() as tmp:
+        for n in (1, ranks):
+            out = Path(tmp) / f"r{n}.json"
+            r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(n), "--json-out", str(out)]
+                               + base, capture_output=True, text=True, timeout=400, env=env, cwd="/tmp")
+            assert r.returncode == 0, r.stderr[-3000:]
+            d = _last_json(r.stdout)
+            assert d["n_gpus"] == n and d["failed"] == 0 and d["scheduled"] == 8000
+            diag = json.loads(out.read_text())["diagnostics"]
+            assert diag["python_requests_per_pod_rank0"] == 0.0   # every bind stayed native
+            if n > 1:
+                assert d["bind_handoffs"] > 0 and d["value_mode"].startswith("one kube-scheduler stand-in")
+            io[n] = {k: v[0] for k, v in diag["io_per_pod_rank0"].items()}
+            spans = diag["schedule_ms_each_step_rank0"]
+            rate[n] = 1e3 * d["scheduled"] / len(spans) / min(spans)
+    one, many = io[1], io[ranks]
+    for k in ("fe_verb", "fe_send_cycle", "fe_verb_assume", "fe_verb_pod"):
+        assert one[k] == many[k] == 2.0, (k, one[k], many[k])
+    assert one["fe_verb_cache"] == many["fe_verb_cache"] == 3.0   # filter put (+ handoff), 2 verb lookups
+    assert one["fe_verb_nominate"] == pytest.approx(1.0, abs=0.01) and many["fe_verb_nominate"] == pytest.approx(1.0, abs=0.01)
+    for k in ("ledger_scan", "ledger_revalidate"):   # the memo's work a pod: same stream, same placements
+        assert many[k] == pytest.approx(one[k], rel=0.1), (k, one[k], many[k])
+    assert many["fe_verb_names"] < 2.1   # node lists resolved from the per-list cache
+    assert rate[ranks] >= 0.5 * rate[1], rate
 
 
 @pytest.mark.gpu
