@@ -208,6 +208,9 @@ class Frontend {
   // ledger counts the deferred nominations, and that filter waits until they are made
   // (Ledger::wait_deferred_nominations), so it never sees the ledger without this pod's devices
   bool defer_nominate_ok(const VerbScratch& s) const;
+  // priorities right behind its pod's filter, nothing changed since: the filter's placements
+  bool reuse_assume(VerbScratch& s, std::string_view uid, const Demand& dem, const std::vector<int32_t>& ids,
+                    std::vector<int32_t>* rcs, std::vector<int32_t>* scores);
   void note_bind_wall(uint64_t ns);
   // a response for connection `conn` of worker w, on w's thread: sent, then its next request
   struct Reply;

@@ -635,6 +635,17 @@ struct Frontend::VerbScratch {
   bool defer_put = false;
   bool defer_nominate = false;
   int defer_list = -1;   // the filter's node-list slot whose fitting subset priorities will send
+  // The last filter's placements (Ledger::assume_many) and the ledger's mutation epoch before
+  // them: kube-scheduler's priorities call for the same pod follows, over the same nodes or
+  // the fitting ones, and with no mutation anywhere in between (a bind adopting its nomination
+  // and a commit change no device) the answers are the same, so priorities reads them here
+  // instead of walking the nodes again on the scheduling cycle's path. One use.
+  struct LastAssume {
+    bool valid = false;
+    uint64_t epoch = 0, dem_hash = 0, opt_seen = 0;
+    std::string uid;
+    std::vector<int32_t> ids, rcs, scores;
+  } last_assume;
   int32_t defer_node = -1;
   Demand defer_dem{};
 };
@@ -1631,6 +1642,31 @@ void Frontend::cache_pod(VerbScratch& s, std::string_view uid, const CachedPod& 
 
 bool Frontend::defer_nominate_ok(const VerbScratch& s) const { return s.defer_cache; }
 
+bool Frontend::reuse_assume(VerbScratch& s, std::string_view uid, const Demand& dem, const std::vector<int32_t>& ids,
+                            std::vector<int32_t>* rcs, std::vector<int32_t>* scores) {
+  VerbScratch::LastAssume& la = s.last_assume;
+  if (!la.valid) return false;
+  la.valid = false;   // one use: the priorities call right behind its filter
+  if (uid.empty() || uid != la.uid || la.opt_seen != s.opt_seen || la.dem_hash != dem.hash() ||
+      la.epoch != ledger_->epoch())
+    return false;
+  if (ids == la.ids) {
+    std::copy(la.rcs.begin(), la.rcs.end(), rcs->begin());
+    std::copy(la.scores.begin(), la.scores.end(), scores->begin());
+    return true;
+  }
+  // the filter's fitting nodes, in the filter's order (what kube-scheduler sends when some
+  // nodes did not fit)
+  size_t j = 0;
+  for (size_t i = 0; i < ids.size(); ++i) {
+    while (j < la.ids.size() && la.rcs[j] != kOk) ++j;
+    if (j == la.ids.size() || la.ids[j] != ids[i]) return false;
+    (*rcs)[i] = kOk;
+    (*scores)[i] = la.scores[j++];
+  }
+  return true;
+}
+
 void Frontend::run_deferred(VerbScratch& s) {
   if (s.defer_list >= 0) {
     IoTimer it{kFeVerbNames};
@@ -2041,7 +2077,19 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
     io_end(kFeVerbCache, io0);
     {
       IoTimer it{kFeVerbAssume};
+      const uint64_t epoch0 = ledger_->epoch();
       ledger_->assume_many(ids.data(), static_cast<int>(ids.size()), dem, o, rcs.data(), scores.data());
+      VerbScratch::LastAssume& la = s.last_assume;
+      la.valid = !uid.empty();
+      if (la.valid) {
+        la.epoch = epoch0;
+        la.dem_hash = dem.hash();
+        la.opt_seen = s.opt_seen;
+        la.uid.assign(uid);
+        la.ids.assign(ids.begin(), ids.end());
+        la.rcs.assign(rcs.begin(), rcs.end());
+        la.scores.assign(scores.begin(), scores.end());
+      }
     }
     // decisive: the node priorities would rank first is the only one answered (and nominated)
     const int64_t pick = decisive ? top_pick(scores, rcs, uid) : -1;
@@ -2148,7 +2196,8 @@ bool Frontend::filter_verb(std::string_view body, bool prioritize, std::string* 
   io_end(kFeVerbCache, io0);
   {
     IoTimer it{kFeVerbAssume};
-    ledger_->assume_many(ids.data(), static_cast<int>(ids.size()), dem, o, rcs.data(), scores.data());
+    if (!reuse_assume(s, uid, dem, ids, &rcs, &scores))
+      ledger_->assume_many(ids.data(), static_cast<int>(ids.size()), dem, o, rcs.data(), scores.data());
   }
   int64_t best = -1;
   int n_best = 0;
