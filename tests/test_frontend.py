@@ -819,6 +819,44 @@ def test_sampled_windows_and_their_fitting_subsets_answer_byte_identical():
         fe.stop()
 
 
+def test_priorities_reuse_their_filters_placements_only_while_nothing_changed():
+    """Priorities right behind its pod's filter reads the placements that filter computed
+    (Frontend::reuse_assume) instead of walking the nodes again, as long as the ledger saw no
+    mutation in between. A reservation, a release or a telemetry mark in between makes it
+    compute afresh: every answer equals the Python verb's on the state of its moment."""
+    from nanogpu.extender.verbs import Extender
+    from nanogpu.state.cluster import ClusterState
+
+    st = ClusterState(nominate=False)   # no nominations: only the test's own mutations
+    names = [f"n{i}" for i in range(6)]
+    for n in names:
+        st.register_node(pu.make_node(n, 8, synthetic_mi355x(8).to_json()))
+    ext = Extender(st, InProcKube(FakeKubeStore()))
+    fe = N.Frontend(st.ledger, "127.0.0.1", 0, 1)
+    rng = random.Random(9)
+    try:
+        fe.set_options(st.options, False, st.nominate, False, st.priority_lead)   # the Python verb's rules
+        for k in range(200):
+            pod = pu.make_pod(f"p{k}", [("c", rng.choice([10, 25, 50]))])
+            raw = _dumps({"Pod": pod, "Nodes": None, "NodeNames": names})
+            ok, _, out = fe.time_verb(raw, False, 1)
+            assert ok and out == _dumps(ext.filter(json.loads(raw)))
+            fit = json.loads(out)["NodeNames"]
+            what = k % 4
+            if what == 1:      # a reservation lands on a fitting node between the two verbs
+                st.ledger.reserve(st.ledger.find_node(rng.choice(fit)), f"x{k}", [(rng.choice([10, 50]), 0)],
+                                  st.options)
+            elif what == 2 and k > 8:   # an older one is released
+                st.ledger.release(f"x{k - 7}")
+            elif what == 3:    # a device turns HBM-hot
+                st.ledger.set_mem_hot(st.ledger.find_node(rng.choice(names)), rng.randrange(8), True)
+            praw = _dumps({"Pod": pod, "Nodes": None, "NodeNames": fit})
+            ok, _, out = fe.time_verb(praw, True, 1)
+            assert ok and out == _dumps(ext.prioritize(json.loads(praw))), (k, what)
+    finally:
+        fe.stop()
+
+
 def test_learned_streaming_owner_marks_its_next_pods_memory_bound_on_the_native_path():
     """A device measured HBM-hot while it holds one pod alone makes that pod's controlling
     owner a streaming owner (Ledger::learn_stream_owners). The owner's next unannotated pods
