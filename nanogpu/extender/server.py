@@ -413,6 +413,10 @@ class NativeServer:
                       f"nanogpu_native_api_throttled_total {kw.get('throttled', 0)}",
                       "# TYPE nanogpu_native_bind_window_cuts_total counter",
                       f"nanogpu_native_bind_window_cuts_total {kw.get('window_cuts', 0)}",
+                      "# HELP nanogpu_native_bindings_first_total bindings sent ahead of their label PATCH "
+                      "because the admission window had no room for both",
+                      "# TYPE nanogpu_native_bindings_first_total counter",
+                      f"nanogpu_native_bindings_first_total {kw.get('bindings_first', 0)}",
                       "# HELP nanogpu_native_bind_window binds the writer keeps in flight at most now",
                       "# TYPE nanogpu_native_bind_window gauge",
                       f"nanogpu_native_bind_window {kw.get('window', 0)}"]

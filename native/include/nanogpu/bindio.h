@@ -73,7 +73,7 @@ class BindIo {
   void scan_deadlines(uint64_t now);
   void queue_label(BindJob&& j, std::string&& patch);
   void label_done(int64_t ls, int status, std::string body);
-  void launch_labels();
+  void launch_labels(size_t room);
   // kube-apiserver's max-in-flight admission (429 TooManyRequests, Retry-After): the binds in
   // flight are capped by an AIMD window, halved on a 429 (once per window: only an answer to a
   // request sent after the last cut cuts again), one bind wider after a window's worth of clean
@@ -122,6 +122,9 @@ class BindIo {
   // send and a read or two for all of them, held at most kLabelHoldNs for the batch to fill.
   static constexpr size_t kLabelBatch = 32;
   static constexpr uint64_t kLabelHoldNs = 500'000;
+  // a label left waiting for room in the admission window this long goes before more binds
+  static constexpr uint64_t kLabelStarveNs = 50'000'000;
+  int64_t req_inflight_ = 0;   // requests of the binds in flight (2: binding + label, 1: alone)
   std::vector<std::unique_ptr<Label>> lslots_;
   std::vector<int64_t> lfree_;
   std::deque<int64_t> label_wait_;

@@ -120,6 +120,9 @@ struct KubeWriterStats {
   // smallest over the writer's BindIo drivers)
   std::atomic<uint64_t> throttled{0}, throttle_resends{0}, window_cuts{0};
   std::atomic<int64_t> window{0};
+  // bindings sent ahead of their label because the window had no room for both (the labels
+  // followed in batches when it had)
+  std::atomic<uint64_t> bindings_first{0};
 };
 
 // Two ways to run the writes:

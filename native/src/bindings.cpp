@@ -882,6 +882,7 @@ PYBIND11_MODULE(_native, m) {
              d["throttle_resends"] = w->stats.throttle_resends.load();
              d["window_cuts"] = w->stats.window_cuts.load();
              d["window"] = w->stats.window.load();
+             d["bindings_first"] = w->stats.bindings_first.load();
              return d;
            })
       .def("take",

@@ -187,6 +187,7 @@ struct BindIo::Job {
   double retry_after = -1;    // a 429's Retry-After (seconds)
   bool answered = false;   // kube-scheduler has its answer (the binding landed; the label may follow)
   bool batch_label = false;   // the label goes in a later batch (queue_label), not behind the binding
+  int reqs = 2;               // requests it holds against the admission window (binding + label, or 1)
 };
 
 struct BindIo::Label {
@@ -202,9 +203,11 @@ bool ok2xx(int st) { return st >= 200 && st < 300; }
 
 BindIo::BindIo(KubeWriter* kw, int ep, uint64_t tag_bit, int max_inflight, Reply reply)
     : kw_(kw), ep_(ep), tag_bit_(tag_bit), reply_(std::move(reply)) {
-  slots_.resize(static_cast<size_t>(std::max(1, max_inflight)));
+  // the window counts binds (a binding and its label); under a backlog a binding may go alone
+  // (start_waiting), so twice the slots
+  slots_.resize(static_cast<size_t>(std::max(1, max_inflight)) * (kw_->label_ ? 2 : 1));
   for (int64_t i = static_cast<int64_t>(slots_.size()) - 1; i >= 0; --i) free_slots_.push_back(i);
-  window_ = max_window_ = static_cast<double>(slots_.size());
+  window_ = max_window_ = static_cast<double>(std::max(1, max_inflight));
   auth_ = kw_->auth();
   auth_at_ = ns_now();
   host_hdr_ = host_header(kw_->t_);
@@ -301,6 +304,7 @@ void BindIo::complete(int64_t s) {
   std::unique_ptr<Job> jb = std::move(slots_[static_cast<size_t>(s)]);
   free_slots_.push_back(s);
   --inflight_;
+  req_inflight_ -= jb->reqs;
   KubeWriterStats& st = kw_->stats;
   if (jb->answered && ok2xx(jb->sp)) {   // bound and answered earlier; the label landed too
     widen();
@@ -638,6 +642,8 @@ void BindIo::adopt_handoffs() {
       jb->left = 1;
       jb->sp = 200;
     }
+    jb->reqs = kw_->label_ ? 2 : 1;   // the front door pipelined both
+    req_inflight_ += jb->reqs;
     jb->seq = ++launch_seq_;
     slots_[static_cast<size_t>(s)] = std::move(jb);
     ++inflight_;
@@ -730,7 +736,24 @@ void BindIo::start_waiting() {
     auth_ = kw_->auth();
     auth_at_ = ns_now();
   }
-  while (!waiting_.empty() && !free_slots_.empty() && static_cast<double>(inflight_) < window_) {
+  const bool label = kw_->label_, batch = label && kw_->batch_labels_.load(std::memory_order_relaxed);
+  const double cap = window_ * (label ? 2 : 1);   // requests the admission window allows
+  while (!waiting_.empty() && !free_slots_.empty()) {
+    // labels kept waiting for room too long get it before more binds (bindings first, not only)
+    if (!label_wait_.empty() && ns_now() - label_oldest_ns_ > kLabelStarveNs) break;
+    const double used = static_cast<double>(req_inflight_) + static_cast<double>(labels_out_);
+    int need = label && !batch ? 2 : 1;
+    bool alone = batch;
+    if (need == 2 && used + 2.0 * static_cast<double>(waiting_.size()) > cap) {
+      // more binds waiting than the window has room for with their labels: the binding goes
+      // alone and its label later, in a batch, when the window has room (kube-scheduler waits
+      // on bindings, not on labels: under a saturated API server its binds keep the window's
+      // whole rate). With room to spare, as nearly always, both go together as before.
+      need = 1;
+      alone = true;
+    }
+    if (used + need > cap) break;
+    if (alone && !batch) kw_->stats.bindings_first.fetch_add(1, std::memory_order_relaxed);
     const int64_t s = free_slots_.back();
     free_slots_.pop_back();
     auto jb = std::make_unique<Job>();
@@ -740,13 +763,15 @@ void BindIo::start_waiting() {
       IoTimer it{kWrBuild};
       kw_->build(jb->j, &jb->patch, &jb->binding);
     }
-    if (!kw_->label_) {   // the binding alone carries the annotations
+    if (!label) {   // the binding alone carries the annotations
       jb->left = 1;
       jb->sp = 200;
-    } else if (kw_->batch_labels_.load(std::memory_order_relaxed)) {   // the binding alone now, its label later
+    } else if (alone) {   // the binding alone now, its label later
       jb->left = 1;
       jb->batch_label = true;
     }
+    jb->reqs = need;
+    req_inflight_ += need;
     jb->seq = ++launch_seq_;
     slots_[static_cast<size_t>(s)] = std::move(jb);
     ++inflight_;
@@ -824,8 +849,8 @@ void BindIo::label_done(int64_t ls, int status, std::string body) {
   kw_->to_slow(std::move(sj));
 }
 
-// up to kLabelBatch waiting label PATCHes, pipelined on one idle (or new) connection
-void BindIo::launch_labels() {
+// up to kLabelBatch (and `room`) waiting label PATCHes, pipelined on one idle (or new) connection
+void BindIo::launch_labels(size_t room) {
   size_t k;
   if (!idle_.empty()) {
     k = idle_.back();
@@ -839,7 +864,7 @@ void BindIo::launch_labels() {
   c.pend.clear();
   c.head = 0;
   thread_local std::string one;
-  while (!label_wait_.empty() && c.pend.size() < kLabelBatch) {
+  while (!label_wait_.empty() && c.pend.size() < std::min(kLabelBatch, room)) {
     const int64_t ls = label_wait_.front();
     label_wait_.pop_front();
     Label& l = *lslots_[static_cast<size_t>(ls)];
@@ -878,11 +903,24 @@ void BindIo::pump() {
     kick_.clear();
   }
   if (!label_wait_.empty()) {
+    // labels fill the room the binds leave in the admission window
     const uint64_t now = ns_now();
-    while (label_wait_.size() >= kLabelBatch || (!label_wait_.empty() && now - label_oldest_ns_ >= kLabelHoldNs))
-      launch_labels();
+    const double cap = window_ * (kw_->label_ ? 2 : 1);
+    for (;;) {
+      const double room = cap - static_cast<double>(req_inflight_) - static_cast<double>(labels_out_);
+      if (label_wait_.empty() || room < 1 ||
+          !(label_wait_.size() >= kLabelBatch || now - label_oldest_ns_ >= kLabelHoldNs))
+        break;
+      launch_labels(static_cast<size_t>(room));
+    }
     for (size_t i = 0; i < kick_.size(); ++i) drive(kick_[i], 0);
     kick_.clear();
+    // room the labels did not take goes to binds waiting behind them (kLabelStarveNs)
+    if (!waiting_.empty()) {
+      start_waiting();
+      for (size_t i = 0; i < kick_.size(); ++i) drive(kick_[i], 0);
+      kick_.clear();
+    }
   }
   scan_deadlines(ns_now());
   for (size_t i = 0; i < kick_.size(); ++i) drive(kick_[i], 0);

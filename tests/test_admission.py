@@ -142,6 +142,59 @@ def test_a_burst_over_the_admission_limit_binds_every_pod_once(mode):
     asyncio.run(main())
 
 
+def test_a_saturated_window_sends_bindings_first_and_labels_after():
+    """A burst faster than the admission window drains (a 20-request limit shared as 7 binds, a
+    20 ms round trip): bindings go alone while the window has no room for a binding and its
+    label, so kube-scheduler's binds keep the window's whole rate, and the labels follow in
+    batches as room frees up. Every pod is bound once and labelled, nothing goes over the
+    server's limit (no 429), and the ledger holds exactly the burst's demand."""
+    from nanogpu.sim.driver import NativeSchedulerDriver, node_capacities
+
+    srv = _server(20, 0.02)
+
+    async def main():
+        nodes = []
+        for i in range(16):
+            st, body = srv.call("POST", "/api/v1/nodes", json.dumps(pu.make_node(f"n{i:02d}", 8, synthetic_mi355x(8).to_json())))
+            assert st in (200, 201)
+            nodes.append(json.loads(body))
+        rt = Runtime(Config(kube_api=f"http://127.0.0.1:{srv.port}", port=0, host="127.0.0.1",
+                            policy_config_path="/nonexistent", api_max_inflight=20))
+        assert Config(api_max_inflight=20).writer_max_binds() == 7
+        await rt.start()
+        loop = asyncio.get_running_loop()
+        try:
+            pods = []
+            for i in range(300):
+                p = pu.make_pod(f"s{i}", [("main", (10, 25, 50)[i % 3], 8 * 1024)])
+                st, body = srv.call("POST", "/api/v1/namespaces/default/pods", json.dumps(p))
+                assert st == 201
+                pods.append(json.loads(body))
+            drv = NativeSchedulerDriver("127.0.0.1", rt.bound_port, [n["metadata"]["name"] for n in nodes],
+                                        node_capacities(nodes), bind_threads=64)
+            res = await asyncio.wait_for(loop.run_in_executor(None, drv.run, pods), 90)
+            assert res.scheduled == 300 and res.failed == 0 and res.bind_errors == 0
+            for _ in range(1000):   # the labels trailing the bindings
+                if rt.native.fe.kube_writer_stats()["inflight"] == 0:
+                    break
+                await asyncio.sleep(0.01)
+            kw = rt.native.fe.kube_writer_stats()
+            adm = json.loads(srv.stats())["admission"]
+            assert kw["bindings_first"] > 100, kw         # the window was the bound
+            assert adm["too_many_requests"] == 0 and adm["peak_mutating_inflight"] <= 14, adm
+            assert kw["failed"] == 0 and kw["inflight"] == 0 and kw["label_failures"] == 0, kw
+            for p in pods:
+                st, body = srv.call("GET", f"/api/v1/namespaces/default/pods/{pu.meta(p)['name']}", "")
+                got = json.loads(body)
+                assert got["spec"].get("nodeName") and got["metadata"]["labels"].get(T.GPU_ASSUME) == "true", got
+            assert json.loads(srv.stats())["bindings"] == 300 and rt.state.ledger.n_pods == 300
+        finally:
+            await rt.stop()
+            srv.stop()
+
+    asyncio.run(main())
+
+
 def test_python_writer_honours_retry_after():
     """The Python bind path (fallback, and the reference's semantics) waits out a 429's
     Retry-After instead of its 5 ms backoff, and the fake API server refuses over its limit."""
