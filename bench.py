@@ -438,6 +438,7 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
         "stranded_pct": round(statistics.mean(f["stranded_pct"] for f in fr), 3) if fr else None,
         "scheduled": out["scheduled"], "failed": out["failed"], "bind_retries": out["bind_errors"],
         "api_429s": out.get("api_429s"),
+        "bindings_first_rank0": out.get("bindings_first"),
         "host_selection": "kube-scheduler combining (LeastAllocated + BalancedAllocation + PodTopologySpread + "
                           "10 x extender)",
         "nominations": res["nominations"],
@@ -479,6 +480,7 @@ def headline_line(d: Dist, args, res: dict, out: dict, cpus: list[int], api_proc
             full[f"p50_bind_ms_{tag}"] = variant["p50_bind_ms"]
             full[f"p99_bind_ms_{tag}"] = variant["p99_bind_ms"]
             full[f"api_429s_{tag}"] = variant.get("api_429s")
+            full[f"bindings_first_rank0_{tag}"] = variant.get("bindings_first")
     if one_v is not None:
         if "error" in one_v:
             full["value_independent_schedulers"] = None
@@ -752,6 +754,8 @@ def summarize(d: Dist, args, res: dict) -> dict:
             "bind_hops": hops,
             # the API server's max-in-flight admission: 429s answered in this pass (rank 0 holds it)
             "api_429s": ((res.get("apiserver") or {}).get("admission") or {}).get("too_many_requests"),
+            # rank 0's bindings sent ahead of their labels (a saturated admission window)
+            "bindings_first": res.get("bindings_first"),
             # each rank's mean stand-in span per step: the slowest sets the peak barrier
             "schedule_ms_by_rank": [round(v, 2) for v in d.gather_obj((res.get("phase_ms") or {}).get("schedule_ms", 0.0))]}
 

@@ -1157,6 +1157,8 @@ async def run_rank(d: Dist, args, topo, ledger_path: str, conn=None, api_proc: A
         # priorities runs only when more than one node passed the filter
         results["prio_per_pod"] = round((ns["priorities"]["count"] - prio0) / max(1, results["scheduled"]), 3)
         results["native"]["prio_per_filter"] = round(ns["priorities"]["count"] / max(1, ns["filter"]["count"]), 4)
+        kws = rt.native.fe.kube_writer_stats()
+        results["bindings_first"] = kws.get("bindings_first") if kws else None
     results["phase_ms"] = {k: round(statistics.mean(p[k] for p in results["phases"]), 2)
                            for k in ("create_ms", "schedule_ms", "release_ms", "create_srv_ms", "delete_srv_ms")
                            if all(k in p for p in results["phases"])} if results.get("phases") else None
