@@ -719,8 +719,10 @@ def summarize(d: Dist, args, res: dict) -> dict:
     rows = [h for r in d.gather_obj(res.get("bind_hops_ns", [])) for h in r]
     hops = hop_summary(rows)
     # the extender's own part of each bind: its wall time (request read -> reply handed to the
-    # kernel) without the API server's answer time (the `api` hop)
-    ext = sorted(sum(h) - h[BIND_HOPS.index("api")] for h in rows)
+    # kernel) without the API server's answer time (the `api` hop) and the wait for room in the
+    # admission window (`window`: every slot held by API requests not answered yet, i.e. the
+    # API server's backpressure; both hops are on the line in bind_hops_us)
+    ext = sorted(sum(h) - h[BIND_HOPS.index("api")] - h[BIND_HOPS.index("window")] for h in rows)
     scheduled_all = sum(d.gather_obj(res["scheduled"]))
     api_cpu = res.get("apiserver_cpu_s")
     client = sorted(b for r in d.gather_obj(res["client_bind_ms"]) for b in r)

@@ -1185,7 +1185,9 @@ def _pct(a: list, q: float):
 # the hops of a native bind (nanogpu/bindhops.h), in order: parse + ledger reserve, hand-off to
 # the writer's loop, request built and sent, the API server's answer, commit + reply posted to
 # the front door, reply written to kube-scheduler's connection
-BIND_HOPS = ("reserve", "handoff", "send", "api", "commit", "reply")
+# the writer's wait for room in the admission window ("window": every slot held by unanswered
+# API requests) is the API server's backpressure, apart from the writer's own send
+BIND_HOPS = ("reserve", "handoff", "window", "send", "api", "commit", "reply")
 
 
 def hop_summary(rows: list) -> dict | None:

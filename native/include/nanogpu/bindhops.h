@@ -9,6 +9,8 @@
 //   kRead      first bytes of the bind request read by the front-door worker
 //   kReserved  arguments parsed, pod found, ledger reserve done; handed to the writer
 //   kPickup    the writer's loop took the bind (io thread woken, or the caller's send)
+//   kLaunched  the admission window had room for it (kube-apiserver's max-in-flight share:
+//              with every slot held by unanswered requests, a bind waits here)
 //   kSent      binding (+ label PATCH) written to the API server connection
 //   kAnswer    the binding's answer parsed
 //   kPosted    ledger committed, reply posted to the front-door worker
@@ -27,7 +29,9 @@
 
 namespace nanogpu {
 
-enum BindHop : int { kHopRead, kHopReserved, kHopPickup, kHopSent, kHopAnswer, kHopPosted, kHopReplied, kBindHops };
+enum BindHop : int { kHopRead, kHopReserved, kHopPickup, kHopLaunched, kHopSent, kHopAnswer, kHopPosted, kHopReplied,
+                     kBindHops };
+constexpr int kHopSplits = kBindHops - 1;   // the time between consecutive hops
 
 struct BindHopTable {
   static constexpr size_t kSlots = 8192;   // power of two

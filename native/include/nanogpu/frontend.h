@@ -24,6 +24,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "nanogpu/bindhops.h"
 #include "nanogpu/iotally.h"
 #include "nanogpu/alloc.h"
 #include "nanogpu/kubewriter.h"
@@ -174,12 +175,12 @@ class Frontend {
   // latency"). Bounded at kMaxWallSamples between calls.
   std::vector<uint64_t> take_bind_wall();
   static constexpr size_t kMaxWallSamples = 1u << 20;
-  // Per-hop split of the native binds answered since the last call (bindhops.h), each the six
-  // durations in ns between its seven stamps: parse+reserve, hand-off to the writer, build+send,
-  // API answer, commit+post, reply. Recorded only while switched on (off by default; false
+  // Per-hop split of the native binds answered since the last call (bindhops.h), each the seven
+  // durations in ns between its eight stamps: parse+reserve, hand-off to the writer, wait for the
+  // admission window, build+send, API answer, commit+post, reply. Recorded only while switched on (off by default; false
   // when this host has no invariant TSC to stamp with).
   bool set_bind_hops(bool on);
-  std::vector<std::array<uint32_t, 6>> take_bind_hops();
+  std::vector<std::array<uint32_t, kHopSplits>> take_bind_hops();
   // how many of each are waiting to be taken (a marker between steps, no copy)
   std::pair<size_t, size_t> bind_samples_waiting();
 
@@ -255,7 +256,7 @@ class Frontend {
 
   std::mutex wall_mu_;
   std::vector<uint64_t> bind_wall_ns_;
-  std::vector<std::array<uint32_t, 6>> bind_hops_;
+  std::vector<std::array<uint32_t, kHopSplits>> bind_hops_;
 
   mutable std::mutex pod_mu_;
   // filter -> bind pod cache: kPodWays-way buckets by UID hash whose entries keep their

@@ -937,14 +937,14 @@ PYBIND11_MODULE(_native, m) {
       .def("set_bind_hops", &Frontend::set_bind_hops, py::arg("on"),
            "record each native bind's hop split (false: off, or no invariant TSC on this host)")
       .def("take_bind_hops", [](Frontend& f) {
-             const std::vector<std::array<uint32_t, 6>> v = f.take_bind_hops();
+             const std::vector<std::array<uint32_t, kHopSplits>> v = f.take_bind_hops();
              std::vector<std::vector<uint32_t>> out;
              out.reserve(v.size());
              for (const auto& a : v) out.emplace_back(a.begin(), a.end());
              return out;
            },
-           "per native bind since the last call, ns of: parse+reserve, hand-off to the writer, build+send, "
-           "API answer, commit+post, reply")
+           "per native bind since the last call, ns of: parse+reserve, hand-off to the writer, wait for the "
+           "admission window, build+send, API answer, commit+post, reply")
       .def("stats", [](Frontend& f) {
         auto one = [](const VerbStats& s) {
           py::dict d;

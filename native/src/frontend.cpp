@@ -502,9 +502,9 @@ std::pair<size_t, size_t> Frontend::bind_samples_waiting() {
   return {bind_wall_ns_.size(), bind_hops_.size()};
 }
 
-std::vector<std::array<uint32_t, 6>> Frontend::take_bind_hops() {
+std::vector<std::array<uint32_t, kHopSplits>> Frontend::take_bind_hops() {
   std::lock_guard<std::mutex> g(wall_mu_);
-  std::vector<std::array<uint32_t, 6>> out;
+  std::vector<std::array<uint32_t, kHopSplits>> out;
   out.swap(bind_hops_);
   return out;
 }
@@ -1322,8 +1322,8 @@ void Frontend::deliver_reply(Worker* w, const Reply& r) {
     uint64_t hv[kBindHops];
     if (g_hops.close(make_id(w->idx, conn), hv)) {
       const double k = io_ns_per_tick();
-      std::array<uint32_t, 6> d{};
-      for (int h = 0; h < 6; ++h)
+      std::array<uint32_t, kHopSplits> d{};
+      for (int h = 0; h < kHopSplits; ++h)
         d[h] = static_cast<uint32_t>(std::min(4.0e9, static_cast<double>(hv[h + 1] - hv[h]) * k));
       std::lock_guard<std::mutex> g(wall_mu_);
       if (bind_hops_.size() < kMaxWallSamples) bind_hops_.push_back(d);

@@ -674,6 +674,7 @@ void KubeWriter::process_batch(std::vector<BindJob>& jobs, std::vector<std::uniq
   const uint64_t t1 = now_ns();
   for (size_t i = 0; i < n; ++i) {
     g_hops.stamp(jobs[i].id, kHopPickup);
+    g_hops.stamp(jobs[i].id, kHopLaunched);   // blocking writer threads: no admission window
     build(jobs[i], &patch[i], &binding[i]);
     conns[2 * i + 1]->start("POST", "/api/v1/namespaces/" + jobs[i].ns + "/pods/" + jobs[i].name + "/binding", kJson,
                             binding[i], a);

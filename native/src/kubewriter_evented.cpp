@@ -759,6 +759,7 @@ void BindIo::start_waiting() {
     auto jb = std::make_unique<Job>();
     jb->j = std::move(waiting_.front());
     waiting_.pop_front();
+    g_hops.stamp(jb->j.id, kHopLaunched);
     {
       IoTimer it{kWrBuild};
       kw_->build(jb->j, &jb->patch, &jb->binding);
@@ -1145,6 +1146,7 @@ bool KubeWriter::send_from_caller(BindJob& j) {
   Handoff h;
   h.k = conn.first;
   g_hops.stamp(j.id, kHopPickup);
+  g_hops.stamp(j.id, kHopLaunched);   // sent by the caller: no window wait
   build(j, &h.patch, &h.binding);
   const std::string a = auth();
   compose_request(&h.out, "POST", j, true, kJsonE, h.binding, host_hdr_, a);

@@ -68,7 +68,7 @@ def test_bench_single_rank_cpu(tmp_path, cpu_exclusive):
     # every native bind split by hop: p50 <= p99 per hop; the median binds' hops add up to about
     # the front door's median wall (each hop's median is taken alone, so only roughly)
     hops = d["bind_hops_us"]
-    assert list(hops) == ["reserve", "handoff", "send", "api", "commit", "reply"] and d["bind_tail_hop"] in hops
+    assert list(hops) == ["reserve", "handoff", "window", "send", "api", "commit", "reply"] and d["bind_tail_hop"] in hops
     assert all(len(v) == 3 and 0 <= v[0] <= v[1] for v in hops.values())
     assert 0.2 * d["p50_bind_frontdoor_ms"] <= sum(v[0] for v in hops.values()) / 1e3 <= 3 * d["p50_bind_frontdoor_ms"]
 
@@ -273,10 +273,13 @@ def test_hop_summary_names_the_hop_that_owns_the_tail():
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
     assert bench.hop_summary([]) is None
-    rows = [[1000, 2000, 3000, 40000, 500, 4000]] * 990 + [[1000, 2000, 3000, 40000, 500, 300000]] * 10
+    rows = [[1000, 2000, 0, 3000, 40000, 500, 4000]] * 990 + [[1000, 2000, 0, 3000, 40000, 500, 300000]] * 10
     h = bench.hop_summary(rows)
     assert h["n"] == 1000 and h["tail_hop"] == "reply"
     assert h["us"]["api"] == [40.0, 40.0, 40.0] and h["us"]["reply"] == [4.0, 300.0, 300.0]
+    # binds held for room in the admission window (the API server's backpressure) own their tail
+    rows = [[1000, 2000, 0, 3000, 40000, 500, 4000]] * 990 + [[1000, 2000, 900000, 3000, 40000, 500, 4000]] * 10
+    assert bench.hop_summary(rows)["tail_hop"] == "window"
 
 
 def test_link_weights_fall_back_to_the_reader_and_a_matrix_sets_the_mesh():
