@@ -709,7 +709,9 @@ void KubeWriter::finish_label(HttpConn* c, const BindJob& j, const std::string& 
   const uint64_t t3 = now_ns();
   if (sp != 404) sp = call(c, "PATCH", "/api/v1/namespaces/" + j.ns + "/pods/" + j.name, kMergePatch, patch, rp, true);
   stats.patch_ns.fetch_add(now_ns() - t3, std::memory_order_relaxed);
-  if (sp < 200 || sp >= 300) stats.label_failures.fetch_add(1, std::memory_order_relaxed);
+  // a pod deleted before its label landed (a label trailing its binding under a saturated
+  // admission window can meet the pod's delete) needs none: not a failure
+  if ((sp < 200 || sp >= 300) && sp != 404) stats.label_failures.fetch_add(1, std::memory_order_relaxed);
 }
 
 bool KubeWriter::finish_binding(HttpConn* c2, BindJob& j, const std::string& b, int sb, std::string* rb) {
